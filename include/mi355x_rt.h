@@ -1,0 +1,82 @@
+/*
+ * mi355x_rt.h -- C ABI of libmi355x_rt.so, the thin HIP layer under op/hip and coll/mi355x.
+ *
+ * It replaces, for device buffers, the roles the reference gives to:
+ *   - the CPU op loops            ompi/mca/op/base/op_base_functions.c:39-683 (mi355x_op_*)
+ *   - the CUDA driver shim         ompi/mca/common/cuda/common_cuda.c (pointer query :1687-1783,
+ *                                  memcpy :1796-1889, IPC handles :971-1221)  (mi355x_ptr_*,
+ *                                  mi355x_memcpy*, mi355x_ipc_*)
+ *   - the datatype CUDA hooks      opal/datatype/opal_datatype_cuda.c:43-192 (mi355x_pack_*)
+ *   - the tuned schedules on device buffers, coll/cuda staging   coll_cuda_allreduce.c:30-77
+ *                                  (mi355x_coll_*)
+ * Plain C types only: pointers, sizes, ints.  `stream` is a hipStream_t passed as void*; NULL
+ * means the library's own per-thread stream.  Every function returns MI355X_SUCCESS (0) or a
+ * negative mi355x_status; mi355x_last_error() gives the text of the last failure.
+ * Nothing here falls back to the CPU: when no GPU / no HIP runtime is present the calls fail
+ * with MI355X_ERR_HIP.
+ */
+#ifndef MI355X_RT_H
+#define MI355X_RT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mi355x_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- runtime / diagnostics */
+const char *mi355x_last_error(void);
+int mi355x_version(void);                 /* 100*major + minor of this library */
+int mi355x_device_count(int *count);
+int mi355x_set_device(int dev);
+int mi355x_get_device(int *dev);
+int mi355x_stream_create(void **stream);
+int mi355x_stream_destroy(void *stream);
+int mi355x_stream_sync(void *stream);
+int mi355x_device_sync(void);
+int mi355x_malloc(void **p, size_t bytes);
+int mi355x_free(void *p);
+int mi355x_host_alloc(void **p, size_t bytes);   /* pinned */
+int mi355x_host_free(void *p);
+int mi355x_memcpy(void *dst, const void *src, size_t bytes);                /* synchronous */
+int mi355x_memcpy_async(void *dst, const void *src, size_t bytes, void *stream);
+int mi355x_memset_async(void *dst, int value, size_t bytes, void *stream);
+
+/* Pointer classification (replaces mca_common_cuda_is_gpu_buffer, common_cuda.c:1687-1783):
+ * *is_device = 1 for hipMalloc'd / IPC-mapped device memory, 0 for host memory. */
+int mi355x_ptr_is_device(const void *p, int *is_device);
+
+/* Timing helpers around launches on `stream` (hipEvent based). */
+int mi355x_event_create(void **ev);
+int mi355x_event_destroy(void *ev);
+int mi355x_event_record(void *ev, void *stream);
+int mi355x_event_elapsed_ms(void *start, void *stop, float *ms);
+
+/* ---------------------------------------------------------------- op/hip kernels */
+/* 1 if (op,type) has a GPU kernel.  Slots absent from the reference table are 0, and so are
+ * the x87 `long double` slots (no 80-bit format on CDNA4; op/hip stages those to the host). */
+int mi355x_op_supported(int op, int type);
+size_t mi355x_type_size(int type);
+
+/* 2-buff: inout[i] = inout[i] (op) in[i], count elements, asynchronous on `stream`.
+ * Device pointers only.  Replaces ompi_op_base_2buff_<op>_<type> (op_base_functions.c:39-103). */
+int mi355x_op_reduce(int op, int type, const void *in, void *inout, size_t count, void *stream);
+/* 3-buff: out[i] = in1[i] (op) in2[i]; in1/in2/out must not overlap (restrict, op.h:625-630).
+ * Replaces ompi_op_base_3buff_<op>_<type> (op_base_functions.c:606-683). */
+int mi355x_op_reduce_3buff(int op, int type, const void *in1, const void *in2, void *out,
+                           size_t count, void *stream);
+
+/* Launch-shape knobs for the streaming op kernels.  unroll in {1,2,4,8} (16-byte vectors per
+ * operand per thread per iteration; 0 = keep), blocks_per_cu in 1..64 (0 = keep), nontemporal
+ * 0/1 (-1 = keep).  Only the fp32/fp64 SUM kernels have every variant compiled; the other slots
+ * always run unroll 4, temporal. */
+int mi355x_op_tune(int unroll, int blocks_per_cu, int nontemporal);
+int mi355x_op_get_tune(int *unroll, int *blocks_per_cu, int *nontemporal);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MI355X_RT_H */

@@ -1,0 +1,140 @@
+"""Host-side (Python) view of the MI355X collective-reduction path.
+
+The product is native: ``lib/libmi355x_rt.so`` (HIP kernels behind a C ABI, include/mi355x_rt.h)
+plus the two Open MPI components ``lib/mca_op_hip.so`` and ``lib/mca_coll_mi355x.so`` written in
+C.  This module is the thin ctypes binding used by the tests, ``bench.py`` and
+``__graft_entry__.py``; it mirrors the reference's op vocabulary (ompi/mca/op/op.h:103-235) so a
+test reads like the reference's own.  It has no compute path of its own: every reduction goes
+through the HIP library, and loading fails loudly when the library is missing.
+
+Import it with :func:`load` (the directory name is not a valid Python identifier)::
+
+    import importlib.util, pathlib
+    spec = importlib.util.spec_from_file_location("ompi_release_amd", ".../ompi-release_amd/__init__.py")
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import pathlib
+
+PKG_DIR = pathlib.Path(__file__).resolve().parent
+LIB_DIR = PKG_DIR / "lib"
+REPO_DIR = PKG_DIR.parent
+
+# ---------------------------------------------------------------- reference enums (op.h)
+TYPES = [
+    "INT8", "UINT8", "INT16", "UINT16", "INT32", "UINT32", "INT64", "UINT64",
+    "F_INTEGER", "F_INTEGER1", "F_INTEGER2", "F_INTEGER4", "F_INTEGER8", "F_INTEGER16",
+    "FLOAT", "DOUBLE", "F_REAL", "F_REAL2", "F_REAL4", "F_REAL8", "F_REAL16",
+    "F_DOUBLE_PRECISION", "LONG_DOUBLE", "F_LOGICAL", "BOOL",
+    "C_FLOAT_COMPLEX", "C_DOUBLE_COMPLEX", "C_LONG_DOUBLE_COMPLEX", "BYTE",
+    "F_2REAL", "F_2DOUBLE_PRECISION", "F_2INTEGER",
+    "FLOAT_INT", "DOUBLE_INT", "LONG_INT", "2INT", "SHORT_INT", "LONG_DOUBLE_INT", "WCHAR",
+]
+T = {name: i for i, name in enumerate(TYPES)}
+OPS = ["NULL", "MAX", "MIN", "SUM", "PROD", "LAND", "BAND", "LOR", "BOR", "LXOR", "BXOR",
+       "MAXLOC", "MINLOC", "REPLACE", "NO_OP"]
+OP = {name: i for i, name in enumerate(OPS)}
+
+MI355X_SUCCESS = 0
+
+
+class MI355XError(RuntimeError):
+    pass
+
+
+_rt = None
+
+
+def lib_path(name: str = "libmi355x_rt.so") -> pathlib.Path:
+    return LIB_DIR / name
+
+
+def rt() -> ctypes.CDLL:
+    """Load libmi355x_rt.so (RTLD_GLOBAL so the MCA component DSOs resolve against it)."""
+    global _rt
+    if _rt is None:
+        p = lib_path()
+        if not p.exists():
+            raise MI355XError(f"{p} is missing: run __graft_entry__.build() (make -C ompi-release_amd/csrc)")
+        lib = ctypes.CDLL(str(p), mode=ctypes.RTLD_GLOBAL)
+        _declare(lib)
+        _rt = lib
+    return _rt
+
+
+def _declare(lib: ctypes.CDLL) -> None:
+    c = ctypes
+    vp, sz, i = c.c_void_p, c.c_size_t, c.c_int
+    sigs = {
+        "mi355x_last_error": (c.c_char_p, []),
+        "mi355x_version": (i, []),
+        "mi355x_device_count": (i, [c.POINTER(i)]),
+        "mi355x_set_device": (i, [i]),
+        "mi355x_get_device": (i, [c.POINTER(i)]),
+        "mi355x_stream_create": (i, [c.POINTER(vp)]),
+        "mi355x_stream_destroy": (i, [vp]),
+        "mi355x_stream_sync": (i, [vp]),
+        "mi355x_device_sync": (i, []),
+        "mi355x_malloc": (i, [c.POINTER(vp), sz]),
+        "mi355x_free": (i, [vp]),
+        "mi355x_memcpy": (i, [vp, vp, sz]),
+        "mi355x_memcpy_async": (i, [vp, vp, sz, vp]),
+        "mi355x_memset_async": (i, [vp, i, sz, vp]),
+        "mi355x_ptr_is_device": (i, [vp, c.POINTER(i)]),
+        "mi355x_event_create": (i, [c.POINTER(vp)]),
+        "mi355x_event_destroy": (i, [vp]),
+        "mi355x_event_record": (i, [vp, vp]),
+        "mi355x_event_elapsed_ms": (i, [vp, vp, c.POINTER(c.c_float)]),
+        "mi355x_op_supported": (i, [i, i]),
+        "mi355x_type_size": (sz, [i]),
+        "mi355x_op_reduce": (i, [i, i, vp, vp, sz, vp]),
+        "mi355x_op_reduce_3buff": (i, [i, i, vp, vp, vp, sz, vp]),
+        "mi355x_op_tune": (i, [i, i, i]),
+        "mi355x_op_get_tune": (i, [c.POINTER(i), c.POINTER(i), c.POINTER(i)]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue  # optional symbols are checked by tests/test_boundary.py
+        fn.restype = res
+        fn.argtypes = args
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != MI355X_SUCCESS:
+        msg = rt().mi355x_last_error().decode(errors="replace")
+        raise MI355XError(f"{what} failed ({rc}): {msg}")
+
+
+def op_reduce(op: int, ty: int, src: int, inout: int, count: int, stream: int | None = None) -> None:
+    """2-buff reduction on device pointers (MPI_Reduce_local semantics)."""
+    check(rt().mi355x_op_reduce(op, ty, src, inout, count, stream), "mi355x_op_reduce")
+
+
+def op_reduce_3buff(op: int, ty: int, in1: int, in2: int, out: int, count: int,
+                    stream: int | None = None) -> None:
+    check(rt().mi355x_op_reduce_3buff(op, ty, in1, in2, out, count, stream), "mi355x_op_reduce_3buff")
+
+
+def op_supported(op: int, ty: int) -> bool:
+    return bool(rt().mi355x_op_supported(op, ty))
+
+
+def type_size(ty: int) -> int:
+    return int(rt().mi355x_type_size(ty))
+
+
+def tune(unroll: int = 0, blocks_per_cu: int = 0, nontemporal: int = -1) -> None:
+    check(rt().mi355x_op_tune(unroll, blocks_per_cu, nontemporal), "mi355x_op_tune")
+
+
+def get_tune() -> tuple[int, int, int]:
+    a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    check(rt().mi355x_op_get_tune(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+    return a.value, b.value, c.value
+
+
+def env_flag(name: str, default: str = "") -> str:
+    return os.environ.get(name, default)

@@ -1,0 +1,227 @@
+// op_functors.hpp -- device-side element rules for every (MPI_Op, element type) slot that
+// op/hip computes on the GPU.
+//
+// Each functor F provides
+//     using T;                               the element (a C type or a MAXLOC pair struct)
+//     static T op2(T out, T in);             2-buff rule: new inout value      (op_base_functions.c:39-103)
+//     static T op3(T in1, T in2);            3-buff rule: out value            (op_base_functions.c:606-683)
+// Operand roles follow the reference exactly (see oracle/op_oracle.c for the CPU restatement):
+// MAX/MIN are selects `(o > a) ? o : a`, never v_max/v_min (NaN and signed-zero results depend
+// on which operand is first); integer SUM/PROD wrap in the element width; complex PROD follows
+// the C99 Annex G multiply that GCC emits for `_Complex *=` (inline fast path + libgcc
+// __mulsc3/__muldc3 recovery, libgcc from GCC 11.4 -- the compiler the reference build uses on
+// this host); MAXLOC/MINLOC keep the 2-buff / 3-buff asymmetry on ties.
+// Compiled with -ffp-contract=off: no FMA contraction anywhere (the reference x86-64 build
+// has none), denormals preserved (gfx950 default f32/f64 denormal mode is IEEE).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "../../../include/mi355x_types.h"
+
+namespace mi355x {
+
+// ------------------------------------------------------------------ element types
+struct cf32 { float re, im; };
+struct cf64 { double re, im; };
+// MAXLOC/MINLOC pairs, byte-identical to the C structs of op_base_functions.c:539-555 on
+// x86-64 (gfx950 uses the same sizes and alignments for these members).
+struct p_float_int { float v; int k; };
+struct p_double_int { double v; int k; };
+struct p_long_int { long v; int k; };
+struct p_2int { int v; int k; };
+struct p_short_int { short v; int k; };
+static_assert(sizeof(p_float_int) == 8, "float_int");
+static_assert(sizeof(p_double_int) == 16, "double_int");
+static_assert(sizeof(p_long_int) == 16, "long_int");
+static_assert(sizeof(p_2int) == 8, "2int");
+static_assert(sizeof(p_short_int) == 8, "short_int");
+static_assert(sizeof(cf32) == 8 && sizeof(cf64) == 16, "complex");
+
+// unsigned twin used for wrap-around integer arithmetic (signed overflow is UB in C++; the
+// reference relies on gcc's two's-complement code generation, which this reproduces)
+template <typename T> struct uns { using type = T; };
+template <> struct uns<int8_t> { using type = uint8_t; };
+template <> struct uns<int16_t> { using type = uint16_t; };
+template <> struct uns<int32_t> { using type = uint32_t; };
+template <> struct uns<int64_t> { using type = uint64_t; };
+
+// ------------------------------------------------------------------ elementwise rules
+#define MI_DEV __device__ __forceinline__
+
+template <typename E> struct OpMax {
+    using T = E;
+    static MI_DEV T op2(T o, T a) { return (o > a) ? o : a; }
+    static MI_DEV T op3(T o, T a) { return (o > a) ? o : a; }
+};
+template <typename E> struct OpMin {
+    using T = E;
+    static MI_DEV T op2(T o, T a) { return (o < a) ? o : a; }
+    static MI_DEV T op3(T o, T a) { return (o < a) ? o : a; }
+};
+
+template <typename E, bool IS_INT> struct SumImpl;
+template <typename E> struct SumImpl<E, true> {
+    static MI_DEV E f(E o, E a)
+    {
+        using U = typename uns<E>::type;
+        return (E)(U)((U)o + (U)a);
+    }
+};
+template <typename E> struct SumImpl<E, false> {
+    static MI_DEV E f(E o, E a) { return o + a; }
+};
+template <typename E> struct OpSum {
+    using T = E;
+    static MI_DEV T op2(T o, T a) { return SumImpl<E, __is_integral(E)>::f(o, a); }
+    static MI_DEV T op3(T o, T a) { return SumImpl<E, __is_integral(E)>::f(o, a); }
+};
+
+template <typename E, bool IS_INT> struct ProdImpl;
+template <typename E> struct ProdImpl<E, true> {
+    static MI_DEV E f(E o, E a)
+    {
+        // C promotes 8/16-bit operands to int; the low bits of the product are the same as the
+        // low bits of an unsigned 32-bit product, so compute there and truncate.
+        using W = typename std::conditional<(sizeof(E) <= 4), uint32_t, uint64_t>::type;
+        return (E)(W)((W)(typename uns<E>::type)o * (W)(typename uns<E>::type)a);
+    }
+};
+template <typename E> struct ProdImpl<E, false> {
+    static MI_DEV E f(E o, E a) { return o * a; }
+};
+template <typename E> struct OpProd {
+    using T = E;
+    static MI_DEV T op2(T o, T a) { return ProdImpl<E, __is_integral(E)>::f(o, a); }
+    static MI_DEV T op3(T o, T a) { return ProdImpl<E, __is_integral(E)>::f(o, a); }
+};
+
+template <typename E> struct OpLand {
+    using T = E;
+    static MI_DEV T op2(T o, T a) { return (T)((o != 0) && (a != 0)); }
+    static MI_DEV T op3(T o, T a) { return (T)((o != 0) && (a != 0)); }
+};
+template <typename E> struct OpLor {
+    using T = E;
+    static MI_DEV T op2(T o, T a) { return (T)((o != 0) || (a != 0)); }
+    static MI_DEV T op3(T o, T a) { return (T)((o != 0) || (a != 0)); }
+};
+template <typename E> struct OpLxor {
+    using T = E;
+    static MI_DEV T op2(T o, T a) { return (T)((o != 0 ? 1 : 0) ^ (a != 0 ? 1 : 0)); }
+    static MI_DEV T op3(T o, T a) { return (T)((o != 0 ? 1 : 0) ^ (a != 0 ? 1 : 0)); }
+};
+template <typename E> struct OpBand {
+    using T = E;
+    static MI_DEV T op2(T o, T a) { return (T)(o & a); }
+    static MI_DEV T op3(T o, T a) { return (T)(o & a); }
+};
+template <typename E> struct OpBor {
+    using T = E;
+    static MI_DEV T op2(T o, T a) { return (T)(o | a); }
+    static MI_DEV T op3(T o, T a) { return (T)(o | a); }
+};
+template <typename E> struct OpBxor {
+    using T = E;
+    static MI_DEV T op2(T o, T a) { return (T)(o ^ a); }
+    static MI_DEV T op3(T o, T a) { return (T)(o ^ a); }
+};
+
+// ------------------------------------------------------------------ complex
+template <typename R> struct CplxOf;
+template <> struct CplxOf<float> { using type = cf32; };
+template <> struct CplxOf<double> { using type = cf64; };
+
+template <typename R> MI_DEV bool is_nan(R x) { return x != x; }
+template <typename R> MI_DEV bool is_inf(R x) { return __builtin_isinf(x); }
+template <typename R> MI_DEV R copysgn(R m, R s) { return __builtin_copysign(m, s); }
+
+// (a + ib) * (c + id) as GCC evaluates `_Complex` multiplication without -ffast-math:
+// x = ac - bd, y = ad + bc; if both are NaN, libgcc's __mul?c3 recovery rules (C99 G.5.1).
+template <typename R> MI_DEV typename CplxOf<R>::type cmul(R a, R b, R c, R d)
+{
+    R ac = a * c, bd = b * d, ad = a * d, bc = b * c;
+    R x = ac - bd, y = ad + bc;
+    if (is_nan(x) && is_nan(y)) {
+        bool recalc = false;
+        if (is_inf(a) || is_inf(b)) {
+            a = copysgn(is_inf(a) ? (R)1 : (R)0, a);
+            b = copysgn(is_inf(b) ? (R)1 : (R)0, b);
+            if (is_nan(c)) c = copysgn((R)0, c);
+            if (is_nan(d)) d = copysgn((R)0, d);
+            recalc = true;
+        }
+        if (is_inf(c) || is_inf(d)) {
+            c = copysgn(is_inf(c) ? (R)1 : (R)0, c);
+            d = copysgn(is_inf(d) ? (R)1 : (R)0, d);
+            if (is_nan(a)) a = copysgn((R)0, a);
+            if (is_nan(b)) b = copysgn((R)0, b);
+            recalc = true;
+        }
+        if (!recalc && (is_inf(ac) || is_inf(bd) || is_inf(ad) || is_inf(bc))) {
+            if (is_nan(a)) a = copysgn((R)0, a);
+            if (is_nan(b)) b = copysgn((R)0, b);
+            if (is_nan(c)) c = copysgn((R)0, c);
+            if (is_nan(d)) d = copysgn((R)0, d);
+            recalc = true;
+        }
+        if (recalc) {
+            x = (R)__builtin_inf() * (a * c - b * d);
+            y = (R)__builtin_inf() * (a * d + b * c);
+        }
+    }
+    typename CplxOf<R>::type r;
+    r.re = x;
+    r.im = y;
+    return r;
+}
+
+template <typename C> struct RealOf;
+template <> struct RealOf<cf32> { using type = float; };
+template <> struct RealOf<cf64> { using type = double; };
+
+template <typename C> struct OpCsum {
+    using T = C;
+    static MI_DEV T op2(T o, T a) { T r; r.re = o.re + a.re; r.im = o.im + a.im; return r; }
+    static MI_DEV T op3(T o, T a) { return op2(o, a); }
+};
+template <typename C> struct OpCprod {
+    using T = C;
+    using R = typename RealOf<C>::type;
+    static MI_DEV T op2(T o, T a) { return cmul<R>(o.re, o.im, a.re, a.im); }
+    static MI_DEV T op3(T o, T a) { return cmul<R>(o.re, o.im, a.re, a.im); }
+};
+
+// ------------------------------------------------------------------ MAXLOC / MINLOC
+// CMP(x, y) is x > y (maxloc) or x < y (minloc).
+template <typename P, bool MAX> struct OpLoc {
+    using T = P;
+    static MI_DEV bool cmp(decltype(P::v) x, decltype(P::v) y) { return MAX ? (x > y) : (x < y); }
+    // 2-buff (op_base_functions.c:87-103): o is inout, a is in
+    static MI_DEV T op2(T o, T a)
+    {
+        if (cmp(a.v, o.v)) {
+            o.v = a.v;
+            o.k = a.k;
+        } else if (a.v == o.v) {
+            o.k = (o.k < a.k) ? o.k : a.k;
+        }
+        return o;
+    }
+    // 3-buff (op_base_functions.c:661-683): o is in1, a is in2
+    static MI_DEV T op3(T o, T a)
+    {
+        if (cmp(o.v, a.v)) return o;
+        if (o.v == a.v) {
+            o.k = (a.k < o.k) ? a.k : o.k;
+            return o;
+        }
+        return a;
+    }
+};
+
+#undef MI_DEV
+} // namespace mi355x

@@ -1,0 +1,304 @@
+// op_kernels.hip -- op/hip streaming reduction kernels for gfx950 (MI355X).
+//
+// One kernel template serves every (MPI_Op, type) slot, 2-buff and 3-buff:
+//   * 16-byte accesses per lane (global_load/store_dwordx4): 1 KiB per wave-instruction, full
+//     128-B lines, for every element size (1..16 B); MAXLOC pairs are decoded in registers from
+//     the same 16-byte vectors (no LDS round trip: each pair is consumed by the lane that loads
+//     it, so staging would only add LDS traffic).
+//   * grid-stride loop, U independent 16-B vectors per operand per thread in flight per
+//     iteration (all loads issued before the first use), grid capped at blocks_per_cu x CUs.
+//   * scalar head/tail so any alignment works: when all three operands share the same
+//     misalignment mod 16 the head peels to a 16-B boundary; otherwise the whole range takes
+//     the element-wise path (still coalesced, one element per lane).
+//   * no MFMA, no LDS: the work is 2 reads + 1 write per element -> HBM bound.
+// Algorithmic bytes per call = 3 x count x sizeof(T) (2-buff: read in, read+write inout;
+// 3-buff: read in1, in2, write out).
+#include "op_functors.hpp"
+#include "rt_internal.hpp"
+
+#include <type_traits>
+
+namespace mi355x {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T> struct alignas(16) Vec16 {
+    T e[16 / sizeof(T)];
+};
+
+struct StreamArgs {
+    const void *a;    // 2-buff: in (source)          3-buff: in1
+    const void *b;    // 2-buff: inout (target)       3-buff: in2
+    void *out;        // 2-buff: == b                 3-buff: out
+    size_t head;      // scalar elements before the 16-B aligned body
+    size_t nvec;      // 16-B vectors in the body
+    size_t n;         // total elements
+};
+
+template <class F, bool THREE>
+__device__ __forceinline__ typename F::T apply(const typename F::T &xa, const typename F::T &xb)
+{
+    // 2-buff: new inout = op2(out = inout (b), in = source (a)); 3-buff: op3(in1 (a), in2 (b))
+    if constexpr (THREE)
+        return F::op3(xa, xb);
+    else
+        return F::op2(xb, xa);
+}
+
+template <bool NT, typename V> __device__ __forceinline__ V vload(const V *p)
+{
+    u32x4 raw;
+    if constexpr (NT)
+        raw = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    else
+        raw = *reinterpret_cast<const u32x4 *>(p);
+    V v;
+    __builtin_memcpy(&v, &raw, 16);
+    return v;
+}
+
+template <bool NT, typename V> __device__ __forceinline__ void vstore(V *p, const V &v)
+{
+    u32x4 raw;
+    __builtin_memcpy(&raw, &v, 16);
+    if constexpr (NT)
+        __builtin_nontemporal_store(raw, reinterpret_cast<u32x4 *>(p));
+    else
+        *reinterpret_cast<u32x4 *>(p) = raw;
+}
+
+template <class F, bool THREE, int U, bool NT>
+__global__ __launch_bounds__(256) void k_stream(StreamArgs args)
+{
+    using T = typename F::T;
+    using V = Vec16<T>;
+    constexpr int EPV = 16 / sizeof(T);
+    const T *a = static_cast<const T *>(args.a);
+    const T *b = static_cast<const T *>(args.b);
+    T *o = static_cast<T *>(args.out);
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t nthr = (size_t)gridDim.x * blockDim.x;
+
+    for (size_t i = tid; i < args.head; i += nthr) o[i] = apply<F, THREE>(a[i], b[i]);
+
+    const V *av = reinterpret_cast<const V *>(a + args.head);
+    const V *bv = reinterpret_cast<const V *>(b + args.head);
+    V *ov = reinterpret_cast<V *>(o + args.head);
+    const size_t nvec = args.nvec;
+    for (size_t base = tid; base < nvec; base += nthr * U) {
+        V xa[U], xb[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * nthr;
+            if (i < nvec) {
+                xa[u] = vload<NT>(av + i);
+                xb[u] = vload<NT>(bv + i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * nthr;
+            if (i < nvec) {
+                V r;
+#pragma unroll
+                for (int j = 0; j < EPV; ++j) r.e[j] = apply<F, THREE>(xa[u].e[j], xb[u].e[j]);
+                vstore<NT>(ov + i, r);
+            }
+        }
+    }
+
+    const size_t t0 = args.head + nvec * EPV;
+    for (size_t i = t0 + tid; i < args.n; i += nthr) o[i] = apply<F, THREE>(a[i], b[i]);
+}
+
+// only the bench-critical functors get every launch-shape variant; the rest use U=4, NT=0
+template <class F> struct Tunable : std::false_type {};
+template <> struct Tunable<OpSum<float>> : std::true_type {};
+template <> struct Tunable<OpSum<double>> : std::true_type {};
+
+template <class F, bool THREE, int U, bool NT>
+static int launch_shape(const StreamArgs &args, hipStream_t s)
+{
+    using T = typename F::T;
+    constexpr int EPV = 16 / sizeof(T);
+    const StreamTune &t = stream_tune();
+    const size_t threads = 256;
+    size_t work = args.nvec ? (args.nvec + (size_t)U - 1) / U : 0;
+    size_t scalar = args.head + (args.n - args.head - args.nvec * EPV);
+    if (scalar > work) work = scalar;
+    size_t blocks = (work + threads - 1) / threads;
+    const size_t cap = (size_t)t.blocks_per_cu * (size_t)device_cu_count();
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL((k_stream<F, THREE, U, NT>), dim3((unsigned)blocks), dim3(threads), 0, s,
+                       args);
+    MI_HIP(hipGetLastError());
+    return MI355X_SUCCESS;
+}
+
+template <class F, bool THREE>
+static int launch(const void *a, const void *b, void *out, size_t n, hipStream_t s)
+{
+    using T = typename F::T;
+    constexpr size_t EPV = 16 / sizeof(T);
+    if (n == 0) return MI355X_SUCCESS;
+    StreamArgs args;
+    args.a = a;
+    args.b = b;
+    args.out = out;
+    args.n = n;
+    const uintptr_t ma = (uintptr_t)a & 15, mb = (uintptr_t)b & 15, mo = (uintptr_t)out & 15;
+    if (ma == mb && mb == mo && (ma % sizeof(T)) == 0) {
+        size_t head = ma ? (16 - ma) / sizeof(T) : 0;
+        if (head > n) head = n;
+        args.head = head;
+        args.nvec = (n - head) / EPV;
+    } else {
+        args.head = n; // element-wise path
+        args.nvec = 0;
+    }
+    const StreamTune &t = stream_tune();
+    if constexpr (Tunable<F>::value) {
+        const bool nt = t.nontemporal != 0;
+        switch (t.unroll) {
+        case 1: return nt ? launch_shape<F, THREE, 1, true>(args, s) : launch_shape<F, THREE, 1, false>(args, s);
+        case 2: return nt ? launch_shape<F, THREE, 2, true>(args, s) : launch_shape<F, THREE, 2, false>(args, s);
+        case 8: return nt ? launch_shape<F, THREE, 8, true>(args, s) : launch_shape<F, THREE, 8, false>(args, s);
+        default: return nt ? launch_shape<F, THREE, 4, true>(args, s) : launch_shape<F, THREE, 4, false>(args, s);
+        }
+    } else {
+        return launch_shape<F, THREE, 4, false>(args, s);
+    }
+}
+
+// ------------------------------------------------------------------ dispatch table
+typedef int (*launch_fn)(const void *, const void *, void *, size_t, hipStream_t);
+
+struct Slot {
+    launch_fn two = nullptr;
+    launch_fn three = nullptr;
+};
+
+template <class F> static void put(Slot (&tab)[MI355X_OP_MAX_][MI355X_T_MAX], int op, int ty)
+{
+    tab[op][ty].two = &launch<F, false>;
+    tab[op][ty].three = &launch<F, true>;
+}
+
+template <template <typename> class OP>
+static void put_ints(Slot (&tab)[MI355X_OP_MAX_][MI355X_T_MAX], int op)
+{
+    put<OP<int8_t>>(tab, op, MI355X_T_INT8);
+    put<OP<uint8_t>>(tab, op, MI355X_T_UINT8);
+    put<OP<int16_t>>(tab, op, MI355X_T_INT16);
+    put<OP<uint16_t>>(tab, op, MI355X_T_UINT16);
+    put<OP<int32_t>>(tab, op, MI355X_T_INT32);
+    put<OP<uint32_t>>(tab, op, MI355X_T_UINT32);
+    put<OP<int64_t>>(tab, op, MI355X_T_INT64);
+    put<OP<uint64_t>>(tab, op, MI355X_T_UINT64);
+}
+
+struct Table {
+    Slot s[MI355X_OP_MAX_][MI355X_T_MAX];
+    Table()
+    {
+        // groups as in op_base_functions.c:1373-1457 (Fortran types disabled; long double
+        // slots have no GPU form)
+        put_ints<OpMax>(s, MI355X_OP_MAX);
+        put<OpMax<float>>(s, MI355X_OP_MAX, MI355X_T_FLOAT);
+        put<OpMax<double>>(s, MI355X_OP_MAX, MI355X_T_DOUBLE);
+        put_ints<OpMin>(s, MI355X_OP_MIN);
+        put<OpMin<float>>(s, MI355X_OP_MIN, MI355X_T_FLOAT);
+        put<OpMin<double>>(s, MI355X_OP_MIN, MI355X_T_DOUBLE);
+        put_ints<OpSum>(s, MI355X_OP_SUM);
+        put<OpSum<float>>(s, MI355X_OP_SUM, MI355X_T_FLOAT);
+        put<OpSum<double>>(s, MI355X_OP_SUM, MI355X_T_DOUBLE);
+        put<OpCsum<cf32>>(s, MI355X_OP_SUM, MI355X_T_C_FLOAT_COMPLEX);
+        put<OpCsum<cf64>>(s, MI355X_OP_SUM, MI355X_T_C_DOUBLE_COMPLEX);
+        put_ints<OpProd>(s, MI355X_OP_PROD);
+        put<OpProd<float>>(s, MI355X_OP_PROD, MI355X_T_FLOAT);
+        put<OpProd<double>>(s, MI355X_OP_PROD, MI355X_T_DOUBLE);
+        put<OpCprod<cf32>>(s, MI355X_OP_PROD, MI355X_T_C_FLOAT_COMPLEX);
+        put<OpCprod<cf64>>(s, MI355X_OP_PROD, MI355X_T_C_DOUBLE_COMPLEX);
+        put_ints<OpLand>(s, MI355X_OP_LAND);
+        put<OpLand<uint8_t>>(s, MI355X_OP_LAND, MI355X_T_BOOL);
+        put_ints<OpLor>(s, MI355X_OP_LOR);
+        put<OpLor<uint8_t>>(s, MI355X_OP_LOR, MI355X_T_BOOL);
+        put_ints<OpLxor>(s, MI355X_OP_LXOR);
+        put<OpLxor<uint8_t>>(s, MI355X_OP_LXOR, MI355X_T_BOOL);
+        put_ints<OpBand>(s, MI355X_OP_BAND);
+        put<OpBand<int8_t>>(s, MI355X_OP_BAND, MI355X_T_BYTE);
+        put_ints<OpBor>(s, MI355X_OP_BOR);
+        put<OpBor<int8_t>>(s, MI355X_OP_BOR, MI355X_T_BYTE);
+        put_ints<OpBxor>(s, MI355X_OP_BXOR);
+        put<OpBxor<int8_t>>(s, MI355X_OP_BXOR, MI355X_T_BYTE);
+        put<OpLoc<p_float_int, true>>(s, MI355X_OP_MAXLOC, MI355X_T_FLOAT_INT);
+        put<OpLoc<p_double_int, true>>(s, MI355X_OP_MAXLOC, MI355X_T_DOUBLE_INT);
+        put<OpLoc<p_long_int, true>>(s, MI355X_OP_MAXLOC, MI355X_T_LONG_INT);
+        put<OpLoc<p_2int, true>>(s, MI355X_OP_MAXLOC, MI355X_T_2INT);
+        put<OpLoc<p_short_int, true>>(s, MI355X_OP_MAXLOC, MI355X_T_SHORT_INT);
+        put<OpLoc<p_float_int, false>>(s, MI355X_OP_MINLOC, MI355X_T_FLOAT_INT);
+        put<OpLoc<p_double_int, false>>(s, MI355X_OP_MINLOC, MI355X_T_DOUBLE_INT);
+        put<OpLoc<p_long_int, false>>(s, MI355X_OP_MINLOC, MI355X_T_LONG_INT);
+        put<OpLoc<p_2int, false>>(s, MI355X_OP_MINLOC, MI355X_T_2INT);
+        put<OpLoc<p_short_int, false>>(s, MI355X_OP_MINLOC, MI355X_T_SHORT_INT);
+    }
+};
+
+static const Table &table()
+{
+    static const Table t;
+    return t;
+}
+
+static const Slot *slot_of(int op, int type)
+{
+    if (op < 0 || op >= MI355X_OP_MAX_ || type < 0 || type >= MI355X_T_MAX) return nullptr;
+    const Slot *sl = &table().s[op][type];
+    return sl->two ? sl : nullptr;
+}
+
+} // namespace mi355x
+
+using namespace mi355x;
+
+extern "C" {
+
+int mi355x_op_supported(int op, int type) { return slot_of(op, type) ? 1 : 0; }
+
+size_t mi355x_type_size(int type)
+{
+    switch (type) {
+    case MI355X_T_INT8: case MI355X_T_UINT8: case MI355X_T_BOOL: case MI355X_T_BYTE: return 1;
+    case MI355X_T_INT16: case MI355X_T_UINT16: return 2;
+    case MI355X_T_INT32: case MI355X_T_UINT32: case MI355X_T_FLOAT: return 4;
+    case MI355X_T_INT64: case MI355X_T_UINT64: case MI355X_T_DOUBLE: return 8;
+    case MI355X_T_LONG_DOUBLE: return 16;            /* x86-64 long double storage */
+    case MI355X_T_C_FLOAT_COMPLEX: return 8;
+    case MI355X_T_C_DOUBLE_COMPLEX: return 16;
+    case MI355X_T_C_LONG_DOUBLE_COMPLEX: return 32;
+    case MI355X_T_FLOAT_INT: case MI355X_T_2INT: case MI355X_T_SHORT_INT: return 8;
+    case MI355X_T_DOUBLE_INT: case MI355X_T_LONG_INT: return 16;
+    case MI355X_T_LONG_DOUBLE_INT: return 32;
+    default: return 0;
+    }
+}
+
+int mi355x_op_reduce(int op, int type, const void *in, void *inout, size_t count, void *stream)
+{
+    const Slot *sl = slot_of(op, type);
+    if (!sl) return set_error(MI355X_ERR_UNSUPPORTED, "no GPU kernel for op %d type %d", op, type);
+    if (count && (!in || !inout)) return set_error(MI355X_ERR_ARG, "NULL buffer");
+    return sl->two(in, inout, inout, count, resolve_stream(stream));
+}
+
+int mi355x_op_reduce_3buff(int op, int type, const void *in1, const void *in2, void *out,
+                           size_t count, void *stream)
+{
+    const Slot *sl = slot_of(op, type);
+    if (!sl) return set_error(MI355X_ERR_UNSUPPORTED, "no GPU kernel for op %d type %d", op, type);
+    if (count && (!in1 || !in2 || !out)) return set_error(MI355X_ERR_ARG, "NULL buffer");
+    return sl->three(in1, in2, out, count, resolve_stream(stream));
+}
+
+} // extern "C"

@@ -1,0 +1,216 @@
+// rt_core.cpp -- runtime plumbing of libmi355x_rt: errors, devices, streams, memory, events,
+// pointer classification.  Replaces the CUDA driver shim of the reference
+// (ompi/mca/common/cuda/common_cuda.c: fn table :68-106, is_gpu_buffer :1687-1783,
+// cu_memcpy :1796-1846, memmove :1848-1889) with direct HIP runtime calls: HIP is linked, not
+// dlopen'ed, because this library only exists on a ROCm node.
+#include "rt_internal.hpp"
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+
+namespace mi355x {
+
+static thread_local char g_err[512] = "no error";
+
+int set_error(int code, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int device_cu_count()
+{
+    static int cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cache[dev] == 0) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            cus <= 0)
+            cus = 256;
+        cache[dev] = cus;
+    }
+    return cache[dev];
+}
+
+hipStream_t resolve_stream(void *stream)
+{
+    if (stream) return (hipStream_t)stream;
+    static thread_local hipStream_t own[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    if (!own[dev]) {
+        if (hipStreamCreateWithFlags(&own[dev], hipStreamNonBlocking) != hipSuccess)
+            own[dev] = nullptr;
+    }
+    return own[dev];
+}
+
+StreamTune &stream_tune()
+{
+    static StreamTune t;
+    return t;
+}
+
+} // namespace mi355x
+
+using namespace mi355x;
+
+extern "C" {
+
+const char *mi355x_last_error(void) { return g_err; }
+int mi355x_version(void) { return 100; }
+
+int mi355x_device_count(int *count)
+{
+    if (!count) return set_error(MI355X_ERR_ARG, "count is NULL");
+    MI_HIP(hipGetDeviceCount(count));
+    return MI355X_SUCCESS;
+}
+int mi355x_set_device(int dev)
+{
+    MI_HIP(hipSetDevice(dev));
+    return MI355X_SUCCESS;
+}
+int mi355x_get_device(int *dev)
+{
+    if (!dev) return set_error(MI355X_ERR_ARG, "dev is NULL");
+    MI_HIP(hipGetDevice(dev));
+    return MI355X_SUCCESS;
+}
+int mi355x_stream_create(void **stream)
+{
+    if (!stream) return set_error(MI355X_ERR_ARG, "stream is NULL");
+    hipStream_t s;
+    MI_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = (void *)s;
+    return MI355X_SUCCESS;
+}
+int mi355x_stream_destroy(void *stream)
+{
+    if (stream) MI_HIP(hipStreamDestroy((hipStream_t)stream));
+    return MI355X_SUCCESS;
+}
+int mi355x_stream_sync(void *stream)
+{
+    MI_HIP(hipStreamSynchronize(resolve_stream(stream)));
+    return MI355X_SUCCESS;
+}
+int mi355x_device_sync(void)
+{
+    MI_HIP(hipDeviceSynchronize());
+    return MI355X_SUCCESS;
+}
+int mi355x_malloc(void **p, size_t bytes)
+{
+    if (!p) return set_error(MI355X_ERR_ARG, "p is NULL");
+    MI_HIP(hipMalloc(p, bytes ? bytes : 1));
+    return MI355X_SUCCESS;
+}
+int mi355x_free(void *p)
+{
+    if (p) MI_HIP(hipFree(p));
+    return MI355X_SUCCESS;
+}
+int mi355x_host_alloc(void **p, size_t bytes)
+{
+    if (!p) return set_error(MI355X_ERR_ARG, "p is NULL");
+    MI_HIP(hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocDefault));
+    return MI355X_SUCCESS;
+}
+int mi355x_host_free(void *p)
+{
+    if (p) MI_HIP(hipHostFree(p));
+    return MI355X_SUCCESS;
+}
+int mi355x_memcpy(void *dst, const void *src, size_t bytes)
+{
+    if (bytes == 0) return MI355X_SUCCESS;
+    MI_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
+    return MI355X_SUCCESS;
+}
+int mi355x_memcpy_async(void *dst, const void *src, size_t bytes, void *stream)
+{
+    if (bytes == 0) return MI355X_SUCCESS;
+    MI_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, resolve_stream(stream)));
+    return MI355X_SUCCESS;
+}
+int mi355x_memset_async(void *dst, int value, size_t bytes, void *stream)
+{
+    if (bytes == 0) return MI355X_SUCCESS;
+    MI_HIP(hipMemsetAsync(dst, value, bytes, resolve_stream(stream)));
+    return MI355X_SUCCESS;
+}
+
+int mi355x_ptr_is_device(const void *p, int *is_device)
+{
+    if (!is_device) return set_error(MI355X_ERR_ARG, "is_device is NULL");
+    *is_device = 0;
+    if (!p) return MI355X_SUCCESS;
+    hipPointerAttribute_t attr;
+    std::memset(&attr, 0, sizeof(attr));
+    hipError_t e = hipPointerGetAttributes(&attr, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError(); // unregistered host memory: not an error for the caller
+        return MI355X_SUCCESS;
+    }
+    *is_device = (attr.type == hipMemoryTypeDevice) ? 1 : 0;
+    return MI355X_SUCCESS;
+}
+
+int mi355x_event_create(void **ev)
+{
+    if (!ev) return set_error(MI355X_ERR_ARG, "ev is NULL");
+    hipEvent_t e;
+    MI_HIP(hipEventCreate(&e));
+    *ev = (void *)e;
+    return MI355X_SUCCESS;
+}
+int mi355x_event_destroy(void *ev)
+{
+    if (ev) MI_HIP(hipEventDestroy((hipEvent_t)ev));
+    return MI355X_SUCCESS;
+}
+int mi355x_event_record(void *ev, void *stream)
+{
+    MI_HIP(hipEventRecord((hipEvent_t)ev, resolve_stream(stream)));
+    return MI355X_SUCCESS;
+}
+int mi355x_event_elapsed_ms(void *start, void *stop, float *ms)
+{
+    if (!ms) return set_error(MI355X_ERR_ARG, "ms is NULL");
+    MI_HIP(hipEventSynchronize((hipEvent_t)stop));
+    MI_HIP(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+    return MI355X_SUCCESS;
+}
+
+int mi355x_op_tune(int unroll, int blocks_per_cu, int nontemporal)
+{
+    StreamTune &t = stream_tune();
+    if (unroll) {
+        if (unroll != 1 && unroll != 2 && unroll != 4 && unroll != 8)
+            return set_error(MI355X_ERR_ARG, "unroll must be 1, 2, 4 or 8");
+        t.unroll = unroll;
+    }
+    if (blocks_per_cu) {
+        if (blocks_per_cu < 1 || blocks_per_cu > 64)
+            return set_error(MI355X_ERR_ARG, "blocks_per_cu out of range");
+        t.blocks_per_cu = blocks_per_cu;
+    }
+    if (nontemporal >= 0) t.nontemporal = nontemporal ? 1 : 0;
+    return MI355X_SUCCESS;
+}
+int mi355x_op_get_tune(int *unroll, int *blocks_per_cu, int *nontemporal)
+{
+    StreamTune &t = stream_tune();
+    if (unroll) *unroll = t.unroll;
+    if (blocks_per_cu) *blocks_per_cu = t.blocks_per_cu;
+    if (nontemporal) *nontemporal = t.nontemporal;
+    return MI355X_SUCCESS;
+}
+
+} // extern "C"

@@ -1,0 +1,144 @@
+"""op/hip kernels (libmi355x_rt.so, C ABI) vs the CPU oracle: every (op, type) slot, 2-buff and
+3-buff, aligned / co-misaligned / mutually misaligned operands, odd sizes, empty input.
+
+Reference semantics: ompi/mca/op/base/op_base_functions.c:39-103 (2-buff), :606-683 (3-buff).
+Bar: bit-exact (opdata.assert_same documents the two relaxations: NaN payloads of float
+SUM/PROD, padding bytes of MAXLOC pairs).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+import opdata
+
+pytestmark = pytest.mark.gpu
+
+N = 50_021  # odd: exercises head/tail handling around the 16-B vector body
+
+
+def _slots(pkg, oracle):
+    out = []
+    for op in range(1, 13):
+        for ty in range(len(pkg.TYPES)):
+            if oracle.oracle_has_op(op, ty) and pkg.op_supported(op, ty):
+                out.append((pkg.OPS[op], pkg.TYPES[ty]))
+    return out
+
+
+def _dev(torch, arr: np.ndarray, off_bytes: int = 0):
+    raw = arr.view(np.uint8).reshape(-1)
+    t = torch.zeros(raw.size + 64, dtype=torch.uint8, device="cuda")
+    t[off_bytes:off_bytes + raw.size].copy_(torch.from_numpy(raw.copy()))
+    return t, t.data_ptr() + off_bytes
+
+
+def _host(t, off_bytes, like: np.ndarray) -> np.ndarray:
+    nb = like.view(np.uint8).size
+    return t[off_bytes:off_bytes + nb].cpu().numpy().view(like.dtype).copy()
+
+
+def test_slot_coverage(gpu, pkg, oracle):
+    """every reference slot with a GPU-representable type has a kernel (108 of 116)"""
+    have, missing = 0, []
+    for op in range(15):
+        for ty in range(len(pkg.TYPES)):
+            if oracle.oracle_has_op(op, ty):
+                if pkg.op_supported(op, ty):
+                    have += 1
+                elif "LONG_DOUBLE" not in pkg.TYPES[ty]:
+                    missing.append((pkg.OPS[op], pkg.TYPES[ty]))
+    assert not missing, missing
+    assert have == 108
+
+
+@pytest.mark.parametrize("offs", [(0, 0, 0), (1, 1, 1), (1, 0, 2)], ids=["aligned", "comisaligned", "misaligned"])
+def test_all_slots(gpu, pkg, oracle, offs):
+    torch = gpu
+    bad = []
+    for opname, tname in _slots(pkg, oracle):
+        op, ty = pkg.OP[opname], pkg.T[tname]
+        esz = pkg.type_size(ty)
+        assert esz == oracle.oracle_type_size(ty)
+        a = opdata.make(tname, N, 1)
+        b = opdata.make(tname, N, 2)
+        o1, o2, o3 = (x * esz for x in offs)
+        # 3-buff
+        ta, pa = _dev(torch, a, o1)
+        tb, pb = _dev(torch, b, o2)
+        to, po = _dev(torch, np.zeros_like(a), o3)
+        pkg.op_reduce_3buff(op, ty, pa, pb, po, N, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        want = np.zeros_like(a)
+        assert oracle.oracle_op_3buff(op, ty, a.ctypes.data, b.ctypes.data, want.ctypes.data, N) == 0
+        try:
+            opdata.assert_same(tname, opname, _host(to, o3, want), want, "3buff")
+        except AssertionError as e:
+            bad.append(str(e))
+        # 2-buff: inout = b, in = a
+        tio, pio = _dev(torch, b, o2)
+        pkg.op_reduce(op, ty, pa, pio, N, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        want2 = b.copy()
+        assert oracle.oracle_op_2buff(op, ty, a.ctypes.data, want2.ctypes.data, N) == 0
+        try:
+            opdata.assert_same(tname, opname, _host(tio, o2, want2), want2, "2buff")
+        except AssertionError as e:
+            bad.append(str(e))
+    assert not bad, "\n".join(bad[:20])
+
+
+def test_small_counts(gpu, pkg, oracle):
+    """count = 0, 1, 2, 15, 16, 17 (all of the body empty or one vector)"""
+    torch = gpu
+    for n in (0, 1, 2, 15, 16, 17, 33):
+        for opname, tname in [("SUM", "FLOAT"), ("MAXLOC", "DOUBLE_INT"), ("BXOR", "INT8"), ("PROD", "C_DOUBLE_COMPLEX")]:
+            op, ty = pkg.OP[opname], pkg.T[tname]
+            a = opdata.make(tname, max(n, 1), 3)[:n]
+            b = opdata.make(tname, max(n, 1), 4)[:n]
+            ta, pa = _dev(torch, a)
+            tb, pb = _dev(torch, b)
+            pkg.op_reduce(op, ty, pa, pb, n, torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            want = b.copy()
+            oracle.oracle_op_2buff(op, ty, a.ctypes.data, want.ctypes.data, n)
+            opdata.assert_same(tname, opname, _host(tb, 0, want), want, f"n={n}")
+
+
+def test_large_fp32_sum_property(gpu, pkg):
+    """1 GiB-class buffer (BASELINE config 2 size): out = in1 + in2 on exactly-representable
+    values, checked on device against torch's own add (a size-independent property: the sum of
+    small integers is exact in any order)."""
+    torch = gpu
+    n = 1 << 28  # 268,435,456 fp32 = 1 GiB per operand
+    a = torch.randint(-1000, 1000, (n,), device="cuda", dtype=torch.int32).float()
+    b = torch.randint(-1000, 1000, (n,), device="cuda", dtype=torch.int32).float()
+    o = torch.empty_like(a)
+    pkg.op_reduce_3buff(pkg.OP["SUM"], pkg.T["FLOAT"], a.data_ptr(), b.data_ptr(), o.data_ptr(), n,
+                        torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(o, a + b)
+    del a, b, o
+    torch.cuda.empty_cache()
+
+
+def test_tune_variants_same_result(gpu, pkg):
+    torch = gpu
+    n = 3_000_017
+    a = torch.randn(n, device="cuda")
+    b = torch.randn(n, device="cuda")
+    ref = a + b
+    saved = pkg.get_tune()
+    try:
+        for u in (1, 2, 4, 8):
+            for nt in (0, 1):
+                pkg.tune(u, 4, nt)
+                o = torch.empty_like(a)
+                pkg.op_reduce_3buff(pkg.OP["SUM"], pkg.T["FLOAT"], a.data_ptr(), b.data_ptr(), o.data_ptr(), n,
+                                    torch.cuda.current_stream().cuda_stream)
+                torch.cuda.synchronize()
+                assert torch.equal(o, ref), (u, nt)
+    finally:
+        pkg.tune(*saved)

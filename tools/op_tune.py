@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""Launch-shape sweep for the op/hip streaming kernels on one MI355X (prints a JSON table).
+
+For 3-buff MPI_SUM fp32/fp64 at 1 GiB per operand: unroll x blocks_per_cu x nontemporal, median
+of 7 launches each (HIP events on the launch stream).  Then every (op,type) slot once at the
+best shape (informational GB/s sweep of BASELINE configs[1]).
+"""
+from __future__ import annotations
+
+import importlib.util
+import json
+import pathlib
+import statistics
+import sys
+
+REPO = pathlib.Path(__file__).resolve().parents[1]
+spec = importlib.util.spec_from_file_location("ompi_release_amd", REPO / "ompi-release_amd" / "__init__.py")
+pkg = importlib.util.module_from_spec(spec)
+sys.modules["ompi_release_amd"] = pkg
+spec.loader.exec_module(pkg)
+
+import torch  # noqa: E402
+
+
+def time_launch(fn, reps=7):
+    s = torch.cuda.current_stream()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        fn()
+        b.record(s)
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    return statistics.median(ts)
+
+
+def main():
+    pkg.rt()
+    sh = torch.cuda.current_stream().cuda_stream
+    out = {"shape_sweep": [], "slot_sweep": []}
+    nbytes = 1 << 30
+    x = torch.empty(nbytes, dtype=torch.uint8, device="cuda").random_()
+    y = torch.empty(nbytes, dtype=torch.uint8, device="cuda").random_()
+    z = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    px, py, pz = x.data_ptr(), y.data_ptr(), z.data_ptr()
+    best = (0, None)
+    for tname in ("FLOAT", "DOUBLE"):
+        ty = pkg.T[tname]
+        n = nbytes // pkg.type_size(ty)
+        for u in (1, 2, 4, 8):
+            for bpc in (2, 4, 8, 16, 32):
+                for nt in (0, 1):
+                    pkg.tune(u, bpc, nt)
+                    f = lambda: pkg.op_reduce_3buff(pkg.OP["SUM"], ty, px, py, pz, n, sh)
+                    f()
+                    ms = time_launch(f)
+                    gbs = 3 * nbytes / (ms * 1e-3) / 1e9
+                    out["shape_sweep"].append({"type": tname, "unroll": u, "blocks_per_cu": bpc, "nt": nt,
+                                               "ms": round(ms, 4), "GBps": round(gbs, 1)})
+                    if tname == "FLOAT" and gbs > best[0]:
+                        best = (gbs, (u, bpc, nt))
+                    print(json.dumps(out["shape_sweep"][-1]), flush=True)
+    pkg.tune(*best[1])
+    out["best"] = {"GBps": round(best[0], 1), "unroll": best[1][0], "blocks_per_cu": best[1][1], "nt": best[1][2]}
+    for op in range(1, 13):
+        for ty in range(len(pkg.TYPES)):
+            if not pkg.op_supported(op, ty):
+                continue
+            n = nbytes // pkg.type_size(ty)
+            f3 = lambda: pkg.op_reduce_3buff(op, ty, px, py, pz, n, sh)
+            f2 = lambda: pkg.op_reduce(op, ty, px, pz, n, sh)
+            f3()
+            ms3 = time_launch(f3, 3)
+            ms2 = time_launch(f2, 3)
+            out["slot_sweep"].append({"op": pkg.OPS[op], "type": pkg.TYPES[ty],
+                                      "GBps_3buff": round(3 * nbytes / (ms3 * 1e-3) / 1e9, 1),
+                                      "GBps_2buff": round(3 * nbytes / (ms2 * 1e-3) / 1e9, 1)})
+            print(json.dumps(out["slot_sweep"][-1]), flush=True)
+    print("RESULT " + json.dumps(out["best"]))
+    p = REPO / "gpurun_out" / "op_tune.json"
+    p.parent.mkdir(exist_ok=True)
+    p.write_text(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
