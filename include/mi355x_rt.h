@@ -10,7 +10,7 @@
  *   - the tuned schedules on device buffers, coll/cuda staging   coll_cuda_allreduce.c:30-77
  *                                  (mi355x_coll_*)
  * Plain C types only: pointers, sizes, ints.  `stream` is a hipStream_t passed as void*; NULL
- * means the library's own per-thread stream.  Every function returns MI355X_SUCCESS (0) or a
+ * is the HIP default (null) stream.  Every function returns MI355X_SUCCESS (0) or a
  * negative mi355x_status; mi355x_last_error() gives the text of the last failure.
  * Nothing here falls back to the CPU: when no GPU / no HIP runtime is present the calls fail
  * with MI355X_ERR_HIP.
@@ -75,6 +75,60 @@ int mi355x_op_reduce_3buff(int op, int type, const void *in1, const void *in2, v
  * always run unroll 4, temporal. */
 int mi355x_op_tune(int unroll, int blocks_per_cu, int nontemporal);
 int mi355x_op_get_tune(int *unroll, int *blocks_per_cu, int *nontemporal);
+/* grid shape: 0 = persistent grid-stride (blocks_per_cu x CUs), 1 = one-shot chunked grid */
+int mi355x_op_set_mode(int mode);
+int mi355x_op_get_mode(void);
+
+
+/* ---------------------------------------------------------------- coll/mi355x engine */
+/* A communicator of `size` ranks on one node, one process (or, for tests, one thread) per rank
+ * and GPU.  Buffers are exchanged per call through hipIpcGetMemHandle / hipIpcOpenMemHandle
+ * (cached), and every collective is blocking: it returns once the result is in place and no peer
+ * still reads this rank's buffers.  `stream` orders the call after the caller's prior work on
+ * that stream.  Results replicate the reference coll/tuned (+ coll/basic) schedule's operand
+ * order per element, so they are bit-identical to the reference's for the same algorithm. */
+typedef struct mi355x_comm mi355x_comm_t;
+
+/* Multi-process: every rank calls with the same `key` (node-unique, e.g. job id + comm id). */
+int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_comm_t **comm);
+/* In-process: `size` communicator handles over one device; rank r must be driven from its own
+ * thread (the collectives block until every rank has joined). */
+int mi355x_comm_create_loopback(int size, int device, mi355x_comm_t **comms);
+int mi355x_comm_destroy(mi355x_comm_t *comm);
+int mi355x_comm_rank(const mi355x_comm_t *comm);
+int mi355x_comm_size(const mi355x_comm_t *comm);
+int mi355x_comm_barrier(mi355x_comm_t *comm);
+/* algorithm id of the last collective (AR_*: 1 linear, 2 nonoverlapping, 3 recursive doubling,
+ * 4 ring, 5 segmented ring; reduce: 1 linear .. 5 binomial; reduce_scatter: 1 rec. halving, 2 ring) */
+int mi355x_comm_last_algorithm(const mi355x_comm_t *comm);
+
+enum mi355x_knob {
+    MI355X_KNOB_ALLREDUCE_ALG = 1,      /* coll_tuned_allreduce_algorithm (0 = decision) */
+    MI355X_KNOB_REDUCE_ALG = 2,         /* coll_tuned_reduce_algorithm, used by reduce_scatter_block */
+    MI355X_KNOB_REDUCE_SCATTER_ALG = 3, /* coll_tuned_reduce_scatter_algorithm */
+    MI355X_KNOB_BLOCKS_PER_CU = 4,
+    MI355X_KNOB_TIMEOUT_S = 5
+};
+int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
+
+/* MPI_Allreduce.  sbuf == NULL means MPI_IN_PLACE.  Replaces coll_cuda_allreduce.c:30-77 +
+ * ompi_coll_tuned_allreduce_intra_dec_fixed (coll_tuned_decision_fixed.c:42-85). */
+int mi355x_allreduce(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op,
+                     void *stream);
+/* MPI_Reduce_scatter_block: coll_basic_reduce_scatter_block.c:54-111 order. */
+int mi355x_reduce_scatter_block(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t rcount,
+                                int type, int op, void *stream);
+/* MPI_Reduce_scatter: ompi_coll_tuned_reduce_scatter_intra_dec_fixed order (decision_fixed.c:456-502). */
+int mi355x_reduce_scatter(mi355x_comm_t *comm, const void *sbuf, void *rbuf, const int *rcounts,
+                          int type, int op, void *stream);
+/* MPI_Allgather of `bytes` contiguous bytes per rank (sbuf NULL = MPI_IN_PLACE). */
+int mi355x_allgather(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t bytes, void *stream);
+/* MPI_Bcast of `bytes` contiguous bytes from `root`. */
+int mi355x_bcast(mi355x_comm_t *comm, void *buf, size_t bytes, int root, void *stream);
+
+/* Host-only introspection of the schedule compiler: the per-element program the engine runs for
+ * a given reference algorithm (layout documented in coll_comm.cpp).  For tests; no GPU needed. */
+int mi355x_sched_program(int kind, int n, int alg, int block, int *out, int cap);
 
 #ifdef __cplusplus
 }

@@ -93,6 +93,22 @@ def _declare(lib: ctypes.CDLL) -> None:
         "mi355x_op_reduce_3buff": (i, [i, i, vp, vp, vp, sz, vp]),
         "mi355x_op_tune": (i, [i, i, i]),
         "mi355x_op_get_tune": (i, [c.POINTER(i), c.POINTER(i), c.POINTER(i)]),
+        "mi355x_op_set_mode": (i, [i]),
+        "mi355x_op_get_mode": (i, []),
+        "mi355x_comm_create": (i, [c.c_char_p, i, i, i, c.POINTER(vp)]),
+        "mi355x_comm_create_loopback": (i, [i, i, c.POINTER(vp)]),
+        "mi355x_comm_destroy": (i, [vp]),
+        "mi355x_comm_rank": (i, [vp]),
+        "mi355x_comm_size": (i, [vp]),
+        "mi355x_comm_barrier": (i, [vp]),
+        "mi355x_comm_last_algorithm": (i, [vp]),
+        "mi355x_comm_set": (i, [vp, i, c.c_long]),
+        "mi355x_allreduce": (i, [vp, vp, vp, sz, i, i, vp]),
+        "mi355x_reduce_scatter_block": (i, [vp, vp, vp, sz, i, i, vp]),
+        "mi355x_reduce_scatter": (i, [vp, vp, vp, c.POINTER(i), i, i, vp]),
+        "mi355x_allgather": (i, [vp, vp, vp, sz, vp]),
+        "mi355x_bcast": (i, [vp, vp, sz, i, vp]),
+        "mi355x_sched_program": (i, [i, i, i, i, c.POINTER(i), i]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name, None)
@@ -130,10 +146,90 @@ def tune(unroll: int = 0, blocks_per_cu: int = 0, nontemporal: int = -1) -> None
     check(rt().mi355x_op_tune(unroll, blocks_per_cu, nontemporal), "mi355x_op_tune")
 
 
+def set_mode(mode: int) -> None:
+    check(rt().mi355x_op_set_mode(mode), "mi355x_op_set_mode")
+
+
+def get_mode() -> int:
+    return int(rt().mi355x_op_get_mode())
+
+
 def get_tune() -> tuple[int, int, int]:
     a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     check(rt().mi355x_op_get_tune(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
     return a.value, b.value, c.value
+
+
+# ---------------------------------------------------------------- coll/mi355x engine
+KNOB = {"ALLREDUCE_ALG": 1, "REDUCE_ALG": 2, "REDUCE_SCATTER_ALG": 3, "BLOCKS_PER_CU": 4, "TIMEOUT_S": 5}
+AR_ALG = {"DECISION": 0, "LINEAR": 1, "NONOVERLAPPING": 2, "RECURSIVE_DOUBLING": 3, "RING": 4,
+          "RING_SEGMENTED": 5}
+
+
+class Comm:
+    """A coll/mi355x communicator handle (multi-process via a node-local key, or one loopback
+    rank).  Methods mirror the MPI calls; buffers are device pointers (ints)."""
+
+    def __init__(self, handle: int):
+        self.h = ctypes.c_void_p(handle)
+
+    @classmethod
+    def create(cls, key: str, rank: int, size: int, device: int) -> "Comm":
+        h = ctypes.c_void_p()
+        check(rt().mi355x_comm_create(key.encode(), rank, size, device, ctypes.byref(h)), "mi355x_comm_create")
+        return cls(h.value)
+
+    @classmethod
+    def loopback(cls, size: int, device: int = 0) -> list["Comm"]:
+        arr = (ctypes.c_void_p * size)()
+        check(rt().mi355x_comm_create_loopback(size, device, arr), "mi355x_comm_create_loopback")
+        return [cls(arr[i]) for i in range(size)]
+
+    def destroy(self) -> None:
+        if self.h:
+            rt().mi355x_comm_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    @property
+    def rank(self) -> int:
+        return rt().mi355x_comm_rank(self.h)
+
+    @property
+    def size(self) -> int:
+        return rt().mi355x_comm_size(self.h)
+
+    def barrier(self) -> None:
+        check(rt().mi355x_comm_barrier(self.h), "mi355x_comm_barrier")
+
+    def last_algorithm(self) -> int:
+        return rt().mi355x_comm_last_algorithm(self.h)
+
+    def set(self, knob: str, value: int) -> None:
+        check(rt().mi355x_comm_set(self.h, KNOB[knob], value), "mi355x_comm_set")
+
+    def allreduce(self, sbuf, rbuf, count, ty, op, stream=None) -> None:
+        check(rt().mi355x_allreduce(self.h, sbuf, rbuf, count, ty, op, stream), "mi355x_allreduce")
+
+    def reduce_scatter_block(self, sbuf, rbuf, rcount, ty, op, stream=None) -> None:
+        check(rt().mi355x_reduce_scatter_block(self.h, sbuf, rbuf, rcount, ty, op, stream),
+              "mi355x_reduce_scatter_block")
+
+    def reduce_scatter(self, sbuf, rbuf, rcounts, ty, op, stream=None) -> None:
+        arr = (ctypes.c_int * len(rcounts))(*rcounts)
+        check(rt().mi355x_reduce_scatter(self.h, sbuf, rbuf, arr, ty, op, stream), "mi355x_reduce_scatter")
+
+    def allgather(self, sbuf, rbuf, nbytes, stream=None) -> None:
+        check(rt().mi355x_allgather(self.h, sbuf, rbuf, nbytes, stream), "mi355x_allgather")
+
+    def bcast(self, buf, nbytes, root, stream=None) -> None:
+        check(rt().mi355x_bcast(self.h, buf, nbytes, root, stream), "mi355x_bcast")
+
+
+def sched_program(kind: int, n: int, alg: int, block: int) -> list[int]:
+    buf = (ctypes.c_int * 4096)()
+    k = rt().mi355x_sched_program(kind, n, alg, block, buf, 4096)
+    check(0 if k >= 0 else k, "mi355x_sched_program")
+    return list(buf[:k])
 
 
 def env_flag(name: str, default: str = "") -> str:

@@ -1,0 +1,702 @@
+// coll_comm.cpp -- host side of the coll/mi355x engine: node-local bootstrap, barrier, IPC
+// registration cache, and the device-buffer collectives.
+//
+// Transport (replaces the PML/BTL path the reference takes for device buffers: coll/cuda host
+// staging, coll_cuda_allreduce.c:30-77, and smcuda CUDA-IPC RDMA, btl/smcuda/README:13-113):
+//   * ranks on one node share a small control segment (POSIX shm, or process memory for the
+//     in-process "loopback" communicator used by tests);
+//   * per call each rank publishes the IPC handle + offset of its buffers (hipIpcGetMemHandle on
+//     the allocation base, cached per base: the reference's mpool/rgpusm registration cache,
+//     common_cuda.c:971-1137); peers map them once (hipIpcOpenMemHandle, cached per handle);
+//   * one kernel per rank then reads every rank's input directly over xGMI, folds it in the
+//     reference schedule's order (coll_sched.cpp) and pushes the result into every destination.
+// A call is: sync caller stream -> publish -> barrier -> kernel -> sync -> barrier.  Blocking,
+// like the MPI calls it implements.
+#include <fcntl.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <array>
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "coll_internal.hpp"
+#include "coll_sched.hpp"
+#include "rt_internal.hpp"
+
+namespace mi355x {
+
+CollTune &coll_tune()
+{
+    static CollTune t;
+    return t;
+}
+
+constexpr uint64_t kMagic = 0x4d49333535584331ull;  // "MI355XC1"
+constexpr int kMaxBufs = 3;
+
+struct BufDesc {
+    hipIpcMemHandle_t h;
+    uint64_t off;
+    uint64_t raw;      // loopback: the pointer itself
+    uint64_t present;  // 0: NULL buffer
+};
+
+struct alignas(64) RankSlot {
+    std::atomic<uint64_t> seq;
+    int32_t pid, dev, nbuf, pad;
+    uint64_t sig[4];
+    BufDesc buf[kMaxBufs];
+};
+
+struct Ctrl {
+    uint64_t magic;
+    uint32_t size;
+    uint32_t pad0;
+    alignas(64) std::atomic<uint32_t> attached;
+    alignas(64) std::atomic<uint64_t> bar_count;
+    alignas(64) std::atomic<uint64_t> bar_gen;
+    alignas(64) std::atomic<uint32_t> abort_flag;
+    alignas(64) RankSlot slot[1];
+};
+
+static size_t ctrl_bytes(int size) { return sizeof(Ctrl) + sizeof(RankSlot) * (size_t)(size - 1); }
+
+struct HandleKey {
+    int peer;
+    std::array<char, sizeof(hipIpcMemHandle_t)> h;
+    bool operator<(const HandleKey &o) const
+    {
+        if (peer != o.peer) return peer < o.peer;
+        return h < o.h;
+    }
+};
+
+struct LocalReg {
+    uintptr_t base;
+    size_t size;
+    hipIpcMemHandle_t h;
+};
+
+struct LoopShared {
+    Ctrl *ctrl = nullptr;
+    int refs = 0;
+    std::mutex mtx;
+};
+
+} // namespace mi355x
+
+struct mi355x_comm {
+    int rank = 0, size = 1, device = 0;
+    mi355x::Ctrl *ctrl = nullptr;
+    bool loopback = false;
+    std::shared_ptr<mi355x::LoopShared> loop;
+    std::string shm_name;
+    uint64_t seq = 0;
+    std::map<mi355x::HandleKey, void *> peer_maps;
+    std::vector<mi355x::LocalReg> local_regs;
+    void *scratch = nullptr;
+    size_t scratch_bytes = 0;
+    int knob_allreduce = 0, knob_reduce = 0, knob_rs = 0;
+    int last_alg = -1;
+    double timeout_s = 600.0;
+};
+
+namespace mi355x {
+
+// ----------------------------------------------------------------- barrier
+static int barrier(mi355x_comm *c)
+{
+    if (c->size == 1) return MI355X_SUCCESS;
+    Ctrl *k = c->ctrl;
+    const uint64_t gen = k->bar_gen.load(std::memory_order_acquire);
+    if (k->bar_count.fetch_add(1, std::memory_order_acq_rel) == (uint64_t)c->size - 1) {
+        k->bar_count.store(0, std::memory_order_relaxed);
+        k->bar_gen.fetch_add(1, std::memory_order_release);
+        return MI355X_SUCCESS;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    unsigned spins = 0;
+    while (k->bar_gen.load(std::memory_order_acquire) == gen) {
+        if (k->abort_flag.load(std::memory_order_relaxed))
+            return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
+        if (++spins > 2048) {
+            sched_yield();
+            if ((spins & 0xffff) == 0) {
+                const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                if (el > c->timeout_s) {
+                    k->abort_flag.store(1);
+                    return set_error(MI355X_ERR_TIMEOUT, "barrier timed out after %.0f s (rank %d)", el, c->rank);
+                }
+            }
+        }
+    }
+    return MI355X_SUCCESS;
+}
+
+// ----------------------------------------------------------------- registration
+static int local_handle(mi355x_comm *c, const void *p, BufDesc *d)
+{
+    std::memset(d, 0, sizeof(*d));
+    if (!p) return MI355X_SUCCESS;
+    d->present = 1;
+    if (c->loopback) {
+        d->raw = (uint64_t)(uintptr_t)p;
+        return MI355X_SUCCESS;
+    }
+    const uintptr_t up = (uintptr_t)p;
+    for (const LocalReg &r : c->local_regs) {
+        if (up >= r.base && up < r.base + r.size) {
+            d->h = r.h;
+            d->off = up - r.base;
+            return MI355X_SUCCESS;
+        }
+    }
+    void *base = nullptr;
+    size_t sz = 0;
+    MI_HIP(hipMemGetAddressRange(&base, &sz, (void *)p));
+    LocalReg reg;
+    reg.base = (uintptr_t)base;
+    reg.size = sz;
+    MI_HIP(hipIpcGetMemHandle(&reg.h, base));
+    c->local_regs.push_back(reg);
+    d->h = reg.h;
+    d->off = up - reg.base;
+    return MI355X_SUCCESS;
+}
+
+static int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out)
+{
+    *out = nullptr;
+    if (!d.present) return MI355X_SUCCESS;
+    if (c->loopback) {
+        *out = (void *)(uintptr_t)d.raw;
+        return MI355X_SUCCESS;
+    }
+    HandleKey key;
+    key.peer = peer;
+    std::memcpy(key.h.data(), &d.h, sizeof(d.h));
+    auto it = c->peer_maps.find(key);
+    void *base;
+    if (it != c->peer_maps.end()) {
+        base = it->second;
+    } else {
+        hipError_t e = hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess)
+            return set_error(MI355X_ERR_PEER, "hipIpcOpenMemHandle(rank %d): %s", peer, hipGetErrorString(e));
+        c->peer_maps[key] = base;
+    }
+    *out = (char *)base + d.off;
+    return MI355X_SUCCESS;
+}
+
+// Publish nbuf local buffers, meet every rank, and resolve every rank's buffers:
+// peers[b][r] = rank r's buffer b mapped into this process.
+static int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t sig[4],
+                    std::vector<std::vector<void *>> &peers)
+{
+    c->seq++;
+    RankSlot &s = c->ctrl->slot[c->rank];
+    for (int b = 0; b < nbuf; ++b) {
+        int rc = local_handle(c, mine[b], &s.buf[b]);
+        if (rc) return rc;
+    }
+    s.nbuf = nbuf;
+    for (int i = 0; i < 4; ++i) s.sig[i] = sig[i];
+    s.seq.store(c->seq, std::memory_order_release);
+    int rc = barrier(c);
+    if (rc) return rc;
+    peers.assign(nbuf, std::vector<void *>(c->size, nullptr));
+    for (int r = 0; r < c->size; ++r) {
+        RankSlot &o = c->ctrl->slot[r];
+        if (o.seq.load(std::memory_order_acquire) != c->seq)
+            return set_error(MI355X_ERR_PEER, "rank %d is in call %llu, rank %d in call %llu", r,
+                             (unsigned long long)o.seq.load(), c->rank, (unsigned long long)c->seq);
+        if (o.sig[0] != sig[0] || o.sig[1] != sig[1] || o.sig[2] != sig[2] || o.sig[3] != sig[3])
+            return set_error(MI355X_ERR_ARG, "collective arguments differ between rank %d and rank %d", r, c->rank);
+        for (int b = 0; b < nbuf; ++b) {
+            if (r == c->rank) {
+                peers[b][r] = const_cast<void *>(mine[b]);
+            } else {
+                rc = map_peer(c, r, o.buf[b], &peers[b][r]);
+                if (rc) return rc;
+            }
+        }
+    }
+    return MI355X_SUCCESS;
+}
+
+static int finish(mi355x_comm *c, hipStream_t s)
+{
+    MI_HIP(hipStreamSynchronize(s));
+    return barrier(c);
+}
+
+static int ensure_scratch(mi355x_comm *c, size_t bytes)
+{
+    if (c->scratch_bytes >= bytes) return MI355X_SUCCESS;
+    if (c->scratch) MI_HIP(hipFree(c->scratch));
+    c->scratch = nullptr;
+    c->scratch_bytes = 0;
+    MI_HIP(hipMalloc(&c->scratch, bytes ? bytes : 1));
+    c->scratch_bytes = bytes;
+    return MI355X_SUCCESS;
+}
+
+// ----------------------------------------------------------------- program launch
+// Evaluate `pr` on elements [off, off+len) of every rank's input `in[q]`, writing dst[d] + off.
+static int run_program(int op, int type, const Program &pr, const std::vector<void *> &in,
+                       const std::vector<void *> &dst, size_t off, size_t len, hipStream_t s)
+{
+    if (len == 0) return MI355X_SUCCESS;
+    const size_t esz = mi355x_type_size(type);
+    if ((int)dst.size() > kMaxRanks || (int)in.size() > kMaxRanks)
+        return set_error(MI355X_ERR_UNSUPPORTED, "communicator larger than %d ranks", kMaxRanks);
+    if (pr.is_fold) {
+        FoldArgs a;
+        std::memset(&a, 0, sizeof(a));
+        for (size_t q = 0; q < in.size(); ++q) a.src[q] = (const char *)in[q] + off * esz;
+        for (size_t d = 0; d < dst.size(); ++d) a.dst[d] = (char *)dst[d] + off * esz;
+        a.nr = (int)pr.order.size();
+        for (int j = 0; j < a.nr; ++j) a.order[j] = pr.order[j];
+        a.role_mask = pr.role_mask;
+        a.nd = (int)dst.size();
+        a.n = len;
+        return launch_fold_slot(op, type, a, s);
+    }
+    if ((int)in.size() > kTreeMax) return set_error(MI355X_ERR_UNSUPPORTED, "tree program over > %d ranks", kTreeMax);
+    TreeArgs t;
+    std::memset(&t, 0, sizeof(t));
+    for (size_t q = 0; q < in.size(); ++q) t.src[q] = (const char *)in[q] + off * esz;
+    for (size_t d = 0; d < dst.size(); ++d) t.dst[d] = (char *)dst[d] + off * esz;
+    t.nr = (int)in.size();
+    t.nd = (int)dst.size();
+    t.nsteps = (int)pr.steps.size();
+    for (int k = 0; k < t.nsteps; ++k) t.steps[k] = pr.steps[k];
+    t.result = pr.result;
+    t.n = len;
+    return launch_tree_slot(op, type, t, s);
+}
+
+static int check_common(mi355x_comm *c, int op, int type)
+{
+    if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    if (!mi355x_op_supported(op, type))
+        return set_error(MI355X_ERR_UNSUPPORTED, "no GPU kernel for op %d type %d", op, type);
+    return MI355X_SUCCESS;
+}
+
+static double env_double(const char *name, double dflt)
+{
+    const char *v = getenv(name);
+    return v ? atof(v) : dflt;
+}
+
+} // namespace mi355x
+
+using namespace mi355x;
+
+extern "C" {
+
+int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_comm_t **out)
+{
+    if (!key || !out || size < 1 || size > kMaxRanks || rank < 0 || rank >= size)
+        return set_error(MI355X_ERR_ARG, "bad comm_create arguments");
+    *out = nullptr;
+    MI_HIP(hipSetDevice(device));
+    auto *c = new mi355x_comm();
+    c->rank = rank;
+    c->size = size;
+    c->device = device;
+    c->timeout_s = env_double("MI355X_TIMEOUT_S", 600.0);
+    c->shm_name = std::string("/mi355x_") + key;
+    for (char &ch : c->shm_name)
+        if (ch != '/' && !isalnum((unsigned char)ch) && ch != '_' && ch != '-') ch = '_';
+    const size_t bytes = ctrl_bytes(size);
+    int fd = -1;
+    if (rank == 0) {
+        shm_unlink(c->shm_name.c_str());
+        fd = shm_open(c->shm_name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd < 0 || ftruncate(fd, (off_t)bytes) != 0) {
+            if (fd >= 0) close(fd);
+            delete c;
+            return set_error(MI355X_ERR_PEER, "shm_open(%s) failed", key);
+        }
+    } else {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            fd = shm_open(c->shm_name.c_str(), O_RDWR, 0600);
+            if (fd >= 0) {
+                struct stat st;
+                if (fstat(fd, &st) == 0 && (size_t)st.st_size >= bytes) break;
+                close(fd);
+                fd = -1;
+            }
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
+                delete c;
+                return set_error(MI355X_ERR_TIMEOUT, "rank %d: control segment %s never appeared", rank, key);
+            }
+            usleep(1000);
+        }
+    }
+    void *m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) {
+        delete c;
+        return set_error(MI355X_ERR_PEER, "mmap of the control segment failed");
+    }
+    c->ctrl = (Ctrl *)m;
+    if (rank == 0) {
+        std::memset(m, 0, bytes);
+        c->ctrl->size = (uint32_t)size;
+        std::atomic_thread_fence(std::memory_order_release);
+        __atomic_store_n(&c->ctrl->magic, kMagic, __ATOMIC_RELEASE);
+    } else {
+        const auto t0 = std::chrono::steady_clock::now();
+        while (__atomic_load_n(&c->ctrl->magic, __ATOMIC_ACQUIRE) != kMagic) {
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
+                munmap(m, bytes);
+                delete c;
+                return set_error(MI355X_ERR_TIMEOUT, "rank %d: control segment never initialised", rank);
+            }
+            usleep(200);
+        }
+    }
+    c->ctrl->slot[rank].pid = (int32_t)getpid();
+    c->ctrl->slot[rank].dev = device;
+    c->ctrl->attached.fetch_add(1);
+    int rc = barrier(c);  // everybody mapped the segment: its name can go
+    if (rank == 0) shm_unlink(c->shm_name.c_str());
+    if (rc) {
+        munmap(m, bytes);
+        delete c;
+        return rc;
+    }
+    *out = c;
+    return MI355X_SUCCESS;
+}
+
+int mi355x_comm_create_loopback(int size, int device, mi355x_comm_t **comms)
+{
+    if (!comms || size < 1 || size > kMaxRanks) return set_error(MI355X_ERR_ARG, "bad loopback arguments");
+    MI_HIP(hipSetDevice(device));
+    auto shared = std::make_shared<LoopShared>();
+    shared->ctrl = (Ctrl *)calloc(1, ctrl_bytes(size));
+    if (!shared->ctrl) return set_error(MI355X_ERR_NOMEM, "calloc");
+    shared->ctrl->magic = kMagic;
+    shared->ctrl->size = (uint32_t)size;
+    for (int r = 0; r < size; ++r) {
+        auto *c = new mi355x_comm();
+        c->rank = r;
+        c->size = size;
+        c->device = device;
+        c->ctrl = shared->ctrl;
+        c->loopback = true;
+        c->loop = shared;
+        c->timeout_s = env_double("MI355X_TIMEOUT_S", 600.0);
+        shared->refs++;
+        comms[r] = c;
+    }
+    return MI355X_SUCCESS;
+}
+
+int mi355x_comm_destroy(mi355x_comm_t *c)
+{
+    if (!c) return MI355X_SUCCESS;
+    (void)hipSetDevice(c->device);
+    for (auto &kv : c->peer_maps) (void)hipIpcCloseMemHandle(kv.second);
+    if (c->scratch) (void)hipFree(c->scratch);
+    if (c->loopback) {
+        std::lock_guard<std::mutex> g(c->loop->mtx);
+        if (--c->loop->refs == 0) free(c->loop->ctrl);
+    } else if (c->ctrl) {
+        munmap(c->ctrl, ctrl_bytes(c->size));
+    }
+    delete c;
+    return MI355X_SUCCESS;
+}
+
+int mi355x_comm_rank(const mi355x_comm_t *c) { return c ? c->rank : -1; }
+int mi355x_comm_size(const mi355x_comm_t *c) { return c ? c->size : -1; }
+int mi355x_comm_barrier(mi355x_comm_t *c) { return c ? barrier(c) : set_error(MI355X_ERR_ARG, "comm is NULL"); }
+int mi355x_comm_last_algorithm(const mi355x_comm_t *c) { return c ? c->last_alg : -1; }
+
+int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
+{
+    if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    switch (knob) {
+    case MI355X_KNOB_ALLREDUCE_ALG: c->knob_allreduce = (int)value; break;
+    case MI355X_KNOB_REDUCE_ALG: c->knob_reduce = (int)value; break;
+    case MI355X_KNOB_REDUCE_SCATTER_ALG: c->knob_rs = (int)value; break;
+    case MI355X_KNOB_BLOCKS_PER_CU:
+        if (value < 1 || value > 64) return set_error(MI355X_ERR_ARG, "blocks_per_cu out of range");
+        coll_tune().blocks_per_cu = (int)value;
+        break;
+    case MI355X_KNOB_TIMEOUT_S: c->timeout_s = (double)value; break;
+    default: return set_error(MI355X_ERR_ARG, "unknown knob %d", knob);
+    }
+    return MI355X_SUCCESS;
+}
+
+// Describe the per-element program the engine runs (host only, no GPU needed).  Layout:
+//   fold: [1, nr, len, order[0..len-1], role[0..len-1]]
+//   tree: [0, nr, nsteps, result, (dst, out, in) x nsteps]
+// kind 1: allreduce (alg 3 = recursive doubling, 4/5 = ring block `block`,
+//                    1/2 = reduce-to-0 with reduce algorithm `block` (1..5) + bcast)
+// kind 2: reduce to rank 0 with reduce algorithm `alg`;  kind 3: reduce_scatter ring block;
+// kind 4: reduce_scatter recursive halving block.  Returns the number of ints written or < 0.
+int mi355x_sched_program(int kind, int n, int alg, int block, int *out, int cap)
+{
+    if (!out || n < 1 || n > kMaxRanks) return set_error(MI355X_ERR_ARG, "bad arguments");
+    Program pr;
+    ExprPool ep;
+    bool ok = true;
+    switch (kind) {
+    case 1:
+        if (alg == AR_RING || alg == AR_RING_SEGMENTED) pr = ring_block_program(n, block);
+        else if (alg == AR_RECDBL) ok = compile_expr(ep, expr_allreduce_recursive_doubling(ep, n), n, &pr);
+        else ok = compile_expr(ep, expr_reduce(ep, block, n, 0), n, &pr);
+        break;
+    case 2: ok = compile_expr(ep, expr_reduce(ep, alg, n, 0), n, &pr); break;
+    case 3: pr = reduce_scatter_ring_block_program(n, block); break;
+    case 4: {
+        std::vector<int> roots = expr_reduce_scatter_rechalving(ep, n);
+        ok = compile_expr(ep, roots[block], n, &pr);
+        break;
+    }
+    default: return set_error(MI355X_ERR_ARG, "unknown kind %d", kind);
+    }
+    if (!ok) return set_error(MI355X_ERR_UNSUPPORTED, "schedule does not compile");
+    std::vector<int> v;
+    if (pr.is_fold) {
+        v = {1, pr.nr, (int)pr.order.size()};
+        for (int r : pr.order) v.push_back(r);
+        for (size_t j = 0; j < pr.order.size(); ++j) v.push_back((int)((pr.role_mask >> j) & 1u));
+    } else {
+        v = {0, pr.nr, (int)pr.steps.size(), pr.result};
+        for (const TreeStep &t : pr.steps) {
+            v.push_back(t.dst);
+            v.push_back(t.out);
+            v.push_back(t.in);
+        }
+    }
+    if ((int)v.size() > cap) return set_error(MI355X_ERR_ARG, "cap too small");
+    for (size_t i = 0; i < v.size(); ++i) out[i] = v[i];
+    return (int)v.size();
+}
+
+// MPI_Allreduce (coll_tuned_allreduce_intra_dec_fixed order; sbuf NULL = MPI_IN_PLACE)
+int mi355x_allreduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op,
+                     void *stream)
+{
+    int rc = check_common(c, op, type);
+    if (rc) return rc;
+    if (count == 0) return MI355X_SUCCESS;
+    hipStream_t s = resolve_stream(stream);
+    const size_t esz = mi355x_type_size(type);
+    const void *in = sbuf ? sbuf : rbuf;
+    if (c->size == 1) {
+        c->last_alg = AR_RING;
+        if (sbuf && sbuf != rbuf) MI_HIP(hipMemcpyAsync(rbuf, sbuf, count * esz, hipMemcpyDeviceToDevice, s));
+        MI_HIP(hipStreamSynchronize(s));
+        return MI355X_SUCCESS;
+    }
+    int alg = c->knob_allreduce ? c->knob_allreduce : allreduce_decision(c->size, count, esz);
+    if ((alg == AR_RING || alg == AR_RING_SEGMENTED) && count < (size_t)c->size) alg = AR_RECDBL;
+    c->last_alg = alg;
+    MI_HIP(hipStreamSynchronize(s));  // every rank's input is complete before it is published
+    const void *mine[2] = {in, rbuf};
+    const uint64_t sig[4] = {1, count, (uint64_t)type, (uint64_t)op};
+    std::vector<std::vector<void *>> P;
+    rc = exchange(c, 2, mine, sig, P);
+    if (rc) return rc;
+    size_t off, len;
+    ring_block(count, c->size, c->rank, &off, &len);
+    Program pr;
+    if (alg == AR_RING || alg == AR_RING_SEGMENTED) {
+        // segmented ring splits each ring block into phases but keeps the block's fold order
+        pr = ring_block_program(c->size, c->rank);
+    } else {
+        ExprPool ep;
+        int root;
+        if (alg == AR_RECDBL) {
+            root = expr_allreduce_recursive_doubling(ep, c->size);
+        } else {
+            // nonoverlapping / linear: reduce to 0 (tuned decision) then bcast (:67-100, :897-929)
+            const int ra = (alg == AR_LINEAR) ? RED_LINEAR : reduce_decision(c->size, count, esz);
+            root = expr_reduce(ep, ra, c->size, 0);
+        }
+        if (!compile_expr(ep, root, c->size, &pr)) return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
+    }
+    rc = run_program(op, type, pr, P[0], P[1], off, len, s);
+    if (rc) return rc;
+    return finish(c, s);
+}
+
+// MPI_Reduce_scatter_block as coll/basic runs it: tuned reduce to 0 + scatter
+// (coll_basic_reduce_scatter_block.c:54-111); sbuf NULL = MPI_IN_PLACE (input in rbuf).
+int mi355x_reduce_scatter_block(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t rcount, int type,
+                                int op, void *stream)
+{
+    int rc = check_common(c, op, type);
+    if (rc) return rc;
+    const size_t count = rcount * (size_t)c->size;
+    if (count == 0) return MI355X_SUCCESS;
+    hipStream_t s = resolve_stream(stream);
+    const size_t esz = mi355x_type_size(type);
+    const void *in = sbuf ? sbuf : rbuf;
+    const int ra = c->knob_reduce ? c->knob_reduce : reduce_decision(c->size, count, esz);
+    c->last_alg = ra;
+    const bool inplace = (in == (const void *)rbuf);
+    if (inplace) {
+        rc = ensure_scratch(c, rcount * esz);
+        if (rc) return rc;
+    }
+    MI_HIP(hipStreamSynchronize(s));
+    const void *mine[1] = {in};
+    const uint64_t sig[4] = {2, rcount, (uint64_t)type, (uint64_t)op};
+    std::vector<std::vector<void *>> P;
+    rc = exchange(c, 1, mine, sig, P);
+    if (rc) return rc;
+    ExprPool ep;
+    Program pr;
+    if (!compile_expr(ep, expr_reduce(ep, ra, c->size, 0), c->size, &pr))
+        return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
+    std::vector<void *> dst(1, inplace ? c->scratch : rbuf);
+    // the result block r is written at offset 0 of the destination: shift the destination back
+    std::vector<void *> d0(1, (char *)dst[0] - (size_t)c->rank * rcount * esz);
+    rc = run_program(op, type, pr, P[0], d0, (size_t)c->rank * rcount, rcount, s);
+    if (rc) return rc;
+    rc = finish(c, s);
+    if (rc) return rc;
+    if (inplace) {
+        MI_HIP(hipMemcpyAsync(rbuf, c->scratch, rcount * esz, hipMemcpyDeviceToDevice, s));
+        MI_HIP(hipStreamSynchronize(s));
+    }
+    return MI355X_SUCCESS;
+}
+
+// MPI_Reduce_scatter with vector counts (coll_tuned_reduce_scatter_intra_dec_fixed order)
+int mi355x_reduce_scatter(mi355x_comm_t *c, const void *sbuf, void *rbuf, const int *rcounts, int type,
+                          int op, void *stream)
+{
+    int rc = check_common(c, op, type);
+    if (rc) return rc;
+    if (!rcounts) return set_error(MI355X_ERR_ARG, "rcounts is NULL");
+    std::vector<size_t> disp(c->size + 1, 0);
+    for (int r = 0; r < c->size; ++r) {
+        if (rcounts[r] < 0) return set_error(MI355X_ERR_ARG, "negative rcount");
+        disp[r + 1] = disp[r] + (size_t)rcounts[r];
+    }
+    const size_t count = disp[c->size];
+    if (count == 0) return MI355X_SUCCESS;
+    hipStream_t s = resolve_stream(stream);
+    const size_t esz = mi355x_type_size(type);
+    const void *in = sbuf ? sbuf : rbuf;
+    const int alg = c->knob_rs ? c->knob_rs : reduce_scatter_decision(c->size, count, esz);
+    c->last_alg = alg;
+    const size_t mine_n = (size_t)rcounts[c->rank];
+    const bool inplace = (in == (const void *)rbuf);
+    if (inplace) {
+        rc = ensure_scratch(c, mine_n * esz);
+        if (rc) return rc;
+    }
+    MI_HIP(hipStreamSynchronize(s));
+    const void *mine[1] = {in};
+    uint64_t h = 1469598103934665603ull;
+    for (int r = 0; r < c->size; ++r) h = (h ^ (uint64_t)rcounts[r]) * 1099511628211ull;
+    const uint64_t sig[4] = {3, h, (uint64_t)type, (uint64_t)op};
+    std::vector<std::vector<void *>> P;
+    rc = exchange(c, 1, mine, sig, P);
+    if (rc) return rc;
+    Program pr;
+    if (c->size == 1) {
+        pr.is_fold = true;
+        pr.order = {0};
+        pr.nr = 1;
+    } else if (alg == 2) {
+        pr = reduce_scatter_ring_block_program(c->size, c->rank);
+    } else {
+        ExprPool ep;
+        std::vector<int> roots = expr_reduce_scatter_rechalving(ep, c->size);
+        if (!compile_expr(ep, roots[c->rank], c->size, &pr))
+            return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
+    }
+    void *dst0 = inplace ? c->scratch : rbuf;
+    std::vector<void *> d0(1, (char *)dst0 - disp[c->rank] * esz);
+    rc = run_program(op, type, pr, P[0], d0, disp[c->rank], mine_n, s);
+    if (rc) return rc;
+    rc = finish(c, s);
+    if (rc) return rc;
+    if (inplace && mine_n) {
+        MI_HIP(hipMemcpyAsync(rbuf, c->scratch, mine_n * esz, hipMemcpyDeviceToDevice, s));
+        MI_HIP(hipStreamSynchronize(s));
+    }
+    return MI355X_SUCCESS;
+}
+
+// MPI_Allgather of `bytes` per rank (contiguous); sbuf NULL = MPI_IN_PLACE
+int mi355x_allgather(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, void *stream)
+{
+    if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    if (bytes == 0) return MI355X_SUCCESS;
+    hipStream_t s = resolve_stream(stream);
+    const void *src = sbuf ? sbuf : (const char *)rbuf + (size_t)c->rank * bytes;
+    MI_HIP(hipStreamSynchronize(s));
+    const void *mine[1] = {rbuf};
+    const uint64_t sig[4] = {4, bytes, 0, 0};
+    std::vector<std::vector<void *>> P;
+    int rc = exchange(c, 1, mine, sig, P);
+    if (rc) return rc;
+    c->last_alg = 1;
+    CopyArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.src = src;
+    a.nd = c->size;
+    for (int q = 0; q < c->size; ++q) a.dst[q] = (char *)P[0][q] + (size_t)c->rank * bytes;
+    a.n = bytes;
+    rc = launch_copy(a, s);
+    if (rc) return rc;
+    return finish(c, s);
+}
+
+// MPI_Bcast of `bytes` from root: rank r moves slice r of the root buffer to every non-root rank
+// (scatter + allgather shape: every xGMI link carries ~2/n of the message instead of the root's
+// links carrying all of it).
+int mi355x_bcast(mi355x_comm_t *c, void *buf, size_t bytes, int root, void *stream)
+{
+    if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    if (root < 0 || root >= c->size) return set_error(MI355X_ERR_ARG, "bad root");
+    if (bytes == 0 || c->size == 1) return MI355X_SUCCESS;
+    hipStream_t s = resolve_stream(stream);
+    MI_HIP(hipStreamSynchronize(s));
+    const void *mine[1] = {buf};
+    const uint64_t sig[4] = {5, bytes, (uint64_t)root, 0};
+    std::vector<std::vector<void *>> P;
+    int rc = exchange(c, 1, mine, sig, P);
+    if (rc) return rc;
+    c->last_alg = 1;
+    size_t off, len;
+    ring_block(bytes, c->size, c->rank, &off, &len);
+    CopyArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.src = (const char *)P[0][root] + off;
+    a.nd = 0;
+    for (int q = 0; q < c->size; ++q)
+        if (q != root) a.dst[a.nd++] = (char *)P[0][q] + off;
+    a.n = len;
+    rc = launch_copy(a, s);
+    if (rc) return rc;
+    return finish(c, s);
+}
+
+} // extern "C"

@@ -111,7 +111,54 @@ __global__ __launch_bounds__(256) void k_stream(StreamArgs args)
     for (size_t i = t0 + tid; i < args.n; i += nthr) o[i] = apply<F, THREE>(a[i], b[i]);
 }
 
-// only the bench-critical functors get every launch-shape variant; the rest use U=4, NT=0
+// One-shot variant: no grid-stride loop.  Block b owns the contiguous run of 256*U vectors
+// starting at b*256*U; lane t touches vectors t, t+256, ... (each wave-instruction reads 1 KiB
+// contiguous).  Grid = ceil(nvec / (256*U)) blocks -- the hardware dispatcher, not a loop,
+// balances the 8 XCDs.  Head/tail elements are handled by block 0 / the last block.
+template <class F, bool THREE, int U, bool NT>
+__global__ __launch_bounds__(256) void k_chunk(StreamArgs args)
+{
+    using T = typename F::T;
+    using V = Vec16<T>;
+    constexpr int EPV = 16 / sizeof(T);
+    const T *a = static_cast<const T *>(args.a);
+    const T *b = static_cast<const T *>(args.b);
+    T *o = static_cast<T *>(args.out);
+    const V *av = reinterpret_cast<const V *>(a + args.head);
+    const V *bv = reinterpret_cast<const V *>(b + args.head);
+    V *ov = reinterpret_cast<V *>(o + args.head);
+    const size_t nvec = args.nvec;
+    const size_t base = (size_t)blockIdx.x * (256 * U) + threadIdx.x;
+    V xa[U], xb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t i = base + (size_t)u * 256;
+        if (i < nvec) {
+            xa[u] = vload<NT>(av + i);
+            xb[u] = vload<NT>(bv + i);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t i = base + (size_t)u * 256;
+        if (i < nvec) {
+            V r;
+#pragma unroll
+            for (int j = 0; j < EPV; ++j) r.e[j] = apply<F, THREE>(xa[u].e[j], xb[u].e[j]);
+            vstore<NT>(ov + i, r);
+        }
+    }
+    if (blockIdx.x == 0) {
+        for (size_t i = threadIdx.x; i < args.head; i += 256) o[i] = apply<F, THREE>(a[i], b[i]);
+    }
+    if (blockIdx.x == gridDim.x - 1) {
+        for (size_t i = args.head + nvec * EPV + threadIdx.x; i < args.n; i += 256)
+            o[i] = apply<F, THREE>(a[i], b[i]);
+    }
+}
+
+// only the bench-critical functors get every launch-shape variant; the rest use the default
+constexpr int kDefaultUnroll = 1;
 template <class F> struct Tunable : std::false_type {};
 template <> struct Tunable<OpSum<float>> : std::true_type {};
 template <> struct Tunable<OpSum<double>> : std::true_type {};
@@ -123,8 +170,16 @@ static int launch_shape(const StreamArgs &args, hipStream_t s)
     constexpr int EPV = 16 / sizeof(T);
     const StreamTune &t = stream_tune();
     const size_t threads = 256;
+    const size_t scalar = args.head + (args.n - args.head - args.nvec * EPV);
+    if (t.mode == 1 && args.nvec > 0 && scalar <= 64) {
+        // one-shot chunked grid (head/tail < 16 elements are handled by the edge blocks)
+        size_t blocks = (args.nvec + threads * U - 1) / (threads * U);
+        if (blocks > 0x7fffffffu) return set_error(MI355X_ERR_ARG, "count too large for one launch");
+        hipLaunchKernelGGL((k_chunk<F, THREE, U, NT>), dim3((unsigned)blocks), dim3(threads), 0, s, args);
+        MI_HIP(hipGetLastError());
+        return MI355X_SUCCESS;
+    }
     size_t work = args.nvec ? (args.nvec + (size_t)U - 1) / U : 0;
-    size_t scalar = args.head + (args.n - args.head - args.nvec * EPV);
     if (scalar > work) work = scalar;
     size_t blocks = (work + threads - 1) / threads;
     const size_t cap = (size_t)t.blocks_per_cu * (size_t)device_cu_count();
@@ -167,7 +222,7 @@ static int launch(const void *a, const void *b, void *out, size_t n, hipStream_t
         default: return nt ? launch_shape<F, THREE, 4, true>(args, s) : launch_shape<F, THREE, 4, false>(args, s);
         }
     } else {
-        return launch_shape<F, THREE, 4, false>(args, s);
+        return launch_shape<F, THREE, kDefaultUnroll, false>(args, s);
     }
 }
 

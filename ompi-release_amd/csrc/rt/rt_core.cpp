@@ -39,15 +39,9 @@ int device_cu_count()
 
 hipStream_t resolve_stream(void *stream)
 {
-    if (stream) return (hipStream_t)stream;
-    static thread_local hipStream_t own[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    if (!own[dev]) {
-        if (hipStreamCreateWithFlags(&own[dev], hipStreamNonBlocking) != hipSuccess)
-            own[dev] = nullptr;
-    }
-    return own[dev];
+    // NULL is HIP's default (null) stream, as in every HIP/CUDA API: it orders with the other
+    // blocking streams of the device (torch's default stream is this stream).
+    return (hipStream_t)stream;
 }
 
 StreamTune &stream_tune()
@@ -204,6 +198,14 @@ int mi355x_op_tune(int unroll, int blocks_per_cu, int nontemporal)
     if (nontemporal >= 0) t.nontemporal = nontemporal ? 1 : 0;
     return MI355X_SUCCESS;
 }
+int mi355x_op_set_mode(int mode)
+{
+    if (mode != 0 && mode != 1) return set_error(MI355X_ERR_ARG, "mode must be 0 or 1");
+    stream_tune().mode = mode;
+    return MI355X_SUCCESS;
+}
+int mi355x_op_get_mode(void) { return stream_tune().mode; }
+
 int mi355x_op_get_tune(int *unroll, int *blocks_per_cu, int *nontemporal)
 {
     StreamTune &t = stream_tune();

@@ -25,14 +25,15 @@ int set_error(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3
 // number of compute units of the current device (cached per device)
 int device_cu_count();
 
-// resolve a caller stream (NULL -> per-thread default stream of the library)
+// caller stream as a hipStream_t (NULL = the HIP null stream)
 hipStream_t resolve_stream(void *stream);
 
 // launch-shape knobs for the streaming kernels (see mi355x_op_tune)
 struct StreamTune {
-    int unroll = 4;
-    int blocks_per_cu = 8;
+    int unroll = 1;         // measured best on MI355X for 1 GiB operands (profiles/r01_*)
+    int blocks_per_cu = 2;  // grid-stride mode: 512 resident blocks
     int nontemporal = 0;
+    int mode = 0;           // 0 = grid-stride, 1 = one-shot chunked grid
 };
 StreamTune &stream_tune();
 

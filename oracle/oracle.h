@@ -89,6 +89,9 @@ int oracle_reduce_scatter_block(int n, size_t rcount, int type, int op,
  * recursive halving or ring.  Returns 1 = recursive halving, 2 = ring. */
 int oracle_reduce_scatter(int n, const int *rcounts, int type, int op,
                           const void *const *sbufs, void *const *rbufs);
+/* same with a forced algorithm: 1 = recursive halving, 2 = ring, 0 = decision */
+int oracle_reduce_scatter_alg(int alg, int n, const int *rcounts, int type, int op,
+                              const void *const *sbufs, void *const *rbufs);
 
 /* Expression-order description of the allreduce fold actually applied to element `index`:
  * writes the rank fold order into order[0..n-1] for ring / segmented ring (acc starts at

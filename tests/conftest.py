@@ -84,3 +84,7 @@ def gpu():
     p = load_pkg()
     p.rt()
     return torch
+
+# a failed rank must not leave its peers in a 10-minute barrier
+import os as _os  # noqa: E402
+_os.environ.setdefault("MI355X_TIMEOUT_S", "60")

@@ -1,0 +1,59 @@
+"""One rank of the multi-process coll/mi355x test (test_coll_ipc_gpu.py).
+
+argv: key rank size device.  Every rank builds every rank's input deterministically, runs the
+collectives through the IPC path (mi355x_comm_create + hipIpc* handles), and checks its own
+result against the oracle's simulation of the reference schedule.  Exit 0 on success.
+"""
+from __future__ import annotations
+
+import ctypes
+import pathlib
+import sys
+
+import numpy as np
+
+sys.path.insert(0, str(pathlib.Path(__file__).parent))
+from conftest import load_oracle, load_pkg  # noqa: E402
+import opdata  # noqa: E402
+
+
+def main():
+    key, rank, size, dev = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+    import torch
+    torch.cuda.set_device(dev)
+    pkg = load_pkg()
+    oracle = load_oracle()
+    comm = pkg.Comm.create(key, rank, size, dev)
+    ptrs = lambda arrs: (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    for opname, tname in [("SUM", "FLOAT"), ("MAXLOC", "DOUBLE_INT"), ("PROD", "C_FLOAT_COMPLEX")]:
+        op, ty = pkg.OP[opname], pkg.T[tname]
+        for count in (5, 3001, 300_007):
+            xs = [opdata.make(tname, count, 400 + r) for r in range(size)]
+            outs = [np.zeros_like(xs[0]) for _ in range(size)]
+            oracle.oracle_allreduce(0, size, count, ty, op, 0, ptrs(xs), ptrs(outs))
+            dx = torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda()
+            dr = torch.zeros_like(dx)
+            torch.cuda.synchronize()
+            for rep in range(2):  # second call hits the registration caches
+                comm.allreduce(dx.data_ptr(), dr.data_ptr(), count, ty, op)
+                got = dr.cpu().numpy().view(xs[0].dtype)
+                opdata.assert_same(tname, opname, got, outs[rank], f"ipc allreduce rank={rank} rep={rep}")
+    # bcast + allgather through IPC
+    nb = 1_000_003
+    buf = torch.full((nb,), rank, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    comm.bcast(buf.data_ptr(), nb, size - 1)
+    assert int(buf.min()) == size - 1 and int(buf.max()) == size - 1
+    src = torch.full((nb,), rank + 1, dtype=torch.uint8, device="cuda")
+    dst = torch.zeros(nb * size, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    comm.allgather(src.data_ptr(), dst.data_ptr(), nb)
+    for r in range(size):
+        assert int(dst[r * nb:(r + 1) * nb].min()) == r + 1
+    comm.barrier()
+    comm.destroy()
+    print(f"rank {rank} OK", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -102,25 +102,37 @@ def make(tname: str, n: int, salt: int = 0) -> np.ndarray:
     raise KeyError(tname)
 
 
+def _bytes_equal(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(a)
+    b = np.ascontiguousarray(b)
+    nb = 10 if a.dtype == np.longdouble else a.dtype.itemsize  # x87: 10 significant bytes
+    isz = a.dtype.itemsize
+    return (a.view(np.uint8).reshape(len(a), isz)[:, :nb] == b.view(np.uint8).reshape(len(b), isz)[:, :nb]).all(1)
+
+
 def _nan_equal_fp(a: np.ndarray, b: np.ndarray) -> np.ndarray:
-    return (a.view(np.uint8).reshape(len(a), -1) == b.view(np.uint8).reshape(len(b), -1)).all(1) | (
-        np.isnan(a) & np.isnan(b))
+    return _bytes_equal(a, b) | (np.isnan(a) & np.isnan(b))
 
 
 def mismatches(tname: str, opname: str, got: np.ndarray, want: np.ndarray) -> np.ndarray:
     """indices where got != want under the comparison rules above"""
     if tname in _PAIR:
+        gv = np.ascontiguousarray(got["v"])
+        wv = np.ascontiguousarray(want["v"])
+        nb = 10 if gv.dtype == np.longdouble else gv.dtype.itemsize  # x87: 10 significant bytes
         ok = (got["k"] == want["k"]) & (
-            got["v"].view(np.uint8).reshape(len(got), -1) == want["v"].view(np.uint8).reshape(len(want), -1)).all(1)
+            gv.view(np.uint8).reshape(len(gv), gv.dtype.itemsize)[:, :nb]
+            == wv.view(np.uint8).reshape(len(wv), wv.dtype.itemsize)[:, :nb]).all(1)
         return np.nonzero(~ok)[0]
     if opname in FLOAT_OPS and tname in _FP:
         return np.nonzero(~_nan_equal_fp(got, want))[0]
     if opname in FLOAT_OPS and tname in _CPLX:
         ok = _nan_equal_fp(got.real.copy(), want.real.copy()) & _nan_equal_fp(got.imag.copy(), want.imag.copy())
         return np.nonzero(~ok)[0]
-    g = got.view(np.uint8).reshape(len(got), -1)
-    w = want.view(np.uint8).reshape(len(want), -1)
-    return np.nonzero(~(g == w).all(1))[0]
+    if tname in _CPLX:
+        ok = _bytes_equal(got.real.copy(), want.real.copy()) & _bytes_equal(got.imag.copy(), want.imag.copy())
+        return np.nonzero(~ok)[0]
+    return np.nonzero(~_bytes_equal(got, want))[0]
 
 
 def assert_same(tname: str, opname: str, got: np.ndarray, want: np.ndarray, what: str = "") -> None:

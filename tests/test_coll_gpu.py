@@ -1,0 +1,220 @@
+"""coll/mi355x engine on one MI355X: loopback communicators (n virtual ranks, one thread each,
+one device) vs the oracle's simulation of the reference schedules.
+
+Covers MPI_Allreduce (decision + every forced tuned algorithm), MPI_Reduce_scatter_block,
+MPI_Reduce_scatter (recursive halving + ring), MPI_Allgather and MPI_Bcast, in place and not,
+odd counts, and element types whose results expose operand order (fp32 SUM on N(0,1), MAX with
+NaN/signed zeros, MAXLOC ties, complex PROD).  Bar: bit-exact (NaN payloads of float SUM/PROD
+excepted, see opdata.py).  The multi-process IPC path is covered by test_coll_ipc_gpu.py.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+import opdata
+
+pytestmark = pytest.mark.gpu
+
+CASES = [("SUM", "FLOAT"), ("SUM", "DOUBLE"), ("MAX", "DOUBLE"), ("MAXLOC", "FLOAT_INT"),
+         ("PROD", "C_DOUBLE_COMPLEX"), ("BAND", "INT64"), ("SUM", "INT8"), ("MINLOC", "DOUBLE_INT")]
+
+
+def _ptrs(arrs):
+    return (ctypes.c_void_p * len(arrs))(*[a.ctypes.data if a is not None else None for a in arrs])
+
+
+def run_ranks(n, fn):
+    """run fn(rank) on n threads, re-raising the first failure"""
+    errs = [None] * n
+
+    def body(r):
+        try:
+            fn(r)
+        except BaseException as e:  # noqa: BLE001
+            errs[r] = e
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(n)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    for e in errs:
+        if e is not None:
+            raise e
+
+
+def to_dev(torch, a: np.ndarray):
+    return torch.from_numpy(a.view(np.uint8).copy()).cuda()
+
+
+def from_dev(t, like: np.ndarray, n=None):
+    n = len(like) if n is None else n
+    return t[: n * like.dtype.itemsize].cpu().numpy().view(like.dtype).copy()
+
+
+@pytest.fixture(scope="module")
+def comms(gpu, pkg):
+    made = {}
+
+    def get(n):
+        if n not in made:
+            made[n] = pkg.Comm.loopback(n, 0)
+        return made[n]
+
+    yield get
+    for cs in made.values():
+        for c in cs:
+            c.destroy()
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
+@pytest.mark.parametrize("alg", [0, 3, 4, 5])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_allreduce(gpu, pkg, oracle, comms, n, alg, inplace):
+    torch = gpu
+    cs = comms(n)
+    for opname, tname in CASES:
+        op, ty = pkg.OP[opname], pkg.T[tname]
+        esz = pkg.type_size(ty)
+        for count in (1, 7, 2500 // esz + 3, 40_001):
+            xs = [opdata.make(tname, count, 100 + r) for r in range(n)]
+            outs = [np.zeros_like(xs[0]) for _ in range(n)]
+            ran = oracle.oracle_allreduce(alg, n, count, ty, op, 0, _ptrs(xs), _ptrs(outs))
+            assert ran >= 0
+            dx = [to_dev(torch, x) for x in xs]
+            dr = [t.clone() if inplace else torch.zeros_like(t) for t in dx]
+            torch.cuda.synchronize()
+            for c in cs:
+                c.set("ALLREDUCE_ALG", alg)
+
+            def rank(r):
+                cs[r].allreduce(None if inplace else dx[r].data_ptr(), dr[r].data_ptr(), count, ty, op)
+
+            run_ranks(n, rank)
+            torch.cuda.synchronize()
+            for r in range(n):
+                opdata.assert_same(tname, opname, from_dev(dr[r], outs[r]), outs[r],
+                                   f"allreduce n={n} alg={alg} count={count} rank={r}")
+            assert cs[0].last_algorithm() == ran
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_reduce_scatter_block(gpu, pkg, oracle, comms, n, inplace):
+    torch = gpu
+    cs = comms(n)
+    for opname, tname in CASES:
+        op, ty = pkg.OP[opname], pkg.T[tname]
+        for rcount in (1, 33, 5000):
+            total = rcount * n
+            xs = [opdata.make(tname, total, 200 + r) for r in range(n)]
+            outs = [np.zeros(rcount, dtype=xs[0].dtype) for _ in range(n)]
+            assert oracle.oracle_reduce_scatter_block(n, rcount, ty, op, _ptrs(xs), _ptrs(outs)) >= 0
+            dx = [to_dev(torch, x) for x in xs]
+            dr = [t.clone() for t in dx] if inplace else [torch.zeros(rcount * pkg.type_size(ty), dtype=torch.uint8, device="cuda") for _ in dx]
+            torch.cuda.synchronize()
+
+            def rank(r):
+                cs[r].reduce_scatter_block(None if inplace else dx[r].data_ptr(), dr[r].data_ptr(), rcount, ty, op)
+
+            run_ranks(n, rank)
+            torch.cuda.synchronize()
+            for r in range(n):
+                opdata.assert_same(tname, opname, from_dev(dr[r], outs[r], rcount), outs[r],
+                                   f"rsb n={n} rcount={rcount} rank={r}")
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+@pytest.mark.parametrize("rsalg", [0, 1, 2])
+def test_reduce_scatter(gpu, pkg, oracle, comms, n, rsalg):
+    torch = gpu
+    cs = comms(n)
+    oracle.oracle_reduce_scatter_alg.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                                 ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                                 ctypes.POINTER(ctypes.c_void_p)]
+    rng = np.random.default_rng(n * 10 + rsalg)
+    for opname, tname in CASES:
+        op, ty = pkg.OP[opname], pkg.T[tname]
+        for scale in (3, 3000):
+            rcounts = [int(v) for v in rng.integers(0, scale, n)]
+            total = sum(rcounts)
+            if total == 0:
+                continue
+            xs = [opdata.make(tname, total, 300 + r) for r in range(n)]
+            outs = [np.zeros(max(c, 1), dtype=xs[0].dtype) for c in rcounts]
+            rc = (ctypes.c_int * n)(*rcounts)
+            assert oracle.oracle_reduce_scatter_alg(rsalg, n, rc, ty, op, _ptrs(xs), _ptrs(outs)) >= 0
+            dx = [to_dev(torch, x) for x in xs]
+            dr = [torch.zeros(max(c, 1) * pkg.type_size(ty), dtype=torch.uint8, device="cuda") for c in rcounts]
+            torch.cuda.synchronize()
+            for c in cs:
+                c.set("REDUCE_SCATTER_ALG", rsalg)
+
+            def rank(r):
+                cs[r].reduce_scatter(dx[r].data_ptr(), dr[r].data_ptr(), rcounts, ty, op)
+
+            run_ranks(n, rank)
+            torch.cuda.synchronize()
+            for r in range(n):
+                if rcounts[r]:
+                    opdata.assert_same(tname, opname, from_dev(dr[r], outs[r], rcounts[r]), outs[r][:rcounts[r]],
+                                       f"rs alg={rsalg} n={n} rank={r} rcounts={rcounts}")
+    for c in cs:
+        c.set("REDUCE_SCATTER_ALG", 0)
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("nbytes", [1, 13, 4096, 1_000_003])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_allgather(gpu, pkg, comms, n, nbytes, inplace):
+    torch = gpu
+    cs = comms(n)
+    src = [torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda") for _ in range(n)]
+    dst = [torch.zeros(n * nbytes, dtype=torch.uint8, device="cuda") for _ in range(n)]
+    if inplace:
+        for r in range(n):
+            dst[r][r * nbytes:(r + 1) * nbytes].copy_(src[r])
+    torch.cuda.synchronize()
+    run_ranks(n, lambda r: cs[r].allgather(None if inplace else src[r].data_ptr(), dst[r].data_ptr(), nbytes))
+    torch.cuda.synchronize()
+    want = torch.cat(src)
+    for r in range(n):
+        assert torch.equal(dst[r], want), r
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("nbytes", [1, 7, 65536, 3_000_001])
+def test_bcast(gpu, pkg, comms, n, nbytes):
+    torch = gpu
+    cs = comms(n)
+    for root in (0, n - 1):
+        bufs = [torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda") for _ in range(n)]
+        want = bufs[root].clone()
+        torch.cuda.synchronize()
+        run_ranks(n, lambda r: cs[r].bcast(bufs[r].data_ptr(), nbytes, root))
+        torch.cuda.synchronize()
+        for r in range(n):
+            assert torch.equal(bufs[r], want), (root, r)
+
+
+def test_large_allreduce_exact_property(gpu, pkg, comms):
+    """BASELINE size class on one device: 1 GiB fp32 per rank, n = 2, small-integer values (sum is
+    exact in any order -> equals torch's sum), then the same call repeated: buffers reused (IPC
+    registration cache path) and still correct."""
+    torch = gpu
+    cs = comms(2)
+    n_el = 1 << 28
+    xs = [torch.randint(-64, 64, (n_el,), device="cuda", dtype=torch.int32).float() for _ in range(2)]
+    out = [torch.empty_like(xs[0]) for _ in range(2)]
+    want = xs[0] + xs[1]
+    torch.cuda.synchronize()
+    for _ in range(2):
+        run_ranks(2, lambda r: cs[r].allreduce(xs[r].data_ptr(), out[r].data_ptr(), n_el, pkg.T["FLOAT"], pkg.OP["SUM"]))
+        torch.cuda.synchronize()
+        assert torch.equal(out[0], want) and torch.equal(out[1], want)
+    del xs, out, want
+    torch.cuda.empty_cache()

@@ -1,0 +1,36 @@
+"""coll/mi355x through the real multi-process path: 2 processes, hipIpcGetMemHandle /
+hipIpcOpenMemHandle, node-local shm control segment.  On a one-GPU box both ranks share device 0
+(IPC within one device); on an 8-GPU node the same code maps peer devices over xGMI."""
+from __future__ import annotations
+
+import os
+import pathlib
+import subprocess
+import sys
+import uuid
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = pathlib.Path(__file__).parent
+
+
+@pytest.mark.parametrize("size", [2, 3])
+def test_ipc_ranks(gpu, size):
+    key = "t" + uuid.uuid4().hex[:12]
+    ndev = gpu.cuda.device_count()
+    env = dict(os.environ, MI355X_TIMEOUT_S="60")
+    procs = [subprocess.Popen([sys.executable, str(HERE / "ipc_worker.py"), key, str(r), str(size), str(r % ndev)],
+                              env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for r in range(size)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=300)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, _ = p.communicate()
+        outs.append(out)
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} failed:\n{outs[r][-3000:]}"

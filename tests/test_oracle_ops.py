@@ -105,3 +105,23 @@ def test_mt_equals_st(oracle, pkg):
     oracle.oracle_op_3buff(pkg.OP["SUM"], pkg.T["DOUBLE"], a.ctypes.data, b.ctypes.data, o1.ctypes.data, len(a))
     oracle.oracle_op_3buff_mt(pkg.OP["SUM"], pkg.T["DOUBLE"], a.ctypes.data, b.ctypes.data, o2.ctypes.data, len(a), 4)
     assert o1.tobytes() == o2.tobytes()
+
+
+def test_comparator_every_slot(oracle, pkg):
+    """the GPU-test comparator accepts identical results for every slot (guards the test itself)"""
+    for op in range(1, 13):
+        for ty in range(39):
+            if not oracle.oracle_has_op(op, ty):
+                continue
+            tname, opname = pkg.TYPES[ty], pkg.OPS[op]
+            a = opdata.make(tname, 257, 1)
+            b = opdata.make(tname, 257, 2)
+            o1 = np.zeros_like(a)
+            o2 = np.zeros_like(a)
+            with np.errstate(all="ignore"):
+                oracle.oracle_op_3buff(op, ty, a.ctypes.data, b.ctypes.data, o1.ctypes.data, 257)
+                oracle.oracle_op_3buff(op, ty, a.ctypes.data, b.ctypes.data, o2.ctypes.data, 257)
+            opdata.assert_same(tname, opname, o1, o2, "self")
+            c = b.copy()
+            oracle.oracle_op_2buff(op, ty, a.ctypes.data, c.ctypes.data, 257)
+            assert len(opdata.mismatches(tname, opname, c, c.copy())) == 0
