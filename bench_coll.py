@@ -1,0 +1,92 @@
+"""N > 1 leg of bench.py: MPI_Allreduce MPI_SUM fp32, 1 GiB per rank, through the coll/mi355x
+engine (libmi355x_rt, IPC-mapped peers over xGMI), one process per GPU.
+
+Launched by `python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`.
+torch.distributed (gloo, CPU) is used only for the launcher's rendezvous, the timing barrier and
+the max-over-ranks reduction; every byte of the collective moves through the HIP engine.
+value = busbw = (S / t) * 2 (n - 1) / n with S = 1 GiB and t = max over ranks per step.
+"""
+from __future__ import annotations
+
+import os
+import time
+
+GIB = 1 << 30
+# MI355X Infinity Fabric: 7 links per GPU, 153.6 GB/s per link (spec, both directions)
+# -> 76.8 GB/s per link per direction.  Ring peak busbw with R concurrent rings = R x 76.8.
+XGMI_LINK_DIR_GBS = 76.8
+
+
+def run(args, pkg, torch):
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world < 2:
+        raise SystemExit("bench_coll needs WORLD_SIZE >= 2 (launch under torch.distributed.run)")
+    local = local % max(1, torch.cuda.device_count())  # one-GPU rehearsal: ranks share device 0
+    torch.cuda.set_device(local)
+    if not dist.is_initialized():
+        dist.init_process_group("gloo")
+    key = "bench_{}_{}".format(os.environ.get("TORCHELASTIC_RUN_ID", "x"), os.environ.get("MASTER_PORT", "0"))
+    comm = pkg.Comm.create(key, rank, world, local)
+
+    n = GIB // 4
+    dev = torch.device("cuda", local)
+    ty, op = pkg.T["FLOAT"], pkg.OP["SUM"]
+    # exactness check at the real size: x_r = r + 1 everywhere -> every element = n(n+1)/2
+    x = torch.full((n,), float(rank + 1), device=dev)
+    y = torch.empty_like(x)
+    torch.cuda.synchronize()
+    comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
+    want = world * (world + 1) / 2
+    ok = bool(torch.all(y == want).item())
+    # timed data: N(0,1), order-dependent (the engine replicates the segmented-ring order)
+    x.normal_()
+    torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
+    alg = comm.last_algorithm()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dist.barrier()
+    t = torch.tensor([dt, 0.0 if ok else 1.0], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt, bad = float(t[0]), float(t[1])
+    comm.destroy()
+    if rank != 0:
+        dist.destroy_process_group()
+        return None
+    per = dt / args.steps
+    busbw = (n * 4 / per) * 2 * (world - 1) / world / 1e9
+    peak_all = (world - 1) * XGMI_LINK_DIR_GBS
+    res = {
+        "metric": "MPI_Allreduce busbw GB/s (1 GiB fp32, np=8) + op/hip reduce HBM GB/s",
+        "value": round(busbw, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(per * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (torch normal_ on device)",
+        "config": {"workload": f"MPI_Allreduce MPI_SUM MPI_FLOAT 1 GiB per rank, np={world} (BASELINE configs[2])",
+                   "count": n, "algorithm": {3: "recursive_doubling", 4: "ring", 5: "segmented_ring"}.get(alg, alg),
+                   "exact_check": "ok" if bad == 0 else "FAILED"},
+        "roofline": {"bound": "xgmi", "achieved": round(busbw, 2), "peak": round(peak_all, 1), "unit": "GB/s",
+                     "frac": round(busbw / peak_all, 4), "traffic": None,
+                     "peak_note": f"(n-1) links x {XGMI_LINK_DIR_GBS} GB/s per direction (spec); "
+                                  "busbw convention 2(n-1)/n"},
+        "cpu_baseline": None,
+    }
+    dist.destroy_process_group()
+    return res

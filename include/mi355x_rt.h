@@ -70,14 +70,16 @@ int mi355x_op_reduce_3buff(int op, int type, const void *in1, const void *in2, v
                            size_t count, void *stream);
 
 /* Launch-shape knobs for the streaming op kernels.  unroll in {1,2,4,8} (16-byte vectors per
- * operand per thread per iteration; 0 = keep), blocks_per_cu in 1..64 (0 = keep), nontemporal
- * 0/1 (-1 = keep).  Only the fp32/fp64 SUM kernels have every variant compiled; the other slots
- * always run unroll 4, temporal. */
+ * operand per lane; 0 = keep), blocks_per_cu in 1..64 (grid-stride mode; 0 = keep),
+ * nontemporal: -2 keep, -1 auto (non-temporal when the three streams exceed 256 MiB), or a mask
+ * 0..3 (1 = loads, 2 = stores).  Only the fp32/fp64 SUM kernels have every variant compiled;
+ * the other slots run unroll 1 with masks 0 or 3. */
 int mi355x_op_tune(int unroll, int blocks_per_cu, int nontemporal);
 int mi355x_op_get_tune(int *unroll, int *blocks_per_cu, int *nontemporal);
 /* grid shape: 0 = persistent grid-stride (blocks_per_cu x CUs), 1 = one-shot chunked grid */
 int mi355x_op_set_mode(int mode);
 int mi355x_op_get_mode(void);
+int mi355x_op_set_threads(int threads);   /* block size of the one-shot grid (64..1024) */
 
 
 /* ---------------------------------------------------------------- coll/mi355x engine */

@@ -95,6 +95,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "mi355x_op_get_tune": (i, [c.POINTER(i), c.POINTER(i), c.POINTER(i)]),
         "mi355x_op_set_mode": (i, [i]),
         "mi355x_op_get_mode": (i, []),
+        "mi355x_op_set_threads": (i, [i]),
         "mi355x_comm_create": (i, [c.c_char_p, i, i, i, c.POINTER(vp)]),
         "mi355x_comm_create_loopback": (i, [i, i, c.POINTER(vp)]),
         "mi355x_comm_destroy": (i, [vp]),
@@ -142,7 +143,11 @@ def type_size(ty: int) -> int:
     return int(rt().mi355x_type_size(ty))
 
 
-def tune(unroll: int = 0, blocks_per_cu: int = 0, nontemporal: int = -1) -> None:
+def set_threads(threads: int) -> None:
+    check(rt().mi355x_op_set_threads(threads), "mi355x_op_set_threads")
+
+
+def tune(unroll: int = 0, blocks_per_cu: int = 0, nontemporal: int = -2) -> None:
     check(rt().mi355x_op_tune(unroll, blocks_per_cu, nontemporal), "mi355x_op_tune")
 
 

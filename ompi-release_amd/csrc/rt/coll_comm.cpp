@@ -511,7 +511,11 @@ int mi355x_allreduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t coun
         return MI355X_SUCCESS;
     }
     int alg = c->knob_allreduce ? c->knob_allreduce : allreduce_decision(c->size, count, esz);
-    if ((alg == AR_RING || alg == AR_RING_SEGMENTED) && count < (size_t)c->size) alg = AR_RECDBL;
+    // the reference's own fallbacks: segmented ring -> ring when count < n * segcount
+    // (coll_tuned_allreduce.c:672-679), ring -> recursive doubling when count < n (:398-405)
+    if (alg == AR_RING_SEGMENTED && count < (size_t)c->size * computed_segcount(1u << 20, esz, count))
+        alg = AR_RING;
+    if (alg == AR_RING && count < (size_t)c->size) alg = AR_RECDBL;
     c->last_alg = alg;
     MI_HIP(hipStreamSynchronize(s));  // every rank's input is complete before it is published
     const void *mine[2] = {in, rbuf};

@@ -307,6 +307,16 @@ int reduce_scatter_decision(int n, size_t total_count, size_t dsize)
     return 2;
 }
 
+size_t computed_segcount(size_t segsize, size_t typelng, size_t count)
+{
+    if (segsize >= typelng && segsize < typelng * count) {
+        size_t sc = segsize / typelng;
+        if (segsize - sc * typelng > (typelng >> 1)) sc++;
+        return sc;
+    }
+    return count;
+}
+
 void ring_block(size_t count, int n, int b, size_t *off, size_t *len)
 {
     size_t early = count / (size_t)n, late = early, split = count % (size_t)n;

@@ -68,6 +68,8 @@ int allreduce_decision(int n, size_t count, size_t dsize);            // :42-85
 int reduce_decision(int n, size_t count, size_t dsize);               // :343-446 (commutative)
 int reduce_scatter_decision(int n, size_t total_count, size_t dsize); // :456-502; 1 = rec. halving, 2 = ring
 
+// COLL_TUNED_COMPUTED_SEGCOUNT (coll_tuned.h:525-533)
+size_t computed_segcount(size_t segsize, size_t typelng, size_t count);
 // COLL_TUNED_COMPUTE_BLOCKCOUNT (coll_tuned.h:546-552) block offset/length
 void ring_block(size_t count, int n, int b, size_t *off, size_t *len);
 

@@ -5,8 +5,10 @@
 //     128-B lines, for every element size (1..16 B); MAXLOC pairs are decoded in registers from
 //     the same 16-byte vectors (no LDS round trip: each pair is consumed by the lane that loads
 //     it, so staging would only add LDS traffic).
-//   * grid-stride loop, U independent 16-B vectors per operand per thread in flight per
-//     iteration (all loads issued before the first use), grid capped at blocks_per_cu x CUs.
+//   * default launch: one-shot grid, one 16-B vector per operand per lane, non-temporal loads
+//     and stores when the three streams exceed the 256 MiB Infinity Cache (measured best on
+//     MI355X, profiles/r01_op_tune.json); a persistent grid-stride form (U vectors in flight
+//     per lane, blocks_per_cu x CUs) serves misaligned operands and tuning.
 //   * scalar head/tail so any alignment works: when all three operands share the same
 //     misalignment mod 16 the head peels to a 16-B boundary; otherwise the whole range takes
 //     the element-wise path (still coalesced, one element per lane).
@@ -67,7 +69,9 @@ template <bool NT, typename V> __device__ __forceinline__ void vstore(V *p, cons
         *reinterpret_cast<u32x4 *>(p) = raw;
 }
 
-template <class F, bool THREE, int U, bool NT>
+// NTM bit 0: non-temporal loads, bit 1: non-temporal stores (streams larger than the 256 MiB
+// Infinity Cache gain ~9 % from not allocating in L2/MALL; small, re-read operands lose)
+template <class F, bool THREE, int U, int NTM>
 __global__ __launch_bounds__(256) void k_stream(StreamArgs args)
 {
     using T = typename F::T;
@@ -91,8 +95,8 @@ __global__ __launch_bounds__(256) void k_stream(StreamArgs args)
         for (int u = 0; u < U; ++u) {
             const size_t i = base + (size_t)u * nthr;
             if (i < nvec) {
-                xa[u] = vload<NT>(av + i);
-                xb[u] = vload<NT>(bv + i);
+                xa[u] = vload<(NTM & 1) != 0>(av + i);
+                xb[u] = vload<(NTM & 1) != 0>(bv + i);
             }
         }
 #pragma unroll
@@ -102,7 +106,7 @@ __global__ __launch_bounds__(256) void k_stream(StreamArgs args)
                 V r;
 #pragma unroll
                 for (int j = 0; j < EPV; ++j) r.e[j] = apply<F, THREE>(xa[u].e[j], xb[u].e[j]);
-                vstore<NT>(ov + i, r);
+                vstore<(NTM & 2) != 0>(ov + i, r);
             }
         }
     }
@@ -115,8 +119,8 @@ __global__ __launch_bounds__(256) void k_stream(StreamArgs args)
 // starting at b*256*U; lane t touches vectors t, t+256, ... (each wave-instruction reads 1 KiB
 // contiguous).  Grid = ceil(nvec / (256*U)) blocks -- the hardware dispatcher, not a loop,
 // balances the 8 XCDs.  Head/tail elements are handled by block 0 / the last block.
-template <class F, bool THREE, int U, bool NT>
-__global__ __launch_bounds__(256) void k_chunk(StreamArgs args)
+template <class F, bool THREE, int U, int NTM>
+__global__ __launch_bounds__(1024) void k_chunk(StreamArgs args)
 {
     using T = typename F::T;
     using V = Vec16<T>;
@@ -128,31 +132,32 @@ __global__ __launch_bounds__(256) void k_chunk(StreamArgs args)
     const V *bv = reinterpret_cast<const V *>(b + args.head);
     V *ov = reinterpret_cast<V *>(o + args.head);
     const size_t nvec = args.nvec;
-    const size_t base = (size_t)blockIdx.x * (256 * U) + threadIdx.x;
+    const size_t tpb = blockDim.x;
+    const size_t base = (size_t)blockIdx.x * (tpb * U) + threadIdx.x;
     V xa[U], xb[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const size_t i = base + (size_t)u * 256;
+        const size_t i = base + (size_t)u * tpb;
         if (i < nvec) {
-            xa[u] = vload<NT>(av + i);
-            xb[u] = vload<NT>(bv + i);
+            xa[u] = vload<(NTM & 1) != 0>(av + i);
+            xb[u] = vload<(NTM & 1) != 0>(bv + i);
         }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const size_t i = base + (size_t)u * 256;
+        const size_t i = base + (size_t)u * tpb;
         if (i < nvec) {
             V r;
 #pragma unroll
             for (int j = 0; j < EPV; ++j) r.e[j] = apply<F, THREE>(xa[u].e[j], xb[u].e[j]);
-            vstore<NT>(ov + i, r);
+            vstore<(NTM & 2) != 0>(ov + i, r);
         }
     }
     if (blockIdx.x == 0) {
-        for (size_t i = threadIdx.x; i < args.head; i += 256) o[i] = apply<F, THREE>(a[i], b[i]);
+        for (size_t i = threadIdx.x; i < args.head; i += tpb) o[i] = apply<F, THREE>(a[i], b[i]);
     }
     if (blockIdx.x == gridDim.x - 1) {
-        for (size_t i = args.head + nvec * EPV + threadIdx.x; i < args.n; i += 256)
+        for (size_t i = args.head + nvec * EPV + threadIdx.x; i < args.n; i += tpb)
             o[i] = apply<F, THREE>(a[i], b[i]);
     }
 }
@@ -163,7 +168,7 @@ template <class F> struct Tunable : std::false_type {};
 template <> struct Tunable<OpSum<float>> : std::true_type {};
 template <> struct Tunable<OpSum<double>> : std::true_type {};
 
-template <class F, bool THREE, int U, bool NT>
+template <class F, bool THREE, int U, int NTM>
 static int launch_shape(const StreamArgs &args, hipStream_t s)
 {
     using T = typename F::T;
@@ -173,9 +178,10 @@ static int launch_shape(const StreamArgs &args, hipStream_t s)
     const size_t scalar = args.head + (args.n - args.head - args.nvec * EPV);
     if (t.mode == 1 && args.nvec > 0 && scalar <= 64) {
         // one-shot chunked grid (head/tail < 16 elements are handled by the edge blocks)
-        size_t blocks = (args.nvec + threads * U - 1) / (threads * U);
+        const size_t tpb = (size_t)t.threads;
+        size_t blocks = (args.nvec + tpb * U - 1) / (tpb * U);
         if (blocks > 0x7fffffffu) return set_error(MI355X_ERR_ARG, "count too large for one launch");
-        hipLaunchKernelGGL((k_chunk<F, THREE, U, NT>), dim3((unsigned)blocks), dim3(threads), 0, s, args);
+        hipLaunchKernelGGL((k_chunk<F, THREE, U, NTM>), dim3((unsigned)blocks), dim3((unsigned)tpb), 0, s, args);
         MI_HIP(hipGetLastError());
         return MI355X_SUCCESS;
     }
@@ -185,7 +191,7 @@ static int launch_shape(const StreamArgs &args, hipStream_t s)
     const size_t cap = (size_t)t.blocks_per_cu * (size_t)device_cu_count();
     if (blocks > cap) blocks = cap;
     if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL((k_stream<F, THREE, U, NT>), dim3((unsigned)blocks), dim3(threads), 0, s,
+    hipLaunchKernelGGL((k_stream<F, THREE, U, NTM>), dim3((unsigned)blocks), dim3(threads), 0, s,
                        args);
     MI_HIP(hipGetLastError());
     return MI355X_SUCCESS;
@@ -213,16 +219,27 @@ static int launch(const void *a, const void *b, void *out, size_t n, hipStream_t
         args.nvec = 0;
     }
     const StreamTune &t = stream_tune();
+    // non-temporal policy: explicit 0..3, or auto (-1): streams beyond the Infinity Cache
+    int ntm = t.nontemporal;
+    if (ntm < 0) ntm = (3 * n * sizeof(T) > ((size_t)256 << 20)) ? 3 : 0;
     if constexpr (Tunable<F>::value) {
-        const bool nt = t.nontemporal != 0;
+#define MI_NT(U_)                                                              \
+    switch (ntm) {                                                             \
+    case 1: return launch_shape<F, THREE, U_, 1>(args, s);                     \
+    case 2: return launch_shape<F, THREE, U_, 2>(args, s);                     \
+    case 3: return launch_shape<F, THREE, U_, 3>(args, s);                     \
+    default: return launch_shape<F, THREE, U_, 0>(args, s);                    \
+    }
         switch (t.unroll) {
-        case 1: return nt ? launch_shape<F, THREE, 1, true>(args, s) : launch_shape<F, THREE, 1, false>(args, s);
-        case 2: return nt ? launch_shape<F, THREE, 2, true>(args, s) : launch_shape<F, THREE, 2, false>(args, s);
-        case 8: return nt ? launch_shape<F, THREE, 8, true>(args, s) : launch_shape<F, THREE, 8, false>(args, s);
-        default: return nt ? launch_shape<F, THREE, 4, true>(args, s) : launch_shape<F, THREE, 4, false>(args, s);
+        case 2: MI_NT(2)
+        case 4: MI_NT(4)
+        case 8: MI_NT(8)
+        default: MI_NT(1)
         }
+#undef MI_NT
     } else {
-        return launch_shape<F, THREE, kDefaultUnroll, false>(args, s);
+        return ntm ? launch_shape<F, THREE, kDefaultUnroll, 3>(args, s)
+                   : launch_shape<F, THREE, kDefaultUnroll, 0>(args, s);
     }
 }
 

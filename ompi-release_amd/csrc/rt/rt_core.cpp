@@ -195,7 +195,8 @@ int mi355x_op_tune(int unroll, int blocks_per_cu, int nontemporal)
             return set_error(MI355X_ERR_ARG, "blocks_per_cu out of range");
         t.blocks_per_cu = blocks_per_cu;
     }
-    if (nontemporal >= 0) t.nontemporal = nontemporal ? 1 : 0;
+    if (nontemporal >= -1 && nontemporal <= 3) t.nontemporal = nontemporal;
+    else if (nontemporal != -2) return set_error(MI355X_ERR_ARG, "nontemporal must be -2 (keep), -1 (auto) or 0..3");
     return MI355X_SUCCESS;
 }
 int mi355x_op_set_mode(int mode)
@@ -205,6 +206,13 @@ int mi355x_op_set_mode(int mode)
     return MI355X_SUCCESS;
 }
 int mi355x_op_get_mode(void) { return stream_tune().mode; }
+int mi355x_op_set_threads(int threads)
+{
+    if (threads != 64 && threads != 128 && threads != 256 && threads != 512 && threads != 1024)
+        return set_error(MI355X_ERR_ARG, "threads must be 64..1024, power of two");
+    stream_tune().threads = threads;
+    return MI355X_SUCCESS;
+}
 
 int mi355x_op_get_tune(int *unroll, int *blocks_per_cu, int *nontemporal)
 {

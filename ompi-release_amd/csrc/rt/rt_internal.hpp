@@ -30,10 +30,11 @@ hipStream_t resolve_stream(void *stream);
 
 // launch-shape knobs for the streaming kernels (see mi355x_op_tune)
 struct StreamTune {
-    int unroll = 1;         // measured best on MI355X for 1 GiB operands (profiles/r01_*)
+    int unroll = 1;         // measured best on MI355X for 1 GiB operands (profiles/r01_op_tune.json)
     int blocks_per_cu = 2;  // grid-stride mode: 512 resident blocks
-    int nontemporal = 0;
-    int mode = 0;           // 0 = grid-stride, 1 = one-shot chunked grid
+    int nontemporal = -1;   // -1 auto (streams > 256 MiB), else mask: 1 loads, 2 stores
+    int mode = 1;           // 0 = grid-stride, 1 = one-shot chunked grid
+    int threads = 1024;     // block size of the one-shot grid (measured best, profiles/r01_op_tune.json)
 };
 StreamTune &stream_tune();
 

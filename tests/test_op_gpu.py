@@ -130,15 +130,21 @@ def test_tune_variants_same_result(gpu, pkg):
     a = torch.randn(n, device="cuda")
     b = torch.randn(n, device="cuda")
     ref = a + b
-    saved = pkg.get_tune()
+    saved, mode = pkg.get_tune(), pkg.get_mode()
     try:
-        for u in (1, 2, 4, 8):
-            for nt in (0, 1):
-                pkg.tune(u, 4, nt)
-                o = torch.empty_like(a)
-                pkg.op_reduce_3buff(pkg.OP["SUM"], pkg.T["FLOAT"], a.data_ptr(), b.data_ptr(), o.data_ptr(), n,
-                                    torch.cuda.current_stream().cuda_stream)
-                torch.cuda.synchronize()
-                assert torch.equal(o, ref), (u, nt)
+        for m in (0, 1):
+            pkg.set_mode(m)
+            for u in (1, 2, 4, 8):
+                for nt in (0, 1, 2, 3):
+                    for tpb in (256, 1024):
+                        pkg.set_threads(tpb)
+                        pkg.tune(u, 4, nt)
+                        o = torch.empty_like(a)
+                        pkg.op_reduce_3buff(pkg.OP["SUM"], pkg.T["FLOAT"], a.data_ptr(), b.data_ptr(), o.data_ptr(), n,
+                                            torch.cuda.current_stream().cuda_stream)
+                        torch.cuda.synchronize()
+                        assert torch.equal(o, ref), (m, u, nt, tpb)
     finally:
         pkg.tune(*saved)
+        pkg.set_mode(mode)
+        pkg.set_threads(1024)

@@ -45,22 +45,23 @@ def main():
     z = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     px, py, pz = x.data_ptr(), y.data_ptr(), z.data_ptr()
     best = (0, None)
-    shapes = [(0, u, bpc, nt) for u in (1, 2) for bpc in (1, 2, 3, 4) for nt in (0, 1)]
-    shapes += [(1, u, 0, nt) for u in (1, 2, 4, 8) for nt in (0, 1)]
+    shapes = [(0, u, bpc, nt, 256) for u in (1, 2) for bpc in (1, 2) for nt in (0, 3)]
+    shapes += [(1, u, 0, nt, tpb) for u in (1, 2, 4) for nt in (0, 1, 2, 3) for tpb in (256, 512, 1024)]
     for tname in ("FLOAT", "DOUBLE"):
         ty = pkg.T[tname]
         n = nbytes // pkg.type_size(ty)
-        for mode, u, bpc, nt in shapes:
+        for mode, u, bpc, nt, tpb in shapes:
             pkg.set_mode(mode)
+            pkg.set_threads(tpb)
             pkg.tune(u, bpc or 2, nt)
             f = lambda: pkg.op_reduce_3buff(pkg.OP["SUM"], ty, px, py, pz, n, sh)
             f()
             ms = time_launch(f)
             gbs = 3 * nbytes / (ms * 1e-3) / 1e9
             out["shape_sweep"].append({"type": tname, "mode": mode, "unroll": u, "blocks_per_cu": bpc, "nt": nt,
-                                       "ms": round(ms, 4), "GBps": round(gbs, 1)})
+                                       "threads": tpb, "ms": round(ms, 4), "GBps": round(gbs, 1)})
             if tname == "FLOAT" and gbs > best[0]:
-                best = (gbs, (u, bpc or 2, nt), mode)
+                best = (gbs, (u, bpc or 2, nt), mode, tpb)
             print(json.dumps(out["shape_sweep"][-1]), flush=True)
     # torch's own elementwise add on the same buffers, for reference
     xf, yf, zf = x.view(torch.float32), y.view(torch.float32), z.view(torch.float32)
@@ -69,8 +70,9 @@ def main():
     print("torch add", out["torch_add_GBps"], flush=True)
     pkg.tune(*best[1])
     pkg.set_mode(best[2])
+    pkg.set_threads(best[3])
     out["best"] = {"GBps": round(best[0], 1), "mode": best[2], "unroll": best[1][0], "blocks_per_cu": best[1][1],
-                   "nt": best[1][2]}
+                   "nt": best[1][2], "threads": best[3]}
     for op in range(1, 13):
         for ty in range(len(pkg.TYPES)):
             if not pkg.op_supported(op, ty):
