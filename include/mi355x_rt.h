@@ -109,7 +109,8 @@ enum mi355x_knob {
     MI355X_KNOB_REDUCE_ALG = 2,         /* coll_tuned_reduce_algorithm, used by reduce_scatter_block */
     MI355X_KNOB_REDUCE_SCATTER_ALG = 3, /* coll_tuned_reduce_scatter_algorithm */
     MI355X_KNOB_BLOCKS_PER_CU = 4,
-    MI355X_KNOB_TIMEOUT_S = 5
+    MI355X_KNOB_TIMEOUT_S = 5,
+    MI355X_KNOB_PUSH = 6                /* 1: one-phase push data flow (owners write peers' buffers) */
 };
 int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
 

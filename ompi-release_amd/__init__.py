@@ -166,7 +166,8 @@ def get_tune() -> tuple[int, int, int]:
 
 
 # ---------------------------------------------------------------- coll/mi355x engine
-KNOB = {"ALLREDUCE_ALG": 1, "REDUCE_ALG": 2, "REDUCE_SCATTER_ALG": 3, "BLOCKS_PER_CU": 4, "TIMEOUT_S": 5}
+KNOB = {"ALLREDUCE_ALG": 1, "REDUCE_ALG": 2, "REDUCE_SCATTER_ALG": 3, "BLOCKS_PER_CU": 4, "TIMEOUT_S": 5,
+        "PUSH": 6}
 AR_ALG = {"DECISION": 0, "LINEAR": 1, "NONOVERLAPPING": 2, "RECURSIVE_DOUBLING": 3, "RING": 4,
           "RING_SEGMENTED": 5}
 

@@ -10,8 +10,12 @@
 //     common_cuda.c:971-1137); peers map them once (hipIpcOpenMemHandle, cached per handle);
 //   * one kernel per rank then reads every rank's input directly over xGMI, folds it in the
 //     reference schedule's order (coll_sched.cpp) and pushes the result into every destination.
-// A call is: sync caller stream -> publish -> barrier -> kernel -> sync -> barrier.  Blocking,
-// like the MPI calls it implements.
+// A call is: sync caller stream -> publish -> barrier -> kernel(s) -> sync -> barrier.
+// Default data flow is PULL: every kernel writes only its own rank's memory and reads peers'
+// memory, so coherence rests on kernel-completion release + the host barrier and never on a peer
+// GPU's L2 seeing a remote write.  Allreduce: phase 1 the owner folds its ring block locally,
+// phase 2 every rank pulls the other blocks (one launch, one segment per peer).  A one-phase
+// PUSH variant (owners write into every peer's rbuf) is kept behind MI355X_KNOB_PUSH.
 #include <fcntl.h>
 #include <sched.h>
 #include <sys/mman.h>
@@ -442,6 +446,7 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
         coll_tune().blocks_per_cu = (int)value;
         break;
     case MI355X_KNOB_TIMEOUT_S: c->timeout_s = (double)value; break;
+    case MI355X_KNOB_PUSH: coll_tune().push = value ? 1 : 0; break;
     default: return set_error(MI355X_ERR_ARG, "unknown knob %d", knob);
     }
     return MI355X_SUCCESS;
@@ -523,13 +528,9 @@ int mi355x_allreduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t coun
     std::vector<std::vector<void *>> P;
     rc = exchange(c, 2, mine, sig, P);
     if (rc) return rc;
-    size_t off, len;
-    ring_block(count, c->size, c->rank, &off, &len);
     Program pr;
-    if (alg == AR_RING || alg == AR_RING_SEGMENTED) {
-        // segmented ring splits each ring block into phases but keeps the block's fold order
-        pr = ring_block_program(c->size, c->rank);
-    } else {
+    const bool ring = (alg == AR_RING || alg == AR_RING_SEGMENTED);
+    if (!ring) {
         ExprPool ep;
         int root;
         if (alg == AR_RECDBL) {
@@ -540,8 +541,44 @@ int mi355x_allreduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t coun
             root = expr_reduce(ep, ra, c->size, 0);
         }
         if (!compile_expr(ep, root, c->size, &pr)) return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
+        if (sbuf && sbuf != rbuf) {
+            // tree orders (small messages): every rank evaluates the whole vector from the n
+            // inputs and writes only its own rbuf -- one phase, reads only
+            std::vector<void *> dst(1, rbuf);
+            rc = run_program(op, type, pr, P[0], dst, 0, count, s);
+            if (rc) return rc;
+            return finish(c, s);
+        }
     }
-    rc = run_program(op, type, pr, P[0], P[1], off, len, s);
+    // owner-computes: rank r evaluates ring block r (the reference's block partition, so the
+    // ring's per-block order is one program per launch)
+    size_t off, len;
+    ring_block(count, c->size, c->rank, &off, &len);
+    if (ring) pr = ring_block_program(c->size, c->rank);
+    if (coll_tune().push) {
+        // one phase: the owner writes its block into every rank's rbuf
+        rc = run_program(op, type, pr, P[0], P[1], off, len, s);
+        if (rc) return rc;
+        return finish(c, s);
+    }
+    // phase 1: reduce own block locally; phase 2: pull every other block from its owner
+    std::vector<void *> dst(1, rbuf);
+    rc = run_program(op, type, pr, P[0], dst, off, len, s);
+    if (rc) return rc;
+    rc = finish(c, s);
+    if (rc) return rc;
+    MultiCopyArgs m;
+    std::memset(&m, 0, sizeof(m));
+    for (int q = 0; q < c->size; ++q) {
+        if (q == c->rank) continue;
+        size_t qo, ql;
+        ring_block(count, c->size, q, &qo, &ql);
+        m.src[m.nseg] = (const char *)P[1][q] + qo * esz;
+        m.dst[m.nseg] = (char *)rbuf + qo * esz;
+        m.len[m.nseg] = ql * esz;
+        m.nseg++;
+    }
+    rc = launch_multicopy(m, s);
     if (rc) return rc;
     return finish(c, s);
 }
@@ -648,7 +685,8 @@ int mi355x_reduce_scatter(mi355x_comm_t *c, const void *sbuf, void *rbuf, const 
     return MI355X_SUCCESS;
 }
 
-// MPI_Allgather of `bytes` per rank (contiguous); sbuf NULL = MPI_IN_PLACE
+// MPI_Allgather of `bytes` per rank (contiguous); sbuf NULL = MPI_IN_PLACE.  Pull: one launch
+// copies every peer's block concurrently (one segment per peer -> every link busy).
 int mi355x_allgather(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, void *stream)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
@@ -656,26 +694,42 @@ int mi355x_allgather(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t byte
     hipStream_t s = resolve_stream(stream);
     const void *src = sbuf ? sbuf : (const char *)rbuf + (size_t)c->rank * bytes;
     MI_HIP(hipStreamSynchronize(s));
-    const void *mine[1] = {rbuf};
+    const void *mine[2] = {src, rbuf};
     const uint64_t sig[4] = {4, bytes, 0, 0};
     std::vector<std::vector<void *>> P;
-    int rc = exchange(c, 1, mine, sig, P);
+    int rc = exchange(c, 2, mine, sig, P);
     if (rc) return rc;
     c->last_alg = 1;
-    CopyArgs a;
-    std::memset(&a, 0, sizeof(a));
-    a.src = src;
-    a.nd = c->size;
-    for (int q = 0; q < c->size; ++q) a.dst[q] = (char *)P[0][q] + (size_t)c->rank * bytes;
-    a.n = bytes;
-    rc = launch_copy(a, s);
+    if (coll_tune().push) {
+        CopyArgs a;
+        std::memset(&a, 0, sizeof(a));
+        a.src = src;
+        a.nd = c->size;
+        for (int q = 0; q < c->size; ++q) a.dst[q] = (char *)P[1][q] + (size_t)c->rank * bytes;
+        a.n = bytes;
+        rc = launch_copy(a, s);
+        if (rc) return rc;
+        return finish(c, s);
+    }
+    MultiCopyArgs m;
+    std::memset(&m, 0, sizeof(m));
+    for (int q = 0; q < c->size; ++q) {
+        char *d = (char *)rbuf + (size_t)q * bytes;
+        if (P[0][q] == d) continue;  // in place: own block already there
+        m.src[m.nseg] = P[0][q];
+        m.dst[m.nseg] = d;
+        m.len[m.nseg] = bytes;
+        m.nseg++;
+    }
+    rc = launch_multicopy(m, s);
     if (rc) return rc;
     return finish(c, s);
 }
 
-// MPI_Bcast of `bytes` from root: rank r moves slice r of the root buffer to every non-root rank
-// (scatter + allgather shape: every xGMI link carries ~2/n of the message instead of the root's
-// links carrying all of it).
+// MPI_Bcast of `bytes` from root.  Small messages: every rank pulls the whole buffer from the
+// root.  Large: scatter + allgather shape (each rank first pulls its slice from the root, then the
+// other slices from their owners), so each xGMI link carries ~2/n of the message instead of the
+// root's links carrying all of it.
 int mi355x_bcast(mi355x_comm_t *c, void *buf, size_t bytes, int root, void *stream)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
@@ -688,18 +742,47 @@ int mi355x_bcast(mi355x_comm_t *c, void *buf, size_t bytes, int root, void *stre
     std::vector<std::vector<void *>> P;
     int rc = exchange(c, 1, mine, sig, P);
     if (rc) return rc;
-    c->last_alg = 1;
+    const bool split = bytes >= ((size_t)1 << 20);
+    c->last_alg = split ? 2 : 1;
+    MultiCopyArgs m;
+    std::memset(&m, 0, sizeof(m));
+    if (!split) {
+        if (c->rank != root) {
+            m.src[0] = P[0][root];
+            m.dst[0] = buf;
+            m.len[0] = bytes;
+            m.nseg = 1;
+            rc = launch_multicopy(m, s);
+            if (rc) return rc;
+        }
+        return finish(c, s);
+    }
     size_t off, len;
     ring_block(bytes, c->size, c->rank, &off, &len);
-    CopyArgs a;
-    std::memset(&a, 0, sizeof(a));
-    a.src = (const char *)P[0][root] + off;
-    a.nd = 0;
-    for (int q = 0; q < c->size; ++q)
-        if (q != root) a.dst[a.nd++] = (char *)P[0][q] + off;
-    a.n = len;
-    rc = launch_copy(a, s);
+    if (c->rank != root) {
+        m.src[0] = (const char *)P[0][root] + off;
+        m.dst[0] = (char *)buf + off;
+        m.len[0] = len;
+        m.nseg = 1;
+        rc = launch_multicopy(m, s);
+        if (rc) return rc;
+    }
+    rc = finish(c, s);
     if (rc) return rc;
+    std::memset(&m, 0, sizeof(m));
+    if (c->rank != root) {
+        for (int q = 0; q < c->size; ++q) {
+            if (q == c->rank) continue;
+            size_t qo, ql;
+            ring_block(bytes, c->size, q, &qo, &ql);
+            m.src[m.nseg] = (const char *)P[0][q] + qo;  // slice q is complete at rank q (or root)
+            m.dst[m.nseg] = (char *)buf + qo;
+            m.len[m.nseg] = ql;
+            m.nseg++;
+        }
+        rc = launch_multicopy(m, s);
+        if (rc) return rc;
+    }
     return finish(c, s);
 }
 

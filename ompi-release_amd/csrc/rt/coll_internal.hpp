@@ -46,13 +46,27 @@ struct CopyArgs {
     size_t n, head, nvec;        // n in bytes
 };
 
+// k_multicopy: nseg independent byte segments copied concurrently by one launch (the pull side of
+// allgather / the distribution phase of allreduce: one segment per peer, so every xGMI link is
+// busy at once).  Blocks are dealt to segments in proportion to their length.
+constexpr int kMaxSegs = kMaxRanks;
+struct MultiCopyArgs {
+    const void *src[kMaxSegs];
+    void *dst[kMaxSegs];
+    size_t len[kMaxSegs];
+    unsigned first_block[kMaxSegs + 1];  // segment s owns blocks [first_block[s], first_block[s+1])
+    int nseg;
+};
+
 struct CollTune {
     int blocks_per_cu = 4;
+    int push = 0;   // 1: allreduce owners write into the peers' rbufs (one phase); 0: pull (two phases)
 };
 CollTune &coll_tune();
 
 int launch_fold_slot(int op, int type, const FoldArgs &a, hipStream_t s);
 int launch_tree_slot(int op, int type, const TreeArgs &a, hipStream_t s);
 int launch_copy(CopyArgs a, hipStream_t s);
+int launch_multicopy(MultiCopyArgs a, hipStream_t s);
 
 } // namespace mi355x

@@ -216,6 +216,44 @@ __global__ __launch_bounds__(256) void k_copy(CopyArgs a)
         for (int d = 0; d < a.nd; ++d) static_cast<char *>(a.dst[d])[i] = s[i];
 }
 
+// ------------------------------------------------------------------ multi-segment copy
+__global__ __launch_bounds__(256) void k_multicopy(MultiCopyArgs a)
+{
+    // find this block's segment (<= 64 segments, uniform per block)
+    int sgi = 0;
+    while (sgi + 1 < a.nseg && blockIdx.x >= a.first_block[sgi + 1]) ++sgi;
+    const unsigned nb = a.first_block[sgi + 1] - a.first_block[sgi];
+    const unsigned b = blockIdx.x - a.first_block[sgi];
+    const char *s = static_cast<const char *>(a.src[sgi]);
+    char *d = static_cast<char *>(a.dst[sgi]);
+    const size_t n = a.len[sgi];
+    const size_t tid = (size_t)b * blockDim.x + threadIdx.x;
+    const size_t nthr = (size_t)nb * blockDim.x;
+    const uintptr_t ms = (uintptr_t)s & 15, md = (uintptr_t)d & 15;
+    size_t head = n, nvec = 0;
+    if (ms == md) {
+        head = ms ? 16 - ms : 0;
+        if (head > n) head = n;
+        nvec = (n - head) / 16;
+    }
+    for (size_t i = tid; i < head; i += nthr) d[i] = s[i];
+    constexpr int U = 4;
+    for (size_t base = tid; base < nvec; base += nthr * U) {
+        u32x4c x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t v = base + (size_t)u * nthr;
+            if (v < nvec) x[u] = *reinterpret_cast<const u32x4c *>(s + head + v * 16);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t v = base + (size_t)u * nthr;
+            if (v < nvec) *reinterpret_cast<u32x4c *>(d + head + v * 16) = x[u];
+        }
+    }
+    for (size_t i = head + nvec * 16 + tid; i < n; i += nthr) d[i] = s[i];
+}
+
 // ------------------------------------------------------------------ launchers
 static size_t grid_for(size_t work, int blocks_per_cu)
 {
@@ -280,6 +318,29 @@ int launch_copy(CopyArgs a, hipStream_t s)
     size_t work = a.nvec ? (a.nvec + 3) / 4 : a.n;
     const size_t blocks = grid_for(work, coll_tune().blocks_per_cu);
     hipLaunchKernelGGL(k_copy, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    MI_HIP(hipGetLastError());
+    return MI355X_SUCCESS;
+}
+
+int launch_multicopy(MultiCopyArgs a, hipStream_t s)
+{
+    size_t total = 0;
+    for (int i = 0; i < a.nseg; ++i) total += a.len[i];
+    if (total == 0) return MI355X_SUCCESS;
+    // about 4 KiB of work per thread-block iteration; at most blocks_per_cu x CUs blocks overall
+    const size_t cap = (size_t)coll_tune().blocks_per_cu * (size_t)device_cu_count();
+    unsigned next = 0;
+    for (int i = 0; i < a.nseg; ++i) {
+        a.first_block[i] = next;
+        size_t want = (a.len[i] + 4095) / 4096;
+        size_t share = total ? (cap * a.len[i] + total - 1) / total : 1;
+        size_t nb = want < share ? want : share;
+        if (a.len[i] && nb == 0) nb = 1;
+        next += (unsigned)nb;
+    }
+    a.first_block[a.nseg] = next;
+    if (next == 0) return MI355X_SUCCESS;
+    hipLaunchKernelGGL(k_multicopy, dim3(next), dim3(256), 0, s, a);
     MI_HIP(hipGetLastError());
     return MI355X_SUCCESS;
 }

@@ -74,9 +74,18 @@ def comms(gpu, pkg):
 @pytest.mark.parametrize("n", [2, 3, 4, 8])
 @pytest.mark.parametrize("alg", [0, 3, 4, 5])
 @pytest.mark.parametrize("inplace", [False, True])
-def test_allreduce(gpu, pkg, oracle, comms, n, alg, inplace):
+@pytest.mark.parametrize("push", [0, 1])
+def test_allreduce(gpu, pkg, oracle, comms, n, alg, inplace, push):
     torch = gpu
     cs = comms(n)
+    cs[0].set("PUSH", push)
+    try:
+        _allreduce_cases(torch, pkg, oracle, cs, n, alg, inplace)
+    finally:
+        cs[0].set("PUSH", 0)
+
+
+def _allreduce_cases(torch, pkg, oracle, cs, n, alg, inplace):
     for opname, tname in CASES:
         op, ty = pkg.OP[opname], pkg.T[tname]
         esz = pkg.type_size(ty)
@@ -170,9 +179,11 @@ def test_reduce_scatter(gpu, pkg, oracle, comms, n, rsalg):
 @pytest.mark.parametrize("n", [2, 3, 8])
 @pytest.mark.parametrize("nbytes", [1, 13, 4096, 1_000_003])
 @pytest.mark.parametrize("inplace", [False, True])
-def test_allgather(gpu, pkg, comms, n, nbytes, inplace):
+@pytest.mark.parametrize("push", [0, 1])
+def test_allgather(gpu, pkg, comms, n, nbytes, inplace, push):
     torch = gpu
     cs = comms(n)
+    cs[0].set("PUSH", push)
     src = [torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda") for _ in range(n)]
     dst = [torch.zeros(n * nbytes, dtype=torch.uint8, device="cuda") for _ in range(n)]
     if inplace:
@@ -181,13 +192,14 @@ def test_allgather(gpu, pkg, comms, n, nbytes, inplace):
     torch.cuda.synchronize()
     run_ranks(n, lambda r: cs[r].allgather(None if inplace else src[r].data_ptr(), dst[r].data_ptr(), nbytes))
     torch.cuda.synchronize()
+    cs[0].set("PUSH", 0)
     want = torch.cat(src)
     for r in range(n):
         assert torch.equal(dst[r], want), r
 
 
 @pytest.mark.parametrize("n", [2, 3, 8])
-@pytest.mark.parametrize("nbytes", [1, 7, 65536, 3_000_001])
+@pytest.mark.parametrize("nbytes", [1, 7, 65536, 1 << 20, 3_000_001])
 def test_bcast(gpu, pkg, comms, n, nbytes):
     torch = gpu
     cs = comms(n)
