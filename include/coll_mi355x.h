@@ -1,0 +1,58 @@
+/*
+ * coll_mi355x.h -- the coll/mi355x MCA component (lib/mca_coll_mi355x.so).
+ *
+ * Plugs into the coll framework (ompi/mca/coll/coll.h:357-451) at priority 90 -- above
+ * coll/tuned (30) and coll/cuda (78) -- for intra-communicators whose ranks all live on this
+ * node.  It provides allreduce, reduce_scatter, reduce_scatter_block, allgather and bcast; every
+ * other slot stays with the lower-priority modules.  Entry points have exactly the reference
+ * signatures (coll.h:181-239) and replace, for device buffers:
+ *   mca_coll_cuda_allreduce            (ompi/mca/coll/cuda/coll_cuda_allreduce.c:30-77)
+ *   mca_coll_cuda_reduce_scatter_block (coll_cuda_reduce_scatter_block.c:34-83)
+ *   ompi_coll_tuned_*_intra_dec_fixed  (coll_tuned_decision_fixed.c) reached on device buffers
+ * with results identical to the tuned/basic schedules (same per-element operand order).
+ *
+ * Host buffers, user-defined ops, non-contiguous or non-reducible datatypes go to the function
+ * that was installed in the slot before this module (snapshotted at enable time, retained, as
+ * coll/cuda does at coll_cuda_module.c:120-157).
+ *
+ * Host facts the component reads from the Open MPI 1.8 launcher environment:
+ *   OMPI_COMM_WORLD_SIZE / OMPI_COMM_WORLD_LOCAL_SIZE  (orte/mca/ess/base/ess_base_put.c:76,87)
+ *     -> the job is single-node (else the component declines);
+ *   OMPI_COMM_WORLD_LOCAL_RANK (orte/mca/odls/base/odls_base_default_fns.c:863) -> GPU index;
+ *   OMPI_MCA_ess_base_jobid (:817) + the communicator's c_contextid -> node-unique rendezvous key.
+ * The mini-OMPI harness (libompi_mini) sets the same variables.
+ */
+#ifndef MI355X_COLL_MI355X_H
+#define MI355X_COLL_MI355X_H
+
+#include "ompi_abi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+extern mca_coll_base_component_t mca_coll_mi355x_component;
+
+int mca_coll_mi355x_allreduce(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                              struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                              mca_coll_base_module_t *module);
+int mca_coll_mi355x_reduce_scatter_block(void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dtype,
+                                         struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                                         mca_coll_base_module_t *module);
+int mca_coll_mi355x_reduce_scatter(void *sbuf, void *rbuf, int *rcounts, struct ompi_datatype_t *dtype,
+                                   struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                                   mca_coll_base_module_t *module);
+int mca_coll_mi355x_allgather(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
+                              struct ompi_datatype_t *rdtype, struct ompi_communicator_t *comm,
+                              mca_coll_base_module_t *module);
+int mca_coll_mi355x_bcast(void *buff, int count, struct ompi_datatype_t *datatype, int root,
+                          struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+
+/* MCA parameters (environment: OMPI_MCA_coll_mi355x_<name>) */
+extern int mca_coll_mi355x_priority;            /* 90 */
+extern int mca_coll_mi355x_allreduce_algorithm; /* 0 = tuned decision, else coll_tuned numbering */
+
+#ifdef __cplusplus
+}
+#endif
+#endif

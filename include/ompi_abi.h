@@ -1,0 +1,379 @@
+/*
+ * ompi_abi.h -- the subset of the Open MPI 1.8.5 binary interface that the op/hip and
+ * coll/mi355x MCA components touch, restated from the reference headers (layouts, not code).
+ *
+ * Configure profile this is pinned to (the one the SURVEY's reference build uses):
+ *   x86-64 Linux, LP64, OPAL_ENABLE_DEBUG = 0, POSIX threads, OPAL_MAX_OBJECT_NAME = 64,
+ *   OMPI_WANT_PERUSE defined (the field is present whenever the macro is defined,
+ *   communicator.h:147-152), Fortran bindings disabled.
+ * Every struct cites its reference definition; tests/test_boundary.py checks the offsets the
+ * components depend on against the values derived from those definitions.  Components include
+ * this header instead of the reference tree's headers when built out of tree;
+ * the symbols they need at run time (opal_class_initialize, the module classes,
+ * ompi_op_ddt_map) come from libmpi / libopen-pal, or from libompi_mini in the test harness.
+ */
+#ifndef MI355X_OMPI_ABI_H
+#define MI355X_OMPI_ABI_H
+
+#include <pthread.h>
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ constants */
+#define OMPI_SUCCESS 0                 /* opal/include/opal/constants.h:29 */
+#define OMPI_ERROR (-1)                /* :31 */
+#define OMPI_ERR_OUT_OF_RESOURCE (-2)  /* :32 */
+#define OMPI_ERR_BAD_PARAM (-5)        /* :35 */
+#define OMPI_ERR_NOT_SUPPORTED (-8)    /* :38 */
+#define OMPI_ERR_NOT_FOUND (-13)       /* :43 */
+#define MPI_MAX_OBJECT_NAME 64         /* ompi/include/mpi.h.in:421 (= OPAL_MAX_OBJECT_NAME) */
+#define MPI_IN_PLACE ((void *)1)       /* mpi.h.in:435 */
+#define OMPI_COMM_INTER 0x00000001     /* ompi/communicator/communicator.h:45 */
+#define OMPI_OP_FLAGS_INTRINSIC 0x0001 /* ompi/op/op.h:91 */
+#define OMPI_OP_FLAGS_COMMUTE 0x0040   /* ompi/op/op.h:109 */
+#define OMPI_OP_BASE_TYPE_MAX 39       /* ompi/mca/op/op.h:182 */
+#define OMPI_DATATYPE_MPI_MAX_PREDEFINED 0x30 /* ompi/datatype/ompi_datatype_internal.h:79 */
+
+/* ------------------------------------------------------------------ opal objects */
+/* opal/class/opal_object.h:140-197 (non-debug) */
+typedef struct opal_object_t opal_object_t;
+typedef struct opal_class_t opal_class_t;
+typedef void (*opal_construct_t)(opal_object_t *);
+typedef void (*opal_destruct_t)(opal_object_t *);
+
+struct opal_class_t {
+    const char *cls_name;
+    opal_class_t *cls_parent;
+    opal_construct_t cls_construct;
+    opal_destruct_t cls_destruct;
+    int cls_initialized;
+    int cls_depth;
+    opal_construct_t *cls_construct_array;
+    opal_destruct_t *cls_destruct_array;
+    size_t cls_sizeof;
+};
+
+struct opal_object_t {
+    opal_class_t *obj_class;
+    volatile int32_t obj_reference_count;
+};
+
+/* provided by libopen-pal (opal/class/opal_object.c) or by the harness */
+void opal_class_initialize(opal_class_t *cls);
+
+/* OBJ_NEW / OBJ_RETAIN / OBJ_RELEASE semantics of opal_object.h:250-330, 440-503 */
+static inline opal_object_t *mi355x_obj_new(opal_class_t *cls)
+{
+    opal_object_t *o = (opal_object_t *)malloc(cls->cls_sizeof);
+    if (0 == cls->cls_initialized) opal_class_initialize(cls);
+    if (o) {
+        o->obj_class = cls;
+        o->obj_reference_count = 1;
+        for (opal_construct_t *c = cls->cls_construct_array; c && *c; ++c) (*c)(o);
+    }
+    return o;
+}
+static inline void mi355x_obj_retain(opal_object_t *o)
+{
+    __atomic_add_fetch(&o->obj_reference_count, 1, __ATOMIC_ACQ_REL);
+}
+static inline int mi355x_obj_release(opal_object_t *o)  /* returns 1 if freed */
+{
+    if (0 == __atomic_sub_fetch(&o->obj_reference_count, 1, __ATOMIC_ACQ_REL)) {
+        for (opal_destruct_t *d = o->obj_class->cls_destruct_array; d && *d; ++d) (*d)(o);
+        free(o);
+        return 1;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ MCA component base */
+/* opal/mca/mca.h:230-296 */
+typedef int (*mca_base_open_component_fn_t)(void);
+typedef int (*mca_base_close_component_fn_t)(void);
+typedef int (*mca_base_query_component_fn_t)(void **module, int *priority);
+typedef int (*mca_base_register_component_params_fn_t)(void);
+
+typedef struct mca_base_component_2_0_0_t {
+    int mca_major_version;
+    int mca_minor_version;
+    int mca_release_version;
+    char mca_type_name[32];
+    int mca_type_major_version;
+    int mca_type_minor_version;
+    int mca_type_release_version;
+    char mca_component_name[64];
+    int mca_component_major_version;
+    int mca_component_minor_version;
+    int mca_component_release_version;
+    mca_base_open_component_fn_t mca_open_component;
+    mca_base_close_component_fn_t mca_close_component;
+    mca_base_query_component_fn_t mca_query_component;
+    mca_base_register_component_params_fn_t mca_register_component_params;
+    char reserved[32];
+} mca_base_component_t;
+
+typedef struct mca_base_component_data_2_0_0_t {
+    uint32_t param_field;
+    char reserved[32];
+} mca_base_component_data_t;
+
+#define MCA_BASE_VERSION_2_0_0 2, 0, 0   /* opal/mca/mca.h:312 */
+
+/* ------------------------------------------------------------------ datatypes */
+/* opal/datatype/opal_datatype.h:103-131, opal_datatype_internal.h:148-188 */
+typedef struct dt_elem_desc dt_elem_desc_t;
+typedef struct dt_type_desc {
+    uint32_t length;
+    uint32_t used;
+    dt_elem_desc_t *desc;
+} dt_type_desc_t;
+
+typedef struct opal_datatype_t {
+    opal_object_t super;
+    uint16_t flags;
+    uint16_t id;
+    uint32_t bdt_used;
+    size_t size;
+    ptrdiff_t true_lb;
+    ptrdiff_t true_ub;
+    ptrdiff_t lb;
+    ptrdiff_t ub;
+    size_t nbElems;
+    uint32_t align;
+    char name[64];
+    dt_type_desc_t desc;
+    dt_type_desc_t opt_desc;
+    uint32_t btypes[47];      /* OPAL_DATATYPE_MAX_SUPPORTED */
+} opal_datatype_t;
+
+#define OPAL_DATATYPE_FLAG_PREDEFINED 0x0002  /* opal/datatype/opal_datatype.h:66 */
+#define OPAL_DATATYPE_FLAG_CONTIGUOUS 0x0010  /* :69 */
+#define OPAL_DATATYPE_FLAG_NO_GAPS 0x0020     /* :70, contiguous and extent == size */
+
+/* ompi/datatype/ompi_datatype.h:73-88 */
+typedef struct ompi_datatype_t {
+    opal_datatype_t super;
+    int32_t id;
+    int32_t d_f_to_c_index;
+    void *d_keyhash;
+    void *args;
+    void *packed_description;
+    char name[MPI_MAX_OBJECT_NAME];
+} ompi_datatype_t;
+
+/* ompi/op/op.c:98: datatype id -> OMPI_OP_BASE_TYPE_* slot (-1: not reducible) */
+extern int ompi_op_ddt_map[OMPI_DATATYPE_MPI_MAX_PREDEFINED];
+
+/* ------------------------------------------------------------------ op framework */
+struct ompi_op_base_module_1_0_0_t;
+struct ompi_op_t;
+
+/* ompi/mca/op/op.h:253-266 */
+typedef void (*ompi_op_base_handler_fn_t)(void *, void *, int *, struct ompi_datatype_t **,
+                                          struct ompi_op_base_module_1_0_0_t *);
+typedef void (*ompi_op_base_3buff_handler_fn_t)(void *, void *, void *, int *,
+                                                struct ompi_datatype_t **,
+                                                struct ompi_op_base_module_1_0_0_t *);
+typedef int (*ompi_op_base_component_init_query_fn_t)(bool enable_progress_threads,
+                                                      bool enable_mpi_threads);
+typedef struct ompi_op_base_module_1_0_0_t *(*ompi_op_base_component_op_query_fn_t)(
+    struct ompi_op_t *op, int *priority);
+typedef int (*ompi_op_base_module_enable_fn_t)(struct ompi_op_base_module_1_0_0_t *module,
+                                               struct ompi_op_t *op);
+
+/* op.h:326-336 */
+typedef struct ompi_op_base_component_1_0_0_t {
+    mca_base_component_t opc_version;
+    mca_base_component_data_t opc_data;
+    ompi_op_base_component_init_query_fn_t opc_init_query;
+    ompi_op_base_component_op_query_fn_t opc_op_query;
+} ompi_op_base_component_t;
+
+/* op.h:357-373 */
+typedef struct ompi_op_base_module_1_0_0_t {
+    opal_object_t super;
+    ompi_op_base_module_enable_fn_t opm_enable;
+    struct ompi_op_t *opm_op;
+    ompi_op_base_handler_fn_t opm_fns[OMPI_OP_BASE_TYPE_MAX];
+    ompi_op_base_3buff_handler_fn_t opm_3buff_fns[OMPI_OP_BASE_TYPE_MAX];
+} ompi_op_base_module_t;
+
+/* class object of ompi_op_base_module_t (op_base_frame.c:43-62), exported by libmpi */
+extern opal_class_t ompi_op_base_module_t_class;
+
+/* op.h:388-403 */
+typedef struct ompi_op_base_op_fns_1_0_0_t {
+    ompi_op_base_handler_fn_t fns[OMPI_OP_BASE_TYPE_MAX];
+    ompi_op_base_module_t *modules[OMPI_OP_BASE_TYPE_MAX];
+} ompi_op_base_op_fns_t;
+typedef struct ompi_op_base_op_3buff_fns_1_0_0_t {
+    ompi_op_base_3buff_handler_fn_t fns[OMPI_OP_BASE_TYPE_MAX];
+    ompi_op_base_module_t *modules[OMPI_OP_BASE_TYPE_MAX];
+} ompi_op_base_op_3buff_fns_t;
+
+#define OMPI_OP_BASE_VERSION_1_0_0 MCA_BASE_VERSION_2_0_0, "op", 1, 0, 0  /* op.h:412-414 */
+
+/* ompi/op/op.h:138-188 */
+typedef struct ompi_op_t {
+    opal_object_t super;
+    char o_name[MPI_MAX_OBJECT_NAME];
+    int op_type;                     /* enum ompi_op_type */
+    uint32_t o_flags;
+    int o_f_to_c_index;
+    union {
+        ompi_op_base_op_fns_t intrinsic;
+        void *c_fn;
+        void *fort_fn;
+        struct { void *user_fn; void *intercept_fn; } cxx_data;
+        struct { void *intercept_fn; void *jnienv, *object; int baseType; } java_data;
+    } o_func;
+    ompi_op_base_op_3buff_fns_t o_3buff_intrinsic;
+} ompi_op_t;
+
+/* ------------------------------------------------------------------ communicators */
+/* opal/threads/mutex_unix.h:50-64 (non-debug, POSIX threads) */
+typedef struct opal_mutex_t {
+    opal_object_t super;
+    pthread_mutex_t m_lock_pthread;
+    int32_t m_lock_atomic;           /* opal_atomic_lock_t */
+} opal_mutex_t;
+
+/* ompi/group/group.h:81-98 (prefix used by the components) */
+typedef struct ompi_group_t {
+    opal_object_t super;
+    int grp_proc_count;
+    int grp_my_rank;
+    int grp_f_to_c_index;
+    struct ompi_proc_t **grp_proc_pointers;
+    uint32_t grp_flags;
+    struct ompi_group_t *grp_parent_group_ptr;
+} ompi_group_t;
+
+struct ompi_communicator_t;
+struct mca_coll_base_module_2_0_0_t;
+typedef struct mca_coll_base_module_2_0_0_t mca_coll_base_module_t;
+
+/* ompi/mca/coll/coll.h:181-239 */
+typedef int (*mca_coll_base_module_allgather_fn_t)(void *sbuf, int scount, struct ompi_datatype_t *sdtype,
+                                                   void *rbuf, int rcount, struct ompi_datatype_t *rdtype,
+                                                   struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_allreduce_fn_t)(void *sbuf, void *rbuf, int count,
+                                                   struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                                   struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_bcast_fn_t)(void *buff, int count, struct ompi_datatype_t *datatype, int root,
+                                               struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_reduce_fn_t)(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                                                struct ompi_op_t *op, int root, struct ompi_communicator_t *comm,
+                                                mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_reduce_scatter_fn_t)(void *sbuf, void *rbuf, int *rcounts,
+                                                        struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                                        struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_reduce_scatter_block_fn_t)(void *sbuf, void *rbuf, int rcount,
+                                                              struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                                              struct ompi_communicator_t *comm,
+                                                              mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_enable_fn_t)(mca_coll_base_module_t *module, struct ompi_communicator_t *comm);
+typedef int (*mca_coll_base_module_ft_event_fn_t)(int state);
+typedef void (*mca_coll_base_any_fn_t)(void);   /* slots the components never call */
+
+/* coll.h:390-451: 17 blocking, 17 nonblocking, 10 neighborhood function pointers */
+struct mca_coll_base_module_2_0_0_t {
+    opal_object_t super;
+    mca_coll_base_module_enable_fn_t coll_module_enable;
+    mca_coll_base_module_allgather_fn_t coll_allgather;
+    mca_coll_base_any_fn_t coll_allgatherv;
+    mca_coll_base_module_allreduce_fn_t coll_allreduce;
+    mca_coll_base_any_fn_t coll_alltoall;
+    mca_coll_base_any_fn_t coll_alltoallv;
+    mca_coll_base_any_fn_t coll_alltoallw;
+    mca_coll_base_any_fn_t coll_barrier;
+    mca_coll_base_module_bcast_fn_t coll_bcast;
+    mca_coll_base_any_fn_t coll_exscan;
+    mca_coll_base_any_fn_t coll_gather;
+    mca_coll_base_any_fn_t coll_gatherv;
+    mca_coll_base_module_reduce_fn_t coll_reduce;
+    mca_coll_base_module_reduce_scatter_fn_t coll_reduce_scatter;
+    mca_coll_base_module_reduce_scatter_block_fn_t coll_reduce_scatter_block;
+    mca_coll_base_any_fn_t coll_scan;
+    mca_coll_base_any_fn_t coll_scatter;
+    mca_coll_base_any_fn_t coll_scatterv;
+    mca_coll_base_any_fn_t coll_nonblocking[17];
+    mca_coll_base_any_fn_t coll_neighbor[10];
+    mca_coll_base_module_ft_event_fn_t ft_event;
+};
+
+/* class object of mca_coll_base_module_t (coll_base_frame.c:45-62), exported by libmpi */
+extern opal_class_t mca_coll_base_module_t_class;
+
+/* coll.h:469-566: (fn, module) pairs in the order of the module struct */
+typedef struct mca_coll_base_comm_coll_t {
+    mca_coll_base_module_allgather_fn_t coll_allgather;
+    mca_coll_base_module_t *coll_allgather_module;
+    mca_coll_base_any_fn_t coll_allgatherv;
+    mca_coll_base_module_t *coll_allgatherv_module;
+    mca_coll_base_module_allreduce_fn_t coll_allreduce;
+    mca_coll_base_module_t *coll_allreduce_module;
+    struct { mca_coll_base_any_fn_t fn; mca_coll_base_module_t *module; } coll_a2a[4]; /* alltoall(v,w), barrier */
+    mca_coll_base_module_bcast_fn_t coll_bcast;
+    mca_coll_base_module_t *coll_bcast_module;
+    struct { mca_coll_base_any_fn_t fn; mca_coll_base_module_t *module; } coll_egg[3];  /* exscan, gather(v) */
+    mca_coll_base_module_reduce_fn_t coll_reduce;
+    mca_coll_base_module_t *coll_reduce_module;
+    mca_coll_base_module_reduce_scatter_fn_t coll_reduce_scatter;
+    mca_coll_base_module_t *coll_reduce_scatter_module;
+    mca_coll_base_module_reduce_scatter_block_fn_t coll_reduce_scatter_block;
+    mca_coll_base_module_t *coll_reduce_scatter_block_module;
+    struct { mca_coll_base_any_fn_t fn; mca_coll_base_module_t *module; } coll_rest[3 + 17 + 10];
+} mca_coll_base_comm_coll_t;
+
+/* ompi/communicator/communicator.h:111-166 */
+typedef struct ompi_communicator_t {
+    opal_object_t c_base;
+    opal_mutex_t c_lock;
+    char c_name[MPI_MAX_OBJECT_NAME];
+    uint32_t c_contextid;
+    int c_my_rank;
+    uint32_t c_flags;
+    int c_id_available;
+    int c_id_start_index;
+    ompi_group_t *c_local_group;
+    ompi_group_t *c_remote_group;
+    struct ompi_communicator_t *c_local_comm;
+    void *c_keyhash;
+    int c_cube_dim;
+    void *c_topo;
+    int c_f_to_c_index;
+    void **c_peruse_handles;
+    void *error_handler;
+    int errhandler_type;
+    void *c_pml_comm;
+    mca_coll_base_comm_coll_t c_coll;
+} ompi_communicator_t;
+
+static inline int mi355x_comm_rank_of(const ompi_communicator_t *c) { return c->c_my_rank; }
+static inline int mi355x_comm_size_of(const ompi_communicator_t *c) { return c->c_local_group->grp_proc_count; }
+
+/* coll.h:105-139, 357-367 */
+typedef int (*mca_coll_base_component_init_query_fn_t)(bool enable_progress_threads, bool enable_mpi_threads);
+typedef mca_coll_base_module_t *(*mca_coll_base_component_comm_query_fn_t)(struct ompi_communicator_t *comm,
+                                                                           int *priority);
+typedef struct mca_coll_base_component_2_0_0_t {
+    mca_base_component_t collm_version;
+    mca_base_component_data_t collm_data;
+    mca_coll_base_component_init_query_fn_t collm_init_query;
+    mca_coll_base_component_comm_query_fn_t collm_comm_query;
+} mca_coll_base_component_t;
+
+#define MCA_COLL_BASE_VERSION_2_0_0 MCA_BASE_VERSION_2_0_0, "coll", 2, 0, 0  /* coll.h:576-578 */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MI355X_OMPI_ABI_H */

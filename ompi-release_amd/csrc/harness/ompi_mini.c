@@ -1,0 +1,406 @@
+/*
+ * ompi_mini.c -- "mini Open MPI": the few pieces of libmpi / libopen-pal that the op/hip and
+ * coll/mi355x components link against, restated so the components can be loaded, selected and
+ * called exactly as Open MPI 1.8.5 would, without a built Open MPI (none can be built here,
+ * SURVEY.md §0).  This is the host side the tests and examples drive; it contains no reduction
+ * arithmetic of its own (the "base" op functions are supplied by whoever sets up the harness).
+ *
+ * Restated behaviour (file:line of the reference):
+ *   opal_class_initialize            opal/class/opal_object.c:73-150 (construct/destruct arrays)
+ *   ompi_op_base_module_t class ctor ompi/mca/op/base/op_base_frame.c:43-62 (zeroes the tables)
+ *   mca_coll_base_module_t class ctor ompi/mca/coll/base/coll_base_frame.c:45-52
+ *   ompi_op_ddt_map                  ompi/op/op.c:125-215 (C types)
+ *   op selection                     ompi/mca/op/base/op_base_op_select.c:88-204, including the
+ *                                    2-buff/3-buff module release at :162-168
+ *   ompi_op_reduce / 3buff dispatch  ompi/op/op.h:540-636
+ *   op destruction                   ompi/op/op.c:476-487
+ *   coll selection                   ompi/mca/coll/base/coll_base_comm_select.c:114-262
+ */
+#include "ompi_mini.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ opal objects */
+void opal_class_initialize(opal_class_t *cls)
+{
+    if (cls->cls_initialized) return;
+    int depth = 0, nc = 0, nd = 0;
+    for (opal_class_t *c = cls; c; c = c->cls_parent) {
+        depth++;
+        if (c->cls_construct) nc++;
+        if (c->cls_destruct) nd++;
+    }
+    cls->cls_depth = depth;
+    opal_construct_t *ca = calloc((size_t)nc + 1, sizeof(*ca));
+    opal_destruct_t *da = calloc((size_t)nd + 1, sizeof(*da));
+    /* constructors run base -> derived, destructors derived -> base */
+    int i = nc;
+    for (opal_class_t *c = cls; c; c = c->cls_parent)
+        if (c->cls_construct) ca[--i] = c->cls_construct;
+    int j = 0;
+    for (opal_class_t *c = cls; c; c = c->cls_parent)
+        if (c->cls_destruct) da[j++] = c->cls_destruct;
+    cls->cls_construct_array = ca;
+    cls->cls_destruct_array = da;
+    cls->cls_initialized = 1;
+}
+
+static opal_class_t opal_object_t_class = {"opal_object_t", NULL, NULL, NULL, 0, 0, NULL, NULL,
+                                           sizeof(opal_object_t)};
+
+static void op_module_construct(opal_object_t *o)
+{
+    ompi_op_base_module_t *m = (ompi_op_base_module_t *)o;
+    m->opm_enable = NULL;
+    m->opm_op = NULL;
+    memset(m->opm_fns, 0, sizeof(m->opm_fns));
+    memset(m->opm_3buff_fns, 0, sizeof(m->opm_3buff_fns));
+}
+opal_class_t ompi_op_base_module_t_class = {"ompi_op_base_module_t", &opal_object_t_class, op_module_construct,
+                                            NULL, 0, 0, NULL, NULL, sizeof(ompi_op_base_module_t)};
+
+static void coll_module_construct(opal_object_t *o)
+{
+    mca_coll_base_module_t *m = (mca_coll_base_module_t *)o;
+    memset((char *)m + sizeof(opal_object_t), 0, sizeof(*m) - sizeof(opal_object_t));
+}
+opal_class_t mca_coll_base_module_t_class = {"mca_coll_base_module_t", &opal_object_t_class, coll_module_construct,
+                                             NULL, 0, 0, NULL, NULL, sizeof(mca_coll_base_module_t)};
+
+/* ------------------------------------------------------------------ datatypes / ddt map */
+int ompi_op_ddt_map[OMPI_DATATYPE_MPI_MAX_PREDEFINED];
+
+static struct { int id, slot; size_t size; const char *name; } predefined[] = {
+    {0x01, MI355X_T_INT8, 1, "MPI_INT8_T"},      {0x02, MI355X_T_UINT8, 1, "MPI_UINT8_T"},
+    {0x03, MI355X_T_INT16, 2, "MPI_INT16_T"},    {0x04, MI355X_T_UINT16, 2, "MPI_UINT16_T"},
+    {0x05, MI355X_T_INT32, 4, "MPI_INT32_T"},    {0x06, MI355X_T_UINT32, 4, "MPI_UINT32_T"},
+    {0x07, MI355X_T_INT64, 8, "MPI_INT64_T"},    {0x08, MI355X_T_UINT64, 8, "MPI_UINT64_T"},
+    {0x09, MI355X_T_FLOAT, 4, "MPI_FLOAT"},      {0x0A, MI355X_T_DOUBLE, 8, "MPI_DOUBLE"},
+    {0x0B, MI355X_T_LONG_DOUBLE, 16, "MPI_LONG_DOUBLE"},
+    {0x11, MI355X_T_BOOL, 1, "MPI_CXX_BOOL"},    {0x13, MI355X_T_UINT8, 1, "MPI_CHARACTER"},
+    {0x1A, MI355X_T_2INT, 8, "MPI_2INT"},        {0x20, MI355X_T_FLOAT_INT, 8, "MPI_FLOAT_INT"},
+    {0x21, MI355X_T_DOUBLE_INT, 16, "MPI_DOUBLE_INT"},
+    {0x22, MI355X_T_LONG_DOUBLE_INT, 32, "MPI_LONG_DOUBLE_INT"},
+    {0x23, MI355X_T_LONG_INT, 16, "MPI_LONG_INT"}, {0x24, MI355X_T_SHORT_INT, 8, "MPI_SHORT_INT"},
+    {0x27, MI355X_T_BOOL, 1, "MPI_C_BOOL"},
+    {0x29, MI355X_T_C_FLOAT_COMPLEX, 8, "MPI_C_FLOAT_COMPLEX"},
+    {0x2A, MI355X_T_C_DOUBLE_COMPLEX, 16, "MPI_C_DOUBLE_COMPLEX"},
+    {0x2B, MI355X_T_C_LONG_DOUBLE_COMPLEX, 32, "MPI_C_LONG_DOUBLE_COMPLEX"},
+};
+static ompi_datatype_t *dt_objs[OMPI_DATATYPE_MPI_MAX_PREDEFINED];
+
+static opal_class_t ompi_datatype_t_class = {"ompi_datatype_t", &opal_object_t_class, NULL, NULL, 0, 0, NULL,
+                                             NULL, sizeof(ompi_datatype_t)};
+
+void mini_init(void)
+{
+    static int done = 0;
+    if (done) return;
+    done = 1;
+    for (int i = 0; i < OMPI_DATATYPE_MPI_MAX_PREDEFINED; ++i) ompi_op_ddt_map[i] = -1;
+    for (size_t k = 0; k < sizeof(predefined) / sizeof(predefined[0]); ++k) {
+        ompi_op_ddt_map[predefined[k].id] = predefined[k].slot;
+        ompi_datatype_t *d = (ompi_datatype_t *)mi355x_obj_new(&ompi_datatype_t_class);
+        memset((char *)d + sizeof(opal_object_t), 0, sizeof(*d) - sizeof(opal_object_t));
+        d->super.flags = OPAL_DATATYPE_FLAG_PREDEFINED | OPAL_DATATYPE_FLAG_CONTIGUOUS | OPAL_DATATYPE_FLAG_NO_GAPS;
+        d->super.id = (uint16_t)predefined[k].id;
+        d->super.size = predefined[k].size;
+        d->super.true_ub = d->super.ub = (ptrdiff_t)predefined[k].size;
+        d->id = predefined[k].id;
+        snprintf(d->name, sizeof(d->name), "%s", predefined[k].name);
+        dt_objs[predefined[k].id] = d;
+    }
+}
+
+ompi_datatype_t *mini_datatype(int id)
+{
+    mini_init();
+    return (id >= 0 && id < OMPI_DATATYPE_MPI_MAX_PREDEFINED) ? dt_objs[id] : NULL;
+}
+
+int mini_datatype_id_for_slot(int slot)
+{
+    mini_init();
+    for (size_t k = 0; k < sizeof(predefined) / sizeof(predefined[0]); ++k)
+        if (predefined[k].slot == slot) return predefined[k].id;
+    return -1;
+}
+
+/* ------------------------------------------------------------------ ops */
+static ompi_op_base_handler_fn_t base2[MI355X_OP_MAX_][OMPI_OP_BASE_TYPE_MAX];
+static ompi_op_base_3buff_handler_fn_t base3[MI355X_OP_MAX_][OMPI_OP_BASE_TYPE_MAX];
+
+void mini_set_base_function(int op, int slot, void *fn2, void *fn3)
+{
+    base2[op][slot] = (ompi_op_base_handler_fn_t)fn2;
+    base3[op][slot] = (ompi_op_base_3buff_handler_fn_t)fn3;
+}
+
+static opal_class_t ompi_op_t_class = {"ompi_op_t", &opal_object_t_class, NULL, NULL, 0, 0, NULL, NULL,
+                                       sizeof(ompi_op_t)};
+
+ompi_op_t *mini_op_create(int code)
+{
+    mini_init();
+    ompi_op_t *op = (ompi_op_t *)mi355x_obj_new(&ompi_op_t_class);
+    memset((char *)op + sizeof(opal_object_t), 0, sizeof(*op) - sizeof(opal_object_t));
+    snprintf(op->o_name, sizeof(op->o_name), "MPI_OP_%d", code);
+    op->op_type = code;
+    op->o_f_to_c_index = code;
+    op->o_flags = OMPI_OP_FLAGS_INTRINSIC | OMPI_OP_FLAGS_COMMUTE;
+    return op;
+}
+
+/* ompi_op_base_op_select (op_base_op_select.c:88-204) over an explicit component list sorted by
+ * ascending priority by the caller's query results.  Returns OMPI_SUCCESS or an error. */
+int mini_op_select(ompi_op_t *op, ompi_op_base_component_t **comps, int ncomp)
+{
+    ompi_op_base_module_t *basemod = (ompi_op_base_module_t *)mi355x_obj_new(&ompi_op_base_module_t_class);
+    for (int i = 0; i < OMPI_OP_BASE_TYPE_MAX; ++i) {
+        op->o_func.intrinsic.fns[i] = base2[op->o_f_to_c_index][i];
+        op->o_func.intrinsic.modules[i] = basemod;
+        mi355x_obj_retain(&basemod->super);
+        op->o_3buff_intrinsic.fns[i] = base3[op->o_f_to_c_index][i];
+        op->o_3buff_intrinsic.modules[i] = basemod;
+        mi355x_obj_retain(&basemod->super);
+    }
+    mi355x_obj_release(&basemod->super);
+    /* query, keep the modules, sort by ascending priority (check_components :227-263) */
+    ompi_op_base_module_t *mods[16];
+    int prios[16], nm = 0;
+    for (int c = 0; c < ncomp && nm < 16; ++c) {
+        int prio = 0;
+        ompi_op_base_module_t *m = comps[c]->opc_op_query(op, &prio);
+        if (!m) continue;
+        if (prio > 100) prio = 100;
+        int k = nm++;
+        while (k > 0 && prios[k - 1] > prio) { mods[k] = mods[k - 1]; prios[k] = prios[k - 1]; --k; }
+        mods[k] = m;
+        prios[k] = prio;
+    }
+    for (int k = 0; k < nm; ++k) {
+        ompi_op_base_module_t *m = mods[k];
+        if (m->opm_enable && OMPI_SUCCESS != m->opm_enable(m, op)) {
+            mi355x_obj_release(&m->super);
+            continue;
+        }
+        for (int i = 0; i < OMPI_OP_BASE_TYPE_MAX; ++i) {
+            if (m->opm_fns[i]) {
+                mi355x_obj_release(&op->o_func.intrinsic.modules[i]->super);
+                op->o_func.intrinsic.fns[i] = m->opm_fns[i];
+                op->o_func.intrinsic.modules[i] = m;
+                mi355x_obj_retain(&m->super);
+            }
+            if (m->opm_3buff_fns[i]) {
+                /* op_base_op_select.c:162-168 releases the 2-buff slot's module here */
+                mi355x_obj_release(&op->o_func.intrinsic.modules[i]->super);
+                op->o_3buff_intrinsic.fns[i] = m->opm_3buff_fns[i];
+                op->o_3buff_intrinsic.modules[i] = m;
+                mi355x_obj_retain(&m->super);
+            }
+        }
+        mi355x_obj_release(&m->super);
+    }
+    for (int i = 0; i < OMPI_OP_BASE_TYPE_MAX; ++i) {
+        const int want = base2[op->o_f_to_c_index][i] != NULL;
+        if (want != (op->o_func.intrinsic.fns[i] != NULL)) return OMPI_ERR_NOT_FOUND;
+    }
+    return OMPI_SUCCESS;
+}
+
+void mini_op_reduce(ompi_op_t *op, void *source, void *target, int count, ompi_datatype_t *dtype)
+{
+    const int t = ompi_op_ddt_map[dtype->id];
+    op->o_func.intrinsic.fns[t](source, target, &count, &dtype, op->o_func.intrinsic.modules[t]);
+}
+
+void mini_op_reduce_3buff(ompi_op_t *op, void *s1, void *s2, void *target, int count, ompi_datatype_t *dtype)
+{
+    const int t = ompi_op_ddt_map[dtype->id];
+    op->o_3buff_intrinsic.fns[t](s1, s2, target, &count, &dtype, op->o_3buff_intrinsic.modules[t]);
+}
+
+void *mini_op_fn2(ompi_op_t *op, int slot) { return (void *)op->o_func.intrinsic.fns[slot]; }
+void *mini_op_module2(ompi_op_t *op, int slot) { return op->o_func.intrinsic.modules[slot]; }
+void *mini_op_module3(ompi_op_t *op, int slot) { return op->o_3buff_intrinsic.modules[slot]; }
+int mini_obj_refcount(void *obj) { return ((opal_object_t *)obj)->obj_reference_count; }
+
+/* ompi_op_destruct (op.c:476-487): release every slot's module, 2-buff then 3-buff */
+void mini_op_destroy(ompi_op_t *op)
+{
+    for (int i = 0; i < OMPI_OP_BASE_TYPE_MAX; ++i) {
+        if (op->o_func.intrinsic.modules[i]) mi355x_obj_release(&op->o_func.intrinsic.modules[i]->super);
+        if (op->o_3buff_intrinsic.modules[i]) mi355x_obj_release(&op->o_3buff_intrinsic.modules[i]->super);
+    }
+    free(op);
+}
+
+/* ------------------------------------------------------------------ communicators */
+static opal_class_t comm_class = {"ompi_communicator_t", &opal_object_t_class, NULL, NULL, 0, 0, NULL, NULL,
+                                  sizeof(ompi_communicator_t)};
+static opal_class_t group_class = {"ompi_group_t", &opal_object_t_class, NULL, NULL, 0, 0, NULL, NULL,
+                                   sizeof(ompi_group_t)};
+
+ompi_communicator_t *mini_comm_create(int rank, int size, unsigned cid)
+{
+    mini_init();
+    ompi_communicator_t *c = (ompi_communicator_t *)mi355x_obj_new(&comm_class);
+    memset((char *)c + sizeof(opal_object_t), 0, sizeof(*c) - sizeof(opal_object_t));
+    ompi_group_t *g = (ompi_group_t *)mi355x_obj_new(&group_class);
+    memset((char *)g + sizeof(opal_object_t), 0, sizeof(*g) - sizeof(opal_object_t));
+    g->grp_proc_count = size;
+    g->grp_my_rank = rank;
+    c->c_local_group = g;
+    c->c_remote_group = g;
+    c->c_my_rank = rank;
+    c->c_contextid = cid;
+    snprintf(c->c_name, sizeof(c->c_name), "mini_comm_%u", cid);
+    return c;
+}
+
+/* install a lower-priority module's functions (what coll/basic + tuned would have done) */
+void mini_comm_install(ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+#define INST(FN)                                                                 \
+    if (m->coll_##FN) {                                                          \
+        if (c->c_coll.coll_##FN##_module) mi355x_obj_release(&c->c_coll.coll_##FN##_module->super); \
+        c->c_coll.coll_##FN = m->coll_##FN;                                      \
+        c->c_coll.coll_##FN##_module = m;                                        \
+        mi355x_obj_retain(&m->super);                                            \
+    }
+    INST(allgather)
+    INST(allreduce)
+    INST(bcast)
+    INST(reduce)
+    INST(reduce_scatter)
+    INST(reduce_scatter_block)
+#undef INST
+}
+
+/* mca_coll_base_comm_select for one extra component (coll_base_comm_select.c:114-262): query,
+ * enable, copy non-NULL functions.  Returns the priority, or < 0 when the component declined. */
+int mini_coll_select(ompi_communicator_t *c, mca_coll_base_component_t *comp)
+{
+    int prio = 0;
+    mca_coll_base_module_t *m = comp->collm_comm_query(c, &prio);
+    if (!m) return -1;
+    if (m->coll_module_enable && OMPI_SUCCESS != m->coll_module_enable(m, c)) {
+        mi355x_obj_release(&m->super);
+        return -2;
+    }
+    mini_comm_install(c, m);
+    mi355x_obj_release(&m->super);
+    return prio;
+}
+
+mca_coll_base_module_t *mini_coll_module_new(void)
+{
+    mini_init();
+    return (mca_coll_base_module_t *)mi355x_obj_new(&mca_coll_base_module_t_class);
+}
+
+void mini_comm_destroy(ompi_communicator_t *c)
+{
+#define REL(FN) if (c->c_coll.coll_##FN##_module) mi355x_obj_release(&c->c_coll.coll_##FN##_module->super);
+    REL(allgather)
+    REL(allreduce)
+    REL(bcast)
+    REL(reduce)
+    REL(reduce_scatter)
+    REL(reduce_scatter_block)
+#undef REL
+    mi355x_obj_release(&c->c_local_group->super);
+    free(c);
+}
+
+/* C-callable MPI-style entry points through the communicator's installed functions */
+int mini_allreduce(ompi_communicator_t *c, void *s, void *r, int n, ompi_datatype_t *d, ompi_op_t *op)
+{
+    return c->c_coll.coll_allreduce(s, r, n, d, op, c, c->c_coll.coll_allreduce_module);
+}
+int mini_reduce_scatter_block(ompi_communicator_t *c, void *s, void *r, int n, ompi_datatype_t *d, ompi_op_t *op)
+{
+    return c->c_coll.coll_reduce_scatter_block(s, r, n, d, op, c, c->c_coll.coll_reduce_scatter_block_module);
+}
+int mini_reduce_scatter(ompi_communicator_t *c, void *s, void *r, int *rc, ompi_datatype_t *d, ompi_op_t *op)
+{
+    return c->c_coll.coll_reduce_scatter(s, r, rc, d, op, c, c->c_coll.coll_reduce_scatter_module);
+}
+int mini_allgather(ompi_communicator_t *c, void *s, int sc, ompi_datatype_t *sd, void *r, int rc, ompi_datatype_t *rd)
+{
+    return c->c_coll.coll_allgather(s, sc, sd, r, rc, rd, c, c->c_coll.coll_allgather_module);
+}
+int mini_bcast(ompi_communicator_t *c, void *b, int n, ompi_datatype_t *d, int root)
+{
+    return c->c_coll.coll_bcast(b, n, d, root, c, c->c_coll.coll_bcast_module);
+}
+void *mini_comm_fn(ompi_communicator_t *c, int which)
+{
+    switch (which) {
+    case 0: return (void *)c->c_coll.coll_allreduce;
+    case 1: return (void *)c->c_coll.coll_reduce_scatter_block;
+    case 2: return (void *)c->c_coll.coll_reduce_scatter;
+    case 3: return (void *)c->c_coll.coll_allgather;
+    case 4: return (void *)c->c_coll.coll_bcast;
+    default: return NULL;
+    }
+}
+
+/* a stub "lower-priority" module for tests: records which function ran and returns `marker` */
+static int stub_calls[8];
+static int stub_marker = 77;
+static int st_allreduce(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                        struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{ (void)s; (void)r; (void)n; (void)d; (void)o; (void)c; (void)m; stub_calls[0]++; return stub_marker; }
+static int st_rsb(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                  struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{ (void)s; (void)r; (void)n; (void)d; (void)o; (void)c; (void)m; stub_calls[1]++; return stub_marker; }
+static int st_rs(void *s, void *r, int *n, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                 struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{ (void)s; (void)r; (void)n; (void)d; (void)o; (void)c; (void)m; stub_calls[2]++; return stub_marker; }
+static int st_allgather(void *s, int sc, struct ompi_datatype_t *sd, void *r, int rc, struct ompi_datatype_t *rd,
+                        struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{ (void)s; (void)sc; (void)sd; (void)r; (void)rc; (void)rd; (void)c; (void)m; stub_calls[3]++; return stub_marker; }
+static int st_bcast(void *b, int n, struct ompi_datatype_t *d, int root, struct ompi_communicator_t *c,
+                    mca_coll_base_module_t *m)
+{ (void)b; (void)n; (void)d; (void)root; (void)c; (void)m; stub_calls[4]++; return stub_marker; }
+
+mca_coll_base_module_t *mini_stub_module(void)
+{
+    mca_coll_base_module_t *m = mini_coll_module_new();
+    m->coll_allreduce = st_allreduce;
+    m->coll_reduce_scatter_block = st_rsb;
+    m->coll_reduce_scatter = st_rs;
+    m->coll_allgather = st_allgather;
+    m->coll_bcast = st_bcast;
+    return m;
+}
+int mini_stub_calls(int which) { return (which >= 0 && which < 8) ? stub_calls[which] : -1; }
+int mini_stub_marker(void) { return stub_marker; }
+
+/* layout facts for tests/test_boundary.py */
+size_t mini_offsetof(int which)
+{
+    switch (which) {
+    case 0: return offsetof(ompi_op_t, o_f_to_c_index);
+    case 1: return offsetof(ompi_op_t, o_func);
+    case 2: return offsetof(ompi_op_t, o_3buff_intrinsic);
+    case 3: return offsetof(ompi_op_base_module_t, opm_fns);
+    case 4: return offsetof(ompi_op_base_module_t, opm_3buff_fns);
+    case 5: return offsetof(ompi_datatype_t, id);
+    case 6: return offsetof(opal_datatype_t, size);
+    case 7: return offsetof(ompi_communicator_t, c_my_rank);
+    case 8: return offsetof(ompi_communicator_t, c_local_group);
+    case 9: return offsetof(ompi_communicator_t, c_coll);
+    case 10: return offsetof(mca_coll_base_module_t, coll_allreduce);
+    case 11: return offsetof(mca_coll_base_module_t, ft_event);
+    case 12: return sizeof(mca_base_component_t);
+    case 13: return sizeof(opal_datatype_t);
+    case 14: return sizeof(ompi_datatype_t);
+    case 15: return offsetof(ompi_communicator_t, c_contextid);
+    case 16: return sizeof(mca_coll_base_comm_coll_t);
+    default: return (size_t)-1;
+    }
+}

@@ -1,0 +1,44 @@
+/* ompi_mini.h -- API of the mini-Open-MPI host harness (see ompi_mini.c). */
+#ifndef MI355X_OMPI_MINI_H
+#define MI355X_OMPI_MINI_H
+
+#include "../../../include/mi355x_types.h"
+#include "../../../include/ompi_abi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+void mini_init(void);
+ompi_datatype_t *mini_datatype(int id);
+int mini_datatype_id_for_slot(int slot);
+void mini_set_base_function(int op, int slot, void *fn2, void *fn3);
+ompi_op_t *mini_op_create(int code);
+int mini_op_select(ompi_op_t *op, ompi_op_base_component_t **comps, int ncomp);
+void mini_op_reduce(ompi_op_t *op, void *source, void *target, int count, ompi_datatype_t *dtype);
+void mini_op_reduce_3buff(ompi_op_t *op, void *s1, void *s2, void *target, int count, ompi_datatype_t *dtype);
+void *mini_op_fn2(ompi_op_t *op, int slot);
+void *mini_op_module2(ompi_op_t *op, int slot);
+void *mini_op_module3(ompi_op_t *op, int slot);
+int mini_obj_refcount(void *obj);
+void mini_op_destroy(ompi_op_t *op);
+ompi_communicator_t *mini_comm_create(int rank, int size, unsigned cid);
+void mini_comm_install(ompi_communicator_t *c, mca_coll_base_module_t *m);
+int mini_coll_select(ompi_communicator_t *c, mca_coll_base_component_t *comp);
+mca_coll_base_module_t *mini_coll_module_new(void);
+void mini_comm_destroy(ompi_communicator_t *c);
+int mini_allreduce(ompi_communicator_t *c, void *s, void *r, int n, ompi_datatype_t *d, ompi_op_t *op);
+int mini_reduce_scatter_block(ompi_communicator_t *c, void *s, void *r, int n, ompi_datatype_t *d, ompi_op_t *op);
+int mini_reduce_scatter(ompi_communicator_t *c, void *s, void *r, int *rc, ompi_datatype_t *d, ompi_op_t *op);
+int mini_allgather(ompi_communicator_t *c, void *s, int sc, ompi_datatype_t *sd, void *r, int rc, ompi_datatype_t *rd);
+int mini_bcast(ompi_communicator_t *c, void *b, int n, ompi_datatype_t *d, int root);
+void *mini_comm_fn(ompi_communicator_t *c, int which);
+mca_coll_base_module_t *mini_stub_module(void);
+int mini_stub_calls(int which);
+int mini_stub_marker(void);
+size_t mini_offsetof(int which);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,255 @@
+/*
+ * coll_mi355x_component.c -- coll/mi355x: device-buffer collectives over the MI355X engine.
+ *
+ * Component ABI: ompi/mca/coll/coll.h:357-451 (example: coll_cuda_component.c:37-72).  Selection:
+ * mca_coll_base_comm_select (coll_base_comm_select.c:114-262) calls collm_comm_query per
+ * communicator, then coll_module_enable in ascending priority, then copies every non-NULL
+ * function pointer.  See include/coll_mi355x.h for what is intercepted.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../../../../include/coll_mi355x.h"
+#include "../../../../../include/mi355x_rt.h"
+
+int mca_coll_mi355x_priority = 90;
+int mca_coll_mi355x_allreduce_algorithm = 0;
+
+typedef struct mca_coll_mi355x_module_t {
+    mca_coll_base_module_t super;
+    mi355x_comm_t *engine;
+    /* lower-priority functions snapshotted at enable time (coll_cuda_module.c:126-147) */
+    mca_coll_base_module_allreduce_fn_t prev_allreduce;
+    mca_coll_base_module_t *prev_allreduce_module;
+    mca_coll_base_module_reduce_scatter_fn_t prev_reduce_scatter;
+    mca_coll_base_module_t *prev_reduce_scatter_module;
+    mca_coll_base_module_reduce_scatter_block_fn_t prev_reduce_scatter_block;
+    mca_coll_base_module_t *prev_reduce_scatter_block_module;
+    mca_coll_base_module_allgather_fn_t prev_allgather;
+    mca_coll_base_module_t *prev_allgather_module;
+    mca_coll_base_module_bcast_fn_t prev_bcast;
+    mca_coll_base_module_t *prev_bcast_module;
+} mca_coll_mi355x_module_t;
+
+static void module_construct(opal_object_t *o)
+{
+    mca_coll_mi355x_module_t *m = (mca_coll_mi355x_module_t *)o;
+    memset((char *)m + sizeof(mca_coll_base_module_t), 0, sizeof(*m) - sizeof(mca_coll_base_module_t));
+}
+
+static void release_prev(mca_coll_base_module_t *p)
+{
+    if (p) mi355x_obj_release(&p->super);
+}
+
+static void module_destruct(opal_object_t *o)
+{
+    mca_coll_mi355x_module_t *m = (mca_coll_mi355x_module_t *)o;
+    release_prev(m->prev_allreduce_module);
+    release_prev(m->prev_reduce_scatter_module);
+    release_prev(m->prev_reduce_scatter_block_module);
+    release_prev(m->prev_allgather_module);
+    release_prev(m->prev_bcast_module);
+    if (m->engine) mi355x_comm_destroy(m->engine);
+}
+
+static opal_class_t mca_coll_mi355x_module_t_class = {
+    "mca_coll_mi355x_module_t", &mca_coll_base_module_t_class, module_construct, module_destruct,
+    0, 0, NULL, NULL, sizeof(mca_coll_mi355x_module_t)
+};
+
+/* ------------------------------------------------------------------ helpers */
+static int env_int(const char *name, int dflt)
+{
+    const char *v = getenv(name);
+    return v ? atoi(v) : dflt;
+}
+
+static int is_dev(const void *p)
+{
+    int d = 0;
+    if (!p || p == MPI_IN_PLACE) return 0;
+    if (mi355x_ptr_is_device(p, &d) != MI355X_SUCCESS) return 0;
+    return d;
+}
+
+/* the element type slot when the datatype is a predefined, gap-free reducible type; else -1 */
+static int reducible_type(const struct ompi_datatype_t *dt)
+{
+    if (!(dt->super.flags & OPAL_DATATYPE_FLAG_PREDEFINED)) return -1;
+    if (!(dt->super.flags & OPAL_DATATYPE_FLAG_NO_GAPS)) return -1;
+    if (dt->id < 0 || dt->id >= OMPI_DATATYPE_MPI_MAX_PREDEFINED) return -1;
+    return ompi_op_ddt_map[dt->id];
+}
+
+static int contiguous_bytes(const struct ompi_datatype_t *dt, int count, size_t *bytes)
+{
+    if (count < 0) return 0;
+    if (!(dt->super.flags & OPAL_DATATYPE_FLAG_NO_GAPS) || dt->super.true_lb != 0) return 0;
+    *bytes = (size_t)count * dt->super.size;
+    return 1;
+}
+
+static int map_rc(int rc)
+{
+    switch (rc) {
+    case MI355X_SUCCESS: return OMPI_SUCCESS;
+    case MI355X_ERR_ARG: return OMPI_ERR_BAD_PARAM;
+    case MI355X_ERR_NOMEM: return OMPI_ERR_OUT_OF_RESOURCE;
+    case MI355X_ERR_UNSUPPORTED: return OMPI_ERR_NOT_SUPPORTED;
+    default:
+        fprintf(stderr, "[coll/mi355x] %s\n", mi355x_last_error());
+        return OMPI_ERROR;
+    }
+}
+
+#define MOD(m) ((mca_coll_mi355x_module_t *)(m))
+
+/* ------------------------------------------------------------------ collectives */
+int mca_coll_mi355x_allreduce(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                              struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                              mca_coll_base_module_t *module)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    const int inplace = (sbuf == MPI_IN_PLACE);
+    const int t = reducible_type(dtype);
+    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 ||
+        !mi355x_op_supported(op->o_f_to_c_index, t))
+        return m->prev_allreduce(sbuf, rbuf, count, dtype, op, comm, m->prev_allreduce_module);
+    return map_rc(mi355x_allreduce(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)count, t, op->o_f_to_c_index, NULL));
+}
+
+int mca_coll_mi355x_reduce_scatter_block(void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dtype,
+                                         struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                                         mca_coll_base_module_t *module)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    const int inplace = (sbuf == MPI_IN_PLACE);
+    const int t = reducible_type(dtype);
+    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 ||
+        !mi355x_op_supported(op->o_f_to_c_index, t))
+        return m->prev_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, m->prev_reduce_scatter_block_module);
+    return map_rc(mi355x_reduce_scatter_block(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)rcount, t,
+                                              op->o_f_to_c_index, NULL));
+}
+
+int mca_coll_mi355x_reduce_scatter(void *sbuf, void *rbuf, int *rcounts, struct ompi_datatype_t *dtype,
+                                   struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                                   mca_coll_base_module_t *module)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    const int inplace = (sbuf == MPI_IN_PLACE);
+    const int t = reducible_type(dtype);
+    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 ||
+        !mi355x_op_supported(op->o_f_to_c_index, t))
+        return m->prev_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, m->prev_reduce_scatter_module);
+    return map_rc(mi355x_reduce_scatter(m->engine, inplace ? NULL : sbuf, rbuf, rcounts, t, op->o_f_to_c_index, NULL));
+}
+
+int mca_coll_mi355x_allgather(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
+                              struct ompi_datatype_t *rdtype, struct ompi_communicator_t *comm,
+                              mca_coll_base_module_t *module)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    const int inplace = (sbuf == MPI_IN_PLACE);
+    size_t rb = 0, sb = 0;
+    const int ok = is_dev(rbuf) && (inplace || is_dev(sbuf)) && contiguous_bytes(rdtype, rcount, &rb) &&
+                   (inplace || (contiguous_bytes(sdtype, scount, &sb) && sb == rb));
+    if (!ok)
+        return m->prev_allgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_allgather_module);
+    return map_rc(mi355x_allgather(m->engine, inplace ? NULL : sbuf, rbuf, rb, NULL));
+}
+
+int mca_coll_mi355x_bcast(void *buff, int count, struct ompi_datatype_t *datatype, int root,
+                          struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    size_t bytes = 0;
+    if (!is_dev(buff) || !contiguous_bytes(datatype, count, &bytes))
+        return m->prev_bcast(buff, count, datatype, root, comm, m->prev_bcast_module);
+    return map_rc(mi355x_bcast(m->engine, buff, bytes, root, NULL));
+}
+
+/* ------------------------------------------------------------------ module / component */
+#define SNAP(FN)                                                                \
+    do {                                                                        \
+        m->prev_##FN = comm->c_coll.coll_##FN;                                  \
+        m->prev_##FN##_module = comm->c_coll.coll_##FN##_module;                \
+        if (!m->prev_##FN || !m->prev_##FN##_module) return OMPI_ERROR;         \
+        mi355x_obj_retain(&m->prev_##FN##_module->super);                       \
+    } while (0)
+
+/* coll_module_enable (coll.h:176-178): runs after every lower-priority module is installed */
+static int module_enable(mca_coll_base_module_t *module, struct ompi_communicator_t *comm)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    SNAP(allreduce);
+    SNAP(reduce_scatter);
+    SNAP(reduce_scatter_block);
+    SNAP(allgather);
+    SNAP(bcast);
+    /* node-unique rendezvous key: job id + communicator context id */
+    const char *job = getenv("OMPI_MCA_ess_base_jobid");
+    char key[128];
+    snprintf(key, sizeof(key), "ompi_%s_cid%u", job ? job : "0", (unsigned)comm->c_contextid);
+    int ndev = 1;
+    if (mi355x_device_count(&ndev) != MI355X_SUCCESS || ndev < 1) return OMPI_ERROR;
+    const int dev = env_int("OMPI_COMM_WORLD_LOCAL_RANK", mi355x_comm_rank_of(comm)) % ndev;
+    int rc = mi355x_comm_create(key, mi355x_comm_rank_of(comm), mi355x_comm_size_of(comm), dev, &m->engine);
+    if (rc != MI355X_SUCCESS) return map_rc(rc);
+    if (mca_coll_mi355x_allreduce_algorithm)
+        mi355x_comm_set(m->engine, MI355X_KNOB_ALLREDUCE_ALG, mca_coll_mi355x_allreduce_algorithm);
+    return OMPI_SUCCESS;
+}
+
+static int component_register(void)
+{
+    mca_coll_mi355x_priority = env_int("OMPI_MCA_coll_mi355x_priority", mca_coll_mi355x_priority);
+    mca_coll_mi355x_allreduce_algorithm =
+        env_int("OMPI_MCA_coll_mi355x_allreduce_algorithm", mca_coll_mi355x_allreduce_algorithm);
+    return OMPI_SUCCESS;
+}
+static int component_open(void) { return OMPI_SUCCESS; }
+static int component_close(void) { return OMPI_SUCCESS; }
+
+static int component_init_query(bool enable_progress_threads, bool enable_mpi_threads)
+{
+    (void)enable_progress_threads;
+    (void)enable_mpi_threads;
+    int n = 0;
+    if (mi355x_device_count(&n) != MI355X_SUCCESS || n < 1) return OMPI_ERR_NOT_SUPPORTED;
+    return OMPI_SUCCESS;
+}
+
+/* collm_comm_query (coll.h:137-139); declines like coll/tuned for inter/size-1 communicators
+ * (coll_tuned_module.c:63-75) and when the job spans several nodes */
+static mca_coll_base_module_t *component_comm_query(struct ompi_communicator_t *comm, int *priority)
+{
+    if ((comm->c_flags & OMPI_COMM_INTER) || mi355x_comm_size_of(comm) < 2) return NULL;
+    if (mca_coll_mi355x_priority <= 0) return NULL;
+    const int wsize = env_int("OMPI_COMM_WORLD_SIZE", -1), lsize = env_int("OMPI_COMM_WORLD_LOCAL_SIZE", -2);
+    if (wsize != lsize) return NULL;
+    mca_coll_mi355x_module_t *m = (mca_coll_mi355x_module_t *)mi355x_obj_new(&mca_coll_mi355x_module_t_class);
+    if (!m) return NULL;
+    m->super.coll_module_enable = module_enable;
+    m->super.coll_allreduce = mca_coll_mi355x_allreduce;
+    m->super.coll_reduce_scatter = mca_coll_mi355x_reduce_scatter;
+    m->super.coll_reduce_scatter_block = mca_coll_mi355x_reduce_scatter_block;
+    m->super.coll_allgather = mca_coll_mi355x_allgather;
+    m->super.coll_bcast = mca_coll_mi355x_bcast;
+    m->super.ft_event = NULL;
+    *priority = mca_coll_mi355x_priority > 100 ? 100 : mca_coll_mi355x_priority;
+    return &m->super;
+}
+
+mca_coll_base_component_t mca_coll_mi355x_component = {
+    .collm_version = {
+        MCA_COLL_BASE_VERSION_2_0_0,
+        "mi355x", 1, 0, 0,
+        component_open, component_close, NULL, component_register, {0}
+    },
+    .collm_data = {0, {0}},
+    .collm_init_query = component_init_query,
+    .collm_comm_query = component_comm_query,
+};

@@ -1,0 +1,89 @@
+"""ctypes view of the mini-Open-MPI harness (libompi_mini.so) and the two MCA component DSOs.
+
+Load order mirrors Open MPI: libmi355x_rt and libompi_mini are global (they play libmpi /
+libopen-pal), then the component DSOs are dlopen'ed and their component symbols looked up by the
+MCA naming rule (opal/mca/base/mca_base_component_find.c:619-631).
+"""
+from __future__ import annotations
+
+import ctypes
+
+from conftest import load_pkg
+
+_h = None
+
+
+class Mini:
+    def __init__(self):
+        pkg = load_pkg()
+        pkg.rt()  # RTLD_GLOBAL
+        lib_dir = pkg.LIB_DIR
+        self.pkg = pkg
+        self.lib = ctypes.CDLL(str(lib_dir / "libompi_mini.so"), mode=ctypes.RTLD_GLOBAL)
+        self.op_hip = ctypes.CDLL(str(lib_dir / "mca_op_hip.so"))
+        self.coll = ctypes.CDLL(str(lib_dir / "mca_coll_mi355x.so"))
+        L = self.lib
+        vp, i = ctypes.c_void_p, ctypes.c_int
+        L.mini_datatype.restype = vp
+        L.mini_datatype.argtypes = [i]
+        L.mini_datatype_id_for_slot.argtypes = [i]
+        L.mini_set_base_function.argtypes = [i, i, vp, vp]
+        L.mini_op_create.restype = vp
+        L.mini_op_create.argtypes = [i]
+        L.mini_op_select.argtypes = [vp, ctypes.POINTER(vp), i]
+        L.mini_op_reduce.argtypes = [vp, vp, vp, i, vp]
+        L.mini_op_reduce_3buff.argtypes = [vp, vp, vp, vp, i, vp]
+        for f in ("mini_op_fn2", "mini_op_module2", "mini_op_module3"):
+            getattr(L, f).restype = vp
+            getattr(L, f).argtypes = [vp, i]
+        L.mini_obj_refcount.argtypes = [vp]
+        L.mini_op_destroy.argtypes = [vp]
+        L.mini_comm_create.restype = vp
+        L.mini_comm_create.argtypes = [i, i, ctypes.c_uint]
+        L.mini_comm_install.argtypes = [vp, vp]
+        L.mini_coll_select.argtypes = [vp, vp]
+        L.mini_coll_module_new.restype = vp
+        L.mini_comm_destroy.argtypes = [vp]
+        L.mini_allreduce.argtypes = [vp, vp, vp, i, vp, vp]
+        L.mini_reduce_scatter_block.argtypes = [vp, vp, vp, i, vp, vp]
+        L.mini_reduce_scatter.argtypes = [vp, vp, vp, ctypes.POINTER(i), vp, vp]
+        L.mini_allgather.argtypes = [vp, vp, i, vp, vp, i, vp]
+        L.mini_bcast.argtypes = [vp, vp, i, vp, i]
+        L.mini_comm_fn.restype = vp
+        L.mini_comm_fn.argtypes = [vp, i]
+        L.mini_stub_module.restype = vp
+        L.mini_stub_calls.argtypes = [i]
+        L.mini_offsetof.restype = ctypes.c_size_t
+        L.mini_offsetof.argtypes = [i]
+        L.mini_init()
+
+    def addr(self, lib, sym):
+        return ctypes.cast(getattr(lib, sym), ctypes.c_void_p).value
+
+    def component_ptr(self, lib, sym):
+        return ctypes.addressof(ctypes.c_char.in_dll(lib, sym))
+
+    def dtype_for_slot(self, slot):
+        did = self.lib.mini_datatype_id_for_slot(slot)
+        return None if did < 0 else self.lib.mini_datatype(did)
+
+    def install_oracle_base(self, oracle):
+        """op/base's CPU loops in the harness = the oracle's reference-signature thunks"""
+        for op in range(15):
+            for ty in range(39):
+                if oracle.oracle_has_op(op, ty):
+                    self.lib.mini_set_base_function(op, ty, oracle.oracle_ompi_fn2(op, ty), oracle.oracle_ompi_fn3(op, ty))
+
+    def select_op(self, code, with_hip=True):
+        op = self.lib.mini_op_create(code)
+        comps = (ctypes.c_void_p * 1)(self.component_ptr(self.op_hip, "mca_op_hip_component"))
+        rc = self.lib.mini_op_select(op, comps, 1 if with_hip else 0)
+        assert rc == 0, rc
+        return op
+
+
+def mini() -> Mini:
+    global _h
+    if _h is None:
+        _h = Mini()
+    return _h

@@ -1,0 +1,176 @@
+"""The drop-in boundary, checked on CPU (no GPU needed):
+
+* libmi355x_rt.so exports every entry point include/mi355x_rt.h declares;
+* mca_op_hip.so / mca_coll_mi355x.so export the MCA component symbols (mca_<type>_<name>_component,
+  opal/mca/base/mca_base_component_find.c:619-631) and the reference-signature entry points;
+* the component structs carry the framework names/versions the MCA loader checks;
+* the ABI mirror (include/ompi_abi.h) has the offsets derived from the reference definitions;
+* op/hip goes through the restated ompi_op_base_op_select: every GPU slot is installed, the NULL
+  pattern of the base table is kept, host buffers are routed to the base (reference) loops, and
+  the module reference counts balance despite op_base_op_select.c:162-168;
+* coll/mi355x's comm_query installs exactly the five collectives and declines where coll/tuned
+  does (inter-communicators, size 1) and for multi-node jobs.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import opdata
+from conftest import REPO
+from mini import mini
+
+
+def _declared(header):
+    txt = (REPO / "include" / header).read_text()
+    return sorted(set(re.findall(r"^\s*(?:int|void|size_t|const char \*)\s*\*?(mi355x_\w+)\s*\(", txt, re.M)))
+
+
+def _exports(so):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", str(so)], text=True)
+    return {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+
+
+def test_rt_exports_every_declared_symbol(pkg):
+    names = _declared("mi355x_rt.h")
+    assert len(names) >= 40, names
+    ex = _exports(pkg.lib_path())
+    missing = [n for n in names if n not in ex]
+    assert not missing, missing
+
+
+def test_component_symbols(pkg):
+    op = _exports(pkg.lib_path("mca_op_hip.so"))
+    for s in ("mca_op_hip_component", "mca_op_hip_2buff", "mca_op_hip_3buff"):
+        assert s in op
+    coll = _exports(pkg.lib_path("mca_coll_mi355x.so"))
+    for s in ("mca_coll_mi355x_component", "mca_coll_mi355x_allreduce", "mca_coll_mi355x_reduce_scatter_block",
+              "mca_coll_mi355x_reduce_scatter", "mca_coll_mi355x_allgather", "mca_coll_mi355x_bcast"):
+        assert s in coll
+
+
+class _Comp(ctypes.Structure):
+    _fields_ = [("maj", ctypes.c_int), ("min", ctypes.c_int), ("rel", ctypes.c_int),
+                ("type_name", ctypes.c_char * 32), ("tmaj", ctypes.c_int), ("tmin", ctypes.c_int),
+                ("trel", ctypes.c_int), ("name", ctypes.c_char * 64)]
+
+
+def test_component_headers():
+    m = mini()
+    op = _Comp.from_address(m.component_ptr(m.op_hip, "mca_op_hip_component"))
+    assert (op.maj, op.min, op.rel) == (2, 0, 0)
+    assert op.type_name == b"op" and (op.tmaj, op.tmin, op.trel) == (1, 0, 0) and op.name == b"hip"
+    co = _Comp.from_address(m.component_ptr(m.coll, "mca_coll_mi355x_component"))
+    assert co.type_name == b"coll" and (co.tmaj, co.tmin, co.trel) == (2, 0, 0) and co.name == b"mi355x"
+
+
+def test_abi_offsets():
+    """offsets derived by hand from the reference struct definitions (x86-64, non-debug)"""
+    L = mini().lib
+    want = {
+        0: 16 + 64 + 4 + 4,          # ompi_op_t.o_f_to_c_index (op.h:138-188)
+        1: 96,                       # ompi_op_t.o_func
+        2: 96 + 39 * 8 * 2,          # ompi_op_t.o_3buff_intrinsic (union = intrinsic fns+modules)
+        3: 32,                       # ompi_op_base_module_t.opm_fns (op.h:357-373)
+        4: 32 + 39 * 8,              # ompi_op_base_module_t.opm_3buff_fns
+        5: 368,                      # ompi_datatype_t.id = sizeof(opal_datatype_t)
+        6: 24,                       # opal_datatype_t.size
+        12: 3 * 4 + 32 + 3 * 4 + 64 + 3 * 4 + 4 + 4 * 8 + 32,  # mca_base_component_2_0_0_t
+        13: 368,
+        14: 368 + 4 + 4 + 8 + 8 + 8 + 64,
+        10: 16 + 8 + 2 * 8,          # coll module: allreduce is the 3rd fn after enable
+        11: 16 + 8 + 44 * 8,         # ft_event after 17 + 17 + 10 fns
+        16: 44 * 16,                 # mca_coll_base_comm_coll_t: 44 (fn, module) pairs
+    }
+    for k, v in want.items():
+        assert L.mini_offsetof(k) == v, (k, L.mini_offsetof(k), v)
+    # communicator: c_contextid right after the 64-B name that follows the 64-B opal_mutex_t
+    assert L.mini_offsetof(15) == 16 + 64 + 64
+    assert L.mini_offsetof(7) == L.mini_offsetof(15) + 4
+
+
+@pytest.mark.parametrize("opname", ["MAX", "MIN", "SUM", "PROD", "LAND", "BAND", "LOR", "BOR", "LXOR", "BXOR",
+                                    "MAXLOC", "MINLOC"])
+def test_op_select_installs_and_routes_host(pkg, oracle, opname):
+    m = mini()
+    m.install_oracle_base(oracle)
+    code = pkg.OP[opname]
+    op = m.select_op(code)
+    f2 = m.addr(m.op_hip, "mca_op_hip_2buff")
+    hip_mod = None
+    installed = 0
+    for slot in range(39):
+        base = oracle.oracle_has_op(code, slot)
+        fn = m.lib.mini_op_fn2(op, slot)
+        assert bool(fn) == bool(base), slot          # NULL pattern kept (op_base_op_select.c:185-201)
+        if base and pkg.op_supported(code, slot):
+            assert fn == f2, (opname, slot)
+            installed += 1
+            hip_mod = m.lib.mini_op_module2(op, slot)
+            assert m.lib.mini_op_module3(op, slot) == hip_mod
+    assert installed == sum(pkg.op_supported(code, t) for t in range(39))
+    # references held by the op's tables == the module's count, despite :162-168
+    nslots = sum(1 for t in range(39) if m.lib.mini_op_module2(op, t) == hip_mod) + \
+        sum(1 for t in range(39) if m.lib.mini_op_module3(op, t) == hip_mod)
+    assert m.lib.mini_obj_refcount(hip_mod) == nslots
+    # host buffers are reduced by the base (reference) loop: MPI_Reduce_local semantics
+    for slot in range(39):
+        if not oracle.oracle_has_op(code, slot):
+            continue
+        dt = m.dtype_for_slot(slot)
+        if dt is None:
+            continue
+        tname = pkg.TYPES[slot]
+        a = opdata.make(tname, 97, 1)
+        b = opdata.make(tname, 97, 2)
+        want = b.copy()
+        oracle.oracle_op_2buff(code, slot, a.ctypes.data, want.ctypes.data, 97)
+        got = b.copy()
+        m.lib.mini_op_reduce(op, a.ctypes.data, got.ctypes.data, 97, dt)
+        opdata.assert_same(tname, opname, got, want, "host route")
+    m.lib.mini_op_destroy(op)   # must not double free
+
+
+def _coll_env(monkeypatch, world=4, local=4):
+    monkeypatch.setenv("OMPI_COMM_WORLD_SIZE", str(world))
+    monkeypatch.setenv("OMPI_COMM_WORLD_LOCAL_SIZE", str(local))
+
+
+class _CollComp(ctypes.Structure):
+    _fields_ = [("version", ctypes.c_char * (200)), ("data", ctypes.c_char * 36),
+                ("init_query", ctypes.c_void_p), ("comm_query", ctypes.c_void_p)]
+
+
+def _comm_query(m, comm):
+    comp = _CollComp.from_address(m.component_ptr(m.coll, "mca_coll_mi355x_component"))
+    fn = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int))(comp.comm_query)
+    prio = ctypes.c_int(-1)
+    mod = fn(comm, ctypes.byref(prio))
+    return mod, prio.value
+
+
+def test_coll_comm_query(monkeypatch):
+    m = mini()
+    assert ctypes.sizeof(_CollComp) >= 200
+    _coll_env(monkeypatch)
+    comm = m.lib.mini_comm_create(0, 4, 7)
+    mod, prio = _comm_query(m, comm)
+    assert mod and prio == 90
+    # the module provides exactly allreduce, reduce_scatter(_block), allgather, bcast
+    m.lib.mini_comm_install(comm, mod)
+    names = ["mca_coll_mi355x_allreduce", "mca_coll_mi355x_reduce_scatter_block", "mca_coll_mi355x_reduce_scatter",
+             "mca_coll_mi355x_allgather", "mca_coll_mi355x_bcast"]
+    for which, n in enumerate(names):
+        assert m.lib.mini_comm_fn(comm, which) == m.addr(m.coll, n)
+    m.lib.mini_comm_destroy(comm)
+    # declines: size 1, multi-node job
+    one = m.lib.mini_comm_create(0, 1, 8)
+    assert _comm_query(m, one)[0] is None
+    _coll_env(monkeypatch, world=16, local=8)
+    c2 = m.lib.mini_comm_create(0, 4, 9)
+    assert _comm_query(m, c2)[0] is None

@@ -1,0 +1,96 @@
+"""op/hip and coll/mi355x driven exactly as Open MPI drives them (restated selection + dispatch
+in the mini-OMPI harness), on device buffers, vs the oracle.
+
+* op/hip: every slot through ompi_op_reduce / ompi_3buff_op_reduce dispatch with device
+  operands; mixed host/device operands; x87 long double slots staged to the base loop.
+* coll/mi355x: two processes each select the component over a stub lower-priority module, then
+  MPI_Allreduce / MPI_Reduce_scatter_block / MPI_Allgather / MPI_Bcast on device buffers go
+  through the engine (checked vs the oracle), and host buffers go to the stub.
+"""
+from __future__ import annotations
+
+import os
+import pathlib
+import subprocess
+import sys
+import uuid
+
+import numpy as np
+import pytest
+
+import opdata
+from mini import mini
+
+pytestmark = pytest.mark.gpu
+HERE = pathlib.Path(__file__).parent
+
+
+def _dev(torch, a):
+    return torch.from_numpy(a.view(np.uint8).copy()).cuda()
+
+
+def test_op_hip_device_dispatch(gpu, pkg, oracle):
+    torch = gpu
+    m = mini()
+    m.install_oracle_base(oracle)
+    n = 10_007
+    bad = []
+    for code in range(1, 13):
+        op = m.select_op(code)
+        for slot in range(39):
+            if not oracle.oracle_has_op(code, slot):
+                continue
+            dt = m.dtype_for_slot(slot)
+            if dt is None:
+                continue
+            tname, opname = pkg.TYPES[slot], pkg.OPS[code]
+            a = opdata.make(tname, n, 1)
+            b = opdata.make(tname, n, 2)
+            da, db = _dev(torch, a), _dev(torch, b)
+            torch.cuda.synchronize()
+            m.lib.mini_op_reduce(op, da.data_ptr(), db.data_ptr(), n, dt)        # device / device
+            want = b.copy()
+            oracle.oracle_op_2buff(code, slot, a.ctypes.data, want.ctypes.data, n)
+            got = db.cpu().numpy().view(a.dtype)
+            try:
+                opdata.assert_same(tname, opname, got, want, "2buff dev")
+            except AssertionError as e:
+                bad.append(str(e))
+            hb = b.copy()                                                          # device in, host inout
+            m.lib.mini_op_reduce(op, da.data_ptr(), hb.ctypes.data, n, dt)
+            try:
+                opdata.assert_same(tname, opname, hb, want, "2buff mixed")
+            except AssertionError as e:
+                bad.append(str(e))
+            do = torch.empty_like(da)
+            m.lib.mini_op_reduce_3buff(op, da.data_ptr(), _dev(torch, b).data_ptr(), do.data_ptr(), n, dt)
+            want3 = np.zeros_like(a)
+            oracle.oracle_op_3buff(code, slot, a.ctypes.data, b.ctypes.data, want3.ctypes.data, n)
+            try:
+                opdata.assert_same(tname, opname, do.cpu().numpy().view(a.dtype), want3, "3buff dev")
+            except AssertionError as e:
+                bad.append(str(e))
+        m.lib.mini_op_destroy(op)
+    assert not bad, "\n".join(bad[:10])
+
+
+@pytest.mark.parametrize("size", [2, 3])
+def test_coll_component_processes(gpu, size):
+    key = uuid.uuid4().hex[:10]
+    env = dict(os.environ, MI355X_TIMEOUT_S="60", OMPI_COMM_WORLD_SIZE=str(size),
+               OMPI_COMM_WORLD_LOCAL_SIZE=str(size), OMPI_MCA_ess_base_jobid=key)
+    procs = []
+    for r in range(size):
+        e = dict(env, OMPI_COMM_WORLD_LOCAL_RANK=str(r), OMPI_COMM_WORLD_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, str(HERE / "coll_worker.py"), str(r), str(size)], env=e,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=300)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, _ = p.communicate()
+        outs.append(out)
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r}:\n{outs[r][-3000:]}"
