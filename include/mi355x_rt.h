@@ -129,6 +129,35 @@ int mi355x_allgather(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t b
 /* MPI_Bcast of `bytes` contiguous bytes from `root`. */
 int mi355x_bcast(mi355x_comm_t *comm, void *buf, size_t bytes, int root, void *stream);
 
+/* ---------------------------------------------------------------- GPU convertor */
+/* A datatype layout: instance k at base + k*extent; inside it nblk blocks at j*stride; inside a
+ * block the runs (disp, len) in order.  The packed stream is that type map in order, as
+ * opal_generic_simple_pack produces it (opal/datatype/opal_datatype_pack.c:250-374). */
+typedef struct mi355x_ddt mi355x_ddt_t;
+int mi355x_ddt_create(const int64_t *disp, const int64_t *len, size_t nruns, size_t nblk, int64_t stride,
+                      int64_t extent, mi355x_ddt_t **out);
+/* MPI_Type_vector over a gap-free type of elem_size bytes (ompi_datatype_create_vector.c:36-65) */
+int mi355x_ddt_create_vector(size_t count, size_t blocklen, int64_t stride, size_t elem_size, mi355x_ddt_t **out);
+/* MPI_Type_indexed (ompi_datatype_create_indexed.c:32-66, adjacent blocks merged) */
+int mi355x_ddt_create_indexed(size_t count, const int *blocklens, const int *disps, size_t elem_size,
+                              mi355x_ddt_t **out);
+/* compile an optimized opal description (opal_datatype_t::opt_desc, `used` 32-byte ELEM/LOOP/
+ * END_LOOP records, opal_datatype_internal.h:148-188); basic_sizes[id] = size of opal basic type id */
+int mi355x_ddt_from_opal(const void *desc, uint32_t used, int64_t extent, const uint32_t *basic_sizes,
+                         mi355x_ddt_t **out);
+int mi355x_ddt_destroy(mi355x_ddt_t *d);
+size_t mi355x_ddt_size(const mi355x_ddt_t *d);
+int64_t mi355x_ddt_extent(const mi355x_ddt_t *d);
+int mi355x_ddt_nruns(const mi355x_ddt_t *d);
+/* pack packed bytes [pos, pos+bytes) of `count` instances at device `base` into `dst`
+ * (replaces opal_convertor_set_position + opal_convertor_pack on a CUDA convertor,
+ * opal_convertor.c:223-330 / opal_datatype_cuda.c:93-115).  checksum (may be NULL) receives the
+ * window's share of the convertor checksum (opal_uicsum_partial, opal/util/crc.c:921). */
+int mi355x_pack(const mi355x_ddt_t *d, size_t count, const void *base, size_t pos, void *dst, size_t bytes,
+                uint32_t *checksum, void *stream);
+int mi355x_unpack(const mi355x_ddt_t *d, size_t count, void *base, size_t pos, const void *src, size_t bytes,
+                  uint32_t *checksum, void *stream);
+
 /* Host-only introspection of the schedule compiler: the per-element program the engine runs for
  * a given reference algorithm (layout documented in coll_comm.cpp).  For tests; no GPU needed. */
 int mi355x_sched_program(int kind, int n, int alg, int block, int *out, int cap);

@@ -110,6 +110,16 @@ def _declare(lib: ctypes.CDLL) -> None:
         "mi355x_allgather": (i, [vp, vp, vp, sz, vp]),
         "mi355x_bcast": (i, [vp, vp, sz, i, vp]),
         "mi355x_sched_program": (i, [i, i, i, i, c.POINTER(i), i]),
+        "mi355x_ddt_create": (i, [c.POINTER(c.c_int64), c.POINTER(c.c_int64), sz, sz, c.c_int64, c.c_int64, c.POINTER(vp)]),
+        "mi355x_ddt_create_vector": (i, [sz, sz, c.c_int64, sz, c.POINTER(vp)]),
+        "mi355x_ddt_create_indexed": (i, [sz, c.POINTER(i), c.POINTER(i), sz, c.POINTER(vp)]),
+        "mi355x_ddt_from_opal": (i, [vp, c.c_uint32, c.c_int64, c.POINTER(c.c_uint32), c.POINTER(vp)]),
+        "mi355x_ddt_destroy": (i, [vp]),
+        "mi355x_ddt_size": (sz, [vp]),
+        "mi355x_ddt_extent": (c.c_int64, [vp]),
+        "mi355x_ddt_nruns": (i, [vp]),
+        "mi355x_pack": (i, [vp, sz, vp, sz, vp, sz, c.POINTER(c.c_uint32), vp]),
+        "mi355x_unpack": (i, [vp, sz, vp, sz, vp, sz, c.POINTER(c.c_uint32), vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name, None)
@@ -229,6 +239,72 @@ class Comm:
 
     def bcast(self, buf, nbytes, root, stream=None) -> None:
         check(rt().mi355x_bcast(self.h, buf, nbytes, root, stream), "mi355x_bcast")
+
+
+class Ddt:
+    """A GPU-convertor datatype layout (mi355x_ddt_t)."""
+
+    def __init__(self, h):
+        self.h = h
+
+    @classmethod
+    def vector(cls, count, blocklen, stride, elem_size):
+        h = ctypes.c_void_p()
+        check(rt().mi355x_ddt_create_vector(count, blocklen, stride, elem_size, ctypes.byref(h)), "ddt vector")
+        return cls(h)
+
+    @classmethod
+    def indexed(cls, blocklens, disps, elem_size):
+        n = len(blocklens)
+        h = ctypes.c_void_p()
+        check(rt().mi355x_ddt_create_indexed(n, (ctypes.c_int * n)(*blocklens), (ctypes.c_int * n)(*disps),
+                                             elem_size, ctypes.byref(h)), "ddt indexed")
+        return cls(h)
+
+    @classmethod
+    def runs(cls, disps, lens, nblk=1, stride=0, extent=0):
+        n = len(disps)
+        h = ctypes.c_void_p()
+        check(rt().mi355x_ddt_create((ctypes.c_int64 * n)(*disps), (ctypes.c_int64 * n)(*lens), n, nblk, stride,
+                                     extent, ctypes.byref(h)), "ddt create")
+        return cls(h)
+
+    @classmethod
+    def from_opal(cls, desc_bytes: bytes, used: int, extent: int, basic_sizes):
+        h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(desc_bytes, len(desc_bytes))
+        bs = (ctypes.c_uint32 * len(basic_sizes))(*basic_sizes)
+        check(rt().mi355x_ddt_from_opal(buf, used, extent, bs, ctypes.byref(h)), "ddt from opal")
+        return cls(h)
+
+    @property
+    def size(self):
+        return int(rt().mi355x_ddt_size(self.h))
+
+    @property
+    def extent(self):
+        return int(rt().mi355x_ddt_extent(self.h))
+
+    @property
+    def nruns(self):
+        return int(rt().mi355x_ddt_nruns(self.h))
+
+    def pack(self, count, base, pos, dst, nbytes, stream=None, checksum=False):
+        cs = ctypes.c_uint32()
+        check(rt().mi355x_pack(self.h, count, base, pos, dst, nbytes, ctypes.byref(cs) if checksum else None, stream),
+              "mi355x_pack")
+        return cs.value if checksum else None
+
+    def unpack(self, count, base, pos, src, nbytes, stream=None, checksum=False):
+        cs = ctypes.c_uint32()
+        check(rt().mi355x_unpack(self.h, count, base, pos, src, nbytes, ctypes.byref(cs) if checksum else None,
+                                 stream), "mi355x_unpack")
+        return cs.value if checksum else None
+
+    def destroy(self):
+        if self.h:
+            rt().mi355x_ddt_destroy(self.h)
+            self.h = None
 
 
 def sched_program(kind: int, n: int, alg: int, block: int) -> list[int]:

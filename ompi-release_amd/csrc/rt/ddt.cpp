@@ -1,0 +1,266 @@
+// ddt.cpp -- datatype layouts for the GPU convertor (host side).
+//
+// Builders restate the MPI constructors' type maps (ompi_datatype_create_vector.c:36-65,
+// ompi_datatype_create_indexed.c:32-66 incl. the merge of adjacent blocks) and, for drop-in use
+// inside Open MPI, compile an optimized opal description (opt_desc: ELEM / LOOP / END_LOOP
+// records, opal/datatype/opal_datatype_internal.h:148-188) into the same layout.
+#include <cstring>
+#include <vector>
+
+#include "ddt_internal.hpp"
+#include "rt_internal.hpp"
+
+#include <mutex>
+
+struct mi355x_ddt {
+    std::vector<int64_t> disp, len, elem, pfx;
+    int64_t nblk = 1, stride = 0, extent = 0;
+    int64_t *ddisp = nullptr, *dlen = nullptr, *dpfx = nullptr;  // device copies, made on first use
+    int dev = -1;
+    std::mutex mtx;
+};
+
+namespace mi355x {
+
+static void add_run(mi355x_ddt *d, int64_t disp, int64_t len, int64_t elem)
+{
+    if (len <= 0) return;
+    if (!d->disp.empty() && d->disp.back() + d->len.back() == disp && d->elem.back() == elem) {
+        d->len.back() += len;
+        return;
+    }
+    d->disp.push_back(disp);
+    d->len.push_back(len);
+    d->elem.push_back(elem);
+}
+
+static int finalize(mi355x_ddt *d, mi355x_ddt_t **out)
+{
+    if (d->disp.empty()) {  // empty datatype: one zero-length run keeps the tables non-empty
+        d->disp.push_back(0);
+        d->len.push_back(0);
+        d->elem.push_back(1);
+    }
+    const size_t n = d->disp.size();
+    d->pfx.assign(n, 0);
+    for (size_t r = 1; r < n; ++r) d->pfx[r] = d->pfx[r - 1] + d->len[r - 1];
+    *out = d;
+    return MI355X_SUCCESS;
+}
+
+// device copies of the run tables (uploaded once per datatype)
+static int upload(mi355x_ddt *d)
+{
+    std::lock_guard<std::mutex> g(d->mtx);
+    if (d->ddisp) return MI355X_SUCCESS;
+    const size_t n = d->disp.size() * 8;
+    MI_HIP(hipMalloc(&d->ddisp, n));
+    MI_HIP(hipMalloc(&d->dlen, n));
+    MI_HIP(hipMalloc(&d->dpfx, n));
+    MI_HIP(hipMemcpy(d->ddisp, d->disp.data(), n, hipMemcpyHostToDevice));
+    MI_HIP(hipMemcpy(d->dlen, d->len.data(), n, hipMemcpyHostToDevice));
+    MI_HIP(hipMemcpy(d->dpfx, d->pfx.data(), n, hipMemcpyHostToDevice));
+    return MI355X_SUCCESS;
+}
+
+static int64_t blk_bytes(const mi355x_ddt *d)
+{
+    int64_t b = 0;
+    for (int64_t l : d->len) b += l;
+    return b;
+}
+
+// opal description records (opal_datatype_internal.h:148-188), x86-64 layout: 32 bytes each
+struct OElem { uint16_t flags, type; uint32_t count, blocklen; int64_t extent, disp; };
+struct OLoop { uint16_t flags, type; uint32_t loops, items; uint64_t unused; int64_t extent; };
+struct OEnd { uint16_t flags, type; uint32_t items, unused; uint64_t size; int64_t first_elem_disp; };
+static_assert(sizeof(OElem) == 32 && sizeof(OLoop) == 32 && sizeof(OEnd) == 32, "opal dt_elem_desc is 32 B");
+constexpr uint16_t kOpalLoop = 0, kOpalEndLoop = 1, kOpalLB = 2, kOpalUB = 3;  // :107-110
+
+// expand records [i, end) at displacement `base` into runs (recursing into loops)
+static int expand(mi355x_ddt *d, const unsigned char *desc, uint32_t i, uint32_t end, int64_t base,
+                  const uint32_t *basic, size_t budget)
+{
+    while (i < end) {
+        const uint16_t type = ((const OElem *)(desc + 32 * (size_t)i))->type;
+        if (type == kOpalLoop) {
+            const OLoop *l = (const OLoop *)(desc + 32 * (size_t)i);
+            const uint32_t body_end = i + l->items;  // index of the END_LOOP record
+            for (uint32_t k = 0; k < l->loops; ++k) {
+                int rc = expand(d, desc, i + 1, body_end, base + (int64_t)k * l->extent, basic, budget);
+                if (rc) return rc;
+                if (d->disp.size() > budget) return set_error(MI355X_ERR_UNSUPPORTED, "datatype too irregular");
+            }
+            i = body_end + 1;
+        } else if (type == kOpalEndLoop || type == kOpalLB || type == kOpalUB) {
+            ++i;
+        } else {
+            const OElem *e = (const OElem *)(desc + 32 * (size_t)i);
+            const int64_t sz = basic[type];
+            if (sz <= 0) return set_error(MI355X_ERR_ARG, "unknown basic type %u", type);
+            if (e->extent == sz) {
+                add_run(d, base + e->disp, (int64_t)e->count * sz, sz);
+            } else {
+                for (uint32_t c = 0; c < e->count; ++c) add_run(d, base + e->disp + (int64_t)c * e->extent, sz, sz);
+            }
+            if (d->disp.size() > budget) return set_error(MI355X_ERR_UNSUPPORTED, "datatype too irregular");
+            ++i;
+        }
+    }
+    return MI355X_SUCCESS;
+}
+
+} // namespace mi355x
+
+using namespace mi355x;
+
+extern "C" {
+
+int mi355x_ddt_create(const int64_t *disp, const int64_t *len, size_t nruns, size_t nblk, int64_t stride,
+                      int64_t extent, mi355x_ddt_t **out)
+{
+    if (!out || (nruns && (!disp || !len)) || nblk < 1) return set_error(MI355X_ERR_ARG, "bad ddt arguments");
+    auto *d = new mi355x_ddt();
+    for (size_t r = 0; r < nruns; ++r) add_run(d, disp[r], len[r], 1);
+    d->nblk = (int64_t)nblk;
+    d->stride = stride;
+    d->extent = extent;
+    return finalize(d, out);
+}
+
+// MPI_Type_vector(count, blocklen, stride, oldtype) with a gap-free oldtype of elem_size bytes
+int mi355x_ddt_create_vector(size_t count, size_t blocklen, int64_t stride, size_t elem_size, mi355x_ddt_t **out)
+{
+    if (!out || elem_size == 0) return set_error(MI355X_ERR_ARG, "bad vector arguments");
+    auto *d = new mi355x_ddt();
+    const int64_t e = (int64_t)elem_size;
+    if (count > 0) {
+        if ((int64_t)blocklen == stride || count <= 1) {
+            add_run(d, 0, (int64_t)(count * blocklen) * e, e);
+        } else {
+            add_run(d, 0, (int64_t)blocklen * e, e);
+            d->nblk = (int64_t)count;
+            d->stride = stride * e;
+        }
+        d->extent = ((int64_t)(count - 1) * stride + (int64_t)blocklen) * e;
+    }
+    return finalize(d, out);
+}
+
+// MPI_Type_indexed(count, blocklens, disps, oldtype): adjacent blocks merge, as
+// ompi_datatype_create_indexed.c:48-63 does
+int mi355x_ddt_create_indexed(size_t count, const int *blocklens, const int *disps, size_t elem_size,
+                              mi355x_ddt_t **out)
+{
+    if (!out || elem_size == 0 || (count && (!blocklens || !disps))) return set_error(MI355X_ERR_ARG, "bad indexed arguments");
+    auto *d = new mi355x_ddt();
+    const int64_t e = (int64_t)elem_size;
+    int64_t lo = 0, hi = 0;
+    bool first = true;
+    for (size_t i = 0; i < count; ++i) {
+        add_run(d, (int64_t)disps[i] * e, (int64_t)blocklens[i] * e, e);
+        if (blocklens[i] > 0) {
+            const int64_t a = (int64_t)disps[i] * e, b = a + (int64_t)blocklens[i] * e;
+            if (first || a < lo) lo = a;
+            if (first || b > hi) hi = b;
+            first = false;
+        }
+    }
+    d->extent = hi - lo;
+    return finalize(d, out);
+}
+
+// Compile an opal description (opt_desc.desc, opt_desc.used records) of a datatype whose extent
+// is `extent` (ub - lb).  basic_sizes[type] = size of each opal basic type id.
+int mi355x_ddt_from_opal(const void *desc, uint32_t used, int64_t extent, const uint32_t *basic_sizes,
+                         mi355x_ddt_t **out)
+{
+    if (!desc || !basic_sizes || !out) return set_error(MI355X_ERR_ARG, "bad opal description arguments");
+    auto *d = new mi355x_ddt();
+    const unsigned char *p = (const unsigned char *)desc;
+    // a top-level LOOP covering the whole description (the vector shape) keeps its loop as
+    // the block layer instead of being unrolled into runs
+    const OLoop *l0 = (const OLoop *)p;
+    int rc;
+    if (used >= 2 && l0->type == kOpalLoop && l0->items + 1 == used) {
+        rc = expand(d, p, 1, l0->items, 0, basic_sizes, 1u << 20);
+        d->nblk = l0->loops;
+        d->stride = l0->extent;
+    } else {
+        rc = expand(d, p, 0, used, 0, basic_sizes, 1u << 20);
+    }
+    if (rc) {
+        delete d;
+        return rc;
+    }
+    d->extent = extent;
+    return finalize(d, out);
+}
+
+int mi355x_ddt_destroy(mi355x_ddt_t *d)
+{
+    if (!d) return MI355X_SUCCESS;
+    if (d->ddisp) {
+        (void)hipFree(d->ddisp);
+        (void)hipFree(d->dlen);
+        (void)hipFree(d->dpfx);
+    }
+    delete d;
+    return MI355X_SUCCESS;
+}
+
+size_t mi355x_ddt_size(const mi355x_ddt_t *d) { return d ? (size_t)(d->nblk * blk_bytes(d)) : 0; }
+int64_t mi355x_ddt_extent(const mi355x_ddt_t *d) { return d ? d->extent : 0; }
+int mi355x_ddt_nruns(const mi355x_ddt_t *d) { return d ? (int)d->disp.size() : 0; }
+
+static int ddt_move(const mi355x_ddt_t *d, bool pack, size_t count, void *mem, size_t pos, void *packed,
+                    size_t bytes, uint32_t *checksum, void *stream)
+{
+    if (!d || (bytes && (!mem || !packed))) return set_error(MI355X_ERR_ARG, "bad pack arguments");
+    const int64_t inst = d->nblk * blk_bytes(d);
+    if ((int64_t)(pos + bytes) > (int64_t)count * inst) return set_error(MI355X_ERR_ARG, "window past the message");
+    if (checksum) *checksum = 0;
+    if (bytes == 0 || inst == 0) return MI355X_SUCCESS;
+    hipStream_t s = resolve_stream(stream);
+    int rc0 = upload(const_cast<mi355x_ddt *>(d));
+    if (rc0) return rc0;
+    DdtDev dv;
+    dv.disp = d->ddisp;
+    dv.len = d->dlen;
+    dv.pfx = d->dpfx;
+    dv.nruns = (int)d->disp.size();
+    dv.nblk = d->nblk;
+    dv.stride = d->stride;
+    dv.extent = d->extent;
+    dv.blk_bytes = blk_bytes(d);
+    dv.inst_bytes = inst;
+    unsigned *dsum = nullptr;
+    if (checksum) {
+        MI_HIP(hipMallocAsync((void **)&dsum, sizeof(unsigned), s));
+        MI_HIP(hipMemsetAsync(dsum, 0, sizeof(unsigned), s));
+    }
+    int rc = launch_ddt(dv, pack, mem, packed, (int64_t)pos, (int64_t)bytes, dsum, s);
+    if (rc) return rc;
+    if (checksum) {
+        unsigned h = 0;
+        MI_HIP(hipMemcpyAsync(&h, dsum, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+        MI_HIP(hipFreeAsync(dsum, s));
+        MI_HIP(hipStreamSynchronize(s));
+        *checksum = h;
+    }
+    return MI355X_SUCCESS;
+}
+
+int mi355x_pack(const mi355x_ddt_t *d, size_t count, const void *base, size_t pos, void *dst, size_t bytes,
+                uint32_t *checksum, void *stream)
+{
+    return ddt_move(d, true, count, const_cast<void *>(base), pos, dst, bytes, checksum, stream);
+}
+
+int mi355x_unpack(const mi355x_ddt_t *d, size_t count, void *base, size_t pos, const void *src, size_t bytes,
+                  uint32_t *checksum, void *stream)
+{
+    return ddt_move(d, false, count, base, pos, const_cast<void *>(src), bytes, checksum, stream);
+}
+
+} // extern "C"

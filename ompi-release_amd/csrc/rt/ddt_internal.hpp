@@ -1,0 +1,22 @@
+// ddt_internal.hpp -- device view of a datatype layout (see ddt_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace mi355x {
+
+struct DdtDev {
+    const int64_t *disp;   // run displacement inside a block (device array)
+    const int64_t *len;    // run length in bytes
+    const int64_t *pfx;    // packed offset of the run inside a block
+    int nruns;
+    int64_t nblk, stride, extent;
+    int64_t blk_bytes, inst_bytes;
+};
+
+int launch_ddt(const DdtDev &d, bool pack, void *mem, void *packed, int64_t pos, int64_t bytes, unsigned *csum,
+               hipStream_t s);
+
+} // namespace mi355x

@@ -93,6 +93,24 @@ int oracle_reduce_scatter(int n, const int *rcounts, int type, int op,
 int oracle_reduce_scatter_alg(int alg, int n, const int *rcounts, int type, int op,
                               const void *const *sbufs, void *const *rbufs);
 
+/* ---------------- datatypes / convertor (ddt_oracle.c) ------------------------------------- */
+typedef struct oracle_ddt oracle_ddt_t;
+oracle_ddt_t *oracle_ddt_contiguous(int64_t count, int64_t elem);
+oracle_ddt_t *oracle_ddt_vector(int64_t count, int64_t blocklen, int64_t stride, int64_t elem);
+oracle_ddt_t *oracle_ddt_indexed(int count, const int *blocklens, const int *disps, int64_t elem);
+oracle_ddt_t *oracle_ddt_struct(int n, const int64_t *disp, const int64_t *len, const int64_t *elem,
+                                int64_t extent);
+void oracle_ddt_free(oracle_ddt_t *d);
+int64_t oracle_ddt_size(const oracle_ddt_t *d);
+int64_t oracle_ddt_extent(const oracle_ddt_t *d);
+int64_t oracle_ddt_round_position(const oracle_ddt_t *d, int64_t count, int64_t pos);
+int oracle_ddt_pack(const oracle_ddt_t *d, int64_t count, const void *base, int64_t pos, void *dst, int64_t bytes);
+int oracle_ddt_unpack(const oracle_ddt_t *d, int64_t count, void *base, int64_t pos, const void *src,
+                      int64_t bytes);
+unsigned long oracle_uicsum_partial(const void *source, size_t csumlen, unsigned int *lastPartialInt,
+                                    size_t *lastPartialLength);
+uint32_t oracle_ddt_pack_checksum(const oracle_ddt_t *d, int64_t count, const void *base, void *dst);
+
 /* Expression-order description of the allreduce fold actually applied to element `index`:
  * writes the rank fold order into order[0..n-1] for ring / segmented ring (acc starts at
  * order[0]; each later rank's local value is the `out` operand).  Returns 0 if the element's

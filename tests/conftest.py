@@ -57,6 +57,28 @@ def load_oracle() -> ctypes.CDLL:
         lib.oracle_reduce_decision.argtypes = [i, sz, i, c.POINTER(c.c_uint32)]
         lib.oracle_reduce_scatter_block.argtypes = [i, sz, i, i, c.POINTER(vp), c.POINTER(vp)]
         lib.oracle_ring_fold_order.argtypes = [i, sz, sz, c.POINTER(c.c_int)]
+        i64 = c.c_int64
+        lib.oracle_ddt_contiguous.restype = vp
+        lib.oracle_ddt_contiguous.argtypes = [i64, i64]
+        lib.oracle_ddt_vector.restype = vp
+        lib.oracle_ddt_vector.argtypes = [i64, i64, i64, i64]
+        lib.oracle_ddt_indexed.restype = vp
+        lib.oracle_ddt_indexed.argtypes = [i, c.POINTER(i), c.POINTER(i), i64]
+        lib.oracle_ddt_struct.restype = vp
+        lib.oracle_ddt_struct.argtypes = [i, c.POINTER(i64), c.POINTER(i64), c.POINTER(i64), i64]
+        lib.oracle_ddt_free.argtypes = [vp]
+        lib.oracle_ddt_size.restype = i64
+        lib.oracle_ddt_size.argtypes = [vp]
+        lib.oracle_ddt_extent.restype = i64
+        lib.oracle_ddt_extent.argtypes = [vp]
+        lib.oracle_ddt_round_position.restype = i64
+        lib.oracle_ddt_round_position.argtypes = [vp, i64, i64]
+        lib.oracle_ddt_pack.argtypes = [vp, i64, vp, i64, vp, i64]
+        lib.oracle_ddt_unpack.argtypes = [vp, i64, vp, i64, vp, i64]
+        lib.oracle_uicsum_partial.restype = c.c_ulong
+        lib.oracle_uicsum_partial.argtypes = [vp, sz, c.POINTER(c.c_uint), c.POINTER(sz)]
+        lib.oracle_ddt_pack_checksum.restype = c.c_uint32
+        lib.oracle_ddt_pack_checksum.argtypes = [vp, i64, vp, vp]
         lib.oracle_ompi_fn2.restype = vp
         lib.oracle_ompi_fn2.argtypes = [i, i]
         lib.oracle_ompi_fn3.restype = vp

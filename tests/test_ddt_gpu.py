@@ -1,0 +1,151 @@
+"""GPU convertor (mi355x_pack / mi355x_unpack) vs the oracle, with the reference's datatype
+known-answer tests restated on device buffers (test/datatype/position_noncontig.c,
+position.c, checksum.c), random windows over vector / indexed / struct layouts, and the
+BASELINE config-5 shape (MPI_Type_vector(2^22, 64, 128, MPI_FLOAT): 1 GiB packed) checked against
+torch's strided view."""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+from ddtcases import LDI, ldi_struct, segments, shuffle
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).cuda()
+
+
+def test_position_noncontig_gpu(gpu, pkg, oracle):
+    torch = gpu
+    nelt = 300
+    od = oracle.oracle_ddt_vector(nelt // 2, 1, 2, 4)
+    d = pkg.Ddt.vector(nelt // 2, 1, 2, 4)
+    send = np.arange(nelt, dtype=np.int32)
+    dsend = _dev(torch, send)
+    drecv = _dev(torch, np.full(nelt, 0xdeadbeef, dtype=np.uint32))
+    segs = shuffle(segments(oracle, od, 1, 113))
+    bufs = []
+    for pos, size in segs:
+        b = torch.zeros(128, dtype=torch.uint8, device="cuda")
+        d.pack(1, dsend.data_ptr(), pos, b.data_ptr(), size)
+        want = np.zeros(size, dtype=np.uint8)
+        oracle.oracle_ddt_pack(od, 1, send.ctypes.data, pos, want.ctypes.data, size)
+        assert np.array_equal(b[:size].cpu().numpy(), want), (pos, size)
+        bufs.append(b)
+    for (pos, size), b in zip(segs, bufs):
+        d.unpack(1, drecv.data_ptr(), pos, b.data_ptr(), size)
+    got = drecv.cpu().numpy().view(np.int32)
+    want = np.where(np.arange(nelt) % 2 == 1, np.int32(-559038737), np.arange(nelt, dtype=np.int32))
+    assert np.array_equal(got, want)
+
+
+def test_position_long_double_int_gpu(gpu, pkg, oracle):
+    torch = gpu
+    n = 2048
+    od = ldi_struct(oracle)
+    d = pkg.Ddt.runs([0, 16], [16, 4], extent=32)
+    send = np.zeros(n, dtype=LDI)
+    send["ld"] = np.arange(n, dtype=np.longdouble) + np.arange(n, dtype=np.longdouble) / 100000.0
+    send["i"] = np.arange(n)
+    dsend, drecv = _dev(torch, send), torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+    segs = shuffle(segments(oracle, od, n, 113))
+    for pos, size in segs:
+        b = torch.zeros(128, dtype=torch.uint8, device="cuda")
+        d.pack(n, dsend.data_ptr(), pos, b.data_ptr(), size)
+        d.unpack(n, drecv.data_ptr(), pos, b.data_ptr(), size)
+    recv = drecv.cpu().numpy().view(LDI)
+    assert np.array_equal(recv["ld"], send["ld"]) and np.array_equal(recv["i"], send["i"])
+
+
+def test_checksum_gpu(gpu, pkg, oracle):
+    torch = gpu
+    size = 1024
+    d = pkg.Ddt.vector(size, 1, 2, 4)
+    od = oracle.oracle_ddt_vector(size, 1, 2, 4)
+    rng = np.random.default_rng(11)
+    data = np.zeros(2 * size, dtype=np.int32)
+    data[0::2] = rng.integers(0, 2**31 - 1, size)
+    packed = np.zeros(size, dtype=np.int32)
+    want = oracle.oracle_ddt_pack_checksum(od, 1, data.ctypes.data, packed.ctypes.data)
+    dd = _dev(torch, data)
+    dp = torch.zeros(size * 4, dtype=torch.uint8, device="cuda")
+    cs = d.pack(1, dd.data_ptr(), 0, dp.data_ptr(), size * 4, checksum=True)
+    assert cs == want
+    assert np.array_equal(dp.cpu().numpy().view(np.int32), packed)
+    out = torch.zeros(2 * size * 4, dtype=torch.uint8, device="cuda")
+    half = size * 2
+    c1 = d.unpack(1, out.data_ptr(), 0, dp.data_ptr(), half, checksum=True)
+    c2 = d.unpack(1, out.data_ptr(), half, dp.data_ptr() + half, size * 4 - half, checksum=True)
+    assert (c1 + c2) & 0xFFFFFFFF == want
+    # odd window splits: the per-window sums still add up to the message checksum
+    parts = [0, 3, 101, 2047, 4093, size * 4]
+    tot = 0
+    for a, b in zip(parts[:-1], parts[1:]):
+        tot += d.pack(1, dd.data_ptr(), a, dp.data_ptr(), b - a, checksum=True)
+    assert tot & 0xFFFFFFFF == want
+
+
+@pytest.mark.parametrize("kind", ["vector", "indexed", "struct", "vector_odd"])
+def test_random_windows(gpu, pkg, oracle, kind):
+    torch = gpu
+    rng = np.random.default_rng(["vector", "indexed", "struct", "vector_odd"].index(kind) + 5)
+    if kind == "vector":
+        count, args = 3, (97, 64, 128, 4)
+        d, od = pkg.Ddt.vector(*args), oracle.oracle_ddt_vector(*args)
+    elif kind == "vector_odd":
+        count, args = 5, (33, 3, 7, 2)
+        d, od = pkg.Ddt.vector(*args), oracle.oracle_ddt_vector(*args)
+    elif kind == "indexed":
+        bl = [int(x) for x in rng.integers(0, 9, 40)]
+        dp = list(np.cumsum(rng.integers(0, 12, 40)))
+        dp = [int(x) for x in dp]
+        count = 4
+        d = pkg.Ddt.indexed(bl, dp, 8)
+        od = oracle.oracle_ddt_indexed(40, (ctypes.c_int * 40)(*bl), (ctypes.c_int * 40)(*dp), 8)
+    else:
+        count = 50
+        d = pkg.Ddt.runs([0, 16], [16, 4], extent=32)
+        od = ldi_struct(oracle)
+    total = count * oracle.oracle_ddt_size(od)
+    assert d.size * count == total
+    span = (count - 1) * oracle.oracle_ddt_extent(od) + 4096 + oracle.oracle_ddt_extent(od)
+    base = rng.integers(0, 256, span, dtype=np.uint8)
+    dbase = _dev(torch, base)
+    full = np.zeros(total, dtype=np.uint8)
+    oracle.oracle_ddt_pack(od, count, base.ctypes.data, 0, full.ctypes.data, total)
+    cuts = sorted(set([0, total] + [int(x) for x in rng.integers(0, total, 9)]))
+    out = torch.zeros(total + 64, dtype=torch.uint8, device="cuda")
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        d.pack(count, dbase.data_ptr(), a, out.data_ptr() + a, b - a)
+    assert np.array_equal(out[:total].cpu().numpy(), full)
+    # unpack into zeros reproduces exactly the type map's bytes
+    z = torch.zeros(span, dtype=torch.uint8, device="cuda")
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        d.unpack(count, z.data_ptr(), a, out.data_ptr() + a, b - a)
+    want = np.zeros(span, dtype=np.uint8)
+    oracle.oracle_ddt_unpack(od, count, want.ctypes.data, 0, full.ctypes.data, total)
+    assert np.array_equal(z.cpu().numpy(), want)
+
+
+def test_config5_vector_1gib(gpu, pkg):
+    """MPI_Type_vector(2^22, 64, 128, MPI_FLOAT) over a 2 GiB-extent buffer: pack == the strided
+    view's blocks, unpack into zeros restores them and leaves the gaps untouched"""
+    torch = gpu
+    nblk = 1 << 22
+    d = pkg.Ddt.vector(nblk, 64, 128, 4)
+    x = torch.randn(nblk, 128, device="cuda")
+    packed = torch.empty(nblk, 64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    d.pack(1, x.data_ptr(), 0, packed.data_ptr(), d.size, s)
+    torch.cuda.synchronize()
+    assert torch.equal(packed, x[:, :64])
+    y = torch.zeros_like(x)
+    d.unpack(1, y.data_ptr(), 0, packed.data_ptr(), d.size, s)
+    torch.cuda.synchronize()
+    assert torch.equal(y[:, :64], x[:, :64]) and int(torch.count_nonzero(y[:, 64:])) == 0
+    del x, y, packed
+    torch.cuda.empty_cache()
