@@ -120,6 +120,42 @@ ompi_datatype_t *mini_datatype(int id)
     return (id >= 0 && id < OMPI_DATATYPE_MPI_MAX_PREDEFINED) ? dt_objs[id] : NULL;
 }
 
+/* a committed derived datatype from its optimized description (records of 32 bytes,
+ * opal_datatype_internal.h:148-188) and bounds -- what ompi_datatype_create_* + commit leave in
+ * opal_datatype_t (opal_datatype.h:103-131) */
+ompi_datatype_t *mini_datatype_create_raw(const void *desc, uint32_t used, size_t size, ptrdiff_t lb, ptrdiff_t ub,
+                                          ptrdiff_t true_lb, ptrdiff_t true_ub, uint16_t flags)
+{
+    mini_init();
+    ompi_datatype_t *d = (ompi_datatype_t *)mi355x_obj_new(&ompi_datatype_t_class);
+    memset((char *)d + sizeof(opal_object_t), 0, sizeof(*d) - sizeof(opal_object_t));
+    d->super.flags = flags;
+    d->super.id = 0; /* OPAL_DATATYPE_LOOP: not a predefined id */
+    d->super.size = size;
+    d->super.lb = lb;
+    d->super.ub = ub;
+    d->super.true_lb = true_lb;
+    d->super.true_ub = true_ub;
+    void *copy = malloc((size_t)used * 32);
+    memcpy(copy, desc, (size_t)used * 32);
+    d->super.opt_desc.desc = (dt_elem_desc_t *)copy;
+    d->super.opt_desc.used = used;
+    d->super.opt_desc.length = used;
+    d->super.desc = d->super.opt_desc;
+    d->id = -1;
+    snprintf(d->name, sizeof(d->name), "derived");
+    return d;
+}
+
+void mini_datatype_destroy(ompi_datatype_t *d)
+{
+    if (!d) return;
+    free(d->super.opt_desc.desc);
+    d->super.opt_desc.desc = NULL;
+    d->super.desc.desc = NULL;
+    mi355x_obj_release(&d->super.super);
+}
+
 int mini_datatype_id_for_slot(int slot)
 {
     mini_init();

@@ -12,6 +12,9 @@ extern "C" {
 void mini_init(void);
 ompi_datatype_t *mini_datatype(int id);
 int mini_datatype_id_for_slot(int slot);
+ompi_datatype_t *mini_datatype_create_raw(const void *desc, uint32_t used, size_t size, ptrdiff_t lb, ptrdiff_t ub,
+                                          ptrdiff_t true_lb, ptrdiff_t true_ub, uint16_t flags);
+void mini_datatype_destroy(ompi_datatype_t *d);
 void mini_set_base_function(int op, int slot, void *fn2, void *fn3);
 ompi_op_t *mini_op_create(int code);
 int mini_op_select(ompi_op_t *op, ompi_op_base_component_t **comps, int ncomp);

@@ -30,6 +30,12 @@ typedef struct mca_coll_mi355x_module_t {
     mca_coll_base_module_t *prev_allgather_module;
     mca_coll_base_module_bcast_fn_t prev_bcast;
     mca_coll_base_module_t *prev_bcast_module;
+    /* GPU-convertor layouts of the derived datatypes seen on this communicator, and the packed
+     * staging buffer (device memory; registered once, re-registered when it grows) */
+    struct ddt_slot { uint64_t sig; const void *dt; mi355x_ddt_t *d; } ddt_cache[8];
+    int ddt_next;
+    void *scratch;
+    size_t scratch_bytes;
 } mca_coll_mi355x_module_t;
 
 static void module_construct(opal_object_t *o)
@@ -51,6 +57,9 @@ static void module_destruct(opal_object_t *o)
     release_prev(m->prev_reduce_scatter_block_module);
     release_prev(m->prev_allgather_module);
     release_prev(m->prev_bcast_module);
+    for (int i = 0; i < 8; ++i)
+        if (m->ddt_cache[i].d) mi355x_ddt_destroy(m->ddt_cache[i].d);
+    if (m->scratch) mi355x_free(m->scratch);
     if (m->engine) mi355x_comm_destroy(m->engine);
 }
 
@@ -89,6 +98,77 @@ static int contiguous_bytes(const struct ompi_datatype_t *dt, int count, size_t 
     if (!(dt->super.flags & OPAL_DATATYPE_FLAG_NO_GAPS) || dt->super.true_lb != 0) return 0;
     *bytes = (size_t)count * dt->super.size;
     return 1;
+}
+
+/* ------------------------------------------------------------------ derived datatypes
+ * A non-contiguous datatype on device memory moves through the GPU convertor: the layout is
+ * compiled once from the datatype's optimized description (opt_desc, the one
+ * OPAL_CONVERTOR_PREPARE selects, opal_convertor.c:513), packed into a device staging buffer,
+ * moved as bytes by the engine, and unpacked -- the device-side equivalent of the convertor
+ * pack/unpack the PML runs per fragment (opal_datatype_pack.c:250-374, _unpack.c:245-...). */
+
+/* sizes of the OPAL basic types by id (opal/datatype/opal_datatype_internal.h:107-131; x86-64:
+ * long double is FLOAT16) */
+static const uint32_t opal_basic_sizes[25] = {0, 0, 0, 0, 1, 2, 4, 8, 16, 1, 2, 4, 8, 16, 2, 4, 8, 12, 16,
+                                              8, 16, 32, 1, 4, 0};
+
+static uint64_t fnv1a(uint64_t h, const void *p, size_t n)
+{
+    const unsigned char *b = (const unsigned char *)p;
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+    return h;
+}
+
+/* the layout of dt, or NULL when the convertor cannot take it (the caller then falls back) */
+static mi355x_ddt_t *ddt_of(struct mca_coll_mi355x_module_t *m, const struct ompi_datatype_t *dt)
+{
+    const dt_type_desc_t *td = dt->super.opt_desc.desc ? &dt->super.opt_desc : &dt->super.desc;
+    if (!td->desc || td->used == 0 || dt->super.size == 0) return NULL;
+    const size_t rec = 32; /* sizeof(dt_elem_desc_t), opal_datatype_internal.h:185-189 */
+    uint64_t sig = fnv1a(1469598103934665603ull, td->desc, (size_t)td->used * rec);
+    const int64_t ext = (int64_t)(dt->super.ub - dt->super.lb);
+    sig = fnv1a(sig, &dt->super.size, sizeof(dt->super.size));
+    sig = fnv1a(sig, &ext, sizeof(ext));
+    for (int i = 0; i < 8; ++i)
+        if (m->ddt_cache[i].d && m->ddt_cache[i].dt == dt && m->ddt_cache[i].sig == sig) return m->ddt_cache[i].d;
+    mi355x_ddt_t *d = NULL;
+    if (mi355x_ddt_from_opal(td->desc, td->used, ext, opal_basic_sizes, &d) != MI355X_SUCCESS) return NULL;
+    if (mi355x_ddt_size(d) != dt->super.size) {
+        mi355x_ddt_destroy(d);
+        return NULL;
+    }
+    struct ddt_slot *e = &m->ddt_cache[m->ddt_next];
+    m->ddt_next = (m->ddt_next + 1) & 7;
+    if (e->d) mi355x_ddt_destroy(e->d);
+    e->d = d;
+    e->dt = dt;
+    e->sig = sig;
+    return d;
+}
+
+static void *scratch(struct mca_coll_mi355x_module_t *m, size_t bytes)
+{
+    if (bytes <= m->scratch_bytes) return m->scratch;
+    if (m->scratch) mi355x_free(m->scratch);
+    m->scratch = NULL;
+    m->scratch_bytes = 0;
+    size_t want = bytes < ((size_t)1 << 20) ? ((size_t)1 << 20) : bytes;
+    if (mi355x_malloc(&m->scratch, want) != MI355X_SUCCESS) return NULL;
+    m->scratch_bytes = want;
+    return m->scratch;
+}
+
+/* one side of a convertor move: (buf, count, dt) <-> packed bytes at p */
+static int stage(struct mca_coll_mi355x_module_t *m, int pack, void *buf, int count, const struct ompi_datatype_t *dt,
+                 void *p, size_t bytes)
+{
+    size_t cb;
+    if (contiguous_bytes(dt, count, &cb))
+        return pack ? mi355x_memcpy_async(p, buf, bytes, NULL) : mi355x_memcpy_async(buf, p, bytes, NULL);
+    mi355x_ddt_t *d = ddt_of(m, dt);
+    if (!d) return MI355X_ERR_UNSUPPORTED;
+    return pack ? mi355x_pack(d, (size_t)count, buf, 0, p, bytes, NULL, NULL)
+                : mi355x_unpack(d, (size_t)count, buf, 0, p, bytes, NULL, NULL);
 }
 
 static int map_rc(int rc)
@@ -153,12 +233,29 @@ int mca_coll_mi355x_allgather(void *sbuf, int scount, struct ompi_datatype_t *sd
 {
     mca_coll_mi355x_module_t *m = MOD(module);
     const int inplace = (sbuf == MPI_IN_PLACE);
-    size_t rb = 0, sb = 0;
-    const int ok = is_dev(rbuf) && (inplace || is_dev(sbuf)) && contiguous_bytes(rdtype, rcount, &rb) &&
-                   (inplace || (contiguous_bytes(sdtype, scount, &sb) && sb == rb));
-    if (!ok)
+    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || rcount < 0 || (!inplace && scount < 0))
         return m->prev_allgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_allgather_module);
-    return map_rc(mi355x_allgather(m->engine, inplace ? NULL : sbuf, rbuf, rb, NULL));
+    size_t rb = 0, sb = 0;
+    if (contiguous_bytes(rdtype, rcount, &rb) && (inplace || (contiguous_bytes(sdtype, scount, &sb) && sb == rb)))
+        return map_rc(mi355x_allgather(m->engine, inplace ? NULL : sbuf, rbuf, rb, NULL));
+    /* derived datatypes: pack my block into the staging buffer, gather packed blocks in place,
+     * unpack all n blocks with one launch (block r = instances [r*rcount, (r+1)*rcount)) */
+    const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm);
+    const size_t blk = (size_t)rcount * rdtype->super.size;
+    if (!inplace && (size_t)scount * sdtype->super.size != blk) return OMPI_ERR_BAD_PARAM;
+    if ((!inplace && !contiguous_bytes(sdtype, scount, &sb) && !ddt_of(m, sdtype)) ||
+        (!contiguous_bytes(rdtype, rcount, &rb) && !ddt_of(m, rdtype)))
+        return m->prev_allgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_allgather_module);
+    if (blk == 0) return OMPI_SUCCESS;
+    char *st = (char *)scratch(m, blk * (size_t)n);
+    if (!st) return OMPI_ERR_OUT_OF_RESOURCE;
+    const ptrdiff_t rext = rdtype->super.ub - rdtype->super.lb;
+    int rc = inplace ? stage(m, 1, (char *)rbuf + (ptrdiff_t)me * rcount * rext, rcount, rdtype, st + blk * me, blk)
+                     : stage(m, 1, sbuf, scount, sdtype, st + blk * me, blk);
+    if (rc == MI355X_SUCCESS) rc = mi355x_allgather(m->engine, NULL, st, blk, NULL);
+    if (rc == MI355X_SUCCESS) rc = stage(m, 0, rbuf, rcount * n, rdtype, st, blk * (size_t)n);
+    if (rc == MI355X_SUCCESS) rc = mi355x_stream_sync(NULL);
+    return map_rc(rc);
 }
 
 int mca_coll_mi355x_bcast(void *buff, int count, struct ompi_datatype_t *datatype, int root,
@@ -166,9 +263,22 @@ int mca_coll_mi355x_bcast(void *buff, int count, struct ompi_datatype_t *datatyp
 {
     mca_coll_mi355x_module_t *m = MOD(module);
     size_t bytes = 0;
-    if (!is_dev(buff) || !contiguous_bytes(datatype, count, &bytes))
+    if (!is_dev(buff) || count < 0)
         return m->prev_bcast(buff, count, datatype, root, comm, m->prev_bcast_module);
-    return map_rc(mi355x_bcast(m->engine, buff, bytes, root, NULL));
+    if (contiguous_bytes(datatype, count, &bytes)) return map_rc(mi355x_bcast(m->engine, buff, bytes, root, NULL));
+    /* derived datatype: root packs, the packed bytes are broadcast, the others unpack */
+    if (!ddt_of(m, datatype)) return m->prev_bcast(buff, count, datatype, root, comm, m->prev_bcast_module);
+    bytes = (size_t)count * datatype->super.size;
+    if (bytes == 0) return OMPI_SUCCESS;
+    void *st = scratch(m, bytes);
+    if (!st) return OMPI_ERR_OUT_OF_RESOURCE;
+    const int me = mi355x_comm_rank_of(comm);
+    int rc = MI355X_SUCCESS;
+    if (me == root) rc = stage(m, 1, buff, count, datatype, st, bytes);
+    if (rc == MI355X_SUCCESS) rc = mi355x_bcast(m->engine, st, bytes, root, NULL);
+    if (rc == MI355X_SUCCESS && me != root) rc = stage(m, 0, buff, count, datatype, st, bytes);
+    if (rc == MI355X_SUCCESS) rc = mi355x_stream_sync(NULL);
+    return map_rc(rc);
 }
 
 /* ------------------------------------------------------------------ module / component */

@@ -53,6 +53,8 @@ struct BufDesc {
     uint64_t off;
     uint64_t raw;      // loopback: the pointer itself
     uint64_t present;  // 0: NULL buffer
+    uint64_t base;     // exporter's allocation base (its VA; the peer-map key)
+    uint64_t id;       // exporter's allocation id (HIP_POINTER_ATTRIBUTE_BUFFER_ID)
 };
 
 struct alignas(64) RankSlot {
@@ -75,19 +77,29 @@ struct Ctrl {
 
 static size_t ctrl_bytes(int size) { return sizeof(Ctrl) + sizeof(RankSlot) * (size_t)(size - 1); }
 
+// A peer allocation is keyed by (peer, its base VA) and remembered with its allocation id: when
+// the exporter frees and reallocates at the same address the id changes and the stale mapping
+// is closed and replaced (the invalidation mpool/rgpusm does on a buffer-id mismatch,
+// ompi/mca/mpool/rgpusm/mpool_rgpusm_module.c:243-281, common_cuda.c:1709-1745).
 struct HandleKey {
     int peer;
-    std::array<char, sizeof(hipIpcMemHandle_t)> h;
+    uint64_t base;
     bool operator<(const HandleKey &o) const
     {
         if (peer != o.peer) return peer < o.peer;
-        return h < o.h;
+        return base < o.base;
     }
+};
+
+struct PeerMap {
+    uint64_t id;
+    void *mapped;
 };
 
 struct LocalReg {
     uintptr_t base;
     size_t size;
+    uint64_t id;
     hipIpcMemHandle_t h;
 };
 
@@ -106,7 +118,7 @@ struct mi355x_comm {
     std::shared_ptr<mi355x::LoopShared> loop;
     std::string shm_name;
     uint64_t seq = 0;
-    std::map<mi355x::HandleKey, void *> peer_maps;
+    std::map<mi355x::HandleKey, mi355x::PeerMap> peer_maps;
     std::vector<mi355x::LocalReg> local_regs;
     void *scratch = nullptr;
     size_t scratch_bytes = 0;
@@ -148,6 +160,16 @@ static int barrier(mi355x_comm *c)
 }
 
 // ----------------------------------------------------------------- registration
+static uint64_t buffer_id(const void *p)
+{
+    unsigned long long id = 0;
+    if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)p) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return (uint64_t)id;
+}
+
 static int local_handle(mi355x_comm *c, const void *p, BufDesc *d)
 {
     std::memset(d, 0, sizeof(*d));
@@ -158,11 +180,19 @@ static int local_handle(mi355x_comm *c, const void *p, BufDesc *d)
         return MI355X_SUCCESS;
     }
     const uintptr_t up = (uintptr_t)p;
-    for (const LocalReg &r : c->local_regs) {
+    const uint64_t id = buffer_id(p);
+    for (size_t i = 0; i < c->local_regs.size(); ++i) {
+        const LocalReg &r = c->local_regs[i];
         if (up >= r.base && up < r.base + r.size) {
-            d->h = r.h;
-            d->off = up - r.base;
-            return MI355X_SUCCESS;
+            if (r.id == id && id != 0) {
+                d->h = r.h;
+                d->off = up - r.base;
+                d->base = r.base;
+                d->id = r.id;
+                return MI355X_SUCCESS;
+            }
+            c->local_regs.erase(c->local_regs.begin() + (long)i);  // freed and reallocated: stale
+            break;
         }
     }
     void *base = nullptr;
@@ -171,10 +201,14 @@ static int local_handle(mi355x_comm *c, const void *p, BufDesc *d)
     LocalReg reg;
     reg.base = (uintptr_t)base;
     reg.size = sz;
+    reg.id = id;
     MI_HIP(hipIpcGetMemHandle(&reg.h, base));
-    c->local_regs.push_back(reg);
+    // without an allocation id the entry cannot be validated later: do not cache it
+    if (id != 0) c->local_regs.push_back(reg);
     d->h = reg.h;
     d->off = up - reg.base;
+    d->base = reg.base;
+    d->id = id;
     return MI355X_SUCCESS;
 }
 
@@ -188,16 +222,21 @@ static int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out)
     }
     HandleKey key;
     key.peer = peer;
-    std::memcpy(key.h.data(), &d.h, sizeof(d.h));
+    key.base = d.base;
     auto it = c->peer_maps.find(key);
+    if (it != c->peer_maps.end() && (it->second.id != d.id || d.id == 0)) {
+        (void)hipIpcCloseMemHandle(it->second.mapped);
+        c->peer_maps.erase(it);
+        it = c->peer_maps.end();
+    }
     void *base;
     if (it != c->peer_maps.end()) {
-        base = it->second;
+        base = it->second.mapped;
     } else {
         hipError_t e = hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess);
         if (e != hipSuccess)
             return set_error(MI355X_ERR_PEER, "hipIpcOpenMemHandle(rank %d): %s", peer, hipGetErrorString(e));
-        c->peer_maps[key] = base;
+        c->peer_maps[key] = PeerMap{d.id, base};
     }
     *out = (char *)base + d.off;
     return MI355X_SUCCESS;
@@ -417,7 +456,7 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
 {
     if (!c) return MI355X_SUCCESS;
     (void)hipSetDevice(c->device);
-    for (auto &kv : c->peer_maps) (void)hipIpcCloseMemHandle(kv.second);
+    for (auto &kv : c->peer_maps) (void)hipIpcCloseMemHandle(kv.second.mapped);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->loopback) {
         std::lock_guard<std::mutex> g(c->loop->mtx);

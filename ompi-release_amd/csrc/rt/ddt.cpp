@@ -239,7 +239,10 @@ static int ddt_move(const mi355x_ddt_t *d, bool pack, size_t count, void *mem, s
         MI_HIP(hipMallocAsync((void **)&dsum, sizeof(unsigned), s));
         MI_HIP(hipMemsetAsync(dsum, 0, sizeof(unsigned), s));
     }
-    int rc = launch_ddt(dv, pack, mem, packed, (int64_t)pos, (int64_t)bytes, dsum, s);
+    int rc = 1;
+    if (d->disp.size() == 1)
+        rc = launch_ddt_rows(dv, 1, d->disp[0], d->len[0], pack, mem, packed, (int64_t)pos, (int64_t)bytes, dsum, s);
+    if (rc == 1) rc = launch_ddt(dv, pack, mem, packed, (int64_t)pos, (int64_t)bytes, dsum, s);
     if (rc) return rc;
     if (checksum) {
         unsigned h = 0;

@@ -18,5 +18,8 @@ struct DdtDev {
 
 int launch_ddt(const DdtDev &d, bool pack, void *mem, void *packed, int64_t pos, int64_t bytes, unsigned *csum,
                hipStream_t s);
+// the row kernel (one run per block, 16-B aligned); returns 1 when it does not apply
+int launch_ddt_rows(const DdtDev &d, int nruns_host, int64_t run_disp, int64_t run_len, bool pack, void *mem,
+                    void *packed, int64_t pos, int64_t bytes, unsigned *csum, hipStream_t s);
 
 } // namespace mi355x

@@ -96,6 +96,131 @@ __global__ __launch_bounds__(256) void k_ddt(DdtDev d, char *mem, char *packed, 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Row kernel: the layout is one run of L bytes per block (vector, contiguous-with-gaps: what
+// MPI_Type_vector and most derived types used for halos/columns compile to), everything 16-byte
+// aligned.  Row g (over all instances) starts at (g / nblk) * extent + (g % nblk) * stride + disp.
+// One-shot grid: each lane moves U 16-byte slots, lanes of a wave on consecutive slots, all U
+// loads issued before the stores.  The two divisions per slot are 32-bit multiply-high
+// (Granlund-Montgomery magic numbers computed on the host), no 64-bit division, no search.
+struct FastDiv {
+    uint32_t m, l, d;
+};
+
+static FastDiv make_fastdiv(uint32_t d)
+{
+    FastDiv f;
+    f.d = d;
+    uint32_t l = 0;
+    while (l < 32 && ((uint64_t)1 << l) < d) ++l;
+    f.l = l;
+    f.m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1);
+    return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f)
+{
+    return (uint32_t)(((uint64_t)__umulhi(f.m, n) + n) >> f.l);
+}
+
+struct RowArgs {
+    char *mem;
+    char *packed;
+    int64_t disp, stride, extent;
+    FastDiv per_row;   // slots per row
+    FastDiv per_inst;  // rows per instance (nblk)
+    uint32_t first;    // first slot (pos / 16)
+    uint32_t nslots;
+};
+
+template <bool PACK, bool CSUM, bool NT, int U>
+__global__ __launch_bounds__(256) void k_ddt_rows(RowArgs a, unsigned *csum)
+{
+    const uint32_t tpb = blockDim.x;
+    const uint32_t base = blockIdx.x * (tpb * U) + threadIdx.x;
+    u32x4d v[U];
+    char *mp[U];
+    unsigned acc = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t i = base + (uint32_t)u * tpb;
+        mp[u] = nullptr;
+        if (i < a.nslots) {
+            const uint32_t q = a.first + i;
+            const uint32_t g = fdiv(q, a.per_row);
+            const uint32_t w = q - g * a.per_row.d;
+            const uint32_t k = fdiv(g, a.per_inst);
+            const uint32_t j = g - k * a.per_inst.d;
+            mp[u] = a.mem + (int64_t)k * a.extent + (int64_t)j * a.stride + a.disp + ((int64_t)w << 4);
+            const u32x4d *src = reinterpret_cast<const u32x4d *>(PACK ? mp[u] : a.packed + ((size_t)i << 4));
+            if constexpr (NT) v[u] = __builtin_nontemporal_load(src);
+            else v[u] = *src;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (mp[u]) {
+            u32x4d *dst = reinterpret_cast<u32x4d *>(PACK ? a.packed + ((size_t)(base + (uint32_t)u * tpb) << 4) : mp[u]);
+            if constexpr (NT) __builtin_nontemporal_store(v[u], dst);
+            else *dst = v[u];
+            if constexpr (CSUM) acc += v[u].x + v[u].y + v[u].z + v[u].w;
+        }
+    }
+    if constexpr (CSUM) {
+        for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+        if ((threadIdx.x & 63) == 0) atomicAdd(csum, acc);
+    }
+}
+
+// the row kernel applies: one run per block, every address and the window 16-B aligned, and
+// slot / row counts in 32 bits
+static bool rows_apply(const DdtDev &d, int nruns_host, int64_t run_disp, int64_t run_len, const void *mem,
+                       const void *packed, int64_t pos, int64_t bytes)
+{
+    if (nruns_host != 1 || (run_len & 15) || run_len == 0) return false;
+    if (((uintptr_t)mem + (uint64_t)run_disp) & 15) return false;
+    if ((d.stride & 15) || (d.extent & 15) || ((uintptr_t)packed & 15) || (pos & 15) || (bytes & 15)) return false;
+    const int64_t last_slot = (pos + bytes) >> 4;
+    const int64_t rows = last_slot / (run_len >> 4) + 1;
+    return last_slot < ((int64_t)1 << 32) && rows < ((int64_t)1 << 32) && d.nblk < ((int64_t)1 << 32) &&
+           (run_len >> 4) < ((int64_t)1 << 32);
+}
+
+template <bool PACK, bool CSUM>
+static void launch_rows(const RowArgs &a, bool nt, unsigned *csum, hipStream_t s)
+{
+    constexpr int U = 4;
+    const unsigned blocks = (unsigned)((a.nslots + 256u * U - 1) / (256u * U));
+    if (nt) hipLaunchKernelGGL((k_ddt_rows<PACK, CSUM, true, U>), dim3(blocks), dim3(256), 0, s, a, csum);
+    else hipLaunchKernelGGL((k_ddt_rows<PACK, CSUM, false, U>), dim3(blocks), dim3(256), 0, s, a, csum);
+}
+
+int launch_ddt_rows(const DdtDev &d, int nruns_host, int64_t run_disp, int64_t run_len, bool pack, void *mem,
+                    void *packed, int64_t pos, int64_t bytes, unsigned *csum, hipStream_t s)
+{
+    if (!rows_apply(d, nruns_host, run_disp, run_len, mem, packed, pos, bytes)) return 1;
+    RowArgs a;
+    a.mem = static_cast<char *>(mem);
+    a.packed = static_cast<char *>(packed);
+    a.disp = run_disp;
+    a.stride = d.stride;
+    a.extent = d.extent;
+    a.per_row = make_fastdiv((uint32_t)(run_len >> 4));
+    a.per_inst = make_fastdiv((uint32_t)d.nblk);
+    a.first = (uint32_t)(pos >> 4);
+    a.nslots = (uint32_t)(bytes >> 4);
+    const bool nt = 2 * bytes > ((int64_t)256 << 20);  // streaming sizes bypass the caches
+    if (pack) {
+        if (csum) launch_rows<true, true>(a, nt, csum, s);
+        else launch_rows<true, false>(a, nt, csum, s);
+    } else {
+        if (csum) launch_rows<false, true>(a, nt, csum, s);
+        else launch_rows<false, false>(a, nt, csum, s);
+    }
+    MI_HIP(hipGetLastError());
+    return MI355X_SUCCESS;
+}
+
 int launch_ddt(const DdtDev &d, bool pack, void *mem, void *packed, int64_t pos, int64_t bytes, unsigned *csum,
                hipStream_t s)
 {

@@ -242,3 +242,18 @@ uint32_t oracle_ddt_pack_checksum(const oracle_ddt_t *d, int64_t count, const vo
             }
     return sum;
 }
+
+/* whole-message pack as the reference's homogeneous engine does it for a GPU-less host: one
+ * memcpy per contiguous run (opal_generic_simple_pack -> pack_predefined_data / MEMCPY,
+ * opal/datatype/opal_datatype_pack.h:24-76).  Used as the timed CPU baseline. */
+void oracle_ddt_pack_runs(const oracle_ddt_t *d, int64_t count, const void *base, void *dst)
+{
+    char *o = (char *)dst;
+    const char *b = (const char *)base;
+    for (int64_t k = 0; k < count; ++k)
+        for (int64_t j = 0; j < d->nblk; ++j)
+            for (int r = 0; r < d->nruns; ++r) {
+                memcpy(o, b + k * d->extent + j * d->stride + d->disp[r], (size_t)d->len[r]);
+                o += d->len[r];
+            }
+}

@@ -63,6 +63,13 @@ enum oracle_allreduce_alg {
 int oracle_allreduce(int alg, int n, size_t count, int type, int op, uint32_t segsize,
                      const void *const *sbufs, void *const *rbufs);
 
+/* The reference's CPU allreduce (segmented ring over sm-BTL-style 32 KiB shared-memory fragments)
+ * run by n concurrent ranks (threads pinned to cores core0..core0+n-1; core0 < 0: unpinned);
+ * 1 warm-up + reps timed calls, *sec_per_call = slowest rank's time per call.  segsize 0 = ring.
+ * cpu_ring.c; its results equal oracle_allreduce(RING_SEGMENTED / RING). */
+int oracle_cpu_allreduce(int n, size_t count, int type, int op, uint32_t segsize, const void *const *sbufs,
+                         void *const *rbufs, int reps, int core0, double *sec_per_call);
+
 /* The algorithm ompi_coll_tuned_allreduce_intra_dec_fixed picks (decision_fixed.c:42-85). */
 int oracle_allreduce_decision(int n, size_t count, int type, uint32_t *segsize_out);
 
@@ -110,6 +117,7 @@ int oracle_ddt_unpack(const oracle_ddt_t *d, int64_t count, void *base, int64_t 
 unsigned long oracle_uicsum_partial(const void *source, size_t csumlen, unsigned int *lastPartialInt,
                                     size_t *lastPartialLength);
 uint32_t oracle_ddt_pack_checksum(const oracle_ddt_t *d, int64_t count, const void *base, void *dst);
+void oracle_ddt_pack_runs(const oracle_ddt_t *d, int64_t count, const void *base, void *dst);
 
 /* Expression-order description of the allreduce fold actually applied to element `index`:
  * writes the rank fold order into order[0..n-1] for ring / segmented ring (acc starts at

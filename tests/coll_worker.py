@@ -13,6 +13,59 @@ sys.path.insert(0, str(pathlib.Path(__file__).parent))
 from conftest import load_oracle  # noqa: E402
 from mini import mini  # noqa: E402
 import opdata  # noqa: E402
+from ddtcases import OPAL_FLOAT4, opal_strided_elems, opal_vector  # noqa: E402
+
+
+SENT = 0xA5
+
+
+def derived_bcast(m, comm, oracle, rank, size, torch):
+    nblk, count = 1000, 2
+    desc, used, tsize, lb, ub = opal_vector(nblk, 256, 512)  # vector(1000, 64, 128, MPI_FLOAT)
+    dt = m.derived(desc, used, tsize, lb, ub)
+    od = oracle.oracle_ddt_vector(nblk, 64, 128, 4)
+    span = (count - 1) * (ub - lb) + ub
+    root = size - 1
+    rootbuf = np.random.default_rng(77).integers(0, 256, span, dtype=np.uint8)
+    mine = rootbuf.copy() if rank == root else np.full(span, SENT, dtype=np.uint8)
+    want = rootbuf.copy()
+    if rank != root:  # expected: the type map's bytes from the root, the gaps untouched
+        packed = np.zeros(count * tsize, dtype=np.uint8)
+        oracle.oracle_ddt_pack(od, count, rootbuf.ctypes.data, 0, packed.ctypes.data, count * tsize)
+        want = np.full(span, SENT, dtype=np.uint8)
+        oracle.oracle_ddt_unpack(od, count, want.ctypes.data, 0, packed.ctypes.data, count * tsize)
+    d = torch.from_numpy(mine).cuda()
+    torch.cuda.synchronize()
+    assert m.lib.mini_bcast(comm, d.data_ptr(), count, dt, root) == 0
+    assert np.array_equal(d.cpu().numpy(), want), "derived bcast"
+    m.lib.mini_datatype_destroy(dt)
+    oracle.oracle_ddt_free(od)
+
+
+def derived_allgather(m, comm, oracle, rank, size, torch):
+    n = 300
+    # rdtype = vector(300, 1, 2, MPI_FLOAT): one strided ELEM record
+    desc, used, tsize, lb, ub = opal_strided_elems(n, OPAL_FLOAT4, 4, 8)
+    rdt = m.derived(desc, used, tsize, lb, ub)
+    ext = ub - lb
+    od = oracle.oracle_ddt_vector(n, 1, 2, 4)
+    fdt = m.dtype_for_slot(m.pkg.T["FLOAT"])
+    contrib = [np.arange(n, dtype=np.float32) + 1000 * r for r in range(size)]
+    want = np.full(size * ext, SENT, dtype=np.uint8)
+    for r in range(size):
+        oracle.oracle_ddt_unpack(od, 1, want.ctypes.data + r * ext, 0, contrib[r].ctypes.data, n * 4)
+    for inplace in (False, True):
+        rb = np.full(size * ext, SENT, dtype=np.uint8)
+        if inplace:  # my block already sits in rbuf, laid out by rdtype
+            oracle.oracle_ddt_unpack(od, 1, rb.ctypes.data + rank * ext, 0, contrib[rank].ctypes.data, n * 4)
+        drb = torch.from_numpy(rb).cuda()
+        dsb = torch.from_numpy(contrib[rank].copy()).cuda()
+        torch.cuda.synchronize()
+        sp = 1 if inplace else dsb.data_ptr()  # MPI_IN_PLACE == (void *)1
+        assert m.lib.mini_allgather(comm, sp, n, fdt, drb.data_ptr(), 1, rdt) == 0
+        assert np.array_equal(drb.cpu().numpy(), want), f"derived allgather inplace={inplace}"
+    m.lib.mini_datatype_destroy(rdt)
+    oracle.oracle_ddt_free(od)
 
 
 def main():
@@ -66,6 +119,9 @@ def main():
     torch.cuda.synchronize()
     assert m.lib.mini_bcast(comm, buf.data_ptr(), n, fdt, size - 1) == 0
     assert bool((buf == size - 1).all())
+    # derived datatypes through the GPU convertor: bcast of a vector type ...
+    derived_bcast(m, comm, oracle, rank, size, torch)
+    derived_allgather(m, comm, oracle, rank, size, torch)
     # host buffers -> the lower-priority (stub) module
     h = np.zeros(16, dtype=np.float32)
     op = m.select_op(pkg.OP["SUM"])

@@ -52,6 +52,8 @@ def load_oracle() -> ctypes.CDLL:
         lib.oracle_op_3buff.argtypes = [i, i, vp, vp, vp, sz]
         lib.oracle_op_3buff_mt.argtypes = [i, i, vp, vp, vp, sz, i]
         lib.oracle_allreduce.argtypes = [i, i, sz, i, i, c.c_uint32, c.POINTER(vp), c.POINTER(vp)]
+        lib.oracle_cpu_allreduce.argtypes = [i, sz, i, i, c.c_uint32, c.POINTER(vp), c.POINTER(vp), i, i,
+                                             c.POINTER(c.c_double)]
         lib.oracle_allreduce_decision.argtypes = [i, sz, i, c.POINTER(c.c_uint32)]
         lib.oracle_reduce.argtypes = [i, i, i, sz, i, i, c.c_uint32, c.POINTER(vp), vp]
         lib.oracle_reduce_decision.argtypes = [i, sz, i, c.POINTER(c.c_uint32)]
@@ -79,6 +81,7 @@ def load_oracle() -> ctypes.CDLL:
         lib.oracle_uicsum_partial.argtypes = [vp, sz, c.POINTER(c.c_uint), c.POINTER(sz)]
         lib.oracle_ddt_pack_checksum.restype = c.c_uint32
         lib.oracle_ddt_pack_checksum.argtypes = [vp, i64, vp, vp]
+        lib.oracle_ddt_pack_runs.argtypes = [vp, i64, vp, vp]
         lib.oracle_ompi_fn2.restype = vp
         lib.oracle_ompi_fn2.argtypes = [i, i]
         lib.oracle_ompi_fn3.restype = vp

@@ -41,3 +41,35 @@ def ldi_struct(oracle):
 
 
 LDI = np.dtype([("ld", np.longdouble), ("i", "<i4")], align=True)
+
+
+# ---- opal description records (dt_elem_desc_t, 32 bytes each; opal_datatype_internal.h:148-188)
+import struct  # noqa: E402
+
+OPAL_UINT1, OPAL_INT4, OPAL_FLOAT4 = 9, 6, 15
+
+
+def rec_loop(loops, items, extent):
+    return struct.pack("<HHII4xQq", 0, 0, loops, items, 0, extent)
+
+
+def rec_elem(typ, count, extent, disp):
+    return struct.pack("<HHII4xqq", 0x0100, typ, count, 1, extent, disp)
+
+
+def rec_end(items, size, first):
+    return struct.pack("<HHII4xQq", 0, 1, items, 0, size, first)
+
+
+def opal_vector(nblk, block_bytes, stride_bytes):
+    """optimized description of a vector of byte-granular blocks: LOOP nblk x {UINT1 x block}
+    extent stride (what opal_datatype_optimize_short leaves for vector(n, 64, 128, MPI_FLOAT),
+    SURVEY.md §0).  Returns (desc, used, size, lb, ub)."""
+    desc = rec_loop(nblk, 2, stride_bytes) + rec_elem(OPAL_UINT1, block_bytes, 1, 0) + rec_end(2, block_bytes, 0)
+    return desc, 3, nblk * block_bytes, 0, (nblk - 1) * stride_bytes + block_bytes
+
+
+def opal_strided_elems(n, elem_type, elem_size, stride_bytes, disp=0):
+    """one ELEM record of n strided basic elements (extent != size): e.g. vector(n, 1, 2, MPI_FLOAT)"""
+    desc = rec_elem(elem_type, n, stride_bytes, disp)
+    return desc, 1, n * elem_size, disp, disp + (n - 1) * stride_bytes + elem_size

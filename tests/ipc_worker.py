@@ -17,6 +17,29 @@ from conftest import load_oracle, load_pkg  # noqa: E402
 import opdata  # noqa: E402
 
 
+def realloc_same_address(pkg, comm, rank, size):
+    """free + hipMalloc usually returns the same address: the registration caches must notice the
+    new allocation (buffer id) instead of reusing the stale IPC mapping"""
+    lib = pkg.rt()
+    n = 1 << 18
+    nbytes = n * 4
+    addrs = []
+    for gen in range(3):
+        p = ctypes.c_void_p()
+        assert lib.mi355x_malloc(ctypes.byref(p), nbytes) == 0
+        addrs.append(p.value)
+        host = np.full(n, float(rank + 1 + 10 * gen), dtype=np.float32)
+        assert lib.mi355x_memcpy(p, host.ctypes.data, nbytes) == 0
+        comm.allreduce(None, p.value, n, pkg.T["FLOAT"], pkg.OP["SUM"])  # MPI_IN_PLACE
+        out = np.empty(n, dtype=np.float32)
+        assert lib.mi355x_memcpy(out.ctypes.data, p, nbytes) == 0
+        want = sum(r + 1 + 10 * gen for r in range(size))
+        assert np.all(out == want), (gen, out[:4], want)
+        comm.barrier()  # every rank is done with the peers' allocations before they are freed
+        assert lib.mi355x_free(p) == 0
+    print(f"rank {rank} realloc addresses {'same' if len(set(addrs)) == 1 else 'differ'}", flush=True)
+
+
 def main():
     key, rank, size, dev = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
     import torch
@@ -50,6 +73,7 @@ def main():
     comm.allgather(src.data_ptr(), dst.data_ptr(), nb)
     for r in range(size):
         assert int(dst[r * nb:(r + 1) * nb].min()) == r + 1
+    realloc_same_address(pkg, comm, rank, size)
     comm.barrier()
     comm.destroy()
     print(f"rank {rank} OK", flush=True)

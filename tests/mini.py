@@ -55,6 +55,10 @@ class Mini:
         L.mini_stub_calls.argtypes = [i]
         L.mini_offsetof.restype = ctypes.c_size_t
         L.mini_offsetof.argtypes = [i]
+        L.mini_datatype_create_raw.restype = vp
+        L.mini_datatype_create_raw.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_size_t] + \
+            [ctypes.c_ssize_t] * 4 + [ctypes.c_uint16]
+        L.mini_datatype_destroy.argtypes = [vp]
         L.mini_init()
 
     def addr(self, lib, sym):
@@ -66,6 +70,10 @@ class Mini:
     def dtype_for_slot(self, slot):
         did = self.lib.mini_datatype_id_for_slot(slot)
         return None if did < 0 else self.lib.mini_datatype(did)
+
+    def derived(self, desc, used, size, lb, ub):
+        """a committed derived datatype (not predefined, with gaps) from an opal description"""
+        return self.lib.mini_datatype_create_raw(desc, used, size, lb, ub, lb, ub, 0)
 
     def install_oracle_base(self, oracle):
         """op/base's CPU loops in the harness = the oracle's reference-signature thunks"""

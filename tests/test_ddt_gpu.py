@@ -89,11 +89,25 @@ def test_checksum_gpu(gpu, pkg, oracle):
     assert tot & 0xFFFFFFFF == want
 
 
-@pytest.mark.parametrize("kind", ["vector", "indexed", "struct", "vector_odd"])
+KINDS = ["vector", "indexed", "struct", "vector_odd", "vector_rows", "gapped_rows"]
+
+
+@pytest.mark.parametrize("kind", KINDS)
 def test_random_windows(gpu, pkg, oracle, kind):
+    """random fragment windows; the *_rows kinds keep every window 16-B aligned so the row
+    kernel (one run per block) takes them, the others exercise the general kernel"""
     torch = gpu
-    rng = np.random.default_rng(["vector", "indexed", "struct", "vector_odd"].index(kind) + 5)
-    if kind == "vector":
+    rng = np.random.default_rng(KINDS.index(kind) + 5)
+    align = 16 if kind.endswith("rows") else 1
+    if kind == "vector_rows":
+        count, args = 3, (1001, 32, 48, 4)
+        d, od = pkg.Ddt.vector(*args), oracle.oracle_ddt_vector(*args)
+    elif kind == "gapped_rows":  # one run of 48 B at disp 16 in a 96-B extent, count 700
+        count = 700
+        d = pkg.Ddt.runs([16], [48], extent=96)
+        i64 = ctypes.c_int64 * 1
+        od = oracle.oracle_ddt_struct(1, i64(16), i64(48), i64(8), 96)
+    elif kind == "vector":
         count, args = 3, (97, 64, 128, 4)
         d, od = pkg.Ddt.vector(*args), oracle.oracle_ddt_vector(*args)
     elif kind == "vector_odd":
@@ -117,7 +131,7 @@ def test_random_windows(gpu, pkg, oracle, kind):
     dbase = _dev(torch, base)
     full = np.zeros(total, dtype=np.uint8)
     oracle.oracle_ddt_pack(od, count, base.ctypes.data, 0, full.ctypes.data, total)
-    cuts = sorted(set([0, total] + [int(x) for x in rng.integers(0, total, 9)]))
+    cuts = sorted(set([0, total] + [int(x) // align * align for x in rng.integers(0, total, 9)]))
     out = torch.zeros(total + 64, dtype=torch.uint8, device="cuda")
     for a, b in zip(cuts[:-1], cuts[1:]):
         d.pack(count, dbase.data_ptr(), a, out.data_ptr() + a, b - a)
@@ -129,6 +143,21 @@ def test_random_windows(gpu, pkg, oracle, kind):
     want = np.zeros(span, dtype=np.uint8)
     oracle.oracle_ddt_unpack(od, count, want.ctypes.data, 0, full.ctypes.data, total)
     assert np.array_equal(z.cpu().numpy(), want)
+
+
+def test_row_kernel_checksum(gpu, pkg, oracle):
+    torch = gpu
+    args = (5000, 64, 128, 4)
+    d, od = pkg.Ddt.vector(*args), oracle.oracle_ddt_vector(*args)
+    data = np.random.default_rng(8).integers(0, 2**32, 5000 * 128, dtype=np.uint32)
+    packed = np.zeros(5000 * 64, dtype=np.uint32)
+    want = oracle.oracle_ddt_pack_checksum(od, 1, data.ctypes.data, packed.ctypes.data)
+    dd = _dev(torch, data)
+    dp = torch.zeros(d.size, dtype=torch.uint8, device="cuda")
+    assert d.pack(1, dd.data_ptr(), 0, dp.data_ptr(), d.size, checksum=True) == want
+    assert np.array_equal(dp.cpu().numpy().view(np.uint32), packed)
+    out = torch.zeros_like(dd)
+    assert d.unpack(1, out.data_ptr(), 0, dp.data_ptr(), d.size, checksum=True) == want
 
 
 def test_config5_vector_1gib(gpu, pkg):

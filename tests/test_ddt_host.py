@@ -4,9 +4,10 @@ opal_datatype_internal.h:148-188) compiles to the same layout as the constructor
 from __future__ import annotations
 
 import ctypes
-import struct
 
 import pytest
+
+from ddtcases import rec_elem, rec_end, rec_loop
 
 
 @pytest.mark.parametrize("count,blocklen,stride,elem", [(4, 64, 128, 4), (150, 1, 2, 4), (7, 3, 3, 8), (1, 5, 9, 2),
@@ -28,29 +29,17 @@ def test_indexed_merges_adjacent(pkg, oracle):
     assert d.nruns == 2
 
 
-def _rec_loop(loops, items, extent):
-    return struct.pack("<HHII4xQq", 0, 0, loops, items, 0, extent)
-
-
-def _rec_elem(typ, count, extent, disp):
-    return struct.pack("<HHII4xqq", 0x0100, typ, count, 1, extent, disp)
-
-
-def _rec_end(items, size, first):
-    return struct.pack("<HHII4xQq", 0, 1, items, 0, size, first)
-
-
 def test_from_opal_vector_description(pkg):
     """'LOOP n x {UINT1 count 256} extent 512' -- the optimized description of
     vector(n, 64, 128, MPI_FLOAT)"""
     n = 4
-    desc = _rec_loop(n, 2, 512) + _rec_elem(9, 256, 1, 0) + _rec_end(2, 256, 0)
+    desc = rec_loop(n, 2, 512) + rec_elem(9, 256, 1, 0) + rec_end(2, 256, 0)
     sizes = [0] * 32
     sizes[9] = 1  # OPAL_DATATYPE_UINT1
     d = pkg.Ddt.from_opal(desc, 3, (n - 1) * 512 + 256, sizes)
     assert d.size == n * 256 and d.nruns == 1
     # a strided element (extent != size) unrolls into one run per element
-    desc2 = _rec_elem(6, 5, 8, 4)  # INT4 x5 every 8 bytes starting at 4
+    desc2 = rec_elem(6, 5, 8, 4)  # INT4 x5 every 8 bytes starting at 4
     sizes[6] = 4
     d2 = pkg.Ddt.from_opal(desc2, 1, 40, sizes)
     assert d2.size == 20 and d2.nruns == 5
