@@ -149,6 +149,10 @@ int mi355x_ddt_destroy(mi355x_ddt_t *d);
 size_t mi355x_ddt_size(const mi355x_ddt_t *d);
 int64_t mi355x_ddt_extent(const mi355x_ddt_t *d);
 int mi355x_ddt_nruns(const mi355x_ddt_t *d);
+/* launch shape of the single-run (row) pack/unpack kernel: 16-B slots per lane for pack and for
+ * unpack (2/4/8; 0 keeps), threads per block (256/512/1024; 0 keeps), nontemporal -2 keep,
+ * -1 auto (non-temporal above 256 MiB moved), 0..3 mask (1 = loads, 2 = stores) */
+int mi355x_ddt_tune(int unroll_pack, int unroll_unpack, int threads, int nontemporal);
 /* pack packed bytes [pos, pos+bytes) of `count` instances at device `base` into `dst`
  * (replaces opal_convertor_set_position + opal_convertor_pack on a CUDA convertor,
  * opal_convertor.c:223-330 / opal_datatype_cuda.c:93-115).  checksum (may be NULL) receives the

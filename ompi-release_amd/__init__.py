@@ -118,6 +118,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "mi355x_ddt_size": (sz, [vp]),
         "mi355x_ddt_extent": (c.c_int64, [vp]),
         "mi355x_ddt_nruns": (i, [vp]),
+        "mi355x_ddt_tune": (i, [i, i, i, i]),
         "mi355x_pack": (i, [vp, sz, vp, sz, vp, sz, c.POINTER(c.c_uint32), vp]),
         "mi355x_unpack": (i, [vp, sz, vp, sz, vp, sz, c.POINTER(c.c_uint32), vp]),
     }
@@ -305,6 +306,11 @@ class Ddt:
         if self.h:
             rt().mi355x_ddt_destroy(self.h)
             self.h = None
+
+
+def ddt_tune(unroll_pack: int = 0, unroll_unpack: int = 0, threads: int = 0, nontemporal: int = -2) -> None:
+    """launch shape of the single-run pack/unpack kernel (see mi355x_ddt_tune)"""
+    check(rt().mi355x_ddt_tune(unroll_pack, unroll_unpack, threads, nontemporal), "mi355x_ddt_tune")
 
 
 def sched_program(kind: int, n: int, alg: int, block: int) -> list[int]:

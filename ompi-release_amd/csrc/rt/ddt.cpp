@@ -235,10 +235,7 @@ static int ddt_move(const mi355x_ddt_t *d, bool pack, size_t count, void *mem, s
     dv.blk_bytes = blk_bytes(d);
     dv.inst_bytes = inst;
     unsigned *dsum = nullptr;
-    if (checksum) {
-        MI_HIP(hipMallocAsync((void **)&dsum, sizeof(unsigned), s));
-        MI_HIP(hipMemsetAsync(dsum, 0, sizeof(unsigned), s));
-    }
+    if (checksum) MI_HIP(hipMallocAsync((void **)&dsum, sizeof(unsigned), s));
     int rc = 1;
     if (d->disp.size() == 1)
         rc = launch_ddt_rows(dv, 1, d->disp[0], d->len[0], pack, mem, packed, (int64_t)pos, (int64_t)bytes, dsum, s);
@@ -251,6 +248,21 @@ static int ddt_move(const mi355x_ddt_t *d, bool pack, size_t count, void *mem, s
         MI_HIP(hipStreamSynchronize(s));
         *checksum = h;
     }
+    return MI355X_SUCCESS;
+}
+
+int mi355x_ddt_tune(int unroll_pack, int unroll_unpack, int threads, int nontemporal)
+{
+    auto ok_u = [](int u) { return u == 0 || u == 2 || u == 4 || u == 8; };
+    if (!ok_u(unroll_pack) || !ok_u(unroll_unpack)) return set_error(MI355X_ERR_ARG, "unroll must be 2, 4 or 8");
+    if (threads != 0 && threads != 256 && threads != 512 && threads != 1024)
+        return set_error(MI355X_ERR_ARG, "threads must be 256, 512 or 1024");
+    if (nontemporal < -2 || nontemporal > 3) return set_error(MI355X_ERR_ARG, "nontemporal must be -2..3");
+    DdtTune &t = ddt_tune();
+    if (unroll_pack) t.unroll_pack = unroll_pack;
+    if (unroll_unpack) t.unroll_unpack = unroll_unpack;
+    if (threads) t.threads = threads;
+    if (nontemporal != -2) t.nontemporal = nontemporal;
     return MI355X_SUCCESS;
 }
 

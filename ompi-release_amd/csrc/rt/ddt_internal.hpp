@@ -16,6 +16,17 @@ struct DdtDev {
     int64_t blk_bytes, inst_bytes;
 };
 
+// launch shape of the row kernel: slots per lane (2, 4, 8) and the non-temporal mask
+// (-1 auto: kDdtAutoNT above 256 MiB of traffic; else 1 = loads, 2 = stores)
+constexpr int kDdtAutoNT = 3;
+struct DdtTune {
+    int unroll_pack = 4;
+    int unroll_unpack = 2;
+    int threads = 256;
+    int nontemporal = -1;
+};
+DdtTune &ddt_tune();
+
 int launch_ddt(const DdtDev &d, bool pack, void *mem, void *packed, int64_t pos, int64_t bytes, unsigned *csum,
                hipStream_t s);
 // the row kernel (one run per block, 16-B aligned); returns 1 when it does not apply

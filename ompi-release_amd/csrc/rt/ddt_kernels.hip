@@ -46,6 +46,36 @@ __device__ __forceinline__ Where locate(const DdtDev &d, int64_t p)
     return w;
 }
 
+// checksum: every block stores its partial sum (waves reduced by shuffles, then through LDS);
+// k_csum_finish adds the partials -- no atomics on one hot word
+__device__ __forceinline__ void block_sum_store(unsigned acc, unsigned *partial)
+{
+    __shared__ unsigned ws[16];
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned t = 0;
+        for (unsigned i = 0; i < (blockDim.x + 63) / 64; ++i) t += ws[i];
+        partial[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_csum_finish(const unsigned *partial, unsigned n, unsigned *out)
+{
+    unsigned acc = 0;
+    for (unsigned i = threadIdx.x; i < n; i += blockDim.x) acc += partial[i];
+    __shared__ unsigned ws[16];
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned t = 0;
+        for (unsigned i = 0; i < (blockDim.x + 63) / 64; ++i) t += ws[i];
+        *out = t;
+    }
+}
+
 template <bool PACK, bool CSUM>
 __global__ __launch_bounds__(256) void k_ddt(DdtDev d, char *mem, char *packed, int64_t pos, int64_t bytes,
                                              unsigned *csum)
@@ -89,11 +119,7 @@ __global__ __launch_bounds__(256) void k_ddt(DdtDev d, char *mem, char *packed, 
             }
         }
     }
-    if constexpr (CSUM) {
-        // wave reduction then one atomic per wave (sum mod 2^32)
-        for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
-        if ((threadIdx.x & 63) == 0) atomicAdd(csum, acc);
-    }
+    if constexpr (CSUM) block_sum_store(acc, csum);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -133,8 +159,8 @@ struct RowArgs {
     uint32_t nslots;
 };
 
-template <bool PACK, bool CSUM, bool NT, int U>
-__global__ __launch_bounds__(256) void k_ddt_rows(RowArgs a, unsigned *csum)
+template <bool PACK, bool CSUM, int NTM, int U>
+__global__ __launch_bounds__(1024) void k_ddt_rows(RowArgs a, unsigned *csum)
 {
     const uint32_t tpb = blockDim.x;
     const uint32_t base = blockIdx.x * (tpb * U) + threadIdx.x;
@@ -153,7 +179,7 @@ __global__ __launch_bounds__(256) void k_ddt_rows(RowArgs a, unsigned *csum)
             const uint32_t j = g - k * a.per_inst.d;
             mp[u] = a.mem + (int64_t)k * a.extent + (int64_t)j * a.stride + a.disp + ((int64_t)w << 4);
             const u32x4d *src = reinterpret_cast<const u32x4d *>(PACK ? mp[u] : a.packed + ((size_t)i << 4));
-            if constexpr (NT) v[u] = __builtin_nontemporal_load(src);
+            if constexpr ((NTM & 1) != 0) v[u] = __builtin_nontemporal_load(src);
             else v[u] = *src;
         }
     }
@@ -161,15 +187,12 @@ __global__ __launch_bounds__(256) void k_ddt_rows(RowArgs a, unsigned *csum)
     for (int u = 0; u < U; ++u) {
         if (mp[u]) {
             u32x4d *dst = reinterpret_cast<u32x4d *>(PACK ? a.packed + ((size_t)(base + (uint32_t)u * tpb) << 4) : mp[u]);
-            if constexpr (NT) __builtin_nontemporal_store(v[u], dst);
+            if constexpr ((NTM & 2) != 0) __builtin_nontemporal_store(v[u], dst);
             else *dst = v[u];
             if constexpr (CSUM) acc += v[u].x + v[u].y + v[u].z + v[u].w;
         }
     }
-    if constexpr (CSUM) {
-        for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
-        if ((threadIdx.x & 63) == 0) atomicAdd(csum, acc);
-    }
+    if constexpr (CSUM) block_sum_store(acc, csum);
 }
 
 // the row kernel applies: one run per block, every address and the window 16-B aligned, and
@@ -186,13 +209,51 @@ static bool rows_apply(const DdtDev &d, int nruns_host, int64_t run_disp, int64_
            (run_len >> 4) < ((int64_t)1 << 32);
 }
 
-template <bool PACK, bool CSUM>
-static void launch_rows(const RowArgs &a, bool nt, unsigned *csum, hipStream_t s)
+DdtTune &ddt_tune()
 {
-    constexpr int U = 4;
-    const unsigned blocks = (unsigned)((a.nslots + 256u * U - 1) / (256u * U));
-    if (nt) hipLaunchKernelGGL((k_ddt_rows<PACK, CSUM, true, U>), dim3(blocks), dim3(256), 0, s, a, csum);
-    else hipLaunchKernelGGL((k_ddt_rows<PACK, CSUM, false, U>), dim3(blocks), dim3(256), 0, s, a, csum);
+    static DdtTune t;
+    return t;
+}
+
+// checksum partials: one word per block, summed by k_csum_finish into *csum
+struct Partials {
+    unsigned *p = nullptr;
+    int get(unsigned *csum, unsigned blocks, hipStream_t s)
+    {
+        if (!csum) return MI355X_SUCCESS;
+        MI_HIP(hipMallocAsync((void **)&p, sizeof(unsigned) * blocks, s));
+        return MI355X_SUCCESS;
+    }
+    int finish(unsigned *csum, unsigned blocks, hipStream_t s)
+    {
+        if (!csum) return MI355X_SUCCESS;
+        hipLaunchKernelGGL(k_csum_finish, dim3(1), dim3(1024), 0, s, p, blocks, csum);
+        MI_HIP(hipGetLastError());
+        MI_HIP(hipFreeAsync(p, s));
+        return MI355X_SUCCESS;
+    }
+};
+
+template <bool PACK, bool CSUM, int NTM>
+static void launch_rows_u(const RowArgs &a, int unroll, unsigned tpb, unsigned blocks, unsigned *part, hipStream_t s)
+{
+    switch (unroll) {
+    case 2: hipLaunchKernelGGL((k_ddt_rows<PACK, CSUM, NTM, 2>), dim3(blocks), dim3(tpb), 0, s, a, part); break;
+    case 8: hipLaunchKernelGGL((k_ddt_rows<PACK, CSUM, NTM, 8>), dim3(blocks), dim3(tpb), 0, s, a, part); break;
+    default: hipLaunchKernelGGL((k_ddt_rows<PACK, CSUM, NTM, 4>), dim3(blocks), dim3(tpb), 0, s, a, part); break;
+    }
+}
+
+template <bool PACK, bool CSUM>
+static void launch_rows(const RowArgs &a, int ntm, int unroll, unsigned tpb, unsigned blocks, unsigned *part,
+                        hipStream_t s)
+{
+    switch (ntm & 3) {
+    case 0: launch_rows_u<PACK, CSUM, 0>(a, unroll, tpb, blocks, part, s); break;
+    case 1: launch_rows_u<PACK, CSUM, 1>(a, unroll, tpb, blocks, part, s); break;
+    case 2: launch_rows_u<PACK, CSUM, 2>(a, unroll, tpb, blocks, part, s); break;
+    default: launch_rows_u<PACK, CSUM, 3>(a, unroll, tpb, blocks, part, s); break;
+    }
 }
 
 int launch_ddt_rows(const DdtDev &d, int nruns_host, int64_t run_disp, int64_t run_len, bool pack, void *mem,
@@ -209,16 +270,26 @@ int launch_ddt_rows(const DdtDev &d, int nruns_host, int64_t run_disp, int64_t r
     a.per_inst = make_fastdiv((uint32_t)d.nblk);
     a.first = (uint32_t)(pos >> 4);
     a.nslots = (uint32_t)(bytes >> 4);
-    const bool nt = 2 * bytes > ((int64_t)256 << 20);  // streaming sizes bypass the caches
+    const DdtTune &t = ddt_tune();
+    int unroll = pack ? t.unroll_pack : t.unroll_unpack;
+    if (unroll != 2 && unroll != 8) unroll = 4;
+    const unsigned tpb = (t.threads == 256 || t.threads == 512) ? (unsigned)t.threads : 1024u;
+    int ntm = t.nontemporal;
+    if (ntm < 0) ntm = (2 * bytes > ((int64_t)256 << 20)) ? kDdtAutoNT : 0;  // streaming sizes
+    const uint64_t per = (uint64_t)tpb * (uint64_t)unroll;
+    const unsigned blocks = (unsigned)((a.nslots + per - 1) / per);
+    Partials part;
+    int rc = part.get(csum, blocks, s);
+    if (rc) return rc;
     if (pack) {
-        if (csum) launch_rows<true, true>(a, nt, csum, s);
-        else launch_rows<true, false>(a, nt, csum, s);
+        if (csum) launch_rows<true, true>(a, ntm, unroll, tpb, blocks, part.p, s);
+        else launch_rows<true, false>(a, ntm, unroll, tpb, blocks, nullptr, s);
     } else {
-        if (csum) launch_rows<false, true>(a, nt, csum, s);
-        else launch_rows<false, false>(a, nt, csum, s);
+        if (csum) launch_rows<false, true>(a, ntm, unroll, tpb, blocks, part.p, s);
+        else launch_rows<false, false>(a, ntm, unroll, tpb, blocks, nullptr, s);
     }
     MI_HIP(hipGetLastError());
-    return MI355X_SUCCESS;
+    return part.finish(csum, blocks, s);
 }
 
 int launch_ddt(const DdtDev &d, bool pack, void *mem, void *packed, int64_t pos, int64_t bytes, unsigned *csum,
@@ -231,15 +302,19 @@ int launch_ddt(const DdtDev &d, bool pack, void *mem, void *packed, int64_t pos,
     if (blocks > cap) blocks = cap;
     if (blocks == 0) blocks = 1;
     char *m = static_cast<char *>(mem), *pk = static_cast<char *>(packed);
+    Partials part;
+    int rc = part.get(csum, (unsigned)blocks, s);
+    if (rc) return rc;
+    unsigned *pp = part.p;
     if (pack) {
-        if (csum) hipLaunchKernelGGL((k_ddt<true, true>), dim3((unsigned)blocks), dim3(256), 0, s, d, m, pk, pos, bytes, csum);
-        else hipLaunchKernelGGL((k_ddt<true, false>), dim3((unsigned)blocks), dim3(256), 0, s, d, m, pk, pos, bytes, csum);
+        if (csum) hipLaunchKernelGGL((k_ddt<true, true>), dim3((unsigned)blocks), dim3(256), 0, s, d, m, pk, pos, bytes, pp);
+        else hipLaunchKernelGGL((k_ddt<true, false>), dim3((unsigned)blocks), dim3(256), 0, s, d, m, pk, pos, bytes, pp);
     } else {
-        if (csum) hipLaunchKernelGGL((k_ddt<false, true>), dim3((unsigned)blocks), dim3(256), 0, s, d, m, pk, pos, bytes, csum);
-        else hipLaunchKernelGGL((k_ddt<false, false>), dim3((unsigned)blocks), dim3(256), 0, s, d, m, pk, pos, bytes, csum);
+        if (csum) hipLaunchKernelGGL((k_ddt<false, true>), dim3((unsigned)blocks), dim3(256), 0, s, d, m, pk, pos, bytes, pp);
+        else hipLaunchKernelGGL((k_ddt<false, false>), dim3((unsigned)blocks), dim3(256), 0, s, d, m, pk, pos, bytes, pp);
     }
     MI_HIP(hipGetLastError());
-    return MI355X_SUCCESS;
+    return part.finish(csum, (unsigned)blocks, s);
 }
 
 } // namespace mi355x
