@@ -134,22 +134,36 @@ __global__ __launch_bounds__(1024) void k_chunk(StreamArgs args)
     const size_t nvec = args.nvec;
     const size_t tpb = blockDim.x;
     const size_t base = (size_t)blockIdx.x * (tpb * U) + threadIdx.x;
-    V xa[U], xb[U];
+    u32x4 ra[U], rb[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const size_t i = base + (size_t)u * tpb;
         if (i < nvec) {
-            xa[u] = vload<(NTM & 1) != 0>(av + i);
-            xb[u] = vload<(NTM & 1) != 0>(bv + i);
+            if constexpr ((NTM & 1) != 0) {
+                ra[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(av + i));
+                rb[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(bv + i));
+            } else {
+                ra[u] = *reinterpret_cast<const u32x4 *>(av + i);
+                rb[u] = *reinterpret_cast<const u32x4 *>(bv + i);
+            }
         }
+    }
+    // Pin the loaded dwordx4 values (after all loads are issued): without it the byte-element
+    // kernels get their loads re-typed to <16 x i8> and the non-temporal hint is dropped.
+    if constexpr ((NTM & 1) != 0 && sizeof(T) == 1) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) asm volatile("" : "+v"(ra[u]), "+v"(rb[u]));
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const size_t i = base + (size_t)u * tpb;
         if (i < nvec) {
+            V xa[1], xb[1];
+            __builtin_memcpy(&xa[0], &ra[u], 16);
+            __builtin_memcpy(&xb[0], &rb[u], 16);
             V r;
 #pragma unroll
-            for (int j = 0; j < EPV; ++j) r.e[j] = apply<F, THREE>(xa[u].e[j], xb[u].e[j]);
+            for (int j = 0; j < EPV; ++j) r.e[j] = apply<F, THREE>(xa[0].e[j], xb[0].e[j]);
             vstore<(NTM & 2) != 0>(ov + i, r);
         }
     }
