@@ -141,6 +141,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-legs", action="store_true", help="N > 1: skip the other configs' legs")
     args = ap.parse_args()
 
     import torch

@@ -8,6 +8,7 @@ value = busbw = (S / t) * 2 (n - 1) / n with S = 1 GiB and t = max over ranks pe
 """
 from __future__ import annotations
 
+import datetime
 import os
 import time
 
@@ -15,6 +16,107 @@ GIB = 1 << 30
 # MI355X Infinity Fabric: 7 links per GPU, 153.6 GB/s per link (spec, both directions)
 # -> 76.8 GB/s per link per direction.  Ring peak busbw with R concurrent rings = R x 76.8.
 XGMI_LINK_DIR_GBS = 76.8
+
+
+def _timed(dist, torch, fn, reps, warm=1):
+    """max-over-ranks seconds per call of fn (barrier + synchronize around the timed calls)"""
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0])
+
+
+def extra_legs(args, pkg, torch, comm, world, rank, dev):
+    """The other multi-GPU BASELINE configs, measured on the same communicator after the headline
+    (not part of `value`): configs[2] size sweep, configs[3] reduce_scatter_block + allgather fp64
+    (4 GiB per rank), configs[4] 4 GiB bcast and the vector-datatype bcast / allreduce through the
+    GPU convertor.  Every leg checks an exact-integer result."""
+    import torch.distributed as dist
+    legs = {}
+    f32, f64, SUM = pkg.T["FLOAT"], pkg.T["DOUBLE"], pkg.OP["SUM"]
+    want = world * (world + 1) / 2
+    # configs[2]: latency / busbw over message sizes (ring vs recursive-doubling regions)
+    sweep = []
+    for nbytes in (8, 1024, 8192, 65536, 1 << 20, 16 << 20, 256 << 20):
+        cnt = nbytes // 4
+        x = torch.full((cnt,), float(rank + 1), device=dev)
+        y = torch.empty_like(x)
+        sec = _timed(dist, torch, lambda: comm.allreduce(x.data_ptr(), y.data_ptr(), cnt, f32, SUM),
+                     20 if nbytes <= (1 << 20) else 5, 2)
+        sweep.append({"bytes": nbytes, "us": round(sec * 1e6, 2), "alg": comm.last_algorithm(),
+                      "busbw_GBs": round(nbytes / sec * 2 * (world - 1) / world / 1e9, 3),
+                      "exact": bool(torch.all(y == want).item())})
+        del x, y
+    legs["allreduce_sweep_f32"] = sweep
+    # configs[3]: reduce_scatter_block + allgather, fp64, 4 GiB per rank
+    total = (4 << 30) // 8
+    rcount = total // world
+    x = torch.full((rcount * world,), float(rank + 1), dtype=torch.float64, device=dev)
+    r = torch.empty((rcount,), dtype=torch.float64, device=dev)
+    g = torch.empty((rcount * world,), dtype=torch.float64, device=dev)
+    S = rcount * world * 8
+    t_rs = _timed(dist, torch, lambda: comm.reduce_scatter_block(x.data_ptr(), r.data_ptr(), rcount, f64, SUM), 3)
+    ok_rs = bool(torch.all(r == want).item())
+    t_ag = _timed(dist, torch, lambda: comm.allgather(r.data_ptr(), g.data_ptr(), rcount * 8), 3)
+    ok_ag = bool(torch.all(g == want).item())
+    legs["rsb_allgather_f64_4GiB"] = {
+        "rsb_ms": round(t_rs * 1e3, 3), "rsb_busbw_GBs": round(S / t_rs * (world - 1) / world / 1e9, 2),
+        "rsb_alg": comm.last_algorithm(), "allgather_ms": round(t_ag * 1e3, 3),
+        "allgather_busbw_GBs": round(S / t_ag * (world - 1) / world / 1e9, 2), "exact": ok_rs and ok_ag}
+    del r, g
+    # configs[4]: 4 GiB bcast (as MPI_FLOAT count 2^30), root 0
+    xb = x.view(torch.uint8)
+    nb = xb.numel()
+    if rank != 0:
+        x.zero_()
+    torch.cuda.synchronize()
+    t_b = _timed(dist, torch, lambda: comm.bcast(xb.data_ptr(), nb, 0), 3)
+    ok_b = bool(torch.all(x == 1.0).item())
+    legs["bcast_4GiB"] = {"ms": round(t_b * 1e3, 3), "busbw_GBs": round(nb / t_b / 1e9, 2), "exact": ok_b}
+    del x, xb
+    # configs[4]: vector(2^22, 64, 128, MPI_FLOAT) over a 2 GiB extent: root packs, 1 GiB packed
+    # bytes broadcast, the others unpack (what coll/mi355x does for a derived datatype)
+    nblk = 1 << 22
+    d = pkg.Ddt.vector(nblk, 64, 128, 4)
+    buf = torch.full((nblk, 128), float(rank + 1), device=dev)
+    packed = torch.empty((nblk, 64), device=dev)
+
+    def vbcast():
+        if rank == 0:
+            d.pack(1, buf.data_ptr(), 0, packed.data_ptr(), d.size)
+        comm.bcast(packed.data_ptr(), d.size, 0)
+        if rank != 0:
+            d.unpack(1, buf.data_ptr(), 0, packed.data_ptr(), d.size)
+    t_vb = _timed(dist, torch, vbcast, 3)
+    ok_vb = bool(torch.all(buf[:, :64] == 1.0).item()) and bool(torch.all(buf[:, 64:] == rank + 1).item())
+    legs["bcast_vector_1GiB_packed"] = {"ms": round(t_vb * 1e3, 3), "busbw_GBs": round(d.size / t_vb / 1e9, 2),
+                                        "exact": ok_vb}
+    # MPI_Allreduce of the vector's elements: pack -> contiguous allreduce -> unpack (the reference
+    # rejects an intrinsic op on a derived type, op.h:490-501, so this is the parity definition)
+    buf.fill_(float(rank + 1))
+    red = torch.empty_like(packed)
+
+    def vallreduce():
+        d.pack(1, buf.data_ptr(), 0, packed.data_ptr(), d.size)
+        comm.allreduce(packed.data_ptr(), red.data_ptr(), nblk * 64, f32, SUM)
+        d.unpack(1, buf.data_ptr(), 0, red.data_ptr(), d.size)
+    t_va = _timed(dist, torch, vallreduce, 1, 0)
+    ok_va = bool(torch.all(buf[:, :64] == want).item()) and bool(torch.all(buf[:, 64:] == rank + 1).item())
+    t_va = _timed(dist, torch, vallreduce, 3, 0)
+    legs["allreduce_vector_1GiB_packed"] = {
+        "ms": round(t_va * 1e3, 3), "busbw_GBs": round(d.size / t_va * 2 * (world - 1) / world / 1e9, 2),
+        "exact": ok_va}
+    del buf, packed, red
+    d.destroy()
+    torch.cuda.empty_cache()
+    return legs
 
 
 def run(args, pkg, torch):
@@ -28,9 +130,11 @@ def run(args, pkg, torch):
     local = local % max(1, torch.cuda.device_count())  # one-GPU rehearsal: ranks share device 0
     torch.cuda.set_device(local)
     if not dist.is_initialized():
-        dist.init_process_group("gloo")
+        # bounded waits: a failing rank surfaces as an error on the others, not a hang
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
     key = "bench_{}_{}".format(os.environ.get("TORCHELASTIC_RUN_ID", "x"), os.environ.get("MASTER_PORT", "0"))
     comm = pkg.Comm.create(key, rank, world, local)
+    comm.set("TIMEOUT_S", 120)
 
     n = GIB // 4
     dev = torch.device("cuda", local)
@@ -77,6 +181,14 @@ def run(args, pkg, torch):
     t = torch.tensor([dt, 0.0 if ok else 1.0], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt, bad = float(t[0]), float(t[1])
+    legs = None
+    if not args.no_legs:
+        del x, y
+        torch.cuda.empty_cache()
+        try:
+            legs = extra_legs(args, pkg, torch, comm, world, rank, dev)
+        except Exception as e:  # a failing extra leg must not hide the headline line
+            legs = {"error": repr(e)[:300]}
     comm.destroy()
     if rank != 0:
         dist.destroy_process_group()
@@ -112,6 +224,7 @@ def run(args, pkg, torch):
                       "frac": None, "traffic": None,
                       "peak_note": "REHEARSAL: all ranks share one GPU, no xGMI traffic; not a valid busbw"}),
         "cpu_baseline": None,
+        "legs": legs,
     }
     dist.destroy_process_group()
     return res
