@@ -9,13 +9,22 @@ value = busbw = (S / t) * 2 (n - 1) / n with S = 1 GiB and t = max over ranks pe
 from __future__ import annotations
 
 import datetime
+import json
 import os
+import threading
+import sys
 import time
 
 GIB = 1 << 30
 # MI355X Infinity Fabric: 7 links per GPU, 153.6 GB/s per link (spec, both directions)
 # -> 76.8 GB/s per link per direction.  Ring peak busbw with R concurrent rings = R x 76.8.
 XGMI_LINK_DIR_GBS = 76.8
+
+
+def _log(rank, msg):
+    """progress on stderr (rank 0), so a long multi-GPU run is visibly alive"""
+    if rank == 0:
+        print(f"[bench_coll {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 def _timed(dist, torch, fn, reps, warm=1):
@@ -33,18 +42,18 @@ def _timed(dist, torch, fn, reps, warm=1):
     return float(t[0])
 
 
-def extra_legs(args, pkg, torch, comm, world, rank, dev):
+def extra_legs(args, pkg, torch, comm, world, rank, dev, legs):
     """The other multi-GPU BASELINE configs, measured on the same communicator after the headline
     (not part of `value`): configs[2] size sweep, configs[3] reduce_scatter_block + allgather fp64
     (4 GiB per rank), configs[4] 4 GiB bcast and the vector-datatype bcast / allreduce through the
     GPU convertor.  Every leg checks an exact-integer result."""
     import torch.distributed as dist
-    legs = {}
     f32, f64, SUM = pkg.T["FLOAT"], pkg.T["DOUBLE"], pkg.OP["SUM"]
     want = world * (world + 1) / 2
     # configs[2]: latency / busbw over message sizes (ring vs recursive-doubling regions)
     sweep = []
     for nbytes in (8, 1024, 8192, 65536, 1 << 20, 16 << 20, 256 << 20):
+        _log(rank, f"leg allreduce_sweep {nbytes} B")
         cnt = nbytes // 4
         x = torch.full((cnt,), float(rank + 1), device=dev)
         y = torch.empty_like(x)
@@ -56,6 +65,7 @@ def extra_legs(args, pkg, torch, comm, world, rank, dev):
         del x, y
     legs["allreduce_sweep_f32"] = sweep
     # configs[3]: reduce_scatter_block + allgather, fp64, 4 GiB per rank
+    _log(rank, "leg rsb_allgather_f64_4GiB")
     total = (4 << 30) // 8
     rcount = total // world
     x = torch.full((rcount * world,), float(rank + 1), dtype=torch.float64, device=dev)
@@ -72,6 +82,7 @@ def extra_legs(args, pkg, torch, comm, world, rank, dev):
         "allgather_busbw_GBs": round(S / t_ag * (world - 1) / world / 1e9, 2), "exact": ok_rs and ok_ag}
     del r, g
     # configs[4]: 4 GiB bcast (as MPI_FLOAT count 2^30), root 0
+    _log(rank, "leg bcast_4GiB")
     xb = x.view(torch.uint8)
     nb = xb.numel()
     if rank != 0:
@@ -83,6 +94,7 @@ def extra_legs(args, pkg, torch, comm, world, rank, dev):
     del x, xb
     # configs[4]: vector(2^22, 64, 128, MPI_FLOAT) over a 2 GiB extent: root packs, 1 GiB packed
     # bytes broadcast, the others unpack (what coll/mi355x does for a derived datatype)
+    _log(rank, "leg bcast_vector")
     nblk = 1 << 22
     d = pkg.Ddt.vector(nblk, 64, 128, 4)
     buf = torch.full((nblk, 128), float(rank + 1), device=dev)
@@ -100,6 +112,7 @@ def extra_legs(args, pkg, torch, comm, world, rank, dev):
                                         "exact": ok_vb}
     # MPI_Allreduce of the vector's elements: pack -> contiguous allreduce -> unpack (the reference
     # rejects an intrinsic op on a derived type, op.h:490-501, so this is the parity definition)
+    _log(rank, "leg allreduce_vector")
     buf.fill_(float(rank + 1))
     red = torch.empty_like(packed)
 
@@ -149,6 +162,7 @@ def run(args, pkg, torch):
     tried = []
     for push in (0, 1):
         for bpc in (2, 4, 8):
+            _log(rank, f"autotune push={push} blocks_per_cu={bpc}")
             comm.set("PUSH", push)
             comm.set("BLOCKS_PER_CU", bpc)
             torch.cuda.synchronize()
@@ -165,6 +179,7 @@ def run(args, pkg, torch):
     comm.set("PUSH", best["push"])
     comm.set("BLOCKS_PER_CU", best["blocks_per_cu"])
     # timed data: N(0,1), order-dependent (the engine replicates the segmented-ring order)
+    _log(rank, f"timed: {args.steps} steps, best {best}")
     x.normal_()
     torch.cuda.synchronize()
     for _ in range(args.warmup):
@@ -181,18 +196,6 @@ def run(args, pkg, torch):
     t = torch.tensor([dt, 0.0 if ok else 1.0], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt, bad = float(t[0]), float(t[1])
-    legs = None
-    if not args.no_legs:
-        del x, y
-        torch.cuda.empty_cache()
-        try:
-            legs = extra_legs(args, pkg, torch, comm, world, rank, dev)
-        except Exception as e:  # a failing extra leg must not hide the headline line
-            legs = {"error": repr(e)[:300]}
-    comm.destroy()
-    if rank != 0:
-        dist.destroy_process_group()
-        return None
     per = dt / args.steps
     busbw = (n * 4 / per) * 2 * (world - 1) / world / 1e9
     peak_all = (world - 1) * XGMI_LINK_DIR_GBS
@@ -224,7 +227,32 @@ def run(args, pkg, torch):
                       "frac": None, "traffic": None,
                       "peak_note": "REHEARSAL: all ranks share one GPU, no xGMI traffic; not a valid busbw"}),
         "cpu_baseline": None,
-        "legs": legs,
+        "legs": None,
     }
+    if not args.no_legs:
+        del x, y
+        torch.cuda.empty_cache()
+        legs = {}
+        # watchdog: a leg that never returns must not take the headline line with it
+        done = threading.Event()
+
+        def watchdog():
+            if not done.wait(args.legs_timeout):
+                if rank == 0:
+                    legs["error"] = f"legs exceeded {args.legs_timeout:.0f} s; partial results above"
+                    res["legs"] = legs
+                    print(json.dumps(res), flush=True)
+                os._exit(0)
+        threading.Thread(target=watchdog, daemon=True).start()
+        try:
+            extra_legs(args, pkg, torch, comm, world, rank, dev, legs)
+        except Exception as e:  # a failing extra leg must not hide the headline line
+            legs["error"] = repr(e)[:300]
+        done.set()
+        res["legs"] = legs
+    comm.destroy()
+    if rank != 0:
+        dist.destroy_process_group()
+        return None
     dist.destroy_process_group()
     return res

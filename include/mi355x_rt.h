@@ -110,7 +110,11 @@ enum mi355x_knob {
     MI355X_KNOB_REDUCE_SCATTER_ALG = 3, /* coll_tuned_reduce_scatter_algorithm */
     MI355X_KNOB_BLOCKS_PER_CU = 4,
     MI355X_KNOB_TIMEOUT_S = 5,
-    MI355X_KNOB_PUSH = 6                /* 1: one-phase push data flow (owners write peers' buffers) */
+    MI355X_KNOB_PUSH = 6,               /* 1: one-phase push data flow (owners write peers' buffers) */
+    MI355X_KNOB_IPC_MAX_BYTES = 7,      /* buffers in allocations of >= this many bytes are never
+                                           exported; calls touching one take the staged data flow
+                                           (default 2^31: hipIpcOpenMemHandle hangs from 2 GiB) */
+    MI355X_KNOB_STAGE_BYTES = 8         /* size of the per-communicator staging buffer (default 1 GiB) */
 };
 int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
 

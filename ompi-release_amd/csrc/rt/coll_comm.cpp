@@ -16,15 +16,24 @@
 // GPU's L2 seeing a remote write.  Allreduce: phase 1 the owner folds its ring block locally,
 // phase 2 every rank pulls the other blocks (one launch, one segment per peer).  A one-phase
 // PUSH variant (owners write into every peer's rbuf) is kept behind MI355X_KNOB_PUSH.
+//
+// Large allocations: hipIpcOpenMemHandle never returns for an allocation of 2 GiB or more on
+// this platform (ROCm 7.2, dmabuf IPC; measured: 2046 MiB maps, 2048 MiB hangs).  A buffer whose
+// allocation is at least `ipc_max` bytes is therefore never exported: the call switches, on every
+// rank (the decision is taken after the exchange, from every rank's descriptors), to the STAGED
+// data flow -- the message moves through each rank's persistent staging buffer (one allocation
+// < 2 GiB, mapped once) in block-strided windows, like the segmented ring's phases.
 #include <fcntl.h>
 #include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <array>
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -38,6 +47,21 @@
 #include "rt_internal.hpp"
 
 namespace mi355x {
+
+// MI355X_DEBUG=1: trace every stage of a collective on stderr (rank, stage, elapsed time)
+static bool debug_on()
+{
+    static const bool on = getenv("MI355X_DEBUG") && atoi(getenv("MI355X_DEBUG")) > 0;
+    return on;
+}
+#define TRACE(c, ...)                                                                          \
+    do {                                                                                       \
+        if (debug_on()) {                                                                      \
+            fprintf(stderr, "[mi355x r%d seq %llu] ", (c)->rank, (unsigned long long)(c)->seq); \
+            fprintf(stderr, __VA_ARGS__);                                                      \
+            fputc('\n', stderr);                                                               \
+        }                                                                                      \
+    } while (0)
 
 CollTune &coll_tune()
 {
@@ -55,6 +79,7 @@ struct BufDesc {
     uint64_t present;  // 0: NULL buffer
     uint64_t base;     // exporter's allocation base (its VA; the peer-map key)
     uint64_t id;       // exporter's allocation id (HIP_POINTER_ATTRIBUTE_BUFFER_ID)
+    uint64_t staged;   // 1: allocation too large to export -> the call takes the staged data flow
 };
 
 struct alignas(64) RankSlot {
@@ -101,6 +126,7 @@ struct LocalReg {
     size_t size;
     uint64_t id;
     hipIpcMemHandle_t h;
+    bool has_h;       // false: too large to export (never passed to hipIpcGetMemHandle)
 };
 
 struct LoopShared {
@@ -122,6 +148,9 @@ struct mi355x_comm {
     std::vector<mi355x::LocalReg> local_regs;
     void *scratch = nullptr;
     size_t scratch_bytes = 0;
+    void *stage = nullptr;                        // staging buffer of the staged data flow
+    size_t stage_bytes = (size_t)1 << 30;         // its size (an allocation below ipc_max)
+    size_t ipc_max = (size_t)1 << 31;             // allocations >= this are never exported
     int knob_allreduce = 0, knob_reduce = 0, knob_rs = 0;
     int last_alg = -1;
     double timeout_s = 600.0;
@@ -170,13 +199,19 @@ static uint64_t buffer_id(const void *p)
     return (uint64_t)id;
 }
 
-static int local_handle(mi355x_comm *c, const void *p, BufDesc *d)
+static int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
 {
     std::memset(d, 0, sizeof(*d));
     if (!p) return MI355X_SUCCESS;
     d->present = 1;
     if (c->loopback) {
         d->raw = (uint64_t)(uintptr_t)p;
+        if (!force) {
+            void *base = nullptr;
+            size_t sz = 0;
+            MI_HIP(hipMemGetAddressRange(&base, &sz, (void *)p));
+            d->staged = sz >= c->ipc_max;
+        }
         return MI355X_SUCCESS;
     }
     const uintptr_t up = (uintptr_t)p;
@@ -184,7 +219,11 @@ static int local_handle(mi355x_comm *c, const void *p, BufDesc *d)
     for (size_t i = 0; i < c->local_regs.size(); ++i) {
         const LocalReg &r = c->local_regs[i];
         if (up >= r.base && up < r.base + r.size) {
-            if (r.id == id && id != 0) {
+            if (r.id == id && id != 0 && (r.has_h || !force)) {
+                if (!force && r.size >= c->ipc_max) {
+                    d->staged = 1;
+                    return MI355X_SUCCESS;
+                }
                 d->h = r.h;
                 d->off = up - r.base;
                 d->base = r.base;
@@ -198,11 +237,21 @@ static int local_handle(mi355x_comm *c, const void *p, BufDesc *d)
     void *base = nullptr;
     size_t sz = 0;
     MI_HIP(hipMemGetAddressRange(&base, &sz, (void *)p));
+    TRACE(c, "register %p: base %p size %zu id %llu", p, base, sz, (unsigned long long)id);
     LocalReg reg;
+    std::memset(&reg, 0, sizeof(reg));
     reg.base = (uintptr_t)base;
     reg.size = sz;
     reg.id = id;
+    if (!force && sz >= c->ipc_max) {
+        // never exported (hipIpcOpenMemHandle hangs on such allocations): staged data flow
+        reg.has_h = false;
+        if (id != 0) c->local_regs.push_back(reg);
+        d->staged = 1;
+        return MI355X_SUCCESS;
+    }
     MI_HIP(hipIpcGetMemHandle(&reg.h, base));
+    reg.has_h = true;
     // without an allocation id the entry cannot be validated later: do not cache it
     if (id != 0) c->local_regs.push_back(reg);
     d->h = reg.h;
@@ -233,7 +282,9 @@ static int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out)
     if (it != c->peer_maps.end()) {
         base = it->second.mapped;
     } else {
+        TRACE(c, "open peer %d base %llx id %llu", peer, (unsigned long long)d.base, (unsigned long long)d.id);
         hipError_t e = hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess);
+        TRACE(c, "opened peer %d -> %p (%s)", peer, base, hipGetErrorString(e));
         if (e != hipSuccess)
             return set_error(MI355X_ERR_PEER, "hipIpcOpenMemHandle(rank %d): %s", peer, hipGetErrorString(e));
         c->peer_maps[key] = PeerMap{d.id, base};
@@ -243,22 +294,28 @@ static int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out)
 }
 
 // Publish nbuf local buffers, meet every rank, and resolve every rank's buffers:
-// peers[b][r] = rank r's buffer b mapped into this process.
+// peers[b][r] = rank r's buffer b mapped into this process.  When any rank published a buffer
+// that cannot be exported, nothing is mapped and *staged is set on every rank alike (callers
+// that pass staged == NULL get an error instead).  force: export regardless of allocation size
+// (the staging buffers themselves).
 static int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t sig[4],
-                    std::vector<std::vector<void *>> &peers)
+                    std::vector<std::vector<void *>> &peers, bool *staged = nullptr, bool force = false)
 {
     c->seq++;
+    if (staged) *staged = false;
     RankSlot &s = c->ctrl->slot[c->rank];
     for (int b = 0; b < nbuf; ++b) {
-        int rc = local_handle(c, mine[b], &s.buf[b]);
+        int rc = local_handle(c, mine[b], &s.buf[b], force);
         if (rc) return rc;
     }
     s.nbuf = nbuf;
     for (int i = 0; i < 4; ++i) s.sig[i] = sig[i];
     s.seq.store(c->seq, std::memory_order_release);
+    TRACE(c, "published %d buffers", nbuf);
     int rc = barrier(c);
+    TRACE(c, "exchange barrier passed (rc %d)", rc);
     if (rc) return rc;
-    peers.assign(nbuf, std::vector<void *>(c->size, nullptr));
+    bool any_staged = false;
     for (int r = 0; r < c->size; ++r) {
         RankSlot &o = c->ctrl->slot[r];
         if (o.seq.load(std::memory_order_acquire) != c->seq)
@@ -266,6 +323,19 @@ static int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uin
                              (unsigned long long)o.seq.load(), c->rank, (unsigned long long)c->seq);
         if (o.sig[0] != sig[0] || o.sig[1] != sig[1] || o.sig[2] != sig[2] || o.sig[3] != sig[3])
             return set_error(MI355X_ERR_ARG, "collective arguments differ between rank %d and rank %d", r, c->rank);
+        for (int b = 0; b < nbuf; ++b) any_staged = any_staged || o.buf[b].staged;
+    }
+    peers.assign(nbuf, std::vector<void *>(c->size, nullptr));
+    if (any_staged) {
+        if (!staged) return set_error(MI355X_ERR_UNSUPPORTED, "buffer allocation too large to export");
+        *staged = true;
+        TRACE(c, "staged data flow");
+        // the staged flow publishes again at once (the staging buffers): nobody may overwrite
+        // its slot before every rank has read this exchange's slots
+        return barrier(c);
+    }
+    for (int r = 0; r < c->size; ++r) {
+        RankSlot &o = c->ctrl->slot[r];
         for (int b = 0; b < nbuf; ++b) {
             if (r == c->rank) {
                 peers[b][r] = const_cast<void *>(mine[b]);
@@ -280,7 +350,9 @@ static int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uin
 
 static int finish(mi355x_comm *c, hipStream_t s)
 {
+    TRACE(c, "finish: stream sync");
     MI_HIP(hipStreamSynchronize(s));
+    TRACE(c, "finish: barrier");
     return barrier(c);
 }
 
@@ -302,6 +374,9 @@ static int run_program(int op, int type, const Program &pr, const std::vector<vo
 {
     if (len == 0) return MI355X_SUCCESS;
     const size_t esz = mi355x_type_size(type);
+    if (debug_on())
+        fprintf(stderr, "[mi355x] run_program op %d type %d %s nr %d off %zu len %zu\n", op, type,
+                pr.is_fold ? "fold" : "tree", pr.nr, off, len);
     if ((int)dst.size() > kMaxRanks || (int)in.size() > kMaxRanks)
         return set_error(MI355X_ERR_UNSUPPORTED, "communicator larger than %d ranks", kMaxRanks);
     if (pr.is_fold) {
@@ -328,6 +403,191 @@ static int run_program(int op, int type, const Program &pr, const std::vector<vo
     t.result = pr.result;
     t.n = len;
     return launch_tree_slot(op, type, t, s);
+}
+
+// ----------------------------------------------------------------- staged data flow
+// Every rank's staging buffer, exported and mapped once (cached like any other buffer).
+static int stage_peers(mi355x_comm *c, std::vector<void *> &sp)
+{
+    if (!c->stage) MI_HIP(hipMalloc(&c->stage, c->stage_bytes));
+    const void *mine[1] = {c->stage};
+    const uint64_t sig[4] = {9, c->stage_bytes, 0, 0};
+    std::vector<std::vector<void *>> P;
+    int rc = exchange(c, 1, mine, sig, P, nullptr, true);
+    if (rc) return rc;
+    sp = P[0];
+    return MI355X_SUCCESS;
+}
+
+// Staged reduction.  Rank b's result is elements [boff[b], boff[b] + blen[b]) of the vector; this
+// rank folds its own range with program `pr` over every rank's input `in` and writes it at
+// `mine_dst` (pointer of its first result element).  Window w covers elements
+// [w*Wb, (w+1)*Wb) of EVERY rank's range (block-strided, as the segmented ring's phases are), so
+// all ranks fold at once.  Per window: copy-in (each rank copies the other ranks' slices of its
+// input into staging slot b) -> barrier -> fold (own slice read in place, peers' from their slot
+// `me`) -> barrier.  With `distribute` (allreduce) the fold also writes the result into slot n,
+// and every rank then pulls the other ranks' results into rbuf -> barrier.
+static int staged_reduce(mi355x_comm *c, int op, int type, const Program &pr, const void *in,
+                         const std::vector<size_t> &boff, const std::vector<size_t> &blen, void *mine_dst,
+                         bool distribute, void *rbuf, hipStream_t s)
+{
+    const int n = c->size, me = c->rank;
+    const size_t esz = mi355x_type_size(type);
+    std::vector<void *> sp;
+    int rc = stage_peers(c, sp);
+    if (rc) return rc;
+    const size_t slots = (size_t)n + (distribute ? 1 : 0);
+    size_t wb = c->stage_bytes / (slots * esz);
+    wb -= wb % 16;  // slots stay 16-byte aligned
+    if (wb == 0) return set_error(MI355X_ERR_NOMEM, "staging buffer too small for %d ranks", n);
+    size_t maxlen = 0;
+    for (int b = 0; b < n; ++b) maxlen = std::max(maxlen, blen[b]);
+    const size_t nwin = (maxlen + wb - 1) / wb;
+    char *stage = (char *)c->stage;
+    auto wlen = [&](int b, size_t w) -> size_t {
+        const size_t lo = w * wb;
+        return lo >= blen[b] ? 0 : std::min(wb, blen[b] - lo);
+    };
+    for (size_t w = 0; w < nwin; ++w) {
+        MultiCopyArgs m;
+        std::memset(&m, 0, sizeof(m));
+        for (int b = 0; b < n; ++b) {
+            const size_t l = wlen(b, w);
+            if (b == me || l == 0) continue;
+            m.src[m.nseg] = (const char *)in + (boff[b] + w * wb) * esz;
+            m.dst[m.nseg] = stage + (size_t)b * wb * esz;
+            m.len[m.nseg] = l * esz;
+            m.nseg++;
+        }
+        rc = launch_multicopy(m, s);
+        if (rc) return rc;
+        rc = finish(c, s);
+        if (rc) return rc;
+        const size_t lme = wlen(me, w);
+        std::vector<void *> ins(n);
+        for (int q = 0; q < n; ++q)
+            ins[q] = (q == me) ? (void *)((const char *)in + (boff[me] + w * wb) * esz)
+                               : (void *)((char *)sp[q] + (size_t)me * wb * esz);
+        std::vector<void *> dst(1, (char *)mine_dst + w * wb * esz);
+        if (distribute) dst.push_back(stage + (size_t)n * wb * esz);
+        rc = run_program(op, type, pr, ins, dst, 0, lme, s);
+        if (rc) return rc;
+        rc = finish(c, s);
+        if (rc) return rc;
+        if (!distribute) continue;
+        std::memset(&m, 0, sizeof(m));
+        for (int q = 0; q < n; ++q) {
+            const size_t l = wlen(q, w);
+            if (q == me || l == 0) continue;
+            m.src[m.nseg] = (const char *)sp[q] + (size_t)n * wb * esz;
+            m.dst[m.nseg] = (char *)rbuf + (boff[q] + w * wb) * esz;
+            m.len[m.nseg] = l * esz;
+            m.nseg++;
+        }
+        rc = launch_multicopy(m, s);
+        if (rc) return rc;
+        rc = finish(c, s);
+        if (rc) return rc;
+    }
+    return MI355X_SUCCESS;
+}
+
+// Staged allgather: per window of W bytes every rank copies its slice into staging, then pulls
+// the peers' slices.
+static int staged_allgather(mi355x_comm *c, const void *src, void *rbuf, size_t bytes, hipStream_t s)
+{
+    const int n = c->size, me = c->rank;
+    std::vector<void *> sp;
+    int rc = stage_peers(c, sp);
+    if (rc) return rc;
+    char *own = (char *)rbuf + (size_t)me * bytes;
+    if (src != own) MI_HIP(hipMemcpyAsync(own, src, bytes, hipMemcpyDeviceToDevice, s));
+    const size_t W = c->stage_bytes & ~(size_t)15;
+    for (size_t lo = 0; lo < bytes; lo += W) {
+        const size_t l = std::min(W, bytes - lo);
+        MI_HIP(hipMemcpyAsync(c->stage, (const char *)src + lo, l, hipMemcpyDeviceToDevice, s));
+        rc = finish(c, s);
+        if (rc) return rc;
+        MultiCopyArgs m;
+        std::memset(&m, 0, sizeof(m));
+        for (int q = 0; q < n; ++q) {
+            if (q == me) continue;
+            m.src[m.nseg] = sp[q];
+            m.dst[m.nseg] = (char *)rbuf + (size_t)q * bytes + lo;
+            m.len[m.nseg] = l;
+            m.nseg++;
+        }
+        rc = launch_multicopy(m, s);
+        if (rc) return rc;
+        rc = finish(c, s);
+        if (rc) return rc;
+    }
+    return MI355X_SUCCESS;
+}
+
+// Staged bcast: per window the root copies into its staging; windows of >= 1 MiB take the
+// scatter + allgather shape (each rank pulls its slice from the root into its buffer and its own
+// staging, then the other slices from their owners), smaller ones a direct pull from the root.
+static int staged_bcast(mi355x_comm *c, void *buf, size_t bytes, int root, hipStream_t s)
+{
+    const int n = c->size, me = c->rank;
+    std::vector<void *> sp;
+    int rc = stage_peers(c, sp);
+    if (rc) return rc;
+    const size_t W = c->stage_bytes & ~(size_t)15;
+    for (size_t lo = 0; lo < bytes; lo += W) {
+        const size_t l = std::min(W, bytes - lo);
+        if (me == root) MI_HIP(hipMemcpyAsync(c->stage, (const char *)buf + lo, l, hipMemcpyDeviceToDevice, s));
+        rc = finish(c, s);
+        if (rc) return rc;
+        MultiCopyArgs m;
+        std::memset(&m, 0, sizeof(m));
+        if (l < ((size_t)1 << 20)) {
+            if (me != root) {
+                m.src[0] = sp[root];
+                m.dst[0] = (char *)buf + lo;
+                m.len[0] = l;
+                m.nseg = 1;
+                rc = launch_multicopy(m, s);
+                if (rc) return rc;
+            }
+            rc = finish(c, s);
+            if (rc) return rc;
+            continue;
+        }
+        size_t off, len;
+        ring_block(l, n, me, &off, &len);
+        if (me != root && len) {
+            CopyArgs a;
+            std::memset(&a, 0, sizeof(a));
+            a.src = (const char *)sp[root] + off;
+            a.dst[0] = (char *)buf + lo + off;
+            a.dst[1] = (char *)c->stage + off;
+            a.nd = 2;
+            a.n = len;
+            rc = launch_copy(a, s);
+            if (rc) return rc;
+        }
+        rc = finish(c, s);
+        if (rc) return rc;
+        if (me != root) {
+            for (int q = 0; q < n; ++q) {
+                if (q == me) continue;
+                size_t qo, ql;
+                ring_block(l, n, q, &qo, &ql);
+                if (!ql) continue;
+                m.src[m.nseg] = (const char *)sp[q] + qo;  // slice q sits at rank q (and the root)
+                m.dst[m.nseg] = (char *)buf + lo + qo;
+                m.len[m.nseg] = ql;
+                m.nseg++;
+            }
+            rc = launch_multicopy(m, s);
+            if (rc) return rc;
+        }
+        rc = finish(c, s);
+        if (rc) return rc;
+    }
+    return MI355X_SUCCESS;
 }
 
 static int check_common(mi355x_comm *c, int op, int type)
@@ -458,6 +718,7 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
     (void)hipSetDevice(c->device);
     for (auto &kv : c->peer_maps) (void)hipIpcCloseMemHandle(kv.second.mapped);
     if (c->scratch) (void)hipFree(c->scratch);
+    if (c->stage) (void)hipFree(c->stage);
     if (c->loopback) {
         std::lock_guard<std::mutex> g(c->loop->mtx);
         if (--c->loop->refs == 0) free(c->loop->ctrl);
@@ -486,6 +747,16 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
         break;
     case MI355X_KNOB_TIMEOUT_S: c->timeout_s = (double)value; break;
     case MI355X_KNOB_PUSH: coll_tune().push = value ? 1 : 0; break;
+    case MI355X_KNOB_IPC_MAX_BYTES:
+        if (value < 0) return set_error(MI355X_ERR_ARG, "ipc_max_bytes < 0");
+        c->ipc_max = (size_t)value;
+        break;
+    case MI355X_KNOB_STAGE_BYTES:
+        if (value < 4096 || value >= (1l << 31)) return set_error(MI355X_ERR_ARG, "stage_bytes out of range");
+        if (c->stage) (void)hipFree(c->stage);
+        c->stage = nullptr;
+        c->stage_bytes = (size_t)value & ~(size_t)4095;
+        break;
     default: return set_error(MI355X_ERR_ARG, "unknown knob %d", knob);
     }
     return MI355X_SUCCESS;
@@ -565,7 +836,8 @@ int mi355x_allreduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t coun
     const void *mine[2] = {in, rbuf};
     const uint64_t sig[4] = {1, count, (uint64_t)type, (uint64_t)op};
     std::vector<std::vector<void *>> P;
-    rc = exchange(c, 2, mine, sig, P);
+    bool staged = false;
+    rc = exchange(c, 2, mine, sig, P, &staged);
     if (rc) return rc;
     Program pr;
     const bool ring = (alg == AR_RING || alg == AR_RING_SEGMENTED);
@@ -580,7 +852,7 @@ int mi355x_allreduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t coun
             root = expr_reduce(ep, ra, c->size, 0);
         }
         if (!compile_expr(ep, root, c->size, &pr)) return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
-        if (sbuf && sbuf != rbuf) {
+        if (sbuf && sbuf != rbuf && !staged) {
             // tree orders (small messages): every rank evaluates the whole vector from the n
             // inputs and writes only its own rbuf -- one phase, reads only
             std::vector<void *> dst(1, rbuf);
@@ -594,6 +866,11 @@ int mi355x_allreduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t coun
     size_t off, len;
     ring_block(count, c->size, c->rank, &off, &len);
     if (ring) pr = ring_block_program(c->size, c->rank);
+    if (staged) {
+        std::vector<size_t> boff(c->size), blen(c->size);
+        for (int q = 0; q < c->size; ++q) ring_block(count, c->size, q, &boff[q], &blen[q]);
+        return staged_reduce(c, op, type, pr, in, boff, blen, (char *)rbuf + off * esz, true, rbuf, s);
+    }
     if (coll_tune().push) {
         // one phase: the owner writes its block into every rank's rbuf
         rc = run_program(op, type, pr, P[0], P[1], off, len, s);
@@ -645,12 +922,24 @@ int mi355x_reduce_scatter_block(mi355x_comm_t *c, const void *sbuf, void *rbuf, 
     const void *mine[1] = {in};
     const uint64_t sig[4] = {2, rcount, (uint64_t)type, (uint64_t)op};
     std::vector<std::vector<void *>> P;
-    rc = exchange(c, 1, mine, sig, P);
+    bool staged = false;
+    rc = exchange(c, 1, mine, sig, P, &staged);
     if (rc) return rc;
     ExprPool ep;
     Program pr;
     if (!compile_expr(ep, expr_reduce(ep, ra, c->size, 0), c->size, &pr))
         return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
+    if (staged) {
+        std::vector<size_t> boff(c->size), blen(c->size, rcount);
+        for (int q = 0; q < c->size; ++q) boff[q] = (size_t)q * rcount;
+        rc = staged_reduce(c, op, type, pr, in, boff, blen, inplace ? c->scratch : rbuf, false, nullptr, s);
+        if (rc) return rc;
+        if (inplace) {
+            MI_HIP(hipMemcpyAsync(rbuf, c->scratch, rcount * esz, hipMemcpyDeviceToDevice, s));
+            MI_HIP(hipStreamSynchronize(s));
+        }
+        return MI355X_SUCCESS;
+    }
     std::vector<void *> dst(1, inplace ? c->scratch : rbuf);
     // the result block r is written at offset 0 of the destination: shift the destination back
     std::vector<void *> d0(1, (char *)dst[0] - (size_t)c->rank * rcount * esz);
@@ -696,7 +985,8 @@ int mi355x_reduce_scatter(mi355x_comm_t *c, const void *sbuf, void *rbuf, const 
     for (int r = 0; r < c->size; ++r) h = (h ^ (uint64_t)rcounts[r]) * 1099511628211ull;
     const uint64_t sig[4] = {3, h, (uint64_t)type, (uint64_t)op};
     std::vector<std::vector<void *>> P;
-    rc = exchange(c, 1, mine, sig, P);
+    bool staged = false;
+    rc = exchange(c, 1, mine, sig, P, &staged);
     if (rc) return rc;
     Program pr;
     if (c->size == 1) {
@@ -712,6 +1002,17 @@ int mi355x_reduce_scatter(mi355x_comm_t *c, const void *sbuf, void *rbuf, const 
             return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
     }
     void *dst0 = inplace ? c->scratch : rbuf;
+    if (staged) {
+        std::vector<size_t> boff(disp.begin(), disp.end() - 1), blen(c->size);
+        for (int q = 0; q < c->size; ++q) blen[q] = (size_t)rcounts[q];
+        rc = staged_reduce(c, op, type, pr, in, boff, blen, dst0, false, nullptr, s);
+        if (rc) return rc;
+        if (inplace && mine_n) {
+            MI_HIP(hipMemcpyAsync(rbuf, c->scratch, mine_n * esz, hipMemcpyDeviceToDevice, s));
+            MI_HIP(hipStreamSynchronize(s));
+        }
+        return MI355X_SUCCESS;
+    }
     std::vector<void *> d0(1, (char *)dst0 - disp[c->rank] * esz);
     rc = run_program(op, type, pr, P[0], d0, disp[c->rank], mine_n, s);
     if (rc) return rc;
@@ -733,13 +1034,17 @@ int mi355x_allgather(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t byte
     hipStream_t s = resolve_stream(stream);
     const void *src = sbuf ? sbuf : (const char *)rbuf + (size_t)c->rank * bytes;
     MI_HIP(hipStreamSynchronize(s));
+    // pull reads only the peers' send blocks; push also writes into their rbufs
+    const bool push = coll_tune().push != 0;
     const void *mine[2] = {src, rbuf};
-    const uint64_t sig[4] = {4, bytes, 0, 0};
+    const uint64_t sig[4] = {4, bytes, (uint64_t)push, 0};
     std::vector<std::vector<void *>> P;
-    int rc = exchange(c, 2, mine, sig, P);
+    bool staged = false;
+    int rc = exchange(c, push ? 2 : 1, mine, sig, P, &staged);
     if (rc) return rc;
     c->last_alg = 1;
-    if (coll_tune().push) {
+    if (staged) return staged_allgather(c, src, rbuf, bytes, s);
+    if (push) {
         CopyArgs a;
         std::memset(&a, 0, sizeof(a));
         a.src = src;
@@ -779,10 +1084,12 @@ int mi355x_bcast(mi355x_comm_t *c, void *buf, size_t bytes, int root, void *stre
     const void *mine[1] = {buf};
     const uint64_t sig[4] = {5, bytes, (uint64_t)root, 0};
     std::vector<std::vector<void *>> P;
-    int rc = exchange(c, 1, mine, sig, P);
+    bool staged = false;
+    int rc = exchange(c, 1, mine, sig, P, &staged);
     if (rc) return rc;
     const bool split = bytes >= ((size_t)1 << 20);
     c->last_alg = split ? 2 : 1;
+    if (staged) return staged_bcast(c, buf, bytes, root, s);
     MultiCopyArgs m;
     std::memset(&m, 0, sizeof(m));
     if (!split) {

@@ -40,6 +40,45 @@ def realloc_same_address(pkg, comm, rank, size):
     print(f"rank {rank} realloc addresses {'same' if len(set(addrs)) == 1 else 'differ'}", flush=True)
 
 
+def staged(pkg, comm, rank, size, torch):
+    """the staged data flow through real IPC: first forced on small buffers (every allocation
+    treated as unexportable, 1 MiB staging), then for real on allocations of >= 2 GiB, which
+    hipIpcOpenMemHandle cannot map on this platform (a hang without the staged flow)"""
+    comm.set("IPC_MAX_BYTES", 0)
+    comm.set("STAGE_BYTES", 1 << 20)
+    n = 700_001
+    x = torch.full((n,), float(rank + 1), device="cuda")
+    y = torch.empty_like(x)
+    want = size * (size + 1) / 2
+    torch.cuda.synchronize()
+    comm.allreduce(x.data_ptr(), y.data_ptr(), n, pkg.T["FLOAT"], pkg.OP["SUM"])
+    assert bool(torch.all(y == want)), "staged allreduce"
+    r = torch.empty((n // size,), device="cuda")
+    comm.reduce_scatter_block(x.data_ptr(), r.data_ptr(), n // size, pkg.T["FLOAT"], pkg.OP["SUM"])
+    assert bool(torch.all(r == want)), "staged rsb"
+    g = torch.empty((n // size * size,), device="cuda")
+    comm.allgather(r.data_ptr(), g.data_ptr(), r.numel() * 4)
+    assert bool(torch.all(g == want)), "staged allgather"
+    b = torch.full((3_000_001,), rank, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    comm.bcast(b.data_ptr(), b.numel(), 0)
+    assert int(b.max()) == 0, "staged bcast"
+    comm.set("IPC_MAX_BYTES", 1 << 31)
+    comm.set("STAGE_BYTES", 256 << 20)
+    del x, y, r, g, b
+    if size == 2:
+        big = torch.full(((1 << 28) + (1 << 20),), float(rank + 1), dtype=torch.float64, device="cuda")  # 2 GiB + 8 MiB
+        torch.cuda.synchronize()
+        comm.allreduce(None, big.data_ptr(), big.numel(), pkg.T["DOUBLE"], pkg.OP["SUM"])
+        assert bool(torch.all(big == want)), "allreduce on a >= 2 GiB allocation"
+        out = torch.empty((big.numel() // 2,), dtype=torch.float64, device="cuda")
+        comm.reduce_scatter_block(big.data_ptr(), out.data_ptr(), out.numel(), pkg.T["DOUBLE"], pkg.OP["SUM"])
+        assert bool(torch.all(out == size * want)), "rsb on a >= 2 GiB allocation"
+        del big, out
+        torch.cuda.empty_cache()
+    print(f"rank {rank} staged OK", flush=True)
+
+
 def main():
     key, rank, size, dev = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
     import torch
@@ -74,6 +113,7 @@ def main():
     for r in range(size):
         assert int(dst[r * nb:(r + 1) * nb].min()) == r + 1
     realloc_same_address(pkg, comm, rank, size)
+    staged(pkg, comm, rank, size, torch)
     comm.barrier()
     comm.destroy()
     print(f"rank {rank} OK", flush=True)

@@ -230,3 +230,128 @@ def test_large_allreduce_exact_property(gpu, pkg, comms):
         assert torch.equal(out[0], want) and torch.equal(out[1], want)
     del xs, out, want
     torch.cuda.empty_cache()
+
+
+@pytest.fixture(scope="module")
+def staged_comms(gpu, pkg):
+    """loopback communicators forced onto the staged data flow (every buffer treated as
+    unexportable) with a 64 KiB staging buffer, so every call runs several windows"""
+    made = {}
+
+    def get(n):
+        if n not in made:
+            cs = pkg.Comm.loopback(n, 0)
+            for c in cs:
+                c.set("IPC_MAX_BYTES", 0)
+                c.set("STAGE_BYTES", 64 << 10)
+            made[n] = cs
+        return made[n]
+
+    yield get
+    for cs in made.values():
+        for c in cs:
+            c.destroy()
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("alg", [0, 3, 5])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_staged_allreduce(gpu, pkg, oracle, staged_comms, n, alg, inplace):
+    """staged data flow (allocations too large to export): same bits as the reference schedule"""
+    _allreduce_cases(gpu, pkg, oracle, staged_comms(n), n, alg, inplace)
+    for c in staged_comms(n):
+        c.set("ALLREDUCE_ALG", 0)
+
+
+@pytest.mark.parametrize("n", [2, 5])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_staged_reduce_scatter_block(gpu, pkg, oracle, staged_comms, n, inplace):
+    torch = gpu
+    cs = staged_comms(n)
+    for opname, tname in CASES[:4]:
+        op, ty = pkg.OP[opname], pkg.T[tname]
+        for rcount in (1, 5000, 20_011):
+            xs = [opdata.make(tname, rcount * n, 500 + r) for r in range(n)]
+            outs = [np.zeros(rcount, dtype=xs[0].dtype) for _ in range(n)]
+            assert oracle.oracle_reduce_scatter_block(n, rcount, ty, op, _ptrs(xs), _ptrs(outs)) >= 0
+            dx = [to_dev(torch, x) for x in xs]
+            dr = [t.clone() for t in dx] if inplace else [torch.zeros(rcount * pkg.type_size(ty), dtype=torch.uint8, device="cuda") for _ in dx]
+            torch.cuda.synchronize()
+            run_ranks(n, lambda r: cs[r].reduce_scatter_block(None if inplace else dx[r].data_ptr(), dr[r].data_ptr(),
+                                                              rcount, ty, op))
+            torch.cuda.synchronize()
+            for r in range(n):
+                opdata.assert_same(tname, opname, from_dev(dr[r], outs[r], rcount), outs[r],
+                                   f"staged rsb n={n} rcount={rcount} rank={r}")
+
+
+@pytest.mark.parametrize("rsalg", [1, 2])
+def test_staged_reduce_scatter(gpu, pkg, oracle, staged_comms, rsalg):
+    torch = gpu
+    n = 4
+    cs = staged_comms(n)
+    oracle.oracle_reduce_scatter_alg.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                                 ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                                 ctypes.POINTER(ctypes.c_void_p)]
+    rcounts = [9000, 0, 17, 30_000]
+    total = sum(rcounts)
+    for opname, tname in CASES[:4]:
+        op, ty = pkg.OP[opname], pkg.T[tname]
+        xs = [opdata.make(tname, total, 600 + r) for r in range(n)]
+        outs = [np.zeros(max(c, 1), dtype=xs[0].dtype) for c in rcounts]
+        rc = (ctypes.c_int * n)(*rcounts)
+        assert oracle.oracle_reduce_scatter_alg(rsalg, n, rc, ty, op, _ptrs(xs), _ptrs(outs)) >= 0
+        dx = [to_dev(torch, x) for x in xs]
+        dr = [torch.zeros(max(c, 1) * pkg.type_size(ty), dtype=torch.uint8, device="cuda") for c in rcounts]
+        torch.cuda.synchronize()
+        for c in cs:
+            c.set("REDUCE_SCATTER_ALG", rsalg)
+        run_ranks(n, lambda r: cs[r].reduce_scatter(dx[r].data_ptr(), dr[r].data_ptr(), rcounts, ty, op))
+        torch.cuda.synchronize()
+        for r in range(n):
+            if rcounts[r]:
+                opdata.assert_same(tname, opname, from_dev(dr[r], outs[r], rcounts[r]), outs[r][:rcounts[r]],
+                                   f"staged rs alg={rsalg} rank={r}")
+    for c in cs:
+        c.set("REDUCE_SCATTER_ALG", 0)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("nbytes", [13, 200_003])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_staged_allgather(gpu, pkg, staged_comms, n, nbytes, inplace):
+    torch = gpu
+    cs = staged_comms(n)
+    src = [torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda") for _ in range(n)]
+    dst = [torch.zeros(n * nbytes, dtype=torch.uint8, device="cuda") for _ in range(n)]
+    if inplace:
+        for r in range(n):
+            dst[r][r * nbytes:(r + 1) * nbytes].copy_(src[r])
+    torch.cuda.synchronize()
+    run_ranks(n, lambda r: cs[r].allgather(None if inplace else src[r].data_ptr(), dst[r].data_ptr(), nbytes))
+    torch.cuda.synchronize()
+    want = torch.cat(src)
+    for r in range(n):
+        assert torch.equal(dst[r], want), r
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("nbytes", [7, 65536, 3_000_001])
+def test_staged_bcast(gpu, pkg, staged_comms, n, nbytes):
+    """windows of >= 1 MiB take the scatter + allgather shape: a 1 MiB staging buffer covers it"""
+    torch = gpu
+    cs = staged_comms(n)
+    for c in cs:
+        c.set("STAGE_BYTES", 1 << 20)
+    try:
+        for root in (0, n - 1):
+            bufs = [torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda") for _ in range(n)]
+            want = bufs[root].clone()
+            torch.cuda.synchronize()
+            run_ranks(n, lambda r: cs[r].bcast(bufs[r].data_ptr(), nbytes, root))
+            torch.cuda.synchronize()
+            for r in range(n):
+                assert torch.equal(bufs[r], want), (root, r)
+    finally:
+        for c in cs:
+            c.set("STAGE_BYTES", 64 << 10)
