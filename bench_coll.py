@@ -57,11 +57,21 @@ def extra_legs(args, pkg, torch, comm, world, rank, dev, legs):
         cnt = nbytes // 4
         x = torch.full((cnt,), float(rank + 1), device=dev)
         y = torch.empty_like(x)
-        sec = _timed(dist, torch, lambda: comm.allreduce(x.data_ptr(), y.data_ptr(), cnt, f32, SUM),
-                     20 if nbytes <= (1 << 20) else 5, 2)
-        sweep.append({"bytes": nbytes, "us": round(sec * 1e6, 2), "alg": comm.last_algorithm(),
-                      "busbw_GBs": round(nbytes / sec * 2 * (world - 1) / world / 1e9, 3),
-                      "exact": bool(torch.all(y == want).item())})
+        run = lambda: comm.allreduce(x.data_ptr(), y.data_ptr(), cnt, f32, SUM)
+        reps = 20 if nbytes <= (1 << 20) else 5
+        sec = _timed(dist, torch, run, reps, 2)
+        row = {"bytes": nbytes, "us": round(sec * 1e6, 2), "alg": comm.last_algorithm(),
+               "busbw_GBs": round(nbytes / sec * 2 * (world - 1) / world / 1e9, 3),
+               "exact": bool(torch.all(y == want).item())}
+        if nbytes <= (1 << 20):
+            # both data flows at this size, for the LL threshold: one-shot LL vs host-synchronised
+            for name, llmax in (("us_ll", 1 << 20), ("us_host", 0)):
+                comm.set("LL_MAX_BYTES", llmax)
+                y.zero_()
+                row[name] = round(_timed(dist, torch, run, reps, 2) * 1e6, 2)
+                row["exact"] = row["exact"] and bool(torch.all(y == want).item())
+            comm.set("LL_MAX_BYTES", 64 << 10)  # the default
+        sweep.append(row)
         del x, y
     legs["allreduce_sweep_f32"] = sweep
     # configs[3]: reduce_scatter_block + allgather, fp64, 4 GiB per rank
@@ -129,6 +139,25 @@ def extra_legs(args, pkg, torch, comm, world, rank, dev, legs):
     del buf, packed, red
     d.destroy()
     torch.cuda.empty_cache()
+    # comparison point only (BASELINE north star): RCCL's allreduce on the same device buffers,
+    # through torch.distributed's "nccl" backend (= RCCL on ROCm).  Needs one GPU per rank.
+    if torch.cuda.device_count() >= world:
+        _log(rank, "leg rccl_allreduce")
+        try:
+            pg = dist.new_group(backend="nccl")
+            rows = []
+            for nbytes in (8, 65536, 1 << 20, 16 << 20, 256 << 20, 1 << 30):
+                cnt = max(1, nbytes // 4)
+                x = torch.full((cnt,), float(rank + 1), device=dev)
+                sec = _timed(dist, torch, lambda: dist.all_reduce(x, group=pg), 20 if nbytes <= (1 << 20) else 5, 2)
+                rows.append({"bytes": nbytes, "us": round(sec * 1e6, 2),
+                             "busbw_GBs": round(nbytes / sec * 2 * (world - 1) / world / 1e9, 3)})
+                del x
+            legs["rccl_allreduce_f32"] = rows
+            dist.destroy_process_group(pg)
+        except Exception as e:  # comparison only: never fails the run
+            legs["rccl_allreduce_f32"] = {"error": repr(e)[:300]}
+        torch.cuda.empty_cache()
     return legs
 
 

@@ -114,7 +114,10 @@ enum mi355x_knob {
     MI355X_KNOB_IPC_MAX_BYTES = 7,      /* buffers in allocations of >= this many bytes are never
                                            exported; calls touching one take the staged data flow
                                            (default 2^31: hipIpcOpenMemHandle hangs from 2 GiB) */
-    MI355X_KNOB_STAGE_BYTES = 8         /* size of the per-communicator staging buffer (default 1 GiB) */
+    MI355X_KNOB_STAGE_BYTES = 8,        /* size of the per-communicator staging buffer (default 1 GiB) */
+    MI355X_KNOB_LL_MAX_BYTES = 9        /* per-rank message bytes up to which allreduce / allgather /
+                                           bcast take the one-shot low-latency path (0 = never;
+                                           default 64 KiB; multi-process communicators only) */
 };
 int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
 

@@ -178,7 +178,8 @@ def get_tune() -> tuple[int, int, int]:
 
 # ---------------------------------------------------------------- coll/mi355x engine
 KNOB = {"ALLREDUCE_ALG": 1, "REDUCE_ALG": 2, "REDUCE_SCATTER_ALG": 3, "BLOCKS_PER_CU": 4, "TIMEOUT_S": 5,
-        "PUSH": 6, "IPC_MAX_BYTES": 7, "STAGE_BYTES": 8}
+        "PUSH": 6, "IPC_MAX_BYTES": 7, "STAGE_BYTES": 8,
+        "LL_MAX_BYTES": 9}
 AR_ALG = {"DECISION": 0, "LINEAR": 1, "NONOVERLAPPING": 2, "RECURSIVE_DOUBLING": 3, "RING": 4,
           "RING_SEGMENTED": 5}
 

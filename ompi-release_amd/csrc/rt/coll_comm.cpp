@@ -151,6 +151,13 @@ struct mi355x_comm {
     void *stage = nullptr;                        // staging buffer of the staged data flow
     size_t stage_bytes = (size_t)1 << 30;         // its size (an allocation below ipc_max)
     size_t ipc_max = (size_t)1 << 31;             // allocations >= this are never exported
+    // low-latency path (coll_ll.hip): uncached LL region [flags 2 x n x kmax][data 2 x n x slot]
+    size_t ll_max = (size_t)64 << 10;             // per-rank message bytes served by the LL path
+    char *ll_base = nullptr;
+    size_t ll_slot = 0, ll_kmax = 0, ll_flag_bytes = 0;
+    std::vector<char *> ll_peer;                  // every rank's LL region, mapped
+    uint64_t ll_seq = 0;
+    uint32_t *ll_err = nullptr;                   // host-visible timeout word
     int knob_allreduce = 0, knob_reduce = 0, knob_rs = 0;
     int last_alg = -1;
     double timeout_s = 600.0;
@@ -590,6 +597,89 @@ static int staged_bcast(mi355x_comm *c, void *buf, size_t bytes, int root, hipSt
     return MI355X_SUCCESS;
 }
 
+// ----------------------------------------------------------------- low-latency path
+// Loopback communicators (threads of one process) never take it: their kernels would share the
+// process's few hardware queues and a rank's spinning kernel could sit in front of the peer
+// kernel it waits for.
+static bool ll_usable(const mi355x_comm *c, size_t bytes)
+{
+    return !c->loopback && c->size > 1 && bytes > 0 && bytes <= c->ll_max && c->size <= kMaxRanks;
+}
+
+// (Re)allocate and exchange the LL region.  Collective: every rank reaches it in the same call.
+static int ensure_ll(mi355x_comm *c)
+{
+    if (c->ll_base && c->ll_slot >= c->ll_max) return MI355X_SUCCESS;
+    const size_t n = (size_t)c->size;
+    const size_t slot = (c->ll_max + kLLChunk - 1) / kLLChunk * kLLChunk;
+    const size_t kmax = slot / kLLChunk;
+    const size_t fbytes = (2 * n * kmax * sizeof(uint64_t) + 4095) / 4096 * 4096;
+    const size_t total = fbytes + 2 * n * slot;
+    if (c->ll_base) (void)hipFree(c->ll_base);
+    c->ll_base = nullptr;
+    MI_HIP(hipExtMallocWithFlags((void **)&c->ll_base, total, hipDeviceMallocUncached));
+    MI_HIP(hipMemset(c->ll_base, 0, total));
+    MI_HIP(hipDeviceSynchronize());
+    if (!c->ll_err) MI_HIP(hipHostMalloc((void **)&c->ll_err, sizeof(uint32_t), hipHostMallocCoherent));
+    c->ll_slot = slot;
+    c->ll_kmax = kmax;
+    c->ll_flag_bytes = fbytes;
+    c->ll_seq = 0;
+    const void *mine[1] = {c->ll_base};
+    const uint64_t sig[4] = {10, total, 0, 0};
+    std::vector<std::vector<void *>> P;
+    int rc = exchange(c, 1, mine, sig, P, nullptr, true);
+    if (rc) return rc;
+    c->ll_peer.assign(n, nullptr);
+    for (size_t q = 0; q < n; ++q) c->ll_peer[q] = (char *)P[0][q];
+    TRACE(c, "LL region %zu bytes (slot %zu)", total, slot);
+    return barrier(c);  // every rank has read the exchange slots
+}
+
+// one LL call: fills the per-call fields of `a` and runs it to completion
+static int ll_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s)
+{
+    int rc = ensure_ll(c);
+    if (rc) return rc;
+    const uint64_t seq = ++c->ll_seq;
+    const size_t par = seq & 1, n = (size_t)c->size, me = (size_t)c->rank;
+    a.seq = seq;
+    a.n = c->size;
+    a.me = c->rank;
+    a.slot_bytes = c->ll_slot;
+    a.kmax = c->ll_kmax;
+    for (size_t q = 0; q < n; ++q) {
+        a.peer_data[q] = c->ll_peer[q] + c->ll_flag_bytes + (par * n + me) * c->ll_slot;
+        a.peer_flag[q] = reinterpret_cast<uint64_t *>(c->ll_peer[q]) + (par * n + me) * c->ll_kmax;
+    }
+    a.my_data = c->ll_base + c->ll_flag_bytes + par * n * c->ll_slot;
+    a.my_flag = reinterpret_cast<const uint64_t *>(c->ll_base) + par * n * c->ll_kmax;
+    a.err = c->ll_err;
+    *c->ll_err = 0;
+    a.timeout_ticks = (uint64_t)(c->timeout_s * 1e8);  // s_memrealtime: 100 MHz
+    rc = (a.mode == LL_AR) ? launch_ll_slot(op, type, a, s) : launch_ll_copy(a, s);
+    if (rc) return rc;
+    MI_HIP(hipStreamSynchronize(s));
+    if (__atomic_load_n(c->ll_err, __ATOMIC_ACQUIRE))
+        return set_error(MI355X_ERR_TIMEOUT, "rank %d: LL call %llu timed out waiting for a peer", c->rank,
+                         (unsigned long long)seq);
+    return MI355X_SUCCESS;
+}
+
+static void ll_program(LLArgs &a, const Program &pr)
+{
+    if (!pr.is_fold) {
+        a.prog = LL_TREE;
+        a.nsteps = (int)pr.steps.size();
+        for (int k = 0; k < a.nsteps; ++k) a.steps[k] = pr.steps[k];
+        a.result = pr.result;
+        return;
+    }
+    a.prog = LL_FOLD;
+    for (size_t j = 0; j < pr.order.size(); ++j) a.order[j] = pr.order[j];
+    a.role_mask = pr.role_mask;
+}
+
 static int check_common(mi355x_comm *c, int op, int type)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
@@ -719,6 +809,8 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
     for (auto &kv : c->peer_maps) (void)hipIpcCloseMemHandle(kv.second.mapped);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->stage) (void)hipFree(c->stage);
+    if (c->ll_base) (void)hipFree(c->ll_base);
+    if (c->ll_err) (void)hipHostFree(c->ll_err);
     if (c->loopback) {
         std::lock_guard<std::mutex> g(c->loop->mtx);
         if (--c->loop->refs == 0) free(c->loop->ctrl);
@@ -750,6 +842,10 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
     case MI355X_KNOB_IPC_MAX_BYTES:
         if (value < 0) return set_error(MI355X_ERR_ARG, "ipc_max_bytes < 0");
         c->ipc_max = (size_t)value;
+        break;
+    case MI355X_KNOB_LL_MAX_BYTES:
+        if (value < 0 || value > (64l << 20)) return set_error(MI355X_ERR_ARG, "ll_max_bytes out of range");
+        c->ll_max = (size_t)value;
         break;
     case MI355X_KNOB_STAGE_BYTES:
         if (value < 4096 || value >= (1l << 31)) return set_error(MI355X_ERR_ARG, "stage_bytes out of range");
@@ -832,6 +928,38 @@ int mi355x_allreduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t coun
         alg = AR_RING;
     if (alg == AR_RING && count < (size_t)c->size) alg = AR_RECDBL;
     c->last_alg = alg;
+    const bool ring = (alg == AR_RING || alg == AR_RING_SEGMENTED);
+    if (ll_usable(c, count * esz) && (ring || c->size <= kTreeMax)) {
+        // one-shot: every rank evaluates the whole vector with the reference's per-element order
+        LLArgs a;
+        std::memset(&a, 0, sizeof(a));
+        a.mode = LL_AR;
+        a.src = in;
+        a.dst = rbuf;
+        a.nbytes = count * esz;
+        a.count = count;
+        a.push_mask = ~0ull;
+        if (ring) {
+            size_t o1, l0, l1;
+            ring_block(count, c->size, 0, &o1, &l0);
+            ring_block(count, c->size, c->size - 1, &o1, &l1);
+            a.prog = LL_RING;
+            a.early = l0;
+            a.late = l1;
+            a.split = count % (size_t)c->size;
+            if (a.late == 0) a.late = 1;  // count < n never reaches the ring (recursive doubling)
+        } else {
+            ExprPool ep;
+            const int root = (alg == AR_RECDBL)
+                                 ? expr_allreduce_recursive_doubling(ep, c->size)
+                                 : expr_reduce(ep, (alg == AR_LINEAR) ? RED_LINEAR : reduce_decision(c->size, count, esz),
+                                               c->size, 0);
+            Program pr;
+            if (!compile_expr(ep, root, c->size, &pr)) return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
+            ll_program(a, pr);
+        }
+        return ll_run(c, a, op, type, s);
+    }
     MI_HIP(hipStreamSynchronize(s));  // every rank's input is complete before it is published
     const void *mine[2] = {in, rbuf};
     const uint64_t sig[4] = {1, count, (uint64_t)type, (uint64_t)op};
@@ -840,7 +968,6 @@ int mi355x_allreduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t coun
     rc = exchange(c, 2, mine, sig, P, &staged);
     if (rc) return rc;
     Program pr;
-    const bool ring = (alg == AR_RING || alg == AR_RING_SEGMENTED);
     if (!ring) {
         ExprPool ep;
         int root;
@@ -1033,6 +1160,17 @@ int mi355x_allgather(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t byte
     if (bytes == 0) return MI355X_SUCCESS;
     hipStream_t s = resolve_stream(stream);
     const void *src = sbuf ? sbuf : (const char *)rbuf + (size_t)c->rank * bytes;
+    if (ll_usable(c, bytes)) {
+        c->last_alg = 3;
+        LLArgs a;
+        std::memset(&a, 0, sizeof(a));
+        a.mode = LL_AG;
+        a.src = src;
+        a.dst = rbuf;
+        a.nbytes = bytes;
+        a.push_mask = ~0ull;
+        return ll_run(c, a, 0, 0, s);
+    }
     MI_HIP(hipStreamSynchronize(s));
     // pull reads only the peers' send blocks; push also writes into their rbufs
     const bool push = coll_tune().push != 0;
@@ -1080,6 +1218,18 @@ int mi355x_bcast(mi355x_comm_t *c, void *buf, size_t bytes, int root, void *stre
     if (root < 0 || root >= c->size) return set_error(MI355X_ERR_ARG, "bad root");
     if (bytes == 0 || c->size == 1) return MI355X_SUCCESS;
     hipStream_t s = resolve_stream(stream);
+    if (ll_usable(c, bytes)) {
+        c->last_alg = 3;
+        LLArgs a;
+        std::memset(&a, 0, sizeof(a));
+        a.mode = LL_BC;
+        a.root = root;
+        a.src = (c->rank == root) ? buf : nullptr;
+        a.dst = buf;
+        a.nbytes = bytes;
+        a.push_mask = ~0ull & ~(1ull << root);
+        return ll_run(c, a, 0, 0, s);
+    }
     MI_HIP(hipStreamSynchronize(s));
     const void *mine[1] = {buf};
     const uint64_t sig[4] = {5, bytes, (uint64_t)root, 0};

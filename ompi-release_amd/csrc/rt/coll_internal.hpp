@@ -58,6 +58,33 @@ struct MultiCopyArgs {
     int nseg;
 };
 
+// Low-latency one-shot path (coll_ll.hip) for small messages: every rank pushes its data into
+// slot (parity, me) of every peer's fine-grained (uncached) LL region over xGMI, raises one flag
+// per 4 KiB slice in every peer, waits for every peer's flags, then finishes locally.  No host
+// barrier, no per-call IPC exchange.  Parity double-buffering makes back-to-back calls safe: a
+// peer can only reuse a parity after every rank has acknowledged the call in between.
+constexpr size_t kLLChunk = 4096;  // bytes per slice = per thread block (256 threads x 16 B)
+enum { LL_AR = 0, LL_AG = 1, LL_BC = 2 };        // allreduce, allgather, bcast
+enum { LL_FOLD = 0, LL_RING = 1, LL_TREE = 2 };   // per-element program of LL_AR
+struct LLArgs {
+    const void *src;                   // this rank's data (NULL: nothing to push)
+    void *dst;                         // result (rbuf / buf)
+    char *peer_data[kMaxRanks];        // slot (parity, me) in peer q's LL data region
+    uint64_t *peer_flag[kMaxRanks];    // flag row (parity, me) in peer q's LL flag region
+    const char *my_data;               // this rank's data region of this parity (slot q at q*slot_bytes)
+    const uint64_t *my_flag;           // this rank's flag region of this parity (row q at q*kmax)
+    uint32_t *err;                     // host-visible error word (timeout)
+    uint64_t push_mask;                // bit q: push the data to rank q
+    uint64_t seq, slot_bytes, kmax, nbytes, timeout_ticks;
+    uint64_t count, early, late, split;  // elements; ring block partition (coll_tuned.h:546-552)
+    uint64_t role_mask;
+    int mode, prog, n, me, root, nsteps, result;
+    int order[kMaxRanks];
+    TreeStep steps[kTreeSteps];
+};
+int launch_ll_slot(int op, int type, const LLArgs &a, hipStream_t s);  // LL_AR
+int launch_ll_copy(const LLArgs &a, hipStream_t s);                   // LL_AG / LL_BC
+
 struct CollTune {
     int blocks_per_cu = 4;
     int push = 0;   // 1: allreduce owners write into the peers' rbufs (one phase); 0: pull (two phases)

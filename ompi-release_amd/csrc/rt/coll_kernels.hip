@@ -22,6 +22,7 @@
 #include "coll_internal.hpp"
 #include "op_functors.hpp"
 #include "rt_internal.hpp"
+#include "slot_list.hpp"
 
 namespace mi355x {
 
@@ -351,66 +352,15 @@ struct CollSlot {
     int (*tree)(const TreeArgs &, hipStream_t) = nullptr;
 };
 
-template <class F> static void cput(CollSlot (&t)[MI355X_OP_MAX_][MI355X_T_MAX], int op, int ty)
-{
-    t[op][ty].fold = &launch_fold<F>;
-    t[op][ty].tree = &launch_tree<F>;
-}
-template <template <typename> class OP>
-static void cput_ints(CollSlot (&t)[MI355X_OP_MAX_][MI355X_T_MAX], int op)
-{
-    cput<OP<int8_t>>(t, op, MI355X_T_INT8);
-    cput<OP<uint8_t>>(t, op, MI355X_T_UINT8);
-    cput<OP<int16_t>>(t, op, MI355X_T_INT16);
-    cput<OP<uint16_t>>(t, op, MI355X_T_UINT16);
-    cput<OP<int32_t>>(t, op, MI355X_T_INT32);
-    cput<OP<uint32_t>>(t, op, MI355X_T_UINT32);
-    cput<OP<int64_t>>(t, op, MI355X_T_INT64);
-    cput<OP<uint64_t>>(t, op, MI355X_T_UINT64);
-}
-
 struct CollTable {
     CollSlot s[MI355X_OP_MAX_][MI355X_T_MAX];
     CollTable()
     {
-        cput_ints<OpMax>(s, MI355X_OP_MAX);
-        cput<OpMax<float>>(s, MI355X_OP_MAX, MI355X_T_FLOAT);
-        cput<OpMax<double>>(s, MI355X_OP_MAX, MI355X_T_DOUBLE);
-        cput_ints<OpMin>(s, MI355X_OP_MIN);
-        cput<OpMin<float>>(s, MI355X_OP_MIN, MI355X_T_FLOAT);
-        cput<OpMin<double>>(s, MI355X_OP_MIN, MI355X_T_DOUBLE);
-        cput_ints<OpSum>(s, MI355X_OP_SUM);
-        cput<OpSum<float>>(s, MI355X_OP_SUM, MI355X_T_FLOAT);
-        cput<OpSum<double>>(s, MI355X_OP_SUM, MI355X_T_DOUBLE);
-        cput<OpCsum<cf32>>(s, MI355X_OP_SUM, MI355X_T_C_FLOAT_COMPLEX);
-        cput<OpCsum<cf64>>(s, MI355X_OP_SUM, MI355X_T_C_DOUBLE_COMPLEX);
-        cput_ints<OpProd>(s, MI355X_OP_PROD);
-        cput<OpProd<float>>(s, MI355X_OP_PROD, MI355X_T_FLOAT);
-        cput<OpProd<double>>(s, MI355X_OP_PROD, MI355X_T_DOUBLE);
-        cput<OpCprod<cf32>>(s, MI355X_OP_PROD, MI355X_T_C_FLOAT_COMPLEX);
-        cput<OpCprod<cf64>>(s, MI355X_OP_PROD, MI355X_T_C_DOUBLE_COMPLEX);
-        cput_ints<OpLand>(s, MI355X_OP_LAND);
-        cput<OpLand<uint8_t>>(s, MI355X_OP_LAND, MI355X_T_BOOL);
-        cput_ints<OpLor>(s, MI355X_OP_LOR);
-        cput<OpLor<uint8_t>>(s, MI355X_OP_LOR, MI355X_T_BOOL);
-        cput_ints<OpLxor>(s, MI355X_OP_LXOR);
-        cput<OpLxor<uint8_t>>(s, MI355X_OP_LXOR, MI355X_T_BOOL);
-        cput_ints<OpBand>(s, MI355X_OP_BAND);
-        cput<OpBand<int8_t>>(s, MI355X_OP_BAND, MI355X_T_BYTE);
-        cput_ints<OpBor>(s, MI355X_OP_BOR);
-        cput<OpBor<int8_t>>(s, MI355X_OP_BOR, MI355X_T_BYTE);
-        cput_ints<OpBxor>(s, MI355X_OP_BXOR);
-        cput<OpBxor<int8_t>>(s, MI355X_OP_BXOR, MI355X_T_BYTE);
-        cput<OpLoc<p_float_int, true>>(s, MI355X_OP_MAXLOC, MI355X_T_FLOAT_INT);
-        cput<OpLoc<p_double_int, true>>(s, MI355X_OP_MAXLOC, MI355X_T_DOUBLE_INT);
-        cput<OpLoc<p_long_int, true>>(s, MI355X_OP_MAXLOC, MI355X_T_LONG_INT);
-        cput<OpLoc<p_2int, true>>(s, MI355X_OP_MAXLOC, MI355X_T_2INT);
-        cput<OpLoc<p_short_int, true>>(s, MI355X_OP_MAXLOC, MI355X_T_SHORT_INT);
-        cput<OpLoc<p_float_int, false>>(s, MI355X_OP_MINLOC, MI355X_T_FLOAT_INT);
-        cput<OpLoc<p_double_int, false>>(s, MI355X_OP_MINLOC, MI355X_T_DOUBLE_INT);
-        cput<OpLoc<p_long_int, false>>(s, MI355X_OP_MINLOC, MI355X_T_LONG_INT);
-        cput<OpLoc<p_2int, false>>(s, MI355X_OP_MINLOC, MI355X_T_2INT);
-        cput<OpLoc<p_short_int, false>>(s, MI355X_OP_MINLOC, MI355X_T_SHORT_INT);
+        for_each_slot([&](auto tag, int op, int ty) {
+            using F = typename decltype(tag)::type;
+            s[op][ty].fold = &launch_fold<F>;
+            s[op][ty].tree = &launch_tree<F>;
+        });
     }
 };
 

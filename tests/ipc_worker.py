@@ -40,6 +40,58 @@ def realloc_same_address(pkg, comm, rank, size):
     print(f"rank {rank} realloc addresses {'same' if len(set(addrs)) == 1 else 'differ'}", flush=True)
 
 
+def ll_checks(pkg, comm, rank, size, oracle, torch):
+    """the one-shot low-latency path (coll_ll.hip): every forced allreduce algorithm against the
+    oracle's schedule simulation, in place and not, allgather / bcast, and many back-to-back calls
+    (parity reuse of the LL slots)"""
+    ptrs = lambda arrs: (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    comm.set("LL_MAX_BYTES", 256 << 10)
+    for alg in (0, 1, 2, 3, 4, 5):
+        comm.set("ALLREDUCE_ALG", alg)
+        for opname, tname in [("SUM", "FLOAT"), ("MAX", "DOUBLE"), ("MINLOC", "FLOAT_INT"), ("PROD", "C_DOUBLE_COMPLEX")]:
+            op, ty = pkg.OP[opname], pkg.T[tname]
+            esz = pkg.type_size(ty)
+            for count in (1, 3, 2500 // esz + 3, 9001, (256 << 10) // esz):
+                xs = [opdata.make(tname, count, 700 + 10 * alg + r) for r in range(size)]
+                outs = [np.zeros_like(xs[0]) for _ in range(size)]
+                ran = oracle.oracle_allreduce(alg, size, count, ty, op, 0, ptrs(xs), ptrs(outs))
+                for inplace in (False, True):
+                    dx = torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda()
+                    dr = dx.clone() if inplace else torch.zeros_like(dx)
+                    torch.cuda.synchronize()
+                    comm.allreduce(None if inplace else dx.data_ptr(), dr.data_ptr(), count, ty, op)
+                    got = dr.cpu().numpy().view(xs[0].dtype)
+                    opdata.assert_same(tname, opname, got, outs[rank],
+                                       f"LL allreduce alg={alg} count={count} inplace={inplace} rank={rank}")
+                    assert comm.last_algorithm() == ran, (comm.last_algorithm(), ran)
+    comm.set("ALLREDUCE_ALG", 0)
+    # back to back: 64 calls, each checked (slot parity reuse)
+    x = torch.empty(1000, device="cuda")
+    y = torch.empty_like(x)
+    for k in range(64):
+        x.fill_(float(rank + k))
+        comm.allreduce(x.data_ptr(), y.data_ptr(), 1000, pkg.T["FLOAT"], pkg.OP["SUM"])
+        want = sum(r + k for r in range(size))
+        assert bool(torch.all(y == want)), ("back-to-back", k)
+    for nb in (1, 4097, 200_003):
+        for inplace in (False, True):
+            src = torch.full((nb,), rank + 1, dtype=torch.uint8, device="cuda")
+            dst = torch.zeros(nb * size, dtype=torch.uint8, device="cuda")
+            if inplace:
+                dst[rank * nb:(rank + 1) * nb] = rank + 1
+            torch.cuda.synchronize()
+            comm.allgather(None if inplace else src.data_ptr(), dst.data_ptr(), nb)
+            assert comm.last_algorithm() == 3
+            for r in range(size):
+                assert int(dst[r * nb:(r + 1) * nb].min()) == r + 1 == int(dst[r * nb:(r + 1) * nb].max()), ("LL ag", nb, r)
+        for root in range(size):
+            b = torch.full((nb,), rank, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
+            comm.bcast(b.data_ptr(), nb, root)
+            assert int(b.min()) == root == int(b.max()), ("LL bcast", nb, root)
+    print(f"rank {rank} LL OK", flush=True)
+
+
 def staged(pkg, comm, rank, size, torch):
     """the staged data flow through real IPC: first forced on small buffers (every allocation
     treated as unexportable, 1 MiB staging), then for real on allocations of >= 2 GiB, which
@@ -113,6 +165,7 @@ def main():
     for r in range(size):
         assert int(dst[r * nb:(r + 1) * nb].min()) == r + 1
     realloc_same_address(pkg, comm, rank, size)
+    ll_checks(pkg, comm, rank, size, oracle, torch)
     staged(pkg, comm, rank, size, torch)
     comm.barrier()
     comm.destroy()

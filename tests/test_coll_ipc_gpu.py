@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 HERE = pathlib.Path(__file__).parent
 
 
-@pytest.mark.parametrize("size", [2, 3])
+@pytest.mark.parametrize("size", [2, 3, 8])
 def test_ipc_ranks(gpu, size):
     key = "t" + uuid.uuid4().hex[:12]
     ndev = gpu.cuda.device_count()
@@ -34,3 +34,5 @@ def test_ipc_ranks(gpu, size):
         outs.append(out)
     for r, p in enumerate(procs):
         assert p.returncode == 0, f"rank {r} failed:\n{outs[r][-3000:]}"
+        for stage in ("LL OK", "staged OK", "OK"):
+            assert f"rank {r} {stage}" in outs[r], f"rank {r} did not report '{stage}':\n{outs[r][-3000:]}"
