@@ -3,12 +3,13 @@
  *
  * Plugs into the coll framework (ompi/mca/coll/coll.h:357-451) at priority 90 -- above
  * coll/tuned (30) and coll/cuda (78) -- for intra-communicators whose ranks all live on this
- * node.  It provides allreduce, reduce_scatter, reduce_scatter_block, allgather and bcast; every
+ * node.  It provides allreduce, reduce, reduce_scatter, reduce_scatter_block, allgather and bcast; every
  * other slot stays with the lower-priority modules.  Entry points have exactly the reference
  * signatures (coll.h:181-239) and replace, for device buffers:
  *   mca_coll_cuda_allreduce            (ompi/mca/coll/cuda/coll_cuda_allreduce.c:30-77)
  *   mca_coll_cuda_reduce_scatter_block (coll_cuda_reduce_scatter_block.c:34-83)
- *   ompi_coll_tuned_*_intra_dec_fixed  (coll_tuned_decision_fixed.c) reached on device buffers
+ *   ompi_coll_tuned_*_intra_dec_fixed  (coll_tuned_decision_fixed.c) reached on device buffers,
+ *                                      incl. ompi_coll_tuned_reduce_intra_dec_fixed (:343-446)
  * with results identical to the tuned/basic schedules (same per-element operand order).
  *
  * Host buffers, user-defined ops, non-contiguous or non-reducible datatypes go to the function
@@ -36,6 +37,8 @@ extern mca_coll_base_component_t mca_coll_mi355x_component;
 int mca_coll_mi355x_allreduce(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
                               struct ompi_op_t *op, struct ompi_communicator_t *comm,
                               mca_coll_base_module_t *module);
+int mca_coll_mi355x_reduce(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                           int root, struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
 int mca_coll_mi355x_reduce_scatter_block(void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dtype,
                                          struct ompi_op_t *op, struct ompi_communicator_t *comm,
                                          mca_coll_base_module_t *module);

@@ -125,6 +125,11 @@ int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
  * ompi_coll_tuned_allreduce_intra_dec_fixed (coll_tuned_decision_fixed.c:42-85). */
 int mi355x_allreduce(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op,
                      void *stream);
+/* MPI_Reduce to `root` (sbuf NULL = MPI_IN_PLACE at the root; rbuf read at the root only).
+ * Replaces ompi_coll_tuned_reduce_intra_dec_fixed (coll_tuned_decision_fixed.c:343-446) and the
+ * tuned reduce trees (coll_tuned_reduce.c:66-721); MI355X_KNOB_REDUCE_ALG forces one. */
+int mi355x_reduce(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op, int root,
+                  void *stream);
 /* MPI_Reduce_scatter_block: coll_basic_reduce_scatter_block.c:54-111 order. */
 int mi355x_reduce_scatter_block(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t rcount,
                                 int type, int op, void *stream);

@@ -106,6 +106,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "mi355x_comm_set": (i, [vp, i, c.c_long]),
         "mi355x_allreduce": (i, [vp, vp, vp, sz, i, i, vp]),
         "mi355x_reduce_scatter_block": (i, [vp, vp, vp, sz, i, i, vp]),
+        "mi355x_reduce": (i, [vp, vp, vp, sz, i, i, i, vp]),
         "mi355x_reduce_scatter": (i, [vp, vp, vp, c.POINTER(i), i, i, vp]),
         "mi355x_allgather": (i, [vp, vp, vp, sz, vp]),
         "mi355x_bcast": (i, [vp, vp, sz, i, vp]),
@@ -227,6 +228,9 @@ class Comm:
 
     def allreduce(self, sbuf, rbuf, count, ty, op, stream=None) -> None:
         check(rt().mi355x_allreduce(self.h, sbuf, rbuf, count, ty, op, stream), "mi355x_allreduce")
+
+    def reduce(self, sbuf, rbuf, count, ty, op, root, stream=None) -> None:
+        check(rt().mi355x_reduce(self.h, sbuf, rbuf, count, ty, op, root, stream), "mi355x_reduce")
 
     def reduce_scatter_block(self, sbuf, rbuf, rcount, ty, op, stream=None) -> None:
         check(rt().mi355x_reduce_scatter_block(self.h, sbuf, rbuf, rcount, ty, op, stream),

@@ -356,6 +356,10 @@ int mini_allreduce(ompi_communicator_t *c, void *s, void *r, int n, ompi_datatyp
 {
     return c->c_coll.coll_allreduce(s, r, n, d, op, c, c->c_coll.coll_allreduce_module);
 }
+int mini_reduce(ompi_communicator_t *c, void *s, void *r, int n, ompi_datatype_t *d, ompi_op_t *op, int root)
+{
+    return c->c_coll.coll_reduce(s, r, n, d, op, root, c, c->c_coll.coll_reduce_module);
+}
 int mini_reduce_scatter_block(ompi_communicator_t *c, void *s, void *r, int n, ompi_datatype_t *d, ompi_op_t *op)
 {
     return c->c_coll.coll_reduce_scatter_block(s, r, n, d, op, c, c->c_coll.coll_reduce_scatter_block_module);
@@ -380,6 +384,7 @@ void *mini_comm_fn(ompi_communicator_t *c, int which)
     case 2: return (void *)c->c_coll.coll_reduce_scatter;
     case 3: return (void *)c->c_coll.coll_allgather;
     case 4: return (void *)c->c_coll.coll_bcast;
+    case 5: return (void *)c->c_coll.coll_reduce;
     default: return NULL;
     }
 }
@@ -402,6 +407,9 @@ static int st_allgather(void *s, int sc, struct ompi_datatype_t *sd, void *r, in
 static int st_bcast(void *b, int n, struct ompi_datatype_t *d, int root, struct ompi_communicator_t *c,
                     mca_coll_base_module_t *m)
 { (void)b; (void)n; (void)d; (void)root; (void)c; (void)m; stub_calls[4]++; return stub_marker; }
+static int st_reduce(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o, int root,
+                     struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{ (void)s; (void)r; (void)n; (void)d; (void)o; (void)root; (void)c; (void)m; stub_calls[5]++; return stub_marker; }
 
 mca_coll_base_module_t *mini_stub_module(void)
 {
@@ -411,6 +419,7 @@ mca_coll_base_module_t *mini_stub_module(void)
     m->coll_reduce_scatter = st_rs;
     m->coll_allgather = st_allgather;
     m->coll_bcast = st_bcast;
+    m->coll_reduce = st_reduce;
     return m;
 }
 int mini_stub_calls(int which) { return (which >= 0 && which < 8) ? stub_calls[which] : -1; }

@@ -30,6 +30,8 @@ typedef struct mca_coll_mi355x_module_t {
     mca_coll_base_module_t *prev_allgather_module;
     mca_coll_base_module_bcast_fn_t prev_bcast;
     mca_coll_base_module_t *prev_bcast_module;
+    mca_coll_base_module_reduce_fn_t prev_reduce;
+    mca_coll_base_module_t *prev_reduce_module;
     /* GPU-convertor layouts of the derived datatypes seen on this communicator, and the packed
      * staging buffer (device memory; registered once, re-registered when it grows) */
     struct ddt_slot { uint64_t sig; const void *dt; mi355x_ddt_t *d; } ddt_cache[8];
@@ -57,6 +59,7 @@ static void module_destruct(opal_object_t *o)
     release_prev(m->prev_reduce_scatter_block_module);
     release_prev(m->prev_allgather_module);
     release_prev(m->prev_bcast_module);
+    release_prev(m->prev_reduce_module);
     for (int i = 0; i < 8; ++i)
         if (m->ddt_cache[i].d) mi355x_ddt_destroy(m->ddt_cache[i].d);
     if (m->scratch) mi355x_free(m->scratch);
@@ -200,6 +203,22 @@ int mca_coll_mi355x_allreduce(void *sbuf, void *rbuf, int count, struct ompi_dat
     return map_rc(mi355x_allreduce(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)count, t, op->o_f_to_c_index, NULL));
 }
 
+/* MPI_Reduce: the root's rbuf and every rank's sbuf (MPI_IN_PLACE: the root's rbuf) on the device;
+ * a non-root's rbuf is not significant and never looked at */
+int mca_coll_mi355x_reduce(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                           int root, struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    const int me = mi355x_comm_rank_of(comm);
+    const int inplace = (sbuf == MPI_IN_PLACE);
+    const int t = reducible_type(dtype);
+    if ((me == root && !is_dev(rbuf)) || (!inplace && !is_dev(sbuf)) || (inplace && me != root) ||
+        !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 || !mi355x_op_supported(op->o_f_to_c_index, t))
+        return m->prev_reduce(sbuf, rbuf, count, dtype, op, root, comm, m->prev_reduce_module);
+    return map_rc(mi355x_reduce(m->engine, inplace ? NULL : sbuf, me == root ? rbuf : NULL, (size_t)count, t,
+                                op->o_f_to_c_index, root, NULL));
+}
+
 int mca_coll_mi355x_reduce_scatter_block(void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dtype,
                                          struct ompi_op_t *op, struct ompi_communicator_t *comm,
                                          mca_coll_base_module_t *module)
@@ -299,6 +318,7 @@ static int module_enable(mca_coll_base_module_t *module, struct ompi_communicato
     SNAP(reduce_scatter_block);
     SNAP(allgather);
     SNAP(bcast);
+    SNAP(reduce);
     /* node-unique rendezvous key: job id + communicator context id */
     const char *job = getenv("OMPI_MCA_ess_base_jobid");
     char key[128];
@@ -348,6 +368,7 @@ static mca_coll_base_module_t *component_comm_query(struct ompi_communicator_t *
     m->super.coll_reduce_scatter_block = mca_coll_mi355x_reduce_scatter_block;
     m->super.coll_allgather = mca_coll_mi355x_allgather;
     m->super.coll_bcast = mca_coll_mi355x_bcast;
+    m->super.coll_reduce = mca_coll_mi355x_reduce;
     m->super.ft_event = NULL;
     *priority = mca_coll_mi355x_priority > 100 ? 100 : mca_coll_mi355x_priority;
     return &m->super;

@@ -657,7 +657,7 @@ static int ll_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s)
     a.err = c->ll_err;
     *c->ll_err = 0;
     a.timeout_ticks = (uint64_t)(c->timeout_s * 1e8);  // s_memrealtime: 100 MHz
-    rc = (a.mode == LL_AR) ? launch_ll_slot(op, type, a, s) : launch_ll_copy(a, s);
+    rc = (a.mode == LL_AR || a.mode == LL_RED) ? launch_ll_slot(op, type, a, s) : launch_ll_copy(a, s);
     if (rc) return rc;
     MI_HIP(hipStreamSynchronize(s));
     if (__atomic_load_n(c->ll_err, __ATOMIC_ACQUIRE))
@@ -1022,6 +1022,71 @@ int mi355x_allreduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t coun
         m.nseg++;
     }
     rc = launch_multicopy(m, s);
+    if (rc) return rc;
+    return finish(c, s);
+}
+
+// MPI_Reduce to `root` (ompi_coll_tuned_reduce_intra_dec_fixed, coll_tuned_decision_fixed.c:343-446,
+// and the forced algorithms of coll_tuned_reduce.c).  sbuf NULL = MPI_IN_PLACE (root only, input in
+// rbuf); rbuf is read on the root only.  The result of every element is the reference tree's
+// expression (linear / chain / pipeline / binary / binomial), evaluated:
+//   small  : LL one-shot, every rank pushes to the root, the root evaluates;
+//   large  : owner-computes -- rank r evaluates ring block r from the n inputs and writes it
+//            straight into the root's rbuf (one phase, each link carries S/n);
+//   staged : (allocations >= ipc_max) the root evaluates everything through the staging buffers.
+int mi355x_reduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int root,
+                  void *stream)
+{
+    int rc = check_common(c, op, type);
+    if (rc) return rc;
+    if (root < 0 || root >= c->size) return set_error(MI355X_ERR_ARG, "bad root");
+    if (!sbuf && c->rank != root) return set_error(MI355X_ERR_ARG, "MPI_IN_PLACE is only valid at the root");
+    if (count == 0) return MI355X_SUCCESS;
+    hipStream_t s = resolve_stream(stream);
+    const size_t esz = mi355x_type_size(type);
+    const void *in = sbuf ? sbuf : rbuf;
+    const bool am_root = (c->rank == root);
+    if (c->size == 1) {
+        c->last_alg = RED_LINEAR;
+        if (sbuf && sbuf != rbuf) MI_HIP(hipMemcpyAsync(rbuf, sbuf, count * esz, hipMemcpyDeviceToDevice, s));
+        MI_HIP(hipStreamSynchronize(s));
+        return MI355X_SUCCESS;
+    }
+    const int ra = c->knob_reduce ? c->knob_reduce : reduce_decision(c->size, count, esz);
+    c->last_alg = ra;
+    ExprPool ep;
+    Program pr;
+    if (!compile_expr(ep, expr_reduce(ep, ra, c->size, root), c->size, &pr))
+        return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
+    if (ll_usable(c, count * esz) && (pr.is_fold || c->size <= kTreeMax)) {
+        LLArgs a;
+        std::memset(&a, 0, sizeof(a));
+        a.mode = LL_RED;
+        a.root = root;
+        a.src = in;
+        a.dst = am_root ? rbuf : nullptr;
+        a.nbytes = count * esz;
+        a.count = count;
+        a.push_mask = 1ull << root;
+        ll_program(a, pr);
+        return ll_run(c, a, op, type, s);
+    }
+    MI_HIP(hipStreamSynchronize(s));
+    const void *mine[2] = {in, am_root ? rbuf : nullptr};
+    const uint64_t sig[4] = {6, count, ((uint64_t)type << 32) | (uint64_t)op, (uint64_t)root};
+    std::vector<std::vector<void *>> P;
+    bool staged = false;
+    rc = exchange(c, 2, mine, sig, P, &staged);
+    if (rc) return rc;
+    if (staged) {
+        std::vector<size_t> boff(c->size, 0), blen(c->size, 0);
+        blen[root] = count;
+        return staged_reduce(c, op, type, pr, in, boff, blen, am_root ? rbuf : nullptr, false, nullptr, s);
+    }
+    size_t off, len;
+    ring_block(count, c->size, c->rank, &off, &len);
+    std::vector<void *> dst(1, P[1][root]);
+    rc = run_program(op, type, pr, P[0], dst, off, len, s);
     if (rc) return rc;
     return finish(c, s);
 }

@@ -64,7 +64,7 @@ struct MultiCopyArgs {
 // barrier, no per-call IPC exchange.  Parity double-buffering makes back-to-back calls safe: a
 // peer can only reuse a parity after every rank has acknowledged the call in between.
 constexpr size_t kLLChunk = 4096;  // bytes per slice = per thread block (256 threads x 16 B)
-enum { LL_AR = 0, LL_AG = 1, LL_BC = 2 };        // allreduce, allgather, bcast
+enum { LL_AR = 0, LL_AG = 1, LL_BC = 2, LL_RED = 3 };  // allreduce, allgather, bcast, reduce
 enum { LL_FOLD = 0, LL_RING = 1, LL_TREE = 2 };   // per-element program of LL_AR
 struct LLArgs {
     const void *src;                   // this rank's data (NULL: nothing to push)
@@ -82,7 +82,7 @@ struct LLArgs {
     int order[kMaxRanks];
     TreeStep steps[kTreeSteps];
 };
-int launch_ll_slot(int op, int type, const LLArgs &a, hipStream_t s);  // LL_AR
+int launch_ll_slot(int op, int type, const LLArgs &a, hipStream_t s);  // LL_AR / LL_RED
 int launch_ll_copy(const LLArgs &a, hipStream_t s);                   // LL_AG / LL_BC
 
 struct CollTune {

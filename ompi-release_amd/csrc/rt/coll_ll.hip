@@ -11,7 +11,8 @@
 //   3. waits until flag (parity, q, b) = seq for every q in its own region (bounded spin: after
 //      ~10 s it records a timeout in the host-visible error word and gives up),
 //   4. finishes locally from the slots: the reference schedule's per-element program over the n
-//      inputs (allreduce), or copies (allgather / bcast).
+//      inputs (allreduce; reduce: the root only, the others push to the root alone), or copies
+//      (allgather / bcast).
 // Slices are independent, so blocks never wait on each other.  The LL region is allocated with
 // hipDeviceMallocUncached: remote xGMI writes do not update the owner's L2, so the flags and
 // data a rank polls must never be cached there.
@@ -166,6 +167,7 @@ template <class F> __global__ __launch_bounds__(256) void k_ll_allreduce(LLArgs 
     using V = LLVec<T>;
     constexpr int EPV = 16 / sizeof(T);
     if (!ll_exchange(a)) return;
+    if (a.mode == LL_RED && a.me != a.root) return;  // reduce: only the root evaluates
     const size_t i0 = ((size_t)blockIdx.x * kLLChunk + (size_t)threadIdx.x * 16) / sizeof(T);
     if (i0 >= a.count) return;
     const int ne = (a.count - i0) < (size_t)EPV ? (int)(a.count - i0) : EPV;

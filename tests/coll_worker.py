@@ -95,6 +95,19 @@ def main():
             torch.cuda.synchronize()
             assert m.lib.mini_allreduce(comm, dx.data_ptr(), dr.data_ptr(), count, dt, op) == 0
             opdata.assert_same(tname, opname, dr.cpu().numpy().view(xs[0].dtype), outs[rank], "component allreduce")
+        # reduce to the last rank
+        count, root = 3001, size - 1
+        xs = [opdata.make(tname, count, 650 + r) for r in range(size)]
+        want = np.zeros_like(xs[0])
+        oracle.oracle_reduce.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]
+        oracle.oracle_reduce(0, size, root, count, slot, code, 0, ptrs(xs), want.ctypes.data)
+        dx = torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda()
+        dr = torch.zeros_like(dx)
+        torch.cuda.synchronize()
+        assert m.lib.mini_reduce(comm, dx.data_ptr(), dr.data_ptr() if rank == root else None, count, dt, op, root) == 0
+        if rank == root:
+            opdata.assert_same(tname, opname, dr.cpu().numpy().view(xs[0].dtype), want, "component reduce")
         # reduce_scatter_block
         rcount = 1001
         xs = [opdata.make(tname, rcount * size, 600 + r) for r in range(size)]

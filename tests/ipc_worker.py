@@ -65,6 +65,26 @@ def ll_checks(pkg, comm, rank, size, oracle, torch):
                                        f"LL allreduce alg={alg} count={count} inplace={inplace} rank={rank}")
                     assert comm.last_algorithm() == ran, (comm.last_algorithm(), ran)
     comm.set("ALLREDUCE_ALG", 0)
+    # MPI_Reduce: LL (every rank pushes to the root) and, above the LL size, owner-computes
+    oracle.oracle_reduce.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]
+    for alg in (0, 1, 2, 3, 4, 5):
+        comm.set("REDUCE_ALG", alg)
+        for opname, tname in [("SUM", "FLOAT"), ("MAXLOC", "DOUBLE_INT")]:
+            op, ty = pkg.OP[opname], pkg.T[tname]
+            for count in (3, 5001, 100_003):
+                xs = [opdata.make(tname, count, 750 + 10 * alg + r) for r in range(size)]
+                for root in (0, size - 1):
+                    want = np.zeros_like(xs[0])
+                    oracle.oracle_reduce(alg, size, root, count, ty, op, 0, ptrs(xs), want.ctypes.data)
+                    dx = torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda()
+                    dr = torch.zeros_like(dx)
+                    torch.cuda.synchronize()
+                    comm.reduce(dx.data_ptr(), dr.data_ptr() if rank == root else None, count, ty, op, root)
+                    if rank == root:
+                        opdata.assert_same(tname, opname, dr.cpu().numpy().view(xs[0].dtype), want,
+                                           f"reduce alg={alg} count={count} root={root}")
+    comm.set("REDUCE_ALG", 0)
     # back to back: 64 calls, each checked (slot parity reuse)
     x = torch.empty(1000, device="cuda")
     y = torch.empty_like(x)

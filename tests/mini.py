@@ -46,6 +46,7 @@ class Mini:
         L.mini_comm_destroy.argtypes = [vp]
         L.mini_allreduce.argtypes = [vp, vp, vp, i, vp, vp]
         L.mini_reduce_scatter_block.argtypes = [vp, vp, vp, i, vp, vp]
+        L.mini_reduce.argtypes = [vp, vp, vp, i, vp, vp, i]
         L.mini_reduce_scatter.argtypes = [vp, vp, vp, ctypes.POINTER(i), vp, vp]
         L.mini_allgather.argtypes = [vp, vp, i, vp, vp, i, vp]
         L.mini_bcast.argtypes = [vp, vp, i, vp, i]

@@ -50,7 +50,8 @@ def test_component_symbols(pkg):
         assert s in op
     coll = _exports(pkg.lib_path("mca_coll_mi355x.so"))
     for s in ("mca_coll_mi355x_component", "mca_coll_mi355x_allreduce", "mca_coll_mi355x_reduce_scatter_block",
-              "mca_coll_mi355x_reduce_scatter", "mca_coll_mi355x_allgather", "mca_coll_mi355x_bcast"):
+              "mca_coll_mi355x_reduce_scatter", "mca_coll_mi355x_allgather", "mca_coll_mi355x_bcast",
+              "mca_coll_mi355x_reduce"):
         assert s in coll
 
 
@@ -161,10 +162,10 @@ def test_coll_comm_query(monkeypatch):
     comm = m.lib.mini_comm_create(0, 4, 7)
     mod, prio = _comm_query(m, comm)
     assert mod and prio == 90
-    # the module provides exactly allreduce, reduce_scatter(_block), allgather, bcast
+    # the module provides exactly allreduce, reduce_scatter(_block), allgather, bcast, reduce
     m.lib.mini_comm_install(comm, mod)
     names = ["mca_coll_mi355x_allreduce", "mca_coll_mi355x_reduce_scatter_block", "mca_coll_mi355x_reduce_scatter",
-             "mca_coll_mi355x_allgather", "mca_coll_mi355x_bcast"]
+             "mca_coll_mi355x_allgather", "mca_coll_mi355x_bcast", "mca_coll_mi355x_reduce"]
     for which, n in enumerate(names):
         assert m.lib.mini_comm_fn(comm, which) == m.addr(m.coll, n)
     m.lib.mini_comm_destroy(comm)

@@ -111,6 +111,45 @@ def _allreduce_cases(torch, pkg, oracle, cs, n, alg, inplace):
             assert cs[0].last_algorithm() == ran
 
 
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+@pytest.mark.parametrize("alg", [0, 1, 2, 3, 4, 5])
+def test_reduce(gpu, pkg, oracle, comms, n, alg):
+    """MPI_Reduce: every tuned reduce tree (forced) and the decision, roots 0 and n-1, in place at
+    the root and not; non-roots pass no rbuf"""
+    torch = gpu
+    cs = comms(n)
+    oracle.oracle_reduce.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]
+    for c in cs:
+        c.set("REDUCE_ALG", alg)
+    try:
+        for opname, tname in CASES[:6]:
+            op, ty = pkg.OP[opname], pkg.T[tname]
+            for count in (1, 7, 40_001):
+                xs = [opdata.make(tname, count, 800 + r) for r in range(n)]
+                for root in (0, n - 1):
+                    want = np.zeros_like(xs[0])
+                    ran = oracle.oracle_reduce(alg, n, root, count, ty, op, 0, _ptrs(xs), want.ctypes.data)
+                    assert ran >= 0
+                    for inplace in (False, True):
+                        dx = [to_dev(torch, x) for x in xs]
+                        dr = dx[root].clone() if inplace else torch.zeros_like(dx[root])
+                        torch.cuda.synchronize()
+
+                        def rank(r):
+                            sb = None if (inplace and r == root) else dx[r].data_ptr()
+                            cs[r].reduce(sb, dr.data_ptr() if r == root else None, count, ty, op, root)
+
+                        run_ranks(n, rank)
+                        torch.cuda.synchronize()
+                        opdata.assert_same(tname, opname, from_dev(dr, want), want,
+                                           f"reduce n={n} alg={alg} root={root} count={count} inplace={inplace}")
+                        assert cs[0].last_algorithm() == ran
+    finally:
+        for c in cs:
+            c.set("REDUCE_ALG", 0)
+
+
 @pytest.mark.parametrize("n", [2, 3, 4, 8])
 @pytest.mark.parametrize("inplace", [False, True])
 def test_reduce_scatter_block(gpu, pkg, oracle, comms, n, inplace):
@@ -283,6 +322,28 @@ def test_staged_reduce_scatter_block(gpu, pkg, oracle, staged_comms, n, inplace)
             for r in range(n):
                 opdata.assert_same(tname, opname, from_dev(dr[r], outs[r], rcount), outs[r],
                                    f"staged rsb n={n} rcount={rcount} rank={r}")
+
+
+def test_staged_reduce(gpu, pkg, oracle, staged_comms):
+    torch = gpu
+    n = 3
+    cs = staged_comms(n)
+    oracle.oracle_reduce.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]
+    for opname, tname in CASES[:4]:
+        op, ty = pkg.OP[opname], pkg.T[tname]
+        count = 30_011
+        xs = [opdata.make(tname, count, 900 + r) for r in range(n)]
+        for root in range(n):
+            want = np.zeros_like(xs[0])
+            assert oracle.oracle_reduce(0, n, root, count, ty, op, 0, _ptrs(xs), want.ctypes.data) >= 0
+            dx = [to_dev(torch, x) for x in xs]
+            dr = torch.zeros_like(dx[0])
+            torch.cuda.synchronize()
+            run_ranks(n, lambda r: cs[r].reduce(dx[r].data_ptr(), dr.data_ptr() if r == root else None, count, ty, op,
+                                                root))
+            torch.cuda.synchronize()
+            opdata.assert_same(tname, opname, from_dev(dr, want), want, f"staged reduce root={root}")
 
 
 @pytest.mark.parametrize("rsalg", [1, 2])
