@@ -141,6 +141,27 @@ int mi355x_allgather(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t b
 /* MPI_Bcast of `bytes` contiguous bytes from `root`. */
 int mi355x_bcast(mi355x_comm_t *comm, void *buf, size_t bytes, int root, void *stream);
 
+/* Nonblocking collectives (MPI_Iallreduce, MPI_Ireduce, MPI_Ireduce_scatter_block, MPI_Iallgather,
+ * MPI_Ibcast; the coll framework's nonblocking slots, coll.h:241-356, served in the reference by
+ * coll/libnbc: nbc_iallreduce.c etc.).  Each call is queued behind the caller's prior work on
+ * `stream` and run, in posting order, by the communicator's progress thread; results are
+ * identical to the blocking call's.  A blocking collective on the same communicator first waits
+ * for every posted one.  Requests: test (non-blocking; *done = 1 once finished, then returns the
+ * collective's status), wait (blocks; returns the status), free (only once finished). */
+typedef struct mi355x_request mi355x_request_t;
+int mi355x_iallreduce(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op,
+                      void *stream, mi355x_request_t **req);
+int mi355x_ireduce(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op, int root,
+                   void *stream, mi355x_request_t **req);
+int mi355x_ireduce_scatter_block(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t rcount, int type,
+                                 int op, void *stream, mi355x_request_t **req);
+int mi355x_iallgather(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t bytes, void *stream,
+                      mi355x_request_t **req);
+int mi355x_ibcast(mi355x_comm_t *comm, void *buf, size_t bytes, int root, void *stream, mi355x_request_t **req);
+int mi355x_request_test(mi355x_request_t *req, int *done);
+int mi355x_request_wait(mi355x_request_t *req);
+int mi355x_request_free(mi355x_request_t *req);
+
 /* ---------------------------------------------------------------- GPU convertor */
 /* A datatype layout: instance k at base + k*extent; inside it nblk blocks at j*stride; inside a
  * block the runs (disp, len) in order.  The packed stream is that type map in order, as

@@ -107,6 +107,14 @@ def _declare(lib: ctypes.CDLL) -> None:
         "mi355x_allreduce": (i, [vp, vp, vp, sz, i, i, vp]),
         "mi355x_reduce_scatter_block": (i, [vp, vp, vp, sz, i, i, vp]),
         "mi355x_reduce": (i, [vp, vp, vp, sz, i, i, i, vp]),
+        "mi355x_iallreduce": (i, [vp, vp, vp, sz, i, i, vp, c.POINTER(vp)]),
+        "mi355x_ireduce": (i, [vp, vp, vp, sz, i, i, i, vp, c.POINTER(vp)]),
+        "mi355x_ireduce_scatter_block": (i, [vp, vp, vp, sz, i, i, vp, c.POINTER(vp)]),
+        "mi355x_iallgather": (i, [vp, vp, vp, sz, vp, c.POINTER(vp)]),
+        "mi355x_ibcast": (i, [vp, vp, sz, i, vp, c.POINTER(vp)]),
+        "mi355x_request_test": (i, [vp, c.POINTER(i)]),
+        "mi355x_request_wait": (i, [vp]),
+        "mi355x_request_free": (i, [vp]),
         "mi355x_reduce_scatter": (i, [vp, vp, vp, c.POINTER(i), i, i, vp]),
         "mi355x_allgather": (i, [vp, vp, vp, sz, vp]),
         "mi355x_bcast": (i, [vp, vp, sz, i, vp]),
@@ -229,6 +237,26 @@ class Comm:
     def allreduce(self, sbuf, rbuf, count, ty, op, stream=None) -> None:
         check(rt().mi355x_allreduce(self.h, sbuf, rbuf, count, ty, op, stream), "mi355x_allreduce")
 
+    def _post(self, fn, *args) -> Request:
+        h = ctypes.c_void_p()
+        check(getattr(rt(), fn)(self.h, *args, ctypes.byref(h)), fn)
+        return Request(h.value)
+
+    def iallreduce(self, sbuf, rbuf, count, ty, op, stream=None) -> Request:
+        return self._post("mi355x_iallreduce", sbuf, rbuf, count, ty, op, stream)
+
+    def ireduce(self, sbuf, rbuf, count, ty, op, root, stream=None) -> Request:
+        return self._post("mi355x_ireduce", sbuf, rbuf, count, ty, op, root, stream)
+
+    def ireduce_scatter_block(self, sbuf, rbuf, rcount, ty, op, stream=None) -> Request:
+        return self._post("mi355x_ireduce_scatter_block", sbuf, rbuf, rcount, ty, op, stream)
+
+    def iallgather(self, sbuf, rbuf, nbytes, stream=None) -> Request:
+        return self._post("mi355x_iallgather", sbuf, rbuf, nbytes, stream)
+
+    def ibcast(self, buf, nbytes, root, stream=None) -> Request:
+        return self._post("mi355x_ibcast", buf, nbytes, root, stream)
+
     def reduce(self, sbuf, rbuf, count, ty, op, root, stream=None) -> None:
         check(rt().mi355x_reduce(self.h, sbuf, rbuf, count, ty, op, root, stream), "mi355x_reduce")
 
@@ -245,6 +273,25 @@ class Comm:
 
     def bcast(self, buf, nbytes, root, stream=None) -> None:
         check(rt().mi355x_bcast(self.h, buf, nbytes, root, stream), "mi355x_bcast")
+
+
+class Request:
+    """A posted nonblocking collective (mi355x_request_t)."""
+
+    def __init__(self, h: int):
+        self.h = ctypes.c_void_p(h)
+
+    def test(self) -> bool:
+        done = ctypes.c_int(0)
+        check(rt().mi355x_request_test(self.h, ctypes.byref(done)), "mi355x_request_test")
+        return bool(done.value)
+
+    def wait(self) -> None:
+        try:
+            check(rt().mi355x_request_wait(self.h), "mi355x_request_wait")
+        finally:
+            rt().mi355x_request_free(self.h)
+            self.h = ctypes.c_void_p()
 
 
 class Ddt:

@@ -33,6 +33,9 @@
 #include <array>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -40,6 +43,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "coll_internal.hpp"
@@ -137,6 +141,14 @@ struct LoopShared {
 
 } // namespace mi355x
 
+struct mi355x_request {
+    std::atomic<int> done{0};
+    int rc = MI355X_SUCCESS;
+    std::string err;
+    std::function<int(hipStream_t)> run;  // the blocking algorithm, on the progress stream
+    hipEvent_t ev = nullptr;              // the caller-stream point the call starts after
+};
+
 struct mi355x_comm {
     int rank = 0, size = 1, device = 0;
     mi355x::Ctrl *ctrl = nullptr;
@@ -158,6 +170,15 @@ struct mi355x_comm {
     std::vector<char *> ll_peer;                  // every rank's LL region, mapped
     uint64_t ll_seq = 0;
     uint32_t *ll_err = nullptr;                   // host-visible timeout word
+    // nonblocking collectives: one progress thread per communicator runs the posted calls in
+    // order on its own stream; blocking calls first wait until nothing is pending
+    std::thread worker;
+    std::mutex q_mtx;
+    std::condition_variable q_cv;
+    std::deque<mi355x_request *> queue;
+    bool stop = false;
+    int pending = 0;                              // posted, not finished (guarded by q_mtx)
+    hipStream_t nb_stream = nullptr;
     int knob_allreduce = 0, knob_reduce = 0, knob_rs = 0;
     int last_alg = -1;
     double timeout_s = 600.0;
@@ -694,6 +715,72 @@ static double env_double(const char *name, double dflt)
     return v ? atof(v) : dflt;
 }
 
+// ----------------------------------------------------------------- nonblocking
+// Wait until every posted nonblocking call of this communicator has finished (MPI orders a
+// blocking collective after the nonblocking ones posted before it on every rank).
+static void drain(mi355x_comm *c)
+{
+    std::unique_lock<std::mutex> g(c->q_mtx);
+    c->q_cv.wait(g, [c] { return c->pending == 0; });
+}
+
+static void worker_main(mi355x_comm *c)
+{
+    (void)hipSetDevice(c->device);
+    for (;;) {
+        mi355x_request *r;
+        {
+            std::unique_lock<std::mutex> g(c->q_mtx);
+            c->q_cv.wait(g, [c] { return c->stop || !c->queue.empty(); });
+            if (c->queue.empty()) return;  // stop requested and nothing left
+            r = c->queue.front();
+            c->queue.pop_front();
+        }
+        int rc = MI355X_SUCCESS;
+        if (hipStreamWaitEvent(c->nb_stream, r->ev, 0) != hipSuccess)
+            rc = set_error(MI355X_ERR_HIP, "hipStreamWaitEvent failed");
+        if (rc == MI355X_SUCCESS) rc = r->run(c->nb_stream);
+        r->rc = rc;
+        if (rc != MI355X_SUCCESS) r->err = mi355x_last_error();
+        r->run = nullptr;
+        r->done.store(1, std::memory_order_release);
+        {
+            std::lock_guard<std::mutex> g(c->q_mtx);
+            c->pending--;
+        }
+        c->q_cv.notify_all();
+    }
+}
+
+// queue `run` after the caller's work on `stream`; the request completes when it has run
+static int post(mi355x_comm *c, void *stream, std::function<int(hipStream_t)> run, mi355x_request **out)
+{
+    if (!out) return set_error(MI355X_ERR_ARG, "request pointer is NULL");
+    *out = nullptr;
+    if (!c->nb_stream) {
+        MI_HIP(hipSetDevice(c->device));
+        MI_HIP(hipStreamCreateWithFlags(&c->nb_stream, hipStreamNonBlocking));
+    }
+    auto *r = new mi355x_request();
+    hipError_t e = hipEventCreateWithFlags(&r->ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(r->ev, resolve_stream(stream));
+    if (e != hipSuccess) {
+        if (r->ev) (void)hipEventDestroy(r->ev);
+        delete r;
+        return set_error(MI355X_ERR_HIP, "event on the caller stream: %s", hipGetErrorString(e));
+    }
+    r->run = std::move(run);
+    {
+        std::lock_guard<std::mutex> g(c->q_mtx);
+        if (!c->worker.joinable()) c->worker = std::thread(worker_main, c);
+        c->queue.push_back(r);
+        c->pending++;
+    }
+    c->q_cv.notify_all();
+    *out = r;
+    return MI355X_SUCCESS;
+}
+
 } // namespace mi355x
 
 using namespace mi355x;
@@ -805,7 +892,16 @@ int mi355x_comm_create_loopback(int size, int device, mi355x_comm_t **comms)
 int mi355x_comm_destroy(mi355x_comm_t *c)
 {
     if (!c) return MI355X_SUCCESS;
+    if (c->worker.joinable()) {
+        {
+            std::lock_guard<std::mutex> g(c->q_mtx);
+            c->stop = true;
+        }
+        c->q_cv.notify_all();
+        c->worker.join();
+    }
     (void)hipSetDevice(c->device);
+    if (c->nb_stream) (void)hipStreamDestroy(c->nb_stream);
     for (auto &kv : c->peer_maps) (void)hipIpcCloseMemHandle(kv.second.mapped);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->stage) (void)hipFree(c->stage);
@@ -823,7 +919,12 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
 
 int mi355x_comm_rank(const mi355x_comm_t *c) { return c ? c->rank : -1; }
 int mi355x_comm_size(const mi355x_comm_t *c) { return c ? c->size : -1; }
-int mi355x_comm_barrier(mi355x_comm_t *c) { return c ? barrier(c) : set_error(MI355X_ERR_ARG, "comm is NULL"); }
+int mi355x_comm_barrier(mi355x_comm_t *c)
+{
+    if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    drain(c);
+    return barrier(c);
+}
 int mi355x_comm_last_algorithm(const mi355x_comm_t *c) { return c ? c->last_alg : -1; }
 
 int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
@@ -906,7 +1007,7 @@ int mi355x_sched_program(int kind, int n, int alg, int block, int *out, int cap)
 }
 
 // MPI_Allreduce (coll_tuned_allreduce_intra_dec_fixed order; sbuf NULL = MPI_IN_PLACE)
-int mi355x_allreduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op,
+static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op,
                      void *stream)
 {
     int rc = check_common(c, op, type);
@@ -1034,7 +1135,7 @@ int mi355x_allreduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t coun
 //   large  : owner-computes -- rank r evaluates ring block r from the n inputs and writes it
 //            straight into the root's rbuf (one phase, each link carries S/n);
 //   staged : (allocations >= ipc_max) the root evaluates everything through the staging buffers.
-int mi355x_reduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int root,
+static int reduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int root,
                   void *stream)
 {
     int rc = check_common(c, op, type);
@@ -1093,7 +1194,7 @@ int mi355x_reduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, 
 
 // MPI_Reduce_scatter_block as coll/basic runs it: tuned reduce to 0 + scatter
 // (coll_basic_reduce_scatter_block.c:54-111); sbuf NULL = MPI_IN_PLACE (input in rbuf).
-int mi355x_reduce_scatter_block(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t rcount, int type,
+static int reduce_scatter_block_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t rcount, int type,
                                 int op, void *stream)
 {
     int rc = check_common(c, op, type);
@@ -1147,7 +1248,7 @@ int mi355x_reduce_scatter_block(mi355x_comm_t *c, const void *sbuf, void *rbuf, 
 }
 
 // MPI_Reduce_scatter with vector counts (coll_tuned_reduce_scatter_intra_dec_fixed order)
-int mi355x_reduce_scatter(mi355x_comm_t *c, const void *sbuf, void *rbuf, const int *rcounts, int type,
+static int reduce_scatter_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, const int *rcounts, int type,
                           int op, void *stream)
 {
     int rc = check_common(c, op, type);
@@ -1219,7 +1320,7 @@ int mi355x_reduce_scatter(mi355x_comm_t *c, const void *sbuf, void *rbuf, const 
 
 // MPI_Allgather of `bytes` per rank (contiguous); sbuf NULL = MPI_IN_PLACE.  Pull: one launch
 // copies every peer's block concurrently (one segment per peer -> every link busy).
-int mi355x_allgather(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, void *stream)
+static int allgather_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, void *stream)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     if (bytes == 0) return MI355X_SUCCESS;
@@ -1277,7 +1378,7 @@ int mi355x_allgather(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t byte
 // root.  Large: scatter + allgather shape (each rank first pulls its slice from the root, then the
 // other slices from their owners), so each xGMI link carries ~2/n of the message instead of the
 // root's links carrying all of it.
-int mi355x_bcast(mi355x_comm_t *c, void *buf, size_t bytes, int root, void *stream)
+static int bcast_impl(mi355x_comm_t *c, void *buf, size_t bytes, int root, void *stream)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     if (root < 0 || root >= c->size) return set_error(MI355X_ERR_ARG, "bad root");
@@ -1345,6 +1446,110 @@ int mi355x_bcast(mi355x_comm_t *c, void *buf, size_t bytes, int root, void *stre
         if (rc) return rc;
     }
     return finish(c, s);
+}
+
+// ----------------------------------------------------------------- public entry points
+int mi355x_allreduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, void *stream)
+{
+    if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    drain(c);
+    return allreduce_impl(c, sbuf, rbuf, count, type, op, stream);
+}
+int mi355x_reduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int root,
+                  void *stream)
+{
+    if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    drain(c);
+    return reduce_impl(c, sbuf, rbuf, count, type, op, root, stream);
+}
+int mi355x_reduce_scatter_block(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t rcount, int type, int op,
+                                void *stream)
+{
+    if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    drain(c);
+    return reduce_scatter_block_impl(c, sbuf, rbuf, rcount, type, op, stream);
+}
+int mi355x_reduce_scatter(mi355x_comm_t *c, const void *sbuf, void *rbuf, const int *rcounts, int type, int op,
+                          void *stream)
+{
+    if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    drain(c);
+    return reduce_scatter_impl(c, sbuf, rbuf, rcounts, type, op, stream);
+}
+int mi355x_allgather(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, void *stream)
+{
+    if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    drain(c);
+    return allgather_impl(c, sbuf, rbuf, bytes, stream);
+}
+int mi355x_bcast(mi355x_comm_t *c, void *buf, size_t bytes, int root, void *stream)
+{
+    if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    drain(c);
+    return bcast_impl(c, buf, bytes, root, stream);
+}
+
+// nonblocking: argument checks at post time, the collective itself on the progress thread
+int mi355x_iallreduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, void *stream,
+                      mi355x_request_t **req)
+{
+    int rc = check_common(c, op, type);
+    if (rc) return rc;
+    return post(c, stream, [=](hipStream_t s) { return allreduce_impl(c, sbuf, rbuf, count, type, op, s); }, req);
+}
+int mi355x_ireduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int root,
+                   void *stream, mi355x_request_t **req)
+{
+    int rc = check_common(c, op, type);
+    if (rc) return rc;
+    if (root < 0 || root >= c->size) return set_error(MI355X_ERR_ARG, "bad root");
+    return post(c, stream, [=](hipStream_t s) { return reduce_impl(c, sbuf, rbuf, count, type, op, root, s); }, req);
+}
+int mi355x_ireduce_scatter_block(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t rcount, int type, int op,
+                                 void *stream, mi355x_request_t **req)
+{
+    int rc = check_common(c, op, type);
+    if (rc) return rc;
+    return post(c, stream,
+                [=](hipStream_t s) { return reduce_scatter_block_impl(c, sbuf, rbuf, rcount, type, op, s); }, req);
+}
+int mi355x_iallgather(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, void *stream,
+                      mi355x_request_t **req)
+{
+    if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    return post(c, stream, [=](hipStream_t s) { return allgather_impl(c, sbuf, rbuf, bytes, s); }, req);
+}
+int mi355x_ibcast(mi355x_comm_t *c, void *buf, size_t bytes, int root, void *stream, mi355x_request_t **req)
+{
+    if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    if (root < 0 || root >= c->size) return set_error(MI355X_ERR_ARG, "bad root");
+    return post(c, stream, [=](hipStream_t s) { return bcast_impl(c, buf, bytes, root, s); }, req);
+}
+
+int mi355x_request_test(mi355x_request_t *r, int *done)
+{
+    if (!r || !done) return set_error(MI355X_ERR_ARG, "NULL request");
+    *done = r->done.load(std::memory_order_acquire);
+    if (*done && r->rc != MI355X_SUCCESS) return set_error(r->rc, "%s", r->err.c_str());
+    return MI355X_SUCCESS;
+}
+int mi355x_request_wait(mi355x_request_t *r)
+{
+    if (!r) return set_error(MI355X_ERR_ARG, "NULL request");
+    unsigned spins = 0;
+    while (!r->done.load(std::memory_order_acquire)) {
+        if (++spins > 64) sched_yield();
+    }
+    if (r->rc != MI355X_SUCCESS) return set_error(r->rc, "%s", r->err.c_str());
+    return MI355X_SUCCESS;
+}
+int mi355x_request_free(mi355x_request_t *r)
+{
+    if (!r) return MI355X_SUCCESS;
+    if (!r->done.load(std::memory_order_acquire)) return set_error(MI355X_ERR_ARG, "request still active");
+    if (r->ev) (void)hipEventDestroy(r->ev);
+    delete r;
+    return MI355X_SUCCESS;
 }
 
 } // extern "C"

@@ -109,6 +109,16 @@ def ll_checks(pkg, comm, rank, size, oracle, torch):
             torch.cuda.synchronize()
             comm.bcast(b.data_ptr(), nb, root)
             assert int(b.min()) == root == int(b.max()), ("LL bcast", nb, root)
+    # nonblocking through the progress thread: an LL-sized and a large allreduce posted together
+    xs = torch.full((1000,), float(rank + 1), device="cuda")
+    xl = torch.full((3_000_000,), float(rank + 1), device="cuda")
+    ys, yl = torch.empty_like(xs), torch.empty_like(xl)
+    reqs = [comm.iallreduce(xs.data_ptr(), ys.data_ptr(), xs.numel(), pkg.T["FLOAT"], pkg.OP["SUM"]),
+            comm.iallreduce(xl.data_ptr(), yl.data_ptr(), xl.numel(), pkg.T["FLOAT"], pkg.OP["SUM"])]
+    for q in reqs:
+        q.wait()
+    want = size * (size + 1) / 2
+    assert bool(torch.all(ys == want)) and bool(torch.all(yl == want)), "nonblocking allreduce"
     print(f"rank {rank} LL OK", flush=True)
 
 

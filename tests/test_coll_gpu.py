@@ -416,3 +416,61 @@ def test_staged_bcast(gpu, pkg, staged_comms, n, nbytes):
     finally:
         for c in cs:
             c.set("STAGE_BYTES", 64 << 10)
+
+
+@pytest.mark.parametrize("n", [2, 3, 5])
+def test_nonblocking(gpu, pkg, oracle, comms, n):
+    """MPI_I* collectives: several posted back to back on every rank, then a blocking allreduce
+    (ordered after them), then all waited -- each result bit-identical to the oracle's schedule"""
+    torch = gpu
+    cs = comms(n)
+    oracle.oracle_reduce.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]
+    op, ty = pkg.OP["SUM"], pkg.T["FLOAT"]
+    count, rcount, nb = 50_001, 7001, 100_003
+    xa = [opdata.make("FLOAT", count, 1000 + r) for r in range(n)]
+    wa = [np.zeros_like(xa[0]) for _ in range(n)]
+    assert oracle.oracle_allreduce(0, n, count, ty, op, 0, _ptrs(xa), _ptrs(wa)) >= 0
+    xb = [opdata.make("FLOAT", rcount * n, 1100 + r) for r in range(n)]
+    wb = [np.zeros(rcount, dtype=np.float32) for _ in range(n)]
+    assert oracle.oracle_reduce_scatter_block(n, rcount, ty, op, _ptrs(xb), _ptrs(wb)) >= 0
+    wr = np.zeros_like(xa[0])
+    assert oracle.oracle_reduce(0, n, n - 1, count, ty, op, 0, _ptrs(xa), wr.ctypes.data) >= 0
+    xc = [opdata.make("FLOAT", count, 1200 + r) for r in range(n)]
+    wc = [np.zeros_like(xc[0]) for _ in range(n)]
+    assert oracle.oracle_allreduce(0, n, count, ty, op, 0, _ptrs(xc), _ptrs(wc)) >= 0
+    da = [to_dev(torch, x) for x in xa]
+    ra = [torch.zeros_like(t) for t in da]
+    db = [to_dev(torch, x) for x in xb]
+    rb = [torch.zeros(rcount * 4, dtype=torch.uint8, device="cuda") for _ in range(n)]
+    rr = torch.zeros_like(da[0])
+    gsrc = [torch.randint(0, 256, (nb,), dtype=torch.uint8, device="cuda") for _ in range(n)]
+    gdst = [torch.zeros(n * nb, dtype=torch.uint8, device="cuda") for _ in range(n)]
+    bb = [torch.randint(0, 256, (nb,), dtype=torch.uint8, device="cuda") for _ in range(n)]
+    bwant = bb[0].clone()
+    dc = [to_dev(torch, x) for x in xc]
+    rc = [torch.zeros_like(t) for t in dc]
+    torch.cuda.synchronize()
+
+    def rank(r):
+        c = cs[r]
+        reqs = [c.iallreduce(da[r].data_ptr(), ra[r].data_ptr(), count, ty, op),
+                c.ireduce_scatter_block(db[r].data_ptr(), rb[r].data_ptr(), rcount, ty, op),
+                c.ireduce(da[r].data_ptr(), rr.data_ptr() if r == n - 1 else None, count, ty, op, n - 1),
+                c.iallgather(gsrc[r].data_ptr(), gdst[r].data_ptr(), nb),
+                c.ibcast(bb[r].data_ptr(), nb, 0)]
+        c.allreduce(dc[r].data_ptr(), rc[r].data_ptr(), count, ty, op)  # waits for the posted ones
+        assert all(q.test() for q in reqs)
+        for q in reqs:
+            q.wait()
+
+    run_ranks(n, rank)
+    torch.cuda.synchronize()
+    want_g = torch.cat(gsrc)
+    for r in range(n):
+        opdata.assert_same("FLOAT", "SUM", from_dev(ra[r], wa[r]), wa[r], f"iallreduce rank={r}")
+        opdata.assert_same("FLOAT", "SUM", from_dev(rb[r], wb[r], rcount), wb[r], f"ireduce_scatter_block rank={r}")
+        opdata.assert_same("FLOAT", "SUM", from_dev(rc[r], wc[r]), wc[r], f"blocking after nonblocking rank={r}")
+        assert torch.equal(gdst[r], want_g), r
+        assert torch.equal(bb[r], bwant), r
+    opdata.assert_same("FLOAT", "SUM", from_dev(rr, wr), wr, "ireduce")
