@@ -3,7 +3,8 @@
  *
  * Plugs into the coll framework (ompi/mca/coll/coll.h:357-451) at priority 90 -- above
  * coll/tuned (30) and coll/cuda (78) -- for intra-communicators whose ranks all live on this
- * node.  It provides allreduce, reduce, reduce_scatter, reduce_scatter_block, allgather and bcast; every
+ * node.  It provides allreduce, reduce, reduce_scatter, reduce_scatter_block, allgather and bcast, and
+ * the nonblocking iallreduce, ireduce, ireduce_scatter_block, iallgather and ibcast; every
  * other slot stays with the lower-priority modules.  Entry points have exactly the reference
  * signatures (coll.h:181-239) and replace, for device buffers:
  *   mca_coll_cuda_allreduce            (ompi/mca/coll/cuda/coll_cuda_allreduce.c:30-77)
@@ -39,6 +40,21 @@ int mca_coll_mi355x_allreduce(void *sbuf, void *rbuf, int count, struct ompi_dat
                               mca_coll_base_module_t *module);
 int mca_coll_mi355x_reduce(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
                            int root, struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+/* nonblocking (coll.h:241-356; reference: coll/libnbc) */
+int mca_coll_mi355x_iallreduce(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                               struct ompi_communicator_t *comm, ompi_request_t **request,
+                               mca_coll_base_module_t *module);
+int mca_coll_mi355x_ireduce(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                            int root, struct ompi_communicator_t *comm, ompi_request_t **request,
+                            mca_coll_base_module_t *module);
+int mca_coll_mi355x_ireduce_scatter_block(void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dtype,
+                                          struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                                          ompi_request_t **request, mca_coll_base_module_t *module);
+int mca_coll_mi355x_iallgather(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
+                               struct ompi_datatype_t *rdtype, struct ompi_communicator_t *comm,
+                               ompi_request_t **request, mca_coll_base_module_t *module);
+int mca_coll_mi355x_ibcast(void *buff, int count, struct ompi_datatype_t *datatype, int root,
+                           struct ompi_communicator_t *comm, ompi_request_t **request, mca_coll_base_module_t *module);
 int mca_coll_mi355x_reduce_scatter_block(void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dtype,
                                          struct ompi_op_t *op, struct ompi_communicator_t *comm,
                                          mca_coll_base_module_t *module);

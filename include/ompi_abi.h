@@ -256,6 +256,124 @@ typedef struct ompi_group_t {
     struct ompi_group_t *grp_parent_group_ptr;
 } ompi_group_t;
 
+/* ---- requests (the nonblocking collective slots hand one back) ------------------------------ */
+/* opal/class/opal_list.h:100-116 (non-debug) */
+typedef struct opal_list_item_t {
+    opal_object_t super;
+    volatile struct opal_list_item_t *opal_list_next;
+    volatile struct opal_list_item_t *opal_list_prev;
+    int32_t item_free;
+} opal_list_item_t;
+
+/* ompi/class/ompi_free_list.h:62-67 */
+typedef struct ompi_free_list_item_t {
+    opal_list_item_t super;
+    struct mca_mpool_base_registration_t *registration;
+    void *ptr;
+} ompi_free_list_item_t;
+
+/* ompi/include/mpi.h.in:344-356 */
+typedef struct ompi_status_public_t {
+    int MPI_SOURCE;
+    int MPI_TAG;
+    int MPI_ERROR;
+    int _cancelled;
+    size_t _ucount;
+} ompi_status_public_t;
+
+/* ompi/request/request_dbg.h:25-50 */
+typedef enum {
+    OMPI_REQUEST_PML, OMPI_REQUEST_IO, OMPI_REQUEST_GEN, OMPI_REQUEST_WIN, OMPI_REQUEST_COLL,
+    OMPI_REQUEST_NULL, OMPI_REQUEST_NOOP, OMPI_REQUEST_COMM, OMPI_REQUEST_MAX
+} ompi_request_type_t;
+typedef enum {
+    OMPI_REQUEST_INVALID, OMPI_REQUEST_INACTIVE, OMPI_REQUEST_ACTIVE, OMPI_REQUEST_CANCELLED
+} ompi_request_state_t;
+
+struct ompi_request_t;
+/* ompi/request/request.h:58-78 */
+typedef int (*ompi_request_free_fn_t)(struct ompi_request_t **rptr);
+typedef int (*ompi_request_cancel_fn_t)(struct ompi_request_t *request, int flag);
+typedef int (*ompi_request_complete_fn_t)(struct ompi_request_t *request);
+typedef union ompi_mpi_object_t {
+    struct ompi_communicator_t *comm;
+    struct ompi_file_t *file;
+    struct ompi_win_t *win;
+} ompi_mpi_object_t;
+
+/* ompi/request/request.h:98-110 */
+typedef struct ompi_request_t {
+    ompi_free_list_item_t super;
+    ompi_request_type_t req_type;
+    ompi_status_public_t req_status;
+    volatile bool req_complete;
+    volatile ompi_request_state_t req_state;
+    bool req_persistent;
+    int req_f_to_c_index;
+    ompi_request_free_fn_t req_free;
+    ompi_request_cancel_fn_t req_cancel;
+    ompi_request_complete_fn_t req_complete_cb;
+    void *req_complete_cb_data;
+    ompi_mpi_object_t req_mpi_object;
+} ompi_request_t;
+
+/* request.h:122-127: MPI_REQUEST_NULL is &ompi_request_null.request */
+typedef struct ompi_predefined_request_t {
+    ompi_request_t request;
+    char padding[sizeof(void *) * 32 - sizeof(ompi_request_t)];
+} ompi_predefined_request_t;
+
+/* opal/threads/condition.h:46-50 */
+typedef struct opal_condition_t {
+    opal_object_t super;
+    volatile int c_waiting;
+    volatile int c_signaled;
+} opal_condition_t;
+
+#define MPI_UNDEFINED (-32766)  /* mpi.h.in:423 */
+#define MPI_ERR_REQUEST 7       /* mpi.h.in:539 */
+#define MPI_ERR_INTERN 17       /* mpi.h.in:549 */
+
+/* exported by libmpi (request.c) / libopen-pal (opal_progress.c), or by the harness */
+extern opal_class_t ompi_request_t_class;
+extern size_t ompi_request_waiting;
+extern size_t ompi_request_completed;
+extern size_t ompi_request_failed;
+extern opal_condition_t ompi_request_cond;
+extern ompi_predefined_request_t ompi_request_null;
+struct opal_pointer_array_t;
+extern struct opal_pointer_array_t ompi_request_f_to_c_table;
+int opal_pointer_array_set_item(struct opal_pointer_array_t *array, int index, void *value);
+typedef int (*opal_progress_callback_t)(void);
+int opal_progress_register(opal_progress_callback_t cb);
+int opal_progress_unregister(opal_progress_callback_t cb);
+
+/* OMPI_REQUEST_FINI (request.h:161-169) */
+static inline void mi355x_ompi_request_fini(ompi_request_t *request)
+{
+    request->req_state = OMPI_REQUEST_INVALID;
+    if (MPI_UNDEFINED != request->req_f_to_c_index) {
+        opal_pointer_array_set_item(&ompi_request_f_to_c_table, request->req_f_to_c_index, NULL);
+        request->req_f_to_c_index = MPI_UNDEFINED;
+    }
+}
+
+/* ompi_request_complete (request.h:397-416; opal_condition_broadcast, condition.h:138-142, is
+ * `c_signaled = c_waiting`), restated because it is static inline in the reference */
+static inline int mi355x_ompi_request_complete(ompi_request_t *request, bool with_signal)
+{
+    ompi_request_complete_fn_t tmp = request->req_complete_cb;
+    if (NULL != tmp) {
+        request->req_complete_cb = NULL;
+        tmp(request);
+    }
+    ompi_request_completed++;
+    request->req_complete = true;
+    if (0 != request->req_status.MPI_ERROR) ompi_request_failed++;
+    if (with_signal && ompi_request_waiting) ompi_request_cond.c_signaled = ompi_request_cond.c_waiting;
+    return OMPI_SUCCESS;
+}
+
 struct ompi_communicator_t;
 struct mca_coll_base_module_2_0_0_t;
 typedef struct mca_coll_base_module_2_0_0_t mca_coll_base_module_t;
@@ -279,6 +397,25 @@ typedef int (*mca_coll_base_module_reduce_scatter_block_fn_t)(void *sbuf, void *
                                                               struct ompi_datatype_t *dtype, struct ompi_op_t *op,
                                                               struct ompi_communicator_t *comm,
                                                               mca_coll_base_module_t *module);
+/* coll.h:241-356 (the nonblocking slots coll/mi355x provides) */
+typedef int (*mca_coll_base_module_iallgather_fn_t)(void *sbuf, int scount, struct ompi_datatype_t *sdtype,
+                                                    void *rbuf, int rcount, struct ompi_datatype_t *rdtype,
+                                                    struct ompi_communicator_t *comm, ompi_request_t **request,
+                                                    mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_iallreduce_fn_t)(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                                                    struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                                                    ompi_request_t **request, mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_ibcast_fn_t)(void *buff, int count, struct ompi_datatype_t *datatype, int root,
+                                                struct ompi_communicator_t *comm, ompi_request_t **request,
+                                                mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_ireduce_fn_t)(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                                                 struct ompi_op_t *op, int root, struct ompi_communicator_t *comm,
+                                                 ompi_request_t **request, mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_ireduce_scatter_block_fn_t)(void *sbuf, void *rbuf, int rcount,
+                                                               struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                                               struct ompi_communicator_t *comm,
+                                                               ompi_request_t **request,
+                                                               mca_coll_base_module_t *module);
 typedef int (*mca_coll_base_module_enable_fn_t)(mca_coll_base_module_t *module, struct ompi_communicator_t *comm);
 typedef int (*mca_coll_base_module_ft_event_fn_t)(int state);
 typedef void (*mca_coll_base_any_fn_t)(void);   /* slots the components never call */
@@ -304,7 +441,17 @@ struct mca_coll_base_module_2_0_0_t {
     mca_coll_base_any_fn_t coll_scan;
     mca_coll_base_any_fn_t coll_scatter;
     mca_coll_base_any_fn_t coll_scatterv;
-    mca_coll_base_any_fn_t coll_nonblocking[17];
+    /* coll.h:418-434 */
+    mca_coll_base_module_iallgather_fn_t coll_iallgather;
+    mca_coll_base_any_fn_t coll_iallgatherv;
+    mca_coll_base_module_iallreduce_fn_t coll_iallreduce;
+    mca_coll_base_any_fn_t coll_ialltoall, coll_ialltoallv, coll_ialltoallw, coll_ibarrier;
+    mca_coll_base_module_ibcast_fn_t coll_ibcast;
+    mca_coll_base_any_fn_t coll_iexscan, coll_igather, coll_igatherv;
+    mca_coll_base_module_ireduce_fn_t coll_ireduce;
+    mca_coll_base_any_fn_t coll_ireduce_scatter;
+    mca_coll_base_module_ireduce_scatter_block_fn_t coll_ireduce_scatter_block;
+    mca_coll_base_any_fn_t coll_iscan, coll_iscatter, coll_iscatterv;
     mca_coll_base_any_fn_t coll_neighbor[10];
     mca_coll_base_module_ft_event_fn_t ft_event;
 };
@@ -330,7 +477,24 @@ typedef struct mca_coll_base_comm_coll_t {
     mca_coll_base_module_t *coll_reduce_scatter_module;
     mca_coll_base_module_reduce_scatter_block_fn_t coll_reduce_scatter_block;
     mca_coll_base_module_t *coll_reduce_scatter_block_module;
-    struct { mca_coll_base_any_fn_t fn; mca_coll_base_module_t *module; } coll_rest[3 + 17 + 10];
+    struct { mca_coll_base_any_fn_t fn; mca_coll_base_module_t *module; } coll_sss[3];  /* scan, scatter(v) */
+    /* coll.h:505-540 */
+    mca_coll_base_module_iallgather_fn_t coll_iallgather;
+    mca_coll_base_module_t *coll_iallgather_module;
+    struct { mca_coll_base_any_fn_t fn; mca_coll_base_module_t *module; } coll_iallgatherv_pair;
+    mca_coll_base_module_iallreduce_fn_t coll_iallreduce;
+    mca_coll_base_module_t *coll_iallreduce_module;
+    struct { mca_coll_base_any_fn_t fn; mca_coll_base_module_t *module; } coll_ia2a[4];  /* ialltoall(v,w), ibarrier */
+    mca_coll_base_module_ibcast_fn_t coll_ibcast;
+    mca_coll_base_module_t *coll_ibcast_module;
+    struct { mca_coll_base_any_fn_t fn; mca_coll_base_module_t *module; } coll_iegg[3];  /* iexscan, igather(v) */
+    mca_coll_base_module_ireduce_fn_t coll_ireduce;
+    mca_coll_base_module_t *coll_ireduce_module;
+    struct { mca_coll_base_any_fn_t fn; mca_coll_base_module_t *module; } coll_ireduce_scatter_pair;
+    mca_coll_base_module_ireduce_scatter_block_fn_t coll_ireduce_scatter_block;
+    mca_coll_base_module_t *coll_ireduce_scatter_block_module;
+    struct { mca_coll_base_any_fn_t fn; mca_coll_base_module_t *module; } coll_isss[3];  /* iscan, iscatter(v) */
+    struct { mca_coll_base_any_fn_t fn; mca_coll_base_module_t *module; } coll_neighbor[10];
 } mca_coll_base_comm_coll_t;
 
 /* ompi/communicator/communicator.h:111-166 */

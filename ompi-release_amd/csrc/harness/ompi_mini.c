@@ -99,6 +99,11 @@ void mini_init(void)
     static int done = 0;
     if (done) return;
     done = 1;
+    /* MPI_REQUEST_NULL (ompi_request_init, request.c:108-150): complete, inactive, index 0 */
+    ompi_request_null.request.req_type = OMPI_REQUEST_NULL;
+    ompi_request_null.request.req_complete = true;
+    ompi_request_null.request.req_state = OMPI_REQUEST_INACTIVE;
+    ompi_request_null.request.req_f_to_c_index = 0;
     for (int i = 0; i < OMPI_DATATYPE_MPI_MAX_PREDEFINED; ++i) ompi_op_ddt_map[i] = -1;
     for (size_t k = 0; k < sizeof(predefined) / sizeof(predefined[0]); ++k) {
         ompi_op_ddt_map[predefined[k].id] = predefined[k].slot;
@@ -312,6 +317,11 @@ void mini_comm_install(ompi_communicator_t *c, mca_coll_base_module_t *m)
     INST(reduce)
     INST(reduce_scatter)
     INST(reduce_scatter_block)
+    INST(iallgather)
+    INST(iallreduce)
+    INST(ibcast)
+    INST(ireduce)
+    INST(ireduce_scatter_block)
 #undef INST
 }
 
@@ -346,15 +356,109 @@ void mini_comm_destroy(ompi_communicator_t *c)
     REL(reduce)
     REL(reduce_scatter)
     REL(reduce_scatter_block)
+    REL(iallgather)
+    REL(iallreduce)
+    REL(ibcast)
+    REL(ireduce)
+    REL(ireduce_scatter_block)
 #undef REL
     mi355x_obj_release(&c->c_local_group->super);
     free(c);
 }
 
+/* ---- requests + progress (ompi/request/request.c, req_wait.c; opal/runtime/opal_progress.c) ---- */
+static void request_construct(opal_object_t *o)  /* ompi_request_construct, request.c:52-65 */
+{
+    ompi_request_t *req = (ompi_request_t *)o;
+    req->req_state = OMPI_REQUEST_INVALID;
+    req->req_complete = false;
+    req->req_persistent = false;
+    req->req_free = NULL;
+    req->req_cancel = NULL;
+    req->req_complete_cb = NULL;
+    req->req_complete_cb_data = NULL;
+    req->req_f_to_c_index = MPI_UNDEFINED;
+    req->req_mpi_object.comm = NULL;
+}
+opal_class_t ompi_request_t_class = {"ompi_request_t", &opal_object_t_class, request_construct, NULL, 0, 0,
+                                     NULL, NULL, sizeof(ompi_request_t)};
+size_t ompi_request_waiting = 0, ompi_request_completed = 0, ompi_request_failed = 0;
+opal_condition_t ompi_request_cond;
+ompi_predefined_request_t ompi_request_null;
+struct opal_pointer_array_t { int unused; } ompi_request_f_to_c_table;
+int opal_pointer_array_set_item(struct opal_pointer_array_t *array, int index, void *value)
+{
+    (void)array; (void)index; (void)value;
+    return 0;
+}
+
+static opal_progress_callback_t progress_cbs[16];
+static int progress_n;
+int opal_progress_register(opal_progress_callback_t cb)
+{
+    for (int i = 0; i < progress_n; ++i)
+        if (progress_cbs[i] == cb) return 0;
+    if (progress_n == 16) return -1;
+    progress_cbs[progress_n++] = cb;
+    return 0;
+}
+int opal_progress_unregister(opal_progress_callback_t cb)
+{
+    for (int i = 0; i < progress_n; ++i)
+        if (progress_cbs[i] == cb) {
+            progress_cbs[i] = progress_cbs[--progress_n];
+            return 0;
+        }
+    return -1;
+}
+int mini_progress(void)  /* opal_progress: run every registered callback */
+{
+    int events = 0;
+    for (int i = 0; i < progress_n; ++i) events += progress_cbs[i]();
+    return events;
+}
+int mini_progress_callbacks(void) { return progress_n; }
+/* MPI_Wait on a nonpersistent request (ompi_request_default_wait, req_wait.c:33-90): progress
+ * until complete, then free it unless it failed; *req becomes MPI_REQUEST_NULL */
+int mini_wait(ompi_request_t **req)
+{
+    ompi_request_t *r = *req;
+    while (!r->req_complete) mini_progress();
+    if (r->req_status.MPI_ERROR != 0) return r->req_status.MPI_ERROR;
+    int rc = r->req_free(req);
+    return rc;
+}
+int mini_request_is_null(ompi_request_t *r) { return r == &ompi_request_null.request; }
+int mini_request_complete(ompi_request_t *r) { return r->req_complete ? 1 : 0; }
+
 /* C-callable MPI-style entry points through the communicator's installed functions */
 int mini_allreduce(ompi_communicator_t *c, void *s, void *r, int n, ompi_datatype_t *d, ompi_op_t *op)
 {
     return c->c_coll.coll_allreduce(s, r, n, d, op, c, c->c_coll.coll_allreduce_module);
+}
+int mini_iallreduce(ompi_communicator_t *c, void *s, void *r, int n, ompi_datatype_t *d, ompi_op_t *op,
+                    ompi_request_t **req)
+{
+    return c->c_coll.coll_iallreduce(s, r, n, d, op, c, req, c->c_coll.coll_iallreduce_module);
+}
+int mini_ireduce(ompi_communicator_t *c, void *s, void *r, int n, ompi_datatype_t *d, ompi_op_t *op, int root,
+                 ompi_request_t **req)
+{
+    return c->c_coll.coll_ireduce(s, r, n, d, op, root, c, req, c->c_coll.coll_ireduce_module);
+}
+int mini_ireduce_scatter_block(ompi_communicator_t *c, void *s, void *r, int n, ompi_datatype_t *d, ompi_op_t *op,
+                               ompi_request_t **req)
+{
+    return c->c_coll.coll_ireduce_scatter_block(s, r, n, d, op, c, req, c->c_coll.coll_ireduce_scatter_block_module);
+}
+int mini_iallgather(ompi_communicator_t *c, void *s, int sc, ompi_datatype_t *sd, void *r, int rc, ompi_datatype_t *rd,
+                    ompi_request_t **req)
+{
+    return c->c_coll.coll_iallgather(s, sc, sd, r, rc, rd, c, req, c->c_coll.coll_iallgather_module);
+}
+int mini_ibcast(ompi_communicator_t *c, void *b, int n, ompi_datatype_t *d, int root, ompi_request_t **req)
+{
+    return c->c_coll.coll_ibcast(b, n, d, root, c, req, c->c_coll.coll_ibcast_module);
 }
 int mini_reduce(ompi_communicator_t *c, void *s, void *r, int n, ompi_datatype_t *d, ompi_op_t *op, int root)
 {
@@ -385,6 +489,11 @@ void *mini_comm_fn(ompi_communicator_t *c, int which)
     case 3: return (void *)c->c_coll.coll_allgather;
     case 4: return (void *)c->c_coll.coll_bcast;
     case 5: return (void *)c->c_coll.coll_reduce;
+    case 6: return (void *)c->c_coll.coll_iallreduce;
+    case 7: return (void *)c->c_coll.coll_ireduce;
+    case 8: return (void *)c->c_coll.coll_ireduce_scatter_block;
+    case 9: return (void *)c->c_coll.coll_iallgather;
+    case 10: return (void *)c->c_coll.coll_ibcast;
     default: return NULL;
     }
 }
@@ -411,6 +520,10 @@ static int st_reduce(void *s, void *r, int n, struct ompi_datatype_t *d, struct 
                      struct ompi_communicator_t *c, mca_coll_base_module_t *m)
 { (void)s; (void)r; (void)n; (void)d; (void)o; (void)root; (void)c; (void)m; stub_calls[5]++; return stub_marker; }
 
+static int st_iallreduce(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                         struct ompi_communicator_t *c, ompi_request_t **req, mca_coll_base_module_t *m)
+{ (void)s; (void)r; (void)n; (void)d; (void)o; (void)c; (void)m; *req = &ompi_request_null.request; stub_calls[6]++; return stub_marker; }
+
 mca_coll_base_module_t *mini_stub_module(void)
 {
     mca_coll_base_module_t *m = mini_coll_module_new();
@@ -420,6 +533,7 @@ mca_coll_base_module_t *mini_stub_module(void)
     m->coll_allgather = st_allgather;
     m->coll_bcast = st_bcast;
     m->coll_reduce = st_reduce;
+    m->coll_iallreduce = st_iallreduce;
     return m;
 }
 int mini_stub_calls(int which) { return (which >= 0 && which < 8) ? stub_calls[which] : -1; }
@@ -446,6 +560,12 @@ size_t mini_offsetof(int which)
     case 14: return sizeof(ompi_datatype_t);
     case 15: return offsetof(ompi_communicator_t, c_contextid);
     case 16: return sizeof(mca_coll_base_comm_coll_t);
+    case 17: return offsetof(mca_coll_base_module_t, coll_iallreduce);
+    case 18: return sizeof(ompi_request_t);
+    case 19: return offsetof(ompi_request_t, req_status);
+    case 20: return offsetof(ompi_request_t, req_free);
+    case 21: return offsetof(mca_coll_base_comm_coll_t, coll_iallreduce);
+    case 22: return sizeof(ompi_predefined_request_t);
     default: return (size_t)-1;
     }
 }

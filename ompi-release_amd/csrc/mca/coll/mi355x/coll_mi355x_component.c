@@ -32,6 +32,17 @@ typedef struct mca_coll_mi355x_module_t {
     mca_coll_base_module_t *prev_bcast_module;
     mca_coll_base_module_reduce_fn_t prev_reduce;
     mca_coll_base_module_t *prev_reduce_module;
+    /* nonblocking slots: the previous owner (normally coll/libnbc) may be absent */
+    mca_coll_base_module_iallreduce_fn_t prev_iallreduce;
+    mca_coll_base_module_t *prev_iallreduce_module;
+    mca_coll_base_module_ireduce_fn_t prev_ireduce;
+    mca_coll_base_module_t *prev_ireduce_module;
+    mca_coll_base_module_ireduce_scatter_block_fn_t prev_ireduce_scatter_block;
+    mca_coll_base_module_t *prev_ireduce_scatter_block_module;
+    mca_coll_base_module_iallgather_fn_t prev_iallgather;
+    mca_coll_base_module_t *prev_iallgather_module;
+    mca_coll_base_module_ibcast_fn_t prev_ibcast;
+    mca_coll_base_module_t *prev_ibcast_module;
     /* GPU-convertor layouts of the derived datatypes seen on this communicator, and the packed
      * staging buffer (device memory; registered once, re-registered when it grows) */
     struct ddt_slot { uint64_t sig; const void *dt; mi355x_ddt_t *d; } ddt_cache[8];
@@ -60,6 +71,11 @@ static void module_destruct(opal_object_t *o)
     release_prev(m->prev_allgather_module);
     release_prev(m->prev_bcast_module);
     release_prev(m->prev_reduce_module);
+    release_prev(m->prev_iallreduce_module);
+    release_prev(m->prev_ireduce_module);
+    release_prev(m->prev_ireduce_scatter_block_module);
+    release_prev(m->prev_iallgather_module);
+    release_prev(m->prev_ibcast_module);
     for (int i = 0; i < 8; ++i)
         if (m->ddt_cache[i].d) mi355x_ddt_destroy(m->ddt_cache[i].d);
     if (m->scratch) mi355x_free(m->scratch);
@@ -300,6 +316,188 @@ int mca_coll_mi355x_bcast(void *buff, int count, struct ompi_datatype_t *datatyp
     return map_rc(rc);
 }
 
+/* ------------------------------------------------------------------ nonblocking collectives
+ * The engine runs a posted collective on the communicator's progress thread (mi355x_i*); the
+ * component hands MPI an ompi_request_t subclass -- as coll/libnbc does
+ * (coll_libnbc_component.c:300-333, coll_libnbc.h:120-135) -- and completes it from an
+ * opal_progress callback (libnbc: ompi_coll_libnbc_progress, :239-268) when the engine request
+ * has finished.  MPI_Wait / MPI_Test then find it complete and call req_free. */
+typedef struct mi355x_nbreq_t {
+    ompi_request_t super;
+    mi355x_request_t *eng;
+    struct mi355x_nbreq_t *next;   /* active list */
+} mi355x_nbreq_t;
+
+static pthread_mutex_t nb_lock = PTHREAD_MUTEX_INITIALIZER;
+static mi355x_nbreq_t *nb_active;
+static int nb_registered;
+
+static int nbreq_free(ompi_request_t **rp)
+{
+    mi355x_nbreq_t *r = (mi355x_nbreq_t *)*rp;
+    if (true != r->super.req_complete) return MPI_ERR_REQUEST;
+    mi355x_ompi_request_fini(&r->super);
+    mi355x_obj_release(&r->super.super.super.super);
+    *rp = &ompi_request_null.request;
+    return OMPI_SUCCESS;
+}
+
+static int nbreq_cancel(ompi_request_t *r, int flag)
+{
+    (void)r;
+    (void)flag;
+    return OMPI_SUCCESS;  /* collectives cannot be cancelled (libnbc's request_cancel does nothing) */
+}
+
+static void nbreq_construct(opal_object_t *o)
+{
+    mi355x_nbreq_t *r = (mi355x_nbreq_t *)o;
+    r->super.req_type = OMPI_REQUEST_COLL;
+    r->super.req_status._cancelled = 0;
+    r->super.req_free = nbreq_free;
+    r->super.req_cancel = nbreq_cancel;
+    r->eng = NULL;
+    r->next = NULL;
+}
+
+static opal_class_t mi355x_nbreq_t_class = {"mca_coll_mi355x_request_t", &ompi_request_t_class, nbreq_construct,
+                                            NULL, 0, 0, NULL, NULL, sizeof(mi355x_nbreq_t)};
+
+/* opal_progress callback: complete the requests whose engine call has finished */
+static int nb_progress(void)
+{
+    if (pthread_mutex_trylock(&nb_lock)) return 0;
+    int completed = 0;
+    for (mi355x_nbreq_t **p = &nb_active; *p;) {
+        mi355x_nbreq_t *r = *p;
+        int done = 0;
+        const int rc = mi355x_request_test(r->eng, &done);
+        if (!done) {
+            p = &r->next;
+            continue;
+        }
+        *p = r->next;
+        if (rc != MI355X_SUCCESS) fprintf(stderr, "[coll/mi355x] %s\n", mi355x_last_error());
+        r->super.req_status.MPI_ERROR = (rc == MI355X_SUCCESS) ? 0 : MPI_ERR_INTERN;
+        mi355x_request_free(r->eng);
+        r->eng = NULL;
+        mi355x_ompi_request_complete(&r->super, true);
+        completed++;
+    }
+    pthread_mutex_unlock(&nb_lock);
+    return completed;
+}
+
+/* wrap an engine request into an active MPI request (OMPI_REQUEST_INIT + ACTIVE, coll_libnbc.h:
+ * 126-131) */
+static int nb_start(mi355x_request_t *eng, struct ompi_communicator_t *comm, ompi_request_t **request)
+{
+    mi355x_nbreq_t *r = (mi355x_nbreq_t *)mi355x_obj_new(&mi355x_nbreq_t_class);
+    if (!r) {
+        mi355x_request_wait(eng);
+        mi355x_request_free(eng);
+        return OMPI_ERR_OUT_OF_RESOURCE;
+    }
+    r->super.req_complete = false;
+    r->super.req_persistent = false;
+    r->super.req_state = OMPI_REQUEST_ACTIVE;
+    r->super.req_status.MPI_ERROR = 0;
+    r->super.req_mpi_object.comm = comm;
+    r->eng = eng;
+    pthread_mutex_lock(&nb_lock);
+    r->next = nb_active;
+    nb_active = r;
+    if (!nb_registered) {
+        opal_progress_register(nb_progress);
+        nb_registered = 1;
+    }
+    pthread_mutex_unlock(&nb_lock);
+    *request = &r->super;
+    return OMPI_SUCCESS;
+}
+
+#define NB_FALLBACK(FN, ...)                                                          \
+    do {                                                                              \
+        if (!m->prev_##FN) return OMPI_ERR_NOT_SUPPORTED;                             \
+        return m->prev_##FN(__VA_ARGS__, m->prev_##FN##_module);                      \
+    } while (0)
+
+int mca_coll_mi355x_iallreduce(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                               struct ompi_communicator_t *comm, ompi_request_t **request,
+                               mca_coll_base_module_t *module)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    const int inplace = (sbuf == MPI_IN_PLACE);
+    const int t = reducible_type(dtype);
+    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 ||
+        !mi355x_op_supported(op->o_f_to_c_index, t))
+        NB_FALLBACK(iallreduce, sbuf, rbuf, count, dtype, op, comm, request);
+    mi355x_request_t *eng = NULL;
+    int rc = mi355x_iallreduce(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)count, t, op->o_f_to_c_index, NULL, &eng);
+    return rc ? map_rc(rc) : nb_start(eng, comm, request);
+}
+
+int mca_coll_mi355x_ireduce(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                            int root, struct ompi_communicator_t *comm, ompi_request_t **request,
+                            mca_coll_base_module_t *module)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    const int me = mi355x_comm_rank_of(comm);
+    const int inplace = (sbuf == MPI_IN_PLACE);
+    const int t = reducible_type(dtype);
+    if ((me == root && !is_dev(rbuf)) || (!inplace && !is_dev(sbuf)) || (inplace && me != root) ||
+        !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 || !mi355x_op_supported(op->o_f_to_c_index, t))
+        NB_FALLBACK(ireduce, sbuf, rbuf, count, dtype, op, root, comm, request);
+    mi355x_request_t *eng = NULL;
+    int rc = mi355x_ireduce(m->engine, inplace ? NULL : sbuf, me == root ? rbuf : NULL, (size_t)count, t,
+                            op->o_f_to_c_index, root, NULL, &eng);
+    return rc ? map_rc(rc) : nb_start(eng, comm, request);
+}
+
+int mca_coll_mi355x_ireduce_scatter_block(void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dtype,
+                                          struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                                          ompi_request_t **request, mca_coll_base_module_t *module)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    const int inplace = (sbuf == MPI_IN_PLACE);
+    const int t = reducible_type(dtype);
+    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 ||
+        !mi355x_op_supported(op->o_f_to_c_index, t))
+        NB_FALLBACK(ireduce_scatter_block, sbuf, rbuf, rcount, dtype, op, comm, request);
+    mi355x_request_t *eng = NULL;
+    int rc = mi355x_ireduce_scatter_block(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)rcount, t,
+                                          op->o_f_to_c_index, NULL, &eng);
+    return rc ? map_rc(rc) : nb_start(eng, comm, request);
+}
+
+/* contiguous layouts only; derived datatypes go to the previous owner (libnbc) */
+int mca_coll_mi355x_iallgather(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
+                               struct ompi_datatype_t *rdtype, struct ompi_communicator_t *comm,
+                               ompi_request_t **request, mca_coll_base_module_t *module)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    const int inplace = (sbuf == MPI_IN_PLACE);
+    size_t rb = 0, sb = 0;
+    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || rcount < 0 || !contiguous_bytes(rdtype, rcount, &rb) ||
+        (!inplace && (scount < 0 || !contiguous_bytes(sdtype, scount, &sb) || sb != rb)))
+        NB_FALLBACK(iallgather, sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, request);
+    mi355x_request_t *eng = NULL;
+    int rc = mi355x_iallgather(m->engine, inplace ? NULL : sbuf, rbuf, rb, NULL, &eng);
+    return rc ? map_rc(rc) : nb_start(eng, comm, request);
+}
+
+int mca_coll_mi355x_ibcast(void *buff, int count, struct ompi_datatype_t *datatype, int root,
+                           struct ompi_communicator_t *comm, ompi_request_t **request, mca_coll_base_module_t *module)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    size_t bytes = 0;
+    if (!is_dev(buff) || count < 0 || !contiguous_bytes(datatype, count, &bytes))
+        NB_FALLBACK(ibcast, buff, count, datatype, root, comm, request);
+    mi355x_request_t *eng = NULL;
+    int rc = mi355x_ibcast(m->engine, buff, bytes, root, NULL, &eng);
+    return rc ? map_rc(rc) : nb_start(eng, comm, request);
+}
+
 /* ------------------------------------------------------------------ module / component */
 #define SNAP(FN)                                                                \
     do {                                                                        \
@@ -307,6 +505,13 @@ int mca_coll_mi355x_bcast(void *buff, int count, struct ompi_datatype_t *datatyp
         m->prev_##FN##_module = comm->c_coll.coll_##FN##_module;                \
         if (!m->prev_##FN || !m->prev_##FN##_module) return OMPI_ERROR;         \
         mi355x_obj_retain(&m->prev_##FN##_module->super);                       \
+    } while (0)
+
+#define SNAP_OPT(FN)                                                            \
+    do {                                                                        \
+        m->prev_##FN = comm->c_coll.coll_##FN;                                  \
+        m->prev_##FN##_module = comm->c_coll.coll_##FN##_module;                \
+        if (m->prev_##FN##_module) mi355x_obj_retain(&m->prev_##FN##_module->super); \
     } while (0)
 
 /* coll_module_enable (coll.h:176-178): runs after every lower-priority module is installed */
@@ -319,6 +524,11 @@ static int module_enable(mca_coll_base_module_t *module, struct ompi_communicato
     SNAP(allgather);
     SNAP(bcast);
     SNAP(reduce);
+    SNAP_OPT(iallreduce);
+    SNAP_OPT(ireduce);
+    SNAP_OPT(ireduce_scatter_block);
+    SNAP_OPT(iallgather);
+    SNAP_OPT(ibcast);
     /* node-unique rendezvous key: job id + communicator context id */
     const char *job = getenv("OMPI_MCA_ess_base_jobid");
     char key[128];
@@ -369,6 +579,11 @@ static mca_coll_base_module_t *component_comm_query(struct ompi_communicator_t *
     m->super.coll_allgather = mca_coll_mi355x_allgather;
     m->super.coll_bcast = mca_coll_mi355x_bcast;
     m->super.coll_reduce = mca_coll_mi355x_reduce;
+    m->super.coll_iallreduce = mca_coll_mi355x_iallreduce;
+    m->super.coll_ireduce = mca_coll_mi355x_ireduce;
+    m->super.coll_ireduce_scatter_block = mca_coll_mi355x_ireduce_scatter_block;
+    m->super.coll_iallgather = mca_coll_mi355x_iallgather;
+    m->super.coll_ibcast = mca_coll_mi355x_ibcast;
     m->super.ft_event = NULL;
     *priority = mca_coll_mi355x_priority > 100 ? 100 : mca_coll_mi355x_priority;
     return &m->super;

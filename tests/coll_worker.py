@@ -68,6 +68,60 @@ def derived_allgather(m, comm, oracle, rank, size, torch):
     oracle.oracle_ddt_free(od)
 
 
+def nonblocking(m, comm, oracle, rank, size, torch, ptrs):
+    pkg = m.pkg
+    code, slot = pkg.OP["SUM"], pkg.T["DOUBLE"]
+    dt = m.dtype_for_slot(slot)
+    op = m.select_op(code)
+    count, rcount, nb = 20_001, 3001, 70_001
+    xa = [opdata.make("DOUBLE", count, 1300 + r) for r in range(size)]
+    wa = [np.zeros_like(xa[0]) for _ in range(size)]
+    oracle.oracle_allreduce(0, size, count, slot, code, 0, ptrs(xa), ptrs(wa))
+    xb = [opdata.make("DOUBLE", rcount * size, 1400 + r) for r in range(size)]
+    wb = [np.zeros(rcount, dtype=np.float64) for _ in range(size)]
+    oracle.oracle_reduce_scatter_block(size, rcount, slot, code, ptrs(xb), ptrs(wb))
+    wr = np.zeros_like(xa[0])
+    oracle.oracle_reduce.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]
+    oracle.oracle_reduce(0, size, 0, count, slot, code, 0, ptrs(xa), wr.ctypes.data)
+    da = torch.from_numpy(xa[rank].view(np.uint8).copy()).cuda()
+    ra, rr = torch.zeros_like(da), torch.zeros_like(da)
+    db = torch.from_numpy(xb[rank].view(np.uint8).copy()).cuda()
+    rb = torch.zeros(rcount * 8, dtype=torch.uint8, device="cuda")
+    bdt = m.dtype_for_slot(pkg.T["FLOAT"])
+    assert bdt
+    gs = torch.full((nb,), float(rank + 1), device="cuda")
+    gd = torch.zeros(nb * size, device="cuda")
+    bc = torch.full((nb,), float(rank + 7), device="cuda")
+    torch.cuda.synchronize()
+    reqs = [ctypes.c_void_p() for _ in range(5)]
+    L = m.lib
+    assert L.mini_iallreduce(comm, da.data_ptr(), ra.data_ptr(), count, dt, op, ctypes.byref(reqs[0])) == 0
+    assert L.mini_ireduce_scatter_block(comm, db.data_ptr(), rb.data_ptr(), rcount, dt, op, ctypes.byref(reqs[1])) == 0
+    assert L.mini_ireduce(comm, da.data_ptr(), rr.data_ptr() if rank == 0 else None, count, dt, op, 0,
+                          ctypes.byref(reqs[2])) == 0
+    assert L.mini_iallgather(comm, gs.data_ptr(), nb, bdt, gd.data_ptr(), nb, bdt, ctypes.byref(reqs[3])) == 0
+    assert L.mini_ibcast(comm, bc.data_ptr(), nb, bdt, size - 1, ctypes.byref(reqs[4])) == 0
+    assert L.mini_progress_callbacks() >= 1
+    for q in reqs:
+        assert L.mini_wait(ctypes.byref(q)) == 0
+        assert L.mini_request_is_null(q), "MPI_Wait leaves MPI_REQUEST_NULL"
+    opdata.assert_same("DOUBLE", "SUM", ra.cpu().numpy().view(np.float64), wa[rank], "component iallreduce")
+    opdata.assert_same("DOUBLE", "SUM", rb.cpu().numpy().view(np.float64), wb[rank], "component ireduce_scatter_block")
+    if rank == 0:
+        opdata.assert_same("DOUBLE", "SUM", rr.cpu().numpy().view(np.float64), wr, "component ireduce")
+    for r in range(size):
+        assert int(gd[r * nb:(r + 1) * nb].min()) == r + 1 == int(gd[r * nb:(r + 1) * nb].max())
+    assert int(bc.min()) == size - 1 + 7 == int(bc.max())
+    assert dt
+    # host buffers -> the previous owner of the slot (the stub)
+    h = np.zeros(16, dtype=np.float64)
+    q = ctypes.c_void_p()
+    assert L.mini_iallreduce(comm, h.ctypes.data, h.ctypes.data, 16, dt, op, ctypes.byref(q)) == L.mini_stub_marker()
+    assert L.mini_stub_calls(6) == 1
+    m.lib.mini_op_destroy(op)
+
+
 def main():
     rank, size = int(sys.argv[1]), int(sys.argv[2])
     import torch
@@ -132,6 +186,9 @@ def main():
     torch.cuda.synchronize()
     assert m.lib.mini_bcast(comm, buf.data_ptr(), n, fdt, size - 1) == 0
     assert bool((buf == size - 1).all())
+    # nonblocking slots: MPI_Iallreduce / Ireduce / Ireduce_scatter_block / Iallgather / Ibcast posted
+    # together, then MPI_Wait on each (requests progressed by the component's opal_progress callback)
+    nonblocking(m, comm, oracle, rank, size, torch, ptrs)
     # derived datatypes through the GPU convertor: bcast of a vector type ...
     derived_bcast(m, comm, oracle, rank, size, torch)
     derived_allgather(m, comm, oracle, rank, size, torch)

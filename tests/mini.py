@@ -47,6 +47,15 @@ class Mini:
         L.mini_allreduce.argtypes = [vp, vp, vp, i, vp, vp]
         L.mini_reduce_scatter_block.argtypes = [vp, vp, vp, i, vp, vp]
         L.mini_reduce.argtypes = [vp, vp, vp, i, vp, vp, i]
+        P = ctypes.POINTER(vp)
+        L.mini_iallreduce.argtypes = [vp, vp, vp, i, vp, vp, P]
+        L.mini_ireduce.argtypes = [vp, vp, vp, i, vp, vp, i, P]
+        L.mini_ireduce_scatter_block.argtypes = [vp, vp, vp, i, vp, vp, P]
+        L.mini_iallgather.argtypes = [vp, vp, i, vp, vp, i, vp, P]
+        L.mini_ibcast.argtypes = [vp, vp, i, vp, i, P]
+        L.mini_wait.argtypes = [P]
+        L.mini_request_is_null.argtypes = [vp]
+        L.mini_request_complete.argtypes = [vp]
         L.mini_reduce_scatter.argtypes = [vp, vp, vp, ctypes.POINTER(i), vp, vp]
         L.mini_allgather.argtypes = [vp, vp, i, vp, vp, i, vp]
         L.mini_bcast.argtypes = [vp, vp, i, vp, i]

@@ -51,7 +51,8 @@ def test_component_symbols(pkg):
     coll = _exports(pkg.lib_path("mca_coll_mi355x.so"))
     for s in ("mca_coll_mi355x_component", "mca_coll_mi355x_allreduce", "mca_coll_mi355x_reduce_scatter_block",
               "mca_coll_mi355x_reduce_scatter", "mca_coll_mi355x_allgather", "mca_coll_mi355x_bcast",
-              "mca_coll_mi355x_reduce"):
+              "mca_coll_mi355x_reduce", "mca_coll_mi355x_iallreduce", "mca_coll_mi355x_ireduce",
+              "mca_coll_mi355x_ireduce_scatter_block", "mca_coll_mi355x_iallgather", "mca_coll_mi355x_ibcast"):
         assert s in coll
 
 
@@ -87,6 +88,14 @@ def test_abi_offsets():
         10: 16 + 8 + 2 * 8,          # coll module: allreduce is the 3rd fn after enable
         11: 16 + 8 + 44 * 8,         # ft_event after 17 + 17 + 10 fns
         16: 44 * 16,                 # mca_coll_base_comm_coll_t: 44 (fn, module) pairs
+        17: 16 + 8 + 19 * 8,         # coll module: iallreduce = 3rd nonblocking fn (coll.h:418-420)
+        # ompi_request_t (request.h:98-110): free-list item 56 B (list item 40 = object 16 +
+        # next/prev 16 + item_free 4 + pad), req_type 4 + pad, status 24, flags, 4 fn pointers, union
+        18: 144,
+        19: 64,                      # req_status
+        20: 104,                     # req_free
+        21: 19 * 16,                 # comm coll table: iallreduce pair after 17 blocking + 2
+        22: 8 * 32,                  # ompi_predefined_request_t padded to 32 pointers
     }
     for k, v in want.items():
         assert L.mini_offsetof(k) == v, (k, L.mini_offsetof(k), v)
@@ -165,7 +174,9 @@ def test_coll_comm_query(monkeypatch):
     # the module provides exactly allreduce, reduce_scatter(_block), allgather, bcast, reduce
     m.lib.mini_comm_install(comm, mod)
     names = ["mca_coll_mi355x_allreduce", "mca_coll_mi355x_reduce_scatter_block", "mca_coll_mi355x_reduce_scatter",
-             "mca_coll_mi355x_allgather", "mca_coll_mi355x_bcast", "mca_coll_mi355x_reduce"]
+             "mca_coll_mi355x_allgather", "mca_coll_mi355x_bcast", "mca_coll_mi355x_reduce",
+             "mca_coll_mi355x_iallreduce", "mca_coll_mi355x_ireduce", "mca_coll_mi355x_ireduce_scatter_block",
+             "mca_coll_mi355x_iallgather", "mca_coll_mi355x_ibcast"]
     for which, n in enumerate(names):
         assert m.lib.mini_comm_fn(comm, which) == m.addr(m.coll, n)
     m.lib.mini_comm_destroy(comm)
