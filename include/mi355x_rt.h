@@ -100,8 +100,9 @@ int mi355x_comm_destroy(mi355x_comm_t *comm);
 int mi355x_comm_rank(const mi355x_comm_t *comm);
 int mi355x_comm_size(const mi355x_comm_t *comm);
 int mi355x_comm_barrier(mi355x_comm_t *comm);
-/* algorithm id of the last collective (AR_*: 1 linear, 2 nonoverlapping, 3 recursive doubling,
- * 4 ring, 5 segmented ring; reduce: 1 linear .. 5 binomial; reduce_scatter: 1 rec. halving, 2 ring) */
+/* algorithm id of the last collective, coll/tuned numbering (allreduce: 1 linear, 2 nonoverlapping,
+ * 3 recursive doubling, 4 ring, 5 segmented ring; reduce: 1 linear, 2 chain, 3 pipeline, 4 binary,
+ * 5 binomial; reduce_scatter: 1 non-overlapping, 2 recursive halving, 3 ring) */
 int mi355x_comm_last_algorithm(const mi355x_comm_t *comm);
 
 enum mi355x_knob {
@@ -115,11 +116,33 @@ enum mi355x_knob {
                                            exported; calls touching one take the staged data flow
                                            (default 2^31: hipIpcOpenMemHandle hangs from 2 GiB) */
     MI355X_KNOB_STAGE_BYTES = 8,        /* size of the per-communicator staging buffer (default 1 GiB) */
+    MI355X_KNOB_REDUCE_CHAIN_FANOUT = 10, /* coll_tuned_reduce_algorithm_chain_fanout (default 4) */
     MI355X_KNOB_LL_MAX_BYTES = 9        /* per-rank message bytes up to which allreduce / allgather /
                                            bcast take the one-shot low-latency path (0 = never;
                                            default 64 KiB; multi-process communicators only) */
 };
 int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
+
+/* coll/tuned's dynamic rules file (coll_tuned_dynamic_file.c:56-251; MCA
+ * coll_tuned_dynamic_rules_filename with coll_tuned_use_dynamic_rules).  Collective ids are
+ * coll/tuned's COLLTYPE (coll_tuned.h:41-58); algorithm numbers are coll/tuned's per collective.
+ * A communicator with rules picks, per call: rule > forced algorithm (knobs) > fixed decision, as
+ * the dec_dynamic functions do (coll_tuned_decision_dynamic.c:59-99).  Rules change the operand
+ * order of allreduce / reduce / reduce_scatter(_block) results (reduce chain fan-out included);
+ * bcast / allgather rules are read but do not change any result. */
+enum mi355x_coll_id {
+    MI355X_COLL_ALLGATHER = 0, MI355X_COLL_ALLREDUCE = 2, MI355X_COLL_BCAST = 7, MI355X_COLL_REDUCE = 11,
+    MI355X_COLL_REDUCESCATTER = 12, MI355X_COLL_COUNT = 16
+};
+typedef struct mi355x_rules mi355x_rules_t;
+/* returns the number of collectives with rules (>= 0) or a negative status */
+int mi355x_rules_load(const char *path, mi355x_rules_t **rules);
+int mi355x_rules_destroy(mi355x_rules_t *rules);
+/* *alg = 0 when no rule applies; faninout / segsize may be NULL */
+int mi355x_rules_decide(const mi355x_rules_t *rules, int coll, int comm_size, size_t msg_bytes, int *alg,
+                        int *faninout, int *segsize);
+/* the communicator consults `rules` (not owned; NULL = none) from the next call on */
+int mi355x_comm_set_rules(mi355x_comm_t *comm, const mi355x_rules_t *rules);
 
 /* MPI_Allreduce.  sbuf == NULL means MPI_IN_PLACE.  Replaces coll_cuda_allreduce.c:30-77 +
  * ompi_coll_tuned_allreduce_intra_dec_fixed (coll_tuned_decision_fixed.c:42-85). */

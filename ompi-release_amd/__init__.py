@@ -119,6 +119,10 @@ def _declare(lib: ctypes.CDLL) -> None:
         "mi355x_allgather": (i, [vp, vp, vp, sz, vp]),
         "mi355x_bcast": (i, [vp, vp, sz, i, vp]),
         "mi355x_sched_program": (i, [i, i, i, i, c.POINTER(i), i]),
+        "mi355x_rules_load": (i, [c.c_char_p, c.POINTER(vp)]),
+        "mi355x_rules_destroy": (i, [vp]),
+        "mi355x_rules_decide": (i, [vp, i, i, sz, c.POINTER(i), c.POINTER(i), c.POINTER(i)]),
+        "mi355x_comm_set_rules": (i, [vp, vp]),
         "mi355x_ddt_create": (i, [c.POINTER(c.c_int64), c.POINTER(c.c_int64), sz, sz, c.c_int64, c.c_int64, c.POINTER(vp)]),
         "mi355x_ddt_create_vector": (i, [sz, sz, c.c_int64, sz, c.POINTER(vp)]),
         "mi355x_ddt_create_indexed": (i, [sz, c.POINTER(i), c.POINTER(i), sz, c.POINTER(vp)]),
@@ -188,7 +192,9 @@ def get_tune() -> tuple[int, int, int]:
 # ---------------------------------------------------------------- coll/mi355x engine
 KNOB = {"ALLREDUCE_ALG": 1, "REDUCE_ALG": 2, "REDUCE_SCATTER_ALG": 3, "BLOCKS_PER_CU": 4, "TIMEOUT_S": 5,
         "PUSH": 6, "IPC_MAX_BYTES": 7, "STAGE_BYTES": 8,
-        "LL_MAX_BYTES": 9}
+        "LL_MAX_BYTES": 9, "REDUCE_CHAIN_FANOUT": 10}
+# coll/tuned COLLTYPE ids (coll_tuned.h:41-58)
+COLL = {"ALLGATHER": 0, "ALLREDUCE": 2, "BCAST": 7, "REDUCE": 11, "REDUCESCATTER": 12}
 AR_ALG = {"DECISION": 0, "LINEAR": 1, "NONOVERLAPPING": 2, "RECURSIVE_DOUBLING": 3, "RING": 4,
           "RING_SEGMENTED": 5}
 
@@ -237,6 +243,9 @@ class Comm:
     def allreduce(self, sbuf, rbuf, count, ty, op, stream=None) -> None:
         check(rt().mi355x_allreduce(self.h, sbuf, rbuf, count, ty, op, stream), "mi355x_allreduce")
 
+    def set_rules(self, rules) -> None:
+        check(rt().mi355x_comm_set_rules(self.h, rules.h if rules else None), "mi355x_comm_set_rules")
+
     def _post(self, fn, *args) -> Request:
         h = ctypes.c_void_p()
         check(getattr(rt(), fn)(self.h, *args, ctypes.byref(h)), fn)
@@ -273,6 +282,29 @@ class Comm:
 
     def bcast(self, buf, nbytes, root, stream=None) -> None:
         check(rt().mi355x_bcast(self.h, buf, nbytes, root, stream), "mi355x_bcast")
+
+
+class Rules:
+    """coll/tuned dynamic rules (mi355x_rules_t), loaded from a coll_tuned_dynamic_rules_filename file."""
+
+    def __init__(self, path: str):
+        h = ctypes.c_void_p()
+        n = rt().mi355x_rules_load(str(path).encode(), ctypes.byref(h))
+        if n < 0:
+            check(n, "mi355x_rules_load")
+        self.h = h
+        self.ncoll = n
+
+    def decide(self, coll: int, comm_size: int, msg_bytes: int) -> tuple[int, int, int]:
+        a, f, g = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(rt().mi355x_rules_decide(self.h, coll, comm_size, msg_bytes, ctypes.byref(a), ctypes.byref(f),
+                                       ctypes.byref(g)), "mi355x_rules_decide")
+        return a.value, f.value, g.value
+
+    def destroy(self) -> None:
+        if self.h:
+            rt().mi355x_rules_destroy(self.h)
+            self.h = ctypes.c_void_p()
 
 
 class Request:

@@ -507,6 +507,36 @@ int mca_coll_mi355x_ibcast(void *buff, int count, struct ompi_datatype_t *dataty
         mi355x_obj_retain(&m->prev_##FN##_module->super);                       \
     } while (0)
 
+/* coll/tuned's own tuning, honoured so that a job tuned for the reference keeps its choices:
+ * with coll_tuned_use_dynamic_rules set (coll_tuned_component.c:151-167), the forced algorithms
+ * (coll_tuned_{allreduce,reduce,reduce_scatter}_algorithm, reduce_algorithm_chain_fanout) and
+ * the rules file coll_tuned_dynamic_rules_filename (read once per process, like
+ * mca_coll_tuned_component.all_base_rules, coll_tuned_component.c:213-229) */
+static mi355x_rules_t *tuned_rules;
+static int tuned_rules_read;
+
+static void apply_tuned_params(mca_coll_mi355x_module_t *m)
+{
+    if (!env_int("OMPI_MCA_coll_tuned_use_dynamic_rules", 0)) return;
+    const int ar = env_int("OMPI_MCA_coll_tuned_allreduce_algorithm", 0);
+    const int red = env_int("OMPI_MCA_coll_tuned_reduce_algorithm", 0);
+    const int fo = env_int("OMPI_MCA_coll_tuned_reduce_algorithm_chain_fanout", 0);
+    const int rs = env_int("OMPI_MCA_coll_tuned_reduce_scatter_algorithm", 0);
+    if (ar && !mca_coll_mi355x_allreduce_algorithm) mi355x_comm_set(m->engine, MI355X_KNOB_ALLREDUCE_ALG, ar);
+    if (red) mi355x_comm_set(m->engine, MI355X_KNOB_REDUCE_ALG, red);
+    if (fo) mi355x_comm_set(m->engine, MI355X_KNOB_REDUCE_CHAIN_FANOUT, fo);
+    if (rs) mi355x_comm_set(m->engine, MI355X_KNOB_REDUCE_SCATTER_ALG, rs);
+    const char *file = getenv("OMPI_MCA_coll_tuned_dynamic_rules_filename");
+    if (file && !tuned_rules_read) {
+        tuned_rules_read = 1;
+        if (mi355x_rules_load(file, &tuned_rules) < 0) {
+            fprintf(stderr, "[coll/mi355x] %s -- ignoring the rules file\n", mi355x_last_error());
+            tuned_rules = NULL;
+        }
+    }
+    if (tuned_rules) mi355x_comm_set_rules(m->engine, tuned_rules);
+}
+
 #define SNAP_OPT(FN)                                                            \
     do {                                                                        \
         m->prev_##FN = comm->c_coll.coll_##FN;                                  \
@@ -540,6 +570,7 @@ static int module_enable(mca_coll_base_module_t *module, struct ompi_communicato
     if (rc != MI355X_SUCCESS) return map_rc(rc);
     if (mca_coll_mi355x_allreduce_algorithm)
         mi355x_comm_set(m->engine, MI355X_KNOB_ALLREDUCE_ALG, mca_coll_mi355x_allreduce_algorithm);
+    apply_tuned_params(m);
     return OMPI_SUCCESS;
 }
 
@@ -551,7 +582,13 @@ static int component_register(void)
     return OMPI_SUCCESS;
 }
 static int component_open(void) { return OMPI_SUCCESS; }
-static int component_close(void) { return OMPI_SUCCESS; }
+static int component_close(void)
+{
+    if (tuned_rules) mi355x_rules_destroy(tuned_rules);
+    tuned_rules = NULL;
+    tuned_rules_read = 0;
+    return OMPI_SUCCESS;
+}
 
 static int component_init_query(bool enable_progress_threads, bool enable_mpi_threads)
 {

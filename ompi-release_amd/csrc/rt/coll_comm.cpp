@@ -180,6 +180,8 @@ struct mi355x_comm {
     int pending = 0;                              // posted, not finished (guarded by q_mtx)
     hipStream_t nb_stream = nullptr;
     int knob_allreduce = 0, knob_reduce = 0, knob_rs = 0;
+    int chain_fanout = mi355x::kDefaultChainFanout;
+    const mi355x_rules_t *rules = nullptr;        // coll/tuned dynamic rules (not owned)
     int last_alg = -1;
     double timeout_s = 600.0;
 };
@@ -208,7 +210,14 @@ static int barrier(mi355x_comm *c)
                 const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
                 if (el > c->timeout_s) {
                     k->abort_flag.store(1);
-                    return set_error(MI355X_ERR_TIMEOUT, "barrier timed out after %.0f s (rank %d)", el, c->rank);
+                    // which rank is behind: every rank's published call number
+                    char who[256] = "";
+                    size_t w = 0;
+                    for (int r = 0; r < c->size && w + 24 < sizeof(who); ++r)
+                        w += (size_t)snprintf(who + w, sizeof(who) - w, " r%d:%llu", r,
+                                              (unsigned long long)k->slot[r].seq.load());
+                    return set_error(MI355X_ERR_TIMEOUT, "barrier timed out after %.0f s (rank %d, %llu of %d arrived; calls%s)",
+                                     el, c->rank, (unsigned long long)k->bar_count.load(), c->size, who);
                 }
             }
         }
@@ -701,6 +710,72 @@ static void ll_program(LLArgs &a, const Program &pr)
     a.role_mask = pr.role_mask;
 }
 
+// ----------------------------------------------------------------- algorithm choice
+// The order of coll/tuned's dec_dynamic functions (coll_tuned_decision_dynamic.c:59-99): a file
+// rule for this communicator size and message size, else the forced (MCA) algorithm, else the
+// fixed decision.
+static int rule_alg(const mi355x_comm *c, int coll, size_t bytes, int *faninout)
+{
+    int alg = 0;
+    if (c->rules) mi355x_rules_decide(c->rules, coll, c->size, bytes, &alg, faninout, nullptr);
+    return alg;
+}
+
+static int pick_allreduce(const mi355x_comm *c, size_t count, size_t esz)
+{
+    const int r = rule_alg(c, MI355X_COLL_ALLREDUCE, count * esz, nullptr);
+    if (r) return r;
+    return c->knob_allreduce ? c->knob_allreduce : allreduce_decision(c->size, count, esz);
+}
+
+// what comm->c_coll.coll_reduce would run for `count` elements (ompi_coll_tuned_reduce_intra_
+// dec_dynamic): used by MPI_Reduce and by the algorithms that call it (nonoverlapping allreduce,
+// coll/basic reduce_scatter_block, nonoverlapping reduce_scatter)
+static int pick_reduce(const mi355x_comm *c, size_t count, size_t esz, int *chain_fanout)
+{
+    int fio = 0;
+    const int r = rule_alg(c, MI355X_COLL_REDUCE, count * esz, &fio);
+    if (r) {
+        *chain_fanout = fio;
+        return r;
+    }
+    *chain_fanout = c->chain_fanout;
+    return c->knob_reduce ? c->knob_reduce : reduce_decision(c->size, count, esz);
+}
+
+static int pick_reduce_scatter(const mi355x_comm *c, size_t total, size_t esz)
+{
+    const int r = rule_alg(c, MI355X_COLL_REDUCESCATTER, total * esz, nullptr);
+    if (r) return r;
+    return c->knob_rs ? c->knob_rs : reduce_scatter_decision(c->size, total, esz);
+}
+
+// per-element program of a reduce to `root` of `count` elements
+static bool reduce_program(const mi355x_comm *c, size_t count, size_t esz, int root, Program *pr, int *alg)
+{
+    int fanout = kDefaultChainFanout;
+    *alg = pick_reduce(c, count, esz, &fanout);
+    ExprPool ep;
+    return compile_expr(ep, expr_reduce(ep, *alg, c->size, root, fanout), c->size, pr);
+}
+
+// program of the non-ring allreduce algorithms: recursive doubling, or reduce to 0 + bcast
+// (nonoverlapping: comm->c_coll.coll_reduce, coll_tuned_allreduce.c:67-100; linear: the linear
+// reduce, :897-929)
+static bool allreduce_tree_program(const mi355x_comm *c, int alg, size_t count, size_t esz, Program *pr)
+{
+    if (alg == AR_RECDBL) {
+        ExprPool ep;
+        return compile_expr(ep, expr_allreduce_recursive_doubling(ep, c->size), c->size, pr);
+    }
+    if (alg == AR_LINEAR) {
+        ExprPool ep;
+        return compile_expr(ep, expr_reduce(ep, RED_LINEAR, c->size, 0), c->size, pr);
+    }
+    int ra;
+    return reduce_program(c, count, esz, 0, pr, &ra);
+}
+
 static int check_common(mi355x_comm *c, int op, int type)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
@@ -917,6 +992,14 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
     return MI355X_SUCCESS;
 }
 
+int mi355x_comm_set_rules(mi355x_comm_t *c, const mi355x_rules_t *rules)
+{
+    if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    drain(c);
+    c->rules = rules;
+    return MI355X_SUCCESS;
+}
+
 int mi355x_comm_rank(const mi355x_comm_t *c) { return c ? c->rank : -1; }
 int mi355x_comm_size(const mi355x_comm_t *c) { return c ? c->size : -1; }
 int mi355x_comm_barrier(mi355x_comm_t *c)
@@ -944,6 +1027,10 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
         if (value < 0) return set_error(MI355X_ERR_ARG, "ipc_max_bytes < 0");
         c->ipc_max = (size_t)value;
         break;
+    case MI355X_KNOB_REDUCE_CHAIN_FANOUT:
+        if (value < 1 || value > 32) return set_error(MI355X_ERR_ARG, "chain fan-out out of range");
+        c->chain_fanout = (int)value;
+        break;
     case MI355X_KNOB_LL_MAX_BYTES:
         if (value < 0 || value > (64l << 20)) return set_error(MI355X_ERR_ARG, "ll_max_bytes out of range");
         c->ll_max = (size_t)value;
@@ -964,8 +1051,9 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
 //   tree: [0, nr, nsteps, result, (dst, out, in) x nsteps]
 // kind 1: allreduce (alg 3 = recursive doubling, 4/5 = ring block `block`,
 //                    1/2 = reduce-to-0 with reduce algorithm `block` (1..5) + bcast)
-// kind 2: reduce to rank 0 with reduce algorithm `alg`;  kind 3: reduce_scatter ring block;
-// kind 4: reduce_scatter recursive halving block.  Returns the number of ints written or < 0.
+// kind 2: reduce to rank `block` with reduce algorithm `alg`;  kind 3: reduce_scatter ring block;
+// kind 4: reduce_scatter recursive halving block; kind 5: reduce chain to 0 with fan-out `block`.
+// Returns the number of ints written or < 0.
 int mi355x_sched_program(int kind, int n, int alg, int block, int *out, int cap)
 {
     if (!out || n < 1 || n > kMaxRanks) return set_error(MI355X_ERR_ARG, "bad arguments");
@@ -978,7 +1066,8 @@ int mi355x_sched_program(int kind, int n, int alg, int block, int *out, int cap)
         else if (alg == AR_RECDBL) ok = compile_expr(ep, expr_allreduce_recursive_doubling(ep, n), n, &pr);
         else ok = compile_expr(ep, expr_reduce(ep, block, n, 0), n, &pr);
         break;
-    case 2: ok = compile_expr(ep, expr_reduce(ep, alg, n, 0), n, &pr); break;
+    case 2: ok = compile_expr(ep, expr_reduce(ep, alg, n, block), n, &pr); break;  // block = root
+    case 5: ok = compile_expr(ep, expr_reduce(ep, RED_CHAIN, n, 0, block), n, &pr); break;  // block = fan-out
     case 3: pr = reduce_scatter_ring_block_program(n, block); break;
     case 4: {
         std::vector<int> roots = expr_reduce_scatter_rechalving(ep, n);
@@ -1022,7 +1111,7 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
         MI_HIP(hipStreamSynchronize(s));
         return MI355X_SUCCESS;
     }
-    int alg = c->knob_allreduce ? c->knob_allreduce : allreduce_decision(c->size, count, esz);
+    int alg = pick_allreduce(c, count, esz);
     // the reference's own fallbacks: segmented ring -> ring when count < n * segcount
     // (coll_tuned_allreduce.c:672-679), ring -> recursive doubling when count < n (:398-405)
     if (alg == AR_RING_SEGMENTED && count < (size_t)c->size * computed_segcount(1u << 20, esz, count))
@@ -1050,13 +1139,9 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
             a.split = count % (size_t)c->size;
             if (a.late == 0) a.late = 1;  // count < n never reaches the ring (recursive doubling)
         } else {
-            ExprPool ep;
-            const int root = (alg == AR_RECDBL)
-                                 ? expr_allreduce_recursive_doubling(ep, c->size)
-                                 : expr_reduce(ep, (alg == AR_LINEAR) ? RED_LINEAR : reduce_decision(c->size, count, esz),
-                                               c->size, 0);
             Program pr;
-            if (!compile_expr(ep, root, c->size, &pr)) return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
+            if (!allreduce_tree_program(c, alg, count, esz, &pr))
+                return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
             ll_program(a, pr);
         }
         return ll_run(c, a, op, type, s);
@@ -1070,16 +1155,8 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
     if (rc) return rc;
     Program pr;
     if (!ring) {
-        ExprPool ep;
-        int root;
-        if (alg == AR_RECDBL) {
-            root = expr_allreduce_recursive_doubling(ep, c->size);
-        } else {
-            // nonoverlapping / linear: reduce to 0 (tuned decision) then bcast (:67-100, :897-929)
-            const int ra = (alg == AR_LINEAR) ? RED_LINEAR : reduce_decision(c->size, count, esz);
-            root = expr_reduce(ep, ra, c->size, 0);
-        }
-        if (!compile_expr(ep, root, c->size, &pr)) return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
+        if (!allreduce_tree_program(c, alg, count, esz, &pr))
+            return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
         if (sbuf && sbuf != rbuf && !staged) {
             // tree orders (small messages): every rank evaluates the whole vector from the n
             // inputs and writes only its own rbuf -- one phase, reads only
@@ -1153,12 +1230,10 @@ static int reduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t co
         MI_HIP(hipStreamSynchronize(s));
         return MI355X_SUCCESS;
     }
-    const int ra = c->knob_reduce ? c->knob_reduce : reduce_decision(c->size, count, esz);
-    c->last_alg = ra;
-    ExprPool ep;
     Program pr;
-    if (!compile_expr(ep, expr_reduce(ep, ra, c->size, root), c->size, &pr))
-        return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
+    int ra;
+    if (!reduce_program(c, count, esz, root, &pr, &ra)) return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
+    c->last_alg = ra;
     if (ll_usable(c, count * esz) && (pr.is_fold || c->size <= kTreeMax)) {
         LLArgs a;
         std::memset(&a, 0, sizeof(a));
@@ -1204,7 +1279,9 @@ static int reduce_scatter_block_impl(mi355x_comm_t *c, const void *sbuf, void *r
     hipStream_t s = resolve_stream(stream);
     const size_t esz = mi355x_type_size(type);
     const void *in = sbuf ? sbuf : rbuf;
-    const int ra = c->knob_reduce ? c->knob_reduce : reduce_decision(c->size, count, esz);
+    Program pr;
+    int ra;
+    if (!reduce_program(c, count, esz, 0, &pr, &ra)) return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
     c->last_alg = ra;
     const bool inplace = (in == (const void *)rbuf);
     if (inplace) {
@@ -1218,10 +1295,6 @@ static int reduce_scatter_block_impl(mi355x_comm_t *c, const void *sbuf, void *r
     bool staged = false;
     rc = exchange(c, 1, mine, sig, P, &staged);
     if (rc) return rc;
-    ExprPool ep;
-    Program pr;
-    if (!compile_expr(ep, expr_reduce(ep, ra, c->size, 0), c->size, &pr))
-        return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
     if (staged) {
         std::vector<size_t> boff(c->size), blen(c->size, rcount);
         for (int q = 0; q < c->size; ++q) boff[q] = (size_t)q * rcount;
@@ -1264,7 +1337,7 @@ static int reduce_scatter_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, c
     hipStream_t s = resolve_stream(stream);
     const size_t esz = mi355x_type_size(type);
     const void *in = sbuf ? sbuf : rbuf;
-    const int alg = c->knob_rs ? c->knob_rs : reduce_scatter_decision(c->size, count, esz);
+    const int alg = pick_reduce_scatter(c, count, esz);
     c->last_alg = alg;
     const size_t mine_n = (size_t)rcounts[c->rank];
     const bool inplace = (in == (const void *)rbuf);
@@ -1286,8 +1359,13 @@ static int reduce_scatter_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, c
         pr.is_fold = true;
         pr.order = {0};
         pr.nr = 1;
-    } else if (alg == 2) {
+    } else if (alg == RS_RING) {
         pr = reduce_scatter_ring_block_program(c->size, c->rank);
+    } else if (alg == RS_NONOVERLAPPING) {
+        // reduce of the whole vector to rank 0 (comm->c_coll.coll_reduce) + scatterv
+        // (coll_tuned_reduce_scatter.c:60-121): every block carries the reduce tree's order
+        int ra;
+        if (!reduce_program(c, count, esz, 0, &pr, &ra)) return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
     } else {
         ExprPool ep;
         std::vector<int> roots = expr_reduce_scatter_rechalving(ep, c->size);

@@ -212,18 +212,63 @@ static int calc_level(int f, int r)
     return level - 1;
 }
 
-static std::vector<int> children(int alg, int n, int root, int rank)
+// ompi_coll_tuned_topo_build_chain(fanout, comm, root) (coll_tuned_topo.c:457-603): children of
+// `rank`; the non-root ranks form `fanout` chains hanging off the root
+static void chain_children(int fanout, int n, int root, int sr, std::vector<int> &ch)
+{
+    if (fanout < 1) fanout = 1;
+    if (fanout > 32) fanout = 32;  // MAXTREEFANOUT
+    if (n - 1 < fanout) fanout = n - 1;
+    if (fanout == 1) {
+        if (sr + 1 < n) ch.push_back((sr + 1 + root) % n);
+        return;
+    }
+    if (n == 1) return;
+    int maxchainlen = (n - 1) / fanout, mark;
+    if ((n - 1) % fanout != 0) {
+        maxchainlen++;
+        mark = (n - 1) % fanout;
+    } else {
+        mark = fanout + 1;
+    }
+    if (sr == 0) {  // the root: the heads of the chains (:584-594)
+        int next = (root + 1) % n;
+        ch.push_back(next);
+        for (int i = 1; i < fanout; ++i) {
+            next += maxchainlen;
+            if (i > mark) next--;
+            next %= n;
+            ch.push_back(next);
+        }
+        return;
+    }
+    int head, len;  // (:550-579)
+    if (sr - 1 < mark * maxchainlen) {
+        const int column = (sr - 1) / maxchainlen;
+        head = 1 + column * maxchainlen;
+        len = maxchainlen;
+    } else {
+        const int column = mark + (sr - 1 - mark * maxchainlen) / (maxchainlen - 1);
+        head = mark * maxchainlen + 1 + (column - mark) * (maxchainlen - 1);
+        len = maxchainlen - 1;
+    }
+    if (sr != head + len - 1 && sr + 1 < n) ch.push_back((sr + 1 + root) % n);
+}
+
+static std::vector<int> children(int alg, int n, int root, int rank, int chain_fanout)
 {
     std::vector<int> ch;
     int sr = rank - root;
     if (sr < 0) sr += n;
     switch (alg) {
     case RED_LINEAR:
-    case RED_CHAIN:
     case RED_PIPELINE:
-        // fanout-1 chain (coll_tuned_topo.c:499-511); linear has the order of the chain rooted
+        // fanout-1 chain (coll_tuned_topo.c:515-527); linear has the order of the chain rooted
         // at rank 0 whatever the root (coll_tuned_reduce.c:673-703)
-        if (sr + 1 < n) ch.push_back((sr + 1 + root) % n);
+        chain_children(1, n, root, sr, ch);
+        break;
+    case RED_CHAIN:
+        chain_children(chain_fanout, n, root, sr, ch);
         break;
     case RED_BINARY: {
         // ompi_coll_tuned_topo_build_tree(2, ...) (coll_tuned_topo.c:76-189)
@@ -254,14 +299,14 @@ static std::vector<int> children(int alg, int n, int root, int rank)
     return ch;
 }
 
-int expr_reduce(ExprPool &p, int alg, int n, int root)
+int expr_reduce(ExprPool &p, int alg, int n, int root, int chain_fanout)
 {
     // ompi_coll_tuned_reduce_generic (coll_tuned_reduce.c:66-361), commutative op, not in place:
     //   one child : acc = child (op) own          (child received into accumbuf, :150-160, :211-221)
     //   k children: acc = ((c0 (op) own) (op) c1) ... (op) c(k-1)                      (:189-222)
     const int top = (alg == RED_LINEAR) ? 0 : root;
     std::function<int(int)> eval = [&](int r) -> int {
-        const std::vector<int> ch = children(alg, n, alg == RED_LINEAR ? 0 : root, r);
+        const std::vector<int> ch = children(alg, n, alg == RED_LINEAR ? 0 : root, r, chain_fanout);
         if (ch.empty()) return p.leaf(r);
         int acc = p.op(eval(ch[0]), p.leaf(r));
         for (size_t i = 1; i < ch.size(); ++i) acc = p.op(acc, eval(ch[i]));
@@ -303,8 +348,8 @@ int reduce_scatter_decision(int n, size_t total_count, size_t dsize)
     const size_t total = total_count * dsize;
     int pow2 = 1;
     while (pow2 < n) pow2 <<= 1;
-    if (total <= small || (total <= large && pow2 == n) || (n >= a * (double)total + b)) return 1;
-    return 2;
+    if (total <= small || (total <= large && pow2 == n) || (n >= a * (double)total + b)) return RS_RECHALVING;
+    return RS_RING;
 }
 
 size_t computed_segcount(size_t segsize, size_t typelng, size_t count)

@@ -53,8 +53,12 @@ int expr_allreduce_recursive_doubling(ExprPool &p, int n);
 // as `in` (:480-496).
 Program ring_block_program(int n, int b);
 // MPI_Reduce trees (coll_tuned_reduce.c:66-361, :618-721; topologies coll_tuned_topo.c).
+// The chain (alg 2) hangs `chain_fanout` chains off the root (coll_tuned_topo.c:457-603); the
+// reference's value is the MCA parameter coll_tuned_reduce_algorithm_chain_fanout (default 4,
+// coll_tuned_component.c:51) or the fan-in/out of a dynamic rule.
 enum ReduceAlg { RED_LINEAR = 1, RED_CHAIN = 2, RED_PIPELINE = 3, RED_BINARY = 4, RED_BINOMIAL = 5 };
-int expr_reduce(ExprPool &p, int alg, int n, int root);
+constexpr int kDefaultChainFanout = 4;
+int expr_reduce(ExprPool &p, int alg, int n, int root, int chain_fanout = kDefaultChainFanout);
 // MPI_Reduce_scatter recursive halving (coll_tuned_reduce_scatter.c:141-400): expression of
 // every rank block b (independent of rcounts).
 std::vector<int> expr_reduce_scatter_rechalving(ExprPool &p, int n);
@@ -66,7 +70,9 @@ enum AllreduceAlg { AR_DECISION = 0, AR_LINEAR = 1, AR_NONOVERLAPPING = 2, AR_RE
                     AR_RING_SEGMENTED = 5 };
 int allreduce_decision(int n, size_t count, size_t dsize);            // :42-85
 int reduce_decision(int n, size_t count, size_t dsize);               // :343-446 (commutative)
-int reduce_scatter_decision(int n, size_t total_count, size_t dsize); // :456-502; 1 = rec. halving, 2 = ring
+// reduce_scatter algorithm ids of coll/tuned (coll_tuned_reduce_scatter.c:46-52)
+enum ReduceScatterAlg { RS_NONOVERLAPPING = 1, RS_RECHALVING = 2, RS_RING = 3 };
+int reduce_scatter_decision(int n, size_t total_count, size_t dsize); // :456-502; RS_RECHALVING or RS_RING
 
 // COLL_TUNED_COMPUTED_SEGCOUNT (coll_tuned.h:525-533)
 size_t computed_segcount(size_t segsize, size_t typelng, size_t count);

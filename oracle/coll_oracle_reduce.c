@@ -12,7 +12,8 @@
  *     k >= 2 : acc = ((c0 (op) x) (op) c1) ... (op) c(k-1)     (:189-222)
  * with acc always the `out` (target) operand.  Leaves send x unchanged.  Segmentation does not
  * change the per-element order, so a whole-vector evaluation over the tree is exact.
- * Trees: chain fanout 1 (pipeline, coll_tuned_topo.c:458-527), binary (build_tree(2),
+ * Trees: chain (coll_tuned_topo.c:457-603; fanout 1 = pipeline; reduce_intra_chain uses the
+ * chain_fanout MCA value, default 4), binary (build_tree(2),
  * :76-189), binomial (build_bmtree, :324-398).  basic_linear (coll_tuned_reduce.c:618-721)
  * is rbuf = x(n-1); rbuf = rbuf (op) x(i) for i = n-2..0 -- the chain's order.
  */
@@ -75,13 +76,50 @@ static void bmtree_children(int n, int root, int rank, struct tnode *t)
     }
 }
 
-/* chain with fanout 1 (pipeline) */
-static void chain1_children(int n, int root, int rank, struct tnode *t)
+/* children in ompi_coll_tuned_topo_build_chain(fanout, comm, root) (coll_tuned_topo.c:457-603):
+ * the non-root ranks form `fanout` chains hanging off the root; fanout 1 is the pipeline */
+static void chain_children(int fanout, int n, int root, int rank, struct tnode *t)
 {
     int sr = rank - root;
     if (sr < 0) sr += n;
     t->nchild = 0;
-    if (sr + 1 < n) t->child[t->nchild++] = (sr + 1 + root) % n;
+    if (fanout < 1) fanout = 1;
+    if (fanout > MAXF) fanout = MAXF;
+    if (n - 1 < fanout) fanout = n - 1;
+    if (fanout == 1) {
+        if (sr + 1 < n) t->child[t->nchild++] = (sr + 1 + root) % n;
+        return;
+    }
+    if (n == 1) return;
+    int maxchainlen = (n - 1) / fanout, mark;
+    if ((n - 1) % fanout != 0) {
+        maxchainlen++;
+        mark = (n - 1) % fanout;
+    } else {
+        mark = fanout + 1;
+    }
+    if (sr == 0) {
+        int next = (root + 1) % n;
+        t->child[t->nchild++] = next;
+        for (int i = 1; i < fanout; ++i) {
+            next = next + maxchainlen;
+            if (i > mark) next--;
+            next %= n;
+            t->child[t->nchild++] = next;
+        }
+        return;
+    }
+    int head, len;
+    if (sr - 1 < mark * maxchainlen) {
+        int column = (sr - 1) / maxchainlen;
+        head = 1 + column * maxchainlen;
+        len = maxchainlen;
+    } else {
+        int column = mark + (sr - 1 - mark * maxchainlen) / (maxchainlen - 1);
+        head = mark * maxchainlen + 1 + (column - mark) * (maxchainlen - 1);
+        len = maxchainlen - 1;
+    }
+    if (sr != head + len - 1 && sr + 1 < n) t->child[t->nchild++] = (sr + 1 + root) % n;
 }
 
 struct rctx {
@@ -143,6 +181,13 @@ int oracle_reduce(int alg, int n, int root, size_t count, int type, int op, uint
                   const void *const *sbufs, void *root_rbuf)
 {
     (void)segsize; /* segmentation does not change the per-element order */
+    /* chain fanout: the MCA default ompi_coll_tuned_init_chain_fanout = 4 (coll_tuned_component.c:51) */
+    return oracle_reduce_fo(alg, n, root, 4, count, type, op, sbufs, root_rbuf);
+}
+
+int oracle_reduce_fo(int alg, int n, int root, int chain_fanout, size_t count, int type, int op,
+                     const void *const *sbufs, void *root_rbuf)
+{
     if (n < 1 || root < 0 || root >= n || !oracle_has_op(op, type)) return MI355X_ERR_ARG;
     if (alg == ORACLE_RED_DECISION) alg = oracle_reduce_decision(n, count, type, NULL);
     struct rctx c;
@@ -156,9 +201,9 @@ int oracle_reduce(int alg, int n, int root, size_t count, int type, int op, uint
             /* linear folds x(n-1), x(n-2), .., x(0) whatever the root: the order of a
              * fanout-1 chain rooted at rank 0 */
         case ORACLE_RED_PIPELINE:
-        case ORACLE_RED_CHAIN:
-            chain1_children(n, alg == ORACLE_RED_LINEAR ? 0 : root, r, &c.nodes[r]);
+            chain_children(1, n, alg == ORACLE_RED_LINEAR ? 0 : root, r, &c.nodes[r]);
             break;
+        case ORACLE_RED_CHAIN: chain_children(chain_fanout, n, root, r, &c.nodes[r]); break;
         case ORACLE_RED_BINARY: tree_children(2, n, root, r, &c.nodes[r]); break;
         case ORACLE_RED_BINOMIAL: bmtree_children(n, root, r, &c.nodes[r]); break;
         default: free(c.nodes); return MI355X_ERR_ARG;

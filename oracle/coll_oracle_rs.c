@@ -3,6 +3,7 @@
  * over n ranks in one process with real data.
  *
  * TEST INFRASTRUCTURE ONLY (see oracle.h).
+ *   non-overlapping    coll_tuned_reduce_scatter.c:60-121 (reduce to 0 + scatterv)
  *   recursive halving  coll_tuned_reduce_scatter.c:141-400
  *   ring               coll_tuned_reduce_scatter.c:466-636
  *   decision           coll_tuned_decision_fixed.c:456-502
@@ -96,7 +97,7 @@ static int rs_rechalving(int n, const int *rcounts, int type, int op, const void
     for (int r = 0; r < n; ++r) { free(res[r]); free(snap[r]); }
     free(res); free(snap); free(tmp_rank); free(tmp_rc); free(tmp_d); free(sidx); free(ridx); free(lidx);
     free(disps);
-    return 1;
+    return 2;
 }
 
 static int rs_ring(int n, const int *rcounts, int type, int op, const void *const *sbufs,
@@ -143,7 +144,31 @@ static int rs_ring(int n, const int *rcounts, int type, int op, const void *cons
         free(acc[r]);
     }
     free(acc); free(msg); free(nxt); free(mb); free(nb); free(displs);
-    return 2;
+    return 3;
+}
+
+/* ompi_coll_tuned_reduce_scatter_intra_nonoverlapping (coll_tuned_reduce_scatter.c:60-121):
+ * reduce the whole vector to rank 0 through comm->c_coll.coll_reduce (the tuned reduce
+ * decision on the total count), then scatterv */
+static int rs_nonoverlapping(int n, const int *rcounts, int type, int op, const void *const *sbufs,
+                             void *const *rbufs)
+{
+    size_t total = 0;
+    for (int r = 0; r < n; ++r) total += (size_t)rcounts[r];
+    const size_t esz = oracle_type_size(type);
+    char *full = malloc(total * esz + 1);
+    int rc = oracle_reduce(0, n, 0, total, type, op, 0, sbufs, full);
+    if (rc < 0) {
+        free(full);
+        return rc;
+    }
+    size_t off = 0;
+    for (int r = 0; r < n; ++r) {
+        memcpy(rbufs[r], full + off * esz, (size_t)rcounts[r] * esz);
+        off += (size_t)rcounts[r];
+    }
+    free(full);
+    return 1;
 }
 
 int oracle_reduce_scatter(int n, const int *rcounts, int type, int op,
@@ -155,7 +180,7 @@ int oracle_reduce_scatter(int n, const int *rcounts, int type, int op,
     if (total == 0) return 0;
     if (n == 1) {
         memcpy(rbufs[0], sbufs[0] ? sbufs[0] : rbufs[0], total * oracle_type_size(type));
-        return 2;
+        return 3;
     }
     /* decision_fixed.c:456-502 (commutative) */
     size_t tot_bytes = total * oracle_type_size(type);
@@ -170,7 +195,8 @@ int oracle_reduce_scatter(int n, const int *rcounts, int type, int op,
 int oracle_reduce_scatter_alg(int alg, int n, const int *rcounts, int type, int op,
                               const void *const *sbufs, void *const *rbufs)
 {
-    if (alg == 1) return rs_rechalving(n, rcounts, type, op, sbufs, rbufs);
-    if (alg == 2) return rs_ring(n, rcounts, type, op, sbufs, rbufs);
+    if (alg == 1) return rs_nonoverlapping(n, rcounts, type, op, sbufs, rbufs);
+    if (alg == 2) return rs_rechalving(n, rcounts, type, op, sbufs, rbufs);
+    if (alg == 3) return rs_ring(n, rcounts, type, op, sbufs, rbufs);
     return oracle_reduce_scatter(n, rcounts, type, op, sbufs, rbufs);
 }

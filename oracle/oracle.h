@@ -86,6 +86,9 @@ enum oracle_reduce_alg {
 int oracle_reduce(int alg, int n, int root, size_t count, int type, int op, uint32_t segsize,
                   const void *const *sbufs, void *root_rbuf);
 int oracle_reduce_decision(int n, size_t count, int type, uint32_t *segsize_out);
+/* same with an explicit chain fanout for ORACLE_RED_CHAIN (oracle_reduce uses the default 4) */
+int oracle_reduce_fo(int alg, int n, int root, int chain_fanout, size_t count, int type, int op,
+                     const void *const *sbufs, void *root_rbuf);
 
 /* MPI_Reduce_scatter_block as run by coll/basic (coll_basic_reduce_scatter_block.c:54-111):
  * tuned reduce to rank 0 + scatter.  sbufs[r]: n*rcount elems; rbufs[r]: rcount elems. */
@@ -93,10 +96,11 @@ int oracle_reduce_scatter_block(int n, size_t rcount, int type, int op,
                                 const void *const *sbufs, void *const *rbufs);
 
 /* MPI_Reduce_scatter (vector counts) with the tuned decision (decision_fixed.c:456-502):
- * recursive halving or ring.  Returns 1 = recursive halving, 2 = ring. */
+ * recursive halving or ring.  Algorithm ids are coll/tuned's (coll_tuned_reduce_scatter.c:46-52):
+ * 1 = non-overlapping (reduce to 0 + scatterv), 2 = recursive halving, 3 = ring. */
 int oracle_reduce_scatter(int n, const int *rcounts, int type, int op,
                           const void *const *sbufs, void *const *rbufs);
-/* same with a forced algorithm: 1 = recursive halving, 2 = ring, 0 = decision */
+/* same with a forced algorithm (ids above, 0 = decision) */
 int oracle_reduce_scatter_alg(int alg, int n, const int *rcounts, int type, int op,
                               const void *const *sbufs, void *const *rbufs);
 

@@ -57,6 +57,8 @@ def load_oracle() -> ctypes.CDLL:
         lib.oracle_allreduce_decision.argtypes = [i, sz, i, c.POINTER(c.c_uint32)]
         lib.oracle_reduce.argtypes = [i, i, i, sz, i, i, c.c_uint32, c.POINTER(vp), vp]
         lib.oracle_reduce_decision.argtypes = [i, sz, i, c.POINTER(c.c_uint32)]
+        lib.oracle_reduce_fo.argtypes = [i, i, i, i, sz, i, i, c.POINTER(vp), vp]
+        lib.oracle_reduce_scatter_alg.argtypes = [i, i, c.POINTER(i), i, i, c.POINTER(vp), c.POINTER(vp)]
         lib.oracle_reduce_scatter_block.argtypes = [i, sz, i, i, c.POINTER(vp), c.POINTER(vp)]
         lib.oracle_ring_fold_order.argtypes = [i, sz, sz, c.POINTER(c.c_int)]
         i64 = c.c_int64

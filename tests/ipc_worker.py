@@ -163,6 +163,8 @@ def staged(pkg, comm, rank, size, torch):
 
 def main():
     key, rank, size, dev = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+    import faulthandler
+    faulthandler.dump_traceback_later(150, exit=True)  # a rank stuck in a HIP call names its line
     import torch
     torch.cuda.set_device(dev)
     pkg = load_pkg()

@@ -177,7 +177,7 @@ def test_reduce_scatter_block(gpu, pkg, oracle, comms, n, inplace):
 
 
 @pytest.mark.parametrize("n", [2, 3, 5, 8])
-@pytest.mark.parametrize("rsalg", [0, 1, 2])
+@pytest.mark.parametrize("rsalg", [0, 1, 2, 3])
 def test_reduce_scatter(gpu, pkg, oracle, comms, n, rsalg):
     torch = gpu
     cs = comms(n)
@@ -346,7 +346,7 @@ def test_staged_reduce(gpu, pkg, oracle, staged_comms):
             opdata.assert_same(tname, opname, from_dev(dr, want), want, f"staged reduce root={root}")
 
 
-@pytest.mark.parametrize("rsalg", [1, 2])
+@pytest.mark.parametrize("rsalg", [1, 2, 3])
 def test_staged_reduce_scatter(gpu, pkg, oracle, staged_comms, rsalg):
     torch = gpu
     n = 4
@@ -474,3 +474,76 @@ def test_nonblocking(gpu, pkg, oracle, comms, n):
         assert torch.equal(gdst[r], want_g), r
         assert torch.equal(bb[r], bwant), r
     opdata.assert_same("FLOAT", "SUM", from_dev(rr, wr), wr, "ireduce")
+
+
+def test_dynamic_rules(gpu, pkg, oracle, comms, tmp_path):
+    """coll/tuned's dynamic rules file drives the choice per message size: allreduce recursive
+    doubling below 4 KiB and ring above it for 4-rank communicators; reduce = chain with fan-out 2;
+    reduce_scatter = ring.  Results equal the oracle's for the algorithm the rule names."""
+    torch = gpu
+    n = 4
+    cs = comms(n)
+    f = tmp_path / "rules.conf"
+    f.write_text("""# collectives
+3
+2   # ALLREDUCE
+1   # one communicator size
+4 2 # size 4, two message sizes
+0    3 0 0
+4096 4 0 0
+11  # REDUCE
+1
+2 1
+0 2 2 0
+12  # REDUCESCATTER
+1
+2 1
+0 3 0 0
+""")
+    rules = pkg.Rules(str(f))
+    assert rules.ncoll == 3
+    for c in cs:
+        c.set_rules(rules)
+    try:
+        op, ty = pkg.OP["SUM"], pkg.T["FLOAT"]
+        for count, alg in ((100, 3), (5000, 4)):
+            xs = [opdata.make("FLOAT", count, 1500 + r) for r in range(n)]
+            outs = [np.zeros_like(xs[0]) for _ in range(n)]
+            assert oracle.oracle_allreduce(alg, n, count, ty, op, 0, _ptrs(xs), _ptrs(outs)) == alg
+            dx = [to_dev(torch, x) for x in xs]
+            dr = [torch.zeros_like(t) for t in dx]
+            torch.cuda.synchronize()
+            run_ranks(n, lambda r: cs[r].allreduce(dx[r].data_ptr(), dr[r].data_ptr(), count, ty, op))
+            torch.cuda.synchronize()
+            assert cs[0].last_algorithm() == alg
+            for r in range(n):
+                opdata.assert_same("FLOAT", "SUM", from_dev(dr[r], outs[r]), outs[r], f"rules allreduce {count}")
+        count = 3001
+        xs = [opdata.make("FLOAT", count, 1600 + r) for r in range(n)]
+        want = np.zeros_like(xs[0])
+        assert oracle.oracle_reduce_fo(2, n, 1, 2, count, ty, op, _ptrs(xs), want.ctypes.data) == 2
+        dx = [to_dev(torch, x) for x in xs]
+        dr = torch.zeros_like(dx[0])
+        torch.cuda.synchronize()
+        run_ranks(n, lambda r: cs[r].reduce(dx[r].data_ptr(), dr.data_ptr() if r == 1 else None, count, ty, op, 1))
+        torch.cuda.synchronize()
+        assert cs[0].last_algorithm() == 2
+        opdata.assert_same("FLOAT", "SUM", from_dev(dr, want), want, "rules reduce chain fan-out 2")
+        rcounts = [100, 7, 0, 900]
+        xs = [opdata.make("FLOAT", sum(rcounts), 1700 + r) for r in range(n)]
+        outs = [np.zeros(max(k, 1), dtype=np.float32) for k in rcounts]
+        rc = (ctypes.c_int * n)(*rcounts)
+        assert oracle.oracle_reduce_scatter_alg(3, n, rc, ty, op, _ptrs(xs), _ptrs(outs)) == 3
+        dx = [to_dev(torch, x) for x in xs]
+        dr = [torch.zeros(max(k, 1) * 4, dtype=torch.uint8, device="cuda") for k in rcounts]
+        torch.cuda.synchronize()
+        run_ranks(n, lambda r: cs[r].reduce_scatter(dx[r].data_ptr(), dr[r].data_ptr(), rcounts, ty, op))
+        torch.cuda.synchronize()
+        assert cs[0].last_algorithm() == 3
+        for r in range(n):
+            if rcounts[r]:
+                opdata.assert_same("FLOAT", "SUM", from_dev(dr[r], outs[r], rcounts[r]), outs[r][:rcounts[r]], "rules rs")
+    finally:
+        for c in cs:
+            c.set_rules(None)
+        rules.destroy()

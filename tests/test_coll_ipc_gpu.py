@@ -32,7 +32,8 @@ def test_ipc_ranks(gpu, size):
             p.kill()
             out, _ = p.communicate()
         outs.append(out)
+    failed = [r for r, p in enumerate(procs) if p.returncode != 0]
+    assert not failed, "\n".join(f"rank {r} failed (rc {procs[r].returncode}):\n{outs[r][-2500:]}" for r in failed)
     for r, p in enumerate(procs):
-        assert p.returncode == 0, f"rank {r} failed:\n{outs[r][-3000:]}"
         for stage in ("LL OK", "staged OK", "OK"):
             assert f"rank {r} {stage}" in outs[r], f"rank {r} did not report '{stage}':\n{outs[r][-3000:]}"

@@ -83,25 +83,47 @@ def _ring_block(count, n, b):
 
 
 @pytest.mark.parametrize("n", [2, 3, 4, 5, 7, 8, 13])
-@pytest.mark.parametrize("ralg", [1, 3, 4, 5])
+@pytest.mark.parametrize("ralg", [1, 2, 3, 4, 5])
 def test_reduce_programs(pkg, oracle, n, ralg):
     count = 101
     for opname, tname in CASES:
         op, ty = pkg.OP[opname], pkg.T[tname]
         xs = [opdata.make(tname, count, 30 + r) for r in range(n)]
-        want = np.zeros_like(xs[0])
-        assert oracle.oracle_reduce(ralg, n, 0, count, ty, op, 0, _ptrs(xs), want.ctypes.data) == ralg
-        prog = pkg.sched_program(2, n, ralg, 0)
-        got = eval_program(oracle, prog, op, ty, xs)
-        opdata.assert_same(tname, opname, got, want, f"reduce alg={ralg} n={n}")
+        for root in sorted({0, n // 2, n - 1}):
+            want = np.zeros_like(xs[0])
+            assert oracle.oracle_reduce(ralg, n, root, count, ty, op, 0, _ptrs(xs), want.ctypes.data) == ralg
+            prog = pkg.sched_program(2, n, ralg, root)
+            got = eval_program(oracle, prog, op, ty, xs)
+            opdata.assert_same(tname, opname, got, want, f"reduce alg={ralg} n={n} root={root}")
+
+
+@pytest.mark.parametrize("n", [3, 5, 6, 8, 13, 16])
+@pytest.mark.parametrize("fanout", [1, 2, 3, 4, 7, 32])
+def test_reduce_chain_fanouts(pkg, oracle, n, fanout):
+    """ompi_coll_tuned_topo_build_chain with every shape of chains (even and uneven splits)"""
+    count = 64
+    xs = [opdata.make("FLOAT", count, 60 + r) for r in range(n)]
+    want = np.zeros_like(xs[0])
+    assert oracle.oracle_reduce_fo(2, n, 0, fanout, count, pkg.T["FLOAT"], pkg.OP["SUM"], _ptrs(xs),
+                                   want.ctypes.data) == 2
+    got = eval_program(oracle, pkg.sched_program(5, n, 0, fanout), pkg.OP["SUM"], pkg.T["FLOAT"], xs)
+    opdata.assert_same("FLOAT", "SUM", got, want, f"chain n={n} fanout={fanout}")
+
+
+def test_chain_fanout_changes_the_order(pkg, oracle):
+    """the forced chain (alg 2) is NOT the pipeline when the fan-out is > 1 (default 4)"""
+    n, count = 9, 4096
+    xs = [np.nan_to_num(opdata.make("FLOAT", count, 80 + r), nan=0.0, posinf=1.0, neginf=-1.0) for r in range(n)]
+    a, b = np.zeros_like(xs[0]), np.zeros_like(xs[0])
+    oracle.oracle_reduce_fo(2, n, 0, 4, count, 14, 3, _ptrs(xs), a.ctypes.data)
+    oracle.oracle_reduce_fo(2, n, 0, 1, count, 14, 3, _ptrs(xs), b.ctypes.data)
+    assert (a.view(np.uint32) != b.view(np.uint32)).sum() > 100
 
 
 @pytest.mark.parametrize("n", [2, 3, 4, 5, 6, 7, 8, 12])
-@pytest.mark.parametrize("rsalg", [1, 2])
+@pytest.mark.parametrize("rsalg", [1, 2, 3])
 def test_reduce_scatter_programs(pkg, oracle, n, rsalg):
-    oracle.oracle_reduce_scatter_alg.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
-                                                 ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
-                                                 ctypes.POINTER(ctypes.c_void_p)]
+    """coll/tuned ids: 1 non-overlapping (reduce to 0 + scatterv), 2 recursive halving, 3 ring"""
     rng = np.random.default_rng(n)
     rcounts = [int(v) for v in rng.integers(0, 9, n)]
     rcounts[0] = max(rcounts[0], 1)
@@ -116,7 +138,11 @@ def test_reduce_scatter_programs(pkg, oracle, n, rsalg):
         for b in range(n):
             if rcounts[b] == 0:
                 continue
-            prog = pkg.sched_program(3 if rsalg == 2 else 4, n, 0, b)
+            if rsalg == 1:   # every block carries the reduce tree (decision on the total count)
+                ralg = oracle.oracle_reduce_decision(n, total, ty, None)
+                prog = pkg.sched_program(2, n, ralg, 0)
+            else:
+                prog = pkg.sched_program(3 if rsalg == 3 else 4, n, 0, b)
             lo, hi = disp[b], disp[b + 1]
             got = eval_program(oracle, prog, op, ty, [x[lo:hi] for x in xs])
             opdata.assert_same(tname, opname, got, outs[b][:rcounts[b]], f"rs alg={rsalg} n={n} b={b}")
