@@ -139,6 +139,41 @@ def extra_legs(args, pkg, torch, comm, world, rank, dev, legs):
     del buf, packed, red
     d.destroy()
     torch.cuda.empty_cache()
+    # xGMI link bandwidth (the busbw denominator, BASELINE.md §2: "must be measured"): ranks 0 and
+    # 1 alone, each pulling 256 MiB from the other over their one link (both directions at once)
+    if torch.cuda.device_count() >= world:
+        _log(rank, "leg xgmi_link")
+        try:
+            nb = 256 << 20
+            if rank < 2:
+                pair = pkg.Comm.create(f"{os.environ.get('TORCHELASTIC_RUN_ID', 'x')}_{os.environ.get('MASTER_PORT', '0')}_pair",
+                                       rank, 2, dev.index)
+                pair.set("TIMEOUT_S", 120)
+                src = torch.full((nb,), rank + 1, dtype=torch.uint8, device=dev)
+                dst = torch.empty((2 * nb,), dtype=torch.uint8, device=dev)
+                for _ in range(2):
+                    pair.allgather(src.data_ptr(), dst.data_ptr(), nb)
+                torch.cuda.synchronize()
+                pair.barrier()
+                t0 = time.perf_counter()
+                for _ in range(5):
+                    pair.allgather(src.data_ptr(), dst.data_ptr(), nb)
+                torch.cuda.synchronize()
+                t_l = (time.perf_counter() - t0) / 5
+                ok_l = int(dst[:nb].max()) == 1 and int(dst[nb:].min()) == 2
+                pair.destroy()
+                del src, dst
+            else:
+                t_l, ok_l = 0.0, True
+            t = torch.tensor([t_l, 0.0 if ok_l else 1.0], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            legs["xgmi_link_pull_256MiB"] = {"ms": round(float(t[0]) * 1e3, 3),
+                                             "GBs_per_direction": round(nb / float(t[0]) / 1e9, 2),
+                                             "exact": float(t[1]) == 0.0,
+                                             "note": "ranks 0,1 only; each pulls 256 MiB from the other"}
+        except Exception as e:
+            legs["xgmi_link_pull_256MiB"] = {"error": repr(e)[:300]}
+        torch.cuda.empty_cache()
     # comparison point only (BASELINE north star): RCCL's allreduce on the same device buffers,
     # through torch.distributed's "nccl" backend (= RCCL on ROCm).  Needs one GPU per rank.
     if torch.cuda.device_count() >= world:
