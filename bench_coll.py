@@ -216,7 +216,7 @@ def run(args, pkg, torch):
     n = GIB // 4
     dev = torch.device("cuda", local)
     ty, op = pkg.T["FLOAT"], pkg.OP["SUM"]
-    # launch-shape autotune on the real size (pull vs push data flow x blocks per CU), with the
+    # launch-shape autotune on the real size (blocks per CU of the pull data flow), with the
     # exactness check on every candidate: x_r = r + 1 everywhere -> every element = n(n+1)/2.
     # All ranks see the same max-over-ranks times, so they pick the same candidate.
     x = torch.full((n,), float(rank + 1), device=dev)
@@ -224,7 +224,9 @@ def run(args, pkg, torch):
     want = world * (world + 1) / 2
     ok = True
     tried = []
-    for push in (0, 1):
+    # pull only: the push flow writes into peers' memory behind their L2 (coarse-grained memory is
+    # not probed), which is safe on one device but not across xGMI -- it is not a valid candidate
+    for push in (0,):
         for bpc in (2, 4, 8):
             _log(rank, f"autotune push={push} blocks_per_cu={bpc}")
             comm.set("PUSH", push)

@@ -111,7 +111,9 @@ enum mi355x_knob {
     MI355X_KNOB_REDUCE_SCATTER_ALG = 3, /* coll_tuned_reduce_scatter_algorithm */
     MI355X_KNOB_BLOCKS_PER_CU = 4,
     MI355X_KNOB_TIMEOUT_S = 5,
-    MI355X_KNOB_PUSH = 6,               /* 1: one-phase push data flow (owners write peers' buffers) */
+    MI355X_KNOB_PUSH = 6,               /* 1: one-phase push data flow (owners write peers' buffers);
+                                           single-device use only: across xGMI the remote writes land
+                                           behind the owner's L2 (see coll_internal.hpp) */
     MI355X_KNOB_IPC_MAX_BYTES = 7,      /* buffers in allocations of >= this many bytes are never
                                            exported; calls touching one take the staged data flow
                                            (default 2^31: hipIpcOpenMemHandle hangs from 2 GiB) */

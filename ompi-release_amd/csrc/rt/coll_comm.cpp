@@ -123,6 +123,7 @@ struct HandleKey {
 struct PeerMap {
     uint64_t id;
     void *mapped;
+    uint64_t last_use;  // call (seq) that last used the mapping
 };
 
 struct LocalReg {
@@ -318,13 +319,33 @@ static int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out)
     void *base;
     if (it != c->peer_maps.end()) {
         base = it->second.mapped;
+        it->second.last_use = c->seq;
     } else {
         TRACE(c, "open peer %d base %llx id %llu", peer, (unsigned long long)d.base, (unsigned long long)d.id);
         hipError_t e = hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess);
         TRACE(c, "opened peer %d -> %p (%s)", peer, base, hipGetErrorString(e));
-        if (e != hipSuccess)
-            return set_error(MI355X_ERR_PEER, "hipIpcOpenMemHandle(rank %d): %s", peer, hipGetErrorString(e));
-        c->peer_maps[key] = PeerMap{d.id, base};
+        if (e != hipSuccess) {
+            // A mapping of an allocation the peer has since freed can still hold the block the new
+            // allocation was carved from (small allocations share blocks): the open then fails
+            // with "invalid device pointer".  Drop this peer's mappings that the current call does
+            // not use and try once more.
+            (void)hipGetLastError();
+            int dropped = 0;
+            for (auto m = c->peer_maps.begin(); m != c->peer_maps.end();) {
+                if (m->first.peer == peer && m->second.last_use != c->seq) {
+                    (void)hipIpcCloseMemHandle(m->second.mapped);
+                    m = c->peer_maps.erase(m);
+                    dropped++;
+                } else {
+                    ++m;
+                }
+            }
+            TRACE(c, "open failed; dropped %d stale mappings of peer %d, retrying", dropped, peer);
+            e = dropped ? hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess) : e;
+            if (e != hipSuccess)
+                return set_error(MI355X_ERR_PEER, "hipIpcOpenMemHandle(rank %d): %s", peer, hipGetErrorString(e));
+        }
+        c->peer_maps[key] = PeerMap{d.id, base, c->seq};
     }
     *out = (char *)base + d.off;
     return MI355X_SUCCESS;
@@ -393,14 +414,19 @@ static int finish(mi355x_comm *c, hipStream_t s)
     return barrier(c);
 }
 
+// The scratch may be exported to peers (MPI_Reduce's owner blocks): never a small allocation
+// (small hipMallocs can fail hipIpcOpenMemHandle on the importer with "invalid device
+// pointer"), and grown geometrically so it is rarely freed while peers hold a mapping.
 static int ensure_scratch(mi355x_comm *c, size_t bytes)
 {
     if (c->scratch_bytes >= bytes) return MI355X_SUCCESS;
+    size_t want = std::max<size_t>((size_t)8 << 20, c->scratch_bytes * 2);
+    while (want < bytes) want *= 2;
     if (c->scratch) MI_HIP(hipFree(c->scratch));
     c->scratch = nullptr;
     c->scratch_bytes = 0;
-    MI_HIP(hipMalloc(&c->scratch, bytes ? bytes : 1));
-    c->scratch_bytes = bytes;
+    MI_HIP(hipMalloc(&c->scratch, want));
+    c->scratch_bytes = want;
     return MI355X_SUCCESS;
 }
 
@@ -1209,8 +1235,8 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
 // rbuf); rbuf is read on the root only.  The result of every element is the reference tree's
 // expression (linear / chain / pipeline / binary / binomial), evaluated:
 //   small  : LL one-shot, every rank pushes to the root, the root evaluates;
-//   large  : owner-computes -- rank r evaluates ring block r from the n inputs and writes it
-//            straight into the root's rbuf (one phase, each link carries S/n);
+//   large  : owner-computes -- rank r evaluates ring block r from the n inputs into its own
+//            memory, then the root pulls the blocks (each link carries 2 S/n, writes stay local);
 //   staged : (allocations >= ipc_max) the root evaluates everything through the staging buffers.
 static int reduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int root,
                   void *stream)
@@ -1247,8 +1273,14 @@ static int reduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t co
         ll_program(a, pr);
         return ll_run(c, a, op, type, s);
     }
+    size_t off, len;
+    ring_block(count, c->size, c->rank, &off, &len);
+    if (!am_root) {
+        rc = ensure_scratch(c, len * esz);
+        if (rc) return rc;
+    }
     MI_HIP(hipStreamSynchronize(s));
-    const void *mine[2] = {in, am_root ? rbuf : nullptr};
+    const void *mine[2] = {in, am_root ? nullptr : c->scratch};
     const uint64_t sig[4] = {6, count, ((uint64_t)type << 32) | (uint64_t)op, (uint64_t)root};
     std::vector<std::vector<void *>> P;
     bool staged = false;
@@ -1259,12 +1291,32 @@ static int reduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t co
         blen[root] = count;
         return staged_reduce(c, op, type, pr, in, boff, blen, am_root ? rbuf : nullptr, false, nullptr, s);
     }
-    size_t off, len;
-    ring_block(count, c->size, c->rank, &off, &len);
-    std::vector<void *> dst(1, P[1][root]);
-    rc = run_program(op, type, pr, P[0], dst, off, len, s);
+    // phase 1: every rank evaluates its ring block from the n inputs into its own memory (the root
+    // straight into rbuf); phase 2: the root pulls the other blocks (one segment per peer).  Only
+    // local writes: a remote write would land in HBM behind the root's L2, which may hold the
+    // old lines of rbuf (coarse-grained memory is not probed).
+    void *mydst = am_root ? (void *)((char *)rbuf + off * esz) : c->scratch;
+    std::vector<void *> d0(1, (char *)mydst - off * esz);  // run_program offsets by off
+    rc = run_program(op, type, pr, P[0], d0, off, len, s);
     if (rc) return rc;
-    return finish(c, s);
+    rc = finish(c, s);
+    if (rc) return rc;
+    if (am_root) {
+        MultiCopyArgs m;
+        std::memset(&m, 0, sizeof(m));
+        for (int q = 0; q < c->size; ++q) {
+            size_t qo, ql;
+            ring_block(count, c->size, q, &qo, &ql);
+            if (q == root || ql == 0) continue;
+            m.src[m.nseg] = P[1][q];
+            m.dst[m.nseg] = (char *)rbuf + qo * esz;
+            m.len[m.nseg] = ql * esz;
+            m.nseg++;
+        }
+        rc = launch_multicopy(m, s);
+        if (rc) return rc;
+    }
+    return finish(c, s);  // the peers keep their scratch until the root has pulled it
 }
 
 // MPI_Reduce_scatter_block as coll/basic runs it: tuned reduce to 0 + scatter

@@ -87,7 +87,11 @@ int launch_ll_copy(const LLArgs &a, hipStream_t s);                   // LL_AG /
 
 struct CollTune {
     int blocks_per_cu = 4;
-    int push = 0;   // 1: allreduce owners write into the peers' rbufs (one phase); 0: pull (two phases)
+    // 1: allreduce owners write into the peers' rbufs (one phase); 0: pull (two phases, default).
+    // Push is correct on one device only: across xGMI a remote write lands in HBM behind the
+    // owner's L2, which may still hold old lines of the destination (coarse-grained memory is not
+    // probed), so the owner could read stale data afterwards.
+    int push = 0;
 };
 CollTune &coll_tune();
 

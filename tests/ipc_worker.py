@@ -38,6 +38,22 @@ def realloc_same_address(pkg, comm, rank, size):
         comm.barrier()  # every rank is done with the peers' allocations before they are freed
         assert lib.mi355x_free(p) == 0
     print(f"rank {rank} realloc addresses {'same' if len(set(addrs)) == 1 else 'differ'}", flush=True)
+    # small allocations of changing sizes share blocks: a freed allocation's stale mapping must
+    # not make the next import fail (direct path: LL off)
+    comm.set("LL_MAX_BYTES", 0)
+    for gen, kib in enumerate((64, 200, 48, 800, 96, 1500, 32)):
+        n = kib * 256
+        p = ctypes.c_void_p()
+        assert lib.mi355x_malloc(ctypes.byref(p), n * 4) == 0
+        host = np.full(n, float(rank + 1 + gen), dtype=np.float32)
+        assert lib.mi355x_memcpy(p, host.ctypes.data, n * 4) == 0
+        comm.allreduce(None, p.value, n, pkg.T["FLOAT"], pkg.OP["SUM"])
+        out = np.empty(n, dtype=np.float32)
+        assert lib.mi355x_memcpy(out.ctypes.data, p, n * 4) == 0
+        assert np.all(out == sum(r + 1 + gen for r in range(size))), ("growing realloc", kib)
+        comm.barrier()
+        assert lib.mi355x_free(p) == 0
+    comm.set("LL_MAX_BYTES", 64 << 10)
 
 
 def ll_checks(pkg, comm, rank, size, oracle, torch):
