@@ -26,6 +26,8 @@
 #include <fcntl.h>
 #include <sched.h>
 #include <sys/mman.h>
+#include <sys/prctl.h>
+#include <sys/syscall.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -83,7 +85,10 @@ struct BufDesc {
     uint64_t present;  // 0: NULL buffer
     uint64_t base;     // exporter's allocation base (its VA; the peer-map key)
     uint64_t id;       // exporter's allocation id (HIP_POINTER_ATTRIBUTE_BUFFER_ID)
-    uint64_t staged;   // 1: allocation too large to export -> the call takes the staged data flow
+    uint64_t staged;   // 1: allocation too large for hipIpc* (>= ipc_max): dmabuf or staged flow
+    uint64_t size;     // dmabuf: the exported allocation's size
+    int32_t dmabuf;    // 1: exported as a dmabuf fd (fd is a descriptor of the exporter process)
+    int32_t fd;
 };
 
 struct alignas(64) RankSlot {
@@ -91,6 +96,8 @@ struct alignas(64) RankSlot {
     int32_t pid, dev, nbuf, pad;
     uint64_t sig[4];
     BufDesc buf[kMaxBufs];
+    int32_t probe_fd, probe_ok;   // dmabuf capability probe
+    uint64_t probe_size;
 };
 
 struct Ctrl {
@@ -123,16 +130,34 @@ struct HandleKey {
 struct PeerMap {
     uint64_t id;
     void *mapped;
-    uint64_t last_use;  // call (seq) that last used the mapping
+    uint64_t last_use;             // call (seq) that last used the mapping
+    hipExternalMemory_t ext;       // dmabuf import (NULL: hipIpcOpenMemHandle mapping)
 };
+
+static void close_map(PeerMap &m)
+{
+    if (m.ext) {
+        (void)hipFree(m.mapped);
+        (void)hipDestroyExternalMemory(m.ext);
+    } else {
+        (void)hipIpcCloseMemHandle(m.mapped);
+    }
+}
 
 struct LocalReg {
     uintptr_t base;
     size_t size;
     uint64_t id;
     hipIpcMemHandle_t h;
-    bool has_h;       // false: too large to export (never passed to hipIpcGetMemHandle)
+    bool has_h;       // false: too large for hipIpc* (never passed to hipIpcGetMemHandle)
+    int fd;           // dmabuf export of a large allocation (-1: none yet)
 };
+
+static void drop_reg(LocalReg &r)
+{
+    if (r.fd >= 0) close(r.fd);
+    r.fd = -1;
+}
 
 struct LoopShared {
     Ctrl *ctrl = nullptr;
@@ -161,6 +186,9 @@ struct mi355x_comm {
     std::vector<mi355x::LocalReg> local_regs;
     void *scratch = nullptr;
     size_t scratch_bytes = 0;
+    int dmabuf_state = 0;                         // large allocations via dmabuf: 0 unknown, 1 yes, -1 no
+    bool ptracer_any = false;                     // PR_SET_PTRACER_ANY done (peers pidfd_getfd our fds)
+    std::map<int, int> pidfds;                    // peer rank -> pidfd
     void *stage = nullptr;                        // staging buffer of the staged data flow
     size_t stage_bytes = (size_t)1 << 30;         // its size (an allocation below ipc_max)
     size_t ipc_max = (size_t)1 << 31;             // allocations >= this are never exported
@@ -260,6 +288,10 @@ static int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
             if (r.id == id && id != 0 && (r.has_h || !force)) {
                 if (!force && r.size >= c->ipc_max) {
                     d->staged = 1;
+                    d->base = r.base;
+                    d->off = up - r.base;
+                    d->id = r.id;
+                    d->size = r.size;
                     return MI355X_SUCCESS;
                 }
                 d->h = r.h;
@@ -268,6 +300,7 @@ static int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
                 d->id = r.id;
                 return MI355X_SUCCESS;
             }
+            drop_reg(c->local_regs[i]);
             c->local_regs.erase(c->local_regs.begin() + (long)i);  // freed and reallocated: stale
             break;
         }
@@ -278,6 +311,7 @@ static int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
     TRACE(c, "register %p: base %p size %zu id %llu", p, base, sz, (unsigned long long)id);
     LocalReg reg;
     std::memset(&reg, 0, sizeof(reg));
+    reg.fd = -1;
     reg.base = (uintptr_t)base;
     reg.size = sz;
     reg.id = id;
@@ -286,6 +320,10 @@ static int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
         reg.has_h = false;
         if (id != 0) c->local_regs.push_back(reg);
         d->staged = 1;
+        d->base = reg.base;
+        d->off = up - reg.base;
+        d->id = id;
+        d->size = sz;
         return MI355X_SUCCESS;
     }
     MI_HIP(hipIpcGetMemHandle(&reg.h, base));
@@ -297,6 +335,127 @@ static int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
     d->base = reg.base;
     d->id = id;
     return MI355X_SUCCESS;
+}
+
+// ----------------------------------------------------------------- dmabuf export of large allocations
+// hipIpcOpenMemHandle never returns for allocations of >= 2 GiB (ROCm 7.2, dmabuf IPC), but the
+// allocation exported as a dmabuf fd (hipMemGetHandleForAddressRange), fetched by the peer with
+// pidfd_getfd and imported as external memory maps fine (tools/probe/dmabuf_xproc.hip).  The
+// exporter lets same-user processes read its descriptors (PR_SET_PTRACER_ANY, which yama's
+// ptrace_scope 1 requires for pidfd_getfd between siblings).
+static int export_dmabuf(mi355x_comm *c, BufDesc *d)
+{
+    for (LocalReg &r : c->local_regs) {
+        if (r.base != d->base || r.id != d->id) continue;
+        if (r.fd < 0) {
+            if (!c->ptracer_any) {
+                prctl(PR_SET_PTRACER, PR_SET_PTRACER_ANY, 0, 0, 0);
+                c->ptracer_any = true;
+            }
+            MI_HIP(hipMemGetHandleForAddressRange(&r.fd, (hipDeviceptr_t)r.base, r.size,
+                                                  hipMemRangeHandleTypeDmaBufFd, 0));
+        }
+        d->dmabuf = 1;
+        d->fd = r.fd;
+        d->size = r.size;
+        return MI355X_SUCCESS;
+    }
+    return set_error(MI355X_ERR_PEER, "large allocation not registered (id %llu)", (unsigned long long)d->id);
+}
+
+static int import_dmabuf(mi355x_comm *c, int peer, int fd, size_t size, void **mapped, hipExternalMemory_t *ext)
+{
+    auto pit = c->pidfds.find(peer);
+    if (pit == c->pidfds.end()) {
+        const int pfd = (int)syscall(SYS_pidfd_open, (pid_t)c->ctrl->slot[peer].pid, 0);
+        if (pfd < 0) return set_error(MI355X_ERR_PEER, "pidfd_open(rank %d): %s", peer, strerror(errno));
+        pit = c->pidfds.emplace(peer, pfd).first;
+    }
+    const int myfd = (int)syscall(SYS_pidfd_getfd, pit->second, fd, 0);
+    if (myfd < 0) return set_error(MI355X_ERR_PEER, "pidfd_getfd(rank %d): %s", peer, strerror(errno));
+    hipExternalMemoryHandleDesc hd;
+    std::memset(&hd, 0, sizeof(hd));
+    hd.type = hipExternalMemoryHandleTypeOpaqueFd;
+    hd.handle.fd = myfd;
+    hd.size = size;
+    hipError_t e = hipImportExternalMemory(ext, &hd);
+    if (e != hipSuccess) {
+        close(myfd);
+        return set_error(MI355X_ERR_PEER, "hipImportExternalMemory(rank %d): %s", peer, hipGetErrorString(e));
+    }
+    hipExternalMemoryBufferDesc bd;
+    std::memset(&bd, 0, sizeof(bd));
+    bd.offset = 0;
+    bd.size = size;
+    e = hipExternalMemoryGetMappedBuffer(mapped, *ext, &bd);
+    if (e != hipSuccess) {
+        (void)hipDestroyExternalMemory(*ext);
+        return set_error(MI355X_ERR_PEER, "hipExternalMemoryGetMappedBuffer(rank %d): %s", peer, hipGetErrorString(e));
+    }
+    TRACE(c, "dmabuf import from rank %d: %zu bytes at %p", peer, size, *mapped);
+    return MI355X_SUCCESS;
+}
+
+static int barrier(mi355x_comm *c);
+
+// Collective, once per communicator: every rank exports a 4 MiB buffer as a dmabuf, every rank
+// imports every peer's and checks its bytes; the path is used only if it worked everywhere.
+static int probe_dmabuf(mi355x_comm *c)
+{
+    const char *env = getenv("MI355X_DMABUF");
+    bool ok = !(env && atoi(env) == 0);
+    const size_t sz = (size_t)4 << 20;
+    void *buf = nullptr;
+    int fd = -1;
+    RankSlot &me = c->ctrl->slot[c->rank];
+    if (ok && hipMalloc(&buf, sz) != hipSuccess) ok = false;
+    if (ok && hipMemset(buf, c->rank + 1, sz) != hipSuccess) ok = false;
+    if (ok && hipDeviceSynchronize() != hipSuccess) ok = false;
+    if (ok) {
+        if (!c->ptracer_any) {
+            prctl(PR_SET_PTRACER, PR_SET_PTRACER_ANY, 0, 0, 0);
+            c->ptracer_any = true;
+        }
+        if (hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)buf, sz, hipMemRangeHandleTypeDmaBufFd, 0) != hipSuccess)
+            ok = false;
+    }
+    (void)hipGetLastError();
+    me.probe_fd = ok ? fd : -1;
+    me.probe_size = sz;
+    int rc = barrier(c);
+    if (rc) return rc;
+    for (int q = 0; q < c->size && ok; ++q) {
+        if (q == c->rank) continue;
+        const RankSlot &o = c->ctrl->slot[q];
+        if (o.probe_fd < 0) {
+            ok = false;
+            break;
+        }
+        void *mapped = nullptr;
+        hipExternalMemory_t ext = nullptr;
+        if (import_dmabuf(c, q, o.probe_fd, o.probe_size, &mapped, &ext) != MI355X_SUCCESS) {
+            ok = false;
+            break;
+        }
+        unsigned char v[2] = {0, 0};
+        if (hipMemcpy(&v[0], mapped, 1, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(&v[1], (char *)mapped + sz - 1, 1, hipMemcpyDeviceToHost) != hipSuccess ||
+            v[0] != (unsigned char)(q + 1) || v[1] != (unsigned char)(q + 1))
+            ok = false;
+        (void)hipFree(mapped);
+        (void)hipDestroyExternalMemory(ext);
+        (void)hipGetLastError();
+    }
+    me.probe_ok = ok ? 1 : 0;
+    rc = barrier(c);  // every rank is done importing before the probe buffers go
+    if (fd >= 0) close(fd);
+    if (buf) (void)hipFree(buf);
+    if (rc) return rc;
+    bool all = true;
+    for (int q = 0; q < c->size; ++q) all = all && c->ctrl->slot[q].probe_ok == 1;
+    c->dmabuf_state = all ? 1 : -1;
+    TRACE(c, "dmabuf probe: %s", all ? "usable" : "not usable -> staged flow");
+    return barrier(c);  // nobody rewrites its slot before every rank has read probe_ok
 }
 
 static int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out)
@@ -312,9 +471,16 @@ static int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out)
     key.base = d.base;
     auto it = c->peer_maps.find(key);
     if (it != c->peer_maps.end() && (it->second.id != d.id || d.id == 0)) {
-        (void)hipIpcCloseMemHandle(it->second.mapped);
+        close_map(it->second);
         c->peer_maps.erase(it);
         it = c->peer_maps.end();
+    }
+    if (it == c->peer_maps.end() && d.dmabuf) {
+        void *mapped = nullptr;
+        hipExternalMemory_t ext = nullptr;
+        int rc = import_dmabuf(c, peer, d.fd, d.size, &mapped, &ext);
+        if (rc) return rc;
+        it = c->peer_maps.emplace(key, PeerMap{d.id, mapped, c->seq, ext}).first;
     }
     void *base;
     if (it != c->peer_maps.end()) {
@@ -333,7 +499,7 @@ static int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out)
             int dropped = 0;
             for (auto m = c->peer_maps.begin(); m != c->peer_maps.end();) {
                 if (m->first.peer == peer && m->second.last_use != c->seq) {
-                    (void)hipIpcCloseMemHandle(m->second.mapped);
+                    close_map(m->second);
                     m = c->peer_maps.erase(m);
                     dropped++;
                 } else {
@@ -345,7 +511,7 @@ static int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out)
             if (e != hipSuccess)
                 return set_error(MI355X_ERR_PEER, "hipIpcOpenMemHandle(rank %d): %s", peer, hipGetErrorString(e));
         }
-        c->peer_maps[key] = PeerMap{d.id, base, c->seq};
+        c->peer_maps[key] = PeerMap{d.id, base, c->seq, nullptr};
     }
     *out = (char *)base + d.off;
     return MI355X_SUCCESS;
@@ -384,6 +550,25 @@ static int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uin
         for (int b = 0; b < nbuf; ++b) any_staged = any_staged || o.buf[b].staged;
     }
     peers.assign(nbuf, std::vector<void *>(c->size, nullptr));
+    if (any_staged && !c->loopback) {
+        if (c->dmabuf_state == 0) {
+            rc = barrier(c);  // every rank has read the staged flags before the probe reuses the slots
+            if (rc) return rc;
+            rc = probe_dmabuf(c);
+            if (rc) return rc;
+        }
+        if (c->dmabuf_state == 1) {
+            // second round: the large allocations go out as dmabuf fds, then everything is mapped
+            for (int b = 0; b < nbuf; ++b)
+                if (s.buf[b].staged) {
+                    rc = export_dmabuf(c, &s.buf[b]);
+                    if (rc) return rc;
+                }
+            rc = barrier(c);
+            if (rc) return rc;
+            any_staged = false;
+        }
+    }
     if (any_staged) {
         if (!staged) return set_error(MI355X_ERR_UNSUPPORTED, "buffer allocation too large to export");
         *staged = true;
@@ -1003,7 +1188,9 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
     }
     (void)hipSetDevice(c->device);
     if (c->nb_stream) (void)hipStreamDestroy(c->nb_stream);
-    for (auto &kv : c->peer_maps) (void)hipIpcCloseMemHandle(kv.second.mapped);
+    for (auto &kv : c->peer_maps) close_map(kv.second);
+    for (LocalReg &r : c->local_regs) drop_reg(r);
+    for (auto &kv : c->pidfds) close(kv.second);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->stage) (void)hipFree(c->stage);
     if (c->ll_base) (void)hipFree(c->ll_base);

@@ -138,10 +138,24 @@ def ll_checks(pkg, comm, rank, size, oracle, torch):
     print(f"rank {rank} LL OK", flush=True)
 
 
-def staged(pkg, comm, rank, size, torch):
-    """the staged data flow through real IPC: first forced on small buffers (every allocation
-    treated as unexportable, 1 MiB staging), then for real on allocations of >= 2 GiB, which
-    hipIpcOpenMemHandle cannot map on this platform (a hang without the staged flow)"""
+def staged(pkg, comm, rank, size, torch, key):
+    """allocations too large for hipIpc* (forced here: every allocation; for real: >= 2 GiB, which
+    hipIpcOpenMemHandle cannot map on this platform) through real IPC, twice: on a communicator
+    with the dmabuf path disabled (staged flow, 1 MiB staging) and on the main one (dmabuf fds
+    fetched with pidfd_getfd)"""
+    import os
+    os.environ["MI355X_DMABUF"] = "0"
+    c2 = pkg.Comm.create(key + "_st", rank, size, torch.cuda.current_device())
+    try:
+        large_calls(pkg, c2, rank, size, torch)
+    finally:
+        c2.destroy()
+        del os.environ["MI355X_DMABUF"]
+    large_calls(pkg, comm, rank, size, torch)
+    print(f"rank {rank} staged OK", flush=True)
+
+
+def large_calls(pkg, comm, rank, size, torch):
     comm.set("IPC_MAX_BYTES", 0)
     comm.set("STAGE_BYTES", 1 << 20)
     n = 700_001
@@ -174,7 +188,6 @@ def staged(pkg, comm, rank, size, torch):
         assert bool(torch.all(out == size * want)), "rsb on a >= 2 GiB allocation"
         del big, out
         torch.cuda.empty_cache()
-    print(f"rank {rank} staged OK", flush=True)
 
 
 def main():
@@ -214,7 +227,7 @@ def main():
         assert int(dst[r * nb:(r + 1) * nb].min()) == r + 1
     realloc_same_address(pkg, comm, rank, size)
     ll_checks(pkg, comm, rank, size, oracle, torch)
-    staged(pkg, comm, rank, size, torch)
+    staged(pkg, comm, rank, size, torch, key)
     comm.barrier()
     comm.destroy()
     print(f"rank {rank} OK", flush=True)
