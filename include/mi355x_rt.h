@@ -187,11 +187,47 @@ int mi355x_request_test(mi355x_request_t *req, int *done);
 int mi355x_request_wait(mi355x_request_t *req);
 int mi355x_request_free(mi355x_request_t *req);
 
+/* ---------------------------------------------------------------- device point-to-point */
+/* MPI_Send / MPI_Recv / MPI_Isend / MPI_Irecv / MPI_Sendrecv / MPI_Iprobe on device buffers
+ * between the ranks of a communicator.  Replaces, for device memory, ob1's RGET rendezvous over
+ * btl/smcuda: mca_pml_ob1_send_request_start_cuda (pml_ob1_cuda.c:52-100) announces the
+ * registered buffer, the receiver matches it (ob1 matching: per-source order, posted receives in
+ * posting order, MI355X_ANY_SOURCE / MI355X_ANY_TAG) and pulls it the way
+ * mca_btl_smcuda_get_cuda (btl_smcuda.c:1083-1168) does, then the FIN completes the send.
+ * `ddt` NULL: `count` contiguous bytes; else `count` instances of the datatype (the GPU
+ * convertor packs / unpacks non-contiguous layouts).  Buffers are read / written once the
+ * caller's prior work on `stream` is done.  Blocking sends complete when the receiver has read
+ * the data (rendezvous).  A receive longer than its buffer gets the first bytes, status.bytes =
+ * the message size, status.error = MI355X_ERR_TRUNCATE (pml_ob1_recvreq.h:172-180); the blocking
+ * forms then return MI355X_ERR_TRUNCATE.  Requests: mi355x_request_test / wait / free above
+ * (they drive progress); mi355x_p2p_progress is the opal_progress hook. */
+#define MI355X_ANY_SOURCE (-1)   /* MPI_ANY_SOURCE, mpi.h.in:415 */
+#define MI355X_PROC_NULL  (-2)   /* MPI_PROC_NULL,  mpi.h.in:416 */
+#define MI355X_ANY_TAG    (-1)   /* MPI_ANY_TAG,    mpi.h.in:418 */
+typedef struct mi355x_msg_status {
+    int source, tag, error;
+    size_t bytes;
+} mi355x_status_t;
+typedef struct mi355x_ddt mi355x_ddt_t;
+int mi355x_isend(mi355x_comm_t *comm, const void *buf, size_t count, const mi355x_ddt_t *ddt, int dest, int tag,
+                 void *stream, mi355x_request_t **req);
+int mi355x_irecv(mi355x_comm_t *comm, void *buf, size_t count, const mi355x_ddt_t *ddt, int source, int tag,
+                 void *stream, mi355x_request_t **req);
+int mi355x_send(mi355x_comm_t *comm, const void *buf, size_t count, const mi355x_ddt_t *ddt, int dest, int tag,
+                void *stream);
+int mi355x_recv(mi355x_comm_t *comm, void *buf, size_t count, const mi355x_ddt_t *ddt, int source, int tag,
+                void *stream, mi355x_status_t *status);
+int mi355x_sendrecv(mi355x_comm_t *comm, const void *sbuf, size_t scount, const mi355x_ddt_t *sddt, int dest,
+                    int stag, void *rbuf, size_t rcount, const mi355x_ddt_t *rddt, int source, int rtag,
+                    void *stream, mi355x_status_t *status);
+int mi355x_iprobe(mi355x_comm_t *comm, int source, int tag, int *flag, mi355x_status_t *status);
+int mi355x_p2p_progress(mi355x_comm_t *comm);
+int mi355x_request_get_status(const mi355x_request_t *req, mi355x_status_t *status);
+
 /* ---------------------------------------------------------------- GPU convertor */
 /* A datatype layout: instance k at base + k*extent; inside it nblk blocks at j*stride; inside a
  * block the runs (disp, len) in order.  The packed stream is that type map in order, as
  * opal_generic_simple_pack produces it (opal/datatype/opal_datatype_pack.c:250-374). */
-typedef struct mi355x_ddt mi355x_ddt_t;
 int mi355x_ddt_create(const int64_t *disp, const int64_t *len, size_t nruns, size_t nblk, int64_t stride,
                       int64_t extent, mi355x_ddt_t **out);
 /* MPI_Type_vector over a gap-free type of elem_size bytes (ompi_datatype_create_vector.c:36-65) */

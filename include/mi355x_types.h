@@ -94,7 +94,8 @@ enum mi355x_status {
     MI355X_ERR_HIP = -3,        /* a HIP runtime call failed; see mi355x_last_error() */
     MI355X_ERR_NOMEM = -4,
     MI355X_ERR_PEER = -5,       /* peer unreachable / IPC open failed */
-    MI355X_ERR_TIMEOUT = -6     /* a cross-rank wait exceeded its bound */
+    MI355X_ERR_TIMEOUT = -6,    /* a cross-rank wait exceeded its bound */
+    MI355X_ERR_TRUNCATE = -7    /* message longer than the receive buffer (MPI_ERR_TRUNCATE) */
 };
 
 #ifdef __cplusplus

@@ -64,6 +64,27 @@ def rt() -> ctypes.CDLL:
     return _rt
 
 
+class MsgStatus(ctypes.Structure):
+    """mi355x_status_t: MPI_Status of a device point-to-point receive"""
+    _fields_ = [("source", ctypes.c_int), ("tag", ctypes.c_int), ("error", ctypes.c_int),
+                ("bytes", ctypes.c_size_t)]
+
+    def as_tuple(self) -> tuple[int, int, int, int]:
+        return self.source, self.tag, self.error, self.bytes
+
+
+class TruncateError(MI355XError):
+    """a receive longer than its buffer (MPI_ERR_TRUNCATE); .status holds the message's status"""
+
+    def __init__(self, msg: str, status: tuple[int, int, int, int]):
+        super().__init__(msg)
+        self.status = status
+
+
+ANY_SOURCE, PROC_NULL, ANY_TAG = -1, -2, -1
+ERR_TRUNCATE = -7
+
+
 def _declare(lib: ctypes.CDLL) -> None:
     c = ctypes
     vp, sz, i = c.c_void_p, c.c_size_t, c.c_int
@@ -132,6 +153,14 @@ def _declare(lib: ctypes.CDLL) -> None:
         "mi355x_ddt_extent": (c.c_int64, [vp]),
         "mi355x_ddt_nruns": (i, [vp]),
         "mi355x_ddt_tune": (i, [i, i, i, i]),
+        "mi355x_isend": (i, [vp, vp, sz, vp, i, i, vp, c.POINTER(vp)]),
+        "mi355x_irecv": (i, [vp, vp, sz, vp, i, i, vp, c.POINTER(vp)]),
+        "mi355x_send": (i, [vp, vp, sz, vp, i, i, vp]),
+        "mi355x_recv": (i, [vp, vp, sz, vp, i, i, vp, c.POINTER(MsgStatus)]),
+        "mi355x_sendrecv": (i, [vp, vp, sz, vp, i, i, vp, sz, vp, i, i, vp, c.POINTER(MsgStatus)]),
+        "mi355x_iprobe": (i, [vp, i, i, c.POINTER(i), c.POINTER(MsgStatus)]),
+        "mi355x_p2p_progress": (i, [vp]),
+        "mi355x_request_get_status": (i, [vp, c.POINTER(MsgStatus)]),
         "mi355x_pack": (i, [vp, sz, vp, sz, vp, sz, c.POINTER(c.c_uint32), vp]),
         "mi355x_unpack": (i, [vp, sz, vp, sz, vp, sz, c.POINTER(c.c_uint32), vp]),
     }
@@ -283,6 +312,45 @@ class Comm:
     def bcast(self, buf, nbytes, root, stream=None) -> None:
         check(rt().mi355x_bcast(self.h, buf, nbytes, root, stream), "mi355x_bcast")
 
+    # ---- device point-to-point (count = bytes when ddt is None, else datatype instances)
+    def isend(self, buf, count, dest, tag, ddt=None, stream=None) -> Request:
+        return self._post("mi355x_isend", buf, count, ddt.h if ddt else None, dest, tag, stream)
+
+    def irecv(self, buf, count, source, tag, ddt=None, stream=None) -> Request:
+        return self._post("mi355x_irecv", buf, count, ddt.h if ddt else None, source, tag, stream)
+
+    def send(self, buf, count, dest, tag, ddt=None, stream=None) -> None:
+        check(rt().mi355x_send(self.h, buf, count, ddt.h if ddt else None, dest, tag, stream), "mi355x_send")
+
+    def recv(self, buf, count, source, tag, ddt=None, stream=None) -> tuple[int, int, int, int]:
+        st = MsgStatus()
+        rc = rt().mi355x_recv(self.h, buf, count, ddt.h if ddt else None, source, tag, stream, ctypes.byref(st))
+        _check_p2p(rc, "mi355x_recv", st)
+        return st.as_tuple()
+
+    def sendrecv(self, sbuf, scount, dest, stag, rbuf, rcount, source, rtag, sddt=None, rddt=None,
+                 stream=None) -> tuple[int, int, int, int]:
+        st = MsgStatus()
+        rc = rt().mi355x_sendrecv(self.h, sbuf, scount, sddt.h if sddt else None, dest, stag, rbuf, rcount,
+                                  rddt.h if rddt else None, source, rtag, stream, ctypes.byref(st))
+        _check_p2p(rc, "mi355x_sendrecv", st)
+        return st.as_tuple()
+
+    def iprobe(self, source, tag):
+        """status tuple of the first matching unreceived message, or None"""
+        flag, st = ctypes.c_int(0), MsgStatus()
+        check(rt().mi355x_iprobe(self.h, source, tag, ctypes.byref(flag), ctypes.byref(st)), "mi355x_iprobe")
+        return st.as_tuple() if flag.value else None
+
+    def progress(self) -> None:
+        check(rt().mi355x_p2p_progress(self.h), "mi355x_p2p_progress")
+
+
+def _check_p2p(rc: int, what: str, st: "MsgStatus") -> None:
+    if rc == ERR_TRUNCATE:
+        raise TruncateError(rt().mi355x_last_error().decode(errors="replace"), st.as_tuple())
+    check(rc, what)
+
 
 class Rules:
     """coll/tuned dynamic rules (mi355x_rules_t), loaded from a coll_tuned_dynamic_rules_filename file."""
@@ -308,22 +376,30 @@ class Rules:
 
 
 class Request:
-    """A posted nonblocking collective (mi355x_request_t)."""
+    """A posted nonblocking collective or point-to-point call (mi355x_request_t)."""
 
     def __init__(self, h: int):
         self.h = ctypes.c_void_p(h)
 
     def test(self) -> bool:
         done = ctypes.c_int(0)
-        check(rt().mi355x_request_test(self.h, ctypes.byref(done)), "mi355x_request_test")
+        rc = rt().mi355x_request_test(self.h, ctypes.byref(done))
+        if rc == ERR_TRUNCATE:
+            return True   # complete; wait() reports the truncation
+        check(rc, "mi355x_request_test")
         return bool(done.value)
 
-    def wait(self) -> None:
+    def wait(self):
+        """wait, free; returns the receive status tuple (source, tag, error, bytes)"""
+        st = MsgStatus()
         try:
-            check(rt().mi355x_request_wait(self.h), "mi355x_request_wait")
+            rc = rt().mi355x_request_wait(self.h)
+            rt().mi355x_request_get_status(self.h, ctypes.byref(st))
+            _check_p2p(rc, "mi355x_request_wait", st)
         finally:
             rt().mi355x_request_free(self.h)
             self.h = ctypes.c_void_p()
+        return st.as_tuple()
 
 
 class Ddt:

@@ -52,22 +52,9 @@
 #include "coll_sched.hpp"
 #include "rt_internal.hpp"
 
-namespace mi355x {
+#include "comm_internal.hpp"
 
-// MI355X_DEBUG=1: trace every stage of a collective on stderr (rank, stage, elapsed time)
-static bool debug_on()
-{
-    static const bool on = getenv("MI355X_DEBUG") && atoi(getenv("MI355X_DEBUG")) > 0;
-    return on;
-}
-#define TRACE(c, ...)                                                                          \
-    do {                                                                                       \
-        if (debug_on()) {                                                                      \
-            fprintf(stderr, "[mi355x r%d seq %llu] ", (c)->rank, (unsigned long long)(c)->seq); \
-            fprintf(stderr, __VA_ARGS__);                                                      \
-            fputc('\n', stderr);                                                               \
-        }                                                                                      \
-    } while (0)
+namespace mi355x {
 
 CollTune &coll_tune()
 {
@@ -75,150 +62,12 @@ CollTune &coll_tune()
     return t;
 }
 
-constexpr uint64_t kMagic = 0x4d49333535584331ull;  // "MI355XC1"
-constexpr int kMaxBufs = 3;
-
-struct BufDesc {
-    hipIpcMemHandle_t h;
-    uint64_t off;
-    uint64_t raw;      // loopback: the pointer itself
-    uint64_t present;  // 0: NULL buffer
-    uint64_t base;     // exporter's allocation base (its VA; the peer-map key)
-    uint64_t id;       // exporter's allocation id (HIP_POINTER_ATTRIBUTE_BUFFER_ID)
-    uint64_t staged;   // 1: allocation too large for hipIpc* (>= ipc_max): dmabuf or staged flow
-    uint64_t size;     // dmabuf: the exported allocation's size
-    int32_t dmabuf;    // 1: exported as a dmabuf fd (fd is a descriptor of the exporter process)
-    int32_t fd;
-};
-
-struct alignas(64) RankSlot {
-    std::atomic<uint64_t> seq;
-    int32_t pid, dev, nbuf, pad;
-    uint64_t sig[4];
-    BufDesc buf[kMaxBufs];
-    int32_t probe_fd, probe_ok;   // dmabuf capability probe
-    uint64_t probe_size;
-};
-
-struct Ctrl {
-    uint64_t magic;
-    uint32_t size;
-    uint32_t pad0;
-    alignas(64) std::atomic<uint32_t> attached;
-    alignas(64) std::atomic<uint64_t> bar_count;
-    alignas(64) std::atomic<uint64_t> bar_gen;
-    alignas(64) std::atomic<uint32_t> abort_flag;
-    alignas(64) RankSlot slot[1];
-};
-
-static size_t ctrl_bytes(int size) { return sizeof(Ctrl) + sizeof(RankSlot) * (size_t)(size - 1); }
-
-// A peer allocation is keyed by (peer, its base VA) and remembered with its allocation id: when
-// the exporter frees and reallocates at the same address the id changes and the stale mapping
-// is closed and replaced (the invalidation mpool/rgpusm does on a buffer-id mismatch,
-// ompi/mca/mpool/rgpusm/mpool_rgpusm_module.c:243-281, common_cuda.c:1709-1745).
-struct HandleKey {
-    int peer;
-    uint64_t base;
-    bool operator<(const HandleKey &o) const
-    {
-        if (peer != o.peer) return peer < o.peer;
-        return base < o.base;
-    }
-};
-
-struct PeerMap {
-    uint64_t id;
-    void *mapped;
-    uint64_t last_use;             // call (seq) that last used the mapping
-    hipExternalMemory_t ext;       // dmabuf import (NULL: hipIpcOpenMemHandle mapping)
-};
-
-static void close_map(PeerMap &m)
-{
-    if (m.ext) {
-        (void)hipFree(m.mapped);
-        (void)hipDestroyExternalMemory(m.ext);
-    } else {
-        (void)hipIpcCloseMemHandle(m.mapped);
-    }
-}
-
-struct LocalReg {
-    uintptr_t base;
-    size_t size;
-    uint64_t id;
-    hipIpcMemHandle_t h;
-    bool has_h;       // false: too large for hipIpc* (never passed to hipIpcGetMemHandle)
-    int fd;           // dmabuf export of a large allocation (-1: none yet)
-};
-
-static void drop_reg(LocalReg &r)
-{
-    if (r.fd >= 0) close(r.fd);
-    r.fd = -1;
-}
-
-struct LoopShared {
-    Ctrl *ctrl = nullptr;
-    int refs = 0;
-    std::mutex mtx;
-};
-
 } // namespace mi355x
-
-struct mi355x_request {
-    std::atomic<int> done{0};
-    int rc = MI355X_SUCCESS;
-    std::string err;
-    std::function<int(hipStream_t)> run;  // the blocking algorithm, on the progress stream
-    hipEvent_t ev = nullptr;              // the caller-stream point the call starts after
-};
-
-struct mi355x_comm {
-    int rank = 0, size = 1, device = 0;
-    mi355x::Ctrl *ctrl = nullptr;
-    bool loopback = false;
-    std::shared_ptr<mi355x::LoopShared> loop;
-    std::string shm_name;
-    uint64_t seq = 0;
-    std::map<mi355x::HandleKey, mi355x::PeerMap> peer_maps;
-    std::vector<mi355x::LocalReg> local_regs;
-    void *scratch = nullptr;
-    size_t scratch_bytes = 0;
-    int dmabuf_state = 0;                         // large allocations via dmabuf: 0 unknown, 1 yes, -1 no
-    bool ptracer_any = false;                     // PR_SET_PTRACER_ANY done (peers pidfd_getfd our fds)
-    std::map<int, int> pidfds;                    // peer rank -> pidfd
-    void *stage = nullptr;                        // staging buffer of the staged data flow
-    size_t stage_bytes = (size_t)1 << 30;         // its size (an allocation below ipc_max)
-    size_t ipc_max = (size_t)1 << 31;             // allocations >= this are never exported
-    // low-latency path (coll_ll.hip): uncached LL region [flags 2 x n x kmax][data 2 x n x slot]
-    size_t ll_max = (size_t)64 << 10;             // per-rank message bytes served by the LL path
-    char *ll_base = nullptr;
-    size_t ll_slot = 0, ll_kmax = 0, ll_flag_bytes = 0;
-    std::vector<char *> ll_peer;                  // every rank's LL region, mapped
-    uint64_t ll_seq = 0;
-    uint32_t *ll_err = nullptr;                   // host-visible timeout word
-    // nonblocking collectives: one progress thread per communicator runs the posted calls in
-    // order on its own stream; blocking calls first wait until nothing is pending
-    std::thread worker;
-    std::mutex q_mtx;
-    std::condition_variable q_cv;
-    std::deque<mi355x_request *> queue;
-    bool stop = false;
-    int pending = 0;                              // posted, not finished (guarded by q_mtx)
-    hipStream_t nb_stream = nullptr;
-    int knob_allreduce = 0, knob_reduce = 0, knob_rs = 0;
-    int chain_fanout = mi355x::kDefaultChainFanout;
-    const mi355x_rules_t *rules = nullptr;        // coll/tuned dynamic rules (not owned)
-    int last_alg = -1;
-    double timeout_s = 600.0;
-};
 
 namespace mi355x {
 
 // ----------------------------------------------------------------- barrier
-static int barrier(mi355x_comm *c)
+int barrier(mi355x_comm *c)
 {
     if (c->size == 1) return MI355X_SUCCESS;
     Ctrl *k = c->ctrl;
@@ -265,8 +114,9 @@ static uint64_t buffer_id(const void *p)
     return (uint64_t)id;
 }
 
-static int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
+int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
 {
+    std::lock_guard<std::recursive_mutex> reg_guard(c->reg_mtx);
     std::memset(d, 0, sizeof(*d));
     if (!p) return MI355X_SUCCESS;
     d->present = 1;
@@ -343,8 +193,9 @@ static int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
 // pidfd_getfd and imported as external memory maps fine (tools/probe/dmabuf_xproc.hip).  The
 // exporter lets same-user processes read its descriptors (PR_SET_PTRACER_ANY, which yama's
 // ptrace_scope 1 requires for pidfd_getfd between siblings).
-static int export_dmabuf(mi355x_comm *c, BufDesc *d)
+int export_dmabuf(mi355x_comm *c, BufDesc *d)
 {
+    std::lock_guard<std::recursive_mutex> reg_guard(c->reg_mtx);
     for (LocalReg &r : c->local_regs) {
         if (r.base != d->base || r.id != d->id) continue;
         if (r.fd < 0) {
@@ -396,7 +247,6 @@ static int import_dmabuf(mi355x_comm *c, int peer, int fd, size_t size, void **m
     return MI355X_SUCCESS;
 }
 
-static int barrier(mi355x_comm *c);
 
 // Collective, once per communicator: every rank exports a 4 MiB buffer as a dmabuf, every rank
 // imports every peer's and checks its bytes; the path is used only if it worked everywhere.
@@ -458,9 +308,11 @@ static int probe_dmabuf(mi355x_comm *c)
     return barrier(c);  // nobody rewrites its slot before every rank has read probe_ok
 }
 
-static int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out)
+int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **entry)
 {
+    std::lock_guard<std::recursive_mutex> reg_guard(c->reg_mtx);
     *out = nullptr;
+    if (entry) *entry = nullptr;
     if (!d.present) return MI355X_SUCCESS;
     if (c->loopback) {
         *out = (void *)(uintptr_t)d.raw;
@@ -470,7 +322,7 @@ static int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out)
     key.peer = peer;
     key.base = d.base;
     auto it = c->peer_maps.find(key);
-    if (it != c->peer_maps.end() && (it->second.id != d.id || d.id == 0)) {
+    if (it != c->peer_maps.end() && (it->second.id != d.id || (d.id == 0 && it->second.pins == 0))) {
         close_map(it->second);
         c->peer_maps.erase(it);
         it = c->peer_maps.end();
@@ -498,7 +350,7 @@ static int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out)
             (void)hipGetLastError();
             int dropped = 0;
             for (auto m = c->peer_maps.begin(); m != c->peer_maps.end();) {
-                if (m->first.peer == peer && m->second.last_use != c->seq) {
+                if (m->first.peer == peer && m->second.last_use != c->seq && m->second.pins == 0) {
                     close_map(m->second);
                     m = c->peer_maps.erase(m);
                     dropped++;
@@ -511,8 +363,9 @@ static int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out)
             if (e != hipSuccess)
                 return set_error(MI355X_ERR_PEER, "hipIpcOpenMemHandle(rank %d): %s", peer, hipGetErrorString(e));
         }
-        c->peer_maps[key] = PeerMap{d.id, base, c->seq, nullptr};
+        it = c->peer_maps.emplace(key, PeerMap{d.id, base, c->seq, nullptr}).first;
     }
+    if (entry) *entry = &it->second;
     *out = (char *)base + d.off;
     return MI355X_SUCCESS;
 }
@@ -1187,6 +1040,7 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
         c->worker.join();
     }
     (void)hipSetDevice(c->device);
+    p2p_destroy(c);
     if (c->nb_stream) (void)hipStreamDestroy(c->nb_stream);
     for (auto &kv : c->peer_maps) close_map(kv.second);
     for (LocalReg &r : c->local_regs) drop_reg(r);
@@ -1846,6 +1700,7 @@ int mi355x_ibcast(mi355x_comm_t *c, void *buf, size_t bytes, int root, void *str
 int mi355x_request_test(mi355x_request_t *r, int *done)
 {
     if (!r || !done) return set_error(MI355X_ERR_ARG, "NULL request");
+    if (r->kind != 0 && !r->done.load(std::memory_order_acquire)) p2p_progress(r->comm);
     *done = r->done.load(std::memory_order_acquire);
     if (*done && r->rc != MI355X_SUCCESS) return set_error(r->rc, "%s", r->err.c_str());
     return MI355X_SUCCESS;
@@ -1853,6 +1708,7 @@ int mi355x_request_test(mi355x_request_t *r, int *done)
 int mi355x_request_wait(mi355x_request_t *r)
 {
     if (!r) return set_error(MI355X_ERR_ARG, "NULL request");
+    if (r->kind != 0) return p2p_wait(r);
     unsigned spins = 0;
     while (!r->done.load(std::memory_order_acquire)) {
         if (++spins > 64) sched_yield();

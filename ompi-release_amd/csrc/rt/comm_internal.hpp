@@ -1,0 +1,235 @@
+// comm_internal.hpp -- state shared by the engine's translation units (coll_comm.cpp: bootstrap,
+// registration cache, collectives; p2p.cpp: device point-to-point).  Not part of the C ABI.
+#pragma once
+
+#include <unistd.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <deque>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "coll_internal.hpp"
+#include "coll_sched.hpp"
+#include "rt_internal.hpp"
+
+namespace mi355x {
+
+// MI355X_DEBUG=1: trace every stage of a collective on stderr (rank, stage, elapsed time)
+inline bool debug_on()
+{
+    static const bool on = getenv("MI355X_DEBUG") && atoi(getenv("MI355X_DEBUG")) > 0;
+    return on;
+}
+#define TRACE(c, ...)                                                                          \
+    do {                                                                                       \
+        if (debug_on()) {                                                                      \
+            fprintf(stderr, "[mi355x r%d seq %llu] ", (c)->rank, (unsigned long long)(c)->seq); \
+            fprintf(stderr, __VA_ARGS__);                                                      \
+            fputc('\n', stderr);                                                               \
+        }                                                                                      \
+    } while (0)
+
+constexpr uint64_t kMagic = 0x4d49333535584331ull;  // "MI355XC1"
+constexpr int kMaxBufs = 3;
+
+struct BufDesc {
+    hipIpcMemHandle_t h;
+    uint64_t off;
+    uint64_t raw;      // loopback: the pointer itself
+    uint64_t present;  // 0: NULL buffer
+    uint64_t base;     // exporter's allocation base (its VA; the peer-map key)
+    uint64_t id;       // exporter's allocation id (HIP_POINTER_ATTRIBUTE_BUFFER_ID)
+    uint64_t staged;   // 1: allocation too large for hipIpc* (>= ipc_max): dmabuf or staged flow
+    uint64_t size;     // dmabuf: the exported allocation's size
+    int32_t dmabuf;    // 1: exported as a dmabuf fd (fd is a descriptor of the exporter process)
+    int32_t fd;
+};
+
+struct alignas(64) RankSlot {
+    std::atomic<uint64_t> seq;
+    int32_t pid, dev, nbuf, pad;
+    uint64_t sig[4];
+    BufDesc buf[kMaxBufs];
+    int32_t probe_fd, probe_ok;   // dmabuf capability probe
+    uint64_t probe_size;
+};
+
+struct Ctrl {
+    uint64_t magic;
+    uint32_t size;
+    uint32_t pad0;
+    alignas(64) std::atomic<uint32_t> attached;
+    alignas(64) std::atomic<uint64_t> bar_count;
+    alignas(64) std::atomic<uint64_t> bar_gen;
+    alignas(64) std::atomic<uint32_t> abort_flag;
+    alignas(64) RankSlot slot[1];
+};
+
+// Point-to-point mailboxes (p2p.cpp) follow the rank slots: for every ordered pair (src, dst) a
+// ring of kP2PSlots envelopes that src fills and dst drains (the ob1 match/RGET header plus the
+// FIN the receiver returns, pml_ob1_hdr.h:58-190, carried in shared memory as btl/smcuda's FIFOs
+// carry them, btl_smcuda_fifo.h).
+constexpr int kP2PSlots = 32;
+struct alignas(64) Envelope {
+    std::atomic<uint64_t> full;   // message number + 1 once posted (sender, release)
+    std::atomic<uint64_t> done;   // message number + 1 once the receiver no longer reads it
+    int32_t tag, flags;
+    uint64_t bytes;               // packed size of the message
+    BufDesc buf;                  // where the (packed) bytes are: the sender's export
+};
+inline size_t p2p_offset(int size)
+{
+    return (sizeof(Ctrl) + sizeof(RankSlot) * (size_t)(size - 1) + 4095) & ~(size_t)4095;
+}
+inline size_t ctrl_bytes(int size)
+{
+    return p2p_offset(size) + sizeof(Envelope) * (size_t)kP2PSlots * (size_t)size * (size_t)size;
+}
+inline Envelope *p2p_ring(Ctrl *k, int size, int src, int dst)
+{
+    return (Envelope *)((char *)k + p2p_offset(size)) + ((size_t)src * (size_t)size + (size_t)dst) * kP2PSlots;
+}
+
+// A peer allocation is keyed by (peer, its base VA) and remembered with its allocation id: when
+// the exporter frees and reallocates at the same address the id changes and the stale mapping
+// is closed and replaced (the invalidation mpool/rgpusm does on a buffer-id mismatch,
+// ompi/mca/mpool/rgpusm/mpool_rgpusm_module.c:243-281, common_cuda.c:1709-1745).
+struct HandleKey {
+    int peer;
+    uint64_t base;
+    bool operator<(const HandleKey &o) const
+    {
+        if (peer != o.peer) return peer < o.peer;
+        return base < o.base;
+    }
+};
+
+struct PeerMap {
+    uint64_t id;
+    void *mapped;
+    uint64_t last_use;             // call (seq) that last used the mapping
+    hipExternalMemory_t ext;       // dmabuf import (NULL: hipIpcOpenMemHandle mapping)
+    int pins = 0;                  // in-flight point-to-point reads: never closed meanwhile
+};
+
+inline void close_map(PeerMap &m)
+{
+    if (m.ext) {
+        (void)hipFree(m.mapped);
+        (void)hipDestroyExternalMemory(m.ext);
+    } else {
+        (void)hipIpcCloseMemHandle(m.mapped);
+    }
+}
+
+struct LocalReg {
+    uintptr_t base;
+    size_t size;
+    uint64_t id;
+    hipIpcMemHandle_t h;
+    bool has_h;       // false: too large for hipIpc* (never passed to hipIpcGetMemHandle)
+    int fd;           // dmabuf export of a large allocation (-1: none yet)
+};
+
+inline void drop_reg(LocalReg &r)
+{
+    if (r.fd >= 0) close(r.fd);
+    r.fd = -1;
+}
+
+struct LoopShared {
+    Ctrl *ctrl = nullptr;
+    int refs = 0;
+    std::mutex mtx;
+};
+
+struct P2P;  // point-to-point state of a communicator (p2p.cpp)
+
+} // namespace mi355x
+
+struct mi355x_request {
+    std::atomic<int> done{0};
+    int rc = MI355X_SUCCESS;
+    std::string err;
+    std::function<int(hipStream_t)> run;  // the blocking algorithm, on the progress stream
+    hipEvent_t ev = nullptr;              // the caller-stream point the call starts after
+    // point-to-point requests (p2p.cpp) complete from mi355x_p2p_progress, not from a thread
+    int kind = 0;                         // 0 collective, 1 send, 2 receive
+    mi355x_comm *comm = nullptr;
+    int peer = 0, tag = 0;
+    const mi355x_ddt_t *ddt = nullptr;    // NULL: `count` contiguous bytes
+    size_t count = 0;
+    void *buf = nullptr;
+    size_t bytes = 0;                     // packed bytes: of the message (send), of the buffer (receive)
+    uint64_t msg = 0;                     // send: message number to `peer`
+    mi355x::BufDesc desc;                 // send: the export announced in the envelope
+    mi355x::Envelope *env = nullptr;      // the envelope in flight
+    void *packed = nullptr;               // send: packed copy in the arena (non-contiguous types)
+    mi355x::PeerMap *pin = nullptr;       // receive: the pinned mapping being read
+    int st_source = 0, st_tag = 0, st_error = 0;
+    size_t st_bytes = 0;
+};
+
+struct mi355x_comm {
+    int rank = 0, size = 1, device = 0;
+    mi355x::Ctrl *ctrl = nullptr;
+    bool loopback = false;
+    std::shared_ptr<mi355x::LoopShared> loop;
+    std::string shm_name;
+    uint64_t seq = 0;
+    std::map<mi355x::HandleKey, mi355x::PeerMap> peer_maps;
+    std::vector<mi355x::LocalReg> local_regs;
+    void *scratch = nullptr;
+    size_t scratch_bytes = 0;
+    int dmabuf_state = 0;                         // large allocations via dmabuf: 0 unknown, 1 yes, -1 no
+    bool ptracer_any = false;                     // PR_SET_PTRACER_ANY done (peers pidfd_getfd our fds)
+    std::map<int, int> pidfds;                    // peer rank -> pidfd
+    void *stage = nullptr;                        // staging buffer of the staged data flow
+    size_t stage_bytes = (size_t)1 << 30;         // its size (an allocation below ipc_max)
+    size_t ipc_max = (size_t)1 << 31;             // allocations >= this are never exported
+    // low-latency path (coll_ll.hip): uncached LL region [flags 2 x n x kmax][data 2 x n x slot]
+    size_t ll_max = (size_t)64 << 10;             // per-rank message bytes served by the LL path
+    char *ll_base = nullptr;
+    size_t ll_slot = 0, ll_kmax = 0, ll_flag_bytes = 0;
+    std::vector<char *> ll_peer;                  // every rank's LL region, mapped
+    uint64_t ll_seq = 0;
+    uint32_t *ll_err = nullptr;                   // host-visible timeout word
+    // nonblocking collectives: one progress thread per communicator runs the posted calls in
+    // order on its own stream; blocking calls first wait until nothing is pending
+    std::thread worker;
+    std::mutex q_mtx;
+    std::condition_variable q_cv;
+    std::deque<mi355x_request *> queue;
+    bool stop = false;
+    int pending = 0;                              // posted, not finished (guarded by q_mtx)
+    hipStream_t nb_stream = nullptr;
+    int knob_allreduce = 0, knob_reduce = 0, knob_rs = 0;
+    int chain_fanout = mi355x::kDefaultChainFanout;
+    const mi355x_rules_t *rules = nullptr;        // coll/tuned dynamic rules (not owned)
+    int last_alg = -1;
+    double timeout_s = 600.0;
+    mi355x::P2P *p2p = nullptr;                   // created on first point-to-point call
+    std::recursive_mutex reg_mtx;                 // registration cache: collectives (progress
+                                                  // thread) and point-to-point (caller) share it
+};
+
+namespace mi355x {
+// shared by coll_comm.cpp and p2p.cpp
+int barrier(mi355x_comm *c);
+int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force);
+int export_dmabuf(mi355x_comm *c, BufDesc *d);
+int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **entry = nullptr);
+void p2p_destroy(mi355x_comm *c);
+int p2p_progress(mi355x_comm *c);
+int p2p_wait(mi355x_request *r);
+} // namespace mi355x

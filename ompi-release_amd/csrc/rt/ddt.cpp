@@ -251,6 +251,23 @@ static int ddt_move(const mi355x_ddt_t *d, bool pack, size_t count, void *mem, s
     return MI355X_SUCCESS;
 }
 
+} // extern "C"
+
+namespace mi355x {
+// true when `count` instances of d occupy one gap-free byte range starting at base + *first
+bool ddt_contiguous(const mi355x_ddt *d, size_t count, int64_t *first)
+{
+    *first = 0;
+    if (!d || d->disp.size() != 1) return false;
+    const int64_t len = d->len[0];
+    *first = d->disp[0];
+    if (d->nblk > 1 && d->stride != len) return false;
+    return count <= 1 || d->extent == d->nblk * len;
+}
+} // namespace mi355x
+
+extern "C" {
+
 int mi355x_ddt_tune(int unroll_pack, int unroll_unpack, int threads, int nontemporal)
 {
     auto ok_u = [](int u) { return u == 0 || u == 2 || u == 4 || u == 8; };

@@ -5,7 +5,12 @@
 
 #include <cstdint>
 
+struct mi355x_ddt;
+
 namespace mi355x {
+
+// true when `count` instances occupy one gap-free byte range starting at base + *first (ddt.cpp)
+bool ddt_contiguous(const mi355x_ddt *d, size_t count, int64_t *first);
 
 struct DdtDev {
     const int64_t *disp;   // run displacement inside a block (device array)

@@ -190,6 +190,72 @@ def large_calls(pkg, comm, rank, size, torch):
         torch.cuda.empty_cache()
 
 
+def p2p_checks(pkg, comm, rank, size, oracle, torch):
+    """device point-to-point across processes (IPC-mapped sender buffers pulled by the receiver)"""
+    def pattern(src, n, salt):
+        return np.random.default_rng(1000 * src + salt).integers(0, 256, n, dtype=np.uint8)
+
+    nxt, prv = (rank + 1) % size, (rank - 1) % size
+    for salt, n in enumerate([0, 1, 4096, 1 << 20, (64 << 20) + 3]):
+        s = torch.from_numpy(pattern(rank, n, salt)).cuda() if n else None
+        d = torch.zeros(max(n, 1), dtype=torch.uint8, device="cuda")
+        st = comm.sendrecv(s.data_ptr() if n else None, n, nxt, salt, d.data_ptr(), n, prv, salt)
+        assert st == (prv, salt, 0, n), st
+        assert np.array_equal(d[:n].cpu().numpy(), pattern(prv, n, salt)), f"sendrecv {n} bytes"
+    # every rank to every other, received with MPI_ANY_SOURCE
+    srcs = {q: torch.from_numpy(pattern(rank, 1000 + rank, 50 + q)).cuda() for q in range(size) if q != rank}
+    outs = [torch.zeros(4096, dtype=torch.uint8, device="cuda") for _ in range(size - 1)]
+    rreqs = [comm.irecv(o.data_ptr(), 4096, pkg.ANY_SOURCE, 77) for o in outs]
+    sreqs = [comm.isend(srcs[q].data_ptr(), srcs[q].numel(), q, 77) for q in srcs]
+    sts = [r.wait() for r in rreqs]
+    for r in sreqs:
+        r.wait()
+    assert sorted(s[0] for s in sts) == [q for q in range(size) if q != rank], sts
+    for s, o in zip(sts, outs):
+        assert np.array_equal(o[:s[3]].cpu().numpy(), pattern(s[0], 1000 + s[0], 50 + rank)), "any-source bytes"
+    # more messages in flight than envelopes: queued sends, order kept
+    k = 80
+    src = torch.from_numpy(pattern(rank, 64 * k, 99)).cuda()
+    dst = torch.zeros(64 * k, dtype=torch.uint8, device="cuda")
+    rreqs = [comm.irecv(dst[i * 64:(i + 1) * 64].data_ptr(), 64, prv, pkg.ANY_TAG) for i in range(k)]
+    sreqs = [comm.isend(src[i * 64:(i + 1) * 64].data_ptr(), 64, nxt, i) for i in range(k)]
+    for i, r in enumerate(rreqs):
+        assert r.wait()[1] == i
+    for r in sreqs:
+        r.wait()
+    assert np.array_equal(dst.cpu().numpy(), pattern(prv, 64 * k, 99)), "queued messages"
+    # MPI_Type_vector(stride 2, block 64) floats: packed by the sender, received contiguous
+    nvec = 1000
+    od = oracle.oracle_ddt_vector(nvec, 64, 128, 4)
+    dv = pkg.Ddt.vector(nvec, 64, 128, 4)
+    vsrc = pattern(rank, nvec * 128 * 4, 7)
+    d = torch.zeros(nvec * 64 * 4, dtype=torch.uint8, device="cuda")
+    s = comm.isend(torch.from_numpy(vsrc).cuda().data_ptr(), 1, nxt, 5, ddt=dv)
+    comm.recv(d.data_ptr(), nvec * 64 * 4, prv, 5)
+    s.wait()
+    want = np.zeros(nvec * 64 * 4, dtype=np.uint8)
+    pv = pattern(prv, nvec * 128 * 4, 7)
+    oracle.oracle_ddt_pack(od, 1, pv.ctypes.data, 0, want.ctypes.data, want.size)
+    assert np.array_equal(d.cpu().numpy(), want), "vector send"
+    oracle.oracle_ddt_free(od)
+    dv.destroy()
+    if size == 2:   # a send buffer inside an allocation of >= 2 GiB: dmabuf export
+        big = torch.full(((1 << 31) + (8 << 20),), rank + 1, dtype=torch.uint8, device="cuda")
+        tail = 16 << 20
+        torch.cuda.synchronize()
+        if rank == 0:
+            comm.send(big[-tail:].data_ptr(), tail, 1, 123)
+        else:
+            d = torch.zeros(tail, dtype=torch.uint8, device="cuda")
+            assert comm.recv(d.data_ptr(), tail, 0, 123) == (0, 123, 0, tail)
+            assert int(d.min()) == 1 and int(d.max()) == 1, "send from a >= 2 GiB allocation"
+        comm.barrier()
+        del big
+        torch.cuda.empty_cache()
+    comm.barrier()
+    print(f"rank {rank} p2p OK", flush=True)
+
+
 def main():
     key, rank, size, dev = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
     import faulthandler
@@ -227,6 +293,7 @@ def main():
         assert int(dst[r * nb:(r + 1) * nb].min()) == r + 1
     realloc_same_address(pkg, comm, rank, size)
     ll_checks(pkg, comm, rank, size, oracle, torch)
+    p2p_checks(pkg, comm, rank, size, oracle, torch)
     staged(pkg, comm, rank, size, torch, key)
     comm.barrier()
     comm.destroy()

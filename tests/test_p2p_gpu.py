@@ -1,0 +1,245 @@
+"""Device point-to-point (mi355x_isend / irecv / send / recv / sendrecv / iprobe) on a loopback
+communicator (one process, one rank per comm object).  The semantics checked are ob1's
+(ompi/mca/pml/ob1/pml_ob1_recvfrag.c matching, pml_ob1_recvreq.h:172-180 truncation): messages
+from one source are received in send order, posted receives are matched in posting order,
+MPI_ANY_SOURCE / MPI_ANY_TAG wildcards, MPI_PROC_NULL, zero-byte messages, truncation keeps the
+first bytes and reports the message size.  Bytes moved through derived datatypes must equal the
+oracle's unpack(pack(...)) (the convertor restatement under oracle/)."""
+from __future__ import annotations
+
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture()
+def comms(gpu, pkg):
+    cs = pkg.Comm.loopback(4, 0)
+    yield cs
+    for c in cs:
+        c.destroy()
+
+
+def _bytes(torch, n, seed):
+    g = np.random.default_rng(seed)
+    return torch.from_numpy(g.integers(0, 256, n, dtype=np.uint8)).cuda()
+
+
+def _wait_all(reqs):
+    return [r.wait() for r in reqs]
+
+
+@pytest.mark.parametrize("nbytes", [1, 4096, 1 << 20, 3 * (1 << 20) + 7])
+def test_ring_exchange(gpu, pkg, comms, nbytes):
+    torch = gpu
+    n = len(comms)
+    src = [_bytes(torch, nbytes, r) for r in range(n)]
+    dst = [torch.zeros(nbytes, dtype=torch.uint8, device="cuda") for _ in range(n)]
+    reqs = []
+    for r, c in enumerate(comms):
+        reqs.append(c.irecv(dst[r].data_ptr(), nbytes, (r - 1) % n, 11))
+    sends = [c.isend(src[r].data_ptr(), nbytes, (r + 1) % n, 11) for r, c in enumerate(comms)]
+    st = _wait_all(reqs)
+    _wait_all(sends)
+    for r in range(n):
+        assert torch.equal(dst[r], src[(r - 1) % n])
+        assert st[r] == ((r - 1) % n, 11, 0, nbytes)
+
+
+def test_order_and_tags(gpu, pkg, comms):
+    """non-overtaking per source; a tag-specific receive skips earlier messages of other tags"""
+    torch = gpu
+    a, b = comms[0], comms[1]
+    msgs = [(5, 100), (7, 200), (5, 300), (9, 0)]
+    bufs = [_bytes(torch, ln, i) if ln else torch.zeros(1, dtype=torch.uint8, device="cuda")
+            for i, (_, ln) in enumerate(msgs)]
+    sends = [a.isend(bufs[i].data_ptr(), ln, 1, tag) for i, (tag, ln) in enumerate(msgs)]
+    out = [torch.zeros(512, dtype=torch.uint8, device="cuda") for _ in range(4)]
+    r7 = b.irecv(out[0].data_ptr(), 512, 0, 7)
+    r_any1 = b.irecv(out[1].data_ptr(), 512, pkg.ANY_SOURCE, pkg.ANY_TAG)
+    r_any2 = b.irecv(out[2].data_ptr(), 512, 0, pkg.ANY_TAG)
+    r9 = b.irecv(out[3].data_ptr(), 512, 0, 9)
+    assert r7.wait() == (0, 7, 0, 200)
+    assert r_any1.wait() == (0, 5, 0, 100)
+    assert r_any2.wait() == (0, 5, 0, 300)
+    assert r9.wait() == (0, 9, 0, 0)
+    _wait_all(sends)
+    assert torch.equal(out[0][:200], bufs[1])
+    assert torch.equal(out[1][:100], bufs[0])
+    assert torch.equal(out[2][:300], bufs[2])
+
+
+def test_any_source(gpu, pkg, comms):
+    torch = gpu
+    n = len(comms)
+    src = [_bytes(torch, 64 + r, 40 + r) for r in range(n)]
+    sends = [comms[r].isend(src[r].data_ptr(), 64 + r, 0, 3) for r in range(1, n)]
+    out = [torch.zeros(128, dtype=torch.uint8, device="cuda") for _ in range(n - 1)]
+    sts = _wait_all([comms[0].irecv(o.data_ptr(), 128, pkg.ANY_SOURCE, 3) for o in out])
+    _wait_all(sends)
+    assert sorted(s[0] for s in sts) == list(range(1, n))
+    for s, o in zip(sts, out):
+        assert s[1] == 3 and s[3] == 64 + s[0]
+        assert torch.equal(o[:s[3]], src[s[0]])
+
+
+def test_truncate(gpu, pkg, comms):
+    torch = gpu
+    src = _bytes(torch, 100, 1)
+    dst = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    s = comms[2].isend(src.data_ptr(), 100, 3, 1)
+    r = comms[3].irecv(dst.data_ptr(), 64, 2, 1)
+    with pytest.raises(pkg.TruncateError) as ei:
+        r.wait()
+    assert ei.value.status == (2, 1, pkg.ERR_TRUNCATE, 100)
+    s.wait()
+    assert torch.equal(dst, src[:64])
+
+
+def test_proc_null_and_self(gpu, pkg, comms):
+    torch = gpu
+    c = comms[1]
+    c.send(None, 0, pkg.PROC_NULL, 4)
+    assert c.recv(None, 10, pkg.PROC_NULL, 4) == (pkg.PROC_NULL, pkg.ANY_TAG, 0, 0)
+    src = _bytes(torch, 777, 2)
+    dst = torch.zeros(777, dtype=torch.uint8, device="cuda")
+    s = c.isend(src.data_ptr(), 777, 1, 8)       # to itself
+    assert c.recv(dst.data_ptr(), 777, 1, 8) == (1, 8, 0, 777)
+    s.wait()
+    assert torch.equal(dst, src)
+
+
+def test_ring_wraps(gpu, pkg, comms):
+    """more messages in flight than envelopes per pair (32): later sends queue, order is kept"""
+    torch = gpu
+    k = 100
+    src = _bytes(torch, k * 16, 5)
+    sends = [comms[0].isend(src[i * 16:(i + 1) * 16].data_ptr(), 16, 1, i % 3) for i in range(k)]
+    assert not sends[-1].test()
+    dst = torch.zeros(k * 16, dtype=torch.uint8, device="cuda")
+    for i in range(k):
+        r = comms[1].irecv(dst[i * 16:(i + 1) * 16].data_ptr(), 16, 0, pkg.ANY_TAG)
+        while not r.test():
+            comms[0].progress()   # the sender announces its queued messages as envelopes free up
+        assert r.wait() == (0, i % 3, 0, 16)
+    _wait_all(sends)
+    assert torch.equal(dst, src)
+
+
+def test_iprobe(gpu, pkg, comms):
+    torch = gpu
+    assert comms[0].iprobe(pkg.ANY_SOURCE, pkg.ANY_TAG) is None
+    src = _bytes(torch, 50, 3)
+    s = comms[2].isend(src.data_ptr(), 50, 0, 21)
+    assert comms[0].iprobe(pkg.ANY_SOURCE, 22) is None
+    assert comms[0].iprobe(2, 21) == (2, 21, 0, 50)
+    dst = torch.zeros(50, dtype=torch.uint8, device="cuda")
+    comms[0].recv(dst.data_ptr(), 50, 2, 21)
+    s.wait()
+    assert comms[0].iprobe(pkg.ANY_SOURCE, pkg.ANY_TAG) is None
+
+
+def test_sendrecv_threads(gpu, pkg, comms):
+    """blocking sendrecv ring, one thread per rank (as MPI ranks would be)"""
+    torch = gpu
+    n = len(comms)
+    nbytes = 1 << 16
+    src = [_bytes(torch, nbytes, 60 + r) for r in range(n)]
+    dst = [torch.zeros(nbytes, dtype=torch.uint8, device="cuda") for _ in range(n)]
+    sts, errs = [None] * n, []
+
+    def run(r):
+        try:
+            torch.cuda.set_device(0)
+            sts[r] = comms[r].sendrecv(src[r].data_ptr(), nbytes, (r + 1) % n, 2,
+                                       dst[r].data_ptr(), nbytes, (r - 1) % n, 2)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    assert not errs, errs
+    for r in range(n):
+        assert sts[r] == ((r - 1) % n, 2, 0, nbytes)
+        assert torch.equal(dst[r], src[(r - 1) % n])
+
+
+def _oracle_move(oracle, sd, scount, src, rd, rcount, init):
+    """expected receive buffer: oracle unpack(rd) of oracle pack(sd)"""
+    total = scount * oracle.oracle_ddt_size(sd)
+    packed = np.zeros(max(total, 1), dtype=np.uint8)
+    oracle.oracle_ddt_pack(sd, scount, src.ctypes.data, 0, packed.ctypes.data, total)
+    out = init.copy()
+    oracle.oracle_ddt_unpack(rd, rcount, out.ctypes.data, 0, packed.ctypes.data, total)
+    return out
+
+
+@pytest.mark.parametrize("case", ["vec_to_contig", "contig_to_vec", "vec_to_indexed", "vec_to_vec"])
+def test_datatypes(gpu, pkg, oracle, comms, case):
+    """MPI_Type_vector(stride 2, block 64) from BASELINE config 5 and an indexed type, sent and
+    received through the GPU convertor; bytes equal the oracle convertor's"""
+    torch = gpu
+    nvec, blk, stride = 96, 64, 128          # 96 blocks of 64 floats, every other block
+    vec_elems = nvec * stride
+    blocklens = [3, 64, 1, 200, 5000, 900]
+    disps = [0, 10, 80, 100, 400, 5500]
+    idx_bytes = sum(blocklens) * 4           # 6168 floats: larger than the vector's 6144
+    ov = oracle.oracle_ddt_vector(nvec, blk, stride, 4)
+    dv = pkg.Ddt.vector(nvec, blk, stride, 4)
+    msg = nvec * blk * 4
+    import ctypes
+    oc = oracle.oracle_ddt_contiguous(msg, 1)
+    bl = (ctypes.c_int * len(blocklens))(*blocklens)
+    ds = (ctypes.c_int * len(disps))(*disps)
+    oi = oracle.oracle_ddt_indexed(len(blocklens), bl, ds, 4)
+    di = pkg.Ddt.indexed(blocklens, disps, 4)
+    g = np.random.default_rng(7)
+    if case == "vec_to_contig":
+        sd, od_s, scount, sbytes = dv, ov, 1, vec_elems * 4
+        rd, od_r, rcount, rbytes = None, oc, 1, msg
+    elif case == "contig_to_vec":
+        sd, od_s, scount, sbytes = None, oc, 1, msg
+        rd, od_r, rcount, rbytes = dv, ov, 1, vec_elems * 4
+    elif case == "vec_to_indexed":
+        sd, od_s, scount, sbytes = dv, ov, 1, vec_elems * 4
+        rd, od_r, rcount, rbytes = di, oi, 1, (disps[-1] + blocklens[-1]) * 4
+    else:
+        sd, od_s, scount, sbytes = dv, ov, 2, 2 * vec_elems * 4
+        rd, od_r, rcount, rbytes = dv, ov, 2, 2 * vec_elems * 4
+        msg = 2 * msg
+    src = g.integers(0, 256, sbytes, dtype=np.uint8)
+    init = np.full(rbytes, 0xA5, dtype=np.uint8)
+    dsrc = torch.from_numpy(src).cuda()
+    ddst = torch.from_numpy(init).cuda()
+    s = comms[0].isend(dsrc.data_ptr(), scount if sd else msg, 1, 0, ddt=sd)
+    st = None
+    try:
+        st = comms[1].irecv(ddst.data_ptr(), rcount if rd else msg, 0, 0, ddt=rd).wait()
+    except pkg.TruncateError as e:   # the indexed type is larger than the vector: not truncated
+        raise AssertionError(e)
+    s.wait()
+    assert st == (0, 0, 0, msg)
+    want = _oracle_move(oracle, od_s, scount, src, od_r, rcount, init)
+    assert np.array_equal(ddst.cpu().numpy(), want)
+    for o in {id(x): x for x in (ov, oc, oi)}.values():
+        oracle.oracle_ddt_free(o)
+    dv.destroy()
+    di.destroy()
+
+
+def test_errors(gpu, pkg, comms):
+    torch = gpu
+    buf = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    with pytest.raises(pkg.MI355XError, match="bad destination"):
+        comms[0].isend(buf.data_ptr(), 16, 9, 0)
+    with pytest.raises(pkg.MI355XError, match="bad tag"):
+        comms[0].isend(buf.data_ptr(), 16, 1, -5)
+    host = np.zeros(16, dtype=np.uint8)
+    with pytest.raises(pkg.MI355XError, match="device memory"):
+        comms[0].isend(host.ctypes.data, 16, 1, 0)
