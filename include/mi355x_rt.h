@@ -166,6 +166,32 @@ int mi355x_allgather(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t b
 /* MPI_Bcast of `bytes` contiguous bytes from `root`. */
 int mi355x_bcast(mi355x_comm_t *comm, void *buf, size_t bytes, int root, void *stream);
 
+/* The callers either side of the reduction path, on device buffers (coll_move.cpp).  The
+ * reference has no device form of these (coll/cuda wraps only the reductions,
+ * coll_cuda_module.c:118-140): tuned / basic run them over the PML.  Here every rank pulls what it
+ * receives straight from the owners' memory in one launch.  Counts and displacements are BYTES;
+ * NULL sbuf (rbuf for scatter at the root) = MPI_IN_PLACE.  A sender longer than the receiver's
+ * count fails with MI355X_ERR_TRUNCATE.
+ *   gather(v)   coll_tuned_gather.c / coll_basic_gatherv.c      (rcounts / displs read at the root)
+ *   scatter(v)  coll_tuned_scatter.c / coll_basic_scatterv.c    (scounts / displs read at the root)
+ *   allgatherv  coll_tuned_allgatherv.c
+ *   alltoall(v) coll_tuned_alltoall.c / coll_tuned_alltoallv.c
+ *   scan, exscan  coll_basic_scan.c:40-120 / coll_basic_exscan.c:40-110 operand order, bit-exact:
+ *               rank r = ((x0 op x1) op ...) op x_r (exscan: up to x_{r-1}; rank 0 untouched). */
+int mi355x_gather(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t bytes, int root, void *stream);
+int mi355x_gatherv(mi355x_comm_t *comm, const void *sbuf, size_t sbytes, void *rbuf, const size_t *rcounts,
+                   const size_t *displs, int root, void *stream);
+int mi355x_scatter(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t bytes, int root, void *stream);
+int mi355x_scatterv(mi355x_comm_t *comm, const void *sbuf, const size_t *scounts, const size_t *displs,
+                    void *rbuf, size_t rbytes, int root, void *stream);
+int mi355x_allgatherv(mi355x_comm_t *comm, const void *sbuf, size_t sbytes, void *rbuf, const size_t *rcounts,
+                      const size_t *displs, void *stream);
+int mi355x_alltoall(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t bytes, void *stream);
+int mi355x_alltoallv(mi355x_comm_t *comm, const void *sbuf, const size_t *scounts, const size_t *sdispls,
+                     void *rbuf, const size_t *rcounts, const size_t *rdispls, void *stream);
+int mi355x_scan(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op, void *stream);
+int mi355x_exscan(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op, void *stream);
+
 /* Nonblocking collectives (MPI_Iallreduce, MPI_Ireduce, MPI_Ireduce_scatter_block, MPI_Iallgather,
  * MPI_Ibcast; the coll framework's nonblocking slots, coll.h:241-356, served in the reference by
  * coll/libnbc: nbc_iallreduce.c etc.).  Each call is queued behind the caller's prior work on
@@ -183,6 +209,10 @@ int mi355x_ireduce_scatter_block(mi355x_comm_t *comm, const void *sbuf, void *rb
 int mi355x_iallgather(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t bytes, void *stream,
                       mi355x_request_t **req);
 int mi355x_ibcast(mi355x_comm_t *comm, void *buf, size_t bytes, int root, void *stream, mi355x_request_t **req);
+int mi355x_iscan(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op, void *stream,
+                 mi355x_request_t **req);
+int mi355x_ialltoall(mi355x_comm_t *comm, const void *sbuf, void *rbuf, size_t bytes, void *stream,
+                     mi355x_request_t **req);
 int mi355x_request_test(mi355x_request_t *req, int *done);
 int mi355x_request_wait(mi355x_request_t *req);
 int mi355x_request_free(mi355x_request_t *req);

@@ -153,6 +153,17 @@ def _declare(lib: ctypes.CDLL) -> None:
         "mi355x_ddt_extent": (c.c_int64, [vp]),
         "mi355x_ddt_nruns": (i, [vp]),
         "mi355x_ddt_tune": (i, [i, i, i, i]),
+        "mi355x_gather": (i, [vp, vp, vp, sz, i, vp]),
+        "mi355x_gatherv": (i, [vp, vp, sz, vp, c.POINTER(sz), c.POINTER(sz), i, vp]),
+        "mi355x_scatter": (i, [vp, vp, vp, sz, i, vp]),
+        "mi355x_scatterv": (i, [vp, vp, c.POINTER(sz), c.POINTER(sz), vp, sz, i, vp]),
+        "mi355x_allgatherv": (i, [vp, vp, sz, vp, c.POINTER(sz), c.POINTER(sz), vp]),
+        "mi355x_alltoall": (i, [vp, vp, vp, sz, vp]),
+        "mi355x_alltoallv": (i, [vp, vp, c.POINTER(sz), c.POINTER(sz), vp, c.POINTER(sz), c.POINTER(sz), vp]),
+        "mi355x_scan": (i, [vp, vp, vp, sz, i, i, vp]),
+        "mi355x_exscan": (i, [vp, vp, vp, sz, i, i, vp]),
+        "mi355x_iscan": (i, [vp, vp, vp, sz, i, i, vp, c.POINTER(vp)]),
+        "mi355x_ialltoall": (i, [vp, vp, vp, sz, vp, c.POINTER(vp)]),
         "mi355x_isend": (i, [vp, vp, sz, vp, i, i, vp, c.POINTER(vp)]),
         "mi355x_irecv": (i, [vp, vp, sz, vp, i, i, vp, c.POINTER(vp)]),
         "mi355x_send": (i, [vp, vp, sz, vp, i, i, vp]),
@@ -311,6 +322,48 @@ class Comm:
 
     def bcast(self, buf, nbytes, root, stream=None) -> None:
         check(rt().mi355x_bcast(self.h, buf, nbytes, root, stream), "mi355x_bcast")
+
+    # ---- gather / scatter / allgatherv / alltoall(v) (bytes) and scan / exscan (elements)
+    @staticmethod
+    def _sizes(v):
+        return None if v is None else (ctypes.c_size_t * len(v))(*v)
+
+    def gather(self, sbuf, rbuf, nbytes, root, stream=None) -> None:
+        check(rt().mi355x_gather(self.h, sbuf, rbuf, nbytes, root, stream), "mi355x_gather")
+
+    def gatherv(self, sbuf, sbytes, rbuf, rcounts, displs, root, stream=None) -> None:
+        check(rt().mi355x_gatherv(self.h, sbuf, sbytes, rbuf, self._sizes(rcounts), self._sizes(displs), root,
+                                  stream), "mi355x_gatherv")
+
+    def scatter(self, sbuf, rbuf, nbytes, root, stream=None) -> None:
+        check(rt().mi355x_scatter(self.h, sbuf, rbuf, nbytes, root, stream), "mi355x_scatter")
+
+    def scatterv(self, sbuf, scounts, displs, rbuf, rbytes, root, stream=None) -> None:
+        check(rt().mi355x_scatterv(self.h, sbuf, self._sizes(scounts), self._sizes(displs), rbuf, rbytes, root,
+                                   stream), "mi355x_scatterv")
+
+    def allgatherv(self, sbuf, sbytes, rbuf, rcounts, displs, stream=None) -> None:
+        check(rt().mi355x_allgatherv(self.h, sbuf, sbytes, rbuf, self._sizes(rcounts), self._sizes(displs),
+                                     stream), "mi355x_allgatherv")
+
+    def alltoall(self, sbuf, rbuf, nbytes, stream=None) -> None:
+        check(rt().mi355x_alltoall(self.h, sbuf, rbuf, nbytes, stream), "mi355x_alltoall")
+
+    def alltoallv(self, sbuf, scounts, sdispls, rbuf, rcounts, rdispls, stream=None) -> None:
+        check(rt().mi355x_alltoallv(self.h, sbuf, self._sizes(scounts), self._sizes(sdispls), rbuf,
+                                    self._sizes(rcounts), self._sizes(rdispls), stream), "mi355x_alltoallv")
+
+    def scan(self, sbuf, rbuf, count, ty, op, stream=None) -> None:
+        check(rt().mi355x_scan(self.h, sbuf, rbuf, count, ty, op, stream), "mi355x_scan")
+
+    def exscan(self, sbuf, rbuf, count, ty, op, stream=None) -> None:
+        check(rt().mi355x_exscan(self.h, sbuf, rbuf, count, ty, op, stream), "mi355x_exscan")
+
+    def iscan(self, sbuf, rbuf, count, ty, op, stream=None) -> Request:
+        return self._post("mi355x_iscan", sbuf, rbuf, count, ty, op, stream)
+
+    def ialltoall(self, sbuf, rbuf, nbytes, stream=None) -> Request:
+        return self._post("mi355x_ialltoall", sbuf, rbuf, nbytes, stream)
 
     # ---- device point-to-point (count = bytes when ddt is None, else datatype instances)
     def isend(self, buf, count, dest, tag, ddt=None, stream=None) -> Request:

@@ -375,8 +375,8 @@ int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **e
 // that cannot be exported, nothing is mapped and *staged is set on every rank alike (callers
 // that pass staged == NULL get an error instead).  force: export regardless of allocation size
 // (the staging buffers themselves).
-static int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t sig[4],
-                    std::vector<std::vector<void *>> &peers, bool *staged = nullptr, bool force = false)
+int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t sig[4],
+             std::vector<std::vector<void *>> &peers, bool *staged, bool force)
 {
     c->seq++;
     if (staged) *staged = false;
@@ -444,7 +444,7 @@ static int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uin
     return MI355X_SUCCESS;
 }
 
-static int finish(mi355x_comm *c, hipStream_t s)
+int finish(mi355x_comm *c, hipStream_t s)
 {
     TRACE(c, "finish: stream sync");
     MI_HIP(hipStreamSynchronize(s));
@@ -455,7 +455,7 @@ static int finish(mi355x_comm *c, hipStream_t s)
 // The scratch may be exported to peers (MPI_Reduce's owner blocks): never a small allocation
 // (small hipMallocs can fail hipIpcOpenMemHandle on the importer with "invalid device
 // pointer"), and grown geometrically so it is rarely freed while peers hold a mapping.
-static int ensure_scratch(mi355x_comm *c, size_t bytes)
+int ensure_scratch(mi355x_comm *c, size_t bytes)
 {
     if (c->scratch_bytes >= bytes) return MI355X_SUCCESS;
     size_t want = std::max<size_t>((size_t)8 << 20, c->scratch_bytes * 2);
@@ -470,7 +470,7 @@ static int ensure_scratch(mi355x_comm *c, size_t bytes)
 
 // ----------------------------------------------------------------- program launch
 // Evaluate `pr` on elements [off, off+len) of every rank's input `in[q]`, writing dst[d] + off.
-static int run_program(int op, int type, const Program &pr, const std::vector<void *> &in,
+int run_program(int op, int type, const Program &pr, const std::vector<void *> &in,
                        const std::vector<void *> &dst, size_t off, size_t len, hipStream_t s)
 {
     if (len == 0) return MI355X_SUCCESS;
@@ -840,7 +840,7 @@ static bool allreduce_tree_program(const mi355x_comm *c, int alg, size_t count, 
     return reduce_program(c, count, esz, 0, pr, &ra);
 }
 
-static int check_common(mi355x_comm *c, int op, int type)
+int check_common(mi355x_comm *c, int op, int type)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     if (!mi355x_op_supported(op, type))
@@ -857,7 +857,7 @@ static double env_double(const char *name, double dflt)
 // ----------------------------------------------------------------- nonblocking
 // Wait until every posted nonblocking call of this communicator has finished (MPI orders a
 // blocking collective after the nonblocking ones posted before it on every rank).
-static void drain(mi355x_comm *c)
+void drain(mi355x_comm *c)
 {
     std::unique_lock<std::mutex> g(c->q_mtx);
     c->q_cv.wait(g, [c] { return c->pending == 0; });
@@ -892,7 +892,7 @@ static void worker_main(mi355x_comm *c)
 }
 
 // queue `run` after the caller's work on `stream`; the request completes when it has run
-static int post(mi355x_comm *c, void *stream, std::function<int(hipStream_t)> run, mi355x_request **out)
+int post(mi355x_comm *c, void *stream, std::function<int(hipStream_t)> run, mi355x_request **out)
 {
     if (!out) return set_error(MI355X_ERR_ARG, "request pointer is NULL");
     *out = nullptr;

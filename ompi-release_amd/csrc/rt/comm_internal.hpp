@@ -62,6 +62,7 @@ struct alignas(64) RankSlot {
     BufDesc buf[kMaxBufs];
     int32_t probe_fd, probe_ok;   // dmabuf capability probe
     uint64_t probe_size;
+    int64_t varg[2 * kMaxRanks];  // per-peer counts / displacements of v-collectives (bytes)
 };
 
 struct Ctrl {
@@ -229,6 +230,16 @@ int barrier(mi355x_comm *c);
 int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force);
 int export_dmabuf(mi355x_comm *c, BufDesc *d);
 int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **entry = nullptr);
+// publish nbuf buffers, meet every rank, map every rank's buffers: peers[b][r] (coll_comm.cpp)
+int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t sig[4],
+             std::vector<std::vector<void *>> &peers, bool *staged = nullptr, bool force = false);
+int finish(mi355x_comm *c, hipStream_t s);          // stream sync + barrier
+int ensure_scratch(mi355x_comm *c, size_t bytes);   // exportable per-communicator scratch
+int run_program(int op, int type, const Program &pr, const std::vector<void *> &in,
+                const std::vector<void *> &dst, size_t off, size_t len, hipStream_t s);
+int check_common(mi355x_comm *c, int op, int type);
+void drain(mi355x_comm *c);                         // wait for every posted nonblocking call
+int post(mi355x_comm *c, void *stream, std::function<int(hipStream_t)> run, mi355x_request **out);
 void p2p_destroy(mi355x_comm *c);
 int p2p_progress(mi355x_comm *c);
 int p2p_wait(mi355x_request *r);

@@ -104,6 +104,10 @@ int oracle_reduce_scatter(int n, const int *rcounts, int type, int op,
 int oracle_reduce_scatter_alg(int alg, int n, const int *rcounts, int type, int op,
                               const void *const *sbufs, void *const *rbufs);
 
+/* MPI_Scan (exclusive 0) / MPI_Exscan (1) in coll/basic's linear-chain order (coll_oracle_scan.c) */
+int oracle_scan(int exclusive, int n, size_t count, int type, int op, const void *const *sbufs,
+                void *const *rbufs);
+
 /* ---------------- datatypes / convertor (ddt_oracle.c) ------------------------------------- */
 typedef struct oracle_ddt oracle_ddt_t;
 oracle_ddt_t *oracle_ddt_contiguous(int64_t count, int64_t elem);

@@ -60,6 +60,7 @@ def load_oracle() -> ctypes.CDLL:
         lib.oracle_reduce_fo.argtypes = [i, i, i, i, sz, i, i, c.POINTER(vp), vp]
         lib.oracle_reduce_scatter_alg.argtypes = [i, i, c.POINTER(i), i, i, c.POINTER(vp), c.POINTER(vp)]
         lib.oracle_reduce_scatter_block.argtypes = [i, sz, i, i, c.POINTER(vp), c.POINTER(vp)]
+        lib.oracle_scan.argtypes = [i, i, sz, i, i, c.POINTER(vp), c.POINTER(vp)]
         lib.oracle_ring_fold_order.argtypes = [i, sz, sz, c.POINTER(c.c_int)]
         i64 = c.c_int64
         lib.oracle_ddt_contiguous.restype = vp
