@@ -3,9 +3,10 @@
  *
  * Plugs into the coll framework (ompi/mca/coll/coll.h:357-451) at priority 90 -- above
  * coll/tuned (30) and coll/cuda (78) -- for intra-communicators whose ranks all live on this
- * node.  It provides allreduce, reduce, reduce_scatter, reduce_scatter_block, allgather and bcast, and
- * the nonblocking iallreduce, ireduce, ireduce_scatter_block, iallgather and ibcast; every
- * other slot stays with the lower-priority modules.  Entry points have exactly the reference
+ * node.  It provides allreduce, reduce, reduce_scatter, reduce_scatter_block, allgather, bcast,
+ * gather(v), scatter(v), allgatherv, alltoall(v), scan and exscan, and the nonblocking iallreduce,
+ * ireduce, ireduce_scatter_block, iallgather and ibcast; every other slot (alltoallw, barrier,
+ * the other nonblocking and neighborhood ones) stays with the lower-priority modules.  Entry points have exactly the reference
  * signatures (coll.h:181-239) and replace, for device buffers:
  *   mca_coll_cuda_allreduce            (ompi/mca/coll/cuda/coll_cuda_allreduce.c:30-77)
  *   mca_coll_cuda_reduce_scatter_block (coll_cuda_reduce_scatter_block.c:34-83)
@@ -66,6 +67,35 @@ int mca_coll_mi355x_allgather(void *sbuf, int scount, struct ompi_datatype_t *sd
                               mca_coll_base_module_t *module);
 int mca_coll_mi355x_bcast(void *buff, int count, struct ompi_datatype_t *datatype, int root,
                           struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+
+/* the callers either side of the reduction path (coll.h:185-238; reference: coll/tuned, coll/basic
+ * over the PML); dense datatypes on device buffers, everything else to the previous owner */
+int mca_coll_mi355x_gather(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
+                           struct ompi_datatype_t *rdtype, int root, struct ompi_communicator_t *comm,
+                           mca_coll_base_module_t *module);
+int mca_coll_mi355x_gatherv(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int *rcounts,
+                            int *disps, struct ompi_datatype_t *rdtype, int root, struct ompi_communicator_t *comm,
+                            mca_coll_base_module_t *module);
+int mca_coll_mi355x_scatter(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
+                            struct ompi_datatype_t *rdtype, int root, struct ompi_communicator_t *comm,
+                            mca_coll_base_module_t *module);
+int mca_coll_mi355x_scatterv(void *sbuf, int *scounts, int *disps, struct ompi_datatype_t *sdtype, void *rbuf,
+                             int rcount, struct ompi_datatype_t *rdtype, int root, struct ompi_communicator_t *comm,
+                             mca_coll_base_module_t *module);
+int mca_coll_mi355x_allgatherv(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int *rcounts,
+                               int *disps, struct ompi_datatype_t *rdtype, struct ompi_communicator_t *comm,
+                               mca_coll_base_module_t *module);
+int mca_coll_mi355x_alltoall(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
+                             struct ompi_datatype_t *rdtype, struct ompi_communicator_t *comm,
+                             mca_coll_base_module_t *module);
+int mca_coll_mi355x_alltoallv(void *sbuf, int *scounts, int *sdisps, struct ompi_datatype_t *sdtype, void *rbuf,
+                              int *rcounts, int *rdisps, struct ompi_datatype_t *rdtype,
+                              struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+/* MPI_Scan / MPI_Exscan in coll/basic's chain order (coll_basic_scan.c, coll_basic_exscan.c) */
+int mca_coll_mi355x_scan(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                         struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+int mca_coll_mi355x_exscan(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                           struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
 
 /* MCA parameters (environment: OMPI_MCA_coll_mi355x_<name>) */
 extern int mca_coll_mi355x_priority;            /* 90 */

@@ -397,6 +397,34 @@ typedef int (*mca_coll_base_module_reduce_scatter_block_fn_t)(void *sbuf, void *
                                                               struct ompi_datatype_t *dtype, struct ompi_op_t *op,
                                                               struct ompi_communicator_t *comm,
                                                               mca_coll_base_module_t *module);
+/* coll.h:185-238: the blocking slots of the reduction path's callers that coll/mi355x fills */
+typedef int (*mca_coll_base_module_allgatherv_fn_t)(void *sbuf, int scount, struct ompi_datatype_t *sdtype,
+                                                    void *rbuf, int *rcounts, int *disps,
+                                                    struct ompi_datatype_t *rdtype, struct ompi_communicator_t *comm,
+                                                    mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_alltoall_fn_t)(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf,
+                                                  int rcount, struct ompi_datatype_t *rdtype,
+                                                  struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_alltoallv_fn_t)(void *sbuf, int *scounts, int *sdisps,
+                                                   struct ompi_datatype_t *sdtype, void *rbuf, int *rcounts,
+                                                   int *rdisps, struct ompi_datatype_t *rdtype,
+                                                   struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_exscan_fn_t)(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                                                struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                                                mca_coll_base_module_t *module);
+typedef mca_coll_base_module_exscan_fn_t mca_coll_base_module_scan_fn_t;
+typedef int (*mca_coll_base_module_gather_fn_t)(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf,
+                                                int rcount, struct ompi_datatype_t *rdtype, int root,
+                                                struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+typedef mca_coll_base_module_gather_fn_t mca_coll_base_module_scatter_fn_t;
+typedef int (*mca_coll_base_module_gatherv_fn_t)(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf,
+                                                 int *rcounts, int *disps, struct ompi_datatype_t *rdtype, int root,
+                                                 struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_scatterv_fn_t)(void *sbuf, int *scounts, int *disps,
+                                                  struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
+                                                  struct ompi_datatype_t *rdtype, int root,
+                                                  struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+
 /* coll.h:241-356 (the nonblocking slots coll/mi355x provides) */
 typedef int (*mca_coll_base_module_iallgather_fn_t)(void *sbuf, int scount, struct ompi_datatype_t *sdtype,
                                                     void *rbuf, int rcount, struct ompi_datatype_t *rdtype,
@@ -425,22 +453,22 @@ struct mca_coll_base_module_2_0_0_t {
     opal_object_t super;
     mca_coll_base_module_enable_fn_t coll_module_enable;
     mca_coll_base_module_allgather_fn_t coll_allgather;
-    mca_coll_base_any_fn_t coll_allgatherv;
+    mca_coll_base_module_allgatherv_fn_t coll_allgatherv;
     mca_coll_base_module_allreduce_fn_t coll_allreduce;
-    mca_coll_base_any_fn_t coll_alltoall;
-    mca_coll_base_any_fn_t coll_alltoallv;
+    mca_coll_base_module_alltoall_fn_t coll_alltoall;
+    mca_coll_base_module_alltoallv_fn_t coll_alltoallv;
     mca_coll_base_any_fn_t coll_alltoallw;
     mca_coll_base_any_fn_t coll_barrier;
     mca_coll_base_module_bcast_fn_t coll_bcast;
-    mca_coll_base_any_fn_t coll_exscan;
-    mca_coll_base_any_fn_t coll_gather;
-    mca_coll_base_any_fn_t coll_gatherv;
+    mca_coll_base_module_exscan_fn_t coll_exscan;
+    mca_coll_base_module_gather_fn_t coll_gather;
+    mca_coll_base_module_gatherv_fn_t coll_gatherv;
     mca_coll_base_module_reduce_fn_t coll_reduce;
     mca_coll_base_module_reduce_scatter_fn_t coll_reduce_scatter;
     mca_coll_base_module_reduce_scatter_block_fn_t coll_reduce_scatter_block;
-    mca_coll_base_any_fn_t coll_scan;
-    mca_coll_base_any_fn_t coll_scatter;
-    mca_coll_base_any_fn_t coll_scatterv;
+    mca_coll_base_module_scan_fn_t coll_scan;
+    mca_coll_base_module_scatter_fn_t coll_scatter;
+    mca_coll_base_module_scatterv_fn_t coll_scatterv;
     /* coll.h:418-434 */
     mca_coll_base_module_iallgather_fn_t coll_iallgather;
     mca_coll_base_any_fn_t coll_iallgatherv;
@@ -463,21 +491,35 @@ extern opal_class_t mca_coll_base_module_t_class;
 typedef struct mca_coll_base_comm_coll_t {
     mca_coll_base_module_allgather_fn_t coll_allgather;
     mca_coll_base_module_t *coll_allgather_module;
-    mca_coll_base_any_fn_t coll_allgatherv;
+    mca_coll_base_module_allgatherv_fn_t coll_allgatherv;
     mca_coll_base_module_t *coll_allgatherv_module;
     mca_coll_base_module_allreduce_fn_t coll_allreduce;
     mca_coll_base_module_t *coll_allreduce_module;
-    struct { mca_coll_base_any_fn_t fn; mca_coll_base_module_t *module; } coll_a2a[4]; /* alltoall(v,w), barrier */
+    mca_coll_base_module_alltoall_fn_t coll_alltoall;
+    mca_coll_base_module_t *coll_alltoall_module;
+    mca_coll_base_module_alltoallv_fn_t coll_alltoallv;
+    mca_coll_base_module_t *coll_alltoallv_module;
+    struct { mca_coll_base_any_fn_t fn; mca_coll_base_module_t *module; } coll_aw_bar[2]; /* alltoallw, barrier */
     mca_coll_base_module_bcast_fn_t coll_bcast;
     mca_coll_base_module_t *coll_bcast_module;
-    struct { mca_coll_base_any_fn_t fn; mca_coll_base_module_t *module; } coll_egg[3];  /* exscan, gather(v) */
+    mca_coll_base_module_exscan_fn_t coll_exscan;
+    mca_coll_base_module_t *coll_exscan_module;
+    mca_coll_base_module_gather_fn_t coll_gather;
+    mca_coll_base_module_t *coll_gather_module;
+    mca_coll_base_module_gatherv_fn_t coll_gatherv;
+    mca_coll_base_module_t *coll_gatherv_module;
     mca_coll_base_module_reduce_fn_t coll_reduce;
     mca_coll_base_module_t *coll_reduce_module;
     mca_coll_base_module_reduce_scatter_fn_t coll_reduce_scatter;
     mca_coll_base_module_t *coll_reduce_scatter_module;
     mca_coll_base_module_reduce_scatter_block_fn_t coll_reduce_scatter_block;
     mca_coll_base_module_t *coll_reduce_scatter_block_module;
-    struct { mca_coll_base_any_fn_t fn; mca_coll_base_module_t *module; } coll_sss[3];  /* scan, scatter(v) */
+    mca_coll_base_module_scan_fn_t coll_scan;
+    mca_coll_base_module_t *coll_scan_module;
+    mca_coll_base_module_scatter_fn_t coll_scatter;
+    mca_coll_base_module_t *coll_scatter_module;
+    mca_coll_base_module_scatterv_fn_t coll_scatterv;
+    mca_coll_base_module_t *coll_scatterv_module;
     /* coll.h:505-540 */
     mca_coll_base_module_iallgather_fn_t coll_iallgather;
     mca_coll_base_module_t *coll_iallgather_module;

@@ -322,6 +322,15 @@ void mini_comm_install(ompi_communicator_t *c, mca_coll_base_module_t *m)
     INST(ibcast)
     INST(ireduce)
     INST(ireduce_scatter_block)
+    INST(gather)
+    INST(gatherv)
+    INST(scatter)
+    INST(scatterv)
+    INST(allgatherv)
+    INST(alltoall)
+    INST(alltoallv)
+    INST(scan)
+    INST(exscan)
 #undef INST
 }
 
@@ -361,6 +370,15 @@ void mini_comm_destroy(ompi_communicator_t *c)
     REL(ibcast)
     REL(ireduce)
     REL(ireduce_scatter_block)
+    REL(gather)
+    REL(gatherv)
+    REL(scatter)
+    REL(scatterv)
+    REL(allgatherv)
+    REL(alltoall)
+    REL(alltoallv)
+    REL(scan)
+    REL(exscan)
 #undef REL
     mi355x_obj_release(&c->c_local_group->super);
     free(c);
@@ -480,6 +498,49 @@ int mini_bcast(ompi_communicator_t *c, void *b, int n, ompi_datatype_t *d, int r
 {
     return c->c_coll.coll_bcast(b, n, d, root, c, c->c_coll.coll_bcast_module);
 }
+int mini_gather(ompi_communicator_t *c, void *s, int sc, ompi_datatype_t *sd, void *r, int rc, ompi_datatype_t *rd,
+                int root)
+{
+    return c->c_coll.coll_gather(s, sc, sd, r, rc, rd, root, c, c->c_coll.coll_gather_module);
+}
+int mini_gatherv(ompi_communicator_t *c, void *s, int sc, ompi_datatype_t *sd, void *r, int *rc, int *dp,
+                 ompi_datatype_t *rd, int root)
+{
+    return c->c_coll.coll_gatherv(s, sc, sd, r, rc, dp, rd, root, c, c->c_coll.coll_gatherv_module);
+}
+int mini_scatter(ompi_communicator_t *c, void *s, int sc, ompi_datatype_t *sd, void *r, int rc, ompi_datatype_t *rd,
+                 int root)
+{
+    return c->c_coll.coll_scatter(s, sc, sd, r, rc, rd, root, c, c->c_coll.coll_scatter_module);
+}
+int mini_scatterv(ompi_communicator_t *c, void *s, int *sc, int *dp, ompi_datatype_t *sd, void *r, int rc,
+                  ompi_datatype_t *rd, int root)
+{
+    return c->c_coll.coll_scatterv(s, sc, dp, sd, r, rc, rd, root, c, c->c_coll.coll_scatterv_module);
+}
+int mini_allgatherv(ompi_communicator_t *c, void *s, int sc, ompi_datatype_t *sd, void *r, int *rc, int *dp,
+                    ompi_datatype_t *rd)
+{
+    return c->c_coll.coll_allgatherv(s, sc, sd, r, rc, dp, rd, c, c->c_coll.coll_allgatherv_module);
+}
+int mini_alltoall(ompi_communicator_t *c, void *s, int sc, ompi_datatype_t *sd, void *r, int rc, ompi_datatype_t *rd)
+{
+    return c->c_coll.coll_alltoall(s, sc, sd, r, rc, rd, c, c->c_coll.coll_alltoall_module);
+}
+int mini_alltoallv(ompi_communicator_t *c, void *s, int *sc, int *sdp, ompi_datatype_t *sd, void *r, int *rc,
+                   int *rdp, ompi_datatype_t *rd)
+{
+    return c->c_coll.coll_alltoallv(s, sc, sdp, sd, r, rc, rdp, rd, c, c->c_coll.coll_alltoallv_module);
+}
+int mini_scan(ompi_communicator_t *c, void *s, void *r, int n, ompi_datatype_t *d, ompi_op_t *op)
+{
+    return c->c_coll.coll_scan(s, r, n, d, op, c, c->c_coll.coll_scan_module);
+}
+int mini_exscan(ompi_communicator_t *c, void *s, void *r, int n, ompi_datatype_t *d, ompi_op_t *op)
+{
+    return c->c_coll.coll_exscan(s, r, n, d, op, c, c->c_coll.coll_exscan_module);
+}
+
 void *mini_comm_fn(ompi_communicator_t *c, int which)
 {
     switch (which) {
@@ -494,12 +555,21 @@ void *mini_comm_fn(ompi_communicator_t *c, int which)
     case 8: return (void *)c->c_coll.coll_ireduce_scatter_block;
     case 9: return (void *)c->c_coll.coll_iallgather;
     case 10: return (void *)c->c_coll.coll_ibcast;
+    case 11: return (void *)c->c_coll.coll_gather;
+    case 12: return (void *)c->c_coll.coll_gatherv;
+    case 13: return (void *)c->c_coll.coll_scatter;
+    case 14: return (void *)c->c_coll.coll_scatterv;
+    case 15: return (void *)c->c_coll.coll_allgatherv;
+    case 16: return (void *)c->c_coll.coll_alltoall;
+    case 17: return (void *)c->c_coll.coll_alltoallv;
+    case 18: return (void *)c->c_coll.coll_scan;
+    case 19: return (void *)c->c_coll.coll_exscan;
     default: return NULL;
     }
 }
 
 /* a stub "lower-priority" module for tests: records which function ran and returns `marker` */
-static int stub_calls[8];
+static int stub_calls[16];
 static int stub_marker = 77;
 static int st_allreduce(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o,
                         struct ompi_communicator_t *c, mca_coll_base_module_t *m)
@@ -524,6 +594,28 @@ static int st_iallreduce(void *s, void *r, int n, struct ompi_datatype_t *d, str
                          struct ompi_communicator_t *c, ompi_request_t **req, mca_coll_base_module_t *m)
 { (void)s; (void)r; (void)n; (void)d; (void)o; (void)c; (void)m; *req = &ompi_request_null.request; stub_calls[6]++; return stub_marker; }
 
+static int st_gather(void *s, int sc, struct ompi_datatype_t *sd, void *r, int rc, struct ompi_datatype_t *rd,
+                     int root, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{ (void)s; (void)sc; (void)sd; (void)r; (void)rc; (void)rd; (void)root; (void)c; (void)m; stub_calls[7]++; return stub_marker; }
+static int st_alltoall(void *s, int sc, struct ompi_datatype_t *sd, void *r, int rc, struct ompi_datatype_t *rd,
+                       struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{ (void)s; (void)sc; (void)sd; (void)r; (void)rc; (void)rd; (void)c; (void)m; stub_calls[8]++; return stub_marker; }
+static int st_scan(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                   struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{ (void)s; (void)r; (void)n; (void)d; (void)o; (void)c; (void)m; stub_calls[9]++; return stub_marker; }
+static int st_gatherv(void *s, int sc, struct ompi_datatype_t *sd, void *r, int *rc, int *dp,
+                      struct ompi_datatype_t *rd, int root, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{ (void)s; (void)sc; (void)sd; (void)r; (void)rc; (void)dp; (void)rd; (void)root; (void)c; (void)m; stub_calls[10]++; return stub_marker; }
+static int st_scatterv(void *s, int *sc, int *dp, struct ompi_datatype_t *sd, void *r, int rc,
+                       struct ompi_datatype_t *rd, int root, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{ (void)s; (void)sc; (void)dp; (void)sd; (void)r; (void)rc; (void)rd; (void)root; (void)c; (void)m; stub_calls[11]++; return stub_marker; }
+static int st_allgatherv(void *s, int sc, struct ompi_datatype_t *sd, void *r, int *rc, int *dp,
+                         struct ompi_datatype_t *rd, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{ (void)s; (void)sc; (void)sd; (void)r; (void)rc; (void)dp; (void)rd; (void)c; (void)m; stub_calls[12]++; return stub_marker; }
+static int st_alltoallv(void *s, int *sc, int *sdp, struct ompi_datatype_t *sd, void *r, int *rc, int *rdp,
+                        struct ompi_datatype_t *rd, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{ (void)s; (void)sc; (void)sdp; (void)sd; (void)r; (void)rc; (void)rdp; (void)rd; (void)c; (void)m; stub_calls[13]++; return stub_marker; }
+
 mca_coll_base_module_t *mini_stub_module(void)
 {
     mca_coll_base_module_t *m = mini_coll_module_new();
@@ -534,9 +626,18 @@ mca_coll_base_module_t *mini_stub_module(void)
     m->coll_bcast = st_bcast;
     m->coll_reduce = st_reduce;
     m->coll_iallreduce = st_iallreduce;
+    m->coll_gather = st_gather;
+    m->coll_scatter = st_gather;
+    m->coll_alltoall = st_alltoall;
+    m->coll_scan = st_scan;
+    m->coll_exscan = st_scan;
+    m->coll_gatherv = st_gatherv;
+    m->coll_scatterv = st_scatterv;
+    m->coll_allgatherv = st_allgatherv;
+    m->coll_alltoallv = st_alltoallv;
     return m;
 }
-int mini_stub_calls(int which) { return (which >= 0 && which < 8) ? stub_calls[which] : -1; }
+int mini_stub_calls(int which) { return (which >= 0 && which < 16) ? stub_calls[which] : -1; }
 int mini_stub_marker(void) { return stub_marker; }
 
 /* layout facts for tests/test_boundary.py */
@@ -566,6 +667,9 @@ size_t mini_offsetof(int which)
     case 20: return offsetof(ompi_request_t, req_free);
     case 21: return offsetof(mca_coll_base_comm_coll_t, coll_iallreduce);
     case 22: return sizeof(ompi_predefined_request_t);
+    case 23: return offsetof(mca_coll_base_module_t, coll_scan);
+    case 24: return offsetof(mca_coll_base_comm_coll_t, coll_scatterv);
+    case 25: return offsetof(mca_coll_base_comm_coll_t, coll_gather);
     default: return (size_t)-1;
     }
 }

@@ -32,6 +32,25 @@ typedef struct mca_coll_mi355x_module_t {
     mca_coll_base_module_t *prev_bcast_module;
     mca_coll_base_module_reduce_fn_t prev_reduce;
     mca_coll_base_module_t *prev_reduce_module;
+    /* the callers either side of the reduction path (coll_move.cpp) */
+    mca_coll_base_module_gather_fn_t prev_gather;
+    mca_coll_base_module_t *prev_gather_module;
+    mca_coll_base_module_gatherv_fn_t prev_gatherv;
+    mca_coll_base_module_t *prev_gatherv_module;
+    mca_coll_base_module_scatter_fn_t prev_scatter;
+    mca_coll_base_module_t *prev_scatter_module;
+    mca_coll_base_module_scatterv_fn_t prev_scatterv;
+    mca_coll_base_module_t *prev_scatterv_module;
+    mca_coll_base_module_allgatherv_fn_t prev_allgatherv;
+    mca_coll_base_module_t *prev_allgatherv_module;
+    mca_coll_base_module_alltoall_fn_t prev_alltoall;
+    mca_coll_base_module_t *prev_alltoall_module;
+    mca_coll_base_module_alltoallv_fn_t prev_alltoallv;
+    mca_coll_base_module_t *prev_alltoallv_module;
+    mca_coll_base_module_scan_fn_t prev_scan;
+    mca_coll_base_module_t *prev_scan_module;
+    mca_coll_base_module_exscan_fn_t prev_exscan;
+    mca_coll_base_module_t *prev_exscan_module;
     /* nonblocking slots: the previous owner (normally coll/libnbc) may be absent */
     mca_coll_base_module_iallreduce_fn_t prev_iallreduce;
     mca_coll_base_module_t *prev_iallreduce_module;
@@ -71,6 +90,15 @@ static void module_destruct(opal_object_t *o)
     release_prev(m->prev_allgather_module);
     release_prev(m->prev_bcast_module);
     release_prev(m->prev_reduce_module);
+    release_prev(m->prev_gather_module);
+    release_prev(m->prev_gatherv_module);
+    release_prev(m->prev_scatter_module);
+    release_prev(m->prev_scatterv_module);
+    release_prev(m->prev_allgatherv_module);
+    release_prev(m->prev_alltoall_module);
+    release_prev(m->prev_alltoallv_module);
+    release_prev(m->prev_scan_module);
+    release_prev(m->prev_exscan_module);
     release_prev(m->prev_iallreduce_module);
     release_prev(m->prev_ireduce_module);
     release_prev(m->prev_ireduce_scatter_block_module);
@@ -316,6 +344,153 @@ int mca_coll_mi355x_bcast(void *buff, int count, struct ompi_datatype_t *datatyp
     return map_rc(rc);
 }
 
+/* ------------------------------------------------------------------ gather / scatter / alltoall / scan
+ * Dense datatypes only (gap-free, extent == size: counts and displacements scale by the size);
+ * anything else, host buffers or user-defined ops go to the previous owner of the slot. */
+static int dense(const struct ompi_datatype_t *dt)
+{
+    return (dt->super.flags & OPAL_DATATYPE_FLAG_NO_GAPS) && dt->super.true_lb == 0 &&
+           (size_t)(dt->super.ub - dt->super.lb) == dt->super.size;
+}
+
+/* counts / displacements (in datatype units) -> bytes; NULL when not needed at this rank */
+static int to_bytes(int n, const int *v, size_t unit, size_t *out)
+{
+    for (int i = 0; i < n; ++i) {
+        if (v[i] < 0) return 0;
+        out[i] = (size_t)v[i] * unit;
+    }
+    return 1;
+}
+
+int mca_coll_mi355x_gather(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
+                           struct ompi_datatype_t *rdtype, int root, struct ompi_communicator_t *comm,
+                           mca_coll_base_module_t *module)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    const int me = mi355x_comm_rank_of(comm), inplace = (sbuf == MPI_IN_PLACE);
+    if ((me == root && (!is_dev(rbuf) || !dense(rdtype) || rcount < 0)) ||
+        (!inplace && (!is_dev(sbuf) || !dense(sdtype) || scount < 0)) || (inplace && me != root))
+        return m->prev_gather(sbuf, scount, sdtype, rbuf, rcount, rdtype, root, comm, m->prev_gather_module);
+    const size_t bytes = inplace ? (size_t)rcount * rdtype->super.size : (size_t)scount * sdtype->super.size;
+    return map_rc(mi355x_gather(m->engine, inplace ? NULL : sbuf, me == root ? rbuf : NULL, bytes, root, NULL));
+}
+
+int mca_coll_mi355x_gatherv(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int *rcounts,
+                            int *disps, struct ompi_datatype_t *rdtype, int root, struct ompi_communicator_t *comm,
+                            mca_coll_base_module_t *module)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm), inplace = (sbuf == MPI_IN_PLACE);
+    size_t rc_b[64], dp_b[64];
+    if (n > 64 || (me == root && (!is_dev(rbuf) || !dense(rdtype) || !to_bytes(n, rcounts, rdtype->super.size, rc_b) ||
+                                  !to_bytes(n, disps, rdtype->super.size, dp_b))) ||
+        (!inplace && (!is_dev(sbuf) || !dense(sdtype) || scount < 0)) || (inplace && me != root))
+        return m->prev_gatherv(sbuf, scount, sdtype, rbuf, rcounts, disps, rdtype, root, comm, m->prev_gatherv_module);
+    const size_t sb = inplace ? 0 : (size_t)scount * sdtype->super.size;
+    return map_rc(mi355x_gatherv(m->engine, inplace ? NULL : sbuf, sb, me == root ? rbuf : NULL,
+                                 me == root ? rc_b : NULL, me == root ? dp_b : NULL, root, NULL));
+}
+
+int mca_coll_mi355x_scatter(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
+                            struct ompi_datatype_t *rdtype, int root, struct ompi_communicator_t *comm,
+                            mca_coll_base_module_t *module)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    const int me = mi355x_comm_rank_of(comm), inplace = (rbuf == MPI_IN_PLACE);
+    if ((me == root && (!is_dev(sbuf) || !dense(sdtype) || scount < 0)) ||
+        (!inplace && (!is_dev(rbuf) || !dense(rdtype) || rcount < 0)) || (inplace && me != root))
+        return m->prev_scatter(sbuf, scount, sdtype, rbuf, rcount, rdtype, root, comm, m->prev_scatter_module);
+    const size_t bytes = me == root ? (size_t)scount * sdtype->super.size : (size_t)rcount * rdtype->super.size;
+    return map_rc(mi355x_scatter(m->engine, me == root ? sbuf : NULL, inplace ? NULL : rbuf, bytes, root, NULL));
+}
+
+int mca_coll_mi355x_scatterv(void *sbuf, int *scounts, int *disps, struct ompi_datatype_t *sdtype, void *rbuf,
+                             int rcount, struct ompi_datatype_t *rdtype, int root, struct ompi_communicator_t *comm,
+                             mca_coll_base_module_t *module)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm), inplace = (rbuf == MPI_IN_PLACE);
+    size_t sc_b[64], dp_b[64];
+    if (n > 64 || (me == root && (!is_dev(sbuf) || !dense(sdtype) || !to_bytes(n, scounts, sdtype->super.size, sc_b) ||
+                                  !to_bytes(n, disps, sdtype->super.size, dp_b))) ||
+        (!inplace && (!is_dev(rbuf) || !dense(rdtype) || rcount < 0)) || (inplace && me != root))
+        return m->prev_scatterv(sbuf, scounts, disps, sdtype, rbuf, rcount, rdtype, root, comm,
+                                m->prev_scatterv_module);
+    const size_t rb = inplace ? 0 : (size_t)rcount * rdtype->super.size;
+    return map_rc(mi355x_scatterv(m->engine, me == root ? sbuf : NULL, me == root ? sc_b : NULL,
+                                  me == root ? dp_b : NULL, inplace ? NULL : rbuf, rb, root, NULL));
+}
+
+int mca_coll_mi355x_allgatherv(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int *rcounts,
+                               int *disps, struct ompi_datatype_t *rdtype, struct ompi_communicator_t *comm,
+                               mca_coll_base_module_t *module)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    const int n = mi355x_comm_size_of(comm), inplace = (sbuf == MPI_IN_PLACE);
+    size_t rc_b[64], dp_b[64];
+    if (n > 64 || !is_dev(rbuf) || !dense(rdtype) || !to_bytes(n, rcounts, rdtype->super.size, rc_b) ||
+        !to_bytes(n, disps, rdtype->super.size, dp_b) || (!inplace && (!is_dev(sbuf) || !dense(sdtype) || scount < 0)))
+        return m->prev_allgatherv(sbuf, scount, sdtype, rbuf, rcounts, disps, rdtype, comm, m->prev_allgatherv_module);
+    return map_rc(mi355x_allgatherv(m->engine, inplace ? NULL : sbuf, inplace ? 0 : (size_t)scount * sdtype->super.size,
+                                    rbuf, rc_b, dp_b, NULL));
+}
+
+int mca_coll_mi355x_alltoall(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
+                             struct ompi_datatype_t *rdtype, struct ompi_communicator_t *comm,
+                             mca_coll_base_module_t *module)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    const int inplace = (sbuf == MPI_IN_PLACE);
+    if (!is_dev(rbuf) || !dense(rdtype) || rcount < 0 ||
+        (!inplace && (!is_dev(sbuf) || !dense(sdtype) || (size_t)scount * sdtype->super.size !=
+                                                             (size_t)rcount * rdtype->super.size)))
+        return m->prev_alltoall(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_alltoall_module);
+    return map_rc(mi355x_alltoall(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)rcount * rdtype->super.size, NULL));
+}
+
+int mca_coll_mi355x_alltoallv(void *sbuf, int *scounts, int *sdisps, struct ompi_datatype_t *sdtype, void *rbuf,
+                              int *rcounts, int *rdisps, struct ompi_datatype_t *rdtype, struct ompi_communicator_t *comm,
+                              mca_coll_base_module_t *module)
+{
+    mca_coll_mi355x_module_t *m = MOD(module);
+    const int n = mi355x_comm_size_of(comm), inplace = (sbuf == MPI_IN_PLACE);
+    size_t sc_b[64], sd_b[64], rc_b[64], rd_b[64];
+    if (n > 64 || !is_dev(rbuf) || !dense(rdtype) || !to_bytes(n, rcounts, rdtype->super.size, rc_b) ||
+        !to_bytes(n, rdisps, rdtype->super.size, rd_b) ||
+        (!inplace && (!is_dev(sbuf) || !dense(sdtype) || !to_bytes(n, scounts, sdtype->super.size, sc_b) ||
+                      !to_bytes(n, sdisps, sdtype->super.size, sd_b))))
+        return m->prev_alltoallv(sbuf, scounts, sdisps, sdtype, rbuf, rcounts, rdisps, rdtype, comm,
+                                 m->prev_alltoallv_module);
+    return map_rc(mi355x_alltoallv(m->engine, inplace ? NULL : sbuf, inplace ? NULL : sc_b, inplace ? NULL : sd_b,
+                                   rbuf, rc_b, rd_b, NULL));
+}
+
+static int scan_common(mca_coll_mi355x_module_t *m, int exclusive, void *sbuf, void *rbuf, int count,
+                       struct ompi_datatype_t *dtype, struct ompi_op_t *op, struct ompi_communicator_t *comm)
+{
+    const int inplace = (sbuf == MPI_IN_PLACE);
+    const int t = reducible_type(dtype);
+    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 ||
+        count < 0 || !mi355x_op_supported(op->o_f_to_c_index, t))
+        return exclusive ? m->prev_exscan(sbuf, rbuf, count, dtype, op, comm, m->prev_exscan_module)
+                         : m->prev_scan(sbuf, rbuf, count, dtype, op, comm, m->prev_scan_module);
+    return map_rc((exclusive ? mi355x_exscan : mi355x_scan)(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)count, t,
+                                                            op->o_f_to_c_index, NULL));
+}
+
+int mca_coll_mi355x_scan(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                         struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
+{
+    return scan_common(MOD(module), 0, sbuf, rbuf, count, dtype, op, comm);
+}
+
+int mca_coll_mi355x_exscan(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                           struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
+{
+    return scan_common(MOD(module), 1, sbuf, rbuf, count, dtype, op, comm);
+}
+
 /* ------------------------------------------------------------------ nonblocking collectives
  * The engine runs a posted collective on the communicator's progress thread (mi355x_i*); the
  * component hands MPI an ompi_request_t subclass -- as coll/libnbc does
@@ -554,6 +729,15 @@ static int module_enable(mca_coll_base_module_t *module, struct ompi_communicato
     SNAP(allgather);
     SNAP(bcast);
     SNAP(reduce);
+    SNAP(gather);
+    SNAP(gatherv);
+    SNAP(scatter);
+    SNAP(scatterv);
+    SNAP(allgatherv);
+    SNAP(alltoall);
+    SNAP(alltoallv);
+    SNAP(scan);
+    SNAP(exscan);
     SNAP_OPT(iallreduce);
     SNAP_OPT(ireduce);
     SNAP_OPT(ireduce_scatter_block);
@@ -616,6 +800,15 @@ static mca_coll_base_module_t *component_comm_query(struct ompi_communicator_t *
     m->super.coll_allgather = mca_coll_mi355x_allgather;
     m->super.coll_bcast = mca_coll_mi355x_bcast;
     m->super.coll_reduce = mca_coll_mi355x_reduce;
+    m->super.coll_gather = mca_coll_mi355x_gather;
+    m->super.coll_gatherv = mca_coll_mi355x_gatherv;
+    m->super.coll_scatter = mca_coll_mi355x_scatter;
+    m->super.coll_scatterv = mca_coll_mi355x_scatterv;
+    m->super.coll_allgatherv = mca_coll_mi355x_allgatherv;
+    m->super.coll_alltoall = mca_coll_mi355x_alltoall;
+    m->super.coll_alltoallv = mca_coll_mi355x_alltoallv;
+    m->super.coll_scan = mca_coll_mi355x_scan;
+    m->super.coll_exscan = mca_coll_mi355x_exscan;
     m->super.coll_iallreduce = mca_coll_mi355x_iallreduce;
     m->super.coll_ireduce = mca_coll_mi355x_ireduce;
     m->super.coll_ireduce_scatter_block = mca_coll_mi355x_ireduce_scatter_block;

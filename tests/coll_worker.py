@@ -122,6 +122,88 @@ def nonblocking(m, comm, oracle, rank, size, torch, ptrs):
     m.lib.mini_op_destroy(op)
 
 
+def movement(m, comm, oracle, rank, size, torch, ptrs):
+    """the callers' slots: gather(v) / scatter(v) / allgatherv / alltoall(v) on MPI_INT, scan / exscan
+    on MPI_FLOAT SUM (oracle: coll/basic's chain), host buffers to the stub"""
+    L, pkg = m.lib, m.pkg
+    idt = m.dtype_for_slot(pkg.T["INT32"])
+    fdt = m.dtype_for_slot(pkg.T["FLOAT"])
+    IA = lambda v: (ctypes.c_int * len(v))(*v)
+    n = 1000
+    mine = torch.arange(n, dtype=torch.int32, device="cuda") + 10000 * rank
+    allv = torch.cat([torch.arange(n, dtype=torch.int32) + 10000 * q for q in range(size)])
+    root = size - 1
+    out = torch.zeros(n * size, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    assert L.mini_gather(comm, mine.data_ptr(), n, idt, out.data_ptr() if rank == root else None, n, idt, root) == 0
+    if rank == root:
+        assert torch.equal(out.cpu(), allv), "component gather"
+    back = torch.zeros(n, dtype=torch.int32, device="cuda")
+    assert L.mini_scatter(comm, out.data_ptr() if rank == root else None, n, idt, back.data_ptr(), n, idt, root) == 0
+    assert torch.equal(back, mine), "component scatter"
+    # ragged v-variants: rank q contributes q + 1 ints
+    cnt = [q + 1 for q in range(size)]
+    dsp = [int(sum(cnt[:q])) + 2 * q for q in range(size)]
+    tot = dsp[-1] + cnt[-1]
+    part = torch.full((cnt[rank],), rank + 1, dtype=torch.int32, device="cuda")
+    gv = torch.zeros(tot, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    assert L.mini_allgatherv(comm, part.data_ptr(), cnt[rank], idt, gv.data_ptr(), IA(cnt), IA(dsp), idt) == 0
+    want = torch.zeros(tot, dtype=torch.int32)
+    for q in range(size):
+        want[dsp[q]:dsp[q] + cnt[q]] = q + 1
+    assert torch.equal(gv.cpu(), want), "component allgatherv"
+    gz = torch.zeros(tot, dtype=torch.int32, device="cuda")
+    assert L.mini_gatherv(comm, part.data_ptr(), cnt[rank], idt, gz.data_ptr() if rank == 0 else None, IA(cnt),
+                          IA(dsp), idt, 0) == 0
+    if rank == 0:
+        assert torch.equal(gz.cpu(), want), "component gatherv"
+    sv = torch.zeros(cnt[rank], dtype=torch.int32, device="cuda")
+    assert L.mini_scatterv(comm, gv.data_ptr() if rank == 0 else None, IA(cnt), IA(dsp), idt, sv.data_ptr(),
+                           cnt[rank], idt, 0) == 0
+    assert bool((sv == rank + 1).all()), "component scatterv"
+    # alltoall: block for q = 100 * rank + q
+    a2 = torch.cat([torch.full((7,), 100 * rank + q, dtype=torch.int32) for q in range(size)]).cuda()
+    a2o = torch.zeros_like(a2)
+    torch.cuda.synchronize()
+    assert L.mini_alltoall(comm, a2.data_ptr(), 7, idt, a2o.data_ptr(), 7, idt) == 0
+    assert torch.equal(a2o.cpu(), torch.cat([torch.full((7,), 100 * q + rank, dtype=torch.int32) for q in range(size)]))
+    # alltoallv: rank -> q sends (rank + q) % 3 + 1 ints of value 1000 * rank + q
+    sc = [(rank + q) % 3 + 1 for q in range(size)]
+    sd = [int(sum(sc[:q])) for q in range(size)]
+    rc = [(q + rank) % 3 + 1 for q in range(size)]
+    rd = [int(sum(rc[:q])) + q for q in range(size)]
+    sv2 = torch.cat([torch.full((sc[q],), 1000 * rank + q, dtype=torch.int32) for q in range(size)]).cuda()
+    rv2 = torch.full((rd[-1] + rc[-1],), -1, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    assert L.mini_alltoallv(comm, sv2.data_ptr(), IA(sc), IA(sd), idt, rv2.data_ptr(), IA(rc), IA(rd), idt) == 0
+    got = rv2.cpu()
+    for q in range(size):
+        assert bool((got[rd[q]:rd[q] + rc[q]] == 1000 * q + rank).all()), "component alltoallv"
+    # scan / exscan, MPI_FLOAT SUM: bit-exact with coll/basic's chain
+    op = m.select_op(pkg.OP["SUM"])
+    count = 3001
+    xs = [opdata.make("FLOAT", count, 700 + q) for q in range(size)]
+    for exclusive in (0, 1):
+        want = [np.zeros_like(xs[0]) for _ in range(size)]
+        oracle.oracle_scan(exclusive, size, count, pkg.T["FLOAT"], pkg.OP["SUM"], ptrs(xs), ptrs(want))
+        dx = torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda()
+        dr = torch.zeros_like(dx)
+        torch.cuda.synchronize()
+        fn = L.mini_exscan if exclusive else L.mini_scan
+        assert fn(comm, dx.data_ptr(), dr.data_ptr(), count, fdt, op) == 0
+        if not (exclusive and rank == 0):
+            opdata.assert_same("FLOAT", "SUM", dr.cpu().numpy().view(np.float32), want[rank], "component scan")
+    # host buffers -> the stub
+    h = np.zeros(64, dtype=np.int32)
+    before = L.mini_stub_calls(7)
+    assert L.mini_gather(comm, h.ctypes.data, 4, idt, h.ctypes.data, 4, idt, 0) == L.mini_stub_marker()
+    assert L.mini_stub_calls(7) == before + 1
+    assert L.mini_scan(comm, h.ctypes.data, h.ctypes.data, 4, fdt, op) == L.mini_stub_marker()
+    assert L.mini_alltoall(comm, h.ctypes.data, 4, idt, h.ctypes.data, 4, idt) == L.mini_stub_marker()
+    m.lib.mini_op_destroy(op)
+
+
 def main():
     rank, size = int(sys.argv[1]), int(sys.argv[2])
     import torch
@@ -192,6 +274,7 @@ def main():
     # derived datatypes through the GPU convertor: bcast of a vector type ...
     derived_bcast(m, comm, oracle, rank, size, torch)
     derived_allgather(m, comm, oracle, rank, size, torch)
+    movement(m, comm, oracle, rank, size, torch, ptrs)
     # host buffers -> the lower-priority (stub) module
     h = np.zeros(16, dtype=np.float32)
     op = m.select_op(pkg.OP["SUM"])

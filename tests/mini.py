@@ -59,6 +59,16 @@ class Mini:
         L.mini_reduce_scatter.argtypes = [vp, vp, vp, ctypes.POINTER(i), vp, vp]
         L.mini_allgather.argtypes = [vp, vp, i, vp, vp, i, vp]
         L.mini_bcast.argtypes = [vp, vp, i, vp, i]
+        IP = ctypes.POINTER(i)
+        L.mini_gather.argtypes = [vp, vp, i, vp, vp, i, vp, i]
+        L.mini_scatter.argtypes = [vp, vp, i, vp, vp, i, vp, i]
+        L.mini_gatherv.argtypes = [vp, vp, i, vp, vp, IP, IP, vp, i]
+        L.mini_scatterv.argtypes = [vp, vp, IP, IP, vp, vp, i, vp, i]
+        L.mini_allgatherv.argtypes = [vp, vp, i, vp, vp, IP, IP, vp]
+        L.mini_alltoall.argtypes = [vp, vp, i, vp, vp, i, vp]
+        L.mini_alltoallv.argtypes = [vp, vp, IP, IP, vp, vp, IP, IP, vp]
+        L.mini_scan.argtypes = [vp, vp, vp, i, vp, vp]
+        L.mini_exscan.argtypes = [vp, vp, vp, i, vp, vp]
         L.mini_comm_fn.restype = vp
         L.mini_comm_fn.argtypes = [vp, i]
         L.mini_stub_module.restype = vp

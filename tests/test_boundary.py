@@ -52,7 +52,10 @@ def test_component_symbols(pkg):
     for s in ("mca_coll_mi355x_component", "mca_coll_mi355x_allreduce", "mca_coll_mi355x_reduce_scatter_block",
               "mca_coll_mi355x_reduce_scatter", "mca_coll_mi355x_allgather", "mca_coll_mi355x_bcast",
               "mca_coll_mi355x_reduce", "mca_coll_mi355x_iallreduce", "mca_coll_mi355x_ireduce",
-              "mca_coll_mi355x_ireduce_scatter_block", "mca_coll_mi355x_iallgather", "mca_coll_mi355x_ibcast"):
+              "mca_coll_mi355x_ireduce_scatter_block", "mca_coll_mi355x_iallgather", "mca_coll_mi355x_ibcast",
+              "mca_coll_mi355x_gather", "mca_coll_mi355x_gatherv", "mca_coll_mi355x_scatter",
+              "mca_coll_mi355x_scatterv", "mca_coll_mi355x_allgatherv", "mca_coll_mi355x_alltoall",
+              "mca_coll_mi355x_alltoallv", "mca_coll_mi355x_scan", "mca_coll_mi355x_exscan"):
         assert s in coll
 
 
@@ -96,6 +99,9 @@ def test_abi_offsets():
         20: 104,                     # req_free
         21: 19 * 16,                 # comm coll table: iallreduce pair after 17 blocking + 2
         22: 8 * 32,                  # ompi_predefined_request_t padded to 32 pointers
+        23: 16 + 8 + 14 * 8,         # coll module: scan = 15th blocking fn (coll.h:390-409)
+        24: 16 * 16,                 # comm coll table: scatterv pair = 17th (coll.h:469-504)
+        25: 9 * 16,                  # comm coll table: gather pair = 10th
     }
     for k, v in want.items():
         assert L.mini_offsetof(k) == v, (k, L.mini_offsetof(k), v)
