@@ -139,6 +139,40 @@ def extra_legs(args, pkg, torch, comm, world, rank, dev, legs):
     del buf, packed, red
     d.destroy()
     torch.cuda.empty_cache()
+    # the callers either side of the path: MPI_Alltoall of 1 GiB per rank (pairwise blocks of
+    # 1 GiB / n, each rank pulls n-1 blocks over n-1 links at once), and device point-to-point
+    # (MPI_Sendrecv ring of 256 MiB: each rank pulls its predecessor's buffer)
+    _log(rank, "leg alltoall_1GiB")
+    try:
+        blk = (1 << 30) // world
+        a_s = torch.empty((blk * world,), dtype=torch.uint8, device=dev)
+        for q in range(world):
+            a_s[q * blk:(q + 1) * blk].fill_((rank * 16 + q) & 0xFF)
+        a_r = torch.empty_like(a_s)
+        torch.cuda.synchronize()
+        t_a = _timed(dist, torch, lambda: comm.alltoall(a_s.data_ptr(), a_r.data_ptr(), blk), 3)
+        ok_a = all(int(a_r[q * blk]) == ((q * 16 + rank) & 0xFF) and int(a_r[(q + 1) * blk - 1]) == ((q * 16 + rank) & 0xFF)
+                   for q in range(world))
+        legs["alltoall_1GiB"] = {"ms": round(t_a * 1e3, 3),
+                                 "busbw_GBs": round(blk * world / t_a * (world - 1) / world / 1e9, 2), "exact": ok_a}
+        del a_s, a_r
+    except Exception as e:
+        legs["alltoall_1GiB"] = {"error": repr(e)[:300]}
+    _log(rank, "leg sendrecv_256MiB")
+    try:
+        nb = 256 << 20
+        p_s = torch.full((nb,), rank + 1, dtype=torch.uint8, device=dev)
+        p_r = torch.zeros_like(p_s)
+        torch.cuda.synchronize()
+        nxt, prv = (rank + 1) % world, (rank - 1) % world
+        t_p = _timed(dist, torch, lambda: comm.sendrecv(p_s.data_ptr(), nb, nxt, 0, p_r.data_ptr(), nb, prv, 0), 3)
+        ok_p = int(p_r.min()) == prv + 1 and int(p_r.max()) == prv + 1
+        legs["sendrecv_ring_256MiB"] = {"ms": round(t_p * 1e3, 3), "GBs_per_rank": round(nb / t_p / 1e9, 2),
+                                        "exact": ok_p}
+        del p_s, p_r
+    except Exception as e:
+        legs["sendrecv_ring_256MiB"] = {"error": repr(e)[:300]}
+    torch.cuda.empty_cache()
     # xGMI link bandwidth (the busbw denominator, BASELINE.md §2: "must be measured"): ranks 0 and
     # 1 alone, each pulling 256 MiB from the other over their one link (both directions at once)
     if torch.cuda.device_count() >= world:
