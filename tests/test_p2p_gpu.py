@@ -243,3 +243,59 @@ def test_errors(gpu, pkg, comms):
     host = np.zeros(16, dtype=np.uint8)
     with pytest.raises(pkg.MI355XError, match="device memory"):
         comms[0].isend(host.ctypes.data, 16, 1, 0)
+
+
+def _ob1_match_model(arrived, recvs):
+    """ob1's matching restated (pml_ob1_recvfrag.c: posted receives in posting order, each takes the
+    first message in arrival order whose source and tag match; wildcards -1).  `arrived` is the
+    arrival order; for messages already queued this engine drains sources in rank order (MPI
+    leaves the interleaving of sources unspecified, per-source order is what it guarantees)."""
+    pending = list(arrived)
+    out = []
+    for src, tag in recvs:
+        for i, (s, t, ident) in enumerate(pending):
+            if (src == -1 or src == s) and (tag == -1 or tag == t):
+                out.append(pending.pop(i))
+                break
+        else:
+            out.append(None)
+    return out
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_matching_random(gpu, pkg, comms, seed):
+    """random tags / sources / wildcards vs the ob1 matching model, payload ids checked"""
+    torch = gpu
+    g = np.random.default_rng(seed)
+    n = len(comms)
+    msgs = {s: [] for s in range(1, n)}
+    ident = 0
+    for _ in range(80):
+        s = int(g.integers(1, n))
+        if len(msgs[s]) >= 30:          # stay inside one envelope ring per pair
+            continue
+        msgs[s].append((s, int(g.integers(0, 4)), ident))
+        ident += 1
+    payload = {m[2]: torch.full((2,), m[2], dtype=torch.int32, device="cuda") for s in msgs for m in msgs[s]}
+    sends = [comms[s].isend(payload[m[2]].data_ptr(), 8, 0, m[1]) for s in msgs for m in msgs[s]]
+    comms[0].progress()                 # every envelope drained: arrival order is source-major
+    arrived = [m for s in range(1, n) for m in msgs[s]]
+    model_pending = list(arrived)
+    recvs = []
+    for _ in range(len(arrived)):
+        src = -1 if g.random() < 0.4 else int(g.integers(1, n))
+        tag = -1 if g.random() < 0.4 else int(g.integers(0, 4))
+        if _ob1_match_model(model_pending, [(src, tag)])[0] is None:
+            src, tag = -1, -1
+        hit = _ob1_match_model(model_pending, [(src, tag)])[0]
+        model_pending.remove(hit)
+        recvs.append((src, tag))
+    want = _ob1_match_model(arrived, recvs)
+    bufs = [torch.zeros(2, dtype=torch.int32, device="cuda") for _ in recvs]
+    reqs = [comms[0].irecv(b.data_ptr(), 8, s, t) for b, (s, t) in zip(bufs, recvs)]
+    sts = [r.wait() for r in reqs]
+    for r in sends:
+        r.wait()
+    for st, b, w in zip(sts, bufs, want):
+        assert st[:2] == (w[0], w[1]), (st, w)
+        assert int(b[0]) == w[2], (int(b[0]), w)
