@@ -299,3 +299,39 @@ def test_matching_random(gpu, pkg, comms, seed):
     for st, b, w in zip(sts, bufs, want):
         assert st[:2] == (w[0], w[1]), (st, w)
         assert int(b[0]) == w[2], (int(b[0]), w)
+
+
+def test_p2p_beside_nonblocking_collective(gpu, pkg, comms):
+    """point-to-point on the caller's thread while a posted iallreduce runs on the progress thread
+    (both use the communicator's registration cache)"""
+    torch = gpu
+    n = len(comms)
+    count = 1 << 20
+    xs = [torch.full((count,), float(r + 1), device="cuda") for r in range(n)]
+    ys = [torch.empty_like(x) for x in xs]
+    src = [_bytes(torch, 1 << 20, 80 + r) for r in range(n)]
+    dst = [torch.zeros(1 << 20, dtype=torch.uint8, device="cuda") for _ in range(n)]
+    torch.cuda.synchronize()
+    errs = []
+
+    def run(r):
+        try:
+            torch.cuda.set_device(0)
+            q = comms[r].iallreduce(xs[r].data_ptr(), ys[r].data_ptr(), count, pkg.T["FLOAT"], pkg.OP["SUM"])
+            for _ in range(3):
+                comms[r].sendrecv(src[r].data_ptr(), 1 << 20, (r + 1) % n, 9, dst[r].data_ptr(), 1 << 20,
+                                  (r - 1) % n, 9)
+            q.wait()
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    assert not errs, errs
+    want = float(n * (n + 1) // 2)
+    for r in range(n):
+        assert bool(torch.all(ys[r] == want))
+        assert torch.equal(dst[r], src[(r - 1) % n])
