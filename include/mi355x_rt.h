@@ -119,11 +119,16 @@ enum mi355x_knob {
                                            (default 2^31: hipIpcOpenMemHandle hangs from 2 GiB) */
     MI355X_KNOB_STAGE_BYTES = 8,        /* size of the per-communicator staging buffer (default 1 GiB) */
     MI355X_KNOB_REDUCE_CHAIN_FANOUT = 10, /* coll_tuned_reduce_algorithm_chain_fanout (default 4) */
-    MI355X_KNOB_LL_MAX_BYTES = 9        /* per-rank message bytes up to which allreduce / allgather /
+    MI355X_KNOB_LL_MAX_BYTES = 9,       /* per-rank message bytes up to which allreduce / allgather /
                                            bcast take the one-shot low-latency path (0 = never;
                                            default 64 KiB; multi-process communicators only) */
+    MI355X_KNOB_TIME_PHASES = 11        /* 1: time the two kernels of the direct allreduce with HIP
+                                           events on the call's stream (mi355x_comm_phase_ms) */
 };
 int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
+/* device time of the last timed direct allreduce: phase 1 (k_fold, the owner's block from every
+ * rank) and phase 2 (k_multicopy, the other blocks from their owners); -1 when not measured */
+int mi355x_comm_phase_ms(const mi355x_comm_t *comm, float *phase1_ms, float *phase2_ms);
 
 /* coll/tuned's dynamic rules file (coll_tuned_dynamic_file.c:56-251; MCA
  * coll_tuned_dynamic_rules_filename with coll_tuned_use_dynamic_rules).  Collective ids are

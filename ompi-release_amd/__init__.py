@@ -125,6 +125,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "mi355x_comm_barrier": (i, [vp]),
         "mi355x_comm_last_algorithm": (i, [vp]),
         "mi355x_comm_set": (i, [vp, i, c.c_long]),
+        "mi355x_comm_phase_ms": (i, [vp, c.POINTER(c.c_float), c.POINTER(c.c_float)]),
         "mi355x_allreduce": (i, [vp, vp, vp, sz, i, i, vp]),
         "mi355x_reduce_scatter_block": (i, [vp, vp, vp, sz, i, i, vp]),
         "mi355x_reduce": (i, [vp, vp, vp, sz, i, i, i, vp]),
@@ -232,7 +233,7 @@ def get_tune() -> tuple[int, int, int]:
 # ---------------------------------------------------------------- coll/mi355x engine
 KNOB = {"ALLREDUCE_ALG": 1, "REDUCE_ALG": 2, "REDUCE_SCATTER_ALG": 3, "BLOCKS_PER_CU": 4, "TIMEOUT_S": 5,
         "PUSH": 6, "IPC_MAX_BYTES": 7, "STAGE_BYTES": 8,
-        "LL_MAX_BYTES": 9, "REDUCE_CHAIN_FANOUT": 10}
+        "LL_MAX_BYTES": 9, "REDUCE_CHAIN_FANOUT": 10, "TIME_PHASES": 11}
 # coll/tuned COLLTYPE ids (coll_tuned.h:41-58)
 COLL = {"ALLGATHER": 0, "ALLREDUCE": 2, "BCAST": 7, "REDUCE": 11, "REDUCESCATTER": 12}
 AR_ALG = {"DECISION": 0, "LINEAR": 1, "NONOVERLAPPING": 2, "RECURSIVE_DOUBLING": 3, "RING": 4,
@@ -276,6 +277,12 @@ class Comm:
 
     def last_algorithm(self) -> int:
         return rt().mi355x_comm_last_algorithm(self.h)
+
+    def phase_ms(self) -> tuple[float, float]:
+        """device ms of the last timed direct allreduce's two kernels (knob TIME_PHASES)"""
+        a, b = ctypes.c_float(), ctypes.c_float()
+        check(rt().mi355x_comm_phase_ms(self.h, ctypes.byref(a), ctypes.byref(b)), "mi355x_comm_phase_ms")
+        return a.value, b.value
 
     def set(self, knob: str, value: int) -> None:
         check(rt().mi355x_comm_set(self.h, KNOB[knob], value), "mi355x_comm_set")

@@ -1041,6 +1041,8 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
     }
     (void)hipSetDevice(c->device);
     p2p_destroy(c);
+    for (hipEvent_t e : c->tev)
+        if (e) (void)hipEventDestroy(e);
     if (c->nb_stream) (void)hipStreamDestroy(c->nb_stream);
     for (auto &kv : c->peer_maps) close_map(kv.second);
     for (LocalReg &r : c->local_regs) drop_reg(r);
@@ -1076,6 +1078,13 @@ int mi355x_comm_barrier(mi355x_comm_t *c)
     return barrier(c);
 }
 int mi355x_comm_last_algorithm(const mi355x_comm_t *c) { return c ? c->last_alg : -1; }
+int mi355x_comm_phase_ms(const mi355x_comm_t *c, float *phase1_ms, float *phase2_ms)
+{
+    if (!c || !phase1_ms || !phase2_ms) return set_error(MI355X_ERR_ARG, "NULL argument");
+    *phase1_ms = c->phase_ms[0];
+    *phase2_ms = c->phase_ms[1];
+    return MI355X_SUCCESS;
+}
 
 int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
 {
@@ -1097,6 +1106,13 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
     case MI355X_KNOB_REDUCE_CHAIN_FANOUT:
         if (value < 1 || value > 32) return set_error(MI355X_ERR_ARG, "chain fan-out out of range");
         c->chain_fanout = (int)value;
+        break;
+    case MI355X_KNOB_TIME_PHASES:
+        c->time_phases = value != 0;
+        if (c->time_phases && !c->tev[0]) {
+            MI_HIP(hipSetDevice(c->device));
+            for (hipEvent_t &e : c->tev) MI_HIP(hipEventCreate(&e));
+        }
         break;
     case MI355X_KNOB_LL_MAX_BYTES:
         if (value < 0 || value > (64l << 20)) return set_error(MI355X_ERR_ARG, "ll_max_bytes out of range");
@@ -1250,11 +1266,15 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
         return finish(c, s);
     }
     // phase 1: reduce own block locally; phase 2: pull every other block from its owner
+    const bool tp = c->time_phases && c->tev[0];
+    if (tp) MI_HIP(hipEventRecord(c->tev[0], s));
     std::vector<void *> dst(1, rbuf);
     rc = run_program(op, type, pr, P[0], dst, off, len, s);
     if (rc) return rc;
+    if (tp) MI_HIP(hipEventRecord(c->tev[1], s));
     rc = finish(c, s);
     if (rc) return rc;
+    if (tp) MI_HIP(hipEventRecord(c->tev[2], s));
     MultiCopyArgs m;
     std::memset(&m, 0, sizeof(m));
     for (int q = 0; q < c->size; ++q) {
@@ -1268,7 +1288,13 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
     }
     rc = launch_multicopy(m, s);
     if (rc) return rc;
-    return finish(c, s);
+    if (tp) MI_HIP(hipEventRecord(c->tev[3], s));
+    rc = finish(c, s);
+    if (rc == MI355X_SUCCESS && tp) {
+        MI_HIP(hipEventElapsedTime(&c->phase_ms[0], c->tev[0], c->tev[1]));
+        MI_HIP(hipEventElapsedTime(&c->phase_ms[1], c->tev[2], c->tev[3]));
+    }
+    return rc;
 }
 
 // MPI_Reduce to `root` (ompi_coll_tuned_reduce_intra_dec_fixed, coll_tuned_decision_fixed.c:343-446,

@@ -219,6 +219,9 @@ struct mi355x_comm {
     const mi355x_rules_t *rules = nullptr;        // coll/tuned dynamic rules (not owned)
     int last_alg = -1;
     double timeout_s = 600.0;
+    bool time_phases = false;                     // MI355X_KNOB_TIME_PHASES
+    hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
+    float phase_ms[2] = {-1.f, -1.f};
     mi355x::P2P *p2p = nullptr;                   // created on first point-to-point call
     std::recursive_mutex reg_mtx;                 // registration cache: collectives (progress
                                                   // thread) and point-to-point (caller) share it
