@@ -547,3 +547,22 @@ def test_dynamic_rules(gpu, pkg, oracle, comms, tmp_path):
         for c in cs:
             c.set_rules(None)
         rules.destroy()
+
+
+def test_phase_timing(gpu, pkg, comms):
+    """MI355X_KNOB_TIME_PHASES: both kernels of the direct allreduce timed with HIP events"""
+    torch = gpu
+    cs = comms(2)
+    count = 1 << 22
+    xs = [torch.full((count,), float(r + 1), device="cuda") for r in range(2)]
+    ys = [torch.empty_like(x) for x in xs]
+    for c in cs:
+        c.set("TIME_PHASES", 1)
+    torch.cuda.synchronize()
+    run_ranks(2, lambda r: (torch.cuda.set_device(0),
+                            cs[r].allreduce(xs[r].data_ptr(), ys[r].data_ptr(), count, pkg.T["FLOAT"], pkg.OP["SUM"])))
+    for r, c in enumerate(cs):
+        p1, p2 = c.phase_ms()
+        c.set("TIME_PHASES", 0)
+        assert 0.0 < p1 < 1000.0 and 0.0 < p2 < 1000.0, (p1, p2)
+        assert bool(torch.all(ys[r] == 3.0))
