@@ -261,7 +261,7 @@ def run(args, pkg, torch):
     # pull only: the push flow writes into peers' memory behind their L2 (coarse-grained memory is
     # not probed), which is safe on one device but not across xGMI -- it is not a valid candidate
     for push in (0,):
-        for bpc in (2, 4, 8):
+        for bpc in (2, 8, 64, 1024):   # persistent grids ... one-shot (every thread one pass)
             _log(rank, f"autotune push={push} blocks_per_cu={bpc}")
             comm.set("PUSH", push)
             comm.set("BLOCKS_PER_CU", bpc)

@@ -109,7 +109,7 @@ enum mi355x_knob {
     MI355X_KNOB_ALLREDUCE_ALG = 1,      /* coll_tuned_allreduce_algorithm (0 = decision) */
     MI355X_KNOB_REDUCE_ALG = 2,         /* coll_tuned_reduce_algorithm, used by reduce_scatter_block */
     MI355X_KNOB_REDUCE_SCATTER_ALG = 3, /* coll_tuned_reduce_scatter_algorithm */
-    MI355X_KNOB_BLOCKS_PER_CU = 4,
+    MI355X_KNOB_BLOCKS_PER_CU = 4,      /* grid cap of the coll kernels, 1..1024 (default 1024 = one-shot) */
     MI355X_KNOB_TIMEOUT_S = 5,
     MI355X_KNOB_PUSH = 6,               /* 1: one-phase push data flow (owners write peers' buffers);
                                            single-device use only: across xGMI the remote writes land

@@ -1094,7 +1094,8 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
     case MI355X_KNOB_REDUCE_ALG: c->knob_reduce = (int)value; break;
     case MI355X_KNOB_REDUCE_SCATTER_ALG: c->knob_rs = (int)value; break;
     case MI355X_KNOB_BLOCKS_PER_CU:
-        if (value < 1 || value > 64) return set_error(MI355X_ERR_ARG, "blocks_per_cu out of range");
+        // up to 1024: with that many the streaming kernels' grids are one-shot (every thread one pass)
+        if (value < 1 || value > 1024) return set_error(MI355X_ERR_ARG, "blocks_per_cu out of range");
         coll_tune().blocks_per_cu = (int)value;
         break;
     case MI355X_KNOB_TIMEOUT_S: c->timeout_s = (double)value; break;

@@ -86,7 +86,10 @@ int launch_ll_slot(int op, int type, const LLArgs &a, hipStream_t s);  // LL_AR 
 int launch_ll_copy(const LLArgs &a, hipStream_t s);                   // LL_AG / LL_BC
 
 struct CollTune {
-    int blocks_per_cu = 4;
+    // grid cap of k_fold / k_copy / k_multicopy in blocks per CU; 1024 = one-shot grids (every
+    // thread one pass), measured fastest for 1 GiB allreduce (one-GPU rehearsal: 0.94 ms vs 1.16 ms
+    // at 2 blocks per CU, profiles/r01_bench_n2_rehearsal_1gpu.json); the N > 1 bench re-tunes it
+    int blocks_per_cu = 1024;
     // 1: allreduce owners write into the peers' rbufs (one phase); 0: pull (two phases, default).
     // Push is correct on one device only: across xGMI a remote write lands in HBM behind the
     // owner's L2, which may still hold old lines of the destination (coarse-grained memory is not
