@@ -45,6 +45,25 @@ template <typename V> __device__ __forceinline__ void cstore(void *p, const V &v
     __builtin_memcpy(&raw, &v, 16);
     *reinterpret_cast<u32x4c *>(p) = raw;
 }
+// non-temporal forms: streams larger than the Infinity Cache (same policy as op_kernels.hip)
+template <bool NT, typename V> __device__ __forceinline__ V cload_t(const void *p)
+{
+    if constexpr (!NT) return cload<V>(p);
+    u32x4c raw = __builtin_nontemporal_load(reinterpret_cast<const u32x4c *>(p));
+    V v;
+    __builtin_memcpy(&v, &raw, 16);
+    return v;
+}
+template <bool NT, typename V> __device__ __forceinline__ void cstore_t(void *p, const V &v)
+{
+    if constexpr (!NT) {
+        cstore<V>(p, v);
+    } else {
+        u32x4c raw;
+        __builtin_memcpy(&raw, &v, 16);
+        __builtin_nontemporal_store(raw, reinterpret_cast<u32x4c *>(p));
+    }
+}
 
 // ------------------------------------------------------------------ fold
 template <class F>
@@ -67,7 +86,7 @@ __device__ __forceinline__ typename F::T fold_scalar(const FoldArgs &a, size_t i
     return acc;
 }
 
-template <class F, int U>
+template <class F, int U, bool NT>
 __global__ __launch_bounds__(256) void k_fold(FoldArgs a)
 {
     using T = typename F::T;
@@ -95,7 +114,7 @@ __global__ __launch_bounds__(256) void k_fold(FoldArgs a)
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const size_t v = base + (size_t)u * nthr;
-                        if (v < nvec) x[j][u] = cload<V>(p + v * 16);
+                        if (v < nvec) x[j][u] = cload_t<NT, V>(p + v * 16);
                     }
                 }
             }
@@ -122,7 +141,7 @@ __global__ __launch_bounds__(256) void k_fold(FoldArgs a)
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const size_t v = base + (size_t)u * nthr;
-                        if (v < nvec) x[j][u] = cload<V>(p + v * 16);
+                        if (v < nvec) x[j][u] = cload_t<NT, V>(p + v * 16);
                     }
                 }
             }
@@ -142,7 +161,7 @@ __global__ __launch_bounds__(256) void k_fold(FoldArgs a)
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const size_t v = base + (size_t)u * nthr;
-                if (v < nvec) cstore<V>(q + v * 16, acc[u]);
+                if (v < nvec) cstore_t<NT, V>(q + v * 16, acc[u]);
             }
         }
     }
@@ -218,7 +237,7 @@ __global__ __launch_bounds__(256) void k_copy(CopyArgs a)
 }
 
 // ------------------------------------------------------------------ multi-segment copy
-__global__ __launch_bounds__(256) void k_multicopy(MultiCopyArgs a)
+template <bool NT> __global__ __launch_bounds__(256) void k_multicopy(MultiCopyArgs a)
 {
     // find this block's segment (<= 64 segments, uniform per block)
     int sgi = 0;
@@ -244,12 +263,12 @@ __global__ __launch_bounds__(256) void k_multicopy(MultiCopyArgs a)
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const size_t v = base + (size_t)u * nthr;
-            if (v < nvec) x[u] = *reinterpret_cast<const u32x4c *>(s + head + v * 16);
+            if (v < nvec) x[u] = cload_t<NT, u32x4c>(s + head + v * 16);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const size_t v = base + (size_t)u * nthr;
-            if (v < nvec) *reinterpret_cast<u32x4c *>(d + head + v * 16) = x[u];
+            if (v < nvec) cstore_t<NT, u32x4c>(d + head + v * 16, x[u]);
         }
     }
     for (size_t i = head + nvec * 16 + tid; i < n; i += nthr) d[i] = s[i];
@@ -287,7 +306,10 @@ template <class F> static int launch_fold(FoldArgs a, hipStream_t s)
     const size_t scalar = a.n - a.nvec * EPV;
     if (scalar > work) work = scalar;
     const size_t blocks = grid_for(work, coll_tune().blocks_per_cu);
-    hipLaunchKernelGGL((k_fold<F, U>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    if ((size_t)(a.nr + a.nd) * a.n * sizeof(T) > ((size_t)256 << 20))
+        hipLaunchKernelGGL((k_fold<F, U, true>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_fold<F, U, false>), dim3((unsigned)blocks), dim3(256), 0, s, a);
     MI_HIP(hipGetLastError());
     return MI355X_SUCCESS;
 }
@@ -341,7 +363,10 @@ int launch_multicopy(MultiCopyArgs a, hipStream_t s)
     }
     a.first_block[a.nseg] = next;
     if (next == 0) return MI355X_SUCCESS;
-    hipLaunchKernelGGL(k_multicopy, dim3(next), dim3(256), 0, s, a);
+    if (2 * total > ((size_t)256 << 20))
+        hipLaunchKernelGGL(k_multicopy<true>, dim3(next), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_multicopy<false>, dim3(next), dim3(256), 0, s, a);
     MI_HIP(hipGetLastError());
     return MI355X_SUCCESS;
 }
