@@ -122,8 +122,9 @@ enum mi355x_knob {
     MI355X_KNOB_LL_MAX_BYTES = 9,       /* per-rank message bytes up to which allreduce / allgather /
                                            bcast take the one-shot low-latency path (0 = never;
                                            default 64 KiB; multi-process communicators only) */
-    MI355X_KNOB_TIME_PHASES = 11        /* 1: time the two kernels of the direct allreduce with HIP
+    MI355X_KNOB_TIME_PHASES = 11,       /* 1: time the two kernels of the direct allreduce with HIP
                                            events on the call's stream (mi355x_comm_phase_ms) */
+    MI355X_KNOB_COPY_BLOCK_KIB = 12     /* bytes per block of the pull-copy kernel, KiB (4..256, default 4) */
 };
 int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
 /* device time of the last timed direct allreduce: phase 1 (k_fold, the owner's block from every

@@ -1108,6 +1108,10 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
         if (value < 1 || value > 32) return set_error(MI355X_ERR_ARG, "chain fan-out out of range");
         c->chain_fanout = (int)value;
         break;
+    case MI355X_KNOB_COPY_BLOCK_KIB:
+        if (value < 4 || value > 256) return set_error(MI355X_ERR_ARG, "copy_block_kib out of range");
+        coll_tune().copy_block_kib = (int)value;
+        break;
     case MI355X_KNOB_TIME_PHASES:
         c->time_phases = value != 0;
         if (c->time_phases && !c->tev[0]) {

@@ -90,6 +90,9 @@ struct CollTune {
     // thread one pass), measured fastest for 1 GiB allreduce (one-GPU rehearsal: 0.94 ms vs 1.16 ms
     // at 2 blocks per CU, profiles/r01_bench_n2_rehearsal_1gpu.json); the N > 1 bench re-tunes it
     int blocks_per_cu = 1024;
+    // k_multicopy: KiB per block before the grid cap applies; 4 measured best (tools/ab_copy.py:
+    // 1 GiB pull 0.35 ms vs 0.39 at 16 KiB, 0.41 at 64 KiB, one GPU)
+    int copy_block_kib = 4;
     // 1: allreduce owners write into the peers' rbufs (one phase); 0: pull (two phases, default).
     // Push is correct on one device only: across xGMI a remote write lands in HBM behind the
     // owner's L2, which may still hold old lines of the destination (coarse-grained memory is not

@@ -350,12 +350,14 @@ int launch_multicopy(MultiCopyArgs a, hipStream_t s)
     size_t total = 0;
     for (int i = 0; i < a.nseg; ++i) total += a.len[i];
     if (total == 0) return MI355X_SUCCESS;
-    // about 4 KiB of work per thread-block iteration; at most blocks_per_cu x CUs blocks overall
+    // copy_block_kib per block (default 4 KiB: one 16-B vector per lane); at most
+    // blocks_per_cu x CUs blocks overall (beyond that the blocks loop)
     const size_t cap = (size_t)coll_tune().blocks_per_cu * (size_t)device_cu_count();
     unsigned next = 0;
     for (int i = 0; i < a.nseg; ++i) {
         a.first_block[i] = next;
-        size_t want = (a.len[i] + 4095) / 4096;
+        const size_t cb = (size_t)coll_tune().copy_block_kib << 10;
+        size_t want = (a.len[i] + cb - 1) / cb;
         size_t share = total ? (cap * a.len[i] + total - 1) / total : 1;
         size_t nb = want < share ? want : share;
         if (a.len[i] && nb == 0) nb = 1;
