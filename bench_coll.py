@@ -260,11 +260,12 @@ def run(args, pkg, torch):
     tried = []
     # pull only: the push flow writes into peers' memory behind their L2 (coarse-grained memory is
     # not probed), which is safe on one device but not across xGMI -- it is not a valid candidate
-    for push in (0,):
+    for push, ckib in ((0, 4), (0, 16)):
         for bpc in (2, 8, 64, 1024):   # persistent grids ... one-shot (every thread one pass)
-            _log(rank, f"autotune push={push} blocks_per_cu={bpc}")
+            _log(rank, f"autotune push={push} blocks_per_cu={bpc} copy_block_kib={ckib}")
             comm.set("PUSH", push)
             comm.set("BLOCKS_PER_CU", bpc)
+            comm.set("COPY_BLOCK_KIB", ckib)
             torch.cuda.synchronize()
             comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
             ok = ok and bool(torch.all(y == want).item())
@@ -274,10 +275,12 @@ def run(args, pkg, torch):
                 comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
             dt = torch.tensor([(time.perf_counter() - t0) / 3])
             dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-            tried.append({"push": push, "blocks_per_cu": bpc, "ms": round(float(dt[0]) * 1e3, 4)})
+            tried.append({"push": push, "blocks_per_cu": bpc, "copy_block_kib": ckib,
+                          "ms": round(float(dt[0]) * 1e3, 4)})
     best = min(tried, key=lambda c: c["ms"])
     comm.set("PUSH", best["push"])
     comm.set("BLOCKS_PER_CU", best["blocks_per_cu"])
+    comm.set("COPY_BLOCK_KIB", best["copy_block_kib"])
     # timed data: N(0,1), order-dependent (the engine replicates the segmented-ring order)
     _log(rank, f"timed: {args.steps} steps, best {best}")
     x.normal_()
@@ -336,6 +339,7 @@ def run(args, pkg, torch):
                    "count": n, "algorithm": {3: "recursive_doubling", 4: "ring", 5: "segmented_ring"}.get(alg, alg),
                    "exact_check": "ok" if bad == 0 else "FAILED",
                    "data_flow": "push" if best["push"] else "pull", "blocks_per_cu": best["blocks_per_cu"],
+                   "copy_block_kib": best["copy_block_kib"],
                    "autotune_ms_per_call": tried},
         "roofline": ({"bound": "xgmi", "achieved": round(fold_xgmi, 2), "peak": round(peak_all, 1), "unit": "GB/s",
                       "frac": round(fold_xgmi / peak_all, 4), "traffic": None,
