@@ -127,6 +127,8 @@ enum mi355x_knob {
     MI355X_KNOB_COPY_BLOCK_KIB = 12     /* bytes per block of the pull-copy kernel, KiB (4..256, default 4) */
 };
 int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
+/* current value of a knob (LL_MAX_BYTES reads 0 when the creation-time LL self-test failed) */
+int mi355x_comm_get(const mi355x_comm_t *comm, int knob, long *value);
 /* device time of the last timed direct allreduce: phase 1 (k_fold, the owner's block from every
  * rank) and phase 2 (k_multicopy, the other blocks from their owners); -1 when not measured */
 int mi355x_comm_phase_ms(const mi355x_comm_t *comm, float *phase1_ms, float *phase2_ms);

@@ -126,6 +126,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "mi355x_comm_last_algorithm": (i, [vp]),
         "mi355x_comm_set": (i, [vp, i, c.c_long]),
         "mi355x_comm_phase_ms": (i, [vp, c.POINTER(c.c_float), c.POINTER(c.c_float)]),
+        "mi355x_comm_get": (i, [vp, i, c.POINTER(c.c_long)]),
         "mi355x_allreduce": (i, [vp, vp, vp, sz, i, i, vp]),
         "mi355x_reduce_scatter_block": (i, [vp, vp, vp, sz, i, i, vp]),
         "mi355x_reduce": (i, [vp, vp, vp, sz, i, i, i, vp]),
@@ -284,6 +285,11 @@ class Comm:
         a, b = ctypes.c_float(), ctypes.c_float()
         check(rt().mi355x_comm_phase_ms(self.h, ctypes.byref(a), ctypes.byref(b)), "mi355x_comm_phase_ms")
         return a.value, b.value
+
+    def get(self, knob: str) -> int:
+        v = ctypes.c_long()
+        check(rt().mi355x_comm_get(self.h, KNOB[knob], ctypes.byref(v)), "mi355x_comm_get")
+        return v.value
 
     def set(self, knob: str, value: int) -> None:
         check(rt().mi355x_comm_set(self.h, KNOB[knob], value), "mi355x_comm_set")

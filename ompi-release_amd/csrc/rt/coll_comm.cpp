@@ -760,6 +760,61 @@ static int ll_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s)
     return MI355X_SUCCESS;
 }
 
+static double env_double(const char *name, double dflt);
+
+// Collective, once at communicator creation: the LL region is built and one LL allgather of a
+// rank-tagged 8 KiB pattern per rank runs with a short device-side bound (MI355X_LL_PROBE_S, 5 s).
+// The LL path stays on only if every rank saw every peer's bytes; otherwise small collectives take
+// the host-synchronised path (a flag protocol that misbehaves on some platform would otherwise
+// stall every small call for timeout_s).  MI355X_LL=0 skips it and disables LL.
+static int ll_selftest(mi355x_comm *c)
+{
+    const char *env = getenv("MI355X_LL");
+    if (env && atoi(env) == 0) {
+        c->ll_max = 0;
+        return MI355X_SUCCESS;
+    }
+    int rc = ensure_ll(c);
+    if (rc) return rc;
+    const size_t per = std::min<size_t>(8192, c->ll_slot), n = (size_t)c->size;
+    char *buf = nullptr;
+    bool ok = hipMalloc((void **)&buf, per * (n + 1)) == hipSuccess;
+    if (ok) ok = hipMemset(buf, c->rank + 1, per) == hipSuccess && hipMemset(buf + per, 0, per * n) == hipSuccess &&
+                 hipDeviceSynchronize() == hipSuccess;
+    if (ok) {
+        LLArgs a;
+        std::memset(&a, 0, sizeof(a));
+        a.mode = LL_AG;
+        a.src = buf;
+        a.dst = buf + per;
+        a.nbytes = per;
+        a.push_mask = ~0ull;
+        const double saved = c->timeout_s;
+        c->timeout_s = env_double("MI355X_LL_PROBE_S", 5.0);
+        ok = ll_run(c, a, 0, 0, nullptr) == MI355X_SUCCESS;
+        c->timeout_s = saved;
+    }
+    if (ok) {
+        std::vector<unsigned char> h(per * n);
+        ok = hipMemcpy(h.data(), buf + per, per * n, hipMemcpyDeviceToHost) == hipSuccess;
+        for (size_t q = 0; q < n && ok; ++q)
+            for (size_t i = 0; i < per && ok; i += 509) ok = h[q * per + i] == (unsigned char)(q + 1);
+    }
+    (void)hipGetLastError();
+    if (buf) (void)hipFree(buf);
+    c->ctrl->slot[c->rank].ll_ok = ok ? 1 : 2;
+    rc = barrier(c);
+    if (rc) return rc;
+    bool all = true;
+    for (int q = 0; q < c->size; ++q) all = all && c->ctrl->slot[q].ll_ok == 1;
+    if (!all) {
+        c->ll_max = 0;
+        if (c->rank == 0) fprintf(stderr, "[mi355x] low-latency path self-test failed: small collectives use the host-synchronised path\n");
+    }
+    TRACE(c, "LL self-test: %s", all ? "ok" : "failed -> LL off");
+    return barrier(c);
+}
+
 static void ll_program(LLArgs &a, const Program &pr)
 {
     if (!pr.is_fold) {
@@ -995,9 +1050,9 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     c->ctrl->attached.fetch_add(1);
     int rc = barrier(c);  // everybody mapped the segment: its name can go
     if (rank == 0) shm_unlink(c->shm_name.c_str());
+    if (rc == MI355X_SUCCESS && size > 1 && c->ll_max > 0) rc = ll_selftest(c);
     if (rc) {
-        munmap(m, bytes);
-        delete c;
+        mi355x_comm_destroy(c);
         return rc;
     }
     *out = c;
@@ -1078,6 +1133,27 @@ int mi355x_comm_barrier(mi355x_comm_t *c)
     return barrier(c);
 }
 int mi355x_comm_last_algorithm(const mi355x_comm_t *c) { return c ? c->last_alg : -1; }
+int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
+{
+    if (!c || !value) return set_error(MI355X_ERR_ARG, "NULL argument");
+    switch (knob) {
+    case MI355X_KNOB_ALLREDUCE_ALG: *value = c->knob_allreduce; break;
+    case MI355X_KNOB_REDUCE_ALG: *value = c->knob_reduce; break;
+    case MI355X_KNOB_REDUCE_SCATTER_ALG: *value = c->knob_rs; break;
+    case MI355X_KNOB_BLOCKS_PER_CU: *value = coll_tune().blocks_per_cu; break;
+    case MI355X_KNOB_TIMEOUT_S: *value = (long)c->timeout_s; break;
+    case MI355X_KNOB_PUSH: *value = coll_tune().push; break;
+    case MI355X_KNOB_IPC_MAX_BYTES: *value = (long)c->ipc_max; break;
+    case MI355X_KNOB_STAGE_BYTES: *value = (long)c->stage_bytes; break;
+    case MI355X_KNOB_LL_MAX_BYTES: *value = (long)c->ll_max; break;
+    case MI355X_KNOB_REDUCE_CHAIN_FANOUT: *value = c->chain_fanout; break;
+    case MI355X_KNOB_TIME_PHASES: *value = c->time_phases ? 1 : 0; break;
+    case MI355X_KNOB_COPY_BLOCK_KIB: *value = coll_tune().copy_block_kib; break;
+    default: return set_error(MI355X_ERR_ARG, "unknown knob %d", knob);
+    }
+    return MI355X_SUCCESS;
+}
+
 int mi355x_comm_phase_ms(const mi355x_comm_t *c, float *phase1_ms, float *phase2_ms)
 {
     if (!c || !phase1_ms || !phase2_ms) return set_error(MI355X_ERR_ARG, "NULL argument");

@@ -63,6 +63,7 @@ struct alignas(64) RankSlot {
     int32_t probe_fd, probe_ok;   // dmabuf capability probe
     uint64_t probe_size;
     int64_t varg[2 * kMaxRanks];  // per-peer counts / displacements of v-collectives (bytes)
+    int32_t ll_ok, pad_ll;        // LL self-test result at creation (1 ok, 2 failed)
 };
 
 struct Ctrl {

@@ -60,6 +60,7 @@ def ll_checks(pkg, comm, rank, size, oracle, torch):
     """the one-shot low-latency path (coll_ll.hip): every forced allreduce algorithm against the
     oracle's schedule simulation, in place and not, allgather / bcast, and many back-to-back calls
     (parity reuse of the LL slots)"""
+    assert comm.get("LL_MAX_BYTES") > 0, "the creation-time LL self-test disabled the LL path"
     ptrs = lambda arrs: (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
     comm.set("LL_MAX_BYTES", 256 << 10)
     for alg in (0, 1, 2, 3, 4, 5):
