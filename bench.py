@@ -182,6 +182,8 @@ def main():
         res = bench_op(args, pkg, torch)
         res["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline_op(args.cpu_seconds)
     print(json.dumps(res), flush=True)
+    if res.get("value") is None:  # a failed exactness check or a hung leg: not a valid measurement
+        sys.exit(2)
 
 
 if __name__ == "__main__":

@@ -14,6 +14,7 @@ import os
 import threading
 import sys
 import time
+import uuid
 
 GIB = 1 << 30
 # MI355X Infinity Fabric: 7 links per GPU, 153.6 GB/s per link (spec, both directions)
@@ -42,7 +43,7 @@ def _timed(dist, torch, fn, reps, warm=1):
     return float(t[0])
 
 
-def extra_legs(args, pkg, torch, comm, world, rank, dev, legs):
+def extra_legs(args, pkg, torch, comm, world, rank, dev, legs, key):
     """The other multi-GPU BASELINE configs, measured on the same communicator after the headline
     (not part of `value`): configs[2] size sweep, configs[3] reduce_scatter_block + allgather fp64
     (4 GiB per rank), configs[4] 4 GiB bcast and the vector-datatype bcast / allreduce through the
@@ -180,8 +181,7 @@ def extra_legs(args, pkg, torch, comm, world, rank, dev, legs):
         try:
             nb = 256 << 20
             if rank < 2:
-                pair = pkg.Comm.create(f"{os.environ.get('TORCHELASTIC_RUN_ID', 'x')}_{os.environ.get('MASTER_PORT', '0')}_pair",
-                                       rank, 2, dev.index)
+                pair = pkg.Comm.create(f"{key}_pair", rank, 2, dev.index)
                 pair.set("TIMEOUT_S", 120)
                 src = torch.full((nb,), rank + 1, dtype=torch.uint8, device=dev)
                 dst = torch.empty((2 * nb,), dtype=torch.uint8, device=dev)
@@ -243,7 +243,10 @@ def run(args, pkg, torch):
     if not dist.is_initialized():
         # bounded waits: a failing rank surfaces as an error on the others, not a hang
         dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
-    key = "bench_{}_{}".format(os.environ.get("TORCHELASTIC_RUN_ID", "x"), os.environ.get("MASTER_PORT", "0"))
+    # node-unique rendezvous key: rank 0 picks it, the launcher's process group spreads it
+    key = [f"bench_{os.getpid()}_{uuid.uuid4().hex[:12]}" if rank == 0 else None]
+    dist.broadcast_object_list(key, src=0)
+    key = key[0]
     comm = pkg.Comm.create(key, rank, world, local)
     comm.set("TIMEOUT_S", 120)
 
@@ -371,10 +374,10 @@ def run(args, pkg, torch):
                     legs["error"] = f"legs exceeded {args.legs_timeout:.0f} s; partial results above"
                     res["legs"] = legs
                     print(json.dumps(res), flush=True)
-                os._exit(0)
+                os._exit(3)  # a hung leg is a failed run, whatever the headline said
         threading.Thread(target=watchdog, daemon=True).start()
         try:
-            extra_legs(args, pkg, torch, comm, world, rank, dev, legs)
+            extra_legs(args, pkg, torch, comm, world, rank, dev, legs, key)
         except Exception as e:  # a failing extra leg must not hide the headline line
             legs["error"] = repr(e)[:300]
         done.set()
@@ -384,4 +387,46 @@ def run(args, pkg, torch):
         dist.destroy_process_group()
         return None
     dist.destroy_process_group()
+    if not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_ring(world, args.cpu_seconds)
+    if bad != 0:  # a wrong result is not a measurement
+        res["error"] = "allreduce result differs from the exact sum"
+        res["value"] = None
     return res
+
+
+def cpu_baseline_ring(n, seconds):
+    """BASELINE configs[0] on this host: the reference CPU path (coll/tuned segmented ring, 1 MiB
+    segments, over sm-BTL-style 32 KiB shared-memory fragments; oracle/cpu_ring.c), n ranks as n
+    threads pinned to n distinct host cores, MPI_SUM MPI_FLOAT 16 M elements (64 MiB) per rank --
+    the configs[0] message size, a bounded sample of the same metric.  busbw = S/t * 2(n-1)/n."""
+    import ctypes
+    import pathlib
+    import numpy as np
+    so = pathlib.Path(__file__).resolve().parent / "oracle" / "build" / "liboracle.so"
+    if not so.exists():
+        return None
+    lib = ctypes.CDLL(str(so))
+    vp = ctypes.c_void_p
+    lib.oracle_cpu_allreduce.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
+                                         ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int,
+                                         ctypes.POINTER(ctypes.c_double)]
+    count = 1 << 24
+    xs = [np.full(count, float(r + 1), dtype=np.float32) for r in range(n)]
+    outs = [np.empty(count, dtype=np.float32) for _ in range(n)]
+    P = lambda arrs: (vp * n)(*[a.ctypes.data for a in arrs])
+    cores = sorted(os.sched_getaffinity(0))
+    core0 = cores[0] if len(cores) >= n and cores[n - 1] - cores[0] == n - 1 else -1
+    t = ctypes.c_double()
+    if lib.oracle_cpu_allreduce(n, count, 14, 3, 1 << 20, P(xs), P(outs), 1, core0, ctypes.byref(t)) != 0:
+        return None
+    reps = max(1, min(200, int(seconds / max(t.value, 1e-6))))
+    t0 = time.perf_counter()
+    lib.oracle_cpu_allreduce(n, count, 14, 3, 1 << 20, P(xs), P(outs), reps, core0, ctypes.byref(t))
+    wall = time.perf_counter() - t0
+    S = count * 4
+    exact = all(bool(np.all(o == n * (n + 1) / 2)) for o in outs)
+    return {"value": round(S / t.value * 2 * (n - 1) / n / 1e9, 3), "unit": "GB/s", "cores": n, "kind": "port",
+            "pinned": core0 >= 0, "exact": exact,
+            "sample": f"configs[0] CPU path at np={n}: segmented ring (1 MiB segments, 32 KiB shm fragments), "
+                      f"16 M fp32 (64 MiB) per rank, {reps} calls, {wall:.1f} s; busbw"}

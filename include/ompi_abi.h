@@ -171,6 +171,18 @@ typedef struct ompi_datatype_t {
 /* ompi/op/op.c:98: datatype id -> OMPI_OP_BASE_TYPE_* slot (-1: not reducible) */
 extern int ompi_op_ddt_map[OMPI_DATATYPE_MPI_MAX_PREDEFINED];
 
+/* predefined datatype objects are padded to 512 bytes (ompi/datatype/ompi_datatype.h:103-110);
+ * MPI_BYTE is &ompi_mpi_byte (mpi.h.in:913, OMPI_PREDEFINED_GLOBAL), id OMPI_DATATYPE_MPI_BYTE
+ * = OMPI_DATATYPE_MPI_UINT8_T when char is 1 byte (ompi_datatype_internal.h:122) */
+#define PREDEFINED_DATATYPE_PAD 512
+typedef struct ompi_predefined_datatype_t {
+    ompi_datatype_t dt;
+    char padding[PREDEFINED_DATATYPE_PAD - sizeof(ompi_datatype_t)];
+} ompi_predefined_datatype_t;
+extern ompi_predefined_datatype_t ompi_mpi_byte;
+#define MPI_BYTE (&ompi_mpi_byte.dt)
+#define OMPI_DATATYPE_MPI_BYTE 0x02
+
 /* ------------------------------------------------------------------ op framework */
 struct ompi_op_base_module_1_0_0_t;
 struct ompi_op_t;

@@ -18,9 +18,16 @@
  */
 #include "ompi_mini.h"
 
+#include <fcntl.h>
+#include <sched.h>
+#include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+static void chan_release(ompi_communicator_t *c);
 
 /* ------------------------------------------------------------------ opal objects */
 void opal_class_initialize(opal_class_t *cls)
@@ -94,6 +101,8 @@ static ompi_datatype_t *dt_objs[OMPI_DATATYPE_MPI_MAX_PREDEFINED];
 static opal_class_t ompi_datatype_t_class = {"ompi_datatype_t", &opal_object_t_class, NULL, NULL, 0, 0, NULL,
                                              NULL, sizeof(ompi_datatype_t)};
 
+ompi_predefined_datatype_t ompi_mpi_byte;  /* MPI_BYTE (mpi.h.in:913) */
+
 void mini_init(void)
 {
     static int done = 0;
@@ -117,6 +126,15 @@ void mini_init(void)
         snprintf(d->name, sizeof(d->name), "%s", predefined[k].name);
         dt_objs[predefined[k].id] = d;
     }
+    ompi_datatype_t *b = &ompi_mpi_byte.dt;
+    b->super.super.obj_class = &ompi_datatype_t_class;
+    b->super.super.obj_reference_count = 1;
+    b->super.flags = OPAL_DATATYPE_FLAG_PREDEFINED | OPAL_DATATYPE_FLAG_CONTIGUOUS | OPAL_DATATYPE_FLAG_NO_GAPS;
+    b->super.id = 4; /* OPAL_DATATYPE_UINT1 */
+    b->super.size = 1;
+    b->super.true_ub = b->super.ub = 1;
+    b->id = OMPI_DATATYPE_MPI_BYTE;
+    snprintf(b->name, sizeof(b->name), "MPI_BYTE");
 }
 
 ompi_datatype_t *mini_datatype(int id)
@@ -380,6 +398,7 @@ void mini_comm_destroy(ompi_communicator_t *c)
     REL(scan)
     REL(exscan)
 #undef REL
+    chan_release(c);
     mi355x_obj_release(&c->c_local_group->super);
     free(c);
 }
@@ -568,7 +587,93 @@ void *mini_comm_fn(ompi_communicator_t *c, int which)
     }
 }
 
-/* a stub "lower-priority" module for tests: records which function ran and returns `marker` */
+/* ------------------------------------------------------------------ host channel
+ * What ob1 + the sm BTL give coll/basic and coll/tuned in a real job: a way for the ranks of ONE
+ * communicator to move host bytes.  The harness stands it in with one POSIX shm segment per
+ * communicator, named by the test (each group of a split gets its own, as each group's PML
+ * traffic is its own).  Only bcast of small host buffers is provided: it is what coll/mi355x's
+ * module_enable uses to agree on its rendezvous key. */
+#define MINI_CHAN_MAX 64
+#define MINI_CHAN_BYTES 4096
+struct mini_chan {
+    _Atomic uint64_t gen;                 /* number of the last bcast the root published */
+    _Atomic uint64_t ack[MINI_CHAN_MAX];  /* per rank: last bcast it has copied out */
+    uint64_t len;
+    char data[MINI_CHAN_BYTES];
+};
+static struct { ompi_communicator_t *comm; struct mini_chan *ch; uint64_t calls; char name[128]; } chans[64];
+
+static struct mini_chan *chan_of(ompi_communicator_t *c, uint64_t **calls)
+{
+    for (int i = 0; i < 64; ++i)
+        if (chans[i].comm == c) {
+            if (calls) *calls = &chans[i].calls;
+            return chans[i].ch;
+        }
+    return NULL;
+}
+
+int mini_comm_set_channel(ompi_communicator_t *c, const char *name)
+{
+    int slot = -1;
+    for (int i = 0; i < 64 && slot < 0; ++i)
+        if (!chans[i].comm) slot = i;
+    if (slot < 0 || c->c_local_group->grp_proc_count > MINI_CHAN_MAX) return OMPI_ERR_OUT_OF_RESOURCE;
+    char shm[112];
+    snprintf(shm, sizeof(shm), "/mini_chan_%s", name);
+    /* every rank creates-or-opens; a fresh object is zero-filled by ftruncate */
+    const int fd = shm_open(shm, O_CREAT | O_RDWR, 0600);
+    if (fd < 0) return OMPI_ERROR;
+    if (ftruncate(fd, (off_t)sizeof(struct mini_chan)) != 0) {
+        close(fd);
+        return OMPI_ERROR;
+    }
+    void *m = mmap(NULL, sizeof(struct mini_chan), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) return OMPI_ERROR;
+    chans[slot].comm = c;
+    chans[slot].ch = (struct mini_chan *)m;
+    chans[slot].calls = 0;
+    snprintf(chans[slot].name, sizeof(chans[slot].name), "%s", shm);
+    return OMPI_SUCCESS;
+}
+
+static void chan_release(ompi_communicator_t *c)
+{
+    for (int i = 0; i < 64; ++i)
+        if (chans[i].comm == c) {
+            munmap(chans[i].ch, sizeof(struct mini_chan));
+            if (c->c_my_rank == 0) shm_unlink(chans[i].name);
+            chans[i].comm = NULL;
+        }
+}
+
+/* linear bcast of <= 4 KiB of host memory: the root waits until every rank acknowledged the
+ * previous call, writes, publishes the call number; the others wait for it and copy; every rank
+ * (the root too) acknowledges the call */
+static int chan_bcast(ompi_communicator_t *c, struct mini_chan *ch, uint64_t *calls, void *buf, size_t bytes,
+                      int root)
+{
+    if (bytes > MINI_CHAN_BYTES) return OMPI_ERR_NOT_SUPPORTED;
+    const int n = c->c_local_group->grp_proc_count, me = c->c_my_rank;
+    const uint64_t k = ++*calls;
+    if (me == root) {
+        for (int q = 0; q < n; ++q)
+            while (q != root && atomic_load_explicit(&ch->ack[q], memory_order_acquire) + 1 < k) sched_yield();
+        memcpy(ch->data, buf, bytes);
+        ch->len = bytes;
+        atomic_store_explicit(&ch->gen, k, memory_order_release);
+        atomic_store_explicit(&ch->ack[me], k, memory_order_release);  /* every rank acks every call */
+        return OMPI_SUCCESS;
+    }
+    while (atomic_load_explicit(&ch->gen, memory_order_acquire) < k) sched_yield();
+    memcpy(buf, ch->data, bytes < ch->len ? bytes : ch->len);
+    atomic_store_explicit(&ch->ack[me], k, memory_order_release);
+    return OMPI_SUCCESS;
+}
+
+/* a stub "lower-priority" module for tests: records which function ran and returns `marker`
+ * (bcast on a communicator with a host channel really broadcasts host buffers) */
 static int stub_calls[16];
 static int stub_marker = 77;
 static int st_allreduce(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o,
@@ -585,7 +690,14 @@ static int st_allgather(void *s, int sc, struct ompi_datatype_t *sd, void *r, in
 { (void)s; (void)sc; (void)sd; (void)r; (void)rc; (void)rd; (void)c; (void)m; stub_calls[3]++; return stub_marker; }
 static int st_bcast(void *b, int n, struct ompi_datatype_t *d, int root, struct ompi_communicator_t *c,
                     mca_coll_base_module_t *m)
-{ (void)b; (void)n; (void)d; (void)root; (void)c; (void)m; stub_calls[4]++; return stub_marker; }
+{
+    (void)m;
+    stub_calls[4]++;
+    uint64_t *calls = NULL;
+    struct mini_chan *ch = chan_of(c, &calls);
+    if (!ch || n < 0 || !(d->super.flags & OPAL_DATATYPE_FLAG_NO_GAPS)) return stub_marker;
+    return chan_bcast(c, ch, calls, b, (size_t)n * d->super.size, root);
+}
 static int st_reduce(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o, int root,
                      struct ompi_communicator_t *c, mca_coll_base_module_t *m)
 { (void)s; (void)r; (void)n; (void)d; (void)o; (void)root; (void)c; (void)m; stub_calls[5]++; return stub_marker; }

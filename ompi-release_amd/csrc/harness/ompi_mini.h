@@ -30,6 +30,7 @@ void mini_comm_install(ompi_communicator_t *c, mca_coll_base_module_t *m);
 int mini_coll_select(ompi_communicator_t *c, mca_coll_base_component_t *comp);
 mca_coll_base_module_t *mini_coll_module_new(void);
 void mini_comm_destroy(ompi_communicator_t *c);
+int mini_comm_set_channel(ompi_communicator_t *c, const char *name);  /* host bcast for the stub module */
 int mini_allreduce(ompi_communicator_t *c, void *s, void *r, int n, ompi_datatype_t *d, ompi_op_t *op);
 int mini_reduce_scatter_block(ompi_communicator_t *c, void *s, void *r, int n, ompi_datatype_t *d, ompi_op_t *op);
 int mini_reduce_scatter(ompi_communicator_t *c, void *s, void *r, int *rc, ompi_datatype_t *d, ompi_op_t *op);

@@ -9,6 +9,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
+#include <unistd.h>
 
 #include "../../../../../include/coll_mi355x.h"
 #include "../../../../../include/mi355x_rt.h"
@@ -66,8 +68,8 @@ typedef struct mca_coll_mi355x_module_t {
      * staging buffer (device memory; registered once, re-registered when it grows) */
     struct ddt_slot { uint64_t sig; const void *dt; mi355x_ddt_t *d; } ddt_cache[8];
     int ddt_next;
-    void *scratch;
-    size_t scratch_bytes;
+    void *scratch[2];          /* send-side and receive-side staging (device memory) */
+    size_t scratch_bytes[2];
 } mca_coll_mi355x_module_t;
 
 static void module_construct(opal_object_t *o)
@@ -106,7 +108,8 @@ static void module_destruct(opal_object_t *o)
     release_prev(m->prev_ibcast_module);
     for (int i = 0; i < 8; ++i)
         if (m->ddt_cache[i].d) mi355x_ddt_destroy(m->ddt_cache[i].d);
-    if (m->scratch) mi355x_free(m->scratch);
+    for (int i = 0; i < 2; ++i)
+        if (m->scratch[i]) mi355x_free(m->scratch[i]);
     if (m->engine) mi355x_comm_destroy(m->engine);
 }
 
@@ -193,17 +196,19 @@ static mi355x_ddt_t *ddt_of(struct mca_coll_mi355x_module_t *m, const struct omp
     return d;
 }
 
-static void *scratch(struct mca_coll_mi355x_module_t *m, size_t bytes)
+static void *scratch_slot(struct mca_coll_mi355x_module_t *m, int slot, size_t bytes)
 {
-    if (bytes <= m->scratch_bytes) return m->scratch;
-    if (m->scratch) mi355x_free(m->scratch);
-    m->scratch = NULL;
-    m->scratch_bytes = 0;
+    if (bytes <= m->scratch_bytes[slot]) return m->scratch[slot];
+    if (m->scratch[slot]) mi355x_free(m->scratch[slot]);
+    m->scratch[slot] = NULL;
+    m->scratch_bytes[slot] = 0;
     size_t want = bytes < ((size_t)1 << 20) ? ((size_t)1 << 20) : bytes;
-    if (mi355x_malloc(&m->scratch, want) != MI355X_SUCCESS) return NULL;
-    m->scratch_bytes = want;
-    return m->scratch;
+    if (mi355x_malloc(&m->scratch[slot], want) != MI355X_SUCCESS) return NULL;
+    m->scratch_bytes[slot] = want;
+    return m->scratch[slot];
 }
+
+static void *scratch(struct mca_coll_mi355x_module_t *m, size_t bytes) { return scratch_slot(m, 0, bytes); }
 
 /* one side of a convertor move: (buf, count, dt) <-> packed bytes at p */
 static int stage(struct mca_coll_mi355x_module_t *m, int pack, void *buf, int count, const struct ompi_datatype_t *dt,
@@ -306,9 +311,13 @@ int mca_coll_mi355x_allgather(void *sbuf, int scount, struct ompi_datatype_t *sd
     const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm);
     const size_t blk = (size_t)rcount * rdtype->super.size;
     if (!inplace && (size_t)scount * sdtype->super.size != blk) return OMPI_ERR_BAD_PARAM;
+    /* a layout the convertor cannot describe is an error, never a rank-local fallback: the other
+     * ranks (whose layouts may differ) are already in the engine */
     if ((!inplace && !contiguous_bytes(sdtype, scount, &sb) && !ddt_of(m, sdtype)) ||
-        (!contiguous_bytes(rdtype, rcount, &rb) && !ddt_of(m, rdtype)))
-        return m->prev_allgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_allgather_module);
+        (!contiguous_bytes(rdtype, rcount, &rb) && !ddt_of(m, rdtype))) {
+        fprintf(stderr, "[coll/mi355x] allgather: the GPU convertor cannot describe the datatype\n");
+        return OMPI_ERR_NOT_SUPPORTED;
+    }
     if (blk == 0) return OMPI_SUCCESS;
     char *st = (char *)scratch(m, blk * (size_t)n);
     if (!st) return OMPI_ERR_OUT_OF_RESOURCE;
@@ -330,7 +339,10 @@ int mca_coll_mi355x_bcast(void *buff, int count, struct ompi_datatype_t *datatyp
         return m->prev_bcast(buff, count, datatype, root, comm, m->prev_bcast_module);
     if (contiguous_bytes(datatype, count, &bytes)) return map_rc(mi355x_bcast(m->engine, buff, bytes, root, NULL));
     /* derived datatype: root packs, the packed bytes are broadcast, the others unpack */
-    if (!ddt_of(m, datatype)) return m->prev_bcast(buff, count, datatype, root, comm, m->prev_bcast_module);
+    if (!ddt_of(m, datatype)) {  /* see allgather: no rank-local fallback */
+        fprintf(stderr, "[coll/mi355x] bcast: the GPU convertor cannot describe datatype %s\n", datatype->name);
+        return OMPI_ERR_NOT_SUPPORTED;
+    }
     bytes = (size_t)count * datatype->super.size;
     if (bytes == 0) return OMPI_SUCCESS;
     void *st = scratch(m, bytes);
@@ -345,22 +357,92 @@ int mca_coll_mi355x_bcast(void *buff, int count, struct ompi_datatype_t *datatyp
 }
 
 /* ------------------------------------------------------------------ gather / scatter / alltoall / scan
- * Dense datatypes only (gap-free, extent == size: counts and displacements scale by the size);
- * anything else, host buffers or user-defined ops go to the previous owner of the slot. */
+ * Which path a call takes may depend only on what MPI requires to agree across ranks (the type
+ * SIGNATURES, so the byte counts, and the op) and on where the buffers are: never on a rank-local
+ * datatype LAYOUT, which MPI lets differ between ranks (a root may receive into a resized column
+ * type while the others send MPI_INT).  So every layout goes to the engine: a dense layout in
+ * place, any other through the GPU convertor into a staging buffer -- packed before the call for
+ * the bytes a rank sends, unpacked after for the bytes it receives.  A layout the convertor cannot
+ * compile is an error, not a silent fallback (the other ranks are already in the engine). */
 static int dense(const struct ompi_datatype_t *dt)
 {
     return (dt->super.flags & OPAL_DATATYPE_FLAG_NO_GAPS) && dt->super.true_lb == 0 &&
            (size_t)(dt->super.ub - dt->super.lb) == dt->super.size;
 }
 
-/* counts / displacements (in datatype units) -> bytes; NULL when not needed at this rank */
-static int to_bytes(int n, const int *v, size_t unit, size_t *out)
+#define SIDE_MAX 64
+/* one rank's send or receive side as the engine sees it: `view` + per-piece byte counts and
+ * offsets.  Piece q = cnt[q] instances of dt at base + udisp[q] (bytes). */
+typedef struct {
+    int n;
+    char *base;
+    mi355x_ddt_t *d;          /* NULL: dense, view == base */
+    char *view;
+    size_t bytes[SIDE_MAX], off[SIDE_MAX], cnt[SIDE_MAX];
+    ptrdiff_t udisp[SIDE_MAX];
+} side_t;
+
+/* counts/displacements in instances (NULL disps: consecutive pieces of `counts`; NULL counts:
+ * every piece `count1` instances).  Returns OMPI_SUCCESS or an error. */
+static int side_init(mca_coll_mi355x_module_t *m, side_t *s, int slot, void *buf, const struct ompi_datatype_t *dt,
+                     int n, const int *counts, int count1, const int *disps)
 {
-    for (int i = 0; i < n; ++i) {
-        if (v[i] < 0) return 0;
-        out[i] = (size_t)v[i] * unit;
+    if (n > SIDE_MAX) return OMPI_ERR_NOT_SUPPORTED;
+    memset(s, 0, sizeof(*s));
+    s->n = n;
+    s->base = (char *)buf;
+    const size_t sz = dt->super.size;
+    const ptrdiff_t ext = dt->super.ub - dt->super.lb;
+    ptrdiff_t next = 0;
+    for (int q = 0; q < n; ++q) {
+        const int c = counts ? counts[q] : count1;
+        if (c < 0) return OMPI_ERR_BAD_PARAM;
+        const ptrdiff_t dq = disps ? (ptrdiff_t)disps[q] : next;
+        if (dq < 0) return OMPI_ERR_NOT_SUPPORTED;
+        s->cnt[q] = (size_t)c;
+        s->bytes[q] = (size_t)c * sz;
+        s->udisp[q] = dq * ext;
+        next = dq + c;
     }
-    return 1;
+    if (dense(dt)) {
+        s->view = s->base;
+        for (int q = 0; q < n; ++q) s->off[q] = (size_t)s->udisp[q];
+        return OMPI_SUCCESS;
+    }
+    s->d = ddt_of(m, dt);
+    if (!s->d) {
+        fprintf(stderr, "[coll/mi355x] the GPU convertor cannot describe datatype %s\n", dt->name);
+        return OMPI_ERR_NOT_SUPPORTED;
+    }
+    size_t total = 0;
+    for (int q = 0; q < n; ++q) {
+        s->off[q] = total;
+        total += s->bytes[q];
+    }
+    s->view = (char *)scratch_slot(m, slot, total ? total : 1);
+    return s->view ? OMPI_SUCCESS : OMPI_ERR_OUT_OF_RESOURCE;
+}
+
+/* piece q (or every piece, q < 0): user layout -> view (pack) or view -> user layout (unpack) */
+static int side_move(side_t *s, int q, int pack)
+{
+    if (!s->d) return MI355X_SUCCESS;
+    for (int p = (q < 0 ? 0 : q); p < (q < 0 ? s->n : q + 1); ++p) {
+        if (!s->bytes[p]) continue;
+        int rc = pack ? mi355x_pack(s->d, s->cnt[p], s->base + s->udisp[p], 0, s->view + s->off[p], s->bytes[p], NULL, NULL)
+                      : mi355x_unpack(s->d, s->cnt[p], s->base + s->udisp[p], 0, s->view + s->off[p], s->bytes[p], NULL, NULL);
+        if (rc) return rc;
+    }
+    return MI355X_SUCCESS;
+}
+
+static int finish_unpack(side_t *s, int rc)
+{
+    if (rc == MI355X_SUCCESS && s && s->d) {
+        rc = side_move(s, -1, 0);
+        if (rc == MI355X_SUCCESS) rc = mi355x_stream_sync(NULL);
+    }
+    return map_rc(rc);
 }
 
 int mca_coll_mi355x_gather(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
@@ -368,12 +450,18 @@ int mca_coll_mi355x_gather(void *sbuf, int scount, struct ompi_datatype_t *sdtyp
                            mca_coll_base_module_t *module)
 {
     mca_coll_mi355x_module_t *m = MOD(module);
-    const int me = mi355x_comm_rank_of(comm), inplace = (sbuf == MPI_IN_PLACE);
-    if ((me == root && (!is_dev(rbuf) || !dense(rdtype) || rcount < 0)) ||
-        (!inplace && (!is_dev(sbuf) || !dense(sdtype) || scount < 0)) || (inplace && me != root))
+    const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm), inplace = (sbuf == MPI_IN_PLACE);
+    if ((me == root && !is_dev(rbuf)) || (!inplace && !is_dev(sbuf)) || (inplace && me != root))
         return m->prev_gather(sbuf, scount, sdtype, rbuf, rcount, rdtype, root, comm, m->prev_gather_module);
-    const size_t bytes = inplace ? (size_t)rcount * rdtype->super.size : (size_t)scount * sdtype->super.size;
-    return map_rc(mi355x_gather(m->engine, inplace ? NULL : sbuf, me == root ? rbuf : NULL, bytes, root, NULL));
+    side_t snd, rcv;
+    int rc = OMPI_SUCCESS;
+    if (!inplace && (rc = side_init(m, &snd, 0, sbuf, sdtype, 1, NULL, scount, NULL))) return rc;
+    if (me == root && (rc = side_init(m, &rcv, 1, rbuf, rdtype, n, NULL, rcount, NULL))) return rc;
+    const size_t bytes = inplace ? rcv.bytes[me] : snd.bytes[0];
+    int erc = inplace ? side_move(&rcv, me, 1) : side_move(&snd, 0, 1);
+    if (erc == MI355X_SUCCESS)
+        erc = mi355x_gather(m->engine, inplace ? NULL : snd.view, me == root ? rcv.view : NULL, bytes, root, NULL);
+    return finish_unpack(me == root ? &rcv : NULL, erc);
 }
 
 int mca_coll_mi355x_gatherv(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int *rcounts,
@@ -382,14 +470,18 @@ int mca_coll_mi355x_gatherv(void *sbuf, int scount, struct ompi_datatype_t *sdty
 {
     mca_coll_mi355x_module_t *m = MOD(module);
     const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm), inplace = (sbuf == MPI_IN_PLACE);
-    size_t rc_b[64], dp_b[64];
-    if (n > 64 || (me == root && (!is_dev(rbuf) || !dense(rdtype) || !to_bytes(n, rcounts, rdtype->super.size, rc_b) ||
-                                  !to_bytes(n, disps, rdtype->super.size, dp_b))) ||
-        (!inplace && (!is_dev(sbuf) || !dense(sdtype) || scount < 0)) || (inplace && me != root))
+    if (n > SIDE_MAX || (me == root && !is_dev(rbuf)) || (!inplace && !is_dev(sbuf)) || (inplace && me != root))
         return m->prev_gatherv(sbuf, scount, sdtype, rbuf, rcounts, disps, rdtype, root, comm, m->prev_gatherv_module);
-    const size_t sb = inplace ? 0 : (size_t)scount * sdtype->super.size;
-    return map_rc(mi355x_gatherv(m->engine, inplace ? NULL : sbuf, sb, me == root ? rbuf : NULL,
-                                 me == root ? rc_b : NULL, me == root ? dp_b : NULL, root, NULL));
+    side_t snd, rcv;
+    int rc = OMPI_SUCCESS;
+    if (!inplace && (rc = side_init(m, &snd, 0, sbuf, sdtype, 1, NULL, scount, NULL))) return rc;
+    if (me == root && (rc = side_init(m, &rcv, 1, rbuf, rdtype, n, rcounts, 0, disps))) return rc;
+    int erc = inplace ? side_move(&rcv, me, 1) : side_move(&snd, 0, 1);
+    if (erc == MI355X_SUCCESS)
+        erc = mi355x_gatherv(m->engine, inplace ? NULL : snd.view, inplace ? 0 : snd.bytes[0],
+                             me == root ? rcv.view : NULL, me == root ? rcv.bytes : NULL,
+                             me == root ? rcv.off : NULL, root, NULL);
+    return finish_unpack(me == root ? &rcv : NULL, erc);
 }
 
 int mca_coll_mi355x_scatter(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
@@ -397,12 +489,18 @@ int mca_coll_mi355x_scatter(void *sbuf, int scount, struct ompi_datatype_t *sdty
                             mca_coll_base_module_t *module)
 {
     mca_coll_mi355x_module_t *m = MOD(module);
-    const int me = mi355x_comm_rank_of(comm), inplace = (rbuf == MPI_IN_PLACE);
-    if ((me == root && (!is_dev(sbuf) || !dense(sdtype) || scount < 0)) ||
-        (!inplace && (!is_dev(rbuf) || !dense(rdtype) || rcount < 0)) || (inplace && me != root))
+    const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm), inplace = (rbuf == MPI_IN_PLACE);
+    if ((me == root && !is_dev(sbuf)) || (!inplace && !is_dev(rbuf)) || (inplace && me != root))
         return m->prev_scatter(sbuf, scount, sdtype, rbuf, rcount, rdtype, root, comm, m->prev_scatter_module);
-    const size_t bytes = me == root ? (size_t)scount * sdtype->super.size : (size_t)rcount * rdtype->super.size;
-    return map_rc(mi355x_scatter(m->engine, me == root ? sbuf : NULL, inplace ? NULL : rbuf, bytes, root, NULL));
+    side_t snd, rcv;
+    int rc = OMPI_SUCCESS;
+    if (me == root && (rc = side_init(m, &snd, 0, sbuf, sdtype, n, NULL, scount, NULL))) return rc;
+    if (!inplace && (rc = side_init(m, &rcv, 1, rbuf, rdtype, 1, NULL, rcount, NULL))) return rc;
+    const size_t bytes = me == root ? snd.bytes[0] : rcv.bytes[0];
+    int erc = me == root ? side_move(&snd, -1, 1) : MI355X_SUCCESS;
+    if (erc == MI355X_SUCCESS)
+        erc = mi355x_scatter(m->engine, me == root ? snd.view : NULL, inplace ? NULL : rcv.view, bytes, root, NULL);
+    return finish_unpack(inplace ? NULL : &rcv, erc);
 }
 
 int mca_coll_mi355x_scatterv(void *sbuf, int *scounts, int *disps, struct ompi_datatype_t *sdtype, void *rbuf,
@@ -411,15 +509,19 @@ int mca_coll_mi355x_scatterv(void *sbuf, int *scounts, int *disps, struct ompi_d
 {
     mca_coll_mi355x_module_t *m = MOD(module);
     const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm), inplace = (rbuf == MPI_IN_PLACE);
-    size_t sc_b[64], dp_b[64];
-    if (n > 64 || (me == root && (!is_dev(sbuf) || !dense(sdtype) || !to_bytes(n, scounts, sdtype->super.size, sc_b) ||
-                                  !to_bytes(n, disps, sdtype->super.size, dp_b))) ||
-        (!inplace && (!is_dev(rbuf) || !dense(rdtype) || rcount < 0)) || (inplace && me != root))
+    if (n > SIDE_MAX || (me == root && !is_dev(sbuf)) || (!inplace && !is_dev(rbuf)) || (inplace && me != root))
         return m->prev_scatterv(sbuf, scounts, disps, sdtype, rbuf, rcount, rdtype, root, comm,
                                 m->prev_scatterv_module);
-    const size_t rb = inplace ? 0 : (size_t)rcount * rdtype->super.size;
-    return map_rc(mi355x_scatterv(m->engine, me == root ? sbuf : NULL, me == root ? sc_b : NULL,
-                                  me == root ? dp_b : NULL, inplace ? NULL : rbuf, rb, root, NULL));
+    side_t snd, rcv;
+    int rc = OMPI_SUCCESS;
+    if (me == root && (rc = side_init(m, &snd, 0, sbuf, sdtype, n, scounts, 0, disps))) return rc;
+    if (!inplace && (rc = side_init(m, &rcv, 1, rbuf, rdtype, 1, NULL, rcount, NULL))) return rc;
+    int erc = me == root ? side_move(&snd, -1, 1) : MI355X_SUCCESS;
+    if (erc == MI355X_SUCCESS)
+        erc = mi355x_scatterv(m->engine, me == root ? snd.view : NULL, me == root ? snd.bytes : NULL,
+                              me == root ? snd.off : NULL, inplace ? NULL : rcv.view, inplace ? 0 : rcv.bytes[0], root,
+                              NULL);
+    return finish_unpack(inplace ? NULL : &rcv, erc);
 }
 
 int mca_coll_mi355x_allgatherv(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int *rcounts,
@@ -427,13 +529,18 @@ int mca_coll_mi355x_allgatherv(void *sbuf, int scount, struct ompi_datatype_t *s
                                mca_coll_base_module_t *module)
 {
     mca_coll_mi355x_module_t *m = MOD(module);
-    const int n = mi355x_comm_size_of(comm), inplace = (sbuf == MPI_IN_PLACE);
-    size_t rc_b[64], dp_b[64];
-    if (n > 64 || !is_dev(rbuf) || !dense(rdtype) || !to_bytes(n, rcounts, rdtype->super.size, rc_b) ||
-        !to_bytes(n, disps, rdtype->super.size, dp_b) || (!inplace && (!is_dev(sbuf) || !dense(sdtype) || scount < 0)))
+    const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm), inplace = (sbuf == MPI_IN_PLACE);
+    if (n > SIDE_MAX || !is_dev(rbuf) || (!inplace && !is_dev(sbuf)))
         return m->prev_allgatherv(sbuf, scount, sdtype, rbuf, rcounts, disps, rdtype, comm, m->prev_allgatherv_module);
-    return map_rc(mi355x_allgatherv(m->engine, inplace ? NULL : sbuf, inplace ? 0 : (size_t)scount * sdtype->super.size,
-                                    rbuf, rc_b, dp_b, NULL));
+    side_t snd, rcv;
+    int rc = OMPI_SUCCESS;
+    if (!inplace && (rc = side_init(m, &snd, 0, sbuf, sdtype, 1, NULL, scount, NULL))) return rc;
+    if ((rc = side_init(m, &rcv, 1, rbuf, rdtype, n, rcounts, 0, disps))) return rc;
+    int erc = inplace ? side_move(&rcv, me, 1) : side_move(&snd, 0, 1);
+    if (erc == MI355X_SUCCESS)
+        erc = mi355x_allgatherv(m->engine, inplace ? NULL : snd.view, inplace ? 0 : snd.bytes[0], rcv.view, rcv.bytes,
+                                rcv.off, NULL);
+    return finish_unpack(&rcv, erc);
 }
 
 int mca_coll_mi355x_alltoall(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
@@ -441,12 +548,17 @@ int mca_coll_mi355x_alltoall(void *sbuf, int scount, struct ompi_datatype_t *sdt
                              mca_coll_base_module_t *module)
 {
     mca_coll_mi355x_module_t *m = MOD(module);
-    const int inplace = (sbuf == MPI_IN_PLACE);
-    if (!is_dev(rbuf) || !dense(rdtype) || rcount < 0 ||
-        (!inplace && (!is_dev(sbuf) || !dense(sdtype) || (size_t)scount * sdtype->super.size !=
-                                                             (size_t)rcount * rdtype->super.size)))
+    const int n = mi355x_comm_size_of(comm), inplace = (sbuf == MPI_IN_PLACE);
+    if (n > SIDE_MAX || !is_dev(rbuf) || (!inplace && !is_dev(sbuf)))
         return m->prev_alltoall(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_alltoall_module);
-    return map_rc(mi355x_alltoall(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)rcount * rdtype->super.size, NULL));
+    side_t snd, rcv;
+    int rc = OMPI_SUCCESS;
+    if (!inplace && (rc = side_init(m, &snd, 0, sbuf, sdtype, n, NULL, scount, NULL))) return rc;
+    if ((rc = side_init(m, &rcv, 1, rbuf, rdtype, n, NULL, rcount, NULL))) return rc;
+    if (!inplace && snd.bytes[0] != rcv.bytes[0]) return OMPI_ERR_BAD_PARAM;
+    int erc = inplace ? side_move(&rcv, -1, 1) : side_move(&snd, -1, 1);
+    if (erc == MI355X_SUCCESS) erc = mi355x_alltoall(m->engine, inplace ? NULL : snd.view, rcv.view, rcv.bytes[0], NULL);
+    return finish_unpack(&rcv, erc);
 }
 
 int mca_coll_mi355x_alltoallv(void *sbuf, int *scounts, int *sdisps, struct ompi_datatype_t *sdtype, void *rbuf,
@@ -455,15 +567,18 @@ int mca_coll_mi355x_alltoallv(void *sbuf, int *scounts, int *sdisps, struct ompi
 {
     mca_coll_mi355x_module_t *m = MOD(module);
     const int n = mi355x_comm_size_of(comm), inplace = (sbuf == MPI_IN_PLACE);
-    size_t sc_b[64], sd_b[64], rc_b[64], rd_b[64];
-    if (n > 64 || !is_dev(rbuf) || !dense(rdtype) || !to_bytes(n, rcounts, rdtype->super.size, rc_b) ||
-        !to_bytes(n, rdisps, rdtype->super.size, rd_b) ||
-        (!inplace && (!is_dev(sbuf) || !dense(sdtype) || !to_bytes(n, scounts, sdtype->super.size, sc_b) ||
-                      !to_bytes(n, sdisps, sdtype->super.size, sd_b))))
+    if (n > SIDE_MAX || !is_dev(rbuf) || (!inplace && !is_dev(sbuf)))
         return m->prev_alltoallv(sbuf, scounts, sdisps, sdtype, rbuf, rcounts, rdisps, rdtype, comm,
                                  m->prev_alltoallv_module);
-    return map_rc(mi355x_alltoallv(m->engine, inplace ? NULL : sbuf, inplace ? NULL : sc_b, inplace ? NULL : sd_b,
-                                   rbuf, rc_b, rd_b, NULL));
+    side_t snd, rcv;
+    int rc = OMPI_SUCCESS;
+    if (!inplace && (rc = side_init(m, &snd, 0, sbuf, sdtype, n, scounts, 0, sdisps))) return rc;
+    if ((rc = side_init(m, &rcv, 1, rbuf, rdtype, n, rcounts, 0, rdisps))) return rc;
+    int erc = inplace ? side_move(&rcv, -1, 1) : side_move(&snd, -1, 1);
+    if (erc == MI355X_SUCCESS)
+        erc = mi355x_alltoallv(m->engine, inplace ? NULL : snd.view, inplace ? NULL : snd.bytes,
+                               inplace ? NULL : snd.off, rcv.view, rcv.bytes, rcv.off, NULL);
+    return finish_unpack(&rcv, erc);
 }
 
 static int scan_common(mca_coll_mi355x_module_t *m, int exclusive, void *sbuf, void *rbuf, int count,
@@ -743,14 +858,30 @@ static int module_enable(mca_coll_base_module_t *module, struct ompi_communicato
     SNAP_OPT(ireduce_scatter_block);
     SNAP_OPT(iallgather);
     SNAP_OPT(ibcast);
-    /* node-unique rendezvous key: job id + communicator context id */
-    const char *job = getenv("OMPI_MCA_ess_base_jobid");
-    char key[128];
-    snprintf(key, sizeof(key), "ompi_%s_cid%u", job ? job : "0", (unsigned)comm->c_contextid);
-    int ndev = 1;
-    if (mi355x_device_count(&ndev) != MI355X_SUCCESS || ndev < 1) return OMPI_ERROR;
-    const int dev = env_int("OMPI_COMM_WORLD_LOCAL_RANK", mi355x_comm_rank_of(comm)) % ndev;
-    int rc = mi355x_comm_create(key, mi355x_comm_rank_of(comm), mi355x_comm_size_of(comm), dev, &m->engine);
+    /* Node-unique rendezvous key, picked by rank 0 and broadcast with the lower-priority bcast
+     * just snapshotted (the communicator is p2p-capable during enable, coll.h:125-127).  Neither
+     * the job id nor the context id would do: MPI_Comm_split allocates ONE cid for every color
+     * group of the parent (ompi_comm_nextcid over the parent, comm.c:610), so sibling groups on
+     * one node share (jobid, cid). */
+    char key[64];
+    memset(key, 0, sizeof(key));
+    if (mi355x_comm_rank_of(comm) == 0) {
+        static unsigned counter;
+        unsigned rnd = 0;
+        FILE *ur = fopen("/dev/urandom", "rb");
+        if (!ur || fread(&rnd, sizeof(rnd), 1, ur) != 1) rnd = (unsigned)time(NULL) ^ (unsigned)(uintptr_t)&rnd;
+        if (ur) fclose(ur);
+        snprintf(key, sizeof(key), "ompi_%d_%u_%08x", (int)getpid(), __atomic_add_fetch(&counter, 1, __ATOMIC_RELAXED),
+                 rnd);
+    }
+    int rc = m->prev_bcast(key, (int)sizeof(key), MPI_BYTE, 0, comm, m->prev_bcast_module);
+    if (rc != OMPI_SUCCESS) return rc;
+    key[sizeof(key) - 1] = 0;
+    /* the GPU this process selected before the communicator was created (hipSetDevice), never a
+     * device derived from the local rank: the engine must run where the application's buffers are */
+    int dev = 0;
+    if (mi355x_get_device(&dev) != MI355X_SUCCESS) return OMPI_ERROR;
+    rc = mi355x_comm_create(key, mi355x_comm_rank_of(comm), mi355x_comm_size_of(comm), dev, &m->engine);
     if (rc != MI355X_SUCCESS) return map_rc(rc);
     if (mca_coll_mi355x_allreduce_algorithm)
         mi355x_comm_set(m->engine, MI355X_KNOB_ALLREDUCE_ALG, mca_coll_mi355x_allreduce_algorithm);

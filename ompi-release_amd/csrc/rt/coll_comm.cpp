@@ -24,11 +24,12 @@
 // data flow -- the message moves through each rank's persistent staging buffer (one allocation
 // < 2 GiB, mapped once) in block-strided windows, like the segmented ring's phases.
 #include <fcntl.h>
+#include <poll.h>
 #include <sched.h>
 #include <sys/mman.h>
-#include <sys/prctl.h>
-#include <sys/syscall.h>
+#include <sys/socket.h>
 #include <sys/stat.h>
+#include <sys/un.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -36,6 +37,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstddef>
 #include <deque>
 #include <functional>
 #include <cstdio>
@@ -187,24 +189,175 @@ int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
     return MI355X_SUCCESS;
 }
 
-// ----------------------------------------------------------------- dmabuf export of large allocations
+// ----------------------------------------------------------------- dmabuf fd passing (SCM_RIGHTS)
 // hipIpcOpenMemHandle never returns for allocations of >= 2 GiB (ROCm 7.2, dmabuf IPC), but the
-// allocation exported as a dmabuf fd (hipMemGetHandleForAddressRange), fetched by the peer with
-// pidfd_getfd and imported as external memory maps fine (tools/probe/dmabuf_xproc.hip).  The
-// exporter lets same-user processes read its descriptors (PR_SET_PTRACER_ANY, which yama's
-// ptrace_scope 1 requires for pidfd_getfd between siblings).
-int export_dmabuf(mi355x_comm *c, BufDesc *d)
+// allocation exported as a dmabuf fd (hipMemGetHandleForAddressRange) and imported by the peer as
+// external memory maps fine.  The fd reaches the peer as SCM_RIGHTS ancillary data on an AF_UNIX
+// datagram socket (the smcuda BTL's role of carrying the IPC handle, btl/smcuda/README:13-30):
+// no ptrace permission is granted to anybody.  Every rank binds one socket at communicator
+// creation under an abstract name derived from the control segment's (node-unique) name; the
+// receiver checks the sender's pid (SO_PASSCRED) against the rank's published pid.
+struct FdMsg {
+    int32_t from;
+    int32_t pad;
+    uint64_t id;
+};
+
+static void fd_sock_addr(const mi355x_comm *c, int rank, sockaddr_un *a, socklen_t *len)
+{
+    uint64_t h = 1469598103934665603ull;
+    for (char ch : c->shm_name) h = (h ^ (unsigned char)ch) * 1099511628211ull;
+    std::memset(a, 0, sizeof(*a));
+    a->sun_family = AF_UNIX;
+    // abstract namespace: sun_path[0] = 0, the name is the bytes that follow
+    const int n = snprintf(a->sun_path + 1, sizeof(a->sun_path) - 1, "mi355x_fd_%016llx_%d", (unsigned long long)h, rank);
+    *len = (socklen_t)(offsetof(sockaddr_un, sun_path) + 1 + (size_t)n);
+}
+
+static int fd_sock_open(mi355x_comm *c)
+{
+    const int s = socket(AF_UNIX, SOCK_DGRAM | SOCK_CLOEXEC, 0);
+    if (s < 0) return set_error(MI355X_ERR_PEER, "socket(AF_UNIX): %s", strerror(errno));
+    const int one = 1;
+    sockaddr_un a;
+    socklen_t len;
+    fd_sock_addr(c, c->rank, &a, &len);
+    if (setsockopt(s, SOL_SOCKET, SO_PASSCRED, &one, sizeof(one)) != 0 || bind(s, (sockaddr *)&a, len) != 0) {
+        const int e = errno;
+        close(s);
+        return set_error(MI355X_ERR_PEER, "bind of the fd-passing socket: %s", strerror(e));
+    }
+    c->fd_sock = s;
+    return MI355X_SUCCESS;
+}
+
+// receive every queued fd message into the stash; `wait`: block (bounded) for at least one
+static int fd_drain(mi355x_comm *c, bool wait)
+{
+    for (;;) {
+        FdMsg m;
+        iovec iov{&m, sizeof(m)};
+        alignas(cmsghdr) char ctl[CMSG_SPACE(sizeof(int)) + CMSG_SPACE(sizeof(ucred))];
+        msghdr h;
+        std::memset(&h, 0, sizeof(h));
+        h.msg_iov = &iov;
+        h.msg_iovlen = 1;
+        h.msg_control = ctl;
+        h.msg_controllen = sizeof(ctl);
+        if (wait) {
+            pollfd p{c->fd_sock, POLLIN, 0};
+            const int pr = poll(&p, 1, (int)std::min(c->timeout_s * 1000.0, 2.0e9));
+            if (pr == 0) return set_error(MI355X_ERR_TIMEOUT, "rank %d: no dmabuf fd arrived", c->rank);
+            if (pr < 0 && errno != EINTR) return set_error(MI355X_ERR_PEER, "poll: %s", strerror(errno));
+        }
+        const ssize_t got = recvmsg(c->fd_sock, &h, MSG_DONTWAIT | MSG_CMSG_CLOEXEC);
+        if (got < 0) {
+            if (errno == EAGAIN || errno == EWOULDBLOCK) {
+                if (wait) continue;
+                return MI355X_SUCCESS;
+            }
+            if (errno == EINTR) continue;
+            return set_error(MI355X_ERR_PEER, "recvmsg: %s", strerror(errno));
+        }
+        int fd = -1;
+        pid_t pid = -1;
+        for (cmsghdr *cm = CMSG_FIRSTHDR(&h); cm; cm = CMSG_NXTHDR(&h, cm)) {
+            if (cm->cmsg_level == SOL_SOCKET && cm->cmsg_type == SCM_RIGHTS) std::memcpy(&fd, CMSG_DATA(cm), sizeof(int));
+            if (cm->cmsg_level == SOL_SOCKET && cm->cmsg_type == SCM_CREDENTIALS) {
+                ucred cr;
+                std::memcpy(&cr, CMSG_DATA(cm), sizeof(cr));
+                pid = cr.pid;
+            }
+        }
+        const bool ok = got == (ssize_t)sizeof(m) && fd >= 0 && m.from >= 0 && m.from < c->size &&
+                        pid == (pid_t)c->ctrl->slot[m.from].pid;
+        if (!ok) {  // not from a rank of this communicator: drop it
+            if (fd >= 0) close(fd);
+            continue;
+        }
+        const auto key = std::make_pair((int)m.from, m.id);
+        auto it = c->fd_stash.find(key);
+        if (it != c->fd_stash.end()) close(it->second);
+        c->fd_stash[key] = fd;
+        if (wait) return MI355X_SUCCESS;
+    }
+}
+
+static int send_fd(mi355x_comm *c, int peer, int fd, uint64_t id)
+{
+    FdMsg m{c->rank, 0, id};
+    iovec iov{&m, sizeof(m)};
+    alignas(cmsghdr) char ctl[CMSG_SPACE(sizeof(int))];
+    std::memset(ctl, 0, sizeof(ctl));
+    sockaddr_un a;
+    socklen_t len;
+    fd_sock_addr(c, peer, &a, &len);
+    msghdr h;
+    std::memset(&h, 0, sizeof(h));
+    h.msg_name = &a;
+    h.msg_namelen = len;
+    h.msg_iov = &iov;
+    h.msg_iovlen = 1;
+    h.msg_control = ctl;
+    h.msg_controllen = sizeof(ctl);
+    cmsghdr *cm = CMSG_FIRSTHDR(&h);
+    cm->cmsg_level = SOL_SOCKET;
+    cm->cmsg_type = SCM_RIGHTS;
+    cm->cmsg_len = CMSG_LEN(sizeof(int));
+    std::memcpy(CMSG_DATA(cm), &fd, sizeof(int));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        if (sendmsg(c->fd_sock, &h, MSG_DONTWAIT | MSG_NOSIGNAL) == (ssize_t)sizeof(m)) return MI355X_SUCCESS;
+        if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR)
+            return set_error(MI355X_ERR_PEER, "sending a dmabuf fd to rank %d: %s", peer, strerror(errno));
+        // the peer's queue is full: it may be sending to us -- keep ours drained meanwhile
+        int rc = fd_drain(c, false);
+        if (rc) return rc;
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s)
+            return set_error(MI355X_ERR_TIMEOUT, "rank %d: fd queue of rank %d stays full", c->rank, peer);
+        usleep(100);
+    }
+}
+
+// the fd rank `peer` passed for its allocation `id` (a duplicate: the stash keeps its own)
+static int take_fd(mi355x_comm *c, int peer, uint64_t id, int *out)
+{
+    const auto key = std::make_pair(peer, id);
+    int rc = fd_drain(c, false);
+    if (rc) return rc;
+    while (c->fd_stash.find(key) == c->fd_stash.end()) {
+        rc = fd_drain(c, true);
+        if (rc) return rc;
+    }
+    *out = fcntl(c->fd_stash[key], F_DUPFD_CLOEXEC, 0);
+    if (*out < 0) return set_error(MI355X_ERR_PEER, "dup of a dmabuf fd: %s", strerror(errno));
+    return MI355X_SUCCESS;
+}
+
+// forget the fd of `peer`'s allocation `id` (the allocation was freed or replaced)
+static void drop_stash(mi355x_comm *c, int peer, uint64_t id)
+{
+    auto it = c->fd_stash.find(std::make_pair(peer, id));
+    if (it == c->fd_stash.end()) return;
+    close(it->second);
+    c->fd_stash.erase(it);
+}
+
+int export_dmabuf(mi355x_comm *c, BufDesc *d, uint64_t peers)
 {
     std::lock_guard<std::recursive_mutex> reg_guard(c->reg_mtx);
     for (LocalReg &r : c->local_regs) {
         if (r.base != d->base || r.id != d->id) continue;
         if (r.fd < 0) {
-            if (!c->ptracer_any) {
-                prctl(PR_SET_PTRACER, PR_SET_PTRACER_ANY, 0, 0, 0);
-                c->ptracer_any = true;
-            }
             MI_HIP(hipMemGetHandleForAddressRange(&r.fd, (hipDeviceptr_t)r.base, r.size,
                                                   hipMemRangeHandleTypeDmaBufFd, 0));
+            r.sent = 0;
+        }
+        for (int q = 0; q < c->size; ++q) {
+            if (q == c->rank || !((peers >> q) & 1u) || ((r.sent >> q) & 1u)) continue;
+            int rc = send_fd(c, q, r.fd, r.id);
+            if (rc) return rc;
+            r.sent |= 1ull << q;
         }
         d->dmabuf = 1;
         d->fd = r.fd;
@@ -214,16 +367,11 @@ int export_dmabuf(mi355x_comm *c, BufDesc *d)
     return set_error(MI355X_ERR_PEER, "large allocation not registered (id %llu)", (unsigned long long)d->id);
 }
 
-static int import_dmabuf(mi355x_comm *c, int peer, int fd, size_t size, void **mapped, hipExternalMemory_t *ext)
+static int import_dmabuf(mi355x_comm *c, int peer, uint64_t id, size_t size, void **mapped, hipExternalMemory_t *ext)
 {
-    auto pit = c->pidfds.find(peer);
-    if (pit == c->pidfds.end()) {
-        const int pfd = (int)syscall(SYS_pidfd_open, (pid_t)c->ctrl->slot[peer].pid, 0);
-        if (pfd < 0) return set_error(MI355X_ERR_PEER, "pidfd_open(rank %d): %s", peer, strerror(errno));
-        pit = c->pidfds.emplace(peer, pfd).first;
-    }
-    const int myfd = (int)syscall(SYS_pidfd_getfd, pit->second, fd, 0);
-    if (myfd < 0) return set_error(MI355X_ERR_PEER, "pidfd_getfd(rank %d): %s", peer, strerror(errno));
+    int myfd = -1;
+    int rc = take_fd(c, peer, id, &myfd);
+    if (rc) return rc;
     hipExternalMemoryHandleDesc hd;
     std::memset(&hd, 0, sizeof(hd));
     hd.type = hipExternalMemoryHandleTypeOpaqueFd;
@@ -261,18 +409,15 @@ static int probe_dmabuf(mi355x_comm *c)
     if (ok && hipMalloc(&buf, sz) != hipSuccess) ok = false;
     if (ok && hipMemset(buf, c->rank + 1, sz) != hipSuccess) ok = false;
     if (ok && hipDeviceSynchronize() != hipSuccess) ok = false;
-    if (ok) {
-        if (!c->ptracer_any) {
-            prctl(PR_SET_PTRACER, PR_SET_PTRACER_ANY, 0, 0, 0);
-            c->ptracer_any = true;
-        }
-        if (hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)buf, sz, hipMemRangeHandleTypeDmaBufFd, 0) != hipSuccess)
-            ok = false;
-    }
+    if (ok && hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)buf, sz, hipMemRangeHandleTypeDmaBufFd, 0) != hipSuccess)
+        ok = false;
     (void)hipGetLastError();
-    me.probe_fd = ok ? fd : -1;
+    const uint64_t kProbeId = ~0ull;  // never an allocation id
+    for (int q = 0; q < c->size && ok; ++q)
+        if (q != c->rank && send_fd(c, q, fd, kProbeId) != MI355X_SUCCESS) ok = false;
+    me.probe_fd = ok ? 1 : -1;  // 1: my fd went to every peer
     me.probe_size = sz;
-    int rc = barrier(c);
+    int rc = barrier(c);  // every sent fd is queued at its receiver
     if (rc) return rc;
     for (int q = 0; q < c->size && ok; ++q) {
         if (q == c->rank) continue;
@@ -283,7 +428,9 @@ static int probe_dmabuf(mi355x_comm *c)
         }
         void *mapped = nullptr;
         hipExternalMemory_t ext = nullptr;
-        if (import_dmabuf(c, q, o.probe_fd, o.probe_size, &mapped, &ext) != MI355X_SUCCESS) {
+        const int irc = import_dmabuf(c, q, kProbeId, o.probe_size, &mapped, &ext);
+        drop_stash(c, q, kProbeId);
+        if (irc != MI355X_SUCCESS) {
             ok = false;
             break;
         }
@@ -296,6 +443,7 @@ static int probe_dmabuf(mi355x_comm *c)
         (void)hipDestroyExternalMemory(ext);
         (void)hipGetLastError();
     }
+    for (int q = 0; q < c->size; ++q) drop_stash(c, q, kProbeId);
     me.probe_ok = ok ? 1 : 0;
     rc = barrier(c);  // every rank is done importing before the probe buffers go
     if (fd >= 0) close(fd);
@@ -323,6 +471,7 @@ int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **e
     key.base = d.base;
     auto it = c->peer_maps.find(key);
     if (it != c->peer_maps.end() && (it->second.id != d.id || (d.id == 0 && it->second.pins == 0))) {
+        if (it->second.ext) drop_stash(c, peer, it->second.id);  // the peer replaced that allocation
         close_map(it->second);
         c->peer_maps.erase(it);
         it = c->peer_maps.end();
@@ -330,7 +479,7 @@ int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **e
     if (it == c->peer_maps.end() && d.dmabuf) {
         void *mapped = nullptr;
         hipExternalMemory_t ext = nullptr;
-        int rc = import_dmabuf(c, peer, d.fd, d.size, &mapped, &ext);
+        int rc = import_dmabuf(c, peer, d.id, d.size, &mapped, &ext);
         if (rc) return rc;
         it = c->peer_maps.emplace(key, PeerMap{d.id, mapped, c->seq, ext}).first;
     }
@@ -414,7 +563,7 @@ int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t s
             // second round: the large allocations go out as dmabuf fds, then everything is mapped
             for (int b = 0; b < nbuf; ++b)
                 if (s.buf[b].staged) {
-                    rc = export_dmabuf(c, &s.buf[b]);
+                    rc = export_dmabuf(c, &s.buf[b], ~0ull);
                     if (rc) return rc;
                 }
             rc = barrier(c);
@@ -952,7 +1101,7 @@ int post(mi355x_comm *c, void *stream, std::function<int(hipStream_t)> run, mi35
     if (!out) return set_error(MI355X_ERR_ARG, "request pointer is NULL");
     *out = nullptr;
     if (!c->nb_stream) {
-        MI_HIP(hipSetDevice(c->device));
+        DeviceGuard dg(c->device);
         MI_HIP(hipStreamCreateWithFlags(&c->nb_stream, hipStreamNonBlocking));
     }
     auto *r = new mi355x_request();
@@ -986,7 +1135,9 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     if (!key || !out || size < 1 || size > kMaxRanks || rank < 0 || rank >= size)
         return set_error(MI355X_ERR_ARG, "bad comm_create arguments");
     *out = nullptr;
-    MI_HIP(hipSetDevice(device));
+    DeviceGuard dg(device);
+    char bus[64] = "";
+    MI_HIP(hipDeviceGetPCIBusId(bus, (int)sizeof(bus), device));
     auto *c = new mi355x_comm();
     c->rank = rank;
     c->size = size;
@@ -998,12 +1149,21 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     const size_t bytes = ctrl_bytes(size);
     int fd = -1;
     if (rank == 0) {
-        shm_unlink(c->shm_name.c_str());
+        // the key must be node-unique (coll/mi355x: rank 0's pid + a counter + random bits,
+        // broadcast at enable time); an existing segment of that name belongs to somebody else
+        // and is never unlinked here
         fd = shm_open(c->shm_name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
-        if (fd < 0 || ftruncate(fd, (off_t)bytes) != 0) {
-            if (fd >= 0) close(fd);
+        if (fd < 0) {
+            const int e = errno;
             delete c;
-            return set_error(MI355X_ERR_PEER, "shm_open(%s) failed", key);
+            return set_error(MI355X_ERR_PEER, "control segment %s: %s%s", key, strerror(e),
+                             e == EEXIST ? " (the rendezvous key is in use by another communicator)" : "");
+        }
+        if (ftruncate(fd, (off_t)bytes) != 0) {
+            close(fd);
+            shm_unlink(c->shm_name.c_str());
+            delete c;
+            return set_error(MI355X_ERR_PEER, "ftruncate of control segment %s failed", key);
         }
     } else {
         const auto t0 = std::chrono::steady_clock::now();
@@ -1047,8 +1207,19 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     }
     c->ctrl->slot[rank].pid = (int32_t)getpid();
     c->ctrl->slot[rank].dev = device;
+    uint64_t uid = 1469598103934665603ull;
+    for (const char *p = bus; *p; ++p) uid = (uid ^ (unsigned char)tolower((unsigned char)*p)) * 1099511628211ull;
+    c->ctrl->slot[rank].dev_uid = uid;
     c->ctrl->attached.fetch_add(1);
-    int rc = barrier(c);  // everybody mapped the segment: its name can go
+    int rc = size > 1 ? fd_sock_open(c) : MI355X_SUCCESS;
+    if (rc) {
+        c->ctrl->abort_flag.store(1);  // the others leave their creation barrier with an error
+        if (rank == 0) shm_unlink(c->shm_name.c_str());
+        const std::string msg = mi355x_last_error();
+        mi355x_comm_destroy(c);
+        return set_error(rc, "%s", msg.c_str());
+    }
+    rc = barrier(c);  // everybody mapped the segment and bound its socket: the name can go
     if (rank == 0) shm_unlink(c->shm_name.c_str());
     if (rc == MI355X_SUCCESS && size > 1 && c->ll_max > 0) rc = ll_selftest(c);
     if (rc) {
@@ -1062,7 +1233,6 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
 int mi355x_comm_create_loopback(int size, int device, mi355x_comm_t **comms)
 {
     if (!comms || size < 1 || size > kMaxRanks) return set_error(MI355X_ERR_ARG, "bad loopback arguments");
-    MI_HIP(hipSetDevice(device));
     auto shared = std::make_shared<LoopShared>();
     shared->ctrl = (Ctrl *)calloc(1, ctrl_bytes(size));
     if (!shared->ctrl) return set_error(MI355X_ERR_NOMEM, "calloc");
@@ -1094,14 +1264,17 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
         c->q_cv.notify_all();
         c->worker.join();
     }
-    (void)hipSetDevice(c->device);
+    DeviceGuard dg(c->device);
     p2p_destroy(c);
     for (hipEvent_t e : c->tev)
         if (e) (void)hipEventDestroy(e);
     if (c->nb_stream) (void)hipStreamDestroy(c->nb_stream);
     for (auto &kv : c->peer_maps) close_map(kv.second);
     for (LocalReg &r : c->local_regs) drop_reg(r);
-    for (auto &kv : c->pidfds) close(kv.second);
+    for (auto &kv : c->fd_stash) close(kv.second);
+    if (c->fd_sock >= 0) close(c->fd_sock);
+    if (c->pipe_base) (void)hipFree(c->pipe_base);
+    if (c->pipe_queue) (void)hipFree(c->pipe_queue);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->stage) (void)hipFree(c->stage);
     if (c->ll_base) (void)hipFree(c->ll_base);
@@ -1119,6 +1292,7 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
 int mi355x_comm_set_rules(mi355x_comm_t *c, const mi355x_rules_t *rules)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    DeviceGuard dg(c->device);
     drain(c);
     c->rules = rules;
     return MI355X_SUCCESS;
@@ -1129,6 +1303,7 @@ int mi355x_comm_size(const mi355x_comm_t *c) { return c ? c->size : -1; }
 int mi355x_comm_barrier(mi355x_comm_t *c)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    DeviceGuard dg(c->device);
     drain(c);
     return barrier(c);
 }
@@ -1191,7 +1366,7 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
     case MI355X_KNOB_TIME_PHASES:
         c->time_phases = value != 0;
         if (c->time_phases && !c->tev[0]) {
-            MI_HIP(hipSetDevice(c->device));
+            DeviceGuard dg(c->device);
             for (hipEvent_t &e : c->tev) MI_HIP(hipEventCreate(&e));
         }
         break;
@@ -1730,6 +1905,7 @@ static int bcast_impl(mi355x_comm_t *c, void *buf, size_t bytes, int root, void 
 int mi355x_allreduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, void *stream)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    DeviceGuard dg(c->device);
     drain(c);
     return allreduce_impl(c, sbuf, rbuf, count, type, op, stream);
 }
@@ -1737,6 +1913,7 @@ int mi355x_reduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, 
                   void *stream)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    DeviceGuard dg(c->device);
     drain(c);
     return reduce_impl(c, sbuf, rbuf, count, type, op, root, stream);
 }
@@ -1744,6 +1921,7 @@ int mi355x_reduce_scatter_block(mi355x_comm_t *c, const void *sbuf, void *rbuf, 
                                 void *stream)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    DeviceGuard dg(c->device);
     drain(c);
     return reduce_scatter_block_impl(c, sbuf, rbuf, rcount, type, op, stream);
 }
@@ -1751,18 +1929,21 @@ int mi355x_reduce_scatter(mi355x_comm_t *c, const void *sbuf, void *rbuf, const 
                           void *stream)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    DeviceGuard dg(c->device);
     drain(c);
     return reduce_scatter_impl(c, sbuf, rbuf, rcounts, type, op, stream);
 }
 int mi355x_allgather(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, void *stream)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    DeviceGuard dg(c->device);
     drain(c);
     return allgather_impl(c, sbuf, rbuf, bytes, stream);
 }
 int mi355x_bcast(mi355x_comm_t *c, void *buf, size_t bytes, int root, void *stream)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    DeviceGuard dg(c->device);
     drain(c);
     return bcast_impl(c, buf, bytes, root, stream);
 }

@@ -268,6 +268,7 @@ int mi355x_gatherv(mi355x_comm_t *c, const void *sbuf, size_t sbytes, void *rbuf
                    const size_t *displs, int root, void *stream)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    DeviceGuard dg(c->device);
     drain(c);
     return gatherv_impl(c, sbuf, sbytes, rbuf, rcounts, displs, root, stream);
 }
@@ -277,6 +278,7 @@ int mi355x_gather(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, 
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     std::vector<size_t> cnt((size_t)c->size, bytes), dsp((size_t)c->size);
     for (int q = 0; q < c->size; ++q) dsp[(size_t)q] = (size_t)q * bytes;
+    DeviceGuard dg(c->device);
     drain(c);
     return gatherv_impl(c, sbuf, bytes, rbuf, cnt.data(), dsp.data(), root, stream);
 }
@@ -285,6 +287,7 @@ int mi355x_scatterv(mi355x_comm_t *c, const void *sbuf, const size_t *scounts, c
                     size_t rbytes, int root, void *stream)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    DeviceGuard dg(c->device);
     drain(c);
     return scatterv_impl(c, sbuf, scounts, displs, rbuf, rbytes, root, stream);
 }
@@ -294,6 +297,7 @@ int mi355x_scatter(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t bytes,
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     std::vector<size_t> cnt((size_t)c->size, bytes), dsp((size_t)c->size);
     for (int q = 0; q < c->size; ++q) dsp[(size_t)q] = (size_t)q * bytes;
+    DeviceGuard dg(c->device);
     drain(c);
     return scatterv_impl(c, sbuf, cnt.data(), dsp.data(), rbuf, bytes, root, stream);
 }
@@ -302,6 +306,7 @@ int mi355x_allgatherv(mi355x_comm_t *c, const void *sbuf, size_t sbytes, void *r
                       const size_t *displs, void *stream)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    DeviceGuard dg(c->device);
     drain(c);
     return allgatherv_impl(c, sbuf, sbytes, rbuf, rcounts, displs, stream);
 }
@@ -310,6 +315,7 @@ int mi355x_alltoallv(mi355x_comm_t *c, const void *sbuf, const size_t *scounts, 
                      const size_t *rcounts, const size_t *rdispls, void *stream)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    DeviceGuard dg(c->device);
     drain(c);
     return alltoallv_impl(c, sbuf, scounts, sdispls, rbuf, rcounts, rdispls, stream);
 }
@@ -319,6 +325,7 @@ int mi355x_alltoall(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t bytes
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     std::vector<size_t> cnt((size_t)c->size, bytes), dsp((size_t)c->size);
     for (int q = 0; q < c->size; ++q) dsp[(size_t)q] = (size_t)q * bytes;
+    DeviceGuard dg(c->device);
     drain(c);
     return alltoallv_impl(c, sbuf, cnt.data(), dsp.data(), rbuf, cnt.data(), dsp.data(), stream);
 }
@@ -326,6 +333,7 @@ int mi355x_alltoall(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t bytes
 int mi355x_scan(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, void *stream)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    DeviceGuard dg(c->device);
     drain(c);
     return scan_impl(c, sbuf, rbuf, count, type, op, false, stream);
 }
@@ -333,6 +341,7 @@ int mi355x_scan(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, in
 int mi355x_exscan(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, void *stream)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    DeviceGuard dg(c->device);
     drain(c);
     return scan_impl(c, sbuf, rbuf, count, type, op, true, stream);
 }

@@ -64,6 +64,7 @@ struct alignas(64) RankSlot {
     uint64_t probe_size;
     int64_t varg[2 * kMaxRanks];  // per-peer counts / displacements of v-collectives (bytes)
     int32_t ll_ok, pad_ll;        // LL self-test result at creation (1 ok, 2 failed)
+    uint64_t dev_uid;             // hash of the device's PCI bus id: ranks sharing one GPU
 };
 
 struct Ctrl {
@@ -141,6 +142,7 @@ struct LocalReg {
     hipIpcMemHandle_t h;
     bool has_h;       // false: too large for hipIpc* (never passed to hipIpcGetMemHandle)
     int fd;           // dmabuf export of a large allocation (-1: none yet)
+    uint64_t sent;    // bit q: the dmabuf fd went to rank q (SCM_RIGHTS, once per peer)
 };
 
 inline void drop_reg(LocalReg &r)
@@ -194,8 +196,11 @@ struct mi355x_comm {
     void *scratch = nullptr;
     size_t scratch_bytes = 0;
     int dmabuf_state = 0;                         // large allocations via dmabuf: 0 unknown, 1 yes, -1 no
-    bool ptracer_any = false;                     // PR_SET_PTRACER_ANY done (peers pidfd_getfd our fds)
-    std::map<int, int> pidfds;                    // peer rank -> pidfd
+    // dmabuf fds travel between ranks as SCM_RIGHTS ancillary data over one AF_UNIX datagram
+    // socket per rank (abstract name derived from the control segment's name); received fds wait
+    // here, keyed by (exporting rank, allocation id), until a mapping needs them
+    int fd_sock = -1;
+    std::map<std::pair<int, uint64_t>, int> fd_stash;
     void *stage = nullptr;                        // staging buffer of the staged data flow
     size_t stage_bytes = (size_t)1 << 30;         // its size (an allocation below ipc_max)
     size_t ipc_max = (size_t)1 << 31;             // allocations >= this are never exported
@@ -206,6 +211,15 @@ struct mi355x_comm {
     std::vector<char *> ll_peer;                  // every rank's LL region, mapped
     uint64_t ll_seq = 0;
     uint32_t *ll_err = nullptr;                   // host-visible timeout word
+    // pipelined allreduce (coll_pipe.hip): per-chunk ready flags in an uncached region that
+    // every peer writes into (row q = flags raised by rank q), and the work-queue counter
+    char *pipe_base = nullptr;
+    size_t pipe_kmax = 0;                         // flags per row (chunks per ring block, max)
+    std::vector<char *> pipe_peer;                // every rank's flag region, mapped
+    uint64_t *pipe_queue = nullptr;               // device work-queue counter (monotonic)
+    uint64_t pipe_qbase = 0;                      // its value when the next launch starts
+    uint64_t pipe_seq = 0;                        // calls of the pipelined flow so far
+    int pipe_share = 0;                           // ranks of this communicator on my GPU (0: unknown)
     // nonblocking collectives: one progress thread per communicator runs the posted calls in
     // order on its own stream; blocking calls first wait until nothing is pending
     std::thread worker;
@@ -232,7 +246,9 @@ namespace mi355x {
 // shared by coll_comm.cpp and p2p.cpp
 int barrier(mi355x_comm *c);
 int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force);
-int export_dmabuf(mi355x_comm *c, BufDesc *d);
+// export the large allocation of `d` as a dmabuf fd and pass it to every rank in `peers` that
+// has not received it yet
+int export_dmabuf(mi355x_comm *c, BufDesc *d, uint64_t peers);
 int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **entry = nullptr);
 // publish nbuf buffers, meet every rank, map every rank's buffers: peers[b][r] (coll_comm.cpp)
 int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t sig[4],

@@ -73,7 +73,7 @@ static P2P *p2p_of(mi355x_comm *c)
 static int p2p_stream(mi355x_comm *c, P2P *p, hipStream_t *s)
 {
     if (!p->stream) {
-        MI_HIP(hipSetDevice(c->device));
+        DeviceGuard dg(c->device);
         MI_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
     }
     *s = p->stream;
@@ -243,6 +243,7 @@ static void drain_mailboxes(mi355x_comm *c, P2P *p)
 
 int p2p_progress(mi355x_comm *c)
 {
+    DeviceGuard dg(c->device);
     P2P *p = p2p_of(c);
     std::lock_guard<std::recursive_mutex> g(p->mtx);
     // 1. announce queued sends, in order; a destination whose ring is full holds its later sends
@@ -349,6 +350,7 @@ static int isend(mi355x_comm *c, const void *buf, size_t count, const mi355x_ddt
         delete r;
         return rc;
     }
+    DeviceGuard dg(c->device);
     P2P *p = p2p_of(c);
     std::lock_guard<std::recursive_mutex> g(p->mtx);
     auto bail = [&](int code) {
@@ -383,7 +385,7 @@ static int isend(mi355x_comm *c, const void *buf, size_t count, const mi355x_ddt
             if ((env && atoi(env) == 0) || c->dmabuf_state == -1)
                 return bail(set_error(MI355X_ERR_UNSUPPORTED,
                                       "send buffer in an allocation of >= %zu bytes needs the dmabuf export", c->ipc_max));
-            if ((rc = export_dmabuf(c, &desc))) return bail(rc);
+            if ((rc = export_dmabuf(c, &desc, 1ull << dest))) return bail(rc);
         }
     }
     std::memcpy(&r->desc, &desc, sizeof(desc));

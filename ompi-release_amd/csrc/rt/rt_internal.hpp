@@ -25,6 +25,28 @@ int set_error(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3
 // number of compute units of the current device (cached per device)
 int device_cu_count();
 
+// Makes `dev` current for the scope and restores the caller's device afterwards: the engine
+// never leaves the application's current device changed (an MPI call must not move later
+// application allocations to another GPU).
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev)
+    {
+        int cur = -1;
+        if (hipGetDevice(&cur) != hipSuccess) {
+            (void)hipGetLastError();
+            cur = -1;
+        }
+        if (cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+};
+
 // caller stream as a hipStream_t (NULL = the HIP null stream)
 hipStream_t resolve_stream(void *stream);
 

@@ -13,7 +13,7 @@ sys.path.insert(0, str(pathlib.Path(__file__).parent))
 from conftest import load_oracle  # noqa: E402
 from mini import mini  # noqa: E402
 import opdata  # noqa: E402
-from ddtcases import OPAL_FLOAT4, opal_strided_elems, opal_vector  # noqa: E402
+from ddtcases import OPAL_FLOAT4, OPAL_INT4, opal_strided_elems, opal_vector  # noqa: E402
 
 
 SENT = 0xA5
@@ -194,6 +194,7 @@ def movement(m, comm, oracle, rank, size, torch, ptrs):
         assert fn(comm, dx.data_ptr(), dr.data_ptr(), count, fdt, op) == 0
         if not (exclusive and rank == 0):
             opdata.assert_same("FLOAT", "SUM", dr.cpu().numpy().view(np.float32), want[rank], "component scan")
+    resized_column(m, comm, rank, size, torch)
     # host buffers -> the stub
     h = np.zeros(64, dtype=np.int32)
     before = L.mini_stub_calls(7)
@@ -204,7 +205,80 @@ def movement(m, comm, oracle, rank, size, torch, ptrs):
     m.lib.mini_op_destroy(op)
 
 
+def resized_column(m, comm, rank, size, torch):
+    """MPI_Gather where ONLY the root's layout is derived: the root receives rank q's n ints into
+    column q of an n x size int matrix (vector(n, 1, size, MPI_INT) resized to extent 4), the others
+    send plain MPI_INT -- the path must not depend on the rank-local layout (else the root would
+    fall back while the others enter the engine).  Then MPI_Scatter back out of the columns and
+    MPI_Alltoall with the same column type on the receive side only."""
+    L, pkg = m.lib, m.pkg
+    n = 257
+    idt = m.dtype_for_slot(pkg.T["INT32"])
+    desc, used, tsize, _, true_ub = opal_strided_elems(n, OPAL_INT4, 4, 4 * size)
+    col = L.mini_datatype_create_raw(desc, used, tsize, 0, 4, 0, true_ub, 0)  # MPI_Type_create_resized(.., 0, 4)
+    root = size - 1
+    mine = torch.arange(n, dtype=torch.int32, device="cuda") * 100 + rank
+    mat = torch.full((n * size,), -7, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    if rank == root:
+        assert L.mini_gather(comm, mine.data_ptr(), n, idt, mat.data_ptr(), 1, col, root) == 0
+        want = (torch.arange(n, dtype=torch.int32).view(n, 1) * 100 + torch.arange(size, dtype=torch.int32).view(1, size))
+        assert torch.equal(mat.cpu().view(n, size), want), "gather into a resized column type at the root"
+    else:
+        assert L.mini_gather(comm, mine.data_ptr(), n, idt, None, 1, col, root) == 0
+    back = torch.zeros(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    assert L.mini_scatter(comm, mat.data_ptr() if rank == root else None, 1, col, back.data_ptr(), n, idt, root) == 0
+    assert torch.equal(back, mine), "scatter out of a resized column type at the root"
+    # alltoall: rank r sends block q = n ints (r, q) dense; receives into columns of its matrix
+    snd = torch.cat([torch.arange(n, dtype=torch.int32) * 1000 + rank * 10 + q for q in range(size)]).cuda()
+    got = torch.full((n * size,), -1, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    assert L.mini_alltoall(comm, snd.data_ptr(), n, idt, got.data_ptr(), 1, col) == 0
+    want = torch.arange(n, dtype=torch.int32).view(n, 1) * 1000 + torch.arange(size, dtype=torch.int32).view(1, size) * 10 + rank
+    assert torch.equal(got.cpu().view(n, size), want), "alltoall into resized column types"
+    L.mini_datatype_destroy(col)
+
+
+def split_main():
+    """MPI_Comm_split with two colors on one node: world ranks {0,1} and {2,3} form two
+    2-rank communicators with the SAME job id and the SAME context id (Open MPI 1.8 allocates one
+    cid over the parent for every color, comm.c:610); each group selects coll/mi355x and runs
+    collectives at the same time as the other -- each must see only its own members"""
+    wrank = int(sys.argv[1])
+    group, rank, size = wrank // 2, wrank % 2, 2
+    import torch
+    torch.cuda.set_device(wrank % torch.cuda.device_count())
+    m = mini()
+    oracle = load_oracle()
+    m.install_oracle_base(oracle)
+    comm = m.lib.mini_comm_create(rank, size, 42)
+    m.lib.mini_comm_set_channel(comm, f"{sys.argv[3]}_g{group}".encode())
+    m.lib.mini_comm_install(comm, m.lib.mini_stub_module())
+    assert m.lib.mini_coll_select(comm, m.component_ptr(m.coll, "mca_coll_mi355x_component")) == 90
+    pkg = m.pkg
+    fdt = m.dtype_for_slot(pkg.T["FLOAT"])
+    op = m.select_op(pkg.OP["SUM"])
+    for it in range(20):
+        for count in (1000, 300_001):
+            x = torch.full((count,), float(100 * group + rank + it), device="cuda")
+            y = torch.empty_like(x)
+            torch.cuda.synchronize()
+            assert m.lib.mini_allreduce(comm, x.data_ptr(), y.data_ptr(), count, fdt, op) == 0
+            want = float(2 * (100 * group + it) + 1)
+            assert bool((y == want).all()), (group, it, count, float(y[0]), want)
+        b = torch.full((5000,), float(1000 * group + rank), device="cuda")
+        torch.cuda.synchronize()
+        assert m.lib.mini_bcast(comm, b.data_ptr(), 5000, fdt, 1) == 0
+        assert bool((b == 1000 * group + 1).all()), ("split bcast", group)
+    m.lib.mini_op_destroy(op)
+    m.lib.mini_comm_destroy(comm)
+    print(f"rank {wrank} split OK", flush=True)
+
+
 def main():
+    if len(sys.argv) > 4 and sys.argv[4] == "split":
+        return split_main()
     rank, size = int(sys.argv[1]), int(sys.argv[2])
     import torch
     ndev = torch.cuda.device_count()
@@ -213,6 +287,7 @@ def main():
     oracle = load_oracle()
     m.install_oracle_base(oracle)
     comm = m.lib.mini_comm_create(rank, size, 42)
+    m.lib.mini_comm_set_channel(comm, sys.argv[3].encode())
     m.lib.mini_comm_install(comm, m.lib.mini_stub_module())
     prio = m.lib.mini_coll_select(comm, m.component_ptr(m.coll, "mca_coll_mi355x_component"))
     assert prio == 90, prio

@@ -191,6 +191,34 @@ def large_calls(pkg, comm, rank, size, torch):
         torch.cuda.empty_cache()
 
 
+def _pattern_chunk(torch, lo, hi):
+    """int32 words lo..hi-1 of the big-bcast pattern (an LCG of the word index, wraps in int32)"""
+    return torch.arange(lo, hi, dtype=torch.int32, device="cuda") * 1103515245 + 12345
+
+
+def big_bcast(pkg, comm, rank, size, torch):
+    """BASELINE configs[4]: a 4 GiB MPI_Bcast (MPI_FLOAT x 2^30) on a >= 2 GiB allocation (the
+    dmabuf path: hipIpcOpenMemHandle cannot map it), root size-1, every word checked exactly"""
+    nbytes = 4 << 30
+    words = nbytes // 4
+    chunk = 1 << 26
+    buf = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
+    b32 = buf.view(torch.int32)
+    root = size - 1
+    if rank == root:
+        for lo in range(0, words, chunk):
+            b32[lo:lo + chunk] = _pattern_chunk(torch, lo, lo + chunk)
+    torch.cuda.synchronize()
+    comm.bcast(buf.data_ptr(), nbytes, root)
+    assert comm.last_algorithm() == 2, comm.last_algorithm()  # scatter + allgather shape
+    for lo in range(0, words, chunk):
+        assert torch.equal(b32[lo:lo + chunk], _pattern_chunk(torch, lo, lo + chunk)), ("4 GiB bcast", lo)
+    comm.barrier()
+    del buf, b32
+    torch.cuda.empty_cache()
+    print(f"rank {rank} bcast4g OK", flush=True)
+
+
 def p2p_checks(pkg, comm, rank, size, oracle, torch):
     """device point-to-point across processes (IPC-mapped sender buffers pulled by the receiver)"""
     def pattern(src, n, salt):
@@ -296,6 +324,8 @@ def main():
     ll_checks(pkg, comm, rank, size, oracle, torch)
     p2p_checks(pkg, comm, rank, size, oracle, torch)
     staged(pkg, comm, rank, size, torch, key)
+    if size in (2, 3):
+        big_bcast(pkg, comm, rank, size, torch)
     comm.barrier()
     comm.destroy()
     print(f"rank {rank} OK", flush=True)

@@ -41,6 +41,7 @@ class Mini:
         L.mini_comm_create.restype = vp
         L.mini_comm_create.argtypes = [i, i, ctypes.c_uint]
         L.mini_comm_install.argtypes = [vp, vp]
+        L.mini_comm_set_channel.argtypes = [vp, ctypes.c_char_p]
         L.mini_coll_select.argtypes = [vp, vp]
         L.mini_coll_module_new.restype = vp
         L.mini_comm_destroy.argtypes = [vp]

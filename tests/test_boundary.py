@@ -192,3 +192,41 @@ def test_coll_comm_query(monkeypatch):
     _coll_env(monkeypatch, world=16, local=8)
     c2 = m.lib.mini_comm_create(0, 4, 9)
     assert _comm_query(m, c2)[0] is None
+
+
+def _chan_rank(rank, size, name, q):
+    try:
+        m = mini()
+        L = m.lib
+        comm = L.mini_comm_create(rank, size, 11)
+        assert L.mini_comm_set_channel(comm, name.encode()) == 0
+        L.mini_comm_install(comm, L.mini_stub_module())
+        byte = ctypes.addressof(ctypes.c_char.in_dll(L, "ompi_mpi_byte"))
+        for k in range(50):
+            root = k % size
+            buf = (ctypes.c_char * 64)()
+            if rank == root:
+                buf.value = f"key-{k}-{root}".encode()
+            assert L.mini_bcast(comm, ctypes.addressof(buf), 64, byte, root) == 0
+            assert buf.value == f"key-{k}-{root}".encode(), (k, buf.value)
+        L.mini_comm_destroy(comm)
+        q.put((rank, "ok"))
+    except BaseException as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+def test_harness_host_bcast_channel():
+    """the harness's stand-in for the lower-priority modules' host transport (what coll/mi355x's
+    module_enable uses to agree on its rendezvous key): 3 processes, 50 bcasts with rotating roots"""
+    import multiprocessing as mp
+    import uuid
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    name = "t" + uuid.uuid4().hex[:10]
+    ps = [ctx.Process(target=_chan_rank, args=(r, 3, name, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(30)
+    assert res == {0: "ok", 1: "ok", 2: "ok"}, res

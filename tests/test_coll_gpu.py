@@ -111,6 +111,43 @@ def _allreduce_cases(torch, pkg, oracle, cs, n, alg, inplace):
             assert cs[0].last_algorithm() == ran
 
 
+@pytest.mark.parametrize("n", [3, 4, 8])
+def test_segmented_ring_region(gpu, pkg, oracle, comms, n):
+    """the fixed decision's segmented-ring region at n >= 3 (counts above n x segcount, 1 MiB
+    segments; coll_tuned_allreduce.c:635-873, coll_tuned_decision_fixed.c:64-80), where the ring's
+    per-element fold order is order-sensitive: N(0,1) fp32 SUM and C_DOUBLE_COMPLEX PROD,
+    one phase and three phases with a ragged remainder, compared bit-exact with the oracle's
+    phase-by-phase simulation"""
+    torch = gpu
+    cs = comms(n)
+    for c in cs:
+        c.set("ALLREDUCE_ALG", 0)
+    for opname, tname in (("SUM", "FLOAT"), ("PROD", "C_DOUBLE_COMPLEX")):
+        op, ty = pkg.OP[opname], pkg.T[tname]
+        seg = (1 << 20) // pkg.type_size(ty)
+        ns = n * seg
+        for count in (ns + seg // 2 + 7, 2 * ns + (3 * ns) // 5 + 13):
+            xs = [opdata.make(tname, count, 4000 + 17 * n + r) for r in range(n)]
+            outs = [np.zeros_like(xs[0]) for _ in range(n)]
+            assert oracle.oracle_allreduce(0, n, count, ty, op, 0, _ptrs(xs), _ptrs(outs)) == 5
+            dx = [to_dev(torch, x) for x in xs]
+            dr = [torch.zeros_like(t) for t in dx]
+            torch.cuda.synchronize()
+            run_ranks(n, lambda r: cs[r].allreduce(dx[r].data_ptr(), dr[r].data_ptr(), count, ty, op))
+            torch.cuda.synchronize()
+            assert cs[0].last_algorithm() == 5
+            for r in range(n):
+                opdata.assert_same(tname, opname, from_dev(dr[r], outs[r]), outs[r],
+                                   f"segmented ring n={n} count={count} rank={r}")
+            # the result really is order-sensitive: a naive rank-order fold differs somewhere
+            if opname == "SUM":
+                naive = xs[0].copy()
+                for q in range(1, n):
+                    naive = (naive + xs[q]).astype(np.float32)
+                assert len(opdata.mismatches("FLOAT", "SUM", naive, outs[0])) > 0
+            del dx, dr
+
+
 @pytest.mark.parametrize("n", [2, 3, 5, 8])
 @pytest.mark.parametrize("alg", [0, 1, 2, 3, 4, 5])
 def test_reduce(gpu, pkg, oracle, comms, n, alg):

@@ -82,7 +82,7 @@ def test_coll_component_processes(gpu, size):
     procs = []
     for r in range(size):
         e = dict(env, OMPI_COMM_WORLD_LOCAL_RANK=str(r), OMPI_COMM_WORLD_RANK=str(r))
-        procs.append(subprocess.Popen([sys.executable, str(HERE / "coll_worker.py"), str(r), str(size)], env=e,
+        procs.append(subprocess.Popen([sys.executable, str(HERE / "coll_worker.py"), str(r), str(size), key], env=e,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = []
     for p in procs:
@@ -94,3 +94,26 @@ def test_coll_component_processes(gpu, size):
         outs.append(out)
     for r, p in enumerate(procs):
         assert p.returncode == 0, f"rank {r}:\n{outs[r][-3000:]}"
+
+
+def test_split_communicators_same_cid(gpu):
+    """two disjoint 2-rank communicators of one job with the same context id (the MPI_Comm_split
+    case, comm.c:610) selecting coll/mi355x and running collectives concurrently: the rendezvous
+    key is agreed per communicator (rank 0 picks it, the lower-priority bcast spreads it), so the
+    groups never meet in one control segment"""
+    key = uuid.uuid4().hex[:10]
+    env = dict(os.environ, MI355X_TIMEOUT_S="60", OMPI_COMM_WORLD_SIZE="4", OMPI_COMM_WORLD_LOCAL_SIZE="4",
+               OMPI_MCA_ess_base_jobid=key)
+    procs = [subprocess.Popen([sys.executable, str(HERE / "coll_worker.py"), str(w), "4", key, "split"],
+                              env=dict(env, OMPI_COMM_WORLD_LOCAL_RANK=str(w), OMPI_COMM_WORLD_RANK=str(w)),
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for w in range(4)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=300)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, _ = p.communicate()
+        outs.append(out)
+    for w, p in enumerate(procs):
+        assert p.returncode == 0 and f"rank {w} split OK" in outs[w], f"rank {w}:\n{outs[w][-3000:]}"

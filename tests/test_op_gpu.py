@@ -107,6 +107,48 @@ def test_small_counts(gpu, pkg, oracle):
             opdata.assert_same(tname, opname, _host(tb, 0, want), want, f"n={n}")
 
 
+def test_golden_specials_on_device(gpu, pkg):
+    """every case of tests/golden/op_specials.json (outputs of the reference's compiled op loops:
+    MAX/MIN NaN and signed-zero operand order, int8/int32 wrap) through the HIP kernels, 2-buff as
+    (out, in) and 3-buff as (in1, in2), each case also embedded in a vector body (lane 37 of 4099)
+    so the 16-B vector path sees it as well as the scalar path"""
+    import json
+    import pathlib
+    torch = gpu
+    cases = json.loads((pathlib.Path(__file__).parent / "golden" / "op_specials.json").read_text())["cases"]
+    assert len(cases) >= 10
+    dts = {"FLOAT": np.float32, "DOUBLE": np.float64, "INT8": np.int8, "INT32": np.int32}
+    stream = torch.cuda.current_stream().cuda_stream
+    for c in cases:
+        dt = dts[c["type"]]
+        op, ty = pkg.OP[c["op"]], pkg.T[c["type"]]
+        vals = [float.fromhex(v) if isinstance(v, str) and v != "nan" else (float("nan") if v == "nan" else v)
+                for v in c["args"]]
+        for n, at in ((1, 0), (4099, 37)):
+            first = np.ones(n, dtype=dt)
+            second = np.ones(n, dtype=dt)
+            first[at], second[at] = vals[0], vals[1]
+            t1, p1 = _dev(torch, first)
+            t2, p2 = _dev(torch, second)
+            if c["form"] == "2buff":   # args = (out, in): inout holds the first
+                pkg.op_reduce(op, ty, p2, p1, n, stream)
+                torch.cuda.synchronize()
+                got = _host(t1, 0, first)[at]
+            else:                      # args = (in1, in2)
+                to, po = _dev(torch, np.zeros(n, dtype=dt))
+                pkg.op_reduce_3buff(op, ty, p1, p2, po, n, stream)
+                torch.cuda.synchronize()
+                got = _host(to, 0, first)[at]
+            want = c["want"]
+            if want == "nan":
+                assert np.isnan(got), (c, n, got)
+            elif isinstance(want, str):
+                w = float.fromhex(want)
+                assert got == w and np.signbit(got) == np.signbit(w), (c, n, got)
+            else:
+                assert got == want, (c, n, got)
+
+
 def test_large_fp32_sum_property(gpu, pkg):
     """1 GiB-class buffer (BASELINE config 2 size): out = in1 + in2 on exactly-representable
     values, checked on device against torch's own add (a size-independent property: the sum of
