@@ -124,13 +124,19 @@ enum mi355x_knob {
                                            default 64 KiB; multi-process communicators only) */
     MI355X_KNOB_TIME_PHASES = 11,       /* 1: time the two kernels of the direct allreduce with HIP
                                            events on the call's stream (mi355x_comm_phase_ms) */
-    MI355X_KNOB_COPY_BLOCK_KIB = 12     /* bytes per block of the pull-copy kernel, KiB (4..256, default 4) */
+    MI355X_KNOB_COPY_BLOCK_KIB = 12,    /* bytes per block of the pull-copy kernel, KiB (4..256, default 4) */
+    MI355X_KNOB_PIPE = 13               /* 1 (default): a multi-process ring allreduce runs its reduce and
+                                           copy phases in ONE pipelined launch per rank, overlapped
+                                           chunk by chunk with device-side ready flags (the segmented
+                                           ring's copy/reduce overlap, coll_tuned_allreduce.c:721-831);
+                                           0: two phases separated by a host barrier */
 };
 int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
 /* current value of a knob (LL_MAX_BYTES reads 0 when the creation-time LL self-test failed) */
 int mi355x_comm_get(const mi355x_comm_t *comm, int knob, long *value);
 /* device time of the last timed direct allreduce: phase 1 (k_fold, the owner's block from every
- * rank) and phase 2 (k_multicopy, the other blocks from their owners); -1 when not measured */
+ * rank) and phase 2 (k_multicopy, the other blocks from their owners); with the pipelined flow
+ * phase 1 is the one launch (k_pipe_allreduce) and phase 2 is 0; -1 when not measured */
 int mi355x_comm_phase_ms(const mi355x_comm_t *comm, float *phase1_ms, float *phase2_ms);
 
 /* coll/tuned's dynamic rules file (coll_tuned_dynamic_file.c:56-251; MCA

@@ -68,6 +68,8 @@ CollTune &coll_tune()
 
 namespace mi355x {
 
+static int fd_drain(mi355x_comm *c, bool wait);
+
 // ----------------------------------------------------------------- barrier
 int barrier(mi355x_comm *c)
 {
@@ -86,6 +88,11 @@ int barrier(mi355x_comm *c)
             return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
         if (++spins > 2048) {
             sched_yield();
+            // a peer may be blocked sending us dmabuf fds (full socket queue): drain it while we wait
+            if (c->fd_sock >= 0 && (spins & 255) == 0 && c->reg_mtx.try_lock()) {
+                (void)fd_drain(c, false);
+                c->reg_mtx.unlock();
+            }
             if ((spins & 0xffff) == 0) {
                 const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
                 if (el > c->timeout_s) {
@@ -197,10 +204,11 @@ int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
 // no ptrace permission is granted to anybody.  Every rank binds one socket at communicator
 // creation under an abstract name derived from the control segment's (node-unique) name; the
 // receiver checks the sender's pid (SO_PASSCRED) against the rank's published pid.
+constexpr int kFdMax = 8;  // fds per message (a call exports at most kMaxBufs buffers)
 struct FdMsg {
     int32_t from;
-    int32_t pad;
-    uint64_t id;
+    int32_t nfd;
+    uint64_t id[kFdMax];
 };
 
 static void fd_sock_addr(const mi355x_comm *c, int rank, sockaddr_un *a, socklen_t *len)
@@ -231,13 +239,14 @@ static int fd_sock_open(mi355x_comm *c)
     return MI355X_SUCCESS;
 }
 
-// receive every queued fd message into the stash; `wait`: block (bounded) for at least one
+// receive every queued fd message into the stash; `wait`: block (bounded) for at least one.
+// Caller holds reg_mtx.
 static int fd_drain(mi355x_comm *c, bool wait)
 {
     for (;;) {
         FdMsg m;
         iovec iov{&m, sizeof(m)};
-        alignas(cmsghdr) char ctl[CMSG_SPACE(sizeof(int)) + CMSG_SPACE(sizeof(ucred))];
+        alignas(cmsghdr) char ctl[CMSG_SPACE(sizeof(int) * kFdMax) + CMSG_SPACE(sizeof(ucred))];
         msghdr h;
         std::memset(&h, 0, sizeof(h));
         h.msg_iov = &iov;
@@ -259,35 +268,47 @@ static int fd_drain(mi355x_comm *c, bool wait)
             if (errno == EINTR) continue;
             return set_error(MI355X_ERR_PEER, "recvmsg: %s", strerror(errno));
         }
-        int fd = -1;
+        int fds[kFdMax];
+        int nfd = 0;
         pid_t pid = -1;
         for (cmsghdr *cm = CMSG_FIRSTHDR(&h); cm; cm = CMSG_NXTHDR(&h, cm)) {
-            if (cm->cmsg_level == SOL_SOCKET && cm->cmsg_type == SCM_RIGHTS) std::memcpy(&fd, CMSG_DATA(cm), sizeof(int));
+            if (cm->cmsg_level == SOL_SOCKET && cm->cmsg_type == SCM_RIGHTS) {
+                nfd = (int)((cm->cmsg_len - CMSG_LEN(0)) / sizeof(int));
+                if (nfd > kFdMax) nfd = kFdMax;
+                std::memcpy(fds, CMSG_DATA(cm), sizeof(int) * (size_t)nfd);
+            }
             if (cm->cmsg_level == SOL_SOCKET && cm->cmsg_type == SCM_CREDENTIALS) {
                 ucred cr;
                 std::memcpy(&cr, CMSG_DATA(cm), sizeof(cr));
                 pid = cr.pid;
             }
         }
-        const bool ok = got == (ssize_t)sizeof(m) && fd >= 0 && m.from >= 0 && m.from < c->size &&
+        const bool ok = got == (ssize_t)sizeof(m) && nfd > 0 && m.nfd == nfd && m.from >= 0 && m.from < c->size &&
                         pid == (pid_t)c->ctrl->slot[m.from].pid;
-        if (!ok) {  // not from a rank of this communicator: drop it
-            if (fd >= 0) close(fd);
-            continue;
+        for (int i = 0; i < nfd; ++i) {
+            if (!ok) {  // not from a rank of this communicator: drop it
+                close(fds[i]);
+                continue;
+            }
+            const auto key = std::make_pair((int)m.from, m.id[i]);
+            auto it = c->fd_stash.find(key);
+            if (it != c->fd_stash.end()) close(it->second);
+            c->fd_stash[key] = fds[i];
         }
-        const auto key = std::make_pair((int)m.from, m.id);
-        auto it = c->fd_stash.find(key);
-        if (it != c->fd_stash.end()) close(it->second);
-        c->fd_stash[key] = fd;
-        if (wait) return MI355X_SUCCESS;
+        if (wait && ok) return MI355X_SUCCESS;
     }
 }
 
-static int send_fd(mi355x_comm *c, int peer, int fd, uint64_t id)
+// one message carrying nfd fds and their allocation ids to `peer`.  Caller holds reg_mtx.
+static int send_fds(mi355x_comm *c, int peer, const int *fds, const uint64_t *ids, int nfd)
 {
-    FdMsg m{c->rank, 0, id};
+    FdMsg m;
+    std::memset(&m, 0, sizeof(m));
+    m.from = c->rank;
+    m.nfd = nfd;
+    for (int i = 0; i < nfd; ++i) m.id[i] = ids[i];
     iovec iov{&m, sizeof(m)};
-    alignas(cmsghdr) char ctl[CMSG_SPACE(sizeof(int))];
+    alignas(cmsghdr) char ctl[CMSG_SPACE(sizeof(int) * kFdMax)];
     std::memset(ctl, 0, sizeof(ctl));
     sockaddr_un a;
     socklen_t len;
@@ -299,25 +320,28 @@ static int send_fd(mi355x_comm *c, int peer, int fd, uint64_t id)
     h.msg_iov = &iov;
     h.msg_iovlen = 1;
     h.msg_control = ctl;
-    h.msg_controllen = sizeof(ctl);
+    h.msg_controllen = CMSG_SPACE(sizeof(int) * (size_t)nfd);
     cmsghdr *cm = CMSG_FIRSTHDR(&h);
     cm->cmsg_level = SOL_SOCKET;
     cm->cmsg_type = SCM_RIGHTS;
-    cm->cmsg_len = CMSG_LEN(sizeof(int));
-    std::memcpy(CMSG_DATA(cm), &fd, sizeof(int));
+    cm->cmsg_len = CMSG_LEN(sizeof(int) * (size_t)nfd);
+    std::memcpy(CMSG_DATA(cm), fds, sizeof(int) * (size_t)nfd);
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
         if (sendmsg(c->fd_sock, &h, MSG_DONTWAIT | MSG_NOSIGNAL) == (ssize_t)sizeof(m)) return MI355X_SUCCESS;
         if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR)
-            return set_error(MI355X_ERR_PEER, "sending a dmabuf fd to rank %d: %s", peer, strerror(errno));
-        // the peer's queue is full: it may be sending to us -- keep ours drained meanwhile
+            return set_error(MI355X_ERR_PEER, "sending dmabuf fds to rank %d: %s", peer, strerror(errno));
+        // the peer's queue is full (net.unix.max_dgram_qlen): it drains it whenever it waits
+        // (barrier, its own sends, its imports) -- keep ours drained meanwhile too
         int rc = fd_drain(c, false);
         if (rc) return rc;
         if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s)
             return set_error(MI355X_ERR_TIMEOUT, "rank %d: fd queue of rank %d stays full", c->rank, peer);
-        usleep(100);
+        usleep(50);
     }
 }
+
+static int send_fd(mi355x_comm *c, int peer, int fd, uint64_t id) { return send_fds(c, peer, &fd, &id, 1); }
 
 // the fd rank `peer` passed for its allocation `id` (a duplicate: the stash keeps its own)
 static int take_fd(mi355x_comm *c, int peer, uint64_t id, int *out)
@@ -343,28 +367,53 @@ static void drop_stash(mi355x_comm *c, int peer, uint64_t id)
     c->fd_stash.erase(it);
 }
 
-int export_dmabuf(mi355x_comm *c, BufDesc *d, uint64_t peers)
+// export the large allocations of ds[0..nd) as dmabuf fds and pass every one to every rank in
+// `peers` that has not received it yet: one message per peer
+static int export_dmabufs(mi355x_comm *c, BufDesc *const *ds, int nd, uint64_t peers)
 {
     std::lock_guard<std::recursive_mutex> reg_guard(c->reg_mtx);
-    for (LocalReg &r : c->local_regs) {
-        if (r.base != d->base || r.id != d->id) continue;
+    LocalReg *regs[kFdMax];
+    for (int i = 0; i < nd; ++i) {
+        regs[i] = nullptr;
+        for (LocalReg &r : c->local_regs)
+            if (r.base == ds[i]->base && r.id == ds[i]->id) regs[i] = &r;
+        if (!regs[i])
+            return set_error(MI355X_ERR_PEER, "large allocation not registered (id %llu)", (unsigned long long)ds[i]->id);
+        LocalReg &r = *regs[i];
         if (r.fd < 0) {
             MI_HIP(hipMemGetHandleForAddressRange(&r.fd, (hipDeviceptr_t)r.base, r.size,
                                                   hipMemRangeHandleTypeDmaBufFd, 0));
             r.sent = 0;
         }
-        for (int q = 0; q < c->size; ++q) {
-            if (q == c->rank || !((peers >> q) & 1u) || ((r.sent >> q) & 1u)) continue;
-            int rc = send_fd(c, q, r.fd, r.id);
-            if (rc) return rc;
-            r.sent |= 1ull << q;
-        }
-        d->dmabuf = 1;
-        d->fd = r.fd;
-        d->size = r.size;
-        return MI355X_SUCCESS;
+        ds[i]->dmabuf = 1;
+        ds[i]->fd = r.fd;
+        ds[i]->size = r.size;
     }
-    return set_error(MI355X_ERR_PEER, "large allocation not registered (id %llu)", (unsigned long long)d->id);
+    for (int q = 0; q < c->size; ++q) {
+        if (q == c->rank || !((peers >> q) & 1u)) continue;
+        int fds[kFdMax];
+        uint64_t ids[kFdMax];
+        int k = 0;
+        for (int i = 0; i < nd; ++i) {
+            if ((regs[i]->sent >> q) & 1u) continue;
+            bool dup = false;  // two buffers of one allocation: one fd
+            for (int j = 0; j < k; ++j) dup = dup || ids[j] == regs[i]->id;
+            if (dup) continue;
+            fds[k] = regs[i]->fd;
+            ids[k++] = regs[i]->id;
+        }
+        if (!k) continue;
+        int rc = send_fds(c, q, fds, ids, k);
+        if (rc) return rc;
+        for (int i = 0; i < nd; ++i) regs[i]->sent |= 1ull << q;
+    }
+    return MI355X_SUCCESS;
+}
+
+int export_dmabuf(mi355x_comm *c, BufDesc *d, uint64_t peers)
+{
+    BufDesc *ds[1] = {d};
+    return export_dmabufs(c, ds, 1, peers);
 }
 
 static int import_dmabuf(mi355x_comm *c, int peer, uint64_t id, size_t size, void **mapped, hipExternalMemory_t *ext)
@@ -413,12 +462,16 @@ static int probe_dmabuf(mi355x_comm *c)
         ok = false;
     (void)hipGetLastError();
     const uint64_t kProbeId = ~0ull;  // never an allocation id
-    for (int q = 0; q < c->size && ok; ++q)
-        if (q != c->rank && send_fd(c, q, fd, kProbeId) != MI355X_SUCCESS) ok = false;
+    {
+        std::lock_guard<std::recursive_mutex> reg_guard(c->reg_mtx);  // the fd stash
+        for (int q = 0; q < c->size && ok; ++q)
+            if (q != c->rank && send_fd(c, q, fd, kProbeId) != MI355X_SUCCESS) ok = false;
+    }
     me.probe_fd = ok ? 1 : -1;  // 1: my fd went to every peer
     me.probe_size = sz;
     int rc = barrier(c);  // every sent fd is queued at its receiver
     if (rc) return rc;
+    std::unique_lock<std::recursive_mutex> reg_lock(c->reg_mtx);  // the fd stash
     for (int q = 0; q < c->size && ok; ++q) {
         if (q == c->rank) continue;
         const RankSlot &o = c->ctrl->slot[q];
@@ -444,6 +497,7 @@ static int probe_dmabuf(mi355x_comm *c)
         (void)hipGetLastError();
     }
     for (int q = 0; q < c->size; ++q) drop_stash(c, q, kProbeId);
+    reg_lock.unlock();
     me.probe_ok = ok ? 1 : 0;
     rc = barrier(c);  // every rank is done importing before the probe buffers go
     if (fd >= 0) close(fd);
@@ -561,11 +615,14 @@ int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t s
         }
         if (c->dmabuf_state == 1) {
             // second round: the large allocations go out as dmabuf fds, then everything is mapped
+            BufDesc *ds[kMaxBufs];
+            int nd = 0;
             for (int b = 0; b < nbuf; ++b)
-                if (s.buf[b].staged) {
-                    rc = export_dmabuf(c, &s.buf[b], ~0ull);
-                    if (rc) return rc;
-                }
+                if (s.buf[b].staged) ds[nd++] = &s.buf[b];
+            if (nd) {
+                rc = export_dmabufs(c, ds, nd, ~0ull);
+                if (rc) return rc;
+            }
             rc = barrier(c);
             if (rc) return rc;
             any_staged = false;
@@ -964,6 +1021,150 @@ static int ll_selftest(mi355x_comm *c)
     return barrier(c);
 }
 
+// ----------------------------------------------------------------- pipelined allreduce
+// (Re)build the per-chunk flag region (uncached, every peer writes its row into it over xGMI)
+// and the work-queue counter.  Collective: every rank reaches it in the same call.
+constexpr size_t kPipeKmax = 1024;  // chunks per ring block, at most
+static int ensure_pipe(mi355x_comm *c)
+{
+    if (c->pipe_base) return MI355X_SUCCESS;
+    const size_t n = (size_t)c->size;
+    const size_t bytes = (n * kPipeKmax * sizeof(uint64_t) + 4095) / 4096 * 4096;
+    MI_HIP(hipExtMallocWithFlags((void **)&c->pipe_base, bytes, hipDeviceMallocUncached));
+    MI_HIP(hipMemset(c->pipe_base, 0, bytes));
+    MI_HIP(hipMalloc((void **)&c->pipe_queue, sizeof(uint64_t)));
+    MI_HIP(hipMemset(c->pipe_queue, 0, sizeof(uint64_t)));
+    if (!c->ll_err) MI_HIP(hipHostMalloc((void **)&c->ll_err, sizeof(uint32_t), hipHostMallocCoherent));
+    MI_HIP(hipDeviceSynchronize());
+    c->pipe_kmax = kPipeKmax;
+    c->pipe_qbase = 0;
+    c->pipe_seq = 0;
+    const void *mine[1] = {c->pipe_base};
+    const uint64_t sig[4] = {11, bytes, 0, 0};
+    std::vector<std::vector<void *>> P;
+    int rc = exchange(c, 1, mine, sig, P, nullptr, true);
+    if (rc) return rc;
+    c->pipe_peer.assign(n, nullptr);
+    for (size_t q = 0; q < n; ++q) c->pipe_peer[q] = (char *)P[0][q];
+    // ranks of this communicator on my GPU (a one-GPU rehearsal): they split the CUs, so every
+    // rank's persistent grid stays co-resident with the others'
+    int share = 0;
+    for (int q = 0; q < c->size; ++q) share += c->ctrl->slot[q].dev_uid == c->ctrl->slot[c->rank].dev_uid;
+    c->pipe_share = share > 0 ? share : 1;
+    TRACE(c, "pipe region %zu bytes, %d ranks on this GPU", bytes, c->pipe_share);
+    return barrier(c);  // every rank has read the exchange slots
+}
+
+// One launch per rank: fold my ring block and pull the other blocks, chunk by chunk, with
+// device-side readiness flags (coll_pipe.hip).  P[0] = every rank's input, P[1] = every rbuf.
+static int pipe_allreduce(mi355x_comm *c, int op, int type, const Program &pr,
+                          const std::vector<std::vector<void *>> &P, size_t count, hipStream_t s)
+{
+    if (!c->pipe_base) return set_error(MI355X_ERR_ARG, "pipelined allreduce before its setup");
+    int rc = MI355X_SUCCESS;
+    const size_t esz = mi355x_type_size(type), n = (size_t)c->size;
+    PipeArgs a;
+    std::memset(&a, 0, sizeof(a));
+    size_t maxlen = 0;
+    for (int q = 0; q < c->size; ++q) {
+        size_t o, l;
+        ring_block(count, c->size, q, &o, &l);
+        a.boff[q] = o;
+        a.blen[q] = l;
+        maxlen = std::max(maxlen, l);
+    }
+    // chunks: ~512 per block for big blocks (many more items than workgroups, so the pulls of
+    // chunk k overlap the folds of the chunks after it), at least 64 KiB, whole 16-B vectors,
+    // at most kPipeKmax per block
+    const size_t vec = 16 / esz;
+    size_t chunk = std::max<size_t>(((size_t)64 << 10) / esz, maxlen / 512);
+    chunk = std::max(chunk, (maxlen + kPipeKmax - 1) / kPipeKmax);
+    chunk = (chunk + vec - 1) / vec * vec;
+    const size_t nchunks = std::max<size_t>(1, (maxlen + chunk - 1) / chunk);
+    const int me = c->rank;
+    for (int q = 0; q < c->size; ++q) {
+        a.src[q] = P[0][q];
+        a.peer_rbuf[q] = (const char *)P[1][q];
+        if (q != me)
+            a.peer_flag[q] = reinterpret_cast<uint64_t *>(c->pipe_peer[q]) + (size_t)me * c->pipe_kmax;
+    }
+    a.dst = (char *)P[1][me];
+    a.my_flag = reinterpret_cast<const uint64_t *>(c->pipe_base);
+    a.queue = c->pipe_queue;
+    a.err = c->ll_err;
+    *c->ll_err = 0;
+    a.qbase = c->pipe_qbase;
+    a.seq = ++c->pipe_seq;
+    a.timeout_ticks = (uint64_t)(c->timeout_s * 1e8);  // s_memrealtime: 100 MHz
+    a.kmax = c->pipe_kmax;
+    a.chunk = chunk;
+    a.count = count;
+    a.nchunks = (uint32_t)nchunks;
+    a.n = c->size;
+    a.me = me;
+    for (size_t j = 0; j < pr.order.size(); ++j) a.order[j] = pr.order[j];
+    a.role_mask = pr.role_mask;
+    // vector paths: every fold operand shares the destination's misalignment (a whole element);
+    // a pull needs only its source and destination to agree
+    const uintptr_t m = (uintptr_t)a.dst & 15;
+    a.co_fold = (m % esz) == 0;
+    for (int q = 0; q < c->size && a.co_fold; ++q) a.co_fold = (((uintptr_t)a.src[q]) & 15) == m;
+    for (int q = 0; q < c->size; ++q)
+        if ((((uintptr_t)a.peer_rbuf[q]) & 15) == m) a.co_pull |= 1ull << q;
+    // persistent grid: 2 workgroups of 256 per CU, split among the ranks sharing this GPU
+    const uint64_t total = (uint64_t)nchunks * n;
+    uint64_t grid = (uint64_t)std::max(8, 2 * device_cu_count() / std::max(1, c->pipe_share));
+    if (grid > total) grid = total;
+    const bool tp = c->time_phases && c->tev[0];
+    if (tp) MI_HIP(hipEventRecord(c->tev[0], s));
+    TRACE(c, "pipe launch seq %llu grid %llu chunks %zu x %zu elements qbase %llu co_fold %d co_pull %llx",
+          (unsigned long long)a.seq, (unsigned long long)grid, nchunks, chunk, (unsigned long long)a.qbase, a.co_fold,
+          (unsigned long long)a.co_pull);
+    if (debug_on()) {  // progress words the host can read while the kernel runs
+        if (!c->pipe_dbg) MI_HIP(hipHostMalloc((void **)&c->pipe_dbg, 4 * 4096 * sizeof(uint64_t), hipHostMallocCoherent));
+        std::memset(c->pipe_dbg, 0, 4 * 4096 * sizeof(uint64_t));
+        if (grid <= 4096) a.dbg = c->pipe_dbg;
+    }
+    rc = launch_pipe_slot(op, type, a, (unsigned)grid, s);
+    if (rc) return rc;
+    if (tp) MI_HIP(hipEventRecord(c->tev[1], s));
+    if (a.dbg) {
+        const auto t0 = std::chrono::steady_clock::now();
+        double next = 2.0;
+        while (hipStreamQuery(s) == hipErrorNotReady) {
+            usleep(1000);
+            const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (el > next) {
+                next += 5.0;
+                for (uint64_t g = 0; g < grid; ++g)
+                    TRACE(c, "pipe wg %llu: item %lld stage %lld flag %lld polls %lld", (unsigned long long)g,
+                          (long long)c->pipe_dbg[4 * g], (long long)c->pipe_dbg[4 * g + 1], (long long)c->pipe_dbg[4 * g + 2],
+                          (long long)c->pipe_dbg[4 * g + 3]);
+                uint64_t qv = 0;
+                TRACE(c, "pipe err word %u", (unsigned)__atomic_load_n(c->ll_err, __ATOMIC_ACQUIRE));
+                (void)qv;
+            }
+        }
+    }
+    MI_HIP(hipStreamSynchronize(s));
+    if (__atomic_load_n(c->ll_err, __ATOMIC_ACQUIRE)) {
+        // the counter no longer has its expected value: start it over for the next call
+        (void)hipMemset(c->pipe_queue, 0, sizeof(uint64_t));
+        (void)hipDeviceSynchronize();
+        c->pipe_qbase = 0;
+        c->ctrl->abort_flag.store(1);
+        return set_error(MI355X_ERR_TIMEOUT, "rank %d: pipelined allreduce %llu timed out waiting for a peer", c->rank,
+                         (unsigned long long)a.seq);
+    }
+    c->pipe_qbase += total + grid;  // every workgroup: its items + one dequeue past the end
+    TRACE(c, "pipe done seq %llu", (unsigned long long)a.seq);
+    if (tp) {
+        MI_HIP(hipEventElapsedTime(&c->phase_ms[0], c->tev[0], c->tev[1]));
+        c->phase_ms[1] = 0.f;
+    }
+    return barrier(c);  // peers may still read my rbuf / my input until everybody is done
+}
+
 static void ll_program(LLArgs &a, const Program &pr)
 {
     if (!pr.is_fold) {
@@ -1275,6 +1476,7 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
     if (c->fd_sock >= 0) close(c->fd_sock);
     if (c->pipe_base) (void)hipFree(c->pipe_base);
     if (c->pipe_queue) (void)hipFree(c->pipe_queue);
+    if (c->pipe_dbg) (void)hipHostFree(c->pipe_dbg);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->stage) (void)hipFree(c->stage);
     if (c->ll_base) (void)hipFree(c->ll_base);
@@ -1324,6 +1526,7 @@ int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
     case MI355X_KNOB_REDUCE_CHAIN_FANOUT: *value = c->chain_fanout; break;
     case MI355X_KNOB_TIME_PHASES: *value = c->time_phases ? 1 : 0; break;
     case MI355X_KNOB_COPY_BLOCK_KIB: *value = coll_tune().copy_block_kib; break;
+    case MI355X_KNOB_PIPE: *value = c->pipe_on ? 1 : 0; break;
     default: return set_error(MI355X_ERR_ARG, "unknown knob %d", knob);
     }
     return MI355X_SUCCESS;
@@ -1363,6 +1566,7 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
         if (value < 4 || value > 256) return set_error(MI355X_ERR_ARG, "copy_block_kib out of range");
         coll_tune().copy_block_kib = (int)value;
         break;
+    case MI355X_KNOB_PIPE: c->pipe_on = value != 0; break;
     case MI355X_KNOB_TIME_PHASES:
         c->time_phases = value != 0;
         if (c->time_phases && !c->tev[0]) {
@@ -1485,6 +1689,11 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
         }
         return ll_run(c, a, op, type, s);
     }
+    const bool pipe = ring && !c->loopback && c->pipe_on && !coll_tune().push;
+    if (pipe) {  // collective setup first: it reuses the exchange slots
+        rc = ensure_pipe(c);
+        if (rc) return rc;
+    }
     MI_HIP(hipStreamSynchronize(s));  // every rank's input is complete before it is published
     const void *mine[2] = {in, rbuf};
     const uint64_t sig[4] = {1, count, (uint64_t)type, (uint64_t)op};
@@ -1521,6 +1730,9 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
         if (rc) return rc;
         return finish(c, s);
     }
+    // multi-process: the fold of my block and the pulls of the others in one pipelined launch
+    // (coll_pipe.hip); loopback ranks share one process's queues, so they keep two phases
+    if (pipe) return pipe_allreduce(c, op, type, pr, P, count, s);
     // phase 1: reduce own block locally; phase 2: pull every other block from its owner
     const bool tp = c->time_phases && c->tev[0];
     if (tp) MI_HIP(hipEventRecord(c->tev[0], s));

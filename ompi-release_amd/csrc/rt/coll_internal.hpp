@@ -85,6 +85,28 @@ struct LLArgs {
 int launch_ll_slot(int op, int type, const LLArgs &a, hipStream_t s);  // LL_AR / LL_RED
 int launch_ll_copy(const LLArgs &a, hipStream_t s);                   // LL_AG / LL_BC
 
+// Pipelined allreduce (coll_pipe.hip): fold of my ring block and pulls of the peers' blocks in
+// one launch, chunk by chunk, with per-chunk ready flags (uncached region, written by the
+// producer into every peer over xGMI) and a device work queue.
+struct PipeArgs {
+    const void *src[kMaxRanks];        // every rank's input, mapped (vector base)
+    const char *peer_rbuf[kMaxRanks];  // every rank's rbuf, mapped (vector base)
+    char *dst;                         // my rbuf
+    uint64_t *peer_flag[kMaxRanks];    // row `me` of peer q's flag region (q != me)
+    const uint64_t *my_flag;           // my flag region: row q = flags raised by rank q
+    uint64_t *queue;                   // work-queue counter (device memory, monotonic)
+    uint32_t *err;                     // host-visible error word (timeout)
+    uint64_t qbase, seq, timeout_ticks, kmax, chunk, count;
+    uint64_t boff[kMaxRanks], blen[kMaxRanks];  // ring block partition (elements)
+    uint64_t role_mask;                // my block's fold program (ring_block_program)
+    uint64_t co_pull;                  // bit q: peer q's rbuf and mine share alignment mod 16
+    int order[kMaxRanks];
+    int n, me, co_fold;                // co_fold: every input and dst share alignment mod 16
+    uint32_t nchunks;                  // chunks per block (the longest block)
+    uint64_t *dbg;                     // NULL, or 4 words per workgroup: item, stage, flag seen, polls
+};
+int launch_pipe_slot(int op, int type, const PipeArgs &a, unsigned grid, hipStream_t s);
+
 struct CollTune {
     // grid cap of k_fold / k_copy / k_multicopy in blocks per CU; 1024 = one-shot grids (every
     // thread one pass), measured fastest for 1 GiB allreduce (one-GPU rehearsal: 0.94 ms vs 1.16 ms

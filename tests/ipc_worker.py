@@ -191,6 +191,53 @@ def large_calls(pkg, comm, rank, size, torch):
         torch.cuda.empty_cache()
 
 
+def pipe_checks(pkg, comm, rank, size, oracle, torch):
+    """the pipelined allreduce (coll_pipe.hip: fold + pulls in one launch, device-side chunk
+    flags) against the oracle's schedule simulation and against the two-phase flow: ring and
+    segmented-ring regions, order-sensitive data, in place, every rank's buffers at a different
+    misalignment (scalar fold, per-peer pull paths), many back-to-back calls (flags and the work
+    queue reused)"""
+    ptrs = lambda arrs: (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    assert comm.get("PIPE") == 1
+    comm.set("LL_MAX_BYTES", 0)
+    cases = [("SUM", "FLOAT", 300_007), ("SUM", "FLOAT", size * (1 << 18) * 2 + 12_345),
+             ("PROD", "C_DOUBLE_COMPLEX", 100_003), ("MAXLOC", "DOUBLE_INT", 70_001), ("BAND", "INT64", 4099)]
+    for opname, tname, count in cases:
+        op, ty = pkg.OP[opname], pkg.T[tname]
+        esz = pkg.type_size(ty)
+        xs = [opdata.make(tname, count, 3000 + r) for r in range(size)]
+        outs = [np.zeros_like(xs[0]) for _ in range(size)]
+        ran = oracle.oracle_allreduce(0, size, count, ty, op, 0, ptrs(xs), ptrs(outs))
+        for skew in (False, True):
+            for inplace in (False, True):
+                # skew: this rank's buffers start (4 * rank) bytes into their allocations
+                off = (4 * rank) % 16 if skew else 0
+                raw = torch.zeros(count * esz + 64, dtype=torch.uint8, device="cuda")
+                dx = raw[off:off + count * esz]
+                dx.copy_(torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda())
+                rraw = torch.zeros(count * esz + 64, dtype=torch.uint8, device="cuda")
+                roff = (16 - off) % 16 if skew else 0
+                dr = dx if inplace else rraw[roff:roff + count * esz]
+                torch.cuda.synchronize()
+                comm.allreduce(None if inplace else dx.data_ptr(), dr.data_ptr(), count, ty, op)
+                got = dr.cpu().numpy().view(xs[0].dtype)
+                opdata.assert_same(tname, opname, got, outs[rank],
+                                   f"pipe allreduce {opname}/{tname} count={count} skew={skew} inplace={inplace}")
+                assert comm.last_algorithm() == ran
+    # back to back, values change every call; then the same with the two-phase flow
+    x = torch.empty(1 << 20, device="cuda")
+    y = torch.empty_like(x)
+    for pipe in (1, 0, 1):
+        comm.set("PIPE", pipe)
+        for k in range(16):
+            x.fill_(float(rank + k))
+            comm.allreduce(x.data_ptr(), y.data_ptr(), x.numel(), pkg.T["FLOAT"], pkg.OP["SUM"])
+            assert bool(torch.all(y == sum(r + k for r in range(size)))), ("pipe back-to-back", pipe, k)
+    comm.set("PIPE", 1)
+    comm.set("LL_MAX_BYTES", 64 << 10)
+    print(f"rank {rank} pipe OK", flush=True)
+
+
 def _pattern_chunk(torch, lo, hi):
     """int32 words lo..hi-1 of the big-bcast pattern (an LCG of the word index, wraps in int32)"""
     return torch.arange(lo, hi, dtype=torch.int32, device="cuda") * 1103515245 + 12345
@@ -321,6 +368,7 @@ def main():
     for r in range(size):
         assert int(dst[r * nb:(r + 1) * nb].min()) == r + 1
     realloc_same_address(pkg, comm, rank, size)
+    pipe_checks(pkg, comm, rank, size, oracle, torch)
     ll_checks(pkg, comm, rank, size, oracle, torch)
     p2p_checks(pkg, comm, rank, size, oracle, torch)
     staged(pkg, comm, rank, size, torch, key)
