@@ -553,7 +553,8 @@ int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **e
             (void)hipGetLastError();
             int dropped = 0;
             for (auto m = c->peer_maps.begin(); m != c->peer_maps.end();) {
-                if (m->first.peer == peer && m->second.last_use != c->seq && m->second.pins == 0) {
+                if (m->first.peer == peer && m->second.last_use != c->seq && m->second.pins == 0 &&
+                    !m->second.persistent) {
                     close_map(m->second);
                     m = c->peer_maps.erase(m);
                     dropped++;
@@ -579,7 +580,7 @@ int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **e
 // that pass staged == NULL get an error instead).  force: export regardless of allocation size
 // (the staging buffers themselves).
 int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t sig[4],
-             std::vector<std::vector<void *>> &peers, bool *staged, bool force)
+             std::vector<std::vector<void *>> &peers, bool *staged, bool force, bool persistent)
 {
     c->seq++;
     if (staged) *staged = false;
@@ -642,8 +643,10 @@ int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t s
             if (r == c->rank) {
                 peers[b][r] = const_cast<void *>(mine[b]);
             } else {
-                rc = map_peer(c, r, o.buf[b], &peers[b][r]);
+                PeerMap *pm = nullptr;
+                rc = map_peer(c, r, o.buf[b], &peers[b][r], &pm);
                 if (rc) return rc;
+                if (persistent && pm) pm->persistent = true;
             }
         }
     }
@@ -928,7 +931,7 @@ static int ensure_ll(mi355x_comm *c)
     const void *mine[1] = {c->ll_base};
     const uint64_t sig[4] = {10, total, 0, 0};
     std::vector<std::vector<void *>> P;
-    int rc = exchange(c, 1, mine, sig, P, nullptr, true);
+    int rc = exchange(c, 1, mine, sig, P, nullptr, true, true);
     if (rc) return rc;
     c->ll_peer.assign(n, nullptr);
     for (size_t q = 0; q < n; ++q) c->ll_peer[q] = (char *)P[0][q];
@@ -1042,7 +1045,7 @@ static int ensure_pipe(mi355x_comm *c)
     const void *mine[1] = {c->pipe_base};
     const uint64_t sig[4] = {11, bytes, 0, 0};
     std::vector<std::vector<void *>> P;
-    int rc = exchange(c, 1, mine, sig, P, nullptr, true);
+    int rc = exchange(c, 1, mine, sig, P, nullptr, true, true);
     if (rc) return rc;
     c->pipe_peer.assign(n, nullptr);
     for (size_t q = 0; q < n; ++q) c->pipe_peer[q] = (char *)P[0][q];

@@ -123,6 +123,8 @@ struct PeerMap {
     uint64_t last_use;             // call (seq) that last used the mapping
     hipExternalMemory_t ext;       // dmabuf import (NULL: hipIpcOpenMemHandle mapping)
     int pins = 0;                  // in-flight point-to-point reads: never closed meanwhile
+    bool persistent = false;       // a region the engine keeps mapped for the communicator's
+                                   // life (LL and pipeline flag regions): never dropped
 };
 
 inline void close_map(PeerMap &m)
@@ -253,8 +255,10 @@ int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force);
 int export_dmabuf(mi355x_comm *c, BufDesc *d, uint64_t peers);
 int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **entry = nullptr);
 // publish nbuf buffers, meet every rank, map every rank's buffers: peers[b][r] (coll_comm.cpp)
+// persistent: the mappings stay for the communicator's life (never dropped to make room)
 int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t sig[4],
-             std::vector<std::vector<void *>> &peers, bool *staged = nullptr, bool force = false);
+             std::vector<std::vector<void *>> &peers, bool *staged = nullptr, bool force = false,
+             bool persistent = false);
 int finish(mi355x_comm *c, hipStream_t s);          // stream sync + barrier
 int ensure_scratch(mi355x_comm *c, size_t bytes);   // exportable per-communicator scratch
 int run_program(int op, int type, const Program &pr, const std::vector<void *> &in,
