@@ -71,7 +71,7 @@ def extra_legs(args, pkg, torch, comm, world, rank, dev, legs, key):
                 y.zero_()
                 row[name] = round(_timed(dist, torch, run, reps, 2) * 1e6, 2)
                 row["exact"] = row["exact"] and bool(torch.all(y == want).item())
-            comm.set("LL_MAX_BYTES", 64 << 10)  # the default
+            comm.set("LL_MAX_BYTES", 0)  # the default
         sweep.append(row)
         del x, y
     legs["allreduce_sweep_f32"] = sweep
@@ -253,37 +253,43 @@ def run(args, pkg, torch):
     n = GIB // 4
     dev = torch.device("cuda", local)
     ty, op = pkg.T["FLOAT"], pkg.OP["SUM"]
-    # launch-shape autotune on the real size (blocks per CU of the pull data flow), with the
-    # exactness check on every candidate: x_r = r + 1 everywhere -> every element = n(n+1)/2.
-    # All ranks see the same max-over-ranks times, so they pick the same candidate.
+    # data-flow / launch-shape autotune on the real size, with the exactness check on every
+    # candidate: x_r = r + 1 everywhere -> every element = n(n+1)/2.  Candidates: the pipelined
+    # flow (one launch: fold + pulls with device-side chunk flags; workgroups per CU x chunk size)
+    # and the two-phase flow (fold -> host barrier -> pull; grid cap).  All ranks see the same
+    # max-over-ranks times, so they pick the same candidate.  Push is not a candidate: its remote
+    # writes land behind the owner's L2 (coarse-grained memory is not probed) -- single device only.
     x = torch.full((n,), float(rank + 1), device=dev)
     y = torch.empty_like(x)
     want = world * (world + 1) / 2
     ok = True
     tried = []
-    # pull only: the push flow writes into peers' memory behind their L2 (coarse-grained memory is
-    # not probed), which is safe on one device but not across xGMI -- it is not a valid candidate
-    for push, ckib in ((0, 4), (0, 16)):
-        for bpc in (2, 8, 64, 1024):   # persistent grids ... one-shot (every thread one pass)
-            _log(rank, f"autotune push={push} blocks_per_cu={bpc} copy_block_kib={ckib}")
-            comm.set("PUSH", push)
-            comm.set("BLOCKS_PER_CU", bpc)
-            comm.set("COPY_BLOCK_KIB", ckib)
-            torch.cuda.synchronize()
+    cands = [{"pipe": 1, "pipe_wg_per_cu": wg, "pipe_chunk_kib": ck} for wg in (1, 2, 4) for ck in (0, 2048)]
+    cands += [{"pipe": 0, "blocks_per_cu": bpc, "copy_block_kib": 4} for bpc in (8, 1024)]
+
+    def apply(cand):
+        comm.set("PUSH", 0)
+        comm.set("PIPE", cand["pipe"])
+        for k, knob in (("pipe_wg_per_cu", "PIPE_WG_PER_CU"), ("pipe_chunk_kib", "PIPE_CHUNK_KIB"),
+                        ("blocks_per_cu", "BLOCKS_PER_CU"), ("copy_block_kib", "COPY_BLOCK_KIB")):
+            if k in cand:
+                comm.set(knob, cand[k])
+
+    for cand in cands:
+        _log(rank, f"autotune {cand}")
+        apply(cand)
+        torch.cuda.synchronize()
+        comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
+        ok = ok and bool(torch.all(y == want).item())
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(3):
             comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
-            ok = ok and bool(torch.all(y == want).item())
-            dist.barrier()
-            t0 = time.perf_counter()
-            for _ in range(3):
-                comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
-            dt = torch.tensor([(time.perf_counter() - t0) / 3])
-            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-            tried.append({"push": push, "blocks_per_cu": bpc, "copy_block_kib": ckib,
-                          "ms": round(float(dt[0]) * 1e3, 4)})
+        dt = torch.tensor([(time.perf_counter() - t0) / 3])
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        tried.append(dict(cand, ms=round(float(dt[0]) * 1e3, 4)))
     best = min(tried, key=lambda c: c["ms"])
-    comm.set("PUSH", best["push"])
-    comm.set("BLOCKS_PER_CU", best["blocks_per_cu"])
-    comm.set("COPY_BLOCK_KIB", best["copy_block_kib"])
+    apply(best)
     # timed data: N(0,1), order-dependent (the engine replicates the segmented-ring order)
     _log(rank, f"timed: {args.steps} steps, best {best}")
     x.normal_()
@@ -318,10 +324,17 @@ def run(args, pkg, torch):
     dist.all_reduce(tk, op=dist.ReduceOp.MAX)
     p1, p2 = float(tk[0]), float(tk[1])
     blk = n * 4 / world                              # bytes of one ring block
-    fold_xgmi = (world - 1) * blk / (p1 * 1e-3) / 1e9  # ingress over the n-1 links per rank
-    # rehearsal view (all ranks on one GPU, their phase-1 launches concurrent): the chip streams
-    # every rank's n block reads + 1 block write
-    fold_hbm = world * (world + 1) * blk / (p1 * 1e-3) / 1e9
+    pipe = bool(best["pipe"])
+    # algorithmic bytes of the dominant launch.  xGMI (ingress per rank): pipelined = the fold's
+    # n-1 remote block reads + the n-1 pulled blocks; two-phase phase 1 = the n-1 remote blocks.
+    # Rehearsal (every rank on one GPU, concurrent launches): the chip's HBM reads + writes of all
+    # ranks' launches -- pipelined (3n-1) blocks per rank (fold n reads + 1 write, pulls n-1 reads
+    # + n-1 writes), phase 1 (n+1) blocks per rank.
+    xgmi_bytes = (2 if pipe else 1) * (world - 1) * blk
+    hbm_bytes = world * ((3 * world - 1) if pipe else (world + 1)) * blk
+    fold_xgmi = xgmi_bytes / (p1 * 1e-3) / 1e9
+    fold_hbm = hbm_bytes / (p1 * 1e-3) / 1e9
+    kname = "k_pipe_allreduce (fold + pulls, one launch)" if pipe else "k_fold (allreduce phase 1)"
     peak_all = (world - 1) * XGMI_LINK_DIR_GBS
     # ranks sharing one GPU (a rehearsal on a 1-GPU box): the traffic never leaves local HBM
     shared = torch.cuda.device_count() < world
@@ -341,22 +354,21 @@ def run(args, pkg, torch):
         "config": {"workload": f"MPI_Allreduce MPI_SUM MPI_FLOAT 1 GiB per rank, np={world} (BASELINE configs[2])",
                    "count": n, "algorithm": {3: "recursive_doubling", 4: "ring", 5: "segmented_ring"}.get(alg, alg),
                    "exact_check": "ok" if bad == 0 else "FAILED",
-                   "data_flow": "push" if best["push"] else "pull", "blocks_per_cu": best["blocks_per_cu"],
-                   "copy_block_kib": best["copy_block_kib"],
-                   "autotune_ms_per_call": tried},
+                   "data_flow": "pipelined (fold + pulls, device flags)" if pipe else "two-phase pull",
+                   "best": best, "autotune_ms_per_call": tried},
         "roofline": ({"bound": "xgmi", "achieved": round(fold_xgmi, 2), "peak": round(peak_all, 1), "unit": "GB/s",
-                      "frac": round(fold_xgmi / peak_all, 4), "traffic": None,
-                      "kernel": "k_fold (allreduce phase 1)", "kernel_avg_ms": round(p1, 4),
-                      "alg_bytes_per_launch": int((world - 1) * blk), "phase2_ms": round(p2, 4),
+                      "frac": round(fold_xgmi / peak_all, 4), "traffic": pmc_traffic(pipe, shared=False),
+                      "kernel": kname, "kernel_avg_ms": round(p1, 4),
+                      "alg_bytes_per_launch": int(xgmi_bytes), "phase2_ms": round(p2, 4),
                       "busbw_frac": round(busbw / peak_all, 4),
                       "peak_note": f"(n-1) links x {XGMI_LINK_DIR_GBS} GB/s per direction (spec); achieved = "
-                                   "the (n-1) remote blocks one phase-1 launch reads / its event time"} if not shared else
+                                   "the remote bytes one launch reads over xGMI / its event time"} if not shared else
                      {"bound": "hbm", "achieved": round(fold_hbm, 2), "peak": 8000.0, "unit": "GB/s",
-                      "frac": round(fold_hbm / 8000.0, 4), "traffic": None,
-                      "kernel": "k_fold (allreduce phase 1)", "kernel_avg_ms": round(p1, 4),
-                      "alg_bytes_per_launch": int((world + 1) * blk), "phase2_ms": round(p2, 4),
+                      "frac": round(fold_hbm / 8000.0, 4), "traffic": pmc_traffic(pipe, shared=True),
+                      "kernel": kname, "kernel_avg_ms": round(p1, 4),
+                      "alg_bytes_per_launch": int(hbm_bytes / world), "phase2_ms": round(p2, 4),
                       "peak_note": "REHEARSAL: all ranks share one GPU, no xGMI traffic: the n concurrent "
-                                   "phase-1 launches' reads + writes (n x alg_bytes_per_launch) against the "
+                                   "launches' HBM reads + writes (n x alg_bytes_per_launch) against the "
                                    "chip's HBM; busbw not valid"}),
         "cpu_baseline": None,
         "legs": None,
@@ -393,6 +405,21 @@ def run(args, pkg, torch):
         res["error"] = "allreduce result differs from the exact sum"
         res["value"] = None
     return res
+
+
+def pmc_traffic(pipe, shared):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
+    (profiles/*pmc*.json, FETCH_SIZE x 2 + WRITE_SIZE per MI355X_MICROARCH.md), or None"""
+    import pathlib
+    key = ("k_pipe_allreduce" if pipe else "k_fold") + ("_rehearsal" if shared else "")
+    for p in sorted((pathlib.Path(__file__).resolve().parent / "profiles").glob("*pmc*.json"), reverse=True):
+        try:
+            ent = json.loads(p.read_text()).get("kernels", {}).get(key)
+        except Exception:
+            continue
+        if ent and "hbm_bytes_per_launch" in ent:
+            return ent["hbm_bytes_per_launch"]
+    return None
 
 
 def cpu_baseline_ring(n, seconds):

@@ -120,16 +120,21 @@ enum mi355x_knob {
     MI355X_KNOB_STAGE_BYTES = 8,        /* size of the per-communicator staging buffer (default 1 GiB) */
     MI355X_KNOB_REDUCE_CHAIN_FANOUT = 10, /* coll_tuned_reduce_algorithm_chain_fanout (default 4) */
     MI355X_KNOB_LL_MAX_BYTES = 9,       /* per-rank message bytes up to which allreduce / allgather /
-                                           bcast take the one-shot low-latency path (0 = never;
-                                           default 64 KiB; multi-process communicators only) */
+                                           bcast / reduce take the one-shot low-latency path (0 = never;
+                                           default 0, or env MI355X_LL_MAX_BYTES; multi-process
+                                           communicators of <= 8 ranks whose creation-time self-test
+                                           passed -- otherwise the knob stays 0) */
     MI355X_KNOB_TIME_PHASES = 11,       /* 1: time the two kernels of the direct allreduce with HIP
                                            events on the call's stream (mi355x_comm_phase_ms) */
     MI355X_KNOB_COPY_BLOCK_KIB = 12,    /* bytes per block of the pull-copy kernel, KiB (4..256, default 4) */
-    MI355X_KNOB_PIPE = 13               /* 1 (default): a multi-process ring allreduce runs its reduce and
+    MI355X_KNOB_PIPE = 13,              /* 1 (default): a multi-process ring allreduce runs its reduce and
                                            copy phases in ONE pipelined launch per rank, overlapped
                                            chunk by chunk with device-side ready flags (the segmented
                                            ring's copy/reduce overlap, coll_tuned_allreduce.c:721-831);
                                            0: two phases separated by a host barrier */
+    MI355X_KNOB_PIPE_WG_PER_CU = 14,    /* pipelined allreduce: 256-thread workgroups per CU (1..8, default 2) */
+    MI355X_KNOB_PIPE_CHUNK_KIB = 15     /* pipelined allreduce: chunk size in KiB (0 = auto: ~512 chunks
+                                           per ring block, at least 64 KiB) */
 };
 int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
 /* current value of a knob (LL_MAX_BYTES reads 0 when the creation-time LL self-test failed) */

@@ -484,6 +484,10 @@ static int probe_dmabuf(mi355x_comm *c)
         const int irc = import_dmabuf(c, q, kProbeId, o.probe_size, &mapped, &ext);
         drop_stash(c, q, kProbeId);
         if (irc != MI355X_SUCCESS) {
+            (void)hipGetLastError();  // no sticky error for later calls
+            if (c->rank == 0 || debug_on())
+                fprintf(stderr, "[mi355x] rank %d: dmabuf probe import from rank %d failed: %s\n", c->rank, q,
+                        mi355x_last_error());
             ok = false;
             break;
         }
@@ -906,28 +910,30 @@ static int staged_bcast(mi355x_comm *c, void *buf, size_t bytes, int root, hipSt
 // kernel it waits for.
 static bool ll_usable(const mi355x_comm *c, size_t bytes)
 {
-    return !c->loopback && c->size > 1 && bytes > 0 && bytes <= c->ll_max && c->size <= kMaxRanks;
+    return !c->loopback && c->size > 1 && c->size <= kLLMaxRanks && bytes > 0 && bytes <= c->ll_max;
 }
 
-// (Re)allocate and exchange the LL region.  Collective: every rank reaches it in the same call.
+// (Re)allocate and exchange the LL region: [ack words, one per rank][2 parities x n slots of
+// ll_max payload bytes as 8-byte granules].  Collective: every rank reaches it in the same call.
+constexpr size_t kLLAckBytes = 4096;
 static int ensure_ll(mi355x_comm *c)
 {
-    if (c->ll_base && c->ll_slot >= c->ll_max) return MI355X_SUCCESS;
+    // payload bytes per slot (at least 64 KiB: the creation-time self-test runs with ll_max 0)
+    const size_t want = (std::max<size_t>(c->ll_max, (size_t)64 << 10) + kLLChunk - 1) / kLLChunk * kLLChunk;
+    if (c->ll_base && c->ll_slot >= want) return MI355X_SUCCESS;
     const size_t n = (size_t)c->size;
-    const size_t slot = (c->ll_max + kLLChunk - 1) / kLLChunk * kLLChunk;
-    const size_t kmax = slot / kLLChunk;
-    const size_t fbytes = (2 * n * kmax * sizeof(uint64_t) + 4095) / 4096 * 4096;
-    const size_t total = fbytes + 2 * n * slot;
+    const size_t total = kLLAckBytes + 2 * n * (want / 4) * sizeof(uint64_t);
     if (c->ll_base) (void)hipFree(c->ll_base);
     c->ll_base = nullptr;
     MI_HIP(hipExtMallocWithFlags((void **)&c->ll_base, total, hipDeviceMallocUncached));
     MI_HIP(hipMemset(c->ll_base, 0, total));
+    if (!c->ll_ctr) MI_HIP(hipMalloc((void **)&c->ll_ctr, sizeof(uint64_t)));
+    MI_HIP(hipMemset(c->ll_ctr, 0, sizeof(uint64_t)));
     MI_HIP(hipDeviceSynchronize());
     if (!c->ll_err) MI_HIP(hipHostMalloc((void **)&c->ll_err, sizeof(uint32_t), hipHostMallocCoherent));
-    c->ll_slot = slot;
-    c->ll_kmax = kmax;
-    c->ll_flag_bytes = fbytes;
+    c->ll_slot = want;
     c->ll_seq = 0;
+    c->ll_ctr_base = 0;
     const void *mine[1] = {c->ll_base};
     const uint64_t sig[4] = {10, total, 0, 0};
     std::vector<std::vector<void *>> P;
@@ -935,37 +941,54 @@ static int ensure_ll(mi355x_comm *c)
     if (rc) return rc;
     c->ll_peer.assign(n, nullptr);
     for (size_t q = 0; q < n; ++q) c->ll_peer[q] = (char *)P[0][q];
-    TRACE(c, "LL region %zu bytes (slot %zu)", total, slot);
+    TRACE(c, "LL region %zu bytes (slot %zu payload bytes)", total, want);
     return barrier(c);  // every rank has read the exchange slots
 }
 
-// one LL call: fills the per-call fields of `a` and runs it to completion
+// one LL call: fills the per-call fields of `a` (the caller sets mode, src, dst, nbytes,
+// push_mask, the program) and runs it to completion
 static int ll_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s)
 {
     int rc = ensure_ll(c);
     if (rc) return rc;
     const uint64_t seq = ++c->ll_seq;
     const size_t par = seq & 1, n = (size_t)c->size, me = (size_t)c->rank;
+    const uint64_t all = (1ull << n) - 1;
     a.seq = seq;
     a.n = c->size;
     a.me = c->rank;
-    a.slot_bytes = c->ll_slot;
-    a.kmax = c->ll_kmax;
-    for (size_t q = 0; q < n; ++q) {
-        a.peer_data[q] = c->ll_peer[q] + c->ll_flag_bytes + (par * n + me) * c->ll_slot;
-        a.peer_flag[q] = reinterpret_cast<uint64_t *>(c->ll_peer[q]) + (par * n + me) * c->ll_kmax;
+    a.slot_gran = c->ll_slot / 4;
+    a.push_mask &= all;
+    switch (a.mode) {
+    case LL_RED: a.recv_mask = (a.me == a.root) ? all : 0; break;
+    case LL_BC: a.recv_mask = (a.me == a.root) ? 0 : (1ull << a.root); break;
+    default: a.recv_mask = all; break;
     }
-    a.my_data = c->ll_base + c->ll_flag_bytes + par * n * c->ll_slot;
-    a.my_flag = reinterpret_cast<const uint64_t *>(c->ll_base) + par * n * c->ll_kmax;
+    uint64_t *my = reinterpret_cast<uint64_t *>(c->ll_base);
+    for (size_t q = 0; q < n; ++q) {
+        uint64_t *peer = reinterpret_cast<uint64_t *>(c->ll_peer[q]);
+        a.peer_data[q] = peer + kLLAckBytes / 8 + (par * n + me) * a.slot_gran;
+        a.peer_ack[q] = peer + me;
+    }
+    a.my_data = my + kLLAckBytes / 8 + par * n * a.slot_gran;
+    a.my_ack = my;
+    const uint64_t nblk = (a.nbytes + kLLChunk - 1) / kLLChunk;
+    a.ctr = c->ll_ctr;
+    a.ctr_target = c->ll_ctr_base + nblk;
     a.err = c->ll_err;
     *c->ll_err = 0;
     a.timeout_ticks = (uint64_t)(c->timeout_s * 1e8);  // s_memrealtime: 100 MHz
     rc = (a.mode == LL_AR || a.mode == LL_RED) ? launch_ll_slot(op, type, a, s) : launch_ll_copy(a, s);
     if (rc) return rc;
     MI_HIP(hipStreamSynchronize(s));
-    if (__atomic_load_n(c->ll_err, __ATOMIC_ACQUIRE))
+    if (__atomic_load_n(c->ll_err, __ATOMIC_ACQUIRE)) {
+        (void)hipMemset(c->ll_ctr, 0, sizeof(uint64_t));  // its count is off now: restart it
+        (void)hipDeviceSynchronize();
+        c->ll_ctr_base = 0;
         return set_error(MI355X_ERR_TIMEOUT, "rank %d: LL call %llu timed out waiting for a peer", c->rank,
                          (unsigned long long)seq);
+    }
+    c->ll_ctr_base += nblk;
     return MI355X_SUCCESS;
 }
 
@@ -973,13 +996,14 @@ static double env_double(const char *name, double dflt);
 
 // Collective, once at communicator creation: the LL region is built and one LL allgather of a
 // rank-tagged 8 KiB pattern per rank runs with a short device-side bound (MI355X_LL_PROBE_S, 5 s).
-// The LL path stays on only if every rank saw every peer's bytes; otherwise small collectives take
-// the host-synchronised path (a flag protocol that misbehaves on some platform would otherwise
-// stall every small call for timeout_s).  MI355X_LL=0 skips it and disables LL.
+// The LL path can be enabled (MI355X_KNOB_LL_MAX_BYTES) only if every rank saw every peer's bytes;
+// otherwise small collectives always take the host-synchronised path (a protocol that misbehaves
+// on some platform would otherwise stall every small call for timeout_s).  MI355X_LL=0 skips it.
 static int ll_selftest(mi355x_comm *c)
 {
     const char *env = getenv("MI355X_LL");
-    if (env && atoi(env) == 0) {
+    if ((env && atoi(env) == 0) || c->size > kLLMaxRanks) {
+        c->ll_ok = false;
         c->ll_max = 0;
         return MI355X_SUCCESS;
     }
@@ -1016,6 +1040,7 @@ static int ll_selftest(mi355x_comm *c)
     if (rc) return rc;
     bool all = true;
     for (int q = 0; q < c->size; ++q) all = all && c->ctrl->slot[q].ll_ok == 1;
+    c->ll_ok = all;
     if (!all) {
         c->ll_max = 0;
         if (c->rank == 0) fprintf(stderr, "[mi355x] low-latency path self-test failed: small collectives use the host-synchronised path\n");
@@ -1080,7 +1105,8 @@ static int pipe_allreduce(mi355x_comm *c, int op, int type, const Program &pr,
     // chunk k overlap the folds of the chunks after it), at least 64 KiB, whole 16-B vectors,
     // at most kPipeKmax per block
     const size_t vec = 16 / esz;
-    size_t chunk = std::max<size_t>(((size_t)64 << 10) / esz, maxlen / 512);
+    size_t chunk = coll_tune().pipe_chunk_kib ? ((size_t)coll_tune().pipe_chunk_kib << 10) / esz
+                                              : std::max<size_t>(((size_t)64 << 10) / esz, maxlen / 512);
     chunk = std::max(chunk, (maxlen + kPipeKmax - 1) / kPipeKmax);
     chunk = (chunk + vec - 1) / vec * vec;
     const size_t nchunks = std::max<size_t>(1, (maxlen + chunk - 1) / chunk);
@@ -1114,9 +1140,11 @@ static int pipe_allreduce(mi355x_comm *c, int op, int type, const Program &pr,
     for (int q = 0; q < c->size && a.co_fold; ++q) a.co_fold = (((uintptr_t)a.src[q]) & 15) == m;
     for (int q = 0; q < c->size; ++q)
         if ((((uintptr_t)a.peer_rbuf[q]) & 15) == m) a.co_pull |= 1ull << q;
-    // persistent grid: 2 workgroups of 256 per CU, split among the ranks sharing this GPU
+    // persistent grid: pipe_wg_per_cu workgroups of 256 per CU, split among the ranks sharing
+    // this GPU
     const uint64_t total = (uint64_t)nchunks * n;
-    uint64_t grid = (uint64_t)std::max(8, 2 * device_cu_count() / std::max(1, c->pipe_share));
+    uint64_t grid =
+        (uint64_t)std::max(8, coll_tune().pipe_wg_per_cu * device_cu_count() / std::max(1, c->pipe_share));
     if (grid > total) grid = total;
     const bool tp = c->time_phases && c->tev[0];
     if (tp) MI_HIP(hipEventRecord(c->tev[0], s));
@@ -1425,7 +1453,8 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     }
     rc = barrier(c);  // everybody mapped the segment and bound its socket: the name can go
     if (rank == 0) shm_unlink(c->shm_name.c_str());
-    if (rc == MI355X_SUCCESS && size > 1 && c->ll_max > 0) rc = ll_selftest(c);
+    c->ll_max = (size_t)std::max(0.0, env_double("MI355X_LL_MAX_BYTES", 0.0));
+    if (rc == MI355X_SUCCESS && size > 1) rc = ll_selftest(c);
     if (rc) {
         mi355x_comm_destroy(c);
         return rc;
@@ -1483,6 +1512,7 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->stage) (void)hipFree(c->stage);
     if (c->ll_base) (void)hipFree(c->ll_base);
+    if (c->ll_ctr) (void)hipFree(c->ll_ctr);
     if (c->ll_err) (void)hipHostFree(c->ll_err);
     if (c->loopback) {
         std::lock_guard<std::mutex> g(c->loop->mtx);
@@ -1530,6 +1560,8 @@ int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
     case MI355X_KNOB_TIME_PHASES: *value = c->time_phases ? 1 : 0; break;
     case MI355X_KNOB_COPY_BLOCK_KIB: *value = coll_tune().copy_block_kib; break;
     case MI355X_KNOB_PIPE: *value = c->pipe_on ? 1 : 0; break;
+    case MI355X_KNOB_PIPE_WG_PER_CU: *value = coll_tune().pipe_wg_per_cu; break;
+    case MI355X_KNOB_PIPE_CHUNK_KIB: *value = coll_tune().pipe_chunk_kib; break;
     default: return set_error(MI355X_ERR_ARG, "unknown knob %d", knob);
     }
     return MI355X_SUCCESS;
@@ -1570,6 +1602,14 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
         coll_tune().copy_block_kib = (int)value;
         break;
     case MI355X_KNOB_PIPE: c->pipe_on = value != 0; break;
+    case MI355X_KNOB_PIPE_WG_PER_CU:
+        if (value < 1 || value > 8) return set_error(MI355X_ERR_ARG, "pipe_wg_per_cu out of range");
+        coll_tune().pipe_wg_per_cu = (int)value;
+        break;
+    case MI355X_KNOB_PIPE_CHUNK_KIB:
+        if (value < 0 || value > (1l << 20)) return set_error(MI355X_ERR_ARG, "pipe_chunk_kib out of range");
+        coll_tune().pipe_chunk_kib = (int)value;
+        break;
     case MI355X_KNOB_TIME_PHASES:
         c->time_phases = value != 0;
         if (c->time_phases && !c->tev[0]) {
@@ -1579,7 +1619,7 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
         break;
     case MI355X_KNOB_LL_MAX_BYTES:
         if (value < 0 || value > (64l << 20)) return set_error(MI355X_ERR_ARG, "ll_max_bytes out of range");
-        c->ll_max = (size_t)value;
+        c->ll_max = c->ll_ok ? (size_t)value : 0;  // a failed (or skipped) self-test keeps it off
         break;
     case MI355X_KNOB_STAGE_BYTES:
         if (value < 4096 || value >= (1l << 31)) return set_error(MI355X_ERR_ARG, "stage_bytes out of range");

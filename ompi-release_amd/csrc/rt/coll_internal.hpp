@@ -58,24 +58,29 @@ struct MultiCopyArgs {
     int nseg;
 };
 
-// Low-latency one-shot path (coll_ll.hip) for small messages: every rank pushes its data into
-// slot (parity, me) of every peer's fine-grained (uncached) LL region over xGMI, raises one flag
-// per 4 KiB slice in every peer, waits for every peer's flags, then finishes locally.  No host
-// barrier, no per-call IPC exchange.  Parity double-buffering makes back-to-back calls safe: a
-// peer can only reuse a parity after every rank has acknowledged the call in between.
-constexpr size_t kLLChunk = 4096;  // bytes per slice = per thread block (256 threads x 16 B)
+// Low-latency one-shot path (coll_ll.hip) for small messages (communicators of <= 8 ranks):
+// every rank pushes its data into slot (parity, me) of every peer's uncached LL region over xGMI
+// as 8-byte granules {4 B payload, 4 B call tag} -- one store each, so the tag vouches for the
+// payload and no fence or separate flag is needed -- and the receivers poll their own slots for
+// the tag.  Parity double-buffering + a per-call acknowledgement (written by the last block of
+// every rank into every peer) make back-to-back calls safe.  No host barrier, no per-call IPC
+// exchange.
+constexpr size_t kLLChunk = 4096;  // payload bytes per thread block (256 threads x 16 B)
+constexpr int kLLMaxRanks = 8;     // sources held in registers per thread
 enum { LL_AR = 0, LL_AG = 1, LL_BC = 2, LL_RED = 3 };  // allreduce, allgather, bcast, reduce
 enum { LL_FOLD = 0, LL_RING = 1, LL_TREE = 2 };   // per-element program of LL_AR
 struct LLArgs {
     const void *src;                   // this rank's data (NULL: nothing to push)
     void *dst;                         // result (rbuf / buf)
-    char *peer_data[kMaxRanks];        // slot (parity, me) in peer q's LL data region
-    uint64_t *peer_flag[kMaxRanks];    // flag row (parity, me) in peer q's LL flag region
-    const char *my_data;               // this rank's data region of this parity (slot q at q*slot_bytes)
-    const uint64_t *my_flag;           // this rank's flag region of this parity (row q at q*kmax)
+    uint64_t *peer_data[kMaxRanks];    // granules of slot (parity, me) in peer q's LL region
+    uint64_t *peer_ack[kMaxRanks];     // ack word `me` in peer q's LL region
+    const uint64_t *my_data;           // this rank's slots of this parity (slot q at q * slot_gran)
+    const uint64_t *my_ack;            // this rank's ack words (word q written by rank q)
+    uint64_t *ctr;                     // blocks done, monotonic (device memory)
+    uint64_t ctr_target;               // its value once this call's last block is done
     uint32_t *err;                     // host-visible error word (timeout)
-    uint64_t push_mask;                // bit q: push the data to rank q
-    uint64_t seq, slot_bytes, kmax, nbytes, timeout_ticks;
+    uint64_t push_mask, recv_mask;     // bit q: push to / receive from rank q
+    uint64_t seq, slot_gran, nbytes, timeout_ticks;
     uint64_t count, early, late, split;  // elements; ring block partition (coll_tuned.h:546-552)
     uint64_t role_mask;
     int mode, prog, n, me, root, nsteps, result;
@@ -120,6 +125,10 @@ struct CollTune {
     // owner's L2, which may still hold old lines of the destination (coarse-grained memory is not
     // probed), so the owner could read stale data afterwards.
     int push = 0;
+    // pipelined allreduce: workgroups (256 threads) per CU of its persistent grid, split among the
+    // ranks sharing a GPU; chunk size in KiB (0: ~512 chunks per ring block, >= 64 KiB)
+    int pipe_wg_per_cu = 2;
+    int pipe_chunk_kib = 0;
 };
 CollTune &coll_tune();
 

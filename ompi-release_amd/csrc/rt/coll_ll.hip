@@ -1,21 +1,25 @@
 // coll_ll.hip -- low-latency one-shot collectives for small messages (see coll_internal.hpp).
 //
-// One launch per rank per call, one 256-thread block per 4 KiB slice of the message, no host
-// barrier: the reference's recursive-doubling / small-ring region (coll_tuned_decision_fixed.c:
-// 42-85) is latency-bound, and a host round trip (stream sync + shm barrier, tens of µs) costs more
-// than the data movement.  Block b of every rank:
-//   1. pushes slice b of its data into slot (parity, me) of every peer named in push_mask
-//      (16-B stores over xGMI into the peer's uncached LL region),
-//   2. after a system-scope release, raises flag (parity, me, b) = seq in EVERY peer -- the flag
-//      is also the acknowledgement that makes the parity reusable two calls later,
-//   3. waits until flag (parity, q, b) = seq for every q in its own region (bounded spin: after
-//      ~10 s it records a timeout in the host-visible error word and gives up),
-//   4. finishes locally from the slots: the reference schedule's per-element program over the n
-//      inputs (allreduce; reduce: the root only, the others push to the root alone), or copies
-//      (allgather / bcast).
-// Slices are independent, so blocks never wait on each other.  The LL region is allocated with
-// hipDeviceMallocUncached: remote xGMI writes do not update the owner's L2, so the flags and
-// data a rank polls must never be cached there.
+// The reference's recursive-doubling / small-ring region (coll_tuned_decision_fixed.c:42-85) is
+// latency-bound: a host round trip (stream sync + shm barrier) costs more than the data.  Here
+// one launch per rank per call, no host barrier, and -- unlike a flag-after-data protocol -- no
+// memory fence on the critical path: every 4 bytes of payload travel with the call's tag in one
+// naturally aligned 8-byte granule {payload, tag}, written by ONE 8-byte store (single-copy
+// atomic), so a receiver that sees the tag sees the payload.  The LL region of every rank is
+// uncached device memory (hipDeviceMallocUncached): remote stores land in its HBM, local polls
+// read HBM, nothing stale can sit in a cache.
+//
+// Block b of every rank (256 threads, 4 KiB of payload, 16 B per thread):
+//   1. wait until every peer it pushes to has acknowledged the call two calls back (that peer
+//      then no longer reads the parity slot about to be rewritten; the wait is normally satisfied
+//      at once);
+//   2. pushes its 16 B into slot (parity, me) of every peer named in push_mask as 4 granules;
+//   3. polls its own slots of the ranks it receives from until every granule carries this call's
+//      tag (bounded: on timeout the host-visible error word is set);
+//   4. finishes locally: the reference schedule's per-element program over the n inputs
+//      (allreduce; reduce: the root only), or copies (allgather / bcast);
+//   5. counts itself done; the last block of the call acknowledges the call to every peer.
+// Slices are independent, so blocks never wait on each other.
 #include "coll_internal.hpp"
 #include "op_functors.hpp"
 #include "rt_internal.hpp"
@@ -25,68 +29,69 @@ namespace mi355x {
 
 typedef unsigned int u32x4l __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ uint64_t ll_flag_load(const uint64_t *p)
+__device__ __forceinline__ uint64_t ll_load(const uint64_t *p)
 {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ void ll_flag_store(uint64_t *p, uint64_t v)
+__device__ __forceinline__ void ll_store(uint64_t *p, uint64_t v)
 {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// copy bytes [lo, hi) of src to dst (slot bases are 16-B aligned; user buffers may not be)
-__device__ __forceinline__ void ll_copy_slice(char *dst, const char *src, size_t lo, size_t hi)
-{
-    const size_t t = threadIdx.x;
-    if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
-        const size_t nv = (hi - lo) / 16;
-        for (size_t v = t; v < nv; v += blockDim.x)
-            *reinterpret_cast<u32x4l *>(dst + lo + v * 16) = *reinterpret_cast<const u32x4l *>(src + lo + v * 16);
-        for (size_t k = lo + nv * 16 + t; k < hi; k += blockDim.x) dst[k] = src[k];
-    } else {
-        for (size_t k = lo + t; k < hi; k += blockDim.x) dst[k] = src[k];
-    }
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// steps 1-3; returns false on timeout
-__device__ bool ll_exchange(const LLArgs &a)
+// up to 16 bytes of src at `off` (len valid bytes) as 4 little-endian words (zero padded)
+__device__ __forceinline__ void ll_read16(const char *src, size_t len, uint32_t w[4])
 {
-    const unsigned b = blockIdx.x;
-    const size_t lo = (size_t)b * kLLChunk;
-    const size_t hi = lo + kLLChunk < a.nbytes ? lo + kLLChunk : a.nbytes;
-    if (a.src) {
-        const char *src = static_cast<const char *>(a.src);
-        const size_t t = threadIdx.x;
-        if (((uintptr_t)src & 15) == 0) {
-            const size_t nv = (hi - lo) / 16;  // <= blockDim.x: one vector per thread
-            if (t < nv) {
-                const u32x4l v = *reinterpret_cast<const u32x4l *>(src + lo + t * 16);
-                for (int q = 0; q < a.n; ++q)
-                    if ((a.push_mask >> q) & 1u) *reinterpret_cast<u32x4l *>(a.peer_data[q] + lo + t * 16) = v;
-            }
-            for (size_t k = lo + nv * 16 + t; k < hi; k += blockDim.x)
-                for (int q = 0; q < a.n; ++q)
-                    if ((a.push_mask >> q) & 1u) a.peer_data[q][k] = src[k];
-        } else {
-            for (size_t k = lo + t; k < hi; k += blockDim.x) {
-                const char v = src[k];
-                for (int q = 0; q < a.n; ++q)
-                    if ((a.push_mask >> q) & 1u) a.peer_data[q][k] = v;
-            }
-        }
+    if (len == 16 && (((uintptr_t)src) & 15) == 0) {
+        const u32x4l v = *reinterpret_cast<const u32x4l *>(src);
+        w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
+        return;
     }
-    __threadfence_system();
-    __syncthreads();
-    const int t = (int)threadIdx.x;
-    if (t < a.n) ll_flag_store(a.peer_flag[t] + b, a.seq);
+    unsigned char b[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) b[i] = (size_t)i < len ? (unsigned char)src[i] : 0;
+    __builtin_memcpy(w, b, 16);
+}
+__device__ __forceinline__ void ll_write16(char *dst, size_t len, const uint32_t w[4])
+{
+    if (len == 16 && (((uintptr_t)dst) & 15) == 0) {
+        u32x4l v;
+        v.x = w[0], v.y = w[1], v.z = w[2], v.w = w[3];
+        *reinterpret_cast<u32x4l *>(dst) = v;
+        return;
+    }
+    unsigned char b[16];
+    __builtin_memcpy(b, w, 16);
+    for (size_t i = 0; i < len; ++i) dst[i] = (char)b[i];
+}
+
+struct LLBlock {
+    size_t lo, off, len;   // block payload start; this thread's 16-B chunk offset / valid bytes
+    int ngran;             // granules of this thread (0: past the end)
+    uint32_t tag;
+};
+
+__device__ __forceinline__ LLBlock ll_block(const LLArgs &a)
+{
+    LLBlock k;
+    k.lo = (size_t)blockIdx.x * kLLChunk;
+    k.off = k.lo + (size_t)threadIdx.x * 16;
+    k.len = k.off < a.nbytes ? (a.nbytes - k.off < 16 ? a.nbytes - k.off : 16) : 0;
+    k.ngran = (int)((k.len + 3) / 4);
+    k.tag = (uint32_t)a.seq;
+    return k;
+}
+
+// steps 1-2; false on timeout
+__device__ bool ll_push(const LLArgs &a, const LLBlock &k)
+{
     __shared__ int timed_out;
+    const int t = (int)threadIdx.x;
     if (t == 0) timed_out = 0;
     __syncthreads();
-    if (t < a.n) {
-        const uint64_t *f = a.my_flag + (size_t)t * a.kmax + b;
+    if (a.src && t < a.n && t != a.me && ((a.push_mask >> t) & 1u) && a.seq > 2) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (ll_flag_load(f) != a.seq) {
-            __builtin_amdgcn_s_sleep(2);
+        while (ll_load(a.my_ack + t) + 2 < a.seq) {
+            __builtin_amdgcn_s_sleep(1);
             if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
                 __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 timed_out = 1;
@@ -95,8 +100,71 @@ __device__ bool ll_exchange(const LLArgs &a)
         }
     }
     __syncthreads();
-    __threadfence_system();
-    return timed_out == 0;
+    if (timed_out) return false;
+    if (a.src && k.ngran) {  // (bcast: only the root has data to push)
+        uint32_t w[4];
+        ll_read16(static_cast<const char *>(a.src) + k.off, k.len, w);
+        const size_t g0 = k.off / 4;
+        for (int q = 0; q < a.n; ++q) {
+            if (!((a.push_mask >> q) & 1u)) continue;
+            uint64_t *d = a.peer_data[q] + g0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (i < k.ngran) ll_store(d + i, ((uint64_t)k.tag << 32) | w[i]);
+        }
+    }
+    return true;
+}
+
+// step 3 for the sources in qmask (<= 8 of them, slot index = rank): w[q] gets rank q's 16 B
+__device__ bool ll_recv(const LLArgs &a, const LLBlock &k, uint64_t qmask, uint32_t (&w)[8][4])
+{
+    if (!k.ngran) return true;
+    const size_t g0 = k.off / 4;
+    uint32_t pending = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        if (!((qmask >> q) & 1u)) continue;
+        const uint64_t *p = a.my_data + (size_t)q * a.slot_gran + g0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (i >= k.ngran) continue;
+            const uint64_t v = ll_load(p + i);
+            w[q][i] = (uint32_t)v;
+            if ((uint32_t)(v >> 32) != k.tag) pending |= 1u << (q * 4 + i);
+        }
+    }
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned spins = 0;
+    while (pending) {
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (!((pending >> (q * 4 + i)) & 1u)) continue;
+                const uint64_t v = ll_load(a.my_data + (size_t)q * a.slot_gran + g0 + i);
+                w[q][i] = (uint32_t)v;
+                if ((uint32_t)(v >> 32) == k.tag) pending &= ~(1u << (q * 4 + i));
+            }
+        }
+        if ((++spins & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+            __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return false;
+        }
+    }
+    return true;
+}
+
+// step 5: after every thread of the block is done with its slots
+__device__ void ll_done(const LLArgs &a)
+{
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const uint64_t old = __hip_atomic_fetch_add(a.ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 != a.ctr_target) return;
+    for (int q = 0; q < a.n; ++q)
+        if (q != a.me) ll_store(a.peer_ack[q], a.seq);
 }
 
 template <class F> __device__ __forceinline__ typename F::T ll_pick(const typename F::T (&R)[kTreeMax], int k)
@@ -145,48 +213,34 @@ template <class F, class X> __device__ __forceinline__ typename F::T ll_eval(con
         return a.order[j];
     };
     T acc = x(rank_at(0));
-    for (int j0 = 1; j0 < a.n; j0 += 8) {
-        T v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (j0 + j < a.n) v[j] = x(rank_at(j0 + j));
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (j0 + j < a.n) acc = ((a.role_mask >> (j0 + j)) & 1u) ? F::op2(acc, v[j]) : F::op2(v[j], acc);
+    for (int j = 1; j < a.n; ++j) {
+        const T v = x(rank_at(j));
+        acc = ((a.role_mask >> j) & 1u) ? F::op2(acc, v) : F::op2(v, acc);
     }
     return acc;
 }
 
-// allreduce: exchange, then this slice from the n slots.  Thread t owns the slice's t-th 16-B
-// vector; it loads that vector from every slot with all loads in flight at once (the slots are
-// uncached, so one round of latency per thread instead of one per element).  A vector whose
-// elements straddle two ring blocks (at most n - 1 in a message) is evaluated element-wise.
+// allreduce / reduce: exchange, then this thread's 16 B of the result from the n inputs held in
+// registers (<= 8 ranks: ll_usable)
 template <class F> __global__ __launch_bounds__(256) void k_ll_allreduce(LLArgs a)
 {
     using T = typename F::T;
     using V = LLVec<T>;
     constexpr int EPV = 16 / sizeof(T);
-    if (!ll_exchange(a)) return;
-    if (a.mode == LL_RED && a.me != a.root) return;  // reduce: only the root evaluates
-    const size_t i0 = ((size_t)blockIdx.x * kLLChunk + (size_t)threadIdx.x * 16) / sizeof(T);
-    if (i0 >= a.count) return;
-    const int ne = (a.count - i0) < (size_t)EPV ? (int)(a.count - i0) : EPV;
-    T *dst = static_cast<T *>(a.dst);
-    auto slot = [&](int q) { return reinterpret_cast<const T *>(a.my_data + (size_t)q * a.slot_bytes); };
-    bool uniform = (ne == EPV) && a.n <= 8;
-    if (uniform && a.prog == LL_RING) {
-        const uint64_t se = a.split * a.early;
-        auto blk = [&](size_t i) { return (i < se) ? i / a.early : a.split + (i - se) / a.late; };
-        uniform = blk(i0) == blk(i0 + EPV - 1);
-    }
-    if (uniform) {
+    const LLBlock k = ll_block(a);
+    if (!ll_push(a, k)) return;
+    const bool evaluate = !(a.mode == LL_RED && a.me != a.root);  // reduce: only the root evaluates
+    uint32_t w[8][4];
+    if (evaluate && ll_recv(a, k, a.recv_mask, w) && k.ngran) {
         V xv[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-            if (q < a.n) xv[q] = *reinterpret_cast<const V *>(slot(q) + i0);
+        for (int q = 0; q < 8; ++q) __builtin_memcpy(&xv[q], w[q], 16);
+        const size_t i0 = k.off / sizeof(T);
+        const int ne = (int)(k.len / sizeof(T));
         V r;
 #pragma unroll
-        for (int e = 0; e < EPV; ++e)
+        for (int e = 0; e < EPV; ++e) {
+            if (e >= ne) continue;
             r.e[e] = ll_eval<F>(a, i0 + e, [&](int q) {
                 T v = xv[0].e[e];  // register select (no dynamic indexing into xv)
 #pragma unroll
@@ -194,36 +248,39 @@ template <class F> __global__ __launch_bounds__(256) void k_ll_allreduce(LLArgs 
                     if (s2 == q) v = xv[s2].e[e];
                 return v;
             });
-        if ((((uintptr_t)(dst + i0)) & 15) == 0) {
-            *reinterpret_cast<V *>(dst + i0) = r;
-        } else {
-#pragma unroll
-            for (int e = 0; e < EPV; ++e) dst[i0 + e] = r.e[e];
         }
-        return;
+        uint32_t ow[4];
+        __builtin_memcpy(ow, &r, 16);
+        ll_write16(static_cast<char *>(a.dst) + k.off, k.len, ow);
     }
-    for (int e = 0; e < ne; ++e) {
-        const size_t i = i0 + e;
-        dst[i] = ll_eval<F>(a, i, [&](int q) { return slot(q)[i]; });
-    }
+    ll_done(a);
 }
 
 // allgather (slot q -> dst + q*nbytes) and bcast (slot root -> dst, non-roots)
 __global__ __launch_bounds__(256) void k_ll_copy(LLArgs a)
 {
-    if (!ll_exchange(a)) return;
-    const size_t lo = (size_t)blockIdx.x * kLLChunk;
-    const size_t hi = lo + kLLChunk < a.nbytes ? lo + kLLChunk : a.nbytes;
-    char *dst = static_cast<char *>(a.dst);
-    if (a.mode == LL_BC) {
-        if (a.me != a.root) ll_copy_slice(dst, a.my_data + (size_t)a.root * a.slot_bytes, lo, hi);
-        return;
+    const LLBlock k = ll_block(a);
+    if (!ll_push(a, k)) return;
+    uint32_t w[8][4];
+    if (a.recv_mask && ll_recv(a, k, a.recv_mask, w) && k.ngran) {
+        char *dst = static_cast<char *>(a.dst);
+        if (a.mode == LL_BC) {
+            uint32_t v[4];
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (q == a.root) __builtin_memcpy(v, w[q], 16);
+            ll_write16(dst + k.off, k.len, v);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                if (!((a.recv_mask >> q) & 1u)) continue;
+                char *d = dst + (size_t)q * a.nbytes;
+                if (q == a.me && static_cast<const char *>(a.src) == d) continue;  // in place
+                ll_write16(d + k.off, k.len, w[q]);
+            }
+        }
     }
-    for (int q = 0; q < a.n; ++q) {
-        char *d = dst + (size_t)q * a.nbytes;
-        if (q == a.me && static_cast<const char *>(a.src) == d) continue;  // in place
-        ll_copy_slice(d, a.my_data + (size_t)q * a.slot_bytes, lo, hi);
-    }
+    ll_done(a);
 }
 
 static unsigned ll_grid(const LLArgs &a) { return (unsigned)((a.nbytes + kLLChunk - 1) / kLLChunk); }

@@ -206,12 +206,18 @@ struct mi355x_comm {
     void *stage = nullptr;                        // staging buffer of the staged data flow
     size_t stage_bytes = (size_t)1 << 30;         // its size (an allocation below ipc_max)
     size_t ipc_max = (size_t)1 << 31;             // allocations >= this are never exported
-    // low-latency path (coll_ll.hip): uncached LL region [flags 2 x n x kmax][data 2 x n x slot]
-    size_t ll_max = (size_t)64 << 10;             // per-rank message bytes served by the LL path
+    // low-latency path (coll_ll.hip): uncached LL region [ack words][2 x n slots of 8-B granules]
+    // per-rank message bytes served by the LL path: 0 by default (MI355X_LL_MAX_BYTES) -- on the
+    // one-GPU rehearsal it does not beat the host-synchronised path (profiles/r02_ll_probe.txt);
+    // the 8-GPU bench legs measure both
+    size_t ll_max = 0;
+    bool ll_ok = false;                           // creation-time LL self-test passed on every rank
     char *ll_base = nullptr;
-    size_t ll_slot = 0, ll_kmax = 0, ll_flag_bytes = 0;
+    size_t ll_slot = 0;                           // payload bytes per slot
     std::vector<char *> ll_peer;                  // every rank's LL region, mapped
     uint64_t ll_seq = 0;
+    uint64_t *ll_ctr = nullptr;                   // blocks done (device), monotonic
+    uint64_t ll_ctr_base = 0;                     // its value before the next call
     uint32_t *ll_err = nullptr;                   // host-visible timeout word
     // pipelined allreduce (coll_pipe.hip): per-chunk ready flags in an uncached region that
     // every peer writes into (row q = flags raised by rank q), and the work-queue counter

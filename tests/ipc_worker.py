@@ -53,16 +53,17 @@ def realloc_same_address(pkg, comm, rank, size):
         assert np.all(out == sum(r + 1 + gen for r in range(size))), ("growing realloc", kib)
         comm.barrier()
         assert lib.mi355x_free(p) == 0
-    comm.set("LL_MAX_BYTES", 64 << 10)
+    comm.set("LL_MAX_BYTES", 0)
 
 
 def ll_checks(pkg, comm, rank, size, oracle, torch):
     """the one-shot low-latency path (coll_ll.hip): every forced allreduce algorithm against the
     oracle's schedule simulation, in place and not, allgather / bcast, and many back-to-back calls
     (parity reuse of the LL slots)"""
-    assert comm.get("LL_MAX_BYTES") > 0, "the creation-time LL self-test disabled the LL path"
     ptrs = lambda arrs: (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    assert comm.get("LL_MAX_BYTES") == 0, "the LL path is off by default"
     comm.set("LL_MAX_BYTES", 256 << 10)
+    assert comm.get("LL_MAX_BYTES") > 0, "the creation-time LL self-test disabled the LL path"
     for alg in (0, 1, 2, 3, 4, 5):
         comm.set("ALLREDUCE_ALG", alg)
         for opname, tname in [("SUM", "FLOAT"), ("MAX", "DOUBLE"), ("MINLOC", "FLOAT_INT"), ("PROD", "C_DOUBLE_COMPLEX")]:
@@ -136,6 +137,7 @@ def ll_checks(pkg, comm, rank, size, oracle, torch):
         q.wait()
     want = size * (size + 1) / 2
     assert bool(torch.all(ys == want)) and bool(torch.all(yl == want)), "nonblocking allreduce"
+    comm.set("LL_MAX_BYTES", 0)
     print(f"rank {rank} LL OK", flush=True)
 
 
@@ -234,7 +236,7 @@ def pipe_checks(pkg, comm, rank, size, oracle, torch):
             comm.allreduce(x.data_ptr(), y.data_ptr(), x.numel(), pkg.T["FLOAT"], pkg.OP["SUM"])
             assert bool(torch.all(y == sum(r + k for r in range(size)))), ("pipe back-to-back", pipe, k)
     comm.set("PIPE", 1)
-    comm.set("LL_MAX_BYTES", 64 << 10)
+    comm.set("LL_MAX_BYTES", 0)
     print(f"rank {rank} pipe OK", flush=True)
 
 
@@ -332,7 +334,25 @@ def p2p_checks(pkg, comm, rank, size, oracle, torch):
     print(f"rank {rank} p2p OK", flush=True)
 
 
+def _fd_report(rank):
+    import os
+    import resource
+    try:
+        n = len(os.listdir("/proc/self/fd"))
+    except OSError:
+        n = -1
+    print(f"rank {rank} open fds {n}, RLIMIT_NOFILE {resource.getrlimit(resource.RLIMIT_NOFILE)}", flush=True)
+
+
 def main():
+    try:
+        _main()
+    except BaseException:
+        _fd_report(int(sys.argv[2]))
+        raise
+
+
+def _main():
     key, rank, size, dev = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
     import faulthandler
     faulthandler.dump_traceback_later(150, exit=True)  # a rank stuck in a HIP call names its line
@@ -371,6 +391,7 @@ def main():
     pipe_checks(pkg, comm, rank, size, oracle, torch)
     ll_checks(pkg, comm, rank, size, oracle, torch)
     p2p_checks(pkg, comm, rank, size, oracle, torch)
+    _fd_report(rank)
     staged(pkg, comm, rank, size, torch, key)
     if size in (2, 3):
         big_bcast(pkg, comm, rank, size, torch)
