@@ -97,6 +97,24 @@ int mca_coll_mi355x_scan(void *sbuf, void *rbuf, int count, struct ompi_datatype
 int mca_coll_mi355x_exscan(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
                            struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
 
+/* Device point-to-point through the PML slot: installed over the selected PML's table
+ * (`mca_pml`, pml.h:558) when the component is initialised, the way pml/v parasites the host PML
+ * (pml_v_component.c:110-131).  Device buffers on communicators with the engine go to the engine
+ * (what ob1's CUDA path does over smcuda, pml_ob1_cuda.c:52-210); everything else to the saved
+ * entries.  OMPI_MCA_coll_mi355x_pml_hook=0 leaves the PML untouched. */
+int mca_coll_mi355x_pml_isend(void *buf, size_t count, struct ompi_datatype_t *dt, int dst, int tag,
+                              mca_pml_base_send_mode_t mode, struct ompi_communicator_t *comm,
+                              ompi_request_t **request);
+int mca_coll_mi355x_pml_send(void *buf, size_t count, struct ompi_datatype_t *dt, int dst, int tag,
+                             mca_pml_base_send_mode_t mode, struct ompi_communicator_t *comm);
+int mca_coll_mi355x_pml_irecv(void *buf, size_t count, struct ompi_datatype_t *dt, int src, int tag,
+                              struct ompi_communicator_t *comm, ompi_request_t **request);
+int mca_coll_mi355x_pml_recv(void *buf, size_t count, struct ompi_datatype_t *dt, int src, int tag,
+                             struct ompi_communicator_t *comm, ompi_status_public_t *status);
+int mca_coll_mi355x_pml_iprobe(int src, int tag, struct ompi_communicator_t *comm, int *matched,
+                               ompi_status_public_t *status);
+int mca_coll_mi355x_pml_probe(int src, int tag, struct ompi_communicator_t *comm, ompi_status_public_t *status);
+
 /* MCA parameters (environment: OMPI_MCA_coll_mi355x_<name>) */
 extern int mca_coll_mi355x_priority;            /* 90 */
 extern int mca_coll_mi355x_allreduce_algorithm; /* 0 = tuned decision, else coll_tuned numbering */

@@ -357,6 +357,7 @@ struct opal_pointer_array_t;
 extern struct opal_pointer_array_t ompi_request_f_to_c_table;
 int opal_pointer_array_set_item(struct opal_pointer_array_t *array, int index, void *value);
 typedef int (*opal_progress_callback_t)(void);
+void opal_progress(void);  /* opal/runtime/opal_progress.h:63 */
 int opal_progress_register(opal_progress_callback_t cb);
 int opal_progress_unregister(opal_progress_callback_t cb);
 
@@ -590,6 +591,91 @@ typedef struct mca_coll_base_component_2_0_0_t {
 } mca_coll_base_component_t;
 
 #define MCA_COLL_BASE_VERSION_2_0_0 MCA_BASE_VERSION_2_0_0, "coll", 2, 0, 0  /* coll.h:576-578 */
+
+/* ------------------------------------------------------------------ point-to-point (PML) */
+#define MPI_ANY_SOURCE (-1)     /* mpi.h.in:415 */
+#define MPI_PROC_NULL (-2)      /* mpi.h.in:416 */
+#define MPI_ANY_TAG (-1)        /* mpi.h.in:418 */
+#define MPI_ERR_TRUNCATE 15     /* mpi.h.in:547 */
+
+/* ompi/mca/pml/pml.h:77-84 */
+typedef enum {
+    MCA_PML_BASE_SEND_SYNCHRONOUS,
+    MCA_PML_BASE_SEND_COMPLETE,
+    MCA_PML_BASE_SEND_BUFFERED,
+    MCA_PML_BASE_SEND_READY,
+    MCA_PML_BASE_SEND_STANDARD,
+    MCA_PML_BASE_SEND_SIZE
+} mca_pml_base_send_mode_t;
+
+struct ompi_proc_t;
+struct ompi_message_t;
+/* the module's function types (pml.h:146-470) */
+typedef int (*mca_pml_base_module_add_procs_fn_t)(struct ompi_proc_t **procs, size_t nprocs);
+typedef int (*mca_pml_base_module_del_procs_fn_t)(struct ompi_proc_t **procs, size_t nprocs);
+typedef int (*mca_pml_base_module_enable_fn_t)(bool enable);
+typedef int (*mca_pml_base_module_progress_fn_t)(void);
+typedef int (*mca_pml_base_module_add_comm_fn_t)(struct ompi_communicator_t *comm);
+typedef int (*mca_pml_base_module_del_comm_fn_t)(struct ompi_communicator_t *comm);
+typedef int (*mca_pml_base_module_irecv_init_fn_t)(void *buf, size_t count, struct ompi_datatype_t *datatype, int src,
+                                                   int tag, struct ompi_communicator_t *comm,
+                                                   struct ompi_request_t **request);
+typedef int (*mca_pml_base_module_irecv_fn_t)(void *buf, size_t count, struct ompi_datatype_t *datatype, int src, int tag,
+                                              struct ompi_communicator_t *comm, struct ompi_request_t **request);
+typedef int (*mca_pml_base_module_recv_fn_t)(void *buf, size_t count, struct ompi_datatype_t *datatype, int src, int tag,
+                                             struct ompi_communicator_t *comm, ompi_status_public_t *status);
+typedef int (*mca_pml_base_module_isend_init_fn_t)(void *buf, size_t count, struct ompi_datatype_t *datatype, int dst,
+                                                   int tag, mca_pml_base_send_mode_t mode,
+                                                   struct ompi_communicator_t *comm, struct ompi_request_t **request);
+typedef int (*mca_pml_base_module_isend_fn_t)(void *buf, size_t count, struct ompi_datatype_t *datatype, int dst, int tag,
+                                              mca_pml_base_send_mode_t mode, struct ompi_communicator_t *comm,
+                                              struct ompi_request_t **request);
+typedef int (*mca_pml_base_module_send_fn_t)(void *buf, size_t count, struct ompi_datatype_t *datatype, int dst, int tag,
+                                             mca_pml_base_send_mode_t mode, struct ompi_communicator_t *comm);
+typedef int (*mca_pml_base_module_iprobe_fn_t)(int src, int tag, struct ompi_communicator_t *comm, int *matched,
+                                               ompi_status_public_t *status);
+typedef int (*mca_pml_base_module_probe_fn_t)(int src, int tag, struct ompi_communicator_t *comm,
+                                              ompi_status_public_t *status);
+typedef int (*mca_pml_base_module_start_fn_t)(size_t count, struct ompi_request_t **requests);
+typedef int (*mca_pml_base_module_improbe_fn_t)(int src, int tag, struct ompi_communicator_t *comm, int *matched,
+                                                struct ompi_message_t **message, ompi_status_public_t *status);
+typedef int (*mca_pml_base_module_mprobe_fn_t)(int src, int tag, struct ompi_communicator_t *comm,
+                                               struct ompi_message_t **message, ompi_status_public_t *status);
+typedef int (*mca_pml_base_module_imrecv_fn_t)(void *buf, size_t count, struct ompi_datatype_t *datatype,
+                                               struct ompi_message_t **message, struct ompi_request_t **request);
+typedef int (*mca_pml_base_module_mrecv_fn_t)(void *buf, size_t count, struct ompi_datatype_t *datatype,
+                                              struct ompi_message_t **message, ompi_status_public_t *status);
+typedef int (*mca_pml_base_module_dump_fn_t)(struct ompi_communicator_t *comm, int verbose);
+typedef int (*mca_pml_base_module_ft_event_fn_t)(int status);
+
+/* ompi/mca/pml/pml.h:497-528: the selected PML's function table, the global `mca_pml`
+ * (pml.h:558) that MCA_PML_CALL dispatches through */
+typedef struct mca_pml_base_module_1_0_0_t {
+    mca_pml_base_module_add_procs_fn_t pml_add_procs;
+    mca_pml_base_module_del_procs_fn_t pml_del_procs;
+    mca_pml_base_module_enable_fn_t pml_enable;
+    mca_pml_base_module_progress_fn_t pml_progress;
+    mca_pml_base_module_add_comm_fn_t pml_add_comm;
+    mca_pml_base_module_del_comm_fn_t pml_del_comm;
+    mca_pml_base_module_irecv_init_fn_t pml_irecv_init;
+    mca_pml_base_module_irecv_fn_t pml_irecv;
+    mca_pml_base_module_recv_fn_t pml_recv;
+    mca_pml_base_module_isend_init_fn_t pml_isend_init;
+    mca_pml_base_module_isend_fn_t pml_isend;
+    mca_pml_base_module_send_fn_t pml_send;
+    mca_pml_base_module_iprobe_fn_t pml_iprobe;
+    mca_pml_base_module_probe_fn_t pml_probe;
+    mca_pml_base_module_start_fn_t pml_start;
+    mca_pml_base_module_improbe_fn_t pml_improbe;
+    mca_pml_base_module_mprobe_fn_t pml_mprobe;
+    mca_pml_base_module_imrecv_fn_t pml_imrecv;
+    mca_pml_base_module_mrecv_fn_t pml_mrecv;
+    mca_pml_base_module_dump_fn_t pml_dump;
+    mca_pml_base_module_ft_event_fn_t pml_ft_event;
+    uint32_t pml_max_contextid;
+    int pml_max_tag;
+} mca_pml_base_module_t;
+extern mca_pml_base_module_t mca_pml;
 
 #ifdef __cplusplus
 }

@@ -108,6 +108,7 @@ void mini_init(void)
     static int done = 0;
     if (done) return;
     done = 1;
+    mini_pml_install_stub();
     /* MPI_REQUEST_NULL (ompi_request_init, request.c:108-150): complete, inactive, index 0 */
     ompi_request_null.request.req_type = OMPI_REQUEST_NULL;
     ompi_request_null.request.req_complete = true;
@@ -354,6 +355,17 @@ void mini_comm_install(ompi_communicator_t *c, mca_coll_base_module_t *m)
 
 /* mca_coll_base_comm_select for one extra component (coll_base_comm_select.c:114-262): query,
  * enable, copy non-NULL functions.  Returns the priority, or < 0 when the component declined. */
+/* mca_coll_base_find_available (coll_base_find_available.c:108-160) -> collm_init_query, and
+ * mca_base_component_close -> mca_close_component, for one component */
+int mini_coll_init(mca_coll_base_component_t *comp)
+{
+    return comp->collm_init_query ? comp->collm_init_query(false, false) : OMPI_SUCCESS;
+}
+int mini_coll_close(mca_coll_base_component_t *comp)
+{
+    return comp->collm_version.mca_close_component ? comp->collm_version.mca_close_component() : OMPI_SUCCESS;
+}
+
 int mini_coll_select(ompi_communicator_t *c, mca_coll_base_component_t *comp)
 {
     int prio = 0;
@@ -455,6 +467,7 @@ int mini_progress(void)  /* opal_progress: run every registered callback */
     return events;
 }
 int mini_progress_callbacks(void) { return progress_n; }
+void opal_progress(void) { (void)mini_progress(); }
 /* MPI_Wait on a nonpersistent request (ompi_request_default_wait, req_wait.c:33-90): progress
  * until complete, then free it unless it failed; *req becomes MPI_REQUEST_NULL */
 int mini_wait(ompi_request_t **req)
@@ -465,7 +478,89 @@ int mini_wait(ompi_request_t **req)
     int rc = r->req_free(req);
     return rc;
 }
+/* MPI_Wait with a status (req_wait.c:33-90 copies req_status out before freeing) */
+int mini_wait_status(ompi_request_t **req, ompi_status_public_t *st)
+{
+    ompi_request_t *r = *req;
+    while (!r->req_complete) mini_progress();
+    if (st) *st = r->req_status;
+    if (r->req_status.MPI_ERROR != 0) return r->req_status.MPI_ERROR;
+    return r->req_free(req);
+}
 int mini_request_is_null(ompi_request_t *r) { return r == &ompi_request_null.request; }
+
+/* ---- the PML slot (ompi/mca/pml/pml.h:497-558): `mca_pml` is the selected PML's table and
+ * MCA_PML_CALL(x) is mca_pml.pml_x.  The harness's "selected PML" is a stub (no transport):
+ * it counts calls and returns the stub marker -- what a host-buffer message would hand to ob1. */
+mca_pml_base_module_t mca_pml;
+static int pml_stub_calls[8];
+static int pst_isend(void *b, size_t n, struct ompi_datatype_t *d, int dst, int tag, mca_pml_base_send_mode_t m,
+                     struct ompi_communicator_t *c, struct ompi_request_t **req)
+{ (void)b; (void)n; (void)d; (void)dst; (void)tag; (void)m; (void)c; *req = &ompi_request_null.request; pml_stub_calls[0]++; return 77; }
+static int pst_send(void *b, size_t n, struct ompi_datatype_t *d, int dst, int tag, mca_pml_base_send_mode_t m,
+                    struct ompi_communicator_t *c)
+{ (void)b; (void)n; (void)d; (void)dst; (void)tag; (void)m; (void)c; pml_stub_calls[1]++; return 77; }
+static int pst_irecv(void *b, size_t n, struct ompi_datatype_t *d, int src, int tag, struct ompi_communicator_t *c,
+                     struct ompi_request_t **req)
+{ (void)b; (void)n; (void)d; (void)src; (void)tag; (void)c; *req = &ompi_request_null.request; pml_stub_calls[2]++; return 77; }
+static int pst_recv(void *b, size_t n, struct ompi_datatype_t *d, int src, int tag, struct ompi_communicator_t *c,
+                    ompi_status_public_t *st)
+{ (void)b; (void)n; (void)d; (void)src; (void)tag; (void)c; (void)st; pml_stub_calls[3]++; return 77; }
+static int pst_iprobe(int src, int tag, struct ompi_communicator_t *c, int *matched, ompi_status_public_t *st)
+{ (void)src; (void)tag; (void)c; (void)st; *matched = 0; pml_stub_calls[4]++; return 0; }
+static int pst_probe(int src, int tag, struct ompi_communicator_t *c, ompi_status_public_t *st)
+{ (void)src; (void)tag; (void)c; (void)st; pml_stub_calls[5]++; return 77; }
+
+void mini_pml_install_stub(void)
+{
+    memset(&mca_pml, 0, sizeof(mca_pml));
+    mca_pml.pml_isend = pst_isend;
+    mca_pml.pml_send = pst_send;
+    mca_pml.pml_irecv = pst_irecv;
+    mca_pml.pml_recv = pst_recv;
+    mca_pml.pml_iprobe = pst_iprobe;
+    mca_pml.pml_probe = pst_probe;
+    mca_pml.pml_max_tag = 0x7fffffff;
+}
+int mini_pml_stub_calls(int which) { return (which >= 0 && which < 8) ? pml_stub_calls[which] : -1; }
+void *mini_pml_fn(int which)
+{
+    switch (which) {
+    case 0: return (void *)mca_pml.pml_isend;
+    case 1: return (void *)mca_pml.pml_send;
+    case 2: return (void *)mca_pml.pml_irecv;
+    case 3: return (void *)mca_pml.pml_recv;
+    case 4: return (void *)mca_pml.pml_iprobe;
+    case 5: return (void *)mca_pml.pml_probe;
+    default: return NULL;
+    }
+}
+/* MPI_Send / MPI_Recv / MPI_Isend / MPI_Irecv / MPI_Iprobe as the bindings call them
+ * (ompi/mpi/c/send.c:75, recv.c:69, isend.c:76, irecv.c:69, iprobe.c:67): MCA_PML_CALL(...) */
+int mini_send(void *b, int n, ompi_datatype_t *d, int dst, int tag, ompi_communicator_t *c)
+{
+    return mca_pml.pml_send(b, (size_t)n, d, dst, tag, MCA_PML_BASE_SEND_STANDARD, c);
+}
+int mini_ssend(void *b, int n, ompi_datatype_t *d, int dst, int tag, ompi_communicator_t *c)
+{
+    return mca_pml.pml_send(b, (size_t)n, d, dst, tag, MCA_PML_BASE_SEND_SYNCHRONOUS, c);
+}
+int mini_recv(void *b, int n, ompi_datatype_t *d, int src, int tag, ompi_communicator_t *c, ompi_status_public_t *st)
+{
+    return mca_pml.pml_recv(b, (size_t)n, d, src, tag, c, st);
+}
+int mini_isend(void *b, int n, ompi_datatype_t *d, int dst, int tag, ompi_communicator_t *c, ompi_request_t **req)
+{
+    return mca_pml.pml_isend(b, (size_t)n, d, dst, tag, MCA_PML_BASE_SEND_STANDARD, c, req);
+}
+int mini_irecv(void *b, int n, ompi_datatype_t *d, int src, int tag, ompi_communicator_t *c, ompi_request_t **req)
+{
+    return mca_pml.pml_irecv(b, (size_t)n, d, src, tag, c, req);
+}
+int mini_iprobe(int src, int tag, ompi_communicator_t *c, int *flag, ompi_status_public_t *st)
+{
+    return mca_pml.pml_iprobe(src, tag, c, flag, st);
+}
 int mini_request_complete(ompi_request_t *r) { return r->req_complete ? 1 : 0; }
 
 /* C-callable MPI-style entry points through the communicator's installed functions */

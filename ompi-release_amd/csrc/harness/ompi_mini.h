@@ -41,6 +41,19 @@ mca_coll_base_module_t *mini_stub_module(void);
 int mini_stub_calls(int which);
 int mini_stub_marker(void);
 size_t mini_offsetof(int which);
+/* the PML slot: a counting stub as the selected PML, and the bindings' MCA_PML_CALL paths */
+int mini_coll_init(mca_coll_base_component_t *comp);
+int mini_coll_close(mca_coll_base_component_t *comp);
+void mini_pml_install_stub(void);
+int mini_pml_stub_calls(int which);
+void *mini_pml_fn(int which);
+int mini_send(void *b, int n, ompi_datatype_t *d, int dst, int tag, ompi_communicator_t *c);
+int mini_ssend(void *b, int n, ompi_datatype_t *d, int dst, int tag, ompi_communicator_t *c);
+int mini_recv(void *b, int n, ompi_datatype_t *d, int src, int tag, ompi_communicator_t *c, ompi_status_public_t *st);
+int mini_isend(void *b, int n, ompi_datatype_t *d, int dst, int tag, ompi_communicator_t *c, ompi_request_t **req);
+int mini_irecv(void *b, int n, ompi_datatype_t *d, int src, int tag, ompi_communicator_t *c, ompi_request_t **req);
+int mini_iprobe(int src, int tag, ompi_communicator_t *c, int *flag, ompi_status_public_t *st);
+int mini_wait_status(ompi_request_t **req, ompi_status_public_t *st);
 
 #ifdef __cplusplus
 }

@@ -615,6 +615,7 @@ int mca_coll_mi355x_exscan(void *sbuf, void *rbuf, int count, struct ompi_dataty
 typedef struct mi355x_nbreq_t {
     ompi_request_t super;
     mi355x_request_t *eng;
+    int p2p;                       /* 0 collective, 1 send, 2 receive (status filled at completion) */
     struct mi355x_nbreq_t *next;   /* active list */
 } mi355x_nbreq_t;
 
@@ -667,8 +668,20 @@ static int nb_progress(void)
             continue;
         }
         *p = r->next;
-        if (rc != MI355X_SUCCESS) fprintf(stderr, "[coll/mi355x] %s\n", mi355x_last_error());
-        r->super.req_status.MPI_ERROR = (rc == MI355X_SUCCESS) ? 0 : MPI_ERR_INTERN;
+        if (r->p2p == 2) {  /* MPI_Status of a receive (pml_ob1_recvreq.h:172-180 for truncation) */
+            mi355x_status_t st;
+            memset(&st, 0, sizeof(st));
+            mi355x_request_get_status(r->eng, &st);
+            r->super.req_status.MPI_SOURCE = st.source;
+            r->super.req_status.MPI_TAG = st.tag;
+            r->super.req_status._ucount = st.bytes;
+        }
+        if (rc == MI355X_ERR_TRUNCATE) {
+            r->super.req_status.MPI_ERROR = MPI_ERR_TRUNCATE;
+        } else {
+            if (rc != MI355X_SUCCESS) fprintf(stderr, "[coll/mi355x] %s\n", mi355x_last_error());
+            r->super.req_status.MPI_ERROR = (rc == MI355X_SUCCESS) ? 0 : MPI_ERR_INTERN;
+        }
         mi355x_request_free(r->eng);
         r->eng = NULL;
         mi355x_ompi_request_complete(&r->super, true);
@@ -680,7 +693,7 @@ static int nb_progress(void)
 
 /* wrap an engine request into an active MPI request (OMPI_REQUEST_INIT + ACTIVE, coll_libnbc.h:
  * 126-131) */
-static int nb_start(mi355x_request_t *eng, struct ompi_communicator_t *comm, ompi_request_t **request)
+static int nb_start_kind(mi355x_request_t *eng, struct ompi_communicator_t *comm, ompi_request_t **request, int p2p)
 {
     mi355x_nbreq_t *r = (mi355x_nbreq_t *)mi355x_obj_new(&mi355x_nbreq_t_class);
     if (!r) {
@@ -688,6 +701,8 @@ static int nb_start(mi355x_request_t *eng, struct ompi_communicator_t *comm, omp
         mi355x_request_free(eng);
         return OMPI_ERR_OUT_OF_RESOURCE;
     }
+    r->p2p = p2p;
+    if (p2p) r->super.req_type = OMPI_REQUEST_PML;
     r->super.req_complete = false;
     r->super.req_persistent = false;
     r->super.req_state = OMPI_REQUEST_ACTIVE;
@@ -704,6 +719,11 @@ static int nb_start(mi355x_request_t *eng, struct ompi_communicator_t *comm, omp
     pthread_mutex_unlock(&nb_lock);
     *request = &r->super;
     return OMPI_SUCCESS;
+}
+
+static int nb_start(mi355x_request_t *eng, struct ompi_communicator_t *comm, ompi_request_t **request)
+{
+    return nb_start_kind(eng, comm, request, 0);
 }
 
 #define NB_FALLBACK(FN, ...)                                                          \
@@ -786,6 +806,169 @@ int mca_coll_mi355x_ibcast(void *buff, int count, struct ompi_datatype_t *dataty
     mi355x_request_t *eng = NULL;
     int rc = mi355x_ibcast(m->engine, buff, bytes, root, NULL, &eng);
     return rc ? map_rc(rc) : nb_start(eng, comm, request);
+}
+
+/* ------------------------------------------------------------------ device point-to-point (PML hook)
+ * ob1 moves a device message with its CUDA hooks: the send request gets a CUDA convertor and goes
+ * by RGET over smcuda's IPC (pml_ob1_cuda.c:52-100, RDMA btls :104-154, IPC enabling :183-210).
+ * coll/mi355x owns a device engine per communicator that already does that protocol device-
+ * natively (engine p2p: rendezvous envelope in the shared control segment, the receiver pulls
+ * over xGMI), so this shim routes device-buffer point-to-point on those communicators to it.  It
+ * is installed the way pml/v parasites the selected PML (pml_v_component.c:110-131): once the PML
+ * is selected (coll components are queried after it, ompi_mpi_init.c:610-660) the selected
+ * module's table `mca_pml` is saved and its send / receive / probe entries are replaced;
+ * everything else -- host buffers, communicators without the engine, buffered sends, persistent
+ * and matched-probe requests -- goes to the saved entries unchanged.
+ * Matching rule: on an engine communicator a message travels by the engine when
+ * the SENDER's buffer is device memory, so a device send must be received into a device buffer
+ * (and a host send into a host buffer); a probe looks at both. */
+static mca_pml_base_module_t host_pml;
+static int pml_hooked;
+
+static mca_coll_mi355x_module_t *engine_module(struct ompi_communicator_t *comm)
+{
+    if (!comm || comm->c_coll.coll_allreduce != mca_coll_mi355x_allreduce || !comm->c_coll.coll_allreduce_module)
+        return NULL;
+    mca_coll_mi355x_module_t *m = MOD(comm->c_coll.coll_allreduce_module);
+    return m->engine ? m : NULL;
+}
+
+/* `count` instances of dt as the engine's (count, layout): contiguous -> bytes and no layout */
+static int p2p_layout(mca_coll_mi355x_module_t *m, struct ompi_datatype_t *dt, size_t count, size_t *ecount,
+                      mi355x_ddt_t **d)
+{
+    size_t b;
+    if (count <= (size_t)0x7fffffff && contiguous_bytes(dt, (int)count, &b)) {
+        *ecount = b;
+        *d = NULL;
+        return 1;
+    }
+    *d = ddt_of(m, dt);
+    *ecount = count;
+    return *d != NULL;
+}
+
+int mca_coll_mi355x_pml_isend(void *buf, size_t count, struct ompi_datatype_t *dt, int dst, int tag,
+                              mca_pml_base_send_mode_t mode, struct ompi_communicator_t *comm,
+                              ompi_request_t **request)
+{
+    mca_coll_mi355x_module_t *m = engine_module(comm);
+    size_t ec = 0;
+    mi355x_ddt_t *d = NULL;
+    if (!m || mode == MCA_PML_BASE_SEND_BUFFERED || !is_dev(buf) || !p2p_layout(m, dt, count, &ec, &d))
+        return host_pml.pml_isend(buf, count, dt, dst, tag, mode, comm, request);
+    mi355x_request_t *eng = NULL;
+    const int rc = mi355x_isend(m->engine, buf, ec, d, dst, tag, NULL, &eng);
+    return rc ? map_rc(rc) : nb_start_kind(eng, comm, request, 1);
+}
+
+/* the engine's sends are rendezvous: they complete once the receiver has the data, which is
+ * what every send mode but buffered requires (synchronous included) */
+int mca_coll_mi355x_pml_send(void *buf, size_t count, struct ompi_datatype_t *dt, int dst, int tag,
+                             mca_pml_base_send_mode_t mode, struct ompi_communicator_t *comm)
+{
+    mca_coll_mi355x_module_t *m = engine_module(comm);
+    size_t ec = 0;
+    mi355x_ddt_t *d = NULL;
+    if (!m || mode == MCA_PML_BASE_SEND_BUFFERED || !is_dev(buf) || !p2p_layout(m, dt, count, &ec, &d))
+        return host_pml.pml_send(buf, count, dt, dst, tag, mode, comm);
+    return map_rc(mi355x_send(m->engine, buf, ec, d, dst, tag, NULL));
+}
+
+int mca_coll_mi355x_pml_irecv(void *buf, size_t count, struct ompi_datatype_t *dt, int src, int tag,
+                              struct ompi_communicator_t *comm, ompi_request_t **request)
+{
+    mca_coll_mi355x_module_t *m = engine_module(comm);
+    size_t ec = 0;
+    mi355x_ddt_t *d = NULL;
+    if (!m || !is_dev(buf) || !p2p_layout(m, dt, count, &ec, &d))
+        return host_pml.pml_irecv(buf, count, dt, src, tag, comm, request);
+    mi355x_request_t *eng = NULL;
+    const int rc = mi355x_irecv(m->engine, buf, ec, d, src, tag, NULL, &eng);
+    return rc ? map_rc(rc) : nb_start_kind(eng, comm, request, 2);
+}
+
+int mca_coll_mi355x_pml_recv(void *buf, size_t count, struct ompi_datatype_t *dt, int src, int tag,
+                             struct ompi_communicator_t *comm, ompi_status_public_t *status)
+{
+    mca_coll_mi355x_module_t *m = engine_module(comm);
+    size_t ec = 0;
+    mi355x_ddt_t *d = NULL;
+    if (!m || !is_dev(buf) || !p2p_layout(m, dt, count, &ec, &d))
+        return host_pml.pml_recv(buf, count, dt, src, tag, comm, status);
+    mi355x_status_t st;
+    memset(&st, 0, sizeof(st));
+    const int rc = mi355x_recv(m->engine, buf, ec, d, src, tag, NULL, &st);
+    if (status) {  /* MPI_STATUS_IGNORE is NULL */
+        status->MPI_SOURCE = st.source;
+        status->MPI_TAG = st.tag;
+        status->_ucount = st.bytes;
+        status->MPI_ERROR = rc == MI355X_ERR_TRUNCATE ? MPI_ERR_TRUNCATE : (rc ? MPI_ERR_INTERN : 0);
+    }
+    if (rc == MI355X_ERR_TRUNCATE) return MPI_ERR_TRUNCATE;
+    return map_rc(rc);
+}
+
+/* a probe carries no buffer: the engine's envelopes first, then the host PML's */
+int mca_coll_mi355x_pml_iprobe(int src, int tag, struct ompi_communicator_t *comm, int *matched,
+                               ompi_status_public_t *status)
+{
+    mca_coll_mi355x_module_t *m = engine_module(comm);
+    if (m) {
+        mi355x_status_t st;
+        int flag = 0;
+        const int rc = mi355x_iprobe(m->engine, src, tag, &flag, &st);
+        if (rc != MI355X_SUCCESS) return map_rc(rc);
+        if (flag) {
+            *matched = 1;
+            if (status) {
+                status->MPI_SOURCE = st.source;
+                status->MPI_TAG = st.tag;
+                status->_ucount = st.bytes;
+                status->MPI_ERROR = 0;
+            }
+            return OMPI_SUCCESS;
+        }
+    }
+    return host_pml.pml_iprobe(src, tag, comm, matched, status);
+}
+
+int mca_coll_mi355x_pml_probe(int src, int tag, struct ompi_communicator_t *comm, ompi_status_public_t *status)
+{
+    if (!engine_module(comm)) return host_pml.pml_probe(src, tag, comm, status);
+    for (;;) {  /* both sources of messages, progressing everything in between */
+        int matched = 0;
+        const int rc = mca_coll_mi355x_pml_iprobe(src, tag, comm, &matched, status);
+        if (rc != OMPI_SUCCESS || matched) return rc;
+        opal_progress();
+    }
+}
+
+/* install / remove the hook (idempotent) */
+static void pml_hook_install(void)
+{
+    if (pml_hooked || env_int("OMPI_MCA_coll_mi355x_pml_hook", 1) == 0) return;
+    if (!mca_pml.pml_isend || !mca_pml.pml_irecv || !mca_pml.pml_send || !mca_pml.pml_recv) return;  /* no PML */
+    host_pml = mca_pml;
+    mca_pml.pml_isend = mca_coll_mi355x_pml_isend;
+    mca_pml.pml_send = mca_coll_mi355x_pml_send;
+    mca_pml.pml_irecv = mca_coll_mi355x_pml_irecv;
+    mca_pml.pml_recv = mca_coll_mi355x_pml_recv;
+    if (mca_pml.pml_iprobe) mca_pml.pml_iprobe = mca_coll_mi355x_pml_iprobe;
+    if (mca_pml.pml_probe) mca_pml.pml_probe = mca_coll_mi355x_pml_probe;
+    pml_hooked = 1;
+}
+
+static void pml_hook_remove(void)
+{
+    if (!pml_hooked) return;
+    if (mca_pml.pml_isend == mca_coll_mi355x_pml_isend) mca_pml.pml_isend = host_pml.pml_isend;
+    if (mca_pml.pml_send == mca_coll_mi355x_pml_send) mca_pml.pml_send = host_pml.pml_send;
+    if (mca_pml.pml_irecv == mca_coll_mi355x_pml_irecv) mca_pml.pml_irecv = host_pml.pml_irecv;
+    if (mca_pml.pml_recv == mca_coll_mi355x_pml_recv) mca_pml.pml_recv = host_pml.pml_recv;
+    if (mca_pml.pml_iprobe == mca_coll_mi355x_pml_iprobe) mca_pml.pml_iprobe = host_pml.pml_iprobe;
+    if (mca_pml.pml_probe == mca_coll_mi355x_pml_probe) mca_pml.pml_probe = host_pml.pml_probe;
+    pml_hooked = 0;
 }
 
 /* ------------------------------------------------------------------ module / component */
@@ -899,6 +1082,7 @@ static int component_register(void)
 static int component_open(void) { return OMPI_SUCCESS; }
 static int component_close(void)
 {
+    pml_hook_remove();
     if (tuned_rules) mi355x_rules_destroy(tuned_rules);
     tuned_rules = NULL;
     tuned_rules_read = 0;
@@ -911,6 +1095,7 @@ static int component_init_query(bool enable_progress_threads, bool enable_mpi_th
     (void)enable_mpi_threads;
     int n = 0;
     if (mi355x_device_count(&n) != MI355X_SUCCESS || n < 1) return OMPI_ERR_NOT_SUPPORTED;
+    pml_hook_install();  /* the PML is selected by now (ompi_mpi_init.c:610 before :660) */
     return OMPI_SUCCESS;
 }
 

@@ -6,6 +6,7 @@ from __future__ import annotations
 import ctypes
 import pathlib
 import sys
+import time
 
 import numpy as np
 
@@ -276,9 +277,132 @@ def split_main():
     print(f"rank {wrank} split OK", flush=True)
 
 
+class Status(ctypes.Structure):  # ompi_status_public_t (mpi.h.in:344-356)
+    _fields_ = [("MPI_SOURCE", ctypes.c_int), ("MPI_TAG", ctypes.c_int), ("MPI_ERROR", ctypes.c_int),
+                ("_cancelled", ctypes.c_int), ("_ucount", ctypes.c_size_t)]
+
+
+def pml_main():
+    """MPI_Send / MPI_Ssend / MPI_Recv / MPI_Isend / MPI_Irecv / MPI_Iprobe through the PML slot
+    (`mca_pml`, the table the MPI layer calls, e.g. ompi/mpi/c/send.c:67) once coll/mi355x's
+    init_query has hooked it: device buffers on the engine communicator move device data, host
+    buffers reach the saved (stub) PML, and closing the component restores the table"""
+    rank, size = int(sys.argv[1]), int(sys.argv[2])
+    import torch
+    torch.cuda.set_device(rank % torch.cuda.device_count())
+    m = mini()
+    L, pkg = m.lib, m.pkg
+    oracle = load_oracle()
+    m.install_oracle_base(oracle)
+    comp = m.component_ptr(m.coll, "mca_coll_mi355x_component")
+    stub_send = L.mini_pml_fn(1)
+    assert L.mini_coll_init(comp) == 0
+    hooked = [L.mini_pml_fn(w) for w in range(6)]
+    names = ["isend", "send", "irecv", "recv", "iprobe", "probe"]
+    for w, nm in enumerate(names):
+        assert hooked[w] == m.addr(m.coll, f"mca_coll_mi355x_pml_{nm}"), f"pml_{nm} not hooked"
+    comm = L.mini_comm_create(rank, size, 42)
+    L.mini_comm_set_channel(comm, sys.argv[3].encode())
+    L.mini_comm_install(comm, L.mini_stub_module())
+    assert L.mini_coll_select(comm, comp) == 90
+    fdt = m.dtype_for_slot(pkg.T["FLOAT"])
+    ANY = -1
+    st = Status()
+    n = 1 << 20
+    # 1. MPI_Send from rank 0 to every rank, MPI_Recv(MPI_ANY_SOURCE) with the status
+    if rank == 0:
+        for q in range(1, size):
+            x = torch.arange(n, dtype=torch.float32, device="cuda") + 1000 * q
+            torch.cuda.synchronize()
+            assert L.mini_send(x.data_ptr(), n, fdt, q, 11, comm) == 0
+    else:
+        y = torch.zeros(n, device="cuda")
+        assert L.mini_recv(y.data_ptr(), n, fdt, ANY, 11, comm, ctypes.byref(st)) == 0
+        assert torch.equal(y, torch.arange(n, dtype=torch.float32, device="cuda") + 1000 * rank), "send/recv data"
+        assert (st.MPI_SOURCE, st.MPI_TAG, st.MPI_ERROR, st._ucount) == (0, 11, 0, 4 * n), \
+            (st.MPI_SOURCE, st.MPI_TAG, st.MPI_ERROR, st._ucount)
+    # 2. MPI_Ssend back to rank 0, received by source in rank order, MPI_STATUS_IGNORE
+    if rank == 0:
+        for q in range(1, size):
+            y = torch.zeros(777, dtype=torch.int32, device="cuda")
+            assert L.mini_recv(y.data_ptr(), 777, m.dtype_for_slot(pkg.T["INT32"]), q, ANY, comm, None) == 0
+            assert torch.equal(y, torch.full((777,), 7 * q, dtype=torch.int32, device="cuda")), "ssend data"
+    else:
+        x = torch.full((777,), 7 * rank, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        assert L.mini_ssend(x.data_ptr(), 777, m.dtype_for_slot(pkg.T["INT32"]), 0, 12, comm) == 0
+    # 3. ring of MPI_Irecv + MPI_Isend (receive posted first), MPI_Wait with status
+    nr = 3_000_001
+    src = torch.full((nr,), float(rank + 1), device="cuda")
+    dst = torch.zeros(nr, device="cuda")
+    torch.cuda.synchronize()
+    rq, sq = ctypes.c_void_p(), ctypes.c_void_p()
+    left, right = (rank - 1) % size, (rank + 1) % size
+    assert L.mini_irecv(dst.data_ptr(), nr, fdt, left, 13, comm, ctypes.byref(rq)) == 0
+    assert L.mini_isend(src.data_ptr(), nr, fdt, right, 13, comm, ctypes.byref(sq)) == 0
+    assert L.mini_wait_status(ctypes.byref(sq), None) == 0
+    assert L.mini_wait_status(ctypes.byref(rq), ctypes.byref(st)) == 0
+    assert L.mini_request_is_null(rq) and L.mini_request_is_null(sq)
+    assert (st.MPI_SOURCE, st.MPI_TAG, st._ucount) == (left, 13, 4 * nr)
+    assert bool((dst == left + 1).all()), "isend/irecv ring"
+    # 4. a derived send type (vector(1000, 64, 128, MPI_FLOAT)) into a contiguous receive
+    if size >= 2 and rank in (0, 1):
+        nblk = 1000
+        desc, used, tsize, lb, ub = opal_vector(nblk, 256, 512)
+        vdt = m.derived(desc, used, tsize, lb, ub)
+        if rank == 0:
+            full = torch.arange(nblk * 128, dtype=torch.float32, device="cuda")
+            torch.cuda.synchronize()
+            assert L.mini_send(full.data_ptr(), 1, vdt, 1, 14, comm) == 0
+        else:
+            got = torch.zeros(nblk * 64, device="cuda")
+            assert L.mini_recv(got.data_ptr(), nblk * 64, fdt, 0, 14, comm, ctypes.byref(st)) == 0
+            want = torch.arange(nblk * 128, dtype=torch.float32).view(nblk, 128)[:, :64].reshape(-1)
+            assert torch.equal(got.cpu(), want), "derived send -> contiguous recv"
+            assert st._ucount == tsize
+        L.mini_datatype_destroy(vdt)
+    # 5. MPI_Iprobe sees the envelope before the receive; truncation reports MPI_ERR_TRUNCATE
+    if rank == 0:
+        x = torch.ones(1000, device="cuda")
+        torch.cuda.synchronize()
+        q = ctypes.c_void_p()
+        assert L.mini_isend(x.data_ptr(), 1000, fdt, size - 1, 15, comm, ctypes.byref(q)) == 0
+        assert L.mini_wait_status(ctypes.byref(q), None) == 0
+    elif rank == size - 1:
+        flag = ctypes.c_int(0)
+        t0 = time.time()
+        while not flag.value:
+            assert L.mini_iprobe(0, 15, comm, ctypes.byref(flag), ctypes.byref(st)) == 0
+            assert time.time() - t0 < 30, "iprobe never matched"
+        assert (st.MPI_SOURCE, st.MPI_TAG, st._ucount) == (0, 15, 4000)
+        y = torch.zeros(500, device="cuda")
+        rc = L.mini_recv(y.data_ptr(), 500, fdt, 0, 15, comm, ctypes.byref(st))
+        assert rc == 15 and st.MPI_ERROR == 15, (rc, st.MPI_ERROR)  # MPI_ERR_TRUNCATE
+        assert bool((y == 1).all())
+    # 6. host buffers and buffered sends -> the saved PML (the stub answers 77)
+    h = np.zeros(16, dtype=np.float32)
+    before = [L.mini_pml_stub_calls(w) for w in range(6)]
+    assert L.mini_send(h.ctypes.data, 16, fdt, right, 16, comm) == 77
+    assert L.mini_recv(h.ctypes.data, 16, fdt, left, 16, comm, None) == 77
+    assert L.mini_isend(h.ctypes.data, 16, fdt, right, 16, comm, ctypes.byref(sq)) == 77
+    assert L.mini_irecv(h.ctypes.data, 16, fdt, left, 16, comm, ctypes.byref(rq)) == 77
+    after = [L.mini_pml_stub_calls(w) for w in range(6)]
+    assert [a - b for a, b in zip(after, before)][:4] == [1, 1, 1, 1], (before, after)
+    # a probe with nothing pending asks the engine, then the saved PML
+    flag = ctypes.c_int(1)
+    assert L.mini_iprobe(ANY, 999, comm, ctypes.byref(flag), ctypes.byref(st)) == 0 and flag.value == 0
+    assert L.mini_pml_stub_calls(4) == before[4] + 1
+    L.mini_comm_destroy(comm)
+    assert L.mini_coll_close(comp) == 0
+    assert L.mini_pml_fn(1) == stub_send, "component close restores the PML table"
+    print(f"rank {rank} pml OK", flush=True)
+
+
 def main():
     if len(sys.argv) > 4 and sys.argv[4] == "split":
         return split_main()
+    if len(sys.argv) > 4 and sys.argv[4] == "pml":
+        return pml_main()
     rank, size = int(sys.argv[1]), int(sys.argv[2])
     import torch
     ndev = torch.cuda.device_count()

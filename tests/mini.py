@@ -43,6 +43,18 @@ class Mini:
         L.mini_comm_install.argtypes = [vp, vp]
         L.mini_comm_set_channel.argtypes = [vp, ctypes.c_char_p]
         L.mini_coll_select.argtypes = [vp, vp]
+        L.mini_coll_init.argtypes = [vp]
+        L.mini_coll_close.argtypes = [vp]
+        L.mini_pml_fn.restype = vp
+        L.mini_pml_fn.argtypes = [i]
+        L.mini_pml_stub_calls.argtypes = [i]
+        L.mini_send.argtypes = [vp, i, vp, i, i, vp]
+        L.mini_ssend.argtypes = [vp, i, vp, i, i, vp]
+        L.mini_recv.argtypes = [vp, i, vp, i, i, vp, vp]
+        L.mini_isend.argtypes = [vp, i, vp, i, i, vp, ctypes.POINTER(vp)]
+        L.mini_irecv.argtypes = [vp, i, vp, i, i, vp, ctypes.POINTER(vp)]
+        L.mini_iprobe.argtypes = [i, i, vp, ctypes.POINTER(i), vp]
+        L.mini_wait_status.argtypes = [ctypes.POINTER(vp), vp]
         L.mini_coll_module_new.restype = vp
         L.mini_comm_destroy.argtypes = [vp]
         L.mini_allreduce.argtypes = [vp, vp, vp, i, vp, vp]

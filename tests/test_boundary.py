@@ -230,3 +230,21 @@ def test_harness_host_bcast_channel():
     for p in ps:
         p.join(30)
     assert res == {0: "ok", 1: "ok", 2: "ok"}, res
+
+
+def test_pml_hook_install_and_close():
+    """coll/mi355x's init_query hooks the PML slot only when a device is there (and
+    OMPI_MCA_coll_mi355x_pml_hook is not 0); component close puts the saved entries back"""
+    m = mini()
+    L = m.lib
+    comp = m.component_ptr(m.coll, "mca_coll_mi355x_component")
+    saved = [L.mini_pml_fn(w) for w in range(6)]
+    names = ["isend", "send", "irecv", "recv", "iprobe", "probe"]
+    rc = L.mini_coll_init(comp)
+    now = [L.mini_pml_fn(w) for w in range(6)]
+    if rc != 0:  # no GPU here: the component declines and the PML is untouched
+        assert now == saved
+    else:
+        assert now == [m.addr(m.coll, f"mca_coll_mi355x_pml_{n}") for n in names]
+    assert L.mini_coll_close(comp) == 0
+    assert [L.mini_pml_fn(w) for w in range(6)] == saved

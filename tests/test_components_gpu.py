@@ -117,3 +117,27 @@ def test_split_communicators_same_cid(gpu):
         outs.append(out)
     for w, p in enumerate(procs):
         assert p.returncode == 0 and f"rank {w} split OK" in outs[w], f"rank {w}:\n{outs[w][-3000:]}"
+
+
+@pytest.mark.parametrize("size", [2, 3])
+def test_pml_slot_device_p2p(gpu, size):
+    """MPI point-to-point through the PML slot (`mca_pml`): coll/mi355x's init_query hooks the
+    selected PML the way pml/v does (pml_v_component.c:110-131); MPI_Send/Ssend/Recv/Isend/Irecv/
+    Iprobe on device buffers move device data through the engine (statuses, MPI_ANY_SOURCE, a
+    derived send type, truncation), host buffers reach the saved PML, close restores the table"""
+    key = uuid.uuid4().hex[:10]
+    env = dict(os.environ, MI355X_TIMEOUT_S="60", OMPI_COMM_WORLD_SIZE=str(size),
+               OMPI_COMM_WORLD_LOCAL_SIZE=str(size), OMPI_MCA_ess_base_jobid=key)
+    procs = [subprocess.Popen([sys.executable, str(HERE / "coll_worker.py"), str(r), str(size), key, "pml"],
+                              env=dict(env, OMPI_COMM_WORLD_LOCAL_RANK=str(r), OMPI_COMM_WORLD_RANK=str(r)),
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(size)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=300)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, _ = p.communicate()
+        outs.append(out)
+    for r, p in enumerate(procs):
+        assert p.returncode == 0 and f"rank {r} pml OK" in outs[r], f"rank {r}:\n{outs[r][-3000:]}"
