@@ -73,3 +73,83 @@ def opal_strided_elems(n, elem_type, elem_size, stride_bytes, disp=0):
     """one ELEM record of n strided basic elements (extent != size): e.g. vector(n, 1, 2, MPI_FLOAT)"""
     desc = rec_elem(elem_type, n, stride_bytes, disp)
     return desc, 1, n * elem_size, disp, disp + (n - 1) * stride_bytes + elem_size
+
+
+# ---- the datatype tests of test/datatype/opal_datatype_test.c:338-541, on types restated by
+#      oracle/opal_types.py (opal_datatype_add + the test library's constructors)
+import pathlib  # noqa: E402
+import sys  # noqa: E402
+
+sys.path.insert(0, str(pathlib.Path(__file__).resolve().parent.parent / "oracle"))
+import opal_types as ot  # noqa: E402
+
+
+def _f8():
+    return ot.OpalType.basic("FLOAT8")
+
+
+# (name, builder, count, chunks): every local_copy_with_convertor(pdt, count, chunk) of main()
+CONVERTOR_CASES = [
+    ("contig_int1x10", lambda: ot.contiguous(10, ot.OpalType.basic("INT1")).commit(), 100, [956]),   # :350-354
+    ("strange", ot.strange_dt, 1, [956]),                                                          # :358-362
+    ("upper_matrix_100", lambda: ot.upper_matrix(100), 1, [48]),                                   # :367-371
+    ("float8", _f8, 4500, [12]),                                                                   # :433-436
+    ("contig_f8_4500", lambda: ot.contiguous(4500, _f8()).commit(), 1, [12]),                      # :443-447
+    ("contig_f8_450", lambda: ot.contiguous(450, _f8()).commit(), 10, [12]),
+    ("contig_f8_45", lambda: ot.contiguous(45, _f8()).commit(), 100, [12]),
+    ("contig_f8_100", lambda: ot.contiguous(100, _f8()).commit(), 45, [12]),
+    ("contig_f8_10", lambda: ot.contiguous(10, _f8()).commit(), 450, [12]),
+    ("contig_f8_1", lambda: ot.contiguous(1, _f8()).commit(), 4500, [12]),
+    ("vector_450_10_11", lambda: ot.vector(450, 10, 11, _f8()).commit(), 1, [12, 82, 6000, 36000]),  # :482-493
+    ("struct_char_double", ot.struct_char_double, 4500, [12]),                                     # :499-503
+    ("twice_two_doubles", ot.twice_two_doubles, 4500, [12]),                                       # :509-513
+    ("blacs", ot.blacs, 4500, [956, 16 * 1024, 64 * 1024]),                                        # :519-528
+    ("typeub_hindexed", lambda: ot.typeub3()[0], 7, [5]),  # the LB/UB types moved as data too
+    ("typeub_indexed", lambda: ot.typeub3()[1], 7, [6]),
+    ("typeub_vector", lambda: ot.typeub3()[3], 5, [4]),
+    ("test_struct", ot.test_struct, 33, [7]),
+]
+
+
+def windows(oracle, od, count, chunk):
+    """the successive (pos, size) of a convertor driven with `chunk`-byte iovecs: each stops at the
+    last basic-element boundary that fits (opal_generic_simple_pack packs whole elements)"""
+    total = count * oracle.oracle_ddt_size(od)
+    pos, out = 0, []
+    while pos < total:
+        nxt = oracle.oracle_ddt_round_position(od, count, min(pos + chunk, total))
+        if nxt <= pos:  # an element larger than the chunk: split it (contiguous fast path)
+            nxt = min(pos + chunk, total)
+        out.append((pos, nxt - pos))
+        pos = nxt
+    return out
+
+
+def c_oracle(oracle, t):
+    """the byte-level oracle (oracle/ddt_oracle.c) of a restated type: its merged runs + extent"""
+    runs = t.runs()
+    n = len(runs)
+    a = ctypes.c_int64 * n
+    return oracle.oracle_ddt_struct(n, a(*[r[0] for r in runs]), a(*[r[1] for r in runs]), a(*[r[2] for r in runs]),
+                                    t.extent)
+
+
+def span_of(t, count):
+    """(bytes, origin): a buffer holding `count` instances whose first instance starts at origin"""
+    lo = min(0, t.true_lb, t.lb)
+    hi = max((count - 1) * t.extent + t.true_ub, (count - 1) * t.extent + t.ub)
+    return hi - lo, -lo
+
+
+def fill_pattern(n):
+    """psrc[i] = i % 128 + 32 (opal_datatype_test.c:269-272)"""
+    return (np.arange(n) % 128 + 32).astype(np.uint8)
+
+
+def expected_copy(t, count, src, origin):
+    """what a send/recv convertor pair leaves in a zeroed destination: the type map's bytes"""
+    one = np.concatenate([np.arange(d, d + n) for d, n, _ in t.runs()])
+    idx = (origin + np.arange(count, dtype=np.int64)[:, None] * t.extent + one[None, :]).reshape(-1)
+    want = np.zeros_like(src)
+    want[idx] = src[idx]
+    return want

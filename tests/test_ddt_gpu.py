@@ -178,3 +178,81 @@ def test_config5_vector_1gib(gpu, pkg):
     assert torch.equal(y[:, :64], x[:, :64]) and int(torch.count_nonzero(y[:, 64:])) == 0
     del x, y, packed
     torch.cuda.empty_cache()
+
+
+# ---- opal_datatype_test.c's convertor dances replayed on the GPU convertor, each type compiled
+#      from the description records the reference would hold (oracle/opal_types.py) through
+#      mi355x_ddt_from_opal -- the call coll/mi355x makes for a derived MPI datatype
+from ddtcases import CONVERTOR_CASES, c_oracle, expected_copy, fill_pattern, ot, span_of, windows  # noqa: E402
+
+
+def _gpu_convertor_copy(torch, pkg, oracle, t, count, chunk, recv=None):
+    recv = recv or t
+    sizes = ot.basic_sizes()
+    ds = pkg.Ddt.from_opal(t.desc_bytes(), len(t.desc), t.extent, sizes)
+    dr = pkg.Ddt.from_opal(recv.desc_bytes(), len(recv.desc), recv.extent, sizes)
+    ods = c_oracle(oracle, t)
+    n, origin = span_of(t, count)
+    nr, origin_r = span_of(recv, count)
+    src = fill_pattern(n)
+    dsrc = torch.from_numpy(src).cuda()
+    ddst = torch.zeros(nr, dtype=torch.uint8, device="cuda")
+    total = count * t.size
+    packed = torch.zeros(total + 16, dtype=torch.uint8, device="cuda")
+    for pos, size in windows(oracle, ods, count, chunk):
+        tmp = packed[pos:]  # each window lands at its stream offset so the whole stream can be checked
+        ds.pack(count, dsrc.data_ptr() + origin, pos, tmp.data_ptr(), size)
+        dr.unpack(count, ddst.data_ptr() + origin_r, pos, tmp.data_ptr(), size)
+    want_stream = np.zeros(total, dtype=np.uint8)
+    oracle.oracle_ddt_pack(ods, count, src.ctypes.data + origin, 0, want_stream.ctypes.data, total)
+    oracle.oracle_ddt_free(ods)
+    ds.destroy()
+    dr.destroy()
+    return src, ddst.cpu().numpy(), origin, packed[:total].cpu().numpy(), want_stream
+
+
+@pytest.mark.parametrize("case", [c[0] for c in CONVERTOR_CASES])
+def test_convertor_cases_gpu(gpu, pkg, oracle, case):
+    """local_copy_with_convertor(pdt, count, chunk) for every case of opal_datatype_test.c main()
+    (upper_matrix(100) in 48-byte chunks, vector(450, 10, 11) in 12/82/6000/36000, blacs in
+    956/16K/64K, ...): the packed stream equals the oracle's, the destination holds exactly the
+    type map's bytes"""
+    torch = gpu
+    name, build, count, chunks = next(c for c in CONVERTOR_CASES if c[0] == case)
+    t = build()
+    for chunk in chunks:
+        src, dst, origin, stream, want_stream = _gpu_convertor_copy(torch, pkg, oracle, t, count, chunk)
+        assert np.array_equal(stream, want_stream), (case, chunk, "packed stream")
+        assert np.array_equal(dst, expected_copy(t, count, src, origin)), (case, chunk, "unpacked")
+
+
+def test_convertor_two_datatypes_blacs_gpu(gpu, pkg, oracle):
+    """local_copy_with_convertor_2datatypes(blacs1, 1, blacs2, 1, 100) (opal_datatype_test.c:533-538)"""
+    src, dst, _, _, _ = _gpu_convertor_copy(gpu, pkg, oracle, ot.blacs1(), 1, 100, recv=ot.blacs2())
+    assert np.array_equal(dst[:52].view(np.int32)[0::2], src[:76].view(np.int32)[0::3])
+    assert not dst[:52].view(np.int32)[1::2].any()
+
+
+def test_upper_500_gpu(gpu, pkg):
+    """test_upper(500) (opal_datatype_test.c:46-115) on device memory: the packed upper triangle
+    unpacked in (length + 1) * 8-byte chunks into a zeroed matrix, then check_diag_matrix"""
+    torch = gpu
+    n = 500
+    t = ot.upper_matrix(n)
+    d = pkg.Ddt.from_opal(t.desc_bytes(), len(t.desc), t.extent, ot.basic_sizes())
+    mat1 = torch.zeros(n, n, dtype=torch.float64)
+    iu = torch.triu_indices(n, n)
+    mat1[iu[0], iu[1]] = torch.from_numpy(np.random.default_rng(5).integers(0, 2**31, iu.shape[1]).astype(np.float64))
+    inbuf = mat1[iu[0], iu[1]].contiguous().cuda()
+    mat2 = torch.zeros(n, n, dtype=torch.float64, device="cuda")
+    chunk, pos, nbytes = (n + 1) * 8, 0, inbuf.numel() * 8
+    while pos < nbytes:
+        size = min(chunk, nbytes - pos)
+        d.unpack(1, mat2.data_ptr(), pos, inbuf.data_ptr() + pos, size)
+        pos += size
+    assert torch.equal(mat2.cpu(), mat1), "check_diag_matrix"
+    # and the other direction: pack the matrix back into the triangle stream
+    out = torch.zeros_like(inbuf)
+    d.pack(1, mat2.data_ptr(), 0, out.data_ptr(), nbytes)
+    assert torch.equal(out, inbuf)
+    d.destroy()

@@ -107,3 +107,136 @@ def test_constructor_rules(oracle):
     dp = (ctypes.c_int * 3)(0, 2, 10)                       # first two blocks are adjacent -> merged
     ix = oracle.oracle_ddt_indexed(3, bl, dp, 8)
     assert oracle.oracle_ddt_size(ix) == 48 and oracle.oracle_ddt_extent(ix) == 88
+
+
+# ---- test/datatype/opal_datatype_test.c:366-383 and opal_ddt_lib.c:478-850, restated through
+#      oracle/opal_types.py (opal_datatype_add's bounds rules + the test library's constructors)
+from ddtcases import CONVERTOR_CASES, c_oracle, expected_copy, fill_pattern, ot, span_of  # noqa: E402
+
+import pytest  # noqa: E402
+
+
+def _bounds(t):
+    return t.lb, t.ub, t.extent, t.size
+
+
+def test_mpich_typeub():
+    """mpich_typeub (opal_ddt_lib.c:619-679): a UB marker sets the extent, and a smaller UB marker
+    added later does not shrink it (MPIF semantics: 16, not 4)"""
+    t1, t2, t3 = ot.typeub()
+    assert t1.extent == 5 * 4 and t2.extent == 16 and t3.extent == 16
+
+
+def test_mpich_typeub2():
+    """Example 3.26 of MPI-1 (opal_ddt_lib.c:681-758): {LB -3, int 0, UB 6}, its contiguous(2) and
+    the same as a struct of two instances"""
+    dt1, dt2, dt3 = ot.typeub2()
+    assert (dt1.lb, dt1.ub, dt1.extent) == (-3, 6, 9)
+    assert (dt2.lb, dt2.ub, dt2.extent) == (-3, 15, 18)
+    assert (dt3.lb, dt3.ub, dt3.extent) == (-3, 15, 18)
+    assert dt1.size == 4 and dt2.size == dt3.size == 8
+
+
+def test_mpich_typeub3():
+    """hindexed / indexed / hvector / vector of the explicit-bounds type (opal_ddt_lib.c:760-850)"""
+    hi, ix, hv, ve = ot.typeub3()
+    assert (hi.lb, hi.ub, hi.extent) == (-7, 13, 20)
+    assert (ix.lb, ix.ub, ix.extent) == (-39, 69, 108)
+    assert (hv.lb, hv.ub, hv.extent) == (-3, 20, 23)
+    assert (ve.lb, ve.ub, ve.extent) == (-3, 132, 135)
+
+
+def test_constructed_bounds():
+    """upper_matrix(100): 5050 doubles over a 100x100 extent; test_struct / test_contiguous
+    (alignment epsilon), the resized strange type, matrix borders"""
+    u = ot.upper_matrix(100)
+    assert _bounds(u) == (0, 80000, 80000, 5050 * 8) and (u.true_lb, u.true_ub) == (0, 80000)
+    s = ot.test_struct()
+    assert _bounds(s) == (0, 32, 32, 20) and (s.true_lb, s.true_ub) == (0, 29)
+    c = ot.contiguous_alignment()  # {double, char} -> extent 16 by alignment, x4 x2
+    assert _bounds(c) == (0, 128, 128, 72)
+    st = ot.strange_dt()  # {double, char} resized to 12, x10
+    assert _bounds(st) == (0, 120, 120, 90)
+    assert ot.struct_char_double().extent == 16 and ot.twice_two_doubles().extent == 7 * 8
+
+
+@pytest.mark.parametrize("case", [c[0] for c in CONVERTOR_CASES])
+def test_desc_walk_is_the_type_map(case):
+    """the description records opal_datatype_add writes, walked the way the convertor walks them,
+    visit exactly the type map (for every convertor case type)"""
+    t = dict((c[0], c[1]) for c in CONVERTOR_CASES)[case]()
+    assert ot.walk_desc(t, 2) == [(d + k * t.extent, s) for k in range(2) for d, s in t.tmap]
+
+
+def _convertor_copy(oracle, t, count, chunk, recv=None):
+    """local_copy_with_convertor(_2datatypes) (opal_datatype_test.c:163-329) on the oracle: pack
+    `chunk`-byte windows (ending on element boundaries, as the convertor stops) and unpack each"""
+    from ddtcases import windows
+    recv = recv or t
+    ods, odr = c_oracle(oracle, t), c_oracle(oracle, recv)
+    n, origin = span_of(t, count)
+    nr, origin_r = span_of(recv, count)
+    src = fill_pattern(n)
+    dst = np.zeros(nr, dtype=np.uint8)
+    tmp = np.zeros(chunk + 16, dtype=np.uint8)
+    total = 0
+    for pos, size in windows(oracle, ods, count, chunk):
+        assert oracle.oracle_ddt_pack(ods, count, src.ctypes.data + origin, pos, tmp.ctypes.data, size) == 0
+        assert oracle.oracle_ddt_unpack(odr, count, dst.ctypes.data + origin_r, pos, tmp.ctypes.data, size) == 0
+        total += size
+    oracle.oracle_ddt_free(ods)
+    oracle.oracle_ddt_free(odr)
+    return src, dst, origin, total
+
+
+@pytest.mark.parametrize("case", [c[0] for c in CONVERTOR_CASES])
+def test_convertor_copy_cases(oracle, case):
+    name, build, count, chunks = next(c for c in CONVERTOR_CASES if c[0] == case)
+    t = build()
+    for chunk in chunks[:2]:
+        src, dst, origin, total = _convertor_copy(oracle, t, count, chunk)
+        assert total == count * t.size
+        assert np.array_equal(dst, expected_copy(t, count, src, origin)), (case, chunk)
+
+
+def test_convertor_two_datatypes_blacs(oracle):
+    """local_copy_with_convertor_2datatypes(blacs1, 1, blacs2, 1, 100) (opal_datatype_test.c:533-538):
+    vector(7, 1, 3, int) packed, unpacked as vector(7, 1, 2, int)"""
+    t1, t2 = ot.blacs1(), ot.blacs2()
+    src, dst, _, total = _convertor_copy(oracle, t1, 1, 100, recv=t2)
+    assert total == 28
+    assert np.array_equal(dst[:52].view(np.int32)[0::2], src[:76].view(np.int32)[0::3])
+
+
+def test_upper_500(oracle):
+    """test_upper(500) (opal_datatype_test.c:46-115): the packed upper triangle unpacked through a
+    recv convertor in (length + 1) * 8-byte chunks, then check_diag_matrix"""
+    n = 500
+    t = ot.upper_matrix(n)
+    od = c_oracle(oracle, t)
+    mat1 = np.zeros((n, n))
+    iu = np.triu_indices(n)
+    mat1[iu] = np.random.default_rng(5).integers(0, 2**31, len(iu[0])).astype(np.float64)
+    inbuf = np.ascontiguousarray(mat1[iu])  # row by row from the diagonal, as the test fills it
+    assert inbuf.nbytes == n * (n + 1) * 4
+    mat2 = np.zeros((n, n))
+    chunk, pos = (n + 1) * 8, 0
+    while pos < inbuf.nbytes:
+        size = min(chunk, inbuf.nbytes - pos)
+        assert oracle.oracle_ddt_unpack(od, 1, mat2.ctypes.data, pos, inbuf.ctypes.data + pos, size) == 0
+        assert mat2[0, 0] == inbuf[0]
+        pos += size
+    assert np.array_equal(mat2[iu], mat1[iu]) and not mat2[np.tril_indices(n, -1)].any()
+    oracle.oracle_ddt_free(od)
+
+
+def test_from_opal_matches_restated_types(pkg):
+    """the GPU convertor compiles each restated type's description records (the records the
+    coll/mi355x component hands to mi355x_ddt_from_opal) to the same size and extent"""
+    sizes = ot.basic_sizes()
+    types = [c[1]() for c in CONVERTOR_CASES] + list(ot.typeub2()) + [ot.blacs1(), ot.blacs2()]
+    for t in types:
+        d = pkg.Ddt.from_opal(t.desc_bytes(), len(t.desc), t.extent, sizes)
+        assert (d.size, d.extent) == (t.size, t.extent)
+        assert d.nruns <= len(t.runs())
+        d.destroy()
