@@ -115,9 +115,11 @@ int mca_coll_mi355x_pml_iprobe(int src, int tag, struct ompi_communicator_t *com
                                ompi_status_public_t *status);
 int mca_coll_mi355x_pml_probe(int src, int tag, struct ompi_communicator_t *comm, ompi_status_public_t *status);
 
-/* MCA parameters (environment: OMPI_MCA_coll_mi355x_<name>) */
+/* MCA parameters coll_mi355x_<name>: registered with mca_base_component_var_register when the
+ * component is loaded by an Open MPI that provides it, else read from OMPI_MCA_coll_mi355x_<name> */
 extern int mca_coll_mi355x_priority;            /* 90 */
 extern int mca_coll_mi355x_allreduce_algorithm; /* 0 = tuned decision, else coll_tuned numbering */
+extern int mca_coll_mi355x_pml_hook;            /* 1 = device point-to-point through the engine */
 
 #ifdef __cplusplus
 }

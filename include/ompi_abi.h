@@ -126,6 +126,44 @@ typedef struct mca_base_component_data_2_0_0_t {
 
 #define MCA_BASE_VERSION_2_0_0 2, 0, 0   /* opal/mca/mca.h:312 */
 
+/* ------------------------------------------------------------------ MCA variables */
+/* opal/mca/base/mca_base_var.h:74-160, :401-406.  Declared weak: a component built into an Open
+ * MPI tree binds libopen-pal's definition (parameters then appear in ompi_info and are read from
+ * openmpi-mca-params.conf / the command line / the environment); loaded anywhere without it the
+ * address is NULL and the component reads OMPI_MCA_<framework>_<component>_<name> itself. */
+typedef enum {
+    MCA_BASE_VAR_TYPE_INT,
+    MCA_BASE_VAR_TYPE_UNSIGNED_INT,
+    MCA_BASE_VAR_TYPE_UNSIGNED_LONG,
+    MCA_BASE_VAR_TYPE_UNSIGNED_LONG_LONG,
+    MCA_BASE_VAR_TYPE_SIZE_T,
+    MCA_BASE_VAR_TYPE_STRING,
+    MCA_BASE_VAR_TYPE_BOOL,
+    MCA_BASE_VAR_TYPE_DOUBLE,
+    MCA_BASE_VAR_TYPE_MAX
+} mca_base_var_type_t;
+typedef enum {
+    MCA_BASE_VAR_SCOPE_CONSTANT,
+    MCA_BASE_VAR_SCOPE_READONLY,
+    MCA_BASE_VAR_SCOPE_LOCAL,
+    MCA_BASE_VAR_SCOPE_GROUP,
+    MCA_BASE_VAR_SCOPE_GROUP_EQ,
+    MCA_BASE_VAR_SCOPE_ALL,
+    MCA_BASE_VAR_SCOPE_ALL_EQ,
+    MCA_BASE_VAR_SCOPE_MAX
+} mca_base_var_scope_t;
+typedef enum {
+    OPAL_INFO_LVL_1, OPAL_INFO_LVL_2, OPAL_INFO_LVL_3, OPAL_INFO_LVL_4, OPAL_INFO_LVL_5,
+    OPAL_INFO_LVL_6, OPAL_INFO_LVL_7, OPAL_INFO_LVL_8, OPAL_INFO_LVL_9, OPAL_INFO_LVL_MAX
+} mca_base_var_info_lvl_t;
+typedef int mca_base_var_flag_t;                       /* enum of flag bits, :165-180 */
+typedef struct mca_base_var_enum_t mca_base_var_enum_t;  /* opaque here */
+extern int mca_base_component_var_register(const mca_base_component_t *component, const char *variable_name,
+                                           const char *description, mca_base_var_type_t type,
+                                           mca_base_var_enum_t *enumerator, int bind, mca_base_var_flag_t flags,
+                                           mca_base_var_info_lvl_t info_lvl, mca_base_var_scope_t scope,
+                                           void *storage) __attribute__((weak));
+
 /* ------------------------------------------------------------------ datatypes */
 /* opal/datatype/opal_datatype.h:103-131, opal_datatype_internal.h:148-188 */
 typedef struct dt_elem_desc dt_elem_desc_t;

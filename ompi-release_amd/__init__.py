@@ -19,7 +19,9 @@ import os
 import pathlib
 
 PKG_DIR = pathlib.Path(__file__).resolve().parent
-LIB_DIR = PKG_DIR / "lib"
+# MI355X_LIB_DIR selects another build of the same libraries (the host-sanitizer build in
+# lib_san, csrc/Makefile.san, loaded by tools/san_boundary.sh)
+LIB_DIR = pathlib.Path(os.environ["MI355X_LIB_DIR"]) if os.environ.get("MI355X_LIB_DIR") else PKG_DIR / "lib"
 REPO_DIR = PKG_DIR.parent
 
 # ---------------------------------------------------------------- reference enums (op.h)

@@ -880,3 +880,45 @@ size_t mini_offsetof(int which)
     default: return (size_t)-1;
     }
 }
+
+/* ------------------------------------------------------------------ MCA variable system
+ * mca_base_component_var_register (opal/mca/base/mca_base_var.c): full name
+ * <framework>_<component>_<name>, value from OMPI_MCA_<full name> in the environment (the
+ * highest-priority source the harness has), else the storage's current value as the default. */
+#define MINI_MAX_VARS 64
+static struct { char name[160]; char desc[160]; int type; int lvl; void *storage; } mini_vars[MINI_MAX_VARS];
+static int mini_nvars;
+
+int mca_base_component_var_register(const mca_base_component_t *component, const char *variable_name,
+                                    const char *description, mca_base_var_type_t type,
+                                    mca_base_var_enum_t *enumerator, int bind, mca_base_var_flag_t flags,
+                                    mca_base_var_info_lvl_t info_lvl, mca_base_var_scope_t scope, void *storage)
+{
+    (void)enumerator; (void)bind; (void)flags; (void)scope;
+    if (!component || !variable_name || !storage || type != MCA_BASE_VAR_TYPE_INT) return -1;
+    char full[160], env[200];
+    snprintf(full, sizeof(full), "%s_%s_%s", component->mca_type_name, component->mca_component_name, variable_name);
+    int idx = -1;
+    for (int i = 0; i < mini_nvars; ++i)
+        if (!strcmp(mini_vars[i].name, full)) idx = i;
+    if (idx < 0) {
+        if (mini_nvars == MINI_MAX_VARS) return -1;
+        idx = mini_nvars++;
+    }
+    snprintf(mini_vars[idx].name, sizeof(mini_vars[idx].name), "%s", full);
+    snprintf(mini_vars[idx].desc, sizeof(mini_vars[idx].desc), "%s", description ? description : "");
+    mini_vars[idx].type = type;
+    mini_vars[idx].lvl = info_lvl;
+    mini_vars[idx].storage = storage;
+    snprintf(env, sizeof(env), "OMPI_MCA_%s", full);
+    const char *v = getenv(env);
+    if (v) *(int *)storage = atoi(v);
+    return idx;
+}
+int mini_var_count(void) { return mini_nvars; }
+const char *mini_var_name(int i) { return (i >= 0 && i < mini_nvars) ? mini_vars[i].name : NULL; }
+int mini_var_int(int i) { return (i >= 0 && i < mini_nvars) ? *(int *)mini_vars[i].storage : -1; }
+int mini_component_register(const mca_base_component_t *c)
+{
+    return c->mca_register_component_params ? c->mca_register_component_params() : OMPI_SUCCESS;
+}

@@ -42,6 +42,10 @@ int mini_stub_calls(int which);
 int mini_stub_marker(void);
 size_t mini_offsetof(int which);
 /* the PML slot: a counting stub as the selected PML, and the bindings' MCA_PML_CALL paths */
+int mini_var_count(void);
+const char *mini_var_name(int i);
+int mini_var_int(int i);
+int mini_component_register(const mca_base_component_t *c);
 int mini_coll_init(mca_coll_base_component_t *comp);
 int mini_coll_close(mca_coll_base_component_t *comp);
 void mini_pml_install_stub(void);

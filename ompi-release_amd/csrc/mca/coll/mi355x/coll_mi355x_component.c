@@ -17,6 +17,7 @@
 
 int mca_coll_mi355x_priority = 90;
 int mca_coll_mi355x_allreduce_algorithm = 0;
+int mca_coll_mi355x_pml_hook = 1;
 
 typedef struct mca_coll_mi355x_module_t {
     mca_coll_base_module_t super;
@@ -947,7 +948,7 @@ int mca_coll_mi355x_pml_probe(int src, int tag, struct ompi_communicator_t *comm
 /* install / remove the hook (idempotent) */
 static void pml_hook_install(void)
 {
-    if (pml_hooked || env_int("OMPI_MCA_coll_mi355x_pml_hook", 1) == 0) return;
+    if (pml_hooked || mca_coll_mi355x_pml_hook == 0) return;
     if (!mca_pml.pml_isend || !mca_pml.pml_irecv || !mca_pml.pml_send || !mca_pml.pml_recv) return;  /* no PML */
     host_pml = mca_pml;
     mca_pml.pml_isend = mca_coll_mi355x_pml_isend;
@@ -1072,11 +1073,30 @@ static int module_enable(mca_coll_base_module_t *module, struct ompi_communicato
     return OMPI_SUCCESS;
 }
 
+/* an int parameter: through the MCA variable system when libopen-pal provides it (in-tree build,
+ * coll_cuda_component.c:77-90), else OMPI_MCA_coll_mi355x_<name> from the environment */
+static void register_int(const char *name, const char *desc, mca_base_var_info_lvl_t lvl, int *storage)
+{
+    if (mca_base_component_var_register) {
+        (void)mca_base_component_var_register(&mca_coll_mi355x_component.collm_version, name, desc,
+                                              MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, lvl, MCA_BASE_VAR_SCOPE_READONLY,
+                                              storage);
+        return;
+    }
+    char env[96];
+    snprintf(env, sizeof(env), "OMPI_MCA_coll_mi355x_%s", name);
+    *storage = env_int(env, *storage);
+}
+
 static int component_register(void)
 {
-    mca_coll_mi355x_priority = env_int("OMPI_MCA_coll_mi355x_priority", mca_coll_mi355x_priority);
-    mca_coll_mi355x_allreduce_algorithm =
-        env_int("OMPI_MCA_coll_mi355x_allreduce_algorithm", mca_coll_mi355x_allreduce_algorithm);
+    register_int("priority", "Priority of the mi355x coll component (device-buffer collectives over xGMI)",
+                 OPAL_INFO_LVL_6, &mca_coll_mi355x_priority);
+    register_int("allreduce_algorithm",
+                 "Allreduce algorithm forced on the engine, in coll_tuned's numbering "
+                 "(coll_tuned_allreduce.c:38-47); 0 = coll_tuned's fixed decision", OPAL_INFO_LVL_5, &mca_coll_mi355x_allreduce_algorithm);
+    register_int("pml_hook", "Route device-buffer point-to-point on engine communicators through the engine",
+                 OPAL_INFO_LVL_5, &mca_coll_mi355x_pml_hook);
     return OMPI_SUCCESS;
 }
 static int component_open(void) { return OMPI_SUCCESS; }

@@ -118,8 +118,13 @@ void mca_op_hip_2buff(void *in, void *inout, int *count, struct ompi_datatype_t 
         staged_host2(m, t, in, inout, count, dtype, din, dio);
         return;
     }
+    if (din && dio) {  /* all-device: no shared state, concurrent callers do not serialise */
+        if (mi355x_op_reduce(m->op, t, in, inout, (size_t)*count, NULL) || mi355x_stream_sync(NULL))
+            die("mi355x_op_reduce");
+        return;
+    }
     const size_t bytes = (size_t)*count * mi355x_type_size(t);
-    pthread_mutex_lock(&m->lock);
+    pthread_mutex_lock(&m->lock);  /* guards the staging buffer */
     const void *src = in;
     void *dst = inout;
     if (!din) {                                           /* stage the host operand */
@@ -155,7 +160,12 @@ void mca_op_hip_3buff(void *in1, void *in2, void *out, int *count, struct ompi_d
         free(h1); free(h2); free(ho);
         return;
     }
-    pthread_mutex_lock(&m->lock);
+    if (d1 && d2 && dout) {  /* all-device: lock-free */
+        if (mi355x_op_reduce_3buff(m->op, t, in1, in2, out, (size_t)*count, NULL) || mi355x_stream_sync(NULL))
+            die("mi355x_op_reduce_3buff");
+        return;
+    }
+    pthread_mutex_lock(&m->lock);  /* guards the staging buffer */
     /* stage host operands into one scratch of up to three slices */
     char *s = NULL;
     const void *a = in1, *b = in2;
@@ -197,8 +207,17 @@ static int module_enable(struct ompi_op_base_module_1_0_0_t *module, struct ompi
     return OMPI_SUCCESS;
 }
 
+/* op_hip_priority: through the MCA variable system when libopen-pal provides it (in-tree build;
+ * the same call coll_cuda_component.c:77-82 makes), else OMPI_MCA_op_hip_priority */
 static int component_register(void)
 {
+    if (mca_base_component_var_register) {
+        (void)mca_base_component_var_register(&mca_op_hip_component.opc_version, "priority",
+                                              "Priority of the hip op component (MI355X reduction kernels)",
+                                              MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                              MCA_BASE_VAR_SCOPE_READONLY, &mca_op_hip_priority);
+        return OMPI_SUCCESS;
+    }
     const char *v = getenv("OMPI_MCA_op_hip_priority");
     if (v) mca_op_hip_priority = atoi(v);
     return OMPI_SUCCESS;

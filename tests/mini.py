@@ -44,6 +44,10 @@ class Mini:
         L.mini_comm_set_channel.argtypes = [vp, ctypes.c_char_p]
         L.mini_coll_select.argtypes = [vp, vp]
         L.mini_coll_init.argtypes = [vp]
+        L.mini_var_name.restype = ctypes.c_char_p
+        L.mini_var_name.argtypes = [i]
+        L.mini_var_int.argtypes = [i]
+        L.mini_component_register.argtypes = [vp]
         L.mini_coll_close.argtypes = [vp]
         L.mini_pml_fn.restype = vp
         L.mini_pml_fn.argtypes = [i]

@@ -248,3 +248,31 @@ def test_pml_hook_install_and_close():
         assert now == [m.addr(m.coll, f"mca_coll_mi355x_pml_{n}") for n in names]
     assert L.mini_coll_close(comp) == 0
     assert [L.mini_pml_fn(w) for w in range(6)] == saved
+
+
+def test_mca_variables_registered(monkeypatch):
+    """coll_mi355x_priority / _allreduce_algorithm / _pml_hook and op_hip_priority go through
+    mca_base_component_var_register when the process provides it (here: the harness's variable
+    system standing in for libopen-pal, which reads OMPI_MCA_<name>); the stored value is what
+    comm_query / op_query then use"""
+    m = mini()
+    L = m.lib
+    coll = m.component_ptr(m.coll, "mca_coll_mi355x_component")
+    oph = m.component_ptr(m.op_hip, "mca_op_hip_component")
+    prio = ctypes.c_int.in_dll(m.coll, "mca_coll_mi355x_priority")
+    oprio = ctypes.c_int.in_dll(m.op_hip, "mca_op_hip_priority")
+    saved = prio.value, oprio.value
+    try:
+        monkeypatch.setenv("OMPI_MCA_coll_mi355x_priority", "77")
+        monkeypatch.setenv("OMPI_MCA_op_hip_priority", "33")
+        assert L.mini_component_register(coll) == 0 and L.mini_component_register(oph) == 0
+        names = {L.mini_var_name(i).decode(): L.mini_var_int(i) for i in range(L.mini_var_count())}
+        assert names["coll_mi355x_priority"] == 77 and prio.value == 77
+        assert names["op_hip_priority"] == 33 and oprio.value == 33
+        assert "coll_mi355x_allreduce_algorithm" in names and names["coll_mi355x_pml_hook"] == 1
+        _coll_env(monkeypatch)
+        comm = L.mini_comm_create(0, 4, 17)
+        mod, p = _comm_query(m, comm)
+        assert mod and p == 77
+    finally:
+        prio.value, oprio.value = saved
