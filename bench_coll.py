@@ -358,6 +358,9 @@ def run(args, pkg, torch):
                    "best": best, "autotune_ms_per_call": tried},
         "roofline": ({"bound": "xgmi", "achieved": round(fold_xgmi, 2), "peak": round(peak_all, 1), "unit": "GB/s",
                       "frac": round(fold_xgmi / peak_all, 4), "traffic": pmc_traffic(pipe, shared=False),
+                      "traffic_note": "HBM bytes per launch from a committed rocprofv3 PMC summary of this "
+                                      "kernel on separate GPUs, or null: only the one-GPU rehearsal's "
+                                      "(profiles/r02_pmc_rehearsal.json) exists so far",
                       "kernel": kname, "kernel_avg_ms": round(p1, 4),
                       "alg_bytes_per_launch": int(xgmi_bytes), "phase2_ms": round(p2, 4),
                       "busbw_frac": round(busbw / peak_all, 4),

@@ -74,6 +74,49 @@ def test_op_hip_device_dispatch(gpu, pkg, oracle):
     assert not bad, "\n".join(bad[:10])
 
 
+def test_op_hip_concurrent_callers(gpu, pkg, oracle):
+    """MPI_THREAD_MULTIPLE: several threads reduce through the same MPI_Op's table at once, all-
+    device operands (the lock-free path) mixed with staged host operands (the locked path); every
+    result must match the oracle"""
+    import threading
+    torch = gpu
+    m = mini()
+    m.install_oracle_base(oracle)
+    code, slot = pkg.OP["SUM"], pkg.T["INT32"]
+    op = m.select_op(code)
+    dt = m.dtype_for_slot(slot)
+    n, iters, nthreads = 300_001, 25, 6
+    errors = []
+
+    def worker(k):
+        try:
+            a = np.arange(n, dtype=np.int32) * (k + 1)
+            da = torch.from_numpy(a).cuda()
+            for it in range(iters):
+                b = np.full(n, it - k, dtype=np.int32)
+                want = b + a
+                if k % 3 == 2:  # host inout: staged through the module's scratch under its lock
+                    m.lib.mini_op_reduce(op, da.data_ptr(), b.ctypes.data, n, dt)
+                    got = b
+                else:
+                    db = torch.from_numpy(b).cuda()
+                    torch.cuda.synchronize()
+                    m.lib.mini_op_reduce(op, da.data_ptr(), db.data_ptr(), n, dt)
+                    got = db.cpu().numpy()
+                if not np.array_equal(got, want):
+                    errors.append((k, it))
+        except Exception as e:  # noqa: BLE001
+            errors.append((k, repr(e)))
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(nthreads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    m.lib.mini_op_destroy(op)
+    assert not errors, errors[:5]
+
+
 @pytest.mark.parametrize("size", [2, 3])
 def test_coll_component_processes(gpu, size):
     key = uuid.uuid4().hex[:10]
