@@ -1141,10 +1141,14 @@ static int pipe_allreduce(mi355x_comm *c, int op, int type, const Program &pr,
     for (int q = 0; q < c->size; ++q)
         if ((((uintptr_t)a.peer_rbuf[q]) & 15) == m) a.co_pull |= 1ull << q;
     // persistent grid: pipe_wg_per_cu workgroups of 256 per CU, split among the ranks sharing
-    // this GPU
+    // this GPU.  Ranks that share a GPU must all be resident at once (rank A's pull items spin
+    // until rank B's fold items have run), so their grids together stay within what the CUs hold.
     const uint64_t total = (uint64_t)nchunks * n;
-    uint64_t grid =
-        (uint64_t)std::max(8, coll_tune().pipe_wg_per_cu * device_cu_count() / std::max(1, c->pipe_share));
+    const int share = std::max(1, c->pipe_share);
+    int wpc = coll_tune().pipe_wg_per_cu;
+    if (share > 1) wpc = std::min(wpc, pipe_blocks_per_cu(op, type, count));
+    uint64_t grid = (uint64_t)std::max(1, wpc * device_cu_count() / share);
+    if (share == 1) grid = std::max<uint64_t>(grid, 8);
     if (grid > total) grid = total;
     const bool tp = c->time_phases && c->tev[0];
     if (tp) MI_HIP(hipEventRecord(c->tev[0], s));

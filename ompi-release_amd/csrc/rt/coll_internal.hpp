@@ -111,6 +111,9 @@ struct PipeArgs {
     uint64_t *dbg;                     // NULL, or 4 words per workgroup: item, stage, flag seen, polls
 };
 int launch_pipe_slot(int op, int type, const PipeArgs &a, unsigned grid, hipStream_t s);
+// workgroups of the pipelined kernel for (op, type, count) one CU can hold at once: ranks sharing a
+// GPU must fit their persistent grids side by side (a rank's pulls spin until a peer's folds run)
+int pipe_blocks_per_cu(int op, int type, size_t count);
 
 struct CollTune {
     // grid cap of k_fold / k_copy / k_multicopy in blocks per CU; 1024 = one-shot grids (every

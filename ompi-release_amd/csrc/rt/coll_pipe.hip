@@ -64,30 +64,20 @@ template <class F> __device__ __forceinline__ typename F::T pfold_scalar(const P
     return acc;
 }
 
-// fold elements [lo, hi) (absolute) into dst
-template <class F, bool NT> __device__ void fold_range(const PipeArgs &a, size_t lo, size_t hi)
+// fold the vector body: U 16-B vectors per lane in flight per source, sources loaded FC at a time
+template <class F, bool NT, int U, int FC>
+__device__ __forceinline__ void fold_body(const PipeArgs &a, typename F::T *dst, size_t v0, size_t nvec)
 {
     using T = typename F::T;
     using V = PVec<T>;
     constexpr int EPV = 16 / sizeof(T);
-    constexpr int U = 2;
-    T *dst = reinterpret_cast<T *>(a.dst);
     const size_t t = threadIdx.x, nt = blockDim.x;
-    size_t head = hi - lo, nvec = 0;
-    if (a.co_fold) {
-        const uintptr_t mis = ((uintptr_t)(dst + lo)) & 15;
-        head = mis ? (16 - mis) / sizeof(T) : 0;
-        if (head > hi - lo) head = hi - lo;
-        nvec = (hi - lo - head) / EPV;
-    }
-    for (size_t i = lo + t; i < lo + head; i += nt) dst[i] = pfold_scalar<F>(a, i);
-    const size_t v0 = lo + head;  // first element of the vector body
     for (size_t base = t; base < nvec; base += nt * U) {
         V acc[U];
-        for (int j0 = 0; j0 < a.n; j0 += kFoldChunk) {
-            V x[kFoldChunk][U];
+        for (int j0 = 0; j0 < a.n; j0 += FC) {
+            V x[FC][U];
 #pragma unroll
-            for (int j = 0; j < kFoldChunk; ++j) {
+            for (int j = 0; j < FC; ++j) {
                 if (j0 + j < a.n) {
                     const T *p = static_cast<const T *>(a.src[a.order[j0 + j]]) + v0;
 #pragma unroll
@@ -105,7 +95,7 @@ template <class F, bool NT> __device__ void fold_range(const PipeArgs &a, size_t
                 for (int u = 0; u < U; ++u) acc[u] = x[0][u];
             }
 #pragma unroll
-            for (int j = 0; j < kFoldChunk; ++j) {
+            for (int j = 0; j < FC; ++j) {
                 if (j0 + j > 0 && j0 + j < a.n) {
                     const bool ao = (a.role_mask >> (j0 + j)) & 1u;
 #pragma unroll
@@ -125,6 +115,30 @@ template <class F, bool NT> __device__ void fold_range(const PipeArgs &a, size_t
             }
         }
     }
+}
+
+// fold elements [lo, hi) (absolute) into dst.  Few ranks: 4 vectors per lane per source (a
+// persistent grid of a few workgroups per CU needs that much in flight to stream HBM); many
+// ranks: 2 per source, 8 sources per load group (the n loads already fill the queue).
+template <class F, bool NT> __device__ void fold_range(const PipeArgs &a, size_t lo, size_t hi)
+{
+    using T = typename F::T;
+    constexpr int EPV = 16 / sizeof(T);
+    T *dst = reinterpret_cast<T *>(a.dst);
+    const size_t t = threadIdx.x, nt = blockDim.x;
+    size_t head = hi - lo, nvec = 0;
+    if (a.co_fold) {
+        const uintptr_t mis = ((uintptr_t)(dst + lo)) & 15;
+        head = mis ? (16 - mis) / sizeof(T) : 0;
+        if (head > hi - lo) head = hi - lo;
+        nvec = (hi - lo - head) / EPV;
+    }
+    for (size_t i = lo + t; i < lo + head; i += nt) dst[i] = pfold_scalar<F>(a, i);
+    const size_t v0 = lo + head;  // first element of the vector body
+    if (a.n <= 4)
+        fold_body<F, NT, 4, 4>(a, dst, v0, nvec);
+    else
+        fold_body<F, NT, 2, kFoldChunk>(a, dst, v0, nvec);
     for (size_t i = v0 + nvec * EPV + t; i < hi; i += nt) dst[i] = pfold_scalar<F>(a, i);
 }
 
@@ -141,7 +155,7 @@ template <bool NT> __device__ void copy_range(char *dst, const char *src, size_t
     }
     for (size_t i = lo + t; i < lo + head; i += nt) dst[i] = src[i];
     const size_t b0 = lo + head;
-    constexpr int U = 4;
+    constexpr int U = 8;
     for (size_t base = t; base < nvec; base += nt * U) {
         u32x4p x[U];
 #pragma unroll
@@ -243,10 +257,11 @@ template <class F, bool NT> __global__ __launch_bounds__(256) void k_pipe_allred
     }
 }
 
+static bool pipe_nt(size_t bytes) { return 2 * bytes > ((size_t)256 << 20); }
+
 template <class F> static int launch_pipe(const PipeArgs &a, unsigned grid, hipStream_t s)
 {
-    const size_t bytes = (size_t)a.count * sizeof(typename F::T);
-    if (2 * bytes > ((size_t)256 << 20))
+    if (pipe_nt((size_t)a.count * sizeof(typename F::T)))
         hipLaunchKernelGGL((k_pipe_allreduce<F, true>), dim3(grid), dim3(256), 0, s, a);
     else
         hipLaunchKernelGGL((k_pipe_allreduce<F, false>), dim3(grid), dim3(256), 0, s, a);
@@ -254,23 +269,48 @@ template <class F> static int launch_pipe(const PipeArgs &a, unsigned grid, hipS
     return MI355X_SUCCESS;
 }
 
+// workgroups of the kernel launch_pipe would pick that one CU holds at once
+template <class F> static int occupancy_pipe(size_t count)
+{
+    int nb = 0;
+    hipError_t e = pipe_nt(count * sizeof(typename F::T))
+                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pipe_allreduce<F, true>, 256, 0)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pipe_allreduce<F, false>, 256, 0);
+    return e == hipSuccess && nb > 0 ? nb : 1;
+}
+
 struct PipeTable {
     int (*f[MI355X_OP_MAX_][MI355X_T_MAX])(const PipeArgs &, unsigned, hipStream_t) = {};
+    int (*occ[MI355X_OP_MAX_][MI355X_T_MAX])(size_t) = {};
     PipeTable()
     {
         for_each_slot([&](auto tag, int op, int ty) {
             using F = typename decltype(tag)::type;
             f[op][ty] = &launch_pipe<F>;
+            occ[op][ty] = &occupancy_pipe<F>;
         });
     }
 };
 
-int launch_pipe_slot(int op, int type, const PipeArgs &a, unsigned grid, hipStream_t s)
+static const PipeTable &pipe_table()
 {
     static const PipeTable t;
+    return t;
+}
+
+int launch_pipe_slot(int op, int type, const PipeArgs &a, unsigned grid, hipStream_t s)
+{
+    const PipeTable &t = pipe_table();
     if (op < 0 || op >= MI355X_OP_MAX_ || type < 0 || type >= MI355X_T_MAX || !t.f[op][type])
         return set_error(MI355X_ERR_UNSUPPORTED, "no pipelined allreduce for op %d type %d", op, type);
     return t.f[op][type](a, grid, s);
+}
+
+int pipe_blocks_per_cu(int op, int type, size_t count)
+{
+    const PipeTable &t = pipe_table();
+    if (op < 0 || op >= MI355X_OP_MAX_ || type < 0 || type >= MI355X_T_MAX || !t.occ[op][type]) return 1;
+    return t.occ[op][type](count);
 }
 
 } // namespace mi355x
