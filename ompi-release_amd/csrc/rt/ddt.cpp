@@ -234,20 +234,14 @@ static int ddt_move(const mi355x_ddt_t *d, bool pack, size_t count, void *mem, s
     dv.extent = d->extent;
     dv.blk_bytes = blk_bytes(d);
     dv.inst_bytes = inst;
-    unsigned *dsum = nullptr;
-    if (checksum) MI_HIP(hipMallocAsync((void **)&dsum, sizeof(unsigned), s));
+    unsigned h = 0;
+    unsigned *sum = checksum ? &h : nullptr;  // the launchers wait for the kernel when asked for one
     int rc = 1;
     if (d->disp.size() == 1)
-        rc = launch_ddt_rows(dv, 1, d->disp[0], d->len[0], pack, mem, packed, (int64_t)pos, (int64_t)bytes, dsum, s);
-    if (rc == 1) rc = launch_ddt(dv, pack, mem, packed, (int64_t)pos, (int64_t)bytes, dsum, s);
+        rc = launch_ddt_rows(dv, 1, d->disp[0], d->len[0], pack, mem, packed, (int64_t)pos, (int64_t)bytes, sum, s);
+    if (rc == 1) rc = launch_ddt(dv, pack, mem, packed, (int64_t)pos, (int64_t)bytes, sum, s);
     if (rc) return rc;
-    if (checksum) {
-        unsigned h = 0;
-        MI_HIP(hipMemcpyAsync(&h, dsum, sizeof(unsigned), hipMemcpyDeviceToHost, s));
-        MI_HIP(hipFreeAsync(dsum, s));
-        MI_HIP(hipStreamSynchronize(s));
-        *checksum = h;
-    }
+    if (checksum) *checksum = h;
     return MI355X_SUCCESS;
 }
 

@@ -32,6 +32,7 @@ struct DdtTune {
 };
 DdtTune &ddt_tune();
 
+// csum: NULL, or where the window's checksum goes (the launch is then waited for)
 int launch_ddt(const DdtDev &d, bool pack, void *mem, void *packed, int64_t pos, int64_t bytes, unsigned *csum,
                hipStream_t s);
 // the row kernel (one run per block, 16-B aligned); returns 1 when it does not apply

@@ -17,6 +17,9 @@
 #include "ddt_internal.hpp"
 #include "rt_internal.hpp"
 
+#include <mutex>
+#include <vector>
+
 namespace mi355x {
 
 typedef unsigned int u32x4d __attribute__((ext_vector_type(4)));
@@ -46,39 +49,59 @@ __device__ __forceinline__ Where locate(const DdtDev &d, int64_t p)
     return w;
 }
 
-// checksum: every block stores its partial sum (waves reduced by shuffles, then through LDS);
-// k_csum_finish adds the partials -- no atomics on one hot word
-__device__ __forceinline__ void block_sum_store(unsigned acc, unsigned *partial)
+// checksum: every block stores its partial sum (waves reduced by shuffles, then through LDS) and
+// counts itself done; the last block to finish adds the partials and writes the result straight
+// into host-mapped memory -- no second launch, no device-to-host copy, no atomics on one hot word
+// for the data (one counter increment per block)
+struct CsumSink {
+    unsigned *partial;   // one word per block
+    unsigned *counter;   // blocks done; zero before the launch, reset to zero by the last block
+    unsigned *out;       // host-mapped result word
+    unsigned nblocks;
+};
+
+__device__ __forceinline__ unsigned block_reduce(unsigned acc)
 {
     __shared__ unsigned ws[16];
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+    __syncthreads();  // ws may still be read by a previous call
     if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = acc;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned t = 0;
+    unsigned t = 0;
+    if (threadIdx.x == 0)
         for (unsigned i = 0; i < (blockDim.x + 63) / 64; ++i) t += ws[i];
-        partial[blockIdx.x] = t;
-    }
+    return t;  // valid in thread 0
 }
 
-__global__ __launch_bounds__(1024) void k_csum_finish(const unsigned *partial, unsigned n, unsigned *out)
+__device__ __forceinline__ void block_sum_finish(unsigned acc, const CsumSink &k)
 {
-    unsigned acc = 0;
-    for (unsigned i = threadIdx.x; i < n; i += blockDim.x) acc += partial[i];
-    __shared__ unsigned ws[16];
-    for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = acc;
-    __syncthreads();
+    __shared__ unsigned last;
+    const unsigned t = block_reduce(acc);
     if (threadIdx.x == 0) {
-        unsigned t = 0;
-        for (unsigned i = 0; i < (blockDim.x + 63) / 64; ++i) t += ws[i];
-        *out = t;
+        // the partial is one word written through to memory (agent-scope store), drained before
+        // the count: no L2 write-back fence per block (a release here costs one XCD-wide L2
+        // write-back per block -- 16 K of them for a 1 GiB window)
+        __hip_atomic_store(k.partial + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev = __hip_atomic_fetch_add(k.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = (prev == k.nblocks - 1) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // once per launch; the loads below are agent-scope too
+    unsigned a = 0;
+    for (unsigned i = threadIdx.x; i < k.nblocks; i += blockDim.x)
+        a += __hip_atomic_load(k.partial + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned total = block_reduce(a);
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(k.out, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(k.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 template <bool PACK, bool CSUM>
 __global__ __launch_bounds__(256) void k_ddt(DdtDev d, char *mem, char *packed, int64_t pos, int64_t bytes,
-                                             unsigned *csum)
+                                             CsumSink csum)
 {
     const int64_t first = pos >> 4, last = (pos + bytes + 15) >> 4;   // 16-B slots touching the window
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -119,7 +142,7 @@ __global__ __launch_bounds__(256) void k_ddt(DdtDev d, char *mem, char *packed, 
             }
         }
     }
-    if constexpr (CSUM) block_sum_store(acc, csum);
+    if constexpr (CSUM) block_sum_finish(acc, csum);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -160,10 +183,8 @@ struct RowArgs {
 };
 
 template <bool PACK, bool CSUM, int NTM, int U>
-__global__ __launch_bounds__(1024) void k_ddt_rows(RowArgs a, unsigned *csum)
+__device__ __forceinline__ unsigned rows_pass(const RowArgs &a, uint32_t base, uint32_t tpb)
 {
-    const uint32_t tpb = blockDim.x;
-    const uint32_t base = blockIdx.x * (tpb * U) + threadIdx.x;
     u32x4d v[U];
     char *mp[U];
     unsigned acc = 0;
@@ -192,7 +213,24 @@ __global__ __launch_bounds__(1024) void k_ddt_rows(RowArgs a, unsigned *csum)
             if constexpr (CSUM) acc += v[u].x + v[u].y + v[u].z + v[u].w;
         }
     }
-    if constexpr (CSUM) block_sum_store(acc, csum);
+    return acc;
+}
+
+// without a checksum: one-shot grid, every lane one pass of U slots (measured fastest); with one:
+// a capped grid striding over the window, so that few blocks report a partial
+template <bool PACK, bool CSUM, int NTM, int U>
+__global__ __launch_bounds__(1024) void k_ddt_rows(RowArgs a, CsumSink csum)
+{
+    const uint32_t tpb = blockDim.x;
+    if constexpr (!CSUM) {
+        (void)rows_pass<PACK, false, NTM, U>(a, blockIdx.x * (tpb * U) + threadIdx.x, tpb);
+    } else {
+        unsigned acc = 0;
+        const uint64_t step = (uint64_t)gridDim.x * tpb * U;
+        for (uint64_t base = (uint64_t)blockIdx.x * (tpb * U) + threadIdx.x; base < a.nslots; base += step)
+            acc += rows_pass<PACK, true, NTM, U>(a, (uint32_t)base, tpb);
+        block_sum_finish(acc, csum);
+    }
 }
 
 // the row kernel applies: one run per block, every address and the window 16-B aligned, and
@@ -215,27 +253,84 @@ DdtTune &ddt_tune()
     return t;
 }
 
-// checksum partials: one word per block, summed by k_csum_finish into *csum
-struct Partials {
-    unsigned *p = nullptr;
-    int get(unsigned *csum, unsigned blocks, hipStream_t s)
+// checksum workspaces: partials + counter on the device, the result word in host-mapped memory;
+// pooled per device (a call holds one until its stream has finished with it)
+struct CsumWs {
+    int device = -1;
+    unsigned *partial = nullptr;
+    size_t cap = 0;
+    unsigned *counter = nullptr;
+    unsigned *host = nullptr, *host_dev = nullptr;
+};
+static std::mutex g_csum_mtx;
+static std::vector<CsumWs *> g_csum_free;
+
+struct Csum {
+    CsumWs *ws = nullptr;
+    CsumSink sink{};
+    // take a workspace with room for `blocks` partials (nothing when no checksum is wanted)
+    int get(unsigned *want, unsigned blocks)
     {
-        if (!csum) return MI355X_SUCCESS;
-        MI_HIP(hipMallocAsync((void **)&p, sizeof(unsigned) * blocks, s));
+        if (!want) return MI355X_SUCCESS;
+        int dev = 0;
+        MI_HIP(hipGetDevice(&dev));
+        {
+            std::lock_guard<std::mutex> g(g_csum_mtx);
+            for (size_t i = 0; i < g_csum_free.size(); ++i)
+                if (g_csum_free[i]->device == dev) {
+                    ws = g_csum_free[i];
+                    g_csum_free.erase(g_csum_free.begin() + (long)i);
+                    break;
+                }
+        }
+        if (!ws) {
+            ws = new CsumWs();
+            ws->device = dev;
+            MI_HIP(hipMalloc((void **)&ws->counter, sizeof(unsigned)));
+            MI_HIP(hipMemset(ws->counter, 0, sizeof(unsigned)));
+            MI_HIP(hipHostMalloc((void **)&ws->host, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
+            MI_HIP(hipHostGetDevicePointer((void **)&ws->host_dev, ws->host, 0));
+        }
+        if (ws->cap < blocks) {
+            if (ws->partial) MI_HIP(hipFree(ws->partial));
+            ws->partial = nullptr;
+            ws->cap = 0;
+            MI_HIP(hipMalloc((void **)&ws->partial, sizeof(unsigned) * blocks));
+            ws->cap = blocks;
+        }
+        sink.partial = ws->partial;
+        sink.counter = ws->counter;
+        sink.out = ws->host_dev;
+        sink.nblocks = blocks;
         return MI355X_SUCCESS;
     }
-    int finish(unsigned *csum, unsigned blocks, hipStream_t s)
+    // wait for the launch, hand the checksum over, return the workspace to the pool
+    int finish(unsigned *want, hipStream_t s)
     {
-        if (!csum) return MI355X_SUCCESS;
-        hipLaunchKernelGGL(k_csum_finish, dim3(1), dim3(1024), 0, s, p, blocks, csum);
-        MI_HIP(hipGetLastError());
-        MI_HIP(hipFreeAsync(p, s));
+        if (!want) return MI355X_SUCCESS;
+        MI_HIP(hipStreamSynchronize(s));
+        *want = __atomic_load_n(ws->host, __ATOMIC_ACQUIRE);
+        std::lock_guard<std::mutex> g(g_csum_mtx);
+        g_csum_free.push_back(ws);
+        ws = nullptr;
         return MI355X_SUCCESS;
+    }
+    ~Csum()
+    {
+        // a workspace still held here belongs to a failed launch: its counter may be stale, so it
+        // is dropped rather than pooled
+        if (ws) {
+            (void)hipFree(ws->partial);
+            (void)hipFree(ws->counter);
+            (void)hipHostFree(ws->host);
+            delete ws;
+        }
     }
 };
 
 template <bool PACK, bool CSUM, int NTM>
-static void launch_rows_u(const RowArgs &a, int unroll, unsigned tpb, unsigned blocks, unsigned *part, hipStream_t s)
+static void launch_rows_u(const RowArgs &a, int unroll, unsigned tpb, unsigned blocks, const CsumSink &part,
+                          hipStream_t s)
 {
     switch (unroll) {
     case 2: hipLaunchKernelGGL((k_ddt_rows<PACK, CSUM, NTM, 2>), dim3(blocks), dim3(tpb), 0, s, a, part); break;
@@ -245,7 +340,7 @@ static void launch_rows_u(const RowArgs &a, int unroll, unsigned tpb, unsigned b
 }
 
 template <bool PACK, bool CSUM>
-static void launch_rows(const RowArgs &a, int ntm, int unroll, unsigned tpb, unsigned blocks, unsigned *part,
+static void launch_rows(const RowArgs &a, int ntm, int unroll, unsigned tpb, unsigned blocks, const CsumSink &part,
                         hipStream_t s)
 {
     switch (ntm & 3) {
@@ -277,19 +372,23 @@ int launch_ddt_rows(const DdtDev &d, int nruns_host, int64_t run_disp, int64_t r
     int ntm = t.nontemporal;
     if (ntm < 0) ntm = (2 * bytes > ((int64_t)256 << 20)) ? kDdtAutoNT : 0;  // streaming sizes
     const uint64_t per = (uint64_t)tpb * (uint64_t)unroll;
-    const unsigned blocks = (unsigned)((a.nslots + per - 1) / per);
-    Partials part;
-    int rc = part.get(csum, blocks, s);
+    unsigned blocks = (unsigned)((a.nslots + per - 1) / per);
+    if (csum) {  // checksum: a capped, striding grid (one partial and one count per block)
+        const unsigned cap = (unsigned)(8 * device_cu_count() * (1024 / tpb));
+        if (blocks > cap) blocks = cap;
+    }
+    Csum part;
+    int rc = part.get(csum, blocks);
     if (rc) return rc;
     if (pack) {
-        if (csum) launch_rows<true, true>(a, ntm, unroll, tpb, blocks, part.p, s);
-        else launch_rows<true, false>(a, ntm, unroll, tpb, blocks, nullptr, s);
+        if (csum) launch_rows<true, true>(a, ntm, unroll, tpb, blocks, part.sink, s);
+        else launch_rows<true, false>(a, ntm, unroll, tpb, blocks, part.sink, s);
     } else {
-        if (csum) launch_rows<false, true>(a, ntm, unroll, tpb, blocks, part.p, s);
-        else launch_rows<false, false>(a, ntm, unroll, tpb, blocks, nullptr, s);
+        if (csum) launch_rows<false, true>(a, ntm, unroll, tpb, blocks, part.sink, s);
+        else launch_rows<false, false>(a, ntm, unroll, tpb, blocks, part.sink, s);
     }
     MI_HIP(hipGetLastError());
-    return part.finish(csum, blocks, s);
+    return part.finish(csum, s);
 }
 
 int launch_ddt(const DdtDev &d, bool pack, void *mem, void *packed, int64_t pos, int64_t bytes, unsigned *csum,
@@ -302,10 +401,10 @@ int launch_ddt(const DdtDev &d, bool pack, void *mem, void *packed, int64_t pos,
     if (blocks > cap) blocks = cap;
     if (blocks == 0) blocks = 1;
     char *m = static_cast<char *>(mem), *pk = static_cast<char *>(packed);
-    Partials part;
-    int rc = part.get(csum, (unsigned)blocks, s);
+    Csum part;
+    int rc = part.get(csum, (unsigned)blocks);
     if (rc) return rc;
-    unsigned *pp = part.p;
+    const CsumSink &pp = part.sink;
     if (pack) {
         if (csum) hipLaunchKernelGGL((k_ddt<true, true>), dim3((unsigned)blocks), dim3(256), 0, s, d, m, pk, pos, bytes, pp);
         else hipLaunchKernelGGL((k_ddt<true, false>), dim3((unsigned)blocks), dim3(256), 0, s, d, m, pk, pos, bytes, pp);
@@ -314,7 +413,7 @@ int launch_ddt(const DdtDev &d, bool pack, void *mem, void *packed, int64_t pos,
         else hipLaunchKernelGGL((k_ddt<false, false>), dim3((unsigned)blocks), dim3(256), 0, s, d, m, pk, pos, bytes, pp);
     }
     MI_HIP(hipGetLastError());
-    return part.finish(csum, (unsigned)blocks, s);
+    return part.finish(csum, s);
 }
 
 } // namespace mi355x
