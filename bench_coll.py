@@ -275,20 +275,47 @@ def run(args, pkg, torch):
             if k in cand:
                 comm.set(knob, cand[k])
 
+    # a candidate that fails (e.g. a flag never seen over this machine's links: the engine's
+    # bounded wait turns it into an error on every rank) is dropped with its flow, the
+    # communicator is rebuilt and the search goes on; every rank agrees on the outcome first
+    failed_flows = set()
+    comm.set("TIMEOUT_S", 30)
     for cand in cands:
+        if cand["pipe"] in failed_flows:
+            continue
         _log(rank, f"autotune {cand}")
-        apply(cand)
-        torch.cuda.synchronize()
-        comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
-        ok = ok and bool(torch.all(y == want).item())
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(3):
+        err = None
+        cand_ok = True
+        try:
+            apply(cand)
+            torch.cuda.synchronize()
             comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
-        dt = torch.tensor([(time.perf_counter() - t0) / 3])
-        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-        tried.append(dict(cand, ms=round(float(dt[0]) * 1e3, 4)))
-    best = min(tried, key=lambda c: c["ms"])
+            cand_ok = bool(torch.all(y == want).item())
+            t0 = time.perf_counter()
+            for _ in range(3):
+                comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
+            el = (time.perf_counter() - t0) / 3
+        except pkg.MI355XError as e:
+            err, el = repr(e)[:240], float("inf")
+        agree = torch.tensor([el, 1.0 if err else 0.0])
+        dist.all_reduce(agree, op=dist.ReduceOp.MAX)
+        if agree[1] > 0:
+            failed_flows.add(cand["pipe"])
+            tried.append(dict(cand, ms=None, error=err or "failed on another rank"))
+            torch.cuda.synchronize()
+            dist.barrier()
+            comm.destroy()
+            key = f"{key}_r"
+            comm = pkg.Comm.create(key, rank, world, local)
+            comm.set("TIMEOUT_S", 30)
+            continue
+        ok = ok and cand_ok
+        tried.append(dict(cand, ms=round(float(agree[0]) * 1e3, 4)))
+    comm.set("TIMEOUT_S", 120)
+    timed_ok = [c for c in tried if c["ms"] is not None]
+    if not timed_ok:
+        raise SystemExit("every allreduce candidate failed: " + json.dumps(tried))
+    best = min(timed_ok, key=lambda c: c["ms"])
     apply(best)
     # timed data: N(0,1), order-dependent (the engine replicates the segmented-ring order)
     _log(rank, f"timed: {args.steps} steps, best {best}")
