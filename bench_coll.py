@@ -264,7 +264,7 @@ def run(args, pkg, torch):
     want = world * (world + 1) / 2
     ok = True
     tried = []
-    cands = [{"pipe": 1, "pipe_wg_per_cu": wg, "pipe_chunk_kib": ck} for wg in (1, 2, 4, 8) for ck in (0, 2048, 8192)]
+    cands = [{"pipe": 1, "pipe_wg_per_cu": wg, "pipe_chunk_kib": ck} for wg in (1, 2, 4, 8) for ck in (0, 2048)]
     cands += [{"pipe": 0, "blocks_per_cu": bpc, "copy_block_kib": 4} for bpc in (8, 1024)]
 
     def apply(cand):

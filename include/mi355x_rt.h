@@ -127,11 +127,13 @@ enum mi355x_knob {
     MI355X_KNOB_TIME_PHASES = 11,       /* 1: time the two kernels of the direct allreduce with HIP
                                            events on the call's stream (mi355x_comm_phase_ms) */
     MI355X_KNOB_COPY_BLOCK_KIB = 12,    /* bytes per block of the pull-copy kernel, KiB (4..256, default 4) */
-    MI355X_KNOB_PIPE = 13,              /* 1 (default): a multi-process ring allreduce runs its reduce and
-                                           copy phases in ONE pipelined launch per rank, overlapped
-                                           chunk by chunk with device-side ready flags (the segmented
-                                           ring's copy/reduce overlap, coll_tuned_allreduce.c:721-831);
-                                           0: two phases separated by a host barrier */
+    MI355X_KNOB_PIPE = 13,              /* 1: a multi-process ring allreduce runs its reduce and copy
+                                           phases in ONE pipelined launch per rank, overlapped chunk by
+                                           chunk with device-side ready flags (the segmented ring's
+                                           copy/reduce overlap, coll_tuned_allreduce.c:721-831);
+                                           0 (default; environment MI355X_PIPE at creation): two phases
+                                           separated by a host barrier -- faster in every one-GPU
+                                           rehearsal measured so far (profiles/r02_bench_n2_*) */
     MI355X_KNOB_PIPE_WG_PER_CU = 14,    /* pipelined allreduce: 256-thread workgroups per CU (1..8, default 2) */
     MI355X_KNOB_PIPE_CHUNK_KIB = 15     /* pipelined allreduce: chunk size in KiB (0 = auto: ~512 chunks
                                            per ring block, at least 64 KiB) */
