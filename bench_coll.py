@@ -384,7 +384,7 @@ def run(args, pkg, torch):
                    "data_flow": "pipelined (fold + pulls, device flags)" if pipe else "two-phase pull",
                    "best": best, "autotune_ms_per_call": tried},
         "roofline": ({"bound": "xgmi", "achieved": round(fold_xgmi, 2), "peak": round(peak_all, 1), "unit": "GB/s",
-                      "frac": round(fold_xgmi / peak_all, 4), "traffic": pmc_traffic(pipe, shared=False),
+                      "frac": round(fold_xgmi / peak_all, 4), "traffic": pmc_traffic(pipe, shared=False, world=world),
                       "traffic_note": "HBM bytes per launch from a committed rocprofv3 PMC summary of this "
                                       "kernel on separate GPUs, or null: only the one-GPU rehearsal's "
                                       "(profiles/r02_pmc_rehearsal.json) exists so far",
@@ -394,7 +394,7 @@ def run(args, pkg, torch):
                       "peak_note": f"(n-1) links x {XGMI_LINK_DIR_GBS} GB/s per direction (spec); achieved = "
                                    "the remote bytes one launch reads over xGMI / its event time"} if not shared else
                      {"bound": "hbm", "achieved": round(fold_hbm, 2), "peak": 8000.0, "unit": "GB/s",
-                      "frac": round(fold_hbm / 8000.0, 4), "traffic": pmc_traffic(pipe, shared=True),
+                      "frac": round(fold_hbm / 8000.0, 4), "traffic": pmc_traffic(pipe, shared=True, world=world),
                       "kernel": kname, "kernel_avg_ms": round(p1, 4),
                       "alg_bytes_per_launch": int(hbm_bytes / world), "phase2_ms": round(p2, 4),
                       "peak_note": "REHEARSAL: all ranks share one GPU, no xGMI traffic: the n concurrent "
@@ -437,11 +437,12 @@ def run(args, pkg, torch):
     return res
 
 
-def pmc_traffic(pipe, shared):
+def pmc_traffic(pipe, shared, world):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
-    (profiles/*pmc*.json, FETCH_SIZE x 2 + WRITE_SIZE per MI355X_MICROARCH.md), or None"""
+    (profiles/*pmc*.json, FETCH_SIZE x 2 + WRITE_SIZE per MI355X_MICROARCH.md) measured at this
+    world size, or None"""
     import pathlib
-    key = ("k_pipe_allreduce" if pipe else "k_fold") + ("_rehearsal" if shared else "")
+    key = ("k_pipe_allreduce" if pipe else "k_fold") + ("_rehearsal" if shared else "") + f"_n{world}"
     for p in sorted((pathlib.Path(__file__).resolve().parent / "profiles").glob("*pmc*.json"), reverse=True):
         try:
             ent = json.loads(p.read_text()).get("kernels", {}).get(key)

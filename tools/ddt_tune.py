@@ -25,8 +25,8 @@ def main():
     alg = 2 * d.size
     best = {}
     for threads in (256, 512, 1024):
-        for unroll in (2, 4):
-            for nt in (1, 3):
+        for unroll in (2, 4, 8):
+            for nt in (0, 1, 2, 3):
                 pkg.ddt_tune(unroll, unroll, threads, nt)
                 for name, fn in (("pack", lambda s: d.pack(1, x.data_ptr(), 0, p.data_ptr(), d.size, s)),
                                  ("unpack", lambda s: d.unpack(1, y.data_ptr(), 0, p.data_ptr(), d.size, s))):
