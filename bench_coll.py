@@ -264,13 +264,14 @@ def run(args, pkg, torch):
     want = world * (world + 1) / 2
     ok = True
     tried = []
-    cands = [{"pipe": 1, "pipe_wg_per_cu": wg, "pipe_chunk_kib": ck} for wg in (1, 2, 4, 8) for ck in (0, 2048)]
+    cands = [{"pipe": 1, "pipe_wg_per_cu": wg, "pipe_chunk_kib": ck, "pipe_wt": wt}
+             for wt in (0, 1) for wg in (1, 2, 4, 8) for ck in (0, 2048)]
     cands += [{"pipe": 0, "blocks_per_cu": bpc, "copy_block_kib": 4} for bpc in (8, 1024)]
 
     def apply(cand):
         comm.set("PUSH", 0)
         comm.set("PIPE", cand["pipe"])
-        for k, knob in (("pipe_wg_per_cu", "PIPE_WG_PER_CU"), ("pipe_chunk_kib", "PIPE_CHUNK_KIB"),
+        for k, knob in (("pipe_wg_per_cu", "PIPE_WG_PER_CU"), ("pipe_chunk_kib", "PIPE_CHUNK_KIB"), ("pipe_wt", "PIPE_WT"),
                         ("blocks_per_cu", "BLOCKS_PER_CU"), ("copy_block_kib", "COPY_BLOCK_KIB")):
             if k in cand:
                 comm.set(knob, cand[k])
@@ -317,6 +318,12 @@ def run(args, pkg, torch):
         raise SystemExit("every allreduce candidate failed: " + json.dumps(tried))
     best = min(timed_ok, key=lambda c: c["ms"])
     apply(best)
+    # the chosen flow on data that changes every call (a stale hand-off would show here, where the
+    # constant data of the search above cannot)
+    for k in range(4):
+        x.fill_(float(rank + 1 + 3 * k))
+        comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
+        ok = ok and bool(torch.all(y == want + 3 * k * world).item())
     # timed data: N(0,1), order-dependent (the engine replicates the segmented-ring order)
     _log(rank, f"timed: {args.steps} steps, best {best}")
     x.normal_()

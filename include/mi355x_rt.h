@@ -135,8 +135,11 @@ enum mi355x_knob {
                                            separated by a host barrier -- faster in every one-GPU
                                            rehearsal measured so far (profiles/r02_bench_n2_*) */
     MI355X_KNOB_PIPE_WG_PER_CU = 14,    /* pipelined allreduce: 256-thread workgroups per CU (1..8, default 2) */
-    MI355X_KNOB_PIPE_CHUNK_KIB = 15     /* pipelined allreduce: chunk size in KiB (0 = auto: ~512 chunks
+    MI355X_KNOB_PIPE_CHUNK_KIB = 15,    /* pipelined allreduce: chunk size in KiB (0 = auto: ~512 chunks
                                            per ring block, at least 64 KiB) */
+    MI355X_KNOB_PIPE_WT = 16            /* pipelined allreduce: 1 = fold results stored write-through
+                                           (system-coherent policy) and pulled with coherent loads,
+                                           no per-chunk L2 write-back / invalidate; 0 (default) = fences */
 };
 int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
 /* current value of a knob (LL_MAX_BYTES reads 0 when the creation-time LL self-test failed) */

@@ -1136,6 +1136,7 @@ static int pipe_allreduce(mi355x_comm *c, int op, int type, const Program &pr,
     // vector paths: every fold operand shares the destination's misalignment (a whole element);
     // a pull needs only its source and destination to agree
     const uintptr_t m = (uintptr_t)a.dst & 15;
+    a.wt = coll_tune().pipe_wt;
     a.co_fold = (m % esz) == 0;
     for (int q = 0; q < c->size && a.co_fold; ++q) a.co_fold = (((uintptr_t)a.src[q]) & 15) == m;
     for (int q = 0; q < c->size; ++q)
@@ -1567,6 +1568,7 @@ int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
     case MI355X_KNOB_PIPE: *value = c->pipe_on ? 1 : 0; break;
     case MI355X_KNOB_PIPE_WG_PER_CU: *value = coll_tune().pipe_wg_per_cu; break;
     case MI355X_KNOB_PIPE_CHUNK_KIB: *value = coll_tune().pipe_chunk_kib; break;
+    case MI355X_KNOB_PIPE_WT: *value = coll_tune().pipe_wt; break;
     default: return set_error(MI355X_ERR_ARG, "unknown knob %d", knob);
     }
     return MI355X_SUCCESS;
@@ -1615,6 +1617,7 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
         if (value < 0 || value > (1l << 20)) return set_error(MI355X_ERR_ARG, "pipe_chunk_kib out of range");
         coll_tune().pipe_chunk_kib = (int)value;
         break;
+    case MI355X_KNOB_PIPE_WT: coll_tune().pipe_wt = value != 0; break;
     case MI355X_KNOB_TIME_PHASES:
         c->time_phases = value != 0;
         if (c->time_phases && !c->tev[0]) {

@@ -107,6 +107,7 @@ struct PipeArgs {
     uint64_t co_pull;                  // bit q: peer q's rbuf and mine share alignment mod 16
     int order[kMaxRanks];
     int n, me, co_fold;                // co_fold: every input and dst share alignment mod 16
+    int wt;                            // publish write-through (sc0 sc1), no per-chunk fences
     uint32_t nchunks;                  // chunks per block (the longest block)
     uint64_t *dbg;                     // NULL, or 4 words per workgroup: item, stage, flag seen, polls
 };
@@ -132,6 +133,8 @@ struct CollTune {
     // ranks sharing a GPU; chunk size in KiB (0: ~512 chunks per ring block, >= 64 KiB)
     int pipe_wg_per_cu = 2;
     int pipe_chunk_kib = 0;
+    // pipelined allreduce: publish chunks write-through instead of L2 write-back + invalidate fences
+    int pipe_wt = 0;
 };
 CollTune &coll_tune();
 

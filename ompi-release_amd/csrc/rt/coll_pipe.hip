@@ -49,6 +49,17 @@ template <bool NT> __device__ __forceinline__ void pstore(void *p, const u32x4p 
     else *reinterpret_cast<u32x4p *>(p) = v;
 }
 
+// write-through publishing (MI355X_KNOB_PIPE_WT): fold results stored with the system-coherent
+// cache policy (sc0 sc1: through the XCD's L2 to memory) and peers' results loaded the same way,
+// so a chunk needs neither the producer's L2 write-back fence nor the consumer's invalidate --
+// the hand-off form MI355X_MICROARCH.md measures faster for tens of KB per workgroup
+// ("publish-large").  Raw buffer ops carry the policy bits; the resource covers <= 2 GiB from base.
+constexpr int kSysCoherent = 1 | 16;  // gfx950 cache-policy bits: sc0 (1) | sc1 (16)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void *base)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, 0x7fffffff, 0x00020000);
+}
+
 template <class F>
 __device__ __forceinline__ typename F::T pfold_step(const typename F::T &acc, const typename F::T &x, bool acc_is_out)
 {
@@ -66,12 +77,13 @@ template <class F> __device__ __forceinline__ typename F::T pfold_scalar(const P
 
 // fold the vector body: U 16-B vectors per lane in flight per source, sources loaded FC at a time
 template <class F, bool NT, int U, int FC>
-__device__ __forceinline__ void fold_body(const PipeArgs &a, typename F::T *dst, size_t v0, size_t nvec)
+__device__ __forceinline__ void fold_body(const PipeArgs &a, typename F::T *dst, size_t v0, size_t nvec, bool wt)
 {
     using T = typename F::T;
     using V = PVec<T>;
     constexpr int EPV = 16 / sizeof(T);
     const size_t t = threadIdx.x, nt = blockDim.x;
+    const __amdgpu_buffer_rsrc_t rs = wt_rsrc(dst + v0);
     for (size_t base = t; base < nvec; base += nt * U) {
         V acc[U];
         for (int j0 = 0; j0 < a.n; j0 += FC) {
@@ -111,7 +123,8 @@ __device__ __forceinline__ void fold_body(const PipeArgs &a, typename F::T *dst,
             if (v < nvec) {
                 u32x4p raw;
                 __builtin_memcpy(&raw, &acc[u], 16);
-                pstore<NT>(dst + v0 + v * EPV, raw);
+                if (wt) __builtin_amdgcn_raw_buffer_store_b128(raw, rs, (unsigned)(v * 16), 0, kSysCoherent);
+                else pstore<NT>(dst + v0 + v * EPV, raw);
             }
         }
     }
@@ -120,7 +133,7 @@ __device__ __forceinline__ void fold_body(const PipeArgs &a, typename F::T *dst,
 // fold elements [lo, hi) (absolute) into dst.  Few ranks: 4 vectors per lane per source (a
 // persistent grid of a few workgroups per CU needs that much in flight to stream HBM); many
 // ranks: 2 per source, 8 sources per load group (the n loads already fill the queue).
-template <class F, bool NT> __device__ void fold_range(const PipeArgs &a, size_t lo, size_t hi)
+template <class F, bool NT> __device__ void fold_range(const PipeArgs &a, size_t lo, size_t hi, bool wt)
 {
     using T = typename F::T;
     constexpr int EPV = 16 / sizeof(T);
@@ -136,14 +149,14 @@ template <class F, bool NT> __device__ void fold_range(const PipeArgs &a, size_t
     for (size_t i = lo + t; i < lo + head; i += nt) dst[i] = pfold_scalar<F>(a, i);
     const size_t v0 = lo + head;  // first element of the vector body
     if (a.n <= 4)
-        fold_body<F, NT, 4, 4>(a, dst, v0, nvec);
+        fold_body<F, NT, 4, 4>(a, dst, v0, nvec, wt);
     else
-        fold_body<F, NT, 2, kFoldChunk>(a, dst, v0, nvec);
+        fold_body<F, NT, 2, kFoldChunk>(a, dst, v0, nvec, wt);
     for (size_t i = v0 + nvec * EPV + t; i < hi; i += nt) dst[i] = pfold_scalar<F>(a, i);
 }
 
 // copy bytes [lo, hi) (absolute byte offsets) from src to dst
-template <bool NT> __device__ void copy_range(char *dst, const char *src, size_t lo, size_t hi, bool co)
+template <bool NT> __device__ void copy_range(char *dst, const char *src, size_t lo, size_t hi, bool co, bool wt)
 {
     const size_t t = threadIdx.x, nt = blockDim.x;
     size_t head = hi - lo, nvec = 0;
@@ -156,12 +169,15 @@ template <bool NT> __device__ void copy_range(char *dst, const char *src, size_t
     for (size_t i = lo + t; i < lo + head; i += nt) dst[i] = src[i];
     const size_t b0 = lo + head;
     constexpr int U = 8;
+    const __amdgpu_buffer_rsrc_t rs = wt_rsrc(src + b0);
     for (size_t base = t; base < nvec; base += nt * U) {
         u32x4p x[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const size_t v = base + (size_t)u * nt;
-            if (v < nvec) x[u] = pload<NT>(src + b0 + v * 16);
+            if (v < nvec)
+                x[u] = wt ? __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(v * 16), 0, kSysCoherent)
+                          : pload<NT>(src + b0 + v * 16);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -209,11 +225,14 @@ template <class F, bool NT> __global__ __launch_bounds__(256) void k_pipe_allred
             // ---- fold chunk `it` of my block, then publish it to every peer
             const uint64_t k = it;
             const size_t blen = a.blen[a.me], lo = k * a.chunk, hi = lo + a.chunk < blen ? lo + a.chunk : blen;
-            if (lo < hi) fold_range<F, NT>(a, a.boff[a.me] + lo, a.boff[a.me] + hi);
+            // write-through needs every store of the chunk to be a vector one: no scalar edges
+            const bool wt = a.wt && a.co_fold && ((uintptr_t)(a.dst + (a.boff[a.me] + lo) * esz) & 15) == 0 &&
+                            (((hi - lo) * esz) & 15) == 0;
+            if (lo < hi) fold_range<F, NT>(a, a.boff[a.me] + lo, a.boff[a.me] + hi, wt);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its stores done
             __syncthreads();
             if (threadIdx.x == 0) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: L2 written back
+                if (!wt) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: L2 written back
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 for (int q = 0; q < a.n; ++q)
                     if (q != a.me) __hip_atomic_store(a.peer_flag[q] + k, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -225,6 +244,9 @@ template <class F, bool NT> __global__ __launch_bounds__(256) void k_pipe_allred
             const uint64_t k = j / (uint64_t)(a.n - 1);
             const int q = (int)((a.me + 1 + (int)(j % (uint64_t)(a.n - 1))) % a.n);
             const size_t blen = a.blen[q], lo = k * a.chunk, hi = lo + a.chunk < blen ? lo + a.chunk : blen;
+            const size_t b0 = (a.boff[q] + lo) * esz, b1 = (a.boff[q] + hi) * esz;
+            const bool co = (a.co_pull >> q) & 1u;
+            const bool wt = a.wt && co && ((uintptr_t)(a.dst + b0) & 15) == 0 && ((b1 - b0) & 15) == 0;
             if (threadIdx.x == 0) {
                 uint32_t give_up = 0;
                 const uint64_t *f = a.my_flag + (size_t)q * a.kmax + k;
@@ -240,7 +262,7 @@ template <class F, bool NT> __global__ __launch_bounds__(256) void k_pipe_allred
                         break;
                     }
                 }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale peer lines
+                if (!wt) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale peer lines
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 give_up_s = give_up;
                 dbg_store(a, 1, give_up ? 8 : 4);
@@ -248,10 +270,7 @@ template <class F, bool NT> __global__ __launch_bounds__(256) void k_pipe_allred
             }
             __syncthreads();
             const bool give_up = __builtin_amdgcn_readfirstlane(give_up_s) != 0;
-            if (!give_up && lo < hi) {
-                const size_t b0 = (a.boff[q] + lo) * esz, b1 = (a.boff[q] + hi) * esz;
-                copy_range<NT>(a.dst, a.peer_rbuf[q], b0, b1, (a.co_pull >> q) & 1u);
-            }
+            if (!give_up && lo < hi) copy_range<NT>(a.dst, a.peer_rbuf[q], b0, b1, co, wt);
         }
         __syncthreads();  // every lane is done with item_s / give_up_s before lane 0 rewrites them
     }

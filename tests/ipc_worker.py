@@ -205,7 +205,8 @@ def pipe_checks(pkg, comm, rank, size, oracle, torch):
     comm.set("LL_MAX_BYTES", 0)
     cases = [("SUM", "FLOAT", 300_007), ("SUM", "FLOAT", size * (1 << 18) * 2 + 12_345),
              ("PROD", "C_DOUBLE_COMPLEX", 100_003), ("MAXLOC", "DOUBLE_INT", 70_001), ("BAND", "INT64", 4099)]
-    for opname, tname, count in cases:
+    for opname, tname, count, wt in [c + (w,) for c in cases for w in (0, 1)]:
+        comm.set("PIPE_WT", wt)  # fenced publishing, then write-through publishing
         op, ty = pkg.OP[opname], pkg.T[tname]
         esz = pkg.type_size(ty)
         xs = [opdata.make(tname, count, 3000 + r) for r in range(size)]
@@ -225,18 +226,20 @@ def pipe_checks(pkg, comm, rank, size, oracle, torch):
                 comm.allreduce(None if inplace else dx.data_ptr(), dr.data_ptr(), count, ty, op)
                 got = dr.cpu().numpy().view(xs[0].dtype)
                 opdata.assert_same(tname, opname, got, outs[rank],
-                                   f"pipe allreduce {opname}/{tname} count={count} skew={skew} inplace={inplace}")
+                                   f"pipe allreduce {opname}/{tname} count={count} skew={skew} inplace={inplace} wt={wt}")
                 assert comm.last_algorithm() == ran
     # back to back, values change every call; then the same with the two-phase flow
     x = torch.empty(1 << 20, device="cuda")
     y = torch.empty_like(x)
-    for pipe in (1, 0, 1):
+    for pipe, wt in ((1, 0), (0, 0), (1, 1), (1, 0), (1, 1)):
         comm.set("PIPE", pipe)
+        comm.set("PIPE_WT", wt)
         for k in range(16):
             x.fill_(float(rank + k))
             comm.allreduce(x.data_ptr(), y.data_ptr(), x.numel(), pkg.T["FLOAT"], pkg.OP["SUM"])
-            assert bool(torch.all(y == sum(r + k for r in range(size)))), ("pipe back-to-back", pipe, k)
+            assert bool(torch.all(y == sum(r + k for r in range(size)))), ("pipe back-to-back", pipe, wt, k)
     comm.set("PIPE", 0)
+    comm.set("PIPE_WT", 0)
     comm.set("LL_MAX_BYTES", 0)
     print(f"rank {rank} pipe OK", flush=True)
 
