@@ -131,15 +131,16 @@ enum mi355x_knob {
                                            phases in ONE pipelined launch per rank, overlapped chunk by
                                            chunk with device-side ready flags (the segmented ring's
                                            copy/reduce overlap, coll_tuned_allreduce.c:721-831);
-                                           0 (default; environment MI355X_PIPE at creation): two phases
-                                           separated by a host barrier -- faster in every one-GPU
-                                           rehearsal measured so far (profiles/r02_bench_n2_*) */
+                                           0: two phases separated by a host barrier.  Default (environment
+                                           MI355X_PIPE=0/1 at creation overrides): 1 from 4 ranks up,
+                                           where the one-GPU rehearsal measured it ahead (n = 4: 2.03 vs
+                                           2.14 ms, n = 8: 3.85 vs 4.47), 0 below (n = 2: 1.01 vs 0.93) */
     MI355X_KNOB_PIPE_WG_PER_CU = 14,    /* pipelined allreduce: 256-thread workgroups per CU (1..8, default 2) */
     MI355X_KNOB_PIPE_CHUNK_KIB = 15,    /* pipelined allreduce: chunk size in KiB (0 = auto: ~512 chunks
                                            per ring block, at least 64 KiB) */
-    MI355X_KNOB_PIPE_WT = 16            /* pipelined allreduce: 1 = fold results stored write-through
-                                           (system-coherent policy) and pulled with coherent loads,
-                                           no per-chunk L2 write-back / invalidate; 0 (default) = fences */
+    MI355X_KNOB_PIPE_WT = 16            /* pipelined allreduce: 1 (default) = fold results stored write-
+                                           through (system-coherent policy) and pulled with coherent
+                                           loads, no per-chunk L2 write-back / invalidate; 0 = fences */
 };
 int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
 /* current value of a knob (LL_MAX_BYTES reads 0 when the creation-time LL self-test failed) */

@@ -1459,7 +1459,9 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     rc = barrier(c);  // everybody mapped the segment and bound its socket: the name can go
     if (rank == 0) shm_unlink(c->shm_name.c_str());
     c->ll_max = (size_t)std::max(0.0, env_double("MI355X_LL_MAX_BYTES", 0.0));
-    c->pipe_on = env_double("MI355X_PIPE", 0.0) != 0.0;
+    // pipelined allreduce by default from 4 ranks up: ahead of the two-phase flow at n = 4 and 8,
+    // behind at n = 2 in the one-GPU rehearsal (profiles/r02_bench_n{2,4,8}_*); MI355X_PIPE=0/1 decides
+    c->pipe_on = env_double("MI355X_PIPE", size >= 4 ? 1.0 : 0.0) != 0.0;
     if (rc == MI355X_SUCCESS && size > 1) rc = ll_selftest(c);
     if (rc) {
         mi355x_comm_destroy(c);

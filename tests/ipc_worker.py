@@ -200,7 +200,8 @@ def pipe_checks(pkg, comm, rank, size, oracle, torch):
     misalignment (scalar fold, per-peer pull paths), many back-to-back calls (flags and the work
     queue reused)"""
     ptrs = lambda arrs: (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
-    assert comm.get("PIPE") == 0  # off by default (two-phase measured faster in the rehearsal)
+    assert comm.get("PIPE") == (1 if size >= 4 else 0)  # default: on from 4 ranks up
+    assert comm.get("PIPE_WT") == 1
     comm.set("PIPE", 1)
     comm.set("LL_MAX_BYTES", 0)
     cases = [("SUM", "FLOAT", 300_007), ("SUM", "FLOAT", size * (1 << 18) * 2 + 12_345),
@@ -238,8 +239,8 @@ def pipe_checks(pkg, comm, rank, size, oracle, torch):
             x.fill_(float(rank + k))
             comm.allreduce(x.data_ptr(), y.data_ptr(), x.numel(), pkg.T["FLOAT"], pkg.OP["SUM"])
             assert bool(torch.all(y == sum(r + k for r in range(size)))), ("pipe back-to-back", pipe, wt, k)
-    comm.set("PIPE", 0)
-    comm.set("PIPE_WT", 0)
+    comm.set("PIPE", 1 if size >= 4 else 0)
+    comm.set("PIPE_WT", 1)
     comm.set("LL_MAX_BYTES", 0)
     print(f"rank {rank} pipe OK", flush=True)
 
