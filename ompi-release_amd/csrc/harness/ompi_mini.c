@@ -877,6 +877,12 @@ size_t mini_offsetof(int which)
     case 23: return offsetof(mca_coll_base_module_t, coll_scan);
     case 24: return offsetof(mca_coll_base_comm_coll_t, coll_scatterv);
     case 25: return offsetof(mca_coll_base_comm_coll_t, coll_gather);
+    case 26: return offsetof(mca_pml_base_module_t, pml_irecv);
+    case 27: return offsetof(mca_pml_base_module_t, pml_isend);
+    case 28: return offsetof(mca_pml_base_module_t, pml_probe);
+    case 29: return offsetof(mca_pml_base_module_t, pml_max_tag);
+    case 30: return sizeof(mca_pml_base_module_t);
+    case 31: return sizeof(ompi_status_public_t);
     default: return (size_t)-1;
     }
 }

@@ -102,6 +102,13 @@ def test_abi_offsets():
         23: 16 + 8 + 14 * 8,         # coll module: scan = 15th blocking fn (coll.h:390-409)
         24: 16 * 16,                 # comm coll table: scatterv pair = 17th (coll.h:469-504)
         25: 9 * 16,                  # comm coll table: gather pair = 10th
+        # mca_pml_base_module_t (pml.h:497-531): 21 function pointers, then two 4-byte limits
+        26: 7 * 8,                   # pml_irecv: 8th (add/del procs, enable, progress, add/del comm, irecv_init)
+        27: 10 * 8,                  # pml_isend: 11th
+        28: 13 * 8,                  # pml_probe: 14th
+        29: 21 * 8 + 4,              # pml_max_tag after pml_max_contextid
+        30: 21 * 8 + 8,
+        31: 4 * 4 + 8,               # ompi_status_public_t (mpi.h.in:344-356)
     }
     for k, v in want.items():
         assert L.mini_offsetof(k) == v, (k, L.mini_offsetof(k), v)
