@@ -910,7 +910,11 @@ static int staged_bcast(mi355x_comm *c, void *buf, size_t bytes, int root, hipSt
 // kernel it waits for.
 static bool ll_usable(const mi355x_comm *c, size_t bytes)
 {
-    return !c->loopback && c->size > 1 && c->size <= kLLMaxRanks && bytes > 0 && bytes <= c->ll_max;
+    if (c->loopback || c->size < 2 || c->size > kLLMaxRanks || bytes == 0 || bytes > c->ll_max) return false;
+    // ranks sharing a GPU: every rank's blocks spin until the others' have pushed, so all of them
+    // must be resident at once -- at most one block per CU for the ranks together
+    const size_t blocks = (bytes + kLLChunk - 1) / kLLChunk;
+    return c->pipe_share <= 1 || blocks * (size_t)c->pipe_share <= (size_t)device_cu_count();
 }
 
 // (Re)allocate and exchange the LL region: [ack words, one per rank][2 parities x n slots of
@@ -1074,11 +1078,6 @@ static int ensure_pipe(mi355x_comm *c)
     if (rc) return rc;
     c->pipe_peer.assign(n, nullptr);
     for (size_t q = 0; q < n; ++q) c->pipe_peer[q] = (char *)P[0][q];
-    // ranks of this communicator on my GPU (a one-GPU rehearsal): they split the CUs, so every
-    // rank's persistent grid stays co-resident with the others'
-    int share = 0;
-    for (int q = 0; q < c->size; ++q) share += c->ctrl->slot[q].dev_uid == c->ctrl->slot[c->rank].dev_uid;
-    c->pipe_share = share > 0 ? share : 1;
     TRACE(c, "pipe region %zu bytes, %d ranks on this GPU", bytes, c->pipe_share);
     return barrier(c);  // every rank has read the exchange slots
 }
@@ -1458,6 +1457,11 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     }
     rc = barrier(c);  // everybody mapped the segment and bound its socket: the name can go
     if (rank == 0) shm_unlink(c->shm_name.c_str());
+    // ranks of this communicator on my GPU (a one-GPU rehearsal, or an oversubscribed node): they
+    // split the CUs, and a persistent or spinning launch of one must stay co-resident with the others'
+    int share = 0;
+    for (int q = 0; q < size; ++q) share += c->ctrl->slot[q].dev_uid == uid;
+    c->pipe_share = std::max(1, share);
     c->ll_max = (size_t)std::max(0.0, env_double("MI355X_LL_MAX_BYTES", 0.0));
     // pipelined allreduce by default from 4 ranks up: ahead of the two-phase flow at n = 4 and 8,
     // behind at n = 2 in the one-GPU rehearsal (profiles/r02_bench_n{2,4,8}_*); MI355X_PIPE=0/1 decides

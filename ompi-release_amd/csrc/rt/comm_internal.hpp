@@ -227,7 +227,7 @@ struct mi355x_comm {
     uint64_t *pipe_queue = nullptr;               // device work-queue counter (monotonic)
     uint64_t pipe_qbase = 0;                      // its value when the next launch starts
     uint64_t pipe_seq = 0;                        // calls of the pipelined flow so far
-    int pipe_share = 0;                           // ranks of this communicator on my GPU (0: unknown)
+    int pipe_share = 1;                           // ranks of this communicator on my GPU (set at creation)
     bool pipe_on = false;                         // MI355X_KNOB_PIPE (env MI355X_PIPE; default: size >= 4)
     uint64_t *pipe_dbg = nullptr;                 // MI355X_DEBUG: per-workgroup progress words
     // nonblocking collectives: one progress thread per communicator runs the posted calls in
