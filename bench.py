@@ -165,6 +165,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-legs", action="store_true", help="N > 1: skip the other configs' legs")
+    ap.add_argument("--no-autotune", action="store_true",
+                    help="N > 1: time the engine's default allreduce flow only (for profiling one configuration)")
     ap.add_argument("--legs-timeout", type=float, default=300.0,
                     help="N > 1: seconds after which the legs are abandoned and the headline printed")
     args = ap.parse_args()

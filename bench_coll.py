@@ -267,6 +267,10 @@ def run(args, pkg, torch):
     cands = [{"pipe": 1, "pipe_wg_per_cu": wg, "pipe_chunk_kib": ck, "pipe_wt": wt}
              for wt in (0, 1) for wg in (1, 2, 4, 8) for ck in (0, 2048)]
     cands += [{"pipe": 0, "blocks_per_cu": bpc, "copy_block_kib": 4} for bpc in (8, 1024)]
+    if getattr(args, "no_autotune", False):  # the engine's defaults only
+        cands = [{"pipe": comm.get("PIPE"), "pipe_wg_per_cu": comm.get("PIPE_WG_PER_CU"),
+                  "pipe_chunk_kib": comm.get("PIPE_CHUNK_KIB"), "pipe_wt": comm.get("PIPE_WT"),
+                  "blocks_per_cu": comm.get("BLOCKS_PER_CU"), "copy_block_kib": comm.get("COPY_BLOCK_KIB")}]
 
     def apply(cand):
         comm.set("PUSH", 0)
