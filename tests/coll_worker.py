@@ -379,7 +379,49 @@ def pml_main():
         rc = L.mini_recv(y.data_ptr(), 500, fdt, 0, 15, comm, ctypes.byref(st))
         assert rc == 15 and st.MPI_ERROR == 15, (rc, st.MPI_ERROR)  # MPI_ERR_TRUNCATE
         assert bool((y == 1).all())
-    # 6. host buffers and buffered sends -> the saved PML (the stub answers 77)
+    # 6. edge cases: zero-count messages, MPI_PROC_NULL, MPI_ANY_TAG, a derived receive type, many
+    #    outstanding nonblocking messages between the same pair (ob1's per-pair ordering)
+    z = torch.zeros(4, device="cuda")
+    if rank == 0:
+        assert L.mini_send(z.data_ptr(), 0, fdt, 1, 20, comm) == 0
+    elif rank == 1:
+        assert L.mini_recv(z.data_ptr(), 0, fdt, 0, 20, comm, ctypes.byref(st)) == 0
+        assert (st.MPI_SOURCE, st.MPI_TAG, st._ucount) == (0, 20, 0)
+    PROC_NULL = -2
+    assert L.mini_send(z.data_ptr(), 4, fdt, PROC_NULL, 21, comm) == 0
+    assert L.mini_recv(z.data_ptr(), 4, fdt, PROC_NULL, 21, comm, ctypes.byref(st)) == 0
+    assert st.MPI_SOURCE == PROC_NULL and st._ucount == 0, (st.MPI_SOURCE, st._ucount)
+    if rank in (0, 1):
+        nblk = 300
+        desc, used, tsize, lb, ub = opal_vector(nblk, 256, 512)
+        vdt = m.derived(desc, used, tsize, lb, ub)
+        if rank == 1:
+            flat = torch.arange(nblk * 64, dtype=torch.float32, device="cuda") * 3
+            torch.cuda.synchronize()
+            assert L.mini_send(flat.data_ptr(), nblk * 64, fdt, 0, 22, comm) == 0
+        else:
+            strided = torch.full((nblk * 128,), -1.0, device="cuda")
+            assert L.mini_recv(strided.data_ptr(), 1, vdt, 1, ANY, comm, ctypes.byref(st)) == 0
+            got = strided.view(nblk, 128)
+            assert torch.equal(got[:, :64].reshape(-1), torch.arange(nblk * 64, dtype=torch.float32, device="cuda") * 3)
+            assert bool((got[:, 64:] == -1).all()), "gaps of the receive type untouched"
+            assert st.MPI_TAG == 22
+        L.mini_datatype_destroy(vdt)
+        nmsg, cnt = 24, 5000
+        bufs = [torch.full((cnt,), float(100 * rank + i), device="cuda") for i in range(nmsg)]
+        torch.cuda.synchronize()
+        reqs = [ctypes.c_void_p() for _ in range(nmsg)]
+        for i in range(nmsg):  # same tag: the messages must match in sending order
+            if rank == 0:
+                assert L.mini_isend(bufs[i].data_ptr(), cnt, fdt, 1, 23, comm, ctypes.byref(reqs[i])) == 0
+            else:
+                assert L.mini_irecv(bufs[i].data_ptr(), cnt, fdt, 0, 23, comm, ctypes.byref(reqs[i])) == 0
+        for i in range(nmsg):
+            assert L.mini_wait_status(ctypes.byref(reqs[i]), None) == 0
+        if rank == 1:
+            for i in range(nmsg):
+                assert bool((bufs[i] == float(i)).all()), ("ordering", i, float(bufs[i][0]))
+    # 7. host buffers and buffered sends -> the saved PML (the stub answers 77)
     h = np.zeros(16, dtype=np.float32)
     before = [L.mini_pml_stub_calls(w) for w in range(6)]
     assert L.mini_send(h.ctypes.data, 16, fdt, right, 16, comm) == 77
