@@ -9,6 +9,7 @@ in the mini-OMPI harness), on device buffers, vs the oracle.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 import pathlib
 import subprocess
@@ -184,3 +185,27 @@ def test_pml_slot_device_p2p(gpu, size):
         outs.append(out)
     for r, p in enumerate(procs):
         assert p.returncode == 0 and f"rank {r} pml OK" in outs[r], f"rank {r}:\n{outs[r][-3000:]}"
+
+
+def test_pml_hook_opt_out(gpu, monkeypatch):
+    """coll_mi355x_pml_hook=0 (MCA variable, here through OMPI_MCA_*) leaves the PML table alone;
+    by default init_query hooks it and close restores it"""
+    m = mini()
+    L = m.lib
+    comp = m.component_ptr(m.coll, "mca_coll_mi355x_component")
+    saved = [L.mini_pml_fn(w) for w in range(6)]
+    hook = ctypes.c_int.in_dll(m.coll, "mca_coll_mi355x_pml_hook")
+    try:
+        monkeypatch.setenv("OMPI_MCA_coll_mi355x_pml_hook", "0")
+        assert L.mini_component_register(comp) == 0 and hook.value == 0
+        assert L.mini_coll_init(comp) == 0
+        assert [L.mini_pml_fn(w) for w in range(6)] == saved, "opted out, yet the PML was hooked"
+        assert L.mini_coll_close(comp) == 0
+        monkeypatch.setenv("OMPI_MCA_coll_mi355x_pml_hook", "1")
+        assert L.mini_component_register(comp) == 0 and hook.value == 1
+        assert L.mini_coll_init(comp) == 0
+        assert L.mini_pml_fn(1) == m.addr(m.coll, "mca_coll_mi355x_pml_send")
+    finally:
+        assert L.mini_coll_close(comp) == 0
+        hook.value = 1
+    assert [L.mini_pml_fn(w) for w in range(6)] == saved
