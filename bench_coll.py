@@ -402,6 +402,8 @@ def run(args, pkg, torch):
                       "kernel": kname, "kernel_avg_ms": round(p1, 4),
                       "alg_bytes_per_launch": int(xgmi_bytes), "phase2_ms": round(p2, 4),
                       "busbw_frac": round(busbw / peak_all, 4),
+                      # against one ring (one link per direction) as well as all n-1
+                      "busbw_frac_ring1": round(busbw / XGMI_LINK_DIR_GBS, 4),
                       "peak_note": f"(n-1) links x {XGMI_LINK_DIR_GBS} GB/s per direction (spec); achieved = "
                                    "the remote bytes one launch reads over xGMI / its event time"} if not shared else
                      {"bound": "hbm", "achieved": round(fold_hbm, 2), "peak": 8000.0, "unit": "GB/s",
