@@ -49,13 +49,12 @@ __device__ __forceinline__ Where locate(const DdtDev &d, int64_t p)
     return w;
 }
 
-// checksum: every block stores its partial sum (waves reduced by shuffles, then through LDS) and
-// counts itself done; the last block to finish adds the partials and writes the result straight
-// into host-mapped memory -- no second launch, no device-to-host copy, no atomics on one hot word
-// for the data (one counter increment per block)
+// checksum: every block stores its partial sum (waves reduced by shuffles, then through LDS);
+// k_csum_finish, the next launch on the stream, adds the partials and writes the result straight
+// into host-mapped memory -- no device-to-host copy, and no atomics (a one-shot grid has tens of
+// thousands of blocks: one counter for them all would serialise, MI355X_MICROARCH.md "fanin")
 struct CsumSink {
     unsigned *partial;   // one word per block
-    unsigned *counter;   // blocks done; zero before the launch, reset to zero by the last block
     unsigned *out;       // host-mapped result word
     unsigned nblocks;
 };
@@ -64,7 +63,6 @@ __device__ __forceinline__ unsigned block_reduce(unsigned acc)
 {
     __shared__ unsigned ws[16];
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
-    __syncthreads();  // ws may still be read by a previous call
     if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = acc;
     __syncthreads();
     unsigned t = 0;
@@ -73,30 +71,31 @@ __device__ __forceinline__ unsigned block_reduce(unsigned acc)
     return t;  // valid in thread 0
 }
 
-__device__ __forceinline__ void block_sum_finish(unsigned acc, const CsumSink &k)
+__device__ __forceinline__ void block_sum_store(unsigned acc, const CsumSink &k)
 {
-    __shared__ unsigned last;
     const unsigned t = block_reduce(acc);
-    if (threadIdx.x == 0) {
-        // the partial is one word written through to memory (agent-scope store), drained before
-        // the count: no L2 write-back fence per block (a release here costs one XCD-wide L2
-        // write-back per block -- 16 K of them for a 1 GiB window)
-        __hip_atomic_store(k.partial + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned prev = __hip_atomic_fetch_add(k.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = (prev == k.nblocks - 1) ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // once per launch; the loads below are agent-scope too
+    if (threadIdx.x == 0) k.partial[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(1024) void k_csum_finish(CsumSink k)
+{
+    // tens of thousands of partials through one workgroup: 16-B loads, 8 in flight per lane
     unsigned a = 0;
-    for (unsigned i = threadIdx.x; i < k.nblocks; i += blockDim.x)
-        a += __hip_atomic_load(k.partial + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned total = block_reduce(a);
-    if (threadIdx.x == 0) {
-        __hip_atomic_store(k.out, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(k.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned nv = k.nblocks / 4;
+    const u32x4d *pv = reinterpret_cast<const u32x4d *>(k.partial);
+    for (unsigned base = threadIdx.x; base < nv; base += 8 * blockDim.x) {
+        u32x4d v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const unsigned i = base + u * blockDim.x;
+            v[u] = i < nv ? pv[i] : u32x4d{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a += v[u].x + v[u].y + v[u].z + v[u].w;
     }
+    for (unsigned i = 4 * nv + threadIdx.x; i < k.nblocks; i += blockDim.x) a += k.partial[i];
+    const unsigned total = block_reduce(a);
+    if (threadIdx.x == 0) __hip_atomic_store(k.out, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <bool PACK, bool CSUM>
@@ -142,7 +141,7 @@ __global__ __launch_bounds__(256) void k_ddt(DdtDev d, char *mem, char *packed, 
             }
         }
     }
-    if constexpr (CSUM) block_sum_finish(acc, csum);
+    if constexpr (CSUM) block_sum_store(acc, csum);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -216,21 +215,14 @@ __device__ __forceinline__ unsigned rows_pass(const RowArgs &a, uint32_t base, u
     return acc;
 }
 
-// without a checksum: one-shot grid, every lane one pass of U slots (measured fastest); with one:
-// a capped grid striding over the window, so that few blocks report a partial
+// one-shot grid, every lane one pass of U slots (measured fastest); with a checksum every block
+// then stores its partial
 template <bool PACK, bool CSUM, int NTM, int U>
 __global__ __launch_bounds__(1024) void k_ddt_rows(RowArgs a, CsumSink csum)
 {
     const uint32_t tpb = blockDim.x;
-    if constexpr (!CSUM) {
-        (void)rows_pass<PACK, false, NTM, U>(a, blockIdx.x * (tpb * U) + threadIdx.x, tpb);
-    } else {
-        unsigned acc = 0;
-        const uint64_t step = (uint64_t)gridDim.x * tpb * U;
-        for (uint64_t base = (uint64_t)blockIdx.x * (tpb * U) + threadIdx.x; base < a.nslots; base += step)
-            acc += rows_pass<PACK, true, NTM, U>(a, (uint32_t)base, tpb);
-        block_sum_finish(acc, csum);
-    }
+    const unsigned acc = rows_pass<PACK, CSUM, NTM, U>(a, blockIdx.x * (tpb * U) + threadIdx.x, tpb);
+    if constexpr (CSUM) block_sum_store(acc, csum);
 }
 
 // the row kernel applies: one run per block, every address and the window 16-B aligned, and
@@ -253,13 +245,12 @@ DdtTune &ddt_tune()
     return t;
 }
 
-// checksum workspaces: partials + counter on the device, the result word in host-mapped memory;
-// pooled per device (a call holds one until its stream has finished with it)
+// checksum workspaces: partials on the device, the result word in host-mapped memory; pooled per
+// device (a call holds one until its stream has finished with it)
 struct CsumWs {
     int device = -1;
     unsigned *partial = nullptr;
     size_t cap = 0;
-    unsigned *counter = nullptr;
     unsigned *host = nullptr, *host_dev = nullptr;
 };
 static std::mutex g_csum_mtx;
@@ -286,8 +277,6 @@ struct Csum {
         if (!ws) {
             ws = new CsumWs();
             ws->device = dev;
-            MI_HIP(hipMalloc((void **)&ws->counter, sizeof(unsigned)));
-            MI_HIP(hipMemset(ws->counter, 0, sizeof(unsigned)));
             MI_HIP(hipHostMalloc((void **)&ws->host, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
             MI_HIP(hipHostGetDevicePointer((void **)&ws->host_dev, ws->host, 0));
         }
@@ -299,15 +288,17 @@ struct Csum {
             ws->cap = blocks;
         }
         sink.partial = ws->partial;
-        sink.counter = ws->counter;
         sink.out = ws->host_dev;
         sink.nblocks = blocks;
         return MI355X_SUCCESS;
     }
-    // wait for the launch, hand the checksum over, return the workspace to the pool
+    // add the partials (next launch on the stream), wait, hand the checksum over, return the
+    // workspace to the pool
     int finish(unsigned *want, hipStream_t s)
     {
         if (!want) return MI355X_SUCCESS;
+        hipLaunchKernelGGL(k_csum_finish, dim3(1), dim3(1024), 0, s, sink);
+        MI_HIP(hipGetLastError());
         MI_HIP(hipStreamSynchronize(s));
         *want = __atomic_load_n(ws->host, __ATOMIC_ACQUIRE);
         std::lock_guard<std::mutex> g(g_csum_mtx);
@@ -317,11 +308,10 @@ struct Csum {
     }
     ~Csum()
     {
-        // a workspace still held here belongs to a failed launch: its counter may be stale, so it
+        // a workspace still held here belongs to a failed launch (a kernel may still use it): it
         // is dropped rather than pooled
         if (ws) {
             (void)hipFree(ws->partial);
-            (void)hipFree(ws->counter);
             (void)hipHostFree(ws->host);
             delete ws;
         }
@@ -372,11 +362,7 @@ int launch_ddt_rows(const DdtDev &d, int nruns_host, int64_t run_disp, int64_t r
     int ntm = t.nontemporal;
     if (ntm < 0) ntm = (2 * bytes > ((int64_t)256 << 20)) ? kDdtAutoNT : 0;  // streaming sizes
     const uint64_t per = (uint64_t)tpb * (uint64_t)unroll;
-    unsigned blocks = (unsigned)((a.nslots + per - 1) / per);
-    if (csum) {  // checksum: a capped, striding grid (one partial and one count per block)
-        const unsigned cap = (unsigned)(8 * device_cu_count() * (1024 / tpb));
-        if (blocks > cap) blocks = cap;
-    }
+    const unsigned blocks = (unsigned)((a.nslots + per - 1) / per);
     Csum part;
     int rc = part.get(csum, blocks);
     if (rc) return rc;
