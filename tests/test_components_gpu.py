@@ -118,7 +118,7 @@ def test_op_hip_concurrent_callers(gpu, pkg, oracle):
     assert not errors, errors[:5]
 
 
-@pytest.mark.parametrize("size", [2, 3])
+@pytest.mark.parametrize("size", [2, 3, 4])  # 4: the pipelined allreduce is the default from 4 ranks
 def test_coll_component_processes(gpu, size):
     key = uuid.uuid4().hex[:10]
     env = dict(os.environ, MI355X_TIMEOUT_S="60", OMPI_COMM_WORLD_SIZE=str(size),
