@@ -128,6 +128,9 @@ def leg_ddt(pkg, torch, args, emit, oracle):
     avg, _ = timed(torch, lambda s: p.copy_(x[:, :64]), args.steps, args.warmup)
     emit({"leg": "torch_strided_copy_ref", "alg_bytes": alg, "kernel_avg_ms": round(avg, 5),
           "achieved_GBs": round(alg / (avg * 1e-3) / 1e9, 1)})
+    avg, _ = timed(torch, lambda s: y[:, :64].copy_(p), args.steps, args.warmup)  # the unpack direction
+    emit({"leg": "torch_strided_unpack_ref", "alg_bytes": alg, "kernel_avg_ms": round(avg, 5),
+          "achieved_GBs": round(alg / (avg * 1e-3) / 1e9, 1)})
     del x, p, y
     if oracle is not None and not args.no_cpu_baseline:
         import numpy as np
