@@ -142,8 +142,9 @@ def test_segmented_ring_region(gpu, pkg, oracle, comms, n):
             # the result really is order-sensitive: a naive rank-order fold differs somewhere
             if opname == "SUM":
                 naive = xs[0].copy()
-                for q in range(1, n):
-                    naive = (naive + xs[q]).astype(np.float32)
+                with np.errstate(over="ignore", invalid="ignore"):  # the inputs carry ±Inf / NaN specials
+                    for q in range(1, n):
+                        naive = (naive + xs[q]).astype(np.float32)
                 assert len(opdata.mismatches("FLOAT", "SUM", naive, outs[0])) > 0
             del dx, dr
 
