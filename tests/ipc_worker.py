@@ -249,6 +249,44 @@ def pipe_checks(pkg, comm, rank, size, oracle, torch):
     print(f"rank {rank} pipe OK", flush=True)
 
 
+def pipe_all_slots(pkg, comm, rank, size, oracle, torch):
+    """every (op, type) slot of the pipelined kernel (one instantiation each) on the ring path,
+    fenced and write-through publishing, against the oracle's schedule simulation"""
+    ptrs = lambda arrs: (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    comm.set("PIPE", 1)
+    comm.set("LL_MAX_BYTES", 0)
+    bad = []
+    k = 0
+    for code in range(1, 13):
+        for ty in range(len(pkg.TYPES)):
+            if not (oracle.oracle_has_op(code, ty) and pkg.op_supported(code, ty)):
+                continue
+            tname, opname = pkg.TYPES[ty], pkg.OPS[code]
+            esz = pkg.type_size(ty)
+            count = (64 << 10) // esz + 2 * k + 1  # above the ring threshold, odd, a different tail per slot
+            xs = [opdata.make(tname, count, 5000 + 7 * k + r) for r in range(size)]
+            outs = [np.zeros_like(xs[0]) for _ in range(size)]
+            ran = oracle.oracle_allreduce(0, size, count, ty, code, 0, ptrs(xs), ptrs(outs))
+            if ran not in (4, 5):
+                continue
+            comm.set("PIPE_WT", k & 1)
+            dx = torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda()
+            dr = torch.zeros_like(dx)
+            torch.cuda.synchronize()
+            comm.allreduce(dx.data_ptr(), dr.data_ptr(), count, ty, code)
+            try:
+                opdata.assert_same(tname, opname, dr.cpu().numpy().view(xs[0].dtype), outs[rank],
+                                   f"pipe slot {opname}/{tname} count={count}")
+            except AssertionError as e:
+                bad.append(str(e)[:300])
+            k += 1
+    comm.set("PIPE", 1 if size >= 4 else 0)
+    comm.set("PIPE_WT", 1)
+    assert not bad, "\n".join(bad[:8])
+    assert k >= 100, k  # every GPU slot ran
+    print(f"rank {rank} pipe slots OK ({k})", flush=True)
+
+
 def _pattern_chunk(torch, lo, hi):
     """int32 words lo..hi-1 of the big-bcast pattern (an LCG of the word index, wraps in int32)"""
     return torch.arange(lo, hi, dtype=torch.int32, device="cuda") * 1103515245 + 12345
@@ -398,6 +436,8 @@ def _main():
         assert int(dst[r * nb:(r + 1) * nb].min()) == r + 1
     realloc_same_address(pkg, comm, rank, size)
     pipe_checks(pkg, comm, rank, size, oracle, torch)
+    if size == 3:
+        pipe_all_slots(pkg, comm, rank, size, oracle, torch)
     ll_checks(pkg, comm, rank, size, oracle, torch)
     p2p_checks(pkg, comm, rank, size, oracle, torch)
     _fd_report(rank)
