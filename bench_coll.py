@@ -263,7 +263,6 @@ def run(args, pkg, torch):
     y = torch.empty_like(x)
     want = world * (world + 1) / 2
     ok = True
-    tried = []
     cands = [{"pipe": 1, "pipe_wg_per_cu": wg, "pipe_chunk_kib": ck, "pipe_wt": wt}
              for wt in (0, 1) for wg in (1, 2, 4, 8) for ck in (0, 2048)]
     cands += [{"pipe": 0, "blocks_per_cu": bpc, "copy_block_kib": 4} for bpc in (8, 1024)]
@@ -272,56 +271,9 @@ def run(args, pkg, torch):
                   "pipe_chunk_kib": comm.get("PIPE_CHUNK_KIB"), "pipe_wt": comm.get("PIPE_WT"),
                   "blocks_per_cu": comm.get("BLOCKS_PER_CU"), "copy_block_kib": comm.get("COPY_BLOCK_KIB")}]
 
-    def apply(cand):
-        comm.set("PUSH", 0)
-        comm.set("PIPE", cand["pipe"])
-        for k, knob in (("pipe_wg_per_cu", "PIPE_WG_PER_CU"), ("pipe_chunk_kib", "PIPE_CHUNK_KIB"), ("pipe_wt", "PIPE_WT"),
-                        ("blocks_per_cu", "BLOCKS_PER_CU"), ("copy_block_kib", "COPY_BLOCK_KIB")):
-            if k in cand:
-                comm.set(knob, cand[k])
-
-    # a candidate that fails (e.g. a flag never seen over this machine's links: the engine's
-    # bounded wait turns it into an error on every rank) is dropped with its flow, the
-    # communicator is rebuilt and the search goes on; every rank agrees on the outcome first
-    failed_flows = set()
-    comm.set("TIMEOUT_S", 30)
-    for cand in cands:
-        if cand["pipe"] in failed_flows:
-            continue
-        _log(rank, f"autotune {cand}")
-        err = None
-        cand_ok = True
-        try:
-            apply(cand)
-            torch.cuda.synchronize()
-            comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
-            cand_ok = bool(torch.all(y == want).item())
-            t0 = time.perf_counter()
-            for _ in range(3):
-                comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
-            el = (time.perf_counter() - t0) / 3
-        except pkg.MI355XError as e:
-            err, el = repr(e)[:240], float("inf")
-        agree = torch.tensor([el, 1.0 if err else 0.0])
-        dist.all_reduce(agree, op=dist.ReduceOp.MAX)
-        if agree[1] > 0:
-            failed_flows.add(cand["pipe"])
-            tried.append(dict(cand, ms=None, error=err or "failed on another rank"))
-            torch.cuda.synchronize()
-            dist.barrier()
-            comm.destroy()
-            key = f"{key}_r"
-            comm = pkg.Comm.create(key, rank, world, local)
-            comm.set("TIMEOUT_S", 30)
-            continue
-        ok = ok and cand_ok
-        tried.append(dict(cand, ms=round(float(agree[0]) * 1e3, 4)))
-    comm.set("TIMEOUT_S", 120)
-    timed_ok = [c for c in tried if c["ms"] is not None]
-    if not timed_ok:
-        raise SystemExit("every allreduce candidate failed: " + json.dumps(tried))
-    best = min(timed_ok, key=lambda c: c["ms"])
-    apply(best)
+    comm, key, tried, ok, best = autotune(comm, key, cands, pkg=pkg, dist=dist, rank=rank, world=world,
+                                          local=local, x=x, y=y, n=n, ty=ty, op=op, want=want,
+                                          sync=torch.cuda.synchronize, ok=ok)
     # the chosen flow on data that changes every call (a stale hand-off would show here, where the
     # constant data of the search above cannot)
     for k in range(4):
@@ -448,6 +400,66 @@ def run(args, pkg, torch):
         res["error"] = "allreduce result differs from the exact sum"
         res["value"] = None
     return res
+
+
+def apply_cand(comm, cand):
+    """set a candidate's knobs on the engine communicator"""
+    comm.set("PUSH", 0)
+    comm.set("PIPE", cand["pipe"])
+    for k, knob in (("pipe_wg_per_cu", "PIPE_WG_PER_CU"), ("pipe_chunk_kib", "PIPE_CHUNK_KIB"), ("pipe_wt", "PIPE_WT"),
+                    ("blocks_per_cu", "BLOCKS_PER_CU"), ("copy_block_kib", "COPY_BLOCK_KIB")):
+        if k in cand:
+            comm.set(knob, cand[k])
+
+
+def autotune(comm, key, cands, *, pkg, dist, rank, world, local, x, y, n, ty, op, want, sync, ok=True):
+    """time every candidate (3 calls, max over ranks) after an exactness check on constant data.
+    A candidate that fails -- e.g. a flag never seen over this machine's links: the engine's
+    bounded wait turns it into an error on every rank, or on some -- is dropped with its flow;
+    every rank agrees on the outcome first, then the communicator is rebuilt under a new key and
+    the search goes on.  Returns (comm, key, tried, ok, best); best is applied."""
+    import torch
+    tried = []
+    failed_flows = set()
+    comm.set("TIMEOUT_S", 30)
+    for cand in cands:
+        if cand["pipe"] in failed_flows:
+            continue
+        _log(rank, f"autotune {cand}")
+        err = None
+        cand_ok = True
+        try:
+            apply_cand(comm, cand)
+            sync()
+            comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
+            cand_ok = bool(torch.all(y == want).item())
+            t0 = time.perf_counter()
+            for _ in range(3):
+                comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
+            el = (time.perf_counter() - t0) / 3
+        except pkg.MI355XError as e:
+            err, el = repr(e)[:240], float("inf")
+        agree = torch.tensor([el, 1.0 if err else 0.0])
+        dist.all_reduce(agree, op=dist.ReduceOp.MAX)
+        if agree[1] > 0:
+            failed_flows.add(cand["pipe"])
+            tried.append(dict(cand, ms=None, error=err or "failed on another rank"))
+            sync()
+            dist.barrier()
+            comm.destroy()
+            key = f"{key}_r"
+            comm = pkg.Comm.create(key, rank, world, local)
+            comm.set("TIMEOUT_S", 30)
+            continue
+        ok = ok and cand_ok
+        tried.append(dict(cand, ms=round(float(agree[0]) * 1e3, 4)))
+    comm.set("TIMEOUT_S", 120)
+    timed_ok = [c for c in tried if c["ms"] is not None]
+    if not timed_ok:
+        raise SystemExit("every allreduce candidate failed: " + json.dumps(tried))
+    best = min(timed_ok, key=lambda c: c["ms"])
+    apply_cand(comm, best)
+    return comm, key, tried, ok, best
 
 
 def pmc_traffic(pipe, shared, world):
