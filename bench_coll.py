@@ -350,7 +350,7 @@ def run(args, pkg, torch):
                       "frac": round(fold_xgmi / peak_all, 4), "traffic": pmc_traffic(pipe, shared=False, world=world),
                       "traffic_note": "HBM bytes per launch from a committed rocprofv3 PMC summary of this "
                                       "kernel on separate GPUs, or null: only the one-GPU rehearsal's "
-                                      "(profiles/r02_pmc_rehearsal.json) exists so far",
+                                      "(profiles/r02_pmc_rehearsal_n*.json) exists so far",
                       "kernel": kname, "kernel_avg_ms": round(p1, 4),
                       "alg_bytes_per_launch": int(xgmi_bytes), "phase2_ms": round(p2, 4),
                       "busbw_frac": round(busbw / peak_all, 4),
