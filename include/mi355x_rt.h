@@ -105,6 +105,10 @@ int mi355x_comm_barrier(mi355x_comm_t *comm);
  * 5 binomial; reduce_scatter: 1 non-overlapping, 2 recursive halving, 3 ring) */
 int mi355x_comm_last_algorithm(const mi355x_comm_t *comm);
 
+/* Knobs BLOCKS_PER_CU, PUSH, COPY_BLOCK_KIB, PIPE_WG_PER_CU, PIPE_CHUNK_KIB and PIPE_WT are launch
+ * shapes shared by every communicator of the process (setting one through any communicator sets
+ * it for all; every rank of a communicator must use the same values); the others belong to the
+ * communicator they are set on. */
 enum mi355x_knob {
     MI355X_KNOB_ALLREDUCE_ALG = 1,      /* coll_tuned_allreduce_algorithm (0 = decision) */
     MI355X_KNOB_REDUCE_ALG = 2,         /* coll_tuned_reduce_algorithm, used by reduce_scatter_block */
