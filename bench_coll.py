@@ -253,8 +253,8 @@ def run(args, pkg, torch):
     n = GIB // 4
     dev = torch.device("cuda", local)
     ty, op = pkg.T["FLOAT"], pkg.OP["SUM"]
-    # data-flow / launch-shape autotune on the real size, with the exactness check on every
-    # candidate: x_r = r + 1 everywhere -> every element = n(n+1)/2.  Candidates: the pipelined
+    # data-flow / launch-shape autotune on the real size, with an exactness check on every
+    # candidate (check_calls: data that changes per call, rbuf poisoned first).  Candidates: the pipelined
     # flow (one launch: fold + pulls with device-side chunk flags; workgroups per CU x chunk size)
     # and the two-phase flow (fold -> host barrier -> pull; grid cap).  All ranks see the same
     # max-over-ranks times, so they pick the same candidate.  Push is not a candidate: its remote
@@ -274,12 +274,6 @@ def run(args, pkg, torch):
     comm, key, tried, ok, best = autotune(comm, key, cands, pkg=pkg, dist=dist, rank=rank, world=world,
                                           local=local, x=x, y=y, n=n, ty=ty, op=op, want=want,
                                           sync=torch.cuda.synchronize, ok=ok)
-    # the chosen flow on data that changes every call (a stale hand-off would show here, where the
-    # constant data of the search above cannot)
-    for k in range(4):
-        x.fill_(float(rank + 1 + 3 * k))
-        comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
-        ok = ok and bool(torch.all(y == want + 3 * k * world).item())
     # timed data: N(0,1), order-dependent (the engine replicates the segmented-ring order)
     _log(rank, f"timed: {args.steps} steps, best {best}")
     x.normal_()
@@ -412,17 +406,34 @@ def apply_cand(comm, cand):
             comm.set(knob, cand[k])
 
 
+def check_calls(comm, x, y, n, ty, op, *, rank, world, want, ks):
+    """exactness on data that changes every call, with rbuf poisoned (NaN) before each call: a
+    stale hand-off -- a peer's block read before its owner's result reached memory -- shows here,
+    where constant data (the same sum every call) cannot.  x_r = r + 1 + 3k -> want + 3k*world."""
+    import torch
+    good = True
+    for k in ks:
+        x.fill_(float(rank + 1 + 3 * k))
+        y.fill_(float("nan"))
+        comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
+        good = good and bool(torch.all(y == want + 3 * k * world).item())
+    return good
+
+
 def autotune(comm, key, cands, *, pkg, dist, rank, world, local, x, y, n, ty, op, want, sync, ok=True):
-    """time every candidate (3 calls, max over ranks) after an exactness check on constant data.
+    """time every candidate (3 calls, max over ranks) after an exactness check on changing data.
     A candidate that fails -- e.g. a flag never seen over this machine's links: the engine's
     bounded wait turns it into an error on every rank, or on some -- is dropped with its flow;
     every rank agrees on the outcome first, then the communicator is rebuilt under a new key and
-    the search goes on.  Returns (comm, key, tried, ok, best); best is applied."""
+    the search goes on.  A candidate whose result is wrong on any rank (a stale hand-off) is
+    dropped alone.  The winner is re-checked on fresh data; if that fails the next best is taken.
+    Returns (comm, key, tried, ok, best); best is applied, ok is False only when no candidate
+    passed the re-check."""
     import torch
     tried = []
     failed_flows = set()
     comm.set("TIMEOUT_S", 30)
-    for cand in cands:
+    for ci, cand in enumerate(cands):
         if cand["pipe"] in failed_flows:
             continue
         _log(rank, f"autotune {cand}")
@@ -431,15 +442,14 @@ def autotune(comm, key, cands, *, pkg, dist, rank, world, local, x, y, n, ty, op
         try:
             apply_cand(comm, cand)
             sync()
-            comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
-            cand_ok = bool(torch.all(y == want).item())
+            cand_ok = check_calls(comm, x, y, n, ty, op, rank=rank, world=world, want=want, ks=(2 * ci, 2 * ci + 1))
             t0 = time.perf_counter()
             for _ in range(3):
                 comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
             el = (time.perf_counter() - t0) / 3
         except pkg.MI355XError as e:
             err, el = repr(e)[:240], float("inf")
-        agree = torch.tensor([el, 1.0 if err else 0.0])
+        agree = torch.tensor([el, 1.0 if err else 0.0, 0.0 if cand_ok else 1.0])
         dist.all_reduce(agree, op=dist.ReduceOp.MAX)
         if agree[1] > 0:
             failed_flows.add(cand["pipe"])
@@ -451,15 +461,26 @@ def autotune(comm, key, cands, *, pkg, dist, rank, world, local, x, y, n, ty, op
             comm = pkg.Comm.create(key, rank, world, local)
             comm.set("TIMEOUT_S", 30)
             continue
-        ok = ok and cand_ok
+        if agree[2] > 0:
+            tried.append(dict(cand, ms=None, error="wrong result" + ("" if not cand_ok else " on another rank")))
+            continue
         tried.append(dict(cand, ms=round(float(agree[0]) * 1e3, 4)))
     comm.set("TIMEOUT_S", 120)
-    timed_ok = [c for c in tried if c["ms"] is not None]
-    if not timed_ok:
+    ranked = sorted((c for c in tried if c["ms"] is not None), key=lambda c: c["ms"])
+    if not ranked:
         raise SystemExit("every allreduce candidate failed: " + json.dumps(tried))
-    best = min(timed_ok, key=lambda c: c["ms"])
-    apply_cand(comm, best)
-    return comm, key, tried, ok, best
+    for i, best in enumerate(ranked):
+        apply_cand(comm, best)
+        sync()
+        good = check_calls(comm, x, y, n, ty, op, rank=rank, world=world, want=want,
+                           ks=range(1000 + 4 * i, 1004 + 4 * i))
+        agree = torch.tensor([0.0 if good else 1.0])
+        dist.all_reduce(agree, op=dist.ReduceOp.MAX)
+        if agree[0] == 0:
+            return comm, key, tried, ok, best
+        best["recheck"] = "wrong result on fresh data: dropped"
+    apply_cand(comm, ranked[0])
+    return comm, key, tried, False, ranked[0]
 
 
 def pmc_traffic(pipe, shared, world):

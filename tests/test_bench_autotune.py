@@ -1,6 +1,7 @@
 """bench_coll.autotune on CPU (gloo, 2 processes, a fake engine): a flow that fails on one rank
 only is dropped by both (they agree before acting), the communicator is rebuilt under a new key,
-the other flow is timed and chosen, and every rank ends with the same choice."""
+a candidate whose result is stale on one rank is dropped by both, the remaining one is timed and
+chosen, and every rank ends with the same choice."""
 from __future__ import annotations
 
 import ctypes
@@ -37,7 +38,12 @@ class FakeComm:
     def allreduce(self, sbuf, rbuf, n, ty, op):
         if self.knobs.get("PIPE") == 1 and self.rank == 0:  # the pipelined flow fails on rank 0 only
             raise FakeError("pipelined allreduce timed out waiting for a peer")
-        want = (ctypes.c_float * n)(*([3.0] * n))
+        # 2 ranks, x_r = r + 1 + 3k (bench_coll.check_calls) -> sum = 3 + 6k; the two-phase flow
+        # with a 1024-block grid returns the previous call's sum on rank 1 (a stale hand-off)
+        v = ctypes.c_float.from_address(sbuf).value
+        k = round((v - self.rank - 1) / 3)
+        stale = self.knobs.get("BLOCKS_PER_CU") == 1024 and self.rank == 1
+        want = (ctypes.c_float * n)(*([3.0 + 6 * (k - (1 if stale else 0))] * n))
         ctypes.memmove(rbuf, want, 4 * n)
 
 
@@ -63,7 +69,8 @@ def _rank(rank, port, q):
         y = torch.zeros(n)
         cands = [{"pipe": 1, "pipe_wg_per_cu": 2, "pipe_chunk_kib": 0, "pipe_wt": 1},
                  {"pipe": 1, "pipe_wg_per_cu": 4, "pipe_chunk_kib": 0, "pipe_wt": 1},
-                 {"pipe": 0, "blocks_per_cu": 1024, "copy_block_kib": 4}]
+                 {"pipe": 0, "blocks_per_cu": 1024, "copy_block_kib": 4},
+                 {"pipe": 0, "blocks_per_cu": 8, "copy_block_kib": 4}]
         comm0 = FakeComm("k", rank)
         comm, key, tried, ok, best = bench_coll.autotune(
             comm0, "k", cands, pkg=FakePkg, dist=dist, rank=rank, world=2, local=0, x=x, y=y, n=n, ty=0, op=3,
@@ -90,8 +97,11 @@ def test_autotune_drops_a_flow_failing_on_one_rank():
         assert isinstance(out, dict), out
         assert out["key"] == "k_r" and out["old_destroyed"], out      # rebuilt once, on both ranks
         assert out["best"]["pipe"] == 0 and out["new_pipe"] == 0, out  # the surviving flow, applied
+        assert out["best"]["blocks_per_cu"] == 8, out                  # not the stale candidate
         assert out["ok"], out
         pipe_rows = [t for t in out["tried"] if t["pipe"] == 1]
         assert len(pipe_rows) == 1 and pipe_rows[0]["ms"] is None, out  # the flow dropped after its first failure
         assert "error" in pipe_rows[0]
+        stale = [t for t in out["tried"] if t.get("blocks_per_cu") == 1024]
+        assert len(stale) == 1 and stale[0]["ms"] is None and "wrong result" in stale[0]["error"], out
     assert res[0]["best"] == res[1]["best"]
