@@ -306,6 +306,11 @@ int mi355x_ddt_nruns(const mi355x_ddt_t *d);
  * unpack (2/4/8; 0 keeps), threads per block (256/512/1024; 0 keeps), nontemporal -2 keep,
  * -1 auto (non-temporal above 256 MiB moved), 0..3 mask (1 = loads, 2 = stores) */
 int mi355x_ddt_tune(int unroll_pack, int unroll_unpack, int threads, int nontemporal);
+/* which pack/unpack kernels may run: 2 (default) the row kernel for every one-run-per-block
+ * layout, with the widest slot (16/8/4/2/1 B) its addresses and window allow, and the unit
+ * kernel (LDS-staged run tables, W-byte units) for run lists of up to 4096 runs; 1 the row kernel
+ * with 16-B slots only; 0 neither (the general kernel for everything; A/B measurement, tests) */
+int mi355x_ddt_tune_rows(int mode);
 /* pack packed bytes [pos, pos+bytes) of `count` instances at device `base` into `dst`
  * (replaces opal_convertor_set_position + opal_convertor_pack on a CUDA convertor,
  * opal_convertor.c:223-330 / opal_datatype_cuda.c:93-115).  checksum (may be NULL) receives the

@@ -157,6 +157,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "mi355x_ddt_extent": (c.c_int64, [vp]),
         "mi355x_ddt_nruns": (i, [vp]),
         "mi355x_ddt_tune": (i, [i, i, i, i]),
+        "mi355x_ddt_tune_rows": (i, [i]),
         "mi355x_gather": (i, [vp, vp, vp, sz, i, vp]),
         "mi355x_gatherv": (i, [vp, vp, sz, vp, c.POINTER(sz), c.POINTER(sz), i, vp]),
         "mi355x_scatter": (i, [vp, vp, vp, sz, i, vp]),
@@ -540,6 +541,11 @@ class Ddt:
 def ddt_tune(unroll_pack: int = 0, unroll_unpack: int = 0, threads: int = 0, nontemporal: int = -2) -> None:
     """launch shape of the single-run pack/unpack kernel (see mi355x_ddt_tune)"""
     check(rt().mi355x_ddt_tune(unroll_pack, unroll_unpack, threads, nontemporal), "mi355x_ddt_tune")
+
+
+def ddt_tune_rows(mode: int) -> None:
+    """which layouts take the row pack/unpack kernel: 2 any slot width, 1 16-B only, 0 none"""
+    check(rt().mi355x_ddt_tune_rows(mode), "mi355x_ddt_tune_rows")
 
 
 def sched_program(kind: int, n: int, alg: int, block: int) -> list[int]:

@@ -15,6 +15,7 @@
 struct mi355x_ddt {
     std::vector<int64_t> disp, len, elem, pfx;
     int64_t nblk = 1, stride = 0, extent = 0;
+    uint64_t run_bits = 0;  // OR of every run's displacement and length (their common alignment)
     int64_t *ddisp = nullptr, *dlen = nullptr, *dpfx = nullptr;  // device copies, made on first use
     int dev = -1;
     std::mutex mtx;
@@ -44,6 +45,8 @@ static int finalize(mi355x_ddt *d, mi355x_ddt_t **out)
     const size_t n = d->disp.size();
     d->pfx.assign(n, 0);
     for (size_t r = 1; r < n; ++r) d->pfx[r] = d->pfx[r - 1] + d->len[r - 1];
+    d->run_bits = 0;
+    for (size_t r = 0; r < n; ++r) d->run_bits |= (uint64_t)d->disp[r] | (uint64_t)d->len[r];
     *out = d;
     return MI355X_SUCCESS;
 }
@@ -234,6 +237,7 @@ static int ddt_move(const mi355x_ddt_t *d, bool pack, size_t count, void *mem, s
     dv.extent = d->extent;
     dv.blk_bytes = blk_bytes(d);
     dv.inst_bytes = inst;
+    dv.run_bits = d->run_bits;
     unsigned h = 0;
     unsigned *sum = checksum ? &h : nullptr;  // the launchers wait for the kernel when asked for one
     int rc = 1;
@@ -274,6 +278,13 @@ int mi355x_ddt_tune(int unroll_pack, int unroll_unpack, int threads, int nontemp
     if (unroll_unpack) t.unroll_unpack = unroll_unpack;
     if (threads) t.threads = threads;
     if (nontemporal != -2) t.nontemporal = nontemporal;
+    return MI355X_SUCCESS;
+}
+
+int mi355x_ddt_tune_rows(int mode)
+{
+    if (mode < 0 || mode > 2) return set_error(MI355X_ERR_ARG, "row-kernel mode must be 0, 1 or 2");
+    ddt_tune().rows = mode;
     return MI355X_SUCCESS;
 }
 

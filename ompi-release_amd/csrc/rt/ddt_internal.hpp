@@ -19,6 +19,7 @@ struct DdtDev {
     int nruns;
     int64_t nblk, stride, extent;
     int64_t blk_bytes, inst_bytes;
+    uint64_t run_bits;     // OR of every run's displacement and length (their common alignment)
 };
 
 // launch shape of the row kernel: slots per lane (2, 4, 8) and the non-temporal mask
@@ -29,13 +30,15 @@ struct DdtTune {
     int unroll_unpack = 2;
     int threads = 256;
     int nontemporal = -1;
+    int rows = 2;  // mi355x_ddt_tune_rows: 2 row kernel any slot width + unit kernel, 1 16-B rows only, 0 none
 };
 DdtTune &ddt_tune();
 
 // csum: NULL, or where the window's checksum goes (the launch is then waited for)
 int launch_ddt(const DdtDev &d, bool pack, void *mem, void *packed, int64_t pos, int64_t bytes, unsigned *csum,
                hipStream_t s);
-// the row kernel (one run per block, 16-B aligned); returns 1 when it does not apply
+// the row kernel (one run per block, slots of the widest power-of-two width <= 16 B every
+// address and length allows); returns 1 when it does not apply
 int launch_ddt_rows(const DdtDev &d, int nruns_host, int64_t run_disp, int64_t run_len, bool pack, void *mem,
                     void *packed, int64_t pos, int64_t bytes, unsigned *csum, hipStream_t s);
 

@@ -146,10 +146,14 @@ __global__ __launch_bounds__(256) void k_ddt(DdtDev d, char *mem, char *packed, 
 
 // ---------------------------------------------------------------------------------------------
 // Row kernel: the layout is one run of L bytes per block (vector, contiguous-with-gaps: what
-// MPI_Type_vector and most derived types used for halos/columns compile to), everything 16-byte
-// aligned.  Row g (over all instances) starts at (g / nblk) * extent + (g % nblk) * stride + disp.
-// One-shot grid: each lane moves U 16-byte slots, lanes of a wave on consecutive slots, all U
-// loads issued before the stores.  The two divisions per slot are 32-bit multiply-high
+// MPI_Type_vector and most derived types used for halos/columns compile to).  The packed stream
+// is cut into W-byte slots, W the largest power of two (<= 16) dividing the run length, the run's
+// address, the stride, the extent, the packed address and the window: 16 for the configs[4]
+// shape, 8 for a column of doubles (MPI_Type_vector(n, 1, s, MPI_DOUBLE)), 4 for 3-float blocks,
+// down to 1 for odd byte windows.  Row g (over all instances) starts at
+// (g / nblk) * extent + (g % nblk) * stride + disp.  One-shot grid: each lane moves U slots,
+// lanes of a wave on consecutive slots (one wave-instruction = 64 W contiguous packed bytes), all
+// U loads issued before the stores.  The two divisions per slot are 32-bit multiply-high
 // (Granlund-Montgomery magic numbers computed on the host), no 64-bit division, no search.
 struct FastDiv {
     uint32_t m, l, d;
@@ -177,14 +181,33 @@ struct RowArgs {
     int64_t disp, stride, extent;
     FastDiv per_row;   // slots per row
     FastDiv per_inst;  // rows per instance (nblk)
-    uint32_t first;    // first slot (pos / 16)
+    uint32_t first;    // first slot (pos / W)
     uint32_t nslots;
 };
 
-template <bool PACK, bool CSUM, int NTM, int U>
+template <int W> struct SlotT;
+template <> struct SlotT<16> { typedef u32x4d type; };
+template <> struct SlotT<8> { typedef unsigned long long type; };
+template <> struct SlotT<4> { typedef unsigned type; };
+template <> struct SlotT<2> { typedef unsigned short type; };
+template <> struct SlotT<1> { typedef unsigned char type; };
+
+// the slot's share of the checksum (opal_uicsum_partial: the sum of the stream's native 32-bit
+// words; q = absolute slot index, so the slot starts at packed byte q * W)
+template <int W> __device__ __forceinline__ unsigned slot_csum(const typename SlotT<W>::type &v, uint32_t q)
+{
+    if constexpr (W == 16) return v.x + v.y + v.z + v.w;
+    else if constexpr (W == 8) return (unsigned)v + (unsigned)(v >> 32);
+    else if constexpr (W == 4) return v;
+    else if constexpr (W == 2) return (unsigned)v << (16 * (q & 1));
+    else return (unsigned)v << (8 * (q & 3));
+}
+
+template <bool PACK, bool CSUM, int NTM, int U, int W>
 __device__ __forceinline__ unsigned rows_pass(const RowArgs &a, uint32_t base, uint32_t tpb)
 {
-    u32x4d v[U];
+    typedef typename SlotT<W>::type S;
+    S v[U];
     char *mp[U];
     unsigned acc = 0;
 #pragma unroll
@@ -197,8 +220,8 @@ __device__ __forceinline__ unsigned rows_pass(const RowArgs &a, uint32_t base, u
             const uint32_t w = q - g * a.per_row.d;
             const uint32_t k = fdiv(g, a.per_inst);
             const uint32_t j = g - k * a.per_inst.d;
-            mp[u] = a.mem + (int64_t)k * a.extent + (int64_t)j * a.stride + a.disp + ((int64_t)w << 4);
-            const u32x4d *src = reinterpret_cast<const u32x4d *>(PACK ? mp[u] : a.packed + ((size_t)i << 4));
+            mp[u] = a.mem + (int64_t)k * a.extent + (int64_t)j * a.stride + a.disp + (int64_t)w * W;
+            const S *src = reinterpret_cast<const S *>(PACK ? mp[u] : a.packed + (size_t)i * W);
             if constexpr ((NTM & 1) != 0) v[u] = __builtin_nontemporal_load(src);
             else v[u] = *src;
         }
@@ -206,10 +229,11 @@ __device__ __forceinline__ unsigned rows_pass(const RowArgs &a, uint32_t base, u
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         if (mp[u]) {
-            u32x4d *dst = reinterpret_cast<u32x4d *>(PACK ? a.packed + ((size_t)(base + (uint32_t)u * tpb) << 4) : mp[u]);
+            const uint32_t i = base + (uint32_t)u * tpb;
+            S *dst = reinterpret_cast<S *>(PACK ? a.packed + (size_t)i * W : mp[u]);
             if constexpr ((NTM & 2) != 0) __builtin_nontemporal_store(v[u], dst);
             else *dst = v[u];
-            if constexpr (CSUM) acc += v[u].x + v[u].y + v[u].z + v[u].w;
+            if constexpr (CSUM) acc += slot_csum<W>(v[u], a.first + i);
         }
     }
     return acc;
@@ -217,26 +241,30 @@ __device__ __forceinline__ unsigned rows_pass(const RowArgs &a, uint32_t base, u
 
 // one-shot grid, every lane one pass of U slots (measured fastest); with a checksum every block
 // then stores its partial
-template <bool PACK, bool CSUM, int NTM, int U>
+template <bool PACK, bool CSUM, int NTM, int U, int W>
 __global__ __launch_bounds__(1024) void k_ddt_rows(RowArgs a, CsumSink csum)
 {
     const uint32_t tpb = blockDim.x;
-    const unsigned acc = rows_pass<PACK, CSUM, NTM, U>(a, blockIdx.x * (tpb * U) + threadIdx.x, tpb);
+    const unsigned acc = rows_pass<PACK, CSUM, NTM, U, W>(a, blockIdx.x * (tpb * U) + threadIdx.x, tpb);
     if constexpr (CSUM) block_sum_store(acc, csum);
 }
 
-// the row kernel applies: one run per block, every address and the window 16-B aligned, and
-// slot / row counts in 32 bits
-static bool rows_apply(const DdtDev &d, int nruns_host, int64_t run_disp, int64_t run_len, const void *mem,
-                       const void *packed, int64_t pos, int64_t bytes)
+// the slot width the row kernel can use (0: it does not apply): one run per block, and every
+// address, length and window a multiple of W; slot / row counts in 32 bits
+static int rows_width(const DdtDev &d, int nruns_host, int64_t run_disp, int64_t run_len, const void *mem,
+                      const void *packed, int64_t pos, int64_t bytes)
 {
-    if (nruns_host != 1 || (run_len & 15) || run_len == 0) return false;
-    if (((uintptr_t)mem + (uint64_t)run_disp) & 15) return false;
-    if ((d.stride & 15) || (d.extent & 15) || ((uintptr_t)packed & 15) || (pos & 15) || (bytes & 15)) return false;
-    const int64_t last_slot = (pos + bytes) >> 4;
-    const int64_t rows = last_slot / (run_len >> 4) + 1;
-    return last_slot < ((int64_t)1 << 32) && rows < ((int64_t)1 << 32) && d.nblk < ((int64_t)1 << 32) &&
-           (run_len >> 4) < ((int64_t)1 << 32);
+    if (nruns_host != 1 || run_len <= 0) return 0;
+    const uint64_t bits = (uint64_t)run_len | ((uintptr_t)mem + (uint64_t)run_disp) | (uint64_t)d.stride |
+                          (uint64_t)d.extent | (uintptr_t)packed | (uint64_t)pos | (uint64_t)bytes;
+    int w = 16;
+    while (w > 1 && (bits & (uint64_t)(w - 1))) w >>= 1;
+    const int64_t last_slot = (pos + bytes) / w;
+    const int64_t rows = last_slot / (run_len / w) + 1;
+    if (last_slot >= ((int64_t)1 << 32) || rows >= ((int64_t)1 << 32) || d.nblk >= ((int64_t)1 << 32) ||
+        (run_len / w) >= ((int64_t)1 << 32))
+        return 0;
+    return w;
 }
 
 DdtTune &ddt_tune()
@@ -323,9 +351,9 @@ static void launch_rows_u(const RowArgs &a, int unroll, unsigned tpb, unsigned b
                           hipStream_t s)
 {
     switch (unroll) {
-    case 2: hipLaunchKernelGGL((k_ddt_rows<PACK, CSUM, NTM, 2>), dim3(blocks), dim3(tpb), 0, s, a, part); break;
-    case 8: hipLaunchKernelGGL((k_ddt_rows<PACK, CSUM, NTM, 8>), dim3(blocks), dim3(tpb), 0, s, a, part); break;
-    default: hipLaunchKernelGGL((k_ddt_rows<PACK, CSUM, NTM, 4>), dim3(blocks), dim3(tpb), 0, s, a, part); break;
+    case 2: hipLaunchKernelGGL((k_ddt_rows<PACK, CSUM, NTM, 2, 16>), dim3(blocks), dim3(tpb), 0, s, a, part); break;
+    case 8: hipLaunchKernelGGL((k_ddt_rows<PACK, CSUM, NTM, 8, 16>), dim3(blocks), dim3(tpb), 0, s, a, part); break;
+    default: hipLaunchKernelGGL((k_ddt_rows<PACK, CSUM, NTM, 4, 16>), dim3(blocks), dim3(tpb), 0, s, a, part); break;
     }
 }
 
@@ -341,23 +369,47 @@ static void launch_rows(const RowArgs &a, int ntm, int unroll, unsigned tpb, uns
     }
 }
 
+// narrow slots (W < 16): fixed shape, kNarrowUnroll slots per lane, non-temporal or not
+constexpr int kNarrowUnroll = 8;
+template <bool PACK, bool CSUM, int W>
+static void launch_rows_w(const RowArgs &a, bool nt, unsigned tpb, unsigned blocks, const CsumSink &part, hipStream_t s)
+{
+    if (nt) hipLaunchKernelGGL((k_ddt_rows<PACK, CSUM, 3, kNarrowUnroll, W>), dim3(blocks), dim3(tpb), 0, s, a, part);
+    else hipLaunchKernelGGL((k_ddt_rows<PACK, CSUM, 0, kNarrowUnroll, W>), dim3(blocks), dim3(tpb), 0, s, a, part);
+}
+
+template <bool PACK, bool CSUM>
+static void launch_rows_narrow(int w, const RowArgs &a, bool nt, unsigned tpb, unsigned blocks, const CsumSink &part,
+                               hipStream_t s)
+{
+    switch (w) {
+    case 8: launch_rows_w<PACK, CSUM, 8>(a, nt, tpb, blocks, part, s); break;
+    case 4: launch_rows_w<PACK, CSUM, 4>(a, nt, tpb, blocks, part, s); break;
+    case 2: launch_rows_w<PACK, CSUM, 2>(a, nt, tpb, blocks, part, s); break;
+    default: launch_rows_w<PACK, CSUM, 1>(a, nt, tpb, blocks, part, s); break;
+    }
+}
+
 int launch_ddt_rows(const DdtDev &d, int nruns_host, int64_t run_disp, int64_t run_len, bool pack, void *mem,
                     void *packed, int64_t pos, int64_t bytes, unsigned *csum, hipStream_t s)
 {
-    if (!rows_apply(d, nruns_host, run_disp, run_len, mem, packed, pos, bytes)) return 1;
+    const int mode = ddt_tune().rows;
+    const int w = mode > 0 ? rows_width(d, nruns_host, run_disp, run_len, mem, packed, pos, bytes) : 0;
+    if (w == 0 || (w < 16 && mode < 2)) return 1;
     RowArgs a;
     a.mem = static_cast<char *>(mem);
     a.packed = static_cast<char *>(packed);
     a.disp = run_disp;
     a.stride = d.stride;
     a.extent = d.extent;
-    a.per_row = make_fastdiv((uint32_t)(run_len >> 4));
+    a.per_row = make_fastdiv((uint32_t)(run_len / w));
     a.per_inst = make_fastdiv((uint32_t)d.nblk);
-    a.first = (uint32_t)(pos >> 4);
-    a.nslots = (uint32_t)(bytes >> 4);
+    a.first = (uint32_t)(pos / w);
+    a.nslots = (uint32_t)(bytes / w);
     const DdtTune &t = ddt_tune();
     int unroll = pack ? t.unroll_pack : t.unroll_unpack;
     if (unroll != 2 && unroll != 8) unroll = 4;
+    if (w < 16) unroll = kNarrowUnroll;
     const unsigned tpb = (t.threads == 256 || t.threads == 512) ? (unsigned)t.threads : 1024u;
     int ntm = t.nontemporal;
     if (ntm < 0) ntm = (2 * bytes > ((int64_t)256 << 20)) ? kDdtAutoNT : 0;  // streaming sizes
@@ -366,7 +418,15 @@ int launch_ddt_rows(const DdtDev &d, int nruns_host, int64_t run_disp, int64_t r
     Csum part;
     int rc = part.get(csum, blocks);
     if (rc) return rc;
-    if (pack) {
+    if (w < 16) {
+        if (pack) {
+            if (csum) launch_rows_narrow<true, true>(w, a, ntm != 0, tpb, blocks, part.sink, s);
+            else launch_rows_narrow<true, false>(w, a, ntm != 0, tpb, blocks, part.sink, s);
+        } else {
+            if (csum) launch_rows_narrow<false, true>(w, a, ntm != 0, tpb, blocks, part.sink, s);
+            else launch_rows_narrow<false, false>(w, a, ntm != 0, tpb, blocks, part.sink, s);
+        }
+    } else if (pack) {
         if (csum) launch_rows<true, true>(a, ntm, unroll, tpb, blocks, part.sink, s);
         else launch_rows<true, false>(a, ntm, unroll, tpb, blocks, part.sink, s);
     } else {
@@ -377,10 +437,145 @@ int launch_ddt_rows(const DdtDev &d, int nruns_host, int64_t run_disp, int64_t r
     return part.finish(csum, s);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Unit kernel: any run list (indexed, struct, several runs per block) whose runs, strides, the
+// buffers and the window are all multiples of a W-byte unit (W = 16, 8, 4, 2 or 1).  The run
+// tables are staged into LDS once per workgroup (packed prefix in units as 32-bit words, run
+// displacements) -- the "gathered datatype" staging: every unit's run lookup is then a binary
+// search in LDS instead of dependent global loads; instance and block come from two 32-bit
+// multiply-high divisions.  Lanes of a wave take consecutive units (the packed side coalesces);
+// a persistent grid so the table staging is paid once per workgroup, not per unit.
+struct UnitArgs {
+    char *mem;
+    char *packed;
+    const int64_t *disp;   // device run tables (bytes)
+    const int64_t *pfx;
+    int nruns;
+    int lw;                // log2(W)
+    int64_t stride, extent;
+    FastDiv per_inst;      // units per instance
+    FastDiv per_blk;       // units per block
+    uint32_t first;        // first unit (pos / W)
+    uint32_t nunits;
+};
+
+constexpr int kUnitMaxRuns = 4096;   // LDS: 12 B per run -> 48 KiB
+constexpr int kUnitU = 4;            // units per lane per pass
+
+template <bool PACK, bool CSUM, int W>
+__global__ __launch_bounds__(256) void k_ddt_units(UnitArgs a, CsumSink csum)
+{
+    typedef typename SlotT<W>::type S;
+    extern __shared__ int64_t unit_lds[];
+    int64_t *sdisp = unit_lds;
+    uint32_t *spfx = reinterpret_cast<uint32_t *>(unit_lds + a.nruns);
+    for (int r = threadIdx.x; r < a.nruns; r += blockDim.x) {
+        sdisp[r] = a.disp[r];
+        spfx[r] = (uint32_t)(a.pfx[r] >> a.lw);
+    }
+    __syncthreads();
+    const uint32_t tpb = blockDim.x, stride = gridDim.x * tpb * kUnitU;
+    unsigned acc = 0;
+    for (uint32_t base = blockIdx.x * tpb * kUnitU + threadIdx.x; base < a.nunits; base += stride) {
+        S v[kUnitU];
+        char *mp[kUnitU];
+#pragma unroll
+        for (int u = 0; u < kUnitU; ++u) {
+            const uint32_t i = base + (uint32_t)u * tpb;
+            mp[u] = nullptr;
+            if (i < a.nunits) {
+                const uint32_t q = a.first + i;
+                const uint32_t k = fdiv(q, a.per_inst);
+                const uint32_t rem = q - k * a.per_inst.d;
+                const uint32_t j = fdiv(rem, a.per_blk);
+                const uint32_t o = rem - j * a.per_blk.d;
+                int lo = 0, hi = a.nruns - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (spfx[mid] <= o) lo = mid;
+                    else hi = mid - 1;
+                }
+                mp[u] = a.mem + (int64_t)k * a.extent + (int64_t)j * a.stride + sdisp[lo] + (int64_t)(o - spfx[lo]) * W;
+                v[u] = *reinterpret_cast<const S *>(PACK ? mp[u] : a.packed + (size_t)i * W);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kUnitU; ++u) {
+            if (mp[u]) {
+                const uint32_t i = base + (uint32_t)u * tpb;
+                *reinterpret_cast<S *>(PACK ? a.packed + (size_t)i * W : mp[u]) = v[u];
+                if constexpr (CSUM) acc += slot_csum<W>(v[u], a.first + i);
+            }
+        }
+    }
+    if constexpr (CSUM) block_sum_store(acc, csum);
+}
+
+template <bool PACK, bool CSUM>
+static void launch_units_w(int w, const UnitArgs &a, unsigned blocks, size_t lds, const CsumSink &part, hipStream_t s)
+{
+    switch (w) {
+    case 16: hipLaunchKernelGGL((k_ddt_units<PACK, CSUM, 16>), dim3(blocks), dim3(256), lds, s, a, part); break;
+    case 8: hipLaunchKernelGGL((k_ddt_units<PACK, CSUM, 8>), dim3(blocks), dim3(256), lds, s, a, part); break;
+    case 4: hipLaunchKernelGGL((k_ddt_units<PACK, CSUM, 4>), dim3(blocks), dim3(256), lds, s, a, part); break;
+    case 2: hipLaunchKernelGGL((k_ddt_units<PACK, CSUM, 2>), dim3(blocks), dim3(256), lds, s, a, part); break;
+    default: hipLaunchKernelGGL((k_ddt_units<PACK, CSUM, 1>), dim3(blocks), dim3(256), lds, s, a, part); break;
+    }
+}
+
+// returns 1 when the unit kernel does not apply
+static int launch_ddt_units(const DdtDev &d, bool pack, void *mem, void *packed, int64_t pos, int64_t bytes,
+                            unsigned *csum, hipStream_t s)
+{
+    if (ddt_tune().rows < 2 || d.nruns > kUnitMaxRuns || d.nruns < 1 || d.blk_bytes <= 0) return 1;
+    const uint64_t bits = d.run_bits | (uint64_t)d.stride | (uint64_t)d.extent | (uintptr_t)mem | (uintptr_t)packed |
+                          (uint64_t)pos | (uint64_t)bytes | (uint64_t)d.blk_bytes;
+    int w = 16, lw = 4;
+    while (w > 1 && (bits & (uint64_t)(w - 1))) {
+        w >>= 1;
+        --lw;
+    }
+    const int64_t last = (pos + bytes) / w;
+    if (last >= ((int64_t)1 << 32) || d.inst_bytes / w >= ((int64_t)1 << 32) || d.nblk >= ((int64_t)1 << 32)) return 1;
+    UnitArgs a;
+    a.mem = static_cast<char *>(mem);
+    a.packed = static_cast<char *>(packed);
+    a.disp = d.disp;
+    a.pfx = d.pfx;
+    a.nruns = d.nruns;
+    a.lw = lw;
+    a.stride = d.stride;
+    a.extent = d.extent;
+    a.per_inst = make_fastdiv((uint32_t)(d.inst_bytes / w));
+    a.per_blk = make_fastdiv((uint32_t)(d.blk_bytes / w));
+    a.first = (uint32_t)(pos / w);
+    a.nunits = (uint32_t)(bytes / w);
+    const uint64_t per = 256u * kUnitU;
+    uint64_t blocks = (a.nunits + per - 1) / per;
+    const uint64_t cap = (uint64_t)8 * (uint64_t)device_cu_count();
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) blocks = 1;
+    const size_t lds = (size_t)d.nruns * (sizeof(int64_t) + sizeof(uint32_t));
+    Csum part;
+    int rc = part.get(csum, (unsigned)blocks);
+    if (rc) return rc;
+    if (pack) {
+        if (csum) launch_units_w<true, true>(w, a, (unsigned)blocks, lds, part.sink, s);
+        else launch_units_w<true, false>(w, a, (unsigned)blocks, lds, part.sink, s);
+    } else {
+        if (csum) launch_units_w<false, true>(w, a, (unsigned)blocks, lds, part.sink, s);
+        else launch_units_w<false, false>(w, a, (unsigned)blocks, lds, part.sink, s);
+    }
+    MI_HIP(hipGetLastError());
+    return part.finish(csum, s);
+}
+
 int launch_ddt(const DdtDev &d, bool pack, void *mem, void *packed, int64_t pos, int64_t bytes, unsigned *csum,
                hipStream_t s)
 {
     if (bytes <= 0) return MI355X_SUCCESS;
+    const int urc = launch_ddt_units(d, pack, mem, packed, pos, bytes, csum, s);
+    if (urc != 1) return urc;
     const int64_t slots = ((pos + bytes + 15) >> 4) - (pos >> 4);
     size_t blocks = (size_t)((slots + 255) / 256);
     const size_t cap = (size_t)8 * (size_t)device_cu_count();

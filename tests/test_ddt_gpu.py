@@ -256,3 +256,100 @@ def test_upper_500_gpu(gpu, pkg):
     d.pack(1, mat2.data_ptr(), 0, out.data_ptr(), nbytes)
     assert torch.equal(out, inbuf)
     d.destroy()
+
+
+NARROW = [  # (vector args, count): the widest slot every address allows
+    ((5001, 1, 3, 8), 2),    # a column of doubles: 8-B runs, 24-B stride -> 8-B slots
+    ((1001, 2, 3, 8), 3),    # 16-B runs at a 24-B stride -> 8-B slots
+    ((3001, 3, 5, 4), 2),    # 3-float blocks -> 4-B slots
+    ((2001, 3, 4, 2), 3),    # 6-B runs -> 2-B slots
+    ((1001, 5, 7, 1), 3),    # 5-B runs -> 1-B slots
+]
+
+
+@pytest.mark.parametrize("case", range(len(NARROW)))
+def test_narrow_row_slots(gpu, pkg, oracle, case):
+    """the row kernel with 8/4/2/1-byte slots (mode 2) against the oracle: packed stream, unpacked
+    bytes and the per-window checksums (additive to the whole message's), windows cut at multiples
+    of the element size and at odd bytes; modes 1 (16-B slots only) and 0 (general kernel) give
+    the same bytes"""
+    torch = gpu
+    args, count = NARROW[case]
+    d, od = pkg.Ddt.vector(*args), oracle.oracle_ddt_vector(*args)
+    total = count * oracle.oracle_ddt_size(od)
+    span = (count - 1) * oracle.oracle_ddt_extent(od) + oracle.oracle_ddt_extent(od) + 64
+    rng = np.random.default_rng(40 + case)
+    base = rng.integers(0, 256, span, dtype=np.uint8)
+    dbase = _dev(torch, base)
+    full = np.zeros(total, dtype=np.uint8)
+    want_cs = oracle.oracle_ddt_pack_checksum(od, count, base.ctypes.data, full.ctypes.data)
+    want_mem = np.zeros(span, dtype=np.uint8)
+    oracle.oracle_ddt_unpack(od, count, want_mem.ctypes.data, 0, full.ctypes.data, total)
+    esz = args[3]
+    cuts = sorted(set([0, total] + [int(x) // esz * esz for x in rng.integers(0, total, 6)] +
+                      [int(x) for x in rng.integers(0, total, 2)]))
+    try:
+        for mode in (2, 1, 0):
+            pkg.ddt_tune_rows(mode)
+            out = torch.zeros(total + 64, dtype=torch.uint8, device="cuda")
+            cs = 0
+            for a, b in zip(cuts[:-1], cuts[1:]):
+                # packed windows at their stream offset (alignment = the window's own)
+                cs += d.pack(count, dbase.data_ptr(), a, out.data_ptr() + a, b - a, checksum=True)
+            assert np.array_equal(out[:total].cpu().numpy(), full), mode
+            assert cs % 2**32 == want_cs, (mode, cs, want_cs)
+            z = torch.zeros(span, dtype=torch.uint8, device="cuda")
+            cs = 0
+            for a, b in zip(cuts[:-1], cuts[1:]):
+                cs += d.unpack(count, z.data_ptr(), a, out.data_ptr() + a, b - a, checksum=True)
+            assert np.array_equal(z.cpu().numpy(), want_mem), mode
+            assert cs % 2**32 == want_cs, mode
+    finally:
+        pkg.ddt_tune_rows(2)
+
+
+UNIT_CASES = [  # run lists (several runs per block): (blocklens, disps, elem size, count)
+    ([int(100 - i) for i in range(100)], [int(101 * i) for i in range(100)], 8, 2),  # upper triangle of 100x100 doubles
+    ([1, 3, 2, 7, 1, 1, 4], [0, 2, 9, 13, 25, 27, 40], 4, 300),
+    ([3, 1, 5, 2], [1, 6, 9, 17], 2, 500),
+    ([2, 5, 1], [0, 4, 13], 1, 900),
+]
+
+
+@pytest.mark.parametrize("case", range(len(UNIT_CASES)))
+def test_unit_kernel(gpu, pkg, oracle, case):
+    """the unit kernel (run tables staged in LDS, W-byte units) against the oracle for indexed run
+    lists, windows at element multiples and at odd bytes, with checksums; mode 0 (the general
+    kernel) gives the same bytes"""
+    torch = gpu
+    bl, dp, esz, count = UNIT_CASES[case]
+    n = len(bl)
+    d = pkg.Ddt.indexed(bl, dp, esz)
+    od = oracle.oracle_ddt_indexed(n, (ctypes.c_int * n)(*bl), (ctypes.c_int * n)(*dp), esz)
+    total = count * oracle.oracle_ddt_size(od)
+    assert d.size * count == total
+    span = count * oracle.oracle_ddt_extent(od) + 64
+    rng = np.random.default_rng(60 + case)
+    base = rng.integers(0, 256, span, dtype=np.uint8)
+    dbase = _dev(torch, base)
+    full = np.zeros(total, dtype=np.uint8)
+    want_cs = oracle.oracle_ddt_pack_checksum(od, count, base.ctypes.data, full.ctypes.data)
+    want_mem = np.zeros(span, dtype=np.uint8)
+    oracle.oracle_ddt_unpack(od, count, want_mem.ctypes.data, 0, full.ctypes.data, total)
+    cuts = sorted(set([0, total] + [int(x) // esz * esz for x in rng.integers(0, total, 6)] +
+                      [int(x) for x in rng.integers(0, total, 2)]))
+    try:
+        for mode in (2, 0):
+            pkg.ddt_tune_rows(mode)
+            out = torch.zeros(total + 64, dtype=torch.uint8, device="cuda")
+            cs = sum(d.pack(count, dbase.data_ptr(), a, out.data_ptr() + a, b - a, checksum=True)
+                     for a, b in zip(cuts[:-1], cuts[1:]))
+            assert np.array_equal(out[:total].cpu().numpy(), full), mode
+            assert cs % 2**32 == want_cs, mode
+            z = torch.zeros(span, dtype=torch.uint8, device="cuda")
+            cs = sum(d.unpack(count, z.data_ptr(), a, out.data_ptr() + a, b - a, checksum=True)
+                     for a, b in zip(cuts[:-1], cuts[1:]))
+            assert np.array_equal(z.cpu().numpy(), want_mem), mode
+            assert cs % 2**32 == want_cs, mode
+    finally:
+        pkg.ddt_tune_rows(2)

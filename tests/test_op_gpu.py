@@ -190,3 +190,31 @@ def test_tune_variants_same_result(gpu, pkg):
         pkg.tune(*saved)
         pkg.set_mode(mode)
         pkg.set_threads(1024)
+
+
+def test_max_mpi_count(gpu, pkg):
+    """The largest count an MPI call can pass (INT_MAX elements, `int *count` in op.h:253-266):
+    int8 SUM (wraps, 2 GiB - 1 byte per operand: byte offsets past 2^31) and fp32 SUM (8 GiB per
+    operand: offsets past 2^32), 3-buff and 2-buff, against torch's own wrapping / exact add."""
+    torch = gpu
+    n = 2**31 - 1
+    s = torch.cuda.current_stream().cuda_stream
+    a = torch.randint(-128, 128, (n,), device="cuda", dtype=torch.int8)
+    b = torch.randint(-128, 128, (n,), device="cuda", dtype=torch.int8)
+    o = torch.empty_like(a)
+    pkg.op_reduce_3buff(pkg.OP["SUM"], pkg.T["INT8"], a.data_ptr(), b.data_ptr(), o.data_ptr(), n, s)
+    torch.cuda.synchronize()
+    assert torch.equal(o, a + b)
+    pkg.op_reduce(pkg.OP["SUM"], pkg.T["INT8"], a.data_ptr(), b.data_ptr(), n, s)  # b = b + a
+    torch.cuda.synchronize()
+    assert torch.equal(o, b)
+    del a, b, o
+    torch.cuda.empty_cache()
+    a = torch.randint(-1000, 1000, (n,), device="cuda", dtype=torch.int16).float()
+    b = torch.randint(-1000, 1000, (n,), device="cuda", dtype=torch.int16).float()
+    o = torch.empty_like(a)
+    pkg.op_reduce_3buff(pkg.OP["SUM"], pkg.T["FLOAT"], a.data_ptr(), b.data_ptr(), o.data_ptr(), n, s)
+    torch.cuda.synchronize()
+    assert torch.equal(o, a + b)
+    del a, b, o
+    torch.cuda.empty_cache()

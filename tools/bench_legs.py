@@ -150,6 +150,75 @@ def leg_ddt(pkg, torch, args, emit, oracle):
         oracle.oracle_ddt_free(od)
 
 
+def leg_ddt_narrow(pkg, torch, args, emit):
+    """vector layouts whose runs are not 16-B multiples (a column of doubles, 3-float blocks),
+    256 MiB packed: the row kernel with narrow slots (mi355x_ddt_tune_rows 2) vs the general
+    kernel (0) vs torch's strided copy of the same view.  alg_bytes = 2 x packed; the strided side
+    moves whole 128-B lines, so a column's reads cost 2 x its packed bytes of HBM traffic."""
+    cases = [("vector(2^25,1,2,DOUBLE)", (1 << 25, 1, 2, 8), torch.float64, 2, 1),
+             ("vector(22369621,3,4,FLOAT)", (22369621, 3, 4, 4), torch.float32, 4, 3)]
+    for name, vargs, dt, width, take in cases:
+        d = pkg.Ddt.vector(*vargs)
+        x = torch.randn(vargs[0], width, device="cuda", dtype=dt)
+        p = torch.empty(vargs[0], take, device="cuda", dtype=dt)
+        y = torch.zeros_like(x)
+        size = d.size
+        alg = 2 * size
+        for mode in (2, 0):
+            pkg.ddt_tune_rows(mode)
+            for dirn, fn in (("pack", lambda s: d.pack(1, x.data_ptr(), 0, p.data_ptr(), size, s)),
+                             ("unpack", lambda s: d.unpack(1, y.data_ptr(), 0, p.data_ptr(), size, s))):
+                avg, med = timed(torch, fn, args.steps, args.warmup)
+                emit({"leg": "ddt_narrow_" + dirn, "type": name, "kernel": "rows" if mode == 2 else "general",
+                      "alg_bytes": alg, "kernel_avg_ms": round(avg, 5), "kernel_med_ms": round(med, 5),
+                      "achieved_GBs": round(alg / (avg * 1e-3) / 1e9, 1),
+                      "frac": round(alg / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+            assert torch.equal(p, x[:, :take]) and torch.equal(y[:, :take], x[:, :take]), (name, mode)
+            y.zero_()
+        pkg.ddt_tune_rows(2)
+        for dirn, fn in (("pack", lambda s: p.copy_(x[:, :take])), ("unpack", lambda s: y[:, :take].copy_(p))):
+            avg, _ = timed(torch, fn, args.steps, args.warmup)
+            emit({"leg": "torch_strided_ref_" + dirn, "type": name, "alg_bytes": alg, "kernel_avg_ms": round(avg, 5),
+                  "achieved_GBs": round(alg / (avg * 1e-3) / 1e9, 1)})
+        del x, p, y
+
+
+def leg_ddt_runs(pkg, torch, args, emit):
+    """run-list layouts (several runs per block), 256 MiB packed: the unit kernel (LDS-staged run
+    tables; mi355x_ddt_tune_rows 2) vs the general kernel (0).  Upper triangle of a 256 x 256
+    double matrix (indexed, 256 runs per instance) and a 7-run indexed float layout."""
+    import numpy as np
+    tri_bl = [256 - i for i in range(256)]
+    tri_dp = [257 * i for i in range(256)]
+    f7_bl, f7_dp = [1, 3, 2, 7, 1, 1, 4], [0, 2, 9, 13, 25, 27, 40]
+    cases = [("indexed upper-triangle 256x256 DOUBLE", tri_bl, tri_dp, 8),
+             ("indexed 7 runs of FLOAT (19 of 44 elements)", f7_bl, f7_dp, 4)]
+    for name, bl, dp, esz in cases:
+        d = pkg.Ddt.indexed(bl, dp, esz)
+        ext = (max(a + b for a, b in zip(dp, bl)) - min(dp)) * esz
+        count = (256 << 20) // d.size
+        x = torch.randint(0, 255, (count * ext,), dtype=torch.uint8, device="cuda")
+        p = torch.empty(count * d.size, dtype=torch.uint8, device="cuda")
+        y = torch.zeros_like(x)
+        size = count * d.size
+        alg = 2 * size
+        outs = {}
+        for mode in (2, 0):
+            pkg.ddt_tune_rows(mode)
+            for dirn, fn in (("pack", lambda s: d.pack(count, x.data_ptr(), 0, p.data_ptr(), size, s)),
+                             ("unpack", lambda s: d.unpack(count, y.data_ptr(), 0, p.data_ptr(), size, s))):
+                avg, med = timed(torch, fn, args.steps, args.warmup)
+                emit({"leg": "ddt_runs_" + dirn, "type": name, "kernel": "units" if mode == 2 else "general",
+                      "count": count, "alg_bytes": alg, "kernel_avg_ms": round(avg, 5), "kernel_med_ms": round(med, 5),
+                      "achieved_GBs": round(alg / (avg * 1e-3) / 1e9, 1),
+                      "frac": round(alg / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+            outs[mode] = (p.clone(), y.clone())
+            y.zero_()
+        assert torch.equal(outs[2][0], outs[0][0]) and torch.equal(outs[2][1], outs[0][1]), name
+        pkg.ddt_tune_rows(2)
+        del x, p, y, outs
+
+
 def leg_cpu_allreduce(args, emit, oracle):
     """BASELINE configs[0]: the reference CPU path (coll/tuned segmented ring over sm-BTL-style
     32 KiB shared-memory fragments), 4 ranks on 4 distinct host cores, MPI_SUM MPI_FLOAT 16 M
@@ -202,7 +271,7 @@ def main():
     import bench
     pkg = bench.load_pkg()
     torch = None
-    if "op" in legs or "ddt" in legs:
+    if "op" in legs or any(l.startswith("ddt") for l in legs):
         import torch
         pkg.rt()
     oracle = None
@@ -225,6 +294,10 @@ def main():
         leg_op(pkg, torch, args, emit)
     if "ddt" in legs:
         leg_ddt(pkg, torch, args, emit, oracle)
+    if "ddt_narrow" in legs:
+        leg_ddt_narrow(pkg, torch, args, emit)
+    if "ddt_runs" in legs:
+        leg_ddt_runs(pkg, torch, args, emit)
     if "cpu_ar" in legs:
         leg_cpu_allreduce(args, emit, oracle)
     fh.close()
