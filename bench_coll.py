@@ -65,13 +65,18 @@ def extra_legs(args, pkg, torch, comm, world, rank, dev, legs, key):
                "busbw_GBs": round(nbytes / sec * 2 * (world - 1) / world / 1e9, 3),
                "exact": bool(torch.all(y == want).item())}
         if nbytes <= (1 << 20):
-            # both data flows at this size, for the LL threshold: one-shot LL vs host-synchronised
-            for name, llmax in (("us_ll", 1 << 20), ("us_host", 0)):
+            # every data flow at this size, for the thresholds: one-shot LL, host-synchronised with
+            # ring orders in one phase (k_ring_all, below ONE_PHASE_MAX_BYTES) and in two
+            one_phase = comm.get("ONE_PHASE_MAX_BYTES")
+            for name, llmax, op1 in (("us_ll", 1 << 20, one_phase), ("us_host", 0, 1 << 20),
+                                     ("us_host_2phase", 0, 0)):
                 comm.set("LL_MAX_BYTES", llmax)
+                comm.set("ONE_PHASE_MAX_BYTES", op1)
                 y.zero_()
                 row[name] = round(_timed(dist, torch, run, reps, 2) * 1e6, 2)
                 row["exact"] = row["exact"] and bool(torch.all(y == want).item())
-            comm.set("LL_MAX_BYTES", 0)  # the default
+            comm.set("LL_MAX_BYTES", 0)  # the defaults
+            comm.set("ONE_PHASE_MAX_BYTES", one_phase)
         sweep.append(row)
         del x, y
     legs["allreduce_sweep_f32"] = sweep

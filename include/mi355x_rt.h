@@ -142,9 +142,14 @@ enum mi355x_knob {
     MI355X_KNOB_PIPE_WG_PER_CU = 14,    /* pipelined allreduce: 256-thread workgroups per CU (1..8, default 2) */
     MI355X_KNOB_PIPE_CHUNK_KIB = 15,    /* pipelined allreduce: chunk size in KiB (0 = auto: ~512 chunks
                                            per ring block, at least 64 KiB) */
-    MI355X_KNOB_PIPE_WT = 16            /* pipelined allreduce: 1 (default) = fold results stored write-
+    MI355X_KNOB_PIPE_WT = 16,           /* pipelined allreduce: 1 (default) = fold results stored write-
                                            through (system-coherent policy) and pulled with coherent
                                            loads, no per-chunk L2 write-back / invalidate; 0 = fences */
+    MI355X_KNOB_ONE_PHASE_MAX_BYTES = 17 /* ring-ordered allreduce (not in place) up to this many bytes
+                                           per rank: every rank evaluates every ring block from the n
+                                           inputs in one launch (reads n x S, one host barrier and
+                                           stream sync fewer than the two phases); default 1 MiB,
+                                           0 = always two phases */
 };
 int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
 /* current value of a knob (LL_MAX_BYTES reads 0 when the creation-time LL self-test failed) */

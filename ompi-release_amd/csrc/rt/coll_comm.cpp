@@ -1575,6 +1575,7 @@ int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
     case MI355X_KNOB_PIPE_WG_PER_CU: *value = coll_tune().pipe_wg_per_cu; break;
     case MI355X_KNOB_PIPE_CHUNK_KIB: *value = coll_tune().pipe_chunk_kib; break;
     case MI355X_KNOB_PIPE_WT: *value = coll_tune().pipe_wt; break;
+    case MI355X_KNOB_ONE_PHASE_MAX_BYTES: *value = (long)coll_tune().one_phase_max; break;
     default: return set_error(MI355X_ERR_ARG, "unknown knob %d", knob);
     }
     return MI355X_SUCCESS;
@@ -1624,6 +1625,10 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
         coll_tune().pipe_chunk_kib = (int)value;
         break;
     case MI355X_KNOB_PIPE_WT: coll_tune().pipe_wt = value != 0; break;
+    case MI355X_KNOB_ONE_PHASE_MAX_BYTES:
+        if (value < 0 || value > (1l << 30)) return set_error(MI355X_ERR_ARG, "one_phase_max_bytes out of range");
+        coll_tune().one_phase_max = (size_t)value;
+        break;
     case MI355X_KNOB_TIME_PHASES:
         c->time_phases = value != 0;
         if (c->time_phases && !c->tev[0]) {
@@ -1770,6 +1775,26 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
             if (rc) return rc;
             return finish(c, s);
         }
+    }
+    if (ring && sbuf && sbuf != rbuf && !staged && !coll_tune().push && count * esz <= coll_tune().one_phase_max &&
+        count <= 0xffffffffull) {
+        // small ring-ordered messages: every rank evaluates every block from the n inputs (reads
+        // n x S, writes only its own rbuf) -- one launch and one barrier, like the tree orders
+        RingAllArgs ra;
+        std::memset(&ra, 0, sizeof(ra));
+        for (int q = 0; q < c->size; ++q) ra.src[q] = P[0][q];
+        ra.dst = rbuf;
+        ra.n = c->size;
+        size_t o1, l0, l1;
+        ring_block(count, c->size, 0, &o1, &l0);
+        ring_block(count, c->size, c->size - 1, &o1, &l1);
+        ra.count = (uint32_t)count;
+        ra.early = (uint32_t)l0;
+        ra.late = (uint32_t)(l1 ? l1 : 1);
+        ra.split = (uint32_t)(count % (size_t)c->size);
+        rc = launch_ring_all_slot(op, type, ra, s);
+        if (rc) return rc;
+        return finish(c, s);
     }
     // owner-computes: rank r evaluates ring block r (the reference's block partition, so the
     // ring's per-block order is one program per launch)

@@ -38,6 +38,16 @@ struct TreeArgs {
     size_t n;
 };
 
+// k_ring_all: the ring allreduce's per-element order over the WHOLE vector in one launch -- element
+// i of ring block b folds x_b, x_{b+1}, ..., x_{b+n-1} with the partial as the `in` operand
+// (coll_tuned_allreduce.c:470-512); block b = the reference partition (coll_tuned.h:546-552)
+struct RingAllArgs {
+    const void *src[kMaxRanks];  // every rank's input (vector base)
+    void *dst;                   // my rbuf
+    int n;
+    uint32_t count, early, late, split;  // elements; the first `split` blocks hold `early` elements
+};
+
 // k_copy: bytes from one source to nd destinations
 struct CopyArgs {
     const void *src;
@@ -136,10 +146,17 @@ struct CollTune {
     // pipelined allreduce: publish chunks write-through instead of L2 write-back + invalidate fences
     // (faster at every n measured: rehearsal n = 8 3.85 vs 4.69 ms, n = 4 2.03 vs 2.29)
     int pipe_wt = 1;
+    // ring-ordered allreduce up to this many bytes per rank in one phase (k_ring_all); beyond it
+    // the n-fold reads outweigh the host barrier + stream sync the second phase costs: a rank reads
+    // (n-1) S over n-1 links instead of 2 (n-1) S / n, i.e. S (1 - 2/n) more per link, against
+    // ~17 us saved (one-GPU rehearsal, n = 2: 64 KiB 18.4 vs 34.7 us, 1 MiB 18.6 vs 35.8 us) --
+    // break-even near 1.7 MB at n = 8 with 76.8 GB/s per link and direction
+    size_t one_phase_max = (size_t)1 << 20;
 };
 CollTune &coll_tune();
 
 int launch_fold_slot(int op, int type, const FoldArgs &a, hipStream_t s);
+int launch_ring_all_slot(int op, int type, const RingAllArgs &a, hipStream_t s);
 int launch_tree_slot(int op, int type, const TreeArgs &a, hipStream_t s);
 int launch_copy(CopyArgs a, hipStream_t s);
 int launch_multicopy(MultiCopyArgs a, hipStream_t s);

@@ -173,6 +173,32 @@ __global__ __launch_bounds__(256) void k_fold(FoldArgs a)
     }
 }
 
+// ------------------------------------------------------------------ ring order, whole vector
+// Small ring-ordered messages: every rank evaluates every block (one element per lane, the n loads
+// issued before the fold), so the allreduce needs one launch and one host barrier instead of two.
+template <class F> __global__ __launch_bounds__(256) void k_ring_all(RingAllArgs a)
+{
+    using T = typename F::T;
+    const uint32_t se = a.split * a.early;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.count; i += gridDim.x * blockDim.x) {
+        const int b = (int)(i < se ? i / a.early : a.split + (i - se) / a.late);
+        T acc{};
+        for (int j0 = 0; j0 < a.n; j0 += kFoldChunk) {  // up to 8 loads in flight, then fold them
+            T x[kFoldChunk];
+#pragma unroll
+            for (int j = 0; j < kFoldChunk; ++j) {
+                const int jj = j0 + j, r = b + jj < a.n ? b + jj : b + jj - a.n;
+                if (jj < a.n) x[j] = static_cast<const T *>(a.src[r])[i];
+            }
+#pragma unroll
+            for (int j = 0; j < kFoldChunk; ++j) {
+                if (j0 + j < a.n) acc = (j0 + j == 0) ? x[0] : F::op2(x[j], acc);
+            }
+        }
+        static_cast<T *>(a.dst)[i] = acc;
+    }
+}
+
 // ------------------------------------------------------------------ tree program
 template <class F>
 __device__ __forceinline__ typename F::T pick(const typename F::T (&R)[kTreeMax], int k)
@@ -314,6 +340,14 @@ template <class F> static int launch_fold(FoldArgs a, hipStream_t s)
     return MI355X_SUCCESS;
 }
 
+template <class F> static int launch_ring_all(const RingAllArgs &a, hipStream_t s)
+{
+    if (a.count == 0) return MI355X_SUCCESS;
+    hipLaunchKernelGGL((k_ring_all<F>), dim3((unsigned)grid_for(a.count, 8)), dim3(256), 0, s, a);
+    MI_HIP(hipGetLastError());
+    return MI355X_SUCCESS;
+}
+
 template <class F> static int launch_tree(const TreeArgs &a, hipStream_t s)
 {
     if (a.n == 0) return MI355X_SUCCESS;
@@ -377,6 +411,7 @@ int launch_multicopy(MultiCopyArgs a, hipStream_t s)
 struct CollSlot {
     int (*fold)(FoldArgs, hipStream_t) = nullptr;
     int (*tree)(const TreeArgs &, hipStream_t) = nullptr;
+    int (*ring_all)(const RingAllArgs &, hipStream_t) = nullptr;
 };
 
 struct CollTable {
@@ -387,6 +422,7 @@ struct CollTable {
             using F = typename decltype(tag)::type;
             s[op][ty].fold = &launch_fold<F>;
             s[op][ty].tree = &launch_tree<F>;
+            s[op][ty].ring_all = &launch_ring_all<F>;
         });
     }
 };
@@ -404,6 +440,13 @@ int launch_fold_slot(int op, int type, const FoldArgs &a, hipStream_t s)
     const CollSlot *sl = cslot(op, type);
     if (!sl) return set_error(MI355X_ERR_UNSUPPORTED, "no device fold for op %d type %d", op, type);
     return sl->fold(a, s);
+}
+
+int launch_ring_all_slot(int op, int type, const RingAllArgs &a, hipStream_t s)
+{
+    const CollSlot *sl = cslot(op, type);
+    if (!sl) return set_error(MI355X_ERR_UNSUPPORTED, "no device ring fold for op %d type %d", op, type);
+    return sl->ring_all(a, s);
 }
 
 int launch_tree_slot(int op, int type, const TreeArgs &a, hipStream_t s)

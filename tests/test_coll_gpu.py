@@ -604,3 +604,35 @@ def test_phase_timing(gpu, pkg, comms):
         c.set("TIME_PHASES", 0)
         assert 0.0 < p1 < 1000.0 and 0.0 < p2 < 1000.0, (p1, p2)
         assert bool(torch.all(ys[r] == 3.0))
+
+
+@pytest.mark.parametrize("n", [3, 5, 8])
+def test_one_phase_ring(gpu, pkg, oracle, comms, n):
+    """ring-ordered allreduce below ONE_PHASE_MAX_BYTES: every rank evaluates every ring block
+    (k_ring_all) -- bit-exact with the oracle's ring and with the two-phase flow (knob 0), on
+    order-sensitive data, ragged block partitions (count % n != 0) included"""
+    torch = gpu
+    cs = comms(n)
+    for c in cs:
+        c.set("ALLREDUCE_ALG", 4)
+    try:
+        for opname, tname in (("SUM", "FLOAT"), ("PROD", "C_DOUBLE_COMPLEX"), ("MAXLOC", "DOUBLE_INT")):
+            op, ty = pkg.OP[opname], pkg.T[tname]
+            for count in (n, 3 * n + 1, 10_007, (200 << 10) // pkg.type_size(ty) + n - 1):
+                xs = [opdata.make(tname, count, 7000 + 13 * n + r) for r in range(n)]
+                outs = [np.zeros_like(xs[0]) for _ in range(n)]
+                assert oracle.oracle_allreduce(4, n, count, ty, op, 0, _ptrs(xs), _ptrs(outs)) == 4
+                dx = [to_dev(torch, x) for x in xs]
+                for one_phase in (1 << 20, 0):
+                    cs[0].set("ONE_PHASE_MAX_BYTES", one_phase)
+                    dr = [torch.zeros_like(t) for t in dx]
+                    torch.cuda.synchronize()
+                    run_ranks(n, lambda r: cs[r].allreduce(dx[r].data_ptr(), dr[r].data_ptr(), count, ty, op))
+                    torch.cuda.synchronize()
+                    for r in range(n):
+                        opdata.assert_same(tname, opname, from_dev(dr[r], outs[r]), outs[r],
+                                           f"ring n={n} count={count} one_phase={one_phase} rank={r}")
+    finally:
+        cs[0].set("ONE_PHASE_MAX_BYTES", 1 << 20)
+        for c in cs:
+            c.set("ALLREDUCE_ALG", 0)
