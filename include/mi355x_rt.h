@@ -145,7 +145,9 @@ enum mi355x_knob {
     MI355X_KNOB_PIPE_WT = 16,           /* pipelined allreduce: 1 (default) = fold results stored write-
                                            through (system-coherent policy) and pulled with coherent
                                            loads, no per-chunk L2 write-back / invalidate; 0 = fences */
-    MI355X_KNOB_ONE_PHASE_MAX_BYTES = 17 /* ring-ordered allreduce (not in place) up to this many bytes
+    MI355X_KNOB_ONE_PHASE_MAX_BYTES = 17 /* (per communicator, same value on every rank; env
+                                           MI355X_ONE_PHASE_MAX_BYTES at creation) ring-ordered
+                                           allreduce (not in place) up to this many bytes
                                            per rank: every rank evaluates every ring block from the n
                                            inputs in one launch (reads n x S, one host barrier and
                                            stream sync fewer than the two phases); default 1 MiB,

@@ -1466,6 +1466,7 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     // pipelined allreduce by default from 4 ranks up: ahead of the two-phase flow at n = 4 and 8,
     // behind at n = 2 in the one-GPU rehearsal (profiles/r02_bench_n{2,4,8}_*); MI355X_PIPE=0/1 decides
     c->pipe_on = env_double("MI355X_PIPE", size >= 4 ? 1.0 : 0.0) != 0.0;
+    c->one_phase_max = (size_t)std::max(0.0, env_double("MI355X_ONE_PHASE_MAX_BYTES", (double)c->one_phase_max));
     if (rc == MI355X_SUCCESS && size > 1) rc = ll_selftest(c);
     if (rc) {
         mi355x_comm_destroy(c);
@@ -1575,7 +1576,7 @@ int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
     case MI355X_KNOB_PIPE_WG_PER_CU: *value = coll_tune().pipe_wg_per_cu; break;
     case MI355X_KNOB_PIPE_CHUNK_KIB: *value = coll_tune().pipe_chunk_kib; break;
     case MI355X_KNOB_PIPE_WT: *value = coll_tune().pipe_wt; break;
-    case MI355X_KNOB_ONE_PHASE_MAX_BYTES: *value = (long)coll_tune().one_phase_max; break;
+    case MI355X_KNOB_ONE_PHASE_MAX_BYTES: *value = (long)c->one_phase_max; break;
     default: return set_error(MI355X_ERR_ARG, "unknown knob %d", knob);
     }
     return MI355X_SUCCESS;
@@ -1627,7 +1628,7 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
     case MI355X_KNOB_PIPE_WT: coll_tune().pipe_wt = value != 0; break;
     case MI355X_KNOB_ONE_PHASE_MAX_BYTES:
         if (value < 0 || value > (1l << 30)) return set_error(MI355X_ERR_ARG, "one_phase_max_bytes out of range");
-        coll_tune().one_phase_max = (size_t)value;
+        c->one_phase_max = (size_t)value;
         break;
     case MI355X_KNOB_TIME_PHASES:
         c->time_phases = value != 0;
@@ -1776,7 +1777,7 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
             return finish(c, s);
         }
     }
-    if (ring && sbuf && sbuf != rbuf && !staged && !coll_tune().push && count * esz <= coll_tune().one_phase_max &&
+    if (ring && sbuf && sbuf != rbuf && !staged && !coll_tune().push && count * esz <= c->one_phase_max &&
         count <= 0xffffffffull) {
         // small ring-ordered messages: every rank evaluates every block from the n inputs (reads
         // n x S, writes only its own rbuf) -- one launch and one barrier, like the tree orders

@@ -146,12 +146,6 @@ struct CollTune {
     // pipelined allreduce: publish chunks write-through instead of L2 write-back + invalidate fences
     // (faster at every n measured: rehearsal n = 8 3.85 vs 4.69 ms, n = 4 2.03 vs 2.29)
     int pipe_wt = 1;
-    // ring-ordered allreduce up to this many bytes per rank in one phase (k_ring_all); beyond it
-    // the n-fold reads outweigh the host barrier + stream sync the second phase costs: a rank reads
-    // (n-1) S over n-1 links instead of 2 (n-1) S / n, i.e. S (1 - 2/n) more per link, against
-    // ~17 us saved (one-GPU rehearsal, n = 2: 64 KiB 18.4 vs 34.7 us, 1 MiB 18.6 vs 35.8 us) --
-    // break-even near 1.7 MB at n = 8 with 76.8 GB/s per link and direction
-    size_t one_phase_max = (size_t)1 << 20;
 };
 CollTune &coll_tune();
 

@@ -228,6 +228,13 @@ struct mi355x_comm {
     uint64_t pipe_qbase = 0;                      // its value when the next launch starts
     uint64_t pipe_seq = 0;                        // calls of the pipelined flow so far
     int pipe_share = 1;                           // ranks of this communicator on my GPU (set at creation)
+    // ring-ordered allreduce up to this many bytes per rank in one phase (k_ring_all); beyond it
+    // the n-fold reads outweigh the host barrier + stream sync the second phase costs: a rank reads
+    // (n-1) S over n-1 links instead of 2 (n-1) S / n, i.e. S (1 - 2/n) more per link, against
+    // ~17 us saved (one-GPU rehearsal, n = 2: 64 KiB 18.4 vs 34.7 us, 1 MiB 18.6 vs 35.8 us) --
+    // break-even near 1.7 MB at n = 8 with 76.8 GB/s per link and direction
+    // (MI355X_KNOB_ONE_PHASE_MAX_BYTES, env MI355X_ONE_PHASE_MAX_BYTES)
+    size_t one_phase_max = (size_t)1 << 20;
     bool pipe_on = false;                         // MI355X_KNOB_PIPE (env MI355X_PIPE; default: size >= 4)
     uint64_t *pipe_dbg = nullptr;                 // MI355X_DEBUG: per-workgroup progress words
     // nonblocking collectives: one progress thread per communicator runs the posted calls in

@@ -624,7 +624,8 @@ def test_one_phase_ring(gpu, pkg, oracle, comms, n):
                 assert oracle.oracle_allreduce(4, n, count, ty, op, 0, _ptrs(xs), _ptrs(outs)) == 4
                 dx = [to_dev(torch, x) for x in xs]
                 for one_phase in (1 << 20, 0):
-                    cs[0].set("ONE_PHASE_MAX_BYTES", one_phase)
+                    for c in cs:  # per communicator: every rank must take the same flow
+                        c.set("ONE_PHASE_MAX_BYTES", one_phase)
                     dr = [torch.zeros_like(t) for t in dx]
                     torch.cuda.synchronize()
                     run_ranks(n, lambda r: cs[r].allreduce(dx[r].data_ptr(), dr[r].data_ptr(), count, ty, op))
@@ -633,6 +634,6 @@ def test_one_phase_ring(gpu, pkg, oracle, comms, n):
                         opdata.assert_same(tname, opname, from_dev(dr[r], outs[r]), outs[r],
                                            f"ring n={n} count={count} one_phase={one_phase} rank={r}")
     finally:
-        cs[0].set("ONE_PHASE_MAX_BYTES", 1 << 20)
         for c in cs:
+            c.set("ONE_PHASE_MAX_BYTES", 1 << 20)
             c.set("ALLREDUCE_ALG", 0)
