@@ -1852,7 +1852,8 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
 // and the forced algorithms of coll_tuned_reduce.c).  sbuf NULL = MPI_IN_PLACE (root only, input in
 // rbuf); rbuf is read on the root only.  The result of every element is the reference tree's
 // expression (linear / chain / pipeline / binary / binomial), evaluated:
-//   small  : LL one-shot, every rank pushes to the root, the root evaluates;
+//   small  : LL one-shot, every rank pushes to the root, the root evaluates (when enabled);
+//   <= one_phase_max: the root evaluates everything from the mapped inputs, one launch;
 //   large  : owner-computes -- rank r evaluates ring block r from the n inputs into its own
 //            memory, then the root pulls the blocks (each link carries 2 S/n, writes stay local);
 //   staged : (allocations >= ipc_max) the root evaluates everything through the staging buffers.
@@ -1908,6 +1909,17 @@ static int reduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t co
         std::vector<size_t> boff(c->size, 0), blen(c->size, 0);
         blen[root] = count;
         return staged_reduce(c, op, type, pr, in, boff, blen, am_root ? rbuf : nullptr, false, nullptr, s);
+    }
+    if (count * esz <= c->one_phase_max) {
+        // small messages: the root evaluates every element from the n inputs (one launch, reads
+        // only; in place at the root each lane reads its element of rbuf before writing it); the
+        // others wait in the closing barrier until the root is done with their inputs
+        if (am_root) {
+            std::vector<void *> d0(1, rbuf);
+            rc = run_program(op, type, pr, P[0], d0, 0, count, s);
+            if (rc) return rc;
+        }
+        return finish(c, s);
     }
     // phase 1: every rank evaluates its ring block from the n inputs into its own memory (the root
     // straight into rbuf); phase 2: the root pulls the other blocks (one segment per peer).  Only

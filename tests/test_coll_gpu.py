@@ -153,7 +153,8 @@ def test_segmented_ring_region(gpu, pkg, oracle, comms, n):
 @pytest.mark.parametrize("alg", [0, 1, 2, 3, 4, 5])
 def test_reduce(gpu, pkg, oracle, comms, n, alg):
     """MPI_Reduce: every tuned reduce tree (forced) and the decision, roots 0 and n-1, in place at
-    the root and not; non-roots pass no rbuf"""
+    the root and not; non-roots pass no rbuf; small messages in one phase (the root evaluates
+    everything) and, with ONE_PHASE_MAX_BYTES 0, owner-computes + pull"""
     torch = gpu
     cs = comms(n)
     oracle.oracle_reduce.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
@@ -163,7 +164,9 @@ def test_reduce(gpu, pkg, oracle, comms, n, alg):
     try:
         for opname, tname in CASES[:6]:
             op, ty = pkg.OP[opname], pkg.T[tname]
-            for count in (1, 7, 40_001):
+            for count, one_phase in ((1, 1 << 20), (7, 1 << 20), (40_001, 1 << 20), (40_001, 0)):
+                for c in cs:
+                    c.set("ONE_PHASE_MAX_BYTES", one_phase)
                 xs = [opdata.make(tname, count, 800 + r) for r in range(n)]
                 for root in (0, n - 1):
                     want = np.zeros_like(xs[0])
@@ -186,6 +189,7 @@ def test_reduce(gpu, pkg, oracle, comms, n, alg):
     finally:
         for c in cs:
             c.set("REDUCE_ALG", 0)
+            c.set("ONE_PHASE_MAX_BYTES", 1 << 20)
 
 
 @pytest.mark.parametrize("n", [2, 3, 4, 8])
