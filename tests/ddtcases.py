@@ -88,6 +88,10 @@ def _f8():
     return ot.OpalType.basic("FLOAT8")
 
 
+def _ddt_pack_hindexed():
+    return ot.hindexed([10, 10], [0, 20 * 8], _f8()).commit()
+
+
 # (name, builder, count, chunks): every local_copy_with_convertor(pdt, count, chunk) of main()
 CONVERTOR_CASES = [
     ("contig_int1x10", lambda: ot.contiguous(10, ot.OpalType.basic("INT1")).commit(), 100, [956]),   # :350-354
@@ -108,6 +112,12 @@ CONVERTOR_CASES = [
     ("typeub_indexed", lambda: ot.typeub3()[1], 7, [6]),
     ("typeub_vector", lambda: ot.typeub3()[3], 5, [4]),
     ("test_struct", ot.test_struct, 33, [7]),
+    # test/datatype/ddt_pack.c:70-101: hindexed(2, {10, 10}, {0, 20 * sizeof(double)}, MPI_DOUBLE)
+    # and struct {11 x MPI_INT at 0, 2 x that hindexed at 64} -- the types whose descriptions it
+    # packs, moved here as data
+    ("ddt_pack_hindexed", lambda: _ddt_pack_hindexed(), 7, [12, 100, 956]),
+    ("ddt_pack_struct", lambda: ot.struct_([11, 2], [0, 64], [ot.OpalType.basic("INT4"), _ddt_pack_hindexed()]).commit(),
+     5, [12, 100, 956]),
 ]
 
 

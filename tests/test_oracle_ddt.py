@@ -240,3 +240,16 @@ def test_from_opal_matches_restated_types(pkg):
         assert (d.size, d.extent) == (t.size, t.extent)
         assert d.nruns <= len(t.runs())
         d.destroy()
+
+
+def test_ddt_pack_c_types():
+    """the types test/datatype/ddt_pack.c:70-101 builds: hindexed(2, {10, 10}, {0, 160 B},
+    MPI_DOUBLE) = 160 B of data over a 240-B extent; struct {11 x MPI_INT at 0, 2 x the hindexed at
+    64} = 44 + 320 B over [0, 544)"""
+    from ddtcases import _ddt_pack_hindexed
+    h = _ddt_pack_hindexed()
+    assert (h.size, h.lb, h.ub) == (160, 0, 240)
+    s = ot.struct_([11, 2], [0, 64], [ot.OpalType.basic("INT4"), h]).commit()
+    assert (s.size, s.lb, s.ub) == (364, 0, 544)
+    elems = ot.walk_desc(s)  # the convertor's visit order: 11 ints, then 2 x (10 + 10) doubles
+    assert sum(n for _, n in elems) == 364 and [a for a, _ in elems[:12]] == [4 * i for i in range(11)] + [64]
