@@ -25,6 +25,7 @@ import time
 REPO = pathlib.Path(__file__).resolve().parent
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 GIB = 1 << 30
+EV_EVERY = 4  # N = 1: HIP events around every 4th launch of the timed region
 
 
 def load_pkg():
@@ -119,16 +120,23 @@ def bench_op(args, pkg, torch):
     torch.cuda.synchronize()
     # parity spot-check of the measured kernel on the real size (size-independent property)
     assert torch.equal(o, a + b), "op/hip SUM result differs from a + b"
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # HIP events bracket every EV_EVERY-th launch of the timed region (k = 0, 4, 8, ...): an event
+    # pair around every launch adds ~7 us per step to the wall clock (0.500 vs 0.493 ms per step,
+    # tools/ev_probe.py), so the instrumentation samples the launches instead of perturbing them all
+    timed = [k for k in range(args.steps) if k % EV_EVERY == 0]
+    ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in timed}
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        ev[k][0].record(s)
+        e = ev.get(k)
+        if e:
+            e[0].record(s)
         pkg.op_reduce_3buff(op, ty, pa, pb, po, n, sh)
-        ev[k][1].record(s)
+        if e:
+            e[1].record(s)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kern_ms = [x.elapsed_time(y) for x, y in ev]
+    kern_ms = [x.elapsed_time(y) for x, y in ev.values()]
     avg_ms = sum(kern_ms) / len(kern_ms)
     alg_bytes = 3 * n * 4
     value = alg_bytes * args.steps / wall / 1e9
@@ -153,7 +161,8 @@ def bench_op(args, pkg, torch):
                                                                       "nontemporal": nt}},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel_avg_ms": round(avg_ms, 5), "alg_bytes_per_launch": alg_bytes},
+                     "kernel_avg_ms": round(avg_ms, 5), "kernel_launches_timed": len(kern_ms),
+                     "alg_bytes_per_launch": alg_bytes},
     }
 
 
