@@ -422,6 +422,12 @@ def check_calls(comm, x, y, n, ty, op, *, rank, world, want, ks):
         y.fill_(float("nan"))
         comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
         good = good and bool(torch.all(y == want + 3 * k * world).item())
+    # and once in place (MPI_IN_PLACE: a rank's block boundaries share cache lines between the
+    # peers' inputs it folds and the results it pulls)
+    k = ks[-1] + 1
+    y.fill_(float(rank + 1 + 3 * k))
+    comm.allreduce(None, y.data_ptr(), n, ty, op)
+    good = good and bool(torch.all(y == want + 3 * k * world).item())
     return good
 
 

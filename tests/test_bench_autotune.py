@@ -40,7 +40,7 @@ class FakeComm:
             raise FakeError("pipelined allreduce timed out waiting for a peer")
         # 2 ranks, x_r = r + 1 + 3k (bench_coll.check_calls) -> sum = 3 + 6k; the two-phase flow
         # with a 1024-block grid returns the previous call's sum on rank 1 (a stale hand-off)
-        v = ctypes.c_float.from_address(sbuf).value
+        v = ctypes.c_float.from_address(sbuf if sbuf else rbuf).value  # sbuf None: MPI_IN_PLACE
         k = round((v - self.rank - 1) / 3)
         stale = self.knobs.get("BLOCKS_PER_CU") == 1024 and self.rank == 1
         want = (ctypes.c_float * n)(*([3.0 + 6 * (k - (1 if stale else 0))] * n))
