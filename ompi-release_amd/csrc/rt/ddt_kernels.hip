@@ -249,6 +249,10 @@ __global__ __launch_bounds__(1024) void k_ddt_rows(RowArgs a, CsumSink csum)
     if constexpr (CSUM) block_sum_store(acc, csum);
 }
 
+// largest slot index the 32-bit row / unit kernels take: their grid-stride and last-block index
+// arithmetic (at most 2^22 slots past the end) must not wrap
+constexpr int64_t kSlot32Max = ((int64_t)1 << 32) - ((int64_t)1 << 22);
+
 // the slot width the row kernel can use (0: it does not apply): one run per block, and every
 // address, length and window a multiple of W; slot / row counts in 32 bits
 static int rows_width(const DdtDev &d, int nruns_host, int64_t run_disp, int64_t run_len, const void *mem,
@@ -261,7 +265,8 @@ static int rows_width(const DdtDev &d, int nruns_host, int64_t run_disp, int64_t
     while (w > 1 && (bits & (uint64_t)(w - 1))) w >>= 1;
     const int64_t last_slot = (pos + bytes) / w;
     const int64_t rows = last_slot / (run_len / w) + 1;
-    if (last_slot >= ((int64_t)1 << 32) || rows >= ((int64_t)1 << 32) || d.nblk >= ((int64_t)1 << 32) ||
+    // 32-bit slot arithmetic, with headroom for the last block's (tpb x U)-slot stride
+    if (last_slot >= kSlot32Max || rows >= ((int64_t)1 << 32) || d.nblk >= ((int64_t)1 << 32) ||
         (run_len / w) >= ((int64_t)1 << 32))
         return 0;
     return w;
@@ -536,7 +541,7 @@ static int launch_ddt_units(const DdtDev &d, bool pack, void *mem, void *packed,
         --lw;
     }
     const int64_t last = (pos + bytes) / w;
-    if (last >= ((int64_t)1 << 32) || d.inst_bytes / w >= ((int64_t)1 << 32) || d.nblk >= ((int64_t)1 << 32)) return 1;
+    if (last >= kSlot32Max || d.inst_bytes / w >= ((int64_t)1 << 32) || d.nblk >= ((int64_t)1 << 32)) return 1;
     UnitArgs a;
     a.mem = static_cast<char *>(mem);
     a.packed = static_cast<char *>(packed);
