@@ -170,7 +170,23 @@ static uint64_t fnv1a(uint64_t h, const void *p, size_t n)
     return h;
 }
 
-/* the layout of dt, or NULL when the convertor cannot take it (the caller then falls back) */
+/* a new layout of dt (the caller owns it), or NULL when the convertor cannot take it */
+static mi355x_ddt_t *ddt_private(const struct ompi_datatype_t *dt)
+{
+    const dt_type_desc_t *td = dt->super.opt_desc.desc ? &dt->super.opt_desc : &dt->super.desc;
+    if (!td->desc || td->used == 0 || dt->super.size == 0) return NULL;
+    const int64_t ext = (int64_t)(dt->super.ub - dt->super.lb);
+    mi355x_ddt_t *d = NULL;
+    if (mi355x_ddt_from_opal(td->desc, td->used, ext, opal_basic_sizes, &d) != MI355X_SUCCESS) return NULL;
+    if (mi355x_ddt_size(d) != dt->super.size) {
+        mi355x_ddt_destroy(d);
+        return NULL;
+    }
+    return d;
+}
+
+/* the layout of dt, or NULL when the convertor cannot take it (the caller then falls back);
+ * cached per module (8 entries: valid until the call returns) */
 static mi355x_ddt_t *ddt_of(struct mca_coll_mi355x_module_t *m, const struct ompi_datatype_t *dt)
 {
     const dt_type_desc_t *td = dt->super.opt_desc.desc ? &dt->super.opt_desc : &dt->super.desc;
@@ -182,12 +198,8 @@ static mi355x_ddt_t *ddt_of(struct mca_coll_mi355x_module_t *m, const struct omp
     sig = fnv1a(sig, &ext, sizeof(ext));
     for (int i = 0; i < 8; ++i)
         if (m->ddt_cache[i].d && m->ddt_cache[i].dt == dt && m->ddt_cache[i].sig == sig) return m->ddt_cache[i].d;
-    mi355x_ddt_t *d = NULL;
-    if (mi355x_ddt_from_opal(td->desc, td->used, ext, opal_basic_sizes, &d) != MI355X_SUCCESS) return NULL;
-    if (mi355x_ddt_size(d) != dt->super.size) {
-        mi355x_ddt_destroy(d);
-        return NULL;
-    }
+    mi355x_ddt_t *d = ddt_private(dt);
+    if (!d) return NULL;
     struct ddt_slot *e = &m->ddt_cache[m->ddt_next];
     m->ddt_next = (m->ddt_next + 1) & 7;
     if (e->d) mi355x_ddt_destroy(e->d);
@@ -618,6 +630,15 @@ typedef struct mi355x_nbreq_t {
     mi355x_request_t *eng;
     int p2p;                       /* 0 collective, 1 send, 2 receive (status filled at completion) */
     struct mi355x_nbreq_t *next;   /* active list */
+    /* derived datatypes (iallgather / ibcast): the packed bytes travel through `stage` (owned by
+     * the request); at completion they are unpacked into (ubuf, ucount, ud) -- ud NULL: copied --
+     * before MPI sees the request complete, then stage and ud are released */
+    void *stage;
+    size_t stage_bytes;
+    void *ubuf;
+    int ucount;
+    mi355x_ddt_t *ud;
+    mi355x_ddt_t *pd;              /* layout of the initiation-time pack (kept until completion) */
 } mi355x_nbreq_t;
 
 static pthread_mutex_t nb_lock = PTHREAD_MUTEX_INITIALIZER;
@@ -650,6 +671,31 @@ static void nbreq_construct(opal_object_t *o)
     r->super.req_cancel = nbreq_cancel;
     r->eng = NULL;
     r->next = NULL;
+    r->stage = NULL;
+    r->stage_bytes = 0;
+    r->ubuf = NULL;
+    r->ucount = 0;
+    r->ud = NULL;
+    r->pd = NULL;
+}
+
+/* completion-time unpack of a derived-datatype nonblocking collective (local work only) */
+static int nb_finish_stage(mi355x_nbreq_t *r, int rc)
+{
+    if (!r->stage) return rc;
+    if (rc == MI355X_SUCCESS && r->ubuf) {
+        rc = r->ud ? mi355x_unpack(r->ud, (size_t)r->ucount, r->ubuf, 0, r->stage, r->stage_bytes, NULL, NULL)
+                   : mi355x_memcpy_async(r->ubuf, r->stage, r->stage_bytes, NULL);
+        if (rc == MI355X_SUCCESS) rc = mi355x_stream_sync(NULL);
+    } else {
+        (void)mi355x_stream_sync(NULL);
+    }
+    mi355x_free(r->stage);
+    r->stage = NULL;
+    if (r->ud) mi355x_ddt_destroy(r->ud);
+    if (r->pd) mi355x_ddt_destroy(r->pd);
+    r->ud = r->pd = NULL;
+    return rc;
 }
 
 static opal_class_t mi355x_nbreq_t_class = {"mca_coll_mi355x_request_t", &ompi_request_t_class, nbreq_construct,
@@ -663,12 +709,13 @@ static int nb_progress(void)
     for (mi355x_nbreq_t **p = &nb_active; *p;) {
         mi355x_nbreq_t *r = *p;
         int done = 0;
-        const int rc = mi355x_request_test(r->eng, &done);
+        const int rc0 = mi355x_request_test(r->eng, &done);
         if (!done) {
             p = &r->next;
             continue;
         }
         *p = r->next;
+        const int rc = nb_finish_stage(r, rc0);
         if (r->p2p == 2) {  /* MPI_Status of a receive (pml_ob1_recvreq.h:172-180 for truncation) */
             mi355x_status_t st;
             memset(&st, 0, sizeof(st));
@@ -694,15 +741,43 @@ static int nb_progress(void)
 
 /* wrap an engine request into an active MPI request (OMPI_REQUEST_INIT + ACTIVE, coll_libnbc.h:
  * 126-131) */
-static int nb_start_kind(mi355x_request_t *eng, struct ompi_communicator_t *comm, ompi_request_t **request, int p2p)
+struct nb_stage {
+    void *stage;
+    size_t bytes;
+    void *ubuf;       /* NULL: nothing to unpack on this rank */
+    int ucount;
+    mi355x_ddt_t *ud; /* owned by the request; NULL with ubuf set: a plain copy */
+    mi355x_ddt_t *pd; /* layout of the initiation-time pack, owned by the request */
+};
+
+static void nb_stage_release(struct nb_stage *st)
+{
+    if (!st) return;
+    (void)mi355x_stream_sync(NULL);
+    if (st->stage) mi355x_free(st->stage);
+    if (st->ud) mi355x_ddt_destroy(st->ud);
+    if (st->pd) mi355x_ddt_destroy(st->pd);
+}
+
+static int nb_start_full(mi355x_request_t *eng, struct ompi_communicator_t *comm, ompi_request_t **request, int p2p,
+                         struct nb_stage *st)
 {
     mi355x_nbreq_t *r = (mi355x_nbreq_t *)mi355x_obj_new(&mi355x_nbreq_t_class);
     if (!r) {
         mi355x_request_wait(eng);
         mi355x_request_free(eng);
+        nb_stage_release(st);
         return OMPI_ERR_OUT_OF_RESOURCE;
     }
     r->p2p = p2p;
+    if (st) {
+        r->stage = st->stage;
+        r->stage_bytes = st->bytes;
+        r->ubuf = st->ubuf;
+        r->ucount = st->ucount;
+        r->ud = st->ud;
+        r->pd = st->pd;
+    }
     if (p2p) r->super.req_type = OMPI_REQUEST_PML;
     r->super.req_complete = false;
     r->super.req_persistent = false;
@@ -720,6 +795,11 @@ static int nb_start_kind(mi355x_request_t *eng, struct ompi_communicator_t *comm
     pthread_mutex_unlock(&nb_lock);
     *request = &r->super;
     return OMPI_SUCCESS;
+}
+
+static int nb_start_kind(mi355x_request_t *eng, struct ompi_communicator_t *comm, ompi_request_t **request, int p2p)
+{
+    return nb_start_full(eng, comm, request, p2p, NULL);
 }
 
 static int nb_start(mi355x_request_t *eng, struct ompi_communicator_t *comm, ompi_request_t **request)
@@ -781,7 +861,35 @@ int mca_coll_mi355x_ireduce_scatter_block(void *sbuf, void *rbuf, int rcount, st
     return rc ? map_rc(rc) : nb_start(eng, comm, request);
 }
 
-/* contiguous layouts only; derived datatypes go to the previous owner (libnbc) */
+/* the (count, dt) side of a staged nonblocking move: pack it into `p` now (local work), or set up
+ * the completion-time unpack into `st` (the request then owns a private layout of dt) */
+static int nb_stage_side(int pack, void *buf, int count, const struct ompi_datatype_t *dt, void *p, size_t bytes,
+                         struct nb_stage *st)
+{
+    size_t cb;
+    if (contiguous_bytes(dt, count, &cb)) {
+        if (pack) return mi355x_memcpy_async(p, buf, bytes, NULL);
+        st->ubuf = buf;
+        return MI355X_SUCCESS;
+    }
+    mi355x_ddt_t *d = ddt_private(dt);
+    if (!d) return MI355X_ERR_UNSUPPORTED;
+    if (pack) {
+        st->pd = d;  /* the pack kernel reads its run tables until it finishes: released at completion */
+        return mi355x_pack(d, (size_t)count, buf, 0, p, bytes, NULL, NULL);
+    }
+    st->ubuf = buf;
+    st->ucount = count;
+    st->ud = d;
+    return MI355X_SUCCESS;
+}
+
+/* Contiguous layouts go straight to the engine.  Derived layouts -- on any rank, whatever the
+ * others use (MPI lets layouts differ; only the type signatures match) -- also stay in the
+ * engine: my block is packed into a per-request staging buffer at initiation, the engine gathers
+ * the packed blocks in place, and the completion unpacks them into rbuf (all local work, so the
+ * call stays nonblocking); rank-local fallbacks to libnbc would leave the ranks in different
+ * components. */
 int mca_coll_mi355x_iallgather(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
                                struct ompi_datatype_t *rdtype, struct ompi_communicator_t *comm,
                                ompi_request_t **request, mca_coll_base_module_t *module)
@@ -789,24 +897,57 @@ int mca_coll_mi355x_iallgather(void *sbuf, int scount, struct ompi_datatype_t *s
     mca_coll_mi355x_module_t *m = MOD(module);
     const int inplace = (sbuf == MPI_IN_PLACE);
     size_t rb = 0, sb = 0;
-    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || rcount < 0 || !contiguous_bytes(rdtype, rcount, &rb) ||
-        (!inplace && (scount < 0 || !contiguous_bytes(sdtype, scount, &sb) || sb != rb)))
+    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || rcount < 0 || (!inplace && scount < 0))
         NB_FALLBACK(iallgather, sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, request);
     mi355x_request_t *eng = NULL;
-    int rc = mi355x_iallgather(m->engine, inplace ? NULL : sbuf, rbuf, rb, NULL, &eng);
-    return rc ? map_rc(rc) : nb_start(eng, comm, request);
+    if (contiguous_bytes(rdtype, rcount, &rb) && (inplace || (contiguous_bytes(sdtype, scount, &sb) && sb == rb))) {
+        int rc = mi355x_iallgather(m->engine, inplace ? NULL : sbuf, rbuf, rb, NULL, &eng);
+        return rc ? map_rc(rc) : nb_start(eng, comm, request);
+    }
+    const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm);
+    const size_t blk = (size_t)rcount * rdtype->super.size;
+    if (!inplace && (size_t)scount * sdtype->super.size != blk) return OMPI_ERR_BAD_PARAM;
+    struct nb_stage st = {NULL, blk * (size_t)n, NULL, 0, NULL, NULL};
+    if (mi355x_malloc(&st.stage, st.bytes ? st.bytes : 1) != MI355X_SUCCESS) return OMPI_ERR_OUT_OF_RESOURCE;
+    const ptrdiff_t rext = rdtype->super.ub - rdtype->super.lb;
+    int rc = inplace ? nb_stage_side(1, (char *)rbuf + (ptrdiff_t)me * rcount * rext, rcount, rdtype,
+                                     (char *)st.stage + blk * me, blk, &st)
+                     : nb_stage_side(1, sbuf, scount, sdtype, (char *)st.stage + blk * me, blk, &st);
+    if (rc == MI355X_SUCCESS) rc = nb_stage_side(0, rbuf, rcount * n, rdtype, st.stage, st.bytes, &st);
+    if (rc == MI355X_SUCCESS) rc = mi355x_iallgather(m->engine, NULL, st.stage, blk, NULL, &eng);
+    if (rc != MI355X_SUCCESS) {
+        if (rc == MI355X_ERR_UNSUPPORTED)
+            fprintf(stderr, "[coll/mi355x] iallgather: the GPU convertor cannot describe the datatype\n");
+        nb_stage_release(&st);
+        return map_rc(rc);
+    }
+    return nb_start_full(eng, comm, request, 0, &st);
 }
 
+/* derived layouts as in iallgather: the root packs at initiation, the others unpack at completion */
 int mca_coll_mi355x_ibcast(void *buff, int count, struct ompi_datatype_t *datatype, int root,
                            struct ompi_communicator_t *comm, ompi_request_t **request, mca_coll_base_module_t *module)
 {
     mca_coll_mi355x_module_t *m = MOD(module);
     size_t bytes = 0;
-    if (!is_dev(buff) || count < 0 || !contiguous_bytes(datatype, count, &bytes))
-        NB_FALLBACK(ibcast, buff, count, datatype, root, comm, request);
+    if (!is_dev(buff) || count < 0) NB_FALLBACK(ibcast, buff, count, datatype, root, comm, request);
     mi355x_request_t *eng = NULL;
-    int rc = mi355x_ibcast(m->engine, buff, bytes, root, NULL, &eng);
-    return rc ? map_rc(rc) : nb_start(eng, comm, request);
+    if (contiguous_bytes(datatype, count, &bytes)) {
+        int rc = mi355x_ibcast(m->engine, buff, bytes, root, NULL, &eng);
+        return rc ? map_rc(rc) : nb_start(eng, comm, request);
+    }
+    const int me = mi355x_comm_rank_of(comm);
+    struct nb_stage st = {NULL, (size_t)count * datatype->super.size, NULL, 0, NULL, NULL};
+    if (mi355x_malloc(&st.stage, st.bytes ? st.bytes : 1) != MI355X_SUCCESS) return OMPI_ERR_OUT_OF_RESOURCE;
+    int rc = nb_stage_side(me == root, buff, count, datatype, st.stage, st.bytes, &st);
+    if (rc == MI355X_SUCCESS) rc = mi355x_ibcast(m->engine, st.stage, st.bytes, root, NULL, &eng);
+    if (rc != MI355X_SUCCESS) {
+        if (rc == MI355X_ERR_UNSUPPORTED)
+            fprintf(stderr, "[coll/mi355x] ibcast: the GPU convertor cannot describe datatype %s\n", datatype->name);
+        nb_stage_release(&st);
+        return map_rc(rc);
+    }
+    return nb_start_full(eng, comm, request, 0, &st);
 }
 
 /* ------------------------------------------------------------------ device point-to-point (PML hook)

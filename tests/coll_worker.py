@@ -69,6 +69,63 @@ def derived_allgather(m, comm, oracle, rank, size, torch):
     oracle.oracle_ddt_free(od)
 
 
+def nonblocking_mixed_layouts(m, comm, oracle, rank, size, torch):
+    """MPI_Iallgather / MPI_Ibcast where the LAYOUTS differ between ranks (only the type signatures
+    match, as MPI allows): even ranks receive n floats per rank into vector(n, 1, 2, MPI_FLOAT)
+    blocks and send dense, odd ranks receive dense and send out of a strided buffer; the bcast root
+    uses the vector layout while the others use n dense floats, then the other way round.  Every
+    rank must stay in the engine (derived layouts staged at initiation / unpacked at completion);
+    a rank-local fallback to the previous component would leave the ranks in different protocols.
+    Two calls are in flight before the first wait."""
+    L = m.lib
+    n = 300
+    desc, used, tsize, lb, ub = opal_strided_elems(n, OPAL_FLOAT4, 4, 8)
+    vec = m.derived(desc, used, tsize, lb, ub)
+    ext = ub - lb
+    fdt = m.dtype_for_slot(m.pkg.T["FLOAT"])
+    contrib = [np.arange(n, dtype=np.float32) + 1000 * r for r in range(size)]
+    strided = lambda a: np.stack([a, np.full(n, -1, np.float32)], 1).reshape(-1)[: 2 * n - 1]  # vector layout
+    even = rank % 2 == 0
+    # iallgather
+    if even:
+        send = torch.from_numpy(contrib[rank].copy()).cuda()
+        rbuf = torch.full((size * ext // 4,), -5.0, device="cuda")
+        sargs, rargs = (send.data_ptr(), n, fdt), (rbuf.data_ptr(), 1, vec)
+    else:
+        send = torch.from_numpy(strided(contrib[rank]).copy()).cuda()
+        rbuf = torch.full((size * n,), -5.0, device="cuda")
+        sargs, rargs = (send.data_ptr(), 1, vec), (rbuf.data_ptr(), n, fdt)
+    # ibcast #1: the root's layout is the vector, the others dense; #2 the reverse
+    root = size - 1
+    b1 = torch.from_numpy(strided(contrib[root]).copy()).cuda() if rank == root else torch.full((n,), -3.0, device="cuda")
+    b1args = (b1.data_ptr(), 1, vec) if rank == root else (b1.data_ptr(), n, fdt)
+    torch.cuda.synchronize()
+    reqs = [ctypes.c_void_p() for _ in range(2)]
+    assert L.mini_iallgather(comm, *sargs, *rargs, ctypes.byref(reqs[0])) == 0
+    assert L.mini_ibcast(comm, *b1args, root, ctypes.byref(reqs[1])) == 0
+    for q in reqs:
+        assert L.mini_wait(ctypes.byref(q)) == 0
+    got = rbuf.cpu().numpy()
+    for r in range(size):
+        if even:
+            blk = got[r * ext // 4: r * ext // 4 + 2 * n - 1]
+            assert np.array_equal(blk[0::2], contrib[r]) and (blk[1::2] == -5).all(), ("iallgather into vector blocks", r)
+        else:
+            assert np.array_equal(got[r * n:(r + 1) * n], contrib[r]), ("iallgather dense", r)
+    g1 = b1.cpu().numpy()
+    assert np.array_equal(g1[0::2] if rank == root else g1, contrib[root]), "ibcast, vector at the root"
+    b2 = torch.from_numpy(contrib[root].copy()).cuda() if rank == root else torch.full((2 * n - 1,), -4.0, device="cuda")
+    b2args = (b2.data_ptr(), n, fdt) if rank == root else (b2.data_ptr(), 1, vec)
+    torch.cuda.synchronize()
+    req = ctypes.c_void_p()
+    assert L.mini_ibcast(comm, *b2args, root, ctypes.byref(req)) == 0
+    assert L.mini_wait(ctypes.byref(req)) == 0
+    g2 = b2.cpu().numpy()
+    if rank != root:
+        assert np.array_equal(g2[0::2], contrib[root]) and (g2[1::2] == -4).all(), "ibcast into vectors off the root"
+    L.mini_datatype_destroy(vec)
+
+
 def nonblocking(m, comm, oracle, rank, size, torch, ptrs):
     pkg = m.pkg
     code, slot = pkg.OP["SUM"], pkg.T["DOUBLE"]
@@ -512,6 +569,7 @@ def main():
     # nonblocking slots: MPI_Iallreduce / Ireduce / Ireduce_scatter_block / Iallgather / Ibcast posted
     # together, then MPI_Wait on each (requests progressed by the component's opal_progress callback)
     nonblocking(m, comm, oracle, rank, size, torch, ptrs)
+    nonblocking_mixed_layouts(m, comm, oracle, rank, size, torch)
     # derived datatypes through the GPU convertor: bcast of a vector type ...
     derived_bcast(m, comm, oracle, rank, size, torch)
     derived_allgather(m, comm, oracle, rank, size, torch)
