@@ -197,6 +197,31 @@ def large_calls(pkg, comm, rank, size, torch):
         torch.cuda.empty_cache()
 
 
+def max_count(pkg, comm, rank, size, torch):
+    """the largest count an MPI_Allreduce can pass (INT_MAX elements, `int count` at coll.h:189-191)
+    of fp32: 8 GiB per buffer, dmabuf-exported allocations, byte offsets past 2^32 -- two-phase and
+    pipelined flows, in place and not; x_r = r + 1 -> every element n(n+1)/2 exactly"""
+    n = 2**31 - 1
+    want = size * (size + 1) / 2
+    x = torch.full((n,), float(rank + 1), device="cuda")
+    y = torch.full((n,), -1.0, device="cuda")
+    torch.cuda.synchronize()
+    try:
+        for pipe in (0, 1):
+            comm.set("PIPE", pipe)
+            comm.allreduce(x.data_ptr(), y.data_ptr(), n, pkg.T["FLOAT"], pkg.OP["SUM"])
+            assert bool(torch.all(y == want)), ("INT_MAX-count allreduce", pipe)
+            y.fill_(float(rank + 1))
+            torch.cuda.synchronize()
+            comm.allreduce(None, y.data_ptr(), n, pkg.T["FLOAT"], pkg.OP["SUM"])
+            assert bool(torch.all(y == want)), ("INT_MAX-count allreduce in place", pipe)
+    finally:
+        comm.set("PIPE", 1 if size >= 4 else 0)
+    del x, y
+    torch.cuda.empty_cache()
+    print(f"rank {rank} maxcount OK", flush=True)
+
+
 def pipe_checks(pkg, comm, rank, size, oracle, torch):
     """the pipelined allreduce (coll_pipe.hip: fold + pulls in one launch, device-side chunk
     flags) against the oracle's schedule simulation and against the two-phase flow: ring and
@@ -444,6 +469,8 @@ def _main():
     staged(pkg, comm, rank, size, torch, key)
     if size in (2, 3):
         big_bcast(pkg, comm, rank, size, torch)
+    if size == 2:
+        max_count(pkg, comm, rank, size, torch)
     comm.barrier()
     comm.destroy()
     print(f"rank {rank} OK", flush=True)

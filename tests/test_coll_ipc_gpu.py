@@ -36,6 +36,7 @@ def test_ipc_ranks(gpu, size):
     assert not failed, "\n".join(f"rank {r} failed (rc {procs[r].returncode}):\n{outs[r][-2500:]}" for r in failed)
     for r, p in enumerate(procs):
         stages = ("pipe OK", "LL OK", "p2p OK", "staged OK", "OK") + (("bcast4g OK",) if size in (2, 3) else ()) \
+            + (("maxcount OK",) if size == 2 else ()) \
             + (("pipe slots OK",) if size == 3 else ())
         for stage in stages:
             assert f"rank {r} {stage}" in outs[r], f"rank {r} did not report '{stage}':\n{outs[r][-3000:]}"
