@@ -120,6 +120,7 @@ int mca_coll_mi355x_pml_probe(int src, int tag, struct ompi_communicator_t *comm
 extern int mca_coll_mi355x_priority;            /* 90 */
 extern int mca_coll_mi355x_allreduce_algorithm; /* 0 = tuned decision, else coll_tuned numbering */
 extern int mca_coll_mi355x_pml_hook;            /* 1 = device point-to-point through the engine */
+extern int mca_coll_mi355x_mixed_buffers;       /* 1 = ranks may mix host and device buffers in a call */
 
 #ifdef __cplusplus
 }

@@ -100,6 +100,14 @@ int mi355x_comm_destroy(mi355x_comm_t *comm);
 int mi355x_comm_rank(const mi355x_comm_t *comm);
 int mi355x_comm_size(const mi355x_comm_t *comm);
 int mi355x_comm_barrier(mi355x_comm_t *comm);
+/* Buffer-kind agreement for one collective call.  coll/cuda tolerates ranks that mix host and
+ * device buffers in one collective (each rank stages its own, coll_cuda_allreduce.c:30-77); the
+ * engine needs every rank in the same protocol.  Every rank calls this once per collective, in the
+ * collective's call order: a rank whose buffers are device memory (device = 1) publishes and
+ * returns at once with *any_device = 1 (it will run the engine); a rank with host buffers waits
+ * until every rank has published this call and learns whether any of them holds device buffers
+ * (then it runs the engine too, on staged copies; else every rank takes the host path). */
+int mi355x_comm_vote(mi355x_comm_t *comm, int device, int *any_device);
 /* algorithm id of the last collective, coll/tuned numbering (allreduce: 1 linear, 2 nonoverlapping,
  * 3 recursive doubling, 4 ring, 5 segmented ring; reduce: 1 linear, 2 chain, 3 pipeline, 4 binary,
  * 5 binomial; reduce_scatter: 1 non-overlapping, 2 recursive halving, 3 ring) */

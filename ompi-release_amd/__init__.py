@@ -158,6 +158,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "mi355x_ddt_nruns": (i, [vp]),
         "mi355x_ddt_tune": (i, [i, i, i, i]),
         "mi355x_ddt_tune_rows": (i, [i]),
+        "mi355x_comm_vote": (i, [vp, i, c.POINTER(i)]),
         "mi355x_gather": (i, [vp, vp, vp, sz, i, vp]),
         "mi355x_gatherv": (i, [vp, vp, sz, vp, c.POINTER(sz), c.POINTER(sz), i, vp]),
         "mi355x_scatter": (i, [vp, vp, vp, sz, i, vp]),

@@ -251,6 +251,66 @@ static int map_rc(int rc)
 
 #define MOD(m) ((mca_coll_mi355x_module_t *)(m))
 
+/* ------------------------------------------------------------------ mixed host / device buffers
+ * coll/cuda lets ranks mix host and device buffers in one collective: each rank stages its own to
+ * the host and runs the host algorithm (coll_cuda_allreduce.c:30-77).  Here the engine runs only
+ * if every rank joins it, so for the collectives below every rank votes its buffer kind
+ * (mi355x_comm_vote, coll_mi355x_mixed_buffers = 1, the default): a rank with device buffers goes
+ * to the engine at once; a rank with host buffers learns whether any peer has device buffers --
+ * if so it joins the engine on device copies of its buffers (the staging runs the other way from
+ * coll/cuda's), if not every rank takes the previous component's host path.  Ranks with host
+ * buffers need contiguous layouts to join (derived host layouts are an error in a mixed call). */
+int mca_coll_mi355x_mixed_buffers = 1;
+
+/* 1: run the engine (*dev: this rank's buffers are all device memory); 0: the host path on every
+ * rank; < 0: an error (the vote failed or timed out) */
+static int route(mca_coll_mi355x_module_t *m, int dev)
+{
+    if (!mca_coll_mi355x_mixed_buffers) return dev;
+    int any = dev;
+    const int rc = mi355x_comm_vote(m->engine, dev, &any);
+    if (rc != MI355X_SUCCESS) {
+        fprintf(stderr, "[coll/mi355x] %s\n", mi355x_last_error());
+        return -1;
+    }
+    return any;
+}
+
+/* device copy of a host input (scratch slot `slot`), or the buffer itself when it is on the device */
+static void *dev_in(mca_coll_mi355x_module_t *m, int slot, const void *buf, size_t bytes, int *rc)
+{
+    if (is_dev(buf)) return (void *)buf;
+    void *d = scratch_slot(m, slot, bytes ? bytes : 1);
+    if (!d) {
+        *rc = MI355X_ERR_NOMEM;
+        return NULL;
+    }
+    if (bytes && *rc == MI355X_SUCCESS) *rc = mi355x_memcpy(d, buf, bytes);
+    return d;
+}
+
+/* device stand-in for a host output (contents undefined until the call fills it) */
+static void *dev_out(mca_coll_mi355x_module_t *m, int slot, void *buf, size_t bytes, int *rc)
+{
+    if (is_dev(buf)) return buf;
+    void *d = scratch_slot(m, slot, bytes ? bytes : 1);
+    if (!d) *rc = MI355X_ERR_NOMEM;
+    return d;
+}
+
+static int copy_back(void *host, const void *dev, size_t bytes, int rc)
+{
+    if (rc != MI355X_SUCCESS || host == dev || bytes == 0) return rc;
+    return mi355x_memcpy(host, dev, bytes);
+}
+
+#define ROUTE_OR(PREV_CALL)                                                            \
+    do {                                                                               \
+        const int r_ = route(m, dev);                                                  \
+        if (r_ < 0) return OMPI_ERROR;                                                 \
+        if (r_ == 0) return PREV_CALL;                                                 \
+    } while (0)
+
 /* ------------------------------------------------------------------ collectives */
 int mca_coll_mi355x_allreduce(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
                               struct ompi_op_t *op, struct ompi_communicator_t *comm,
@@ -259,10 +319,17 @@ int mca_coll_mi355x_allreduce(void *sbuf, void *rbuf, int count, struct ompi_dat
     mca_coll_mi355x_module_t *m = MOD(module);
     const int inplace = (sbuf == MPI_IN_PLACE);
     const int t = reducible_type(dtype);
-    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 ||
-        !mi355x_op_supported(op->o_f_to_c_index, t))
+    if (!(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 || !mi355x_op_supported(op->o_f_to_c_index, t) || count < 0)
         return m->prev_allreduce(sbuf, rbuf, count, dtype, op, comm, m->prev_allreduce_module);
-    return map_rc(mi355x_allreduce(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)count, t, op->o_f_to_c_index, NULL));
+    const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
+    ROUTE_OR(m->prev_allreduce(sbuf, rbuf, count, dtype, op, comm, m->prev_allreduce_module));
+    if (dev) return map_rc(mi355x_allreduce(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)count, t, op->o_f_to_c_index, NULL));
+    const size_t bytes = (size_t)count * mi355x_type_size(t);
+    int rc = MI355X_SUCCESS;
+    void *rd = inplace ? dev_in(m, 1, rbuf, bytes, &rc) : dev_out(m, 1, rbuf, bytes, &rc);
+    const void *sd = inplace ? NULL : dev_in(m, 0, sbuf, bytes, &rc);
+    if (rc == MI355X_SUCCESS) rc = mi355x_allreduce(m->engine, sd, rd, (size_t)count, t, op->o_f_to_c_index, NULL);
+    return map_rc(copy_back(rbuf, rd, bytes, rc));
 }
 
 /* MPI_Reduce: the root's rbuf and every rank's sbuf (MPI_IN_PLACE: the root's rbuf) on the device;
@@ -274,11 +341,20 @@ int mca_coll_mi355x_reduce(void *sbuf, void *rbuf, int count, struct ompi_dataty
     const int me = mi355x_comm_rank_of(comm);
     const int inplace = (sbuf == MPI_IN_PLACE);
     const int t = reducible_type(dtype);
-    if ((me == root && !is_dev(rbuf)) || (!inplace && !is_dev(sbuf)) || (inplace && me != root) ||
-        !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 || !mi355x_op_supported(op->o_f_to_c_index, t))
+    if ((inplace && me != root) || !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 ||
+        !mi355x_op_supported(op->o_f_to_c_index, t) || count < 0)
         return m->prev_reduce(sbuf, rbuf, count, dtype, op, root, comm, m->prev_reduce_module);
-    return map_rc(mi355x_reduce(m->engine, inplace ? NULL : sbuf, me == root ? rbuf : NULL, (size_t)count, t,
-                                op->o_f_to_c_index, root, NULL));
+    const int dev = (me != root || is_dev(rbuf)) && (inplace || is_dev(sbuf));
+    ROUTE_OR(m->prev_reduce(sbuf, rbuf, count, dtype, op, root, comm, m->prev_reduce_module));
+    if (dev)
+        return map_rc(mi355x_reduce(m->engine, inplace ? NULL : sbuf, me == root ? rbuf : NULL, (size_t)count, t,
+                                    op->o_f_to_c_index, root, NULL));
+    const size_t bytes = (size_t)count * mi355x_type_size(t);
+    int rc = MI355X_SUCCESS;
+    void *rd = me != root ? NULL : inplace ? dev_in(m, 1, rbuf, bytes, &rc) : dev_out(m, 1, rbuf, bytes, &rc);
+    const void *sd = inplace ? NULL : dev_in(m, 0, sbuf, bytes, &rc);
+    if (rc == MI355X_SUCCESS) rc = mi355x_reduce(m->engine, sd, rd, (size_t)count, t, op->o_f_to_c_index, root, NULL);
+    return map_rc(me == root ? copy_back(rbuf, rd, bytes, rc) : rc);
 }
 
 int mca_coll_mi355x_reduce_scatter_block(void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dtype,
@@ -288,11 +364,20 @@ int mca_coll_mi355x_reduce_scatter_block(void *sbuf, void *rbuf, int rcount, str
     mca_coll_mi355x_module_t *m = MOD(module);
     const int inplace = (sbuf == MPI_IN_PLACE);
     const int t = reducible_type(dtype);
-    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 ||
-        !mi355x_op_supported(op->o_f_to_c_index, t))
+    if (!(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 || !mi355x_op_supported(op->o_f_to_c_index, t) || rcount < 0)
         return m->prev_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, m->prev_reduce_scatter_block_module);
-    return map_rc(mi355x_reduce_scatter_block(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)rcount, t,
-                                              op->o_f_to_c_index, NULL));
+    const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
+    ROUTE_OR(m->prev_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, m->prev_reduce_scatter_block_module));
+    if (dev)
+        return map_rc(mi355x_reduce_scatter_block(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)rcount, t,
+                                                  op->o_f_to_c_index, NULL));
+    const size_t out = (size_t)rcount * mi355x_type_size(t), in = out * (size_t)mi355x_comm_size_of(comm);
+    int rc = MI355X_SUCCESS;
+    void *rd = inplace ? dev_in(m, 1, rbuf, in, &rc) : dev_out(m, 1, rbuf, out, &rc);
+    const void *sd = inplace ? NULL : dev_in(m, 0, sbuf, in, &rc);
+    if (rc == MI355X_SUCCESS)
+        rc = mi355x_reduce_scatter_block(m->engine, sd, rd, (size_t)rcount, t, op->o_f_to_c_index, NULL);
+    return map_rc(copy_back(rbuf, rd, out, rc));
 }
 
 int mca_coll_mi355x_reduce_scatter(void *sbuf, void *rbuf, int *rcounts, struct ompi_datatype_t *dtype,
@@ -302,10 +387,20 @@ int mca_coll_mi355x_reduce_scatter(void *sbuf, void *rbuf, int *rcounts, struct 
     mca_coll_mi355x_module_t *m = MOD(module);
     const int inplace = (sbuf == MPI_IN_PLACE);
     const int t = reducible_type(dtype);
-    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 ||
-        !mi355x_op_supported(op->o_f_to_c_index, t))
+    if (!(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 || !mi355x_op_supported(op->o_f_to_c_index, t))
         return m->prev_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, m->prev_reduce_scatter_module);
-    return map_rc(mi355x_reduce_scatter(m->engine, inplace ? NULL : sbuf, rbuf, rcounts, t, op->o_f_to_c_index, NULL));
+    const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
+    ROUTE_OR(m->prev_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, m->prev_reduce_scatter_module));
+    if (dev) return map_rc(mi355x_reduce_scatter(m->engine, inplace ? NULL : sbuf, rbuf, rcounts, t, op->o_f_to_c_index, NULL));
+    const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm);
+    size_t total = 0;
+    for (int q = 0; q < n; ++q) total += (size_t)(rcounts[q] > 0 ? rcounts[q] : 0);
+    const size_t esz = mi355x_type_size(t), in = total * esz, out = (size_t)(rcounts[me] > 0 ? rcounts[me] : 0) * esz;
+    int rc = MI355X_SUCCESS;
+    void *rd = inplace ? dev_in(m, 1, rbuf, in, &rc) : dev_out(m, 1, rbuf, out, &rc);
+    const void *sd = inplace ? NULL : dev_in(m, 0, sbuf, in, &rc);
+    if (rc == MI355X_SUCCESS) rc = mi355x_reduce_scatter(m->engine, sd, rd, rcounts, t, op->o_f_to_c_index, NULL);
+    return map_rc(copy_back(rbuf, rd, out, rc));
 }
 
 int mca_coll_mi355x_allgather(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
@@ -314,14 +409,27 @@ int mca_coll_mi355x_allgather(void *sbuf, int scount, struct ompi_datatype_t *sd
 {
     mca_coll_mi355x_module_t *m = MOD(module);
     const int inplace = (sbuf == MPI_IN_PLACE);
-    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || rcount < 0 || (!inplace && scount < 0))
+    if (rcount < 0 || (!inplace && scount < 0))
         return m->prev_allgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_allgather_module);
+    const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
+    ROUTE_OR(m->prev_allgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_allgather_module));
+    const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm);
     size_t rb = 0, sb = 0;
+    if (!dev) {  /* host buffers in a call where peers hold device ones: dense layouts, staged */
+        if (!contiguous_bytes(rdtype, rcount, &rb) || (!inplace && (!contiguous_bytes(sdtype, scount, &sb) || sb != rb))) {
+            fprintf(stderr, "[coll/mi355x] allgather: host buffers with a derived layout in a call with device peers\n");
+            return OMPI_ERR_NOT_SUPPORTED;
+        }
+        int rc = MI355X_SUCCESS;
+        void *rd = inplace ? dev_in(m, 1, rbuf, rb * (size_t)n, &rc) : dev_out(m, 1, rbuf, rb * (size_t)n, &rc);
+        const void *sd = inplace ? NULL : dev_in(m, 0, sbuf, rb, &rc);
+        if (rc == MI355X_SUCCESS) rc = mi355x_allgather(m->engine, sd, rd, rb, NULL);
+        return map_rc(copy_back(rbuf, rd, rb * (size_t)n, rc));
+    }
     if (contiguous_bytes(rdtype, rcount, &rb) && (inplace || (contiguous_bytes(sdtype, scount, &sb) && sb == rb)))
         return map_rc(mi355x_allgather(m->engine, inplace ? NULL : sbuf, rbuf, rb, NULL));
     /* derived datatypes: pack my block into the staging buffer, gather packed blocks in place,
      * unpack all n blocks with one launch (block r = instances [r*rcount, (r+1)*rcount)) */
-    const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm);
     const size_t blk = (size_t)rcount * rdtype->super.size;
     if (!inplace && (size_t)scount * sdtype->super.size != blk) return OMPI_ERR_BAD_PARAM;
     /* a layout the convertor cannot describe is an error, never a rank-local fallback: the other
@@ -348,8 +456,20 @@ int mca_coll_mi355x_bcast(void *buff, int count, struct ompi_datatype_t *datatyp
 {
     mca_coll_mi355x_module_t *m = MOD(module);
     size_t bytes = 0;
-    if (!is_dev(buff) || count < 0)
-        return m->prev_bcast(buff, count, datatype, root, comm, m->prev_bcast_module);
+    if (count < 0) return m->prev_bcast(buff, count, datatype, root, comm, m->prev_bcast_module);
+    const int dev = is_dev(buff);
+    ROUTE_OR(m->prev_bcast(buff, count, datatype, root, comm, m->prev_bcast_module));
+    const int me = mi355x_comm_rank_of(comm);
+    if (!dev) {  /* host buffer in a call where peers hold device ones: dense layouts, staged */
+        if (!contiguous_bytes(datatype, count, &bytes)) {
+            fprintf(stderr, "[coll/mi355x] bcast: a host buffer with a derived layout in a call with device peers\n");
+            return OMPI_ERR_NOT_SUPPORTED;
+        }
+        int rc = MI355X_SUCCESS;
+        void *bd = me == root ? dev_in(m, 1, buff, bytes, &rc) : dev_out(m, 1, buff, bytes, &rc);
+        if (rc == MI355X_SUCCESS) rc = mi355x_bcast(m->engine, bd, bytes, root, NULL);
+        return map_rc(me == root ? rc : copy_back(buff, bd, bytes, rc));
+    }
     if (contiguous_bytes(datatype, count, &bytes)) return map_rc(mi355x_bcast(m->engine, buff, bytes, root, NULL));
     /* derived datatype: root packs, the packed bytes are broadcast, the others unpack */
     if (!ddt_of(m, datatype)) {  /* see allgather: no rank-local fallback */
@@ -360,7 +480,6 @@ int mca_coll_mi355x_bcast(void *buff, int count, struct ompi_datatype_t *datatyp
     if (bytes == 0) return OMPI_SUCCESS;
     void *st = scratch(m, bytes);
     if (!st) return OMPI_ERR_OUT_OF_RESOURCE;
-    const int me = mi355x_comm_rank_of(comm);
     int rc = MI355X_SUCCESS;
     if (me == root) rc = stage(m, 1, buff, count, datatype, st, bytes);
     if (rc == MI355X_SUCCESS) rc = mi355x_bcast(m->engine, st, bytes, root, NULL);
@@ -1238,6 +1357,9 @@ static int component_register(void)
                  "(coll_tuned_allreduce.c:38-47); 0 = coll_tuned's fixed decision", OPAL_INFO_LVL_5, &mca_coll_mi355x_allreduce_algorithm);
     register_int("pml_hook", "Route device-buffer point-to-point on engine communicators through the engine",
                  OPAL_INFO_LVL_5, &mca_coll_mi355x_pml_hook);
+    register_int("mixed_buffers", "Let ranks mix host and device buffers in one allreduce / reduce / reduce_scatter(_block) / "
+                 "allgather / bcast (every rank votes its buffer kind; 0: every rank must use the same kind)",
+                 OPAL_INFO_LVL_5, &mca_coll_mi355x_mixed_buffers);
     return OMPI_SUCCESS;
 }
 static int component_open(void) { return OMPI_SUCCESS; }

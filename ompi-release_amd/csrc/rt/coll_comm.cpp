@@ -1555,6 +1555,44 @@ int mi355x_comm_barrier(mi355x_comm_t *c)
     drain(c);
     return barrier(c);
 }
+int mi355x_comm_vote(mi355x_comm_t *c, int device, int *any_device)
+{
+    if (!c || !any_device) return set_error(MI355X_ERR_ARG, "NULL argument");
+    *any_device = device ? 1 : 0;
+    if (c->size == 1) return MI355X_SUCCESS;
+    const uint64_t s = ++c->vote_seq;
+    Ctrl *k = c->ctrl;
+    k->slot[c->rank].vote[s % kVoteRing].store((s << 1) | (device ? 1u : 0u), std::memory_order_release);
+    if (device) return MI355X_SUCCESS;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int r = 0; r < c->size; ++r) {
+        if (r == c->rank) continue;
+        unsigned spins = 0;
+        for (;;) {
+            const uint64_t v = k->slot[r].vote[s % kVoteRing].load(std::memory_order_acquire);
+            if ((v >> 1) == s) {
+                if (v & 1u) *any_device = 1;
+                break;
+            }
+            if ((v >> 1) > s)
+                return set_error(MI355X_ERR_PEER, "rank %d is %d or more collectives ahead of rank %d", r,
+                                 kVoteRing, c->rank);
+            if (k->abort_flag.load(std::memory_order_relaxed))
+                return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
+            if (++spins > 2048) {
+                sched_yield();
+                if ((spins & 0xffff) == 0 &&
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
+                    k->abort_flag.store(1);
+                    return set_error(MI355X_ERR_TIMEOUT, "rank %d: buffer-kind vote %llu timed out waiting for rank %d",
+                                     c->rank, (unsigned long long)s, r);
+                }
+            }
+        }
+    }
+    return MI355X_SUCCESS;
+}
+
 int mi355x_comm_last_algorithm(const mi355x_comm_t *c) { return c ? c->last_alg : -1; }
 int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
 {

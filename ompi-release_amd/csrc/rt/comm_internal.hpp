@@ -41,6 +41,7 @@ inline bool debug_on()
 
 constexpr uint64_t kMagic = 0x4d49333535584331ull;  // "MI355XC1"
 constexpr int kMaxBufs = 3;
+constexpr int kVoteRing = 64;  // buffer-kind votes a rank keeps (mi355x_comm_vote)
 
 struct BufDesc {
     hipIpcMemHandle_t h;
@@ -65,6 +66,9 @@ struct alignas(64) RankSlot {
     int64_t varg[2 * kMaxRanks];  // per-peer counts / displacements of v-collectives (bytes)
     int32_t ll_ok, pad_ll;        // LL self-test result at creation (1 ok, 2 failed)
     uint64_t dev_uid;             // hash of the device's PCI bus id: ranks sharing one GPU
+    // mi355x_comm_vote: call v's entry at [v % kVoteRing] = (v << 1) | (this rank's buffers are
+    // device memory); a ring because a rank with device buffers publishes and moves on
+    std::atomic<uint64_t> vote[kVoteRing];
 };
 
 struct Ctrl {
@@ -193,6 +197,7 @@ struct mi355x_comm {
     std::shared_ptr<mi355x::LoopShared> loop;
     std::string shm_name;
     uint64_t seq = 0;
+    uint64_t vote_seq = 0;                        // mi355x_comm_vote calls made
     std::map<mi355x::HandleKey, mi355x::PeerMap> peer_maps;
     std::vector<mi355x::LocalReg> local_regs;
     void *scratch = nullptr;

@@ -126,6 +126,71 @@ def nonblocking_mixed_layouts(m, comm, oracle, rank, size, torch):
     L.mini_datatype_destroy(vec)
 
 
+def mixed_buffers(m, comm, oracle, rank, size, torch):
+    """coll/cuda lets ranks mix host and device buffers in one collective (coll_cuda_allreduce.c:
+    30-77); here rank 0 passes host memory and the others device memory to MPI_Allreduce (also in
+    place), MPI_Reduce (host root, device root), MPI_Reduce_scatter_block, MPI_Reduce_scatter,
+    MPI_Allgather (also in place) and MPI_Bcast (host root, device root).  Every rank must end in the
+    engine (rank 0 staging its buffers) with exact results; the previous (stub) component is never
+    called (checked by the caller's stub count)."""
+    L, pkg = m.lib, m.pkg
+    fdt = m.dtype_for_slot(pkg.T["FLOAT"])
+    op = m.select_op(pkg.OP["SUM"])
+    host = rank == 0
+    want = size * (size + 1) / 2
+
+    def buf(vals):
+        a = np.ascontiguousarray(vals, dtype=np.float32)
+        return (a, a.ctypes.data) if host else (lambda t: (t, t.data_ptr()))(torch.from_numpy(a.copy()).cuda())
+
+    def val(b):
+        return b if host else b.cpu().numpy()
+
+    n = 10_007
+    x, px = buf(np.full(n, rank + 1))
+    y, py = buf(np.zeros(n))
+    torch.cuda.synchronize()
+    assert L.mini_allreduce(comm, px, py, n, fdt, op) == 0
+    assert (val(y) == want).all(), "mixed allreduce"
+    z, pz = buf(np.full(n, rank + 1))
+    torch.cuda.synchronize()
+    assert L.mini_allreduce(comm, 1, pz, n, fdt, op) == 0  # MPI_IN_PLACE
+    assert (val(z) == want).all(), "mixed allreduce in place"
+    for root in (0, size - 1):
+        r, pr = buf(np.zeros(n))
+        torch.cuda.synchronize()
+        assert L.mini_reduce(comm, px, pr if rank == root else None, n, fdt, op, root) == 0
+        if rank == root:
+            assert (val(r) == want).all(), ("mixed reduce", root)
+    rc = 777
+    s, ps = buf(np.full(rc * size, rank + 1))
+    o, po = buf(np.zeros(rc))
+    torch.cuda.synchronize()
+    assert L.mini_reduce_scatter_block(comm, ps, po, rc, fdt, op) == 0
+    assert (val(o) == want).all(), "mixed reduce_scatter_block"
+    counts = [100 + 37 * q for q in range(size)]
+    v, pv = buf(np.full(sum(counts), rank + 1))
+    w, pw = buf(np.zeros(counts[rank]))
+    torch.cuda.synchronize()
+    assert L.mini_reduce_scatter(comm, pv, pw, (ctypes.c_int * size)(*counts), fdt, op) == 0
+    assert (val(w) == want).all(), "mixed reduce_scatter"
+    g, pg = buf(np.zeros(n * size))
+    torch.cuda.synchronize()
+    assert L.mini_allgather(comm, px, n, fdt, pg, n, fdt) == 0
+    gv = val(g)
+    assert all((gv[q * n:(q + 1) * n] == q + 1).all() for q in range(size)), "mixed allgather"
+    gi, pgi = buf(np.concatenate([np.full(n, q + 1 if q == rank else -1) for q in range(size)]))
+    torch.cuda.synchronize()
+    assert L.mini_allgather(comm, 1, 0, fdt, pgi, n, fdt) == 0  # MPI_IN_PLACE
+    gv = val(gi)
+    assert all((gv[q * n:(q + 1) * n] == q + 1).all() for q in range(size)), "mixed allgather in place"
+    for root in (0, size - 1):
+        b, pb = buf(np.full(n, 5 + root if rank == root else -1))
+        torch.cuda.synchronize()
+        assert L.mini_bcast(comm, pb, n, fdt, root) == 0
+        assert (val(b) == 5 + root).all(), ("mixed bcast", root)
+
+
 def nonblocking(m, comm, oracle, rank, size, torch, ptrs):
     pkg = m.pkg
     code, slot = pkg.OP["SUM"], pkg.T["DOUBLE"]
@@ -570,6 +635,7 @@ def main():
     # together, then MPI_Wait on each (requests progressed by the component's opal_progress callback)
     nonblocking(m, comm, oracle, rank, size, torch, ptrs)
     nonblocking_mixed_layouts(m, comm, oracle, rank, size, torch)
+    mixed_buffers(m, comm, oracle, rank, size, torch)
     # derived datatypes through the GPU convertor: bcast of a vector type ...
     derived_bcast(m, comm, oracle, rank, size, torch)
     derived_allgather(m, comm, oracle, rank, size, torch)
