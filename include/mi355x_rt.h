@@ -323,8 +323,10 @@ int mi355x_ddt_nruns(const mi355x_ddt_t *d);
 int mi355x_ddt_tune(int unroll_pack, int unroll_unpack, int threads, int nontemporal);
 /* which pack/unpack kernels may run: 2 (default) the row kernel for every one-run-per-block
  * layout, with the widest slot (16/8/4/2/1 B) its addresses and window allow, and the unit
- * kernel (LDS-staged run tables, W-byte units) for run lists of up to 4096 runs; 1 the row kernel
- * with 16-B slots only; 0 neither (the general kernel for everything; A/B measurement, tests) */
+ * kernel (LDS-staged run tables; 16-B packed slots over 8- or 4-B aligned runs when the packed
+ * side is 16-B aligned, else W-byte units) for run lists of up to 4096 runs; 3 as 2 with W-byte
+ * units only; 1 the row kernel with 16-B slots only; 0 neither (the general kernel for
+ * everything; A/B measurement, tests) */
 int mi355x_ddt_tune_rows(int mode);
 /* pack packed bytes [pos, pos+bytes) of `count` instances at device `base` into `dst`
  * (replaces opal_convertor_set_position + opal_convertor_pack on a CUDA convertor,

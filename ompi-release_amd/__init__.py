@@ -546,7 +546,8 @@ def ddt_tune(unroll_pack: int = 0, unroll_unpack: int = 0, threads: int = 0, non
 
 
 def ddt_tune_rows(mode: int) -> None:
-    """which layouts take the row pack/unpack kernel: 2 any slot width, 1 16-B only, 0 none"""
+    """pack/unpack kernel choice (mi355x_ddt_tune_rows): 2 default, 3 unit kernel with W-byte units
+    only, 1 16-B row kernel only, 0 the general kernel only"""
     check(rt().mi355x_ddt_tune_rows(mode), "mi355x_ddt_tune_rows")
 
 

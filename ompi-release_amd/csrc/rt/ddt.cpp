@@ -283,7 +283,7 @@ int mi355x_ddt_tune(int unroll_pack, int unroll_unpack, int threads, int nontemp
 
 int mi355x_ddt_tune_rows(int mode)
 {
-    if (mode < 0 || mode > 2) return set_error(MI355X_ERR_ARG, "row-kernel mode must be 0, 1 or 2");
+    if (mode < 0 || mode > 3) return set_error(MI355X_ERR_ARG, "row-kernel mode must be 0..3");
     ddt_tune().rows = mode;
     return MI355X_SUCCESS;
 }

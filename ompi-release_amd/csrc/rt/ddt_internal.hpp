@@ -30,7 +30,10 @@ struct DdtTune {
     int unroll_unpack = 2;
     int threads = 256;
     int nontemporal = -1;
-    int rows = 2;  // mi355x_ddt_tune_rows: 2 row kernel any slot width + unit kernel, 1 16-B rows only, 0 none
+    // mi355x_ddt_tune_rows: 2 row kernel any slot width + unit kernel (16-B packed slots over 8/4-B
+    // aligned runs where the packed side allows), 3 the same with W-byte units only, 1 16-B rows
+    // only, 0 neither
+    int rows = 2;
 };
 DdtTune &ddt_tune();
 

@@ -466,6 +466,7 @@ struct UnitArgs {
 
 constexpr int kUnitMaxRuns = 4096;   // LDS: 12 B per run -> 48 KiB
 constexpr int kUnitU = 4;            // units per lane per pass
+constexpr int kWideRunUnits = 8;     // wide slots only for runs this long on average
 
 template <bool PACK, bool CSUM, int W>
 __global__ __launch_bounds__(256) void k_ddt_units(UnitArgs a, CsumSink csum)
@@ -516,6 +517,104 @@ __global__ __launch_bounds__(256) void k_ddt_units(UnitArgs a, CsumSink csum)
     if constexpr (CSUM) block_sum_store(acc, csum);
 }
 
+// packed unit o of a block (o < units per block) -> its run, by binary search in the LDS table
+__device__ __forceinline__ int unit_run(const uint32_t *spfx, int nruns, uint32_t o)
+{
+    int lo = 0, hi = nruns - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (spfx[mid] <= o) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// Wide slots: the packed side is 16-B aligned but the memory side only W-aligned (W = 8 or 4: a
+// triangle of doubles, runs of 3 floats): a lane moves a 16-B packed slot = 16 / W units; when the
+// slot lies inside one run the memory side is one 16-B access at a W-aligned address (global
+// dwordx4 needs only dword alignment), else the units go one by one.  The run tables are in LDS as
+// in k_ddt_units (units of W).
+template <bool PACK, bool CSUM, int W>
+__global__ __launch_bounds__(256) void k_ddt_units_wide(UnitArgs a, CsumSink csum)
+{
+    typedef typename SlotT<W>::type S;
+    constexpr uint32_t UPS = 16 / W;  // units per slot
+    extern __shared__ int64_t unit_lds[];
+    int64_t *sdisp = unit_lds;
+    uint32_t *spfx = reinterpret_cast<uint32_t *>(unit_lds + a.nruns);
+    for (int r = threadIdx.x; r < a.nruns; r += blockDim.x) {
+        sdisp[r] = a.disp[r];
+        spfx[r] = (uint32_t)(a.pfx[r] >> a.lw);
+    }
+    __syncthreads();
+    const uint32_t blk_u = a.per_blk.d, nblk = a.per_inst.d / a.per_blk.d, nslots = a.nunits / UPS;
+    const uint32_t tpb = blockDim.x, stride = gridDim.x * tpb * kUnitU;
+    unsigned acc = 0;
+    for (uint32_t base = blockIdx.x * tpb * kUnitU + threadIdx.x; base < nslots; base += stride) {
+        u32x4d v[kUnitU];
+        char *mp[kUnitU];   // the slot's memory address when it lies inside one run, else NULL
+        bool live[kUnitU];
+#pragma unroll
+        for (int u = 0; u < kUnitU; ++u) {
+            const uint32_t i = base + (uint32_t)u * tpb;
+            live[u] = i < nslots;
+            mp[u] = nullptr;
+            if (!live[u]) continue;
+            uint32_t q = a.first + i * UPS;
+            uint32_t k = fdiv(q, a.per_inst);
+            const uint32_t rem = q - k * a.per_inst.d;
+            uint32_t j = fdiv(rem, a.per_blk);
+            uint32_t o = rem - j * blk_u;
+            int r = unit_run(spfx, a.nruns, o);
+            o -= spfx[r];
+            const uint32_t rl = (r + 1 < a.nruns ? spfx[r + 1] : blk_u) - spfx[r];
+            char *m0 = a.mem + (int64_t)k * a.extent + (int64_t)j * a.stride + sdisp[r] + (int64_t)o * W;
+            if (o + UPS <= rl) {
+                mp[u] = m0;
+                v[u] = *reinterpret_cast<const u32x4d *>(PACK ? m0 : a.packed + (size_t)i * 16);
+                continue;
+            }
+            // the slot crosses a run boundary: unit by unit
+            S part[UPS];
+            const S *pk = reinterpret_cast<const S *>(a.packed + (size_t)i * 16);
+#pragma unroll
+            for (uint32_t t = 0; t < UPS; ++t) {
+                char *mt = a.mem + (int64_t)k * a.extent + (int64_t)j * a.stride + sdisp[r] + (int64_t)o * W;
+                if (PACK) part[t] = *reinterpret_cast<const S *>(mt);
+                else *reinterpret_cast<S *>(mt) = pk[t];
+                if (++o == (r + 1 < a.nruns ? spfx[r + 1] : blk_u) - spfx[r]) {
+                    o = 0;
+                    if (++r == a.nruns) {
+                        r = 0;
+                        if (++j == nblk) {
+                            j = 0;
+                            ++k;
+                        }
+                    }
+                }
+            }
+            if (PACK) __builtin_memcpy(&v[u], part, 16);
+            else v[u] = *reinterpret_cast<const u32x4d *>(a.packed + (size_t)i * 16);
+        }
+#pragma unroll
+        for (int u = 0; u < kUnitU; ++u) {
+            if (!live[u]) continue;
+            const uint32_t i = base + (uint32_t)u * tpb;
+            if (PACK) *reinterpret_cast<u32x4d *>(a.packed + (size_t)i * 16) = v[u];
+            else if (mp[u]) *reinterpret_cast<u32x4d *>(mp[u]) = v[u];
+            if constexpr (CSUM) acc += slot_csum<16>(v[u], 0);
+        }
+    }
+    if constexpr (CSUM) block_sum_store(acc, csum);
+}
+
+template <bool PACK, bool CSUM>
+static void launch_units_wide(int w, const UnitArgs &a, unsigned blocks, size_t lds, const CsumSink &part, hipStream_t s)
+{
+    if (w == 8) hipLaunchKernelGGL((k_ddt_units_wide<PACK, CSUM, 8>), dim3(blocks), dim3(256), lds, s, a, part);
+    else hipLaunchKernelGGL((k_ddt_units_wide<PACK, CSUM, 4>), dim3(blocks), dim3(256), lds, s, a, part);
+}
+
 template <bool PACK, bool CSUM>
 static void launch_units_w(int w, const UnitArgs &a, unsigned blocks, size_t lds, const CsumSink &part, hipStream_t s)
 {
@@ -555,7 +654,15 @@ static int launch_ddt_units(const DdtDev &d, bool pack, void *mem, void *packed,
     a.per_blk = make_fastdiv((uint32_t)(d.blk_bytes / w));
     a.first = (uint32_t)(pos / w);
     a.nunits = (uint32_t)(bytes / w);
-    const uint64_t per = 256u * kUnitU;
+    // wide slots: the packed side 16-B aligned, the memory side 4- or 8-B, pack only and runs of at
+    // least kWideRunUnits units on average (mode 3 keeps W-byte units).  Measured (256 MiB packed,
+    // profiles/r02_legs_ddt_wide.jsonl): triangle of doubles pack 4.70 vs 4.24 TB/s, but its unpack
+    // 3.53 vs 3.73 (16-B stores at 8-B alignment) and 7-run floats pack 3.18 vs 3.30 (short runs:
+    // most slots cross a run boundary)
+    const uint64_t pk_bits = (uintptr_t)packed | (uint64_t)pos | (uint64_t)bytes;
+    const bool wide = ddt_tune().rows == 2 && pack && (w == 8 || w == 4) && (pk_bits & 15) == 0 &&
+                      (uint64_t)(d.blk_bytes / w) >= (uint64_t)kWideRunUnits * (uint64_t)d.nruns;
+    const uint64_t per = 256u * kUnitU * (wide ? 16u / (unsigned)w : 1u);
     uint64_t blocks = (a.nunits + per - 1) / per;
     const uint64_t cap = (uint64_t)8 * (uint64_t)device_cu_count();
     if (blocks > cap) blocks = cap;
@@ -564,7 +671,15 @@ static int launch_ddt_units(const DdtDev &d, bool pack, void *mem, void *packed,
     Csum part;
     int rc = part.get(csum, (unsigned)blocks);
     if (rc) return rc;
-    if (pack) {
+    if (wide) {
+        if (pack) {
+            if (csum) launch_units_wide<true, true>(w, a, (unsigned)blocks, lds, part.sink, s);
+            else launch_units_wide<true, false>(w, a, (unsigned)blocks, lds, part.sink, s);
+        } else {
+            if (csum) launch_units_wide<false, true>(w, a, (unsigned)blocks, lds, part.sink, s);
+            else launch_units_wide<false, false>(w, a, (unsigned)blocks, lds, part.sink, s);
+        }
+    } else if (pack) {
         if (csum) launch_units_w<true, true>(w, a, (unsigned)blocks, lds, part.sink, s);
         else launch_units_w<true, false>(w, a, (unsigned)blocks, lds, part.sink, s);
     } else {

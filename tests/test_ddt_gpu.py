@@ -313,14 +313,16 @@ UNIT_CASES = [  # run lists (several runs per block): (blocklens, disps, elem si
     ([1, 3, 2, 7, 1, 1, 4], [0, 2, 9, 13, 25, 27, 40], 4, 300),
     ([3, 1, 5, 2], [1, 6, 9, 17], 2, 500),
     ([2, 5, 1], [0, 4, 13], 1, 900),
+    ([37, 50, 23], [1, 41, 97], 4, 400),  # long runs of floats at odd float offsets: wide slots, W = 4
 ]
 
 
 @pytest.mark.parametrize("case", range(len(UNIT_CASES)))
 def test_unit_kernel(gpu, pkg, oracle, case):
-    """the unit kernel (run tables staged in LDS, W-byte units) against the oracle for indexed run
-    lists, windows at element multiples and at odd bytes, with checksums; mode 0 (the general
-    kernel) gives the same bytes"""
+    """the unit kernel (run tables staged in LDS; 16-B packed slots over 8/4-B aligned runs where
+    the window allows, else W-byte units) against the oracle for indexed run lists, windows at
+    element multiples, at 16-B multiples and at odd bytes, with checksums; mode 3 (W-byte units
+    only) and mode 0 (the general kernel) give the same bytes"""
     torch = gpu
     bl, dp, esz, count = UNIT_CASES[case]
     n = len(bl)
@@ -337,9 +339,10 @@ def test_unit_kernel(gpu, pkg, oracle, case):
     want_mem = np.zeros(span, dtype=np.uint8)
     oracle.oracle_ddt_unpack(od, count, want_mem.ctypes.data, 0, full.ctypes.data, total)
     cuts = sorted(set([0, total] + [int(x) // esz * esz for x in rng.integers(0, total, 6)] +
+                      [int(x) // 16 * 16 for x in rng.integers(0, total, 6)] +
                       [int(x) for x in rng.integers(0, total, 2)]))
     try:
-        for mode in (2, 0):
+        for mode in (2, 3, 0):
             pkg.ddt_tune_rows(mode)
             out = torch.zeros(total + 64, dtype=torch.uint8, device="cuda")
             cs = sum(d.pack(count, dbase.data_ptr(), a, out.data_ptr() + a, b - a, checksum=True)

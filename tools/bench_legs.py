@@ -203,18 +203,19 @@ def leg_ddt_runs(pkg, torch, args, emit):
         size = count * d.size
         alg = 2 * size
         outs = {}
-        for mode in (2, 0):
+        for mode in (2, 3, 0):
             pkg.ddt_tune_rows(mode)
             for dirn, fn in (("pack", lambda s: d.pack(count, x.data_ptr(), 0, p.data_ptr(), size, s)),
                              ("unpack", lambda s: d.unpack(count, y.data_ptr(), 0, p.data_ptr(), size, s))):
                 avg, med = timed(torch, fn, args.steps, args.warmup)
-                emit({"leg": "ddt_runs_" + dirn, "type": name, "kernel": "units" if mode == 2 else "general",
+                emit({"leg": "ddt_runs_" + dirn, "type": name, "kernel": {2: "units", 3: "units_w", 0: "general"}[mode],
                       "count": count, "alg_bytes": alg, "kernel_avg_ms": round(avg, 5), "kernel_med_ms": round(med, 5),
                       "achieved_GBs": round(alg / (avg * 1e-3) / 1e9, 1),
                       "frac": round(alg / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
             outs[mode] = (p.clone(), y.clone())
             y.zero_()
-        assert torch.equal(outs[2][0], outs[0][0]) and torch.equal(outs[2][1], outs[0][1]), name
+        for mode in (2, 3):
+            assert torch.equal(outs[mode][0], outs[0][0]) and torch.equal(outs[mode][1], outs[0][1]), (name, mode)
         pkg.ddt_tune_rows(2)
         del x, p, y, outs
 
