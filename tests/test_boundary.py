@@ -258,7 +258,7 @@ def test_pml_hook_install_and_close():
 
 
 def test_mca_variables_registered(monkeypatch):
-    """coll_mi355x_priority / _allreduce_algorithm / _pml_hook and op_hip_priority go through
+    """coll_mi355x_priority / _allreduce_algorithm / _pml_hook / _mixed_buffers and op_hip_priority go through
     mca_base_component_var_register when the process provides it (here: the harness's variable
     system standing in for libopen-pal, which reads OMPI_MCA_<name>); the stored value is what
     comm_query / op_query then use"""
@@ -277,6 +277,7 @@ def test_mca_variables_registered(monkeypatch):
         assert names["coll_mi355x_priority"] == 77 and prio.value == 77
         assert names["op_hip_priority"] == 33 and oprio.value == 33
         assert "coll_mi355x_allreduce_algorithm" in names and names["coll_mi355x_pml_hook"] == 1
+        assert names["coll_mi355x_mixed_buffers"] == 1  # mixed host / device buffers: on by default
         _coll_env(monkeypatch)
         comm = L.mini_comm_create(0, 4, 17)
         mod, p = _comm_query(m, comm)
