@@ -8,7 +8,9 @@ Metric (BASELINE.json): "MPI_Allreduce busbw GB/s (1 GiB fp32, np=8) + op/hip re
   N > 1  (configs[2] at 1 GiB): MPI_Allreduce MPI_SUM fp32 1 GiB per rank through coll/mi355x's
          engine over IPC-mapped peers; value = busbw = (S/t) x 2(n-1)/n, max time over ranks.
 
-Launch: `python bench.py --gpus 1 --steps K --warmup W`; N > 1 under torch.distributed.run.
+Launch: `python bench.py --gpus N --steps K --warmup W`.  N > 1 runs one rank per GPU: under
+torch.distributed.run as the driver launches it, or -- with no launcher environment -- bench.py starts
+torch.distributed.run itself as a child process and forwards rank 0's line (spawn_ranks).
 Rank 0 prints ONE JSON line.  Timed region = exactly K steps between barrier+synchronize pairs.
 """
 from __future__ import annotations
@@ -162,6 +164,34 @@ def bench_op(args, pkg, torch):
     }
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(nproc: int, script: str, script_args: list[str]) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: start the N ranks the way the driver
+    does (`python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1`),
+    as a CHILD process -- never an exec, and before this process has touched the GPU -- forward rank
+    0's JSON line to stdout and return the child's exit code.  mpirun launches its own ranks the
+    same way (orte/tools/orterun/orterun.c:611)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", script, *script_args]
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, bufsize=1)
+    for line in proc.stdout:  # rank 0 prints the one JSON line; anything else is progress
+        s = line.strip()
+        if s.startswith("{") and '"metric"' in s:
+            print(s, flush=True)
+        elif s:
+            print(s, file=sys.stderr, flush=True)
+    return proc.wait()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -175,6 +205,10 @@ def main():
     ap.add_argument("--legs-timeout", type=float, default=300.0,
                     help="N > 1: seconds after which the legs are abandoned and the headline printed")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start the ranks ourselves (child process, nothing GPU-side touched yet)
+        sys.exit(spawn_ranks(args.gpus, str(pathlib.Path(__file__).resolve()), sys.argv[1:]))
 
     import torch
     pkg = load_pkg()

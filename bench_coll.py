@@ -179,40 +179,6 @@ def extra_legs(args, pkg, torch, comm, world, rank, dev, legs, key):
     except Exception as e:
         legs["sendrecv_ring_256MiB"] = {"error": repr(e)[:300]}
     torch.cuda.empty_cache()
-    # xGMI link bandwidth (the busbw denominator, BASELINE.md §2: "must be measured"): ranks 0 and
-    # 1 alone, each pulling 256 MiB from the other over their one link (both directions at once)
-    if torch.cuda.device_count() >= world:
-        _log(rank, "leg xgmi_link")
-        try:
-            nb = 256 << 20
-            if rank < 2:
-                pair = pkg.Comm.create(f"{key}_pair", rank, 2, dev.index)
-                pair.set("TIMEOUT_S", 120)
-                src = torch.full((nb,), rank + 1, dtype=torch.uint8, device=dev)
-                dst = torch.empty((2 * nb,), dtype=torch.uint8, device=dev)
-                for _ in range(2):
-                    pair.allgather(src.data_ptr(), dst.data_ptr(), nb)
-                torch.cuda.synchronize()
-                pair.barrier()
-                t0 = time.perf_counter()
-                for _ in range(5):
-                    pair.allgather(src.data_ptr(), dst.data_ptr(), nb)
-                torch.cuda.synchronize()
-                t_l = (time.perf_counter() - t0) / 5
-                ok_l = int(dst[:nb].max()) == 1 and int(dst[nb:].min()) == 2
-                pair.destroy()
-                del src, dst
-            else:
-                t_l, ok_l = 0.0, True
-            t = torch.tensor([t_l, 0.0 if ok_l else 1.0], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            legs["xgmi_link_pull_256MiB"] = {"ms": round(float(t[0]) * 1e3, 3),
-                                             "GBs_per_direction": round(nb / float(t[0]) / 1e9, 2),
-                                             "exact": float(t[1]) == 0.0,
-                                             "note": "ranks 0,1 only; each pulls 256 MiB from the other"}
-        except Exception as e:
-            legs["xgmi_link_pull_256MiB"] = {"error": repr(e)[:300]}
-        torch.cuda.empty_cache()
     # comparison point only (BASELINE north star): RCCL's allreduce on the same device buffers,
     # through torch.distributed's "nccl" backend (= RCCL on ROCm).  Needs one GPU per rank.
     if torch.cuda.device_count() >= world:
@@ -235,14 +201,57 @@ def extra_legs(args, pkg, torch, comm, world, rank, dev, legs, key):
     return legs
 
 
+def measure_link(pkg, torch, dist, world, rank, dev, key):
+    """xGMI link bandwidth, the roofline denominator (SURVEY.md §8(d) C3 and BASELINE.md §2: "must
+    be measured"): ranks 0 and 1 alone, each pulling 256 MiB from the other over their one link
+    (both directions at once) through the engine's own copy kernel.  Every rank returns the same
+    dict (max over ranks)."""
+    nb = 256 << 20
+    try:
+        if rank < 2:
+            pair = pkg.Comm.create(f"{key}_pair", rank, 2, dev.index)
+            pair.set("TIMEOUT_S", 120)
+            src = torch.full((nb,), rank + 1, dtype=torch.uint8, device=dev)
+            dst = torch.empty((2 * nb,), dtype=torch.uint8, device=dev)
+            for _ in range(2):
+                pair.allgather(src.data_ptr(), dst.data_ptr(), nb)
+            torch.cuda.synchronize()
+            pair.barrier()
+            t0 = time.perf_counter()
+            for _ in range(5):
+                pair.allgather(src.data_ptr(), dst.data_ptr(), nb)
+            torch.cuda.synchronize()
+            t_l = (time.perf_counter() - t0) / 5
+            ok_l = int(dst[:nb].max()) == 1 and int(dst[nb:].min()) == 2
+            pair.destroy()
+            del src, dst
+        else:
+            t_l, ok_l = 0.0, True
+        err = 0.0
+    except Exception:  # noqa: BLE001 -- reported as an error entry, the spec peak is used then
+        t_l, ok_l, err = 0.0, False, 1.0
+    t = torch.tensor([t_l, 0.0 if ok_l else 1.0, err], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    torch.cuda.empty_cache()
+    if t[2] > 0 or t[0] <= 0:
+        return {"error": "link measurement failed on some rank"}
+    return {"ms": round(float(t[0]) * 1e3, 3), "GBs_per_direction": round(nb / float(t[0]) / 1e9, 2),
+            "exact": float(t[1]) == 0.0, "note": "ranks 0,1 only; each pulls 256 MiB from the other"}
+
+
 def run(args, pkg, torch):
     import torch.distributed as dist
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    if "WORLD_SIZE" not in os.environ or "MASTER_ADDR" not in os.environ:
+        # bench.py --gpus N spawns its ranks itself (bench.spawn_ranks); reaching here without the
+        # launcher's environment means this module was driven some other way
+        raise SystemExit("bench_coll needs a launcher environment (WORLD_SIZE, MASTER_ADDR): "
+                         "run `python bench.py --gpus N` or torch.distributed.run")
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     if world < 2:
-        raise SystemExit("bench_coll needs WORLD_SIZE >= 2 (launch under torch.distributed.run)")
+        raise SystemExit("bench_coll needs WORLD_SIZE >= 2")
     local = local % max(1, torch.cuda.device_count())  # one-GPU rehearsal: ranks share device 0
     torch.cuda.set_device(local)
     if not dist.is_initialized():
@@ -324,9 +333,13 @@ def run(args, pkg, torch):
     fold_xgmi = xgmi_bytes / (p1 * 1e-3) / 1e9
     fold_hbm = hbm_bytes / (p1 * 1e-3) / 1e9
     kname = "k_pipe_allreduce (fold + pulls, one launch)" if pipe else "k_fold (allreduce phase 1)"
-    peak_all = (world - 1) * XGMI_LINK_DIR_GBS
     # ranks sharing one GPU (a rehearsal on a 1-GPU box): the traffic never leaves local HBM
     shared = torch.cuda.device_count() < world
+    # the denominator: the measured per-direction link rate x (n-1) links; the spec rate rides along
+    link = None if shared else measure_link(pkg, torch, dist, world, rank, dev, key)
+    link_gbs = link.get("GBs_per_direction") if link and link.get("exact") else None
+    peak_spec = (world - 1) * XGMI_LINK_DIR_GBS
+    peak_all = (world - 1) * link_gbs if link_gbs else peak_spec
     res = {
         "metric": "MPI_Allreduce busbw GB/s (1 GiB fp32, np=8) + op/hip reduce HBM GB/s",
         "value": round(busbw, 2),
@@ -354,9 +367,13 @@ def run(args, pkg, torch):
                       "alg_bytes_per_launch": int(xgmi_bytes), "phase2_ms": round(p2, 4),
                       "busbw_frac": round(busbw / peak_all, 4),
                       # against one ring (one link per direction) as well as all n-1
-                      "busbw_frac_ring1": round(busbw / XGMI_LINK_DIR_GBS, 4),
-                      "peak_note": f"(n-1) links x {XGMI_LINK_DIR_GBS} GB/s per direction (spec); achieved = "
-                                   "the remote bytes one launch reads over xGMI / its event time"} if not shared else
+                      "busbw_frac_ring1": round(busbw / (link_gbs or XGMI_LINK_DIR_GBS), 4),
+                      "peak_spec": round(peak_spec, 1), "frac_spec": round(fold_xgmi / peak_spec, 4),
+                      "link": link,
+                      "peak_note": (f"(n-1) links x {link_gbs} GB/s per direction, measured (link.GBs_per_direction)"
+                                    if link_gbs else f"(n-1) links x {XGMI_LINK_DIR_GBS} GB/s per direction (spec; "
+                                    "the link measurement failed)") + "; achieved = the remote bytes one launch "
+                                   "reads over xGMI / its event time"} if not shared else
                      {"bound": "hbm", "achieved": round(fold_hbm, 2), "peak": 8000.0, "unit": "GB/s",
                       "frac": round(fold_hbm / 8000.0, 4), "traffic": pmc_traffic(pipe, shared=True, world=world),
                       "kernel": kname, "kernel_avg_ms": round(p1, 4),
