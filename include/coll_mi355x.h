@@ -97,11 +97,14 @@ int mca_coll_mi355x_scan(void *sbuf, void *rbuf, int count, struct ompi_datatype
 int mca_coll_mi355x_exscan(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
                            struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
 
-/* Device point-to-point through the PML slot: installed over the selected PML's table
- * (`mca_pml`, pml.h:558) when the component is initialised, the way pml/v parasites the host PML
- * (pml_v_component.c:110-131).  Device buffers on communicators with the engine go to the engine
- * (what ob1's CUDA path does over smcuda, pml_ob1_cuda.c:52-210); everything else to the saved
- * entries.  OMPI_MCA_coll_mi355x_pml_hook=0 leaves the PML untouched. */
+/* Point-to-point through the PML slot: installed over the selected PML's table (`mca_pml`,
+ * pml.h:558) when the component is initialised, the way pml/v parasites the host PML
+ * (pml_v_component.c:110-131).  On a communicator with the engine EVERY point-to-point call goes to
+ * the engine -- device and host buffers, every send mode, persistent and matched-probe requests --
+ * so all of its messages share one matching queue, as ob1's do (pml_ob1_cuda.c:52-100,
+ * pml_ob1_recvreq.c:647-663, pml_ob1_recvfrag.c:487); other communicators keep the saved entries.
+ * Each function has the signature of the pml.h:146-470 slot it fills.
+ * OMPI_MCA_coll_mi355x_pml_hook=0 leaves the PML untouched. */
 int mca_coll_mi355x_pml_isend(void *buf, size_t count, struct ompi_datatype_t *dt, int dst, int tag,
                               mca_pml_base_send_mode_t mode, struct ompi_communicator_t *comm,
                               ompi_request_t **request);
@@ -114,12 +117,26 @@ int mca_coll_mi355x_pml_recv(void *buf, size_t count, struct ompi_datatype_t *dt
 int mca_coll_mi355x_pml_iprobe(int src, int tag, struct ompi_communicator_t *comm, int *matched,
                                ompi_status_public_t *status);
 int mca_coll_mi355x_pml_probe(int src, int tag, struct ompi_communicator_t *comm, ompi_status_public_t *status);
+int mca_coll_mi355x_pml_improbe(int src, int tag, struct ompi_communicator_t *comm, int *matched,
+                                struct ompi_message_t **message, ompi_status_public_t *status);
+int mca_coll_mi355x_pml_mprobe(int src, int tag, struct ompi_communicator_t *comm, struct ompi_message_t **message,
+                               ompi_status_public_t *status);
+int mca_coll_mi355x_pml_imrecv(void *buf, size_t count, struct ompi_datatype_t *dt, struct ompi_message_t **message,
+                               ompi_request_t **request);
+int mca_coll_mi355x_pml_mrecv(void *buf, size_t count, struct ompi_datatype_t *dt, struct ompi_message_t **message,
+                              ompi_status_public_t *status);
+int mca_coll_mi355x_pml_isend_init(void *buf, size_t count, struct ompi_datatype_t *dt, int dst, int tag,
+                                   mca_pml_base_send_mode_t mode, struct ompi_communicator_t *comm,
+                                   ompi_request_t **request);
+int mca_coll_mi355x_pml_irecv_init(void *buf, size_t count, struct ompi_datatype_t *dt, int src, int tag,
+                                   struct ompi_communicator_t *comm, ompi_request_t **request);
+int mca_coll_mi355x_pml_start(size_t count, ompi_request_t **requests);
 
 /* MCA parameters coll_mi355x_<name>: registered with mca_base_component_var_register when the
  * component is loaded by an Open MPI that provides it, else read from OMPI_MCA_coll_mi355x_<name> */
 extern int mca_coll_mi355x_priority;            /* 90 */
 extern int mca_coll_mi355x_allreduce_algorithm; /* 0 = tuned decision, else coll_tuned numbering */
-extern int mca_coll_mi355x_pml_hook;            /* 1 = device point-to-point through the engine */
+extern int mca_coll_mi355x_pml_hook;            /* 1 = point-to-point on engine communicators through the engine */
 extern int mca_coll_mi355x_mixed_buffers;       /* 1 = ranks may mix host and device buffers in a call */
 
 #ifdef __cplusplus

@@ -261,20 +261,28 @@ int mi355x_request_test(mi355x_request_t *req, int *done);
 int mi355x_request_wait(mi355x_request_t *req);
 int mi355x_request_free(mi355x_request_t *req);
 
-/* ---------------------------------------------------------------- device point-to-point */
-/* MPI_Send / MPI_Recv / MPI_Isend / MPI_Irecv / MPI_Sendrecv / MPI_Iprobe on device buffers
- * between the ranks of a communicator.  Replaces, for device memory, ob1's RGET rendezvous over
- * btl/smcuda: mca_pml_ob1_send_request_start_cuda (pml_ob1_cuda.c:52-100) announces the
- * registered buffer, the receiver matches it (ob1 matching: per-source order, posted receives in
- * posting order, MI355X_ANY_SOURCE / MI355X_ANY_TAG) and pulls it the way
- * mca_btl_smcuda_get_cuda (btl_smcuda.c:1083-1168) does, then the FIN completes the send.
+/* ---------------------------------------------------------------- point-to-point */
+/* MPI_Send / MPI_Recv / MPI_Isend / MPI_Irecv / MPI_Sendrecv / MPI_Iprobe / MPI_Improbe +
+ * MPI_Imrecv between the ranks of a communicator, on device AND host buffers, in ONE matching
+ * queue per communicator (ob1's: per-source order, posted receives in posting order,
+ * MI355X_ANY_SOURCE; MI355X_ANY_TAG matches tags >= 0 only, pml_ob1_recvfrag.c:487; negative
+ * system tags are allowed).  A device payload travels as ob1's RGET over btl/smcuda does: the
+ * sender announces its registered buffer (mca_pml_ob1_send_request_start_cuda,
+ * pml_ob1_cuda.c:52-100), the receiver matches and pulls it over xGMI (mca_btl_smcuda_get_cuda,
+ * btl_smcuda.c:1083-1168), the FIN completes the send.  A host payload -- and a device payload of
+ * at most 4 KiB (the sm/smcuda eager limit, btl_sm_component.c:244) -- is copied into the
+ * sender's shared-memory arena, as the sm BTL copies fragments; the receiver copies it out (into
+ * host memory, or to the device).  Either side may be host or device memory (ob1 decides the
+ * convertor per request on each side, pml_ob1_cuda.c:52-100 / pml_ob1_recvreq.c:647-663).
  * `ddt` NULL: `count` contiguous bytes; else `count` instances of the datatype (the GPU
- * convertor packs / unpacks non-contiguous layouts).  Buffers are read / written once the
- * caller's prior work on `stream` is done.  Blocking sends complete when the receiver has read
- * the data (rendezvous).  A receive longer than its buffer gets the first bytes, status.bytes =
- * the message size, status.error = MI355X_ERR_TRUNCATE (pml_ob1_recvreq.h:172-180); the blocking
- * forms then return MI355X_ERR_TRUNCATE.  Requests: mi355x_request_test / wait / free above
- * (they drive progress); mi355x_p2p_progress is the opal_progress hook. */
+ * convertor on device memory, the host convertor on host memory).  Buffers are read / written
+ * once the caller's prior work on `stream` is done.  Completion of a send: messages of at most
+ * 4 KiB and buffered sends complete once copied (eager); synchronous sends and larger messages
+ * when the receiver has the data (rendezvous).  A receive longer than its buffer gets the first
+ * bytes, status.bytes = the message size, status.error = MI355X_ERR_TRUNCATE
+ * (pml_ob1_recvreq.h:172-180); the blocking forms then return MI355X_ERR_TRUNCATE.  Requests:
+ * mi355x_request_test / wait / free above (they drive progress); mi355x_p2p_progress is the
+ * opal_progress hook. */
 #define MI355X_ANY_SOURCE (-1)   /* MPI_ANY_SOURCE, mpi.h.in:415 */
 #define MI355X_PROC_NULL  (-2)   /* MPI_PROC_NULL,  mpi.h.in:416 */
 #define MI355X_ANY_TAG    (-1)   /* MPI_ANY_TAG,    mpi.h.in:418 */
@@ -297,6 +305,34 @@ int mi355x_sendrecv(mi355x_comm_t *comm, const void *sbuf, size_t scount, const 
 int mi355x_iprobe(mi355x_comm_t *comm, int source, int tag, int *flag, mi355x_status_t *status);
 int mi355x_p2p_progress(mi355x_comm_t *comm);
 int mi355x_request_get_status(const mi355x_request_t *req, mi355x_status_t *status);
+/* send modes: mca_pml_base_send_mode_t (pml.h:78-85), same values */
+enum mi355x_send_mode {
+    MI355X_SEND_SYNCHRONOUS = 0, MI355X_SEND_COMPLETE = 1, MI355X_SEND_BUFFERED = 2, MI355X_SEND_READY = 3,
+    MI355X_SEND_STANDARD = 4
+};
+/* mi355x_isend / mi355x_send with a send mode (the plain forms are MI355X_SEND_STANDARD):
+ * SYNCHRONOUS completes only once the receiver has matched and read the message; BUFFERED
+ * completes at once (the payload is copied; MPI_Bsend's attached buffer plays no role). */
+int mi355x_isend_mode(mi355x_comm_t *comm, const void *buf, size_t count, const mi355x_ddt_t *ddt, int dest, int tag,
+                      int mode, void *stream, mi355x_request_t **req);
+int mi355x_send_mode(mi355x_comm_t *comm, const void *buf, size_t count, const mi355x_ddt_t *ddt, int dest, int tag,
+                     int mode, void *stream);
+/* MPI_Improbe / MPI_Mprobe (mca_pml_ob1_improbe, pml_ob1_iprobe.c:83-134): the first matching
+ * message is taken out of the queue (no receive can match it any more) and handed back as *msg;
+ * MPI_Imrecv / MPI_Mrecv receive exactly that message (consuming msg). */
+typedef struct mi355x_message mi355x_message_t;
+int mi355x_improbe(mi355x_comm_t *comm, int source, int tag, int *flag, mi355x_message_t **msg,
+                   mi355x_status_t *status);
+int mi355x_imrecv(mi355x_comm_t *comm, void *buf, size_t count, const mi355x_ddt_t *ddt, mi355x_message_t *msg,
+                  void *stream, mi355x_request_t **req);
+/* MPI_Cancel of a receive not matched yet (mca_pml_ob1_recv_request_cancel,
+ * pml_ob1_recvreq.c:101-137): it completes with *cancelled = 1; a matched receive or a send is not
+ * cancelled (ob1 cancels no send either, pml_ob1_sendreq.c:126-131). */
+int mi355x_request_cancel(mi355x_request_t *req);
+int mi355x_request_cancelled(const mi355x_request_t *req, int *cancelled);
+/* the engine's waits on host-buffer collectives (the buffer-kind vote) call this between polls:
+ * coll/mi355x passes opal_progress, so requests other ranks depend on keep moving */
+int mi355x_set_progress_hook(void (*progress)(void));
 
 /* ---------------------------------------------------------------- GPU convertor */
 /* A datatype layout: instance k at base + k*extent; inside it nblk blocks at j*stride; inside a
@@ -336,6 +372,16 @@ int mi355x_pack(const mi355x_ddt_t *d, size_t count, const void *base, size_t po
                 uint32_t *checksum, void *stream);
 int mi355x_unpack(const mi355x_ddt_t *d, size_t count, void *base, size_t pos, const void *src, size_t bytes,
                   uint32_t *checksum, void *stream);
+/* the same windows on HOST memory (ob1's convertor for a host buffer, opal_datatype_pack.c:250-374,
+ * opal_datatype_unpack.c:245-…); synchronous, no GPU */
+int mi355x_pack_host(const mi355x_ddt_t *d, size_t count, const void *base, size_t pos, void *dst, size_t bytes);
+int mi355x_unpack_host(const mi355x_ddt_t *d, size_t count, void *base, size_t pos, const void *src, size_t bytes);
+/* opal_convertor_raw (opal_convertor_raw.c:37-…): up to *iov_count memory pieces (offset from the
+ * buffer, length) of the type map from packed position *pos onwards; *iov_count = pieces returned,
+ * *max_data = their bytes, *pos advanced; returns 1 once the whole message is described, else 0.
+ * No GPU. */
+int mi355x_ddt_raw(const mi355x_ddt_t *d, size_t count, size_t *pos, int64_t *disp, size_t *len, uint32_t *iov_count,
+                   size_t *max_data);
 
 /* Host-only introspection of the schedule compiler: the per-element program the engine runs for
  * a given reference algorithm (layout documented in coll_comm.cpp).  For tests; no GPU needed. */

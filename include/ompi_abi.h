@@ -163,6 +163,22 @@ extern int mca_base_component_var_register(const mca_base_component_t *component
                                            mca_base_var_enum_t *enumerator, int bind, mca_base_var_flag_t flags,
                                            mca_base_var_info_lvl_t info_lvl, mca_base_var_scope_t scope,
                                            void *storage) __attribute__((weak));
+/* reading another component's variable (mca_base_var.h:96-115, :559-562; mca_base_var.c:421-455):
+ * find its index by (project, framework, component, name), then get a pointer to its storage
+ * (int *, bool * or char ** by the variable's type).  Weak like the registration above. */
+typedef enum {
+    MCA_BASE_VAR_SOURCE_DEFAULT,
+    MCA_BASE_VAR_SOURCE_COMMAND_LINE,
+    MCA_BASE_VAR_SOURCE_ENV,
+    MCA_BASE_VAR_SOURCE_FILE,
+    MCA_BASE_VAR_SOURCE_SET,
+    MCA_BASE_VAR_SOURCE_OVERRIDE,
+    MCA_BASE_VAR_SOURCE_MAX
+} mca_base_var_source_t;
+extern int mca_base_var_find(const char *project_name, const char *type_name, const char *component_name,
+                             const char *param_name) __attribute__((weak));
+extern int mca_base_var_get_value(int vari, const void *value, mca_base_var_source_t *source,
+                                  const char **source_file) __attribute__((weak));
 
 /* ------------------------------------------------------------------ datatypes */
 /* opal/datatype/opal_datatype.h:103-131, opal_datatype_internal.h:148-188 */
@@ -373,6 +389,24 @@ typedef struct ompi_predefined_request_t {
     char padding[sizeof(void *) * 32 - sizeof(ompi_request_t)];
 } ompi_predefined_request_t;
 
+/* ompi/message/message.h:21-29: the handle MPI_Mprobe / MPI_Improbe hand back (the PML allocates it
+ * and frees it in mrecv / imrecv, pml_ob1_iprobe.c:83-134); opal_free_list_item_t is
+ * { opal_list_item_t super; } (opal/class/opal_free_list.h:47-50) */
+typedef struct ompi_message_t {
+    opal_list_item_t super;
+    int m_f_to_c_index;
+    struct ompi_communicator_t *comm;
+    void *req_ptr;
+    int peer;
+    size_t count;
+} ompi_message_t;
+typedef struct ompi_predefined_message_t {  /* message.h:40-45 */
+    ompi_message_t message;
+    char padding[sizeof(void *) * 32 - sizeof(ompi_message_t)];
+} ompi_predefined_message_t;
+extern opal_class_t ompi_message_t_class;              /* message.h:31 */
+extern ompi_predefined_message_t ompi_message_null;    /* MPI_MESSAGE_NULL, mpi.h.in:739,886 */
+
 /* opal/threads/condition.h:46-50 */
 typedef struct opal_condition_t {
     opal_object_t super;
@@ -381,6 +415,7 @@ typedef struct opal_condition_t {
 } opal_condition_t;
 
 #define MPI_UNDEFINED (-32766)  /* mpi.h.in:423 */
+#define MPI_ERR_TYPE 3          /* mpi.h.in:535 */
 #define MPI_ERR_REQUEST 7       /* mpi.h.in:539 */
 #define MPI_ERR_INTERN 17       /* mpi.h.in:549 */
 

@@ -178,6 +178,17 @@ def _declare(lib: ctypes.CDLL) -> None:
         "mi355x_iprobe": (i, [vp, i, i, c.POINTER(i), c.POINTER(MsgStatus)]),
         "mi355x_p2p_progress": (i, [vp]),
         "mi355x_request_get_status": (i, [vp, c.POINTER(MsgStatus)]),
+        "mi355x_isend_mode": (i, [vp, vp, sz, vp, i, i, i, vp, c.POINTER(vp)]),
+        "mi355x_send_mode": (i, [vp, vp, sz, vp, i, i, i, vp]),
+        "mi355x_improbe": (i, [vp, i, i, c.POINTER(i), c.POINTER(vp), c.POINTER(MsgStatus)]),
+        "mi355x_imrecv": (i, [vp, vp, sz, vp, vp, vp, c.POINTER(vp)]),
+        "mi355x_request_cancel": (i, [vp]),
+        "mi355x_request_cancelled": (i, [vp, c.POINTER(i)]),
+        "mi355x_set_progress_hook": (i, [vp]),
+        "mi355x_pack_host": (i, [vp, sz, vp, sz, vp, sz]),
+        "mi355x_unpack_host": (i, [vp, sz, vp, sz, vp, sz]),
+        "mi355x_ddt_raw": (i, [vp, sz, c.POINTER(sz), c.POINTER(c.c_int64), c.POINTER(sz), c.POINTER(c.c_uint32),
+                               c.POINTER(sz)]),
         "mi355x_pack": (i, [vp, sz, vp, sz, vp, sz, c.POINTER(c.c_uint32), vp]),
         "mi355x_unpack": (i, [vp, sz, vp, sz, vp, sz, c.POINTER(c.c_uint32), vp]),
     }
@@ -384,14 +395,35 @@ class Comm:
     def ialltoall(self, sbuf, rbuf, nbytes, stream=None) -> Request:
         return self._post("mi355x_ialltoall", sbuf, rbuf, nbytes, stream)
 
-    # ---- device point-to-point (count = bytes when ddt is None, else datatype instances)
-    def isend(self, buf, count, dest, tag, ddt=None, stream=None) -> Request:
+    # ---- point-to-point, device or host buffers (count = bytes when ddt is None, else datatype
+    #      instances); mode: SEND_MODE (mca_pml_base_send_mode_t)
+    def isend(self, buf, count, dest, tag, ddt=None, stream=None, mode=None) -> Request:
+        if mode is not None:
+            return self._post("mi355x_isend_mode", buf, count, ddt.h if ddt else None, dest, tag, SEND_MODE[mode],
+                              stream)
         return self._post("mi355x_isend", buf, count, ddt.h if ddt else None, dest, tag, stream)
+
+    def improbe(self, source, tag):
+        """(Message, status tuple) of the first matching message, taken out of the queue, or None"""
+        flag, st, msg = ctypes.c_int(0), MsgStatus(), ctypes.c_void_p()
+        check(rt().mi355x_improbe(self.h, source, tag, ctypes.byref(flag), ctypes.byref(msg), ctypes.byref(st)),
+              "mi355x_improbe")
+        return (msg.value, st.as_tuple()) if flag.value else None
+
+    def imrecv(self, buf, count, msg, ddt=None, stream=None) -> Request:
+        h = ctypes.c_void_p()
+        check(rt().mi355x_imrecv(self.h, buf, count, ddt.h if ddt else None, msg, stream, ctypes.byref(h)),
+              "mi355x_imrecv")
+        return Request(h.value)
 
     def irecv(self, buf, count, source, tag, ddt=None, stream=None) -> Request:
         return self._post("mi355x_irecv", buf, count, ddt.h if ddt else None, source, tag, stream)
 
-    def send(self, buf, count, dest, tag, ddt=None, stream=None) -> None:
+    def send(self, buf, count, dest, tag, ddt=None, stream=None, mode=None) -> None:
+        if mode is not None:
+            check(rt().mi355x_send_mode(self.h, buf, count, ddt.h if ddt else None, dest, tag, SEND_MODE[mode], stream),
+                  "mi355x_send_mode")
+            return
         check(rt().mi355x_send(self.h, buf, count, ddt.h if ddt else None, dest, tag, stream), "mi355x_send")
 
     def recv(self, buf, count, source, tag, ddt=None, stream=None) -> tuple[int, int, int, int]:
@@ -422,6 +454,10 @@ def _check_p2p(rc: int, what: str, st: "MsgStatus") -> None:
     if rc == ERR_TRUNCATE:
         raise TruncateError(rt().mi355x_last_error().decode(errors="replace"), st.as_tuple())
     check(rc, what)
+
+
+# mca_pml_base_send_mode_t (pml.h:78-85)
+SEND_MODE = {"SYNCHRONOUS": 0, "COMPLETE": 1, "BUFFERED": 2, "READY": 3, "STANDARD": 4}
 
 
 class Rules:
@@ -460,6 +496,14 @@ class Request:
             return True   # complete; wait() reports the truncation
         check(rc, "mi355x_request_test")
         return bool(done.value)
+
+    def cancel(self) -> None:
+        check(rt().mi355x_request_cancel(self.h), "mi355x_request_cancel")
+
+    def cancelled(self) -> bool:
+        f = ctypes.c_int(0)
+        check(rt().mi355x_request_cancelled(self.h, ctypes.byref(f)), "mi355x_request_cancelled")
+        return bool(f.value)
 
     def wait(self):
         """wait, free; returns the receive status tuple (source, tag, error, bytes)"""
@@ -533,6 +577,30 @@ class Ddt:
         check(rt().mi355x_unpack(self.h, count, base, pos, src, nbytes, ctypes.byref(cs) if checksum else None,
                                  stream), "mi355x_unpack")
         return cs.value if checksum else None
+
+    def pack_host(self, count, base, pos, dst, nbytes):
+        """the same window on host memory (no GPU)"""
+        check(rt().mi355x_pack_host(self.h, count, base, pos, dst, nbytes), "mi355x_pack_host")
+
+    def unpack_host(self, count, base, pos, src, nbytes):
+        check(rt().mi355x_unpack_host(self.h, count, base, pos, src, nbytes), "mi355x_unpack_host")
+
+    def raw(self, count, iov_num=5):
+        """opal_convertor_raw's walk: a list of calls, each a list of (offset, length) pieces of at
+        most iov_num entries; the last call returns 1 (no GPU)"""
+        pos = ctypes.c_size_t(0)
+        calls = []
+        while True:
+            disp = (ctypes.c_int64 * iov_num)()
+            lens = (ctypes.c_size_t * iov_num)()
+            cnt, got = ctypes.c_uint32(iov_num), ctypes.c_size_t(0)
+            rc = rt().mi355x_ddt_raw(self.h, count, ctypes.byref(pos), disp, lens, ctypes.byref(cnt), ctypes.byref(got))
+            if rc < 0:
+                check(rc, "mi355x_ddt_raw")
+            calls.append([(disp[k], lens[k]) for k in range(cnt.value)])
+            assert sum(ln for _, ln in calls[-1]) == got.value
+            if rc == 1:
+                return calls
 
     def destroy(self):
         if self.h:

@@ -468,32 +468,63 @@ int mini_progress(void)  /* opal_progress: run every registered callback */
 }
 int mini_progress_callbacks(void) { return progress_n; }
 void opal_progress(void) { (void)mini_progress(); }
-/* MPI_Wait on a nonpersistent request (ompi_request_default_wait, req_wait.c:33-90): progress
- * until complete, then free it unless it failed; *req becomes MPI_REQUEST_NULL */
-int mini_wait(ompi_request_t **req)
-{
-    ompi_request_t *r = *req;
-    while (!r->req_complete) mini_progress();
-    if (r->req_status.MPI_ERROR != 0) return r->req_status.MPI_ERROR;
-    int rc = r->req_free(req);
-    return rc;
-}
-/* MPI_Wait with a status (req_wait.c:33-90 copies req_status out before freeing) */
+/* MPI_Wait (ompi_request_default_wait, req_wait.c:33-76): progress until complete, copy the status
+ * out (not MPI_ERROR), then a persistent request goes INACTIVE (:59-63) and any other is freed
+ * unless it failed; *req becomes MPI_REQUEST_NULL */
 int mini_wait_status(ompi_request_t **req, ompi_status_public_t *st)
 {
     ompi_request_t *r = *req;
+    if (r == &ompi_request_null.request) return 0;
     while (!r->req_complete) mini_progress();
-    if (st) *st = r->req_status;
+    if (st) {
+        st->MPI_SOURCE = r->req_status.MPI_SOURCE;
+        st->MPI_TAG = r->req_status.MPI_TAG;
+        st->_ucount = r->req_status._ucount;
+        st->_cancelled = r->req_status._cancelled;
+        st->MPI_ERROR = r->req_status.MPI_ERROR;  /* (MPI_Wait returns it; kept here for the tests) */
+    }
+    if (r->req_persistent) {
+        if (r->req_state == OMPI_REQUEST_INACTIVE) return 0;
+        r->req_state = OMPI_REQUEST_INACTIVE;
+        return r->req_status.MPI_ERROR;
+    }
     if (r->req_status.MPI_ERROR != 0) return r->req_status.MPI_ERROR;
     return r->req_free(req);
 }
+int mini_wait(ompi_request_t **req) { return mini_wait_status(req, NULL); }
+/* MPI_Test (ompi_request_default_test, req_test.c:30-90): one progress pass; complete -> as wait */
+int mini_test(ompi_request_t **req, int *flag, ompi_status_public_t *st)
+{
+    ompi_request_t *r = *req;
+    *flag = 0;
+    if (r == &ompi_request_null.request) {
+        *flag = 1;
+        return 0;
+    }
+    if (!r->req_complete) mini_progress();
+    if (!r->req_complete) return 0;
+    *flag = 1;
+    return mini_wait_status(req, st);
+}
+/* MPI_Request_free (ompi/mpi/c/request_free.c:54-60 -> req_free) */
+int mini_request_free(ompi_request_t **req) { return (*req)->req_free(req); }
+/* MPI_Cancel (ompi/mpi/c/cancel.c -> ompi_request_cancel, request.h:353-360) */
+int mini_cancel(ompi_request_t *r) { return r->req_cancel ? r->req_cancel(r, r->req_complete) : 0; }
+/* MPI_Start (ompi/mpi/c/start.c:66-72: a PML request -> MCA_PML_CALL(start(1, request))) */
+int mini_start(ompi_request_t **req) { return mca_pml.pml_start(1, req); }
+
+/* MPI_MESSAGE_NULL (message.c) and the message class; the PML allocates messages */
+opal_class_t ompi_message_t_class = {"ompi_message_t", &opal_object_t_class, NULL, NULL, 0, 0, NULL, NULL,
+                                     sizeof(ompi_message_t)};
+ompi_predefined_message_t ompi_message_null;
+int mini_message_is_null(ompi_message_t *m) { return m == &ompi_message_null.message; }
 int mini_request_is_null(ompi_request_t *r) { return r == &ompi_request_null.request; }
 
 /* ---- the PML slot (ompi/mca/pml/pml.h:497-558): `mca_pml` is the selected PML's table and
  * MCA_PML_CALL(x) is mca_pml.pml_x.  The harness's "selected PML" is a stub (no transport):
  * it counts calls and returns the stub marker -- what a host-buffer message would hand to ob1. */
 mca_pml_base_module_t mca_pml;
-static int pml_stub_calls[8];
+static int pml_stub_calls[16];
 static int pst_isend(void *b, size_t n, struct ompi_datatype_t *d, int dst, int tag, mca_pml_base_send_mode_t m,
                      struct ompi_communicator_t *c, struct ompi_request_t **req)
 { (void)b; (void)n; (void)d; (void)dst; (void)tag; (void)m; (void)c; *req = &ompi_request_null.request; pml_stub_calls[0]++; return 77; }
@@ -510,6 +541,22 @@ static int pst_iprobe(int src, int tag, struct ompi_communicator_t *c, int *matc
 { (void)src; (void)tag; (void)c; (void)st; *matched = 0; pml_stub_calls[4]++; return 0; }
 static int pst_probe(int src, int tag, struct ompi_communicator_t *c, ompi_status_public_t *st)
 { (void)src; (void)tag; (void)c; (void)st; pml_stub_calls[5]++; return 77; }
+static int pst_isend_init(void *b, size_t n, struct ompi_datatype_t *d, int dst, int tag, mca_pml_base_send_mode_t m,
+                          struct ompi_communicator_t *c, struct ompi_request_t **req)
+{ (void)b; (void)n; (void)d; (void)dst; (void)tag; (void)m; (void)c; *req = &ompi_request_null.request; pml_stub_calls[6]++; return 77; }
+static int pst_irecv_init(void *b, size_t n, struct ompi_datatype_t *d, int src, int tag, struct ompi_communicator_t *c,
+                          struct ompi_request_t **req)
+{ (void)b; (void)n; (void)d; (void)src; (void)tag; (void)c; *req = &ompi_request_null.request; pml_stub_calls[7]++; return 77; }
+static int pst_start(size_t n, struct ompi_request_t **reqs) { (void)n; (void)reqs; pml_stub_calls[8]++; return 77; }
+static int pst_improbe(int src, int tag, struct ompi_communicator_t *c, int *matched, struct ompi_message_t **msg,
+                       ompi_status_public_t *st)
+{ (void)src; (void)tag; (void)c; (void)st; *matched = 0; *msg = &ompi_message_null.message; pml_stub_calls[9]++; return 0; }
+static int pst_mprobe(int src, int tag, struct ompi_communicator_t *c, struct ompi_message_t **msg, ompi_status_public_t *st)
+{ (void)src; (void)tag; (void)c; (void)msg; (void)st; pml_stub_calls[10]++; return 77; }
+static int pst_imrecv(void *b, size_t n, struct ompi_datatype_t *d, struct ompi_message_t **msg, struct ompi_request_t **req)
+{ (void)b; (void)n; (void)d; (void)msg; *req = &ompi_request_null.request; pml_stub_calls[11]++; return 77; }
+static int pst_mrecv(void *b, size_t n, struct ompi_datatype_t *d, struct ompi_message_t **msg, ompi_status_public_t *st)
+{ (void)b; (void)n; (void)d; (void)msg; (void)st; pml_stub_calls[12]++; return 77; }
 
 void mini_pml_install_stub(void)
 {
@@ -520,9 +567,16 @@ void mini_pml_install_stub(void)
     mca_pml.pml_recv = pst_recv;
     mca_pml.pml_iprobe = pst_iprobe;
     mca_pml.pml_probe = pst_probe;
+    mca_pml.pml_isend_init = pst_isend_init;
+    mca_pml.pml_irecv_init = pst_irecv_init;
+    mca_pml.pml_start = pst_start;
+    mca_pml.pml_improbe = pst_improbe;
+    mca_pml.pml_mprobe = pst_mprobe;
+    mca_pml.pml_imrecv = pst_imrecv;
+    mca_pml.pml_mrecv = pst_mrecv;
     mca_pml.pml_max_tag = 0x7fffffff;
 }
-int mini_pml_stub_calls(int which) { return (which >= 0 && which < 8) ? pml_stub_calls[which] : -1; }
+int mini_pml_stub_calls(int which) { return (which >= 0 && which < 16) ? pml_stub_calls[which] : -1; }
 void *mini_pml_fn(int which)
 {
     switch (which) {
@@ -532,6 +586,13 @@ void *mini_pml_fn(int which)
     case 3: return (void *)mca_pml.pml_recv;
     case 4: return (void *)mca_pml.pml_iprobe;
     case 5: return (void *)mca_pml.pml_probe;
+    case 6: return (void *)mca_pml.pml_isend_init;
+    case 7: return (void *)mca_pml.pml_irecv_init;
+    case 8: return (void *)mca_pml.pml_start;
+    case 9: return (void *)mca_pml.pml_improbe;
+    case 10: return (void *)mca_pml.pml_mprobe;
+    case 11: return (void *)mca_pml.pml_imrecv;
+    case 12: return (void *)mca_pml.pml_mrecv;
     default: return NULL;
     }
 }
@@ -560,6 +621,47 @@ int mini_irecv(void *b, int n, ompi_datatype_t *d, int src, int tag, ompi_commun
 int mini_iprobe(int src, int tag, ompi_communicator_t *c, int *flag, ompi_status_public_t *st)
 {
     return mca_pml.pml_iprobe(src, tag, c, flag, st);
+}
+/* any send mode: MPI_Bsend (bsend.c: MCA_PML_BASE_SEND_BUFFERED), MPI_Rsend (READY), MPI_Ssend */
+int mini_send_mode(void *b, int n, ompi_datatype_t *d, int dst, int tag, int mode, ompi_communicator_t *c)
+{
+    return mca_pml.pml_send(b, (size_t)n, d, dst, tag, (mca_pml_base_send_mode_t)mode, c);
+}
+int mini_isend_mode(void *b, int n, ompi_datatype_t *d, int dst, int tag, int mode, ompi_communicator_t *c,
+                    ompi_request_t **req)
+{
+    return mca_pml.pml_isend(b, (size_t)n, d, dst, tag, (mca_pml_base_send_mode_t)mode, c, req);
+}
+int mini_probe(int src, int tag, ompi_communicator_t *c, ompi_status_public_t *st)
+{
+    return mca_pml.pml_probe(src, tag, c, st);
+}
+/* MPI_Send_init / MPI_Recv_init (send_init.c:74-77, recv_init.c:66-67) */
+int mini_send_init(void *b, int n, ompi_datatype_t *d, int dst, int tag, int mode, ompi_communicator_t *c,
+                   ompi_request_t **req)
+{
+    return mca_pml.pml_isend_init(b, (size_t)n, d, dst, tag, (mca_pml_base_send_mode_t)mode, c, req);
+}
+int mini_recv_init(void *b, int n, ompi_datatype_t *d, int src, int tag, ompi_communicator_t *c, ompi_request_t **req)
+{
+    return mca_pml.pml_irecv_init(b, (size_t)n, d, src, tag, c, req);
+}
+/* MPI_Improbe / MPI_Mprobe / MPI_Imrecv / MPI_Mrecv (improbe.c:73, mprobe.c:72, imrecv.c:69, mrecv.c:71) */
+int mini_improbe(int src, int tag, ompi_communicator_t *c, int *flag, ompi_message_t **msg, ompi_status_public_t *st)
+{
+    return mca_pml.pml_improbe(src, tag, c, flag, msg, st);
+}
+int mini_mprobe(int src, int tag, ompi_communicator_t *c, ompi_message_t **msg, ompi_status_public_t *st)
+{
+    return mca_pml.pml_mprobe(src, tag, c, msg, st);
+}
+int mini_imrecv(void *b, int n, ompi_datatype_t *d, ompi_message_t **msg, ompi_request_t **req)
+{
+    return mca_pml.pml_imrecv(b, (size_t)n, d, msg, req);
+}
+int mini_mrecv(void *b, int n, ompi_datatype_t *d, ompi_message_t **msg, ompi_status_public_t *st)
+{
+    return mca_pml.pml_mrecv(b, (size_t)n, d, msg, st);
 }
 int mini_request_complete(ompi_request_t *r) { return r->req_complete ? 1 : 0; }
 
@@ -892,7 +994,11 @@ size_t mini_offsetof(int which)
  * <framework>_<component>_<name>, value from OMPI_MCA_<full name> in the environment (the
  * highest-priority source the harness has), else the storage's current value as the default. */
 #define MINI_MAX_VARS 64
-static struct { char name[160]; char desc[160]; int type; int lvl; void *storage; } mini_vars[MINI_MAX_VARS];
+static struct {
+    char name[160], desc[160], type_name[32], comp_name[64], var_name[64];
+    int type, lvl;
+    void *storage;
+} mini_vars[MINI_MAX_VARS];
 static int mini_nvars;
 
 int mca_base_component_var_register(const mca_base_component_t *component, const char *variable_name,
@@ -901,7 +1007,8 @@ int mca_base_component_var_register(const mca_base_component_t *component, const
                                     mca_base_var_info_lvl_t info_lvl, mca_base_var_scope_t scope, void *storage)
 {
     (void)enumerator; (void)bind; (void)flags; (void)scope;
-    if (!component || !variable_name || !storage || type != MCA_BASE_VAR_TYPE_INT) return -1;
+    if (!component || !variable_name || !storage) return -1;
+    if (type != MCA_BASE_VAR_TYPE_INT && type != MCA_BASE_VAR_TYPE_BOOL && type != MCA_BASE_VAR_TYPE_STRING) return -1;
     char full[160], env[200];
     snprintf(full, sizeof(full), "%s_%s_%s", component->mca_type_name, component->mca_component_name, variable_name);
     int idx = -1;
@@ -916,14 +1023,80 @@ int mca_base_component_var_register(const mca_base_component_t *component, const
     mini_vars[idx].type = type;
     mini_vars[idx].lvl = info_lvl;
     mini_vars[idx].storage = storage;
+    snprintf(mini_vars[idx].type_name, sizeof(mini_vars[idx].type_name), "%s", component->mca_type_name);
+    snprintf(mini_vars[idx].comp_name, sizeof(mini_vars[idx].comp_name), "%s", component->mca_component_name);
+    snprintf(mini_vars[idx].var_name, sizeof(mini_vars[idx].var_name), "%s", variable_name);
     snprintf(env, sizeof(env), "OMPI_MCA_%s", full);
     const char *v = getenv(env);
-    if (v) *(int *)storage = atoi(v);
+    if (v) {
+        if (type == MCA_BASE_VAR_TYPE_INT) *(int *)storage = atoi(v);
+        else if (type == MCA_BASE_VAR_TYPE_BOOL) *(bool *)storage = atoi(v) != 0;
+        else *(char **)storage = strdup(v);
+    }
     return idx;
+}
+/* mca_base_var_find / mca_base_var_get_value (mca_base_var.c:816-820, :421-455): the index of a
+ * registered variable, and a pointer to its storage */
+int mca_base_var_find(const char *project_name, const char *type_name, const char *component_name,
+                      const char *param_name)
+{
+    (void)project_name;
+    for (int i = 0; i < mini_nvars; ++i)
+        if (!strcmp(mini_vars[i].type_name, type_name) && !strcmp(mini_vars[i].comp_name, component_name) &&
+            !strcmp(mini_vars[i].var_name, param_name))
+            return i;
+    return OMPI_ERR_NOT_FOUND;
+}
+int mca_base_var_get_value(int vari, const void *value, mca_base_var_source_t *source, const char **source_file)
+{
+    if (vari < 0 || vari >= mini_nvars) return OMPI_ERR_BAD_PARAM;
+    if (value) *(void **)value = mini_vars[vari].storage;
+    if (source) *source = MCA_BASE_VAR_SOURCE_FILE;
+    if (source_file) *source_file = "mini-mca-params.conf";
+    return OMPI_SUCCESS;
+}
+/* coll/tuned as the variable system knows it after tuned_register (coll_tuned_component.c:151-167
+ * and the forced-algorithm registrations, coll_tuned_allreduce.c:949-1005): values as if they came
+ * from openmpi-mca-params.conf -- nothing in the environment */
+static mca_base_component_t mini_tuned_version = {2, 0, 0, "coll", 2, 0, 0, "tuned", 1, 8, 5, NULL, NULL, NULL, NULL, {0}};
+static bool tuned_use_dynamic_rules;
+static int tuned_allreduce_alg, tuned_reduce_alg, tuned_chain_fanout, tuned_rs_alg;
+static char *tuned_rules_file;
+int mini_tuned_register(int use_dynamic_rules, int allreduce_alg, int reduce_alg, int chain_fanout, int rs_alg,
+                        const char *rules_file)
+{
+    tuned_use_dynamic_rules = use_dynamic_rules != 0;
+    tuned_allreduce_alg = allreduce_alg;
+    tuned_reduce_alg = reduce_alg;
+    tuned_chain_fanout = chain_fanout;
+    tuned_rs_alg = rs_alg;
+    free(tuned_rules_file);
+    tuned_rules_file = rules_file ? strdup(rules_file) : NULL;
+    const mca_base_component_t *c = &mini_tuned_version;
+    int rc = 0;
+    rc |= mca_base_component_var_register(c, "use_dynamic_rules", "", MCA_BASE_VAR_TYPE_BOOL, NULL, 0, 0,
+                                          OPAL_INFO_LVL_6, MCA_BASE_VAR_SCOPE_READONLY, &tuned_use_dynamic_rules) < 0;
+    rc |= mca_base_component_var_register(c, "dynamic_rules_filename", "", MCA_BASE_VAR_TYPE_STRING, NULL, 0, 0,
+                                          OPAL_INFO_LVL_6, MCA_BASE_VAR_SCOPE_READONLY, &tuned_rules_file) < 0;
+    rc |= mca_base_component_var_register(c, "allreduce_algorithm", "", MCA_BASE_VAR_TYPE_INT, NULL, 0, 0,
+                                          OPAL_INFO_LVL_5, MCA_BASE_VAR_SCOPE_READONLY, &tuned_allreduce_alg) < 0;
+    rc |= mca_base_component_var_register(c, "reduce_algorithm", "", MCA_BASE_VAR_TYPE_INT, NULL, 0, 0,
+                                          OPAL_INFO_LVL_5, MCA_BASE_VAR_SCOPE_READONLY, &tuned_reduce_alg) < 0;
+    rc |= mca_base_component_var_register(c, "reduce_algorithm_chain_fanout", "", MCA_BASE_VAR_TYPE_INT, NULL, 0, 0,
+                                          OPAL_INFO_LVL_5, MCA_BASE_VAR_SCOPE_READONLY, &tuned_chain_fanout) < 0;
+    rc |= mca_base_component_var_register(c, "reduce_scatter_algorithm", "", MCA_BASE_VAR_TYPE_INT, NULL, 0, 0,
+                                          OPAL_INFO_LVL_5, MCA_BASE_VAR_SCOPE_READONLY, &tuned_rs_alg) < 0;
+    return rc ? -1 : 0;
 }
 int mini_var_count(void) { return mini_nvars; }
 const char *mini_var_name(int i) { return (i >= 0 && i < mini_nvars) ? mini_vars[i].name : NULL; }
-int mini_var_int(int i) { return (i >= 0 && i < mini_nvars) ? *(int *)mini_vars[i].storage : -1; }
+int mini_var_int(int i)
+{
+    if (i < 0 || i >= mini_nvars) return -1;
+    if (mini_vars[i].type == MCA_BASE_VAR_TYPE_BOOL) return *(bool *)mini_vars[i].storage;
+    if (mini_vars[i].type == MCA_BASE_VAR_TYPE_STRING) return *(char **)mini_vars[i].storage != NULL;
+    return *(int *)mini_vars[i].storage;
+}
 int mini_component_register(const mca_base_component_t *c)
 {
     return c->mca_register_component_params ? c->mca_register_component_params() : OMPI_SUCCESS;

@@ -58,6 +58,23 @@ int mini_isend(void *b, int n, ompi_datatype_t *d, int dst, int tag, ompi_commun
 int mini_irecv(void *b, int n, ompi_datatype_t *d, int src, int tag, ompi_communicator_t *c, ompi_request_t **req);
 int mini_iprobe(int src, int tag, ompi_communicator_t *c, int *flag, ompi_status_public_t *st);
 int mini_wait_status(ompi_request_t **req, ompi_status_public_t *st);
+int mini_wait(ompi_request_t **req);
+int mini_test(ompi_request_t **req, int *flag, ompi_status_public_t *st);
+int mini_request_free(ompi_request_t **req);
+int mini_cancel(ompi_request_t *r);
+int mini_start(ompi_request_t **req);
+int mini_message_is_null(ompi_message_t *m);
+int mini_send_mode(void *b, int n, ompi_datatype_t *d, int dst, int tag, int mode, ompi_communicator_t *c);
+int mini_isend_mode(void *b, int n, ompi_datatype_t *d, int dst, int tag, int mode, ompi_communicator_t *c,
+                    ompi_request_t **req);
+int mini_probe(int src, int tag, ompi_communicator_t *c, ompi_status_public_t *st);
+int mini_send_init(void *b, int n, ompi_datatype_t *d, int dst, int tag, int mode, ompi_communicator_t *c,
+                   ompi_request_t **req);
+int mini_recv_init(void *b, int n, ompi_datatype_t *d, int src, int tag, ompi_communicator_t *c, ompi_request_t **req);
+int mini_improbe(int src, int tag, ompi_communicator_t *c, int *flag, ompi_message_t **msg, ompi_status_public_t *st);
+int mini_mprobe(int src, int tag, ompi_communicator_t *c, ompi_message_t **msg, ompi_status_public_t *st);
+int mini_imrecv(void *b, int n, ompi_datatype_t *d, ompi_message_t **msg, ompi_request_t **req);
+int mini_mrecv(void *b, int n, ompi_datatype_t *d, ompi_message_t **msg, ompi_status_public_t *st);
 
 #ifdef __cplusplus
 }

@@ -758,27 +758,52 @@ typedef struct mi355x_nbreq_t {
     int ucount;
     mi355x_ddt_t *ud;
     mi355x_ddt_t *pd;              /* layout of the initiation-time pack (kept until completion) */
+    /* persistent point-to-point (pml_isend_init / pml_irecv_init): 1 send, 2 receive, 0 none; the
+     * arguments each MPI_Start posts */
+    int pers;
+    void *pbuf;
+    size_t pcount;
+    struct ompi_datatype_t *pdt;
+    int ppeer, ptag, pmode;
+    int free_called;               /* MPI_Request_free while active: released at completion */
 } mi355x_nbreq_t;
 
 static pthread_mutex_t nb_lock = PTHREAD_MUTEX_INITIALIZER;
 static mi355x_nbreq_t *nb_active;
 static int nb_registered;
 
+/* MPI_Request_free.  A collective must be complete (libnbc likewise); a point-to-point request
+ * may be freed while active -- it is released once it completes (ob1's req_free_called,
+ * pml_ob1_sendreq.c:97-122) */
 static int nbreq_free(ompi_request_t **rp)
 {
     mi355x_nbreq_t *r = (mi355x_nbreq_t *)*rp;
-    if (true != r->super.req_complete) return MPI_ERR_REQUEST;
+    if (true != r->super.req_complete && r->eng) {
+        if (!r->p2p) return MPI_ERR_REQUEST;
+        pthread_mutex_lock(&nb_lock);
+        const int active = r->eng != NULL;
+        if (active) r->free_called = 1;
+        pthread_mutex_unlock(&nb_lock);
+        if (active) {
+            *rp = &ompi_request_null.request;
+            return OMPI_SUCCESS;
+        }
+    }
     mi355x_ompi_request_fini(&r->super);
     mi355x_obj_release(&r->super.super.super.super);
     *rp = &ompi_request_null.request;
     return OMPI_SUCCESS;
 }
 
-static int nbreq_cancel(ompi_request_t *r, int flag)
+/* MPI_Cancel: a receive not matched yet completes as cancelled (ob1,
+ * pml_ob1_recvreq.c:101-137); sends and collectives are not cancelled (ob1's send cancel and
+ * libnbc's do nothing) */
+static int nbreq_cancel(ompi_request_t *q, int flag)
 {
-    (void)r;
     (void)flag;
-    return OMPI_SUCCESS;  /* collectives cannot be cancelled (libnbc's request_cancel does nothing) */
+    mi355x_nbreq_t *r = (mi355x_nbreq_t *)q;
+    if (r->p2p == 2 && r->eng) (void)mi355x_request_cancel(r->eng);
+    return OMPI_SUCCESS;
 }
 
 static void nbreq_construct(opal_object_t *o)
@@ -796,6 +821,12 @@ static void nbreq_construct(opal_object_t *o)
     r->ucount = 0;
     r->ud = NULL;
     r->pd = NULL;
+    r->pers = 0;
+    r->pbuf = NULL;
+    r->pcount = 0;
+    r->pdt = NULL;
+    r->ppeer = r->ptag = r->pmode = 0;
+    r->free_called = 0;
 }
 
 /* completion-time unpack of a derived-datatype nonblocking collective (local work only) */
@@ -837,11 +868,14 @@ static int nb_progress(void)
         const int rc = nb_finish_stage(r, rc0);
         if (r->p2p == 2) {  /* MPI_Status of a receive (pml_ob1_recvreq.h:172-180 for truncation) */
             mi355x_status_t st;
+            int cancelled = 0;
             memset(&st, 0, sizeof(st));
             mi355x_request_get_status(r->eng, &st);
+            mi355x_request_cancelled(r->eng, &cancelled);
             r->super.req_status.MPI_SOURCE = st.source;
             r->super.req_status.MPI_TAG = st.tag;
             r->super.req_status._ucount = st.bytes;
+            r->super.req_status._cancelled = cancelled;
         }
         if (rc == MI355X_ERR_TRUNCATE) {
             r->super.req_status.MPI_ERROR = MPI_ERR_TRUNCATE;
@@ -852,6 +886,10 @@ static int nb_progress(void)
         mi355x_request_free(r->eng);
         r->eng = NULL;
         mi355x_ompi_request_complete(&r->super, true);
+        if (r->free_called) {  /* freed by the application while active */
+            mi355x_ompi_request_fini(&r->super);
+            mi355x_obj_release(&r->super.super.super.super);
+        }
         completed++;
     }
     pthread_mutex_unlock(&nb_lock);
@@ -876,6 +914,19 @@ static void nb_stage_release(struct nb_stage *st)
     if (st->stage) mi355x_free(st->stage);
     if (st->ud) mi355x_ddt_destroy(st->ud);
     if (st->pd) mi355x_ddt_destroy(st->pd);
+}
+
+/* put r on the active list (completed by nb_progress) */
+static void nb_activate(mi355x_nbreq_t *r)
+{
+    pthread_mutex_lock(&nb_lock);
+    r->next = nb_active;
+    nb_active = r;
+    if (!nb_registered) {
+        opal_progress_register(nb_progress);
+        nb_registered = 1;
+    }
+    pthread_mutex_unlock(&nb_lock);
 }
 
 static int nb_start_full(mi355x_request_t *eng, struct ompi_communicator_t *comm, ompi_request_t **request, int p2p,
@@ -904,14 +955,7 @@ static int nb_start_full(mi355x_request_t *eng, struct ompi_communicator_t *comm
     r->super.req_status.MPI_ERROR = 0;
     r->super.req_mpi_object.comm = comm;
     r->eng = eng;
-    pthread_mutex_lock(&nb_lock);
-    r->next = nb_active;
-    nb_active = r;
-    if (!nb_registered) {
-        opal_progress_register(nb_progress);
-        nb_registered = 1;
-    }
-    pthread_mutex_unlock(&nb_lock);
+    nb_activate(r);
     *request = &r->super;
     return OMPI_SUCCESS;
 }
@@ -1069,20 +1113,18 @@ int mca_coll_mi355x_ibcast(void *buff, int count, struct ompi_datatype_t *dataty
     return nb_start_full(eng, comm, request, 0, &st);
 }
 
-/* ------------------------------------------------------------------ device point-to-point (PML hook)
- * ob1 moves a device message with its CUDA hooks: the send request gets a CUDA convertor and goes
- * by RGET over smcuda's IPC (pml_ob1_cuda.c:52-100, RDMA btls :104-154, IPC enabling :183-210).
- * coll/mi355x owns a device engine per communicator that already does that protocol device-
- * natively (engine p2p: rendezvous envelope in the shared control segment, the receiver pulls
- * over xGMI), so this shim routes device-buffer point-to-point on those communicators to it.  It
- * is installed the way pml/v parasites the selected PML (pml_v_component.c:110-131): once the PML
- * is selected (coll components are queried after it, ompi_mpi_init.c:610-660) the selected
- * module's table `mca_pml` is saved and its send / receive / probe entries are replaced;
- * everything else -- host buffers, communicators without the engine, buffered sends, persistent
- * and matched-probe requests -- goes to the saved entries unchanged.
- * Matching rule: on an engine communicator a message travels by the engine when
- * the SENDER's buffer is device memory, so a device send must be received into a device buffer
- * (and a host send into a host buffer); a probe looks at both. */
+/* ------------------------------------------------------------------ point-to-point (PML hook)
+ * ob1 matches every message of a communicator in ONE queue whatever the buffer kind, deciding per
+ * request on each side how the bytes move (pml_ob1_cuda.c:52-100, pml_ob1_recvreq.c:647-663): a
+ * device send can meet a host receive, MPI_ANY_SOURCE sees every sender, and messages between a
+ * pair never overtake each other.  coll/mi355x owns an engine per communicator whose point-to-
+ * point does exactly that device-natively (device payloads pulled over xGMI, host payloads through
+ * a shared-memory arena, one match queue; engine p2p.cpp), so on those communicators EVERY
+ * point-to-point call goes to the engine -- host or device buffer, any send mode, persistent and
+ * matched-probe requests included -- and routing never depends on a buffer's kind.  Communicators
+ * without the engine keep the selected PML.  The hook is installed the way pml/v parasites the
+ * selected PML (pml_v_component.c:110-131): once the PML is selected (coll components are queried
+ * after it, ompi_mpi_init.c:610-660) its table `mca_pml` is saved and the entries are replaced. */
 static mca_pml_base_module_t host_pml;
 static int pml_hooked;
 
@@ -1094,7 +1136,8 @@ static mca_coll_mi355x_module_t *engine_module(struct ompi_communicator_t *comm)
     return m->engine ? m : NULL;
 }
 
-/* `count` instances of dt as the engine's (count, layout): contiguous -> bytes and no layout */
+/* `count` instances of dt as the engine's (count, layout): contiguous -> bytes and no layout.
+ * Fails (MPI_ERR_TYPE) only for a layout the convertor cannot describe (more than 2^20 runs). */
 static int p2p_layout(mca_coll_mi355x_module_t *m, struct ompi_datatype_t *dt, size_t count, size_t *ecount,
                       mi355x_ddt_t **d)
 {
@@ -1102,11 +1145,22 @@ static int p2p_layout(mca_coll_mi355x_module_t *m, struct ompi_datatype_t *dt, s
     if (count <= (size_t)0x7fffffff && contiguous_bytes(dt, (int)count, &b)) {
         *ecount = b;
         *d = NULL;
-        return 1;
+        return OMPI_SUCCESS;
     }
     *d = ddt_of(m, dt);
     *ecount = count;
-    return *d != NULL;
+    if (*d) return OMPI_SUCCESS;
+    fprintf(stderr, "[coll/mi355x] point-to-point: the convertor cannot describe datatype %s\n", dt->name);
+    return MPI_ERR_TYPE;
+}
+
+static void status_from(ompi_status_public_t *status, const mi355x_status_t *st, int rc)
+{
+    if (!status) return;  /* MPI_STATUS_IGNORE is NULL */
+    status->MPI_SOURCE = st->source;
+    status->MPI_TAG = st->tag;
+    status->_ucount = st->bytes;
+    status->MPI_ERROR = rc == MI355X_ERR_TRUNCATE ? MPI_ERR_TRUNCATE : (rc ? MPI_ERR_INTERN : 0);
 }
 
 int mca_coll_mi355x_pml_isend(void *buf, size_t count, struct ompi_datatype_t *dt, int dst, int tag,
@@ -1114,38 +1168,41 @@ int mca_coll_mi355x_pml_isend(void *buf, size_t count, struct ompi_datatype_t *d
                               ompi_request_t **request)
 {
     mca_coll_mi355x_module_t *m = engine_module(comm);
+    if (!m) return host_pml.pml_isend(buf, count, dt, dst, tag, mode, comm, request);
     size_t ec = 0;
     mi355x_ddt_t *d = NULL;
-    if (!m || mode == MCA_PML_BASE_SEND_BUFFERED || !is_dev(buf) || !p2p_layout(m, dt, count, &ec, &d))
-        return host_pml.pml_isend(buf, count, dt, dst, tag, mode, comm, request);
+    int rc = p2p_layout(m, dt, count, &ec, &d);
+    if (rc) return rc;
     mi355x_request_t *eng = NULL;
-    const int rc = mi355x_isend(m->engine, buf, ec, d, dst, tag, NULL, &eng);
+    rc = mi355x_isend_mode(m->engine, buf, ec, d, dst, tag, (int)mode, NULL, &eng);
     return rc ? map_rc(rc) : nb_start_kind(eng, comm, request, 1);
 }
 
-/* the engine's sends are rendezvous: they complete once the receiver has the data, which is
- * what every send mode but buffered requires (synchronous included) */
+/* synchronous sends complete once the receiver has the data; buffered and small sends once the
+ * payload is copied (ob1's eager protocol); larger standard sends are rendezvous (engine p2p.cpp) */
 int mca_coll_mi355x_pml_send(void *buf, size_t count, struct ompi_datatype_t *dt, int dst, int tag,
                              mca_pml_base_send_mode_t mode, struct ompi_communicator_t *comm)
 {
     mca_coll_mi355x_module_t *m = engine_module(comm);
+    if (!m) return host_pml.pml_send(buf, count, dt, dst, tag, mode, comm);
     size_t ec = 0;
     mi355x_ddt_t *d = NULL;
-    if (!m || mode == MCA_PML_BASE_SEND_BUFFERED || !is_dev(buf) || !p2p_layout(m, dt, count, &ec, &d))
-        return host_pml.pml_send(buf, count, dt, dst, tag, mode, comm);
-    return map_rc(mi355x_send(m->engine, buf, ec, d, dst, tag, NULL));
+    int rc = p2p_layout(m, dt, count, &ec, &d);
+    if (rc) return rc;
+    return map_rc(mi355x_send_mode(m->engine, buf, ec, d, dst, tag, (int)mode, NULL));
 }
 
 int mca_coll_mi355x_pml_irecv(void *buf, size_t count, struct ompi_datatype_t *dt, int src, int tag,
                               struct ompi_communicator_t *comm, ompi_request_t **request)
 {
     mca_coll_mi355x_module_t *m = engine_module(comm);
+    if (!m) return host_pml.pml_irecv(buf, count, dt, src, tag, comm, request);
     size_t ec = 0;
     mi355x_ddt_t *d = NULL;
-    if (!m || !is_dev(buf) || !p2p_layout(m, dt, count, &ec, &d))
-        return host_pml.pml_irecv(buf, count, dt, src, tag, comm, request);
+    int rc = p2p_layout(m, dt, count, &ec, &d);
+    if (rc) return rc;
     mi355x_request_t *eng = NULL;
-    const int rc = mi355x_irecv(m->engine, buf, ec, d, src, tag, NULL, &eng);
+    rc = mi355x_irecv(m->engine, buf, ec, d, src, tag, NULL, &eng);
     return rc ? map_rc(rc) : nb_start_kind(eng, comm, request, 2);
 }
 
@@ -1153,82 +1210,264 @@ int mca_coll_mi355x_pml_recv(void *buf, size_t count, struct ompi_datatype_t *dt
                              struct ompi_communicator_t *comm, ompi_status_public_t *status)
 {
     mca_coll_mi355x_module_t *m = engine_module(comm);
+    if (!m) return host_pml.pml_recv(buf, count, dt, src, tag, comm, status);
     size_t ec = 0;
     mi355x_ddt_t *d = NULL;
-    if (!m || !is_dev(buf) || !p2p_layout(m, dt, count, &ec, &d))
-        return host_pml.pml_recv(buf, count, dt, src, tag, comm, status);
+    int rc = p2p_layout(m, dt, count, &ec, &d);
+    if (rc) return rc;
     mi355x_status_t st;
     memset(&st, 0, sizeof(st));
-    const int rc = mi355x_recv(m->engine, buf, ec, d, src, tag, NULL, &st);
-    if (status) {  /* MPI_STATUS_IGNORE is NULL */
-        status->MPI_SOURCE = st.source;
-        status->MPI_TAG = st.tag;
-        status->_ucount = st.bytes;
-        status->MPI_ERROR = rc == MI355X_ERR_TRUNCATE ? MPI_ERR_TRUNCATE : (rc ? MPI_ERR_INTERN : 0);
-    }
+    rc = mi355x_recv(m->engine, buf, ec, d, src, tag, NULL, &st);
+    status_from(status, &st, rc);
     if (rc == MI355X_ERR_TRUNCATE) return MPI_ERR_TRUNCATE;
     return map_rc(rc);
 }
 
-/* a probe carries no buffer: the engine's envelopes first, then the host PML's */
+/* every message of an engine communicator is in the engine's queue */
 int mca_coll_mi355x_pml_iprobe(int src, int tag, struct ompi_communicator_t *comm, int *matched,
                                ompi_status_public_t *status)
 {
     mca_coll_mi355x_module_t *m = engine_module(comm);
-    if (m) {
-        mi355x_status_t st;
-        int flag = 0;
-        const int rc = mi355x_iprobe(m->engine, src, tag, &flag, &st);
-        if (rc != MI355X_SUCCESS) return map_rc(rc);
-        if (flag) {
-            *matched = 1;
-            if (status) {
-                status->MPI_SOURCE = st.source;
-                status->MPI_TAG = st.tag;
-                status->_ucount = st.bytes;
-                status->MPI_ERROR = 0;
-            }
-            return OMPI_SUCCESS;
-        }
-    }
-    return host_pml.pml_iprobe(src, tag, comm, matched, status);
+    if (!m) return host_pml.pml_iprobe(src, tag, comm, matched, status);
+    mi355x_status_t st;
+    int flag = 0;
+    memset(&st, 0, sizeof(st));
+    const int rc = mi355x_iprobe(m->engine, src, tag, &flag, &st);
+    if (rc != MI355X_SUCCESS) return map_rc(rc);
+    *matched = flag;
+    if (flag) status_from(status, &st, 0);
+    else opal_progress();  /* ob1's iprobe progresses when nothing matched (pml_ob1_iprobe.c:46-50) */
+    return OMPI_SUCCESS;
 }
 
 int mca_coll_mi355x_pml_probe(int src, int tag, struct ompi_communicator_t *comm, ompi_status_public_t *status)
 {
     if (!engine_module(comm)) return host_pml.pml_probe(src, tag, comm, status);
-    for (;;) {  /* both sources of messages, progressing everything in between */
+    for (;;) {
         int matched = 0;
         const int rc = mca_coll_mi355x_pml_iprobe(src, tag, comm, &matched, status);
         if (rc != OMPI_SUCCESS || matched) return rc;
-        opal_progress();
     }
 }
 
+/* ---- matched probe (MPI_Improbe / MPI_Mprobe + MPI_Imrecv / MPI_Mrecv): the message leaves the
+ * queue at the probe and travels in an ompi_message_t, as ob1 does (pml_ob1_iprobe.c:83-134);
+ * req_ptr holds the engine's message */
+int mca_coll_mi355x_pml_improbe(int src, int tag, struct ompi_communicator_t *comm, int *matched,
+                                struct ompi_message_t **message, ompi_status_public_t *status)
+{
+    mca_coll_mi355x_module_t *m = engine_module(comm);
+    if (!m) return host_pml.pml_improbe(src, tag, comm, matched, message, status);
+    mi355x_status_t st;
+    mi355x_message_t *em = NULL;
+    int flag = 0;
+    memset(&st, 0, sizeof(st));
+    const int rc = mi355x_improbe(m->engine, src, tag, &flag, &em, &st);
+    if (rc != MI355X_SUCCESS) return map_rc(rc);
+    *matched = flag && em;
+    if (!*matched) {
+        *message = &ompi_message_null.message;
+        opal_progress();
+        return OMPI_SUCCESS;
+    }
+    ompi_message_t *msg = (ompi_message_t *)mi355x_obj_new(&ompi_message_t_class);
+    if (!msg) return OMPI_ERR_OUT_OF_RESOURCE;  /* (the engine message stays out of the queue) */
+    msg->m_f_to_c_index = MPI_UNDEFINED;
+    msg->comm = comm;
+    msg->req_ptr = em;
+    msg->peer = st.source;
+    msg->count = st.bytes;
+    *message = msg;
+    status_from(status, &st, 0);
+    return OMPI_SUCCESS;
+}
+
+int mca_coll_mi355x_pml_mprobe(int src, int tag, struct ompi_communicator_t *comm, struct ompi_message_t **message,
+                               ompi_status_public_t *status)
+{
+    if (!engine_module(comm)) return host_pml.pml_mprobe(src, tag, comm, message, status);
+    for (;;) {
+        int matched = 0;
+        const int rc = mca_coll_mi355x_pml_improbe(src, tag, comm, &matched, message, status);
+        if (rc != OMPI_SUCCESS || matched) return rc;
+    }
+}
+
+/* the engine message of an ompi_message_t from our improbe, or NULL (another PML's) */
+static mi355x_message_t *engine_message(struct ompi_message_t *msg, mca_coll_mi355x_module_t **mm)
+{
+    if (!msg || msg == &ompi_message_null.message) return NULL;
+    *mm = engine_module(msg->comm);
+    return *mm ? (mi355x_message_t *)msg->req_ptr : NULL;
+}
+
+int mca_coll_mi355x_pml_imrecv(void *buf, size_t count, struct ompi_datatype_t *dt, struct ompi_message_t **message,
+                               ompi_request_t **request)
+{
+    mca_coll_mi355x_module_t *m = NULL;
+    mi355x_message_t *em = engine_message(*message, &m);
+    if (!em) return host_pml.pml_imrecv(buf, count, dt, message, request);
+    size_t ec = 0;
+    mi355x_ddt_t *d = NULL;
+    int rc = p2p_layout(m, dt, count, &ec, &d);
+    if (rc) return rc;
+    struct ompi_communicator_t *comm = (*message)->comm;
+    mi355x_request_t *eng = NULL;
+    rc = mi355x_imrecv(m->engine, buf, ec, d, em, NULL, &eng);
+    if (rc) return map_rc(rc);
+    mi355x_obj_release(&(*message)->super.super);   /* ob1: ompi_message_return */
+    *message = &ompi_message_null.message;
+    return nb_start_kind(eng, comm, request, 2);
+}
+
+int mca_coll_mi355x_pml_mrecv(void *buf, size_t count, struct ompi_datatype_t *dt, struct ompi_message_t **message,
+                              ompi_status_public_t *status)
+{
+    mca_coll_mi355x_module_t *m = NULL;
+    mi355x_message_t *em = engine_message(*message, &m);
+    if (!em) return host_pml.pml_mrecv(buf, count, dt, message, status);
+    size_t ec = 0;
+    mi355x_ddt_t *d = NULL;
+    int rc = p2p_layout(m, dt, count, &ec, &d);
+    if (rc) return rc;
+    mi355x_request_t *eng = NULL;
+    rc = mi355x_imrecv(m->engine, buf, ec, d, em, NULL, &eng);
+    if (rc) return map_rc(rc);
+    mi355x_obj_release(&(*message)->super.super);
+    *message = &ompi_message_null.message;
+    rc = mi355x_request_wait(eng);
+    mi355x_status_t st;
+    memset(&st, 0, sizeof(st));
+    mi355x_request_get_status(eng, &st);
+    if (rc != MI355X_ERR_TIMEOUT) mi355x_request_free(eng);
+    status_from(status, &st, rc);
+    if (rc == MI355X_ERR_TRUNCATE) return MPI_ERR_TRUNCATE;
+    return map_rc(rc);
+}
+
+/* ---- persistent requests (MPI_Send_init / MPI_Recv_init / MPI_Start): the arguments are kept in
+ * the request and every MPI_Start posts them to the engine (ob1: mca_pml_ob1_start,
+ * pml_ob1_start.c:29-…); completion leaves the request INACTIVE for the next start (the MPI
+ * layer's wait does that, req_wait.c:59-63) */
+static int pers_init(int kind, void *buf, size_t count, struct ompi_datatype_t *dt, int peer, int tag, int mode,
+                     struct ompi_communicator_t *comm, ompi_request_t **request)
+{
+    mi355x_nbreq_t *r = (mi355x_nbreq_t *)mi355x_obj_new(&mi355x_nbreq_t_class);
+    if (!r) return OMPI_ERR_OUT_OF_RESOURCE;
+    r->p2p = kind;
+    r->pers = kind;
+    r->pbuf = buf;
+    r->pcount = count;
+    r->pdt = dt;
+    r->ppeer = peer;
+    r->ptag = tag;
+    r->pmode = mode;
+    r->super.req_type = OMPI_REQUEST_PML;
+    r->super.req_complete = false;    /* OMPI_REQUEST_INIT(req, persistent), request.h:139-144 */
+    r->super.req_state = OMPI_REQUEST_INACTIVE;
+    r->super.req_persistent = true;
+    r->super.req_mpi_object.comm = comm;
+    *request = &r->super;
+    return OMPI_SUCCESS;
+}
+
+int mca_coll_mi355x_pml_isend_init(void *buf, size_t count, struct ompi_datatype_t *dt, int dst, int tag,
+                                   mca_pml_base_send_mode_t mode, struct ompi_communicator_t *comm,
+                                   ompi_request_t **request)
+{
+    if (!engine_module(comm)) return host_pml.pml_isend_init(buf, count, dt, dst, tag, mode, comm, request);
+    return pers_init(1, buf, count, dt, dst, tag, (int)mode, comm, request);
+}
+
+int mca_coll_mi355x_pml_irecv_init(void *buf, size_t count, struct ompi_datatype_t *dt, int src, int tag,
+                                   struct ompi_communicator_t *comm, ompi_request_t **request)
+{
+    if (!engine_module(comm)) return host_pml.pml_irecv_init(buf, count, dt, src, tag, comm, request);
+    return pers_init(2, buf, count, dt, src, tag, 0, comm, request);
+}
+
+static int pers_start(mi355x_nbreq_t *r)
+{
+    if (r->eng) return MPI_ERR_REQUEST;  /* still in flight: MPI forbids a second start */
+    struct ompi_communicator_t *comm = r->super.req_mpi_object.comm;
+    mca_coll_mi355x_module_t *m = engine_module(comm);
+    if (!m) return OMPI_ERROR;
+    size_t ec = 0;
+    mi355x_ddt_t *d = NULL;
+    int rc = p2p_layout(m, r->pdt, r->pcount, &ec, &d);
+    if (rc) return rc;
+    mi355x_request_t *eng = NULL;
+    rc = r->pers == 1 ? mi355x_isend_mode(m->engine, r->pbuf, ec, d, r->ppeer, r->ptag, r->pmode, NULL, &eng)
+                      : mi355x_irecv(m->engine, r->pbuf, ec, d, r->ppeer, r->ptag, NULL, &eng);
+    if (rc) return map_rc(rc);
+    memset(&r->super.req_status, 0, sizeof(r->super.req_status));
+    r->super.req_complete = false;
+    r->super.req_state = OMPI_REQUEST_ACTIVE;
+    r->eng = eng;
+    nb_activate(r);
+    return OMPI_SUCCESS;
+}
+
+int mca_coll_mi355x_pml_start(size_t count, ompi_request_t **requests)
+{
+    for (size_t i = 0; i < count; ++i) {
+        ompi_request_t *q = requests[i];
+        if (!q || q->req_type != OMPI_REQUEST_PML) continue;
+        int rc;
+        if (q->req_free == nbreq_free && ((mi355x_nbreq_t *)q)->pers) rc = pers_start((mi355x_nbreq_t *)q);
+        else rc = host_pml.pml_start ? host_pml.pml_start(1, &requests[i]) : OMPI_ERR_NOT_SUPPORTED;
+        if (rc != OMPI_SUCCESS) return rc;
+    }
+    return OMPI_SUCCESS;
+}
+
 /* install / remove the hook (idempotent) */
+#define HOOK(F)                                                                 \
+    do {                                                                        \
+        if (mca_pml.pml_##F) mca_pml.pml_##F = mca_coll_mi355x_pml_##F;         \
+    } while (0)
+#define UNHOOK(F)                                                               \
+    do {                                                                        \
+        if (mca_pml.pml_##F == mca_coll_mi355x_pml_##F) mca_pml.pml_##F = host_pml.pml_##F; \
+    } while (0)
+
 static void pml_hook_install(void)
 {
     if (pml_hooked || mca_coll_mi355x_pml_hook == 0) return;
     if (!mca_pml.pml_isend || !mca_pml.pml_irecv || !mca_pml.pml_send || !mca_pml.pml_recv) return;  /* no PML */
     host_pml = mca_pml;
-    mca_pml.pml_isend = mca_coll_mi355x_pml_isend;
-    mca_pml.pml_send = mca_coll_mi355x_pml_send;
-    mca_pml.pml_irecv = mca_coll_mi355x_pml_irecv;
-    mca_pml.pml_recv = mca_coll_mi355x_pml_recv;
-    if (mca_pml.pml_iprobe) mca_pml.pml_iprobe = mca_coll_mi355x_pml_iprobe;
-    if (mca_pml.pml_probe) mca_pml.pml_probe = mca_coll_mi355x_pml_probe;
+    HOOK(isend);
+    HOOK(send);
+    HOOK(irecv);
+    HOOK(recv);
+    HOOK(iprobe);
+    HOOK(probe);
+    HOOK(improbe);
+    HOOK(mprobe);
+    HOOK(imrecv);
+    HOOK(mrecv);
+    HOOK(isend_init);
+    HOOK(irecv_init);
+    HOOK(start);
     pml_hooked = 1;
 }
 
 static void pml_hook_remove(void)
 {
     if (!pml_hooked) return;
-    if (mca_pml.pml_isend == mca_coll_mi355x_pml_isend) mca_pml.pml_isend = host_pml.pml_isend;
-    if (mca_pml.pml_send == mca_coll_mi355x_pml_send) mca_pml.pml_send = host_pml.pml_send;
-    if (mca_pml.pml_irecv == mca_coll_mi355x_pml_irecv) mca_pml.pml_irecv = host_pml.pml_irecv;
-    if (mca_pml.pml_recv == mca_coll_mi355x_pml_recv) mca_pml.pml_recv = host_pml.pml_recv;
-    if (mca_pml.pml_iprobe == mca_coll_mi355x_pml_iprobe) mca_pml.pml_iprobe = host_pml.pml_iprobe;
-    if (mca_pml.pml_probe == mca_coll_mi355x_pml_probe) mca_pml.pml_probe = host_pml.pml_probe;
+    UNHOOK(isend);
+    UNHOOK(send);
+    UNHOOK(irecv);
+    UNHOOK(recv);
+    UNHOOK(iprobe);
+    UNHOOK(probe);
+    UNHOOK(improbe);
+    UNHOOK(mprobe);
+    UNHOOK(imrecv);
+    UNHOOK(mrecv);
+    UNHOOK(isend_init);
+    UNHOOK(irecv_init);
+    UNHOOK(start);
     pml_hooked = 0;
 }
 
@@ -1243,25 +1482,61 @@ static void pml_hook_remove(void)
 
 /* coll/tuned's own tuning, honoured so that a job tuned for the reference keeps its choices:
  * with coll_tuned_use_dynamic_rules set (coll_tuned_component.c:151-167), the forced algorithms
- * (coll_tuned_{allreduce,reduce,reduce_scatter}_algorithm, reduce_algorithm_chain_fanout) and
- * the rules file coll_tuned_dynamic_rules_filename (read once per process, like
- * mca_coll_tuned_component.all_base_rules, coll_tuned_component.c:213-229) */
+ * (coll_tuned_{allreduce,reduce,reduce_scatter}_algorithm, reduce_algorithm_chain_fanout;
+ * coll_tuned_allreduce.c:949-1005 and siblings) and the rules file
+ * coll_tuned_dynamic_rules_filename (read once per process, like
+ * mca_coll_tuned_component.all_base_rules, coll_tuned_component.c:213-229).  The values are read
+ * from coll/tuned's own registered variables through the MCA variable system (mca_base_var_find +
+ * mca_base_var_get_value, as tuned_open reads coll_base_verbose, coll_tuned_component.c:200-209),
+ * so every source opal knows -- command line, environment, openmpi-mca-params.conf,
+ * mca_base_param_files -- reaches the engine exactly as it reaches coll/tuned.  Only when no
+ * variable system or no coll/tuned registration is present does the component read
+ * OMPI_MCA_coll_tuned_<name> from the environment itself. */
 static mi355x_rules_t *tuned_rules;
 static int tuned_rules_read;
 
+/* pointer to coll/tuned's storage of variable `name`, or NULL */
+static const void *tuned_var(const char *name)
+{
+    if (!mca_base_var_find || !mca_base_var_get_value) return NULL;
+    const int idx = mca_base_var_find("ompi", "coll", "tuned", name);
+    if (idx < 0) return NULL;
+    const void *storage = NULL;
+    if (mca_base_var_get_value(idx, &storage, NULL, NULL) != OMPI_SUCCESS) return NULL;
+    return storage;
+}
+
+static int tuned_int(const char *name, int is_bool)
+{
+    const void *p = tuned_var(name);
+    if (p) return is_bool ? (int)*(const bool *)p : *(const int *)p;
+    char env[96];
+    snprintf(env, sizeof(env), "OMPI_MCA_coll_tuned_%s", name);
+    return env_int(env, 0);
+}
+
+static const char *tuned_string(const char *name)
+{
+    const void *p = tuned_var(name);
+    if (p) return *(char *const *)p;
+    char env[96];
+    snprintf(env, sizeof(env), "OMPI_MCA_coll_tuned_%s", name);
+    return getenv(env);
+}
+
 static void apply_tuned_params(mca_coll_mi355x_module_t *m)
 {
-    if (!env_int("OMPI_MCA_coll_tuned_use_dynamic_rules", 0)) return;
-    const int ar = env_int("OMPI_MCA_coll_tuned_allreduce_algorithm", 0);
-    const int red = env_int("OMPI_MCA_coll_tuned_reduce_algorithm", 0);
-    const int fo = env_int("OMPI_MCA_coll_tuned_reduce_algorithm_chain_fanout", 0);
-    const int rs = env_int("OMPI_MCA_coll_tuned_reduce_scatter_algorithm", 0);
+    if (!tuned_int("use_dynamic_rules", 1)) return;
+    const int ar = tuned_int("allreduce_algorithm", 0);
+    const int red = tuned_int("reduce_algorithm", 0);
+    const int fo = tuned_int("reduce_algorithm_chain_fanout", 0);
+    const int rs = tuned_int("reduce_scatter_algorithm", 0);
     if (ar && !mca_coll_mi355x_allreduce_algorithm) mi355x_comm_set(m->engine, MI355X_KNOB_ALLREDUCE_ALG, ar);
     if (red) mi355x_comm_set(m->engine, MI355X_KNOB_REDUCE_ALG, red);
     if (fo) mi355x_comm_set(m->engine, MI355X_KNOB_REDUCE_CHAIN_FANOUT, fo);
     if (rs) mi355x_comm_set(m->engine, MI355X_KNOB_REDUCE_SCATTER_ALG, rs);
-    const char *file = getenv("OMPI_MCA_coll_tuned_dynamic_rules_filename");
-    if (file && !tuned_rules_read) {
+    const char *file = tuned_string("dynamic_rules_filename");
+    if (file && *file && !tuned_rules_read) {
         tuned_rules_read = 1;
         if (mi355x_rules_load(file, &tuned_rules) < 0) {
             fprintf(stderr, "[coll/mi355x] %s -- ignoring the rules file\n", mi355x_last_error());
@@ -1379,6 +1654,7 @@ static int component_init_query(bool enable_progress_threads, bool enable_mpi_th
     int n = 0;
     if (mi355x_device_count(&n) != MI355X_SUCCESS || n < 1) return OMPI_ERR_NOT_SUPPORTED;
     pml_hook_install();  /* the PML is selected by now (ompi_mpi_init.c:610 before :660) */
+    mi355x_set_progress_hook(opal_progress);  /* the engine's host-side waits keep MPI progressing */
     return OMPI_SUCCESS;
 }
 

@@ -1555,6 +1555,19 @@ int mi355x_comm_barrier(mi355x_comm_t *c)
     drain(c);
     return barrier(c);
 }
+static void (*g_progress_hook)(void) = nullptr;
+int mi355x_set_progress_hook(void (*progress)(void))
+{
+    g_progress_hook = progress;
+    return MI355X_SUCCESS;
+}
+
+// A host-buffer rank waits here for its peers' votes.  It must not stall other work meanwhile: the
+// wait drives the caller's progress engine (opal_progress through the hook) and this
+// communicator's point-to-point, so a peer that first needs an outstanding send of ours to
+// complete still gets there (ob1's blocking waits progress the same way, req_wait.c).  The wait is
+// unbounded, like a host collective's receive: a rank that is late by minutes (checkpoint I/O) is
+// not an error, and nothing poisons the communicator.
 int mi355x_comm_vote(mi355x_comm_t *c, int device, int *any_device)
 {
     if (!c || !any_device) return set_error(MI355X_ERR_ARG, "NULL argument");
@@ -1564,7 +1577,6 @@ int mi355x_comm_vote(mi355x_comm_t *c, int device, int *any_device)
     Ctrl *k = c->ctrl;
     k->slot[c->rank].vote[s % kVoteRing].store((s << 1) | (device ? 1u : 0u), std::memory_order_release);
     if (device) return MI355X_SUCCESS;
-    const auto t0 = std::chrono::steady_clock::now();
     for (int r = 0; r < c->size; ++r) {
         if (r == c->rank) continue;
         unsigned spins = 0;
@@ -1580,13 +1592,11 @@ int mi355x_comm_vote(mi355x_comm_t *c, int device, int *any_device)
             if (k->abort_flag.load(std::memory_order_relaxed))
                 return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
             if (++spins > 2048) {
-                sched_yield();
-                if ((spins & 0xffff) == 0 &&
-                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
-                    k->abort_flag.store(1);
-                    return set_error(MI355X_ERR_TIMEOUT, "rank %d: buffer-kind vote %llu timed out waiting for rank %d",
-                                     c->rank, (unsigned long long)s, r);
+                if ((spins & 63) == 0) {
+                    if (c->p2p) (void)p2p_progress(c);
+                    if (g_progress_hook) g_progress_hook();
                 }
+                sched_yield();
             }
         }
     }

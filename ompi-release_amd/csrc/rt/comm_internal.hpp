@@ -90,9 +90,10 @@ constexpr int kP2PSlots = 32;
 struct alignas(64) Envelope {
     std::atomic<uint64_t> full;   // message number + 1 once posted (sender, release)
     std::atomic<uint64_t> done;   // message number + 1 once the receiver no longer reads it
-    int32_t tag, flags;
+    int32_t tag, flags;           // flags: kEnvPacked, kEnvHost (p2p.cpp)
     uint64_t bytes;               // packed size of the message
-    BufDesc buf;                  // where the (packed) bytes are: the sender's export
+    BufDesc buf;                  // where the (packed) bytes are: the sender's device export, or
+                                  // (kEnvHost) its host arena: id = segment generation, off = offset
 };
 inline size_t p2p_offset(int size)
 {
@@ -184,10 +185,19 @@ struct mi355x_request {
     uint64_t msg = 0;                     // send: message number to `peer`
     mi355x::BufDesc desc;                 // send: the export announced in the envelope
     mi355x::Envelope *env = nullptr;      // the envelope in flight
-    void *packed = nullptr;               // send: packed copy in the arena (non-contiguous types)
+    void *packed = nullptr;               // send: copy in the device arena (packed layout / buffered)
     mi355x::PeerMap *pin = nullptr;       // receive: the pinned mapping being read
     int st_source = 0, st_tag = 0, st_error = 0;
     size_t st_bytes = 0;
+    int mode = 4;                         // send mode (MI355X_SEND_*; 4 standard)
+    bool host = false;                    // the caller's buffer is host memory
+    bool internal = false;                // send owned by the engine: the caller's request completed
+                                          // when the payload was copied (eager / buffered)
+    bool cancelled = false;               // receive cancelled before it matched
+    int32_t env_flags = 0;                // send: kEnvPacked / kEnvHost (p2p.cpp)
+    void *hslot = nullptr;                // send: payload slot in the host shared-memory arena
+    void *stage = nullptr;                // receive: device staging slot (host destination)
+    std::vector<char> htmp;               // receive: host copy awaiting the host convertor
 };
 
 struct mi355x_comm {

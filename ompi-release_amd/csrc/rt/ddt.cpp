@@ -4,6 +4,7 @@
 // ompi_datatype_create_indexed.c:32-66 incl. the merge of adjacent blocks) and, for drop-in use
 // inside Open MPI, compile an optimized opal description (opt_desc: ELEM / LOOP / END_LOOP
 // records, opal/datatype/opal_datatype_internal.h:148-188) into the same layout.
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -292,6 +293,114 @@ int mi355x_pack(const mi355x_ddt_t *d, size_t count, const void *base, size_t po
                 uint32_t *checksum, void *stream)
 {
     return ddt_move(d, true, count, const_cast<void *>(base), pos, dst, bytes, checksum, stream);
+}
+
+} // extern "C"
+
+namespace mi355x {
+// The type map as memory pieces in packed-stream order, from packed position `pos`: fn(offset of
+// the piece from base, its length, its packed position) for pieces covering [pos, pos + bytes).
+// Instance k, block j, run r sits at k*extent + j*stride + disp[r]; a run is cut only at the
+// window's edges; fn returns false to stop early.  Returns false when the window runs past count
+// instances.
+template <class F>
+static bool walk(const mi355x_ddt *d, size_t count, size_t pos, size_t bytes, F &&fn)
+{
+    const int64_t blk = blk_bytes(d), inst = d->nblk * blk;
+    if ((int64_t)(pos + bytes) > (int64_t)count * inst) return false;
+    if (bytes == 0 || inst == 0) return true;
+    int64_t k = (int64_t)pos / inst, rem = (int64_t)pos % inst;
+    int64_t j = rem / blk, in_blk = rem % blk;
+    size_t r = (size_t)(std::upper_bound(d->pfx.begin(), d->pfx.end(), in_blk) - d->pfx.begin()) - 1;
+    while (r + 1 < d->len.size() && d->len[r] == 0) ++r;  // zero-length runs hold no bytes
+    int64_t within = in_blk - d->pfx[r];
+    size_t done = 0;
+    while (done < bytes) {
+        const int64_t avail = d->len[r] - within;
+        const size_t take = (size_t)std::min<int64_t>(avail, (int64_t)(bytes - done));
+        if (take && !fn(k * d->extent + j * d->stride + d->disp[r] + within, take, pos + done)) return true;
+        done += take;
+        within += (int64_t)take;
+        if (within == d->len[r]) {
+            within = 0;
+            if (++r == d->len.size()) {
+                r = 0;
+                if (++j == d->nblk) {
+                    j = 0;
+                    ++k;
+                }
+            }
+        }
+    }
+    return true;
+}
+} // namespace mi355x
+
+extern "C" {
+
+// the convertor on host memory: what ob1 does for a host buffer with a derived datatype
+// (opal_generic_simple_pack / _unpack, opal_datatype_pack.c:250-374, opal_datatype_unpack.c:245-…)
+int mi355x_pack_host(const mi355x_ddt_t *d, size_t count, const void *base, size_t pos, void *dst, size_t bytes)
+{
+    if (!d || (bytes && (!base || !dst))) return set_error(MI355X_ERR_ARG, "bad host pack arguments");
+    const char *b = (const char *)base;
+    char *o = (char *)dst;
+    if (!walk(d, count, pos, bytes, [&](int64_t off, size_t len, size_t p) {
+            std::memcpy(o + (p - pos), b + off, len);
+            return true;
+        }))
+        return set_error(MI355X_ERR_ARG, "window past the message");
+    return MI355X_SUCCESS;
+}
+
+int mi355x_unpack_host(const mi355x_ddt_t *d, size_t count, void *base, size_t pos, const void *src, size_t bytes)
+{
+    if (!d || (bytes && (!base || !src))) return set_error(MI355X_ERR_ARG, "bad host unpack arguments");
+    char *b = (char *)base;
+    const char *i = (const char *)src;
+    if (!walk(d, count, pos, bytes, [&](int64_t off, size_t len, size_t p) {
+            std::memcpy(b + off, i + (p - pos), len);
+            return true;
+        }))
+        return set_error(MI355X_ERR_ARG, "window past the message");
+    return MI355X_SUCCESS;
+}
+
+// opal_convertor_raw (opal/datatype/opal_convertor_raw.c:37-…): the memory pieces of the type map
+// from packed position *pos, at most *iov_count of them; *iov_count = pieces returned, *max_data =
+// their bytes, *pos advanced.  Returns 1 once the whole message has been described, else 0 (the
+// reference's return convention).  Runs are merged where the layout merges them (adjacent blocks of
+// one constructor), so a piece may cover several of the reference's iovecs; the byte sequence is
+// the same.
+int mi355x_ddt_raw(const mi355x_ddt_t *d, size_t count, size_t *pos, int64_t *disp, size_t *len, uint32_t *iov_count,
+                   size_t *max_data)
+{
+    if (!d || !pos || !iov_count || !max_data || (*iov_count && (!disp || !len)))
+        return set_error(MI355X_ERR_ARG, "bad raw arguments");
+    const size_t total = count * (size_t)(d->nblk * blk_bytes(d));
+    const uint32_t cap = *iov_count;
+    uint32_t n = 0;
+    size_t got = 0;
+    size_t p = *pos;
+    while (n < cap && p < total) {
+        // one piece: the rest of the current run
+        int64_t off0 = 0;
+        size_t len0 = 0;
+        (void)walk(d, count, p, total - p, [&](int64_t off, size_t l, size_t) {
+            off0 = off;
+            len0 = l;
+            return false;
+        });
+        disp[n] = off0;
+        len[n] = len0;
+        ++n;
+        got += len0;
+        p += len0;
+    }
+    *iov_count = n;
+    *max_data = got;
+    *pos = p;
+    return p >= total ? 1 : 0;
 }
 
 int mi355x_unpack(const mi355x_ddt_t *d, size_t count, void *base, size_t pos, const void *src, size_t bytes,

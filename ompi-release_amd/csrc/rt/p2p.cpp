@@ -1,30 +1,46 @@
-// p2p.cpp -- device point-to-point (MPI_Send / MPI_Recv / MPI_Isend / MPI_Irecv / MPI_Sendrecv /
-// MPI_Iprobe) between the ranks of a coll/mi355x communicator.
+// p2p.cpp -- point-to-point (MPI_Send / MPI_Recv / MPI_Isend / MPI_Irecv / MPI_Sendrecv /
+// MPI_Iprobe / MPI_Improbe + MPI_Imrecv) between the ranks of a coll/mi355x communicator, on device
+// and host buffers, in one matching queue.
 //
-// What it replaces: the reference moves a device message with ob1's RGET protocol over
-// btl/smcuda.  The sender registers its buffer (CUDA IPC handle, mpool/rgpusm cache) and sends a
-// rendezvous header carrying the handle (pml_ob1_cuda.c:52-100, pml_ob1_sendreq.c RGET start);
-// the receiver matches it (pml_ob1_recvfrag.c match loop: per-source order, posted receives in
-// posting order, MPI_ANY_SOURCE / MPI_ANY_TAG), opens the handle and copies out of the sender's
-// GPU buffer (mca_btl_smcuda_get_cuda, btl_smcuda.c:1083-1168), then returns a FIN so the send
-// completes.  Non-contiguous layouts go through the GPU convertor (opal_datatype_cuda.c).
+// What it replaces: ob1 matches every message of a communicator in one queue whatever the buffer
+// kind, and decides per request, on each side, how the bytes move (pml_ob1_cuda.c:52-100 on the
+// send side, pml_ob1_recvreq.c:647-663 on the receive side).  A device message goes by RGET over
+// btl/smcuda: the sender registers its buffer (CUDA IPC handle, mpool/rgpusm cache) and sends a
+// rendezvous header carrying the handle; the receiver matches it (pml_ob1_recvfrag.c match loop:
+// per-source order, posted receives in posting order, MPI_ANY_SOURCE / MPI_ANY_TAG), opens the
+// handle and copies out of the sender's GPU buffer (mca_btl_smcuda_get_cuda,
+// btl_smcuda.c:1083-1168), then returns a FIN so the send completes.  A host message (and a small
+// device one) goes through the sm BTL's shared-memory fragments: eager up to 4 KiB
+// (btl_sm_component.c:244), rendezvous beyond.
 //
 // Here, MI355X-first:
-//   * the rendezvous header is an Envelope in the communicator's shared control segment: one
+//   * the match / RGET header is an Envelope in the communicator's shared control segment: one
 //     ring of kP2PSlots per ordered pair (src, dst), filled by src, drained by dst in order
 //     (comm_internal.hpp); `full` announces message m, `done` is the FIN;
-//   * the sender exports its buffer once (the registration cache of coll_comm.cpp; dmabuf for
-//     allocations of 2 GiB or more); a non-contiguous send is first packed by the GPU convertor
-//     into the communicator's exportable arena;
-//   * the receiver PULLS: one kernel on its own GPU reads the sender's bytes over xGMI and writes
-//     them into the receive buffer (k_multicopy for a contiguous receive, the unpack kernel for a
-//     derived datatype) -- nothing is ever written into the peer's memory;
+//   * where the bytes wait for the receiver:
+//       - a device payload above 4 KiB: the sender's own buffer, exported once (the registration
+//         cache of coll_comm.cpp; dmabuf for allocations of 2 GiB or more), or -- a non-contiguous
+//         layout, or a buffered send -- a copy in the communicator's exportable device arena
+//         (the GPU convertor packs into it);
+//       - a host payload, or a device payload of at most 4 KiB: a copy in the sender's host
+//         arena, a POSIX shared-memory segment the receiver maps (the sm BTL's role);
+//   * the receiver PULLS: a device payload is read over xGMI by one kernel on its own GPU
+//     (k_multicopy, or the convertor's unpack kernel for a derived datatype) into the receive
+//     buffer -- or into a device staging slot, then to host memory, for a host receive; a host
+//     payload is copied out of the mapped segment (memcpy / host convertor, or host-to-device
+//     copy).  Nothing is ever written into the peer's memory;
+//   * completion of a send: eager (the caller's request completes once the payload is copied --
+//     the engine keeps an internal request for the envelope) for messages of at most 4 KiB and
+//     buffered sends, rendezvous (the FIN) otherwise and for synchronous sends;
 //   * progress is polled (mi355x_p2p_progress, the opal_progress hook; test / wait call it):
 //     queued sends are announced, mailboxes drained, posted receives matched, finished reads
 //     acknowledged, acknowledged sends completed.
 // Truncation follows ob1 (pml_ob1_recvreq.h:172-180): the receive gets as many bytes as its
 // buffer holds, status.bytes is the message size and status.error MI355X_ERR_TRUNCATE.
+#include <fcntl.h>
 #include <sched.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 
 #include <algorithm>
 #include <chrono>
@@ -35,10 +51,38 @@
 
 namespace mi355x {
 
+constexpr size_t kEagerLimit = 4096;          // btl_sm_component.c:244, btl_smcuda_component.c:183
+constexpr int32_t kEnvPacked = 1;             // the payload is a packed copy (layout unused)
+constexpr int32_t kEnvHost = 2;               // the payload is in the sender's host arena
+
 struct P2PMsg {   // an announced message not matched yet (ob1's unexpected queue)
     int src;
     uint64_t m;
     Envelope *env;
+};
+
+// bump-allocated staging; reset when no slot is in use; a full arena is replaced by a larger one
+// and kept (retired) until its last slot is released
+struct DevArena {
+    char *base = nullptr;
+    size_t bytes = 0, used = 0;
+    int users = 0;
+    std::vector<void *> retired;
+};
+
+// the sender's host arena: one shared-memory segment per generation, named after the control
+// segment, the rank and the generation; receivers map it on first use
+struct HostSeg {
+    char *base;
+    size_t bytes;
+    uint32_t gen;
+    std::string name;
+};
+struct HostArena {
+    HostSeg cur{nullptr, 0, 0, std::string()};
+    size_t used = 0;
+    int users = 0;
+    std::vector<HostSeg> retired;
 };
 
 struct P2P {
@@ -51,13 +95,13 @@ struct P2P {
     std::deque<mi355x_request *> queued;   // sends waiting for a free envelope, posting order
     std::vector<mi355x_request *> sending; // announced, waiting for the receiver's FIN
     std::vector<mi355x_request *> reading; // matched receives whose pull is in flight
-    // exportable arena for packed copies of non-contiguous sends (bump allocated; reset when no
-    // packed send is outstanding; never a small allocation, see ensure_scratch)
-    char *arena = nullptr;
-    size_t arena_bytes = 0, arena_used = 0;
-    int arena_users = 0;
-    std::vector<void *> retired;
+    DevArena arena;                        // exportable: packed / buffered device payloads
+    DevArena rstage;                       // receive side: device staging of host receives
+    HostArena harena;                      // host payloads (shared memory)
+    std::map<std::pair<int, uint32_t>, HostSeg> peer_segs;  // peers' host arenas, mapped
 };
+
+static void seg_drop(HostSeg &g, bool owner);
 
 static P2P *p2p_of(mi355x_comm *c)
 {
@@ -90,40 +134,158 @@ void p2p_destroy(mi355x_comm *c)
     }
     for (mi355x_request *r : p->reading)
         if (r->pin) r->pin->pins--;
-    if (p->arena) (void)hipFree(p->arena);
-    for (void *a : p->retired) (void)hipFree(a);
+    // sends the engine owns (eager / buffered) that never saw their FIN
+    for (mi355x_request *r : p->queued)
+        if (r->internal) delete r;
+    for (mi355x_request *r : p->sending)
+        if (r->internal) delete r;
+    for (DevArena *a : {&p->arena, &p->rstage}) {
+        if (a->base) (void)hipFree(a->base);
+        for (void *x : a->retired) (void)hipFree(x);
+    }
+    seg_drop(p->harena.cur, true);
+    for (HostSeg &g : p->harena.retired) seg_drop(g, true);
+    for (auto &kv : p->peer_segs) seg_drop(kv.second, false);
     delete p;
     c->p2p = nullptr;
 }
 
-static int arena_alloc(P2P *p, size_t bytes, void **out)
+static int arena_alloc(DevArena &a, size_t bytes, void **out)
 {
     const size_t need = (bytes + 255) & ~(size_t)255;
-    if (p->arena_used + need > p->arena_bytes) {
-        if (p->arena) {
-            if (p->arena_users > 0) p->retired.push_back(p->arena);  // peers may still read it
-            else MI_HIP(hipFree(p->arena));
+    if (a.used + need > a.bytes) {
+        if (a.base) {
+            if (a.users > 0) a.retired.push_back(a.base);  // peers may still read it
+            else MI_HIP(hipFree(a.base));
         }
-        p->arena = nullptr;
-        size_t want = std::max<size_t>((size_t)8 << 20, p->arena_bytes * 2);
+        a.base = nullptr;
+        size_t want = std::max<size_t>((size_t)8 << 20, a.bytes * 2);
         while (want < need) want *= 2;
-        p->arena_bytes = 0;
-        p->arena_used = 0;
-        MI_HIP(hipMalloc((void **)&p->arena, want));
-        p->arena_bytes = want;
+        a.bytes = 0;
+        a.used = 0;
+        MI_HIP(hipMalloc((void **)&a.base, want));
+        a.bytes = want;
     }
-    *out = p->arena + p->arena_used;
-    p->arena_used += need;
-    p->arena_users++;
+    *out = a.base + a.used;
+    a.used += need;
+    a.users++;
     return MI355X_SUCCESS;
 }
 
-static void arena_release(P2P *p)
+static void arena_release(DevArena &a)
 {
-    if (--p->arena_users > 0) return;
-    p->arena_used = 0;
-    for (void *a : p->retired) (void)hipFree(a);
-    p->retired.clear();
+    if (--a.users > 0) return;
+    a.used = 0;
+    for (void *x : a.retired) (void)hipFree(x);
+    a.retired.clear();
+}
+
+static void seg_drop(HostSeg &g, bool owner)
+{
+    if (!g.base) return;
+    munmap(g.base, g.bytes);
+    if (owner && !g.name.empty()) shm_unlink(g.name.c_str());
+    g.base = nullptr;
+}
+
+static std::string seg_name(const mi355x_comm *c, int rank, uint32_t gen)
+{
+    return c->shm_name + "_h" + std::to_string(rank) + "_" + std::to_string(gen);
+}
+
+// a slot of `bytes` in my host arena; desc describes it to the receiver
+static int harena_alloc(mi355x_comm *c, P2P *p, size_t bytes, void **out, BufDesc *desc)
+{
+    HostArena &h = p->harena;
+    const size_t need = (bytes + 63) & ~(size_t)63;
+    if (h.used + need > h.cur.bytes) {
+        if (h.cur.base) {
+            if (h.users > 0) h.retired.push_back(h.cur);
+            else seg_drop(h.cur, true);
+        }
+        size_t want = std::max<size_t>((size_t)1 << 20, h.cur.bytes * 2);
+        while (want < need) want *= 2;
+        HostSeg g{nullptr, want, h.cur.gen + 1, std::string()};
+        if (c->loopback) {  // threads of one process: plain memory, read through the pointer
+            void *m = mmap(nullptr, want, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+            if (m == MAP_FAILED) return set_error(MI355X_ERR_NOMEM, "host arena of %zu bytes", want);
+            g.base = (char *)m;
+        } else {
+            g.name = seg_name(c, c->rank, g.gen);
+            const int fd = shm_open(g.name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+            if (fd < 0) return set_error(MI355X_ERR_NOMEM, "host arena %s: %s", g.name.c_str(), strerror(errno));
+            void *m = MAP_FAILED;
+            if (ftruncate(fd, (off_t)want) == 0) m = mmap(nullptr, want, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            close(fd);
+            if (m == MAP_FAILED) {
+                shm_unlink(g.name.c_str());
+                return set_error(MI355X_ERR_NOMEM, "host arena %s of %zu bytes", g.name.c_str(), want);
+            }
+            g.base = (char *)m;
+        }
+        h.cur = g;
+        h.used = 0;
+    }
+    *out = h.cur.base + h.used;
+    std::memset(desc, 0, sizeof(*desc));
+    desc->present = 1;
+    desc->raw = (uint64_t)(uintptr_t)*out;
+    desc->off = h.used;
+    desc->id = h.cur.gen;
+    desc->size = h.cur.bytes;
+    h.used += need;
+    h.users++;
+    return MI355X_SUCCESS;
+}
+
+static void harena_release(P2P *p)
+{
+    HostArena &h = p->harena;
+    if (--h.users > 0) return;
+    h.used = 0;
+    for (HostSeg &g : h.retired) seg_drop(g, true);
+    h.retired.clear();
+}
+
+// where a peer's host payload is readable: the pointer itself (same process), else the peer's
+// segment of that generation, mapped once (older generations of that peer are unmapped: their
+// slots were read synchronously, and a message still pending keeps its segment alive on the
+// sender's side, so it can be mapped again by name)
+static int host_src(mi355x_comm *c, P2P *p, int src, const BufDesc &d, const char **out)
+{
+    if (c->loopback || src == c->rank) {
+        *out = (const char *)(uintptr_t)d.raw;
+        return MI355X_SUCCESS;
+    }
+    const uint32_t gen = (uint32_t)d.id;
+    auto it = p->peer_segs.find({src, gen});
+    if (it == p->peer_segs.end()) {
+        for (auto j = p->peer_segs.begin(); j != p->peer_segs.end();) {
+            if (j->first.first == src && j->first.second < gen) {
+                seg_drop(j->second, false);
+                j = p->peer_segs.erase(j);
+            } else {
+                ++j;
+            }
+        }
+        HostSeg g{nullptr, 0, gen, seg_name(c, src, gen)};
+        const int fd = shm_open(g.name.c_str(), O_RDONLY, 0600);
+        if (fd < 0) return set_error(MI355X_ERR_PEER, "host arena %s of rank %d: %s", g.name.c_str(), src, strerror(errno));
+        struct stat st;
+        void *m = MAP_FAILED;
+        if (fstat(fd, &st) == 0) {
+            g.bytes = (size_t)st.st_size;
+            m = mmap(nullptr, g.bytes, PROT_READ, MAP_SHARED, fd, 0);
+        }
+        close(fd);
+        if (m == MAP_FAILED) return set_error(MI355X_ERR_PEER, "mapping host arena %s failed", g.name.c_str());
+        g.base = (char *)m;
+        g.name.clear();  // not ours to unlink
+        it = p->peer_segs.emplace(std::make_pair(src, gen), g).first;
+    }
+    if (d.off > it->second.bytes) return set_error(MI355X_ERR_PEER, "host payload outside rank %d's arena", src);
+    *out = it->second.base + d.off;
+    return MI355X_SUCCESS;
 }
 
 static void complete(mi355x_request *r, int rc)
@@ -152,7 +314,7 @@ static bool try_announce(mi355x_comm *c, mi355x_request *r)
         env->done.load(std::memory_order_acquire) < r->msg - (uint64_t)kP2PSlots + 1)
         return false;
     env->tag = r->tag;
-    env->flags = r->packed ? 1 : 0;
+    env->flags = r->env_flags;
     env->bytes = r->bytes;
     std::memcpy(&env->buf, &r->desc, sizeof(BufDesc));
     env->full.store(r->msg + 1, std::memory_order_release);
@@ -160,7 +322,7 @@ static bool try_announce(mi355x_comm *c, mi355x_request *r)
     return true;
 }
 
-// matched receive r <- message msg: pull the bytes (or complete at once for an empty message)
+// matched receive r <- message msg: copy the bytes into place (complete now), or start the pull
 static void start_read(mi355x_comm *c, P2P *p, mi355x_request *r, const P2PMsg &msg)
 {
     Envelope *env = msg.env;
@@ -171,12 +333,43 @@ static void start_read(mi355x_comm *c, P2P *p, mi355x_request *r, const P2PMsg &
     r->st_bytes = env->bytes;
     r->st_error = env->bytes > r->bytes ? MI355X_ERR_TRUNCATE : MI355X_SUCCESS;
     const size_t n = std::min<size_t>(env->bytes, r->bytes);
+    auto fin = [&]() { env->done.store(msg.m + 1, std::memory_order_release); };
     auto fail = [&](int rc) {
-        env->done.store(msg.m + 1, std::memory_order_release);  // the sender must not hang
+        fin();  // the sender must not hang
         complete(r, rc);
     };
     if (n == 0) {
-        env->done.store(msg.m + 1, std::memory_order_release);
+        fin();
+        complete_recv(r);
+        return;
+    }
+    int64_t first = 0;
+    const bool contig = !r->ddt || ddt_contiguous(r->ddt, r->count, &first);
+    char *dst = (char *)r->buf + first;
+    hipStream_t s;
+    int rc = p2p_stream(c, p, &s);
+    if (rc) return fail(rc);
+    if (env->flags & kEnvHost) {
+        // host payload (sm-BTL style): copied out synchronously, FIN at once
+        const char *src = nullptr;
+        if ((rc = host_src(c, p, msg.src, env->buf, &src))) return fail(rc);
+        if (r->host) {
+            if (contig) std::memcpy(dst, src, n);
+            else rc = mi355x_unpack_host(r->ddt, r->count, r->buf, 0, src, n);
+        } else if (contig) {
+            if (hipMemcpy(dst, src, n, hipMemcpyHostToDevice) != hipSuccess)
+                rc = set_error(MI355X_ERR_HIP, "host-to-device copy of a %zu-byte message failed", n);
+        } else {
+            void *stage = nullptr;
+            if ((rc = arena_alloc(p->rstage, n, &stage))) return fail(rc);
+            if (hipMemcpy(stage, src, n, hipMemcpyHostToDevice) != hipSuccess)
+                rc = set_error(MI355X_ERR_HIP, "host-to-device copy of a %zu-byte message failed", n);
+            if (!rc) rc = mi355x_unpack(r->ddt, r->count, r->buf, 0, stage, n, nullptr, s);
+            if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = set_error(MI355X_ERR_HIP, "unpack of a message failed");
+            arena_release(p->rstage);
+        }
+        if (rc) return fail(rc);
+        fin();
         complete_recv(r);
         return;
     }
@@ -186,7 +379,7 @@ static void start_read(mi355x_comm *c, P2P *p, mi355x_request *r, const P2PMsg &
     } else {
         void *mapped = nullptr;
         PeerMap *pm = nullptr;
-        int rc = map_peer(c, msg.src, env->buf, &mapped, &pm);
+        rc = map_peer(c, msg.src, env->buf, &mapped, &pm);
         if (rc) return fail(rc);
         if (pm) {
             pm->pins++;
@@ -194,37 +387,54 @@ static void start_read(mi355x_comm *c, P2P *p, mi355x_request *r, const P2PMsg &
         }
         src = mapped;
     }
-    hipStream_t s;
-    int rc = p2p_stream(c, p, &s);
-    if (rc) return fail(rc);
-    int64_t first = 0;
-    if (!r->ddt || ddt_contiguous(r->ddt, r->count, &first)) {
+    auto pull = [&](void *to) {  // one launch reads the sender's bytes over xGMI
         MultiCopyArgs m;
         std::memset(&m, 0, sizeof(m));
         m.src[0] = src;
-        m.dst[0] = (char *)r->buf + first;
+        m.dst[0] = to;
         m.len[0] = n;
         m.nseg = 1;
-        rc = launch_multicopy(m, s);
+        return launch_multicopy(m, s);
+    };
+    if (!r->host) {
+        rc = contig ? pull(dst) : mi355x_unpack(r->ddt, r->count, r->buf, 0, src, n, nullptr, s);
     } else {
-        rc = mi355x_unpack(r->ddt, r->count, r->buf, 0, src, n, nullptr, s);
+        // host receive of a device payload: pull into device staging, then one device-to-host copy
+        // (ob1's receive-side CUDA convertor does the same copy, pml_ob1_recvreq.c:647-663)
+        if (!(rc = arena_alloc(p->rstage, n, &r->stage))) {
+            rc = pull(r->stage);
+            void *to = dst;
+            if (!contig) {
+                r->htmp.resize(n);
+                to = r->htmp.data();
+            }
+            if (!rc && hipMemcpyAsync(to, r->stage, n, hipMemcpyDeviceToHost, s) != hipSuccess)
+                rc = set_error(MI355X_ERR_HIP, "device-to-host copy of a %zu-byte message failed", n);
+        }
     }
     if (rc == MI355X_SUCCESS && hipEventRecord(r->ev, s) != hipSuccess)
         rc = set_error(MI355X_ERR_HIP, "hipEventRecord on the point-to-point stream failed");
     if (rc) {
+        (void)hipStreamSynchronize(s);
         if (r->pin) {
-            (void)hipStreamSynchronize(s);
             r->pin->pins--;
             r->pin = nullptr;
         }
+        if (r->stage) {
+            arena_release(p->rstage);
+            r->stage = nullptr;
+        }
+        r->htmp.clear();
         return fail(rc);
     }
     p->reading.push_back(r);
 }
 
+// ob1's match test: MPI_ANY_TAG matches user tags only (tag >= 0), pml_ob1_recvfrag.c:487
 static bool matches(const mi355x_request *r, const P2PMsg &m)
 {
-    return (r->peer == MI355X_ANY_SOURCE || r->peer == m.src) && (r->tag == MI355X_ANY_TAG || r->tag == m.env->tag);
+    const int t = m.env->tag;
+    return (r->peer == MI355X_ANY_SOURCE || r->peer == m.src) && (r->tag == MI355X_ANY_TAG ? t >= 0 : r->tag == t);
 }
 
 static void drain_mailboxes(mi355x_comm *c, P2P *p)
@@ -239,6 +449,16 @@ static void drain_mailboxes(mi355x_comm *c, P2P *p)
             p->recv_seq[(size_t)q] = m + 1;
         }
     }
+}
+
+// a send whose FIN arrived: its payload slot is free; an engine-owned send is finished
+static void send_done(P2P *p, mi355x_request *r)
+{
+    if (r->packed) arena_release(p->arena);
+    if (r->hslot) harena_release(p);
+    r->packed = r->hslot = nullptr;
+    if (r->internal) delete r;
+    else complete(r, MI355X_SUCCESS);
 }
 
 int p2p_progress(mi355x_comm *c)
@@ -273,7 +493,7 @@ int p2p_progress(mi355x_comm *c)
         it = p->posted.erase(it);
         start_read(c, p, r, msg);
     }
-    // 4. finished pulls: FIN to the sender, receive complete
+    // 4. finished pulls: host receives get their host-convertor pass, FIN to the sender, complete
     for (auto it = p->reading.begin(); it != p->reading.end();) {
         mi355x_request *r = *it;
         const hipError_t e = hipEventQuery(r->ev);
@@ -285,9 +505,18 @@ int p2p_progress(mi355x_comm *c)
             r->pin->pins--;
             r->pin = nullptr;
         }
+        if (r->stage) {
+            arena_release(p->rstage);
+            r->stage = nullptr;
+        }
         r->env->done.store(r->msg + 1, std::memory_order_release);
-        if (e == hipSuccess) complete_recv(r);
-        else complete(r, set_error(MI355X_ERR_HIP, "point-to-point read: %s", hipGetErrorString(e)));
+        int rc = e == hipSuccess ? MI355X_SUCCESS
+                                 : set_error(MI355X_ERR_HIP, "point-to-point read: %s", hipGetErrorString(e));
+        if (!rc && !r->htmp.empty()) rc = mi355x_unpack_host(r->ddt, r->count, r->buf, 0, r->htmp.data(), r->htmp.size());
+        r->htmp.clear();
+        r->htmp.shrink_to_fit();
+        if (rc == MI355X_SUCCESS) complete_recv(r);
+        else complete(r, rc);
         it = p->reading.erase(it);
     }
     // 5. acknowledged sends
@@ -298,23 +527,19 @@ int p2p_progress(mi355x_comm *c)
             ++it;
             continue;
         }
-        if (r->packed) arena_release(p);
-        r->packed = nullptr;
-        complete(r, MI355X_SUCCESS);
         it = p->sending.erase(it);
+        send_done(p, r);
     }
     return MI355X_SUCCESS;
 }
 
-static int check_buffer(const void *buf, size_t bytes)
+// 1 when `buf` is device memory; 0 for host memory (or an empty message)
+static int buffer_kind(const void *buf, size_t bytes, int *dev)
 {
+    *dev = 0;
     if (bytes == 0) return MI355X_SUCCESS;
     if (!buf) return set_error(MI355X_ERR_ARG, "NULL buffer");
-    int dev = 0;
-    int rc = mi355x_ptr_is_device(buf, &dev);
-    if (rc) return rc;
-    if (!dev) return set_error(MI355X_ERR_ARG, "point-to-point buffers must be device memory");
-    return MI355X_SUCCESS;
+    return mi355x_ptr_is_device(buf, dev);
 }
 
 static mi355x_request *new_request(mi355x_comm *c, int kind)
@@ -325,13 +550,14 @@ static mi355x_request *new_request(mi355x_comm *c, int kind)
     return r;
 }
 
-static int isend(mi355x_comm *c, const void *buf, size_t count, const mi355x_ddt_t *d, int dest, int tag,
+static int isend(mi355x_comm *c, const void *buf, size_t count, const mi355x_ddt_t *d, int dest, int tag, int mode,
                  void *stream, mi355x_request **out)
 {
     if (!c || !out) return set_error(MI355X_ERR_ARG, "NULL argument");
     *out = nullptr;
     if (dest != MI355X_PROC_NULL && (dest < 0 || dest >= c->size)) return set_error(MI355X_ERR_ARG, "bad destination %d", dest);
-    if (tag < 0) return set_error(MI355X_ERR_ARG, "bad tag %d", tag);
+    if (tag == MI355X_ANY_TAG) return set_error(MI355X_ERR_ARG, "a send cannot carry MPI_ANY_TAG");
+    if (mode < MI355X_SEND_SYNCHRONOUS || mode > MI355X_SEND_STANDARD) return set_error(MI355X_ERR_ARG, "bad send mode %d", mode);
     const size_t bytes = d ? count * mi355x_ddt_size(d) : count;
     mi355x_request *r = new_request(c, 1);
     r->peer = dest;
@@ -340,44 +566,80 @@ static int isend(mi355x_comm *c, const void *buf, size_t count, const mi355x_ddt
     r->count = count;
     r->buf = const_cast<void *>(buf);
     r->bytes = bytes;
+    r->mode = mode;
     if (dest == MI355X_PROC_NULL) {
         complete(r, MI355X_SUCCESS);
         *out = r;
         return MI355X_SUCCESS;
     }
-    int rc = check_buffer(buf, bytes);
+    int dev = 0;
+    int rc = buffer_kind(buf, bytes, &dev);
     if (rc) {
         delete r;
         return rc;
     }
+    r->host = !dev;
     DeviceGuard dg(c->device);
     P2P *p = p2p_of(c);
     std::lock_guard<std::recursive_mutex> g(p->mtx);
     auto bail = [&](int code) {
-        if (r->packed) arena_release(p);
+        if (r->packed) arena_release(p->arena);
+        if (r->hslot) harena_release(p);
         delete r;
         return code;
     };
     // the send buffer is complete once the caller's prior work on `stream` is
-    if (bytes && hipStreamSynchronize(resolve_stream(stream)) != hipSuccess)
+    if (bytes && (dev || stream) && hipStreamSynchronize(resolve_stream(stream)) != hipSuccess)
         return bail(set_error(MI355X_ERR_HIP, "caller stream failed"));
-    const void *src = buf;
+    const bool small = bytes <= kEagerLimit && mode != MI355X_SEND_SYNCHRONOUS;
+    const bool eager = small || mode == MI355X_SEND_BUFFERED;
     int64_t first = 0;
-    if (bytes && d && !ddt_contiguous(d, count, &first)) {
-        hipStream_t s;
-        if ((rc = p2p_stream(c, p, &s))) return bail(rc);
-        void *packed = nullptr;
-        if ((rc = arena_alloc(p, bytes, &packed))) return bail(rc);
-        r->packed = packed;
-        if ((rc = mi355x_pack(d, count, buf, 0, packed, bytes, nullptr, s))) return bail(rc);
-        if (hipStreamSynchronize(s) != hipSuccess) return bail(set_error(MI355X_ERR_HIP, "pack for send failed"));
-        src = packed;
-    } else if (bytes) {
-        src = (const char *)buf + first;
-    }
+    const bool contig = !d || ddt_contiguous(d, count, &first);
+    const char *ubuf = (const char *)buf + first;
     BufDesc desc;
     std::memset(&desc, 0, sizeof(desc));
-    if (bytes) {
+    hipStream_t s = nullptr;
+    if (bytes && (!dev || small)) {
+        // the host arena: host payloads of any size, device payloads up to the eager limit
+        void *slot = nullptr;
+        if ((rc = harena_alloc(c, p, bytes, &slot, &desc))) return bail(rc);
+        r->hslot = slot;
+        r->env_flags = kEnvHost;
+        if (!dev) {
+            if (contig) std::memcpy(slot, ubuf, bytes);
+            else if ((rc = mi355x_pack_host(d, count, buf, 0, slot, bytes))) return bail(rc);
+        } else if (contig) {
+            if (hipMemcpy(slot, ubuf, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+                return bail(set_error(MI355X_ERR_HIP, "device-to-host copy of a %zu-byte send failed", bytes));
+        } else {
+            void *tmp = nullptr;
+            if ((rc = p2p_stream(c, p, &s)) || (rc = arena_alloc(p->arena, bytes, &tmp))) return bail(rc);
+            rc = mi355x_pack(d, count, buf, 0, tmp, bytes, nullptr, s);
+            if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = set_error(MI355X_ERR_HIP, "pack for send failed");
+            if (!rc && hipMemcpy(slot, tmp, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+                rc = set_error(MI355X_ERR_HIP, "device-to-host copy of a %zu-byte send failed", bytes);
+            arena_release(p->arena);
+            if (rc) return bail(rc);
+        }
+    } else if (bytes) {
+        // device payload: the caller's buffer itself, or a copy in the exportable device arena
+        // (a layout to pack, or a buffered send whose buffer the caller may reuse at once)
+        const void *src = ubuf;
+        if (!contig || mode == MI355X_SEND_BUFFERED) {
+            if ((rc = p2p_stream(c, p, &s))) return bail(rc);
+            void *copy = nullptr;
+            if ((rc = arena_alloc(p->arena, bytes, &copy))) return bail(rc);
+            r->packed = copy;
+            if (!contig) {
+                r->env_flags = kEnvPacked;
+                rc = mi355x_pack(d, count, buf, 0, copy, bytes, nullptr, s);
+            } else if (hipMemcpyAsync(copy, ubuf, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess) {
+                rc = set_error(MI355X_ERR_HIP, "copy of a buffered send failed");
+            }
+            if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = set_error(MI355X_ERR_HIP, "pack for send failed");
+            if (rc) return bail(rc);
+            src = copy;
+        }
         if ((rc = local_handle(c, src, &desc, false))) return bail(rc);
         desc.raw = (uint64_t)(uintptr_t)src;
         if (desc.staged && !c->loopback && dest != c->rank) {
@@ -390,10 +652,54 @@ static int isend(mi355x_comm *c, const void *buf, size_t count, const mi355x_ddt
     }
     std::memcpy(&r->desc, &desc, sizeof(desc));
     r->msg = p->send_seq[(size_t)dest]++;
+    mi355x_request *user = r;
+    if (eager) {  // the caller's request completes now; the engine keeps r until the FIN
+        r->internal = true;
+        user = new_request(c, 1);
+        user->peer = dest;
+        user->tag = tag;
+        user->bytes = bytes;
+        user->mode = mode;
+        complete(user, MI355X_SUCCESS);
+    }
     bool earlier = false;   // an earlier send to the same destination still queued: keep order
     for (mi355x_request *q : p->queued) earlier = earlier || q->peer == dest;
     if (!earlier && try_announce(c, r)) p->sending.push_back(r);
     else p->queued.push_back(r);
+    *out = user;
+    return MI355X_SUCCESS;
+}
+
+// a receive request for (buf, count, d), not posted yet
+static int make_recv(mi355x_comm *c, void *buf, size_t count, const mi355x_ddt_t *d, int source, int tag, void *stream,
+                     mi355x_request **out)
+{
+    const size_t bytes = d ? count * mi355x_ddt_size(d) : count;
+    mi355x_request *r = new_request(c, 2);
+    r->peer = source;
+    r->tag = tag;
+    r->ddt = d;
+    r->count = count;
+    r->buf = buf;
+    r->bytes = bytes;
+    int dev = 0;
+    int rc = buffer_kind(buf, bytes, &dev);
+    if (rc) {
+        delete r;
+        return rc;
+    }
+    r->host = !dev;
+    DeviceGuard dg(c->device);
+    if (hipEventCreateWithFlags(&r->ev, hipEventDisableTiming) != hipSuccess) {
+        delete r;
+        return set_error(MI355X_ERR_HIP, "hipEventCreate failed");
+    }
+    // the receive buffer may be written once the caller's prior work on `stream` is done
+    if (bytes && (dev || stream) && hipStreamSynchronize(resolve_stream(stream)) != hipSuccess) {
+        (void)hipEventDestroy(r->ev);
+        delete r;
+        return set_error(MI355X_ERR_HIP, "caller stream failed");
+    }
     *out = r;
     return MI355X_SUCCESS;
 }
@@ -405,37 +711,19 @@ static int irecv(mi355x_comm *c, void *buf, size_t count, const mi355x_ddt_t *d,
     *out = nullptr;
     if (source != MI355X_PROC_NULL && source != MI355X_ANY_SOURCE && (source < 0 || source >= c->size))
         return set_error(MI355X_ERR_ARG, "bad source %d", source);
-    if (tag < 0 && tag != MI355X_ANY_TAG) return set_error(MI355X_ERR_ARG, "bad tag %d", tag);
-    const size_t bytes = d ? count * mi355x_ddt_size(d) : count;
-    mi355x_request *r = new_request(c, 2);
-    r->peer = source;
-    r->tag = tag;
-    r->ddt = d;
-    r->count = count;
-    r->buf = buf;
-    r->bytes = bytes;
     if (source == MI355X_PROC_NULL) {   // MPI: source PROC_NULL, tag ANY_TAG, count 0
+        mi355x_request *r = new_request(c, 2);
+        r->peer = source;
+        r->tag = tag;
         r->st_source = MI355X_PROC_NULL;
         r->st_tag = MI355X_ANY_TAG;
         complete(r, MI355X_SUCCESS);
         *out = r;
         return MI355X_SUCCESS;
     }
-    int rc = check_buffer(buf, bytes);
-    if (rc) {
-        delete r;
-        return rc;
-    }
-    if (hipEventCreateWithFlags(&r->ev, hipEventDisableTiming) != hipSuccess) {
-        delete r;
-        return set_error(MI355X_ERR_HIP, "hipEventCreate failed");
-    }
-    // the receive buffer may be written once the caller's prior work on `stream` is done
-    if (bytes && hipStreamSynchronize(resolve_stream(stream)) != hipSuccess) {
-        (void)hipEventDestroy(r->ev);
-        delete r;
-        return set_error(MI355X_ERR_HIP, "caller stream failed");
-    }
+    mi355x_request *r = nullptr;
+    int rc = make_recv(c, buf, count, d, source, tag, stream, &r);
+    if (rc) return rc;
     P2P *p = p2p_of(c);
     {
         std::lock_guard<std::recursive_mutex> g(p->mtx);
@@ -478,6 +766,11 @@ static void fill_status(const mi355x_request *r, mi355x_status_t *st)
 
 } // namespace mi355x
 
+struct mi355x_message {   // a message taken out of the queue by a matched probe
+    mi355x_comm *comm;
+    mi355x::P2PMsg m;
+};
+
 using namespace mi355x;
 
 extern "C" {
@@ -485,7 +778,13 @@ extern "C" {
 int mi355x_isend(mi355x_comm_t *c, const void *buf, size_t count, const mi355x_ddt_t *d, int dest, int tag,
                  void *stream, mi355x_request_t **req)
 {
-    return isend(c, buf, count, d, dest, tag, stream, req);
+    return isend(c, buf, count, d, dest, tag, MI355X_SEND_STANDARD, stream, req);
+}
+
+int mi355x_isend_mode(mi355x_comm_t *c, const void *buf, size_t count, const mi355x_ddt_t *d, int dest, int tag,
+                      int mode, void *stream, mi355x_request_t **req)
+{
+    return isend(c, buf, count, d, dest, tag, mode, stream, req);
 }
 
 int mi355x_irecv(mi355x_comm_t *c, void *buf, size_t count, const mi355x_ddt_t *d, int source, int tag,
@@ -494,16 +793,22 @@ int mi355x_irecv(mi355x_comm_t *c, void *buf, size_t count, const mi355x_ddt_t *
     return irecv(c, buf, count, d, source, tag, stream, req);
 }
 
-int mi355x_send(mi355x_comm_t *c, const void *buf, size_t count, const mi355x_ddt_t *d, int dest, int tag,
-                void *stream)
+int mi355x_send_mode(mi355x_comm_t *c, const void *buf, size_t count, const mi355x_ddt_t *d, int dest, int tag,
+                     int mode, void *stream)
 {
     mi355x_request *r = nullptr;
-    int rc = isend(c, buf, count, d, dest, tag, stream, &r);
+    int rc = isend(c, buf, count, d, dest, tag, mode, stream, &r);
     if (rc) return rc;
     rc = p2p_wait(r);
     if (rc == MI355X_ERR_TIMEOUT) return rc;  // still announced: the request cannot be freed
     (void)mi355x_request_free(r);
     return rc;
+}
+
+int mi355x_send(mi355x_comm_t *c, const void *buf, size_t count, const mi355x_ddt_t *d, int dest, int tag,
+                void *stream)
+{
+    return mi355x_send_mode(c, buf, count, d, dest, tag, MI355X_SEND_STANDARD, stream);
 }
 
 int mi355x_recv(mi355x_comm_t *c, void *buf, size_t count, const mi355x_ddt_t *d, int source, int tag,
@@ -526,7 +831,7 @@ int mi355x_sendrecv(mi355x_comm_t *c, const void *sbuf, size_t scount, const mi3
     mi355x_request *rr = nullptr, *sr = nullptr;
     int rc = irecv(c, rbuf, rcount, rd, source, rtag, stream, &rr);
     if (rc) return rc;
-    rc = isend(c, sbuf, scount, sd, dest, stag, stream, &sr);
+    rc = isend(c, sbuf, scount, sd, dest, stag, MI355X_SEND_STANDARD, stream, &sr);
     if (rc) {
         // the receive stays posted; wait for it so nothing is left behind
         (void)p2p_wait(rr);
@@ -541,18 +846,22 @@ int mi355x_sendrecv(mi355x_comm_t *c, const void *sbuf, size_t scount, const mi3
     return rc_s ? rc_s : rc_r;
 }
 
+static void proc_null_status(mi355x_status_t *status)
+{
+    if (!status) return;
+    status->source = MI355X_PROC_NULL;
+    status->tag = MI355X_ANY_TAG;
+    status->error = 0;
+    status->bytes = 0;
+}
+
 int mi355x_iprobe(mi355x_comm_t *c, int source, int tag, int *flag, mi355x_status_t *status)
 {
     if (!c || !flag) return set_error(MI355X_ERR_ARG, "NULL argument");
     *flag = 0;
     if (source == MI355X_PROC_NULL) {
         *flag = 1;
-        if (status) {
-            status->source = MI355X_PROC_NULL;
-            status->tag = MI355X_ANY_TAG;
-            status->error = 0;
-            status->bytes = 0;
-        }
+        proc_null_status(status);
         return MI355X_SUCCESS;
     }
     p2p_progress(c);
@@ -572,6 +881,77 @@ int mi355x_iprobe(mi355x_comm_t *c, int source, int tag, int *flag, mi355x_statu
             }
             break;
         }
+    return MI355X_SUCCESS;
+}
+
+int mi355x_improbe(mi355x_comm_t *c, int source, int tag, int *flag, mi355x_message_t **msg, mi355x_status_t *status)
+{
+    if (!c || !flag || !msg) return set_error(MI355X_ERR_ARG, "NULL argument");
+    *flag = 0;
+    *msg = nullptr;
+    if (source == MI355X_PROC_NULL) {  // the MPI layer answers this itself (ompi_message_no_proc)
+        *flag = 1;
+        proc_null_status(status);
+        return MI355X_SUCCESS;
+    }
+    p2p_progress(c);
+    P2P *p = p2p_of(c);
+    std::lock_guard<std::recursive_mutex> g(p->mtx);
+    mi355x_request probe;
+    probe.peer = source;
+    probe.tag = tag;
+    auto it = std::find_if(p->unexpected.begin(), p->unexpected.end(),
+                           [&](const P2PMsg &x) { return matches(&probe, x); });
+    if (it == p->unexpected.end()) return MI355X_SUCCESS;
+    *msg = new mi355x_message{c, *it};
+    p->unexpected.erase(it);
+    *flag = 1;
+    if (status) {
+        status->source = (*msg)->m.src;
+        status->tag = (*msg)->m.env->tag;
+        status->error = 0;
+        status->bytes = (*msg)->m.env->bytes;
+    }
+    return MI355X_SUCCESS;
+}
+
+int mi355x_imrecv(mi355x_comm_t *c, void *buf, size_t count, const mi355x_ddt_t *d, mi355x_message_t *msg,
+                  void *stream, mi355x_request_t **req)
+{
+    if (!c || !msg || !req || msg->comm != c) return set_error(MI355X_ERR_ARG, "bad matched receive arguments");
+    *req = nullptr;
+    mi355x_request *r = nullptr;
+    int rc = make_recv(c, buf, count, d, msg->m.src, msg->m.env->tag, stream, &r);
+    if (rc) return rc;  // msg stays valid: the caller may retry
+    DeviceGuard dg(c->device);
+    P2P *p = p2p_of(c);
+    {
+        std::lock_guard<std::recursive_mutex> g(p->mtx);
+        start_read(c, p, r, msg->m);
+    }
+    delete msg;
+    *req = r;
+    return MI355X_SUCCESS;
+}
+
+int mi355x_request_cancel(mi355x_request_t *r)
+{
+    if (!r) return set_error(MI355X_ERR_ARG, "NULL request");
+    if (r->kind != 2 || r->done.load(std::memory_order_acquire)) return MI355X_SUCCESS;
+    P2P *p = p2p_of(r->comm);
+    std::lock_guard<std::recursive_mutex> g(p->mtx);
+    auto it = std::find(p->posted.begin(), p->posted.end(), r);
+    if (it == p->posted.end()) return MI355X_SUCCESS;  // matched already: too late (ob1 likewise)
+    p->posted.erase(it);
+    r->cancelled = true;
+    complete(r, MI355X_SUCCESS);
+    return MI355X_SUCCESS;
+}
+
+int mi355x_request_cancelled(const mi355x_request_t *r, int *cancelled)
+{
+    if (!r || !cancelled) return set_error(MI355X_ERR_ARG, "NULL argument");
+    *cancelled = r->cancelled ? 1 : 0;
     return MI355X_SUCCESS;
 }
 

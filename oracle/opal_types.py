@@ -423,3 +423,78 @@ def walk_desc(t: OpalType, count: int = 1):
     for k in range(count):
         body(0, len(recs), k * t.extent)
     return out
+
+
+def convertor_raw(t: OpalType, count: int = 1, iov_num: int = 5):
+    """opal_convertor_raw (opal/datatype/opal_convertor_raw.c:37-180) over the restated records:
+    the iovecs the reference hands back, one list per call of at most `iov_num` entries (the
+    function stops when the iovec array is full and resumes there on the next call; the last call
+    returns 1).  Emission rules: a data ELEM whose extent equals its basic size is one iovec of
+    count * size (:87-101), any other ELEM one iovec per element (:102-114); a LOOP flagged
+    CONTIGUOUS one iovec of the END_LOOP's size per iteration at first_elem_disp (:145-158); any
+    other LOOP is walked into; instance k at k * (ub - lb) (:131).  (The reference walks opt_desc
+    for a homogeneous convertor; the optimized records are not restated -- the same bytes in the
+    same order, possibly cut into different iovecs.)"""
+    sizes = basic_sizes()
+    recs = t.desc
+    flat = []
+
+    def body(i, end, base):
+        while i < end:
+            r = recs[i]
+            if r[0] == "L":
+                stop = i + r[3]  # the matching END_LOOP
+                if r[1] & F_CONTIGUOUS:
+                    x = recs[stop]
+                    flat.extend((base + x[4] + k * r[4], x[3]) for k in range(r[2]))
+                else:
+                    for k in range(r[2]):
+                        body(i + 1, stop, base + k * r[4])
+                i = stop + 1
+            elif r[0] == "E":
+                if r[1] & F_DATA:
+                    sz = sizes[r[2]]
+                    if sz == r[4]:
+                        flat.append((base + r[5], sz * r[3]))
+                    else:
+                        flat.extend((base + r[5] + c * r[4], sz) for c in range(r[3]))
+                i += 1
+            else:
+                i += 1
+
+    for k in range(count):
+        body(0, len(recs), k * t.extent)
+    flat = [p for p in flat if p[1]]
+    return [flat[i:i + iov_num] for i in range(0, len(flat), iov_num)] or [[]]
+
+
+def merge_pieces(pieces):
+    """adjacent (offset, length) pieces merged: the byte sequence they describe"""
+    out = []
+    for d, n in pieces:
+        if out and out[-1][0] + out[-1][1] == d:
+            out[-1][1] += n
+        else:
+            out.append([d, n])
+    return [tuple(p) for p in out]
+
+
+def ddt_test_zero_count_types():
+    """test/datatype/ddt_test.c:401-411: three types grown from contiguous(0, MPI_DATATYPE_NULL)
+    by ompi_datatype_add -- pdt3 = 10 int + 5 float at 40; pdt2 = float + 3 x pdt3 at 4; pdt1 =
+    5 long long + 2 long double at 40 (returns pdt1, pdt2, pdt3)"""
+    i4, f4, i8, f16 = (OpalType.basic(n) for n in ("INT4", "FLOAT4", "INT8", "FLOAT16"))
+    p3 = contiguous(0, i4)
+    p3.add(i4, 10, 0, -1)
+    p3.add(f4, 5, 10 * 4, -1)
+    p2 = contiguous(0, i4)
+    p2.add(f4, 1, 0, -1)
+    p2.add(p3, 3, 4, -1)
+    p1 = contiguous(0, i4)
+    p1.add(i8, 5, 0, -1)
+    p1.add(f16, 2, 8 * 5, -1)
+    return p1.commit(), p2.commit(), p3.commit()
+
+
+def inversed_vector(length):  # create_inversed_vector, test/datatype/ddt_lib.c:59-67 (vector(length, 1, 2, int))
+    return vector(length, 1, 2, OpalType.basic("INT4")).commit()

@@ -404,11 +404,171 @@ class Status(ctypes.Structure):  # ompi_status_public_t (mpi.h.in:344-356)
                 ("_cancelled", ctypes.c_int), ("_ucount", ctypes.c_size_t)]
 
 
+BSEND, SSEND, STANDARD = 2, 0, 4   # mca_pml_base_send_mode_t (pml.h:78-85)
+
+
+def pml_mixed(m, comm, rank, size, torch, fdt):
+    """MPI semantics across buffer kinds through the component: dev->host, host->dev, dev->dev,
+    host->host (eager and rendezvous sizes, MPI_FLOAT and a derived vector type), MPI_ANY_SOURCE
+    over senders of both kinds, same-tag order across kinds, MPI_Bsend(dev) -> MPI_Recv(dev), the
+    small unsafe exchange (both ranks send first), persistent MPI_Send_init / MPI_Recv_init /
+    MPI_Start, MPI_Mprobe + MPI_Mrecv / MPI_Improbe + MPI_Imrecv, MPI_Cancel, MPI_Probe"""
+    L = m.lib
+    st = Status()
+    ANY = -1
+    left, right = (rank - 1) % size, (rank + 1) % size
+
+    def mk(kind, vals):
+        a = np.asarray(vals, dtype=np.float32)
+        if kind == "host":
+            h = a.copy()
+            return h.ctypes.data, (lambda: h.copy()), h
+        d = torch.from_numpy(a.copy()).cuda()
+        torch.cuda.synchronize()
+        return d.data_ptr(), (lambda: d.cpu().numpy()), d
+
+    # a) every kind pairing around the ring, sizes either side of the 4 KiB eager limit
+    for skind in ("dev", "host"):
+        for rkind in ("dev", "host"):
+            for n in (0, 5, 1024, 1025, 300_001):
+                sp, _, ks = mk(skind, np.arange(n) + 1000 * rank)
+                rp, read, kr = mk(rkind, np.full(n + 3, -1.0))
+                rq, sq = ctypes.c_void_p(), ctypes.c_void_p()
+                assert L.mini_irecv(rp, n + 3, fdt, left, 30, comm, ctypes.byref(rq)) == 0
+                assert L.mini_isend(sp, n, fdt, right, 30, comm, ctypes.byref(sq)) == 0
+                assert L.mini_wait_status(ctypes.byref(rq), ctypes.byref(st)) == 0
+                assert L.mini_wait_status(ctypes.byref(sq), None) == 0
+                assert (st.MPI_SOURCE, st.MPI_TAG, st._ucount) == (left, 30, 4 * n), (skind, rkind, n)
+                got = read()
+                assert np.array_equal(got[:n], np.arange(n, dtype=np.float32) + 1000 * left), (skind, rkind, n)
+                assert (got[n:] == -1).all()
+    # b) a derived send type from host memory into a contiguous device receive, and the reverse
+    nblk = 700
+    desc, used, tsize, lb, ub = opal_vector(nblk, 256, 512)
+    vdt = m.derived(desc, used, tsize, lb, ub)
+    full = np.arange(nblk * 128, dtype=np.float32) + rank
+    hp, _, kh = mk("host", full)
+    dp, dread, kd = mk("dev", np.zeros(nblk * 64))
+    rq, sq = ctypes.c_void_p(), ctypes.c_void_p()
+    assert L.mini_irecv(dp, nblk * 64, fdt, left, 31, comm, ctypes.byref(rq)) == 0
+    assert L.mini_isend(hp, 1, vdt, right, 31, comm, ctypes.byref(sq)) == 0
+    assert L.mini_wait(ctypes.byref(rq)) == 0 and L.mini_wait(ctypes.byref(sq)) == 0
+    assert np.array_equal(dread(), (np.arange(nblk * 128, dtype=np.float32) + left).reshape(nblk, 128)[:, :64].ravel())
+    back, bread, kb = mk("host", np.full(nblk * 128, -5.0))
+    flat, _, kf = mk("dev", np.arange(nblk * 64) * 2.0 + rank)
+    assert L.mini_irecv(back, 1, vdt, left, 32, comm, ctypes.byref(rq)) == 0
+    assert L.mini_isend(flat, nblk * 64, fdt, right, 32, comm, ctypes.byref(sq)) == 0
+    assert L.mini_wait(ctypes.byref(rq)) == 0 and L.mini_wait(ctypes.byref(sq)) == 0
+    b = bread().reshape(nblk, 128)
+    assert np.array_equal(b[:, :64].ravel(), np.arange(nblk * 64, dtype=np.float32) * 2 + left) and (b[:, 64:] == -5).all()
+    L.mini_datatype_destroy(vdt)
+    # c) same-tag order across kinds and sizes between one pair; ANY_SOURCE over both kinds
+    sizes = [3, 2000, 64, 262_144, 1024, 5000, 1]
+    if rank == 0:
+        keep = []
+        for i, n in enumerate(sizes):
+            p_, _, k_ = mk("dev" if i % 2 else "host", np.full(n, float(i)))
+            keep.append(k_)
+            q = ctypes.c_void_p()
+            assert L.mini_isend(p_, n, fdt, 1, 33, comm, ctypes.byref(q)) == 0
+            keep.append(q)
+        for q in keep[1::2]:
+            assert L.mini_wait(ctypes.byref(q)) == 0
+    elif rank == 1:
+        for i, n in enumerate(sizes):
+            p_, read, k_ = mk("host" if i % 3 else "dev", np.zeros(262_144))
+            assert L.mini_recv(p_, 262_144, fdt, 0, 33, comm, ctypes.byref(st)) == 0
+            assert st._ucount == 4 * n and (read()[:n] == i).all(), ("order across kinds", i)
+    if rank != 0:
+        p_, _, k_ = mk("host" if rank % 2 else "dev", np.full(50 + rank, float(rank)))
+        assert L.mini_send(p_, 50 + rank, fdt, 0, 34, comm) == 0
+    else:
+        seen = set()
+        for i in range(1, size):
+            p_, read, k_ = mk("dev" if i % 2 else "host", np.zeros(64))
+            assert L.mini_recv(p_, 64, fdt, ANY, 34, comm, ctypes.byref(st)) == 0
+            r = st.MPI_SOURCE
+            assert r not in seen and st._ucount == 4 * (50 + r) and (read()[:50 + r] == r).all()
+            seen.add(r)
+        assert seen == set(range(1, size))
+    # d) MPI_Bsend from device memory into a device receive; the unsafe small exchange
+    bp, _, kbp = mk("dev", np.full(100_000, 3.0 + rank))
+    assert L.mini_send_mode(bp, 100_000, fdt, right, 35, BSEND, comm) == 0   # completes at once
+    kbp.fill_(0)  # the caller may reuse a buffered send's buffer immediately
+    rp, read, kr = mk("dev", np.zeros(100_000))
+    assert L.mini_recv(rp, 100_000, fdt, left, 35, comm, None) == 0
+    assert (read() == 3.0 + left).all(), "bsend payload"
+    sp, _, ks = mk("dev", np.full(512, 1.0 + rank))
+    hp, read, kh = mk("host", np.zeros(512))
+    assert L.mini_send(sp, 512, fdt, right, 36, comm) == 0    # eager: returns before the peer receives
+    assert L.mini_recv(hp, 512, fdt, left, 36, comm, None) == 0
+    assert (read() == 1.0 + left).all()
+    # e) persistent requests: 3 rounds of MPI_Start on one send / receive pair (host send buffer,
+    #    device receive buffer); the buffers are re-read at every start
+    sbuf = np.zeros(2048, dtype=np.float32)
+    rp, read, kr = mk("dev", np.zeros(2048))
+    ps, pr = ctypes.c_void_p(), ctypes.c_void_p()
+    assert L.mini_send_init(sbuf.ctypes.data, 2048, fdt, right, 37, STANDARD, comm, ctypes.byref(ps)) == 0
+    assert L.mini_recv_init(rp, 2048, fdt, left, 37, comm, ctypes.byref(pr)) == 0
+    for it in range(3):
+        sbuf[:] = 100 * it + rank
+        assert L.mini_start(ctypes.byref(pr)) == 0 and L.mini_start(ctypes.byref(ps)) == 0
+        assert L.mini_wait_status(ctypes.byref(pr), ctypes.byref(st)) == 0 and st.MPI_SOURCE == left
+        assert L.mini_wait(ctypes.byref(ps)) == 0
+        assert not L.mini_request_is_null(ps) and not L.mini_request_is_null(pr), "persistent requests stay"
+        assert (read() == 100 * it + left).all(), ("persistent round", it)
+    assert L.mini_request_free(ctypes.byref(ps)) == 0 and L.mini_request_free(ctypes.byref(pr)) == 0
+    assert L.mini_request_is_null(ps) and L.mini_request_is_null(pr)
+    # f) matched probe: MPI_Mprobe + MPI_Mrecv (host), MPI_Improbe + MPI_Imrecv (device); the probed
+    #    message can no longer be matched by a wildcard receive
+    sp1, _, k1 = mk("dev", np.full(300, 11.0 + rank))
+    sp2, _, k2 = mk("host", np.full(300, 22.0 + rank))
+    q1, q2 = ctypes.c_void_p(), ctypes.c_void_p()
+    assert L.mini_isend(sp1, 300, fdt, right, 38, comm, ctypes.byref(q1)) == 0
+    assert L.mini_isend(sp2, 300, fdt, right, 38, comm, ctypes.byref(q2)) == 0
+    msg = ctypes.c_void_p()
+    assert L.mini_mprobe(left, 38, comm, ctypes.byref(msg), ctypes.byref(st)) == 0
+    assert (st.MPI_SOURCE, st.MPI_TAG, st._ucount) == (left, 38, 1200) and not L.mini_message_is_null(msg)
+    other, oread, ko = mk("host", np.zeros(300))
+    assert L.mini_recv(other, 300, fdt, ANY, ANY, comm, None) == 0
+    assert (oread() == 22.0 + left).all(), "a wildcard receive took the probed message"
+    mine, mread, km = mk("host", np.zeros(300))
+    assert L.mini_mrecv(mine, 300, fdt, ctypes.byref(msg), ctypes.byref(st)) == 0 and L.mini_message_is_null(msg)
+    assert (mread() == 11.0 + left).all() and st._ucount == 1200
+    assert L.mini_wait(ctypes.byref(q1)) == 0 and L.mini_wait(ctypes.byref(q2)) == 0
+    sp3, _, k3 = mk("host", np.full(10, 7.0 + rank))
+    assert L.mini_isend(sp3, 10, fdt, right, 39, comm, ctypes.byref(q1)) == 0
+    flag = ctypes.c_int(0)
+    t0 = time.time()
+    while not flag.value:
+        assert L.mini_improbe(ANY, 39, comm, ctypes.byref(flag), ctypes.byref(msg), ctypes.byref(st)) == 0
+        assert time.time() - t0 < 30, "improbe never matched"
+    dv, dread, kdv = mk("dev", np.zeros(10))
+    rq = ctypes.c_void_p()
+    assert L.mini_imrecv(dv, 10, fdt, ctypes.byref(msg), ctypes.byref(rq)) == 0 and L.mini_message_is_null(msg)
+    assert L.mini_wait_status(ctypes.byref(rq), ctypes.byref(st)) == 0 and st.MPI_SOURCE == left
+    assert (dread() == 7.0 + left).all()
+    assert L.mini_wait(ctypes.byref(q1)) == 0
+    # g) MPI_Cancel of a receive nothing will match; MPI_Probe (blocking) sees a host message
+    cq = ctypes.c_void_p()
+    cb = np.zeros(4, dtype=np.float32)
+    assert L.mini_irecv(cb.ctypes.data, 4, fdt, left, 999, comm, ctypes.byref(cq)) == 0
+    assert L.mini_cancel(cq) == 0
+    assert L.mini_wait_status(ctypes.byref(cq), ctypes.byref(st)) == 0 and st._cancelled == 1
+    pb, _, kpb = mk("host", np.full(6, 1.5))
+    assert L.mini_isend(pb, 6, fdt, right, 40, comm, ctypes.byref(q1)) == 0
+    assert L.mini_probe(left, 40, comm, ctypes.byref(st)) == 0 and st._ucount == 24
+    assert L.mini_recv(cb.ctypes.data, 4, fdt, left, 40, comm, ctypes.byref(st)) == 15   # truncated
+    assert st._ucount == 24 and (cb == 1.5).all()
+    assert L.mini_wait(ctypes.byref(q1)) == 0
+
+
 def pml_main():
-    """MPI_Send / MPI_Ssend / MPI_Recv / MPI_Isend / MPI_Irecv / MPI_Iprobe through the PML slot
-    (`mca_pml`, the table the MPI layer calls, e.g. ompi/mpi/c/send.c:67) once coll/mi355x's
-    init_query has hooked it: device buffers on the engine communicator move device data, host
-    buffers reach the saved (stub) PML, and closing the component restores the table"""
+    """MPI_Send / MPI_Ssend / MPI_Recv / MPI_Isend / MPI_Irecv / MPI_Iprobe (and the persistent and
+    matched-probe calls) through the PML slot (`mca_pml`, the table the MPI layer calls, e.g.
+    ompi/mpi/c/send.c:67) once coll/mi355x's init_query has hooked it: every call on the engine
+    communicator -- device or host buffer -- goes to the engine's one matching queue, nothing reaches
+    the saved (stub) PML, and closing the component restores the table"""
     rank, size = int(sys.argv[1]), int(sys.argv[2])
     import torch
     torch.cuda.set_device(rank % torch.cuda.device_count())
@@ -419,8 +579,9 @@ def pml_main():
     comp = m.component_ptr(m.coll, "mca_coll_mi355x_component")
     stub_send = L.mini_pml_fn(1)
     assert L.mini_coll_init(comp) == 0
-    hooked = [L.mini_pml_fn(w) for w in range(6)]
-    names = ["isend", "send", "irecv", "recv", "iprobe", "probe"]
+    hooked = [L.mini_pml_fn(w) for w in range(13)]
+    names = ["isend", "send", "irecv", "recv", "iprobe", "probe", "isend_init", "irecv_init", "start", "improbe",
+             "mprobe", "imrecv", "mrecv"]
     for w, nm in enumerate(names):
         assert hooked[w] == m.addr(m.coll, f"mca_coll_mi355x_pml_{nm}"), f"pml_{nm} not hooked"
     comm = L.mini_comm_create(rank, size, 42)
@@ -543,23 +704,58 @@ def pml_main():
         if rank == 1:
             for i in range(nmsg):
                 assert bool((bufs[i] == float(i)).all()), ("ordering", i, float(bufs[i][0]))
-    # 7. host buffers and buffered sends -> the saved PML (the stub answers 77)
-    h = np.zeros(16, dtype=np.float32)
-    before = [L.mini_pml_stub_calls(w) for w in range(6)]
-    assert L.mini_send(h.ctypes.data, 16, fdt, right, 16, comm) == 77
-    assert L.mini_recv(h.ctypes.data, 16, fdt, left, 16, comm, None) == 77
-    assert L.mini_isend(h.ctypes.data, 16, fdt, right, 16, comm, ctypes.byref(sq)) == 77
-    assert L.mini_irecv(h.ctypes.data, 16, fdt, left, 16, comm, ctypes.byref(rq)) == 77
-    after = [L.mini_pml_stub_calls(w) for w in range(6)]
-    assert [a - b for a, b in zip(after, before)][:4] == [1, 1, 1, 1], (before, after)
-    # a probe with nothing pending asks the engine, then the saved PML
-    flag = ctypes.c_int(1)
-    assert L.mini_iprobe(ANY, 999, comm, ctypes.byref(flag), ctypes.byref(st)) == 0 and flag.value == 0
-    assert L.mini_pml_stub_calls(4) == before[4] + 1
+    # 7. one matching queue for every buffer kind (ob1: pml_ob1_cuda.c:52-100 / pml_ob1_recvreq.c:647-663)
+    pml_mixed(m, comm, rank, size, torch, fdt)
+    # nothing of the above reached the saved (stub) PML: every call on an engine communicator is the engine's
+    assert [L.mini_pml_stub_calls(w) for w in range(13)] == [0] * 13, [L.mini_pml_stub_calls(w) for w in range(13)]
     L.mini_comm_destroy(comm)
     assert L.mini_coll_close(comp) == 0
     assert L.mini_pml_fn(1) == stub_send, "component close restores the PML table"
     print(f"rank {rank} pml OK", flush=True)
+
+
+def tuned_vars_main():
+    """coll/tuned's variables read through the MCA variable system (no OMPI_MCA_coll_tuned_* in the
+    environment): forced allreduce algorithm 3 (recursive doubling) on one communicator, then a
+    rules file naming algorithm 2 (nonoverlapping) for every size on the next"""
+    rank, size = int(sys.argv[1]), int(sys.argv[2])
+    import torch
+    torch.cuda.set_device(rank % torch.cuda.device_count())
+    m = mini()
+    L, pkg = m.lib, m.pkg
+    oracle = load_oracle()
+    m.install_oracle_base(oracle)
+    L.mini_tuned_register.argtypes = [ctypes.c_int] * 5 + [ctypes.c_char_p]
+    comp = m.component_ptr(m.coll, "mca_coll_mi355x_component")
+    ptrs = lambda arrs: (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    ty, code = pkg.T["FLOAT"], pkg.OP["SUM"]
+    fdt = m.dtype_for_slot(ty)
+    op = m.select_op(code)
+    count = 300_001
+    xs = [opdata.make("FLOAT", count, 900 + r) for r in range(size)]
+    want = {}
+    for alg in (0, 2, 3):
+        outs = [np.zeros_like(xs[0]) for _ in range(size)]
+        oracle.oracle_allreduce(alg, size, count, ty, code, 0, ptrs(xs), ptrs(outs))
+        want[alg] = outs[rank]
+    assert not np.array_equal(want[3], want[0]) and not np.array_equal(want[2], want[0]), "orders must differ"
+    rules = pathlib.Path(f"/tmp/mi355x_rules_{sys.argv[3]}_{rank}.conf")
+    rules.write_text(f"1\n2\n1\n{size} 1\n0 2 0 0\n")
+    for step, (args, alg) in enumerate((((1, 3, 0, 0, 0, None), 3), ((1, 0, 0, 0, 0, str(rules).encode()), 2))):
+        assert L.mini_tuned_register(*args) == 0
+        comm = L.mini_comm_create(rank, size, 42 + step)
+        L.mini_comm_set_channel(comm, f"{sys.argv[3]}_{step}".encode())
+        L.mini_comm_install(comm, L.mini_stub_module())
+        assert L.mini_coll_select(comm, comp) == 90
+        dx = torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda()
+        dr = torch.zeros_like(dx)
+        torch.cuda.synchronize()
+        assert L.mini_allreduce(comm, dx.data_ptr(), dr.data_ptr(), count, fdt, op) == 0
+        opdata.assert_same("FLOAT", "SUM", dr.cpu().numpy().view(np.float32), want[alg], f"tuned variables step {step}")
+        L.mini_comm_destroy(comm)
+    rules.unlink()
+    L.mini_op_destroy(op)
+    print(f"rank {rank} tuned_vars OK", flush=True)
 
 
 def main():
@@ -567,6 +763,8 @@ def main():
         return split_main()
     if len(sys.argv) > 4 and sys.argv[4] == "pml":
         return pml_main()
+    if len(sys.argv) > 4 and sys.argv[4] == "tuned_vars":
+        return tuned_vars_main()
     rank, size = int(sys.argv[1]), int(sys.argv[2])
     import torch
     ndev = torch.cuda.device_count()

@@ -163,3 +163,43 @@ def expected_copy(t, count, src, origin):
     want = np.zeros_like(src)
     want[idx] = src[idx]
     return want
+
+
+RAW_CASES = [  # ddt_raw.c:150-177 (local_copy_ddt_raw with iov_num = 5) and test_upper(500) (:45-80)
+    ("inversed_vector_int_10", lambda: ot.inversed_vector(10), 100),
+    ("strange_dt", ot.strange_dt, 1),
+    ("upper_matrix_100", lambda: ot.upper_matrix(100), 1),
+    ("upper_matrix_500", lambda: ot.upper_matrix(500), 1),
+    ("mpi_double", lambda: ot.OpalType.basic("FLOAT8"), 4500),                              # :232-235
+    ("contig_4500x1", lambda: ot.contiguous(4500, ot.OpalType.basic("FLOAT8")).commit(), 1),  # :238-263
+    ("contig_450x10", lambda: ot.contiguous(450, ot.OpalType.basic("FLOAT8")).commit(), 10),
+    ("contig_45x100", lambda: ot.contiguous(45, ot.OpalType.basic("FLOAT8")).commit(), 100),
+    ("contig_100x45", lambda: ot.contiguous(100, ot.OpalType.basic("FLOAT8")).commit(), 45),
+    ("contig_10x450", lambda: ot.contiguous(10, ot.OpalType.basic("FLOAT8")).commit(), 450),
+    ("contig_1x4500", lambda: ot.contiguous(1, ot.OpalType.basic("FLOAT8")).commit(), 4500),
+    ("vector_450_10_11", lambda: ot.vector(450, 10, 11, ot.OpalType.basic("FLOAT8")).commit(), 1),  # :268-277
+    ("struct_char_double", ot.struct_char_double, 4500),                                    # :279-285
+    ("twice_two_doubles", ot.twice_two_doubles, 4500),                                      # :287-293
+    ("blacs", ot.blacs, 4500),                                                              # :295-304
+    ("blacs1_int", ot.blacs1, 1),                                                           # :306-311
+    ("ddt_test_pdt1", lambda: ot.ddt_test_zero_count_types()[0], 1),
+]
+
+
+COPY_CASES = [  # ddt_test.c:350-372, 433-524: local_copy_ddt_count(pdt, count)
+    ("inversed_vector_int_10", lambda: ot.inversed_vector(10), 100),
+    ("strange_dt", ot.strange_dt, 1),
+    ("upper_matrix_100", lambda: ot.upper_matrix(100), 1),
+    ("mpi_double", lambda: ot.OpalType.basic("FLOAT8"), 4500),
+    ("contig_4500x1", lambda: ot.contiguous(4500, ot.OpalType.basic("FLOAT8")).commit(), 1),  # :442-477
+    ("contig_450x10", lambda: ot.contiguous(450, ot.OpalType.basic("FLOAT8")).commit(), 10),
+    ("contig_45x100", lambda: ot.contiguous(45, ot.OpalType.basic("FLOAT8")).commit(), 100),
+    ("contig_100x45", lambda: ot.contiguous(100, ot.OpalType.basic("FLOAT8")).commit(), 45),
+    ("contig_10x450", lambda: ot.contiguous(10, ot.OpalType.basic("FLOAT8")).commit(), 450),
+    ("contig_1x4500", lambda: ot.contiguous(1, ot.OpalType.basic("FLOAT8")).commit(), 4500),
+    ("vector_450_10_11", lambda: ot.vector(450, 10, 11, ot.OpalType.basic("FLOAT8")).commit(), 1),  # :482-486
+    ("struct_char_double", ot.struct_char_double, 4500),                                    # :498-505
+    ("twice_two_doubles", ot.twice_two_doubles, 4500),                                      # :508-515
+    ("blacs_2", ot.blacs, 2),                                                               # :518-524
+    ("blacs_4500", ot.blacs, 4500),
+]

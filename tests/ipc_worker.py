@@ -389,6 +389,23 @@ def p2p_checks(pkg, comm, rank, size, oracle, torch):
     assert np.array_equal(d.cpu().numpy(), want), "vector send"
     oracle.oracle_ddt_free(od)
     dv.destroy()
+    # host buffers across processes, in the same queue: host -> host through the sender's shared-
+    # memory arena (sizes that outgrow it: new segment generations the receiver maps by name),
+    # host -> device, device -> host (pulled into device staging, then copied out)
+    for salt, n in enumerate([5, 4097, 3 << 20, (40 << 20) + 1]):
+        hs = pattern(rank, n, 200 + salt)
+        want = pattern(prv, n, 200 + salt)
+        hd = np.zeros(n, dtype=np.uint8)
+        st = comm.sendrecv(hs.ctypes.data, n, nxt, 300 + salt, hd.ctypes.data, n, prv, 300 + salt)
+        assert st == (prv, 300 + salt, 0, n) and np.array_equal(hd, want), f"host->host {n}"
+        dd = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        comm.sendrecv(hs.ctypes.data, n, nxt, 400 + salt, dd.data_ptr(), n, prv, 400 + salt)
+        assert np.array_equal(dd.cpu().numpy(), want), f"host->device {n}"
+        ds = torch.from_numpy(hs).cuda()
+        torch.cuda.synchronize()
+        hd[:] = 0
+        comm.sendrecv(ds.data_ptr(), n, nxt, 500 + salt, hd.ctypes.data, n, prv, 500 + salt)
+        assert np.array_equal(hd, want), f"device->host {n}"
     if size == 2:   # a send buffer inside an allocation of >= 2 GiB: dmabuf export
         big = torch.full(((1 << 31) + (8 << 20),), rank + 1, dtype=torch.uint8, device="cuda")
         tail = 16 << 20

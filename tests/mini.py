@@ -59,6 +59,20 @@ class Mini:
         L.mini_irecv.argtypes = [vp, i, vp, i, i, vp, ctypes.POINTER(vp)]
         L.mini_iprobe.argtypes = [i, i, vp, ctypes.POINTER(i), vp]
         L.mini_wait_status.argtypes = [ctypes.POINTER(vp), vp]
+        L.mini_send_mode.argtypes = [vp, i, vp, i, i, i, vp]
+        L.mini_isend_mode.argtypes = [vp, i, vp, i, i, i, vp, ctypes.POINTER(vp)]
+        L.mini_probe.argtypes = [i, i, vp, vp]
+        L.mini_send_init.argtypes = [vp, i, vp, i, i, i, vp, ctypes.POINTER(vp)]
+        L.mini_recv_init.argtypes = [vp, i, vp, i, i, vp, ctypes.POINTER(vp)]
+        L.mini_start.argtypes = [ctypes.POINTER(vp)]
+        L.mini_request_free.argtypes = [ctypes.POINTER(vp)]
+        L.mini_cancel.argtypes = [vp]
+        L.mini_test.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(i), vp]
+        L.mini_improbe.argtypes = [i, i, vp, ctypes.POINTER(i), ctypes.POINTER(vp), vp]
+        L.mini_mprobe.argtypes = [i, i, vp, ctypes.POINTER(vp), vp]
+        L.mini_imrecv.argtypes = [vp, i, vp, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+        L.mini_mrecv.argtypes = [vp, i, vp, ctypes.POINTER(vp), vp]
+        L.mini_message_is_null.argtypes = [vp]
         L.mini_coll_module_new.restype = vp
         L.mini_comm_destroy.argtypes = [vp]
         L.mini_allreduce.argtypes = [vp, vp, vp, i, vp, vp]

@@ -163,28 +163,46 @@ def test_split_communicators_same_cid(gpu):
         assert p.returncode == 0 and f"rank {w} split OK" in outs[w], f"rank {w}:\n{outs[w][-3000:]}"
 
 
-@pytest.mark.parametrize("size", [2, 3])
-def test_pml_slot_device_p2p(gpu, size):
-    """MPI point-to-point through the PML slot (`mca_pml`): coll/mi355x's init_query hooks the
-    selected PML the way pml/v does (pml_v_component.c:110-131); MPI_Send/Ssend/Recv/Isend/Irecv/
-    Iprobe on device buffers move device data through the engine (statuses, MPI_ANY_SOURCE, a
-    derived send type, truncation), host buffers reach the saved PML, close restores the table"""
+def _run_workers(size, mode, extra_env=None, timeout=300):
+    """coll_worker.py <rank> <size> <key> <mode> as `size` processes; every rank must print
+    'rank <r> <mode> OK'"""
     key = uuid.uuid4().hex[:10]
     env = dict(os.environ, MI355X_TIMEOUT_S="60", OMPI_COMM_WORLD_SIZE=str(size),
-               OMPI_COMM_WORLD_LOCAL_SIZE=str(size), OMPI_MCA_ess_base_jobid=key)
-    procs = [subprocess.Popen([sys.executable, str(HERE / "coll_worker.py"), str(r), str(size), key, "pml"],
+               OMPI_COMM_WORLD_LOCAL_SIZE=str(size), OMPI_MCA_ess_base_jobid=key, **(extra_env or {}))
+    for k in [k for k in env if k.startswith("OMPI_MCA_coll_tuned_")]:
+        del env[k]   # coll/tuned's variables come from the variable system in these tests
+    procs = [subprocess.Popen([sys.executable, str(HERE / "coll_worker.py"), str(r), str(size), key, mode],
                               env=dict(env, OMPI_COMM_WORLD_LOCAL_RANK=str(r), OMPI_COMM_WORLD_RANK=str(r)),
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(size)]
     outs = []
     for p in procs:
         try:
-            out, _ = p.communicate(timeout=300)
+            out, _ = p.communicate(timeout=timeout)
         except subprocess.TimeoutExpired:
             p.kill()
             out, _ = p.communicate()
         outs.append(out)
     for r, p in enumerate(procs):
-        assert p.returncode == 0 and f"rank {r} pml OK" in outs[r], f"rank {r}:\n{outs[r][-3000:]}"
+        assert p.returncode == 0 and f"rank {r} {mode} OK" in outs[r], f"rank {r}:\n{outs[r][-3000:]}"
+
+
+@pytest.mark.parametrize("size", [2, 3])
+def test_pml_slot_device_p2p(gpu, size):
+    """MPI point-to-point through the PML slot (`mca_pml`): coll/mi355x's init_query hooks the
+    selected PML the way pml/v does (pml_v_component.c:110-131); on the engine communicator every
+    call -- MPI_Send/Ssend/Bsend/Recv/Isend/Irecv/Iprobe/Probe, persistent Send_init/Recv_init/Start,
+    Mprobe/Mrecv/Improbe/Imrecv, Cancel -- goes to the engine's one matching queue whatever the
+    buffer kinds (dev->host, host->dev, dev->dev, host->host; ANY_SOURCE and same-tag order across
+    kinds; derived types either side), nothing reaches the saved PML, close restores the table"""
+    _run_workers(size, "pml")
+
+
+def test_tuned_variables_through_mca_var_system(gpu):
+    """coll/tuned's use_dynamic_rules / allreduce_algorithm / dynamic_rules_filename as the MCA
+    variable system holds them (registered the way tuned_register does, values from a parameter
+    file, nothing in the environment) reach the engine: the forced algorithm's operand order,
+    then the rules file's (coll_tuned_component.c:151-167, coll_tuned_allreduce.c:949-1005)"""
+    _run_workers(2, "tuned_vars")
 
 
 def test_pml_hook_opt_out(gpu, monkeypatch):

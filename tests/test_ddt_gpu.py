@@ -356,3 +356,76 @@ def test_unit_kernel(gpu, pkg, oracle, case):
             assert cs % 2**32 == want_cs, mode
     finally:
         pkg.ddt_tune_rows(2)
+
+
+# ---- ddt_raw.c / ddt_test.c on the GPU convertor
+from ddtcases import COPY_CASES, RAW_CASES  # noqa: E402
+
+
+def _compiled(pkg, t):
+    return pkg.Ddt.from_opal(t.desc_bytes(), len(t.desc), t.extent, ot.basic_sizes())
+
+
+@pytest.mark.parametrize("case", [c[0] for c in RAW_CASES])
+def test_raw_pieces_are_the_packed_stream_gpu(gpu, pkg, case):
+    """the memory pieces mi355x_ddt_raw describes, read in order, are exactly the stream the GPU
+    pack kernel produces (opal_convertor_raw vs opal_convertor_pack on one convertor)"""
+    torch = gpu
+    _, build, count = next(c for c in RAW_CASES if c[0] == case)
+    t = build()
+    n, origin = span_of(t, count)
+    src = fill_pattern(n)
+    d = _compiled(pkg, t)
+    pieces = [p for c in d.raw(count, 5) for p in c]
+    want = np.concatenate([src[origin + off:origin + off + ln] for off, ln in pieces])
+    dsrc = torch.from_numpy(src).cuda()
+    out = torch.zeros(count * t.size, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    d.pack(count, dsrc.data_ptr() + origin, 0, out.data_ptr(), count * t.size)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), want)
+    d.destroy()
+
+
+@pytest.mark.parametrize("case", [c[0] for c in COPY_CASES])
+def test_local_copy_ddt_count_gpu(gpu, pkg, case):
+    """ompi_datatype_copy_content_same_ddt (ddt_test.c:141-170) on device memory: pack + unpack
+    kernels leave exactly the type map's bytes in a zeroed destination, and agree with the host
+    convertor"""
+    torch = gpu
+    _, build, count = next(c for c in COPY_CASES if c[0] == case)
+    t = build()
+    n, origin = span_of(t, count)
+    src = fill_pattern(n)
+    total = count * t.size
+    d = _compiled(pkg, t)
+    dsrc = torch.from_numpy(src).cuda()
+    ddst = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    tmp = torch.zeros(total, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    d.pack(count, dsrc.data_ptr() + origin, 0, tmp.data_ptr(), total)
+    d.unpack(count, ddst.data_ptr() + origin, 0, tmp.data_ptr(), total)
+    torch.cuda.synchronize()
+    assert np.array_equal(ddst.cpu().numpy(), expected_copy(t, count, src, origin))
+    hp = np.zeros(total, dtype=np.uint8)
+    d.pack_host(count, src.ctypes.data + origin, 0, hp.ctypes.data, total)
+    assert np.array_equal(tmp.cpu().numpy(), hp)
+    d.destroy()
+
+
+def test_zero_count_contiguous_types_gpu(gpu, pkg):
+    """ddt_test.c:401-411 types (pdt1 with long double elements) packed on the GPU == host convertor"""
+    torch = gpu
+    for t in ot.ddt_test_zero_count_types():
+        d = _compiled(pkg, t)
+        n, origin = span_of(t, 5)
+        src = fill_pattern(n)
+        dsrc = torch.from_numpy(src).cuda()
+        out = torch.zeros(5 * t.size, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        d.pack(5, dsrc.data_ptr() + origin, 0, out.data_ptr(), 5 * t.size)
+        torch.cuda.synchronize()
+        hp = np.zeros(5 * t.size, dtype=np.uint8)
+        d.pack_host(5, src.ctypes.data + origin, 0, hp.ctypes.data, hp.size)
+        assert np.array_equal(out.cpu().numpy(), hp)
+        d.destroy()

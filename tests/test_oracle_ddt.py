@@ -253,3 +253,97 @@ def test_ddt_pack_c_types():
     assert (s.size, s.lb, s.ub) == (364, 0, 544)
     elems = ot.walk_desc(s)  # the convertor's visit order: 11 ints, then 2 x (10 + 10) doubles
     assert sum(n for _, n in elems) == 364 and [a for a, _ in elems[:12]] == [4 * i for i in range(11)] + [64]
+
+
+# ---- test/datatype/ddt_raw.c and ddt_test.c, restated (VERDICT r2 missing #4)
+from ddtcases import COPY_CASES, RAW_CASES  # noqa: E402
+
+
+def _compiled(pkg, t):
+    """the engine's layout of a restated type: its description records through mi355x_ddt_from_opal
+    (what coll/mi355x hands the engine for a committed derived datatype)"""
+    return pkg.Ddt.from_opal(t.desc_bytes(), len(t.desc), t.extent, ot.basic_sizes())
+
+
+@pytest.mark.parametrize("case", [c[0] for c in RAW_CASES])
+def test_raw_walk_kat(pkg, case):
+    """opal_convertor_raw's walk: calls of at most 5 iovecs that together describe every byte
+    (ddt_raw.c:118-131 -- the reference's check is `remaining_length == 0`) in type-map order, on the
+    restated convertor walk and on the engine's mi355x_ddt_raw (no GPU)"""
+    _, build, count = next(c for c in RAW_CASES if c[0] == case)
+    t = build()
+    tmap = ot.merge_pieces([(d + k * t.extent, s) for k in range(count) for d, s in t.tmap])
+    calls = ot.convertor_raw(t, count, 5)
+    assert all(len(c) <= 5 for c in calls) and all(len(c) == 5 for c in calls[:-1])
+    assert sum(n for c in calls for _, n in c) == count * t.size
+    assert ot.merge_pieces([p for c in calls for p in c]) == tmap
+    d = _compiled(pkg, t)
+    ecalls = d.raw(count, 5)
+    assert all(len(c) <= 5 for c in ecalls) and all(len(c) == 5 for c in ecalls[:-1])
+    assert sum(n for c in ecalls for _, n in c) == count * t.size
+    assert ot.merge_pieces([p for c in ecalls for p in c]) == tmap
+    # resuming at any packed position describes the rest (opal_convertor_raw restarts from its stack)
+    for cut in (1, 7, count * t.size // 3):
+        pos = ctypes.c_size_t(cut)
+        got = []
+        while True:
+            disp = (ctypes.c_int64 * 5)()
+            lens = (ctypes.c_size_t * 5)()
+            cnt, mx = ctypes.c_uint32(5), ctypes.c_size_t()
+            rc = pkg.rt().mi355x_ddt_raw(d.h, count, ctypes.byref(pos), disp, lens, ctypes.byref(cnt), ctypes.byref(mx))
+            got += [(disp[i], lens[i]) for i in range(cnt.value)]
+            if rc == 1:
+                break
+        assert sum(n for _, n in got) == count * t.size - cut
+    d.destroy()
+
+
+@pytest.mark.parametrize("case", [c[0] for c in COPY_CASES])
+def test_local_copy_ddt_count_host(pkg, oracle, case):
+    """ompi_datatype_copy_content_same_ddt(pdt, count, dst, src) (ddt_test.c:141-170) through the
+    engine's host convertor (pack then unpack, the bytes a same-type copy moves): the destination
+    holds exactly the type map's bytes of the source; the packed stream equals the oracle's"""
+    _, build, count = next(c for c in COPY_CASES if c[0] == case)
+    t = build()
+    n, origin = span_of(t, count)
+    src = fill_pattern(n)
+    dst = np.zeros(n, dtype=np.uint8)
+    total = count * t.size
+    d = _compiled(pkg, t)
+    packed = np.zeros(total, dtype=np.uint8)
+    d.pack_host(count, src.ctypes.data + origin, 0, packed.ctypes.data, total)
+    d.unpack_host(count, dst.ctypes.data + origin, 0, packed.ctypes.data, total)
+    assert np.array_equal(dst, expected_copy(t, count, src, origin))
+    od = c_oracle(oracle, t)
+    want = np.zeros(total, dtype=np.uint8)
+    assert oracle.oracle_ddt_pack(od, count, src.ctypes.data + origin, 0, want.ctypes.data, total) == 0
+    assert np.array_equal(packed, want)
+    # and in arbitrary windows (the convertor's fragments): 956-byte chunks as ddt_test.c:353
+    dst2 = np.zeros(n, dtype=np.uint8)
+    for pos in range(0, total, 956):
+        sz = min(956, total - pos)
+        d.unpack_host(count, dst2.ctypes.data + origin, pos, packed.ctypes.data + pos, sz)
+    assert np.array_equal(dst2, dst)
+    oracle.oracle_ddt_free(od)
+    d.destroy()
+
+
+def test_zero_count_contiguous_types(pkg, oracle):
+    """ddt_test.c:401-411: types grown from contiguous(0, MPI_DATATYPE_NULL) by ompi_datatype_add --
+    sizes / extents by opal_datatype_add's rules (long double's 16-byte alignment pads pdt1's extent
+    to 80), compiled by the engine to the same layout, packed like the oracle"""
+    p1, p2, p3 = ot.ddt_test_zero_count_types()
+    assert [(t.size, t.extent) for t in (p1, p2, p3)] == [(72, 80), (184, 184), (60, 60)]
+    for t in (p1, p2, p3):
+        d = _compiled(pkg, t)
+        assert (d.size, d.extent) == (t.size, t.extent)
+        n, origin = span_of(t, 3)
+        src = fill_pattern(n)
+        got = np.zeros(3 * t.size, dtype=np.uint8)
+        d.pack_host(3, src.ctypes.data + origin, 0, got.ctypes.data, got.size)
+        od = c_oracle(oracle, t)
+        want = np.zeros_like(got)
+        assert oracle.oracle_ddt_pack(od, 3, src.ctypes.data + origin, 0, want.ctypes.data, want.size) == 0
+        assert np.array_equal(got, want)
+        oracle.oracle_ddt_free(od)
+        d.destroy()

@@ -1,9 +1,9 @@
-"""Device point-to-point (mi355x_isend / irecv / send / recv / sendrecv / iprobe) on a loopback
+"""Point-to-point (mi355x_isend / irecv / send / recv / sendrecv / iprobe / improbe / imrecv) on a loopback
 communicator (one process, one rank per comm object).  The semantics checked are ob1's
 (ompi/mca/pml/ob1/pml_ob1_recvfrag.c matching, pml_ob1_recvreq.h:172-180 truncation): messages
 from one source are received in send order, posted receives are matched in posting order,
 MPI_ANY_SOURCE / MPI_ANY_TAG wildcards, MPI_PROC_NULL, zero-byte messages, truncation keeps the
-first bytes and reports the message size.  Bytes moved through derived datatypes must equal the
+first bytes and reports the message size; host and device buffers share the queue.  Bytes moved through derived datatypes must equal the
 oracle's unpack(pack(...)) (the convertor restatement under oracle/)."""
 from __future__ import annotations
 
@@ -112,13 +112,16 @@ def test_proc_null_and_self(gpu, pkg, comms):
     assert torch.equal(dst, src)
 
 
-def test_ring_wraps(gpu, pkg, comms):
-    """more messages in flight than envelopes per pair (32): later sends queue, order is kept"""
+@pytest.mark.parametrize("mode", ["STANDARD", "SYNCHRONOUS"])
+def test_ring_wraps(gpu, pkg, comms, mode):
+    """more messages in flight than envelopes per pair (32): later sends queue, order is kept.  Small
+    standard sends complete for the caller at once (eager: the engine keeps the queued envelope);
+    synchronous ones only once received"""
     torch = gpu
     k = 100
     src = _bytes(torch, k * 16, 5)
-    sends = [comms[0].isend(src[i * 16:(i + 1) * 16].data_ptr(), 16, 1, i % 3) for i in range(k)]
-    assert not sends[-1].test()
+    sends = [comms[0].isend(src[i * 16:(i + 1) * 16].data_ptr(), 16, 1, i % 3, mode=mode) for i in range(k)]
+    assert sends[-1].test() == (mode == "STANDARD")
     dst = torch.zeros(k * 16, dtype=torch.uint8, device="cuda")
     for i in range(k):
         r = comms[1].irecv(dst[i * 16:(i + 1) * 16].data_ptr(), 16, 0, pkg.ANY_TAG)
@@ -238,11 +241,207 @@ def test_errors(gpu, pkg, comms):
     buf = torch.zeros(16, dtype=torch.uint8, device="cuda")
     with pytest.raises(pkg.MI355XError, match="bad destination"):
         comms[0].isend(buf.data_ptr(), 16, 9, 0)
-    with pytest.raises(pkg.MI355XError, match="bad tag"):
-        comms[0].isend(buf.data_ptr(), 16, 1, -5)
-    host = np.zeros(16, dtype=np.uint8)
-    with pytest.raises(pkg.MI355XError, match="device memory"):
-        comms[0].isend(host.ctypes.data, 16, 1, 0)
+    with pytest.raises(pkg.MI355XError, match="MPI_ANY_TAG"):
+        comms[0].isend(buf.data_ptr(), 16, 1, pkg.ANY_TAG)
+    with pytest.raises(pkg.MI355XError, match="bad send mode"):
+        rt = pkg.rt()
+        import ctypes
+        h = ctypes.c_void_p()
+        pkg.check(rt.mi355x_isend_mode(comms[0].h, buf.data_ptr(), 16, None, 1, 0, 9, None, ctypes.byref(h)), "isend_mode")
+
+
+# ---- one matching queue for host and device buffers (ob1: pml_ob1_cuda.c:52-100 decides the
+#      convertor per request on the send side, pml_ob1_recvreq.c:647-663 on the receive side; the
+#      match itself never looks at the buffer kind)
+def _buf(torch, kind, data: np.ndarray):
+    """a host (numpy) or device (torch) buffer holding `data` (uint8); returns (ptr, reader, keep)"""
+    if kind == "host":
+        h = np.ascontiguousarray(data).copy()
+        return h.ctypes.data, (lambda: h.copy()), h
+    d = torch.from_numpy(np.ascontiguousarray(data).copy()).cuda()
+    torch.cuda.synchronize()
+    return d.data_ptr(), (lambda: d.cpu().numpy()), d
+
+
+KINDS = [("dev", "dev"), ("dev", "host"), ("host", "dev"), ("host", "host")]
+
+
+@pytest.mark.parametrize("skind,rkind", KINDS)
+@pytest.mark.parametrize("nbytes", [0, 17, 4096, 4097, (1 << 20) + 3])
+def test_host_device_pairs(gpu, pkg, comms, skind, rkind, nbytes):
+    """every pairing of buffer kinds meets in one queue, sizes either side of the 4 KiB eager limit"""
+    torch = gpu
+    data = np.random.default_rng(nbytes + 7).integers(0, 256, max(nbytes, 1), dtype=np.uint8)
+    sp, _, keep_s = _buf(torch, skind, data)
+    rp, read, keep_r = _buf(torch, rkind, np.zeros(max(nbytes, 1) + 5, dtype=np.uint8))
+    rq = comms[1].irecv(rp, nbytes + 5, 0, 4)
+    sq = comms[0].isend(sp, nbytes, 1, 4)
+    assert rq.wait() == (0, 4, 0, nbytes)
+    sq.wait()
+    got = read()
+    assert np.array_equal(got[:nbytes], data[:nbytes]) and not got[nbytes:].any()
+
+
+def test_any_source_and_order_across_kinds(gpu, pkg, comms):
+    """MPI_ANY_SOURCE sees senders of both kinds; between one pair, same-tag messages of alternating
+    kinds and sizes (eager and rendezvous) match in send order into alternating receive kinds"""
+    torch = gpu
+    n = len(comms)
+    g = np.random.default_rng(11)
+    # non-overtaking across kinds: 12 messages 0 -> 1 on one tag
+    sizes = [3, 5000, 64, 1 << 20, 4096, 9000, 1, 70000, 4097, 12, 2 << 20, 100]
+    payload = [g.integers(0, 256, ln, dtype=np.uint8) for ln in sizes]
+    sends = [_buf(torch, "dev" if i % 2 else "host", payload[i]) for i in range(len(sizes))]
+    sq = [comms[0].isend(sends[i][0], sizes[i], 1, 21) for i in range(len(sizes))]
+    recvs = [_buf(torch, "host" if i % 3 else "dev", np.zeros(2 << 20, dtype=np.uint8)) for i in range(len(sizes))]
+    rq = [comms[1].irecv(recvs[i][0], 2 << 20, 0, 21) for i in range(len(sizes))]
+    for i, q in enumerate(rq):
+        assert q.wait() == (0, 21, 0, sizes[i]), i
+        assert np.array_equal(recvs[i][1]()[:sizes[i]], payload[i]), ("order", i)
+    for q in sq:
+        q.wait()
+    # ANY_SOURCE: ranks 1..n-1 send (odd ranks from host memory), rank 0 receives into host and device
+    src = {r: _buf(torch, "host" if r % 2 else "dev", np.full(40 + r, r, dtype=np.uint8)) for r in range(1, n)}
+    sq = [comms[r].isend(src[r][0], 40 + r, 0, 5) for r in range(1, n)]
+    seen = set()
+    for i in range(1, n):
+        rb = _buf(torch, "dev" if i % 2 else "host", np.zeros(64, dtype=np.uint8))
+        st = comms[0].recv(rb[0], 64, pkg.ANY_SOURCE, 5)
+        r = st[0]
+        assert st == (r, 5, 0, 40 + r) and r not in seen
+        assert np.array_equal(rb[1]()[:40 + r], np.full(40 + r, r, dtype=np.uint8))
+        seen.add(r)
+    assert seen == set(range(1, n))
+    for q in sq:
+        q.wait()
+
+
+def test_send_completion_modes(gpu, pkg, comms):
+    """ob1's completion rules: a standard send of <= 4 KiB completes before any receive is posted
+    (eager), a synchronous one does not; a buffered send of any size completes at once and the
+    receiver gets the bytes as they were at the send"""
+    torch = gpu
+    a, b = comms[0], comms[1]
+    small = _buf(torch, "dev", np.full(4096, 7, dtype=np.uint8))
+    q_std = a.isend(small[0], 4096, 1, 1)
+    assert q_std.test(), "standard 4 KiB send is eager"
+    q_sync = a.isend(small[0], 4096, 1, 2, mode="SYNCHRONOUS")
+    for _ in range(50):
+        assert not q_sync.test(), "a synchronous send completed before its receive was posted"
+    big = torch.full((3 << 20,), 9, dtype=torch.uint8, device="cuda")
+    hbig = np.full(3 << 20, 5, dtype=np.uint8)
+    torch.cuda.synchronize()
+    q_buf = a.isend(big.data_ptr(), 3 << 20, 1, 3, mode="BUFFERED")
+    q_hbuf = a.isend(hbig.ctypes.data, 3 << 20, 1, 4, mode="BUFFERED")
+    assert q_buf.test() and q_hbuf.test(), "buffered sends complete at once"
+    big.fill_(0)
+    hbig[:] = 0
+    torch.cuda.synchronize()
+    q_big = a.isend(big.data_ptr(), 3 << 20, 1, 5)
+    assert not q_big.test(), "a 3 MiB standard send is rendezvous"
+    out = [np.zeros(3 << 20, dtype=np.uint8) for _ in range(5)]
+    for tag, o in zip((1, 2, 3, 4, 5), out):
+        b.recv(o.ctypes.data, 3 << 20, 0, tag)
+    for q in (q_std, q_sync, q_buf, q_hbuf, q_big):
+        q.wait()
+    assert (out[0][:4096] == 7).all() and (out[1][:4096] == 7).all()
+    assert (out[2] == 9).all() and (out[3] == 5).all(), "buffered payload changed after completion"
+    assert not out[4].any()
+
+
+def test_unsafe_exchange_small(gpu, pkg, comms):
+    """both ranks MPI_Send before MPI_Recv: legal to deadlock in MPI, but ob1's eager protocol lets
+    it through for small messages -- and so must this engine (threads, blocking calls)"""
+    torch = gpu
+    bufs = {r: (_buf(torch, "dev", np.full(1000, r + 1, dtype=np.uint8)), np.zeros(1000, dtype=np.uint8))
+            for r in (0, 1)}
+    errs = []
+
+    def run(r):
+        try:
+            torch.cuda.set_device(0)
+            comms[r].send(bufs[r][0][0], 1000, 1 - r, 8)
+            comms[r].recv(bufs[r][1].ctypes.data, 1000, 1 - r, 8)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in (0, 1)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    assert not errs, errs
+    assert (bufs[0][1] == 2).all() and (bufs[1][1] == 1).all()
+
+
+def test_matched_probe_and_cancel(gpu, pkg, comms):
+    """MPI_Improbe takes the message out of the queue (a later wildcard receive gets the NEXT one),
+    MPI_Imrecv receives exactly it, into host memory; MPI_Cancel of an unmatched receive; negative
+    (system) tags travel but MPI_ANY_TAG never matches them (pml_ob1_recvfrag.c:487)"""
+    torch = gpu
+    a, b = comms[2], comms[3]
+    m1 = _buf(torch, "dev", np.arange(100, dtype=np.uint8))
+    m2 = _buf(torch, "host", np.arange(100, 200, dtype=np.uint8))
+    s1 = a.isend(m1[0], 100, 3, 6)
+    s2 = a.isend(m2[0], 100, 3, 6)
+    hit = None
+    while hit is None:
+        hit = b.improbe(2, 6)
+    msg, st = hit
+    assert st == (2, 6, 0, 100)
+    other = np.zeros(100, dtype=np.uint8)
+    assert b.recv(other.ctypes.data, 100, pkg.ANY_SOURCE, pkg.ANY_TAG) == (2, 6, 0, 100)
+    assert np.array_equal(other, np.arange(100, 200, dtype=np.uint8)), "the probed message was stolen"
+    mine = np.zeros(100, dtype=np.uint8)
+    assert b.imrecv(mine.ctypes.data, 100, msg).wait() == (2, 6, 0, 100)
+    assert np.array_equal(mine, np.arange(100, dtype=np.uint8))
+    s1.wait()
+    s2.wait()
+    # cancel
+    dummy = np.zeros(8, dtype=np.uint8)
+    q = b.irecv(dummy.ctypes.data, 8, 2, 77)
+    q.cancel()
+    assert q.test() and q.cancelled()
+    q.wait()
+    # system tags
+    neg = _buf(torch, "host", np.full(8, 3, dtype=np.uint8))
+    sq = a.isend(neg[0], 8, 3, -17)
+    anyq = b.irecv(dummy.ctypes.data, 8, 2, pkg.ANY_TAG)
+    for _ in range(20):
+        assert not anyq.test(), "MPI_ANY_TAG matched a system tag"
+    got = np.zeros(8, dtype=np.uint8)
+    assert b.recv(got.ctypes.data, 8, 2, -17) == (2, -17, 0, 8) and (got == 3).all()
+    sq.wait()
+    anyq.cancel()
+    anyq.wait()
+
+
+@pytest.mark.parametrize("skind,rkind", KINDS)
+def test_host_device_datatypes(gpu, pkg, oracle, comms, skind, rkind):
+    """derived layouts on either side, either kind: host layouts go through the host convertor
+    (mi355x_pack_host / unpack_host), device layouts through the GPU convertor; vector -> indexed"""
+    torch = gpu
+    nblk = 3000
+    dv = pkg.Ddt.vector(nblk, 3, 5, 4)              # 3 floats every 5: 12-B runs, 36000 B packed
+    di = pkg.Ddt.indexed([5, 2, 8, 9], [0, 7, 11, 30], 4)  # 24 floats = 96 B per instance
+    assert dv.size == 36000 and di.size == 96
+    g = np.random.default_rng(3)
+    src = g.integers(0, 256, dv.extent, dtype=np.uint8)
+    inst = 36000 // 96
+    dst0 = np.full(di.extent * inst + 64, 0xAB, dtype=np.uint8)
+    sp, _, ks = _buf(torch, skind, src)
+    rp, read, kr = _buf(torch, rkind, dst0)
+    rq = comms[1].irecv(rp, inst, 0, 2, ddt=di)
+    sq = comms[0].isend(sp, 1, 1, 2, ddt=dv)
+    assert rq.wait() == (0, 2, 0, 36000)
+    sq.wait()
+    packed = np.zeros(36000, dtype=np.uint8)
+    dv.pack_host(1, src.ctypes.data, 0, packed.ctypes.data, 36000)
+    want = dst0.copy()
+    di.unpack_host(inst, want.ctypes.data, 0, packed.ctypes.data, 36000)
+    assert np.array_equal(read(), want)
+    dv.destroy()
+    di.destroy()
 
 
 def _ob1_match_model(arrived, recvs):
