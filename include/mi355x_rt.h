@@ -153,13 +153,16 @@ enum mi355x_knob {
     MI355X_KNOB_PIPE_WT = 16,           /* pipelined allreduce: 1 (default) = fold results stored write-
                                            through (system-coherent policy) and pulled with coherent
                                            loads, no per-chunk L2 write-back / invalidate; 0 = fences */
-    MI355X_KNOB_ONE_PHASE_MAX_BYTES = 17 /* (per communicator, same value on every rank; env
+    MI355X_KNOB_ONE_PHASE_MAX_BYTES = 17, /* (per communicator, same value on every rank; env
                                            MI355X_ONE_PHASE_MAX_BYTES at creation) ring-ordered
                                            allreduce (not in place) up to this many bytes
                                            per rank: every rank evaluates every ring block from the n
                                            inputs in one launch (reads n x S, one host barrier and
                                            stream sync fewer than the two phases); default 1 MiB,
                                            0 = always two phases */
+    MI355X_KNOB_PIPE_REFUSED = 18       /* (read-only) calls of this communicator that were to run pipelined
+                                           but fell back to two phases because another communicator's
+                                           pipelined grid held a GPU (the per-GPU admission token) */
 };
 int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
 /* current value of a knob (LL_MAX_BYTES reads 0 when the creation-time LL self-test failed) */

@@ -657,11 +657,76 @@ int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t s
     return MI355X_SUCCESS;
 }
 
+// finish: every rank's work queued on its stream so far has completed (so no rank still reads a
+// peer's buffer, and my results are in place).  With the control segment registered, the GPU's
+// command processor writes this finish point's number into my RankSlot::done right behind my
+// kernels (hipStreamWriteValue64) and I poll every rank's word: the kernel's completion reaches
+// every host without a hipStreamSynchronize wake-up and without a second barrier round.
+// Otherwise: stream sync + barrier.
 int finish(mi355x_comm *c, hipStream_t s)
 {
-    TRACE(c, "finish: stream sync");
-    MI_HIP(hipStreamSynchronize(s));
-    TRACE(c, "finish: barrier");
+    if (!c->ctrl_dev || c->size == 1) {
+        TRACE(c, "finish: stream sync");
+        MI_HIP(hipStreamSynchronize(s));
+        TRACE(c, "finish: barrier");
+        return barrier(c);
+    }
+    const uint64_t v = ++c->done_seq;
+    char *word = c->ctrl_dev + ((char *)&c->ctrl->slot[c->rank].done - (char *)c->ctrl);
+    MI_HIP(hipStreamWriteValue64(s, word, v, 0));
+    TRACE(c, "finish %llu: polling the ranks' completion words", (unsigned long long)v);
+    Ctrl *k = c->ctrl;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int q = 0; q < c->size; ++q) {
+        unsigned spins = 0;
+        while (k->slot[q].done.load(std::memory_order_acquire) < v) {
+            if (k->abort_flag.load(std::memory_order_relaxed))
+                return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
+            if (++spins > 4096) {
+                sched_yield();
+                if ((spins & 0xffff) == 0 && hipStreamQuery(s) != hipErrorNotReady && q == c->rank &&
+                    k->slot[q].done.load(std::memory_order_acquire) < v)
+                    return set_error(MI355X_ERR_HIP, "stream finished without writing its completion word");
+                if ((spins & 0xffff) == 0 &&
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
+                    k->abort_flag.store(1);
+                    return set_error(MI355X_ERR_TIMEOUT, "rank %d: finish %llu timed out waiting for rank %d (at %llu)",
+                                     c->rank, (unsigned long long)v, q, (unsigned long long)k->slot[q].done.load());
+                }
+            }
+        }
+    }
+    return MI355X_SUCCESS;
+}
+
+// register the control segment with HIP so the command processor can write completion words into
+// it (multi-process communicators; MI355X_DONE_WORDS=0 keeps stream sync + barrier).  Every rank
+// decides the same way or the finish points would not pair: the outcome is agreed on with a
+// barrier round through the segment.
+static int setup_done_words(mi355x_comm *c)
+{
+    const char *env = getenv("MI355X_DONE_WORDS");
+    bool ok = !(env && atoi(env) == 0) && c->size > 1 && !c->loopback;
+    if (ok) {
+        ok = hipHostRegister(c->ctrl, ctrl_bytes(c->size), hipHostRegisterMapped) == hipSuccess;
+        if (ok) {
+            c->ctrl_registered = true;
+            void *dptr = nullptr;
+            ok = hipHostGetDevicePointer(&dptr, c->ctrl, 0) == hipSuccess && dptr;
+            c->ctrl_dev = ok ? (char *)dptr : nullptr;
+        }
+        (void)hipGetLastError();
+    }
+    c->ctrl->slot[c->rank].done.store(ok ? 1 : 2, std::memory_order_release);
+    int rc = barrier(c);
+    if (rc) return rc;
+    bool all = true;
+    for (int q = 0; q < c->size; ++q) all = all && c->ctrl->slot[q].done.load(std::memory_order_acquire) == 1;
+    rc = barrier(c);   // every rank has read the setup words before they are reset
+    if (rc) return rc;
+    c->ctrl->slot[c->rank].done.store(0, std::memory_order_release);
+    if (!all) c->ctrl_dev = nullptr;
+    c->done_seq = 0;
     return barrier(c);
 }
 
@@ -1082,6 +1147,81 @@ static int ensure_pipe(mi355x_comm *c)
     return barrier(c);  // every rank has read the exchange slots
 }
 
+// ---- admission of the pipelined grid.  k_pipe_allreduce is persistent and spins on flags its
+// peers' grids raise, so it must never wait behind another spinning grid: two communicators whose
+// grids each hold one GPU while waiting for the other's would wait forever (a cross-GPU circular
+// wait, possible in any MPI_THREAD_MULTIPLE program that overlaps collectives on several
+// communicators).  Every GPU therefore carries a node-wide token: one communicator at a time may
+// have pipelined grids on it (its ranks sharing that GPU -- a rehearsal -- count up the same
+// token).  Per call every rank tries its GPU's token WITHOUT waiting and publishes the outcome with
+// the call's buffer exchange; the call is pipelined only if every rank holds its token, otherwise
+// every rank releases and the call takes the two-phase flow, whose kernels never wait on a peer.
+// Nothing ever spins for admission (the never-blocking progress rule of opal_progress.c:150).
+// The table lives in a per-user shared-memory segment (64 GPUs); a process that dies holding a
+// token leaves that GPU on the two-phase flow, never hung.
+struct GpuTokens {
+    std::atomic<uint64_t> uid[64];    // device uid (hash of the PCI bus id), 0 = free slot
+    std::atomic<uint64_t> word[64];   // (holder << 16) | holders' count; 0 = free
+};
+
+static GpuTokens *gpu_tokens()
+{
+    static GpuTokens *t = nullptr;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        char name[64];
+        snprintf(name, sizeof(name), "/mi355x_gpu_tokens_%u", (unsigned)getuid());
+        const int fd = shm_open(name, O_CREAT | O_RDWR, 0600);
+        if (fd < 0) return;
+        struct stat st;
+        if (fstat(fd, &st) == 0 && (size_t)st.st_size < sizeof(GpuTokens) && ftruncate(fd, sizeof(GpuTokens)) != 0) {
+            close(fd);
+            return;
+        }
+        void *m = mmap(nullptr, sizeof(GpuTokens), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        close(fd);
+        if (m != MAP_FAILED) t = (GpuTokens *)m;  // a fresh segment is zero-filled: every slot free
+    });
+    return t;
+}
+
+static bool pipe_token_acquire(mi355x_comm *c)
+{
+    GpuTokens *t = gpu_tokens();
+    if (!t) return false;
+    if (c->pipe_token < 0) {
+        const uint64_t uid = c->ctrl->slot[c->rank].dev_uid | 1;
+        for (int i = 0; i < 64 && c->pipe_token < 0; ++i) {
+            uint64_t cur = t->uid[i].load(std::memory_order_acquire);
+            if (cur == 0 && t->uid[i].compare_exchange_strong(cur, uid)) cur = uid;
+            if (cur == uid) c->pipe_token = i;
+        }
+        if (c->pipe_token < 0) return false;
+        uint64_t h = 1469598103934665603ull;
+        for (char ch : c->shm_name) h = (h ^ (unsigned char)ch) * 1099511628211ull;
+        c->pipe_holder = (h & 0xffffffffffffull) | 1;
+    }
+    std::atomic<uint64_t> &w = t->word[c->pipe_token];
+    uint64_t cur = w.load(std::memory_order_acquire);
+    for (;;) {
+        const uint64_t holder = cur >> 16, cnt = cur & 0xffff;
+        if (cnt != 0 && holder != c->pipe_holder) return false;
+        if (cnt == 0xffff) return false;
+        if (w.compare_exchange_weak(cur, (c->pipe_holder << 16) | (cnt + 1), std::memory_order_acq_rel)) return true;
+    }
+}
+
+static void pipe_token_release(mi355x_comm *c)
+{
+    std::atomic<uint64_t> &w = gpu_tokens()->word[c->pipe_token];
+    uint64_t cur = w.load(std::memory_order_acquire);
+    for (;;) {
+        const uint64_t cnt = cur & 0xffff;
+        const uint64_t next = cnt <= 1 ? 0 : (cur & ~0xffffull) | (cnt - 1);
+        if (w.compare_exchange_weak(cur, next, std::memory_order_acq_rel)) return;
+    }
+}
+
 // One launch per rank: fold my ring block and pull the other blocks, chunk by chunk, with
 // device-side readiness flags (coll_pipe.hip).  P[0] = every rank's input, P[1] = every rbuf.
 static int pipe_allreduce(mi355x_comm *c, int op, int type, const Program &pr,
@@ -1467,6 +1607,7 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     // behind at n = 2 in the one-GPU rehearsal (profiles/r02_bench_n{2,4,8}_*); MI355X_PIPE=0/1 decides
     c->pipe_on = env_double("MI355X_PIPE", size >= 4 ? 1.0 : 0.0) != 0.0;
     c->one_phase_max = (size_t)std::max(0.0, env_double("MI355X_ONE_PHASE_MAX_BYTES", (double)c->one_phase_max));
+    if (rc == MI355X_SUCCESS && size > 1) rc = setup_done_words(c);
     if (rc == MI355X_SUCCESS && size > 1) rc = ll_selftest(c);
     if (rc) {
         mi355x_comm_destroy(c);
@@ -1527,6 +1668,7 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
     if (c->ll_base) (void)hipFree(c->ll_base);
     if (c->ll_ctr) (void)hipFree(c->ll_ctr);
     if (c->ll_err) (void)hipHostFree(c->ll_err);
+    if (c->ctrl_registered) (void)hipHostUnregister(c->ctrl);
     if (c->loopback) {
         std::lock_guard<std::mutex> g(c->loop->mtx);
         if (--c->loop->refs == 0) free(c->loop->ctrl);
@@ -1616,6 +1758,7 @@ int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
     case MI355X_KNOB_PUSH: *value = coll_tune().push; break;
     case MI355X_KNOB_IPC_MAX_BYTES: *value = (long)c->ipc_max; break;
     case MI355X_KNOB_STAGE_BYTES: *value = (long)c->stage_bytes; break;
+    case MI355X_KNOB_PIPE_REFUSED: *value = (long)c->pipe_refused; break;
     case MI355X_KNOB_LL_MAX_BYTES: *value = (long)c->ll_max; break;
     case MI355X_KNOB_REDUCE_CHAIN_FANOUT: *value = c->chain_fanout; break;
     case MI355X_KNOB_TIME_PHASES: *value = c->time_phases ? 1 : 0; break;
@@ -1800,18 +1943,43 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
         }
         return ll_run(c, a, op, type, s);
     }
-    const bool pipe = ring && !c->loopback && c->pipe_on && !coll_tune().push;
+    bool pipe = ring && !c->loopback && c->pipe_on && !coll_tune().push;
     if (pipe) {  // collective setup first: it reuses the exchange slots
         rc = ensure_pipe(c);
         if (rc) return rc;
     }
+    // admission (above): try my GPU's token, publish the outcome with the exchange
+    const bool held = pipe && pipe_token_acquire(c);
+    if (pipe) c->ctrl->slot[c->rank].pipe_adm.store(((c->seq + 1) << 1) | (held ? 1u : 0u), std::memory_order_release);
     MI_HIP(hipStreamSynchronize(s));  // every rank's input is complete before it is published
     const void *mine[2] = {in, rbuf};
     const uint64_t sig[4] = {1, count, (uint64_t)type, (uint64_t)op};
     std::vector<std::vector<void *>> P;
     bool staged = false;
     rc = exchange(c, 2, mine, sig, P, &staged);
-    if (rc) return rc;
+    if (rc) {
+        if (held) pipe_token_release(c);
+        return rc;
+    }
+    if (pipe) {
+        bool all = true;
+        for (int q = 0; q < c->size; ++q)
+            all = all && c->ctrl->slot[q].pipe_adm.load(std::memory_order_acquire) == ((c->seq << 1) | 1u);
+        if (!all) {
+            pipe = false;
+            c->pipe_refused++;
+            TRACE(c, "pipelined grid not admitted on every GPU: two-phase flow");
+        }
+        if (held && !all) pipe_token_release(c);
+    }
+    struct TokenGuard {  // an admitted grid gives its token back once the call is over
+        mi355x_comm *c;
+        bool on;
+        ~TokenGuard()
+        {
+            if (on) pipe_token_release(c);
+        }
+    } token_guard{c, pipe && held};
     Program pr;
     if (!ring) {
         if (!allreduce_tree_program(c, alg, count, esz, &pr))

@@ -69,6 +69,13 @@ struct alignas(64) RankSlot {
     // mi355x_comm_vote: call v's entry at [v % kVoteRing] = (v << 1) | (this rank's buffers are
     // device memory); a ring because a rank with device buffers publishes and moves on
     std::atomic<uint64_t> vote[kVoteRing];
+    // pipelined allreduce admission for the call whose exchange carries sequence s:
+    // (s << 1) | (this rank holds its GPU's pipelined-grid token)
+    std::atomic<uint64_t> pipe_adm;
+    // finish(): the number of finish points this rank's stream has passed, written by the GPU's
+    // command processor behind the rank's kernels (hipStreamWriteValue64 into the host-registered
+    // control segment); every rank polls every rank's word instead of a stream sync + barrier
+    alignas(64) std::atomic<uint64_t> done;
 };
 
 struct Ctrl {
@@ -251,6 +258,14 @@ struct mi355x_comm {
     // (MI355X_KNOB_ONE_PHASE_MAX_BYTES, env MI355X_ONE_PHASE_MAX_BYTES)
     size_t one_phase_max = (size_t)1 << 20;
     bool pipe_on = false;                         // MI355X_KNOB_PIPE (env MI355X_PIPE; default: size >= 4)
+    uint64_t pipe_holder = 0;                     // this communicator's id in the GPU token table
+    int pipe_token = -1;                          // token table slot of my GPU (-1: not looked up)
+    uint64_t pipe_refused = 0;                    // calls that fell back because a token was taken
+    // finish() by device-written completion words (see RankSlot::done): the control segment
+    // registered with HIP (hipHostRegister) and its device address; 0 = stream sync + barrier
+    char *ctrl_dev = nullptr;
+    bool ctrl_registered = false;
+    uint64_t done_seq = 0;
     uint64_t *pipe_dbg = nullptr;                 // MI355X_DEBUG: per-workgroup progress words
     // nonblocking collectives: one progress thread per communicator runs the posted calls in
     // order on its own stream; blocking calls first wait until nothing is pending

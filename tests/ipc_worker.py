@@ -433,6 +433,62 @@ def _fd_report(rank):
     print(f"rank {rank} open fds {n}, RLIMIT_NOFILE {resource.getrlimit(resource.RLIMIT_NOFILE)}", flush=True)
 
 
+def concurrent_comms(key, rank, size, dev):
+    """4 communicators over the same ranks, each driven by its own thread and stream, running 1 GiB
+    fp32 allreduces at the same time with the pipelined flow on: the per-GPU admission token lets
+    one communicator's persistent grids onto a GPU at a time and sends the others down the
+    two-phase flow, so nothing waits on a grid that cannot be resident.  Every result exact, no
+    timeout (concurrent communicators)."""
+    import threading
+    import torch
+    torch.cuda.set_device(dev)
+    pkg = load_pkg()
+    ncomm, n, iters = 4, (1 << 30) // 4, 3
+    comms = [pkg.Comm.create(f"{key}_c{i}", rank, size, dev) for i in range(ncomm)]
+    for c in comms:
+        c.set("PIPE", 1)
+        c.set("TIMEOUT_S", 60)
+    xs = [torch.empty(n, device="cuda") for _ in range(ncomm)]
+    ys = [torch.empty(n, device="cuda") for _ in range(ncomm)]
+    errs, bad = [], []
+    start = threading.Barrier(ncomm)
+
+    def run(i):
+        try:
+            torch.cuda.set_device(dev)
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                for it in range(iters):
+                    xs[i].fill_(float(rank + 1 + 10 * i + 100 * it))
+                    ys[i].fill_(float("nan"))
+                    if it == 0:
+                        st.synchronize()
+                        start.wait()   # every thread's first call at the same moment
+                    comms[i].allreduce(xs[i].data_ptr(), ys[i].data_ptr(), n, pkg.T["FLOAT"], pkg.OP["SUM"],
+                                       stream=st.cuda_stream)
+                    want = size * (size + 1) / 2 + size * (10 * i + 100 * it)
+                    if not bool(torch.all(ys[i] == want).item()):
+                        bad.append((i, it))
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(ncomm)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(240)
+    assert not any(t.is_alive() for t in ts), "a communicator's allreduce never returned"
+    assert not errs, errs
+    assert not bad, f"wrong results {bad}"
+    refused = sum(c.get("PIPE_REFUSED") for c in comms)
+    print(f"rank {rank} concurrent: {ncomm} communicators x {iters} calls exact; {refused} calls fell back "
+          "to two phases", flush=True)
+    for c in comms:
+        c.barrier()
+        c.destroy()
+    print(f"rank {rank} concurrent OK", flush=True)
+
+
 def main():
     try:
         _main()
@@ -443,6 +499,8 @@ def main():
 
 def _main():
     key, rank, size, dev = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+    if len(sys.argv) > 5 and sys.argv[5] == "concurrent":
+        return concurrent_comms(key, rank, size, dev)
     import faulthandler
     faulthandler.dump_traceback_later(150, exit=True)  # a rank stuck in a HIP call names its line
     import torch

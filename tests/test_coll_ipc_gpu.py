@@ -40,3 +40,24 @@ def test_ipc_ranks(gpu, size):
             + (("pipe slots OK",) if size == 3 else ())
         for stage in stages:
             assert f"rank {r} {stage}" in outs[r], f"rank {r} did not report '{stage}':\n{outs[r][-3000:]}"
+
+
+def test_concurrent_communicators(gpu):
+    """4 communicators over the same 2 ranks, 4 threads each, concurrent 1 GiB pipelined-flow
+    allreduces: exact, no timeout (per-GPU admission of the persistent grid, coll_comm.cpp)"""
+    key = "t" + uuid.uuid4().hex[:12]
+    ndev = gpu.cuda.device_count()
+    env = dict(os.environ, MI355X_TIMEOUT_S="60")
+    procs = [subprocess.Popen([sys.executable, str(HERE / "ipc_worker.py"), key, str(r), "2", str(r % ndev), "concurrent"],
+                              env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=280)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, _ = p.communicate()
+        outs.append(out)
+    for r, p in enumerate(procs):
+        assert p.returncode == 0 and f"rank {r} concurrent OK" in outs[r], f"rank {r}:\n{outs[r][-3000:]}"
+    print(outs[0].strip().splitlines()[-2])

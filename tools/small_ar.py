@@ -20,7 +20,7 @@ sys.path.insert(0, str(pathlib.Path(__file__).resolve().parents[1]))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--sizes", default="8,65536,1048576")
+    ap.add_argument("--sizes", default="8,1024,65536,1048576")
     ap.add_argument("--reps", type=int, default=500)
     ap.add_argument("--sched", type=int, default=-1, help="hipSetDeviceFlags schedule (1 spin, 2 yield, 4 blocking)")
     args = ap.parse_args()
@@ -57,6 +57,18 @@ def main():
             if rank == 0:
                 print(json.dumps({"bytes": nbytes, "us_per_call": round(dt * 1e6, 2), "alg": comm.last_algorithm(),
                                   "n": world, "exact": ok}), flush=True)
+        # the buffer-kind vote coll/mi355x adds to every component collective (mi355x_comm_vote):
+        # a device-buffer rank only publishes; a host-buffer rank waits for every vote
+        for kind, dev in (("vote_device_us", True), ("vote_host_us", False)):
+            for _ in range(20):
+                comm.vote(dev)
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.reps):
+                comm.vote(dev)
+            dt = (time.perf_counter() - t0) / args.reps
+            if rank == 0:
+                print(json.dumps({kind: round(dt * 1e6, 3), "n": world}), flush=True)
     finally:
         comm.destroy()
         dist.destroy_process_group()
