@@ -143,12 +143,19 @@ static int reducible_type(const struct ompi_datatype_t *dt)
     return ompi_op_ddt_map[dt->id];
 }
 
+/* counts are size_t here: a block count times the communicator size (allgather's unpack of n
+ * blocks) may exceed INT_MAX; negative int counts are rejected by the callers */
+static int contiguous_bytes_n(const struct ompi_datatype_t *dt, size_t count, size_t *bytes)
+{
+    if (!(dt->super.flags & OPAL_DATATYPE_FLAG_NO_GAPS) || dt->super.true_lb != 0) return 0;
+    *bytes = count * dt->super.size;
+    return 1;
+}
+
 static int contiguous_bytes(const struct ompi_datatype_t *dt, int count, size_t *bytes)
 {
     if (count < 0) return 0;
-    if (!(dt->super.flags & OPAL_DATATYPE_FLAG_NO_GAPS) || dt->super.true_lb != 0) return 0;
-    *bytes = (size_t)count * dt->super.size;
-    return 1;
+    return contiguous_bytes_n(dt, (size_t)count, bytes);
 }
 
 /* ------------------------------------------------------------------ derived datatypes
@@ -224,16 +231,16 @@ static void *scratch_slot(struct mca_coll_mi355x_module_t *m, int slot, size_t b
 static void *scratch(struct mca_coll_mi355x_module_t *m, size_t bytes) { return scratch_slot(m, 0, bytes); }
 
 /* one side of a convertor move: (buf, count, dt) <-> packed bytes at p */
-static int stage(struct mca_coll_mi355x_module_t *m, int pack, void *buf, int count, const struct ompi_datatype_t *dt,
+static int stage(struct mca_coll_mi355x_module_t *m, int pack, void *buf, size_t count, const struct ompi_datatype_t *dt,
                  void *p, size_t bytes)
 {
     size_t cb;
-    if (contiguous_bytes(dt, count, &cb))
+    if (contiguous_bytes_n(dt, count, &cb))
         return pack ? mi355x_memcpy_async(p, buf, bytes, NULL) : mi355x_memcpy_async(buf, p, bytes, NULL);
     mi355x_ddt_t *d = ddt_of(m, dt);
     if (!d) return MI355X_ERR_UNSUPPORTED;
-    return pack ? mi355x_pack(d, (size_t)count, buf, 0, p, bytes, NULL, NULL)
-                : mi355x_unpack(d, (size_t)count, buf, 0, p, bytes, NULL, NULL);
+    return pack ? mi355x_pack(d, count, buf, 0, p, bytes, NULL, NULL)
+                : mi355x_unpack(d, count, buf, 0, p, bytes, NULL, NULL);
 }
 
 static int map_rc(int rc)
@@ -446,7 +453,7 @@ int mca_coll_mi355x_allgather(void *sbuf, int scount, struct ompi_datatype_t *sd
     int rc = inplace ? stage(m, 1, (char *)rbuf + (ptrdiff_t)me * rcount * rext, rcount, rdtype, st + blk * me, blk)
                      : stage(m, 1, sbuf, scount, sdtype, st + blk * me, blk);
     if (rc == MI355X_SUCCESS) rc = mi355x_allgather(m->engine, NULL, st, blk, NULL);
-    if (rc == MI355X_SUCCESS) rc = stage(m, 0, rbuf, rcount * n, rdtype, st, blk * (size_t)n);
+    if (rc == MI355X_SUCCESS) rc = stage(m, 0, rbuf, (size_t)rcount * (size_t)n, rdtype, st, blk * (size_t)n);
     if (rc == MI355X_SUCCESS) rc = mi355x_stream_sync(NULL);
     return map_rc(rc);
 }
@@ -755,7 +762,7 @@ typedef struct mi355x_nbreq_t {
     void *stage;
     size_t stage_bytes;
     void *ubuf;
-    int ucount;
+    size_t ucount;
     mi355x_ddt_t *ud;
     mi355x_ddt_t *pd;              /* layout of the initiation-time pack (kept until completion) */
     /* persistent point-to-point (pml_isend_init / pml_irecv_init): 1 send, 2 receive, 0 none; the
@@ -834,7 +841,7 @@ static int nb_finish_stage(mi355x_nbreq_t *r, int rc)
 {
     if (!r->stage) return rc;
     if (rc == MI355X_SUCCESS && r->ubuf) {
-        rc = r->ud ? mi355x_unpack(r->ud, (size_t)r->ucount, r->ubuf, 0, r->stage, r->stage_bytes, NULL, NULL)
+        rc = r->ud ? mi355x_unpack(r->ud, r->ucount, r->ubuf, 0, r->stage, r->stage_bytes, NULL, NULL)
                    : mi355x_memcpy_async(r->ubuf, r->stage, r->stage_bytes, NULL);
         if (rc == MI355X_SUCCESS) rc = mi355x_stream_sync(NULL);
     } else {
@@ -902,7 +909,7 @@ struct nb_stage {
     void *stage;
     size_t bytes;
     void *ubuf;       /* NULL: nothing to unpack on this rank */
-    int ucount;
+    size_t ucount;
     mi355x_ddt_t *ud; /* owned by the request; NULL with ubuf set: a plain copy */
     mi355x_ddt_t *pd; /* layout of the initiation-time pack, owned by the request */
 };
@@ -1026,11 +1033,11 @@ int mca_coll_mi355x_ireduce_scatter_block(void *sbuf, void *rbuf, int rcount, st
 
 /* the (count, dt) side of a staged nonblocking move: pack it into `p` now (local work), or set up
  * the completion-time unpack into `st` (the request then owns a private layout of dt) */
-static int nb_stage_side(int pack, void *buf, int count, const struct ompi_datatype_t *dt, void *p, size_t bytes,
+static int nb_stage_side(int pack, void *buf, size_t count, const struct ompi_datatype_t *dt, void *p, size_t bytes,
                          struct nb_stage *st)
 {
     size_t cb;
-    if (contiguous_bytes(dt, count, &cb)) {
+    if (contiguous_bytes_n(dt, count, &cb)) {
         if (pack) return mi355x_memcpy_async(p, buf, bytes, NULL);
         st->ubuf = buf;
         return MI355X_SUCCESS;
@@ -1039,7 +1046,7 @@ static int nb_stage_side(int pack, void *buf, int count, const struct ompi_datat
     if (!d) return MI355X_ERR_UNSUPPORTED;
     if (pack) {
         st->pd = d;  /* the pack kernel reads its run tables until it finishes: released at completion */
-        return mi355x_pack(d, (size_t)count, buf, 0, p, bytes, NULL, NULL);
+        return mi355x_pack(d, count, buf, 0, p, bytes, NULL, NULL);
     }
     st->ubuf = buf;
     st->ucount = count;
@@ -1076,7 +1083,7 @@ int mca_coll_mi355x_iallgather(void *sbuf, int scount, struct ompi_datatype_t *s
     int rc = inplace ? nb_stage_side(1, (char *)rbuf + (ptrdiff_t)me * rcount * rext, rcount, rdtype,
                                      (char *)st.stage + blk * me, blk, &st)
                      : nb_stage_side(1, sbuf, scount, sdtype, (char *)st.stage + blk * me, blk, &st);
-    if (rc == MI355X_SUCCESS) rc = nb_stage_side(0, rbuf, rcount * n, rdtype, st.stage, st.bytes, &st);
+    if (rc == MI355X_SUCCESS) rc = nb_stage_side(0, rbuf, (size_t)rcount * (size_t)n, rdtype, st.stage, st.bytes, &st);
     if (rc == MI355X_SUCCESS) rc = mi355x_iallgather(m->engine, NULL, st.stage, blk, NULL, &eng);
     if (rc != MI355X_SUCCESS) {
         if (rc == MI355X_ERR_UNSUPPORTED)

@@ -215,6 +215,7 @@ static void fd_sock_addr(const mi355x_comm *c, int rank, sockaddr_un *a, socklen
 {
     uint64_t h = 1469598103934665603ull;
     for (char ch : c->shm_name) h = (h ^ (unsigned char)ch) * 1099511628211ull;
+    for (int b = 0; b < 8; ++b) h = (h ^ ((c->ctrl->secret >> (8 * b)) & 0xff)) * 1099511628211ull;
     std::memset(a, 0, sizeof(*a));
     a->sun_family = AF_UNIX;
     // abstract namespace: sun_path[0] = 0, the name is the bytes that follow
@@ -706,7 +707,7 @@ int finish(mi355x_comm *c, hipStream_t s)
 static int setup_done_words(mi355x_comm *c)
 {
     const char *env = getenv("MI355X_DONE_WORDS");
-    bool ok = !(env && atoi(env) == 0) && c->size > 1 && !c->loopback;
+    bool ok = env && atoi(env) != 0 && c->size > 1 && !c->loopback;
     if (ok) {
         ok = hipHostRegister(c->ctrl, ctrl_bytes(c->size), hipHostRegisterMapped) == hipSuccess;
         if (ok) {
@@ -1406,15 +1407,23 @@ static bool reduce_program(const mi355x_comm *c, size_t count, size_t esz, int r
 // program of the non-ring allreduce algorithms: recursive doubling, or reduce to 0 + bcast
 // (nonoverlapping: comm->c_coll.coll_reduce, coll_tuned_allreduce.c:67-100; linear: the linear
 // reduce, :897-929)
-static bool allreduce_tree_program(const mi355x_comm *c, int alg, size_t count, size_t esz, Program *pr)
+static bool allreduce_tree_program(mi355x_comm *c, int alg, size_t count, size_t esz, Program *pr)
 {
-    if (alg == AR_RECDBL) {
+    if (alg == AR_RECDBL || alg == AR_LINEAR) {
+        // these depend on the communicator size only: compiled once (the symbolic re-execution of
+        // the schedule costs about a microsecond, a visible share of a small allreduce)
+        std::lock_guard<std::mutex> g(c->prog_mtx);
+        auto it = c->prog_cache.find(alg);
+        if (it != c->prog_cache.end()) {
+            *pr = it->second;
+            return true;
+        }
         ExprPool ep;
-        return compile_expr(ep, expr_allreduce_recursive_doubling(ep, c->size), c->size, pr);
-    }
-    if (alg == AR_LINEAR) {
-        ExprPool ep;
-        return compile_expr(ep, expr_reduce(ep, RED_LINEAR, c->size, 0), c->size, pr);
+        const bool ok = compile_expr(ep, alg == AR_RECDBL ? expr_allreduce_recursive_doubling(ep, c->size)
+                                                          : expr_reduce(ep, RED_LINEAR, c->size, 0),
+                                     c->size, pr);
+        if (ok) c->prog_cache.emplace(alg, *pr);
+        return ok;
     }
     int ra;
     return reduce_program(c, count, esz, 0, pr, &ra);
@@ -1568,6 +1577,12 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     if (rank == 0) {
         std::memset(m, 0, bytes);
         c->ctrl->size = (uint32_t)size;
+        uint64_t secret = 0;
+        FILE *ur = fopen("/dev/urandom", "rb");
+        if (!ur || fread(&secret, sizeof(secret), 1, ur) != 1)
+            secret = (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() ^ ((uint64_t)getpid() << 32);
+        if (ur) fclose(ur);
+        c->ctrl->secret = secret;
         std::atomic_thread_fence(std::memory_order_release);
         __atomic_store_n(&c->ctrl->magic, kMagic, __ATOMIC_RELEASE);
     } else {
@@ -1607,6 +1622,7 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     // behind at n = 2 in the one-GPU rehearsal (profiles/r02_bench_n{2,4,8}_*); MI355X_PIPE=0/1 decides
     c->pipe_on = env_double("MI355X_PIPE", size >= 4 ? 1.0 : 0.0) != 0.0;
     c->one_phase_max = (size_t)std::max(0.0, env_double("MI355X_ONE_PHASE_MAX_BYTES", (double)c->one_phase_max));
+    c->lat_on = env_double("MI355X_LAT_PROFILE", 0.0) != 0.0;
     if (rc == MI355X_SUCCESS && size > 1) rc = setup_done_words(c);
     if (rc == MI355X_SUCCESS && size > 1) rc = ll_selftest(c);
     if (rc) {
@@ -1668,6 +1684,10 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
     if (c->ll_base) (void)hipFree(c->ll_base);
     if (c->ll_ctr) (void)hipFree(c->ll_ctr);
     if (c->ll_err) (void)hipHostFree(c->ll_err);
+    if (c->lat_on && c->lat_n)
+        fprintf(stderr, "[mi355x r%d] small allreduce steps over %llu calls (us): input sync %.2f, exchange %.2f, "
+                "launch %.2f, finish %.2f\n", c->rank, (unsigned long long)c->lat_n, c->lat_acc[0] / c->lat_n,
+                c->lat_acc[1] / c->lat_n, c->lat_acc[2] / c->lat_n, c->lat_acc[3] / c->lat_n);
     if (c->ctrl_registered) (void)hipHostUnregister(c->ctrl);
     if (c->loopback) {
         std::lock_guard<std::mutex> g(c->loop->mtx);
@@ -1951,12 +1971,27 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
     // admission (above): try my GPU's token, publish the outcome with the exchange
     const bool held = pipe && pipe_token_acquire(c);
     if (pipe) c->ctrl->slot[c->rank].pipe_adm.store(((c->seq + 1) << 1) | (held ? 1u : 0u), std::memory_order_release);
+    using lclk = std::chrono::steady_clock;
+    lclk::time_point lt[4];
+    if (c->lat_on) lt[0] = lclk::now();
     MI_HIP(hipStreamSynchronize(s));  // every rank's input is complete before it is published
+    if (c->lat_on) lt[1] = lclk::now();
     const void *mine[2] = {in, rbuf};
     const uint64_t sig[4] = {1, count, (uint64_t)type, (uint64_t)op};
     std::vector<std::vector<void *>> P;
     bool staged = false;
     rc = exchange(c, 2, mine, sig, P, &staged);
+    if (c->lat_on) lt[2] = lclk::now();
+    auto lat_done = [&](int rc2) {  // the one-launch paths: launch done at lt[3], then finish
+        if (!c->lat_on || rc2) return rc2;
+        lt[3] = lclk::now();
+        rc2 = finish(c, s);
+        const lclk::time_point e = lclk::now();
+        for (int i = 0; i < 3; ++i) c->lat_acc[i] += std::chrono::duration<double, std::micro>(lt[i + 1] - lt[i]).count();
+        c->lat_acc[3] += std::chrono::duration<double, std::micro>(e - lt[3]).count();
+        c->lat_n++;
+        return rc2;
+    };
     if (rc) {
         if (held) pipe_token_release(c);
         return rc;
@@ -1990,6 +2025,7 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
             std::vector<void *> dst(1, rbuf);
             rc = run_program(op, type, pr, P[0], dst, 0, count, s);
             if (rc) return rc;
+            if (c->lat_on) return lat_done(rc);
             return finish(c, s);
         }
     }
@@ -2011,6 +2047,7 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
         ra.split = (uint32_t)(count % (size_t)c->size);
         rc = launch_ring_all_slot(op, type, ra, s);
         if (rc) return rc;
+        if (c->lat_on) return lat_done(rc);
         return finish(c, s);
     }
     // owner-computes: rank r evaluates ring block r (the reference's block partition, so the

@@ -82,6 +82,10 @@ struct Ctrl {
     uint64_t magic;
     uint32_t size;
     uint32_t pad0;
+    // random bits rank 0 draws at creation: part of the fd-passing sockets' names, so only a
+    // process that can read this 0600 segment (the job's user) can compute them -- the segment's
+    // name alone (visible in /dev/shm) does not give them away
+    uint64_t secret;
     alignas(64) std::atomic<uint32_t> attached;
     alignas(64) std::atomic<uint64_t> bar_count;
     alignas(64) std::atomic<uint64_t> bar_gen;
@@ -263,6 +267,13 @@ struct mi355x_comm {
     uint64_t pipe_refused = 0;                    // calls that fell back because a token was taken
     // finish() by device-written completion words (see RankSlot::done): the control segment
     // registered with HIP (hipHostRegister) and its device address; 0 = stream sync + barrier
+    // MI355X_LAT_PROFILE=1: host time of the small-message allreduce's steps (entry -> input sync
+    // -> exchange -> launch -> finish), averaged and printed at destroy
+    std::mutex prog_mtx;                          // compiled size-only programs (recursive doubling,
+    std::map<int, mi355x::Program> prog_cache;    // linear), keyed by the coll/tuned algorithm id
+    bool lat_on = false;
+    double lat_acc[4] = {0, 0, 0, 0};
+    uint64_t lat_n = 0;
     char *ctrl_dev = nullptr;
     bool ctrl_registered = false;
     uint64_t done_seq = 0;

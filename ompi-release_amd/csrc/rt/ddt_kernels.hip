@@ -23,6 +23,10 @@
 namespace mi355x {
 
 typedef unsigned int u32x4d __attribute__((ext_vector_type(4)));
+// the same 16 bytes at an address only 4-B aligned (the memory side of k_ddt_units_wide): the
+// type's alignment says so, so the compiler may not assume 16 (the dwordx4 access is legal on any
+// 4-B boundary)
+typedef unsigned int u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 struct Where {
     int64_t mem;     // byte offset in memory (relative to base)
@@ -571,7 +575,8 @@ __global__ __launch_bounds__(256) void k_ddt_units_wide(UnitArgs a, CsumSink csu
             char *m0 = a.mem + (int64_t)k * a.extent + (int64_t)j * a.stride + sdisp[r] + (int64_t)o * W;
             if (o + UPS <= rl) {
                 mp[u] = m0;
-                v[u] = *reinterpret_cast<const u32x4d *>(PACK ? m0 : a.packed + (size_t)i * 16);
+                v[u] = PACK ? *reinterpret_cast<const u32x4a4 *>(m0)
+                            : *reinterpret_cast<const u32x4d *>(a.packed + (size_t)i * 16);
                 continue;
             }
             // the slot crosses a run boundary: unit by unit
@@ -601,7 +606,7 @@ __global__ __launch_bounds__(256) void k_ddt_units_wide(UnitArgs a, CsumSink csu
             if (!live[u]) continue;
             const uint32_t i = base + (uint32_t)u * tpb;
             if (PACK) *reinterpret_cast<u32x4d *>(a.packed + (size_t)i * 16) = v[u];
-            else if (mp[u]) *reinterpret_cast<u32x4d *>(mp[u]) = v[u];
+            else if (mp[u]) *reinterpret_cast<u32x4a4 *>(mp[u]) = v[u];
             if constexpr (CSUM) acc += slot_csum<16>(v[u], 0);
         }
     }

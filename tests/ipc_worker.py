@@ -149,7 +149,7 @@ def staged(pkg, comm, rank, size, torch, key):
     """allocations too large for hipIpc* (forced here: every allocation; for real: >= 2 GiB, which
     hipIpcOpenMemHandle cannot map on this platform) through real IPC, twice: on a communicator
     with the dmabuf path disabled (staged flow, 1 MiB staging) and on the main one (dmabuf fds
-    fetched with pidfd_getfd)"""
+    passed with SCM_RIGHTS over the communicator's Unix datagram sockets)"""
     import os
     os.environ["MI355X_DMABUF"] = "0"
     c2 = pkg.Comm.create(key + "_st", rank, size, torch.cuda.current_device())
@@ -489,6 +489,41 @@ def concurrent_comms(key, rank, size, dev):
     print(f"rank {rank} concurrent OK", flush=True)
 
 
+def done_words(key, rank, size, dev):
+    """MI355X_DONE_WORDS=1 (finish points by command-processor-written completion words, off by
+    default: slower back to back on this platform, profiles/r03_small_latency.jsonl): every flow that
+    ends in a finish point stays exact -- one-phase and two-phase allreduce, reduce_scatter_block,
+    allgather, bcast"""
+    import os
+    import torch
+    os.environ["MI355X_DONE_WORDS"] = "1"
+    torch.cuda.set_device(dev)
+    pkg = load_pkg()
+    comm = pkg.Comm.create(key + "_dw", rank, size, dev)
+    comm.set("PIPE", 0)
+    f32, SUM = pkg.T["FLOAT"], pkg.OP["SUM"]
+    for it, n in enumerate((2, 16384, 262144, 4_000_000)):
+        x = torch.full((n * size,), float(rank + 1 + it), device="cuda")
+        y = torch.empty_like(x)
+        torch.cuda.synchronize()
+        comm.allreduce(x.data_ptr(), y.data_ptr(), n * size, f32, SUM)
+        want = sum(r + 1 + it for r in range(size))
+        assert bool(torch.all(y == want).item()), ("done-words allreduce", n)
+        r = torch.empty(n, device="cuda")
+        comm.reduce_scatter_block(x.data_ptr(), r.data_ptr(), n, f32, SUM)
+        assert bool(torch.all(r == want).item()), ("done-words rsb", n)
+        g = torch.empty(n * size, device="cuda")
+        comm.allgather(r.data_ptr(), g.data_ptr(), n * 4)
+        assert bool(torch.all(g == want).item()), ("done-words allgather", n)
+        b = torch.full((n,), float(rank), device="cuda")
+        torch.cuda.synchronize()
+        comm.bcast(b.data_ptr(), n * 4, size - 1)
+        assert bool(torch.all(b == size - 1).item()), ("done-words bcast", n)
+    comm.barrier()
+    comm.destroy()
+    print(f"rank {rank} done_words OK", flush=True)
+
+
 def main():
     try:
         _main()
@@ -501,6 +536,8 @@ def _main():
     key, rank, size, dev = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
     if len(sys.argv) > 5 and sys.argv[5] == "concurrent":
         return concurrent_comms(key, rank, size, dev)
+    if len(sys.argv) > 5 and sys.argv[5] == "done_words":
+        return done_words(key, rank, size, dev)
     import faulthandler
     faulthandler.dump_traceback_later(150, exit=True)  # a rank stuck in a HIP call names its line
     import torch

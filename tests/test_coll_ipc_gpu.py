@@ -42,6 +42,31 @@ def test_ipc_ranks(gpu, size):
             assert f"rank {r} {stage}" in outs[r], f"rank {r} did not report '{stage}':\n{outs[r][-3000:]}"
 
 
+def _run_mode(gpu, mode, size=2, timeout=280):
+    key = "t" + uuid.uuid4().hex[:12]
+    ndev = gpu.cuda.device_count()
+    env = dict(os.environ, MI355X_TIMEOUT_S="60")
+    procs = [subprocess.Popen([sys.executable, str(HERE / "ipc_worker.py"), key, str(r), str(size), str(r % ndev), mode],
+                              env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(size)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, _ = p.communicate()
+        outs.append(out)
+    for r, p in enumerate(procs):
+        assert p.returncode == 0 and f"rank {r} {mode} OK" in outs[r], f"rank {r}:\n{outs[r][-3000:]}"
+    return outs
+
+
+@pytest.mark.parametrize("size", [2, 3])
+def test_done_words(gpu, size):
+    """finish points by device-written completion words (MI355X_DONE_WORDS=1) stay exact"""
+    _run_mode(gpu, "done_words", size)
+
+
 def test_concurrent_communicators(gpu):
     """4 communicators over the same 2 ranks, 4 threads each, concurrent 1 GiB pipelined-flow
     allreduces: exact, no timeout (per-GPU admission of the persistent grid, coll_comm.cpp)"""

@@ -1,0 +1,77 @@
+/* small_ar_c.c -- small-message MPI_Allreduce latency through the engine's C ABI, no Python in the
+ * loop: N processes forked before any HIP call (all on device 0: the one-GPU rehearsal), each times
+ * `reps` calls per size, plus mi355x_comm_barrier alone.  Rank 0 prints one JSON line per row.
+ * usage: small_ar_c <nranks> <reps>
+ * build: gcc -O2 -o tools/build/small_ar_c tools/small_ar_c.c -Iinclude -Lompi-release_amd/lib -lmi355x_rt
+ *        -Wl,-rpath,'$ORIGIN/../../ompi-release_amd/lib' */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/wait.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "mi355x_rt.h"
+
+static double now_us(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e6 + t.tv_nsec * 1e-3;
+}
+
+static int run(int rank, int n, int reps, const char *key)
+{
+    mi355x_comm_t *c = NULL;
+    if (mi355x_set_device(0) || mi355x_comm_create(key, rank, n, 0, &c)) {
+        fprintf(stderr, "rank %d: %s\n", rank, mi355x_last_error());
+        return 1;
+    }
+    const size_t sizes[] = {8, 1024, 65536, 1 << 20};
+    void *s = NULL, *r = NULL;
+    mi355x_malloc(&s, 1 << 20);
+    mi355x_malloc(&r, 1 << 20);
+    mi355x_memset_async(s, 0, 1 << 20, NULL);
+    mi355x_device_sync();
+    for (int k = 0; k < 4; ++k) {
+        const size_t cnt = sizes[k] / 4;
+        for (int i = 0; i < 50; ++i) mi355x_allreduce(c, s, r, cnt, 14, 3, NULL);
+        mi355x_comm_barrier(c);
+        const double t0 = now_us();
+        for (int i = 0; i < reps; ++i)
+            if (mi355x_allreduce(c, s, r, cnt, 14, 3, NULL)) {
+                fprintf(stderr, "rank %d: %s\n", rank, mi355x_last_error());
+                return 1;
+            }
+        const double us = (now_us() - t0) / reps;
+        if (rank == 0)
+            printf("{\"bytes\": %zu, \"us_per_call\": %.2f, \"alg\": %d, \"n\": %d, \"caller\": \"C\"}\n", sizes[k], us,
+                   mi355x_comm_last_algorithm(c), n);
+    }
+    mi355x_comm_barrier(c);
+    double t0 = now_us();
+    for (int i = 0; i < reps; ++i) mi355x_comm_barrier(c);
+    if (rank == 0) printf("{\"barrier_us\": %.3f, \"n\": %d}\n", (now_us() - t0) / reps, n);
+    fflush(stdout);
+    mi355x_free(s);
+    mi355x_free(r);
+    mi355x_comm_destroy(c);
+    return 0;
+}
+
+int main(int argc, char **argv)
+{
+    const int n = argc > 1 ? atoi(argv[1]) : 2, reps = argc > 2 ? atoi(argv[2]) : 2000;
+    char key[64];
+    snprintf(key, sizeof(key), "lat_%d", (int)getpid());
+    for (int r = 1; r < n; ++r)
+        if (fork() == 0) _exit(run(r, n, reps, key));
+    int rc = run(0, n, reps, key);
+    for (int r = 1; r < n; ++r) {
+        int st = 0;
+        wait(&st);
+        if (!WIFEXITED(st) || WEXITSTATUS(st)) rc = 1;
+    }
+    return rc;
+}
