@@ -2,10 +2,13 @@
 // unpack: how fast can ANY kernel scatter a packed stream into a layout whose
 // runs leave gaps that must stay untouched?
 //
-// Two layouts, 256 MiB packed each, timed with HIP events on one MI355X (algorithmic bytes =
+// Three layouts, 256 MiB packed each, timed with HIP events on one MI355X (algorithmic bytes =
 // 2 x packed, as the convertor legs count them):
 //   F7  MPI_Type_indexed 7 runs of FLOAT {1,3,2,7,1,1,4} at {0,2,9,13,25,27,40} (19 of 44 floats,
-//       176-B extent; tools/bench_legs.py leg_ddt_runs)
+//       176-B extent; tools/bench_legs.py leg_ddt_runs) -- unpack and pack
+//   TRI upper triangle of a 256 x 256 double matrix (256 runs of 8..2048 B per instance, the
+//       long-run case) -- unpack and pack; specialised form: one wave per row moving 16-B ALIGNED
+//       memory slots (odd rows start mid-slot), 8-B head / tail
 //   COL vector(2^25, 1, 2, DOUBLE): a column of doubles, 8-B runs at a 16-B stride
 // Kernels per layout, every one a hand-specialised form of the same scatter (compile-time run
 // tables, no run search, nothing the general engine has to do):
@@ -147,6 +150,57 @@ __global__ __launch_bounds__(256) void k_col_unit(const double *__restrict__ p, 
     }
 }
 
+// ---- F7 pack: one 4-B unit per lane (the gather mirror of k_f7_unit)
+__global__ __launch_bounds__(256) void k_f7_pack_unit(const float *__restrict__ m, float *__restrict__ p, uint64_t units)
+{
+    const uint64_t base = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t u = base + 256 * k;
+        if (u >= units) return;
+        const uint64_t inst = u / F7_UNITS;
+        const int j = (int)(u - inst * F7_UNITS);
+        __builtin_nontemporal_store(m[inst * F7_EXT + f7_off[j]], p + u);
+    }
+}
+
+// ---- TRI: upper triangle of a 256 x 256 double matrix (indexed, row i = (256 - i) doubles at
+// (257 i) doubles), the convertor's long-run case.  One wave per row; the memory side moves in
+// 16-B ALIGNED slots (row starts are 8-B aligned: odd rows begin mid-slot), the packed side in
+// 8-B aligned 16-B accesses, the row's 8-B head and tail with one 8-B access each.
+constexpr int TRI_N = 256;
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+typedef unsigned long long u64x2a8 __attribute__((ext_vector_type(2), aligned(8)));
+
+template <bool PACK>
+__global__ __launch_bounds__(256) void k_tri_rows(char *__restrict__ mem, char *__restrict__ packed, uint64_t rows)
+{
+    const uint64_t row = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const int lane = threadIdx.x & 63;
+    const uint64_t inst = row / TRI_N;
+    const int i = (int)(row - inst * TRI_N);
+    const uint64_t len = (uint64_t)(TRI_N - i) * 8;
+    const uint64_t pfx = (uint64_t)i * TRI_N * 8 - (uint64_t)i * (i - 1) / 2 * 8;   // sum_{k<i} (256-k) * 8
+    char *m = mem + inst * (uint64_t)TRI_N * TRI_N * 8 + (uint64_t)i * (TRI_N + 1) * 8;
+    char *pk = packed + inst * ((uint64_t)TRI_N * (TRI_N + 1) / 2 * 8) + pfx;
+    const uint64_t head = ((uintptr_t)m & 15) ? 8 : 0;
+    const uint64_t body = (len - head) & ~(uint64_t)15;
+    if (lane == 0 && head) {
+        if (PACK) *(uint64_t *)pk = *(const uint64_t *)m;
+        else *(uint64_t *)m = *(const uint64_t *)pk;
+    }
+    for (uint64_t o = head + (uint64_t)lane * 16; o < head + body; o += 64 * 16) {
+        if (PACK) *(u64x2a8 *)(pk + o) = *(const u64x2 *)(m + o);
+        else *(u64x2 *)(m + o) = *(const u64x2a8 *)(pk + o);
+    }
+    if (lane == 63 && head + body < len) {
+        const uint64_t o = head + body;
+        if (PACK) *(uint64_t *)(pk + o) = *(const uint64_t *)(m + o);
+        else *(uint64_t *)(m + o) = *(const uint64_t *)(pk + o);
+    }
+}
+
 static float time_ms(void (*launch)(void *), void *ctx, int reps)
 {
     hipEvent_t a, b;
@@ -251,7 +305,83 @@ int main(int argc, char **argv)
         snprintf(note, sizeof(note), "\"note\": \"writes all %zu span bytes (gaps too: not a valid unpack); "
                  "span GB/s %.1f\"", span, ((double)span + packed) / (ms * 1e-3) / 1e9);
         emit("F7", "dense (full-sector writes of the span)", alg, ms, note);
+        // pack direction: gather the span into the packed stream
+        float *p2;
+        CK(hipMalloc(&p2, packed));
+        Ctx cpk{d_eng, p, 0, 0, ddt, count, packed};
+        ms = time_ms([](void *x) {
+            Ctx *c = (Ctx *)x;
+            CKM(mi355x_pack(c->ddt, c->count, c->p, 0, c->d, c->bytes, nullptr, nullptr));
+        }, &cpk, reps);
+        emit("F7", "PACK engine mi355x_pack", alg, ms, nullptr);
+        Ctx cpu2{d_eng, p2, 0, 0, ddt, count, packed};
+        ms = time_ms([](void *x) {
+            Ctx *c = (Ctx *)x;
+            const uint64_t units = c->bytes / 4;
+            k_f7_pack_unit<<<(unsigned)((units + 1023) / 1024), 256>>>((const float *)c->p, (float *)c->d, units);
+        }, &cpu2, reps);
+        snprintf(note, sizeof(note), "\"equals_engine\": %s", same(p, p2, packed) ? "true" : "false");
+        emit("F7", "PACK unit (4-B units, constexpr table)", alg, ms, note);
+        CK(hipFree(p2));
         CK(hipFree(p));
+        CK(hipFree(d));
+        CK(hipFree(d_eng));
+        mi355x_ddt_destroy(ddt);
+    }
+    // ---------------- TRI
+    {
+        std::vector<int> bl(TRI_N), dp(TRI_N);
+        for (int i = 0; i < TRI_N; ++i) {
+            bl[i] = TRI_N - i;
+            dp[i] = i * (TRI_N + 1);
+        }
+        mi355x_ddt_t *ddt = nullptr;
+        CKM(mi355x_ddt_create_indexed(TRI_N, bl.data(), dp.data(), 8, &ddt));
+        const size_t inst_bytes = mi355x_ddt_size(ddt);   // 263168
+        const size_t count = ((size_t)256 << 20) / inst_bytes;
+        const size_t packed = count * inst_bytes, span = count * (size_t)TRI_N * TRI_N * 8;
+        char *p, *d_eng, *d, *p2;
+        CK(hipMalloc(&p, packed));
+        CK(hipMalloc(&p2, packed));
+        CK(hipMalloc(&d_eng, span));
+        CK(hipMalloc(&d, span));
+        std::vector<uint64_t> hp(packed / 8);
+        for (size_t i = 0; i < hp.size(); ++i) hp[i] = i * 0x9e3779b97f4a7c15ull;
+        CK(hipMemcpy(p, hp.data(), packed, hipMemcpyHostToDevice));
+        CK(hipMemset(d_eng, 0x5a, span));
+        CK(hipMemset(d, 0x5a, span));
+        const double alg = 2.0 * (double)packed;
+        Ctx c{p, d_eng, 0, 0, ddt, count, packed};
+        float ms = time_ms([](void *x) {
+            Ctx *c = (Ctx *)x;
+            CKM(mi355x_unpack(c->ddt, c->count, c->d, 0, c->p, c->bytes, nullptr, nullptr));
+        }, &c, reps);
+        emit("TRI", "engine mi355x_unpack", alg, ms, nullptr);
+        Ctx cr{p, d, count * TRI_N, 0, ddt, count, packed};
+        ms = time_ms([](void *x) {
+            Ctx *c = (Ctx *)x;
+            k_tri_rows<false><<<(unsigned)((c->n + 3) / 4), 256>>>((char *)c->d, (char *)c->p, c->n);
+        }, &cr, reps);
+        char note[96];
+        snprintf(note, sizeof(note), "\"equals_engine\": %s", same(d, d_eng, span) ? "true" : "false");
+        emit("TRI", "rows (wave per row, 16-B aligned memory slots)", alg, ms, note);
+        Ctx cpk{d_eng, p2, 0, 0, ddt, count, packed};
+        ms = time_ms([](void *x) {
+            Ctx *c = (Ctx *)x;
+            CKM(mi355x_pack(c->ddt, c->count, c->p, 0, c->d, c->bytes, nullptr, nullptr));
+        }, &cpk, reps);
+        snprintf(note, sizeof(note), "\"equals_input\": %s", same(p, p2, packed) ? "true" : "false");
+        emit("TRI", "PACK engine mi355x_pack", alg, ms, note);
+        CK(hipMemset(p2, 0, packed));
+        Ctx crp{p2, d_eng, count * TRI_N, 0, ddt, count, packed};
+        ms = time_ms([](void *x) {
+            Ctx *c = (Ctx *)x;
+            k_tri_rows<true><<<(unsigned)((c->n + 3) / 4), 256>>>((char *)c->d, (char *)c->p, c->n);
+        }, &crp, reps);
+        snprintf(note, sizeof(note), "\"equals_input\": %s", same(p, p2, packed) ? "true" : "false");
+        emit("TRI", "PACK rows (wave per row, 16-B aligned memory slots)", alg, ms, note);
+        CK(hipFree(p));
+        CK(hipFree(p2));
         CK(hipFree(d));
         CK(hipFree(d_eng));
         mi355x_ddt_destroy(ddt);
