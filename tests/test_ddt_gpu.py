@@ -429,3 +429,40 @@ def test_zero_count_contiguous_types_gpu(gpu, pkg):
         d.pack_host(5, src.ctypes.data + origin, 0, hp.ctypes.data, hp.size)
         assert np.array_equal(out.cpu().numpy(), hp)
         d.destroy()
+
+
+RUNS_CASES = [  # (disps, lens, nblk, stride, extent, count): long 8- / 4-B aligned runs (>= 512 B on
+    # average) with unaligned heads / tails, 16-B multiple extents
+    ([int(i * 257 * 8) for i in range(256)], [int((256 - i) * 8) for i in range(256)], 1, 0, 256 * 256 * 8, 2),  # triangle
+    ([4, 2052, 6000], [1000, 3000, 604], 1, 0, 8192, 60),          # floats, W = 4: 12-B heads and tails
+    ([8, 40, 1000], [8, 24, 9000], 1, 0, 10016, 40),               # doubles: a run inside its head; a run over 3 chunks
+    ([16, 1032], [1000, 1000], 50, 2048, 50 * 2048, 12),           # blocks: 2 runs per block, 50 blocks
+]
+
+
+@pytest.mark.parametrize("case", range(len(RUNS_CASES)))
+def test_long_run_unpack(gpu, pkg, case):
+    """whole-message unpack of long W-aligned runs (the triangle of the unpack ceiling probe, floats
+    with 12-B heads and tails, runs spanning several 4-KiB spans, two runs per block): the bytes equal
+    the host convertor's under both row modes of the unit kernel, gaps untouched"""
+    torch = gpu
+    disps, lens, nblk, stride, extent, count = RUNS_CASES[case]
+    d = pkg.Ddt.runs(disps, lens, nblk, stride, extent)
+    total = count * d.size
+    span = count * extent + 64
+    rng = np.random.default_rng(90 + case)
+    packed = rng.integers(0, 256, total, dtype=np.uint8)
+    init = rng.integers(0, 256, span, dtype=np.uint8)
+    want = init.copy()
+    d.unpack_host(count, want.ctypes.data, 0, packed.ctypes.data, total)
+    dp = _dev(torch, packed)
+    try:
+        for mode in (2, 3):
+            pkg.ddt_tune_rows(mode)
+            z = _dev(torch, init)
+            d.unpack(count, z.data_ptr(), 0, dp.data_ptr(), total)
+            torch.cuda.synchronize()
+            assert np.array_equal(z.cpu().numpy(), want), (case, mode)
+    finally:
+        pkg.ddt_tune_rows(2)
+    d.destroy()
