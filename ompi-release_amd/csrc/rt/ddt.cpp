@@ -17,6 +17,7 @@ struct mi355x_ddt {
     std::vector<int64_t> disp, len, elem, pfx;
     int64_t nblk = 1, stride = 0, extent = 0;
     uint64_t run_bits = 0;  // OR of every run's displacement and length (their common alignment)
+    int64_t max_len = 0;    // longest run
     int64_t *ddisp = nullptr, *dlen = nullptr, *dpfx = nullptr;  // device copies, made on first use
     int dev = -1;
     std::mutex mtx;
@@ -47,7 +48,11 @@ static int finalize(mi355x_ddt *d, mi355x_ddt_t **out)
     d->pfx.assign(n, 0);
     for (size_t r = 1; r < n; ++r) d->pfx[r] = d->pfx[r - 1] + d->len[r - 1];
     d->run_bits = 0;
-    for (size_t r = 0; r < n; ++r) d->run_bits |= (uint64_t)d->disp[r] | (uint64_t)d->len[r];
+    d->max_len = 0;
+    for (size_t r = 0; r < n; ++r) {
+        d->run_bits |= (uint64_t)d->disp[r] | (uint64_t)d->len[r];
+        d->max_len = std::max<int64_t>(d->max_len, d->len[r]);
+    }
     *out = d;
     return MI355X_SUCCESS;
 }
@@ -239,6 +244,7 @@ static int ddt_move(const mi355x_ddt_t *d, bool pack, size_t count, void *mem, s
     dv.blk_bytes = blk_bytes(d);
     dv.inst_bytes = inst;
     dv.run_bits = d->run_bits;
+    dv.max_len = d->max_len;
     unsigned h = 0;
     unsigned *sum = checksum ? &h : nullptr;  // the launchers wait for the kernel when asked for one
     int rc = 1;

@@ -20,6 +20,7 @@ struct DdtDev {
     int64_t nblk, stride, extent;
     int64_t blk_bytes, inst_bytes;
     uint64_t run_bits;     // OR of every run's displacement and length (their common alignment)
+    int64_t max_len;       // longest run
 };
 
 // launch shape of the row kernel: slots per lane (2, 4, 8) and the non-temporal mask

@@ -632,6 +632,81 @@ static void launch_units_w(int w, const UnitArgs &a, unsigned blocks, size_t lds
     }
 }
 
+// Unpack of long W-aligned runs (W = 8 or 4, e.g. an upper triangle of doubles): one WAVE per run
+// of one block of one instance, one-shot grid, no run search -- the wave's index is the run's
+// (instance, block, run) and its table entries are uniform loads.  The lanes store 16-B ALIGNED
+// memory slots (the unit kernel stores W bytes, its wide form unaligned 16-B vectors: both slower,
+// profiles/r03_unpack_ceiling.jsonl) and read the packed side with 16-B loads at W-aligned
+// addresses; the run's unaligned head and tail move as W-byte units.  Needs the base, extent and
+// stride 16-B aligned (a run's misalignment is then its displacement's), whole instances and runs
+// of balanced length (ddt_move checks kRunsMinBytes / kRunsMaxSkew).
+struct RunsArgs {
+    char *mem;
+    const char *packed;
+    const int64_t *disp, *len, *pfx;
+    int64_t stride, extent, blk_bytes, inst_bytes;
+    FastDiv per_inst;   // runs per instance (nblk * nruns)
+    FastDiv nruns;
+    uint32_t nwaves;    // runs in the message
+};
+
+constexpr int64_t kRunsMinBytes = 512;   // average run length the wave-per-run unpack needs
+constexpr int64_t kRunsMaxSkew = 8;      // longest run at most this many times the average
+
+template <int W>
+__global__ __launch_bounds__(256) void k_ddt_runs_unpack(RunsArgs a)
+{
+    typedef typename SlotT<W>::type S;
+    const uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= a.nwaves) return;
+    const int lane = threadIdx.x & 63;
+    const uint32_t k = fdiv(q, a.per_inst);
+    const uint32_t rem = q - k * a.per_inst.d;
+    const uint32_t j = fdiv(rem, a.nruns);
+    const uint32_t r = rem - j * a.nruns.d;
+    const int64_t len = a.len[r];
+    char *m = a.mem + (int64_t)k * a.extent + (int64_t)j * a.stride + a.disp[r];
+    const char *pk = a.packed + (int64_t)k * a.inst_bytes + (int64_t)j * a.blk_bytes + a.pfx[r];
+    int64_t h = (16 - ((uintptr_t)m & 15)) & 15;
+    if (h > len) h = len;
+    const int64_t end = h + ((len - h) & ~(int64_t)15);
+    if (lane < h / W) *reinterpret_cast<S *>(m + lane * W) = *reinterpret_cast<const S *>(pk + lane * W);
+    for (int64_t o = h + (int64_t)lane * 16; o < end; o += 64 * 16)
+        *reinterpret_cast<u32x4d *>(m + o) = *reinterpret_cast<const u32x4a4 *>(pk + o);
+    if (lane < (len - end) / W)
+        *reinterpret_cast<S *>(m + end + lane * W) = *reinterpret_cast<const S *>(pk + end + lane * W);
+}
+
+// returns 1 when the wave-per-run unpack does not apply
+static int launch_runs_unpack(const DdtDev &d, int w, void *mem, const void *packed, int64_t pos, int64_t bytes,
+                              hipStream_t s)
+{
+    if (pos != 0 || d.inst_bytes <= 0 || bytes % d.inst_bytes != 0 || d.max_len <= 0) return 1;
+    if ((((uintptr_t)mem) | (uint64_t)d.extent | (uint64_t)d.stride) & 15) return 1;
+    if (d.blk_bytes < kRunsMinBytes * d.nruns || d.max_len * d.nruns > kRunsMaxSkew * d.blk_bytes) return 1;
+    const uint64_t ninst = (uint64_t)(bytes / d.inst_bytes);
+    const uint64_t per_inst = (uint64_t)d.nblk * (uint64_t)d.nruns;
+    if (per_inst >= ((uint64_t)1 << 32) || ninst * per_inst >= ((uint64_t)1 << 32) - 4) return 1;
+    RunsArgs a;
+    a.mem = static_cast<char *>(mem);
+    a.packed = static_cast<const char *>(packed);
+    a.disp = d.disp;
+    a.len = d.len;
+    a.pfx = d.pfx;
+    a.stride = d.stride;
+    a.extent = d.extent;
+    a.blk_bytes = d.blk_bytes;
+    a.inst_bytes = d.inst_bytes;
+    a.per_inst = make_fastdiv((uint32_t)per_inst);
+    a.nruns = make_fastdiv((uint32_t)d.nruns);
+    a.nwaves = (uint32_t)(ninst * per_inst);
+    const unsigned blocks = (a.nwaves + 3) / 4;
+    if (w == 8) hipLaunchKernelGGL((k_ddt_runs_unpack<8>), dim3(blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_ddt_runs_unpack<4>), dim3(blocks), dim3(256), 0, s, a);
+    MI_HIP(hipGetLastError());
+    return MI355X_SUCCESS;
+}
+
 // returns 1 when the unit kernel does not apply
 static int launch_ddt_units(const DdtDev &d, bool pack, void *mem, void *packed, int64_t pos, int64_t bytes,
                             unsigned *csum, hipStream_t s)
@@ -664,6 +739,10 @@ static int launch_ddt_units(const DdtDev &d, bool pack, void *mem, void *packed,
     // profiles/r02_legs_ddt_wide.jsonl): triangle of doubles pack 4.70 vs 4.24 TB/s, but its unpack
     // 3.53 vs 3.73 (16-B stores at 8-B alignment) and 7-run floats pack 3.18 vs 3.30 (short runs:
     // most slots cross a run boundary)
+    if (ddt_tune().rows == 2 && !pack && !csum && (w == 8 || w == 4)) {
+        const int rrc = launch_runs_unpack(d, w, mem, packed, pos, bytes, s);
+        if (rrc != 1) return rrc;
+    }
     const uint64_t pk_bits = (uintptr_t)packed | (uint64_t)pos | (uint64_t)bytes;
     const bool wide = ddt_tune().rows == 2 && pack && (w == 8 || w == 4) && (pk_bits & 15) == 0 &&
                       (uint64_t)(d.blk_bytes / w) >= (uint64_t)kWideRunUnits * (uint64_t)d.nruns;
