@@ -45,6 +45,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <new>
 
 #include "comm_internal.hpp"
 #include "ddt_internal.hpp"
@@ -54,6 +55,39 @@ namespace mi355x {
 constexpr size_t kEagerLimit = 4096;          // btl_sm_component.c:244, btl_smcuda_component.c:183
 constexpr int32_t kEnvPacked = 1;             // the payload is a packed copy (layout unused)
 constexpr int32_t kEnvHost = 2;               // the payload is in the sender's host arena
+constexpr int32_t kEnvStream = 4;             // ... and is being copied in: a StreamHdr precedes it
+// host payloads of at least kStreamMin bytes are announced before they are copied into the arena
+// and copied in kStreamFrag fragments, the receiver copying fragment k out while the sender copies
+// k + 1 in (the sm BTL's fragment pipeline, btl_sm_sendi / mca_btl_sm_component_progress)
+constexpr size_t kStreamMin = (size_t)1 << 20;   // MI355X_P2P_STREAM_MIN overrides (A/B timing)
+constexpr size_t kStreamFrag = (size_t)256 << 10;  // smallest fragment (stream_frag)
+struct alignas(64) StreamHdr {
+    std::atomic<uint64_t> ready;   // payload bytes copied in so far
+    char pad[56];
+};
+static_assert(sizeof(StreamHdr) == 64, "StreamHdr is one cache line");
+
+// fragment of a streamed n-byte payload: n / 16 within [256 KiB, 1 MiB] (two-process one-way
+// host -> host, profiles/r03_host_p2p.jsonl: 1 MiB fragments lead at 64 MiB, 256 KiB at 1-8 MiB);
+// sender and receiver may fragment differently -- the receiver waits for `ready` to cover its own
+static size_t stream_frag(size_t n)
+{
+    static const size_t env = [] {
+        const char *e = getenv("MI355X_P2P_STREAM_FRAG");
+        return e ? std::max<size_t>((size_t)strtoull(e, nullptr, 0), 4096) : (size_t)0;
+    }();
+    if (env) return env;
+    return std::min<size_t>(std::max<size_t>((n / 16) & ~(size_t)4095, kStreamFrag), kStreamFrag * 4);
+}
+
+static size_t stream_min()
+{
+    static const size_t v = [] {
+        const char *e = getenv("MI355X_P2P_STREAM_MIN");
+        return e ? (size_t)strtoull(e, nullptr, 0) : kStreamMin;
+    }();
+    return v;
+}
 
 struct P2PMsg {   // an announced message not matched yet (ob1's unexpected queue)
     int src;
@@ -322,6 +356,53 @@ static bool try_announce(mi355x_comm *c, mi355x_request *r)
     return true;
 }
 
+// bytes [0, need) of a streamed host payload are in the sender's arena
+static int stream_wait(mi355x_comm *c, const StreamHdr *h, uint64_t need, int src)
+{
+    if (h->ready.load(std::memory_order_acquire) >= need) return MI355X_SUCCESS;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spins = 1;; ++spins) {
+        if (h->ready.load(std::memory_order_acquire) >= need) return MI355X_SUCCESS;
+        if ((spins & 0xff) == 0) {
+            sched_yield();
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s)
+                return set_error(MI355X_ERR_TIMEOUT, "rank %d: streamed message from rank %d stalled at %llu of %llu bytes",
+                                 c->rank, src, (unsigned long long)h->ready.load(), (unsigned long long)need);
+        }
+    }
+}
+
+// copy out a streamed host payload (hdr at `src`, payload after it) fragment by fragment as the
+// sender copies it in: into host memory (memcpy / host convertor window), or into device memory
+// (host-to-device copies; a layout through device staging, unpacked once at the end)
+static int read_stream(mi355x_comm *c, P2P *p, mi355x_request *r, const char *src, size_t n, bool contig, char *dst,
+                       hipStream_t s)
+{
+    const auto *h = reinterpret_cast<const StreamHdr *>(src);
+    const char *pay = src + sizeof(StreamHdr);
+    const int from = r->st_source;
+    void *stage = nullptr;
+    int rc = MI355X_SUCCESS;
+    if (!r->host && !contig && (rc = arena_alloc(p->rstage, n, &stage))) return rc;
+    const size_t frag = stream_frag(n);
+    for (size_t off = 0; off < n && !rc; off += frag) {
+        const size_t k = std::min(frag, n - off);
+        if ((rc = stream_wait(c, h, off + k, from))) break;
+        if (r->host) {
+            if (contig) std::memcpy(dst + off, pay + off, k);
+            else rc = mi355x_unpack_host(r->ddt, r->count, r->buf, off, pay + off, k);
+        } else if (hipMemcpy((contig ? dst : (char *)stage) + off, pay + off, k, hipMemcpyHostToDevice) != hipSuccess) {
+            rc = set_error(MI355X_ERR_HIP, "host-to-device copy of a %zu-byte message failed", n);
+        }
+    }
+    if (stage) {
+        if (!rc) rc = mi355x_unpack(r->ddt, r->count, r->buf, 0, stage, n, nullptr, s);
+        if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = set_error(MI355X_ERR_HIP, "unpack of a message failed");
+        arena_release(p->rstage);
+    }
+    return rc;
+}
+
 // matched receive r <- message msg: copy the bytes into place (complete now), or start the pull
 static void start_read(mi355x_comm *c, P2P *p, mi355x_request *r, const P2PMsg &msg)
 {
@@ -353,6 +434,13 @@ static void start_read(mi355x_comm *c, P2P *p, mi355x_request *r, const P2PMsg &
         // host payload (sm-BTL style): copied out synchronously, FIN at once
         const char *src = nullptr;
         if ((rc = host_src(c, p, msg.src, env->buf, &src))) return fail(rc);
+        if (env->flags & kEnvStream) {
+            rc = read_stream(c, p, r, src, n, contig, dst, s);
+            if (rc) return fail(rc);
+            fin();
+            complete_recv(r);
+            return;
+        }
         if (r->host) {
             if (contig) std::memcpy(dst, src, n);
             else rc = mi355x_unpack_host(r->ddt, r->count, r->buf, 0, src, n);
@@ -550,6 +638,68 @@ static mi355x_request *new_request(mi355x_comm *c, int kind)
     return r;
 }
 
+// announce r (queue it behind an earlier send to the same destination); the caller's request is
+// r, or -- eager -- a completed twin while the engine keeps r until the FIN
+static mi355x_request *post_send(mi355x_comm *c, P2P *p, mi355x_request *r, bool eager)
+{
+    r->msg = p->send_seq[(size_t)r->peer]++;
+    mi355x_request *user = r;
+    if (eager) {
+        r->internal = true;
+        user = new_request(c, 1);
+        user->peer = r->peer;
+        user->tag = r->tag;
+        user->bytes = r->bytes;
+        user->mode = r->mode;
+        complete(user, MI355X_SUCCESS);
+    }
+    bool earlier = false;   // an earlier send to the same destination still queued: keep order
+    for (mi355x_request *q : p->queued) earlier = earlier || q->peer == r->peer;
+    if (!earlier && try_announce(c, r)) p->sending.push_back(r);
+    else p->queued.push_back(r);
+    return user;
+}
+
+// a host payload of >= kStreamMin bytes: announced first, then copied into the arena fragment by
+// fragment behind a StreamHdr the receiver polls (the caller holds p->mtx)
+static int isend_stream(mi355x_comm *c, P2P *p, mi355x_request *r, bool eager, mi355x_request **out)
+{
+    void *slot = nullptr;
+    BufDesc desc;
+    int rc = harena_alloc(c, p, sizeof(StreamHdr) + r->bytes, &slot, &desc);
+    if (rc) {
+        delete r;
+        return rc;
+    }
+    auto *h = new (slot) StreamHdr();
+    h->ready.store(0, std::memory_order_relaxed);
+    char *pay = static_cast<char *>(slot) + sizeof(StreamHdr);
+    r->hslot = slot;
+    r->env_flags = kEnvHost | kEnvStream;
+    std::memcpy(&r->desc, &desc, sizeof(desc));
+    int64_t first = 0;
+    const bool contig = !r->ddt || ddt_contiguous(r->ddt, r->count, &first);
+    const char *ubuf = static_cast<const char *>(r->buf) + first;
+    // the payload must be complete before the receiver is told: a pack that fails is reported
+    // after the fact, so pack into the slot up front when the layout is not contiguous
+    if (!contig && (rc = mi355x_pack_host(r->ddt, r->count, r->buf, 0, pay, r->bytes))) {
+        harena_release(p);
+        delete r;
+        return rc;
+    }
+    if (!contig) h->ready.store(r->bytes, std::memory_order_release);
+    *out = post_send(c, p, r, eager);
+    if (contig) {
+        const size_t frag = stream_frag(r->bytes);
+        for (size_t off = 0; off < r->bytes; off += frag) {
+            const size_t k = std::min(frag, r->bytes - off);
+            std::memcpy(pay + off, ubuf + off, k);
+            h->ready.store(off + k, std::memory_order_release);
+        }
+    }
+    return MI355X_SUCCESS;
+}
+
 static int isend(mi355x_comm *c, const void *buf, size_t count, const mi355x_ddt_t *d, int dest, int tag, int mode,
                  void *stream, mi355x_request **out)
 {
@@ -593,6 +743,7 @@ static int isend(mi355x_comm *c, const void *buf, size_t count, const mi355x_ddt
         return bail(set_error(MI355X_ERR_HIP, "caller stream failed"));
     const bool small = bytes <= kEagerLimit && mode != MI355X_SEND_SYNCHRONOUS;
     const bool eager = small || mode == MI355X_SEND_BUFFERED;
+    if (!dev && bytes >= stream_min()) return isend_stream(c, p, r, eager, out);
     int64_t first = 0;
     const bool contig = !d || ddt_contiguous(d, count, &first);
     const char *ubuf = (const char *)buf + first;
@@ -651,22 +802,7 @@ static int isend(mi355x_comm *c, const void *buf, size_t count, const mi355x_ddt
         }
     }
     std::memcpy(&r->desc, &desc, sizeof(desc));
-    r->msg = p->send_seq[(size_t)dest]++;
-    mi355x_request *user = r;
-    if (eager) {  // the caller's request completes now; the engine keeps r until the FIN
-        r->internal = true;
-        user = new_request(c, 1);
-        user->peer = dest;
-        user->tag = tag;
-        user->bytes = bytes;
-        user->mode = mode;
-        complete(user, MI355X_SUCCESS);
-    }
-    bool earlier = false;   // an earlier send to the same destination still queued: keep order
-    for (mi355x_request *q : p->queued) earlier = earlier || q->peer == dest;
-    if (!earlier && try_announce(c, r)) p->sending.push_back(r);
-    else p->queued.push_back(r);
-    *out = user;
+    *out = post_send(c, p, r, eager);
     return MI355X_SUCCESS;
 }
 

@@ -524,6 +524,56 @@ def done_words(key, rank, size, dev):
     print(f"rank {rank} done_words OK", flush=True)
 
 
+def host_bw(key, rank, size, dev):
+    """host -> host point-to-point rate between two processes, one JSON line per (pattern, size) from
+    rank 0: `oneway` (rank 0 sends, rank 1 is already waiting in MPI_Recv; a 1-byte reply closes
+    each round) and `sendrecv` (both directions at once); MI355X_P2P_STREAM_MIN selects the copy-in
+    protocol"""
+    import json
+    import os
+    import time
+    import torch
+    torch.cuda.set_device(dev)
+    pkg = load_pkg()
+    comm = pkg.Comm.create(key, rank, size, dev)
+    peer = 1 - rank
+    ack = np.zeros(1, dtype=np.uint8)
+    for pattern in ("oneway", "sendrecv"):
+        for n in (1 << 20, 8 << 20, 64 << 20):
+            src = np.random.default_rng(rank + n).integers(0, 256, n, dtype=np.uint8)
+            dst = np.zeros(n, dtype=np.uint8)
+            reps = max(4, min(40, (512 << 20) // n))
+
+            def once():
+                if pattern == "sendrecv":
+                    comm.sendrecv(src.ctypes.data, n, peer, 9, dst.ctypes.data, n, peer, 9)
+                elif rank == 0:
+                    comm.send(src.ctypes.data, n, 1, 9)
+                    comm.recv(ack.ctypes.data, 1, 1, 10)
+                else:
+                    comm.recv(dst.ctypes.data, n, 0, 9)
+                    comm.send(ack.ctypes.data, 1, 0, 10)
+
+            for _ in range(2):
+                once()
+            comm.barrier()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                once()
+            comm.barrier()
+            dt = (time.perf_counter() - t0) / reps
+            if pattern == "sendrecv" or rank == 1:
+                assert np.array_equal(dst, np.random.default_rng(peer + n).integers(0, 256, n, dtype=np.uint8))
+            if rank == 0:
+                print(json.dumps({"leg": "host_p2p_" + pattern, "bytes": n, "us": round(dt * 1e6, 1),
+                                  "GBs_per_direction": round(n / dt / 1e9, 2),
+                                  "stream_min": os.environ.get("MI355X_P2P_STREAM_MIN", "default"),
+                                  "frag": os.environ.get("MI355X_P2P_STREAM_FRAG", "default")}), flush=True)
+    comm.barrier()
+    comm.destroy()
+    print(f"rank {rank} host_bw OK", flush=True)
+
+
 def main():
     try:
         _main()
@@ -538,6 +588,8 @@ def _main():
         return concurrent_comms(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "done_words":
         return done_words(key, rank, size, dev)
+    if len(sys.argv) > 5 and sys.argv[5] == "host_bw":
+        return host_bw(key, rank, size, dev)
     import faulthandler
     faulthandler.dump_traceback_later(150, exit=True)  # a rank stuck in a HIP call names its line
     import torch

@@ -42,10 +42,10 @@ def test_ipc_ranks(gpu, size):
             assert f"rank {r} {stage}" in outs[r], f"rank {r} did not report '{stage}':\n{outs[r][-3000:]}"
 
 
-def _run_mode(gpu, mode, size=2, timeout=280):
+def _run_mode(gpu, mode, size=2, timeout=280, extra_env=None):
     key = "t" + uuid.uuid4().hex[:12]
     ndev = gpu.cuda.device_count()
-    env = dict(os.environ, MI355X_TIMEOUT_S="60")
+    env = dict(os.environ, MI355X_TIMEOUT_S="60", **(extra_env or {}))
     procs = [subprocess.Popen([sys.executable, str(HERE / "ipc_worker.py"), key, str(r), str(size), str(r % ndev), mode],
                               env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(size)]
     outs = []
@@ -65,6 +65,21 @@ def _run_mode(gpu, mode, size=2, timeout=280):
 def test_done_words(gpu, size):
     """finish points by device-written completion words (MI355X_DONE_WORDS=1) stay exact"""
     _run_mode(gpu, "done_words", size)
+
+
+@pytest.mark.parametrize("stream_min", ["default", "off"] + [f"frag{k}" for k in
+                                                           os.environ.get("MI355X_P2P_FRAG_SWEEP", "").split(",") if k])
+def test_host_p2p_between_processes(gpu, stream_min):
+    """host -> host sendrecv between two processes through the shared-memory arenas, 1-64 MiB,
+    with the fragment pipeline (default) and with whole-message copy-in (off); exact both ways,
+    the rates printed (tools/gpu_r03_p2p.sh keeps them)"""
+    extra = {} if stream_min == "default" else {"MI355X_P2P_STREAM_MIN": str(1 << 62)}
+    if stream_min.startswith("frag"):
+        extra = {"MI355X_P2P_STREAM_FRAG": stream_min[4:]}
+    outs = _run_mode(gpu, "host_bw", 2, extra_env=extra)
+    for line in outs[0].splitlines():
+        if line.startswith("{"):
+            print("\n" + line)
 
 
 def test_concurrent_communicators(gpu):

@@ -444,6 +444,81 @@ def test_host_device_datatypes(gpu, pkg, oracle, comms, skind, rkind):
     di.destroy()
 
 
+@pytest.mark.parametrize("rkind", ["host", "dev"])
+@pytest.mark.parametrize("layout", ["contig", "vector_send", "vector_recv"])
+def test_streamed_host_payloads(gpu, pkg, comms, rkind, layout):
+    """host payloads of >= 1 MiB are announced first and copied into the sender's arena in 256-KiB
+    fragments the receiver copies out as they land (the sm BTL's fragment pipeline): contiguous,
+    a packed host layout, a host / device receive layout, and a truncating receive"""
+    torch = gpu
+    g = np.random.default_rng(41)
+    nblk = 70000                                     # 64 floats every 128: 17.9 MB packed
+    dv = pkg.Ddt.vector(nblk, 64, 128, 4)
+    packed_bytes = dv.size
+    if layout == "vector_send":
+        src = g.integers(0, 256, dv.extent, dtype=np.uint8)
+        sq_args = (1, dv)
+    else:
+        src = g.integers(0, 256, packed_bytes, dtype=np.uint8)
+        sq_args = (packed_bytes, None)
+    want_packed = np.zeros(packed_bytes, dtype=np.uint8)
+    if layout == "vector_send":
+        dv.pack_host(1, src.ctypes.data, 0, want_packed.ctypes.data, packed_bytes)
+    else:
+        want_packed[:] = src
+    if layout == "vector_recv":
+        dst0 = np.full(dv.extent, 0xAB, dtype=np.uint8)
+        want = dst0.copy()
+        dv.unpack_host(1, want.ctypes.data, 0, want_packed.ctypes.data, packed_bytes)
+        rcount, rddt = 1, dv
+    else:
+        dst0 = np.zeros(packed_bytes + 64, dtype=np.uint8)
+        want = dst0.copy()
+        want[:packed_bytes] = want_packed
+        rcount, rddt = packed_bytes + 64, None
+    rp, read, kr = _buf(torch, rkind, dst0)
+    rq = comms[1].irecv(rp, rcount, 0, 12, ddt=rddt)
+    sq = comms[0].isend(src.ctypes.data, sq_args[0], 1, 12, ddt=sq_args[1])
+    assert rq.wait() == (0, 12, 0, packed_bytes)
+    sq.wait()
+    assert np.array_equal(read(), want)
+    # truncation: the receive takes what its buffer holds, the status the whole size
+    small = np.zeros((3 << 20) + 1, dtype=np.uint8)
+    sq = comms[0].isend(src.ctypes.data, sq_args[0], 1, 13, ddt=sq_args[1])
+    with pytest.raises(pkg.MI355XError, match="truncated"):
+        comms[1].recv(small.ctypes.data, small.size, 0, 13)
+    sq.wait()
+    assert np.array_equal(small, want_packed[:small.size])
+    dv.destroy()
+
+
+def test_streamed_host_payload_overlap(gpu, pkg, comms):
+    """a receiver already waiting (its own thread) copies a 48 MiB host message out while the sender
+    still copies it in; both directions at once"""
+    torch = gpu
+    n = (48 << 20) + 5
+    data = {r: np.random.default_rng(60 + r).integers(0, 256, n, dtype=np.uint8) for r in (0, 1)}
+    out = {r: np.zeros(n, dtype=np.uint8) for r in (0, 1)}
+    errs = []
+
+    def run(r):
+        try:
+            torch.cuda.set_device(0)
+            rq = comms[r].irecv(out[r].ctypes.data, n, 1 - r, 14)
+            comms[r].send(data[r].ctypes.data, n, 1 - r, 14)
+            assert rq.wait() == (1 - r, 14, 0, n)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in (0, 1)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    assert not errs, errs
+    assert np.array_equal(out[0], data[1]) and np.array_equal(out[1], data[0])
+
+
 def _ob1_match_model(arrived, recvs):
     """ob1's matching restated (pml_ob1_recvfrag.c: posted receives in posting order, each takes the
     first message in arrival order whose source and tag match; wildcards -1).  `arrived` is the
