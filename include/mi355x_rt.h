@@ -160,9 +160,20 @@ enum mi355x_knob {
                                            inputs in one launch (reads n x S, one host barrier and
                                            stream sync fewer than the two phases); default 1 MiB,
                                            0 = always two phases */
-    MI355X_KNOB_PIPE_REFUSED = 18       /* (read-only) calls of this communicator that were to run pipelined
+    MI355X_KNOB_PIPE_REFUSED = 18,      /* (read-only) calls of this communicator that were to run pipelined
                                            but fell back to two phases because another communicator's
                                            pipelined grid held a GPU (the per-GPU admission token) */
+    MI355X_KNOB_SVC_MAX_BYTES = 19,     /* (per communicator, same value on every rank; env MI355X_SVC_MAX_BYTES
+                                           at creation) per-rank message bytes up to which allreduce /
+                                           reduce / allgather / bcast are served by the resident LL service
+                                           (coll_svc.hip: the LL protocol in a kernel that stays resident on a
+                                           private HSA queue and waits on a doorbell -- no launch per call).
+                                           One service per process and GPU, owned by the first communicator
+                                           whose ranks all find it free at creation; reads 0 (and setting it
+                                           is ignored) on every other communicator.  MI355X_SVC=0 disables it */
+    MI355X_KNOB_SVC_CALLS = 20,         /* (read-only) calls served by the resident service */
+    MI355X_KNOB_SVC_LAUNCHES = 21       /* (read-only) launches of the resident service (it leaves after
+                                           MI355X_SVC_IDLE_MS without a call and is relaunched on demand) */
 };
 int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
 /* current value of a knob (LL_MAX_BYTES reads 0 when the creation-time LL self-test failed) */

@@ -24,6 +24,7 @@
 // data flow -- the message moves through each rank's persistent staging buffer (one allocation
 // < 2 GiB, mapped once) in block-strided windows, like the segmented ring's phases.
 #include <fcntl.h>
+#include <immintrin.h>
 #include <poll.h>
 #include <sched.h>
 #include <sys/mman.h>
@@ -974,23 +975,34 @@ static int staged_bcast(mi355x_comm *c, void *buf, size_t bytes, int root, hipSt
 // Loopback communicators (threads of one process) never take it: their kernels would share the
 // process's few hardware queues and a rank's spinning kernel could sit in front of the peer
 // kernel it waits for.
+// the resident service takes every LL-protocol call up to svc_max bytes (svc_ok: created, self-
+// tested and owned on every rank -- the same decision on every rank)
+static bool svc_usable(const mi355x_comm *c, size_t bytes) { return c->svc_ok && bytes > 0 && bytes <= c->svc_max; }
+
 static bool ll_usable(const mi355x_comm *c, size_t bytes)
 {
-    if (c->loopback || c->size < 2 || c->size > kLLMaxRanks || bytes == 0 || bytes > c->ll_max) return false;
+    if (c->loopback || c->size < 2 || c->size > kLLMaxRanks || bytes == 0) return false;
+    if (svc_usable(c, bytes)) return true;
+    if (bytes > c->ll_max) return false;
     // ranks sharing a GPU: every rank's blocks spin until the others' have pushed, so all of them
     // must be resident at once -- at most one block per CU for the ranks together
     const size_t blocks = (bytes + kLLChunk - 1) / kLLChunk;
     return c->pipe_share <= 1 || blocks * (size_t)c->pipe_share <= (size_t)device_cu_count();
 }
 
+static void svc_stop(mi355x_comm *c);
+static int svc_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s);
+
 // (Re)allocate and exchange the LL region: [ack words, one per rank][2 parities x n slots of
 // ll_max payload bytes as 8-byte granules].  Collective: every rank reaches it in the same call.
-constexpr size_t kLLAckBytes = 4096;
+
 static int ensure_ll(mi355x_comm *c)
 {
     // payload bytes per slot (at least 64 KiB: the creation-time self-test runs with ll_max 0)
-    const size_t want = (std::max<size_t>(c->ll_max, (size_t)64 << 10) + kLLChunk - 1) / kLLChunk * kLLChunk;
+    const size_t want =
+        (std::max({c->ll_max, c->svc_max, (size_t)64 << 10}) + kLLChunk - 1) / kLLChunk * kLLChunk;
     if (c->ll_base && c->ll_slot >= want) return MI355X_SUCCESS;
+    svc_stop(c);  // a resident service holds the old region's addresses
     const size_t n = (size_t)c->size;
     const size_t total = kLLAckBytes + 2 * n * (want / 4) * sizeof(uint64_t);
     if (c->ll_base) (void)hipFree(c->ll_base);
@@ -1021,19 +1033,21 @@ static int ll_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s)
 {
     int rc = ensure_ll(c);
     if (rc) return rc;
-    const uint64_t seq = ++c->ll_seq;
-    const size_t par = seq & 1, n = (size_t)c->size, me = (size_t)c->rank;
+    const size_t n = (size_t)c->size;
     const uint64_t all = (1ull << n) - 1;
-    a.seq = seq;
     a.n = c->size;
     a.me = c->rank;
-    a.slot_gran = c->ll_slot / 4;
     a.push_mask &= all;
     switch (a.mode) {
     case LL_RED: a.recv_mask = (a.me == a.root) ? all : 0; break;
     case LL_BC: a.recv_mask = (a.me == a.root) ? 0 : (1ull << a.root); break;
     default: a.recv_mask = all; break;
     }
+    if (svc_usable(c, a.nbytes)) return svc_run(c, a, op, type, s);
+    const uint64_t seq = ++c->ll_seq;
+    const size_t par = seq & 1, me = (size_t)c->rank;
+    a.seq = seq;
+    a.slot_gran = c->ll_slot / 4;
     uint64_t *my = reinterpret_cast<uint64_t *>(c->ll_base);
     for (size_t q = 0; q < n; ++q) {
         uint64_t *peer = reinterpret_cast<uint64_t *>(c->ll_peer[q]);
@@ -1116,6 +1130,237 @@ static int ll_selftest(mi355x_comm *c)
         if (c->rank == 0) fprintf(stderr, "[mi355x] low-latency path self-test failed: small collectives use the host-synchronised path\n");
     }
     TRACE(c, "LL self-test: %s", all ? "ok" : "failed -> LL off");
+    return barrier(c);
+}
+
+// ----------------------------------------------------------------- resident LL service
+// (coll_svc.hip, svc_queue.cpp).  One service per process and GPU, owned by one communicator: the
+// service's kernel serves one communicator's LL region, and a rank whose service were busy with
+// another communicator's call could not take part in this one's (a cross-process circular wait
+// for MPI_THREAD_MULTIPLE programs).  Ownership is agreed at creation: every rank claims its
+// process's service for the new communicator without waiting, and the communicator uses it only if
+// every rank got it; every other communicator keeps the per-call paths.
+static std::mutex g_svc_mtx;
+static std::map<int, mi355x_comm *> g_svc_owner;  // device -> owning communicator
+
+static uint64_t *svc_done_word(mi355x_comm *c) { return c->svc_host; }
+static uint32_t *svc_err_word(mi355x_comm *c) { return reinterpret_cast<uint32_t *>(c->svc_host + 1); }
+
+// ring the doorbell: the page may be write-combined (BAR), so fence the stores out in order
+static void svc_ring(mi355x_comm *c, uint64_t v)
+{
+    _mm_sfence();
+    __atomic_store_n(&c->svc_page->door, v, __ATOMIC_RELEASE);
+    _mm_sfence();
+}
+
+static int svc_launch(mi355x_comm *c, uint64_t first)
+{
+    SvcArgs g;
+    std::memset(&g, 0, sizeof(g));
+    c->svc_page->ctr = 0;  // not resident: nothing else touches it
+    _mm_sfence();
+    g.page = c->svc_page;
+    g.done = svc_done_word(c);
+    g.err = svc_err_word(c);
+    g.my_ll = c->ll_base;
+    for (int q = 0; q < c->size; ++q) g.peer_ll[q] = c->ll_peer[q];
+    g.first = first;
+    g.slot_gran = c->ll_slot / 4;
+    g.idle_ticks = (uint64_t)(c->svc_idle_s * 1e8);  // s_memrealtime: 100 MHz
+    g.timeout_ticks = (uint64_t)(c->timeout_s * 1e8);
+    g.n = c->size;
+    g.me = c->rank;
+    g.nwg = c->svc_nwg;
+    if (svc_dispatch(c->svcq, g, c->svc_nwg)) return set_error(MI355X_ERR_HIP, "service dispatch: the previous launch is still resident");
+    c->svc_launches++;
+    return MI355X_SUCCESS;
+}
+
+// ask a resident service to leave and wait until it has (no call is in flight: calls complete
+// before the engine returns)
+static void svc_stop(mi355x_comm *c)
+{
+    if (!c->svcq || !svc_resident(c->svcq)) return;
+    svc_ring(c, kSvcQuit);
+    if (!svc_wait_exit(c->svcq, c->timeout_s + 5.0))
+        fprintf(stderr, "[mi355x r%d] resident service did not leave\n", c->rank);
+    svc_ring(c, c->ll_seq);  // back to the last call's number: the next launch waits for ll_seq + 1
+}
+
+// one LL call through the service: `a` carries the call (mode, buffers, program, masks)
+static int svc_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s)
+{
+    MI_HIP(hipStreamSynchronize(s));  // the inputs: every earlier operation on the caller's stream
+    const uint64_t seq = ++c->ll_seq;
+    SvcCall call;
+    std::memset(&call, 0, sizeof(call));
+    call.seq = seq;
+    call.src = a.src;
+    call.dst = a.dst;
+    call.nbytes = a.nbytes;
+    call.count = a.count;
+    call.early = a.early;
+    call.late = a.late;
+    call.split = a.split;
+    call.role_mask = a.role_mask;
+    call.push_mask = a.push_mask;
+    call.recv_mask = a.recv_mask;
+    call.op = op;
+    call.type = type;
+    call.mode = a.mode;
+    call.prog = a.prog;
+    call.root = a.root;
+    call.nsteps = a.nsteps;
+    call.result = a.result;
+    for (int j = 0; j < c->size; ++j) call.order[j] = a.order[j];
+    for (int k = 0; k < a.nsteps && k < kTreeSteps; ++k) call.steps[k] = a.steps[k];
+    std::memcpy(&c->svc_page->call, &call, sizeof(call));
+    svc_ring(c, seq);
+    int rc = MI355X_SUCCESS;
+    if (!svc_resident(c->svcq)) rc = svc_launch(c, seq);
+    if (rc) return rc;
+    const uint64_t *done = svc_done_word(c);
+    const uint32_t *err = svc_err_word(c);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spins = 1; __atomic_load_n(done, __ATOMIC_ACQUIRE) != seq; ++spins) {
+        _mm_pause();
+        if (spins & 255u) continue;
+        if (__atomic_load_n(err, __ATOMIC_ACQUIRE)) {
+            rc = set_error(MI355X_ERR_TIMEOUT, "rank %d: service call %llu timed out waiting for a peer", c->rank,
+                           (unsigned long long)seq);
+            break;
+        }
+        if (!svc_resident(c->svcq)) {
+            // it left idle just before the doorbell rang: start it again for this call
+            if (__atomic_load_n(done, __ATOMIC_ACQUIRE) == seq) break;
+            rc = svc_launch(c, seq);
+            if (rc) break;
+        }
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
+            rc = set_error(MI355X_ERR_TIMEOUT, "rank %d: service call %llu did not complete", c->rank,
+                           (unsigned long long)seq);
+            break;
+        }
+    }
+    if (rc) {
+        svc_stop(c);
+        *svc_err_word(c) = 0;
+        return rc;
+    }
+    c->svc_calls++;
+    return MI355X_SUCCESS;
+}
+
+static void svc_release(mi355x_comm *c)
+{
+    svc_stop(c);
+    if (c->svcq) {
+        svc_queue_destroy(c->svcq);
+        delete c->svcq;
+        c->svcq = nullptr;
+    }
+    svc_page_free(c->svc_page, c->svc_page_dev);
+    c->svc_page = nullptr;
+    if (c->svc_host) (void)hipHostFree(c->svc_host);
+    c->svc_host = nullptr;
+    c->svc_ok = false;
+    if (c->svc_owner) {
+        std::lock_guard<std::mutex> g(g_svc_mtx);
+        auto it = g_svc_owner.find(c->device);
+        if (it != g_svc_owner.end() && it->second == c) g_svc_owner.erase(it);
+        c->svc_owner = false;
+    }
+}
+
+// this rank's part of opening the service: queue, doorbell page, host words
+static bool svc_open(mi355x_comm *c)
+{
+    c->svcq = new SvcQueue;
+    std::string why;
+    if (svc_queue_create(c->device, c->svcq, &why)) {
+        TRACE(c, "resident service unavailable: %s", why.c_str());
+        delete c->svcq;
+        c->svcq = nullptr;
+        return false;
+    }
+    void *pg = nullptr;
+    if (svc_page_alloc(c->svcq, (sizeof(SvcPage) + 4095) & ~(size_t)4095, &pg, &c->svc_page_dev)) return false;
+    c->svc_page = static_cast<SvcPage *>(pg);
+    if (hipHostMalloc((void **)&c->svc_host, 4096, hipHostMallocCoherent) != hipSuccess) return false;
+    std::memset(c->svc_host, 0, 4096);
+    return true;
+}
+
+// Collective, at creation (after the LL self-test): claim, open, self-test with one LL allgather
+// of a rank-tagged 8 KiB pattern through the service (bounded, MI355X_LL_PROBE_S); the
+// communicator serves small calls through the service only if every rank passed every step.
+static int svc_setup(mi355x_comm *c)
+{
+    c->svc_max = (size_t)std::max(0.0, env_double("MI355X_SVC_MAX_BYTES", (double)c->svc_max));
+    c->svc_idle_s = std::max(0.001, env_double("MI355X_SVC_IDLE_MS", c->svc_idle_s * 1e3) * 1e-3);
+    c->svc_nwg = (int)std::min(64.0, std::max(1.0, env_double("MI355X_SVC_WGS", (double)c->svc_nwg)));
+    const char *env = getenv("MI355X_SVC");
+    const bool want = c->ll_ok && c->size <= kLLMaxRanks && !(env && atoi(env) == 0);
+    if (want) {
+        std::lock_guard<std::mutex> g(g_svc_mtx);
+        if (!g_svc_owner.count(c->device)) {
+            g_svc_owner[c->device] = c;
+            c->svc_owner = true;
+        }
+    }
+    c->ctrl->slot[c->rank].svc_claim = c->svc_owner ? 1 : 2;
+    int rc = barrier(c);
+    if (rc) return rc;
+    bool all = true;
+    for (int q = 0; q < c->size; ++q) all = all && c->ctrl->slot[q].svc_claim == 1;
+    bool ok = all && svc_open(c);
+    if (ok) {
+        // the self-test call (svc_ok is what svc_usable asks: on for this call only)
+        const size_t per = 8192, n = (size_t)c->size;
+        char *buf = nullptr;
+        ok = hipMalloc((void **)&buf, per * (n + 1)) == hipSuccess &&
+             hipMemset(buf, c->rank + 1, per) == hipSuccess && hipMemset(buf + per, 0, per * n) == hipSuccess &&
+             hipDeviceSynchronize() == hipSuccess;
+        if (ok) {
+            LLArgs a;
+            std::memset(&a, 0, sizeof(a));
+            a.mode = LL_AG;
+            a.src = buf;
+            a.dst = buf + per;
+            a.nbytes = per;
+            a.push_mask = ~0ull;
+            const double saved_t = c->timeout_s;
+            const size_t saved_max = c->svc_max;
+            c->timeout_s = env_double("MI355X_LL_PROBE_S", 5.0);
+            c->svc_max = per;
+            c->svc_ok = true;
+            ok = ll_run(c, a, 0, 0, nullptr) == MI355X_SUCCESS;
+            c->svc_ok = false;
+            c->svc_max = saved_max;
+            c->timeout_s = saved_t;
+        }
+        if (ok) {
+            std::vector<unsigned char> h(per * n);
+            ok = hipMemcpy(h.data(), buf + per, per * n, hipMemcpyDeviceToHost) == hipSuccess;
+            for (size_t q = 0; q < n && ok; ++q)
+                for (size_t i = 0; i < per && ok; i += 509) ok = h[q * per + i] == (unsigned char)(q + 1);
+        }
+        (void)hipGetLastError();
+        if (buf) (void)hipFree(buf);
+    }
+    c->ctrl->slot[c->rank].svc_ok = ok ? 1 : 2;
+    rc = barrier(c);
+    if (rc) return rc;
+    bool every = all;
+    for (int q = 0; q < c->size && every; ++q) every = c->ctrl->slot[q].svc_ok == 1;
+    if (!every) {
+        if (all && c->rank == 0)
+            fprintf(stderr, "[mi355x] resident LL service unavailable: small collectives use the per-call paths\n");
+        svc_release(c);
+    }
+    c->svc_ok = every;
+    TRACE(c, "resident service: %s", every ? "on" : all ? "failed -> off" : "owned by another communicator");
     return barrier(c);
 }
 
@@ -1625,6 +1870,7 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     c->lat_on = env_double("MI355X_LAT_PROFILE", 0.0) != 0.0;
     if (rc == MI355X_SUCCESS && size > 1) rc = setup_done_words(c);
     if (rc == MI355X_SUCCESS && size > 1) rc = ll_selftest(c);
+    if (rc == MI355X_SUCCESS && size > 1) rc = svc_setup(c);
     if (rc) {
         mi355x_comm_destroy(c);
         return rc;
@@ -1668,6 +1914,7 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
         c->worker.join();
     }
     DeviceGuard dg(c->device);
+    svc_release(c);
     p2p_destroy(c);
     for (hipEvent_t e : c->tev)
         if (e) (void)hipEventDestroy(e);
@@ -1788,6 +2035,9 @@ int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
     case MI355X_KNOB_PIPE_CHUNK_KIB: *value = coll_tune().pipe_chunk_kib; break;
     case MI355X_KNOB_PIPE_WT: *value = coll_tune().pipe_wt; break;
     case MI355X_KNOB_ONE_PHASE_MAX_BYTES: *value = (long)c->one_phase_max; break;
+    case MI355X_KNOB_SVC_MAX_BYTES: *value = c->svc_ok ? (long)c->svc_max : 0; break;
+    case MI355X_KNOB_SVC_CALLS: *value = (long)c->svc_calls; break;
+    case MI355X_KNOB_SVC_LAUNCHES: *value = (long)c->svc_launches; break;
     default: return set_error(MI355X_ERR_ARG, "unknown knob %d", knob);
     }
     return MI355X_SUCCESS;
@@ -1851,6 +2101,13 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
     case MI355X_KNOB_LL_MAX_BYTES:
         if (value < 0 || value > (64l << 20)) return set_error(MI355X_ERR_ARG, "ll_max_bytes out of range");
         c->ll_max = c->ll_ok ? (size_t)value : 0;  // a failed (or skipped) self-test keeps it off
+        break;
+    case MI355X_KNOB_SVC_MAX_BYTES:
+        if (value < 0 || value > (64l << 20)) return set_error(MI355X_ERR_ARG, "svc_max_bytes out of range");
+        if (c->svc_ok) {  // a communicator without the service keeps 0
+            drain(c);
+            c->svc_max = (size_t)value;
+        }
         break;
     case MI355X_KNOB_STAGE_BYTES:
         if (value < 4096 || value >= (1l << 31)) return set_error(MI355X_ERR_ARG, "stage_bytes out of range");

@@ -99,6 +99,43 @@ struct LLArgs {
 };
 int launch_ll_slot(int op, int type, const LLArgs &a, hipStream_t s);  // LL_AR / LL_RED
 int launch_ll_copy(const LLArgs &a, hipStream_t s);                   // LL_AG / LL_BC
+constexpr size_t kLLAckBytes = 4096;  // LL region: [ack words][2 parities x n slots of granules]
+
+// Resident LL service (coll_svc.hip, svc_queue.cpp): the LL protocol run by a kernel that stays
+// resident between calls on a private HSA queue and waits on a doorbell, so a small collective
+// costs a host store and a device poll instead of a launch and a completion wait.  The host
+// writes the call into the doorbell page (fine-grained device memory, stored through the BAR),
+// then the call's number into `door`; every workgroup of the service polls `door`, serves the call
+// (chunks wg, wg + nwg, ...), publishes its results and counts itself done; the last one
+// acknowledges the call to every peer and stores its number into the host's completion word.
+constexpr uint64_t kSvcQuit = ~0ull;  // door value that ends the service
+constexpr int kSvcThreads = 256;      // threads per workgroup (16 B each: one LL slice per pass)
+struct SvcCall {
+    uint64_t seq;                     // the call's number (= its LL tag), written with the call
+    const void *src;
+    void *dst;
+    uint64_t nbytes, count, early, late, split, role_mask, push_mask, recv_mask;
+    int32_t op, type, mode, prog, root, nsteps, result, pad;
+    int32_t order[kLLMaxRanks];
+    TreeStep steps[kTreeSteps];
+};
+struct SvcPage {                      // the doorbell page
+    uint64_t door;                    // number of the posted call (kSvcQuit: leave)
+    uint64_t pad0[15];
+    uint64_t ctr;                     // workgroups done, zeroed by the host before every launch
+    uint64_t pad1[15];
+    SvcCall call;
+};
+struct SvcArgs {                      // fixed for one launch
+    const SvcPage *page;
+    uint64_t *done;                   // host word: number of the last call completed
+    uint32_t *err;                    // host word: set on a timeout waiting for a peer
+    char *my_ll;                      // my LL region
+    char *peer_ll[kLLMaxRanks];       // every rank's LL region, mapped
+    uint64_t first;                   // the call number this launch serves first
+    uint64_t slot_gran, idle_ticks, timeout_ticks;
+    int32_t n, me, nwg, probe;        // probe: return at once (loads the code object)
+};
 
 // Pipelined allreduce (coll_pipe.hip): fold of my ring block and pulls of the peers' blocks in
 // one launch, chunk by chunk, with per-chunk ready flags (uncached region, written by the

@@ -20,266 +20,30 @@
 //      (allreduce; reduce: the root only), or copies (allgather / bcast);
 //   5. counts itself done; the last block of the call acknowledges the call to every peer.
 // Slices are independent, so blocks never wait on each other.
-#include "coll_internal.hpp"
-#include "op_functors.hpp"
-#include "rt_internal.hpp"
+#include "coll_ll_dev.hpp"
 #include "slot_list.hpp"
 
 namespace mi355x {
-
-typedef unsigned int u32x4l __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ uint64_t ll_load(const uint64_t *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void ll_store(uint64_t *p, uint64_t v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// up to 16 bytes of src at `off` (len valid bytes) as 4 little-endian words (zero padded)
-__device__ __forceinline__ void ll_read16(const char *src, size_t len, uint32_t w[4])
-{
-    if (len == 16 && (((uintptr_t)src) & 15) == 0) {
-        const u32x4l v = *reinterpret_cast<const u32x4l *>(src);
-        w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
-        return;
-    }
-    unsigned char b[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) b[i] = (size_t)i < len ? (unsigned char)src[i] : 0;
-    __builtin_memcpy(w, b, 16);
-}
-__device__ __forceinline__ void ll_write16(char *dst, size_t len, const uint32_t w[4])
-{
-    if (len == 16 && (((uintptr_t)dst) & 15) == 0) {
-        u32x4l v;
-        v.x = w[0], v.y = w[1], v.z = w[2], v.w = w[3];
-        *reinterpret_cast<u32x4l *>(dst) = v;
-        return;
-    }
-    unsigned char b[16];
-    __builtin_memcpy(b, w, 16);
-    for (size_t i = 0; i < len; ++i) dst[i] = (char)b[i];
-}
-
-struct LLBlock {
-    size_t lo, off, len;   // block payload start; this thread's 16-B chunk offset / valid bytes
-    int ngran;             // granules of this thread (0: past the end)
-    uint32_t tag;
-};
-
-__device__ __forceinline__ LLBlock ll_block(const LLArgs &a)
-{
-    LLBlock k;
-    k.lo = (size_t)blockIdx.x * kLLChunk;
-    k.off = k.lo + (size_t)threadIdx.x * 16;
-    k.len = k.off < a.nbytes ? (a.nbytes - k.off < 16 ? a.nbytes - k.off : 16) : 0;
-    k.ngran = (int)((k.len + 3) / 4);
-    k.tag = (uint32_t)a.seq;
-    return k;
-}
-
-// steps 1-2; false on timeout
-__device__ bool ll_push(const LLArgs &a, const LLBlock &k)
-{
-    __shared__ int timed_out;
-    const int t = (int)threadIdx.x;
-    if (t == 0) timed_out = 0;
-    __syncthreads();
-    if (a.src && t < a.n && t != a.me && ((a.push_mask >> t) & 1u) && a.seq > 2) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (ll_load(a.my_ack + t) + 2 < a.seq) {
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
-                __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                timed_out = 1;
-                break;
-            }
-        }
-    }
-    __syncthreads();
-    if (timed_out) return false;
-    if (a.src && k.ngran) {  // (bcast: only the root has data to push)
-        uint32_t w[4];
-        ll_read16(static_cast<const char *>(a.src) + k.off, k.len, w);
-        const size_t g0 = k.off / 4;
-        for (int q = 0; q < a.n; ++q) {
-            if (!((a.push_mask >> q) & 1u)) continue;
-            uint64_t *d = a.peer_data[q] + g0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (i < k.ngran) ll_store(d + i, ((uint64_t)k.tag << 32) | w[i]);
-        }
-    }
-    return true;
-}
-
-// step 3 for the sources in qmask (<= 8 of them, slot index = rank): w[q] gets rank q's 16 B
-__device__ bool ll_recv(const LLArgs &a, const LLBlock &k, uint64_t qmask, uint32_t (&w)[8][4])
-{
-    if (!k.ngran) return true;
-    const size_t g0 = k.off / 4;
-    uint32_t pending = 0;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        if (!((qmask >> q) & 1u)) continue;
-        const uint64_t *p = a.my_data + (size_t)q * a.slot_gran + g0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (i >= k.ngran) continue;
-            const uint64_t v = ll_load(p + i);
-            w[q][i] = (uint32_t)v;
-            if ((uint32_t)(v >> 32) != k.tag) pending |= 1u << (q * 4 + i);
-        }
-    }
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    unsigned spins = 0;
-    while (pending) {
-        __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                if (!((pending >> (q * 4 + i)) & 1u)) continue;
-                const uint64_t v = ll_load(a.my_data + (size_t)q * a.slot_gran + g0 + i);
-                w[q][i] = (uint32_t)v;
-                if ((uint32_t)(v >> 32) == k.tag) pending &= ~(1u << (q * 4 + i));
-            }
-        }
-        if ((++spins & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
-            __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            return false;
-        }
-    }
-    return true;
-}
-
-// step 5: after every thread of the block is done with its slots
-__device__ void ll_done(const LLArgs &a)
-{
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    const uint64_t old = __hip_atomic_fetch_add(a.ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1 != a.ctr_target) return;
-    for (int q = 0; q < a.n; ++q)
-        if (q != a.me) ll_store(a.peer_ack[q], a.seq);
-}
-
-template <class F> __device__ __forceinline__ typename F::T ll_pick(const typename F::T (&R)[kTreeMax], int k)
-{
-    typename F::T v = R[0];
-#pragma unroll
-    for (int s = 1; s < kTreeMax; ++s)
-        if (s == k) v = R[s];
-    return v;
-}
-
-template <typename T> struct alignas(16) LLVec {
-    T e[16 / sizeof(T)];
-};
-
-// per-element program (scalar); x(q) = rank q's element i
-template <class F, class X> __device__ __forceinline__ typename F::T ll_eval(const LLArgs &a, size_t i, X x)
-{
-    using T = typename F::T;
-    if (a.prog == LL_TREE) {
-        T R[kTreeMax];
-#pragma unroll
-        for (int s = 0; s < kTreeMax; ++s)
-            if (s < a.n) R[s] = x(s);
-        for (int k = 0; k < a.nsteps; ++k) {
-            const TreeStep st = a.steps[k];
-            const T r = F::op2(ll_pick<F>(R, st.out), ll_pick<F>(R, st.in));
-#pragma unroll
-            for (int s = 0; s < kTreeMax; ++s)
-                if (s == st.dst) R[s] = r;
-        }
-        return ll_pick<F>(R, a.result);
-    }
-    // left fold; LL_RING: the order starts at the element's ring block
-    // (coll_tuned_allreduce.c:470-512: the partial is the `in` operand at every step)
-    int b0 = 0;
-    if (a.prog == LL_RING) {
-        const uint64_t se = a.split * a.early;
-        b0 = (i < se) ? (int)(i / a.early) : (int)(a.split + (i - se) / a.late);
-    }
-    auto rank_at = [&](int j) -> int {
-        if (a.prog == LL_RING) {
-            const int r = b0 + j;
-            return r >= a.n ? r - a.n : r;
-        }
-        return a.order[j];
-    };
-    T acc = x(rank_at(0));
-    for (int j = 1; j < a.n; ++j) {
-        const T v = x(rank_at(j));
-        acc = ((a.role_mask >> j) & 1u) ? F::op2(acc, v) : F::op2(v, acc);
-    }
-    return acc;
-}
 
 // allreduce / reduce: exchange, then this thread's 16 B of the result from the n inputs held in
 // registers (<= 8 ranks: ll_usable)
 template <class F> __global__ __launch_bounds__(256) void k_ll_allreduce(LLArgs a)
 {
-    using T = typename F::T;
-    using V = LLVec<T>;
-    constexpr int EPV = 16 / sizeof(T);
-    const LLBlock k = ll_block(a);
+    const LLBlock k = ll_block(a, blockIdx.x);
     if (!ll_push(a, k)) return;
     const bool evaluate = !(a.mode == LL_RED && a.me != a.root);  // reduce: only the root evaluates
     uint32_t w[8][4];
-    if (evaluate && ll_recv(a, k, a.recv_mask, w) && k.ngran) {
-        V xv[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) __builtin_memcpy(&xv[q], w[q], 16);
-        const size_t i0 = k.off / sizeof(T);
-        const int ne = (int)(k.len / sizeof(T));
-        V r;
-#pragma unroll
-        for (int e = 0; e < EPV; ++e) {
-            if (e >= ne) continue;
-            r.e[e] = ll_eval<F>(a, i0 + e, [&](int q) {
-                T v = xv[0].e[e];  // register select (no dynamic indexing into xv)
-#pragma unroll
-                for (int s2 = 1; s2 < 8; ++s2)
-                    if (s2 == q) v = xv[s2].e[e];
-                return v;
-            });
-        }
-        uint32_t ow[4];
-        __builtin_memcpy(ow, &r, 16);
-        ll_write16(static_cast<char *>(a.dst) + k.off, k.len, ow);
-    }
+    if (evaluate && ll_recv(a, k, a.recv_mask, w) && k.ngran) ll_reduce_out<F>(a, k, w);
     ll_done(a);
 }
 
 // allgather (slot q -> dst + q*nbytes) and bcast (slot root -> dst, non-roots)
 __global__ __launch_bounds__(256) void k_ll_copy(LLArgs a)
 {
-    const LLBlock k = ll_block(a);
+    const LLBlock k = ll_block(a, blockIdx.x);
     if (!ll_push(a, k)) return;
     uint32_t w[8][4];
-    if (a.recv_mask && ll_recv(a, k, a.recv_mask, w) && k.ngran) {
-        char *dst = static_cast<char *>(a.dst);
-        if (a.mode == LL_BC) {
-            uint32_t v[4];
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-                if (q == a.root) __builtin_memcpy(v, w[q], 16);
-            ll_write16(dst + k.off, k.len, v);
-        } else {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                if (!((a.recv_mask >> q) & 1u)) continue;
-                char *d = dst + (size_t)q * a.nbytes;
-                if (q == a.me && static_cast<const char *>(a.src) == d) continue;  // in place
-                ll_write16(d + k.off, k.len, w[q]);
-            }
-        }
-    }
+    if (a.recv_mask && ll_recv(a, k, a.recv_mask, w) && k.ngran) ll_copy_out(a, k, w);
     ll_done(a);
 }
 

@@ -21,6 +21,7 @@
 #include "coll_internal.hpp"
 #include "coll_sched.hpp"
 #include "rt_internal.hpp"
+#include "svc_queue.hpp"
 
 namespace mi355x {
 
@@ -65,6 +66,8 @@ struct alignas(64) RankSlot {
     uint64_t probe_size;
     int64_t varg[2 * kMaxRanks];  // per-peer counts / displacements of v-collectives (bytes)
     int32_t ll_ok, pad_ll;        // LL self-test result at creation (1 ok, 2 failed)
+    int32_t svc_claim, svc_ok;    // resident LL service at creation: this process's service is mine
+                                  // (1) or taken (2); its self-test passed (1) or failed (2)
     uint64_t dev_uid;             // hash of the device's PCI bus id: ranks sharing one GPU
     // mi355x_comm_vote: call v's entry at [v % kVoteRing] = (v << 1) | (this rank's buffers are
     // device memory); a ring because a rank with device buffers publishes and moves on
@@ -245,6 +248,20 @@ struct mi355x_comm {
     uint64_t *ll_ctr = nullptr;                   // blocks done (device), monotonic
     uint64_t ll_ctr_base = 0;                     // its value before the next call
     uint32_t *ll_err = nullptr;                   // host-visible timeout word
+    // resident LL service (coll_svc.hip, svc_queue.cpp): small collectives up to svc_max bytes per
+    // rank served by a kernel resident on a private HSA queue.  One service per process and GPU; the
+    // communicator that finds it free on every rank at creation owns it (svc_ok), every other
+    // communicator uses the per-call paths
+    size_t svc_max = 0;                           // MI355X_SVC_MAX_BYTES / MI355X_KNOB_SVC_MAX_BYTES
+    bool svc_ok = false;
+    bool svc_owner = false;                       // this process's service is claimed by this communicator
+    mi355x::SvcQueue *svcq = nullptr;
+    mi355x::SvcPage *svc_page = nullptr;          // doorbell page (host-writable; device address == host address)
+    bool svc_page_dev = false;                    // the page is fine-grained device memory (else pinned host)
+    uint64_t *svc_host = nullptr;                 // pinned host words: [0] call completed, [1] error word
+    int svc_nwg = 8;                              // workgroups of the service (8 x 4 KiB slices per pass)
+    double svc_idle_s = 0.05;                     // the service leaves after this long without a call
+    uint64_t svc_calls = 0, svc_launches = 0;
     // pipelined allreduce (coll_pipe.hip): per-chunk ready flags in an uncached region that
     // every peer writes into (row q = flags raised by rank q), and the work-queue counter
     char *pipe_base = nullptr;

@@ -13,7 +13,7 @@ template <class F> struct SlotTag {
     using type = F;
 };
 
-template <template <typename> class OP, class Put> inline void for_each_int_slot(Put &&put, int op)
+template <template <typename> class OP, class Put> __host__ __device__ inline void for_each_int_slot(Put &&put, int op)
 {
     put(SlotTag<OP<int8_t>>{}, op, MI355X_T_INT8);
     put(SlotTag<OP<uint8_t>>{}, op, MI355X_T_UINT8);
@@ -25,7 +25,7 @@ template <template <typename> class OP, class Put> inline void for_each_int_slot
     put(SlotTag<OP<uint64_t>>{}, op, MI355X_T_UINT64);
 }
 
-template <class Put> inline void for_each_slot(Put &&put)
+template <class Put> __host__ __device__ inline void for_each_slot(Put &&put)
 {
     for_each_int_slot<OpMax>(put, MI355X_OP_MAX);
     put(SlotTag<OpMax<float>>{}, MI355X_OP_MAX, MI355X_T_FLOAT);

@@ -56,14 +56,19 @@ def realloc_same_address(pkg, comm, rank, size):
     comm.set("LL_MAX_BYTES", 0)
 
 
-def ll_checks(pkg, comm, rank, size, oracle, torch):
-    """the one-shot low-latency path (coll_ll.hip): every forced allreduce algorithm against the
-    oracle's schedule simulation, in place and not, allgather / bcast, and many back-to-back calls
-    (parity reuse of the LL slots)"""
+def ll_checks(pkg, comm, rank, size, oracle, torch, knob="LL_MAX_BYTES"):
+    """the one-shot low-latency protocol -- per-call LL kernels (coll_ll.hip, knob LL_MAX_BYTES) or
+    the resident service (coll_svc.hip, knob SVC_MAX_BYTES): every forced allreduce algorithm
+    against the oracle's schedule simulation, in place and not, allgather / bcast, and many
+    back-to-back calls (parity reuse of the LL slots)"""
     ptrs = lambda arrs: (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
-    assert comm.get("LL_MAX_BYTES") == 0, "the LL path is off by default"
-    comm.set("LL_MAX_BYTES", 256 << 10)
-    assert comm.get("LL_MAX_BYTES") > 0, "the creation-time LL self-test disabled the LL path"
+    path = "LL" if knob == "LL_MAX_BYTES" else "SVC"
+    if knob == "LL_MAX_BYTES":
+        assert comm.get("LL_MAX_BYTES") == 0, "the LL path is off by default"
+    saved_svc = comm.get("SVC_MAX_BYTES")
+    comm.set("SVC_MAX_BYTES", 0)
+    comm.set(knob, 256 << 10)
+    assert comm.get(knob) > 0, f"the creation-time self-test disabled the {path} path"
     for alg in (0, 1, 2, 3, 4, 5):
         comm.set("ALLREDUCE_ALG", alg)
         for opname, tname in [("SUM", "FLOAT"), ("MAX", "DOUBLE"), ("MINLOC", "FLOAT_INT"), ("PROD", "C_DOUBLE_COMPLEX")]:
@@ -80,7 +85,7 @@ def ll_checks(pkg, comm, rank, size, oracle, torch):
                     comm.allreduce(None if inplace else dx.data_ptr(), dr.data_ptr(), count, ty, op)
                     got = dr.cpu().numpy().view(xs[0].dtype)
                     opdata.assert_same(tname, opname, got, outs[rank],
-                                       f"LL allreduce alg={alg} count={count} inplace={inplace} rank={rank}")
+                                       f"{path} allreduce alg={alg} count={count} inplace={inplace} rank={rank}")
                     assert comm.last_algorithm() == ran, (comm.last_algorithm(), ran)
     comm.set("ALLREDUCE_ALG", 0)
     # MPI_Reduce: LL (every rank pushes to the root) and, above the LL size, owner-computes
@@ -141,8 +146,9 @@ def ll_checks(pkg, comm, rank, size, oracle, torch):
         q.wait()
     want = size * (size + 1) / 2
     assert bool(torch.all(ys == want)) and bool(torch.all(yl == want)), "nonblocking allreduce"
-    comm.set("LL_MAX_BYTES", 0)
-    print(f"rank {rank} LL OK", flush=True)
+    comm.set(knob, 0)
+    comm.set("SVC_MAX_BYTES", saved_svc)
+    print(f"rank {rank} {path} OK", flush=True)
 
 
 def staged(pkg, comm, rank, size, torch, key):
@@ -489,6 +495,77 @@ def concurrent_comms(key, rank, size, dev):
     print(f"rank {rank} concurrent OK", flush=True)
 
 
+def svc_mode(key, rank, size, dev):
+    """the resident LL service (coll_svc.hip on a private HSA queue, svc_queue.cpp) beside the rest of
+    the process: while it stays resident (MI355X_SVC_IDLE_MS=3000 here) hipDeviceSynchronize and work
+    on fresh streams do not wait for it; back-to-back calls reuse one launch; it leaves when idle and
+    comes back on the next call; one service per process -- a second communicator does not get it
+    (its knob reads 0) and still computes exactly on the per-call paths; a communicator created after
+    the owner is gone gets it"""
+    import os
+    import time
+    import torch
+    torch.cuda.set_device(dev)
+    pkg = load_pkg()
+    f32, SUM = pkg.T["FLOAT"], pkg.OP["SUM"]
+    a = pkg.Comm.create(key + "_a", rank, size, dev)
+    b = pkg.Comm.create(key + "_b", rank, size, dev)
+    a.set("SVC_MAX_BYTES", 64 << 10)
+    b.set("SVC_MAX_BYTES", 64 << 10)
+    assert a.get("SVC_MAX_BYTES") == 64 << 10, "the first communicator owns the service"
+    assert b.get("SVC_MAX_BYTES") == 0, "one service per process: the second communicator has none"
+    x = torch.full((1000,), float(rank + 1), device="cuda")
+    y = torch.empty_like(x)
+    want = size * (size + 1) / 2
+    for c in (a, b, a, b):
+        y.fill_(-1)
+        torch.cuda.synchronize()
+        c.allreduce(x.data_ptr(), y.data_ptr(), 1000, f32, SUM)
+        assert bool(torch.all(y == want).item()), "allreduce next to the service"
+    assert b.get("SVC_CALLS") == 0 and a.get("SVC_CALLS") >= 2
+    # resident now (idle limit 3 s): the device synchronizes without it, a fresh stream runs
+    assert a.get("SVC_LAUNCHES") >= 1
+    t0 = time.perf_counter()
+    torch.cuda.synchronize()
+    dt_sync = time.perf_counter() - t0
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        z = x * 2
+    t0 = time.perf_counter()
+    st.synchronize()
+    dt_stream = time.perf_counter() - t0
+    assert dt_sync < 0.5 and dt_stream < 0.5, (dt_sync, dt_stream)
+    assert bool(torch.all(z == 2 * (rank + 1)).item())
+    launches = a.get("SVC_LAUNCHES")
+    for k in range(200):
+        x.fill_(float(rank + k))
+        a.allreduce(x.data_ptr(), y.data_ptr(), 1000, f32, SUM)
+        assert bool(torch.all(y == sum(r + k for r in range(size))).item()), ("back to back", k)
+    relaunched = a.get("SVC_LAUNCHES") - launches
+    assert relaunched <= 2, f"{relaunched} relaunches over 200 back-to-back calls"
+    # idle exit and relaunch (a short idle limit on a fresh owner)
+    a.barrier()
+    a.destroy()
+    os.environ["MI355X_SVC_IDLE_MS"] = "2"
+    c = pkg.Comm.create(key + "_c", rank, size, dev)
+    c.set("SVC_MAX_BYTES", 64 << 10)
+    assert c.get("SVC_MAX_BYTES") == 64 << 10, "a communicator created after the owner left gets the service"
+    for k in range(20):
+        x.fill_(float(rank + k))
+        c.allreduce(x.data_ptr(), y.data_ptr(), 1000, f32, SUM)
+        assert bool(torch.all(y == sum(r + k for r in range(size))).item()), ("after idle exits", k)
+        time.sleep(0.01)  # longer than the idle limit: the service has left; the next call relaunches
+    assert c.get("SVC_LAUNCHES") >= 10, c.get("SVC_LAUNCHES")
+    print(f"rank {rank} svc: sync {dt_sync * 1e3:.2f} ms, fresh stream {dt_stream * 1e3:.2f} ms while resident; "
+          f"{relaunched} relaunches over 200 calls; {c.get('SVC_LAUNCHES')} launches over 20 spaced calls", flush=True)
+    b.set("SVC_MAX_BYTES", 64 << 10)
+    assert b.get("SVC_MAX_BYTES") == 0, "the service is decided at creation"
+    for cc in (b, c):
+        cc.barrier()
+        cc.destroy()
+    print(f"rank {rank} svc OK", flush=True)
+
+
 def done_words(key, rank, size, dev):
     """MI355X_DONE_WORDS=1 (finish points by command-processor-written completion words, off by
     default: slower back to back on this platform, profiles/r03_small_latency.jsonl): every flow that
@@ -590,6 +667,8 @@ def _main():
         return done_words(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "host_bw":
         return host_bw(key, rank, size, dev)
+    if len(sys.argv) > 5 and sys.argv[5] == "svc":
+        return svc_mode(key, rank, size, dev)
     import faulthandler
     faulthandler.dump_traceback_later(150, exit=True)  # a rank stuck in a HIP call names its line
     import torch
@@ -628,6 +707,11 @@ def _main():
     if size == 3:
         pipe_all_slots(pkg, comm, rank, size, oracle, torch)
     ll_checks(pkg, comm, rank, size, oracle, torch)
+    calls0 = comm.get("SVC_CALLS")
+    ll_checks(pkg, comm, rank, size, oracle, torch, knob="SVC_MAX_BYTES")
+    served, launches = comm.get("SVC_CALLS") - calls0, comm.get("SVC_LAUNCHES")
+    assert served > 100, f"the resident service served {served} calls"
+    print(f"rank {rank} resident service: {served} calls, {launches} launches", flush=True)
     p2p_checks(pkg, comm, rank, size, oracle, torch)
     _fd_report(rank)
     staged(pkg, comm, rank, size, torch, key)

@@ -35,7 +35,7 @@ def test_ipc_ranks(gpu, size):
     failed = [r for r, p in enumerate(procs) if p.returncode != 0]
     assert not failed, "\n".join(f"rank {r} failed (rc {procs[r].returncode}):\n{outs[r][-2500:]}" for r in failed)
     for r, p in enumerate(procs):
-        stages = ("pipe OK", "LL OK", "p2p OK", "staged OK", "OK") + (("bcast4g OK",) if size in (2, 3) else ()) \
+        stages = ("pipe OK", "LL OK", "SVC OK", "p2p OK", "staged OK", "OK") + (("bcast4g OK",) if size in (2, 3) else ()) \
             + (("maxcount OK",) if size == 2 else ()) \
             + (("pipe slots OK",) if size == 3 else ())
         for stage in stages:
@@ -59,6 +59,13 @@ def _run_mode(gpu, mode, size=2, timeout=280, extra_env=None):
     for r, p in enumerate(procs):
         assert p.returncode == 0 and f"rank {r} {mode} OK" in outs[r], f"rank {r}:\n{outs[r][-3000:]}"
     return outs
+
+
+@pytest.mark.parametrize("size", [2, 3])
+def test_resident_service(gpu, size):
+    """the resident LL service beside the rest of the process (ipc_worker.py::svc_mode)"""
+    outs = _run_mode(gpu, "svc", size, extra_env={"MI355X_SVC_IDLE_MS": "3000"})
+    print(next(line for line in outs[0].splitlines() if "svc:" in line))
 
 
 @pytest.mark.parametrize("size", [2, 3])
