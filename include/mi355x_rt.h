@@ -172,8 +172,9 @@ enum mi355x_knob {
                                            whose ranks all find it free at creation; reads 0 (and setting it
                                            is ignored) on every other communicator.  MI355X_SVC=0 disables it */
     MI355X_KNOB_SVC_CALLS = 20,         /* (read-only) calls served by the resident service */
-    MI355X_KNOB_SVC_LAUNCHES = 21       /* (read-only) launches of the resident service (it leaves after
+    MI355X_KNOB_SVC_LAUNCHES = 21,      /* (read-only) launches of the resident service (it leaves after
                                            MI355X_SVC_IDLE_MS without a call and is relaunched on demand) */
+    MI355X_KNOB_SVC_RESIDENT = 22       /* (read-only) 1 while the service's kernel is resident */
 };
 int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
 /* current value of a knob (LL_MAX_BYTES reads 0 when the creation-time LL self-test failed) */

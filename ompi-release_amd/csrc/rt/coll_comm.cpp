@@ -2038,6 +2038,7 @@ int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
     case MI355X_KNOB_SVC_MAX_BYTES: *value = c->svc_ok ? (long)c->svc_max : 0; break;
     case MI355X_KNOB_SVC_CALLS: *value = (long)c->svc_calls; break;
     case MI355X_KNOB_SVC_LAUNCHES: *value = (long)c->svc_launches; break;
+    case MI355X_KNOB_SVC_RESIDENT: *value = c->svcq && svc_resident(c->svcq) ? 1 : 0; break;
     default: return set_error(MI355X_ERR_ARG, "unknown knob %d", knob);
     }
     return MI355X_SUCCESS;

@@ -19,9 +19,33 @@ __device__ __forceinline__ void ll_store(uint64_t *p, uint64_t v)
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// up to 16 bytes of src at `off` (len valid bytes) as 4 little-endian words (zero padded)
-__device__ __forceinline__ void ll_read16(const char *src, size_t len, uint32_t w[4])
+// SYS (the resident service, which has no kernel boundary between calls): the caller's input is
+// read and the result written with the system-coherent cache policy (sc0 sc1, raw buffer ops) --
+// loads skip this CU's L1, which may still hold the lines of an earlier call's input, and stores
+// go through the XCD's L2 to memory, so the call's results need no L2 write-back fence
+constexpr int kLLSysCoherent = 1 | 16;  // gfx950 cache-policy bits: sc0 (1) | sc1 (16)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ll_rsrc(const void *p)
 {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, 16, 0x00020000);
+}
+
+// up to 16 bytes of src at `off` (len valid bytes) as 4 little-endian words (zero padded)
+template <bool SYS = false> __device__ __forceinline__ void ll_read16(const char *src, size_t len, uint32_t w[4])
+{
+    if constexpr (SYS) {
+        const __amdgpu_buffer_rsrc_t rs = ll_rsrc(src);
+        if (len == 16 && (((uintptr_t)src) & 15) == 0) {
+            const u32x4l v = __builtin_amdgcn_raw_buffer_load_b128(rs, 0, 0, kLLSysCoherent);
+            w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
+            return;
+        }
+        unsigned char b[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            b[i] = (size_t)i < len ? __builtin_amdgcn_raw_buffer_load_b8(rs, (unsigned)i, 0, kLLSysCoherent) : 0;
+        __builtin_memcpy(w, b, 16);
+        return;
+    }
     if (len == 16 && (((uintptr_t)src) & 15) == 0) {
         const u32x4l v = *reinterpret_cast<const u32x4l *>(src);
         w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
@@ -32,8 +56,21 @@ __device__ __forceinline__ void ll_read16(const char *src, size_t len, uint32_t 
     for (int i = 0; i < 16; ++i) b[i] = (size_t)i < len ? (unsigned char)src[i] : 0;
     __builtin_memcpy(w, b, 16);
 }
-__device__ __forceinline__ void ll_write16(char *dst, size_t len, const uint32_t w[4])
+template <bool SYS = false> __device__ __forceinline__ void ll_write16(char *dst, size_t len, const uint32_t w[4])
 {
+    if constexpr (SYS) {
+        const __amdgpu_buffer_rsrc_t rs = ll_rsrc(dst);
+        if (len == 16 && (((uintptr_t)dst) & 15) == 0) {
+            u32x4l v;
+            v.x = w[0], v.y = w[1], v.z = w[2], v.w = w[3];
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, 0, 0, kLLSysCoherent);
+            return;
+        }
+        unsigned char b[16];
+        __builtin_memcpy(b, w, 16);
+        for (size_t i = 0; i < len; ++i) __builtin_amdgcn_raw_buffer_store_b8(b[i], rs, (unsigned)i, 0, kLLSysCoherent);
+        return;
+    }
     if (len == 16 && (((uintptr_t)dst) & 15) == 0) {
         u32x4l v;
         v.x = w[0], v.y = w[1], v.z = w[2], v.w = w[3];
@@ -64,7 +101,7 @@ __device__ __forceinline__ LLBlock ll_block(const LLArgs &a, size_t chunk)
 }
 
 // steps 1-2; false on timeout
-static __device__ bool ll_push(const LLArgs &a, const LLBlock &k)
+template <bool SYS = false> static __device__ bool ll_push(const LLArgs &a, const LLBlock &k)
 {
     __shared__ int timed_out;
     const int t = (int)threadIdx.x;
@@ -85,7 +122,7 @@ static __device__ bool ll_push(const LLArgs &a, const LLBlock &k)
     if (timed_out) return false;
     if (a.src && k.ngran) {  // (bcast: only the root has data to push)
         uint32_t w[4];
-        ll_read16(static_cast<const char *>(a.src) + k.off, k.len, w);
+        ll_read16<SYS>(static_cast<const char *>(a.src) + k.off, k.len, w);
         const size_t g0 = k.off / 4;
         for (int q = 0; q < a.n; ++q) {
             if (!((a.push_mask >> q) & 1u)) continue;
@@ -204,7 +241,8 @@ template <class F, class X> __device__ __forceinline__ typename F::T ll_eval(con
 
 // allreduce / reduce: this thread's 16 B of the result from the n inputs held in registers
 // (<= 8 ranks: ll_usable); w[q] = rank q's 16 B
-template <class F> __device__ __forceinline__ void ll_reduce_out(const LLArgs &a, const LLBlock &k, const uint32_t (&w)[8][4])
+template <class F, bool SYS = false>
+__device__ __forceinline__ void ll_reduce_out(const LLArgs &a, const LLBlock &k, const uint32_t (&w)[8][4])
 {
     using T = typename F::T;
     using V = LLVec<T>;
@@ -228,10 +266,11 @@ template <class F> __device__ __forceinline__ void ll_reduce_out(const LLArgs &a
     }
     uint32_t ow[4];
     __builtin_memcpy(ow, &r, 16);
-    ll_write16(static_cast<char *>(a.dst) + k.off, k.len, ow);
+    ll_write16<SYS>(static_cast<char *>(a.dst) + k.off, k.len, ow);
 }
 
 // allgather (slot q -> dst + q*nbytes) and bcast (slot root -> dst, non-roots)
+template <bool SYS = false>
 __device__ __forceinline__ void ll_copy_out(const LLArgs &a, const LLBlock &k, const uint32_t (&w)[8][4])
 {
     char *dst = static_cast<char *>(a.dst);
@@ -240,14 +279,14 @@ __device__ __forceinline__ void ll_copy_out(const LLArgs &a, const LLBlock &k, c
 #pragma unroll
         for (int q = 0; q < 8; ++q)
             if (q == a.root) __builtin_memcpy(v, w[q], 16);
-        ll_write16(dst + k.off, k.len, v);
+        ll_write16<SYS>(dst + k.off, k.len, v);
     } else {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             if (!((a.recv_mask >> q) & 1u)) continue;
             char *d = dst + (size_t)q * a.nbytes;
             if (q == a.me && static_cast<const char *>(a.src) == d) continue;  // in place
-            ll_write16(d + k.off, k.len, w[q]);
+            ll_write16<SYS>(d + k.off, k.len, w[q]);
         }
     }
 }

@@ -14,13 +14,14 @@
 //      service has been idle for idle_ticks: the kernel leaves and the host relaunches it on the
 //      next call);
 //   2. the call's descriptor (SvcCall, in the doorbell page) is copied into LDS and expanded
-//      into LLArgs; an acquire makes the inputs written before the call visible;
+//      into LLArgs;
 //   3. the workgroup serves slices wg, wg + nwg, ... of the call exactly as a per-call LL block
 //      serves its slice (push, receive, evaluate the reference schedule's per-element program or
-//      copy);
-//   4. it releases its results (L2 write-back) and counts itself done; the workgroup that
-//      completes the count acknowledges the call to every peer (the LL parity protocol) and
-//      stores the call number into the host's completion word.
+//      copy), reading the inputs with system-coherent loads and storing the results write-through
+//      (no kernel boundary between calls does the cache maintenance for it);
+//   4. it counts itself done once its stores have reached memory; the workgroup that completes
+//      the count (or the only one, for a call of one slice) acknowledges the call to every peer
+//      (the LL parity protocol) and stores the call number into the host's completion word.
 // Every wait is bounded (timeout_ticks; the error word is set and the workgroup leaves).
 #include "coll_ll_dev.hpp"
 #include "slot_list.hpp"
@@ -36,7 +37,7 @@ static_assert(kSvcCallWords <= kSvcThreads, "one word per thread");
 template <class F>
 static __device__ __noinline__ void svc_slot(const LLArgs &a, const LLBlock &k, const uint32_t (&w)[8][4])
 {
-    ll_reduce_out<F>(a, k, w);
+    ll_reduce_out<F, true>(a, k, w);
 }
 
 // the evaluation for the call's (op, type): one branch per slot with a GPU kernel
@@ -61,7 +62,7 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
     const int t = (int)threadIdx.x;
     SvcPage *page = const_cast<SvcPage *>(g.page);
     uint64_t want = g.first;
-    uint64_t served = 0;  // calls this launch has served
+    uint64_t ctr_base = 0;  // the doorbell page's workgroup counter before this call
     uint64_t idle0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         // 1. the doorbell
@@ -120,16 +121,23 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
         }
         if (t < kTreeSteps) a.steps[t] = sc.steps[t];
         __syncthreads();
-        // inputs written before the call (by any kernel, on any XCD) are visible from here on
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        // 3. my slices
+        // 3. my slices.  The inputs (written by kernels that completed before the call) are read
+        // with system-coherent loads, the results stored write-through (ll_read16 / ll_write16<SYS>):
+        // no acquire or release fence per call.  Workgroups beyond the call's slice count sit it out.
         const uint64_t nchunks = (a.nbytes + kLLChunk - 1) / kLLChunk;
+        const uint64_t part = nchunks < (uint64_t)g.nwg ? nchunks : (uint64_t)g.nwg;
+        if (blockIdx.x >= part) {
+            if (part > 1) ctr_base += part;
+            ++want;
+            idle0 = __builtin_amdgcn_s_memrealtime();
+            continue;
+        }
         const bool reduce = a.mode == LL_AR || a.mode == LL_RED;
         const bool evaluate = reduce ? !(a.mode == LL_RED && me != a.root) : a.recv_mask != 0;
         int failed = 0;
         for (uint64_t c = blockIdx.x; c < nchunks; c += (uint64_t)g.nwg) {
             const LLBlock k = ll_block(a, c);
-            if (!ll_push(a, k)) {
+            if (!ll_push<true>(a, k)) {
                 failed = 1;
                 break;
             }
@@ -141,28 +149,32 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
                 else if (reduce)
                     svc_reduce_out(sc.op, sc.type, a, k, w);
                 else
-                    ll_copy_out(a, k, w);
+                    ll_copy_out<true>(a, k, w);
             }
             if (__syncthreads_or(bad)) {
                 failed = 1;
                 break;
             }
         }
-        // 4. publish, count, acknowledge, complete
+        // 4. every store of the workgroup has reached memory; count; the last participant
+        // acknowledges the call to every peer and completes it for the host
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (t == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const uint64_t old = __hip_atomic_fetch_add(&page->ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (!failed && old + 1 == (served + 1) * (uint64_t)g.nwg) {
+            bool last = part == 1;
+            if (!last) {
+                const uint64_t old =
+                    __hip_atomic_fetch_add(&page->ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last = old + 1 == ctr_base + part;
+            }
+            if (!failed && last) {
                 for (int q = 0; q < n; ++q)
                     if (q != me) ll_store(a.peer_ack[q], want);
                 __hip_atomic_store(g.done, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
         if (failed) break;  // the error word is set; the host ends the service
-        ++served;
+        if (part > 1) ctr_base += part;
         ++want;
         idle0 = __builtin_amdgcn_s_memrealtime();
     }
@@ -177,13 +189,11 @@ int svc_probe_launch(int device)
     SvcArgs probe;
     __builtin_memset(&probe, 0, sizeof(probe));
     probe.probe = 1;
-    hipStream_t s = nullptr;
-    bool ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
-    if (ok) {
-        hipLaunchKernelGGL(mi355x_k_svc, dim3(1), dim3(kSvcThreads), 0, s, probe);
-        ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
-        (void)hipStreamDestroy(s);
-    }
+    // on the null stream: a stream of its own would make HIP create one more hardware queue for
+    // the process, and with two processes on one GPU every hardware queue beyond the second slows
+    // every launch of both (profiles/r03_queue_probe.jsonl)
+    hipLaunchKernelGGL(mi355x_k_svc, dim3(1), dim3(kSvcThreads), 0, nullptr, probe);
+    const bool ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(nullptr) == hipSuccess;
     (void)hipSetDevice(prev);
     return ok ? 0 : -1;
 }

@@ -17,6 +17,7 @@
 #include <sched.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -237,8 +238,11 @@ int svc_page_alloc(SvcQueue *q, size_t bytes, void **p, bool *device)
     // BAR (write-combined: the caller fences them), the kernel polls it without crossing PCIe
     PoolFind pf{{0}, false};
     hsa_agent_t cpu{0};
-    (void)hsa_amd_agent_iterate_memory_pools(hsa_agent_t{q->agent}, find_fine_pool, &pf);
-    (void)hsa_iterate_agents(find_cpu, &cpu);
+    const char *host_only = getenv("MI355X_SVC_HOST_PAGE");
+    if (!(host_only && atoi(host_only))) {
+        (void)hsa_amd_agent_iterate_memory_pools(hsa_agent_t{q->agent}, find_fine_pool, &pf);
+        (void)hsa_iterate_agents(find_cpu, &cpu);
+    }
     if (pf.found && cpu.handle) {
         void *m = nullptr;
         if (hsa_amd_memory_pool_allocate(pf.pool, bytes, 0, &m) == HSA_STATUS_SUCCESS) {

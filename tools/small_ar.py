@@ -22,6 +22,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", default="8,1024,65536,1048576")
     ap.add_argument("--reps", type=int, default=500)
+    ap.add_argument("--paths", default="host", help="comma list of host (per-call launch + host sync), "
+                    "ll (per-call LL kernels), svc (resident LL service)")
     ap.add_argument("--sched", type=int, default=-1, help="hipSetDeviceFlags schedule (1 spin, 2 yield, 4 blocking)")
     args = ap.parse_args()
     if args.sched >= 0:  # before any other HIP call of this process
@@ -40,8 +42,16 @@ def main():
     dist.broadcast_object_list(key, src=0)
     comm = pkg.Comm.create(key[0], rank, world, local)
     comm.set("TIMEOUT_S", 60)
-    try:
-        for nbytes in [int(s) for s in args.sizes.split(",")]:
+    sizes = [int(s) for s in args.sizes.split(",")]
+
+    def run_path(path):
+        comm.set("SVC_MAX_BYTES", max(sizes) if path == "svc" else 0)
+        comm.set("LL_MAX_BYTES", max(sizes) if path == "ll" else 0)
+        if path == "svc" and comm.get("SVC_MAX_BYTES") == 0:
+            if rank == 0:
+                print(json.dumps({"path": "svc", "error": "no resident service on this communicator"}), flush=True)
+            return
+        for nbytes in sizes:
             cnt = nbytes // 4
             x = torch.full((cnt,), float(rank + 1), device="cuda")
             y = torch.empty_like(x)
@@ -55,8 +65,14 @@ def main():
             dt = (time.perf_counter() - t0) / args.reps
             ok = bool(torch.all(y == world * (world + 1) / 2).item())
             if rank == 0:
-                print(json.dumps({"bytes": nbytes, "us_per_call": round(dt * 1e6, 2), "alg": comm.last_algorithm(),
-                                  "n": world, "exact": ok}), flush=True)
+                print(json.dumps({"path": path, "bytes": nbytes, "us_per_call": round(dt * 1e6, 2),
+                                  "alg": comm.last_algorithm(), "n": world, "exact": ok,
+                                  "svc_calls": comm.get("SVC_CALLS"), "svc_launches": comm.get("SVC_LAUNCHES")}),
+                      flush=True)
+
+    try:
+        for path in args.paths.split(","):
+            run_path(path)
         # the buffer-kind vote coll/mi355x adds to every component collective (mi355x_comm_vote):
         # a device-buffer rank only publishes; a host-buffer rank waits for every vote
         for kind, dev in (("vote_device_us", True), ("vote_host_us", False)):

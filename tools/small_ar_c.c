@@ -1,7 +1,8 @@
 /* small_ar_c.c -- small-message MPI_Allreduce latency through the engine's C ABI, no Python in the
  * loop: N processes forked before any HIP call (all on device 0: the one-GPU rehearsal), each times
  * `reps` calls per size, plus mi355x_comm_barrier alone.  Rank 0 prints one JSON line per row.
- * usage: small_ar_c <nranks> <reps>
+ * usage: small_ar_c <nranks> <reps> [paths]   paths: comma list of host (per-call launch + host
+ *        synchronisation), ll (per-call LL kernels), svc (resident LL service); default host
  * build: gcc -O2 -o tools/build/small_ar_c tools/small_ar_c.c -Iinclude -Lompi-release_amd/lib -lmi355x_rt
  *        -Wl,-rpath,'$ORIGIN/../../ompi-release_amd/lib' */
 #include <stdint.h>
@@ -21,7 +22,7 @@ static double now_us(void)
     return t.tv_sec * 1e6 + t.tv_nsec * 1e-3;
 }
 
-static int run(int rank, int n, int reps, const char *key)
+static int run(int rank, int n, int reps, const char *key, const char *paths)
 {
     mi355x_comm_t *c = NULL;
     if (mi355x_set_device(0) || mi355x_comm_create(key, rank, n, 0, &c)) {
@@ -34,6 +35,23 @@ static int run(int rank, int n, int reps, const char *key)
     mi355x_malloc(&r, 1 << 20);
     mi355x_memset_async(s, 0, 1 << 20, NULL);
     mi355x_device_sync();
+    char pl[128];
+    snprintf(pl, sizeof(pl), "%s", paths);
+    for (char *path = strtok(pl, ","); path; path = strtok(NULL, ",")) {
+    const int svc = strcmp(path, "svc") == 0, ll = strcmp(path, "ll") == 0;
+    mi355x_comm_set(c, MI355X_KNOB_SVC_MAX_BYTES, svc ? 1 << 20 : 0);
+    mi355x_comm_set(c, MI355X_KNOB_LL_MAX_BYTES, ll ? 1 << 20 : 0);
+    long on = 0;
+    mi355x_comm_get(c, svc ? MI355X_KNOB_SVC_MAX_BYTES : MI355X_KNOB_LL_MAX_BYTES, &on);
+    if ((svc || ll) && !on) {
+        if (rank == 0) printf("{\"path\": \"%s\", \"error\": \"not available\"}\n", path);
+        continue;
+    }
+    const char *slp = getenv("SMALL_SLEEP_MS");  /* let an idle resident service leave first */
+    if (slp) usleep(atoi(slp) * 1000);
+    long resident = -1;
+    mi355x_comm_get(c, MI355X_KNOB_SVC_RESIDENT, &resident);
+    if (rank == 0) printf("{\"path\": \"%s\", \"svc_resident_before\": %ld}\n", path, resident);
     for (int k = 0; k < 4; ++k) {
         const size_t cnt = sizes[k] / 4;
         for (int i = 0; i < 50; ++i) mi355x_allreduce(c, s, r, cnt, 14, 3, NULL);
@@ -46,8 +64,9 @@ static int run(int rank, int n, int reps, const char *key)
             }
         const double us = (now_us() - t0) / reps;
         if (rank == 0)
-            printf("{\"bytes\": %zu, \"us_per_call\": %.2f, \"alg\": %d, \"n\": %d, \"caller\": \"C\"}\n", sizes[k], us,
-                   mi355x_comm_last_algorithm(c), n);
+            printf("{\"path\": \"%s\", \"bytes\": %zu, \"us_per_call\": %.2f, \"alg\": %d, \"n\": %d, "
+                   "\"caller\": \"C\"}\n", path, sizes[k], us, mi355x_comm_last_algorithm(c), n);
+    }
     }
     mi355x_comm_barrier(c);
     double t0 = now_us();
@@ -63,11 +82,12 @@ static int run(int rank, int n, int reps, const char *key)
 int main(int argc, char **argv)
 {
     const int n = argc > 1 ? atoi(argv[1]) : 2, reps = argc > 2 ? atoi(argv[2]) : 2000;
+    const char *paths = argc > 3 ? argv[3] : "host";
     char key[64];
     snprintf(key, sizeof(key), "lat_%d", (int)getpid());
     for (int r = 1; r < n; ++r)
-        if (fork() == 0) _exit(run(r, n, reps, key));
-    int rc = run(0, n, reps, key);
+        if (fork() == 0) _exit(run(r, n, reps, key, paths));
+    int rc = run(0, n, reps, key, paths);
     for (int r = 1; r < n; ++r) {
         int st = 0;
         wait(&st);
