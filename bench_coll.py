@@ -67,16 +67,21 @@ def extra_legs(args, pkg, torch, comm, world, rank, dev, legs, key):
         if nbytes <= (1 << 20):
             # every data flow at this size, for the thresholds: one-shot LL, host-synchronised with
             # ring orders in one phase (k_ring_all, below ONE_PHASE_MAX_BYTES) and in two
-            one_phase = comm.get("ONE_PHASE_MAX_BYTES")
-            for name, llmax, op1 in (("us_ll", 1 << 20, one_phase), ("us_host", 0, 1 << 20),
-                                     ("us_host_2phase", 0, 0)):
+            # and the resident LL service (coll_svc.hip; reads 0 where this communicator has none)
+            one_phase, svc_max = comm.get("ONE_PHASE_MAX_BYTES"), comm.get("SVC_MAX_BYTES")
+            flows = [("us_ll", 1 << 20, one_phase, 0), ("us_host", 0, 1 << 20, 0), ("us_host_2phase", 0, 0, 0)]
+            if svc_max or comm.get("SVC_LAUNCHES"):
+                flows.append(("us_svc", 0, one_phase, 1 << 20))
+            for name, llmax, op1, svc in flows:
                 comm.set("LL_MAX_BYTES", llmax)
                 comm.set("ONE_PHASE_MAX_BYTES", op1)
+                comm.set("SVC_MAX_BYTES", svc)
                 y.zero_()
                 row[name] = round(_timed(dist, torch, run, reps, 2) * 1e6, 2)
                 row["exact"] = row["exact"] and bool(torch.all(y == want).item())
             comm.set("LL_MAX_BYTES", 0)  # the defaults
             comm.set("ONE_PHASE_MAX_BYTES", one_phase)
+            comm.set("SVC_MAX_BYTES", svc_max)
         sweep.append(row)
         del x, y
     legs["allreduce_sweep_f32"] = sweep

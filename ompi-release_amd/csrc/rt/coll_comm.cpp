@@ -585,9 +585,12 @@ int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **e
 // that cannot be exported, nothing is mapped and *staged is set on every rank alike (callers
 // that pass staged == NULL get an error instead).  force: export regardless of allocation size
 // (the staging buffers themselves).
+static void svc_park(mi355x_comm *c);
+
 int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t sig[4],
              std::vector<std::vector<void *>> &peers, bool *staged, bool force, bool persistent)
 {
+    svc_park(c);  // a host-synchronised call: the resident service steps aside (svc_park)
     c->seq++;
     if (staged) *staged = false;
     RankSlot &s = c->ctrl->slot[c->rank];
@@ -1044,6 +1047,7 @@ static int ll_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s)
     default: a.recv_mask = all; break;
     }
     if (svc_usable(c, a.nbytes)) return svc_run(c, a, op, type, s);
+    svc_park(c);  // a per-call LL launch: the resident service steps aside as for the host flows
     const uint64_t seq = ++c->ll_seq;
     const size_t par = seq & 1, me = (size_t)c->rank;
     a.seq = seq;
@@ -1158,7 +1162,8 @@ static int svc_launch(mi355x_comm *c, uint64_t first)
 {
     SvcArgs g;
     std::memset(&g, 0, sizeof(g));
-    c->svc_page->ctr = 0;  // not resident: nothing else touches it
+    c->svc_page->ctr = 0;  // not resident: nothing else touches them
+    c->svc_page->go = 0;
     _mm_sfence();
     g.page = c->svc_page;
     g.done = svc_done_word(c);
@@ -1172,6 +1177,7 @@ static int svc_launch(mi355x_comm *c, uint64_t first)
     g.n = c->size;
     g.me = c->rank;
     g.nwg = c->svc_nwg;
+    g.trace = c->svc_trace;
     if (svc_dispatch(c->svcq, g, c->svc_nwg)) return set_error(MI355X_ERR_HIP, "service dispatch: the previous launch is still resident");
     c->svc_launches++;
     return MI355X_SUCCESS;
@@ -1186,6 +1192,17 @@ static void svc_stop(mi355x_comm *c)
     if (!svc_wait_exit(c->svcq, c->timeout_s + 5.0))
         fprintf(stderr, "[mi355x r%d] resident service did not leave\n", c->rank);
     svc_ring(c, c->ll_seq);  // back to the last call's number: the next launch waits for ll_seq + 1
+}
+
+// A call that takes a host-synchronised flow asks a resident service to leave, without waiting:
+// with several processes on one GPU (the one-GPU rehearsal) a resident kernel slows every other
+// launch of every process on the device (17 -> 54 us per small host-path allreduce,
+// profiles/r03_queue_probe.jsonl), so the service stays only while small calls keep coming.  If
+// the next service call rings the doorbell before the kernel has read the request, the kernel
+// simply serves it; otherwise it has left and the call relaunches it.
+static void svc_park(mi355x_comm *c)
+{
+    if (c->svc_ok && c->svcq && svc_resident(c->svcq)) svc_ring(c, kSvcQuit);
 }
 
 // one LL call through the service: `a` carries the call (mode, buffers, program, masks)
@@ -1252,9 +1269,30 @@ static int svc_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s)
     return MI355X_SUCCESS;
 }
 
+// MI355X_SVC_TRACE=1: mean microseconds between the stamped stages over the traced calls
+static void svc_trace_report(mi355x_comm *c)
+{
+    if (!c->svc_trace) return;
+    double acc[kSvcTraceCols] = {0};
+    int nrows = 0;
+    for (int r = 0; r < kSvcTraceCalls; ++r) {
+        const uint64_t *row = c->svc_trace + (size_t)r * kSvcTraceCols;
+        if (!row[0] || !row[6] || row[6] < row[1]) continue;
+        for (int k = 2; k <= 6; ++k) acc[k] += (double)(row[k] - row[k - 1]) * 0.01;  // 100 MHz -> us
+        ++nrows;
+    }
+    if (nrows)
+        fprintf(stderr, "[mi355x r%d] resident service, %d traced calls, mean us: door->descriptor %.2f, "
+                "->pushed %.2f, ->received %.2f, ->stored %.2f, ->completed %.2f\n", c->rank, nrows,
+                acc[2] / nrows, acc[3] / nrows, acc[4] / nrows, acc[5] / nrows, acc[6] / nrows);
+    (void)hipHostFree(c->svc_trace);
+    c->svc_trace = nullptr;
+}
+
 static void svc_release(mi355x_comm *c)
 {
     svc_stop(c);
+    svc_trace_report(c);
     if (c->svcq) {
         svc_queue_destroy(c->svcq);
         delete c->svcq;
@@ -1289,6 +1327,10 @@ static bool svc_open(mi355x_comm *c)
     c->svc_page = static_cast<SvcPage *>(pg);
     if (hipHostMalloc((void **)&c->svc_host, 4096, hipHostMallocCoherent) != hipSuccess) return false;
     std::memset(c->svc_host, 0, 4096);
+    if (env_double("MI355X_SVC_TRACE", 0.0) != 0.0) {
+        const size_t tb = sizeof(uint64_t) * kSvcTraceCalls * kSvcTraceCols;
+        if (hipHostMalloc((void **)&c->svc_trace, tb, hipHostMallocCoherent) == hipSuccess) std::memset(c->svc_trace, 0, tb);
+    }
     return true;
 }
 

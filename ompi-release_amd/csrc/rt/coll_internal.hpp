@@ -124,6 +124,9 @@ struct SvcPage {                      // the doorbell page
     uint64_t pad0[15];
     uint64_t ctr;                     // workgroups done, zeroed by the host before every launch
     uint64_t pad1[15];
+    uint64_t go;                      // workgroup 0's verdict on call `want`: want = serve it, kSvcQuit =
+                                      // leave (zeroed by the host before every launch)
+    uint64_t pad2[15];
     SvcCall call;
 };
 struct SvcArgs {                      // fixed for one launch
@@ -135,7 +138,12 @@ struct SvcArgs {                      // fixed for one launch
     uint64_t first;                   // the call number this launch serves first
     uint64_t slot_gran, idle_ticks, timeout_ticks;
     int32_t n, me, nwg, probe;        // probe: return at once (loads the code object)
+    uint64_t *trace;                  // NULL, or kSvcTraceCalls rows of kSvcTraceCols words (MI355X_SVC_TRACE)
 };
+// MI355X_SVC_TRACE=1: workgroup 0 stamps s_memrealtime (100 MHz) at each stage of a call into row
+// seq % kSvcTraceCalls: seq, door seen, descriptor in LDS, slices pushed, peers' slices received,
+// results stored, completion stored
+constexpr int kSvcTraceCalls = 1024, kSvcTraceCols = 8;
 
 // Pipelined allreduce (coll_pipe.hip): fold of my ring block and pulls of the peers' blocks in
 // one launch, chunk by chunk, with per-chunk ready flags (uncached region, written by the

@@ -22,27 +22,43 @@ __device__ __forceinline__ void ll_store(uint64_t *p, uint64_t v)
 // SYS (the resident service, which has no kernel boundary between calls): the caller's input is
 // read and the result written with the system-coherent cache policy (sc0 sc1, raw buffer ops) --
 // loads skip this CU's L1, which may still hold the lines of an earlier call's input, and stores
-// go through the XCD's L2 to memory, so the call's results need no L2 write-back fence
+// go through the XCD's L2 to memory, so the call's results need no L2 write-back fence.
+// A buffer resource lives in scalar registers: it is built from a workgroup-uniform base (made
+// scalar with readfirstlane -- the service keeps its arguments in LDS, where the compiler cannot
+// see they are uniform; a per-lane base would compile to a loop over the wave's distinct values)
+// and each lane passes its own byte offset.
 constexpr int kLLSysCoherent = 1 | 16;  // gfx950 cache-policy bits: sc0 (1) | sc1 (16)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t ll_rsrc(const void *p)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ll_rsrc(const void *uniform_base)
 {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, 16, 0x00020000);
+    const uint64_t u = (uint64_t)(uintptr_t)uniform_base;
+    const uint64_t s = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(u >> 32)) << 32) |
+                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(s), 0, 0x7fffffff, 0x00020000);
 }
 
-// up to 16 bytes of src at `off` (len valid bytes) as 4 little-endian words (zero padded)
-template <bool SYS = false> __device__ __forceinline__ void ll_read16(const char *src, size_t len, uint32_t w[4])
+// up to 16 bytes at base + off (len valid bytes) as 4 little-endian words (zero padded); base is
+// uniform across the workgroup
+template <bool SYS = false>
+__device__ __forceinline__ void ll_read16(const char *base, size_t off, size_t len, uint32_t w[4])
 {
+    const char *src = base + off;
     if constexpr (SYS) {
-        const __amdgpu_buffer_rsrc_t rs = ll_rsrc(src);
+        const __amdgpu_buffer_rsrc_t rs = ll_rsrc(base);
         if (len == 16 && (((uintptr_t)src) & 15) == 0) {
-            const u32x4l v = __builtin_amdgcn_raw_buffer_load_b128(rs, 0, 0, kLLSysCoherent);
+            const u32x4l v = __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)off, 0, kLLSysCoherent);
             w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
+            return;
+        }
+        if ((((uintptr_t)src) & 3) == 0 && (len & 3) == 0) {  // whole words
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                w[i] = (size_t)(4 * i) < len ? __builtin_amdgcn_raw_buffer_load_b32(rs, (unsigned)(off + 4 * i), 0, kLLSysCoherent) : 0;
             return;
         }
         unsigned char b[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i)
-            b[i] = (size_t)i < len ? __builtin_amdgcn_raw_buffer_load_b8(rs, (unsigned)i, 0, kLLSysCoherent) : 0;
+            b[i] = (size_t)i < len ? __builtin_amdgcn_raw_buffer_load_b8(rs, (unsigned)(off + i), 0, kLLSysCoherent) : 0;
         __builtin_memcpy(w, b, 16);
         return;
     }
@@ -56,19 +72,27 @@ template <bool SYS = false> __device__ __forceinline__ void ll_read16(const char
     for (int i = 0; i < 16; ++i) b[i] = (size_t)i < len ? (unsigned char)src[i] : 0;
     __builtin_memcpy(w, b, 16);
 }
-template <bool SYS = false> __device__ __forceinline__ void ll_write16(char *dst, size_t len, const uint32_t w[4])
+template <bool SYS = false>
+__device__ __forceinline__ void ll_write16(char *base, size_t off, size_t len, const uint32_t w[4])
 {
+    char *dst = base + off;
     if constexpr (SYS) {
-        const __amdgpu_buffer_rsrc_t rs = ll_rsrc(dst);
+        const __amdgpu_buffer_rsrc_t rs = ll_rsrc(base);
         if (len == 16 && (((uintptr_t)dst) & 15) == 0) {
             u32x4l v;
             v.x = w[0], v.y = w[1], v.z = w[2], v.w = w[3];
-            __builtin_amdgcn_raw_buffer_store_b128(v, rs, 0, 0, kLLSysCoherent);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, (unsigned)off, 0, kLLSysCoherent);
+            return;
+        }
+        if ((((uintptr_t)dst) & 3) == 0 && (len & 3) == 0) {  // whole words (4- / 8-B elements)
+            for (size_t i = 0; i < len / 4; ++i)
+                __builtin_amdgcn_raw_buffer_store_b32(w[i], rs, (unsigned)(off + 4 * i), 0, kLLSysCoherent);
             return;
         }
         unsigned char b[16];
         __builtin_memcpy(b, w, 16);
-        for (size_t i = 0; i < len; ++i) __builtin_amdgcn_raw_buffer_store_b8(b[i], rs, (unsigned)i, 0, kLLSysCoherent);
+        for (size_t i = 0; i < len; ++i)
+            __builtin_amdgcn_raw_buffer_store_b8(b[i], rs, (unsigned)(off + i), 0, kLLSysCoherent);
         return;
     }
     if (len == 16 && (((uintptr_t)dst) & 15) == 0) {
@@ -100,8 +124,9 @@ __device__ __forceinline__ LLBlock ll_block(const LLArgs &a, size_t chunk)
     return k;
 }
 
-// steps 1-2; false on timeout
-template <bool SYS = false> static __device__ bool ll_push(const LLArgs &a, const LLBlock &k)
+// step 1: every peer this rank pushes to has acknowledged the call two calls back; false on
+// timeout (the error word is set).  Every thread of the workgroup calls it.
+static __device__ bool ll_wait_acks(const LLArgs &a)
 {
     __shared__ int timed_out;
     const int t = (int)threadIdx.x;
@@ -119,39 +144,72 @@ template <bool SYS = false> static __device__ bool ll_push(const LLArgs &a, cons
         }
     }
     __syncthreads();
-    if (timed_out) return false;
-    if (a.src && k.ngran) {  // (bcast: only the root has data to push)
-        uint32_t w[4];
-        ll_read16<SYS>(static_cast<const char *>(a.src) + k.off, k.len, w);
-        const size_t g0 = k.off / 4;
-        for (int q = 0; q < a.n; ++q) {
-            if (!((a.push_mask >> q) & 1u)) continue;
-            uint64_t *d = a.peer_data[q] + g0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (i < k.ngran) ll_store(d + i, ((uint64_t)k.tag << 32) | w[i]);
+    return !timed_out;
+}
+
+// this thread's 16 B of slice k (read with ll_read16<SYS>)
+template <bool SYS = false> __device__ __forceinline__ void ll_read_slice(const LLArgs &a, const LLBlock &k, uint32_t w[4])
+{
+    w[0] = w[1] = w[2] = w[3] = 0;
+    if (a.src && k.ngran) ll_read16<SYS>(static_cast<const char *>(a.src), k.off, k.len, w);
+}
+
+// step 2: the 16 B as granules into slot (parity, me) of every peer in push_mask
+__device__ __forceinline__ void ll_push_slice(const LLArgs &a, const LLBlock &k, const uint32_t w[4])
+{
+    if (!a.src || !k.ngran) return;  // (bcast: only the root has data to push)
+    const size_t g0 = k.off / 4;
+    for (int q = 0; q < a.n; ++q) {
+        if (!((a.push_mask >> q) & 1u)) continue;
+        uint64_t *d = a.peer_data[q] + g0;
+        if (k.ngran == 4) {
+            // two granules per 16-B store (32-B aligned: g0 is a multiple of 4); each 8-B half
+            // carries its own tag, so a store seen half-landed is only partly accepted
+            const __amdgpu_buffer_rsrc_t rs = ll_rsrc(a.peer_data[q]);
+            const unsigned o = (unsigned)(g0 * 8);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4l{w[0], k.tag, w[1], k.tag}, rs, o, 0, kLLSysCoherent);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4l{w[2], k.tag, w[3], k.tag}, rs, o + 16, 0, kLLSysCoherent);
+            continue;
         }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (i < k.ngran) ll_store(d + i, ((uint64_t)k.tag << 32) | w[i]);
     }
+}
+
+// steps 1-2 for one slice (the input read is issued before the acknowledgement wait); false on timeout
+template <bool SYS = false> static __device__ bool ll_push(const LLArgs &a, const LLBlock &k)
+{
+    uint32_t w[4];
+    ll_read_slice<SYS>(a, k, w);
+    if (!ll_wait_acks(a)) return false;
+    ll_push_slice(a, k, w);
     return true;
 }
 
-// step 3 for the sources in qmask (<= 8 of them, slot index = rank): w[q] gets rank q's 16 B
+// step 3 for the sources in qmask (<= 8 of them, slot index = rank): w[q] gets rank q's 16 B.
+// Granules are read in pairs (16-B loads: {payload, tag, payload, tag}), each half checked.
 static __device__ bool ll_recv(const LLArgs &a, const LLBlock &k, uint64_t qmask, uint32_t (&w)[8][4])
 {
     if (!k.ngran) return true;
     const size_t g0 = k.off / 4;
+    const int npair = (k.ngran + 1) / 2;  // pairs holding this thread's granules
+    auto load_pair = [&](int q, int h) {
+        // (a pair past ngran: the slot holds it, so the read stays inside the region)
+        const u32x4l v = __builtin_amdgcn_raw_buffer_load_b128(ll_rsrc(a.my_data + (size_t)q * a.slot_gran),
+                                                               (unsigned)(g0 * 8 + 16 * h), 0, kLLSysCoherent);
+        w[q][2 * h] = v.x;
+        w[q][2 * h + 1] = v.z;
+        const bool lo = v.y == k.tag, hi = v.w == k.tag || 2 * h + 1 >= k.ngran;
+        return lo && hi;
+    };
     uint32_t pending = 0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         if (!((qmask >> q) & 1u)) continue;
-        const uint64_t *p = a.my_data + (size_t)q * a.slot_gran + g0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (i >= k.ngran) continue;
-            const uint64_t v = ll_load(p + i);
-            w[q][i] = (uint32_t)v;
-            if ((uint32_t)(v >> 32) != k.tag) pending |= 1u << (q * 4 + i);
-        }
+        for (int h = 0; h < 2; ++h)
+            if (h < npair && !load_pair(q, h)) pending |= 1u << (q * 2 + h);
     }
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     unsigned spins = 0;
@@ -160,12 +218,8 @@ static __device__ bool ll_recv(const LLArgs &a, const LLBlock &k, uint64_t qmask
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                if (!((pending >> (q * 4 + i)) & 1u)) continue;
-                const uint64_t v = ll_load(a.my_data + (size_t)q * a.slot_gran + g0 + i);
-                w[q][i] = (uint32_t)v;
-                if ((uint32_t)(v >> 32) == k.tag) pending &= ~(1u << (q * 4 + i));
-            }
+            for (int h = 0; h < 2; ++h)
+                if (((pending >> (q * 2 + h)) & 1u) && load_pair(q, h)) pending &= ~(1u << (q * 2 + h));
         }
         if ((++spins & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
             __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -266,7 +320,7 @@ __device__ __forceinline__ void ll_reduce_out(const LLArgs &a, const LLBlock &k,
     }
     uint32_t ow[4];
     __builtin_memcpy(ow, &r, 16);
-    ll_write16<SYS>(static_cast<char *>(a.dst) + k.off, k.len, ow);
+    ll_write16<SYS>(static_cast<char *>(a.dst), k.off, k.len, ow);
 }
 
 // allgather (slot q -> dst + q*nbytes) and bcast (slot root -> dst, non-roots)
@@ -279,14 +333,14 @@ __device__ __forceinline__ void ll_copy_out(const LLArgs &a, const LLBlock &k, c
 #pragma unroll
         for (int q = 0; q < 8; ++q)
             if (q == a.root) __builtin_memcpy(v, w[q], 16);
-        ll_write16<SYS>(dst + k.off, k.len, v);
+        ll_write16<SYS>(dst, k.off, k.len, v);
     } else {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             if (!((a.recv_mask >> q) & 1u)) continue;
             char *d = dst + (size_t)q * a.nbytes;
             if (q == a.me && static_cast<const char *>(a.src) == d) continue;  // in place
-            ll_write16<SYS>(d + k.off, k.len, w[q]);
+            ll_write16<SYS>(d, k.off, k.len, w[q]);
         }
     }
 }

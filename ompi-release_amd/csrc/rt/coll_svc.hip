@@ -31,22 +31,51 @@ namespace mi355x {
 static_assert(sizeof(SvcCall) % 8 == 0, "the descriptor is copied in 8-byte words");
 constexpr int kSvcCallWords = (int)(sizeof(SvcCall) / 8);
 static_assert(kSvcCallWords <= kSvcThreads, "one word per thread");
+constexpr int kSvcPass = 4;  // slices whose inputs one workgroup reads at once
 
-// one out-of-line function per slot (inlining all of them into one body makes the compiler's
-// register allocation take tens of minutes)
+// Step 3's second half for every slice of this workgroup: receive the peers' granules, then the
+// reference program per element (or the copy).  One out-of-line function per (op, type) slot,
+// entered once per call: the call's slot decides which (inlining every slot's evaluation into one
+// body makes the compiler's register allocation take tens of minutes).  Returns 1 on a timeout.
 template <class F>
-static __device__ __noinline__ void svc_slot(const LLArgs &a, const LLBlock &k, const uint32_t (&w)[8][4])
+static __device__ __noinline__ int svc_finish(const LLArgs &a, uint64_t nchunks, uint64_t stride, uint64_t *tr)
 {
-    ll_reduce_out<F, true>(a, k, w);
+    for (uint64_t c = blockIdx.x; c < nchunks; c += stride) {
+        const LLBlock k = ll_block(a, c);
+        uint32_t w[8][4];
+        int bad = 0;
+        if (k.ngran) {
+            bad = !ll_recv(a, k, a.recv_mask, w);
+            if (tr && threadIdx.x == 0 && c == blockIdx.x) tr[4] = __builtin_amdgcn_s_memrealtime();
+            if (!bad) {
+                if constexpr (F::kCopy)
+                    ll_copy_out<true>(a, k, w);
+                else
+                    ll_reduce_out<F, true>(a, k, w);
+            }
+        }
+        if (__syncthreads_or(bad)) return 1;
+    }
+    return 0;
 }
 
-// the evaluation for the call's (op, type): one branch per slot with a GPU kernel
-static __device__ void svc_reduce_out(int op, int type, const LLArgs &a, const LLBlock &k, const uint32_t (&w)[8][4])
+struct SvcCopy {  // allgather / bcast: no evaluation
+    static constexpr bool kCopy = true;
+};
+template <class F> struct SvcReduce : F {
+    static constexpr bool kCopy = false;
+};
+
+static __device__ int svc_finish_call(int op, int type, bool copy, const LLArgs &a, uint64_t nchunks, uint64_t stride,
+                                      uint64_t *tr)
 {
+    if (copy) return svc_finish<SvcCopy>(a, nchunks, stride, tr);
+    int rc = 0;
     for_each_slot([&](auto tag, int o, int t) {
         using F = typename decltype(tag)::type;
-        if (o == op && t == type) svc_slot<F>(a, k, w);
+        if (o == op && t == type) rc = svc_finish<SvcReduce<F>>(a, nchunks, stride, tr);
     });
+    return rc;
 }
 
 } // namespace mi355x
@@ -62,31 +91,60 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
     const int t = (int)threadIdx.x;
     SvcPage *page = const_cast<SvcPage *>(g.page);
     uint64_t want = g.first;
-    uint64_t ctr_base = 0;  // the doorbell page's workgroup counter before this call
     uint64_t idle0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-        // 1. the doorbell
+        // 1. the doorbell.  Workgroup 0 alone decides whether the next call is served or the
+        // service leaves (quit request, idle, a number out of turn) and publishes the verdict in
+        // `go`; the others follow it -- workgroups deciding on their own could split over a call
+        // (some serving it, some gone), and a call served in part never completes
         if (t == 0) {
             uint64_t v;
-            for (;;) {
-                v = __hip_atomic_load(&page->door, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (v >= want) break;
-                __builtin_amdgcn_s_sleep(2);
-                if (__builtin_amdgcn_s_memrealtime() - idle0 > g.idle_ticks) {
-                    v = kSvcQuit;
-                    break;
+            if (blockIdx.x == 0) {
+                for (;;) {
+                    v = __hip_atomic_load(&page->door, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (v >= want) break;
+                    __builtin_amdgcn_s_sleep(2);
+                    if (__builtin_amdgcn_s_memrealtime() - idle0 > g.idle_ticks) {
+                        v = kSvcQuit;
+                        break;
+                    }
                 }
+                if (v != want) v = kSvcQuit;
+                __hip_atomic_store(&page->go, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            } else {
+                for (;;) {  // (bounded too: never longer than the leader's idle limit plus a timeout)
+                    v = __hip_atomic_load(&page->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (v >= want) break;
+                    __builtin_amdgcn_s_sleep(2);
+                    if (__builtin_amdgcn_s_memrealtime() - idle0 > g.idle_ticks + g.timeout_ticks) {
+                        v = kSvcQuit;
+                        break;
+                    }
+                }
+                // (a follower that no call has needed since it last looked may find the verdict of
+                // a later call: those calls completed without it; it joins this one)
             }
             s_door = v;
         }
         __syncthreads();
-        if (s_door != want) break;  // kSvcQuit, idle, or a number out of turn (never posted so)
+        if (s_door == kSvcQuit) break;
+        want = s_door;
+        uint64_t *tr = (g.trace && blockIdx.x == 0) ? g.trace + (want % kSvcTraceCalls) * kSvcTraceCols : nullptr;
+        if (tr && t == 0) {
+            tr[0] = want;
+            tr[1] = __builtin_amdgcn_s_memrealtime();
+        }
         // 2. the descriptor (stored before the doorbell) into LDS
         if (t < kSvcCallWords)
             reinterpret_cast<uint64_t *>(&sc)[t] = __hip_atomic_load(reinterpret_cast<const uint64_t *>(&page->call) + t,
                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __syncthreads();
-        if (sc.seq != want) break;
+        if (sc.seq != want) {
+            // the page already holds a later call: `want` completed without this (follower)
+            // workgroup -- it was not one of its participants -- so wait for the next verdict
+            ++want;
+            continue;
+        }
         const int n = g.n, me = g.me;
         const uint64_t par = want & 1;
         if (t == 0) {
@@ -121,63 +179,72 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
         }
         if (t < kTreeSteps) a.steps[t] = sc.steps[t];
         __syncthreads();
+        if (tr && t == 0) tr[2] = __builtin_amdgcn_s_memrealtime();
         // 3. my slices.  The inputs (written by kernels that completed before the call) are read
         // with system-coherent loads, the results stored write-through (ll_read16 / ll_write16<SYS>):
         // no acquire or release fence per call.  Workgroups beyond the call's slice count sit it out.
         const uint64_t nchunks = (a.nbytes + kLLChunk - 1) / kLLChunk;
         const uint64_t part = nchunks < (uint64_t)g.nwg ? nchunks : (uint64_t)g.nwg;
         if (blockIdx.x >= part) {
-            if (part > 1) ctr_base += part;
             ++want;
             idle0 = __builtin_amdgcn_s_memrealtime();
             continue;
         }
         const bool reduce = a.mode == LL_AR || a.mode == LL_RED;
         const bool evaluate = reduce ? !(a.mode == LL_RED && me != a.root) : a.recv_mask != 0;
+        // push every slice of mine (inputs read kSvcPass slices at a time, so their latencies
+        // overlap; the acknowledgement wait once, behind the first reads), then receive and finish
+        // them: a workgroup with several slices waits one peer round trip, not one per slice
         int failed = 0;
-        for (uint64_t c = blockIdx.x; c < nchunks; c += (uint64_t)g.nwg) {
-            const LLBlock k = ll_block(a, c);
-            if (!ll_push<true>(a, k)) {
-                failed = 1;
-                break;
+        const uint64_t stride = (uint64_t)g.nwg;
+        for (uint64_t c0 = blockIdx.x; c0 < nchunks && !failed; c0 += stride * kSvcPass) {
+            uint32_t w[kSvcPass][4];
+#pragma unroll
+            for (int p = 0; p < kSvcPass; ++p) {
+                const uint64_t c = c0 + (uint64_t)p * stride;
+                if (c < nchunks) ll_read_slice<true>(a, ll_block(a, c), w[p]);
             }
-            uint32_t w[8][4];
-            int bad = 0;
-            if (evaluate && k.ngran) {
-                if (!ll_recv(a, k, a.recv_mask, w))
-                    bad = 1;
-                else if (reduce)
-                    svc_reduce_out(sc.op, sc.type, a, k, w);
-                else
-                    ll_copy_out<true>(a, k, w);
-            }
-            if (__syncthreads_or(bad)) {
-                failed = 1;
-                break;
+            if (c0 == blockIdx.x && !ll_wait_acks(a)) failed = 1;
+            if (failed) break;
+#pragma unroll
+            for (int p = 0; p < kSvcPass; ++p) {
+                const uint64_t c = c0 + (uint64_t)p * stride;
+                if (c < nchunks) ll_push_slice(a, ll_block(a, c), w[p]);
             }
         }
+        if (tr && t == 0) tr[3] = __builtin_amdgcn_s_memrealtime();
+        if (!failed && evaluate) failed = svc_finish_call(sc.op, sc.type, !reduce, a, nchunks, stride, tr);
         // 4. every store of the workgroup has reached memory; count; the last participant
         // acknowledges the call to every peer and completes it for the host
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (tr && t == 0) tr[5] = __builtin_amdgcn_s_memrealtime();
         if (t == 0) {
             bool last = part == 1;
             if (!last) {
                 const uint64_t old =
                     __hip_atomic_fetch_add(&page->ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                last = old + 1 == ctr_base + part;
+                last = old + 1 == part;
+                // the last participant zeroes the counter for the next call, and the reset has
+                // landed before the completion word does (the next call is posted after it)
+                if (last) {
+                    __hip_atomic_store(&page->ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
             }
             if (!failed && last) {
                 for (int q = 0; q < n; ++q)
                     if (q != me) ll_store(a.peer_ack[q], want);
                 __hip_atomic_store(g.done, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
+            if (tr) tr[6] = __builtin_amdgcn_s_memrealtime();
         }
         if (failed) break;  // the error word is set; the host ends the service
-        if (part > 1) ctr_base += part;
         ++want;
         idle0 = __builtin_amdgcn_s_memrealtime();
     }
+    // whatever made the leader leave (quit, idle, a failed call), the followers leave with it
+    if (blockIdx.x == 0 && t == 0) __hip_atomic_store(&page->go, kSvcQuit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 namespace mi355x {

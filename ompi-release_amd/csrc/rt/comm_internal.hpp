@@ -252,7 +252,11 @@ struct mi355x_comm {
     // rank served by a kernel resident on a private HSA queue.  One service per process and GPU; the
     // communicator that finds it free on every rank at creation owns it (svc_ok), every other
     // communicator uses the per-call paths
-    size_t svc_max = 0;                           // MI355X_SVC_MAX_BYTES / MI355X_KNOB_SVC_MAX_BYTES
+    // MI355X_SVC_MAX_BYTES / MI355X_KNOB_SVC_MAX_BYTES: 32 KiB by default, where the service beat the
+    // host-synchronised path at every size measured (one-GPU rehearsal, np = 2: 9.8-11.7 vs
+    // 16.7-17.3 us up to 16 KiB, even at 64 KiB; np = 4: 15-17 vs 22-24 us up to 16 KiB, even at
+    // 64 KiB; profiles/r03_svc_latency.jsonl)
+    size_t svc_max = (size_t)32 << 10;
     bool svc_ok = false;
     bool svc_owner = false;                       // this process's service is claimed by this communicator
     mi355x::SvcQueue *svcq = nullptr;
@@ -260,8 +264,11 @@ struct mi355x_comm {
     bool svc_page_dev = false;                    // the page is fine-grained device memory (else pinned host)
     uint64_t *svc_host = nullptr;                 // pinned host words: [0] call completed, [1] error word
     int svc_nwg = 8;                              // workgroups of the service (8 x 4 KiB slices per pass)
-    double svc_idle_s = 0.05;                     // the service leaves after this long without a call
+    // the service leaves after this long without a call (MI355X_SVC_IDLE_MS, default 1 ms): a burst
+    // of small calls keeps it resident, a call after a longer gap relaunches it
+    double svc_idle_s = 0.001;
     uint64_t svc_calls = 0, svc_launches = 0;
+    uint64_t *svc_trace = nullptr;                // MI355X_SVC_TRACE=1: stage stamps (pinned host), printed at destroy
     // pipelined allreduce (coll_pipe.hip): per-chunk ready flags in an uncached region that
     // every peer writes into (row q = flags raised by rank q), and the work-queue counter
     char *pipe_base = nullptr;

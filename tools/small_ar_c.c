@@ -29,7 +29,15 @@ static int run(int rank, int n, int reps, const char *key, const char *paths)
         fprintf(stderr, "rank %d: %s\n", rank, mi355x_last_error());
         return 1;
     }
-    const size_t sizes[] = {8, 1024, 65536, 1 << 20};
+    size_t sizes[16] = {8, 1024, 65536, 1 << 20};
+    int nsizes = 4;
+    const char *ss = getenv("SMALL_SIZES");  /* comma list of byte counts (<= 1 MiB) */
+    if (ss) {
+        char buf[256];
+        snprintf(buf, sizeof(buf), "%s", ss);
+        nsizes = 0;
+        for (char *p = strtok(buf, ","); p && nsizes < 16; p = strtok(NULL, ",")) sizes[nsizes++] = strtoull(p, NULL, 10);
+    }
     void *s = NULL, *r = NULL;
     mi355x_malloc(&s, 1 << 20);
     mi355x_malloc(&r, 1 << 20);
@@ -52,7 +60,7 @@ static int run(int rank, int n, int reps, const char *key, const char *paths)
     long resident = -1;
     mi355x_comm_get(c, MI355X_KNOB_SVC_RESIDENT, &resident);
     if (rank == 0) printf("{\"path\": \"%s\", \"svc_resident_before\": %ld}\n", path, resident);
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < nsizes; ++k) {
         const size_t cnt = sizes[k] / 4;
         for (int i = 0; i < 50; ++i) mi355x_allreduce(c, s, r, cnt, 14, 3, NULL);
         mi355x_comm_barrier(c);
