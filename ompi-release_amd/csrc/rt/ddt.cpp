@@ -237,6 +237,8 @@ static int ddt_move(const mi355x_ddt_t *d, bool pack, size_t count, void *mem, s
     dv.disp = d->ddisp;
     dv.len = d->dlen;
     dv.pfx = d->dpfx;
+    dv.pfx_host = d->pfx.data();
+    dv.len_host = d->len.data();
     dv.nruns = (int)d->disp.size();
     dv.nblk = d->nblk;
     dv.stride = d->stride;

@@ -16,6 +16,8 @@ struct DdtDev {
     const int64_t *disp;   // run displacement inside a block (device array)
     const int64_t *len;    // run length in bytes
     const int64_t *pfx;    // packed offset of the run inside a block
+    const int64_t *pfx_host;  // the packed offsets and lengths in host memory
+    const int64_t *len_host;
     int nruns;
     int64_t nblk, stride, extent;
     int64_t blk_bytes, inst_bytes;

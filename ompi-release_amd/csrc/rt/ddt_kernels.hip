@@ -14,6 +14,8 @@
 // are not 16-B multiples, window edges) falls back to bytes.  Optional checksum: the sum of the
 // stream's native 32-bit words (opal_uicsum_partial, opal/util/crc.c:921) -- additive over
 // windows, so per-fragment sums add up to the whole-message convertor checksum.
+#include <algorithm>
+
 #include "ddt_internal.hpp"
 #include "rt_internal.hpp"
 
@@ -638,16 +640,21 @@ static void launch_units_w(int w, const UnitArgs &a, unsigned blocks, size_t lds
 // memory slots (the unit kernel stores W bytes, its wide form unaligned 16-B vectors: both slower,
 // profiles/r03_unpack_ceiling.jsonl) and read the packed side with 16-B loads at W-aligned
 // addresses; the run's unaligned head and tail move as W-byte units.  Needs the base, extent and
-// stride 16-B aligned (a run's misalignment is then its displacement's), whole instances and runs
-// of balanced length (ddt_move checks kRunsMinBytes / kRunsMaxSkew).
+// stride 16-B aligned (a run's misalignment is then its displacement's) and runs of balanced length
+// (ddt_move checks kRunsMinBytes / kRunsMaxSkew).  Any W-aligned window [pos, pos + bytes) of the
+// packed stream (the convertor's set_position fragments, a16): the waves cover the runs from the
+// one holding byte pos to the one holding its last byte (found on the host, once per launch), and
+// each wave clips its run to the window.
 struct RunsArgs {
     char *mem;
-    const char *packed;
+    const char *packed;  // the window's bytes (packed stream offset pos)
     const int64_t *disp, *len, *pfx;
     int64_t stride, extent, blk_bytes, inst_bytes;
-    FastDiv per_inst;   // runs per instance (nblk * nruns)
+    int64_t pos, end;    // the window in the packed stream
+    FastDiv per_inst;    // runs per instance (nblk * nruns)
     FastDiv nruns;
-    uint32_t nwaves;    // runs in the message
+    uint32_t q0;         // the window's first run (message-wide index)
+    uint32_t nwaves;     // runs the window touches
 };
 
 constexpr int64_t kRunsMinBytes = 512;   // average run length the wave-per-run unpack needs
@@ -657,16 +664,21 @@ template <int W>
 __global__ __launch_bounds__(256) void k_ddt_runs_unpack(RunsArgs a)
 {
     typedef typename SlotT<W>::type S;
-    const uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (q >= a.nwaves) return;
+    const uint32_t wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (wv >= a.nwaves) return;
+    const uint32_t q = a.q0 + wv;
     const int lane = threadIdx.x & 63;
     const uint32_t k = fdiv(q, a.per_inst);
     const uint32_t rem = q - k * a.per_inst.d;
     const uint32_t j = fdiv(rem, a.nruns);
     const uint32_t r = rem - j * a.nruns.d;
-    const int64_t len = a.len[r];
-    char *m = a.mem + (int64_t)k * a.extent + (int64_t)j * a.stride + a.disp[r];
-    const char *pk = a.packed + (int64_t)k * a.inst_bytes + (int64_t)j * a.blk_bytes + a.pfx[r];
+    // the run in the packed stream, clipped to the window
+    const int64_t P = (int64_t)k * a.inst_bytes + (int64_t)j * a.blk_bytes + a.pfx[r];
+    const int64_t lo = a.pos > P ? a.pos - P : 0;
+    const int64_t hi = a.end - P < a.len[r] ? a.end - P : a.len[r];
+    const int64_t len = hi - lo;
+    char *m = a.mem + (int64_t)k * a.extent + (int64_t)j * a.stride + a.disp[r] + lo;
+    const char *pk = a.packed + (P + lo - a.pos);
     int64_t h = (16 - ((uintptr_t)m & 15)) & 15;
     if (h > len) h = len;
     const int64_t end = h + ((len - h) & ~(int64_t)15);
@@ -677,16 +689,27 @@ __global__ __launch_bounds__(256) void k_ddt_runs_unpack(RunsArgs a)
         *reinterpret_cast<S *>(m + end + lane * W) = *reinterpret_cast<const S *>(pk + end + lane * W);
 }
 
+// message-wide index of the run holding packed byte x (x inside the message)
+static uint64_t run_at(const DdtDev &d, int64_t x)
+{
+    const int64_t k = x / d.inst_bytes, in_inst = x - k * d.inst_bytes;
+    const int64_t j = in_inst / d.blk_bytes, in_blk = in_inst - j * d.blk_bytes;
+    const int64_t r = (int64_t)(std::upper_bound(d.pfx_host, d.pfx_host + d.nruns, in_blk) - d.pfx_host) - 1;
+    return ((uint64_t)k * (uint64_t)d.nblk + (uint64_t)j) * (uint64_t)d.nruns + (uint64_t)r;
+}
+
 // returns 1 when the wave-per-run unpack does not apply
 static int launch_runs_unpack(const DdtDev &d, int w, void *mem, const void *packed, int64_t pos, int64_t bytes,
                               hipStream_t s)
 {
-    if (pos != 0 || d.inst_bytes <= 0 || bytes % d.inst_bytes != 0 || d.max_len <= 0) return 1;
+    if (d.inst_bytes <= 0 || d.max_len <= 0 || bytes <= 0 || !d.pfx_host || !d.len_host) return 1;
+    for (int r = 0; r < d.nruns; ++r)
+        if (d.len_host[r] <= 0) return 1;  // (run_at assumes every run holds bytes)
     if ((((uintptr_t)mem) | (uint64_t)d.extent | (uint64_t)d.stride) & 15) return 1;
     if (d.blk_bytes < kRunsMinBytes * d.nruns || d.max_len * d.nruns > kRunsMaxSkew * d.blk_bytes) return 1;
-    const uint64_t ninst = (uint64_t)(bytes / d.inst_bytes);
     const uint64_t per_inst = (uint64_t)d.nblk * (uint64_t)d.nruns;
-    if (per_inst >= ((uint64_t)1 << 32) || ninst * per_inst >= ((uint64_t)1 << 32) - 4) return 1;
+    const uint64_t q0 = run_at(d, pos), q1 = run_at(d, pos + bytes - 1);
+    if (per_inst >= ((uint64_t)1 << 32) || q1 >= ((uint64_t)1 << 32) - 4) return 1;
     RunsArgs a;
     a.mem = static_cast<char *>(mem);
     a.packed = static_cast<const char *>(packed);
@@ -697,9 +720,12 @@ static int launch_runs_unpack(const DdtDev &d, int w, void *mem, const void *pac
     a.extent = d.extent;
     a.blk_bytes = d.blk_bytes;
     a.inst_bytes = d.inst_bytes;
+    a.pos = pos;
+    a.end = pos + bytes;
     a.per_inst = make_fastdiv((uint32_t)per_inst);
     a.nruns = make_fastdiv((uint32_t)d.nruns);
-    a.nwaves = (uint32_t)(ninst * per_inst);
+    a.q0 = (uint32_t)q0;
+    a.nwaves = (uint32_t)(q1 - q0 + 1);
     const unsigned blocks = (a.nwaves + 3) / 4;
     if (w == 8) hipLaunchKernelGGL((k_ddt_runs_unpack<8>), dim3(blocks), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_ddt_runs_unpack<4>), dim3(blocks), dim3(256), 0, s, a);

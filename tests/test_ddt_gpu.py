@@ -442,9 +442,10 @@ RUNS_CASES = [  # (disps, lens, nblk, stride, extent, count): long 8- / 4-B alig
 
 @pytest.mark.parametrize("case", range(len(RUNS_CASES)))
 def test_long_run_unpack(gpu, pkg, case):
-    """whole-message unpack of long W-aligned runs (the triangle of the unpack ceiling probe, floats
-    with 12-B heads and tails, runs spanning several 4-KiB spans, two runs per block): the bytes equal
-    the host convertor's under both row modes of the unit kernel, gaps untouched"""
+    """unpack of long W-aligned runs (the triangle of the unpack ceiling probe, floats with 12-B heads
+    and tails, runs spanning several 4-KiB spans, two runs per block), whole messages under both row
+    modes of the unit kernel and random convertor windows (the wave-per-run kernel clips the first and
+    last run): the bytes equal the host convertor's, gaps untouched"""
     torch = gpu
     disps, lens, nblk, stride, extent, count = RUNS_CASES[case]
     d = pkg.Ddt.runs(disps, lens, nblk, stride, extent)
@@ -463,6 +464,16 @@ def test_long_run_unpack(gpu, pkg, case):
             d.unpack(count, z.data_ptr(), 0, dp.data_ptr(), total)
             torch.cuda.synchronize()
             assert np.array_equal(z.cpu().numpy(), want), (case, mode)
+        # the same through convertor windows (set_position fragments): W-aligned cut points, windows
+        # starting and ending inside runs, inside heads / tails and on run edges
+        W = 4 if case == 1 else 8
+        for trial in range(3):
+            cuts = sorted(set([0, total] + [int(c) * W for c in rng.integers(1, total // W, 2 + 3 * trial)]))
+            z = _dev(torch, init)
+            for lo, hi in zip(cuts[:-1], cuts[1:]):
+                d.unpack(count, z.data_ptr(), lo, dp.data_ptr() + lo, hi - lo)
+            torch.cuda.synchronize()
+            assert np.array_equal(z.cpu().numpy(), want), (case, "windows", cuts)
     finally:
         pkg.ddt_tune_rows(2)
     d.destroy()

@@ -217,6 +217,23 @@ def leg_ddt_runs(pkg, torch, args, emit):
         for mode in (2, 3):
             assert torch.equal(outs[mode][0], outs[0][0]) and torch.equal(outs[mode][1], outs[0][1]), (name, mode)
         pkg.ddt_tune_rows(2)
+        # the same unpack through 4 convertor windows (set_position fragments at unaligned run
+        # offsets: the wave-per-run kernel clips the first and last run of each window)
+        cuts = [0] + [(size * i // 4) // (2 * esz) * (2 * esz) + esz for i in (1, 2, 3)] + [size]
+
+        def windows(s):
+            for lo, hi in zip(cuts[:-1], cuts[1:]):
+                d.unpack(count, y.data_ptr(), lo, p.data_ptr() + lo, hi - lo, s)
+        for mode in (2, 3):  # 3: W-byte units only (what windows took before the wave-per-run kernel clipped runs)
+            pkg.ddt_tune_rows(mode)
+            y.zero_()
+            avg, med = timed(torch, windows, args.steps, args.warmup)
+            emit({"leg": "ddt_runs_unpack_windows4", "type": name, "kernel": {2: "units", 3: "units_w"}[mode],
+                  "count": count, "alg_bytes": alg, "kernel_avg_ms": round(avg, 5), "kernel_med_ms": round(med, 5),
+                  "achieved_GBs": round(alg / (avg * 1e-3) / 1e9, 1),
+                  "frac": round(alg / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+            assert torch.equal(y, outs[0][1]), (name, "windows", mode)
+        pkg.ddt_tune_rows(2)
         del x, p, y, outs
 
 
