@@ -63,7 +63,8 @@ def extra_legs(args, pkg, torch, comm, world, rank, dev, legs, key):
         sec = _timed(dist, torch, run, reps, 2)
         row = {"bytes": nbytes, "us": round(sec * 1e6, 2), "alg": comm.last_algorithm(),
                "busbw_GBs": round(nbytes / sec * 2 * (world - 1) / world / 1e9, 3),
-               "exact": bool(torch.all(y == want).item())}
+               "exact": bool(torch.all(y == want).item()),
+               "svc_resident": comm.get("SVC_RESIDENT"), "svc_launches": comm.get("SVC_LAUNCHES")}
         if nbytes <= (1 << 20):
             # every data flow at this size, for the thresholds: one-shot LL, host-synchronised with
             # ring orders in one phase (k_ring_all, below ONE_PHASE_MAX_BYTES) and in two

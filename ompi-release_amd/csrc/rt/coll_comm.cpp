@@ -1191,7 +1191,7 @@ static void svc_stop(mi355x_comm *c)
     svc_ring(c, kSvcQuit);
     if (!svc_wait_exit(c->svcq, c->timeout_s + 5.0))
         fprintf(stderr, "[mi355x r%d] resident service did not leave\n", c->rank);
-    svc_ring(c, c->ll_seq);  // back to the last call's number: the next launch waits for ll_seq + 1
+    svc_ring(c, c->ll_seq << kSvcPartBits);  // back to the last call's number: the next launch waits for the next
 }
 
 // A call that takes a host-synchronised flow asks a resident service to leave, without waiting:
@@ -1233,7 +1233,8 @@ static int svc_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s)
     for (int j = 0; j < c->size; ++j) call.order[j] = a.order[j];
     for (int k = 0; k < a.nsteps && k < kTreeSteps; ++k) call.steps[k] = a.steps[k];
     std::memcpy(&c->svc_page->call, &call, sizeof(call));
-    svc_ring(c, seq);
+    const uint64_t nchunks = (a.nbytes + kLLChunk - 1) / kLLChunk;
+    svc_ring(c, (seq << kSvcPartBits) | std::min<uint64_t>(nchunks, (uint64_t)c->svc_nwg));
     int rc = MI355X_SUCCESS;
     if (!svc_resident(c->svcq)) rc = svc_launch(c, seq);
     if (rc) return rc;

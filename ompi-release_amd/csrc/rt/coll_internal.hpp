@@ -109,6 +109,7 @@ constexpr size_t kLLAckBytes = 4096;  // LL region: [ack words][2 parities x n s
 // (chunks wg, wg + nwg, ...), publishes its results and counts itself done; the last one
 // acknowledges the call to every peer and stores its number into the host's completion word.
 constexpr uint64_t kSvcQuit = ~0ull;  // door value that ends the service
+constexpr int kSvcPartBits = 7;       // door = (call number << 7) | workgroups the call needs (<= 64)
 constexpr int kSvcThreads = 256;      // threads per workgroup (16 B each: one LL slice per pass)
 struct SvcCall {
     uint64_t seq;                     // the call's number (= its LL tag), written with the call
@@ -120,7 +121,8 @@ struct SvcCall {
     TreeStep steps[kTreeSteps];
 };
 struct SvcPage {                      // the doorbell page
-    uint64_t door;                    // number of the posted call (kSvcQuit: leave)
+    uint64_t door;                    // (number << kSvcPartBits) | participants of the posted call;
+                                      // kSvcQuit: leave
     uint64_t pad0[15];
     uint64_t ctr;                     // workgroups done, zeroed by the host before every launch
     uint64_t pad1[15];

@@ -93,57 +93,65 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
     uint64_t want = g.first;
     uint64_t idle0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-        // 1. the doorbell.  Workgroup 0 alone decides whether the next call is served or the
-        // service leaves (quit request, idle, a number out of turn) and publishes the verdict in
-        // `go`; the others follow it -- workgroups deciding on their own could split over a call
-        // (some serving it, some gone), and a call served in part never completes
+        // 1. the doorbell: (call number << kSvcPartBits) | participating workgroups.  Workgroup 0
+        // alone decides whether the next call is served or the service leaves (quit request, idle,
+        // a number out of turn) and publishes the verdict in `go`; the others follow it --
+        // workgroups deciding on their own could split over a call (some serving it, some gone),
+        // and a call served in part never completes.  The verdict carries the participant count,
+        // so a workgroup the call does not need never reads the descriptor (which the host may
+        // already be rewriting for the next call once the participants are done).
         if (t == 0) {
             uint64_t v;
             if (blockIdx.x == 0) {
                 for (;;) {
                     v = __hip_atomic_load(&page->door, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    if (v >= want) break;
+                    if ((v >> kSvcPartBits) >= want) break;
                     __builtin_amdgcn_s_sleep(2);
                     if (__builtin_amdgcn_s_memrealtime() - idle0 > g.idle_ticks) {
                         v = kSvcQuit;
                         break;
                     }
                 }
-                if (v != want) v = kSvcQuit;
+                if ((v >> kSvcPartBits) != want) v = kSvcQuit;
                 __hip_atomic_store(&page->go, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             } else {
                 for (;;) {  // (bounded too: never longer than the leader's idle limit plus a timeout)
                     v = __hip_atomic_load(&page->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    if (v >= want) break;
+                    if ((v >> kSvcPartBits) >= want) break;
                     __builtin_amdgcn_s_sleep(2);
                     if (__builtin_amdgcn_s_memrealtime() - idle0 > g.idle_ticks + g.timeout_ticks) {
                         v = kSvcQuit;
                         break;
                     }
                 }
-                // (a follower that no call has needed since it last looked may find the verdict of
-                // a later call: those calls completed without it; it joins this one)
+                // (a follower no call has needed since it last looked may find the verdict of a
+                // later call: those calls completed without it; it joins this one)
             }
             s_door = v;
         }
         __syncthreads();
         if (s_door == kSvcQuit) break;
-        want = s_door;
+        want = s_door >> kSvcPartBits;
+        const uint64_t part = s_door & ((1u << kSvcPartBits) - 1);
+        if (blockIdx.x >= part) {  // not needed by this call: on to the next verdict
+            ++want;
+            idle0 = __builtin_amdgcn_s_memrealtime();
+            continue;
+        }
         uint64_t *tr = (g.trace && blockIdx.x == 0) ? g.trace + (want % kSvcTraceCalls) * kSvcTraceCols : nullptr;
         if (tr && t == 0) {
             tr[0] = want;
             tr[1] = __builtin_amdgcn_s_memrealtime();
         }
-        // 2. the descriptor (stored before the doorbell) into LDS
+        // 2. the descriptor (stored before the doorbell; not rewritten before every participant
+        // of this call is done) into LDS
         if (t < kSvcCallWords)
             reinterpret_cast<uint64_t *>(&sc)[t] = __hip_atomic_load(reinterpret_cast<const uint64_t *>(&page->call) + t,
                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __syncthreads();
-        if (sc.seq != want) {
-            // the page already holds a later call: `want` completed without this (follower)
-            // workgroup -- it was not one of its participants -- so wait for the next verdict
-            ++want;
-            continue;
+        if (sc.seq != want) {  // (never: the host protocol forbids it) -- leave, visibly
+            if (t == 0) __hip_atomic_store(g.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
         }
         const int n = g.n, me = g.me;
         const uint64_t par = want & 1;
@@ -182,14 +190,8 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
         if (tr && t == 0) tr[2] = __builtin_amdgcn_s_memrealtime();
         // 3. my slices.  The inputs (written by kernels that completed before the call) are read
         // with system-coherent loads, the results stored write-through (ll_read16 / ll_write16<SYS>):
-        // no acquire or release fence per call.  Workgroups beyond the call's slice count sit it out.
+        // no acquire or release fence per call.
         const uint64_t nchunks = (a.nbytes + kLLChunk - 1) / kLLChunk;
-        const uint64_t part = nchunks < (uint64_t)g.nwg ? nchunks : (uint64_t)g.nwg;
-        if (blockIdx.x >= part) {
-            ++want;
-            idle0 = __builtin_amdgcn_s_memrealtime();
-            continue;
-        }
         const bool reduce = a.mode == LL_AR || a.mode == LL_RED;
         const bool evaluate = reduce ? !(a.mode == LL_RED && me != a.root) : a.recv_mask != 0;
         // push every slice of mine (inputs read kSvcPass slices at a time, so their latencies
