@@ -69,20 +69,25 @@ def extra_legs(args, pkg, torch, comm, world, rank, dev, legs, key):
             # every data flow at this size, for the thresholds: one-shot LL, host-synchronised with
             # ring orders in one phase (k_ring_all, below ONE_PHASE_MAX_BYTES) and in two
             # and the resident LL service (coll_svc.hip; reads 0 where this communicator has none)
+            # the resident service's two forms (coll_svc.hip; read 0 where this communicator has
+            # none): LL granules (us_svc) and the one-phase ring pulled from the mapped inputs (us_pull)
             one_phase, svc_max = comm.get("ONE_PHASE_MAX_BYTES"), comm.get("SVC_MAX_BYTES")
-            flows = [("us_ll", 1 << 20, one_phase, 0), ("us_host", 0, 1 << 20, 0), ("us_host_2phase", 0, 0, 0)]
-            if svc_max or comm.get("SVC_LAUNCHES"):
-                flows.append(("us_svc", 0, one_phase, 1 << 20))
-            for name, llmax, op1, svc in flows:
+            pull_max = comm.get("SVC_PULL_MAX_BYTES")
+            flows = [("us_ll", 1 << 20, one_phase, 0, 0), ("us_host", 0, 1 << 20, 0, 0), ("us_host_2phase", 0, 0, 0, 0)]
+            if svc_max or pull_max:
+                flows += [("us_svc", 0, one_phase, 1 << 20, 0), ("us_pull", 0, 1 << 20, 0, 1 << 20)]
+            for name, llmax, op1, svc, pull in flows:
                 comm.set("LL_MAX_BYTES", llmax)
                 comm.set("ONE_PHASE_MAX_BYTES", op1)
                 comm.set("SVC_MAX_BYTES", svc)
+                comm.set("SVC_PULL_MAX_BYTES", pull)
                 y.zero_()
                 row[name] = round(_timed(dist, torch, run, reps, 2) * 1e6, 2)
                 row["exact"] = row["exact"] and bool(torch.all(y == want).item())
             comm.set("LL_MAX_BYTES", 0)  # the defaults
             comm.set("ONE_PHASE_MAX_BYTES", one_phase)
             comm.set("SVC_MAX_BYTES", svc_max)
+            comm.set("SVC_PULL_MAX_BYTES", pull_max)
         sweep.append(row)
         del x, y
     legs["allreduce_sweep_f32"] = sweep

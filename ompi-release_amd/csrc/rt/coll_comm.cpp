@@ -590,7 +590,7 @@ static void svc_park(mi355x_comm *c);
 int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t sig[4],
              std::vector<std::vector<void *>> &peers, bool *staged, bool force, bool persistent)
 {
-    svc_park(c);  // a host-synchronised call: the resident service steps aside (svc_park)
+    if (!c->svc_keep) svc_park(c);  // a host-synchronised call: the resident service steps aside (svc_park)
     c->seq++;
     if (staged) *staged = false;
     RankSlot &s = c->ctrl->slot[c->rank];
@@ -1206,35 +1206,12 @@ static void svc_park(mi355x_comm *c)
 }
 
 // one LL call through the service: `a` carries the call (mode, buffers, program, masks)
-static int svc_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s)
+// post `call` (number call.seq, `part` participating workgroups) and wait for its completion
+static int svc_call(mi355x_comm *c, const SvcCall &call, uint64_t part)
 {
-    MI_HIP(hipStreamSynchronize(s));  // the inputs: every earlier operation on the caller's stream
-    const uint64_t seq = ++c->ll_seq;
-    SvcCall call;
-    std::memset(&call, 0, sizeof(call));
-    call.seq = seq;
-    call.src = a.src;
-    call.dst = a.dst;
-    call.nbytes = a.nbytes;
-    call.count = a.count;
-    call.early = a.early;
-    call.late = a.late;
-    call.split = a.split;
-    call.role_mask = a.role_mask;
-    call.push_mask = a.push_mask;
-    call.recv_mask = a.recv_mask;
-    call.op = op;
-    call.type = type;
-    call.mode = a.mode;
-    call.prog = a.prog;
-    call.root = a.root;
-    call.nsteps = a.nsteps;
-    call.result = a.result;
-    for (int j = 0; j < c->size; ++j) call.order[j] = a.order[j];
-    for (int k = 0; k < a.nsteps && k < kTreeSteps; ++k) call.steps[k] = a.steps[k];
+    const uint64_t seq = call.seq;
     std::memcpy(&c->svc_page->call, &call, sizeof(call));
-    const uint64_t nchunks = (a.nbytes + kLLChunk - 1) / kLLChunk;
-    svc_ring(c, (seq << kSvcPartBits) | std::min<uint64_t>(nchunks, (uint64_t)c->svc_nwg));
+    svc_ring(c, (seq << kSvcPartBits) | std::min<uint64_t>(std::max<uint64_t>(part, 1), (uint64_t)c->svc_nwg));
     int rc = MI355X_SUCCESS;
     if (!svc_resident(c->svcq)) rc = svc_launch(c, seq);
     if (rc) return rc;
@@ -1268,6 +1245,68 @@ static int svc_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s)
     }
     c->svc_calls++;
     return MI355X_SUCCESS;
+}
+
+static int svc_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s)
+{
+    MI_HIP(hipStreamSynchronize(s));  // the inputs: every earlier operation on the caller's stream
+    SvcCall call;
+    std::memset(&call, 0, sizeof(call));
+    call.seq = ++c->ll_seq;
+    call.src = a.src;
+    call.dst = a.dst;
+    call.nbytes = a.nbytes;
+    call.count = a.count;
+    call.early = a.early;
+    call.late = a.late;
+    call.split = a.split;
+    call.role_mask = a.role_mask;
+    call.push_mask = a.push_mask;
+    call.recv_mask = a.recv_mask;
+    call.op = op;
+    call.type = type;
+    call.mode = a.mode;
+    call.prog = a.prog;
+    call.root = a.root;
+    call.nsteps = a.nsteps;
+    call.result = a.result;
+    for (int j = 0; j < c->size; ++j) call.order[j] = a.order[j];
+    for (int k = 0; k < a.nsteps && k < kTreeSteps; ++k) call.steps[k] = a.steps[k];
+    return svc_call(c, call, (a.nbytes + kLLChunk - 1) / kLLChunk);
+}
+
+// The one-phase ring-ordered allreduce (k_ring_all's work) served by the resident service
+// (LL_PULL): the caller has exchanged every rank's input and rbuf (P[0], P[1]); the service reads
+// the n inputs where they are, folds every element in its ring block's order, and completes only
+// once every peer has read this rank's input -- the launch, the completion wait and the finishing
+// barrier of the host-synchronised form are gone.  Same decision on every rank (sizes and every
+// rank's buffer alignment, svc_pull_usable).
+static bool svc_pull_usable(const mi355x_comm *c, size_t bytes)
+{
+    return c->svc_ok && !c->loopback && bytes > c->svc_max && bytes <= c->svc_pull_max && bytes < ((size_t)1 << 31);
+}
+
+static int svc_pull_run(mi355x_comm *c, int op, int type, const std::vector<std::vector<void *>> &P, const void *in,
+                        void *rbuf, size_t count, size_t esz, size_t early, size_t late, size_t split)
+{
+    int rc = ensure_ll(c);
+    if (rc) return rc;
+    SvcCall call;
+    std::memset(&call, 0, sizeof(call));
+    call.seq = ++c->ll_seq;
+    call.src = in;
+    call.dst = rbuf;
+    call.nbytes = count * esz;
+    call.count = count;
+    call.early = early;
+    call.late = late;
+    call.split = split;
+    call.op = op;
+    call.type = type;
+    call.mode = LL_PULL;
+    call.prog = LL_RING;
+    for (int q = 0; q < c->size; ++q) call.srcs[q] = P[0][q];
+    return svc_call(c, call, (call.nbytes + kLLChunk - 1) / kLLChunk);
 }
 
 // MI355X_SVC_TRACE=1: mean microseconds between the stamped stages over the traced calls
@@ -1343,6 +1382,7 @@ static int svc_setup(mi355x_comm *c)
     c->svc_max = (size_t)std::max(0.0, env_double("MI355X_SVC_MAX_BYTES", (double)c->svc_max));
     c->svc_idle_s = std::max(0.001, env_double("MI355X_SVC_IDLE_MS", c->svc_idle_s * 1e3) * 1e-3);
     c->svc_nwg = (int)std::min(64.0, std::max(1.0, env_double("MI355X_SVC_WGS", (double)c->svc_nwg)));
+    c->svc_pull_max = (size_t)std::max(0.0, env_double("MI355X_SVC_PULL_MAX_BYTES", (double)c->svc_pull_max));
     const char *env = getenv("MI355X_SVC");
     const bool want = c->ll_ok && c->size <= kLLMaxRanks && !(env && atoi(env) == 0);
     if (want) {
@@ -2082,6 +2122,7 @@ int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
     case MI355X_KNOB_SVC_CALLS: *value = (long)c->svc_calls; break;
     case MI355X_KNOB_SVC_LAUNCHES: *value = (long)c->svc_launches; break;
     case MI355X_KNOB_SVC_RESIDENT: *value = c->svcq && svc_resident(c->svcq) ? 1 : 0; break;
+    case MI355X_KNOB_SVC_PULL_MAX_BYTES: *value = c->svc_ok ? (long)c->svc_pull_max : 0; break;
     default: return set_error(MI355X_ERR_ARG, "unknown knob %d", knob);
     }
     return MI355X_SUCCESS;
@@ -2145,6 +2186,13 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
     case MI355X_KNOB_LL_MAX_BYTES:
         if (value < 0 || value > (64l << 20)) return set_error(MI355X_ERR_ARG, "ll_max_bytes out of range");
         c->ll_max = c->ll_ok ? (size_t)value : 0;  // a failed (or skipped) self-test keeps it off
+        break;
+    case MI355X_KNOB_SVC_PULL_MAX_BYTES:
+        if (value < 0 || value > (1l << 30)) return set_error(MI355X_ERR_ARG, "svc_pull_max_bytes out of range");
+        if (c->svc_ok) {
+            drain(c);
+            c->svc_pull_max = (size_t)value;
+        }
         break;
     case MI355X_KNOB_SVC_MAX_BYTES:
         if (value < 0 || value > (64l << 20)) return set_error(MI355X_ERR_ARG, "svc_max_bytes out of range");
@@ -2281,7 +2329,14 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
     const uint64_t sig[4] = {1, count, (uint64_t)type, (uint64_t)op};
     std::vector<std::vector<void *>> P;
     bool staged = false;
+    // the one-phase ring sizes may go to the resident service (svc_pull_run): its exchange then
+    // leaves the service resident (the same decision on every rank: sizes only)
+    const bool one_phase = ring && sbuf && sbuf != rbuf && !coll_tune().push && count * esz <= c->one_phase_max &&
+                           count <= 0xffffffffull;
+    const bool pull_cand = one_phase && svc_pull_usable(c, count * esz);
+    c->svc_keep = pull_cand;
     rc = exchange(c, 2, mine, sig, P, &staged);
+    c->svc_keep = false;
     if (c->lat_on) lt[2] = lclk::now();
     auto lat_done = [&](int rc2) {  // the one-launch paths: launch done at lt[3], then finish
         if (!c->lat_on || rc2) return rc2;
@@ -2330,8 +2385,17 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
             return finish(c, s);
         }
     }
-    if (ring && sbuf && sbuf != rbuf && !staged && !coll_tune().push && count * esz <= c->one_phase_max &&
-        count <= 0xffffffffull) {
+    bool pull = pull_cand && !staged;
+    for (int q = 0; q < c->size && pull; ++q)
+        pull = !((((uintptr_t)P[0][q]) | ((uintptr_t)P[1][q])) & 15);  // every rank's buffers 16-B aligned
+    if (pull) {
+        size_t o1, l0, l1;
+        ring_block(count, c->size, 0, &o1, &l0);
+        ring_block(count, c->size, c->size - 1, &o1, &l1);
+        return svc_pull_run(c, op, type, P, in, rbuf, count, esz, l0, l1 ? l1 : 1, count % (size_t)c->size);
+    }
+    if (pull_cand) svc_park(c);  // (kept for this call, which now takes a host-synchronised flow)
+    if (one_phase && !staged) {
         // small ring-ordered messages: every rank evaluates every block from the n inputs (reads
         // n x S, writes only its own rbuf) -- one launch and one barrier, like the tree orders
         RingAllArgs ra;

@@ -77,7 +77,8 @@ struct MultiCopyArgs {
 // exchange.
 constexpr size_t kLLChunk = 4096;  // payload bytes per thread block (256 threads x 16 B)
 constexpr int kLLMaxRanks = 8;     // sources held in registers per thread
-enum { LL_AR = 0, LL_AG = 1, LL_BC = 2, LL_RED = 3 };  // allreduce, allgather, bcast, reduce
+enum { LL_AR = 0, LL_AG = 1, LL_BC = 2, LL_RED = 3,     // allreduce, allgather, bcast, reduce
+       LL_PULL = 4 };  // (resident service only) one-phase allreduce pulled from the peers' mapped inputs
 enum { LL_FOLD = 0, LL_RING = 1, LL_TREE = 2 };   // per-element program of LL_AR
 struct LLArgs {
     const void *src;                   // this rank's data (NULL: nothing to push)
@@ -119,7 +120,11 @@ struct SvcCall {
     int32_t op, type, mode, prog, root, nsteps, result, pad;
     int32_t order[kLLMaxRanks];
     TreeStep steps[kTreeSteps];
+    const void *srcs[kLLMaxRanks];    // LL_PULL: every rank's input, mapped (16-B aligned)
 };
+// LL_PULL: rank q tells every peer it has read the peer's input for call k by storing k into word
+// kSvcPullDoneWord + q of the peer's LL acknowledgement page
+constexpr int kSvcPullDoneWord = 256;
 struct SvcPage {                      // the doorbell page
     uint64_t door;                    // (number << kSvcPartBits) | participants of the posted call;
                                       // kSvcQuit: leave

@@ -32,14 +32,105 @@ static_assert(sizeof(SvcCall) % 8 == 0, "the descriptor is copied in 8-byte word
 constexpr int kSvcCallWords = (int)(sizeof(SvcCall) / 8);
 static_assert(kSvcCallWords <= kSvcThreads, "one word per thread");
 constexpr int kSvcPass = 4;  // slices whose inputs one workgroup reads at once
+constexpr int kSvcPullU = 4; // LL_PULL: 16-B vectors per lane per pass
 
 // Step 3's second half for every slice of this workgroup: receive the peers' granules, then the
 // reference program per element (or the copy).  One out-of-line function per (op, type) slot,
 // entered once per call: the call's slot decides which (inlining every slot's evaluation into one
 // body makes the compiler's register allocation take tens of minutes).  Returns 1 on a timeout.
-template <class F>
-static __device__ __noinline__ int svc_finish(const LLArgs &a, uint64_t nchunks, uint64_t stride, uint64_t *tr)
+// LL_PULL (one-phase ring-ordered allreduce from the mapped inputs, no granules): every element
+// of this workgroup's 4-KiB slices folded from the n inputs in its ring block's order, the inputs
+// read with system-coherent 16-B loads, the result stored write-through; the last partial vector's
+// elements one by one
+// element i of ring block b folds x_b, x_{b+1}, ..., x_{b+n-1} with the partial as the `in`
+// operand (coll_tuned_allreduce.c:470-512; the LL_RING program of ll_eval, without its tree form)
+template <class F, class X> __device__ __forceinline__ typename F::T svc_ring_fold(const LLArgs &a, uint64_t i, X x)
 {
+    const uint64_t se = a.split * a.early;
+    const int b0 = (i < se) ? (int)(i / a.early) : (int)(a.split + (i - se) / a.late);
+    typename F::T acc = x(b0);
+    for (int j = 1; j < a.n; ++j) {
+        const int r = b0 + j >= a.n ? b0 + j - a.n : b0 + j;
+        acc = F::op2(x(r), acc);
+    }
+    return acc;
+}
+
+template <class F> static __device__ void svc_pull(const LLArgs &a, const SvcCall &sc, uint64_t stride)
+{
+    using T = typename F::T;
+    using V = LLVec<T>;
+    constexpr int EPV = 16 / sizeof(T);
+    const uint64_t nvec = a.nbytes / 16;
+    // kSvcPullU vectors per lane per pass, every source's loads of the pass issued before any
+    // evaluation: the loads cross xGMI, so the pass is latency-bound, not bandwidth-bound
+    const uint64_t step = stride * kSvcThreads;
+    for (uint64_t v0 = (uint64_t)blockIdx.x * kSvcThreads + threadIdx.x; v0 < nvec; v0 += step * kSvcPullU) {
+        V xv[kSvcPullU][kLLMaxRanks];
+#pragma unroll
+        for (int q = 0; q < kLLMaxRanks; ++q) {
+            if (q >= a.n) continue;
+            const __amdgpu_buffer_rsrc_t rs = ll_rsrc(sc.srcs[q]);
+#pragma unroll
+            for (int u = 0; u < kSvcPullU; ++u) {
+                const uint64_t v = v0 + (uint64_t)u * step;
+                if (v >= nvec) continue;
+                const u32x4l raw = __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(v * 16), 0, kLLSysCoherent);
+                __builtin_memcpy(&xv[u][q], &raw, 16);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kSvcPullU; ++u) {
+            const uint64_t v = v0 + (uint64_t)u * step;
+            if (v >= nvec) continue;
+            V r;
+#pragma unroll
+            for (int e = 0; e < EPV; ++e)
+                r.e[e] = svc_ring_fold<F>(a, v * EPV + e, [&](int q) {
+                    T x = xv[u][0].e[e];
+#pragma unroll
+                    for (int s2 = 1; s2 < kLLMaxRanks; ++s2)
+                        if (s2 == q) x = xv[u][s2].e[e];
+                    return x;
+                });
+            u32x4l out;
+            __builtin_memcpy(&out, &r, 16);
+            __builtin_amdgcn_raw_buffer_store_b128(out, ll_rsrc(a.dst), (unsigned)(v * 16), 0, kLLSysCoherent);
+        }
+    }
+    const uint64_t i = nvec * EPV + threadIdx.x;  // the tail: fewer than EPV elements
+    if (blockIdx.x == 0 && i < a.count) {
+        T xs[kLLMaxRanks];
+#pragma unroll
+        for (int q = 0; q < kLLMaxRanks; ++q) {
+            if (q >= a.n) continue;
+            uint32_t w[4];
+            ll_read16<true>(static_cast<const char *>(sc.srcs[q]), i * sizeof(T), sizeof(T), w);
+            __builtin_memcpy(&xs[q], w, sizeof(T));
+        }
+        const T r = svc_ring_fold<F>(a, i, [&](int q) {
+            T x = xs[0];
+#pragma unroll
+            for (int s2 = 1; s2 < kLLMaxRanks; ++s2)
+                if (s2 == q) x = xs[s2];
+            return x;
+        });
+        uint32_t w[4] = {0, 0, 0, 0};
+        __builtin_memcpy(w, &r, sizeof(T));
+        ll_write16<true>(static_cast<char *>(a.dst), i * sizeof(T), sizeof(T), w);
+    }
+}
+
+template <class F>
+static __device__ __noinline__ int svc_finish(const LLArgs &a, const SvcCall &sc, uint64_t nchunks, uint64_t stride,
+                                              uint64_t *tr)
+{
+    if constexpr (!F::kCopy) {
+        if (a.mode == LL_PULL) {
+            svc_pull<F>(a, sc, stride);
+            return 0;
+        }
+    }
     for (uint64_t c = blockIdx.x; c < nchunks; c += stride) {
         const LLBlock k = ll_block(a, c);
         uint32_t w[8][4];
@@ -66,16 +157,37 @@ template <class F> struct SvcReduce : F {
     static constexpr bool kCopy = false;
 };
 
-static __device__ int svc_finish_call(int op, int type, bool copy, const LLArgs &a, uint64_t nchunks, uint64_t stride,
-                                      uint64_t *tr)
+static __device__ int svc_finish_call(int op, int type, bool copy, const LLArgs &a, const SvcCall &sc,
+                                      uint64_t nchunks, uint64_t stride, uint64_t *tr)
 {
-    if (copy) return svc_finish<SvcCopy>(a, nchunks, stride, tr);
+    if (copy) return svc_finish<SvcCopy>(a, sc, nchunks, stride, tr);
     int rc = 0;
     for_each_slot([&](auto tag, int o, int t) {
         using F = typename decltype(tag)::type;
-        if (o == op && t == type) rc = svc_finish<SvcReduce<F>>(a, nchunks, stride, tr);
+        if (o == op && t == type) rc = svc_finish<SvcReduce<F>>(a, sc, nchunks, stride, tr);
     });
     return rc;
+}
+
+// LL_PULL, the last participant: tell every peer its input has been read, then wait until every
+// peer has read mine (the caller may reuse its input once the call completes); false on timeout
+static __device__ bool svc_pull_handshake(const SvcArgs &g, uint64_t want)
+{
+    for (int q = 0; q < g.n; ++q)
+        if (q != g.me) ll_store(reinterpret_cast<uint64_t *>(g.peer_ll[q]) + kSvcPullDoneWord + g.me, want);
+    const uint64_t *mine = reinterpret_cast<const uint64_t *>(g.my_ll) + kSvcPullDoneWord;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (int q = 0; q < g.n; ++q) {
+        if (q == g.me) continue;
+        while (ll_load(mine + q) < want) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > g.timeout_ticks) {
+                __hip_atomic_store(g.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return false;
+            }
+        }
+    }
+    return true;
 }
 
 } // namespace mi355x
@@ -88,6 +200,7 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
     __shared__ LLArgs a;
     __shared__ SvcCall sc;
     __shared__ uint64_t s_door;
+    __shared__ int s_fail;
     const int t = (int)threadIdx.x;
     SvcPage *page = const_cast<SvcPage *>(g.page);
     uint64_t want = g.first;
@@ -192,14 +305,15 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
         // with system-coherent loads, the results stored write-through (ll_read16 / ll_write16<SYS>):
         // no acquire or release fence per call.
         const uint64_t nchunks = (a.nbytes + kLLChunk - 1) / kLLChunk;
-        const bool reduce = a.mode == LL_AR || a.mode == LL_RED;
+        const bool pull = a.mode == LL_PULL;  // (no granules: the inputs are read where they are)
+        const bool reduce = a.mode == LL_AR || a.mode == LL_RED || pull;
         const bool evaluate = reduce ? !(a.mode == LL_RED && me != a.root) : a.recv_mask != 0;
         // push every slice of mine (inputs read kSvcPass slices at a time, so their latencies
         // overlap; the acknowledgement wait once, behind the first reads), then receive and finish
         // them: a workgroup with several slices waits one peer round trip, not one per slice
         int failed = 0;
         const uint64_t stride = (uint64_t)g.nwg;
-        for (uint64_t c0 = blockIdx.x; c0 < nchunks && !failed; c0 += stride * kSvcPass) {
+        for (uint64_t c0 = blockIdx.x; c0 < nchunks && !failed && !pull; c0 += stride * kSvcPass) {
             uint32_t w[kSvcPass][4];
 #pragma unroll
             for (int p = 0; p < kSvcPass; ++p) {
@@ -215,7 +329,7 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
             }
         }
         if (tr && t == 0) tr[3] = __builtin_amdgcn_s_memrealtime();
-        if (!failed && evaluate) failed = svc_finish_call(sc.op, sc.type, !reduce, a, nchunks, stride, tr);
+        if (!failed && evaluate) failed = svc_finish_call(sc.op, sc.type, !reduce, a, sc, nchunks, stride, tr);
         // 4. every store of the workgroup has reached memory; count; the last participant
         // acknowledges the call to every peer and completes it for the host
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -234,14 +348,18 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
             }
+            // (LL_PULL: not before every peer has read this rank's input)
+            if (!failed && last && pull && !svc_pull_handshake(g, want)) failed = 1;
             if (!failed && last) {
                 for (int q = 0; q < n; ++q)
                     if (q != me) ll_store(a.peer_ack[q], want);
                 __hip_atomic_store(g.done, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
             if (tr) tr[6] = __builtin_amdgcn_s_memrealtime();
+            s_fail = failed;
         }
-        if (failed) break;  // the error word is set; the host ends the service
+        __syncthreads();
+        if (s_fail) break;  // the error word is set; the host ends the service
         ++want;
         idle0 = __builtin_amdgcn_s_memrealtime();
     }

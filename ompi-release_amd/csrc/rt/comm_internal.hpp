@@ -263,11 +263,19 @@ struct mi355x_comm {
     mi355x::SvcPage *svc_page = nullptr;          // doorbell page (host-writable; device address == host address)
     bool svc_page_dev = false;                    // the page is fine-grained device memory (else pinned host)
     uint64_t *svc_host = nullptr;                 // pinned host words: [0] call completed, [1] error word
-    int svc_nwg = 8;                              // workgroups of the service (8 x 4 KiB slices per pass)
+    int svc_nwg = 16;                             // workgroups of the service (16 x 4 KiB slices per pass)
     // the service leaves after this long without a call (MI355X_SVC_IDLE_MS, default 1 ms): a burst
     // of small calls keeps it resident, a call after a longer gap relaunches it
     double svc_idle_s = 0.001;
     uint64_t svc_calls = 0, svc_launches = 0;
+    // one-phase ring-ordered allreduce above svc_max and up to svc_pull_max bytes per rank served by
+    // the service from the peers' mapped inputs (LL_PULL; MI355X_SVC_PULL_MAX_BYTES)
+    // (128 KiB by default: one-GPU rehearsal with 16 service workgroups, np = 2: 64 KiB 12.1 vs 17.4 us,
+    // 128 KiB 15.2 vs 18.7, 256 KiB 22.1 vs 17.5; np = 4: 17.5 vs 25.9, 22.4 vs 23.7, 33.0 vs 22.9 --
+    // the service's 16 workgroups are latency-bound where a one-shot launch has the whole GPU;
+    // profiles/r03_svc_pull.log)
+    size_t svc_pull_max = (size_t)128 << 10;
+    bool svc_keep = false;                        // this call's exchange leaves the service resident
     uint64_t *svc_trace = nullptr;                // MI355X_SVC_TRACE=1: stage stamps (pinned host), printed at destroy
     // pipelined allreduce (coll_pipe.hip): per-chunk ready flags in an uncached region that
     // every peer writes into (row q = flags raised by rank q), and the work-queue counter

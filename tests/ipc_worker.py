@@ -151,6 +151,45 @@ def ll_checks(pkg, comm, rank, size, oracle, torch, knob="LL_MAX_BYTES"):
     print(f"rank {rank} {path} OK", flush=True)
 
 
+def svc_pull_checks(pkg, comm, rank, size, oracle, torch):
+    """the one-phase ring-ordered allreduce served by the resident service from the peers' mapped
+    inputs (LL_PULL, coll_svc.hip): sizes between the service's LL limit and the pull limit, odd
+    counts (a tail shorter than a 16-B vector), every ring algorithm against the oracle's schedule
+    simulation; in place takes the host-synchronised flows"""
+    ptrs = lambda arrs: (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    saved = comm.get("SVC_PULL_MAX_BYTES")
+    comm.set("SVC_PULL_MAX_BYTES", 1 << 20)
+    assert comm.get("SVC_PULL_MAX_BYTES") == 1 << 20
+    svc_max = comm.get("SVC_MAX_BYTES")
+    calls0 = comm.get("SVC_CALLS")
+    for alg in (0, 4, 5):
+        comm.set("ALLREDUCE_ALG", alg)
+        for opname, tname in [("SUM", "FLOAT"), ("MAX", "DOUBLE"), ("MINLOC", "FLOAT_INT"), ("PROD", "C_DOUBLE_COMPLEX"),
+                              ("BXOR", "INT8")]:
+            op, ty = pkg.OP[opname], pkg.T[tname]
+            esz = pkg.type_size(ty)
+            for count in (svc_max // esz + 1, 100_003 // esz, (1 << 20) // esz - 3, (1 << 20) // esz):
+                xs = [opdata.make(tname, count, 800 + 10 * alg + r) for r in range(size)]
+                outs = [np.zeros_like(xs[0]) for _ in range(size)]
+                ran = oracle.oracle_allreduce(alg, size, count, ty, op, 0, ptrs(xs), ptrs(outs))
+                for inplace in (False, True):
+                    dx = torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda()
+                    dr = dx.clone() if inplace else torch.full_like(dx, 0x5a)
+                    torch.cuda.synchronize()
+                    comm.allreduce(None if inplace else dx.data_ptr(), dr.data_ptr(), count, ty, op)
+                    got = dr.cpu().numpy().view(xs[0].dtype)
+                    opdata.assert_same(tname, opname, got, outs[rank],
+                                       f"pull allreduce alg={alg} count={count} inplace={inplace} rank={rank}")
+                    assert comm.last_algorithm() == ran, (comm.last_algorithm(), ran)
+                    # the caller reuses its input at once: the peers must be done reading it
+                    dx.fill_(0x7f)
+    served = comm.get("SVC_CALLS") - calls0
+    assert served >= 3 * 5 * 4, f"the service served {served} pull calls"
+    comm.set("ALLREDUCE_ALG", 0)
+    comm.set("SVC_PULL_MAX_BYTES", saved)
+    print(f"rank {rank} pull OK ({served} service calls)", flush=True)
+
+
 def staged(pkg, comm, rank, size, torch, key):
     """allocations too large for hipIpc* (forced here: every allocation; for real: >= 2 GiB, which
     hipIpcOpenMemHandle cannot map on this platform) through real IPC, twice: on a communicator
@@ -712,6 +751,7 @@ def _main():
     served, launches = comm.get("SVC_CALLS") - calls0, comm.get("SVC_LAUNCHES")
     assert served > 100, f"the resident service served {served} calls"
     print(f"rank {rank} resident service: {served} calls, {launches} launches", flush=True)
+    svc_pull_checks(pkg, comm, rank, size, oracle, torch)
     p2p_checks(pkg, comm, rank, size, oracle, torch)
     _fd_report(rank)
     staged(pkg, comm, rank, size, torch, key)

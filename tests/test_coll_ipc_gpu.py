@@ -35,7 +35,7 @@ def test_ipc_ranks(gpu, size):
     failed = [r for r, p in enumerate(procs) if p.returncode != 0]
     assert not failed, "\n".join(f"rank {r} failed (rc {procs[r].returncode}):\n{outs[r][-2500:]}" for r in failed)
     for r, p in enumerate(procs):
-        stages = ("pipe OK", "LL OK", "SVC OK", "p2p OK", "staged OK", "OK") + (("bcast4g OK",) if size in (2, 3) else ()) \
+        stages = ("pipe OK", "LL OK", "SVC OK", "pull OK", "p2p OK", "staged OK", "OK") + (("bcast4g OK",) if size in (2, 3) else ()) \
             + (("maxcount OK",) if size == 2 else ()) \
             + (("pipe slots OK",) if size == 3 else ())
         for stage in stages:

@@ -11,5 +11,5 @@ import json
 d = json.loads(open("gpurun_out/r03_bench_n2.json").read().strip().splitlines()[-1])
 print("value", d["value"], "ms_per_step", d["ms_per_step"])
 for r in d["legs"]["allreduce_sweep_f32"]:
-    print({k: r.get(k) for k in ("bytes", "us", "us_svc", "us_host", "us_ll", "us_host_2phase", "exact")})
+    print({k: r.get(k) for k in ("bytes", "us", "us_svc", "us_pull", "us_host", "us_ll", "us_host_2phase", "exact")})
 PY
