@@ -1281,9 +1281,10 @@ static int svc_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s)
 // once every peer has read this rank's input -- the launch, the completion wait and the finishing
 // barrier of the host-synchronised form are gone.  Same decision on every rank (sizes and every
 // rank's buffer alignment, svc_pull_usable).
-static bool svc_pull_usable(const mi355x_comm *c, size_t bytes)
+static bool svc_pull_usable(const mi355x_comm *c, size_t bytes, size_t esz)
 {
-    return c->svc_ok && !c->loopback && bytes > c->svc_max && bytes <= c->svc_pull_max && bytes < ((size_t)1 << 31);
+    return c->svc_ok && !c->loopback && esz >= 4 && bytes > c->svc_max && bytes <= c->svc_pull_max &&
+           bytes < ((size_t)1 << 31);
 }
 
 static int svc_pull_run(mi355x_comm *c, int op, int type, const std::vector<std::vector<void *>> &P, const void *in,
@@ -1317,14 +1318,16 @@ static void svc_trace_report(mi355x_comm *c)
     int nrows = 0;
     for (int r = 0; r < kSvcTraceCalls; ++r) {
         const uint64_t *row = c->svc_trace + (size_t)r * kSvcTraceCols;
-        if (!row[0] || !row[6] || row[6] < row[1]) continue;
-        for (int k = 2; k <= 6; ++k) acc[k] += (double)(row[k] - row[k - 1]) * 0.01;  // 100 MHz -> us
+        if (!row[0] || !row[6] || !row[7] || row[6] < row[1]) continue;
+        // stages in time order: 1 door, 2 descriptor, 3 pushed, 4 received, 7 evaluated, 5 stored, 6 completed
+        const int order[] = {1, 2, 3, 4, 7, 5, 6};
+        for (int k = 1; k < 7; ++k) acc[order[k]] += (double)(row[order[k]] - row[order[k - 1]]) * 0.01;  // 100 MHz
         ++nrows;
     }
     if (nrows)
         fprintf(stderr, "[mi355x r%d] resident service, %d traced calls, mean us: door->descriptor %.2f, "
-                "->pushed %.2f, ->received %.2f, ->stored %.2f, ->completed %.2f\n", c->rank, nrows,
-                acc[2] / nrows, acc[3] / nrows, acc[4] / nrows, acc[5] / nrows, acc[6] / nrows);
+                "->pushed %.2f, ->received %.2f, ->evaluated %.2f, ->stored %.2f, ->completed %.2f\n", c->rank, nrows,
+                acc[2] / nrows, acc[3] / nrows, acc[4] / nrows, acc[7] / nrows, acc[5] / nrows, acc[6] / nrows);
     (void)hipHostFree(c->svc_trace);
     c->svc_trace = nullptr;
 }
@@ -2333,7 +2336,7 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
     // leaves the service resident (the same decision on every rank: sizes only)
     const bool one_phase = ring && sbuf && sbuf != rbuf && !coll_tune().push && count * esz <= c->one_phase_max &&
                            count <= 0xffffffffull;
-    const bool pull_cand = one_phase && svc_pull_usable(c, count * esz);
+    const bool pull_cand = one_phase && svc_pull_usable(c, count * esz, esz);
     c->svc_keep = pull_cand;
     rc = exchange(c, 2, mine, sig, P, &staged);
     c->svc_keep = false;

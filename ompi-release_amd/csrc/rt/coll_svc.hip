@@ -122,13 +122,17 @@ template <class F> static __device__ void svc_pull(const LLArgs &a, const SvcCal
 }
 
 template <class F>
-static __device__ __noinline__ int svc_finish(const LLArgs &a, const SvcCall &sc, uint64_t nchunks, uint64_t stride,
-                                              uint64_t *tr)
+static __device__ __forceinline__ int svc_finish_body(const LLArgs &a, const SvcCall &sc, uint64_t nchunks,
+                                                      uint64_t stride, uint64_t *tr)
 {
     if constexpr (!F::kCopy) {
-        if (a.mode == LL_PULL) {
-            svc_pull<F>(a, sc, stride);
-            return 0;
+        // (the pull form serves element types of 4 bytes and more -- svc_pull_usable -- so the
+        // 16- and 8-element vectors of the 1- and 2-byte types never instantiate it)
+        if constexpr (sizeof(typename F::T) >= 4) {
+            if (a.mode == LL_PULL) {
+                svc_pull<F>(a, sc, stride);
+                return 0;
+            }
         }
     }
     for (uint64_t c = blockIdx.x; c < nchunks; c += stride) {
@@ -150,6 +154,13 @@ static __device__ __noinline__ int svc_finish(const LLArgs &a, const SvcCall &sc
     return 0;
 }
 
+template <class F>
+static __device__ __noinline__ int svc_finish(const LLArgs &a, const SvcCall &sc, uint64_t nchunks, uint64_t stride,
+                                              uint64_t *tr)
+{
+    return svc_finish_body<F>(a, sc, nchunks, stride, tr);
+}
+
 struct SvcCopy {  // allgather / bcast: no evaluation
     static constexpr bool kCopy = true;
 };
@@ -161,6 +172,9 @@ static __device__ int svc_finish_call(int op, int type, bool copy, const LLArgs 
                                       uint64_t nchunks, uint64_t stride, uint64_t *tr)
 {
     if (copy) return svc_finish<SvcCopy>(a, sc, nchunks, stride, tr);
+    // the hot slots inline: no call, so none of the call's register saves and scratch reloads
+    if (op == MI355X_OP_SUM && type == MI355X_T_FLOAT) return svc_finish_body<SvcReduce<OpSum<float>>>(a, sc, nchunks, stride, tr);
+    if (op == MI355X_OP_SUM && type == MI355X_T_DOUBLE) return svc_finish_body<SvcReduce<OpSum<double>>>(a, sc, nchunks, stride, tr);
     int rc = 0;
     for_each_slot([&](auto tag, int o, int t) {
         using F = typename decltype(tag)::type;
@@ -330,6 +344,7 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
         }
         if (tr && t == 0) tr[3] = __builtin_amdgcn_s_memrealtime();
         if (!failed && evaluate) failed = svc_finish_call(sc.op, sc.type, !reduce, a, sc, nchunks, stride, tr);
+        if (tr && t == 0) tr[7] = __builtin_amdgcn_s_memrealtime();
         // 4. every store of the workgroup has reached memory; count; the last participant
         // acknowledges the call to every peer and completes it for the host
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

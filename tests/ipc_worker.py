@@ -155,7 +155,7 @@ def svc_pull_checks(pkg, comm, rank, size, oracle, torch):
     """the one-phase ring-ordered allreduce served by the resident service from the peers' mapped
     inputs (LL_PULL, coll_svc.hip): sizes between the service's LL limit and the pull limit, odd
     counts (a tail shorter than a 16-B vector), every ring algorithm against the oracle's schedule
-    simulation; in place takes the host-synchronised flows"""
+    simulation; in place and 1-byte types (BXOR INT8) take the host-synchronised flows"""
     ptrs = lambda arrs: (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
     saved = comm.get("SVC_PULL_MAX_BYTES")
     comm.set("SVC_PULL_MAX_BYTES", 1 << 20)
@@ -184,7 +184,7 @@ def svc_pull_checks(pkg, comm, rank, size, oracle, torch):
                     # the caller reuses its input at once: the peers must be done reading it
                     dx.fill_(0x7f)
     served = comm.get("SVC_CALLS") - calls0
-    assert served >= 3 * 5 * 4, f"the service served {served} pull calls"
+    assert served >= 3 * 4 * 4, f"the service served {served} pull calls"
     comm.set("ALLREDUCE_ALG", 0)
     comm.set("SVC_PULL_MAX_BYTES", saved)
     print(f"rank {rank} pull OK ({served} service calls)", flush=True)

@@ -60,13 +60,16 @@ static int run(int rank, int n, int reps, const char *key, const char *paths)
     long resident = -1;
     mi355x_comm_get(c, MI355X_KNOB_SVC_RESIDENT, &resident);
     if (rank == 0) printf("{\"path\": \"%s\", \"svc_resident_before\": %ld}\n", path, resident);
+    /* SMALL_TYPE / SMALL_OP: the (type, op) slot (default 14 = MPI_FLOAT, 3 = MPI_SUM), 4-B types */
+    const int ty = getenv("SMALL_TYPE") ? atoi(getenv("SMALL_TYPE")) : 14;
+    const int op = getenv("SMALL_OP") ? atoi(getenv("SMALL_OP")) : 3;
     for (int k = 0; k < nsizes; ++k) {
         const size_t cnt = sizes[k] / 4;
-        for (int i = 0; i < 50; ++i) mi355x_allreduce(c, s, r, cnt, 14, 3, NULL);
+        for (int i = 0; i < 50; ++i) mi355x_allreduce(c, s, r, cnt, ty, op, NULL);
         mi355x_comm_barrier(c);
         const double t0 = now_us();
         for (int i = 0; i < reps; ++i)
-            if (mi355x_allreduce(c, s, r, cnt, 14, 3, NULL)) {
+            if (mi355x_allreduce(c, s, r, cnt, ty, op, NULL)) {
                 fprintf(stderr, "rank %d: %s\n", rank, mi355x_last_error());
                 return 1;
             }
