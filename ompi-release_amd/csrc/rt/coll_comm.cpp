@@ -1205,7 +1205,6 @@ static void svc_park(mi355x_comm *c)
     if (c->svc_ok && c->svcq && svc_resident(c->svcq)) svc_ring(c, kSvcQuit);
 }
 
-// one LL call through the service: `a` carries the call (mode, buffers, program, masks)
 // post `call` (number call.seq, `part` participating workgroups) and wait for its completion
 static int svc_call(mi355x_comm *c, const SvcCall &call, uint64_t part)
 {
@@ -1247,6 +1246,7 @@ static int svc_call(mi355x_comm *c, const SvcCall &call, uint64_t part)
     return MI355X_SUCCESS;
 }
 
+// one LL call through the service: `a` carries the call (mode, buffers, program, masks)
 static int svc_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s)
 {
     MI_HIP(hipStreamSynchronize(s));  // the inputs: every earlier operation on the caller's stream

@@ -10,11 +10,12 @@
 // into host memory.
 //
 // Every workgroup runs the same loop:
-//   1. lane 0 polls the doorbell until it carries the next call number (or kSvcQuit; or the
+//   1. workgroup 0 polls the doorbell until it carries the next call number (or kSvcQuit; or the
 //      service has been idle for idle_ticks: the kernel leaves and the host relaunches it on the
-//      next call);
-//   2. the call's descriptor (SvcCall, in the doorbell page) is copied into LDS and expanded
-//      into LLArgs;
+//      next call) and publishes its verdict -- serve call k with p workgroups, or leave -- which
+//      the other workgroups follow (one decision per call);
+//   2. a workgroup the call needs copies the call's descriptor (SvcCall, in the doorbell page)
+//      into LDS and expands it into LLArgs;
 //   3. the workgroup serves slices wg, wg + nwg, ... of the call exactly as a per-call LL block
 //      serves its slice (push, receive, evaluate the reference schedule's per-element program or
 //      copy), reading the inputs with system-coherent loads and storing the results write-through
@@ -22,6 +23,8 @@
 //   4. it counts itself done once its stores have reached memory; the workgroup that completes
 //      the count (or the only one, for a call of one slice) acknowledges the call to every peer
 //      (the LL parity protocol) and stores the call number into the host's completion word.
+// The pull form (LL_PULL, the one-phase ring allreduce of 32-128 KiB) replaces step 3's granules
+// by reads of the peers' mapped inputs, and step 4 waits until every peer has read this rank's.
 // Every wait is bounded (timeout_ticks; the error word is set and the workgroup leaves).
 #include "coll_ll_dev.hpp"
 #include "slot_list.hpp"
@@ -34,14 +37,6 @@ static_assert(kSvcCallWords <= kSvcThreads, "one word per thread");
 constexpr int kSvcPass = 4;  // slices whose inputs one workgroup reads at once
 constexpr int kSvcPullU = 4; // LL_PULL: 16-B vectors per lane per pass
 
-// Step 3's second half for every slice of this workgroup: receive the peers' granules, then the
-// reference program per element (or the copy).  One out-of-line function per (op, type) slot,
-// entered once per call: the call's slot decides which (inlining every slot's evaluation into one
-// body makes the compiler's register allocation take tens of minutes).  Returns 1 on a timeout.
-// LL_PULL (one-phase ring-ordered allreduce from the mapped inputs, no granules): every element
-// of this workgroup's 4-KiB slices folded from the n inputs in its ring block's order, the inputs
-// read with system-coherent 16-B loads, the result stored write-through; the last partial vector's
-// elements one by one
 // element i of ring block b folds x_b, x_{b+1}, ..., x_{b+n-1} with the partial as the `in`
 // operand (coll_tuned_allreduce.c:470-512; the LL_RING program of ll_eval, without its tree form)
 template <class F, class X> __device__ __forceinline__ typename F::T svc_ring_fold(const LLArgs &a, uint64_t i, X x)
@@ -56,6 +51,10 @@ template <class F, class X> __device__ __forceinline__ typename F::T svc_ring_fo
     return acc;
 }
 
+// LL_PULL (one-phase ring-ordered allreduce from the mapped inputs, no granules): every element
+// of this workgroup's 4-KiB slices folded from the n inputs in its ring block's order, the inputs
+// read with system-coherent 16-B loads, the result stored write-through; the last partial vector's
+// elements one by one
 template <class F> static __device__ void svc_pull(const LLArgs &a, const SvcCall &sc, uint64_t stride)
 {
     using T = typename F::T;
@@ -121,6 +120,11 @@ template <class F> static __device__ void svc_pull(const LLArgs &a, const SvcCal
     }
 }
 
+// Step 3's second half for every slice of this workgroup: receive the peers' granules, then the
+// reference program per element (or the copy); or the pull form.  One out-of-line function per
+// (op, type) slot, entered once per call: the call's slot decides which (inlining every slot's
+// evaluation into one body makes the compiler's register allocation take tens of minutes; the
+// hot float / double SUM slots are inlined, svc_finish_call).  Returns 1 on a timeout.
 template <class F>
 static __device__ __forceinline__ int svc_finish_body(const LLArgs &a, const SvcCall &sc, uint64_t nchunks,
                                                       uint64_t stride, uint64_t *tr)
