@@ -7,6 +7,7 @@ result against the oracle's simulation of the reference schedule.  Exit 0 on suc
 from __future__ import annotations
 
 import ctypes
+import os
 import pathlib
 import sys
 
@@ -605,6 +606,84 @@ def svc_mode(key, rank, size, dev):
     print(f"rank {rank} svc OK", flush=True)
 
 
+def svc_stress(key, rank, size, dev):
+    """a long random mix of calls every rank makes in the same order (shared seed): small allreduces
+    and reduces through the resident service's LL form, 32-128 KiB ones through its pull form, in
+    place (host flows), 1 MiB ones (host flows: the service steps aside), allgather and bcast of LL
+    sizes, and pauses shorter and longer than the idle limit (the service leaves and comes back, and
+    a pause can end just as it leaves) -- every result checked exactly"""
+    import time
+    import torch
+    torch.cuda.set_device(dev)
+    pkg = load_pkg()
+    comm = pkg.Comm.create(key + "_stress", rank, size, dev)
+    assert comm.get("SVC_MAX_BYTES") > 0, "the stress communicator owns the service"
+    rng = np.random.default_rng(20261017)
+    f32, f64, i32 = pkg.T["FLOAT"], pkg.T["DOUBLE"], pkg.T["INT32"]
+    SUM, MAX = pkg.OP["SUM"], pkg.OP["MAX"]
+    iters = int(os.environ.get("SVC_STRESS_ITERS", "6000"))
+    kinds = ["ar_small", "ar_pull", "ar_inplace", "ar_host", "reduce", "allgather", "bcast", "pause"]
+    probs = [0.35, 0.15, 0.08, 0.05, 0.1, 0.1, 0.07, 0.1]
+    counts = {k: 0 for k in kinds}
+    calls0, launches0 = comm.get("SVC_CALLS"), comm.get("SVC_LAUNCHES")
+    for it in range(iters):
+        kind = kinds[rng.choice(len(kinds), p=probs)]
+        counts[kind] += 1
+        base = float(1 + it % 5)
+        if kind == "pause":
+            time.sleep(float(rng.choice([0.0002, 0.0009, 0.0011, 0.003])))
+            continue
+        if kind in ("ar_small", "ar_pull", "ar_inplace", "ar_host"):
+            nbytes = {"ar_small": int(rng.integers(1, 32 << 10)), "ar_pull": int(rng.integers((32 << 10) + 16, 128 << 10)),
+                      "ar_inplace": int(rng.integers(1, 128 << 10)), "ar_host": 1 << 20}[kind]
+            ty, tdt = [(f32, torch.float32), (f64, torch.float64), (i32, torch.int32)][it % 3]
+            esz = 8 if ty == f64 else 4
+            n = max(1, nbytes // esz)
+            op = MAX if ty == i32 else SUM
+            x = torch.full((n,), base + rank, dtype=tdt, device="cuda")
+            want = (base + size - 1) if op == MAX else sum(base + r for r in range(size))
+            if kind == "ar_inplace":
+                torch.cuda.synchronize()
+                comm.allreduce(None, x.data_ptr(), n, ty, op)
+                y = x
+            else:
+                y = torch.full_like(x, -7)
+                torch.cuda.synchronize()
+                comm.allreduce(x.data_ptr(), y.data_ptr(), n, ty, op)
+            assert bool(torch.all(y == want).item()), (it, kind, n, ty, op)
+        elif kind == "reduce":
+            n = int(rng.integers(1, 8 << 10))
+            root = int(rng.integers(0, size))
+            x = torch.full((n,), base + rank, dtype=torch.float32, device="cuda")
+            y = torch.full_like(x, -7)
+            torch.cuda.synchronize()
+            comm.reduce(x.data_ptr(), y.data_ptr() if rank == root else None, n, f32, SUM, root)
+            if rank == root:
+                assert bool(torch.all(y == sum(base + r for r in range(size))).item()), (it, kind, n, root)
+        elif kind == "allgather":
+            nb = int(rng.integers(1, 32 << 10))
+            src = torch.full((nb,), (rank + it) % 251, dtype=torch.uint8, device="cuda")
+            dst = torch.zeros(nb * size, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
+            comm.allgather(src.data_ptr(), dst.data_ptr(), nb)
+            for r in range(size):
+                assert bool(torch.all(dst[r * nb:(r + 1) * nb] == (r + it) % 251).item()), (it, kind, nb, r)
+        else:  # bcast
+            nb = int(rng.integers(1, 32 << 10))
+            root = int(rng.integers(0, size))
+            b = torch.full((nb,), (rank * 7 + it) % 251, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
+            comm.bcast(b.data_ptr(), nb, root)
+            assert bool(torch.all(b == (root * 7 + it) % 251).item()), (it, kind, nb, root)
+    served, launches = comm.get("SVC_CALLS") - calls0, comm.get("SVC_LAUNCHES") - launches0
+    assert served > iters // 3, served
+    print(f"rank {rank} svc stress: {iters} calls {counts}, {served} served by the service, {launches} launches",
+          flush=True)
+    comm.barrier()
+    comm.destroy()
+    print(f"rank {rank} svc_stress OK", flush=True)
+
+
 def done_words(key, rank, size, dev):
     """MI355X_DONE_WORDS=1 (finish points by command-processor-written completion words, off by
     default: slower back to back on this platform, profiles/r03_small_latency.jsonl): every flow that
@@ -708,6 +787,8 @@ def _main():
         return host_bw(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "svc":
         return svc_mode(key, rank, size, dev)
+    if len(sys.argv) > 5 and sys.argv[5] == "svc_stress":
+        return svc_stress(key, rank, size, dev)
     import faulthandler
     faulthandler.dump_traceback_later(150, exit=True)  # a rank stuck in a HIP call names its line
     import torch

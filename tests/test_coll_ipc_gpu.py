@@ -69,6 +69,15 @@ def test_resident_service(gpu, size):
 
 
 @pytest.mark.parametrize("size", [2, 3])
+def test_resident_service_stress(gpu, size):
+    """6000 random calls in the same order on every rank -- the service's LL and pull forms, host
+    flows it steps aside for, pauses around its idle limit -- every result exact
+    (ipc_worker.py::svc_stress)"""
+    outs = _run_mode(gpu, "svc_stress", size, timeout=250)
+    print(next(line for line in outs[0].splitlines() if "svc stress:" in line))
+
+
+@pytest.mark.parametrize("size", [2, 3])
 def test_done_words(gpu, size):
     """finish points by device-written completion words (MI355X_DONE_WORDS=1) stay exact"""
     _run_mode(gpu, "done_words", size)
