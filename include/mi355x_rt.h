@@ -175,12 +175,17 @@ enum mi355x_knob {
     MI355X_KNOB_SVC_LAUNCHES = 21,      /* (read-only) launches of the resident service (it leaves after
                                            MI355X_SVC_IDLE_MS without a call and is relaunched on demand) */
     MI355X_KNOB_SVC_RESIDENT = 22,      /* (read-only) 1 while the service's kernel is resident */
-    MI355X_KNOB_SVC_PULL_MAX_BYTES = 23 /* (per communicator, same value on every rank; env
+    MI355X_KNOB_SVC_PULL_MAX_BYTES = 23, /* (per communicator, same value on every rank; env
                                            MI355X_SVC_PULL_MAX_BYTES at creation) ring-ordered allreduce,
                                            not in place, above SVC_MAX_BYTES and up to this many bytes per
                                            rank: the resident service evaluates it from the peers' mapped
                                            inputs (buffers 16-B aligned on every rank) instead of a launch
                                            and a host barrier; 0 = never; reads 0 without a service */
+    MI355X_KNOB_SVC_PULL_COPY_MAX_BYTES = 24 /* (per communicator, same value on every rank; env
+                                           MI355X_SVC_PULL_COPY_MAX_BYTES at creation) allgather / bcast
+                                           above SVC_MAX_BYTES and up to this many bytes per rank (default
+                                           1 MiB): the resident service copies from the peers' mapped
+                                           buffers instead of a launch and a host barrier; 0 = never */
 };
 int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
 /* current value of a knob (LL_MAX_BYTES reads 0 when the creation-time LL self-test failed) */

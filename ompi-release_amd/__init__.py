@@ -252,7 +252,8 @@ KNOB = {"ALLREDUCE_ALG": 1, "REDUCE_ALG": 2, "REDUCE_SCATTER_ALG": 3, "BLOCKS_PE
         "LL_MAX_BYTES": 9, "REDUCE_CHAIN_FANOUT": 10, "TIME_PHASES": 11,
         "COPY_BLOCK_KIB": 12, "PIPE": 13, "PIPE_WG_PER_CU": 14, "PIPE_CHUNK_KIB": 15, "PIPE_WT": 16,
         "ONE_PHASE_MAX_BYTES": 17, "PIPE_REFUSED": 18, "SVC_MAX_BYTES": 19, "SVC_CALLS": 20,
-        "SVC_LAUNCHES": 21, "SVC_RESIDENT": 22, "SVC_PULL_MAX_BYTES": 23}
+        "SVC_LAUNCHES": 21, "SVC_RESIDENT": 22, "SVC_PULL_MAX_BYTES": 23,
+        "SVC_PULL_COPY_MAX_BYTES": 24}
 # coll/tuned COLLTYPE ids (coll_tuned.h:41-58)
 COLL = {"ALLGATHER": 0, "ALLREDUCE": 2, "BCAST": 7, "REDUCE": 11, "REDUCESCATTER": 12}
 AR_ALG = {"DECISION": 0, "LINEAR": 1, "NONOVERLAPPING": 2, "RECURSIVE_DOUBLING": 3, "RING": 4,

@@ -1287,6 +1287,33 @@ static bool svc_pull_usable(const mi355x_comm *c, size_t bytes, size_t esz)
            bytes < ((size_t)1 << 31);
 }
 
+// the same for allgather / bcast (LL_PULL_AG / LL_PULL_BC): `bytes` per rank between the LL form's
+// limit and the copy limit (svc_copy_max); no alignment condition (each rank copies into its own buffer, with
+// 16-B vectors where both ends allow)
+static bool svc_pull_copy_usable(const mi355x_comm *c, size_t bytes)
+{
+    return c->svc_ok && !c->loopback && bytes > c->svc_max && bytes <= c->svc_copy_max &&
+           bytes * (size_t)c->size < ((size_t)1 << 31);
+}
+
+static int svc_pull_copy_run(mi355x_comm *c, int mode, const std::vector<std::vector<void *>> &P, const void *src,
+                             void *dst, size_t bytes, int root)
+{
+    int rc = ensure_ll(c);
+    if (rc) return rc;
+    SvcCall call;
+    std::memset(&call, 0, sizeof(call));
+    call.seq = ++c->ll_seq;
+    call.src = src;
+    call.dst = dst;
+    call.nbytes = bytes;
+    call.mode = mode;
+    call.root = root;
+    for (int q = 0; q < c->size; ++q) call.srcs[q] = P[0][q];
+    const size_t total = mode == LL_PULL_AG ? bytes * (size_t)c->size : bytes;
+    return svc_call(c, call, (total + kLLChunk - 1) / kLLChunk);
+}
+
 static int svc_pull_run(mi355x_comm *c, int op, int type, const std::vector<std::vector<void *>> &P, const void *in,
                         void *rbuf, size_t count, size_t esz, size_t early, size_t late, size_t split)
 {
@@ -1386,6 +1413,7 @@ static int svc_setup(mi355x_comm *c)
     c->svc_idle_s = std::max(0.001, env_double("MI355X_SVC_IDLE_MS", c->svc_idle_s * 1e3) * 1e-3);
     c->svc_nwg = (int)std::min(64.0, std::max(1.0, env_double("MI355X_SVC_WGS", (double)c->svc_nwg)));
     c->svc_pull_max = (size_t)std::max(0.0, env_double("MI355X_SVC_PULL_MAX_BYTES", (double)c->svc_pull_max));
+    c->svc_copy_max = (size_t)std::max(0.0, env_double("MI355X_SVC_PULL_COPY_MAX_BYTES", (double)c->svc_copy_max));
     const char *env = getenv("MI355X_SVC");
     const bool want = c->ll_ok && c->size <= kLLMaxRanks && !(env && atoi(env) == 0);
     if (want) {
@@ -2126,6 +2154,7 @@ int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
     case MI355X_KNOB_SVC_LAUNCHES: *value = (long)c->svc_launches; break;
     case MI355X_KNOB_SVC_RESIDENT: *value = c->svcq && svc_resident(c->svcq) ? 1 : 0; break;
     case MI355X_KNOB_SVC_PULL_MAX_BYTES: *value = c->svc_ok ? (long)c->svc_pull_max : 0; break;
+    case MI355X_KNOB_SVC_PULL_COPY_MAX_BYTES: *value = c->svc_ok ? (long)c->svc_copy_max : 0; break;
     default: return set_error(MI355X_ERR_ARG, "unknown knob %d", knob);
     }
     return MI355X_SUCCESS;
@@ -2195,6 +2224,13 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
         if (c->svc_ok) {
             drain(c);
             c->svc_pull_max = (size_t)value;
+        }
+        break;
+    case MI355X_KNOB_SVC_PULL_COPY_MAX_BYTES:
+        if (value < 0 || value > (1l << 30)) return set_error(MI355X_ERR_ARG, "svc_pull_copy_max_bytes out of range");
+        if (c->svc_ok) {
+            drain(c);
+            c->svc_copy_max = (size_t)value;
         }
         break;
     case MI355X_KNOB_SVC_MAX_BYTES:
@@ -2725,9 +2761,14 @@ static int allgather_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
     const uint64_t sig[4] = {4, bytes, (uint64_t)push, 0};
     std::vector<std::vector<void *>> P;
     bool staged = false;
+    const bool pull_cand = !push && svc_pull_copy_usable(c, bytes);  // the resident service copies
+    c->svc_keep = pull_cand;
     int rc = exchange(c, push ? 2 : 1, mine, sig, P, &staged);
+    c->svc_keep = false;
     if (rc) return rc;
     c->last_alg = 1;
+    if (pull_cand && !staged) return svc_pull_copy_run(c, LL_PULL_AG, P, src, rbuf, bytes, 0);
+    if (pull_cand) svc_park(c);
     if (staged) return staged_allgather(c, src, rbuf, bytes, s);
     if (push) {
         CopyArgs a;
@@ -2782,10 +2823,15 @@ static int bcast_impl(mi355x_comm_t *c, void *buf, size_t bytes, int root, void 
     const uint64_t sig[4] = {5, bytes, (uint64_t)root, 0};
     std::vector<std::vector<void *>> P;
     bool staged = false;
-    int rc = exchange(c, 1, mine, sig, P, &staged);
-    if (rc) return rc;
     const bool split = bytes >= ((size_t)1 << 20);
+    const bool pull_cand = !split && svc_pull_copy_usable(c, bytes);  // the resident service copies
+    c->svc_keep = pull_cand;
+    int rc = exchange(c, 1, mine, sig, P, &staged);
+    c->svc_keep = false;
+    if (rc) return rc;
     c->last_alg = split ? 2 : 1;
+    if (pull_cand && !staged) return svc_pull_copy_run(c, LL_PULL_BC, P, buf, buf, bytes, root);
+    if (pull_cand) svc_park(c);
     if (staged) return staged_bcast(c, buf, bytes, root, s);
     MultiCopyArgs m;
     std::memset(&m, 0, sizeof(m));

@@ -120,6 +120,58 @@ template <class F> static __device__ void svc_pull(const LLArgs &a, const SvcCal
     }
 }
 
+// len bytes from src (a peer's mapped buffer) to dst (mine), this workgroup's share of the 16-B
+// vectors (4 per lane in flight), or of the words / bytes when an end is not 16-B aligned; src and
+// dst are the same for the whole workgroup
+static __device__ void svc_copy_seg(const char *src, char *dst, uint64_t len, uint64_t stride)
+{
+    const __amdgpu_buffer_rsrc_t rs = ll_rsrc(src), rd = ll_rsrc(dst);
+    const uint64_t step = stride * kSvcThreads;
+    const uint64_t first = (uint64_t)blockIdx.x * kSvcThreads + threadIdx.x;
+    if (((((uintptr_t)src) | ((uintptr_t)dst) | len) & 15) == 0) {
+        const uint64_t nvec = len / 16;
+        for (uint64_t v0 = first; v0 < nvec; v0 += step * kSvcPullU) {
+            u32x4l x[kSvcPullU];
+#pragma unroll
+            for (int u = 0; u < kSvcPullU; ++u) {
+                const uint64_t v = v0 + (uint64_t)u * step;
+                if (v < nvec) x[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(v * 16), 0, kLLSysCoherent);
+            }
+#pragma unroll
+            for (int u = 0; u < kSvcPullU; ++u) {
+                const uint64_t v = v0 + (uint64_t)u * step;
+                if (v < nvec) __builtin_amdgcn_raw_buffer_store_b128(x[u], rd, (unsigned)(v * 16), 0, kLLSysCoherent);
+            }
+        }
+        return;
+    }
+    if (((((uintptr_t)src) | ((uintptr_t)dst) | len) & 3) == 0) {
+        for (uint64_t w = first; w < len / 4; w += step)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_raw_buffer_load_b32(rs, (unsigned)(w * 4), 0, kLLSysCoherent),
+                                                  rd, (unsigned)(w * 4), 0, kLLSysCoherent);
+        return;
+    }
+    for (uint64_t b = first; b < len; b += step)
+        __builtin_amdgcn_raw_buffer_store_b8(__builtin_amdgcn_raw_buffer_load_b8(rs, (unsigned)b, 0, kLLSysCoherent), rd,
+                                             (unsigned)b, 0, kLLSysCoherent);
+}
+
+// LL_PULL_AG / LL_PULL_BC: allgather (block q from rank q's input, own block skipped in place) and
+// bcast (the root's buffer) copied from the mapped peers
+static __device__ void svc_pull_copy(const LLArgs &a, const SvcCall &sc, uint64_t stride)
+{
+    char *dst = static_cast<char *>(a.dst);
+    if (a.mode == LL_PULL_BC) {
+        if (a.me != a.root) svc_copy_seg(static_cast<const char *>(sc.srcs[a.root]), dst, a.nbytes, stride);
+        return;
+    }
+    for (int q = 0; q < a.n; ++q) {
+        char *d = dst + (uint64_t)q * a.nbytes;
+        if (q == a.me && static_cast<const char *>(a.src) == d) continue;  // in place: already there
+        svc_copy_seg(static_cast<const char *>(sc.srcs[q]), d, a.nbytes, stride);
+    }
+}
+
 // Step 3's second half for every slice of this workgroup: receive the peers' granules, then the
 // reference program per element (or the copy); or the pull form.  One out-of-line function per
 // (op, type) slot, entered once per call: the call's slot decides which (inlining every slot's
@@ -129,6 +181,12 @@ template <class F>
 static __device__ __forceinline__ int svc_finish_body(const LLArgs &a, const SvcCall &sc, uint64_t nchunks,
                                                       uint64_t stride, uint64_t *tr)
 {
+    if constexpr (F::kCopy) {
+        if (a.mode == LL_PULL_AG || a.mode == LL_PULL_BC) {
+            svc_pull_copy(a, sc, stride);
+            return 0;
+        }
+    }
     if constexpr (!F::kCopy) {
         // (the pull form serves element types of 4 bytes and more -- svc_pull_usable -- so the
         // 16- and 8-element vectors of the 1- and 2-byte types never instantiate it)
@@ -323,14 +381,18 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
         // with system-coherent loads, the results stored write-through (ll_read16 / ll_write16<SYS>):
         // no acquire or release fence per call.
         const uint64_t nchunks = (a.nbytes + kLLChunk - 1) / kLLChunk;
-        const bool pull = a.mode == LL_PULL;  // (no granules: the inputs are read where they are)
-        const bool reduce = a.mode == LL_AR || a.mode == LL_RED || pull;
-        const bool evaluate = reduce ? !(a.mode == LL_RED && me != a.root) : a.recv_mask != 0;
+        // pull forms: no granules, the inputs are read where they are
+        const bool pull = a.mode == LL_PULL || a.mode == LL_PULL_AG || a.mode == LL_PULL_BC;
+        const bool reduce = a.mode == LL_AR || a.mode == LL_RED || a.mode == LL_PULL;
+        const bool evaluate = reduce ? !(a.mode == LL_RED && me != a.root) : (a.recv_mask != 0 || pull);
         // push every slice of mine (inputs read kSvcPass slices at a time, so their latencies
         // overlap; the acknowledgement wait once, behind the first reads), then receive and finish
         // them: a workgroup with several slices waits one peer round trip, not one per slice
         int failed = 0;
-        const uint64_t stride = (uint64_t)g.nwg;
+        // the call's participants share its work: slice / vector / word / byte k*part + wg (the
+        // granule slices and 16-B vectors come 4 KiB per workgroup per step, the pull copy's words
+        // and bytes less: striding by nwg while only part workgroups take part would skip some)
+        const uint64_t stride = part;
         for (uint64_t c0 = blockIdx.x; c0 < nchunks && !failed && !pull; c0 += stride * kSvcPass) {
             uint32_t w[kSvcPass][4];
 #pragma unroll

@@ -275,6 +275,13 @@ struct mi355x_comm {
     // the service's 16 workgroups are latency-bound where a one-shot launch has the whole GPU;
     // profiles/r03_svc_pull.log)
     size_t svc_pull_max = (size_t)128 << 10;
+    // allgather / bcast above svc_max and up to svc_copy_max bytes per rank copied by the service
+    // from the peers' mapped buffers (LL_PULL_AG / LL_PULL_BC; MI355X_SVC_PULL_COPY_MAX_BYTES)
+    // (1 MiB by default: the copies are read-bound on every link at once, no fold, so the service's
+    // workgroups keep up -- one-GPU rehearsal, allgather np = 2: 256 KiB 8.9 vs 16.1 us, 1 MiB 11.9 vs
+    // 16.8; np = 4: 11.9 vs 20.7, 19.2 vs 23.1; bcast np = 2 512 KiB 8.8 vs 15.3;
+    // profiles/r03_svc_pull_copy.log).  bcast of 1 MiB and more takes the scatter + allgather shape.
+    size_t svc_copy_max = (size_t)1 << 20;
     bool svc_keep = false;                        // this call's exchange leaves the service resident
     uint64_t *svc_trace = nullptr;                // MI355X_SVC_TRACE=1: stage stamps (pinned host), printed at destroy
     // pipelined allreduce (coll_pipe.hip): per-chunk ready flags in an uncached region that

@@ -187,8 +187,37 @@ def svc_pull_checks(pkg, comm, rank, size, oracle, torch):
     served = comm.get("SVC_CALLS") - calls0
     assert served >= 3 * 4 * 4, f"the service served {served} pull calls"
     comm.set("ALLREDUCE_ALG", 0)
+    # allgather / bcast copied by the service (LL_PULL_AG / LL_PULL_BC): 16-B multiples, odd sizes
+    # (word and byte copies), odd offsets, in place
+    assert comm.get("SVC_PULL_COPY_MAX_BYTES") == 1 << 20
+    comm.set("SVC_PULL_COPY_MAX_BYTES", 1 << 19)
+    assert comm.get("SVC_PULL_COPY_MAX_BYTES") == 1 << 19
+    comm.set("SVC_PULL_COPY_MAX_BYTES", 1 << 20)
+    calls1 = comm.get("SVC_CALLS")
+    # the last size is above the copy limit: host-synchronised flows, not counted
+    for nb in (svc_max + 16, svc_max + 1, 100_003, (1 << 20) - 4, (1 << 20) + 16):
+        for inplace in (False, True):
+            for shift in (0, 3):
+                src = torch.full((nb + shift,), (rank * 3 + nb) % 251, dtype=torch.uint8, device="cuda")
+                dst = torch.zeros(nb * size + shift, dtype=torch.uint8, device="cuda")
+                if inplace:
+                    dst[shift + rank * nb: shift + (rank + 1) * nb] = (rank * 3 + nb) % 251
+                torch.cuda.synchronize()
+                comm.allgather(None if inplace else src.data_ptr() + shift, dst.data_ptr() + shift, nb)
+                assert comm.last_algorithm() == 1
+                for r in range(size):
+                    blk = dst[shift + r * nb: shift + (r + 1) * nb]
+                    assert bool(torch.all(blk == (r * 3 + nb) % 251).item()), ("pull allgather", nb, inplace, shift, r)
+                src.fill_(0)  # reused at once: every peer is done reading it
+        for root in range(size):
+            b = torch.full((nb + 5,), (rank * 7 + nb) % 251, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
+            comm.bcast(b.data_ptr() + 5, nb, root)
+            assert bool(torch.all(b[5:] == (root * 7 + nb) % 251).item()), ("pull bcast", nb, root)
+    copies = comm.get("SVC_CALLS") - calls1
+    assert copies == 4 * 2 * 2 + 4 * size, f"the service served {copies} allgather / bcast calls"
     comm.set("SVC_PULL_MAX_BYTES", saved)
-    print(f"rank {rank} pull OK ({served} service calls)", flush=True)
+    print(f"rank {rank} pull OK ({served} allreduce and {copies} allgather / bcast service calls)", flush=True)
 
 
 def staged(pkg, comm, rank, size, torch, key):
@@ -609,8 +638,8 @@ def svc_mode(key, rank, size, dev):
 def svc_stress(key, rank, size, dev):
     """a long random mix of calls every rank makes in the same order (shared seed): small allreduces
     and reduces through the resident service's LL form, 32-128 KiB ones through its pull form, in
-    place (host flows), 1 MiB ones (host flows: the service steps aside), allgather and bcast of LL
-    sizes, and pauses shorter and longer than the idle limit (the service leaves and comes back, and
+    place (host flows), 1 MiB ones (host flows: the service steps aside), allgather and bcast up to
+    128 KiB (LL and pull-copy forms), and pauses shorter and longer than the idle limit (the service leaves and comes back, and
     a pause can end just as it leaves) -- every result checked exactly"""
     import time
     import torch
@@ -661,7 +690,7 @@ def svc_stress(key, rank, size, dev):
             if rank == root:
                 assert bool(torch.all(y == sum(base + r for r in range(size))).item()), (it, kind, n, root)
         elif kind == "allgather":
-            nb = int(rng.integers(1, 32 << 10))
+            nb = int(rng.integers(1, 128 << 10))
             src = torch.full((nb,), (rank + it) % 251, dtype=torch.uint8, device="cuda")
             dst = torch.zeros(nb * size, dtype=torch.uint8, device="cuda")
             torch.cuda.synchronize()
@@ -669,7 +698,7 @@ def svc_stress(key, rank, size, dev):
             for r in range(size):
                 assert bool(torch.all(dst[r * nb:(r + 1) * nb] == (r + it) % 251).item()), (it, kind, nb, r)
         else:  # bcast
-            nb = int(rng.integers(1, 32 << 10))
+            nb = int(rng.integers(1, 128 << 10))
             root = int(rng.integers(0, size))
             b = torch.full((nb,), (rank * 7 + it) % 251, dtype=torch.uint8, device="cuda")
             torch.cuda.synchronize()

@@ -31,17 +31,26 @@ static int run(int rank, int n, int reps, const char *key, const char *paths)
     }
     size_t sizes[16] = {8, 1024, 65536, 1 << 20};
     int nsizes = 4;
-    const char *ss = getenv("SMALL_SIZES");  /* comma list of byte counts (<= 1 MiB) */
+    const char *ss = getenv("SMALL_SIZES");  /* comma list of byte counts (<= 64 MiB) */
     if (ss) {
         char buf[256];
         snprintf(buf, sizeof(buf), "%s", ss);
         nsizes = 0;
         for (char *p = strtok(buf, ","); p && nsizes < 16; p = strtok(NULL, ",")) sizes[nsizes++] = strtoull(p, NULL, 10);
     }
+    /* buffers sized for the largest message (allgather: n blocks of it); refuse what they cannot hold */
+    size_t maxb = 0;
+    for (int k = 0; k < nsizes; ++k) maxb = sizes[k] > maxb ? sizes[k] : maxb;
+    if (maxb == 0 || maxb > ((size_t)64 << 20)) {
+        fprintf(stderr, "SMALL_SIZES: sizes must be 1 .. 64 MiB\n");
+        return 1;
+    }
     void *s = NULL, *r = NULL;
-    mi355x_malloc(&s, 1 << 20);
-    mi355x_malloc(&r, 1 << 20);
-    mi355x_memset_async(s, 0, 1 << 20, NULL);
+    if (mi355x_malloc(&s, maxb) || mi355x_malloc(&r, (size_t)n * maxb)) {
+        fprintf(stderr, "rank %d: %s\n", rank, mi355x_last_error());
+        return 1;
+    }
+    mi355x_memset_async(s, 0, maxb, NULL);
     mi355x_device_sync();
     char pl[128];
     snprintf(pl, sizeof(pl), "%s", paths);
@@ -63,20 +72,25 @@ static int run(int rank, int n, int reps, const char *key, const char *paths)
     /* SMALL_TYPE / SMALL_OP: the (type, op) slot (default 14 = MPI_FLOAT, 3 = MPI_SUM), 4-B types */
     const int ty = getenv("SMALL_TYPE") ? atoi(getenv("SMALL_TYPE")) : 14;
     const int op = getenv("SMALL_OP") ? atoi(getenv("SMALL_OP")) : 3;
+    /* SMALL_COLL: allreduce (default), allgather (bytes per rank) or bcast (from rank 0) */
+    const char *coll = getenv("SMALL_COLL") ? getenv("SMALL_COLL") : "allreduce";
+    const int kind = strcmp(coll, "allgather") == 0 ? 1 : strcmp(coll, "bcast") == 0 ? 2 : 0;
     for (int k = 0; k < nsizes; ++k) {
         const size_t cnt = sizes[k] / 4;
-        for (int i = 0; i < 50; ++i) mi355x_allreduce(c, s, r, cnt, ty, op, NULL);
+#define ONE_CALL() (kind == 1 ? mi355x_allgather(c, s, r, sizes[k], NULL) \
+                   : kind == 2 ? mi355x_bcast(c, s, sizes[k], 0, NULL) : mi355x_allreduce(c, s, r, cnt, ty, op, NULL))
+        for (int i = 0; i < 50; ++i) ONE_CALL();
         mi355x_comm_barrier(c);
         const double t0 = now_us();
         for (int i = 0; i < reps; ++i)
-            if (mi355x_allreduce(c, s, r, cnt, ty, op, NULL)) {
+            if (ONE_CALL()) {
                 fprintf(stderr, "rank %d: %s\n", rank, mi355x_last_error());
                 return 1;
             }
         const double us = (now_us() - t0) / reps;
         if (rank == 0)
-            printf("{\"path\": \"%s\", \"bytes\": %zu, \"us_per_call\": %.2f, \"alg\": %d, \"n\": %d, "
-                   "\"caller\": \"C\"}\n", path, sizes[k], us, mi355x_comm_last_algorithm(c), n);
+            printf("{\"coll\": \"%s\", \"path\": \"%s\", \"bytes\": %zu, \"us_per_call\": %.2f, \"alg\": %d, "
+                   "\"n\": %d, \"caller\": \"C\"}\n", coll, path, sizes[k], us, mi355x_comm_last_algorithm(c), n);
     }
     }
     mi355x_comm_barrier(c);
