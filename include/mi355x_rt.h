@@ -180,7 +180,10 @@ enum mi355x_knob {
                                            not in place, above SVC_MAX_BYTES and up to this many bytes per
                                            rank: the resident service evaluates it from the peers' mapped
                                            inputs (buffers 16-B aligned on every rank) instead of a launch
-                                           and a host barrier; 0 = never; reads 0 without a service */
+                                           and a host barrier; also the largest block of a
+                                           reduce_scatter(_block), not in place, that the service
+                                           evaluates from the peers' inputs (any size up to it);
+                                           0 = never; reads 0 without a service */
     MI355X_KNOB_SVC_PULL_COPY_MAX_BYTES = 24 /* (per communicator, same value on every rank; env
                                            MI355X_SVC_PULL_COPY_MAX_BYTES at creation) allgather / bcast
                                            above SVC_MAX_BYTES and up to this many bytes per rank (default

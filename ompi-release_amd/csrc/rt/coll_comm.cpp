@@ -1714,6 +1714,51 @@ static void ll_program(LLArgs &a, const Program &pr)
     a.role_mask = pr.role_mask;
 }
 
+// MPI_Reduce_scatter(_block) served by the resident service (LL_PULL_RS): after the handle
+// exchange every rank evaluates its own block from the n mapped inputs with the reference
+// schedule's per-element program (fold order or tree, as the LL form evaluates it), stores it
+// write-through into rbuf, and completes once every peer has read its input -- the launch, the
+// completion wait and the finishing barrier of the host-synchronised flow are gone.  Not in place
+// (MPI_IN_PLACE is all-or-none: the block would overwrite input the peers still read).  Every
+// rank decides alike: the largest block, the program and the sizes are the same everywhere.
+static bool svc_rs_usable(const mi355x_comm *c, size_t max_block_bytes, const Program &pr)
+{
+    return c->svc_ok && !c->loopback && c->size >= 2 && c->size <= kLLMaxRanks && max_block_bytes <= c->svc_pull_max &&
+           (pr.is_fold ? pr.order.size() == (size_t)c->size
+                       : (c->size <= kTreeMax && pr.steps.size() <= (size_t)kTreeSteps));
+}
+
+// off: my block's byte offset in every rank's input; bytes: my block's length
+static int svc_rs_run(mi355x_comm *c, int op, int type, const Program &pr, const std::vector<std::vector<void *>> &P,
+                      const void *in, size_t off, void *rbuf, size_t bytes, size_t esz)
+{
+    int rc = ensure_ll(c);
+    if (rc) return rc;
+    LLArgs a;
+    std::memset(&a, 0, sizeof(a));
+    ll_program(a, pr);
+    SvcCall call;
+    std::memset(&call, 0, sizeof(call));
+    call.seq = ++c->ll_seq;
+    call.src = in;
+    call.dst = rbuf;
+    call.nbytes = bytes;
+    call.count = bytes / esz;
+    call.role_mask = a.role_mask;
+    call.op = op;
+    call.type = type;
+    call.mode = LL_PULL_RS;
+    call.prog = a.prog;
+    call.nsteps = a.nsteps;
+    call.result = a.result;
+    for (int q = 0; q < c->size; ++q) {
+        call.order[q] = a.order[q];
+        call.srcs[q] = (const char *)P[0][q] + off;
+    }
+    for (int k = 0; k < a.nsteps; ++k) call.steps[k] = a.steps[k];
+    return svc_call(c, call, (bytes + kLLChunk - 1) / kLLChunk);
+}
+
 // ----------------------------------------------------------------- algorithm choice
 // The order of coll/tuned's dec_dynamic functions (coll_tuned_decision_dynamic.c:59-99): a file
 // rule for this communicator size and message size, else the forced (MCA) algorithm, else the
@@ -2632,8 +2677,13 @@ static int reduce_scatter_block_impl(mi355x_comm_t *c, const void *sbuf, void *r
     const uint64_t sig[4] = {2, rcount, (uint64_t)type, (uint64_t)op};
     std::vector<std::vector<void *>> P;
     bool staged = false;
+    const bool pull_cand = !inplace && svc_rs_usable(c, rcount * esz, pr);  // the resident service evaluates
+    c->svc_keep = pull_cand;
     rc = exchange(c, 1, mine, sig, P, &staged);
+    c->svc_keep = false;
     if (rc) return rc;
+    if (pull_cand && !staged) return svc_rs_run(c, op, type, pr, P, in, (size_t)c->rank * rcount * esz, rbuf, rcount * esz, esz);
+    if (pull_cand) svc_park(c);
     if (staged) {
         std::vector<size_t> boff(c->size), blen(c->size, rcount);
         for (int q = 0; q < c->size; ++q) boff[q] = (size_t)q * rcount;
@@ -2691,8 +2741,6 @@ static int reduce_scatter_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, c
     const uint64_t sig[4] = {3, h, (uint64_t)type, (uint64_t)op};
     std::vector<std::vector<void *>> P;
     bool staged = false;
-    rc = exchange(c, 1, mine, sig, P, &staged);
-    if (rc) return rc;
     Program pr;
     if (c->size == 1) {
         pr.is_fold = true;
@@ -2711,6 +2759,15 @@ static int reduce_scatter_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, c
         if (!compile_expr(ep, roots[c->rank], c->size, &pr))
             return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
     }
+    size_t max_block = 0;
+    for (int r = 0; r < c->size; ++r) max_block = std::max(max_block, (size_t)rcounts[r]);
+    const bool pull_cand = !inplace && svc_rs_usable(c, max_block * esz, pr);  // the resident service evaluates
+    c->svc_keep = pull_cand;
+    rc = exchange(c, 1, mine, sig, P, &staged);
+    c->svc_keep = false;
+    if (rc) return rc;
+    if (pull_cand && !staged) return svc_rs_run(c, op, type, pr, P, in, disp[c->rank] * esz, rbuf, mine_n * esz, esz);
+    if (pull_cand) svc_park(c);
     void *dst0 = inplace ? c->scratch : rbuf;
     if (staged) {
         std::vector<size_t> boff(disp.begin(), disp.end() - 1), blen(c->size);

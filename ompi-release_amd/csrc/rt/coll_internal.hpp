@@ -80,7 +80,8 @@ constexpr int kLLMaxRanks = 8;     // sources held in registers per thread
 enum { LL_AR = 0, LL_AG = 1, LL_BC = 2, LL_RED = 3,     // allreduce, allgather, bcast, reduce
        LL_PULL = 4,    // (resident service only) one-phase allreduce pulled from the peers' mapped inputs,
        LL_PULL_AG = 5, // allgather and
-       LL_PULL_BC = 6 };  // bcast copied from them
+       LL_PULL_BC = 6, // bcast copied from them,
+       LL_PULL_RS = 7 };  // reduce_scatter(_block): this rank's block evaluated from them
 enum { LL_FOLD = 0, LL_RING = 1, LL_TREE = 2 };   // per-element program of LL_AR
 struct LLArgs {
     const void *src;                   // this rank's data (NULL: nothing to push)

@@ -23,8 +23,10 @@
 //   4. it counts itself done once its stores have reached memory; the workgroup that completes
 //      the count (or the only one, for a call of one slice) acknowledges the call to every peer
 //      (the LL parity protocol) and stores the call number into the host's completion word.
-// The pull form (LL_PULL, the one-phase ring allreduce of 32-128 KiB) replaces step 3's granules
-// by reads of the peers' mapped inputs, and step 4 waits until every peer has read this rank's.
+// The pull forms (LL_PULL, the one-phase ring allreduce of 32-128 KiB; LL_PULL_AG / LL_PULL_BC,
+// allgather and bcast to 1 MiB; LL_PULL_RS, reduce_scatter(_block) up to 128 KiB per block) replace
+// step 3's granules by reads of the peers' mapped inputs, and step 4 waits until every peer has
+// read this rank's.
 // Every wait is bounded (timeout_ticks; the error word is set and the workgroup leaves).
 #include "coll_ll_dev.hpp"
 #include "slot_list.hpp"
@@ -172,8 +174,8 @@ static __device__ void svc_pull_copy(const LLArgs &a, const SvcCall &sc, uint64_
     }
 }
 
-// Step 3's second half for every slice of this workgroup: receive the peers' granules, then the
-// reference program per element (or the copy); or the pull form.  One out-of-line function per
+// Step 3's second half for every slice of this workgroup: receive the peers' granules (LL_PULL_RS:
+// read the peers' blocks), then the reference program per element (or the copy); or the pull form.  One out-of-line function per
 // (op, type) slot, entered once per call: the call's slot decides which (inlining every slot's
 // evaluation into one body makes the compiler's register allocation take tens of minutes; the
 // hot float / double SUM slots are inlined, svc_finish_call).  Returns 1 on a timeout.
@@ -202,7 +204,18 @@ static __device__ __forceinline__ int svc_finish_body(const LLArgs &a, const Svc
         uint32_t w[8][4];
         int bad = 0;
         if (k.ngran) {
-            bad = !ll_recv(a, k, a.recv_mask, w);
+            bool pulled = false;
+            if constexpr (!F::kCopy) {
+                if (a.mode == LL_PULL_RS) {  // this thread's 16 B of every rank's block, where they are
+#pragma unroll
+                    for (int q = 0; q < kLLMaxRanks; ++q) {
+                        w[q][0] = w[q][1] = w[q][2] = w[q][3] = 0;
+                        if (q < a.n) ll_read16<true>(static_cast<const char *>(sc.srcs[q]), k.off, k.len, w[q]);
+                    }
+                    pulled = true;
+                }
+            }
+            if (!pulled) bad = !ll_recv(a, k, a.recv_mask, w);
             if (tr && threadIdx.x == 0 && c == blockIdx.x) tr[4] = __builtin_amdgcn_s_memrealtime();
             if (!bad) {
                 if constexpr (F::kCopy)
@@ -382,8 +395,8 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
         // no acquire or release fence per call.
         const uint64_t nchunks = (a.nbytes + kLLChunk - 1) / kLLChunk;
         // pull forms: no granules, the inputs are read where they are
-        const bool pull = a.mode == LL_PULL || a.mode == LL_PULL_AG || a.mode == LL_PULL_BC;
-        const bool reduce = a.mode == LL_AR || a.mode == LL_RED || a.mode == LL_PULL;
+        const bool pull = a.mode == LL_PULL || a.mode == LL_PULL_AG || a.mode == LL_PULL_BC || a.mode == LL_PULL_RS;
+        const bool reduce = a.mode == LL_AR || a.mode == LL_RED || a.mode == LL_PULL || a.mode == LL_PULL_RS;
         const bool evaluate = reduce ? !(a.mode == LL_RED && me != a.root) : (a.recv_mask != 0 || pull);
         // push every slice of mine (inputs read kSvcPass slices at a time, so their latencies
         // overlap; the acknowledgement wait once, behind the first reads), then receive and finish

@@ -269,7 +269,8 @@ struct mi355x_comm {
     double svc_idle_s = 0.001;
     uint64_t svc_calls = 0, svc_launches = 0;
     // one-phase ring-ordered allreduce above svc_max and up to svc_pull_max bytes per rank served by
-    // the service from the peers' mapped inputs (LL_PULL; MI355X_SVC_PULL_MAX_BYTES)
+    // the service from the peers' mapped inputs (LL_PULL; MI355X_SVC_PULL_MAX_BYTES); also the
+    // largest block of a reduce_scatter(_block) the service evaluates (LL_PULL_RS, any size up to it)
     // (128 KiB by default: one-GPU rehearsal with 16 service workgroups, np = 2: 64 KiB 12.1 vs 17.4 us,
     // 128 KiB 15.2 vs 18.7, 256 KiB 22.1 vs 17.5; np = 4: 17.5 vs 25.9, 22.4 vs 23.7, 33.0 vs 22.9 --
     // the service's 16 workgroups are latency-bound where a one-shot launch has the whole GPU;

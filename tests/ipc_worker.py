@@ -217,7 +217,66 @@ def svc_pull_checks(pkg, comm, rank, size, oracle, torch):
     copies = comm.get("SVC_CALLS") - calls1
     assert copies == 4 * 2 * 2 + 4 * size, f"the service served {copies} allgather / bcast calls"
     comm.set("SVC_PULL_MAX_BYTES", saved)
-    print(f"rank {rank} pull OK ({served} allreduce and {copies} allgather / bcast service calls)", flush=True)
+    rs = svc_rs_checks(pkg, comm, rank, size, oracle, torch)
+    print(f"rank {rank} pull OK ({served} allreduce, {copies} allgather / bcast, {rs} reduce_scatter service calls)",
+          flush=True)
+
+
+def svc_rs_checks(pkg, comm, rank, size, oracle, torch):
+    """reduce_scatter(_block) evaluated by the resident service from the peers' mapped inputs
+    (LL_PULL_RS, coll_svc.hip): every reduce_scatter algorithm (decision, non-overlapping's reduce
+    tree, recursive halving's trees, ring folds) over 1- to 16-byte types, single-element, ragged,
+    empty and 128 KiB blocks, against the oracle's schedule simulation; a block above the pull
+    limit and the in-place forms take the host-synchronised flows"""
+    ptrs = lambda arrs: (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    limit = comm.get("SVC_PULL_MAX_BYTES")
+    calls0 = comm.get("SVC_CALLS")
+    expect = 0
+    for rsalg in (0, 1, 2, 3):
+        comm.set("REDUCE_SCATTER_ALG", rsalg)
+        for opname, tname in [("SUM", "FLOAT"), ("MAX", "DOUBLE"), ("MINLOC", "FLOAT_INT"), ("PROD", "C_DOUBLE_COMPLEX"),
+                              ("BXOR", "INT8"), ("SUM", "INT16")]:
+            op, ty = pkg.OP[opname], pkg.T[tname]
+            esz = pkg.type_size(ty)
+            for rcounts in ([1] * size, [7 * r + 3 for r in range(size)], [0 if r == 1 else 5000 + r for r in range(size)],
+                            [limit // esz - r for r in range(size)], [limit // esz + 1] + [3] * (size - 1)):
+                total = sum(rcounts)
+                xs = [opdata.make(tname, total, 900 + 10 * rsalg + r) for r in range(size)]
+                outs = [np.zeros(max(k, 1), dtype=xs[0].dtype) for k in rcounts]
+                rc = (ctypes.c_int * size)(*rcounts)
+                assert oracle.oracle_reduce_scatter_alg(rsalg, size, rc, ty, op, ptrs(xs), ptrs(outs)) >= 0
+                dx = torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda()
+                dr = torch.full((max(rcounts[rank], 1) * esz,), 0x5a, dtype=torch.uint8, device="cuda")
+                torch.cuda.synchronize()
+                comm.reduce_scatter(dx.data_ptr(), dr.data_ptr(), rcounts, ty, op)
+                mine = rcounts[rank]
+                if mine:
+                    got = dr.cpu().numpy().view(xs[0].dtype)[:mine]
+                    opdata.assert_same(tname, opname, got, outs[rank][:mine],
+                                       f"service rs alg={rsalg} rcounts={rcounts[:3]} rank={rank}")
+                dx.fill_(0x7f)  # reused at once: every peer is done reading it
+                expect += max(rcounts) * esz <= limit
+    comm.set("REDUCE_SCATTER_ALG", 0)
+    # reduce_scatter_block (the reduce decision's program per block), not in place and in place
+    for opname, tname in [("SUM", "FLOAT"), ("MAXLOC", "DOUBLE_INT"), ("BAND", "UINT8")]:
+        op, ty = pkg.OP[opname], pkg.T[tname]
+        esz = pkg.type_size(ty)
+        for rcount in (1, 1001, limit // esz):
+            xs = [opdata.make(tname, rcount * size, 950 + r) for r in range(size)]
+            outs = [np.zeros(rcount, dtype=xs[0].dtype) for _ in range(size)]
+            assert oracle.oracle_reduce_scatter_block(size, rcount, ty, op, ptrs(xs), ptrs(outs)) >= 0
+            for inplace in (False, True):
+                dx = torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda()
+                dr = dx.clone() if inplace else torch.full((rcount * esz,), 0x5a, dtype=torch.uint8, device="cuda")
+                torch.cuda.synchronize()
+                comm.reduce_scatter_block(None if inplace else dx.data_ptr(), dr.data_ptr(), rcount, ty, op)
+                got = dr[:rcount * esz].cpu().numpy().view(xs[0].dtype)
+                opdata.assert_same(tname, opname, got, outs[rank], f"service rsb rcount={rcount} inplace={inplace} rank={rank}")
+                dx.fill_(0x7f)
+                expect += not inplace
+    served = comm.get("SVC_CALLS") - calls0
+    assert served == expect, f"the service served {served} reduce_scatter calls, expected {expect}"
+    return served
 
 
 def staged(pkg, comm, rank, size, torch, key):
@@ -651,8 +710,8 @@ def svc_stress(key, rank, size, dev):
     f32, f64, i32 = pkg.T["FLOAT"], pkg.T["DOUBLE"], pkg.T["INT32"]
     SUM, MAX = pkg.OP["SUM"], pkg.OP["MAX"]
     iters = int(os.environ.get("SVC_STRESS_ITERS", "6000"))
-    kinds = ["ar_small", "ar_pull", "ar_inplace", "ar_host", "reduce", "allgather", "bcast", "pause"]
-    probs = [0.35, 0.15, 0.08, 0.05, 0.1, 0.1, 0.07, 0.1]
+    kinds = ["ar_small", "ar_pull", "ar_inplace", "ar_host", "reduce", "allgather", "bcast", "pause", "rs"]
+    probs = [0.3, 0.14, 0.08, 0.05, 0.1, 0.09, 0.07, 0.09, 0.08]
     counts = {k: 0 for k in kinds}
     calls0, launches0 = comm.get("SVC_CALLS"), comm.get("SVC_LAUNCHES")
     for it in range(iters):
@@ -697,6 +756,14 @@ def svc_stress(key, rank, size, dev):
             comm.allgather(src.data_ptr(), dst.data_ptr(), nb)
             for r in range(size):
                 assert bool(torch.all(dst[r * nb:(r + 1) * nb] == (r + it) % 251).item()), (it, kind, nb, r)
+        elif kind == "rs":  # reduce_scatter_block: service pull form, or the host flow in place
+            n = int(rng.integers(1, 40 << 10))
+            inplace = it % 4 == 0
+            x = torch.full((n * size,), base + rank, dtype=torch.float32, device="cuda")
+            y = x if inplace else torch.full((n,), -7.0, dtype=torch.float32, device="cuda")
+            torch.cuda.synchronize()
+            comm.reduce_scatter_block(None if inplace else x.data_ptr(), y.data_ptr(), n, f32, SUM)
+            assert bool(torch.all(y[:n] == sum(base + r for r in range(size))).item()), (it, kind, n, inplace)
         else:  # bcast
             nb = int(rng.integers(1, 128 << 10))
             root = int(rng.integers(0, size))

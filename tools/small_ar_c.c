@@ -72,13 +72,16 @@ static int run(int rank, int n, int reps, const char *key, const char *paths)
     /* SMALL_TYPE / SMALL_OP: the (type, op) slot (default 14 = MPI_FLOAT, 3 = MPI_SUM), 4-B types */
     const int ty = getenv("SMALL_TYPE") ? atoi(getenv("SMALL_TYPE")) : 14;
     const int op = getenv("SMALL_OP") ? atoi(getenv("SMALL_OP")) : 3;
-    /* SMALL_COLL: allreduce (default), allgather (bytes per rank) or bcast (from rank 0) */
+    /* SMALL_COLL: allreduce (default), allgather (bytes per rank), bcast (from rank 0) or
+     * reduce_scatter_block (bytes per rank's block; the input is n blocks) */
     const char *coll = getenv("SMALL_COLL") ? getenv("SMALL_COLL") : "allreduce";
-    const int kind = strcmp(coll, "allgather") == 0 ? 1 : strcmp(coll, "bcast") == 0 ? 2 : 0;
+    const int kind = strcmp(coll, "allgather") == 0 ? 1 : strcmp(coll, "bcast") == 0 ? 2
+                   : strcmp(coll, "reduce_scatter_block") == 0 ? 3 : 0;
     for (int k = 0; k < nsizes; ++k) {
         const size_t cnt = sizes[k] / 4;
 #define ONE_CALL() (kind == 1 ? mi355x_allgather(c, s, r, sizes[k], NULL) \
-                   : kind == 2 ? mi355x_bcast(c, s, sizes[k], 0, NULL) : mi355x_allreduce(c, s, r, cnt, ty, op, NULL))
+                   : kind == 2 ? mi355x_bcast(c, s, sizes[k], 0, NULL) \
+                   : kind == 3 ? mi355x_reduce_scatter_block(c, r, s, cnt, ty, op, NULL) : mi355x_allreduce(c, s, r, cnt, ty, op, NULL))
         for (int i = 0; i < 50; ++i) ONE_CALL();
         mi355x_comm_barrier(c);
         const double t0 = now_us();
