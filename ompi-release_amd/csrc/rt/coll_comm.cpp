@@ -1414,6 +1414,7 @@ static int svc_setup(mi355x_comm *c)
     c->svc_nwg = (int)std::min(64.0, std::max(1.0, env_double("MI355X_SVC_WGS", (double)c->svc_nwg)));
     c->svc_pull_max = (size_t)std::max(0.0, env_double("MI355X_SVC_PULL_MAX_BYTES", (double)c->svc_pull_max));
     c->svc_copy_max = (size_t)std::max(0.0, env_double("MI355X_SVC_PULL_COPY_MAX_BYTES", (double)c->svc_copy_max));
+    c->svc_rs = env_double("MI355X_SVC_RS", 0.0) != 0.0;
     const char *env = getenv("MI355X_SVC");
     const bool want = c->ll_ok && c->size <= kLLMaxRanks && !(env && atoi(env) == 0);
     if (want) {
@@ -1723,7 +1724,7 @@ static void ll_program(LLArgs &a, const Program &pr)
 // rank decides alike: the largest block, the program and the sizes are the same everywhere.
 static bool svc_rs_usable(const mi355x_comm *c, size_t max_block_bytes, const Program &pr)
 {
-    return c->svc_ok && !c->loopback && c->size >= 2 && c->size <= kLLMaxRanks && max_block_bytes <= c->svc_pull_max &&
+    return c->svc_ok && c->svc_rs && !c->loopback && c->size >= 2 && c->size <= kLLMaxRanks && max_block_bytes <= c->svc_pull_max &&
            (pr.is_fold ? pr.order.size() == (size_t)c->size
                        : (c->size <= kTreeMax && pr.steps.size() <= (size_t)kTreeSteps));
 }

@@ -283,6 +283,9 @@ struct mi355x_comm {
     // 16.8; np = 4: 11.9 vs 20.7, 19.2 vs 23.1; bcast np = 2 512 KiB 8.8 vs 15.3;
     // profiles/r03_svc_pull_copy.log).  bcast of 1 MiB and more takes the scatter + allgather shape.
     size_t svc_copy_max = (size_t)1 << 20;
+    // reduce_scatter(_block) through the service (LL_PULL_RS): opt-in (MI355X_SVC_RS=1) until it
+    // has run on a GPU
+    bool svc_rs = false;
     bool svc_keep = false;                        // this call's exchange leaves the service resident
     uint64_t *svc_trace = nullptr;                // MI355X_SVC_TRACE=1: stage stamps (pinned host), printed at destroy
     // pipelined allreduce (coll_pipe.hip): per-chunk ready flags in an uncached region that
