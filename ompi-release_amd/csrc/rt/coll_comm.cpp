@@ -1414,7 +1414,7 @@ static int svc_setup(mi355x_comm *c)
     c->svc_nwg = (int)std::min(64.0, std::max(1.0, env_double("MI355X_SVC_WGS", (double)c->svc_nwg)));
     c->svc_pull_max = (size_t)std::max(0.0, env_double("MI355X_SVC_PULL_MAX_BYTES", (double)c->svc_pull_max));
     c->svc_copy_max = (size_t)std::max(0.0, env_double("MI355X_SVC_PULL_COPY_MAX_BYTES", (double)c->svc_copy_max));
-    c->svc_rs = env_double("MI355X_SVC_RS", 0.0) != 0.0;
+    c->svc_rs = env_double("MI355X_SVC_RS", c->svc_rs ? 1.0 : 0.0) != 0.0;
     const char *env = getenv("MI355X_SVC");
     const bool want = c->ll_ok && c->size <= kLLMaxRanks && !(env && atoi(env) == 0);
     if (want) {

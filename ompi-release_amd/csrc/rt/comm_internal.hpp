@@ -283,9 +283,10 @@ struct mi355x_comm {
     // 16.8; np = 4: 11.9 vs 20.7, 19.2 vs 23.1; bcast np = 2 512 KiB 8.8 vs 15.3;
     // profiles/r03_svc_pull_copy.log).  bcast of 1 MiB and more takes the scatter + allgather shape.
     size_t svc_copy_max = (size_t)1 << 20;
-    // reduce_scatter(_block) through the service (LL_PULL_RS): opt-in (MI355X_SVC_RS=1) until it
-    // has run on a GPU
-    bool svc_rs = false;
+    // reduce_scatter(_block) through the service (LL_PULL_RS): on by default since round 4 (exact on
+    // the GPU at 2 and 3 ranks; np = 2 10.2-16.1 vs 17.0-19.4 us, np = 4 12.5-21.1 vs 20.6-22.2 us for
+    // the host-synchronised flow, profiles/r04_svc_rs_latency.jsonl); MI355X_SVC_RS=0 turns it off
+    bool svc_rs = true;
     bool svc_keep = false;                        // this call's exchange leaves the service resident
     uint64_t *svc_trace = nullptr;                // MI355X_SVC_TRACE=1: stage stamps (pinned host), printed at destroy
     // pipelined allreduce (coll_pipe.hip): per-chunk ready flags in an uncached region that

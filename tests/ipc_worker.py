@@ -217,8 +217,8 @@ def svc_pull_checks(pkg, comm, rank, size, oracle, torch):
     copies = comm.get("SVC_CALLS") - calls1
     assert copies == 4 * 2 * 2 + 4 * size, f"the service served {copies} allgather / bcast calls"
     comm.set("SVC_PULL_MAX_BYTES", saved)
-    # (the reduce_scatter form is opt-in, MI355X_SVC_RS=1, until it has run on a GPU)
-    rs = svc_rs_checks(pkg, comm, rank, size, oracle, torch) if os.environ.get("MI355X_SVC_RS") == "1" else 0
+    # the reduce_scatter form (on by default; MI355X_SVC_RS=0 turns it off on every rank)
+    rs = svc_rs_checks(pkg, comm, rank, size, oracle, torch) if os.environ.get("MI355X_SVC_RS", "1") != "0" else 0
     print(f"rank {rank} pull OK ({served} allreduce, {copies} allgather / bcast, {rs} reduce_scatter service calls)",
           flush=True)
 
