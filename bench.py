@@ -41,8 +41,9 @@ def load_pkg():
 
 
 def pmc_traffic(kernel_key: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (corrected per
-    MI355X_MICROARCH.md §HBM: FETCH_SIZE x 2 for 16-B streaming reads), or None."""
+    """(HBM bytes per launch, the profiles/ file it is read from) from the newest committed
+    rocprofv3 PMC summary holding the kernel (corrected per MI355X_MICROARCH.md §HBM: FETCH_SIZE x 2
+    for 16-B streaming reads), or (None, None)."""
     for p in sorted((REPO / "profiles").glob("*pmc*.json"), reverse=True):
         try:
             d = json.loads(p.read_text())
@@ -50,8 +51,8 @@ def pmc_traffic(kernel_key: str):
             continue
         ent = d.get("kernels", {}).get(kernel_key)
         if ent and "hbm_bytes_per_launch" in ent:
-            return ent["hbm_bytes_per_launch"]
-    return None
+            return ent["hbm_bytes_per_launch"], f"profiles/{p.name}"
+    return None, None
 
 
 def cpu_baseline_op(target_s: float = 10.0):
@@ -139,7 +140,7 @@ def bench_op(args, pkg, torch):
     alg_bytes = 3 * n * 4
     value = alg_bytes * args.steps / wall / 1e9
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
-    traffic = pmc_traffic("op_3buff_sum_float")
+    traffic, traffic_from = pmc_traffic("op_3buff_sum_float")
     u, bpc, nt = pkg.get_tune()
     return {
         "metric": "MPI_Allreduce busbw GB/s (1 GiB fp32, np=8) + op/hip reduce HBM GB/s",
@@ -158,7 +159,7 @@ def bench_op(args, pkg, torch):
                    "count": n, "bytes_per_operand": n * 4, "launch": {"unroll": u, "blocks_per_cu": bpc,
                                                                       "nontemporal": nt}},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_from": traffic_from,
                      "kernel_avg_ms": round(avg_ms, 5), "kernel_avg_from": "HIP events around the K launches / K",
                      "alg_bytes_per_launch": alg_bytes},
     }

@@ -138,6 +138,8 @@ extern int mca_coll_mi355x_priority;            /* 90 */
 extern int mca_coll_mi355x_allreduce_algorithm; /* 0 = tuned decision, else coll_tuned numbering */
 extern int mca_coll_mi355x_pml_hook;            /* 1 = point-to-point on engine communicators through the engine */
 extern int mca_coll_mi355x_mixed_buffers;       /* 1 = ranks may mix host and device buffers in a call */
+extern int mca_coll_mi355x_rcache_max_maps;     /* peer mappings kept open per communicator (0 = unlimited) */
+extern unsigned long long mca_coll_mi355x_rcache_size_limit; /* the same in bytes (mpool_rgpusm_rcache_size_limit) */
 
 #ifdef __cplusplus
 }

@@ -112,6 +112,12 @@ int mi355x_comm_vote(mi355x_comm_t *comm, int device, int *any_device);
  * 3 recursive doubling, 4 ring, 5 segmented ring; reduce: 1 linear, 2 chain, 3 pipeline, 4 binary,
  * 5 binomial; reduce_scatter: 1 non-overlapping, 2 recursive halving, 3 ring) */
 int mi355x_comm_last_algorithm(const mi355x_comm_t *comm);
+/* Test hook (no reference counterpart): take (acquire = 1) or give back (0) the communicator's
+ * pipelined-grid admission token of its GPU outside any call, as a rank inside a pipelined
+ * allreduce holds it.  Returns 1 if the token is now held.  Tests kill a holder with SIGKILL and
+ * check that the next communicator on that GPU is admitted again (the token is reclaimed from a
+ * dead process, coll_comm.cpp). */
+int mi355x_debug_pipe_token(mi355x_comm_t *comm, int acquire);
 
 /* Knobs BLOCKS_PER_CU, PUSH, COPY_BLOCK_KIB, PIPE_WG_PER_CU, PIPE_CHUNK_KIB and PIPE_WT are launch
  * shapes shared by every communicator of the process (setting one through any communicator sets
@@ -146,7 +152,7 @@ enum mi355x_knob {
                                            0: two phases separated by a host barrier.  Default (environment
                                            MI355X_PIPE=0/1 at creation overrides): 1 from 4 ranks up,
                                            where the one-GPU rehearsal measured it ahead (n = 4: 2.03 vs
-                                           2.14 ms, n = 8: 3.85 vs 4.47), 0 below (n = 2: 1.01 vs 0.93) */
+                                           2.14 ms, n = 8: 3.50-3.78 vs 4.47), 0 below (n = 2: 1.01 vs 0.93) */
     MI355X_KNOB_PIPE_WG_PER_CU = 14,    /* pipelined allreduce: 256-thread workgroups per CU (1..8, default 2) */
     MI355X_KNOB_PIPE_CHUNK_KIB = 15,    /* pipelined allreduce: chunk size in KiB (0 = auto: ~512 chunks
                                            per ring block, at least 64 KiB) */
@@ -184,11 +190,40 @@ enum mi355x_knob {
                                            reduce_scatter(_block), not in place, that the service
                                            evaluates from the peers' inputs (any size up to it);
                                            0 = never; reads 0 without a service */
-    MI355X_KNOB_SVC_PULL_COPY_MAX_BYTES = 24 /* (per communicator, same value on every rank; env
+    MI355X_KNOB_SVC_PULL_COPY_MAX_BYTES = 24, /* (per communicator, same value on every rank; env
                                            MI355X_SVC_PULL_COPY_MAX_BYTES at creation) allgather / bcast
                                            above SVC_MAX_BYTES and up to this many bytes per rank (default
                                            1 MiB): the resident service copies from the peers' mapped
                                            buffers instead of a launch and a host barrier; 0 = never */
+    MI355X_KNOB_RCACHE_MAX_MAPS = 25,   /* peer-mapping cache: at most this many hipIpc mappings of peers'
+                                           allocations stay open; least recently used ones beyond it are
+                                           closed (mpool_rgpusm's LRU, mpool_rgpusm_module.c:104-120).  0 =
+                                           unlimited (default; env MI355X_RCACHE_MAX_MAPS at creation) */
+    MI355X_KNOB_RCACHE_SIZE_LIMIT = 26, /* the same bound in bytes of the mapped allocations
+                                           (mpool_rgpusm_rcache_size_limit, mpool_rgpusm_component.c:92-100);
+                                           0 = unlimited (default; env MI355X_RCACHE_SIZE_LIMIT) */
+    MI355X_KNOB_PEER_MAPS = 27,         /* (read-only) hipIpc mappings of peers' allocations open now */
+    MI355X_KNOB_RCACHE_EVICTIONS = 28,  /* (read-only) mappings closed by the cache bounds */
+    MI355X_KNOB_FLOWS = 29,             /* (read-only) cross-device flows this communicator may use, a mask
+                                           of MI355X_FLOW_*: every default-on flow is self-tested for exact
+                                           results on changing data before its first use, the outcome agreed
+                                           by every rank, and a flow that failed on any rank stays off on
+                                           every rank (the host-synchronised flows take its calls) */
+    MI355X_KNOB_FLOWS_FAILED = 30,      /* (read-only) the flows whose self-test failed on some rank */
+    MI355X_KNOB_CREATE_US = 31,         /* (read-only) wall time of mi355x_comm_create, microseconds */
+    MI355X_KNOB_SELFTEST_US = 32,       /* (read-only) of which the flow self-tests at creation; plus the
+                                           service flows' self-test at the service's first claim */
+    MI355X_KNOB_SVC_OWNER = 33,         /* (read-only) 1 while this communicator owns its process's
+                                           resident service */
+    MI355X_KNOB_SVC_CLAIMS = 34         /* (read-only) times this communicator has taken the service */
+};
+/* cross-device flows (MI355X_KNOB_FLOWS) */
+enum mi355x_flow {
+    MI355X_FLOW_SVC_LL = 1,    /* resident service, LL form (granules pushed into the peers) */
+    MI355X_FLOW_SVC_PULL = 2,  /* resident service, one-phase ring allreduce from the peers' inputs */
+    MI355X_FLOW_SVC_COPY = 4,  /* resident service, allgather / bcast copied from the peers' buffers */
+    MI355X_FLOW_SVC_RS = 8,    /* resident service, reduce_scatter(_block) from the peers' inputs */
+    MI355X_FLOW_PIPE = 16      /* pipelined allreduce (per-chunk flags written into the peers) */
 };
 int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
 /* current value of a knob (LL_MAX_BYTES reads 0 when the creation-time LL self-test failed) */

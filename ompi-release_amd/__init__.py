@@ -126,6 +126,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "mi355x_comm_size": (i, [vp]),
         "mi355x_comm_barrier": (i, [vp]),
         "mi355x_comm_last_algorithm": (i, [vp]),
+        "mi355x_debug_pipe_token": (i, [vp, i]),
         "mi355x_comm_set": (i, [vp, i, c.c_long]),
         "mi355x_comm_phase_ms": (i, [vp, c.POINTER(c.c_float), c.POINTER(c.c_float)]),
         "mi355x_comm_get": (i, [vp, i, c.POINTER(c.c_long)]),
@@ -253,7 +254,10 @@ KNOB = {"ALLREDUCE_ALG": 1, "REDUCE_ALG": 2, "REDUCE_SCATTER_ALG": 3, "BLOCKS_PE
         "COPY_BLOCK_KIB": 12, "PIPE": 13, "PIPE_WG_PER_CU": 14, "PIPE_CHUNK_KIB": 15, "PIPE_WT": 16,
         "ONE_PHASE_MAX_BYTES": 17, "PIPE_REFUSED": 18, "SVC_MAX_BYTES": 19, "SVC_CALLS": 20,
         "SVC_LAUNCHES": 21, "SVC_RESIDENT": 22, "SVC_PULL_MAX_BYTES": 23,
-        "SVC_PULL_COPY_MAX_BYTES": 24}
+        "SVC_PULL_COPY_MAX_BYTES": 24, "RCACHE_MAX_MAPS": 25, "RCACHE_SIZE_LIMIT": 26, "PEER_MAPS": 27,
+        "RCACHE_EVICTIONS": 28, "FLOWS": 29, "FLOWS_FAILED": 30, "CREATE_US": 31, "SELFTEST_US": 32,
+        "SVC_OWNER": 33, "SVC_CLAIMS": 34}
+FLOW = {"SVC_LL": 1, "SVC_PULL": 2, "SVC_COPY": 4, "SVC_RS": 8, "PIPE": 16}
 # coll/tuned COLLTYPE ids (coll_tuned.h:41-58)
 COLL = {"ALLGATHER": 0, "ALLREDUCE": 2, "BCAST": 7, "REDUCE": 11, "REDUCESCATTER": 12}
 AR_ALG = {"DECISION": 0, "LINEAR": 1, "NONOVERLAPPING": 2, "RECURSIVE_DOUBLING": 3, "RING": 4,
@@ -303,6 +307,13 @@ class Comm:
 
     def last_algorithm(self) -> int:
         return rt().mi355x_comm_last_algorithm(self.h)
+
+    def debug_pipe_token(self, acquire: bool) -> bool:
+        """test hook: hold (or give back) this communicator's pipelined-grid token of its GPU"""
+        rc = rt().mi355x_debug_pipe_token(self.h, 1 if acquire else 0)
+        if rc < 0:
+            check(rc, "mi355x_debug_pipe_token")
+        return rc == 1
 
     def phase_ms(self) -> tuple[float, float]:
         """device ms of the last timed direct allreduce's two kernels (knob TIME_PHASES)"""

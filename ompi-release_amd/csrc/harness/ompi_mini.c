@@ -1008,7 +1008,9 @@ int mca_base_component_var_register(const mca_base_component_t *component, const
 {
     (void)enumerator; (void)bind; (void)flags; (void)scope;
     if (!component || !variable_name || !storage) return -1;
-    if (type != MCA_BASE_VAR_TYPE_INT && type != MCA_BASE_VAR_TYPE_BOOL && type != MCA_BASE_VAR_TYPE_STRING) return -1;
+    if (type != MCA_BASE_VAR_TYPE_INT && type != MCA_BASE_VAR_TYPE_BOOL && type != MCA_BASE_VAR_TYPE_STRING &&
+        type != MCA_BASE_VAR_TYPE_UNSIGNED_LONG_LONG)
+        return -1;
     char full[160], env[200];
     snprintf(full, sizeof(full), "%s_%s_%s", component->mca_type_name, component->mca_component_name, variable_name);
     int idx = -1;
@@ -1031,6 +1033,7 @@ int mca_base_component_var_register(const mca_base_component_t *component, const
     if (v) {
         if (type == MCA_BASE_VAR_TYPE_INT) *(int *)storage = atoi(v);
         else if (type == MCA_BASE_VAR_TYPE_BOOL) *(bool *)storage = atoi(v) != 0;
+        else if (type == MCA_BASE_VAR_TYPE_UNSIGNED_LONG_LONG) *(unsigned long long *)storage = strtoull(v, NULL, 10);
         else *(char **)storage = strdup(v);
     }
     return idx;
@@ -1095,6 +1098,7 @@ int mini_var_int(int i)
     if (i < 0 || i >= mini_nvars) return -1;
     if (mini_vars[i].type == MCA_BASE_VAR_TYPE_BOOL) return *(bool *)mini_vars[i].storage;
     if (mini_vars[i].type == MCA_BASE_VAR_TYPE_STRING) return *(char **)mini_vars[i].storage != NULL;
+    if (mini_vars[i].type == MCA_BASE_VAR_TYPE_UNSIGNED_LONG_LONG) return (int)*(unsigned long long *)mini_vars[i].storage;
     return *(int *)mini_vars[i].storage;
 }
 int mini_component_register(const mca_base_component_t *c)

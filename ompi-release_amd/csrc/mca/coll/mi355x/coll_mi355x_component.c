@@ -268,6 +268,8 @@ static int map_rc(int rc)
  * coll/cuda's), if not every rank takes the previous component's host path.  Ranks with host
  * buffers need contiguous layouts to join (derived host layouts are an error in a mixed call). */
 int mca_coll_mi355x_mixed_buffers = 1;
+int mca_coll_mi355x_rcache_max_maps = 0;
+unsigned long long mca_coll_mi355x_rcache_size_limit = 0;
 
 /* 1: run the engine (*dev: this rank's buffers are all device memory); 0: the host path on every
  * rank; < 0: an error (the vote failed or timed out) */
@@ -1611,6 +1613,11 @@ static int module_enable(mca_coll_base_module_t *module, struct ompi_communicato
     if (rc != MI355X_SUCCESS) return map_rc(rc);
     if (mca_coll_mi355x_allreduce_algorithm)
         mi355x_comm_set(m->engine, MI355X_KNOB_ALLREDUCE_ALG, mca_coll_mi355x_allreduce_algorithm);
+    /* the peer-mapping cache bounds (mpool_rgpusm_rcache_size_limit's role) */
+    if (mca_coll_mi355x_rcache_max_maps > 0)
+        mi355x_comm_set(m->engine, MI355X_KNOB_RCACHE_MAX_MAPS, mca_coll_mi355x_rcache_max_maps);
+    if (mca_coll_mi355x_rcache_size_limit > 0)
+        mi355x_comm_set(m->engine, MI355X_KNOB_RCACHE_SIZE_LIMIT, (long)mca_coll_mi355x_rcache_size_limit);
     apply_tuned_params(m);
     return OMPI_SUCCESS;
 }
@@ -1630,6 +1637,21 @@ static void register_int(const char *name, const char *desc, mca_base_var_info_l
     *storage = env_int(env, *storage);
 }
 
+/* an unsigned long long parameter (a byte count), the same two sources */
+static void register_ull(const char *name, const char *desc, mca_base_var_info_lvl_t lvl, unsigned long long *storage)
+{
+    if (mca_base_component_var_register) {
+        (void)mca_base_component_var_register(&mca_coll_mi355x_component.collm_version, name, desc,
+                                              MCA_BASE_VAR_TYPE_UNSIGNED_LONG_LONG, NULL, 0, 0, lvl,
+                                              MCA_BASE_VAR_SCOPE_READONLY, storage);
+        return;
+    }
+    char env[96];
+    snprintf(env, sizeof(env), "OMPI_MCA_coll_mi355x_%s", name);
+    const char *v = getenv(env);
+    if (v) *storage = strtoull(v, NULL, 10);
+}
+
 static int component_register(void)
 {
     register_int("priority", "Priority of the mi355x coll component (device-buffer collectives over xGMI)",
@@ -1642,6 +1664,10 @@ static int component_register(void)
     register_int("mixed_buffers", "Let ranks mix host and device buffers in one allreduce / reduce / reduce_scatter(_block) / "
                  "allgather / bcast (every rank votes its buffer kind; 0: every rank must use the same kind)",
                  OPAL_INFO_LVL_5, &mca_coll_mi355x_mixed_buffers);
+    register_int("rcache_max_maps", "Most mappings of peers' device allocations kept open per communicator; the least "
+                 "recently used beyond it are closed (0 = unlimited)", OPAL_INFO_LVL_9, &mca_coll_mi355x_rcache_max_maps);
+    register_ull("rcache_size_limit", "The same bound in bytes of mapped peer allocations, as mpool_rgpusm_rcache_size_limit "
+                 "(0 = unlimited)", OPAL_INFO_LVL_9, &mca_coll_mi355x_rcache_size_limit);
     return OMPI_SUCCESS;
 }
 static int component_open(void) { return OMPI_SUCCESS; }

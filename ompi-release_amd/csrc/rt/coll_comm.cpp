@@ -27,6 +27,7 @@
 #include <immintrin.h>
 #include <poll.h>
 #include <sched.h>
+#include <signal.h>
 #include <sys/mman.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
@@ -36,6 +37,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <cerrno>
 #include <chrono>
 #include <condition_variable>
 #include <cstddef>
@@ -71,6 +73,43 @@ namespace mi355x {
 
 static int fd_drain(mi355x_comm *c, bool wait);
 
+// ----------------------------------------------------------------- liveness
+// a process exists and has not exited (a zombie -- exited, not yet reaped by its parent -- is gone)
+static bool pid_alive(pid_t pid)
+{
+    if (pid <= 0) return false;
+    if (kill(pid, 0) != 0 && errno == ESRCH) return false;
+    char path[64], buf[512];
+    snprintf(path, sizeof(path), "/proc/%d/stat", (int)pid);
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return true;  // (no /proc: trust kill)
+    const ssize_t n = read(fd, buf, sizeof(buf) - 1);
+    close(fd);
+    if (n <= 0) return true;
+    buf[n] = 0;
+    const char *p = strrchr(buf, ')');
+    return !(p && p[1] == ' ' && (p[2] == 'Z' || p[2] == 'X'));
+}
+
+// A peer process that died without setting the abort flag (SIGKILL, the OOM killer) would leave
+// the others spinning in an unbounded wait (the buffer-kind vote) or until timeout_s.  Waits check
+// every rank's published pid now and then; a rank whose process is gone aborts the communicator.
+// (Loopback ranks share this process.)
+static bool peer_gone(mi355x_comm *c)
+{
+    if (c->loopback || c->size == 1) return false;
+    for (int q = 0; q < c->size; ++q) {
+        const pid_t pid = (pid_t)c->ctrl->slot[q].pid;
+        if (q == c->rank || pid <= 0) continue;
+        if (!pid_alive(pid)) {
+            c->ctrl->abort_flag.store(1);
+            set_error(MI355X_ERR_PEER, "rank %d (pid %d) is gone: the communicator is aborted", q, (int)pid);
+            return true;
+        }
+    }
+    return false;
+}
+
 // ----------------------------------------------------------------- barrier
 int barrier(mi355x_comm *c)
 {
@@ -95,6 +134,7 @@ int barrier(mi355x_comm *c)
                 c->reg_mtx.unlock();
             }
             if ((spins & 0xffff) == 0) {
+                if (peer_gone(c)) return MI355X_ERR_PEER;
                 const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
                 if (el > c->timeout_s) {
                     k->abort_flag.store(1);
@@ -158,6 +198,7 @@ int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
                 d->off = up - r.base;
                 d->base = r.base;
                 d->id = r.id;
+                d->size = r.size;
                 return MI355X_SUCCESS;
             }
             drop_reg(c->local_regs[i]);
@@ -194,6 +235,7 @@ int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
     d->off = up - reg.base;
     d->base = reg.base;
     d->id = id;
+    d->size = sz;
     return MI355X_SUCCESS;
 }
 
@@ -516,6 +558,49 @@ static int probe_dmabuf(mi355x_comm *c)
     return barrier(c);  // nobody rewrites its slot before every rank has read probe_ok
 }
 
+// Bounded peer-mapping cache (mpool/rgpusm's rcache_size_limit with LRU eviction,
+// mpool_rgpusm_component.c:92-100, mpool_rgpusm_module.c:104-120,396-419): when the hipIpc mappings
+// of peers' allocations exceed rcache_max_maps (count) or rcache_limit (bytes), the least recently
+// used ones that the current call does not use, that no point-to-point read has pinned and that
+// are not the communicator's own regions are closed.  A mapping keeps the exporter's allocation
+// alive on ROCm, so a long job that churns allocations would otherwise hold every freed block of
+// every peer.  Both limits default to 0 = unlimited, as in the reference.  dmabuf imports (>= 2 GiB
+// allocations) are not evicted: their fd reaches a peer once.
+static bool evictable(const mi355x_comm *c, const PeerMap &m, const PeerMap *keep)
+{
+    return &m != keep && !m.persistent && m.pins == 0 && !m.ext && m.last_use != c->seq;
+}
+
+static void rcache_trim(mi355x_comm *c, const PeerMap *keep)
+{
+    if (!c->rcache_max_maps && !c->rcache_limit) return;
+    for (;;) {
+        size_t nmaps = 0, bytes = 0;
+        auto lru = c->peer_maps.end();
+        for (auto it = c->peer_maps.begin(); it != c->peer_maps.end(); ++it) {
+            if (it->second.persistent || it->second.ext) continue;
+            nmaps++;
+            bytes += it->second.bytes;
+            if (evictable(c, it->second, keep) && (lru == c->peer_maps.end() || it->second.last_use < lru->second.last_use))
+                lru = it;
+        }
+        const bool over = (c->rcache_max_maps && nmaps > c->rcache_max_maps) || (c->rcache_limit && bytes > c->rcache_limit);
+        if (!over || lru == c->peer_maps.end()) return;
+        TRACE(c, "rcache: evict peer %d base %llx (%zu maps, %zu bytes)", lru->first.peer,
+              (unsigned long long)lru->first.base, nmaps, bytes);
+        close_map(lru->second);
+        c->peer_maps.erase(lru);
+        c->rcache_evictions++;
+    }
+}
+
+size_t peer_map_count(const mi355x_comm *c)
+{
+    size_t n = 0;
+    for (const auto &kv : c->peer_maps) n += !kv.second.persistent && !kv.second.ext;
+    return n;
+}
+
 int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **entry)
 {
     std::lock_guard<std::recursive_mutex> reg_guard(c->reg_mtx);
@@ -574,6 +659,8 @@ int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **e
                 return set_error(MI355X_ERR_PEER, "hipIpcOpenMemHandle(rank %d): %s", peer, hipGetErrorString(e));
         }
         it = c->peer_maps.emplace(key, PeerMap{d.id, base, c->seq, nullptr}).first;
+        it->second.bytes = d.size;
+        rcache_trim(c, &it->second);
     }
     if (entry) *entry = &it->second;
     *out = (char *)base + d.off;
@@ -692,6 +779,7 @@ int finish(mi355x_comm *c, hipStream_t s)
                 if ((spins & 0xffff) == 0 && hipStreamQuery(s) != hipErrorNotReady && q == c->rank &&
                     k->slot[q].done.load(std::memory_order_acquire) < v)
                     return set_error(MI355X_ERR_HIP, "stream finished without writing its completion word");
+                if ((spins & 0xffff) == 0 && peer_gone(c)) return MI355X_ERR_PEER;
                 if ((spins & 0xffff) == 0 &&
                     std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
                     k->abort_flag.store(1);
@@ -980,7 +1068,10 @@ static int staged_bcast(mi355x_comm *c, void *buf, size_t bytes, int root, hipSt
 // kernel it waits for.
 // the resident service takes every LL-protocol call up to svc_max bytes (svc_ok: created, self-
 // tested and owned on every rank -- the same decision on every rank)
-static bool svc_usable(const mi355x_comm *c, size_t bytes) { return c->svc_ok && bytes > 0 && bytes <= c->svc_max; }
+static bool svc_usable(const mi355x_comm *c, size_t bytes)
+{
+    return c->svc_ok && (c->flows & MI355X_FLOW_SVC_LL) && bytes > 0 && bytes <= c->svc_max;
+}
 
 static bool ll_usable(const mi355x_comm *c, size_t bytes)
 {
@@ -993,7 +1084,7 @@ static bool ll_usable(const mi355x_comm *c, size_t bytes)
     return c->pipe_share <= 1 || blocks * (size_t)c->pipe_share <= (size_t)device_cu_count();
 }
 
-static void svc_stop(mi355x_comm *c);
+static bool svc_stop(mi355x_comm *c);
 static int svc_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s);
 
 // (Re)allocate and exchange the LL region: [ack words, one per rank][2 parities x n slots of
@@ -1005,7 +1096,8 @@ static int ensure_ll(mi355x_comm *c)
     const size_t want =
         (std::max({c->ll_max, c->svc_max, (size_t)64 << 10}) + kLLChunk - 1) / kLLChunk * kLLChunk;
     if (c->ll_base && c->ll_slot >= want) return MI355X_SUCCESS;
-    svc_stop(c);  // a resident service holds the old region's addresses
+    // a resident service holds the old region's addresses
+    if (!svc_stop(c)) return set_error(MI355X_ERR_HIP, "rank %d: the resident service did not leave", c->rank);
     const size_t n = (size_t)c->size;
     const size_t total = kLLAckBytes + 2 * n * (want / 4) * sizeof(uint64_t);
     if (c->ll_base) (void)hipFree(c->ll_base);
@@ -1017,6 +1109,7 @@ static int ensure_ll(mi355x_comm *c)
     MI_HIP(hipDeviceSynchronize());
     if (!c->ll_err) MI_HIP(hipHostMalloc((void **)&c->ll_err, sizeof(uint32_t), hipHostMallocCoherent));
     c->ll_slot = want;
+    c->ll_bytes = total;
     c->ll_seq = 0;
     c->ll_ctr_base = 0;
     const void *mine[1] = {c->ll_base};
@@ -1138,14 +1231,25 @@ static int ll_selftest(mi355x_comm *c)
 }
 
 // ----------------------------------------------------------------- resident LL service
-// (coll_svc.hip, svc_queue.cpp).  One service per process and GPU, owned by one communicator: the
-// service's kernel serves one communicator's LL region, and a rank whose service were busy with
-// another communicator's call could not take part in this one's (a cross-process circular wait
-// for MPI_THREAD_MULTIPLE programs).  Ownership is agreed at creation: every rank claims its
-// process's service for the new communicator without waiting, and the communicator uses it only if
-// every rank got it; every other communicator keeps the per-call paths.
+// (coll_svc.hip, svc_queue.cpp).  One service per process and GPU, owned by one communicator at a
+// time: the service's kernel serves one communicator's LL region, and a rank whose service were
+// busy with another communicator's call could not take part in this one's (a cross-process
+// circular wait for MPI_THREAD_MULTIPLE programs).  Ownership is taken where it is used: a
+// communicator claims its process's service at its first service-sized call (svc_claim; every
+// rank of the call claims without waiting and the communicator uses the service only if every rank
+// got it), so the communicator that issues the small collectives -- typically a dup or split of
+// MPI_COMM_WORLD -- gets it, not the first one created.  An owner that has been idle on every rank
+// for svc_handover_s hands it over to another communicator of the process that wants it
+// (svc_revoke), at a point where every one of its ranks is between the same two calls.
 static std::mutex g_svc_mtx;
 static std::map<int, mi355x_comm *> g_svc_owner;  // device -> owning communicator
+
+static uint64_t mono_ns()
+{
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);  // (one clock for every process of the node)
+    return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
 
 static uint64_t *svc_done_word(mi355x_comm *c) { return c->svc_host; }
 static uint32_t *svc_err_word(mi355x_comm *c) { return reinterpret_cast<uint32_t *>(c->svc_host + 1); }
@@ -1184,14 +1288,23 @@ static int svc_launch(mi355x_comm *c, uint64_t first)
 }
 
 // ask a resident service to leave and wait until it has (no call is in flight: calls complete
-// before the engine returns)
-static void svc_stop(mi355x_comm *c)
+// before the engine returns).  False if it never left: its kernel may still poll the doorbell page
+// and write the host words and the LL regions, so none of them may be freed (svc_release leaks
+// them and the communicator is aborted).
+static bool svc_stop(mi355x_comm *c)
 {
-    if (!c->svcq || !svc_resident(c->svcq)) return;
+    if (c->svc_stuck) return false;
+    if (!c->svcq || !svc_resident(c->svcq)) return true;
     svc_ring(c, kSvcQuit);
-    if (!svc_wait_exit(c->svcq, c->timeout_s + 5.0))
-        fprintf(stderr, "[mi355x r%d] resident service did not leave\n", c->rank);
+    if (!svc_wait_exit(c->svcq, c->timeout_s + 5.0)) {
+        fprintf(stderr, "[mi355x r%d] resident service did not leave: its memory is kept, the communicator is aborted\n",
+                c->rank);
+        c->svc_stuck = true;
+        if (c->ctrl) c->ctrl->abort_flag.store(1);
+        return false;
+    }
     svc_ring(c, c->ll_seq << kSvcPartBits);  // back to the last call's number: the next launch waits for the next
+    return true;
 }
 
 // A call that takes a host-synchronised flow asks a resident service to leave, without waiting:
@@ -1243,6 +1356,7 @@ static int svc_call(mi355x_comm *c, const SvcCall &call, uint64_t part)
         return rc;
     }
     c->svc_calls++;
+    c->ctrl->slot[c->rank].svc_last_ns.store(mono_ns(), std::memory_order_relaxed);
     return MI355X_SUCCESS;
 }
 
@@ -1283,7 +1397,8 @@ static int svc_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s)
 // rank's buffer alignment, svc_pull_usable).
 static bool svc_pull_usable(const mi355x_comm *c, size_t bytes, size_t esz)
 {
-    return c->svc_ok && !c->loopback && esz >= 4 && bytes > c->svc_max && bytes <= c->svc_pull_max &&
+    return c->svc_ok && (c->flows & MI355X_FLOW_SVC_PULL) && !c->loopback && esz >= 4 && bytes > c->svc_max &&
+           bytes <= c->svc_pull_max &&
            bytes < ((size_t)1 << 31);
 }
 
@@ -1292,7 +1407,7 @@ static bool svc_pull_usable(const mi355x_comm *c, size_t bytes, size_t esz)
 // 16-B vectors where both ends allow)
 static bool svc_pull_copy_usable(const mi355x_comm *c, size_t bytes)
 {
-    return c->svc_ok && !c->loopback && bytes > c->svc_max && bytes <= c->svc_copy_max &&
+    return c->svc_ok && (c->flows & MI355X_FLOW_SVC_COPY) && !c->loopback && bytes > c->svc_max && bytes <= c->svc_copy_max &&
            bytes * (size_t)c->size < ((size_t)1 << 31);
 }
 
@@ -1359,124 +1474,550 @@ static void svc_trace_report(mi355x_comm *c)
     c->svc_trace = nullptr;
 }
 
-static void svc_release(mi355x_comm *c)
-{
-    svc_stop(c);
-    svc_trace_report(c);
-    if (c->svcq) {
-        svc_queue_destroy(c->svcq);
-        delete c->svcq;
-        c->svcq = nullptr;
-    }
-    svc_page_free(c->svc_page, c->svc_page_dev);
-    c->svc_page = nullptr;
-    if (c->svc_host) (void)hipHostFree(c->svc_host);
-    c->svc_host = nullptr;
-    c->svc_ok = false;
-    if (c->svc_owner) {
-        std::lock_guard<std::mutex> g(g_svc_mtx);
-        auto it = g_svc_owner.find(c->device);
-        if (it != g_svc_owner.end() && it->second == c) g_svc_owner.erase(it);
-        c->svc_owner = false;
-    }
-}
+// The service's resources -- its HSA queue, doorbell page and host words -- exist once per process
+// and GPU: created at the first claim on that GPU, shared by the communicators that own the service
+// in turn (a handover creates no queue), freed with the last communicator that used them.
+struct SvcRes {
+    SvcQueue *q = nullptr;
+    SvcPage *page = nullptr;
+    bool page_dev = false;
+    uint64_t *host = nullptr;
+    int users = 0;       // communicators attached (claimed once at least, not destroyed)
+    bool stuck = false;  // a service kernel never left: never freed
+};
+static std::map<int, SvcRes> g_svc_res;  // device -> resources (g_svc_mtx)
 
-// this rank's part of opening the service: queue, doorbell page, host words
-static bool svc_open(mi355x_comm *c)
+// (g_svc_mtx held) this communicator's view of the process's service resources, created on first use
+static bool svc_attach(mi355x_comm *c)
 {
-    c->svcq = new SvcQueue;
-    std::string why;
-    if (svc_queue_create(c->device, c->svcq, &why)) {
-        TRACE(c, "resident service unavailable: %s", why.c_str());
-        delete c->svcq;
-        c->svcq = nullptr;
-        return false;
+    SvcRes &r = g_svc_res[c->device];
+    if (r.stuck) return false;
+    if (!r.q) {
+        auto *q = new SvcQueue;
+        std::string why;
+        if (svc_queue_create(c->device, q, &why)) {
+            TRACE(c, "resident service unavailable: %s", why.c_str());
+            delete q;
+            return false;
+        }
+        void *pg = nullptr;
+        if (svc_page_alloc(q, (sizeof(SvcPage) + 4095) & ~(size_t)4095, &pg, &r.page_dev)) {
+            svc_queue_destroy(q);
+            delete q;
+            return false;
+        }
+        uint64_t *host = nullptr;
+        if (hipHostMalloc((void **)&host, 4096, hipHostMallocCoherent) != hipSuccess) {
+            svc_page_free(pg, r.page_dev);
+            svc_queue_destroy(q);
+            delete q;
+            return false;
+        }
+        std::memset(host, 0, 4096);
+        r.q = q;
+        r.page = static_cast<SvcPage *>(pg);
+        r.host = host;
     }
-    void *pg = nullptr;
-    if (svc_page_alloc(c->svcq, (sizeof(SvcPage) + 4095) & ~(size_t)4095, &pg, &c->svc_page_dev)) return false;
-    c->svc_page = static_cast<SvcPage *>(pg);
-    if (hipHostMalloc((void **)&c->svc_host, 4096, hipHostMallocCoherent) != hipSuccess) return false;
-    std::memset(c->svc_host, 0, 4096);
-    if (env_double("MI355X_SVC_TRACE", 0.0) != 0.0) {
+    if (svc_resident(r.q)) return false;  // (never: a previous owner's kernel leaves before it lets go)
+    c->svcq = r.q;
+    c->svc_page = r.page;
+    c->svc_page_dev = r.page_dev;
+    c->svc_host = r.host;
+    // the previous owner's call numbers mean nothing here: the completion and error words start over
+    __atomic_store_n(c->svc_host, 0ull, __ATOMIC_RELEASE);
+    __atomic_store_n(reinterpret_cast<uint32_t *>(c->svc_host + 1), 0u, __ATOMIC_RELEASE);
+    svc_ring(c, c->ll_seq << kSvcPartBits);
+    if (!c->svc_attached) {
+        r.users++;
+        c->svc_attached = true;
+    }
+    if (!c->svc_trace && env_double("MI355X_SVC_TRACE", 0.0) != 0.0) {
         const size_t tb = sizeof(uint64_t) * kSvcTraceCalls * kSvcTraceCols;
         if (hipHostMalloc((void **)&c->svc_trace, tb, hipHostMallocCoherent) == hipSuccess) std::memset(c->svc_trace, 0, tb);
     }
     return true;
 }
 
-// Collective, at creation (after the LL self-test): claim, open, self-test with one LL allgather
-// of a rank-tagged 8 KiB pattern through the service (bounded, MI355X_LL_PROBE_S); the
-// communicator serves small calls through the service only if every rank passed every step.
-static int svc_setup(mi355x_comm *c)
+// the kernel leaves; this communicator stops using the resources (which stay for the next owner)
+static void svc_detach(mi355x_comm *c)
+{
+    if (!svc_stop(c)) g_svc_res[c->device].stuck = true;
+    c->svcq = nullptr;
+    c->svc_page = nullptr;
+    c->svc_host = nullptr;
+    c->svc_ok = false;
+}
+
+// (g_svc_mtx held) give up ownership
+static void svc_unclaim_locked(mi355x_comm *c)
+{
+    if (!c->svc_owner) return;
+    auto it = g_svc_owner.find(c->device);
+    if (it != g_svc_owner.end() && it->second == c) g_svc_owner.erase(it);
+    c->svc_owner = false;
+}
+
+static void svc_let_go(mi355x_comm *c)
+{
+    std::lock_guard<std::mutex> g(g_svc_mtx);
+    svc_detach(c);
+    svc_unclaim_locked(c);
+}
+
+// at destruction: let go, and free the process's resources with their last user
+static void svc_release(mi355x_comm *c)
+{
+    std::lock_guard<std::mutex> g(g_svc_mtx);
+    const bool had = c->svcq != nullptr;
+    svc_detach(c);
+    svc_unclaim_locked(c);
+    if (had || c->svc_attached) svc_trace_report(c);
+    if (!c->svc_attached) return;
+    c->svc_attached = false;
+    SvcRes &r = g_svc_res[c->device];
+    if (--r.users > 0 || r.stuck) return;  // (stuck: leaked on purpose -- its kernel may still touch them)
+    svc_queue_destroy(r.q);
+    delete r.q;
+    svc_page_free(r.page, r.page_dev);
+    (void)hipHostFree(r.host);
+    g_svc_res.erase(c->device);
+}
+
+// The call gate.  Every engine collective of a multi-process communicator runs inside it: the
+// rank's RankSlot::gate is 1 for the call's duration and its call count advances when it leaves.
+// A process that wants the service another communicator owns may take it (svc_revoke) only by
+// closing the gates of every rank of the owner while all of them are between the same two calls;
+// the owner's ranks then let go of the service at their next call, on every rank at the same call.
+void gate_enter(mi355x_comm *c)
+{
+    std::atomic<uint32_t> &g = c->ctrl->slot[c->rank].gate;
+    unsigned spins = 0;
+    for (uint32_t z = 0; !g.compare_exchange_weak(z, 1u, std::memory_order_acq_rel); z = 0) {
+        _mm_pause();
+        if (++spins > 256) sched_yield();  // (held only while a revoker stops this rank's service)
+    }
+    if (c->svc_ok && c->ctrl->svc_revoked.load(std::memory_order_acquire) == c->svc_epoch) {
+        TRACE(c, "the resident service went to another communicator of a peer process: letting go");
+        svc_let_go(c);
+    }
+}
+
+void gate_exit(mi355x_comm *c)
+{
+    RankSlot &s = c->ctrl->slot[c->rank];
+    s.calls.store(++c->gate_calls, std::memory_order_relaxed);
+    s.gate.store(0u, std::memory_order_release);
+}
+
+// (g_svc_mtx held) take the process's service from its owner x: only while every rank of x is
+// between the same two calls (all gates closed by us, equal call counts) and none has served a
+// call for svc_handover_s.  x's ranks in other processes let go at their next call (gate_enter).
+static bool svc_revoke(mi355x_comm *x)
+{
+    if (!x->gated) return false;
+    Ctrl *k = x->ctrl;
+    // the gates in rank order; a gate another process's revoker holds (2) is waited for -- revokers
+    // hold gates only briefly and never wait while holding a higher one, so ordered acquisition
+    // cannot deadlock -- while a rank inside a call (1) ends the attempt
+    int got = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (bool busy = false; got < x->size && !busy;) {
+        uint32_t z = 0;
+        if (k->slot[got].gate.compare_exchange_strong(z, 2u, std::memory_order_acq_rel)) {
+            ++got;
+            continue;
+        }
+        busy = z != 2u || std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 0.1;
+        _mm_pause();
+    }
+    bool ok = got == x->size && x->svc_ok;
+    if (ok) {
+        const uint64_t c0 = k->slot[0].calls.load(std::memory_order_acquire);
+        uint64_t last = 0;
+        for (int q = 0; q < x->size; ++q) {
+            ok = ok && k->slot[q].calls.load(std::memory_order_acquire) == c0;
+            last = std::max(last, k->slot[q].svc_last_ns.load(std::memory_order_acquire));
+        }
+        const uint64_t now = mono_ns();
+        ok = ok && now > last && (double)(now - last) * 1e-9 >= x->svc_handover_s;
+        if (ok) {
+            k->svc_revoked.store(x->svc_epoch, std::memory_order_release);
+            svc_detach(x);
+            x->svc_owner = false;
+            x->svc_revocations++;
+        }
+    }
+    for (int q = 0; q < got; ++q) k->slot[q].gate.store(0u, std::memory_order_release);
+    return ok;
+}
+
+// Zero the LL region and start the LL call numbering over on every rank (collective): after a
+// service self-test failed somewhere, ranks may disagree on the call number or hold stale granules.
+static int ll_resync(mi355x_comm *c)
+{
+    (void)svc_stop(c);
+    (void)hipDeviceSynchronize();
+    int rc = barrier(c);
+    if (rc) return rc;
+    if (c->svc_stuck) return set_error(MI355X_ERR_HIP, "rank %d: the resident service did not leave", c->rank);
+    MI_HIP(hipMemset(c->ll_base, 0, c->ll_bytes));
+    MI_HIP(hipMemset(c->ll_ctr, 0, sizeof(uint64_t)));
+    MI_HIP(hipDeviceSynchronize());
+    c->ll_seq = 0;
+    c->ll_ctr_base = 0;
+    if (c->ll_err) *c->ll_err = 0;
+    if (c->svc_host) {
+        __atomic_store_n(c->svc_host, 0ull, __ATOMIC_RELEASE);
+        __atomic_store_n(reinterpret_cast<uint32_t *>(c->svc_host + 1), 0u, __ATOMIC_RELEASE);
+        svc_ring(c, 0);
+    }
+    return barrier(c);
+}
+
+// ---- the flows' self-test.  Every cross-device flow that is on by default runs one short call on
+// data that changes with the communicator (its secret) and the test, into a destination poisoned
+// beforehand, and every rank checks its result exactly; the outcome is agreed in the control
+// segment (every rank's mask ANDed, as the LL self-test agrees ll_ok) and a flow that failed on
+// any rank is turned off on every rank -- its calls take the host-synchronised flows, whose
+// coherence rests on kernel completion and a host barrier.  The reference negotiates CUDA IPC per
+// peer pair the same way before using it, falling back to host staging (btl/smcuda/README:41-100,
+// pml_ob1_cuda.c:183-210).  MI355X_SELFTEST_FAIL=<flow,...> (svc_ll, svc_pull, svc_copy, svc_rs,
+// pipe) makes this rank report those flows failed (fault injection for tests); MI355X_SELFTEST=0
+// skips the tests.
+static unsigned selftest_injected()
+{
+    const char *e = getenv("MI355X_SELFTEST_FAIL");
+    if (!e) return 0;
+    unsigned m = 0;
+    const struct { const char *name; unsigned bit; } names[] = {{"svc_ll", MI355X_FLOW_SVC_LL}, {"svc_pull", MI355X_FLOW_SVC_PULL},
+                                                                {"svc_copy", MI355X_FLOW_SVC_COPY}, {"svc_rs", MI355X_FLOW_SVC_RS},
+                                                                {"pipe", MI355X_FLOW_PIPE}};
+    std::string s(e);
+    for (const auto &n : names)
+        if (s.find(n.name) != std::string::npos) m |= n.bit;
+    return m;
+}
+
+static bool selftest_on() { return env_double("MI355X_SELFTEST", 1.0) != 0.0; }
+
+static uint32_t st_val(uint64_t seed, int q, size_t i)
+{
+    uint64_t x = seed ^ ((uint64_t)(q + 1) << 40) ^ ((uint64_t)i * 0x9e3779b97f4a7c15ull);
+    x ^= x >> 31;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 29;
+    return (uint32_t)(x & 0xffffff);  // (sums of <= 64 ranks stay below 2^31)
+}
+
+// device buffers of the self-test: my input (n x count int32 for the reduce_scatter block), output
+struct SelfTest {
+    mi355x_comm *c;
+    uint64_t seed;
+    char *in = nullptr, *out = nullptr;
+    size_t cap = 0;
+    bool ok = true;
+    SelfTest(mi355x_comm *c_, uint64_t salt, size_t bytes) : c(c_), cap(bytes)
+    {
+        seed = c->ctrl->secret ^ (salt * 0x632be59bd9b4e019ull);
+        ok = hipMalloc((void **)&in, cap) == hipSuccess && hipMalloc((void **)&out, cap) == hipSuccess;
+    }
+    ~SelfTest()
+    {
+        if (in) (void)hipFree(in);
+        if (out) (void)hipFree(out);
+        (void)hipGetLastError();
+    }
+    // my input: `count` int32 of test `t`; the output poisoned
+    bool prepare(int t, size_t count)
+    {
+        std::vector<uint32_t> h(count);
+        for (size_t i = 0; i < count; ++i) h[i] = st_val(seed + (uint64_t)t, c->rank, i);
+        return ok && count * 4 <= cap && hipMemcpy(in, h.data(), count * 4, hipMemcpyHostToDevice) == hipSuccess &&
+               hipMemset(out, 0xa5, cap) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+    }
+    bool fetch(std::vector<uint32_t> &h, size_t count)
+    {
+        h.assign(count, 0);
+        return hipMemcpy(h.data(), out, count * 4, hipMemcpyDeviceToHost) == hipSuccess;
+    }
+    // element i of the SUM over every rank's input of test t
+    uint32_t sum(int t, size_t i) const
+    {
+        uint32_t a = 0;
+        for (int q = 0; q < c->size; ++q) a += st_val(seed + (uint64_t)t, q, i);
+        return a;
+    }
+};
+
+// agree on the masks every rank saw pass; returns the AND (collective)
+static int agree_flows(mi355x_comm *c, unsigned mine, unsigned *all)
+{
+    c->ctrl->slot[c->rank].flow_ok = mine;
+    int rc = barrier(c);
+    if (rc) return rc;
+    unsigned a = ~0u;
+    for (int q = 0; q < c->size; ++q) a &= c->ctrl->slot[q].flow_ok;
+    *all = a;
+    return barrier(c);  // nobody rewrites its word before every rank has read it
+}
+
+} // namespace mi355x
+// (defined below, outside the namespace, with the public entry points)
+static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, void *stream);
+static int allgather_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, void *stream);
+static int bcast_impl(mi355x_comm_t *c, void *buf, size_t bytes, int root, void *stream);
+static int reduce_scatter_block_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t rcount, int type, int op,
+                                     void *stream);
+namespace mi355x {
+
+// The service's flows, at its first claim (the service is claimed on every rank; collective).
+static int svc_selftest(mi355x_comm *c)
+{
+    c->svc_flows_tested = true;
+    const unsigned tested = MI355X_FLOW_SVC_LL | MI355X_FLOW_SVC_PULL | MI355X_FLOW_SVC_COPY | MI355X_FLOW_SVC_RS;
+    if (!selftest_on()) return MI355X_SUCCESS;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int n = c->size;
+    // the flows' mechanisms at fixed sizes, whatever the limits are set to now; nothing forced
+    struct Saved {
+        size_t svc_max, pull, copy, one;
+        bool rs, ok;
+        int ar, red, rs_alg;
+        const mi355x_rules_t *rules;
+        double timeout;
+        unsigned flows;
+    } sv{c->svc_max, c->svc_pull_max, c->svc_copy_max, c->one_phase_max, c->svc_rs, c->svc_ok, c->knob_allreduce,
+         c->knob_reduce, c->knob_rs, c->rules, c->timeout_s, c->flows};
+    c->svc_max = 8192;
+    c->svc_pull_max = c->svc_copy_max = 65536;
+    c->one_phase_max = std::max<size_t>(c->one_phase_max, 65536);
+    c->svc_rs = true;
+    c->svc_ok = true;
+    c->knob_allreduce = c->knob_reduce = c->knob_rs = 0;
+    c->rules = nullptr;
+    c->timeout_s = env_double("MI355X_LL_PROBE_S", 5.0);
+    c->flows |= tested;
+    unsigned pass = 0;
+    {
+        SelfTest st(c, c->svc_epoch, (size_t)n * 65536);
+        const int i32 = MI355X_T_INT32, sum = MI355X_OP_SUM;
+        std::vector<uint32_t> h;
+        // a call of `flow` served by the service: exact, and the service served `calls` of them
+        auto served = [&](uint64_t before, uint64_t calls) { return c->svc_calls - before == calls; };
+        // LL form: an allgather and a reducing allreduce (granules pushed into every peer)
+        {
+            bool ok = st.prepare(1, 2048);
+            const uint64_t b = c->svc_calls;
+            ok = ok && allgather_impl(c, st.in, st.out, 8192, nullptr) == MI355X_SUCCESS && st.fetch(h, 2048 * (size_t)n);
+            for (int q = 0; q < n && ok; ++q)
+                for (size_t i = 0; i < 2048 && ok; ++i) ok = h[(size_t)q * 2048 + i] == st_val(st.seed + 1, q, i);
+            ok = ok && st.prepare(2, 2048) && allreduce_impl(c, st.in, st.out, 2048, i32, sum, nullptr) == MI355X_SUCCESS &&
+                 st.fetch(h, 2048);
+            for (size_t i = 0; i < 2048 && ok; ++i) ok = h[i] == st.sum(2, i);
+            if (ok && served(b, 2)) pass |= MI355X_FLOW_SVC_LL;
+        }
+        // pull form: a one-phase ring allreduce folded from the peers' mapped inputs
+        if (pass & MI355X_FLOW_SVC_LL) {
+            const size_t cnt = 12288;  // 48 KiB
+            bool ok = st.prepare(3, cnt);
+            const uint64_t b = c->svc_calls;
+            ok = ok && allreduce_impl(c, st.in, st.out, cnt, i32, sum, nullptr) == MI355X_SUCCESS && st.fetch(h, cnt);
+            for (size_t i = 0; i < cnt && ok; ++i) ok = h[i] == st.sum(3, i);
+            if (ok && served(b, 1)) pass |= MI355X_FLOW_SVC_PULL;
+            // pull copies: allgather of every peer's block, bcast of the last rank's buffer
+            ok = st.prepare(4, cnt);
+            const uint64_t b2 = c->svc_calls;
+            ok = ok && allgather_impl(c, st.in, st.out, cnt * 4, nullptr) == MI355X_SUCCESS && st.fetch(h, cnt * (size_t)n);
+            for (int q = 0; q < n && ok; ++q)
+                for (size_t i = 0; i < cnt && ok; ++i) ok = h[(size_t)q * cnt + i] == st_val(st.seed + 4, q, i);
+            ok = ok && st.prepare(5, cnt) && hipMemcpy(st.out, st.in, cnt * 4, hipMemcpyDeviceToDevice) == hipSuccess &&
+                 bcast_impl(c, st.out, cnt * 4, n - 1, nullptr) == MI355X_SUCCESS && st.fetch(h, cnt);
+            for (size_t i = 0; i < cnt && ok; ++i) ok = h[i] == st_val(st.seed + 5, n - 1, i);
+            if (ok && served(b2, 2)) pass |= MI355X_FLOW_SVC_COPY;
+            // reduce-scatter form: my 16 KiB block evaluated from the peers' mapped inputs
+            const size_t rc_ = 4096;
+            ok = st.prepare(6, rc_ * (size_t)n);
+            const uint64_t b3 = c->svc_calls;
+            ok = ok && reduce_scatter_block_impl(c, st.in, st.out, rc_, i32, sum, nullptr) == MI355X_SUCCESS &&
+                 st.fetch(h, rc_);
+            for (size_t i = 0; i < rc_ && ok; ++i) ok = h[i] == st.sum(6, (size_t)c->rank * rc_ + i);
+            if (ok && served(b3, 1)) pass |= MI355X_FLOW_SVC_RS;
+        }
+        (void)hipGetLastError();
+    }
+    pass &= ~selftest_injected();
+    c->svc_max = sv.svc_max;
+    c->svc_pull_max = sv.pull;
+    c->svc_copy_max = sv.copy;
+    c->one_phase_max = sv.one;
+    c->svc_rs = sv.rs;
+    c->svc_ok = sv.ok;
+    c->knob_allreduce = sv.ar;
+    c->knob_reduce = sv.red;
+    c->knob_rs = sv.rs_alg;
+    c->rules = sv.rules;
+    c->timeout_s = sv.timeout;
+    c->flows = sv.flows;
+    unsigned all = 0;
+    int rc = agree_flows(c, pass | ~tested, &all);
+    if (rc) return rc;
+    const unsigned failed = tested & ~all;
+    c->flows &= ~failed;
+    c->flows_failed |= failed;
+    if (failed) {
+        if (c->rank == 0)
+            fprintf(stderr, "[mi355x] resident-service flow self-test failed (flows 0x%x): those calls take the "
+                    "host-synchronised flows\n", failed);
+        rc = ll_resync(c);
+        if (rc) return rc;
+    }
+    c->selftest_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    TRACE(c, "service flow self-test: passed here 0x%x, agreed 0x%x", pass, all & tested);
+    return MI355X_SUCCESS;
+}
+
+// The pipelined allreduce's per-chunk flag hand-off, at creation (multi-process, collective): one
+// allreduce of 128 KiB blocks in 16 KiB chunks (8 per block), forced onto the pipelined flow.
+static int pipe_selftest(mi355x_comm *c)
+{
+    if (!selftest_on()) return MI355X_SUCCESS;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int n = c->size;
+    const size_t count = (size_t)n * 32768;
+    struct Saved {
+        bool pipe, want;
+        size_t one;
+        int ar;
+        const mi355x_rules_t *rules;
+        double timeout;
+    } sv{c->pipe_on, c->svc_want, c->one_phase_max, c->knob_allreduce, c->rules, c->timeout_s};
+    c->pipe_on = true;
+    c->svc_want = false;  // (no claim from inside this call, whatever the service limits are)
+    c->one_phase_max = 0;
+    c->knob_allreduce = AR_RING;
+    c->rules = nullptr;
+    c->pipe_chunk_override = 4096;
+    c->timeout_s = env_double("MI355X_LL_PROBE_S", 5.0);
+    unsigned pass = 0;
+    bool admitted = false;
+    {
+        SelfTest st(c, 0x9e37u, count * 4);
+        std::vector<uint32_t> h;
+        const uint64_t refused = c->pipe_refused;
+        bool ok = st.prepare(7, count) &&
+                  allreduce_impl(c, st.in, st.out, count, MI355X_T_INT32, MI355X_OP_SUM, nullptr) == MI355X_SUCCESS &&
+                  st.fetch(h, count);
+        for (size_t i = 0; i < count && ok; ++i) ok = h[i] == st.sum(7, i);
+        admitted = c->pipe_refused == refused;
+        if (ok) pass |= MI355X_FLOW_PIPE;
+        (void)hipGetLastError();
+    }
+    c->pipe_on = sv.pipe;
+    c->svc_want = sv.want;
+    c->one_phase_max = sv.one;
+    c->knob_allreduce = sv.ar;
+    c->rules = sv.rules;
+    c->timeout_s = sv.timeout;
+    c->pipe_chunk_override = 0;
+    pass &= ~selftest_injected();
+    // not admitted (another communicator's grid held a GPU): the call ran two phases -- nothing
+    // learnt about the flag hand-off, so it counts as untested, not failed (every rank agrees:
+    // admission is agreed per call)
+    unsigned all = 0;
+    int rc = agree_flows(c, (pass | ~(unsigned)MI355X_FLOW_PIPE) | (admitted ? 0u : (unsigned)MI355X_FLOW_PIPE), &all);
+    if (rc) return rc;
+    c->pipe_untested = !admitted;
+    if (!(all & MI355X_FLOW_PIPE)) {
+        c->flows &= ~(unsigned)MI355X_FLOW_PIPE;
+        c->flows_failed |= MI355X_FLOW_PIPE;
+        c->pipe_on = false;
+        if (c->rank == 0)
+            fprintf(stderr, "[mi355x] pipelined allreduce self-test failed: large allreduces take the two-phase flow\n");
+    }
+    c->selftest_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    TRACE(c, "pipelined flow self-test: %s", !admitted ? "not admitted (untested)" : (all & MI355X_FLOW_PIPE) ? "ok" : "failed -> off");
+    return MI355X_SUCCESS;
+}
+
+// Collective: claim the process's service for this communicator on every rank, or on none.  Called
+// from a service-sized call on every rank alike (svc_maybe_claim).  A rank whose service another
+// communicator owns takes it over if that owner has been idle long enough (svc_revoke).
+static int svc_claim(mi355x_comm *c)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    int mine = 2;  // 1 claimed, 2 owned by a busy communicator, 3 the service cannot run here
+    {
+        std::lock_guard<std::mutex> g(g_svc_mtx);
+        auto it = g_svc_owner.find(c->device);
+        const bool free_ = it == g_svc_owner.end() || it->second == c;
+        if (free_ || svc_revoke(it->second)) {
+            if (!svc_attach(c)) {
+                mine = 3;
+            } else {
+                g_svc_owner[c->device] = c;
+                c->svc_owner = true;
+                mine = 1;
+            }
+        }
+    }
+    c->ctrl->slot[c->rank].svc_claim = mine;
+    int rc = barrier(c);
+    if (rc) return rc;
+    bool all = true, broken = false;
+    for (int q = 0; q < c->size; ++q) {
+        all = all && c->ctrl->slot[q].svc_claim == 1;
+        broken = broken || c->ctrl->slot[q].svc_claim == 3;
+    }
+    rc = barrier(c);  // every rank has read the claims before they are rewritten
+    if (rc) return rc;
+    if (!all) {
+        if (mine == 1) svc_let_go(c);
+        if (broken) {
+            c->svc_want = false;  // the service cannot run on some rank: stop trying (every rank saw it)
+            if (c->rank == 0) fprintf(stderr, "[mi355x] resident LL service unavailable: small collectives use the per-call paths\n");
+        }
+        TRACE(c, "service claim: %s", broken ? "unavailable" : "owned by another communicator on some rank");
+        return MI355X_SUCCESS;
+    }
+    c->svc_epoch++;
+    c->ctrl->slot[c->rank].svc_last_ns.store(mono_ns(), std::memory_order_relaxed);
+    if (!c->svc_flows_tested) {
+        rc = svc_selftest(c);
+        if (rc) return rc;
+    }
+    if (!(c->flows & MI355X_FLOW_SVC_LL)) {
+        svc_let_go(c);
+        c->svc_want = false;
+        return MI355X_SUCCESS;
+    }
+    c->svc_ok = true;
+    TRACE(c, "service claimed (epoch %llu) in %.0f us", (unsigned long long)c->svc_epoch,
+          std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    return MI355X_SUCCESS;
+}
+
+// at a service-sized call: claim the service if this communicator does not have it (every
+// svc_retry-th such call; the same decision on every rank: sizes and agreed state only)
+static int svc_maybe_claim(mi355x_comm *c, bool sized)
+{
+    if (c->svc_ok || !c->svc_want || !sized) return MI355X_SUCCESS;
+    if (c->svc_tries++ % c->svc_retry != 0) return MI355X_SUCCESS;
+    return svc_claim(c);
+}
+
+// at creation: the service's settings (the claim itself waits for a service-sized call)
+static void svc_setup(mi355x_comm *c)
 {
     c->svc_max = (size_t)std::max(0.0, env_double("MI355X_SVC_MAX_BYTES", (double)c->svc_max));
-    c->svc_idle_s = std::max(0.001, env_double("MI355X_SVC_IDLE_MS", c->svc_idle_s * 1e3) * 1e-3);
+    c->svc_idle_s = std::max(0.0001, env_double("MI355X_SVC_IDLE_MS", c->svc_idle_s * 1e3) * 1e-3);
     c->svc_nwg = (int)std::min(64.0, std::max(1.0, env_double("MI355X_SVC_WGS", (double)c->svc_nwg)));
     c->svc_pull_max = (size_t)std::max(0.0, env_double("MI355X_SVC_PULL_MAX_BYTES", (double)c->svc_pull_max));
     c->svc_copy_max = (size_t)std::max(0.0, env_double("MI355X_SVC_PULL_COPY_MAX_BYTES", (double)c->svc_copy_max));
     c->svc_rs = env_double("MI355X_SVC_RS", c->svc_rs ? 1.0 : 0.0) != 0.0;
+    c->svc_handover_s = std::max(0.0, env_double("MI355X_SVC_HANDOVER_MS", c->svc_handover_s * 1e3) * 1e-3);
+    c->svc_retry = (uint64_t)std::max(1.0, env_double("MI355X_SVC_RETRY_CALLS", (double)c->svc_retry));
     const char *env = getenv("MI355X_SVC");
-    const bool want = c->ll_ok && c->size <= kLLMaxRanks && !(env && atoi(env) == 0);
-    if (want) {
-        std::lock_guard<std::mutex> g(g_svc_mtx);
-        if (!g_svc_owner.count(c->device)) {
-            g_svc_owner[c->device] = c;
-            c->svc_owner = true;
-        }
-    }
-    c->ctrl->slot[c->rank].svc_claim = c->svc_owner ? 1 : 2;
-    int rc = barrier(c);
-    if (rc) return rc;
-    bool all = true;
-    for (int q = 0; q < c->size; ++q) all = all && c->ctrl->slot[q].svc_claim == 1;
-    bool ok = all && svc_open(c);
-    if (ok) {
-        // the self-test call (svc_ok is what svc_usable asks: on for this call only)
-        const size_t per = 8192, n = (size_t)c->size;
-        char *buf = nullptr;
-        ok = hipMalloc((void **)&buf, per * (n + 1)) == hipSuccess &&
-             hipMemset(buf, c->rank + 1, per) == hipSuccess && hipMemset(buf + per, 0, per * n) == hipSuccess &&
-             hipDeviceSynchronize() == hipSuccess;
-        if (ok) {
-            LLArgs a;
-            std::memset(&a, 0, sizeof(a));
-            a.mode = LL_AG;
-            a.src = buf;
-            a.dst = buf + per;
-            a.nbytes = per;
-            a.push_mask = ~0ull;
-            const double saved_t = c->timeout_s;
-            const size_t saved_max = c->svc_max;
-            c->timeout_s = env_double("MI355X_LL_PROBE_S", 5.0);
-            c->svc_max = per;
-            c->svc_ok = true;
-            ok = ll_run(c, a, 0, 0, nullptr) == MI355X_SUCCESS;
-            c->svc_ok = false;
-            c->svc_max = saved_max;
-            c->timeout_s = saved_t;
-        }
-        if (ok) {
-            std::vector<unsigned char> h(per * n);
-            ok = hipMemcpy(h.data(), buf + per, per * n, hipMemcpyDeviceToHost) == hipSuccess;
-            for (size_t q = 0; q < n && ok; ++q)
-                for (size_t i = 0; i < per && ok; i += 509) ok = h[q * per + i] == (unsigned char)(q + 1);
-        }
-        (void)hipGetLastError();
-        if (buf) (void)hipFree(buf);
-    }
-    c->ctrl->slot[c->rank].svc_ok = ok ? 1 : 2;
-    rc = barrier(c);
-    if (rc) return rc;
-    bool every = all;
-    for (int q = 0; q < c->size && every; ++q) every = c->ctrl->slot[q].svc_ok == 1;
-    if (!every) {
-        if (all && c->rank == 0)
-            fprintf(stderr, "[mi355x] resident LL service unavailable: small collectives use the per-call paths\n");
-        svc_release(c);
-    }
-    c->svc_ok = every;
-    TRACE(c, "resident service: %s", every ? "on" : all ? "failed -> off" : "owned by another communicator");
-    return barrier(c);
+    c->svc_want = c->ll_ok && c->size <= kLLMaxRanks && !c->loopback && !(env && atoi(env) == 0);
 }
 
 // ----------------------------------------------------------------- pipelined allreduce
@@ -1518,12 +2059,56 @@ static int ensure_pipe(mi355x_comm *c)
 // the call's buffer exchange; the call is pipelined only if every rank holds its token, otherwise
 // every rank releases and the call takes the two-phase flow, whose kernels never wait on a peer.
 // Nothing ever spins for admission (the never-blocking progress rule of opal_progress.c:150).
-// The table lives in a per-user shared-memory segment (64 GPUs); a process that dies holding a
-// token leaves that GPU on the two-phase flow, never hung.
+// The table lives in a per-user shared-memory segment (64 GPUs) that outlives the job, so a token
+// must not outlive its holder: every process that counts up a token first registers itself in the
+// token's holder list (pid + process start time); a process that finds the token taken by another
+// holder and no live process registered for that holder takes the count back (a holder killed
+// mid-call -- SIGKILL, OOM -- would otherwise leave the GPU on the two-phase flow for every later
+// job of the user on the node).  The reference keeps no node-wide state past a process's death
+// (smcuda's IPC state is per endpoint, btl/smcuda/README:92-100); this is the same guarantee.
+constexpr int kTokHolders = 64;       // registrations per GPU (ranks x communicators sharing it)
+constexpr uint64_t kTokPending = 1ull << 63;  // registration being written (pid valid, rest not yet)
+struct TokHolder {
+    std::atomic<uint64_t> who;        // 0 free; pid | kTokPending while filled in; pid when complete
+    std::atomic<uint64_t> start;      // the process's start time (/proc/<pid>/stat field 22)
+    std::atomic<uint64_t> holder;     // the communicator id it counts up the token for
+};
 struct GpuTokens {
     std::atomic<uint64_t> uid[64];    // device uid (hash of the PCI bus id), 0 = free slot
-    std::atomic<uint64_t> word[64];   // (holder << 16) | holders' count; 0 = free
+    // (holder id << 32) | (generation << 8) | holders' count; count 0 = free.  The generation
+    // changes on every transition, so a reclaim (compare-exchange from the value it inspected)
+    // fails if anything happened in between.
+    std::atomic<uint64_t> word[64];
+    TokHolder h[64][kTokHolders];
 };
+
+static uint64_t proc_start_time(pid_t pid)
+{
+    char path[64], buf[1024];
+    snprintf(path, sizeof(path), "/proc/%d/stat", (int)pid);
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return 0;
+    const ssize_t n = read(fd, buf, sizeof(buf) - 1);
+    close(fd);
+    if (n <= 0) return 0;
+    buf[n] = 0;
+    const char *p = strrchr(buf, ')');  // the command name may hold spaces; fields follow its ')'
+    if (!p) return 0;
+    int field = 2;
+    for (++p; *p && field < 22; ++p)
+        if (*p == ' ') ++field;
+    return strtoull(p, nullptr, 10);
+}
+
+// a registered process still exists (the same process: pid reuse changes the start time)
+static bool holder_alive(uint64_t who, uint64_t start)
+{
+    const pid_t pid = (pid_t)(who & 0x7fffffffull);
+    if (!pid_alive(pid)) return false;
+    if (who & kTokPending) return true;  // still registering: its start time is not written yet
+    const uint64_t now = proc_start_time(pid);
+    return now == 0 || now == start;
+}
 
 static GpuTokens *gpu_tokens()
 {
@@ -1531,7 +2116,7 @@ static GpuTokens *gpu_tokens()
     static std::once_flag once;
     std::call_once(once, [] {
         char name[64];
-        snprintf(name, sizeof(name), "/mi355x_gpu_tokens_%u", (unsigned)getuid());
+        snprintf(name, sizeof(name), "/mi355x_gpu_tokens2_%u", (unsigned)getuid());
         const int fd = shm_open(name, O_CREAT | O_RDWR, 0600);
         if (fd < 0) return;
         struct stat st;
@@ -1544,6 +2129,34 @@ static GpuTokens *gpu_tokens()
         if (m != MAP_FAILED) t = (GpuTokens *)m;  // a fresh segment is zero-filled: every slot free
     });
     return t;
+}
+
+// Take back a token whose count was raised only by processes that no longer exist (the value `cur`
+// was read by the caller; the compare-exchange fails if anything changed since).
+static bool pipe_token_reclaim(GpuTokens *t, int i, uint64_t cur)
+{
+    const uint64_t holder = cur >> 32;
+    for (int e = 0; e < kTokHolders; ++e) {
+        const uint64_t who = t->h[i][e].who.load(std::memory_order_acquire);
+        if (!who) continue;
+        const uint64_t start = t->h[i][e].start.load(std::memory_order_relaxed);
+        const uint64_t hid = t->h[i][e].holder.load(std::memory_order_relaxed);
+        if (!holder_alive(who, start)) {
+            // a dead registration: free it (whatever it counted is what this reclaim takes back)
+            uint64_t w = who;
+            t->h[i][e].who.compare_exchange_strong(w, 0);
+            continue;
+        }
+        // a registration still being written may belong to the dead holder's communicator too: it
+        // has not counted up yet, and when it tries, its compare-exchange from the value this
+        // reclaim replaces fails (the generation changed), so it does not block the reclaim
+        if (who & kTokPending) continue;
+        if (hid == holder) return false;  // a live process counts up this token
+    }
+    const uint64_t next = (((cur >> 8) + 1) & 0xffffff) << 8;  // free (holder 0, count 0), next generation
+    const bool ok = t->word[i].compare_exchange_strong(cur, next, std::memory_order_acq_rel);
+    if (ok) fprintf(stderr, "[mi355x] reclaimed the pipelined-grid token of a GPU from a process that died holding it\n");
+    return ok;
 }
 
 static bool pipe_token_acquire(mi355x_comm *c)
@@ -1560,27 +2173,58 @@ static bool pipe_token_acquire(mi355x_comm *c)
         if (c->pipe_token < 0) return false;
         uint64_t h = 1469598103934665603ull;
         for (char ch : c->shm_name) h = (h ^ (unsigned char)ch) * 1099511628211ull;
-        c->pipe_holder = (h & 0xffffffffffffull) | 1;
+        c->pipe_holder = ((h ^ (h >> 32)) & 0xffffffffull) | 1;
     }
-    std::atomic<uint64_t> &w = t->word[c->pipe_token];
+    const int i = c->pipe_token;
+    // register first (pid, start time, holder), so a reclaimer never takes a count from under me
+    const uint64_t pid = (uint64_t)getpid();
+    static const uint64_t my_start = proc_start_time(getpid());
+    int e = -1;
+    for (int k = 0; k < kTokHolders && e < 0; ++k) {
+        uint64_t z = 0;
+        if (t->h[i][k].who.compare_exchange_strong(z, pid | kTokPending)) e = k;
+    }
+    if (e < 0) return false;  // (a full list: this call simply takes the two-phase flow)
+    t->h[i][e].start.store(my_start, std::memory_order_relaxed);
+    t->h[i][e].holder.store(c->pipe_holder, std::memory_order_relaxed);
+    t->h[i][e].who.store(pid, std::memory_order_release);
+    std::atomic<uint64_t> &w = t->word[i];
     uint64_t cur = w.load(std::memory_order_acquire);
+    bool reclaimed = false;
     for (;;) {
-        const uint64_t holder = cur >> 16, cnt = cur & 0xffff;
-        if (cnt != 0 && holder != c->pipe_holder) return false;
-        if (cnt == 0xffff) return false;
-        if (w.compare_exchange_weak(cur, (c->pipe_holder << 16) | (cnt + 1), std::memory_order_acq_rel)) return true;
+        const uint64_t holder = cur >> 32, cnt = cur & 0xff, gen = (cur >> 8) & 0xffffff;
+        if (cnt != 0 && holder != c->pipe_holder) {
+            if (!reclaimed && pipe_token_reclaim(t, i, cur)) {
+                reclaimed = true;
+                cur = w.load(std::memory_order_acquire);
+                continue;
+            }
+            break;
+        }
+        if (cnt == 0xff) break;
+        const uint64_t next = (c->pipe_holder << 32) | (((gen + 1) & 0xffffff) << 8) | (cnt + 1);
+        if (w.compare_exchange_weak(cur, next, std::memory_order_acq_rel)) {
+            c->pipe_entry = e;
+            return true;
+        }
     }
+    t->h[i][e].who.store(0, std::memory_order_release);
+    return false;
 }
 
 static void pipe_token_release(mi355x_comm *c)
 {
-    std::atomic<uint64_t> &w = gpu_tokens()->word[c->pipe_token];
+    GpuTokens *t = gpu_tokens();
+    std::atomic<uint64_t> &w = t->word[c->pipe_token];
     uint64_t cur = w.load(std::memory_order_acquire);
     for (;;) {
-        const uint64_t cnt = cur & 0xffff;
-        const uint64_t next = cnt <= 1 ? 0 : (cur & ~0xffffull) | (cnt - 1);
-        if (w.compare_exchange_weak(cur, next, std::memory_order_acq_rel)) return;
+        const uint64_t cnt = cur & 0xff, gen = (cur >> 8) & 0xffffff;
+        const uint64_t next = cnt <= 1 ? (((gen + 1) & 0xffffff) << 8)
+                                       : (cur & ~0xffffffffull) | (((gen + 1) & 0xffffff) << 8) | (cnt - 1);
+        if (w.compare_exchange_weak(cur, next, std::memory_order_acq_rel)) break;
     }
+    if (c->pipe_entry >= 0) t->h[c->pipe_token][c->pipe_entry].who.store(0, std::memory_order_release);
+    c->pipe_entry = -1;
 }
 
 // One launch per rank: fold my ring block and pull the other blocks, chunk by chunk, with
@@ -1607,6 +2251,7 @@ static int pipe_allreduce(mi355x_comm *c, int op, int type, const Program &pr,
     const size_t vec = 16 / esz;
     size_t chunk = coll_tune().pipe_chunk_kib ? ((size_t)coll_tune().pipe_chunk_kib << 10) / esz
                                               : std::max<size_t>(((size_t)64 << 10) / esz, maxlen / 512);
+    if (c->pipe_chunk_override) chunk = c->pipe_chunk_override;  // (the self-test's small chunks)
     chunk = std::max(chunk, (maxlen + kPipeKmax - 1) / kPipeKmax);
     chunk = (chunk + vec - 1) / vec * vec;
     const size_t nchunks = std::max<size_t>(1, (maxlen + chunk - 1) / chunk);
@@ -1724,7 +2369,7 @@ static void ll_program(LLArgs &a, const Program &pr)
 // rank decides alike: the largest block, the program and the sizes are the same everywhere.
 static bool svc_rs_usable(const mi355x_comm *c, size_t max_block_bytes, const Program &pr)
 {
-    return c->svc_ok && c->svc_rs && !c->loopback && c->size >= 2 && c->size <= kLLMaxRanks && max_block_bytes <= c->svc_pull_max &&
+    return c->svc_ok && c->svc_rs && (c->flows & MI355X_FLOW_SVC_RS) && !c->loopback && c->size >= 2 && c->size <= kLLMaxRanks && max_block_bytes <= c->svc_pull_max &&
            (pr.is_fold ? pr.order.size() == (size_t)c->size
                        : (c->size <= kTreeMax && pr.steps.size() <= (size_t)kTreeSteps));
 }
@@ -1872,7 +2517,10 @@ static void worker_main(mi355x_comm *c)
         int rc = MI355X_SUCCESS;
         if (hipStreamWaitEvent(c->nb_stream, r->ev, 0) != hipSuccess)
             rc = set_error(MI355X_ERR_HIP, "hipStreamWaitEvent failed");
-        if (rc == MI355X_SUCCESS) rc = r->run(c->nb_stream);
+        if (rc == MI355X_SUCCESS) {
+            CallGate gate(c);
+            rc = r->run(c->nb_stream);
+        }
         r->rc = rc;
         if (rc != MI355X_SUCCESS) r->err = mi355x_last_error();
         r->run = nullptr;
@@ -1925,6 +2573,7 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     if (!key || !out || size < 1 || size > kMaxRanks || rank < 0 || rank >= size)
         return set_error(MI355X_ERR_ARG, "bad comm_create arguments");
     *out = nullptr;
+    const auto t_create = std::chrono::steady_clock::now();
     DeviceGuard dg(device);
     char bus[64] = "";
     MI_HIP(hipDeviceGetPCIBusId(bus, (int)sizeof(bus), device));
@@ -2028,13 +2677,20 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     c->pipe_on = env_double("MI355X_PIPE", size >= 4 ? 1.0 : 0.0) != 0.0;
     c->one_phase_max = (size_t)std::max(0.0, env_double("MI355X_ONE_PHASE_MAX_BYTES", (double)c->one_phase_max));
     c->lat_on = env_double("MI355X_LAT_PROFILE", 0.0) != 0.0;
+    c->rcache_max_maps = (size_t)std::max(0.0, env_double("MI355X_RCACHE_MAX_MAPS", 0.0));
+    c->rcache_limit = (size_t)std::max(0.0, env_double("MI355X_RCACHE_SIZE_LIMIT", 0.0));
+    c->gated = size > 1;
     if (rc == MI355X_SUCCESS && size > 1) rc = setup_done_words(c);
     if (rc == MI355X_SUCCESS && size > 1) rc = ll_selftest(c);
-    if (rc == MI355X_SUCCESS && size > 1) rc = svc_setup(c);
+    if (rc == MI355X_SUCCESS && size > 1) {
+        svc_setup(c);
+        rc = pipe_selftest(c);
+    }
     if (rc) {
         mi355x_comm_destroy(c);
         return rc;
     }
+    c->create_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_create).count();
     *out = c;
     return MI355X_SUCCESS;
 }
@@ -2074,6 +2730,7 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
         c->worker.join();
     }
     DeviceGuard dg(c->device);
+    if (c->gated) gate_enter(c);  // (never while another process's revoker is taking the service from it)
     svc_release(c);
     p2p_destroy(c);
     for (hipEvent_t e : c->tev)
@@ -2088,9 +2745,11 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
     if (c->pipe_dbg) (void)hipHostFree(c->pipe_dbg);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->stage) (void)hipFree(c->stage);
-    if (c->ll_base) (void)hipFree(c->ll_base);
-    if (c->ll_ctr) (void)hipFree(c->ll_ctr);
-    if (c->ll_err) (void)hipHostFree(c->ll_err);
+    if (!c->svc_stuck) {  // (a service kernel that never left may still read and write these)
+        if (c->ll_base) (void)hipFree(c->ll_base);
+        if (c->ll_ctr) (void)hipFree(c->ll_ctr);
+        if (c->ll_err) (void)hipHostFree(c->ll_err);
+    }
     if (c->lat_on && c->lat_n)
         fprintf(stderr, "[mi355x r%d] small allreduce steps over %llu calls (us): input sync %.2f, exchange %.2f, "
                 "launch %.2f, finish %.2f\n", c->rank, (unsigned long long)c->lat_n, c->lat_acc[0] / c->lat_n,
@@ -2165,6 +2824,7 @@ int mi355x_comm_vote(mi355x_comm_t *c, int device, int *any_device)
                     if (c->p2p) (void)p2p_progress(c);
                     if (g_progress_hook) g_progress_hook();
                 }
+                if ((spins & 0xffff) == 0 && peer_gone(c)) return MI355X_ERR_PEER;
                 sched_yield();
             }
         }
@@ -2173,6 +2833,17 @@ int mi355x_comm_vote(mi355x_comm_t *c, int device, int *any_device)
 }
 
 int mi355x_comm_last_algorithm(const mi355x_comm_t *c) { return c ? c->last_alg : -1; }
+
+// test hook: take (1) or give back (0) this communicator's pipelined-grid token of its GPU outside
+// any call, as a rank inside a pipelined allreduce holds it (tests kill a holder, then check that
+// the next communicator on the GPU is admitted again)
+int mi355x_debug_pipe_token(mi355x_comm_t *c, int acquire)
+{
+    if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    if (acquire) return pipe_token_acquire(c) ? 1 : 0;
+    if (c->pipe_entry >= 0) pipe_token_release(c);
+    return 0;
+}
 int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
 {
     if (!c || !value) return set_error(MI355X_ERR_ARG, "NULL argument");
@@ -2195,12 +2866,26 @@ int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
     case MI355X_KNOB_PIPE_CHUNK_KIB: *value = coll_tune().pipe_chunk_kib; break;
     case MI355X_KNOB_PIPE_WT: *value = coll_tune().pipe_wt; break;
     case MI355X_KNOB_ONE_PHASE_MAX_BYTES: *value = (long)c->one_phase_max; break;
-    case MI355X_KNOB_SVC_MAX_BYTES: *value = c->svc_ok ? (long)c->svc_max : 0; break;
+    case MI355X_KNOB_SVC_MAX_BYTES: *value = (c->svc_ok || c->svc_want) ? (long)c->svc_max : 0; break;
     case MI355X_KNOB_SVC_CALLS: *value = (long)c->svc_calls; break;
     case MI355X_KNOB_SVC_LAUNCHES: *value = (long)c->svc_launches; break;
     case MI355X_KNOB_SVC_RESIDENT: *value = c->svcq && svc_resident(c->svcq) ? 1 : 0; break;
-    case MI355X_KNOB_SVC_PULL_MAX_BYTES: *value = c->svc_ok ? (long)c->svc_pull_max : 0; break;
-    case MI355X_KNOB_SVC_PULL_COPY_MAX_BYTES: *value = c->svc_ok ? (long)c->svc_copy_max : 0; break;
+    case MI355X_KNOB_SVC_PULL_MAX_BYTES: *value = (c->svc_ok || c->svc_want) ? (long)c->svc_pull_max : 0; break;
+    case MI355X_KNOB_SVC_PULL_COPY_MAX_BYTES: *value = (c->svc_ok || c->svc_want) ? (long)c->svc_copy_max : 0; break;
+    case MI355X_KNOB_FLOWS: *value = (long)c->flows; break;
+    case MI355X_KNOB_FLOWS_FAILED: *value = (long)c->flows_failed; break;
+    case MI355X_KNOB_CREATE_US: *value = (long)c->create_us; break;
+    case MI355X_KNOB_SELFTEST_US: *value = (long)c->selftest_us; break;
+    case MI355X_KNOB_SVC_OWNER: *value = c->svc_ok ? 1 : 0; break;
+    case MI355X_KNOB_SVC_CLAIMS: *value = (long)c->svc_epoch; break;
+    case MI355X_KNOB_RCACHE_MAX_MAPS: *value = (long)c->rcache_max_maps; break;
+    case MI355X_KNOB_RCACHE_SIZE_LIMIT: *value = (long)c->rcache_limit; break;
+    case MI355X_KNOB_PEER_MAPS: {
+        std::lock_guard<std::recursive_mutex> g(const_cast<mi355x_comm *>(c)->reg_mtx);
+        *value = (long)peer_map_count(c);
+        break;
+    }
+    case MI355X_KNOB_RCACHE_EVICTIONS: *value = (long)c->rcache_evictions; break;
     default: return set_error(MI355X_ERR_ARG, "unknown knob %d", knob);
     }
     return MI355X_SUCCESS;
@@ -2240,7 +2925,7 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
         if (value < 4 || value > 256) return set_error(MI355X_ERR_ARG, "copy_block_kib out of range");
         coll_tune().copy_block_kib = (int)value;
         break;
-    case MI355X_KNOB_PIPE: c->pipe_on = value != 0; break;
+    case MI355X_KNOB_PIPE: c->pipe_on = value != 0 && (c->flows & MI355X_FLOW_PIPE); break;  // (a failed self-test keeps it off)
     case MI355X_KNOB_PIPE_WG_PER_CU:
         if (value < 1 || value > 8) return set_error(MI355X_ERR_ARG, "pipe_wg_per_cu out of range");
         coll_tune().pipe_wg_per_cu = (int)value;
@@ -2267,25 +2952,34 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
         break;
     case MI355X_KNOB_SVC_PULL_MAX_BYTES:
         if (value < 0 || value > (1l << 30)) return set_error(MI355X_ERR_ARG, "svc_pull_max_bytes out of range");
-        if (c->svc_ok) {
+        if (c->svc_ok || c->svc_want) {
             drain(c);
             c->svc_pull_max = (size_t)value;
         }
         break;
     case MI355X_KNOB_SVC_PULL_COPY_MAX_BYTES:
         if (value < 0 || value > (1l << 30)) return set_error(MI355X_ERR_ARG, "svc_pull_copy_max_bytes out of range");
-        if (c->svc_ok) {
+        if (c->svc_ok || c->svc_want) {
             drain(c);
             c->svc_copy_max = (size_t)value;
         }
         break;
     case MI355X_KNOB_SVC_MAX_BYTES:
         if (value < 0 || value > (64l << 20)) return set_error(MI355X_ERR_ARG, "svc_max_bytes out of range");
-        if (c->svc_ok) {  // a communicator without the service keeps 0
+        if (c->svc_ok || c->svc_want) {  // a communicator that cannot have the service keeps 0
             drain(c);
             c->svc_max = (size_t)value;
         }
         break;
+    case MI355X_KNOB_RCACHE_MAX_MAPS:
+    case MI355X_KNOB_RCACHE_SIZE_LIMIT: {
+        if (value < 0) return set_error(MI355X_ERR_ARG, "rcache bound < 0");
+        drain(c);
+        std::lock_guard<std::recursive_mutex> g(c->reg_mtx);
+        (knob == MI355X_KNOB_RCACHE_MAX_MAPS ? c->rcache_max_maps : c->rcache_limit) = (size_t)value;
+        rcache_trim(c, nullptr);
+        break;
+    }
     case MI355X_KNOB_STAGE_BYTES:
         if (value < 4096 || value >= (1l << 31)) return set_error(MI355X_ERR_ARG, "stage_bytes out of range");
         if (c->stage) (void)hipFree(c->stage);
@@ -2362,6 +3056,8 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
         MI_HIP(hipStreamSynchronize(s));
         return MI355X_SUCCESS;
     }
+    rc = svc_maybe_claim(c, count * esz <= std::max(c->svc_max, c->svc_pull_max));
+    if (rc) return rc;
     int alg = pick_allreduce(c, count, esz);
     // the reference's own fallbacks: segmented ring -> ring when count < n * segcount
     // (coll_tuned_allreduce.c:672-679), ring -> recursive doubling when count < n (:398-405)
@@ -2397,7 +3093,7 @@ static int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
         }
         return ll_run(c, a, op, type, s);
     }
-    bool pipe = ring && !c->loopback && c->pipe_on && !coll_tune().push;
+    bool pipe = ring && !c->loopback && c->pipe_on && (c->flows & MI355X_FLOW_PIPE) && !coll_tune().push;
     if (pipe) {  // collective setup first: it reuses the exchange slots
         rc = ensure_pipe(c);
         if (rc) return rc;
@@ -2582,6 +3278,8 @@ static int reduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t co
     int ra;
     if (!reduce_program(c, count, esz, root, &pr, &ra)) return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
     c->last_alg = ra;
+    rc = svc_maybe_claim(c, count * esz <= c->svc_max);
+    if (rc) return rc;
     if (ll_usable(c, count * esz) && (pr.is_fold || c->size <= kTreeMax)) {
         LLArgs a;
         std::memset(&a, 0, sizeof(a));
@@ -2669,6 +3367,8 @@ static int reduce_scatter_block_impl(mi355x_comm_t *c, const void *sbuf, void *r
     if (!reduce_program(c, count, esz, 0, &pr, &ra)) return set_error(MI355X_ERR_UNSUPPORTED, "schedule too large");
     c->last_alg = ra;
     const bool inplace = (in == (const void *)rbuf);
+    rc = svc_maybe_claim(c, !inplace && c->svc_rs && rcount * esz <= c->svc_pull_max);
+    if (rc) return rc;
     if (inplace) {
         rc = ensure_scratch(c, rcount * esz);
         if (rc) return rc;
@@ -2731,6 +3431,12 @@ static int reduce_scatter_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, c
     c->last_alg = alg;
     const size_t mine_n = (size_t)rcounts[c->rank];
     const bool inplace = (in == (const void *)rbuf);
+    {
+        size_t mb = 0;
+        for (int r = 0; r < c->size; ++r) mb = std::max(mb, (size_t)rcounts[r]);
+        rc = svc_maybe_claim(c, !inplace && c->svc_rs && mb * esz <= c->svc_pull_max);
+        if (rc) return rc;
+    }
     if (inplace) {
         rc = ensure_scratch(c, mine_n * esz);
         if (rc) return rc;
@@ -2801,6 +3507,8 @@ static int allgather_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t
     if (bytes == 0) return MI355X_SUCCESS;
     hipStream_t s = resolve_stream(stream);
     const void *src = sbuf ? sbuf : (const char *)rbuf + (size_t)c->rank * bytes;
+    int rc0 = svc_maybe_claim(c, bytes <= std::max(c->svc_max, c->svc_copy_max));
+    if (rc0) return rc0;
     if (ll_usable(c, bytes)) {
         c->last_alg = 3;
         LLArgs a;
@@ -2864,6 +3572,8 @@ static int bcast_impl(mi355x_comm_t *c, void *buf, size_t bytes, int root, void 
     if (root < 0 || root >= c->size) return set_error(MI355X_ERR_ARG, "bad root");
     if (bytes == 0 || c->size == 1) return MI355X_SUCCESS;
     hipStream_t s = resolve_stream(stream);
+    int rc0 = svc_maybe_claim(c, bytes <= std::max(c->svc_max, c->svc_copy_max));
+    if (rc0) return rc0;
     if (ll_usable(c, bytes)) {
         c->last_alg = 3;
         LLArgs a;
@@ -2939,6 +3649,7 @@ int mi355x_allreduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t coun
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     DeviceGuard dg(c->device);
     drain(c);
+    CallGate gate(c);
     return allreduce_impl(c, sbuf, rbuf, count, type, op, stream);
 }
 int mi355x_reduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int root,
@@ -2947,6 +3658,7 @@ int mi355x_reduce(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, 
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     DeviceGuard dg(c->device);
     drain(c);
+    CallGate gate(c);
     return reduce_impl(c, sbuf, rbuf, count, type, op, root, stream);
 }
 int mi355x_reduce_scatter_block(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t rcount, int type, int op,
@@ -2955,6 +3667,7 @@ int mi355x_reduce_scatter_block(mi355x_comm_t *c, const void *sbuf, void *rbuf, 
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     DeviceGuard dg(c->device);
     drain(c);
+    CallGate gate(c);
     return reduce_scatter_block_impl(c, sbuf, rbuf, rcount, type, op, stream);
 }
 int mi355x_reduce_scatter(mi355x_comm_t *c, const void *sbuf, void *rbuf, const int *rcounts, int type, int op,
@@ -2963,6 +3676,7 @@ int mi355x_reduce_scatter(mi355x_comm_t *c, const void *sbuf, void *rbuf, const 
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     DeviceGuard dg(c->device);
     drain(c);
+    CallGate gate(c);
     return reduce_scatter_impl(c, sbuf, rbuf, rcounts, type, op, stream);
 }
 int mi355x_allgather(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, void *stream)
@@ -2970,6 +3684,7 @@ int mi355x_allgather(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t byte
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     DeviceGuard dg(c->device);
     drain(c);
+    CallGate gate(c);
     return allgather_impl(c, sbuf, rbuf, bytes, stream);
 }
 int mi355x_bcast(mi355x_comm_t *c, void *buf, size_t bytes, int root, void *stream)
@@ -2977,6 +3692,7 @@ int mi355x_bcast(mi355x_comm_t *c, void *buf, size_t bytes, int root, void *stre
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     DeviceGuard dg(c->device);
     drain(c);
+    CallGate gate(c);
     return bcast_impl(c, buf, bytes, root, stream);
 }
 

@@ -199,7 +199,7 @@ struct CollTune {
     int pipe_wg_per_cu = 2;
     int pipe_chunk_kib = 0;
     // pipelined allreduce: publish chunks write-through instead of L2 write-back + invalidate fences
-    // (faster at every n measured: rehearsal n = 8 3.85 vs 4.69 ms, n = 4 2.03 vs 2.29)
+    // (faster at every n measured: rehearsal n = 8 3.50-3.78 vs 4.69 ms, n = 4 2.03 vs 2.29)
     int pipe_wt = 1;
 };
 CollTune &coll_tune();

@@ -270,6 +270,7 @@ int mi355x_gatherv(mi355x_comm_t *c, const void *sbuf, size_t sbytes, void *rbuf
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     DeviceGuard dg(c->device);
     drain(c);
+    CallGate gate(c);
     return gatherv_impl(c, sbuf, sbytes, rbuf, rcounts, displs, root, stream);
 }
 
@@ -280,6 +281,7 @@ int mi355x_gather(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, 
     for (int q = 0; q < c->size; ++q) dsp[(size_t)q] = (size_t)q * bytes;
     DeviceGuard dg(c->device);
     drain(c);
+    CallGate gate(c);
     return gatherv_impl(c, sbuf, bytes, rbuf, cnt.data(), dsp.data(), root, stream);
 }
 
@@ -289,6 +291,7 @@ int mi355x_scatterv(mi355x_comm_t *c, const void *sbuf, const size_t *scounts, c
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     DeviceGuard dg(c->device);
     drain(c);
+    CallGate gate(c);
     return scatterv_impl(c, sbuf, scounts, displs, rbuf, rbytes, root, stream);
 }
 
@@ -299,6 +302,7 @@ int mi355x_scatter(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t bytes,
     for (int q = 0; q < c->size; ++q) dsp[(size_t)q] = (size_t)q * bytes;
     DeviceGuard dg(c->device);
     drain(c);
+    CallGate gate(c);
     return scatterv_impl(c, sbuf, cnt.data(), dsp.data(), rbuf, bytes, root, stream);
 }
 
@@ -308,6 +312,7 @@ int mi355x_allgatherv(mi355x_comm_t *c, const void *sbuf, size_t sbytes, void *r
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     DeviceGuard dg(c->device);
     drain(c);
+    CallGate gate(c);
     return allgatherv_impl(c, sbuf, sbytes, rbuf, rcounts, displs, stream);
 }
 
@@ -317,6 +322,7 @@ int mi355x_alltoallv(mi355x_comm_t *c, const void *sbuf, const size_t *scounts, 
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     DeviceGuard dg(c->device);
     drain(c);
+    CallGate gate(c);
     return alltoallv_impl(c, sbuf, scounts, sdispls, rbuf, rcounts, rdispls, stream);
 }
 
@@ -327,6 +333,7 @@ int mi355x_alltoall(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t bytes
     for (int q = 0; q < c->size; ++q) dsp[(size_t)q] = (size_t)q * bytes;
     DeviceGuard dg(c->device);
     drain(c);
+    CallGate gate(c);
     return alltoallv_impl(c, sbuf, cnt.data(), dsp.data(), rbuf, cnt.data(), dsp.data(), stream);
 }
 
@@ -335,6 +342,7 @@ int mi355x_scan(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, in
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     DeviceGuard dg(c->device);
     drain(c);
+    CallGate gate(c);
     return scan_impl(c, sbuf, rbuf, count, type, op, false, stream);
 }
 
@@ -343,6 +351,7 @@ int mi355x_exscan(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, 
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     DeviceGuard dg(c->device);
     drain(c);
+    CallGate gate(c);
     return scan_impl(c, sbuf, rbuf, count, type, op, true, stream);
 }
 

@@ -338,6 +338,9 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
         if (blockIdx.x >= part) {  // not needed by this call: on to the next verdict
             ++want;
             idle0 = __builtin_amdgcn_s_memrealtime();
+            // every wave has read s_door before thread 0 may write the next verdict into it (a
+            // lagging wave would otherwise follow the next call's verdict to a different barrier)
+            __syncthreads();
             continue;
         }
         uint64_t *tr = (g.trace && blockIdx.x == 0) ? g.trace + (want % kSvcTraceCalls) * kSvcTraceCols : nullptr;

@@ -79,6 +79,13 @@ struct alignas(64) RankSlot {
     // command processor behind the rank's kernels (hipStreamWriteValue64 into the host-registered
     // control segment); every rank polls every rank's word instead of a stream sync + barrier
     alignas(64) std::atomic<uint64_t> done;
+    // the call gate (coll_comm.cpp, CallGate): 0 between calls, 1 inside an engine collective, 2
+    // held by a process that is taking the resident service away from this communicator (it may do
+    // so only while every rank is between the same two calls); calls = gated calls completed
+    alignas(64) std::atomic<uint32_t> gate;
+    uint32_t flow_ok;                 // flow self-test: the MI355X_FLOW_* this rank saw exact
+    std::atomic<uint64_t> calls;
+    std::atomic<uint64_t> svc_last_ns;  // CLOCK_MONOTONIC time of this rank's last service call
 };
 
 struct Ctrl {
@@ -93,6 +100,9 @@ struct Ctrl {
     alignas(64) std::atomic<uint64_t> bar_count;
     alignas(64) std::atomic<uint64_t> bar_gen;
     alignas(64) std::atomic<uint32_t> abort_flag;
+    // the service epoch (claim number) another process took the resident service away at: every
+    // rank lets go of it at its next call (CallGate)
+    alignas(64) std::atomic<uint64_t> svc_revoked;
     alignas(64) RankSlot slot[1];
 };
 
@@ -144,6 +154,7 @@ struct PeerMap {
     int pins = 0;                  // in-flight point-to-point reads: never closed meanwhile
     bool persistent = false;       // a region the engine keeps mapped for the communicator's
                                    // life (LL and pipeline flag regions): never dropped
+    size_t bytes = 0;              // the exporter's allocation size (the rcache byte limit)
 };
 
 inline void close_map(PeerMap &m)
@@ -223,6 +234,10 @@ struct mi355x_comm {
     uint64_t seq = 0;
     uint64_t vote_seq = 0;                        // mi355x_comm_vote calls made
     std::map<mi355x::HandleKey, mi355x::PeerMap> peer_maps;
+    // peer-mapping cache bounds (MI355X_RCACHE_MAX_MAPS / MI355X_RCACHE_SIZE_LIMIT, knobs of the same
+    // names; 0 = unlimited, the default, as mpool_rgpusm_rcache_size_limit): LRU eviction
+    size_t rcache_max_maps = 0, rcache_limit = 0;
+    uint64_t rcache_evictions = 0;
     std::vector<mi355x::LocalReg> local_regs;
     void *scratch = nullptr;
     size_t scratch_bytes = 0;
@@ -288,6 +303,27 @@ struct mi355x_comm {
     // the host-synchronised flow, profiles/r04_svc_rs_latency.jsonl); MI355X_SVC_RS=0 turns it off
     bool svc_rs = true;
     bool svc_keep = false;                        // this call's exchange leaves the service resident
+    // ownership (coll_comm.cpp, svc_claim): claimed at a communicator's first service-sized call,
+    // agreed by every rank in that call; handed over when another communicator of the process wants
+    // the service and this one has been idle on every rank for svc_handover_s (svc_revoke)
+    bool svc_want = false;                        // may claim (multi-process, <= 8 ranks, LL self-test ok)
+    bool svc_attached = false;                    // counted among the users of the process's service resources
+    bool svc_flows_tested = false;                // the service flows' self-test has run (first claim)
+    uint64_t svc_epoch = 0;                       // successful claims (same on every rank)
+    uint64_t svc_tries = 0;                       // service-sized calls made without the service
+    uint64_t svc_retry = 16;                      // a claim is attempted every svc_retry such calls
+    uint64_t svc_revocations = 0;                 // times this communicator lost the service to another
+    double svc_handover_s = 0.01;                 // MI355X_SVC_HANDOVER_MS: idle time before a handover
+    // cross-device flows (MI355X_FLOW_*) this communicator may use, and those that failed their
+    // self-test on some rank (creation: the pipelined flow; first claim: the service's flows)
+    unsigned flows = 0x1f, flows_failed = 0;
+    bool pipe_untested = false;                   // the pipelined flow's self-test was not admitted
+    size_t pipe_chunk_override = 0;               // elements per chunk (the self-test's small chunks)
+    bool gated = false;                           // multi-process: engine calls pass the call gate
+    uint64_t gate_calls = 0;                      // gated calls completed (RankSlot::calls)
+    size_t ll_bytes = 0;                          // LL region size (ll_resync)
+    double create_us = 0, selftest_us = 0;
+    bool svc_stuck = false;                       // a service kernel never left (its memory is leaked, never reused)
     uint64_t *svc_trace = nullptr;                // MI355X_SVC_TRACE=1: stage stamps (pinned host), printed at destroy
     // pipelined allreduce (coll_pipe.hip): per-chunk ready flags in an uncached region that
     // every peer writes into (row q = flags raised by rank q), and the work-queue counter
@@ -308,6 +344,7 @@ struct mi355x_comm {
     bool pipe_on = false;                         // MI355X_KNOB_PIPE (env MI355X_PIPE; default: size >= 4)
     uint64_t pipe_holder = 0;                     // this communicator's id in the GPU token table
     int pipe_token = -1;                          // token table slot of my GPU (-1: not looked up)
+    int pipe_entry = -1;                          // my registration in that token's holder list while held
     uint64_t pipe_refused = 0;                    // calls that fell back because a token was taken
     // finish() by device-written completion words (see RankSlot::done): the control segment
     // registered with HIP (hipHostRegister) and its device address; 0 = stream sync + barrier
@@ -352,6 +389,7 @@ int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force);
 // has not received it yet
 int export_dmabuf(mi355x_comm *c, BufDesc *d, uint64_t peers);
 int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **entry = nullptr);
+size_t peer_map_count(const mi355x_comm *c);  // evictable-kind peer mappings currently open
 // publish nbuf buffers, meet every rank, map every rank's buffers: peers[b][r] (coll_comm.cpp)
 // persistent: the mappings stay for the communicator's life (never dropped to make room)
 int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t sig[4],
@@ -365,6 +403,22 @@ int check_common(mi355x_comm *c, int op, int type);
 void drain(mi355x_comm *c);                         // wait for every posted nonblocking call
 int post(mi355x_comm *c, void *stream, std::function<int(hipStream_t)> run, mi355x_request **out);
 void p2p_destroy(mi355x_comm *c);
+// the call gate around every engine collective of a multi-process communicator (coll_comm.cpp)
+void gate_enter(mi355x_comm *c);
+void gate_exit(mi355x_comm *c);
+struct CallGate {
+    mi355x_comm *c;
+    explicit CallGate(mi355x_comm *c_) : c(c_ && c_->gated ? c_ : nullptr)
+    {
+        if (c) gate_enter(c);
+    }
+    ~CallGate()
+    {
+        if (c) gate_exit(c);
+    }
+    CallGate(const CallGate &) = delete;
+    CallGate &operator=(const CallGate &) = delete;
+};
 int p2p_progress(mi355x_comm *c);
 int p2p_wait(mi355x_request *r);
 } // namespace mi355x

@@ -427,9 +427,10 @@ static void start_read(mi355x_comm *c, P2P *p, mi355x_request *r, const P2PMsg &
     int64_t first = 0;
     const bool contig = !r->ddt || ddt_contiguous(r->ddt, r->count, &first);
     char *dst = (char *)r->buf + first;
-    hipStream_t s;
-    int rc = p2p_stream(c, p, &s);
-    if (rc) return fail(rc);
+    hipStream_t s = nullptr;
+    int rc = MI355X_SUCCESS;
+    // (the stream only where a kernel or an async copy runs: not for a host payload into host memory)
+    if ((!(env->flags & kEnvHost) || !r->host || !contig) && (rc = p2p_stream(c, p, &s))) return fail(rc);
     if (env->flags & kEnvHost) {
         // host payload (sm-BTL style): copied out synchronously, FIN at once
         const char *src = nullptr;
@@ -500,6 +501,8 @@ static void start_read(mi355x_comm *c, P2P *p, mi355x_request *r, const P2PMsg &
                 rc = set_error(MI355X_ERR_HIP, "device-to-host copy of a %zu-byte message failed", n);
         }
     }
+    if (rc == MI355X_SUCCESS && !r->ev && hipEventCreateWithFlags(&r->ev, hipEventDisableTiming) != hipSuccess)
+        rc = set_error(MI355X_ERR_HIP, "hipEventCreate failed");
     if (rc == MI355X_SUCCESS && hipEventRecord(r->ev, s) != hipSuccess)
         rc = set_error(MI355X_ERR_HIP, "hipEventRecord on the point-to-point stream failed");
     if (rc) {
@@ -826,13 +829,10 @@ static int make_recv(mi355x_comm *c, void *buf, size_t count, const mi355x_ddt_t
     }
     r->host = !dev;
     DeviceGuard dg(c->device);
-    if (hipEventCreateWithFlags(&r->ev, hipEventDisableTiming) != hipSuccess) {
-        delete r;
-        return set_error(MI355X_ERR_HIP, "hipEventCreate failed");
-    }
+    // (the completion event of a device-side read is created when one starts, start_read: a host
+    // payload copied out on the host needs none -- hipEventCreate would be most of its latency)
     // the receive buffer may be written once the caller's prior work on `stream` is done
     if (bytes && (dev || stream) && hipStreamSynchronize(resolve_stream(stream)) != hipSuccess) {
-        (void)hipEventDestroy(r->ev);
         delete r;
         return set_error(MI355X_ERR_HIP, "caller stream failed");
     }

@@ -628,9 +628,10 @@ def svc_mode(key, rank, size, dev):
     """the resident LL service (coll_svc.hip on a private HSA queue, svc_queue.cpp) beside the rest of
     the process: while it stays resident (MI355X_SVC_IDLE_MS=3000 here) hipDeviceSynchronize and work
     on fresh streams do not wait for it; back-to-back calls reuse one launch; it leaves when idle and
-    comes back on the next call; one service per process -- a second communicator does not get it
-    (its knob reads 0) and still computes exactly on the per-call paths; a communicator created after
-    the owner is gone gets it"""
+    comes back on the next call.  One service per process, owned by the communicator that issues the
+    small calls: claimed at a communicator's first small call, kept while it is busy
+    (MI355X_SVC_HANDOVER_MS=200 here), handed over to the other communicator once it has been idle;
+    the communicator without it computes exactly on the per-call paths"""
     import os
     import time
     import torch
@@ -641,16 +642,21 @@ def svc_mode(key, rank, size, dev):
     b = pkg.Comm.create(key + "_b", rank, size, dev)
     a.set("SVC_MAX_BYTES", 64 << 10)
     b.set("SVC_MAX_BYTES", 64 << 10)
-    assert a.get("SVC_MAX_BYTES") == 64 << 10, "the first communicator owns the service"
-    assert b.get("SVC_MAX_BYTES") == 0, "one service per process: the second communicator has none"
+    assert a.get("SVC_OWNER") == 0 and b.get("SVC_OWNER") == 0, "nothing is claimed before a small call"
     x = torch.full((1000,), float(rank + 1), device="cuda")
     y = torch.empty_like(x)
     want = size * (size + 1) / 2
-    for c in (a, b, a, b):
+
+    def ar(c, k=0):
+        x.fill_(float(rank + 1 + k))
         y.fill_(-1)
         torch.cuda.synchronize()
         c.allreduce(x.data_ptr(), y.data_ptr(), 1000, f32, SUM)
-        assert bool(torch.all(y == want).item()), "allreduce next to the service"
+        assert bool(torch.all(y == want + size * k).item()), "allreduce next to the service"
+
+    for c in (a, b, a, b):  # b asks while a is busy: a keeps it
+        ar(c)
+    assert a.get("SVC_OWNER") == 1 and b.get("SVC_OWNER") == 0
     assert b.get("SVC_CALLS") == 0 and a.get("SVC_CALLS") >= 2
     # resident now (idle limit 3 s): the device synchronizes without it, a fresh stream runs
     assert a.get("SVC_LAUNCHES") >= 1
@@ -667,32 +673,146 @@ def svc_mode(key, rank, size, dev):
     assert bool(torch.all(z == 2 * (rank + 1)).item())
     launches = a.get("SVC_LAUNCHES")
     for k in range(200):
-        x.fill_(float(rank + k))
-        a.allreduce(x.data_ptr(), y.data_ptr(), 1000, f32, SUM)
-        assert bool(torch.all(y == sum(r + k for r in range(size))).item()), ("back to back", k)
+        ar(a, k)
     relaunched = a.get("SVC_LAUNCHES") - launches
     assert relaunched <= 2, f"{relaunched} relaunches over 200 back-to-back calls"
+    # a idle longer than the handover time: b's next claim takes the service over, on every rank
+    time.sleep(0.3)
+    for k in range(40):
+        ar(b, k)
+    assert b.get("SVC_OWNER") == 1 and a.get("SVC_OWNER") == 0, (b.get("SVC_OWNER"), a.get("SVC_OWNER"))
+    assert b.get("SVC_CALLS") > 0
+    handed = b.get("SVC_CALLS")
+    for k in range(5):  # a without the service: the per-call paths, exact
+        ar(a, k)
     # idle exit and relaunch (a short idle limit on a fresh owner)
     a.barrier()
     a.destroy()
+    b.barrier()
+    b.destroy()
     os.environ["MI355X_SVC_IDLE_MS"] = "2"
     c = pkg.Comm.create(key + "_c", rank, size, dev)
     c.set("SVC_MAX_BYTES", 64 << 10)
-    assert c.get("SVC_MAX_BYTES") == 64 << 10, "a communicator created after the owner left gets the service"
     for k in range(20):
-        x.fill_(float(rank + k))
-        c.allreduce(x.data_ptr(), y.data_ptr(), 1000, f32, SUM)
-        assert bool(torch.all(y == sum(r + k for r in range(size))).item()), ("after idle exits", k)
+        ar(c, k)
         time.sleep(0.01)  # longer than the idle limit: the service has left; the next call relaunches
+    assert c.get("SVC_OWNER") == 1, "a communicator created after the owners left gets the service"
     assert c.get("SVC_LAUNCHES") >= 10, c.get("SVC_LAUNCHES")
     print(f"rank {rank} svc: sync {dt_sync * 1e3:.2f} ms, fresh stream {dt_stream * 1e3:.2f} ms while resident; "
-          f"{relaunched} relaunches over 200 calls; {c.get('SVC_LAUNCHES')} launches over 20 spaced calls", flush=True)
-    b.set("SVC_MAX_BYTES", 64 << 10)
-    assert b.get("SVC_MAX_BYTES") == 0, "the service is decided at creation"
-    for cc in (b, c):
-        cc.barrier()
-        cc.destroy()
+          f"{relaunched} relaunches over 200 calls; handed over after idle ({handed} calls served on the second "
+          f"communicator); {c.get('SVC_LAUNCHES')} launches over 20 spaced calls", flush=True)
+    c.barrier()
+    c.destroy()
     print(f"rank {rank} svc OK", flush=True)
+
+
+def svc_dup(key, rank, size, dev):
+    """MPI_COMM_WORLD created first, then a dup that issues the small allreduces (the usual gradient-
+    communicator pattern): the dup is served by the resident service; world's own small calls later
+    take it back once the dup has been idle, and the dup again after world; every result exact and
+    every rank reports the same owner at every step"""
+    import time
+    import torch
+    torch.cuda.set_device(dev)
+    pkg = load_pkg()
+    f32, SUM = pkg.T["FLOAT"], pkg.OP["SUM"]
+    world = pkg.Comm.create(key + "_w", rank, size, dev)
+    dup = pkg.Comm.create(key + "_d", rank, size, dev)
+    x = torch.empty(2048, device="cuda")
+    y = torch.empty_like(x)
+    owners = []
+
+    def burst(c, tag, calls=100):
+        for k in range(calls):
+            x.fill_(float(rank + 1 + k))
+            y.fill_(-1)
+            torch.cuda.synchronize()
+            c.allreduce(x.data_ptr(), y.data_ptr(), 2048, f32, SUM)
+            assert bool(torch.all(y == size * (size + 1) / 2 + size * k).item()), (tag, k)
+        owners.append(f"{tag}:world={world.get('SVC_OWNER')},dup={dup.get('SVC_OWNER')}")
+
+    l0 = dup.get("SVC_LAUNCHES")
+    burst(dup, "dup")
+    assert dup.get("SVC_OWNER") == 1 and dup.get("SVC_LAUNCHES") > l0, "the dup is served"
+    assert world.get("SVC_OWNER") == 0
+    time.sleep(0.05)                  # dup idle: world's small calls take the service over
+    burst(world, "world")
+    assert world.get("SVC_OWNER") == 1 and dup.get("SVC_OWNER") == 0
+    time.sleep(0.05)
+    burst(dup, "dup2")
+    assert dup.get("SVC_OWNER") == 1 and world.get("SVC_OWNER") == 0
+    print(f"rank {rank} owners {' '.join(owners)} claims world={world.get('SVC_CLAIMS')} dup={dup.get('SVC_CLAIMS')}",
+          flush=True)
+    for c in (dup, world):
+        c.barrier()
+        c.destroy()
+    print(f"rank {rank} svc_dup OK", flush=True)
+
+
+def selftest(key, rank, size, dev):
+    """the creation-time / first-claim flow self-tests: with MI355X_SELFTEST_FAIL=<flow> on one rank
+    (fault injection), that flow is off on EVERY rank (FLOWS / FLOWS_FAILED agree) and calls of every
+    kind stay exact vs the oracle; with no injection every flow is on.  Creation time is printed."""
+    import torch
+    torch.cuda.set_device(dev)
+    pkg = load_pkg()
+    oracle = load_oracle()
+    ptrs = lambda arrs: (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    expect = pkg.FLOW.get(os.environ.get("SELFTEST_EXPECT", ""), 0)
+    comm = pkg.Comm.create(key, rank, size, dev)
+    create_us, st_us = comm.get("CREATE_US"), comm.get("SELFTEST_US")
+    f32, i32, SUM = pkg.T["FLOAT"], pkg.T["INT32"], pkg.OP["SUM"]
+    x = torch.full((1000,), float(rank + 1), device="cuda")
+    y = torch.empty_like(x)
+    torch.cuda.synchronize()
+    comm.allreduce(x.data_ptr(), y.data_ptr(), 1000, f32, SUM)  # the first small call claims the service
+    assert bool(torch.all(y == size * (size + 1) / 2).item())
+    flows, failed = comm.get("FLOWS"), comm.get("FLOWS_FAILED")
+    assert failed == expect, f"flows failed {failed:#x}, expected {expect:#x}"
+    assert flows == 0x1f & ~expect, f"flows {flows:#x}"
+    assert comm.get("SVC_OWNER") == (0 if expect == pkg.FLOW["SVC_LL"] else 1)
+    if expect == pkg.FLOW["PIPE"]:
+        comm.set("PIPE", 1)
+        assert comm.get("PIPE") == 0, "a flow that failed its self-test cannot be forced on"
+    else:
+        comm.set("PIPE", 1)
+    calls0 = comm.get("SVC_CALLS")
+    # every kind of call, each size class, exact vs the oracle's schedule simulation
+    for count in (3, 2048, 12288, 100_003, size * 300_000):
+        xs = [opdata.make("FLOAT", count, 60 + r) for r in range(size)]
+        outs = [np.zeros_like(xs[0]) for _ in range(size)]
+        oracle.oracle_allreduce(0, size, count, f32, SUM, 0, ptrs(xs), ptrs(outs))
+        dx = torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda()
+        dr = torch.full_like(dx, 0x5a)
+        torch.cuda.synchronize()
+        comm.allreduce(dx.data_ptr(), dr.data_ptr(), count, f32, SUM)
+        opdata.assert_same("FLOAT", "SUM", dr.cpu().numpy().view(np.float32), outs[rank], f"selftest allreduce {count}")
+    for nb in (100, 48 << 10, 1 << 20):
+        src = torch.full((nb,), rank + 3, dtype=torch.uint8, device="cuda")
+        dst = torch.zeros(nb * size, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        comm.allgather(src.data_ptr(), dst.data_ptr(), nb)
+        for r in range(size):
+            assert int(dst[r * nb:(r + 1) * nb].min()) == r + 3 == int(dst[r * nb:(r + 1) * nb].max()), ("ag", nb, r)
+        b = torch.full((nb,), rank, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        comm.bcast(b.data_ptr(), nb, size - 1)
+        assert int(b.min()) == size - 1 == int(b.max()), ("bcast", nb)
+    for rcount in (5, 4096, 70_000):
+        xs = [opdata.make("INT32", rcount * size, 90 + r) for r in range(size)]
+        outs = [np.zeros(rcount, dtype=xs[0].dtype) for _ in range(size)]
+        oracle.oracle_reduce_scatter_block(size, rcount, i32, SUM, ptrs(xs), ptrs(outs))
+        dx = torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda()
+        dr = torch.full((rcount * 4,), 0x5a, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        comm.reduce_scatter_block(dx.data_ptr(), dr.data_ptr(), rcount, i32, SUM)
+        opdata.assert_same("INT32", "SUM", dr.cpu().numpy().view(xs[0].dtype), outs[rank], f"selftest rsb {rcount}")
+    served = comm.get("SVC_CALLS") - calls0
+    print(f"rank {rank} flows {flows:#x} failed {failed:#x} create_us {create_us} selftest_us {st_us} "
+          f"claim_selftest_us {comm.get('SELFTEST_US') - st_us} served {served}", flush=True)
+    comm.barrier()
+    comm.destroy()
+    print(f"rank {rank} selftest OK", flush=True)
 
 
 def svc_stress(key, rank, size, dev):
@@ -866,6 +986,100 @@ def host_bw(key, rank, size, dev):
     print(f"rank {rank} host_bw OK", flush=True)
 
 
+def rcache(key, rank, size, dev):
+    """the bounded peer-mapping cache (RCACHE_MAX_MAPS, mpool/rgpusm's LRU): 64 distinct allocations
+    per rank, each one a 1 MiB allreduce's input and output, then freed and 64 more -- the open
+    mappings of peers' allocations never exceed the bound, evictions happen, every result exact"""
+    import torch
+    torch.cuda.set_device(dev)
+    pkg = load_pkg()
+    comm = pkg.Comm.create(key, rank, size, dev)
+    comm.set("RCACHE_MAX_MAPS", 16)
+    assert comm.get("RCACHE_MAX_MAPS") == 16
+    n = (1 << 20) // 4
+    peak = 0
+    for rnd in range(2):
+        keep = []
+        for k in range(64):
+            # distinct allocations: each larger than the last, all alive until the round ends
+            x = torch.full((n + k * (1 << 19),), float(rank + 1 + k + 100 * rnd), device="cuda")
+            y = torch.full_like(x, float("nan"))
+            torch.cuda.synchronize()
+            comm.allreduce(x.data_ptr(), y.data_ptr(), n, pkg.T["FLOAT"], pkg.OP["SUM"])
+            want = sum(r + 1 + k + 100 * rnd for r in range(size))
+            assert bool(torch.all(y[:n] == want).item()), ("rcache allreduce", rnd, k)
+            peak = max(peak, comm.get("PEER_MAPS"))
+            keep += [x, y]
+        comm.barrier()  # no peer still reads them
+        del keep, x, y
+        torch.cuda.empty_cache()
+    ev = comm.get("RCACHE_EVICTIONS")
+    assert peak <= 16, f"{peak} peer mappings open under a bound of 16"
+    assert ev > 0, "no evictions"
+    print(f"rank {rank} rcache: peak {peak} mappings, {ev} evictions", flush=True)
+    comm.barrier()
+    comm.destroy()
+    print(f"rank {rank} rcache OK", flush=True)
+
+
+def vote_dead(key, rank, size, dev):
+    """a peer process that dies without a word (os._exit right after creation): the surviving
+    host-buffer rank waiting in the buffer-kind vote (an unbounded wait) returns an error within
+    seconds instead of spinning forever"""
+    import time
+    import torch
+    torch.cuda.set_device(dev)
+    pkg = load_pkg()
+    comm = pkg.Comm.create(key, rank, size, dev)
+    comm.barrier()
+    if rank == 1:
+        os._exit(0)
+    t0 = time.time()
+    try:
+        comm.vote(False)
+        raise AssertionError("the vote returned although its peer is gone")
+    except pkg.MI355XError as e:
+        assert "gone" in str(e), e
+    dt = time.time() - t0
+    assert dt < 30, dt
+    print(f"rank {rank} vote: dead peer noticed after {dt:.2f} s", flush=True)
+    print(f"rank {rank} vote_dead OK", flush=True)
+
+
+def token_hold(key, dev):
+    """a one-rank communicator takes its GPU's pipelined-grid admission token (as a rank inside a
+    pipelined allreduce holds it) and sleeps until the test SIGKILLs it"""
+    import time
+    import torch
+    torch.cuda.set_device(dev)
+    pkg = load_pkg()
+    comm = pkg.Comm.create(key, 0, 1, dev)
+    assert comm.debug_pipe_token(True), "the admission token of a free GPU"
+    print("holding", flush=True)
+    time.sleep(300)
+
+
+def token_check(key, rank, size, dev):
+    """pipelined 64 MiB allreduces (MI355X_PIPE=1): exact, and PIPE_REFUSED reported for the test to
+    compare with whether another process holds this GPU's admission token"""
+    import torch
+    torch.cuda.set_device(dev)
+    pkg = load_pkg()
+    comm = pkg.Comm.create(key, rank, size, dev)
+    comm.set("PIPE", 1)
+    n = (64 << 20) // 4
+    for it in range(3):
+        x = torch.full((n,), float(rank + 1 + it), device="cuda")
+        y = torch.full_like(x, float("nan"))
+        torch.cuda.synchronize()
+        comm.allreduce(x.data_ptr(), y.data_ptr(), n, pkg.T["FLOAT"], pkg.OP["SUM"])
+        assert bool(torch.all(y == sum(r + 1 + it for r in range(size))).item()), ("token check", it)
+    print(f"rank {rank} refused {comm.get('PIPE_REFUSED')}", flush=True)
+    comm.barrier()
+    comm.destroy()
+    print(f"rank {rank} token_check OK", flush=True)
+
+
 def main():
     try:
         _main()
@@ -878,6 +1092,18 @@ def _main():
     key, rank, size, dev = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
     if len(sys.argv) > 5 and sys.argv[5] == "concurrent":
         return concurrent_comms(key, rank, size, dev)
+    if len(sys.argv) > 5 and sys.argv[5] == "svc_dup":
+        return svc_dup(key, rank, size, dev)
+    if len(sys.argv) > 5 and sys.argv[5] == "selftest":
+        return selftest(key, rank, size, dev)
+    if len(sys.argv) > 5 and sys.argv[5] == "vote_dead":
+        return vote_dead(key, rank, size, dev)
+    if len(sys.argv) > 5 and sys.argv[5] == "rcache":
+        return rcache(key, rank, size, dev)
+    if len(sys.argv) > 5 and sys.argv[5] == "token_hold":
+        return token_hold(key, dev)
+    if len(sys.argv) > 5 and sys.argv[5] == "token_check":
+        return token_check(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "done_words":
         return done_words(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "host_bw":

@@ -272,15 +272,20 @@ def test_mca_variables_registered(monkeypatch):
     try:
         monkeypatch.setenv("OMPI_MCA_coll_mi355x_priority", "77")
         monkeypatch.setenv("OMPI_MCA_op_hip_priority", "33")
+        monkeypatch.setenv("OMPI_MCA_coll_mi355x_rcache_size_limit", str(3 << 30))
         assert L.mini_component_register(coll) == 0 and L.mini_component_register(oph) == 0
         names = {L.mini_var_name(i).decode(): L.mini_var_int(i) for i in range(L.mini_var_count())}
         assert names["coll_mi355x_priority"] == 77 and prio.value == 77
         assert names["op_hip_priority"] == 33 and oprio.value == 33
         assert "coll_mi355x_allreduce_algorithm" in names and names["coll_mi355x_pml_hook"] == 1
         assert names["coll_mi355x_mixed_buffers"] == 1  # mixed host / device buffers: on by default
+        # the peer-mapping cache bounds (mpool_rgpusm_rcache_size_limit: bytes, unsigned long long)
+        assert names["coll_mi355x_rcache_max_maps"] == 0
+        assert ctypes.c_ulonglong.in_dll(m.coll, "mca_coll_mi355x_rcache_size_limit").value == 3 << 30
         _coll_env(monkeypatch)
         comm = L.mini_comm_create(0, 4, 17)
         mod, p = _comm_query(m, comm)
         assert mod and p == 77
     finally:
         prio.value, oprio.value = saved
+        ctypes.c_ulonglong.in_dll(m.coll, "mca_coll_mi355x_rcache_size_limit").value = 0

@@ -42,12 +42,13 @@ def test_ipc_ranks(gpu, size):
             assert f"rank {r} {stage}" in outs[r], f"rank {r} did not report '{stage}':\n{outs[r][-3000:]}"
 
 
-def _run_mode(gpu, mode, size=2, timeout=280, extra_env=None):
-    key = "t" + uuid.uuid4().hex[:12]
+def _run_mode(gpu, mode, size=2, timeout=280, extra_env=None, key=None, rank_env=None):
+    key = key or "t" + uuid.uuid4().hex[:12]
     ndev = gpu.cuda.device_count()
     env = dict(os.environ, MI355X_TIMEOUT_S="60", **(extra_env or {}))
     procs = [subprocess.Popen([sys.executable, str(HERE / "ipc_worker.py"), key, str(r), str(size), str(r % ndev), mode],
-                              env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(size)]
+                              env=dict(env, **((rank_env or {}).get(r, {}))), stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(size)]
     outs = []
     for p in procs:
         try:
@@ -63,9 +64,29 @@ def _run_mode(gpu, mode, size=2, timeout=280, extra_env=None):
 
 @pytest.mark.parametrize("size", [2, 3])
 def test_resident_service(gpu, size):
-    """the resident LL service beside the rest of the process (ipc_worker.py::svc_mode)"""
-    outs = _run_mode(gpu, "svc", size, extra_env={"MI355X_SVC_IDLE_MS": "3000"})
+    """the resident LL service beside the rest of the process, and its handover between
+    communicators (ipc_worker.py::svc_mode)"""
+    outs = _run_mode(gpu, "svc", size, extra_env={"MI355X_SVC_IDLE_MS": "3000", "MI355X_SVC_HANDOVER_MS": "200"})
     print(next(line for line in outs[0].splitlines() if "svc:" in line))
+
+
+def test_resident_service_follows_the_busy_communicator(gpu):
+    """world created first, a dup issues the small allreduces: the dup is served; ownership moves
+    back and forth with the bursts, every rank agrees on the owner (ipc_worker.py::svc_dup)"""
+    outs = _run_mode(gpu, "svc_dup", 3)
+    lines = [next(ln for ln in out.splitlines() if " owners " in ln) for out in outs]
+    assert len({ln.split(" owners ", 1)[1] for ln in lines}) == 1, lines  # the same owner on every rank
+    print(lines[0])
+
+
+@pytest.mark.parametrize("flow", ["", "svc_ll", "svc_pull", "svc_copy", "svc_rs", "pipe"])
+def test_flow_selftest(gpu, flow):
+    """every default-on cross-device flow is self-tested before its first use; a failure injected on
+    ONE rank (MI355X_SELFTEST_FAIL) turns that flow off on EVERY rank, and calls of every kind stay
+    exact vs the oracle (ipc_worker.py::selftest)"""
+    rank_env = {1: {"MI355X_SELFTEST_FAIL": flow}} if flow else None
+    outs = _run_mode(gpu, "selftest", 2, extra_env={"SELFTEST_EXPECT": flow.upper()}, rank_env=rank_env)
+    print(next(ln for ln in outs[0].splitlines() if " flows " in ln))
 
 
 @pytest.mark.parametrize("size", [2, 3])
@@ -117,3 +138,53 @@ def test_concurrent_communicators(gpu):
     for r, p in enumerate(procs):
         assert p.returncode == 0 and f"rank {r} concurrent OK" in outs[r], f"rank {r}:\n{outs[r][-3000:]}"
     print(outs[0].strip().splitlines()[-2])
+
+
+def test_admission_token_reclaimed_from_dead_holder(gpu):
+    """a process SIGKILLed while it holds its GPU's pipelined-grid admission token: while it lives a
+    pipelined allreduce on that GPU is refused admission (two-phase flow, PIPE_REFUSED > 0); once it
+    is dead the next communicator takes the token back (PIPE_REFUSED == 0) -- the per-user token
+    table outlives jobs, the token must not (coll_comm.cpp: holder registration + reclaim)"""
+    import signal
+    import time
+    key = "t" + uuid.uuid4().hex[:12]
+    env = dict(os.environ, MI355X_TIMEOUT_S="60")
+    holder = subprocess.Popen([sys.executable, str(HERE / "ipc_worker.py"), key + "_h", "0", "1", "0", "token_hold"],
+                              env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    try:
+        t0 = time.time()
+        line = ""
+        while "holding" not in line:
+            line = holder.stdout.readline()
+            assert line or holder.poll() is None, "the holder exited before taking the token"
+            assert time.time() - t0 < 120, "the holder never took the token"
+        refused = [int(ln.split()[-1]) for ln in _run_mode(gpu, "token_check", 2, extra_env={"MI355X_PIPE": "1"},
+                                                          key=key + "_a")[0].splitlines() if " refused " in ln]
+        assert refused and refused[0] > 0, f"a live holder should refuse admission: {refused}"
+    finally:
+        holder.send_signal(signal.SIGKILL)
+        holder.wait(30)
+    outs = _run_mode(gpu, "token_check", 2, extra_env={"MI355X_PIPE": "1"}, key=key + "_b")
+    for out in outs:
+        refused = [int(ln.split()[-1]) for ln in out.splitlines() if " refused " in ln]
+        assert refused == [0], f"the dead holder's token was not reclaimed: {refused}\n{out[-2000:]}"
+
+
+def test_bounded_peer_mapping_cache(gpu):
+    """RCACHE_MAX_MAPS = 16 at 3 ranks over 2 x 64 distinct allocations: peer mappings stay <= 16
+    (LRU eviction, mpool_rgpusm_module.c:104-120,396-419), results exact (ipc_worker.py::rcache)"""
+    outs = _run_mode(gpu, "rcache", 3)
+    print(next(line for line in outs[0].splitlines() if "rcache:" in line))
+
+
+def test_vote_notices_dead_peer(gpu):
+    """the buffer-kind vote waits without a timeout; a peer that dies without setting the abort flag
+    is noticed by its pid (ipc_worker.py::vote_dead)"""
+    key = "t" + uuid.uuid4().hex[:12]
+    env = dict(os.environ, MI355X_TIMEOUT_S="600")
+    procs = [subprocess.Popen([sys.executable, str(HERE / "ipc_worker.py"), key, str(r), "2", "0", "vote_dead"],
+                              env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    # rank 1 stays an unreaped zombie until rank 0 is done: exited counts as gone
+    out, _ = procs[0].communicate(timeout=120)
+    procs[1].communicate(timeout=60)
+    assert procs[0].returncode == 0 and "rank 0 vote_dead OK" in out, out[-3000:]

@@ -3,6 +3,8 @@
  * `reps` calls per size, plus mi355x_comm_barrier alone.  Rank 0 prints one JSON line per row.
  * usage: small_ar_c <nranks> <reps> [paths]   paths: comma list of host (per-call launch + host
  *        synchronisation), ll (per-call LL kernels), svc (resident LL service); default host
+ *        SMALL_COLL=p2p_host / p2p_dev: MPI_Send / MPI_Recv ping-pong between ranks 0 and 1 through
+ *        the engine (host malloc'd or device buffers), one-way microseconds per size
  * build: gcc -O2 -o tools/build/small_ar_c tools/small_ar_c.c -Iinclude -Lompi-release_amd/lib -lmi355x_rt
  *        -Wl,-rpath,'$ORIGIN/../../ompi-release_amd/lib' */
 #include <stdint.h>
@@ -76,7 +78,40 @@ static int run(int rank, int n, int reps, const char *key, const char *paths)
      * reduce_scatter_block (bytes per rank's block; the input is n blocks) */
     const char *coll = getenv("SMALL_COLL") ? getenv("SMALL_COLL") : "allreduce";
     const int kind = strcmp(coll, "allgather") == 0 ? 1 : strcmp(coll, "bcast") == 0 ? 2
-                   : strcmp(coll, "reduce_scatter_block") == 0 ? 3 : 0;
+                   : strcmp(coll, "reduce_scatter_block") == 0 ? 3 : strncmp(coll, "p2p_", 4) == 0 ? 4 : 0;
+    if (kind == 4) {  /* point-to-point ping-pong: ranks 0 and 1 (the others only take part in barriers) */
+        const int host = strcmp(coll, "p2p_host") == 0;
+        char *hb = host ? malloc(maxb) : NULL;
+        void *buf = host ? (void *)hb : s;
+        if (host) memset(hb, rank, maxb);
+        for (int k = 0; k < nsizes; ++k) {
+            double us = 0;
+            for (int phase = 0; phase < 2; ++phase) {
+                const int it = phase ? reps : 50;
+                mi355x_comm_barrier(c);
+                const double t0 = now_us();
+                for (int i = 0; i < it && rank < 2; ++i) {
+                    int e = 0;
+                    if (rank == 0) {
+                        e = mi355x_send(c, buf, sizes[k], NULL, 1, 5, NULL) || mi355x_recv(c, buf, sizes[k], NULL, 1, 6, NULL, NULL);
+                    } else {
+                        e = mi355x_recv(c, buf, sizes[k], NULL, 0, 5, NULL, NULL) || mi355x_send(c, buf, sizes[k], NULL, 0, 6, NULL);
+                    }
+                    if (e) {
+                        fprintf(stderr, "rank %d: %s\n", rank, mi355x_last_error());
+                        return 1;
+                    }
+                }
+                us = (now_us() - t0) / it / 2;
+            }
+            if (rank == 0)
+                printf("{\"coll\": \"%s\", \"bytes\": %zu, \"one_way_us\": %.2f, \"n\": %d, \"caller\": \"C\"}\n", coll,
+                       sizes[k], us, n);
+        }
+        free(hb);
+        fflush(stdout);
+        break;
+    }
     for (int k = 0; k < nsizes; ++k) {
         const size_t cnt = sizes[k] / 4;
 #define ONE_CALL() (kind == 1 ? mi355x_allgather(c, s, r, sizes[k], NULL) \

@@ -1,0 +1,145 @@
+"""What the resident LL service costs a PyTorch-like process, and what it gains it.
+
+Each rank process keeps 4 streams busy with compute (alternating a bandwidth-bound 128 MiB copy and
+a compute-bound 4096^3 bf16 matmul, queued ahead) while its main thread issues a small (8 B) allreduce
+every `interval` microseconds through the engine -- the pattern of a training loop that
+interleaves small collectives (loss / grad-norm scalars) with compute.  Measured per variant and
+interval: the compute streams' throughput (kernels per second over their own span, HIP events)
+relative to the same window with no allreduce at all, and the allreduce latency (median / p90).
+
+Variants (a process pair each, both ranks on the same GPU -- the one-GPU box, so the two processes
+also contend with each other; on separate GPUs each process has its GPU to itself):
+  svc_off        MI355X_SVC=0: every small call takes the host-synchronised flow (a launch + sync)
+  idle_<t>ms     the service on, leaving after t ms without a call (MI355X_SVC_IDLE_MS)
+
+usage: python tools/svc_interference.py [--out FILE] [--variants svc_off,idle_0.1ms,idle_1ms,idle_5ms]
+       [--intervals 50,200,500]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+import uuid
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def rank_main(rank, key, intervals, window_ms):
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.dirname(HERE))
+    import bench
+    pkg = bench.load_pkg()
+    pkg.rt()
+    torch.cuda.set_device(0)
+    comm = pkg.Comm.create(key, rank, 2, 0)
+    f32, SUM = pkg.T["FLOAT"], pkg.OP["SUM"]
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    big = [torch.empty(32 << 20, device="cuda") for _ in range(8)]  # 128 MiB each
+    a = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+    outs = [torch.empty(4096, 4096, device="cuda", dtype=torch.bfloat16) for _ in range(4)]
+    x = torch.ones(2, device="cuda")
+    y = torch.empty_like(x)
+    torch.cuda.synchronize()
+
+    def one_kernel(i, k):
+        if k % 2:
+            big[2 * i + 1].copy_(big[2 * i])
+        else:
+            torch.matmul(a, b, out=outs[i])
+
+    # kernels per stream for a window of ~window_ms (calibrated once, no allreduce)
+    t0 = time.perf_counter()
+    for k in range(20):
+        for i, st in enumerate(streams):
+            with torch.cuda.stream(st):
+                one_kernel(i, k)
+    torch.cuda.synchronize()
+    per_kernel_ms = (time.perf_counter() - t0) * 1e3 / 20
+    nk = max(20, int(window_ms / per_kernel_ms))
+    rows = []
+    for interval in [0] + intervals:  # 0: no allreduce (the compute baseline)
+        comm.barrier()
+        ev = []
+        for i, st in enumerate(streams):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(st):
+                e0.record(st)
+                for k in range(nk):
+                    one_kernel(i, k)
+                e1.record(st)
+            ev.append((e0, e1))
+        lat = []
+        if interval:
+            n_ar = int(window_ms * 1e3 / interval)
+            tstart = time.perf_counter()
+            for j in range(n_ar):
+                target = tstart + j * interval * 1e-6
+                while time.perf_counter() < target:
+                    pass
+                t1 = time.perf_counter()
+                comm.allreduce(x.data_ptr(), y.data_ptr(), 2, f32, SUM)
+                lat.append((time.perf_counter() - t1) * 1e6)
+        torch.cuda.synchronize()
+        assert float(y[0].item()) == 2.0 or not interval
+        spans = [e0.elapsed_time(e1) for e0, e1 in ev]
+        # the streams' common span: from the earliest start to the latest end
+        first = ev[0][0]
+        span = max(first.elapsed_time(e1) for _, e1 in ev) - min(first.elapsed_time(e0) for e0, _ in ev)
+        rows.append({"interval_us": interval, "kernels": 4 * nk, "span_ms": round(span, 3),
+                     "kernels_per_s": round(4 * nk / span * 1e3, 1), "stream_ms": [round(s_, 2) for s_ in spans],
+                     "ar_calls": len(lat), "ar_us_median": round(float(np.median(lat)), 2) if lat else None,
+                     "ar_us_p90": round(float(np.percentile(lat, 90)), 2) if lat else None,
+                     "svc_launches": comm.get("SVC_LAUNCHES"), "svc_calls": comm.get("SVC_CALLS")})
+    comm.barrier()
+    comm.destroy()
+    if rank == 0:
+        base = rows[0]["kernels_per_s"]
+        for r in rows:
+            r["compute_rel"] = round(r["kernels_per_s"] / base, 4)
+            print(json.dumps(r), flush=True)
+
+
+VARIANTS = {"svc_off": {"MI355X_SVC": "0"}, "idle_0.1ms": {"MI355X_SVC_IDLE_MS": "0.1"},
+            "idle_1ms": {"MI355X_SVC_IDLE_MS": "1"}, "idle_5ms": {"MI355X_SVC_IDLE_MS": "5"}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rank", type=int, default=-1)
+    ap.add_argument("--key", default="")
+    ap.add_argument("--intervals", default="50,200,500")
+    ap.add_argument("--window-ms", type=float, default=300.0)
+    ap.add_argument("--variants", default="svc_off,idle_0.1ms,idle_1ms,idle_5ms")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    intervals = [int(v) for v in a.intervals.split(",") if v]
+    if a.rank >= 0:
+        return rank_main(a.rank, a.key, intervals, a.window_ms)
+    for var in a.variants.split(","):
+        key = "int" + uuid.uuid4().hex[:10]
+        env = dict(os.environ, **VARIANTS[var])
+        procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--rank", str(r), "--key", key,
+                                   "--intervals", a.intervals, "--window-ms", str(a.window_ms)],
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(2)]
+        outs = [p.communicate(timeout=300)[0] for p in procs]
+        if any(p.returncode for p in procs):
+            sys.stderr.write("\n".join(outs))
+            sys.exit(1)
+        lines = []
+        for ln in outs[0].splitlines():
+            if ln.startswith("{"):
+                d = json.loads(ln)
+                d = {"variant": var, **d}
+                lines.append(json.dumps(d))
+        if a.out:
+            with open(a.out, "a") as f:
+                f.write("\n".join(lines) + "\n")
+        print("\n".join(lines), flush=True)
+
+
+if __name__ == "__main__":
+    main()
