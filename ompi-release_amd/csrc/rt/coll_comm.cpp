@@ -1588,13 +1588,22 @@ static void svc_release(mi355x_comm *c)
 // A process that wants the service another communicator owns may take it (svc_revoke) only by
 // closing the gates of every rank of the owner while all of them are between the same two calls;
 // the owner's ranks then let go of the service at their next call, on every rank at the same call.
+// A revoker marks a gate with its pid, (pid << 8) | 2, so a waiter can take the gate back from a
+// revoker that died holding it (pids fit in 24 bits: Linux's pid_max is at most 2^22).
+constexpr uint32_t kGateCall = 1u, kGateRevoker = 2u;
+static uint32_t gate_revoker_word() { return ((uint32_t)getpid() << 8) | kGateRevoker; }
+
 void gate_enter(mi355x_comm *c)
 {
     std::atomic<uint32_t> &g = c->ctrl->slot[c->rank].gate;
     unsigned spins = 0;
-    for (uint32_t z = 0; !g.compare_exchange_weak(z, 1u, std::memory_order_acq_rel); z = 0) {
+    for (uint32_t z = 0; !g.compare_exchange_weak(z, kGateCall, std::memory_order_acq_rel); z = 0) {
         _mm_pause();
         if (++spins > 256) sched_yield();  // (held only while a revoker stops this rank's service)
+        if ((spins & 0xfff) == 0 && (z & 0xff) == kGateRevoker && !pid_alive((pid_t)(z >> 8))) {
+            uint32_t w = z;  // the revoker died holding it
+            g.compare_exchange_strong(w, 0u, std::memory_order_acq_rel);
+        }
     }
     if (c->svc_ok && c->ctrl->svc_revoked.load(std::memory_order_acquire) == c->svc_epoch) {
         TRACE(c, "the resident service went to another communicator of a peer process: letting go");
@@ -1623,11 +1632,12 @@ static bool svc_revoke(mi355x_comm *x)
     const auto t0 = std::chrono::steady_clock::now();
     for (bool busy = false; got < x->size && !busy;) {
         uint32_t z = 0;
-        if (k->slot[got].gate.compare_exchange_strong(z, 2u, std::memory_order_acq_rel)) {
+        if (k->slot[got].gate.compare_exchange_strong(z, gate_revoker_word(), std::memory_order_acq_rel)) {
             ++got;
             continue;
         }
-        busy = z != 2u || std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 0.1;
+        busy = (z & 0xff) != kGateRevoker ||
+               std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 0.1;
         _mm_pause();
     }
     bool ok = got == x->size && x->svc_ok;

@@ -558,14 +558,14 @@ int p2p_progress(mi355x_comm *c)
     P2P *p = p2p_of(c);
     std::lock_guard<std::recursive_mutex> g(p->mtx);
     // 1. announce queued sends, in order; a destination whose ring is full holds its later sends
-    std::vector<char> blocked((size_t)c->size, 0);
+    uint64_t blocked = 0;  // destinations whose ring is full (bit per rank; kMaxRanks = 64)
     for (auto it = p->queued.begin(); it != p->queued.end();) {
         mi355x_request *r = *it;
-        if (!blocked[(size_t)r->peer] && try_announce(c, r)) {
+        if (!((blocked >> r->peer) & 1u) && try_announce(c, r)) {
             p->sending.push_back(r);
             it = p->queued.erase(it);
         } else {
-            blocked[(size_t)r->peer] = 1;
+            blocked |= 1ull << r->peer;
             ++it;
         }
     }

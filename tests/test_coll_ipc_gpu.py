@@ -109,7 +109,7 @@ def test_done_words(gpu, size):
 def test_host_p2p_between_processes(gpu, stream_min):
     """host -> host sendrecv between two processes through the shared-memory arenas, 1-64 MiB,
     with the fragment pipeline (default) and with whole-message copy-in (off); exact both ways,
-    the rates printed (tools/gpu_r03_p2p.sh keeps them)"""
+    the rates printed (tools/gpu_run.sh host_p2p keeps them)"""
     extra = {} if stream_min == "default" else {"MI355X_P2P_STREAM_MIN": str(1 << 62)}
     if stream_min.startswith("frag"):
         extra = {"MI355X_P2P_STREAM_FRAG": stream_min[4:]}
