@@ -1742,8 +1742,9 @@ struct SelfTest {
     {
         std::vector<uint32_t> h(count);
         for (size_t i = 0; i < count; ++i) h[i] = st_val(seed + (uint64_t)t, c->rank, i);
+        // (the null stream only: the application's other streams are not waited for)
         return ok && count * 4 <= cap && hipMemcpy(in, h.data(), count * 4, hipMemcpyHostToDevice) == hipSuccess &&
-               hipMemset(out, 0xa5, cap) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+               hipMemsetAsync(out, 0xa5, cap, nullptr) == hipSuccess && hipStreamSynchronize(nullptr) == hipSuccess;
     }
     bool fetch(std::vector<uint32_t> &h, size_t count)
     {

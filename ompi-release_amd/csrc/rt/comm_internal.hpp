@@ -111,13 +111,17 @@ struct Ctrl {
 // FIN the receiver returns, pml_ob1_hdr.h:58-190, carried in shared memory as btl/smcuda's FIFOs
 // carry them, btl_smcuda_fifo.h).
 constexpr int kP2PSlots = 32;
+constexpr size_t kP2PInline = 128;  // payloads up to this size travel inside the envelope (p2p.cpp)
 struct alignas(64) Envelope {
     std::atomic<uint64_t> full;   // message number + 1 once posted (sender, release)
     std::atomic<uint64_t> done;   // message number + 1 once the receiver no longer reads it
     int32_t tag, flags;           // flags: kEnvPacked, kEnvHost (p2p.cpp)
     uint64_t bytes;               // packed size of the message
-    BufDesc buf;                  // where the (packed) bytes are: the sender's device export, or
+    union {
+        BufDesc buf;              // where the (packed) bytes are: the sender's device export, or
                                   // (kEnvHost) its host arena: id = segment generation, off = offset
+        unsigned char inl[sizeof(BufDesc)];  // (kEnvInline) the payload itself, <= kP2PInline bytes
+    };
 };
 inline size_t p2p_offset(int size)
 {
@@ -223,6 +227,7 @@ struct mi355x_request {
     void *hslot = nullptr;                // send: payload slot in the host shared-memory arena
     void *stage = nullptr;                // receive: device staging slot (host destination)
     std::vector<char> htmp;               // receive: host copy awaiting the host convertor
+    unsigned char inl[mi355x::kP2PInline]; // send: an inline payload until its envelope is posted
 };
 
 struct mi355x_comm {

@@ -56,6 +56,8 @@ constexpr size_t kEagerLimit = 4096;          // btl_sm_component.c:244, btl_smc
 constexpr int32_t kEnvPacked = 1;             // the payload is a packed copy (layout unused)
 constexpr int32_t kEnvHost = 2;               // the payload is in the sender's host arena
 constexpr int32_t kEnvStream = 4;             // ... and is being copied in: a StreamHdr precedes it
+constexpr int32_t kEnvInline = 8;             // the payload is inside the envelope (<= kP2PInline bytes)
+static_assert(sizeof(BufDesc) >= kP2PInline, "an inline payload fits the envelope's descriptor space");
 // host payloads of at least kStreamMin bytes are announced before they are copied into the arena
 // and copied in kStreamFrag fragments, the receiver copying fragment k out while the sender copies
 // k + 1 in (the sm BTL's fragment pipeline, btl_sm_sendi / mca_btl_sm_component_progress)
@@ -350,7 +352,8 @@ static bool try_announce(mi355x_comm *c, mi355x_request *r)
     env->tag = r->tag;
     env->flags = r->env_flags;
     env->bytes = r->bytes;
-    std::memcpy(&env->buf, &r->desc, sizeof(BufDesc));
+    if (r->env_flags & kEnvInline) std::memcpy(env->inl, r->inl, r->bytes);
+    else std::memcpy(&env->buf, &r->desc, sizeof(BufDesc));
     env->full.store(r->msg + 1, std::memory_order_release);
     r->env = env;
     return true;
@@ -430,11 +433,14 @@ static void start_read(mi355x_comm *c, P2P *p, mi355x_request *r, const P2PMsg &
     hipStream_t s = nullptr;
     int rc = MI355X_SUCCESS;
     // (the stream only where a kernel or an async copy runs: not for a host payload into host memory)
-    if ((!(env->flags & kEnvHost) || !r->host || !contig) && (rc = p2p_stream(c, p, &s))) return fail(rc);
-    if (env->flags & kEnvHost) {
-        // host payload (sm-BTL style): copied out synchronously, FIN at once
+    const bool hostpay = (env->flags & (kEnvHost | kEnvInline)) != 0;
+    if ((!hostpay || !r->host || !contig) && (rc = p2p_stream(c, p, &s))) return fail(rc);
+    if (hostpay) {
+        // host payload (sm-BTL style): copied out synchronously, FIN at once -- from the envelope
+        // itself (inline), or from the sender's host arena
         const char *src = nullptr;
-        if ((rc = host_src(c, p, msg.src, env->buf, &src))) return fail(rc);
+        if (env->flags & kEnvInline) src = reinterpret_cast<const char *>(env->inl);
+        else if ((rc = host_src(c, p, msg.src, env->buf, &src))) return fail(rc);
         if (env->flags & kEnvStream) {
             rc = read_stream(c, p, r, src, n, contig, dst, s);
             if (rc) return fail(rc);
@@ -750,6 +756,16 @@ static int isend(mi355x_comm *c, const void *buf, size_t count, const mi355x_ddt
     int64_t first = 0;
     const bool contig = !d || ddt_contiguous(d, count, &first);
     const char *ubuf = (const char *)buf + first;
+    if (bytes && bytes <= kP2PInline && contig && mode != MI355X_SEND_SYNCHRONOUS) {
+        // a few bytes (an MPI scalar, a small header): inside the envelope -- no arena slot, no
+        // export; the request holds them until the envelope is posted
+        if (!dev) std::memcpy(r->inl, ubuf, bytes);
+        else if (hipMemcpy(r->inl, ubuf, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+            return bail(set_error(MI355X_ERR_HIP, "device-to-host copy of a %zu-byte send failed", bytes));
+        r->env_flags = kEnvInline;
+        *out = post_send(c, p, r, eager);
+        return MI355X_SUCCESS;
+    }
     BufDesc desc;
     std::memset(&desc, 0, sizeof(desc));
     hipStream_t s = nullptr;
