@@ -118,6 +118,10 @@ int mi355x_comm_last_algorithm(const mi355x_comm_t *comm);
  * check that the next communicator on that GPU is admitted again (the token is reclaimed from a
  * dead process, coll_comm.cpp). */
 int mi355x_debug_pipe_token(mi355x_comm_t *comm, int acquire);
+/* Test hook (no GPU needed): the same holder protocol for device uid `dev_uid` on behalf of a
+ * communicator named `name` (op 1 take, 0 give back; returns 1 while held).  MI355X_TOKEN_TABLE=/name
+ * points a process at a private token table. */
+int mi355x_debug_token(uint64_t dev_uid, const char *name, int op);
 
 /* Knobs BLOCKS_PER_CU, PUSH, COPY_BLOCK_KIB, PIPE_WG_PER_CU, PIPE_CHUNK_KIB and PIPE_WT are launch
  * shapes shared by every communicator of the process (setting one through any communicator sets

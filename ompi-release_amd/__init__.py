@@ -127,6 +127,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "mi355x_comm_barrier": (i, [vp]),
         "mi355x_comm_last_algorithm": (i, [vp]),
         "mi355x_debug_pipe_token": (i, [vp, i]),
+        "mi355x_debug_token": (i, [c.c_uint64, c.c_char_p, i]),
         "mi355x_comm_set": (i, [vp, i, c.c_long]),
         "mi355x_comm_phase_ms": (i, [vp, c.POINTER(c.c_float), c.POINTER(c.c_float)]),
         "mi355x_comm_get": (i, [vp, i, c.POINTER(c.c_long)]),

@@ -2126,8 +2126,10 @@ static GpuTokens *gpu_tokens()
     static GpuTokens *t = nullptr;
     static std::once_flag once;
     std::call_once(once, [] {
-        char name[64];
+        char name[96];
         snprintf(name, sizeof(name), "/mi355x_gpu_tokens2_%u", (unsigned)getuid());
+        const char *alt = getenv("MI355X_TOKEN_TABLE");  // (tests: a private table)
+        if (alt && *alt == '/' && strlen(alt) < sizeof(name)) snprintf(name, sizeof(name), "%s", alt);
         const int fd = shm_open(name, O_CREAT | O_RDWR, 0600);
         if (fd < 0) return;
         struct stat st;
@@ -2844,6 +2846,27 @@ int mi355x_comm_vote(mi355x_comm_t *c, int device, int *any_device)
 }
 
 int mi355x_comm_last_algorithm(const mi355x_comm_t *c) { return c ? c->last_alg : -1; }
+
+// test hook without a GPU: the token table's holder protocol for a device uid, as a communicator
+// named `name` would use it (op 1: try to take it; 0: give it back).  Returns 1 while held.  The
+// CPU tests kill a holder process and check that the next process takes the token back.
+int mi355x_debug_token(uint64_t dev_uid, const char *name, int op)
+{
+    static std::mutex mtx;
+    static std::map<std::string, mi355x_comm *> comms;
+    if (!name) return set_error(MI355X_ERR_ARG, "name is NULL");
+    std::lock_guard<std::mutex> g(mtx);
+    mi355x_comm *&c = comms[name];
+    if (!c) {
+        c = new mi355x_comm();
+        c->ctrl = (Ctrl *)calloc(1, ctrl_bytes(1));
+        c->ctrl->slot[0].dev_uid = dev_uid;
+        c->shm_name = std::string("/mi355x_") + name;
+    }
+    if (op) return (c->pipe_entry >= 0 || pipe_token_acquire(c)) ? 1 : 0;
+    if (c->pipe_entry >= 0) pipe_token_release(c);
+    return 0;
+}
 
 // test hook: take (1) or give back (0) this communicator's pipelined-grid token of its GPU outside
 // any call, as a rank inside a pipelined allreduce holds it (tests kill a holder, then check that
