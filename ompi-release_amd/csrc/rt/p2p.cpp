@@ -113,9 +113,10 @@ struct HostSeg {
     size_t bytes;
     uint32_t gen;
     std::string name;
+    bool reg = false;  // registered with HIP (seg_register)
 };
 struct HostArena {
-    HostSeg cur{nullptr, 0, 0, std::string()};
+    HostSeg cur{nullptr, 0, 0, std::string(), false};
     size_t used = 0;
     int users = 0;
     std::vector<HostSeg> retired;
@@ -134,6 +135,7 @@ struct P2P {
     DevArena arena;                        // exportable: packed / buffered device payloads
     DevArena rstage;                       // receive side: device staging of host receives
     HostArena harena;                      // host payloads (shared memory)
+    char *bounce = nullptr;                // registered host bounce for an inline payload bound for the device
     std::map<std::pair<int, uint32_t>, HostSeg> peer_segs;  // peers' host arenas, mapped
 };
 
@@ -181,6 +183,7 @@ void p2p_destroy(mi355x_comm *c)
     }
     seg_drop(p->harena.cur, true);
     for (HostSeg &g : p->harena.retired) seg_drop(g, true);
+    if (p->bounce) (void)hipHostFree(p->bounce);
     for (auto &kv : p->peer_segs) seg_drop(kv.second, false);
     delete p;
     c->p2p = nullptr;
@@ -216,9 +219,23 @@ static void arena_release(DevArena &a)
     a.retired.clear();
 }
 
+// Host arenas are registered with HIP (pinned and GPU-mapped; the receiver's mapping read-only), so
+// a small device payload's device-to-host copy into the sender's slot and the receiver's
+// host-to-device copy out of it are one DMA each, not a staged copy through HIP's own pinned
+// buffer (MI355X_P2P_REGISTER=0 leaves them unregistered)
+static void seg_register(HostSeg &g, bool readonly)
+{
+    static const bool on = !(getenv("MI355X_P2P_REGISTER") && atoi(getenv("MI355X_P2P_REGISTER")) == 0);
+    if (!on || !g.base) return;
+    g.reg = hipHostRegister(g.base, g.bytes, readonly ? hipHostRegisterReadOnly : hipHostRegisterDefault) == hipSuccess;
+    if (!g.reg) (void)hipGetLastError();
+}
+
 static void seg_drop(HostSeg &g, bool owner)
 {
     if (!g.base) return;
+    if (g.reg) (void)hipHostUnregister(g.base);
+    g.reg = false;
     munmap(g.base, g.bytes);
     if (owner && !g.name.empty()) shm_unlink(g.name.c_str());
     g.base = nullptr;
@@ -241,7 +258,7 @@ static int harena_alloc(mi355x_comm *c, P2P *p, size_t bytes, void **out, BufDes
         }
         size_t want = std::max<size_t>((size_t)1 << 20, h.cur.bytes * 2);
         while (want < need) want *= 2;
-        HostSeg g{nullptr, want, h.cur.gen + 1, std::string()};
+        HostSeg g{nullptr, want, h.cur.gen + 1, std::string(), false};
         if (c->loopback) {  // threads of one process: plain memory, read through the pointer
             void *m = mmap(nullptr, want, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
             if (m == MAP_FAILED) return set_error(MI355X_ERR_NOMEM, "host arena of %zu bytes", want);
@@ -258,6 +275,7 @@ static int harena_alloc(mi355x_comm *c, P2P *p, size_t bytes, void **out, BufDes
                 return set_error(MI355X_ERR_NOMEM, "host arena %s of %zu bytes", g.name.c_str(), want);
             }
             g.base = (char *)m;
+            seg_register(g, false);
         }
         h.cur = g;
         h.used = 0;
@@ -304,7 +322,7 @@ static int host_src(mi355x_comm *c, P2P *p, int src, const BufDesc &d, const cha
                 ++j;
             }
         }
-        HostSeg g{nullptr, 0, gen, seg_name(c, src, gen)};
+        HostSeg g{nullptr, 0, gen, seg_name(c, src, gen), false};
         const int fd = shm_open(g.name.c_str(), O_RDONLY, 0600);
         if (fd < 0) return set_error(MI355X_ERR_PEER, "host arena %s of rank %d: %s", g.name.c_str(), src, strerror(errno));
         struct stat st;
@@ -317,6 +335,7 @@ static int host_src(mi355x_comm *c, P2P *p, int src, const BufDesc &d, const cha
         if (m == MAP_FAILED) return set_error(MI355X_ERR_PEER, "mapping host arena %s failed", g.name.c_str());
         g.base = (char *)m;
         g.name.clear();  // not ours to unlink
+        seg_register(g, true);
         it = p->peer_segs.emplace(std::make_pair(src, gen), g).first;
     }
     if (d.off > it->second.bytes) return set_error(MI355X_ERR_PEER, "host payload outside rank %d's arena", src);
@@ -439,8 +458,21 @@ static void start_read(mi355x_comm *c, P2P *p, mi355x_request *r, const P2PMsg &
         // host payload (sm-BTL style): copied out synchronously, FIN at once -- from the envelope
         // itself (inline), or from the sender's host arena
         const char *src = nullptr;
-        if (env->flags & kEnvInline) src = reinterpret_cast<const char *>(env->inl);
-        else if ((rc = host_src(c, p, msg.src, env->buf, &src))) return fail(rc);
+        if (env->flags & kEnvInline) {
+            src = reinterpret_cast<const char *>(env->inl);
+            if (!r->host) {  // bound for the device: through a registered bounce (one DMA)
+                if (!p->bounce && hipHostMalloc((void **)&p->bounce, kP2PInline, hipHostMallocDefault) != hipSuccess) {
+                    p->bounce = nullptr;
+                    (void)hipGetLastError();
+                }
+                if (p->bounce) {
+                    std::memcpy(p->bounce, src, std::min<size_t>(n, kP2PInline));
+                    src = p->bounce;
+                }
+            }
+        } else if ((rc = host_src(c, p, msg.src, env->buf, &src))) {
+            return fail(rc);
+        }
         if (env->flags & kEnvStream) {
             rc = read_stream(c, p, r, src, n, contig, dst, s);
             if (rc) return fail(rc);
@@ -756,12 +788,11 @@ static int isend(mi355x_comm *c, const void *buf, size_t count, const mi355x_ddt
     int64_t first = 0;
     const bool contig = !d || ddt_contiguous(d, count, &first);
     const char *ubuf = (const char *)buf + first;
-    if (bytes && bytes <= kP2PInline && contig && mode != MI355X_SEND_SYNCHRONOUS) {
-        // a few bytes (an MPI scalar, a small header): inside the envelope -- no arena slot, no
-        // export; the request holds them until the envelope is posted
-        if (!dev) std::memcpy(r->inl, ubuf, bytes);
-        else if (hipMemcpy(r->inl, ubuf, bytes, hipMemcpyDeviceToHost) != hipSuccess)
-            return bail(set_error(MI355X_ERR_HIP, "device-to-host copy of a %zu-byte send failed", bytes));
+    if (!dev && bytes && bytes <= kP2PInline && contig && mode != MI355X_SEND_SYNCHRONOUS) {
+        // a few host bytes (an MPI scalar, a small header): inside the envelope -- no arena slot,
+        // no export; the request holds them until the envelope is posted.  (A device payload goes
+        // to the registered arena: one DMA into pinned memory beats a staged copy into the heap.)
+        std::memcpy(r->inl, ubuf, bytes);
         r->env_flags = kEnvInline;
         *out = post_send(c, p, r, eager);
         return MI355X_SUCCESS;
