@@ -2029,6 +2029,12 @@ static void svc_setup(mi355x_comm *c)
     c->svc_retry = (uint64_t)std::max(1.0, env_double("MI355X_SVC_RETRY_CALLS", (double)c->svc_retry));
     const char *env = getenv("MI355X_SVC");
     c->svc_want = c->ll_ok && c->size <= kLLMaxRanks && !c->loopback && !(env && atoi(env) == 0);
+    const int prep = (int)env_double("MI355X_SVC_PREP", 0.0);
+    if (prep & 4) {
+        std::lock_guard<std::mutex> g(g_svc_mtx);
+        if (!g_svc_res[c->device].q && svc_attach(c)) svc_detach(c);  // the resources, now
+    }
+    if (prep & ~4) (void)svc_prep(c->device, prep);
 }
 
 // ----------------------------------------------------------------- pipelined allreduce

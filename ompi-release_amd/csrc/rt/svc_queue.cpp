@@ -131,6 +131,32 @@ int fail(std::string *why, const char *what)
 
 } // namespace
 
+// (experiment, MI355X_SVC_PREP) parts of the service's creation on their own, kept for the process
+int svc_prep(int device, int mask)
+{
+    if (mask & 1) (void)hsa_init();
+    if (mask & 2) (void)svc_probe_launch(device);
+    if (mask & (8 | 16)) {
+        (void)hsa_init();
+        int bus = 0, dev = 0, dom = 0;
+        (void)hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device);
+        (void)hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device);
+        (void)hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, device);
+        AgentFind af{(uint32_t)((bus << 8) | (dev << 3)), (uint32_t)dom, {0}, false};
+        (void)hsa_iterate_agents(find_agent, &af);
+        if (!af.found) return -1;
+        if (mask & 8) {
+            hsa_queue_t *hq = nullptr;
+            (void)hsa_queue_create(af.agent, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &hq);
+        }
+        if (mask & 16) {
+            hsa_signal_t sig;
+            (void)hsa_signal_create(0, 0, nullptr, &sig);
+        }
+    }
+    return 0;
+}
+
 int svc_queue_create(int device, SvcQueue *q, std::string *why)
 {
     std::memset(static_cast<void *>(q), 0, sizeof(*q));

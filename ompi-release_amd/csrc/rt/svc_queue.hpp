@@ -21,6 +21,7 @@ struct SvcQueue {
 // one HIP launch of the service kernel that returns at once (coll_svc.hip): HIP then has the
 // code object loaded on `device`
 int svc_probe_launch(int device);
+int svc_prep(int device, int mask);  // (experiment: parts of the service's creation alone)
 // 0 on success; on failure `why` names the step (the service then stays off)
 int svc_queue_create(int device, SvcQueue *q, std::string *why);
 // dispatch nwg workgroups of the service; -1 if the previous launch is still resident

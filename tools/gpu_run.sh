@@ -24,6 +24,7 @@
 #   host_p2p       host -> host point-to-point rates between two processes -> host_p2p.log
 #   p2p_lat        point-to-point ping-pong latency, host and device buffers, 8 B - 64 KiB -> p2p_lat.jsonl
 #   interference   the resident service beside compute streams (tools/svc_interference.py) -> svc_interference.jsonl
+#   ab_host        host-synchronised small-call latency, this tree vs a build staged in ab_old/ (A/B)
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -58,7 +59,7 @@ for step in "$@"; do
         run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
         tail -2 $O/smoke.log ;;
     tests)
-        run pytest_sel 1000 $PYT ${TESTS:-tests} ${K:+-k "$K"}
+        run pytest_sel 1000 $PYT -rP ${TESTS:-tests} ${K:+-k "$K"}
         grep -E "PASSED|FAILED|SKIPPED|ERROR|passed|failed" $O/pytest_sel.log | tail -40 ;;
     smoke)
         run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
@@ -138,6 +139,37 @@ for step in "$@"; do
         done
         run p2p_lat_py 300 python tools/p2p_latency.py --out $O/p2p_lat.jsonl
         grep python $O/p2p_lat.jsonl ;;
+    ab_host)  # host-synchronised small-call latency: this tree vs the build in ab_old/ (if present)
+        for n in 2 4; do
+            for coll in allgather allreduce; do
+                SMALL_COLL=$coll SMALL_SIZES=16384,65536 MI355X_SVC_PULL_COPY_MAX_BYTES=0 MI355X_SVC_PULL_MAX_BYTES=0 \
+                    small_c $n 1000 host host_new
+                SMALL_COLL=$coll SMALL_SIZES=16384,65536 MI355X_SVC_PULL_COPY_MAX_BYTES=0 MI355X_SVC_PULL_MAX_BYTES=0 \
+                    MI355X_SELFTEST=0 small_c $n 1000 host host_new_noselftest
+                if [ -x ab_old/small_ar_c_old ]; then
+                    SMALL_COLL=$coll SMALL_SIZES=16384,65536 MI355X_SVC_PULL_COPY_MAX_BYTES=0 MI355X_SVC_PULL_MAX_BYTES=0 \
+                        timeout -k 10 200 ./ab_old/small_ar_c_old $n 1000 host > $O/small_one.log 2>&1 || { cat $O/small_one.log; exit 1; }
+                    grep us_per_call $O/small_one.log | sed 's/^{/{"tag": "host_old", /' | tee -a $O/small.jsonl
+                fi
+            done
+        done ;;
+    ab_prep)  # the 4-process host-flow latency vs parts of the service's creation done at creation
+        for prep in 0 1 2 8 16 4 27; do
+            MI355X_SVC_PREP=$prep SMALL_COLL=allgather SMALL_SIZES=16384 MI355X_SVC_PULL_COPY_MAX_BYTES=0 \
+                timeout -k 10 200 ./tools/build/small_ar_c 4 1000 host > $O/small_one.log 2>&1 || { cat $O/small_one.log; exit 1; }
+            grep us_per_call $O/small_one.log | sed "s/^{/{\"svc_prep\": $prep, /" | tee -a $O/small.jsonl
+        done ;;
+    ab_host4)  # the 4-process host-flow latency: which setting matters (service / pipelined flow off)
+        for env in "" MI355X_SVC=0 MI355X_PIPE=0 "MI355X_SVC=0 MI355X_PIPE=0"; do
+            tag=$(echo "new ${env:-default}" | tr ' =' '__')
+            env $env SMALL_COLL=allgather SMALL_SIZES=16384 MI355X_SVC_PULL_COPY_MAX_BYTES=0 \
+                timeout -k 10 200 ./tools/build/small_ar_c 4 1000 host > $O/small_one.log 2>&1 || { cat $O/small_one.log; exit 1; }
+            grep us_per_call $O/small_one.log | sed "s/^{/{\"tag\": \"$tag\", /" | tee -a $O/small.jsonl
+            tag=$(echo "old ${env:-default}" | tr ' =' '__')
+            env $env SMALL_COLL=allgather SMALL_SIZES=16384 MI355X_SVC_PULL_COPY_MAX_BYTES=0 \
+                timeout -k 10 200 ./ab_old/small_ar_c_old 4 1000 host > $O/small_one.log 2>&1 || { cat $O/small_one.log; exit 1; }
+            grep us_per_call $O/small_one.log | sed "s/^{/{\"tag\": \"$tag\", /" | tee -a $O/small.jsonl
+        done ;;
     interference)
         run interference 600 python tools/svc_interference.py --out $O/svc_interference.jsonl
         cat $O/svc_interference.jsonl ;;

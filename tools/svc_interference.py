@@ -51,17 +51,39 @@ def rank_main(rank, key, intervals, window_ms):
         else:
             torch.matmul(a, b, out=outs[i])
 
-    # kernels per stream for a window of ~window_ms (calibrated once, no allreduce)
-    t0 = time.perf_counter()
-    for k in range(20):
+    # kernels per stream for a window of ~window_ms: warm the kernels up (library initialisation),
+    # then time whole rounds (one kernel on every stream) with the device synchronised
+    for k in range(6):
         for i, st in enumerate(streams):
             with torch.cuda.stream(st):
                 one_kernel(i, k)
     torch.cuda.synchronize()
-    per_kernel_ms = (time.perf_counter() - t0) * 1e3 / 20
-    nk = max(20, int(window_ms / per_kernel_ms))
+    t0 = time.perf_counter()
+    for k in range(10):
+        for i, st in enumerate(streams):
+            with torch.cuda.stream(st):
+                one_kernel(i, k)
+    torch.cuda.synchronize()
+    per_round_ms = (time.perf_counter() - t0) * 1e3 / 10
+    nk = max(20, int(window_ms / per_round_ms))
+
+    def ar_loop(interval, n_ar):
+        lat = []
+        comm.barrier()  # both ranks start their schedules together
+        tstart = time.perf_counter()
+        for j in range(n_ar):
+            target = tstart + j * interval * 1e-6
+            while time.perf_counter() < target:
+                pass
+            t1 = time.perf_counter()
+            comm.allreduce(x.data_ptr(), y.data_ptr(), 2, f32, SUM)
+            lat.append((time.perf_counter() - t1) * 1e6)
+        return lat, (time.perf_counter() - tstart) * 1e3
+
     rows = []
     for interval in [0] + intervals:  # 0: no allreduce (the compute baseline)
+        n_ar = int(0.8 * window_ms * 1e3 / interval) if interval else 0
+        alone = ar_loop(interval, min(n_ar, 2000))[0] if interval else []  # the same calls, no compute
         comm.barrier()
         ev = []
         for i, st in enumerate(streams):
@@ -72,27 +94,17 @@ def rank_main(rank, key, intervals, window_ms):
                     one_kernel(i, k)
                 e1.record(st)
             ev.append((e0, e1))
-        lat = []
-        if interval:
-            n_ar = int(window_ms * 1e3 / interval)
-            tstart = time.perf_counter()
-            for j in range(n_ar):
-                target = tstart + j * interval * 1e-6
-                while time.perf_counter() < target:
-                    pass
-                t1 = time.perf_counter()
-                comm.allreduce(x.data_ptr(), y.data_ptr(), 2, f32, SUM)
-                lat.append((time.perf_counter() - t1) * 1e6)
+        lat, loop_ms = ar_loop(interval, n_ar) if interval else ([], 0.0)
         torch.cuda.synchronize()
         assert float(y[0].item()) == 2.0 or not interval
         spans = [e0.elapsed_time(e1) for e0, e1 in ev]
-        # the streams' common span: from the earliest start to the latest end
         first = ev[0][0]
         span = max(first.elapsed_time(e1) for _, e1 in ev) - min(first.elapsed_time(e0) for e0, _ in ev)
-        rows.append({"interval_us": interval, "kernels": 4 * nk, "span_ms": round(span, 3),
+        rows.append({"interval_us": interval, "kernels": 4 * nk, "span_ms": round(span, 3), "ar_loop_ms": round(loop_ms, 3),
                      "kernels_per_s": round(4 * nk / span * 1e3, 1), "stream_ms": [round(s_, 2) for s_ in spans],
                      "ar_calls": len(lat), "ar_us_median": round(float(np.median(lat)), 2) if lat else None,
                      "ar_us_p90": round(float(np.percentile(lat, 90)), 2) if lat else None,
+                     "ar_us_median_no_compute": round(float(np.median(alone)), 2) if alone else None,
                      "svc_launches": comm.get("SVC_LAUNCHES"), "svc_calls": comm.get("SVC_CALLS")})
     comm.barrier()
     comm.destroy()
@@ -112,7 +124,7 @@ def main():
     ap.add_argument("--rank", type=int, default=-1)
     ap.add_argument("--key", default="")
     ap.add_argument("--intervals", default="50,200,500")
-    ap.add_argument("--window-ms", type=float, default=300.0)
+    ap.add_argument("--window-ms", type=float, default=400.0)
     ap.add_argument("--variants", default="svc_off,idle_0.1ms,idle_1ms,idle_5ms")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
