@@ -2029,11 +2029,18 @@ static void svc_setup(mi355x_comm *c)
     c->svc_retry = (uint64_t)std::max(1.0, env_double("MI355X_SVC_RETRY_CALLS", (double)c->svc_retry));
     const char *env = getenv("MI355X_SVC");
     c->svc_want = c->ll_ok && c->size <= kLLMaxRanks && !c->loopback && !(env && atoi(env) == 0);
-    const int prep = (int)env_double("MI355X_SVC_PREP", 0.0);
-    if (prep & 4) {
+    // The service's resources (its HSA queue above all) are created now, not at the first claim:
+    // an idle HSA queue in the process changes how the GPU schedules the HIP queues of several
+    // processes sharing it -- the host-synchronised small allreduce / allgather of 4 ranks on one
+    // GPU takes 20 us with it and 55 us without (profiles/r04_host_flow_idle_queue.jsonl: the
+    // queue alone, without any dispatch, makes the difference; hsa_init, a probe launch or a signal
+    // alone do not).  MI355X_SVC_EAGER=0 defers them to the first claim; MI355X_SVC_PREP=<mask>
+    // repeats the experiment (1 hsa_init, 2 probe launch, 8 a bare queue, 16 a signal).
+    if (c->svc_want && env_double("MI355X_SVC_EAGER", 1.0) != 0.0) {
         std::lock_guard<std::mutex> g(g_svc_mtx);
-        if (!g_svc_res[c->device].q && svc_attach(c)) svc_detach(c);  // the resources, now
+        if (!g_svc_res[c->device].q && svc_attach(c)) svc_detach(c);
     }
+    const int prep = (int)env_double("MI355X_SVC_PREP", 0.0);
     if (prep & ~4) (void)svc_prep(c->device, prep);
 }
 
@@ -2209,14 +2216,18 @@ static bool pipe_token_acquire(mi355x_comm *c)
     t->h[i][e].who.store(pid, std::memory_order_release);
     std::atomic<uint64_t> &w = t->word[i];
     uint64_t cur = w.load(std::memory_order_acquire);
-    bool reclaimed = false;
-    for (;;) {
+    for (int looks = 0;;) {
         const uint64_t holder = cur >> 32, cnt = cur & 0xff, gen = (cur >> 8) & 0xffffff;
         if (cnt != 0 && holder != c->pipe_holder) {
-            if (!reclaimed && pipe_token_reclaim(t, i, cur)) {
-                reclaimed = true;
-                cur = w.load(std::memory_order_acquire);
-                continue;
+            // held by another communicator: take it back if its holders are all dead; if the word
+            // changed meanwhile (a peer rank of mine reclaimed it first, or counted up), look again
+            if (looks++ < 8) {
+                const bool took = pipe_token_reclaim(t, i, cur);
+                const uint64_t now = w.load(std::memory_order_acquire);
+                if (took || now != cur) {
+                    cur = now;
+                    continue;
+                }
             }
             break;
         }

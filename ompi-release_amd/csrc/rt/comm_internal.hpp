@@ -216,6 +216,7 @@ struct mi355x_request {
     mi355x::Envelope *env = nullptr;      // the envelope in flight
     void *packed = nullptr;               // send: copy in the device arena (packed layout / buffered)
     mi355x::PeerMap *pin = nullptr;       // receive: the pinned mapping being read
+    void *hpin = nullptr;                 // receive: the peer host-arena segment a copy kernel reads (p2p.cpp)
     int st_source = 0, st_tag = 0, st_error = 0;
     size_t st_bytes = 0;
     int mode = 4;                         // send mode (MI355X_SEND_*; 4 standard)

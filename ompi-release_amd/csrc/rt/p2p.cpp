@@ -114,6 +114,8 @@ struct HostSeg {
     uint32_t gen;
     std::string name;
     bool reg = false;  // registered with HIP (seg_register)
+    char *dbase = nullptr;  // its device-side address (registered and mapped), else null
+    int pins = 0;           // (a peer's segment) copy kernels still reading it: never unmapped meanwhile
 };
 struct HostArena {
     HostSeg cur{nullptr, 0, 0, std::string(), false};
@@ -171,7 +173,7 @@ void p2p_destroy(mi355x_comm *c)
         (void)hipStreamDestroy(p->stream);
     }
     for (mi355x_request *r : p->reading)
-        if (r->pin) r->pin->pins--;
+        if (r->pin) r->pin->pins--;  // (the stream was synchronised above: nothing reads any more)
     // sends the engine owns (eager / buffered) that never saw their FIN
     for (mi355x_request *r : p->queued)
         if (r->internal) delete r;
@@ -227,8 +229,11 @@ static void seg_register(HostSeg &g, bool readonly)
 {
     static const bool on = !(getenv("MI355X_P2P_REGISTER") && atoi(getenv("MI355X_P2P_REGISTER")) == 0);
     if (!on || !g.base) return;
-    g.reg = hipHostRegister(g.base, g.bytes, readonly ? hipHostRegisterReadOnly : hipHostRegisterDefault) == hipSuccess;
-    if (!g.reg) (void)hipGetLastError();
+    const unsigned flags = hipHostRegisterMapped | (readonly ? hipHostRegisterReadOnly : 0u);
+    g.reg = hipHostRegister(g.base, g.bytes, flags) == hipSuccess;
+    void *d = nullptr;
+    if (g.reg && hipHostGetDevicePointer(&d, g.base, 0) == hipSuccess) g.dbase = static_cast<char *>(d);
+    (void)hipGetLastError();
 }
 
 static void seg_drop(HostSeg &g, bool owner)
@@ -236,6 +241,7 @@ static void seg_drop(HostSeg &g, bool owner)
     if (!g.base) return;
     if (g.reg) (void)hipHostUnregister(g.base);
     g.reg = false;
+    g.dbase = nullptr;
     munmap(g.base, g.bytes);
     if (owner && !g.name.empty()) shm_unlink(g.name.c_str());
     g.base = nullptr;
@@ -305,8 +311,11 @@ static void harena_release(P2P *p)
 // segment of that generation, mapped once (older generations of that peer are unmapped: their
 // slots were read synchronously, and a message still pending keeps its segment alive on the
 // sender's side, so it can be mapped again by name)
-static int host_src(mi355x_comm *c, P2P *p, int src, const BufDesc &d, const char **out)
+static int host_src(mi355x_comm *c, P2P *p, int src, const BufDesc &d, const char **out, const char **dev_out = nullptr,
+                    HostSeg **seg = nullptr)
 {
+    if (dev_out) *dev_out = nullptr;
+    if (seg) *seg = nullptr;
     if (c->loopback || src == c->rank) {
         *out = (const char *)(uintptr_t)d.raw;
         return MI355X_SUCCESS;
@@ -315,7 +324,7 @@ static int host_src(mi355x_comm *c, P2P *p, int src, const BufDesc &d, const cha
     auto it = p->peer_segs.find({src, gen});
     if (it == p->peer_segs.end()) {
         for (auto j = p->peer_segs.begin(); j != p->peer_segs.end();) {
-            if (j->first.first == src && j->first.second < gen) {
+            if (j->first.first == src && j->first.second < gen && j->second.pins == 0) {
                 seg_drop(j->second, false);
                 j = p->peer_segs.erase(j);
             } else {
@@ -340,6 +349,8 @@ static int host_src(mi355x_comm *c, P2P *p, int src, const BufDesc &d, const cha
     }
     if (d.off > it->second.bytes) return set_error(MI355X_ERR_PEER, "host payload outside rank %d's arena", src);
     *out = it->second.base + d.off;
+    if (dev_out && it->second.dbase) *dev_out = it->second.dbase + d.off;  // the same bytes, device-mapped
+    if (seg) *seg = &it->second;
     return MI355X_SUCCESS;
 }
 
@@ -470,8 +481,35 @@ static void start_read(mi355x_comm *c, P2P *p, mi355x_request *r, const P2PMsg &
                     src = p->bounce;
                 }
             }
-        } else if ((rc = host_src(c, p, msg.src, env->buf, &src))) {
-            return fail(rc);
+        } else {
+            const char *dsrc = nullptr;
+            HostSeg *seg = nullptr;
+            if ((rc = host_src(c, p, msg.src, env->buf, &src, &dsrc, &seg))) return fail(rc);
+            if (dsrc && !r->host && contig && !(env->flags & kEnvStream)) {
+                // into device memory from the registered, device-mapped arena: one copy kernel on
+                // the point-to-point stream, completed (and FINed) by progress like a device pull
+                MultiCopyArgs m;
+                std::memset(&m, 0, sizeof(m));
+                m.src[0] = dsrc;
+                m.dst[0] = dst;
+                m.len[0] = n;
+                m.nseg = 1;
+                rc = launch_multicopy(m, s);
+                if (!rc && !r->ev && hipEventCreateWithFlags(&r->ev, hipEventDisableTiming) != hipSuccess)
+                    rc = set_error(MI355X_ERR_HIP, "hipEventCreate failed");
+                if (!rc && hipEventRecord(r->ev, s) != hipSuccess)
+                    rc = set_error(MI355X_ERR_HIP, "hipEventRecord on the point-to-point stream failed");
+                if (rc) {
+                    (void)hipStreamSynchronize(s);
+                    return fail(rc);
+                }
+                if (seg) {
+                    seg->pins++;
+                    r->hpin = seg;
+                }
+                p->reading.push_back(r);
+                return;
+            }
         }
         if (env->flags & kEnvStream) {
             rc = read_stream(c, p, r, src, n, contig, dst, s);
@@ -633,6 +671,10 @@ int p2p_progress(mi355x_comm *c)
         if (r->pin) {
             r->pin->pins--;
             r->pin = nullptr;
+        }
+        if (r->hpin) {
+            static_cast<HostSeg *>(r->hpin)->pins--;
+            r->hpin = nullptr;
         }
         if (r->stage) {
             arena_release(p->rstage);
@@ -810,8 +852,22 @@ static int isend(mi355x_comm *c, const void *buf, size_t count, const mi355x_ddt
             if (contig) std::memcpy(slot, ubuf, bytes);
             else if ((rc = mi355x_pack_host(d, count, buf, 0, slot, bytes))) return bail(rc);
         } else if (contig) {
-            if (hipMemcpy(slot, ubuf, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+            // the copy kernel writes the registered slot through its device mapping: one launch on
+            // the point-to-point stream (a DMA-engine copy costs more than a launch for a few KiB)
+            char *dslot = p->harena.cur.dbase ? p->harena.cur.dbase + desc.off : nullptr;
+            if (dslot && !(rc = p2p_stream(c, p, &s))) {
+                MultiCopyArgs m;
+                std::memset(&m, 0, sizeof(m));
+                m.src[0] = ubuf;
+                m.dst[0] = dslot;
+                m.len[0] = bytes;
+                m.nseg = 1;
+                rc = launch_multicopy(m, s);
+                if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = set_error(MI355X_ERR_HIP, "device-to-host copy failed");
+                if (rc) return bail(rc);
+            } else if (hipMemcpy(slot, ubuf, bytes, hipMemcpyDeviceToHost) != hipSuccess) {
                 return bail(set_error(MI355X_ERR_HIP, "device-to-host copy of a %zu-byte send failed", bytes));
+            }
         } else {
             void *tmp = nullptr;
             if ((rc = p2p_stream(c, p, &s)) || (rc = arena_alloc(p->arena, bytes, &tmp))) return bail(rc);
