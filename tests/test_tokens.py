@@ -131,3 +131,23 @@ def test_release_frees_for_others(table):
     err = _finish(b)
     assert "reclaimed" not in err
     _finish(a)
+
+
+def test_ranks_of_one_communicator_race_to_reclaim(table):
+    """after the holder dies, several ranks of the next communicator try at once: one of them takes
+    the token back, the others count up behind it -- none is refused (a rank that lost the race to
+    reclaim must look at the token again, not give up)"""
+    uid = 0x5eed0005
+    for _ in range(5):
+        a, st = _spawn(uid, "commA")
+        assert st == "held"
+        a.send_signal(signal.SIGKILL)
+        a.wait(30)
+        ranks = [subprocess.Popen([sys.executable, "-c", CHILD.format(repo=str(REPO)), str(uid), "commB"],
+                                  stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                 for _ in range(4)]
+        states = [p.stdout.readline().strip() for p in ranks]
+        assert states == ["held"] * 4, states
+        for p in ranks:
+            assert _cmd(p, "release") == "released"
+            _finish(p)
