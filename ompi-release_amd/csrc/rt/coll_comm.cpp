@@ -1962,6 +1962,7 @@ static int svc_claim(mi355x_comm *c)
         auto it = g_svc_owner.find(c->device);
         const bool free_ = it == g_svc_owner.end() || it->second == c;
         if (free_ || svc_revoke(it->second)) {
+            if (it != g_svc_owner.end()) g_svc_owner.erase(it);  // (a revoked owner is no owner any more)
             if (!svc_attach(c)) {
                 mine = 3;
             } else {
