@@ -128,11 +128,24 @@ def bench_op(args, pkg, torch):
     # event pair around every launch would add ~7 us per step to the wall clock (0.500 vs 0.493 ms,
     # tools/ev_probe.py) and slow the bracketed launches themselves by ~1 %.
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    graph = None
+    if args.graph:
+        # --graph: the K launches captured once into a HIP graph (one kernel node per step, every
+        # step the full 1 GiB reduction) and replayed as one submission in the timed region
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            gs = torch.cuda.current_stream().cuda_stream
+            for _ in range(args.steps):
+                pkg.op_reduce_3buff(op, ty, pa, pb, po, n, gs)
+        graph.replay()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     e0.record(s)
-    for _ in range(args.steps):
-        pkg.op_reduce_3buff(op, ty, pa, pb, po, n, sh)
+    if graph is not None:
+        graph.replay()
+    else:
+        for _ in range(args.steps):
+            pkg.op_reduce_3buff(op, ty, pa, pb, po, n, sh)
     e1.record(s)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -160,7 +173,8 @@ def bench_op(args, pkg, torch):
                                                                       "nontemporal": nt}},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_from": traffic_from,
-                     "kernel_avg_ms": round(avg_ms, 5), "kernel_avg_from": "HIP events around the K launches / K",
+                     "kernel_avg_ms": round(avg_ms, 5),
+                     "kernel_avg_from": "HIP events around the K launches / K" + (" (one HIP graph replay)" if graph is not None else ""),
                      "alg_bytes_per_launch": alg_bytes},
     }
 
@@ -199,6 +213,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="N = 1: replay the K timed launches as one HIP graph")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-legs", action="store_true", help="N > 1: skip the other configs' legs")
     ap.add_argument("--no-autotune", action="store_true",

@@ -68,6 +68,14 @@ for step in "$@"; do
         run bench_n1 300 python bench.py --steps ${STEPS:-20} --warmup ${WARM:-5}
         grep '^{' $O/bench_n1.log | tail -1 > $O/bench_n1.json
         cut -c1-600 $O/bench_n1.json ;;
+    bench_ab)  # N = 1: the K timed launches issued one by one vs replayed as one HIP graph, alternated
+        for i in 1 2 3; do
+            for g in "" --graph; do
+                timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup ${WARM:-5} --no-cpu-baseline $g > $O/bench_ab.log 2>&1 \
+                    || { tail -20 $O/bench_ab.log; exit 1; }
+                grep '^{' $O/bench_ab.log | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'graph': '$g' != '', 'value': d['value'], 'ms_per_step': d['ms_per_step'], 'frac': d['roofline']['frac'], 'kernel_avg_ms': d['roofline']['kernel_avg_ms']}))" | tee -a $O/bench_ab.jsonl
+            done
+        done ;;
     prof_bench)
         run prof_bench 300 rocprofv3 --kernel-trace --stats -d $O/prof_bench -o run --output-format csv -- \
             python bench.py --steps 20 --warmup 5 --no-cpu-baseline
