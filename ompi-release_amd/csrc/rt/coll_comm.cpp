@@ -1475,8 +1475,9 @@ static void svc_trace_report(mi355x_comm *c)
 }
 
 // The service's resources -- its HSA queue, doorbell page and host words -- exist once per process
-// and GPU: created at the first claim on that GPU, shared by the communicators that own the service
-// in turn (a handover creates no queue), freed with the last communicator that used them.
+// and GPU: created with the first communicator that may use the service (svc_setup; an idle queue
+// also keeps the host flows of ranks sharing a GPU fast), shared by the communicators that own the
+// service in turn (a handover creates no queue), freed with the last communicator attached.
 struct SvcRes {
     SvcQueue *q = nullptr;
     SvcPage *page = nullptr;
@@ -1487,7 +1488,7 @@ struct SvcRes {
 };
 static std::map<int, SvcRes> g_svc_res;  // device -> resources (g_svc_mtx)
 
-// (g_svc_mtx held) this communicator's view of the process's service resources, created on first use
+// (g_svc_mtx held) this communicator's view of the process's service resources (created if needed)
 static bool svc_attach(mi355x_comm *c)
 {
     SvcRes &r = g_svc_res[c->device];
