@@ -219,7 +219,10 @@ enum mi355x_knob {
                                            service flows' self-test at the service's first claim */
     MI355X_KNOB_SVC_OWNER = 33,         /* (read-only) 1 while this communicator owns its process's
                                            resident service */
-    MI355X_KNOB_SVC_CLAIMS = 34         /* (read-only) times this communicator has taken the service */
+    MI355X_KNOB_SVC_CLAIMS = 34,        /* (read-only) times this communicator has taken the service */
+    MI355X_KNOB_SVC_IDLE_US = 35        /* (per communicator, same value on every rank; env MI355X_SVC_IDLE_MS at
+                                           creation, default 1000) microseconds the resident service stays
+                                           without a call before it leaves (applies from its next launch) */
 };
 /* cross-device flows (MI355X_KNOB_FLOWS) */
 enum mi355x_flow {

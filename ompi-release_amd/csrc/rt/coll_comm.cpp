@@ -2931,6 +2931,7 @@ int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
     case MI355X_KNOB_SELFTEST_US: *value = (long)c->selftest_us; break;
     case MI355X_KNOB_SVC_OWNER: *value = c->svc_ok ? 1 : 0; break;
     case MI355X_KNOB_SVC_CLAIMS: *value = (long)c->svc_epoch; break;
+    case MI355X_KNOB_SVC_IDLE_US: *value = (long)(c->svc_idle_s * 1e6 + 0.5); break;
     case MI355X_KNOB_RCACHE_MAX_MAPS: *value = (long)c->rcache_max_maps; break;
     case MI355X_KNOB_RCACHE_SIZE_LIMIT: *value = (long)c->rcache_limit; break;
     case MI355X_KNOB_PEER_MAPS: {
@@ -3033,6 +3034,16 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
         rcache_trim(c, nullptr);
         break;
     }
+    case MI355X_KNOB_SVC_IDLE_US:
+        if (value < 100 || value > 60000000) return set_error(MI355X_ERR_ARG, "svc_idle_us out of range");
+        drain(c);
+        c->svc_idle_s = (double)value * 1e-6;
+        {  // a resident service picks the new limit up at its next launch (g_svc_mtx: not while a
+           // revoker detaches this communicator)
+            std::lock_guard<std::mutex> g(g_svc_mtx);
+            if (c->svc_ok && c->svcq) svc_park(c);
+        }
+        break;
     case MI355X_KNOB_STAGE_BYTES:
         if (value < 4096 || value >= (1l << 31)) return set_error(MI355X_ERR_ARG, "stage_bytes out of range");
         if (c->stage) (void)hipFree(c->stage);

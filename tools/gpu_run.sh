@@ -179,7 +179,7 @@ for step in "$@"; do
             grep us_per_call $O/small_one.log | sed "s/^{/{\"tag\": \"$tag\", /" | tee -a $O/small.jsonl
         done ;;
     interference)
-        run interference 600 python tools/svc_interference.py --out $O/svc_interference.jsonl
+        run interference 900 python tools/svc_interference.py --out $O/svc_interference.jsonl
         cat $O/svc_interference.jsonl ;;
     *)
         echo "unknown step $step"
