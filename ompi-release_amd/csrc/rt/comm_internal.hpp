@@ -122,6 +122,13 @@ struct alignas(64) Envelope {
                                   // (kEnvHost) its host arena: id = segment generation, off = offset
         unsigned char inl[sizeof(BufDesc)];  // (kEnvInline) the payload itself, <= kP2PInline bytes
     };
+    // (kEnvDual: a small device payload offered two ways) the sender's host copy in its arena --
+    // generation and offset -- and who reads the payload: 0 undecided, 1 the host copy is complete
+    // and the receiver reads it (set by the sender, whose send then completes), 2 the receiver pulls
+    // from the sender's device buffer (set by the receiver; the sender waits for the FIN)
+    uint64_t hoff;
+    uint32_t hgen;
+    std::atomic<uint32_t> claim;
 };
 inline size_t p2p_offset(int size)
 {
@@ -226,6 +233,14 @@ struct mi355x_request {
     bool cancelled = false;               // receive cancelled before it matched
     int32_t env_flags = 0;                // send: kEnvPacked / kEnvHost (p2p.cpp)
     void *hslot = nullptr;                // send: payload slot in the host shared-memory arena
+    mi355x_request *twin = nullptr;       // send (kEnvDual): the caller's request, completed once the
+                                          // payload is safe (host copy taken) or delivered (FIN)
+    bool copy_done = false;               // send (kEnvDual): the host copy's kernel has finished
+    bool copy_launched = false;           // send (kEnvDual): ... has been launched
+    double dual_t0 = 0;                   // send (kEnvDual): when it was posted (steady clock, s)
+    const void *dual_src = nullptr;       // send (kEnvDual): the caller's device bytes
+    uint64_t hoff = 0;                    // send (kEnvDual): the host copy's arena offset and generation
+    uint32_t hgen = 0;
     void *stage = nullptr;                // receive: device staging slot (host destination)
     std::vector<char> htmp;               // receive: host copy awaiting the host convertor
     unsigned char inl[mi355x::kP2PInline]; // send: an inline payload until its envelope is posted

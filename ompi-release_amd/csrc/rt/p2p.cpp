@@ -57,6 +57,7 @@ constexpr int32_t kEnvPacked = 1;             // the payload is a packed copy (l
 constexpr int32_t kEnvHost = 2;               // the payload is in the sender's host arena
 constexpr int32_t kEnvStream = 4;             // ... and is being copied in: a StreamHdr precedes it
 constexpr int32_t kEnvInline = 8;             // the payload is inside the envelope (<= kP2PInline bytes)
+constexpr int32_t kEnvDual = 16;              // a small device payload offered two ways (Envelope::claim)
 static_assert(sizeof(BufDesc) >= kP2PInline, "an inline payload fits the envelope's descriptor space");
 // host payloads of at least kStreamMin bytes are announced before they are copied into the arena
 // and copied in kStreamFrag fragments, the receiver copying fragment k out while the sender copies
@@ -138,6 +139,7 @@ struct P2P {
     DevArena rstage;                       // receive side: device staging of host receives
     HostArena harena;                      // host payloads (shared memory)
     char *bounce = nullptr;                // registered host bounce for an inline payload bound for the device
+    std::vector<hipEvent_t> evpool;        // completion events of dual sends' host copies, for reuse
     std::map<std::pair<int, uint32_t>, HostSeg> peer_segs;  // peers' host arenas, mapped
 };
 
@@ -186,6 +188,7 @@ void p2p_destroy(mi355x_comm *c)
     seg_drop(p->harena.cur, true);
     for (HostSeg &g : p->harena.retired) seg_drop(g, true);
     if (p->bounce) (void)hipHostFree(p->bounce);
+    for (hipEvent_t e : p->evpool) (void)hipEventDestroy(e);
     for (auto &kv : p->peer_segs) seg_drop(kv.second, false);
     delete p;
     c->p2p = nullptr;
@@ -384,6 +387,9 @@ static bool try_announce(mi355x_comm *c, mi355x_request *r)
     env->bytes = r->bytes;
     if (r->env_flags & kEnvInline) std::memcpy(env->inl, r->inl, r->bytes);
     else std::memcpy(&env->buf, &r->desc, sizeof(BufDesc));
+    env->hoff = r->hoff;
+    env->hgen = r->hgen;
+    env->claim.store(0, std::memory_order_relaxed);
     env->full.store(r->msg + 1, std::memory_order_release);
     r->env = env;
     return true;
@@ -462,8 +468,22 @@ static void start_read(mi355x_comm *c, P2P *p, mi355x_request *r, const P2PMsg &
     char *dst = (char *)r->buf + first;
     hipStream_t s = nullptr;
     int rc = MI355X_SUCCESS;
+    // a small device payload offered two ways: pull it from the device buffer unless the sender's
+    // host copy was taken first (claim 1)
+    bool dual_host = false;
+    if (env->flags & kEnvDual) {
+        uint32_t z = 0;
+        dual_host = !env->claim.compare_exchange_strong(z, 2u, std::memory_order_acq_rel);
+    }
+    BufDesc hdesc = env->buf;
+    if (dual_host) {
+        std::memset(&hdesc, 0, sizeof(hdesc));
+        hdesc.present = 1;
+        hdesc.id = env->hgen;
+        hdesc.off = env->hoff;
+    }
+    const bool hostpay = dual_host || (env->flags & (kEnvHost | kEnvInline)) != 0;
     // (the stream only where a kernel or an async copy runs: not for a host payload into host memory)
-    const bool hostpay = (env->flags & (kEnvHost | kEnvInline)) != 0;
     if ((!hostpay || !r->host || !contig) && (rc = p2p_stream(c, p, &s))) return fail(rc);
     if (hostpay) {
         // host payload (sm-BTL style): copied out synchronously, FIN at once -- from the envelope
@@ -484,7 +504,7 @@ static void start_read(mi355x_comm *c, P2P *p, mi355x_request *r, const P2PMsg &
         } else {
             const char *dsrc = nullptr;
             HostSeg *seg = nullptr;
-            if ((rc = host_src(c, p, msg.src, env->buf, &src, &dsrc, &seg))) return fail(rc);
+            if ((rc = host_src(c, p, msg.src, hdesc, &src, &dsrc, &seg))) return fail(rc);
             if (dsrc && !r->host && contig && !(env->flags & kEnvStream)) {
                 // into device memory from the registered, device-mapped arena: one copy kernel on
                 // the point-to-point stream, completed (and FINed) by progress like a device pull
@@ -621,11 +641,64 @@ static void drain_mailboxes(mi355x_comm *c, P2P *p)
 // a send whose FIN arrived: its payload slot is free; an engine-owned send is finished
 static void send_done(P2P *p, mi355x_request *r)
 {
+    if (r->twin) {  // (kEnvDual) delivered before the host copy was taken
+        complete(r->twin, MI355X_SUCCESS);
+        r->twin = nullptr;
+    }
+    if (r->ev && (r->env_flags & kEnvDual)) {
+        p->evpool.push_back(r->ev);
+        r->ev = nullptr;
+    }
     if (r->packed) arena_release(p->arena);
     if (r->hslot) harena_release(p);
     r->packed = r->hslot = nullptr;
     if (r->internal) delete r;
     else complete(r, MI355X_SUCCESS);
+}
+
+// (kEnvDual) time to take the host copy: nobody claimed the device buffer within the delay
+static bool dual_copy_due(const mi355x_request *r)
+{
+    static const double delay = std::max(0.0, (getenv("MI355X_P2P_DUAL_DELAY_US") ? atof(getenv("MI355X_P2P_DUAL_DELAY_US"))
+                                                                                   : 10.0)) * 1e-6;
+    const double now = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    return now - r->dual_t0 >= delay;
+}
+
+// (kEnvDual) the copy kernel of the caller's bytes into the registered arena slot, and its event
+static int dual_copy_launch(mi355x_comm *c, P2P *p, mi355x_request *r)
+{
+    r->copy_launched = true;
+    hipStream_t s = nullptr;
+    int rc = p2p_stream(c, p, &s);
+    if (rc) return rc;
+    HostSeg *g = nullptr;  // the segment the slot is in (the current one, or a retired generation)
+    if (p->harena.cur.gen == r->hgen) g = &p->harena.cur;
+    for (HostSeg &x : p->harena.retired)
+        if (x.gen == r->hgen) g = &x;
+    if (!g || !g->dbase) return set_error(MI355X_ERR_HIP, "host arena slot without a device mapping");
+    MultiCopyArgs m;
+    std::memset(&m, 0, sizeof(m));
+    m.src[0] = r->dual_src;
+    m.dst[0] = g->dbase + r->hoff;
+    m.len[0] = r->bytes;
+    m.nseg = 1;
+    if ((rc = launch_multicopy(m, s))) return rc;
+    if (!r->ev) {
+        if (!p->evpool.empty()) {
+            r->ev = p->evpool.back();
+            p->evpool.pop_back();
+        } else if (hipEventCreateWithFlags(&r->ev, hipEventDisableTiming) != hipSuccess) {
+            r->ev = nullptr;
+            (void)hipStreamSynchronize(s);
+            return set_error(MI355X_ERR_HIP, "hipEventCreate failed");
+        }
+    }
+    if (hipEventRecord(r->ev, s) != hipSuccess) {
+        (void)hipStreamSynchronize(s);
+        return set_error(MI355X_ERR_HIP, "hipEventRecord on the point-to-point stream failed");
+    }
+    return MI355X_SUCCESS;
 }
 
 int p2p_progress(mi355x_comm *c)
@@ -690,11 +763,38 @@ int p2p_progress(mi355x_comm *c)
         else complete(r, rc);
         it = p->reading.erase(it);
     }
-    // 5. acknowledged sends
+    // 5. acknowledged sends (a dual send's caller completes as soon as its host copy is taken --
+    // unless the receiver already chose to pull from the device buffer -- and the slot is released
+    // only once the copy kernel has finished writing it)
     for (auto it = p->sending.begin(); it != p->sending.end();) {
         mi355x_request *r = *it;
+        if ((r->env_flags & kEnvDual) && !r->copy_launched &&
+            r->env->claim.load(std::memory_order_acquire) == 0 && dual_copy_due(r)) {
+            if (dual_copy_launch(c, p, r) != MI355X_SUCCESS) r->copy_done = true;  // (then only the pull remains)
+        }
+        if ((r->env_flags & kEnvDual) && r->copy_launched && !r->copy_done) {
+            const hipError_t e = hipEventQuery(r->ev);
+            if (e != hipErrorNotReady) {
+                r->copy_done = true;
+                uint32_t z = 0;
+                if (e == hipSuccess && r->env->claim.compare_exchange_strong(z, 1u, std::memory_order_acq_rel) && r->twin) {
+                    complete(r->twin, MI355X_SUCCESS);
+                    r->twin = nullptr;
+                }
+            }
+        }
         // >=: the receiver may already have finished the slot's next message too
         if (r->env->done.load(std::memory_order_acquire) < r->msg + 1) {
+            ++it;
+            continue;
+        }
+        if ((r->env_flags & kEnvDual) && r->copy_launched && !r->copy_done) {
+            // delivered (the receiver pulled from the device buffer): the caller completes now; the
+            // engine keeps the arena slot until its copy kernel -- whose bytes nobody reads -- is done
+            if (r->twin) {
+                complete(r->twin, MI355X_SUCCESS);
+                r->twin = nullptr;
+            }
             ++it;
             continue;
         }
@@ -723,18 +823,19 @@ static mi355x_request *new_request(mi355x_comm *c, int kind)
 
 // announce r (queue it behind an earlier send to the same destination); the caller's request is
 // r, or -- eager -- a completed twin while the engine keeps r until the FIN
-static mi355x_request *post_send(mi355x_comm *c, P2P *p, mi355x_request *r, bool eager)
+static mi355x_request *post_send(mi355x_comm *c, P2P *p, mi355x_request *r, bool eager, bool dual = false)
 {
     r->msg = p->send_seq[(size_t)r->peer]++;
     mi355x_request *user = r;
-    if (eager) {
+    if (eager || dual) {
         r->internal = true;
         user = new_request(c, 1);
         user->peer = r->peer;
         user->tag = r->tag;
         user->bytes = r->bytes;
         user->mode = r->mode;
-        complete(user, MI355X_SUCCESS);
+        if (dual) r->twin = user;  // completed by progress: host copy taken, or FIN
+        else complete(user, MI355X_SUCCESS);
     }
     bool earlier = false;   // an earlier send to the same destination still queued: keep order
     for (mi355x_request *q : p->queued) earlier = earlier || q->peer == r->peer;
@@ -818,6 +919,7 @@ static int isend(mi355x_comm *c, const void *buf, size_t count, const mi355x_ddt
     auto bail = [&](int code) {
         if (r->packed) arena_release(p->arena);
         if (r->hslot) harena_release(p);
+        if (r->ev) (void)hipEventDestroy(r->ev);
         delete r;
         return code;
     };
@@ -842,6 +944,36 @@ static int isend(mi355x_comm *c, const void *buf, size_t count, const mi355x_ddt
     BufDesc desc;
     std::memset(&desc, 0, sizeof(desc));
     hipStream_t s = nullptr;
+    // A small device payload is offered two ways at once (kEnvDual): the envelope carries the export
+    // of the caller's buffer AND a copy kernel writes the bytes into the sender's registered host
+    // arena.  A receiver that matches before the copy is taken pulls straight from the device buffer
+    // (one launch on its side, as a rendezvous); otherwise the send completes as soon as the copy is
+    // done (eager: both ranks may send first) and the receiver reads the host copy.  One GPU round
+    // trip per message where a receiver waits, instead of a device-to-host and a host-to-device copy
+    // one after the other.  The copy is launched only if no receiver has claimed the device buffer
+    // within MI355X_P2P_DUAL_DELAY_US (10 us) of the announcement (p2p_progress), so a waiting
+    // receiver's pull never competes with it.  MI355X_P2P_DUAL=0 keeps the host-arena-only form.
+    static const bool dual_on = !(getenv("MI355X_P2P_DUAL") && atoi(getenv("MI355X_P2P_DUAL")) == 0);
+    if (dual_on && dev && small && contig && bytes && dest != c->rank && !c->loopback && p->harena.cur.dbase != nullptr) {
+        BufDesc hd;
+        void *slot = nullptr;
+        if ((rc = local_handle(c, ubuf, &desc, false))) return bail(rc);
+        if (!desc.staged) {
+            desc.raw = (uint64_t)(uintptr_t)ubuf;
+            if ((rc = harena_alloc(c, p, bytes, &slot, &hd))) return bail(rc);
+            r->hslot = slot;
+            if (!p->harena.cur.dbase) return bail(set_error(MI355X_ERR_HIP, "host arena without a device mapping"));
+            r->dual_src = ubuf;
+            r->dual_t0 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+            r->env_flags = kEnvDual;
+            r->hoff = hd.off;
+            r->hgen = (uint32_t)hd.id;
+            std::memcpy(&r->desc, &desc, sizeof(desc));
+            *out = post_send(c, p, r, false, true);
+            return MI355X_SUCCESS;
+        }
+        std::memset(&desc, 0, sizeof(desc));  // (an allocation of >= ipc_max: the host-arena form)
+    }
     if (bytes && (!dev || small)) {
         // the host arena: host payloads of any size, device payloads up to the eager limit
         void *slot = nullptr;

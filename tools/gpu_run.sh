@@ -139,11 +139,12 @@ for step in "$@"; do
         grep -E '^\{|passed|failed' $O/host_p2p.log ;;
     p2p_lat)
         : > $O/p2p_lat.jsonl
-        for kind in p2p_host p2p_dev p2p_dev:unregistered; do
+        for kind in p2p_host p2p_dev p2p_dev:single_offer p2p_dev:unregistered; do
             reg=1; [ "${kind#*:}" = unregistered ] && reg=0
-            MI355X_P2P_REGISTER=$reg SMALL_COLL=${kind%%:*} SMALL_SIZES=8,64,512,1024,4096,16384,65536 \
+            dual=1; [ "${kind#*:}" = single_offer ] && dual=0
+            MI355X_P2P_DUAL=$dual MI355X_P2P_REGISTER=$reg SMALL_COLL=${kind%%:*} SMALL_SIZES=8,64,512,1024,4096,16384,65536 \
                 timeout -k 10 120 ./tools/build/small_ar_c 2 ${REPS:-5000} host > $O/small_one.log 2>&1 || { cat $O/small_one.log; exit 1; }
-            grep one_way_us $O/small_one.log | sed "s/^{/{\"host_arena_registered\": $reg, /" | tee -a $O/p2p_lat.jsonl
+            grep one_way_us $O/small_one.log | sed "s/^{/{\"host_arena_registered\": $reg, \"dual_offer\": $dual, /" | tee -a $O/p2p_lat.jsonl
         done
         run p2p_lat_py 300 python tools/p2p_latency.py --out $O/p2p_lat.jsonl
         grep python $O/p2p_lat.jsonl ;;
