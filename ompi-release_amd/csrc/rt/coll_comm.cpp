@@ -1460,16 +1460,18 @@ static void svc_trace_report(mi355x_comm *c)
     int nrows = 0;
     for (int r = 0; r < kSvcTraceCalls; ++r) {
         const uint64_t *row = c->svc_trace + (size_t)r * kSvcTraceCols;
-        if (!row[0] || !row[6] || !row[7] || row[6] < row[1]) continue;
-        // stages in time order: 1 door, 2 descriptor, 3 pushed, 4 received, 7 evaluated, 5 stored, 6 completed
-        const int order[] = {1, 2, 3, 4, 7, 5, 6};
-        for (int k = 1; k < 7; ++k) acc[order[k]] += (double)(row[order[k]] - row[order[k - 1]]) * 0.01;  // 100 MHz
+        if (!row[0] || !row[6] || !row[7] || !row[8] || !row[9] || row[6] < row[1]) continue;
+        // stages in time order: 1 door, 2 descriptor, 3 pushed, 4 received, 8 results issued (the
+        // first slice), 9 workgroup joined, 7 evaluated (every slice), 5 stored, 6 completed
+        const int order[] = {1, 2, 3, 4, 8, 9, 7, 5, 6};
+        for (int k = 1; k < 9; ++k) acc[order[k]] += (double)(row[order[k]] - row[order[k - 1]]) * 0.01;  // 100 MHz
         ++nrows;
     }
     if (nrows)
         fprintf(stderr, "[mi355x r%d] resident service, %d traced calls, mean us: door->descriptor %.2f, "
-                "->pushed %.2f, ->received %.2f, ->evaluated %.2f, ->stored %.2f, ->completed %.2f\n", c->rank, nrows,
-                acc[2] / nrows, acc[3] / nrows, acc[4] / nrows, acc[7] / nrows, acc[5] / nrows, acc[6] / nrows);
+                "->pushed %.2f, ->received %.2f, ->issued %.2f, ->joined %.2f, ->evaluated %.2f, ->stored %.2f, "
+                "->completed %.2f\n", c->rank, nrows, acc[2] / nrows, acc[3] / nrows, acc[4] / nrows, acc[8] / nrows,
+                acc[9] / nrows, acc[7] / nrows, acc[5] / nrows, acc[6] / nrows);
     (void)hipHostFree(c->svc_trace);
     c->svc_trace = nullptr;
 }
@@ -1493,6 +1495,8 @@ static bool svc_attach(mi355x_comm *c)
 {
     SvcRes &r = g_svc_res[c->device];
     if (r.stuck) return false;
+    const char *inj = getenv("MI355X_SELFTEST_FAIL");  // (tests: this rank's service cannot open)
+    if (inj && std::strstr(inj, "svc_open")) return false;
     if (!r.q) {
         auto *q = new SvcQueue;
         std::string why;

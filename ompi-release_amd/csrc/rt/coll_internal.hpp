@@ -152,8 +152,9 @@ struct SvcArgs {                      // fixed for one launch
 };
 // MI355X_SVC_TRACE=1: workgroup 0 stamps s_memrealtime (100 MHz) at each stage of a call into row
 // seq % kSvcTraceCalls: seq, door seen, descriptor in LDS, slices pushed, peers' slices received,
-// results stored, completion stored
-constexpr int kSvcTraceCalls = 1024, kSvcTraceCols = 8;
+// results stored, completion stored, evaluated; the granule forms also: the first slice's results
+// issued, the workgroup joined after it
+constexpr int kSvcTraceCalls = 1024, kSvcTraceCols = 12;
 
 // Pipelined allreduce (coll_pipe.hip): fold of my ring block and pulls of the peers' blocks in
 // one launch, chunk by chunk, with per-chunk ready flags (uncached region, written by the

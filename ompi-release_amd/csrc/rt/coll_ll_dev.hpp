@@ -240,11 +240,11 @@ static __device__ void ll_done(const LLArgs &a)
         if (q != a.me) ll_store(a.peer_ack[q], a.seq);
 }
 
-template <class F> __device__ __forceinline__ typename F::T ll_pick(const typename F::T (&R)[kTreeMax], int k)
+template <class F> __device__ __forceinline__ typename F::T ll_pick(const typename F::T (&R)[kLLMaxRanks], int k)
 {
     typename F::T v = R[0];
 #pragma unroll
-    for (int s = 1; s < kTreeMax; ++s)
+    for (int s = 1; s < kLLMaxRanks; ++s)
         if (s == k) v = R[s];
     return v;
 }
@@ -258,15 +258,16 @@ template <class F, class X> __device__ __forceinline__ typename F::T ll_eval(con
 {
     using T = typename F::T;
     if (a.prog == LL_TREE) {
-        T R[kTreeMax];
+        // (LL calls have <= kLLMaxRanks ranks, so the program's registers are the ranks' values:
+        // eight of them stay in VGPRs, where the k_tree width of 16 went to scratch)
+        T R[kLLMaxRanks];
 #pragma unroll
-        for (int s = 0; s < kTreeMax; ++s)
-            if (s < a.n) R[s] = x(s);
+        for (int s = 0; s < kLLMaxRanks; ++s) R[s] = x(s < a.n ? s : 0);
         for (int k = 0; k < a.nsteps; ++k) {
             const TreeStep st = a.steps[k];
             const T r = F::op2(ll_pick<F>(R, st.out), ll_pick<F>(R, st.in));
 #pragma unroll
-            for (int s = 0; s < kTreeMax; ++s)
+            for (int s = 0; s < kLLMaxRanks; ++s)
                 if (s == st.dst) R[s] = r;
         }
         return ll_pick<F>(R, a.result);

@@ -223,8 +223,11 @@ static __device__ __forceinline__ int svc_finish_body(const LLArgs &a, const Svc
                 else
                     ll_reduce_out<F, true>(a, k, w);
             }
+            if (tr && threadIdx.x == 0 && c == blockIdx.x) tr[8] = __builtin_amdgcn_s_memrealtime();
         }
-        if (__syncthreads_or(bad)) return 1;
+        const int any_bad = __syncthreads_or(bad);
+        if (tr && threadIdx.x == 0 && c == blockIdx.x) tr[9] = __builtin_amdgcn_s_memrealtime();
+        if (any_bad) return 1;
     }
     return 0;
 }
@@ -243,13 +246,10 @@ template <class F> struct SvcReduce : F {
     static constexpr bool kCopy = false;
 };
 
-static __device__ int svc_finish_call(int op, int type, bool copy, const LLArgs &a, const SvcCall &sc,
-                                      uint64_t nchunks, uint64_t stride, uint64_t *tr)
+// every other slot: one out-of-line function per slot behind one out-of-line dispatcher
+static __device__ __noinline__ int svc_finish_call(int op, int type, const LLArgs &a, const SvcCall &sc,
+                                                   uint64_t nchunks, uint64_t stride, uint64_t *tr)
 {
-    if (copy) return svc_finish<SvcCopy>(a, sc, nchunks, stride, tr);
-    // the hot slots inline: no call, so none of the call's register saves and scratch reloads
-    if (op == MI355X_OP_SUM && type == MI355X_T_FLOAT) return svc_finish_body<SvcReduce<OpSum<float>>>(a, sc, nchunks, stride, tr);
-    if (op == MI355X_OP_SUM && type == MI355X_T_DOUBLE) return svc_finish_body<SvcReduce<OpSum<double>>>(a, sc, nchunks, stride, tr);
     int rc = 0;
     for_each_slot([&](auto tag, int o, int t) {
         using F = typename decltype(tag)::type;
@@ -347,6 +347,7 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
         if (tr && t == 0) {
             tr[0] = want;
             tr[1] = __builtin_amdgcn_s_memrealtime();
+            tr[8] = tr[9] = 0;  // (granule forms only)
         }
         // 2. the descriptor (stored before the doorbell; not rewritten before every participant
         // of this call is done) into LDS
@@ -425,7 +426,19 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
             }
         }
         if (tr && t == 0) tr[3] = __builtin_amdgcn_s_memrealtime();
-        if (!failed && evaluate) failed = svc_finish_call(sc.op, sc.type, !reduce, a, sc, nchunks, stride, tr);
+        // the hot forms inline in the kernel: a function call costs a wait for every outstanding
+        // memory operation at its entry (the pushes, written through to the peers) and its
+        // register saves and scratch reloads -- ~2 us of an 8-B call's 7 on the device
+        if (!failed && evaluate) {
+            if (!reduce)
+                failed = svc_finish_body<SvcCopy>(a, sc, nchunks, stride, tr);
+            else if (sc.op == MI355X_OP_SUM && sc.type == MI355X_T_FLOAT)
+                failed = svc_finish_body<SvcReduce<OpSum<float>>>(a, sc, nchunks, stride, tr);
+            else if (sc.op == MI355X_OP_SUM && sc.type == MI355X_T_DOUBLE)
+                failed = svc_finish_body<SvcReduce<OpSum<double>>>(a, sc, nchunks, stride, tr);
+            else
+                failed = svc_finish_call(sc.op, sc.type, a, sc, nchunks, stride, tr);
+        }
         if (tr && t == 0) tr[7] = __builtin_amdgcn_s_memrealtime();
         // 4. every store of the workgroup has reached memory; count; the last participant
         // acknowledges the call to every peer and completes it for the host

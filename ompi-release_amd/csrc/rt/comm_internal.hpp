@@ -123,12 +123,14 @@ struct alignas(64) Envelope {
         unsigned char inl[sizeof(BufDesc)];  // (kEnvInline) the payload itself, <= kP2PInline bytes
     };
     // (kEnvDual: a small device payload offered two ways) the sender's host copy in its arena --
-    // generation and offset -- and who reads the payload: 0 undecided, 1 the host copy is complete
-    // and the receiver reads it (set by the sender, whose send then completes), 2 the receiver pulls
-    // from the sender's device buffer (set by the receiver; the sender waits for the FIN)
+    // generation and offset -- and who reads the payload, as ((message number + 1) << 2) | state
+    // (p2p.cpp, claim_word): state 0 undecided, 1 the host copy is complete and the receiver reads
+    // it (set by the sender, whose send then completes), 2 the receiver pulls from the sender's
+    // device buffer (set by the receiver; the sender waits for the FIN).  The message number makes
+    // a late compare-and-swap about an earlier message of the slot fail once the slot is reused.
     uint64_t hoff;
-    uint32_t hgen;
-    std::atomic<uint32_t> claim;
+    uint32_t hgen, pad;
+    std::atomic<uint64_t> claim;
 };
 inline size_t p2p_offset(int size)
 {

@@ -374,6 +374,9 @@ static void complete_recv(mi355x_request *r)
         complete(r, MI355X_SUCCESS);
 }
 
+// Envelope::claim of message `msg` in state 0 (undecided), 1 (host copy) or 2 (device pull)
+static inline uint64_t claim_word(uint64_t msg, uint64_t state) { return ((msg + 1) << 2) | state; }
+
 // announce send r in its envelope if the slot is free (the message K before it is done)
 static bool try_announce(mi355x_comm *c, mi355x_request *r)
 {
@@ -389,7 +392,7 @@ static bool try_announce(mi355x_comm *c, mi355x_request *r)
     else std::memcpy(&env->buf, &r->desc, sizeof(BufDesc));
     env->hoff = r->hoff;
     env->hgen = r->hgen;
-    env->claim.store(0, std::memory_order_relaxed);
+    env->claim.store(claim_word(r->msg, 0), std::memory_order_relaxed);
     env->full.store(r->msg + 1, std::memory_order_release);
     r->env = env;
     return true;
@@ -472,8 +475,8 @@ static void start_read(mi355x_comm *c, P2P *p, mi355x_request *r, const P2PMsg &
     // host copy was taken first (claim 1)
     bool dual_host = false;
     if (env->flags & kEnvDual) {
-        uint32_t z = 0;
-        dual_host = !env->claim.compare_exchange_strong(z, 2u, std::memory_order_acq_rel);
+        uint64_t z = claim_word(msg.m, 0);
+        dual_host = !env->claim.compare_exchange_strong(z, claim_word(msg.m, 2), std::memory_order_acq_rel);
     }
     BufDesc hdesc = env->buf;
     if (dual_host) {
@@ -766,25 +769,28 @@ int p2p_progress(mi355x_comm *c)
     // 5. acknowledged sends (a dual send's caller completes as soon as its host copy is taken --
     // unless the receiver already chose to pull from the device buffer -- and the slot is released
     // only once the copy kernel has finished writing it)
+    // (once the FIN is in, the slot may already carry a later message: nothing of r's touches it)
     for (auto it = p->sending.begin(); it != p->sending.end();) {
         mi355x_request *r = *it;
-        if ((r->env_flags & kEnvDual) && !r->copy_launched &&
-            r->env->claim.load(std::memory_order_acquire) == 0 && dual_copy_due(r)) {
+        // >=: the receiver may already have finished the slot's next message too
+        const bool fin = r->env->done.load(std::memory_order_acquire) >= r->msg + 1;
+        if ((r->env_flags & kEnvDual) && !fin && !r->copy_launched &&
+            r->env->claim.load(std::memory_order_acquire) == claim_word(r->msg, 0) && dual_copy_due(r)) {
             if (dual_copy_launch(c, p, r) != MI355X_SUCCESS) r->copy_done = true;  // (then only the pull remains)
         }
         if ((r->env_flags & kEnvDual) && r->copy_launched && !r->copy_done) {
             const hipError_t e = hipEventQuery(r->ev);
             if (e != hipErrorNotReady) {
                 r->copy_done = true;
-                uint32_t z = 0;
-                if (e == hipSuccess && r->env->claim.compare_exchange_strong(z, 1u, std::memory_order_acq_rel) && r->twin) {
+                uint64_t z = claim_word(r->msg, 0);  // (fails after the FIN: the receiver claimed first)
+                if (e == hipSuccess && r->env->claim.compare_exchange_strong(z, claim_word(r->msg, 1), std::memory_order_acq_rel) &&
+                    r->twin) {
                     complete(r->twin, MI355X_SUCCESS);
                     r->twin = nullptr;
                 }
             }
         }
-        // >=: the receiver may already have finished the slot's next message too
-        if (r->env->done.load(std::memory_order_acquire) < r->msg + 1) {
+        if (!fin) {
             ++it;
             continue;
         }

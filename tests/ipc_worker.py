@@ -758,6 +758,8 @@ def selftest(key, rank, size, dev):
     pkg = load_pkg()
     oracle = load_oracle()
     ptrs = lambda arrs: (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    # SVC_OPEN: the service cannot open on one rank -> no rank claims it, nothing is self-tested
+    open_fail = os.environ.get("SELFTEST_EXPECT", "") == "SVC_OPEN"
     expect = pkg.FLOW.get(os.environ.get("SELFTEST_EXPECT", ""), 0)
     comm = pkg.Comm.create(key, rank, size, dev)
     create_us, st_us = comm.get("CREATE_US"), comm.get("SELFTEST_US")
@@ -770,7 +772,7 @@ def selftest(key, rank, size, dev):
     flows, failed = comm.get("FLOWS"), comm.get("FLOWS_FAILED")
     assert failed == expect, f"flows failed {failed:#x}, expected {expect:#x}"
     assert flows == 0x1f & ~expect, f"flows {flows:#x}"
-    assert comm.get("SVC_OWNER") == (0 if expect == pkg.FLOW["SVC_LL"] else 1)
+    assert comm.get("SVC_OWNER") == (0 if expect == pkg.FLOW["SVC_LL"] or open_fail else 1)
     if expect == pkg.FLOW["PIPE"]:
         comm.set("PIPE", 1)
         assert comm.get("PIPE") == 0, "a flow that failed its self-test cannot be forced on"
@@ -808,6 +810,8 @@ def selftest(key, rank, size, dev):
         comm.reduce_scatter_block(dx.data_ptr(), dr.data_ptr(), rcount, i32, SUM)
         opdata.assert_same("INT32", "SUM", dr.cpu().numpy().view(xs[0].dtype), outs[rank], f"selftest rsb {rcount}")
     served = comm.get("SVC_CALLS") - calls0
+    if open_fail:
+        assert served == 0 and comm.get("SVC_LAUNCHES") == 0, "a service that could not open on one rank serves no rank"
     print(f"rank {rank} flows {flows:#x} failed {failed:#x} create_us {create_us} selftest_us {st_us} "
           f"claim_selftest_us {comm.get('SELFTEST_US') - st_us} served {served}", flush=True)
     comm.barrier()

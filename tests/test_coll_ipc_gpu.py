@@ -79,11 +79,12 @@ def test_resident_service_follows_the_busy_communicator(gpu):
     print(lines[0])
 
 
-@pytest.mark.parametrize("flow", ["", "svc_ll", "svc_pull", "svc_copy", "svc_rs", "pipe"])
+@pytest.mark.parametrize("flow", ["", "svc_ll", "svc_pull", "svc_copy", "svc_rs", "pipe", "svc_open"])
 def test_flow_selftest(gpu, flow):
     """every default-on cross-device flow is self-tested before its first use; a failure injected on
     ONE rank (MI355X_SELFTEST_FAIL) turns that flow off on EVERY rank, and calls of every kind stay
-    exact vs the oracle (ipc_worker.py::selftest)"""
+    exact vs the oracle (ipc_worker.py::selftest).  svc_open: the service cannot start on one rank,
+    so no rank claims it (no rank self-tests or serves alone)"""
     rank_env = {1: {"MI355X_SELFTEST_FAIL": flow}} if flow else None
     outs = _run_mode(gpu, "selftest", 2, extra_env={"SELFTEST_EXPECT": flow.upper()}, rank_env=rank_env)
     print(next(ln for ln in outs[0].splitlines() if " flows " in ln))
