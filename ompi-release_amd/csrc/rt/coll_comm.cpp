@@ -1456,10 +1456,13 @@ static int svc_pull_run(mi355x_comm *c, int op, int type, const std::vector<std:
 static void svc_trace_report(mi355x_comm *c)
 {
     if (!c->svc_trace) return;
+    std::vector<uint64_t> rows((size_t)kSvcTraceCalls * kSvcTraceCols, 0);
+    if (hipMemcpy(rows.data(), c->svc_trace, rows.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+        rows.assign(rows.size(), 0);
     double acc[kSvcTraceCols] = {0};
     int nrows = 0;
     for (int r = 0; r < kSvcTraceCalls; ++r) {
-        const uint64_t *row = c->svc_trace + (size_t)r * kSvcTraceCols;
+        const uint64_t *row = rows.data() + (size_t)r * kSvcTraceCols;
         if (!row[0] || !row[6] || !row[7] || !row[8] || !row[9] || row[6] < row[1]) continue;
         // stages in time order: 1 door, 2 descriptor, 3 pushed, 4 received, 8 results issued (the
         // first slice), 9 workgroup joined, 7 evaluated (every slice), 5 stored, 6 completed
@@ -1472,7 +1475,7 @@ static void svc_trace_report(mi355x_comm *c)
                 "->pushed %.2f, ->received %.2f, ->issued %.2f, ->joined %.2f, ->evaluated %.2f, ->stored %.2f, "
                 "->completed %.2f\n", c->rank, nrows, acc[2] / nrows, acc[3] / nrows, acc[4] / nrows, acc[8] / nrows,
                 acc[9] / nrows, acc[7] / nrows, acc[5] / nrows, acc[6] / nrows);
-    (void)hipHostFree(c->svc_trace);
+    (void)hipFree(c->svc_trace);
     c->svc_trace = nullptr;
 }
 
@@ -1538,7 +1541,12 @@ static bool svc_attach(mi355x_comm *c)
     }
     if (!c->svc_trace && env_double("MI355X_SVC_TRACE", 0.0) != 0.0) {
         const size_t tb = sizeof(uint64_t) * kSvcTraceCalls * kSvcTraceCols;
-        if (hipHostMalloc((void **)&c->svc_trace, tb, hipHostMallocCoherent) == hipSuccess) std::memset(c->svc_trace, 0, tb);
+        // (device memory: the kernel keeps a call's stamps in LDS and writes the row once the call is
+        // complete, so the stamps cost no host-memory round trip inside the call)
+        if (hipMalloc((void **)&c->svc_trace, tb) != hipSuccess || hipMemset(c->svc_trace, 0, tb) != hipSuccess) {
+            (void)hipGetLastError();
+            c->svc_trace = nullptr;
+        }
     }
     return true;
 }

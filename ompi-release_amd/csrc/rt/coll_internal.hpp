@@ -150,7 +150,8 @@ struct SvcArgs {                      // fixed for one launch
     int32_t n, me, nwg, probe;        // probe: return at once (loads the code object)
     uint64_t *trace;                  // NULL, or kSvcTraceCalls rows of kSvcTraceCols words (MI355X_SVC_TRACE)
 };
-// MI355X_SVC_TRACE=1: workgroup 0 stamps s_memrealtime (100 MHz) at each stage of a call into row
+// MI355X_SVC_TRACE=1: workgroup 0 stamps s_memrealtime (100 MHz) at each stage of a call (in LDS;
+// the row is written to device memory once the call is complete) into row
 // seq % kSvcTraceCalls: seq, door seen, descriptor in LDS, slices pushed, peers' slices received,
 // results stored, completion stored, evaluated; the granule forms also: the first slice's results
 // issued, the workgroup joined after it

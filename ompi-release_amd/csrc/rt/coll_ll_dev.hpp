@@ -2,6 +2,8 @@
 // coll_ll.hip), shared by the per-call LL kernels and the resident service kernel (coll_svc.hip).
 #pragma once
 
+#include <type_traits>
+
 #include "coll_internal.hpp"
 #include "op_functors.hpp"
 #include "rt_internal.hpp"
@@ -89,10 +91,12 @@ __device__ __forceinline__ void ll_write16(char *base, size_t off, size_t len, c
                 __builtin_amdgcn_raw_buffer_store_b32(w[i], rs, (unsigned)(off + 4 * i), 0, kLLSysCoherent);
             return;
         }
-        unsigned char b[16];
-        __builtin_memcpy(b, w, 16);
-        for (size_t i = 0; i < len; ++i)
-            __builtin_amdgcn_raw_buffer_store_b8(b[i], rs, (unsigned)(off + i), 0, kLLSysCoherent);
+        // (bytes taken from the words by shifts, unrolled: an indexed byte array would live in scratch)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if ((size_t)i < len)
+                __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(w[i >> 2] >> (8 * (i & 3))), rs, (unsigned)(off + i), 0,
+                                                     kLLSysCoherent);
         return;
     }
     if (len == 16 && (((uintptr_t)dst) & 15) == 0) {
@@ -112,12 +116,13 @@ struct LLBlock {
     uint32_t tag;
 };
 
-// the 4 KiB slice `chunk` of the call (the per-call kernels: chunk = blockIdx.x)
-__device__ __forceinline__ LLBlock ll_block(const LLArgs &a, size_t chunk)
+// thread `tid`'s 16 B of the 4 KiB slice `chunk` of the call (the per-call kernels: chunk =
+// blockIdx.x, tid = threadIdx.x)
+__device__ __forceinline__ LLBlock ll_block(const LLArgs &a, size_t chunk, unsigned tid = threadIdx.x)
 {
     LLBlock k;
     k.lo = chunk * kLLChunk;
-    k.off = k.lo + (size_t)threadIdx.x * 16;
+    k.off = k.lo + (size_t)tid * 16;
     k.len = k.off < a.nbytes ? (a.nbytes - k.off < 16 ? a.nbytes - k.off : 16) : 0;
     k.ngran = (int)((k.len + 3) / 4);
     k.tag = (uint32_t)a.seq;
@@ -240,37 +245,53 @@ static __device__ void ll_done(const LLArgs &a)
         if (q != a.me) ll_store(a.peer_ack[q], a.seq);
 }
 
-template <class F> __device__ __forceinline__ typename F::T ll_pick(const typename F::T (&R)[kLLMaxRanks], int k)
-{
-    typename F::T v = R[0];
-#pragma unroll
-    for (int s = 1; s < kLLMaxRanks; ++s)
-        if (s == k) v = R[s];
-    return v;
-}
-
 template <typename T> struct alignas(16) LLVec {
     T e[16 / sizeof(T)];
 };
 
-// per-element program (scalar); x(q) = rank q's element i
-template <class F, class X> __device__ __forceinline__ typename F::T ll_eval(const LLArgs &a, size_t i, X x)
+// One element's value on every rank, indexed by rank at run time (tree programs, ring orders).
+// An array here ends up a dynamically indexed stack slot -- the compiler folds the select chains
+// back into indexed loads -- so every pick is a scratch round trip on the service's latency path
+// (~1.6 us of an 8-B call).  Arithmetic types are kept in one vector register tuple instead,
+// indexed in place; other element types (complex, value-index pairs) keep the array.
+template <typename T, bool kVec = (std::is_integral<T>::value || std::is_floating_point<T>::value) &&
+                                  !std::is_same<T, bool>::value>
+struct RankRegs {
+    T r[kLLMaxRanks];
+    __device__ __forceinline__ T get(int k) const
+    {
+        T v = r[0];
+#pragma unroll
+        for (int s = 1; s < kLLMaxRanks; ++s)
+            if (s == k) v = r[s];
+        return v;
+    }
+    __device__ __forceinline__ void set(int k, T x)
+    {
+#pragma unroll
+        for (int s = 0; s < kLLMaxRanks; ++s)
+            if (s == k) r[s] = x;
+    }
+};
+template <typename T> struct RankRegs<T, true> {
+    typedef T V __attribute__((ext_vector_type(kLLMaxRanks)));
+    V r;
+    __device__ __forceinline__ T get(int k) const { return r[k]; }
+    __device__ __forceinline__ void set(int k, T x) { r[k] = x; }
+};
+
+// per-element program (scalar); X = every rank's element i
+template <class F> __device__ __forceinline__ typename F::T ll_eval(const LLArgs &a, size_t i, const RankRegs<typename F::T> &X)
 {
     using T = typename F::T;
     if (a.prog == LL_TREE) {
-        // (LL calls have <= kLLMaxRanks ranks, so the program's registers are the ranks' values:
-        // eight of them stay in VGPRs, where the k_tree width of 16 went to scratch)
-        T R[kLLMaxRanks];
-#pragma unroll
-        for (int s = 0; s < kLLMaxRanks; ++s) R[s] = x(s < a.n ? s : 0);
+        // (LL calls have <= kLLMaxRanks ranks: the program's registers are the ranks' values)
+        RankRegs<T> R = X;
         for (int k = 0; k < a.nsteps; ++k) {
             const TreeStep st = a.steps[k];
-            const T r = F::op2(ll_pick<F>(R, st.out), ll_pick<F>(R, st.in));
-#pragma unroll
-            for (int s = 0; s < kLLMaxRanks; ++s)
-                if (s == st.dst) R[s] = r;
+            R.set(st.dst, F::op2(R.get(st.out), R.get(st.in)));
         }
-        return ll_pick<F>(R, a.result);
+        return R.get(a.result);
     }
     // left fold; LL_RING: the order starts at the element's ring block
     // (coll_tuned_allreduce.c:470-512: the partial is the `in` operand at every step)
@@ -286,9 +307,9 @@ template <class F, class X> __device__ __forceinline__ typename F::T ll_eval(con
         }
         return a.order[j];
     };
-    T acc = x(rank_at(0));
+    T acc = X.get(rank_at(0));
     for (int j = 1; j < a.n; ++j) {
-        const T v = x(rank_at(j));
+        const T v = X.get(rank_at(j));
         acc = ((a.role_mask >> j) & 1u) ? F::op2(acc, v) : F::op2(v, acc);
     }
     return acc;
@@ -311,13 +332,10 @@ __device__ __forceinline__ void ll_reduce_out(const LLArgs &a, const LLBlock &k,
 #pragma unroll
     for (int e = 0; e < EPV; ++e) {
         if (e >= ne) continue;
-        r.e[e] = ll_eval<F>(a, i0 + e, [&](int q) {
-            T v = xv[0].e[e];  // register select (no dynamic indexing into xv)
+        RankRegs<T> X;
 #pragma unroll
-            for (int s2 = 1; s2 < 8; ++s2)
-                if (s2 == q) v = xv[s2].e[e];
-            return v;
-        });
+        for (int q = 0; q < kLLMaxRanks; ++q) X.set(q, xv[q].e[e]);
+        r.e[e] = ll_eval<F>(a, i0 + e, X);
     }
     uint32_t ow[4];
     __builtin_memcpy(ow, &r, 16);

@@ -41,14 +41,15 @@ constexpr int kSvcPullU = 4; // LL_PULL: 16-B vectors per lane per pass
 
 // element i of ring block b folds x_b, x_{b+1}, ..., x_{b+n-1} with the partial as the `in`
 // operand (coll_tuned_allreduce.c:470-512; the LL_RING program of ll_eval, without its tree form)
-template <class F, class X> __device__ __forceinline__ typename F::T svc_ring_fold(const LLArgs &a, uint64_t i, X x)
+template <class F> __device__ __forceinline__ typename F::T svc_ring_fold(const LLArgs &a, uint64_t i,
+                                                                        const RankRegs<typename F::T> &X)
 {
     const uint64_t se = a.split * a.early;
     const int b0 = (i < se) ? (int)(i / a.early) : (int)(a.split + (i - se) / a.late);
-    typename F::T acc = x(b0);
+    typename F::T acc = X.get(b0);
     for (int j = 1; j < a.n; ++j) {
         const int r = b0 + j >= a.n ? b0 + j - a.n : b0 + j;
-        acc = F::op2(x(r), acc);
+        acc = F::op2(X.get(r), acc);
     }
     return acc;
 }
@@ -86,14 +87,12 @@ template <class F> static __device__ void svc_pull(const LLArgs &a, const SvcCal
             if (v >= nvec) continue;
             V r;
 #pragma unroll
-            for (int e = 0; e < EPV; ++e)
-                r.e[e] = svc_ring_fold<F>(a, v * EPV + e, [&](int q) {
-                    T x = xv[u][0].e[e];
+            for (int e = 0; e < EPV; ++e) {
+                RankRegs<T> X;
 #pragma unroll
-                    for (int s2 = 1; s2 < kLLMaxRanks; ++s2)
-                        if (s2 == q) x = xv[u][s2].e[e];
-                    return x;
-                });
+                for (int q = 0; q < kLLMaxRanks; ++q) X.set(q, xv[u][q].e[e]);
+                r.e[e] = svc_ring_fold<F>(a, v * EPV + e, X);
+            }
             u32x4l out;
             __builtin_memcpy(&out, &r, 16);
             __builtin_amdgcn_raw_buffer_store_b128(out, ll_rsrc(a.dst), (unsigned)(v * 16), 0, kLLSysCoherent);
@@ -109,13 +108,10 @@ template <class F> static __device__ void svc_pull(const LLArgs &a, const SvcCal
             ll_read16<true>(static_cast<const char *>(sc.srcs[q]), i * sizeof(T), sizeof(T), w);
             __builtin_memcpy(&xs[q], w, sizeof(T));
         }
-        const T r = svc_ring_fold<F>(a, i, [&](int q) {
-            T x = xs[0];
+        RankRegs<T> X;
 #pragma unroll
-            for (int s2 = 1; s2 < kLLMaxRanks; ++s2)
-                if (s2 == q) x = xs[s2];
-            return x;
-        });
+        for (int q = 0; q < kLLMaxRanks; ++q) X.set(q, xs[q]);
+        const T r = svc_ring_fold<F>(a, i, X);
         uint32_t w[4] = {0, 0, 0, 0};
         __builtin_memcpy(w, &r, sizeof(T));
         ll_write16<true>(static_cast<char *>(a.dst), i * sizeof(T), sizeof(T), w);
@@ -290,6 +286,7 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
     __shared__ SvcCall sc;
     __shared__ uint64_t s_door;
     __shared__ int s_fail;
+    __shared__ uint64_t s_tr[kSvcTraceCols];  // (MI355X_SVC_TRACE, workgroup 0) this call's stamps
     const int t = (int)threadIdx.x;
     SvcPage *page = const_cast<SvcPage *>(g.page);
     uint64_t want = g.first;
@@ -343,11 +340,11 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
             __syncthreads();
             continue;
         }
-        uint64_t *tr = (g.trace && blockIdx.x == 0) ? g.trace + (want % kSvcTraceCalls) * kSvcTraceCols : nullptr;
+        uint64_t *tr = (g.trace && blockIdx.x == 0) ? s_tr : nullptr;
         if (tr && t == 0) {
+            for (int k = 0; k < kSvcTraceCols; ++k) tr[k] = 0;
             tr[0] = want;
             tr[1] = __builtin_amdgcn_s_memrealtime();
-            tr[8] = tr[9] = 0;  // (granule forms only)
         }
         // 2. the descriptor (stored before the doorbell; not rewritten before every participant
         // of this call is done) into LDS
@@ -410,19 +407,24 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
         // granule slices and 16-B vectors come 4 KiB per workgroup per step, the pull copy's words
         // and bytes less: striding by nwg while only part workgroups take part would skip some)
         const uint64_t stride = part;
+        // a slice's 16-B pieces are pushed by the other half of the workgroup than the one that
+        // receives and evaluates them: a wave's loads wait for its earlier stores to complete (one
+        // counter for both on gfx9), so the small calls' receiving waves (the first) never queue
+        // their polls behind the system-scope pushes
+        const unsigned pt = ((unsigned)t + kSvcThreads / 2) % kSvcThreads;
         for (uint64_t c0 = blockIdx.x; c0 < nchunks && !failed && !pull; c0 += stride * kSvcPass) {
             uint32_t w[kSvcPass][4];
 #pragma unroll
             for (int p = 0; p < kSvcPass; ++p) {
                 const uint64_t c = c0 + (uint64_t)p * stride;
-                if (c < nchunks) ll_read_slice<true>(a, ll_block(a, c), w[p]);
+                if (c < nchunks) ll_read_slice<true>(a, ll_block(a, c, pt), w[p]);
             }
             if (c0 == blockIdx.x && !ll_wait_acks(a)) failed = 1;
             if (failed) break;
 #pragma unroll
             for (int p = 0; p < kSvcPass; ++p) {
                 const uint64_t c = c0 + (uint64_t)p * stride;
-                if (c < nchunks) ll_push_slice(a, ll_block(a, c), w[p]);
+                if (c < nchunks) ll_push_slice(a, ll_block(a, c, pt), w[p]);
             }
         }
         if (tr && t == 0) tr[3] = __builtin_amdgcn_s_memrealtime();
@@ -465,7 +467,11 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
                     if (q != me) ll_store(a.peer_ack[q], want);
                 __hip_atomic_store(g.done, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
-            if (tr) tr[6] = __builtin_amdgcn_s_memrealtime();
+            if (tr) {
+                tr[6] = __builtin_amdgcn_s_memrealtime();
+                uint64_t *row = g.trace + (want % kSvcTraceCalls) * kSvcTraceCols;
+                for (int k = 0; k < kSvcTraceCols; ++k) row[k] = tr[k];
+            }
             s_fail = failed;
         }
         __syncthreads();

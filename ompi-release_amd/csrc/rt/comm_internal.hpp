@@ -347,7 +347,7 @@ struct mi355x_comm {
     size_t ll_bytes = 0;                          // LL region size (ll_resync)
     double create_us = 0, selftest_us = 0;
     bool svc_stuck = false;                       // a service kernel never left (its memory is leaked, never reused)
-    uint64_t *svc_trace = nullptr;                // MI355X_SVC_TRACE=1: stage stamps (pinned host), printed at destroy
+    uint64_t *svc_trace = nullptr;                // MI355X_SVC_TRACE=1: stage stamps (device memory), printed at destroy
     // pipelined allreduce (coll_pipe.hip): per-chunk ready flags in an uncached region that
     // every peer writes into (row q = flags raised by rank q), and the work-queue counter
     char *pipe_base = nullptr;
