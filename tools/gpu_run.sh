@@ -25,6 +25,12 @@
 #   p2p_lat        point-to-point ping-pong latency, host and device buffers, 8 B - 64 KiB -> p2p_lat.jsonl
 #   interference   the resident service beside compute streams (tools/svc_interference.py) -> svc_interference.jsonl
 #   ab_host        host-synchronised small-call latency, this tree vs a build staged in ab_old/ (A/B)
+#   prof_rehearsal rocprofv3 kernel trace of rank 0 of an N-rank (N=${N:-8}) allreduce rehearsal on the
+#                  default flow (--no-autotune): kernel average vs the line's kernel_avg_ms -> prof_n$N/
+#   pmc_rehearsal  FETCH_SIZE / WRITE_SIZE (separate passes) of rank 0 of an N-rank (N=${N:-2})
+#                  rehearsal -> pmc_rehearsal_n$N.json (what bench_coll.py reads as roofline.traffic)
+# (multi-rank profiles start every rank directly -- no launcher under the profiler -- with rank 0
+# under rocprofv3 and the others as plain processes)
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -44,6 +50,26 @@ run() {  # run NAME LIMIT CMD...: output to $O/NAME.log, tail on failure, exit o
         exit 1
     fi
 }
+
+ranks_bench() {  # ranks_bench NAME PROFILER_ARGS... -- rank 0 of an N-rank bench.py run under rocprofv3
+    local name=$1
+    shift
+    local args="--gpus $N --steps ${STEPS:-10} --warmup 3 --no-legs --no-cpu-baseline ${EXTRA:-}"
+    local pids=() rcs=0 r
+    port=$((port + 1))
+    for r in $(seq 1 $((N - 1))); do
+        MASTER_ADDR=127.0.0.1 WORLD_SIZE=$N MASTER_PORT=$port RANK=$r LOCAL_RANK=$r MI355X_TIMEOUT_S=60 \
+            timeout -k 10 400 python bench.py $args > $O/${name}_r$r.log 2>&1 &
+        pids+=($!)
+    done
+    MASTER_ADDR=127.0.0.1 WORLD_SIZE=$N MASTER_PORT=$port RANK=0 LOCAL_RANK=0 MI355X_TIMEOUT_S=60 \
+        timeout -k 10 400 rocprofv3 "$@" -d $O/$name -o run --output-format csv -- python bench.py $args > $O/${name}_r0.log 2>&1
+    local rc0=$?
+    for p in "${pids[@]}"; do wait $p || rcs=1; done
+    echo "== $name: rank0 rc=$rc0 others rc=$rcs"
+    [ $rc0 -eq 0 ] && [ $rcs -eq 0 ] || { tail -20 $O/${name}_r0.log; exit 1; }
+}
+port=29700
 
 small_c() {  # small_c NP REPS PATHS [sed tag]: one small_ar_c run, JSON lines appended to small.jsonl
     local n=$1 reps=$2 paths=$3
@@ -182,6 +208,16 @@ for step in "$@"; do
     interference)
         run interference 900 python tools/svc_interference.py --out $O/svc_interference.jsonl
         cat $O/svc_interference.jsonl ;;
+    prof_rehearsal)
+        N=${N:-8} STEPS=${STEPS:-20} EXTRA=--no-autotune ranks_bench prof_n${N:-8} --kernel-trace --stats
+        grep '^{' $O/prof_n${N:-8}_r0.log | tail -1 | cut -c1-1500
+        head -4 $O/prof_n${N:-8}/run_kernel_stats.csv | cut -c1-200 ;;
+    pmc_rehearsal)
+        n=${N:-2}
+        for c in FETCH_SIZE WRITE_SIZE; do N=$n ranks_bench pmc_reh_n${n}_$c --pmc $c; done
+        python tools/pmc_summary.py $O/pmc_reh_n${n}_FETCH_SIZE $O/pmc_reh_n${n}_WRITE_SIZE $O/pmc_rehearsal_n$n.json \
+            "k_pipe_allreduce=k_pipe_allreduce_rehearsal_n$n" "k_fold=k_fold_rehearsal_n$n" || exit 1
+        cat $O/pmc_rehearsal_n$n.json ;;
     *)
         echo "unknown step $step"
         exit 2 ;;
