@@ -280,6 +280,62 @@ def svc_rs_checks(pkg, comm, rank, size, oracle, torch):
     return served
 
 
+def svc_all_slots(pkg, comm, rank, size, oracle, torch):
+    """every (op, type) slot through the resident service -- the LL form's tree program (recursive
+    doubling, < 10000 B), its ring order, and the reduce-scatter form -- against the oracle's
+    schedule simulation.  The service's evaluation keeps the ranks' values of an element in one
+    vector register tuple for the integer and floating types and in an array for the others
+    (complex, value-index pairs), so every element type is run, not a sample"""
+    ptrs = lambda arrs: (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    saved = comm.get("SVC_MAX_BYTES")
+    comm.set("SVC_MAX_BYTES", 32 << 10)
+    calls0 = comm.get("SVC_CALLS")
+    bad = []
+    k = ncalls = 0
+    for code in range(1, 13):
+        for ty in range(len(pkg.TYPES)):
+            if not (oracle.oracle_has_op(code, ty) and pkg.op_supported(code, ty)):
+                continue
+            tname, opname = pkg.TYPES[ty], pkg.OPS[code]
+            esz = pkg.type_size(ty)
+            for count in (3 + k % 5, (12 << 10) // esz + k % 7):
+                xs = [opdata.make(tname, count, 9000 + 11 * k + r) for r in range(size)]
+                outs = [np.zeros_like(xs[0]) for _ in range(size)]
+                ran = oracle.oracle_allreduce(0, size, count, ty, code, 0, ptrs(xs), ptrs(outs))
+                dx = torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda()
+                dr = torch.full_like(dx, 0x5a)
+                torch.cuda.synchronize()
+                comm.allreduce(dx.data_ptr(), dr.data_ptr(), count, ty, code)
+                ncalls += 1
+                try:
+                    opdata.assert_same(tname, opname, dr.cpu().numpy().view(xs[0].dtype), outs[rank],
+                                       f"service slot {opname}/{tname} count={count}")
+                    assert comm.last_algorithm() == ran, (opname, tname, count, comm.last_algorithm(), ran)
+                except AssertionError as e:
+                    bad.append(str(e)[:300])
+            rcount = 5 + k % 9
+            xs = [opdata.make(tname, rcount * size, 9500 + 11 * k + r) for r in range(size)]
+            outs = [np.zeros(rcount, dtype=xs[0].dtype) for _ in range(size)]
+            assert oracle.oracle_reduce_scatter_block(size, rcount, ty, code, ptrs(xs), ptrs(outs)) >= 0
+            dx = torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda()
+            dr = torch.full((rcount * esz,), 0x5a, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
+            comm.reduce_scatter_block(dx.data_ptr(), dr.data_ptr(), rcount, ty, code)
+            ncalls += 1
+            try:
+                opdata.assert_same(tname, opname, dr.cpu().numpy().view(xs[0].dtype), outs[rank],
+                                   f"service rsb slot {opname}/{tname} rcount={rcount}")
+            except AssertionError as e:
+                bad.append(str(e)[:300])
+            k += 1
+    served = comm.get("SVC_CALLS") - calls0
+    comm.set("SVC_MAX_BYTES", saved)
+    assert not bad, "\n".join(bad[:8])
+    assert k >= 100, k  # every GPU slot ran
+    assert served == ncalls, f"the service served {served} of {ncalls} calls"
+    print(f"rank {rank} service slots OK ({k} slots, {served} service calls)", flush=True)
+
+
 def staged(pkg, comm, rank, size, torch, key):
     """allocations too large for hipIpc* (forced here: every allocation; for real: >= 2 GiB, which
     hipIpcOpenMemHandle cannot map on this platform) through real IPC, twice: on a communicator
@@ -1159,6 +1215,8 @@ def _main():
     served, launches = comm.get("SVC_CALLS") - calls0, comm.get("SVC_LAUNCHES")
     assert served > 100, f"the resident service served {served} calls"
     print(f"rank {rank} resident service: {served} calls, {launches} launches", flush=True)
+    if size in (2, 3):
+        svc_all_slots(pkg, comm, rank, size, oracle, torch)
     svc_pull_checks(pkg, comm, rank, size, oracle, torch)
     p2p_checks(pkg, comm, rank, size, oracle, torch)
     _fd_report(rank)

@@ -37,7 +37,8 @@ def test_ipc_ranks(gpu, size):
     for r, p in enumerate(procs):
         stages = ("pipe OK", "LL OK", "SVC OK", "pull OK", "p2p OK", "staged OK", "OK") + (("bcast4g OK",) if size in (2, 3) else ()) \
             + (("maxcount OK",) if size == 2 else ()) \
-            + (("pipe slots OK",) if size == 3 else ())
+            + (("pipe slots OK",) if size == 3 else ()) \
+            + (("service slots OK",) if size in (2, 3) else ())
         for stage in stages:
             assert f"rank {r} {stage}" in outs[r], f"rank {r} did not report '{stage}':\n{outs[r][-3000:]}"
 
