@@ -286,7 +286,9 @@ def run(args, pkg, torch):
     ty, op = pkg.T["FLOAT"], pkg.OP["SUM"]
     # data-flow / launch-shape autotune on the real size, with an exactness check on every
     # candidate (check_calls: data that changes per call, rbuf poisoned first).  Candidates: the pipelined
-    # flow (one launch: fold + pulls with device-side chunk flags; workgroups per CU x chunk size)
+    # flow (one launch: fold + pulls with device-side chunk flags; workgroups per CU x chunk size:
+    # the engine's own (~512 chunks per block, >= 64 KiB: 256 KiB at n = 8), 512 KiB and 2 MiB, so
+    # separate GPUs' link latency picks its own overlap granularity)
     # and the two-phase flow (fold -> host barrier -> pull; grid cap).  All ranks see the same
     # max-over-ranks times, so they pick the same candidate.  Push is not a candidate: its remote
     # writes land behind the owner's L2 (coarse-grained memory is not probed) -- single device only.
@@ -295,7 +297,7 @@ def run(args, pkg, torch):
     want = world * (world + 1) / 2
     ok = True
     cands = [{"pipe": 1, "pipe_wg_per_cu": wg, "pipe_chunk_kib": ck, "pipe_wt": wt}
-             for wt in (0, 1) for wg in (1, 2, 4, 8) for ck in (0, 2048)]
+             for wt in (0, 1) for wg in (1, 2, 4, 8) for ck in (0, 512, 2048)]
     cands += [{"pipe": 0, "blocks_per_cu": bpc, "copy_block_kib": 4} for bpc in (8, 1024)]
     if getattr(args, "no_autotune", False):  # the engine's defaults only
         cands = [{"pipe": comm.get("PIPE"), "pipe_wg_per_cu": comm.get("PIPE_WG_PER_CU"),
