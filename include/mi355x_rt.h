@@ -220,9 +220,13 @@ enum mi355x_knob {
     MI355X_KNOB_SVC_OWNER = 33,         /* (read-only) 1 while this communicator owns its process's
                                            resident service */
     MI355X_KNOB_SVC_CLAIMS = 34,        /* (read-only) times this communicator has taken the service */
-    MI355X_KNOB_SVC_IDLE_US = 35        /* (per communicator, same value on every rank; env MI355X_SVC_IDLE_MS at
+    MI355X_KNOB_SVC_IDLE_US = 35,       /* (per communicator, same value on every rank; env MI355X_SVC_IDLE_MS at
                                            creation, default 1000) microseconds the resident service stays
                                            without a call before it leaves (applies from its next launch) */
+    MI355X_KNOB_SVC_SHRINK_US = 36,     /* (per communicator; env MI355X_SVC_SHRINK_US, default 100; 0: never)
+                                           microseconds without a call after which every workgroup of the
+                                           service but the first leaves (applies from its next launch) */
+    MI355X_KNOB_SVC_REGROWS = 37        /* (read-only) calls that relaunched a shrunk service's full grid */
 };
 /* cross-device flows (MI355X_KNOB_FLOWS) */
 enum mi355x_flow {

@@ -1268,6 +1268,8 @@ static int svc_launch(mi355x_comm *c, uint64_t first)
     std::memset(&g, 0, sizeof(g));
     c->svc_page->ctr = 0;  // not resident: nothing else touches them
     c->svc_page->go = 0;
+    c->svc_page->shrink = 0;
+    c->svc_host[2] = 0;
     _mm_sfence();
     g.page = c->svc_page;
     g.done = svc_done_word(c);
@@ -1278,6 +1280,8 @@ static int svc_launch(mi355x_comm *c, uint64_t first)
     g.slot_gran = c->ll_slot / 4;
     g.idle_ticks = (uint64_t)(c->svc_idle_s * 1e8);  // s_memrealtime: 100 MHz
     g.timeout_ticks = (uint64_t)(c->timeout_s * 1e8);
+    g.shrink_ticks = (uint64_t)(c->svc_shrink_s * 1e8);
+    g.shrunk = c->svc_host + 2;
     g.n = c->size;
     g.me = c->rank;
     g.nwg = c->svc_nwg;
@@ -1322,6 +1326,13 @@ static void svc_park(mi355x_comm *c)
 static int svc_call(mi355x_comm *c, const SvcCall &call, uint64_t part)
 {
     const uint64_t seq = call.seq;
+    // a service shrunk to its first workgroup while idle serves up to kSvcShrunkMaxPart slices
+    // alone; a call that wants more (the pull forms) relaunches the full grid first
+    if (std::min<uint64_t>(part, (uint64_t)c->svc_nwg) > kSvcShrunkMaxPart && svc_resident(c->svcq) &&
+        __atomic_load_n(c->svc_host + 2, __ATOMIC_ACQUIRE)) {
+        if (!svc_stop(c)) return set_error(MI355X_ERR_TIMEOUT, "rank %d: the resident service did not leave", c->rank);
+        c->svc_regrows++;
+    }
     std::memcpy(&c->svc_page->call, &call, sizeof(call));
     svc_ring(c, (seq << kSvcPartBits) | std::min<uint64_t>(std::max<uint64_t>(part, 1), (uint64_t)c->svc_nwg));
     int rc = MI355X_SUCCESS;
@@ -2035,6 +2046,7 @@ static void svc_setup(mi355x_comm *c)
 {
     c->svc_max = (size_t)std::max(0.0, env_double("MI355X_SVC_MAX_BYTES", (double)c->svc_max));
     c->svc_idle_s = std::max(0.0001, env_double("MI355X_SVC_IDLE_MS", c->svc_idle_s * 1e3) * 1e-3);
+    c->svc_shrink_s = std::max(0.0, env_double("MI355X_SVC_SHRINK_US", c->svc_shrink_s * 1e6) * 1e-6);
     c->svc_nwg = (int)std::min(64.0, std::max(1.0, env_double("MI355X_SVC_WGS", (double)c->svc_nwg)));
     c->svc_pull_max = (size_t)std::max(0.0, env_double("MI355X_SVC_PULL_MAX_BYTES", (double)c->svc_pull_max));
     c->svc_copy_max = (size_t)std::max(0.0, env_double("MI355X_SVC_PULL_COPY_MAX_BYTES", (double)c->svc_copy_max));
@@ -2944,6 +2956,8 @@ int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
     case MI355X_KNOB_SVC_OWNER: *value = c->svc_ok ? 1 : 0; break;
     case MI355X_KNOB_SVC_CLAIMS: *value = (long)c->svc_epoch; break;
     case MI355X_KNOB_SVC_IDLE_US: *value = (long)(c->svc_idle_s * 1e6 + 0.5); break;
+    case MI355X_KNOB_SVC_SHRINK_US: *value = (long)(c->svc_shrink_s * 1e6 + 0.5); break;
+    case MI355X_KNOB_SVC_REGROWS: *value = (long)c->svc_regrows; break;
     case MI355X_KNOB_RCACHE_MAX_MAPS: *value = (long)c->rcache_max_maps; break;
     case MI355X_KNOB_RCACHE_SIZE_LIMIT: *value = (long)c->rcache_limit; break;
     case MI355X_KNOB_PEER_MAPS: {
@@ -3046,10 +3060,12 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
         rcache_trim(c, nullptr);
         break;
     }
+    case MI355X_KNOB_SVC_SHRINK_US:
     case MI355X_KNOB_SVC_IDLE_US:
-        if (value < 100 || value > 60000000) return set_error(MI355X_ERR_ARG, "svc_idle_us out of range");
+        if (knob == MI355X_KNOB_SVC_SHRINK_US ? (value < 0 || value > 60000000) : (value < 100 || value > 60000000))
+            return set_error(MI355X_ERR_ARG, "%s out of range", knob == MI355X_KNOB_SVC_SHRINK_US ? "svc_shrink_us" : "svc_idle_us");
         drain(c);
-        c->svc_idle_s = (double)value * 1e-6;
+        (knob == MI355X_KNOB_SVC_SHRINK_US ? c->svc_shrink_s : c->svc_idle_s) = (double)value * 1e-6;
         {  // a resident service picks the new limit up at its next launch (g_svc_mtx: not while a
            // revoker detaches this communicator)
             std::lock_guard<std::mutex> g(g_svc_mtx);

@@ -137,8 +137,14 @@ struct SvcPage {                      // the doorbell page
     uint64_t go;                      // workgroup 0's verdict on call `want`: want = serve it, kSvcQuit =
                                       // leave (zeroed by the host before every launch)
     uint64_t pad2[15];
+    uint64_t shrink;                  // set by workgroup 0 once idle for shrink_ticks: the other
+                                      // workgroups leave (zeroed by the host before every launch)
+    uint64_t pad3[15];
     SvcCall call;
 };
+// a shrunk service (workgroup 0 alone) serves calls of up to this many 4-KiB slices by itself (the
+// LL form: 32 KiB); a call that wants more workgroups makes the host relaunch the full grid
+constexpr uint64_t kSvcShrunkMaxPart = 8;
 struct SvcArgs {                      // fixed for one launch
     const SvcPage *page;
     uint64_t *done;                   // host word: number of the last call completed
@@ -147,6 +153,8 @@ struct SvcArgs {                      // fixed for one launch
     char *peer_ll[kLLMaxRanks];       // every rank's LL region, mapped
     uint64_t first;                   // the call number this launch serves first
     uint64_t slot_gran, idle_ticks, timeout_ticks;
+    uint64_t shrink_ticks;            // idle time after which the other workgroups leave (0: never)
+    uint64_t *shrunk;                 // host word: set when they have been told to
     int32_t n, me, nwg, probe;        // probe: return at once (loads the code object)
     uint64_t *trace;                  // NULL, or kSvcTraceCalls rows of kSvcTraceCols words (MI355X_SVC_TRACE)
 };

@@ -291,6 +291,7 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
     SvcPage *page = const_cast<SvcPage *>(g.page);
     uint64_t want = g.first;
     uint64_t idle0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t nalive = (uint64_t)g.nwg;  // (workgroup 0, thread 0) workgroups still resident
     for (;;) {
         // 1. the doorbell: (call number << kSvcPartBits) | participating workgroups.  Workgroup 0
         // alone decides whether the next call is served or the service leaves (quit request, idle,
@@ -306,17 +307,35 @@ extern "C" __global__ __launch_bounds__(kSvcThreads) void mi355x_k_svc(SvcArgs g
                     v = __hip_atomic_load(&page->door, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     if ((v >> kSvcPartBits) >= want) break;
                     __builtin_amdgcn_s_sleep(2);
-                    if (__builtin_amdgcn_s_memrealtime() - idle0 > g.idle_ticks) {
+                    const uint64_t idle = __builtin_amdgcn_s_memrealtime() - idle0;
+                    if (idle > g.idle_ticks) {
                         v = kSvcQuit;
                         break;
                     }
+                    // idle between calls (every participant of the last call is done): the other
+                    // workgroups leave, so a service waiting through a compute phase holds one CU
+                    // instead of nwg; it serves the small calls alone from then on
+                    if (nalive > 1 && g.shrink_ticks && idle > g.shrink_ticks) {
+                        nalive = 1;
+                        __hip_atomic_store(&page->shrink, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        __hip_atomic_store(g.shrunk, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
                 }
                 if ((v >> kSvcPartBits) != want) v = kSvcQuit;
+                // the participants: as many as the host asked for, of those still resident
+                if (v != kSvcQuit && (v & ((1u << kSvcPartBits) - 1)) > nalive)
+                    v = (v & ~(uint64_t)((1u << kSvcPartBits) - 1)) | nalive;
                 __hip_atomic_store(&page->go, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             } else {
                 for (;;) {  // (bounded too: never longer than the leader's idle limit plus a timeout)
                     v = __hip_atomic_load(&page->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     if ((v >> kSvcPartBits) >= want) break;
+                    // told to leave while idle: workgroup 0 never again counts this one in (it sets
+                    // `shrink` only between calls, and its later verdicts name itself alone)
+                    if (__hip_atomic_load(&page->shrink, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+                        v = kSvcQuit;
+                        break;
+                    }
                     __builtin_amdgcn_s_sleep(2);
                     if (__builtin_amdgcn_s_memrealtime() - idle0 > g.idle_ticks + g.timeout_ticks) {
                         v = kSvcQuit;

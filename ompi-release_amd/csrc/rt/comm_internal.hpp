@@ -300,12 +300,16 @@ struct mi355x_comm {
     mi355x::SvcQueue *svcq = nullptr;
     mi355x::SvcPage *svc_page = nullptr;          // doorbell page (host-writable; device address == host address)
     bool svc_page_dev = false;                    // the page is fine-grained device memory (else pinned host)
-    uint64_t *svc_host = nullptr;                 // pinned host words: [0] call completed, [1] error word
+    uint64_t *svc_host = nullptr;                 // pinned host words: [0] call completed, [1] error word, [2] shrunk
     int svc_nwg = 16;                             // workgroups of the service (16 x 4 KiB slices per pass)
     // the service leaves after this long without a call (MI355X_SVC_IDLE_MS, default 1 ms): a burst
     // of small calls keeps it resident, a call after a longer gap relaunches it
     double svc_idle_s = 0.001;
-    uint64_t svc_calls = 0, svc_launches = 0;
+    // ... and after this long without a call all its workgroups but the first leave
+    // (MI355X_SVC_SHRINK_US, default 100 us; 0: never): between bursts the service holds one CU, and
+    // serves the small calls alone; a call of more than kSvcShrunkMaxPart slices relaunches the grid
+    double svc_shrink_s = 100e-6;
+    uint64_t svc_calls = 0, svc_launches = 0, svc_regrows = 0;
     // one-phase ring-ordered allreduce above svc_max and up to svc_pull_max bytes per rank served by
     // the service from the peers' mapped inputs (LL_PULL; MI355X_SVC_PULL_MAX_BYTES); also the
     // largest block of a reduce_scatter(_block) the service evaluates (LL_PULL_RS, any size up to it)

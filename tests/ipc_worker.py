@@ -739,6 +739,20 @@ def svc_mode(key, rank, size, dev):
     assert b.get("SVC_OWNER") == 1 and a.get("SVC_OWNER") == 0, (b.get("SVC_OWNER"), a.get("SVC_OWNER"))
     assert b.get("SVC_CALLS") > 0
     handed = b.get("SVC_CALLS")
+    # idle longer than SVC_SHRINK_US (100 us) but not the idle limit: every workgroup but the first
+    # leaves; a small call is served by it alone (no launch), a 16-slice call relaunches the full grid
+    assert b.get("SVC_SHRINK_US") == 100
+    l0, g0 = b.get("SVC_LAUNCHES"), b.get("SVC_REGROWS")
+    for k in range(3):
+        time.sleep(0.002)
+        ar(b, k)
+    assert b.get("SVC_LAUNCHES") == l0 and b.get("SVC_REGROWS") == g0, "the shrunk service serves small calls"
+    xb = torch.full((16384,), float(rank + 1), device="cuda")  # 64 KiB: 16 slices
+    yb = torch.empty_like(xb)
+    torch.cuda.synchronize()
+    b.allreduce(xb.data_ptr(), yb.data_ptr(), xb.numel(), f32, SUM)
+    assert bool(torch.all(yb == want).item()), "allreduce after the grid regrew"
+    assert b.get("SVC_REGROWS") == g0 + 1 and b.get("SVC_LAUNCHES") == l0 + 1, (b.get("SVC_REGROWS"), b.get("SVC_LAUNCHES"))
     for k in range(5):  # a without the service: the per-call paths, exact
         ar(a, k)
     # idle exit and relaunch (a short idle limit on a fresh owner)

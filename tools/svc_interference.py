@@ -12,10 +12,12 @@ calls without compute.
 Variants, interleaved in ONE process pair (both ranks on the box's one GPU, so the two processes
 also contend with each other; on separate GPUs each process has its GPU to itself), repeated:
   svc_off        SVC_MAX_BYTES = 0: every small call takes the host-synchronised flow
-  idle_<t>ms     the service on, leaving after t ms without a call (MI355X_KNOB_SVC_IDLE_US)
+  idle_<t>ms     the service on, leaving after t ms without a call (MI355X_KNOB_SVC_IDLE_US), its
+                 workgroups but the first leaving after 100 us (the default, MI355X_KNOB_SVC_SHRINK_US)
+  idle_<t>ms_full  the same with the whole grid resident until it leaves (SVC_SHRINK_US = 0)
 
 usage: python tools/svc_interference.py [--out FILE] [--variants svc_off,idle_0.1ms,idle_1ms,idle_5ms]
-       [--intervals 50,200,500] [--reps 3]
+       [--intervals 50,200,500] [--reps 3]   (default variants: svc_off,idle_0.1ms,idle_1ms,idle_1ms_full,idle_5ms)
 """
 import argparse
 import json
@@ -39,6 +41,7 @@ def rank_main(rank, key, variants, intervals, window_ms, reps):
     comm = pkg.Comm.create(key, rank, 2, 0)
     f32, SUM = pkg.T["FLOAT"], pkg.OP["SUM"]
     svc_max = comm.get("SVC_MAX_BYTES")
+    shrink_default = comm.get("SVC_SHRINK_US")
     streams = [torch.cuda.Stream() for _ in range(4)]
     big = [torch.empty(32 << 20, device="cuda") for _ in range(8)]  # 128 MiB each
     a = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
@@ -106,8 +109,10 @@ def rank_main(rank, key, variants, intervals, window_ms, reps):
         if var == "svc_off":
             comm.set("SVC_MAX_BYTES", 0)
         else:
+            full = var.endswith("_full")
             comm.set("SVC_MAX_BYTES", svc_max)
-            comm.set("SVC_IDLE_US", int(float(var[len("idle_"):-2]) * 1000))
+            comm.set("SVC_SHRINK_US", 0 if full else shrink_default)
+            comm.set("SVC_IDLE_US", int(float(var[len("idle_"):].split("ms")[0]) * 1000))
 
     rows = []
     for rep in range(reps):
@@ -144,7 +149,7 @@ def main():
     ap.add_argument("--key", default="")
     ap.add_argument("--intervals", default="50,200,500")
     ap.add_argument("--window-ms", type=float, default=400.0)
-    ap.add_argument("--variants", default="svc_off,idle_0.1ms,idle_1ms,idle_5ms")
+    ap.add_argument("--variants", default="svc_off,idle_0.1ms,idle_1ms,idle_1ms_full,idle_5ms")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default="")
     a = ap.parse_args()
