@@ -141,6 +141,14 @@ extern int mca_coll_mi355x_mixed_buffers;       /* 1 = ranks may mix host and de
 extern int mca_coll_mi355x_rcache_max_maps;     /* peer mappings kept open per communicator (0 = unlimited) */
 extern unsigned long long mca_coll_mi355x_rcache_size_limit; /* the same in bytes (mpool_rgpusm_rcache_size_limit) */
 
+/* Reductions the engine declines (user-defined ops; types with no engine slot) go to the
+ * lower-priority component with every device buffer staged through host memory, as coll/cuda does
+ * (coll_cuda_allreduce.c:43-75): this counts those staged calls. */
+extern unsigned long mca_coll_mi355x_staged_calls;
+/* the op slot the engine reduces a datatype as (OMPI-predefined, ompi_op_ddt_map, extent = the
+ * slot's element), or -1 */
+int mca_coll_mi355x_reducible_type(const struct ompi_datatype_t *dt);
+
 #ifdef __cplusplus
 }
 #endif

@@ -57,8 +57,14 @@ int mi355x_event_elapsed_ms(void *start, void *stop, float *ms);
 
 /* ---------------------------------------------------------------- op/hip kernels */
 /* 1 if (op,type) has a GPU kernel.  Slots absent from the reference table are 0, and so are
- * the x87 `long double` slots (no 80-bit format on CDNA4; op/hip stages those to the host). */
+ * the x87 `long double` SUM/PROD slots (no 80-bit arithmetic on CDNA4; op/hip stages those to the
+ * host base loops).  The x87 compare-only slots -- MAX/MIN on MPI_LONG_DOUBLE, MAXLOC/MINLOC on
+ * MPI_LONG_DOUBLE_INT -- are GPU kernels (exact x87 ordering on the 80-bit encoding). */
 int mi355x_op_supported(int op, int type);
+/* 1 if the collective engine (mi355x_allreduce & co.) reduces (op,type) on the device: the
+ * op/hip slots less MPI_LONG_DOUBLE_INT (32-byte pairs).  coll/mi355x stages the others to the
+ * lower-priority component through host memory (coll/cuda's rule, coll_cuda_allreduce.c:43-75). */
+int mi355x_comm_op_supported(int op, int type);
 size_t mi355x_type_size(int type);
 
 /* 2-buff: inout[i] = inout[i] (op) in[i], count elements, asynchronous on `stream`.

@@ -210,6 +210,15 @@ typedef struct opal_datatype_t {
 #define OPAL_DATATYPE_FLAG_PREDEFINED 0x0002  /* opal/datatype/opal_datatype.h:66 */
 #define OPAL_DATATYPE_FLAG_CONTIGUOUS 0x0010  /* :69 */
 #define OPAL_DATATYPE_FLAG_NO_GAPS 0x0020     /* :70, contiguous and extent == size */
+#define OPAL_DATATYPE_FLAG_COMMITTED 0x0004   /* :67 */
+#define OPAL_DATATYPE_FLAG_DATA 0x0100        /* :73 */
+/* predefined as an MPI type, not necessarily as an OPAL type: libmpi clears the OPAL flag and sets
+ * this one on the MPI-2 pair types (ompi/datatype/ompi_datatype.h:51-52, ompi_datatype_module.c:
+ * 415-416, 431-432); ompi_datatype_is_predefined tests it (ompi_datatype.h:149-152) */
+#define OMPI_DATATYPE_FLAG_PREDEFINED 0x0200
+#define OMPI_DATATYPE_FLAG_DATA_INT 0x1000    /* ompi_datatype.h:54 */
+#define OMPI_DATATYPE_FLAG_DATA_FLOAT 0x2000  /* :55 */
+#define OMPI_DATATYPE_FLAG_DATA_C 0x4000      /* :59 */
 
 /* ompi/datatype/ompi_datatype.h:73-88 */
 typedef struct ompi_datatype_t {

@@ -16,9 +16,12 @@
  *   op destruction                   ompi/op/op.c:476-487
  *   coll selection                   ompi/mca/coll/base/coll_base_comm_select.c:114-262
  */
+#define _GNU_SOURCE /* RTLD_DEFAULT */
 #include "ompi_mini.h"
 
+#include <dlfcn.h>
 #include <fcntl.h>
+#include <stdarg.h>
 #include <sched.h>
 #include <stdatomic.h>
 #include <stdio.h>
@@ -79,29 +82,98 @@ opal_class_t mca_coll_base_module_t_class = {"mca_coll_base_module_t", &opal_obj
 /* ------------------------------------------------------------------ datatypes / ddt map */
 int ompi_op_ddt_map[OMPI_DATATYPE_MPI_MAX_PREDEFINED];
 
-static struct { int id, slot; size_t size; const char *name; } predefined[] = {
-    {0x01, MI355X_T_INT8, 1, "MPI_INT8_T"},      {0x02, MI355X_T_UINT8, 1, "MPI_UINT8_T"},
-    {0x03, MI355X_T_INT16, 2, "MPI_INT16_T"},    {0x04, MI355X_T_UINT16, 2, "MPI_UINT16_T"},
-    {0x05, MI355X_T_INT32, 4, "MPI_INT32_T"},    {0x06, MI355X_T_UINT32, 4, "MPI_UINT32_T"},
-    {0x07, MI355X_T_INT64, 8, "MPI_INT64_T"},    {0x08, MI355X_T_UINT64, 8, "MPI_UINT64_T"},
-    {0x09, MI355X_T_FLOAT, 4, "MPI_FLOAT"},      {0x0A, MI355X_T_DOUBLE, 8, "MPI_DOUBLE"},
-    {0x0B, MI355X_T_LONG_DOUBLE, 16, "MPI_LONG_DOUBLE"},
-    {0x11, MI355X_T_BOOL, 1, "MPI_CXX_BOOL"},    {0x13, MI355X_T_UINT8, 1, "MPI_CHARACTER"},
-    {0x1A, MI355X_T_2INT, 8, "MPI_2INT"},        {0x20, MI355X_T_FLOAT_INT, 8, "MPI_FLOAT_INT"},
-    {0x21, MI355X_T_DOUBLE_INT, 16, "MPI_DOUBLE_INT"},
-    {0x22, MI355X_T_LONG_DOUBLE_INT, 32, "MPI_LONG_DOUBLE_INT"},
-    {0x23, MI355X_T_LONG_INT, 16, "MPI_LONG_INT"}, {0x24, MI355X_T_SHORT_INT, 8, "MPI_SHORT_INT"},
-    {0x27, MI355X_T_BOOL, 1, "MPI_C_BOOL"},
-    {0x29, MI355X_T_C_FLOAT_COMPLEX, 8, "MPI_C_FLOAT_COMPLEX"},
-    {0x2A, MI355X_T_C_DOUBLE_COMPLEX, 16, "MPI_C_DOUBLE_COMPLEX"},
-    {0x2B, MI355X_T_C_LONG_DOUBLE_COMPLEX, 32, "MPI_C_LONG_DOUBLE_COMPLEX"},
+/* The predefined types as libmpi leaves them after ompi_datatype_init.  The basic C types are
+ * OPAL basic types (OPAL_DATATYPE_FLAG_BASIC, opal_datatype.h:78-82) that are also MPI-predefined
+ * (OMPI_DATATYPE_INIT_PREDEFINED_BASIC_TYPE, ompi_datatype_internal.h:406-414).  The MPI-2 pair
+ * types are built as a contiguous block or a struct, committed, and then have the OPAL predefined
+ * flag cleared and the MPI one set (DECLARE_MPI2_COMPOSED_{STRUCT,BLOCK}_DDT,
+ * ompi_datatype_module.c:391-437, instantiated :471-509): their size, bounds and contiguity are
+ * what opal_datatype_add computes for the x86-64 C struct -- MPI_DOUBLE_INT / MPI_LONG_INT are 12
+ * bytes in a 16-byte extent, MPI_SHORT_INT 6 bytes with a hole at 2..4 in 8, MPI_LONG_DOUBLE_INT
+ * 20 in 32 -- and their description is the two (or one block of two) basic elements.
+ * tests/test_boundary.py checks every pair row against oracle/opal_types.py's restatement. */
+#define F_BASIC (OPAL_DATATYPE_FLAG_PREDEFINED | OPAL_DATATYPE_FLAG_CONTIGUOUS | OPAL_DATATYPE_FLAG_NO_GAPS | \
+                 OPAL_DATATYPE_FLAG_DATA | OPAL_DATATYPE_FLAG_COMMITTED | OMPI_DATATYPE_FLAG_PREDEFINED)
+#define F_PAIR (OPAL_DATATYPE_FLAG_DATA | OPAL_DATATYPE_FLAG_COMMITTED | OMPI_DATATYPE_FLAG_PREDEFINED | \
+                OMPI_DATATYPE_FLAG_DATA_C)
+#define F_CNG (OPAL_DATATYPE_FLAG_CONTIGUOUS | OPAL_DATATYPE_FLAG_NO_GAPS)
+enum { O_INT2 = 5, O_INT4 = 6, O_INT8 = 7, O_FLOAT4 = 15, O_FLOAT8 = 16, O_FLOAT16 = 18 }; /* opal_datatype_internal.h:107-131 */
+static const struct mini_predef {
+    int id, slot;
+    size_t size;
+    ptrdiff_t ext, true_ub;
+    uint16_t flags;
+    const char *name;
+    int ne;                                                    /* description elements (pair types) */
+    struct { uint16_t type; uint32_t count; int64_t ext, disp; } e[2];
+} predefined[] = {
+    {0x01, MI355X_T_INT8, 1, 1, 1, F_BASIC, "MPI_INT8_T", 0, {{0}}},
+    {0x02, MI355X_T_UINT8, 1, 1, 1, F_BASIC, "MPI_UINT8_T", 0, {{0}}},
+    {0x03, MI355X_T_INT16, 2, 2, 2, F_BASIC, "MPI_INT16_T", 0, {{0}}},
+    {0x04, MI355X_T_UINT16, 2, 2, 2, F_BASIC, "MPI_UINT16_T", 0, {{0}}},
+    {0x05, MI355X_T_INT32, 4, 4, 4, F_BASIC, "MPI_INT32_T", 0, {{0}}},
+    {0x06, MI355X_T_UINT32, 4, 4, 4, F_BASIC, "MPI_UINT32_T", 0, {{0}}},
+    {0x07, MI355X_T_INT64, 8, 8, 8, F_BASIC, "MPI_INT64_T", 0, {{0}}},
+    {0x08, MI355X_T_UINT64, 8, 8, 8, F_BASIC, "MPI_UINT64_T", 0, {{0}}},
+    {0x09, MI355X_T_FLOAT, 4, 4, 4, F_BASIC, "MPI_FLOAT", 0, {{0}}},
+    {0x0A, MI355X_T_DOUBLE, 8, 8, 8, F_BASIC, "MPI_DOUBLE", 0, {{0}}},
+    {0x0B, MI355X_T_LONG_DOUBLE, 16, 16, 16, F_BASIC, "MPI_LONG_DOUBLE", 0, {{0}}},
+    {0x11, MI355X_T_BOOL, 1, 1, 1, F_BASIC, "MPI_CXX_BOOL", 0, {{0}}},
+    {0x13, MI355X_T_UINT8, 1, 1, 1, F_BASIC, "MPI_CHARACTER", 0, {{0}}},
+    {0x1A, MI355X_T_2INT, 8, 8, 8, F_PAIR | F_CNG | OMPI_DATATYPE_FLAG_DATA_INT, "MPI_2INT", 1,
+     {{O_INT4, 2, 4, 0}}},
+    {0x20, MI355X_T_FLOAT_INT, 8, 8, 8, F_PAIR | F_CNG, "MPI_FLOAT_INT", 2, {{O_FLOAT4, 1, 4, 0}, {O_INT4, 1, 4, 4}}},
+    {0x21, MI355X_T_DOUBLE_INT, 12, 16, 12, F_PAIR | OPAL_DATATYPE_FLAG_CONTIGUOUS, "MPI_DOUBLE_INT", 2,
+     {{O_FLOAT8, 1, 8, 0}, {O_INT4, 1, 4, 8}}},
+    {0x22, MI355X_T_LONG_DOUBLE_INT, 20, 32, 20, F_PAIR | OPAL_DATATYPE_FLAG_CONTIGUOUS, "MPI_LONG_DOUBLE_INT", 2,
+     {{O_FLOAT16, 1, 16, 0}, {O_INT4, 1, 4, 16}}},
+    {0x23, MI355X_T_LONG_INT, 12, 16, 12, F_PAIR | OPAL_DATATYPE_FLAG_CONTIGUOUS | OMPI_DATATYPE_FLAG_DATA_INT,
+     "MPI_LONG_INT", 2, {{O_INT8, 1, 8, 0}, {O_INT4, 1, 4, 8}}},
+    {0x24, MI355X_T_SHORT_INT, 6, 8, 8, F_PAIR | OMPI_DATATYPE_FLAG_DATA_INT, "MPI_SHORT_INT", 2,
+     {{O_INT2, 1, 2, 0}, {O_INT4, 1, 4, 4}}},
+    {0x27, MI355X_T_BOOL, 1, 1, 1, F_BASIC, "MPI_C_BOOL", 0, {{0}}},
+    {0x29, MI355X_T_C_FLOAT_COMPLEX, 8, 8, 8, F_BASIC, "MPI_C_FLOAT_COMPLEX", 0, {{0}}},
+    {0x2A, MI355X_T_C_DOUBLE_COMPLEX, 16, 16, 16, F_BASIC, "MPI_C_DOUBLE_COMPLEX", 0, {{0}}},
+    {0x2B, MI355X_T_C_LONG_DOUBLE_COMPLEX, 32, 32, 32, F_BASIC, "MPI_C_LONG_DOUBLE_COMPLEX", 0, {{0}}},
 };
 static ompi_datatype_t *dt_objs[OMPI_DATATYPE_MPI_MAX_PREDEFINED];
 
-static opal_class_t ompi_datatype_t_class = {"ompi_datatype_t", &opal_object_t_class, NULL, NULL, 0, 0, NULL,
-                                             NULL, sizeof(ompi_datatype_t)};
+static opal_class_t ompi_datatype_t_class = {"ompi_datatype_t", &opal_object_t_class, NULL, NULL, 0, 0, NULL, NULL,
+                                             sizeof(ompi_datatype_t)};
 
 ompi_predefined_datatype_t ompi_mpi_byte;  /* MPI_BYTE (mpi.h.in:913) */
+
+/* a committed description (dt_elem_desc_t records of 32 bytes, opal_datatype_internal.h:148-188):
+ * the elements as opal_datatype_add appends them (:276-350), then the END_LOOP that
+ * opal_datatype_commit adds (opal_datatype_optimize.c:255-282) */
+static void put16(unsigned char *p, uint16_t v) { memcpy(p, &v, 2); }
+static void put32(unsigned char *p, uint32_t v) { memcpy(p, &v, 4); }
+static void put64(unsigned char *p, int64_t v) { memcpy(p, &v, 8); }
+static void pair_desc(ompi_datatype_t *d, const struct mini_predef *p)
+{
+    const uint32_t used = (uint32_t)p->ne + 1;
+    unsigned char *r = calloc(used, 32);
+    for (int i = 0; i < p->ne; ++i) {
+        unsigned char *e = r + 32 * i;
+        /* the added basic type's flags less COMMITTED (opal_datatype_add.c:283-290) */
+        put16(e, OPAL_DATATYPE_FLAG_PREDEFINED | OPAL_DATATYPE_FLAG_CONTIGUOUS | OPAL_DATATYPE_FLAG_NO_GAPS |
+                     OPAL_DATATYPE_FLAG_DATA);
+        put16(e + 2, p->e[i].type);
+        put32(e + 4, p->e[i].count);
+        put32(e + 8, 1);
+        put64(e + 16, p->e[i].ext);
+        put64(e + 24, p->e[i].disp);
+    }
+    unsigned char *end = r + 32 * p->ne;
+    put16(end + 2, 1);  /* OPAL_DATATYPE_END_LOOP */
+    put32(end + 4, (uint32_t)p->ne);
+    put64(end + 16, (int64_t)p->size);
+    put64(end + 24, p->e[0].disp);
+    d->super.desc.desc = (dt_elem_desc_t *)r;
+    d->super.desc.used = (uint32_t)p->ne;  /* the END_LOOP sits at desc[used] (opal_datatype_optimize.c:257) */
+    d->super.desc.length = used;
+    d->super.opt_desc = d->super.desc;
+}
 
 void mini_init(void)
 {
@@ -119,18 +191,20 @@ void mini_init(void)
         ompi_op_ddt_map[predefined[k].id] = predefined[k].slot;
         ompi_datatype_t *d = (ompi_datatype_t *)mi355x_obj_new(&ompi_datatype_t_class);
         memset((char *)d + sizeof(opal_object_t), 0, sizeof(*d) - sizeof(opal_object_t));
-        d->super.flags = OPAL_DATATYPE_FLAG_PREDEFINED | OPAL_DATATYPE_FLAG_CONTIGUOUS | OPAL_DATATYPE_FLAG_NO_GAPS;
+        d->super.flags = predefined[k].flags;
         d->super.id = (uint16_t)predefined[k].id;
         d->super.size = predefined[k].size;
-        d->super.true_ub = d->super.ub = (ptrdiff_t)predefined[k].size;
+        d->super.ub = predefined[k].ext;
+        d->super.true_ub = predefined[k].true_ub;
         d->id = predefined[k].id;
+        if (predefined[k].ne) pair_desc(d, &predefined[k]);
         snprintf(d->name, sizeof(d->name), "%s", predefined[k].name);
         dt_objs[predefined[k].id] = d;
     }
     ompi_datatype_t *b = &ompi_mpi_byte.dt;
     b->super.super.obj_class = &ompi_datatype_t_class;
     b->super.super.obj_reference_count = 1;
-    b->super.flags = OPAL_DATATYPE_FLAG_PREDEFINED | OPAL_DATATYPE_FLAG_CONTIGUOUS | OPAL_DATATYPE_FLAG_NO_GAPS;
+    b->super.flags = F_BASIC;
     b->super.id = 4; /* OPAL_DATATYPE_UINT1 */
     b->super.size = 1;
     b->super.true_ub = b->super.ub = 1;
@@ -179,6 +253,20 @@ void mini_datatype_destroy(ompi_datatype_t *d)
     d->super.desc.desc = NULL;
     mi355x_obj_release(&d->super.super);
 }
+
+/* the committed datatype's opal fields, for tests: flags, size, lb, ub, true_lb, true_ub, desc.used,
+ * and its description records (desc.used + 1 with the trailing END_LOOP) */
+void mini_datatype_fields(const ompi_datatype_t *d, int64_t out[7])
+{
+    out[0] = d->super.flags;
+    out[1] = (int64_t)d->super.size;
+    out[2] = d->super.lb;
+    out[3] = d->super.ub;
+    out[4] = d->super.true_lb;
+    out[5] = d->super.true_ub;
+    out[6] = d->super.desc.used;
+}
+const void *mini_datatype_desc(const ompi_datatype_t *d) { return d->super.desc.desc; }
 
 int mini_datatype_id_for_slot(int slot)
 {
@@ -788,17 +876,27 @@ void *mini_comm_fn(ompi_communicator_t *c, int which)
  * What ob1 + the sm BTL give coll/basic and coll/tuned in a real job: a way for the ranks of ONE
  * communicator to move host bytes.  The harness stands it in with one POSIX shm segment per
  * communicator, named by the test (each group of a split gets its own, as each group's PML
- * traffic is its own).  Only bcast of small host buffers is provided: it is what coll/mi355x's
- * module_enable uses to agree on its rendezvous key. */
+ * traffic is its own): a small bcast area (what coll/mi355x's module_enable uses to agree on its
+ * rendezvous key), a barrier, and one data slot per rank through which the host module below
+ * moves and reduces buffers of any size in slot-sized pieces. */
 #define MINI_CHAN_MAX 64
 #define MINI_CHAN_BYTES 4096
+#define MINI_SLOT_BYTES ((size_t)128 << 10)
 struct mini_chan {
     _Atomic uint64_t gen;                 /* number of the last bcast the root published */
     _Atomic uint64_t ack[MINI_CHAN_MAX];  /* per rank: last bcast it has copied out */
+    _Atomic uint64_t bar[MINI_CHAN_MAX];  /* per rank: last barrier it has reached */
     uint64_t len;
     char data[MINI_CHAN_BYTES];
+    /* followed by comm size x MINI_SLOT_BYTES of per-rank data slots */
 };
-static struct { ompi_communicator_t *comm; struct mini_chan *ch; uint64_t calls; char name[128]; } chans[64];
+static struct {
+    ompi_communicator_t *comm;
+    struct mini_chan *ch;
+    uint64_t calls, bars;
+    size_t map_bytes;
+    char name[128];
+} chans[64];
 
 static struct mini_chan *chan_of(ompi_communicator_t *c, uint64_t **calls)
 {
@@ -810,27 +908,43 @@ static struct mini_chan *chan_of(ompi_communicator_t *c, uint64_t **calls)
     return NULL;
 }
 
+static int chan_index(ompi_communicator_t *c)
+{
+    for (int i = 0; i < 64; ++i)
+        if (chans[i].comm == c) return i;
+    return -1;
+}
+
+static char *chan_slot(struct mini_chan *ch, int q)
+{
+    return (char *)ch + sizeof(struct mini_chan) + (size_t)q * MINI_SLOT_BYTES;
+}
+
 int mini_comm_set_channel(ompi_communicator_t *c, const char *name)
 {
     int slot = -1;
     for (int i = 0; i < 64 && slot < 0; ++i)
         if (!chans[i].comm) slot = i;
-    if (slot < 0 || c->c_local_group->grp_proc_count > MINI_CHAN_MAX) return OMPI_ERR_OUT_OF_RESOURCE;
+    const int n = c->c_local_group->grp_proc_count;
+    if (slot < 0 || n > MINI_CHAN_MAX) return OMPI_ERR_OUT_OF_RESOURCE;
     char shm[112];
     snprintf(shm, sizeof(shm), "/mini_chan_%s", name);
+    const size_t bytes = sizeof(struct mini_chan) + (size_t)n * MINI_SLOT_BYTES;
     /* every rank creates-or-opens; a fresh object is zero-filled by ftruncate */
     const int fd = shm_open(shm, O_CREAT | O_RDWR, 0600);
     if (fd < 0) return OMPI_ERROR;
-    if (ftruncate(fd, (off_t)sizeof(struct mini_chan)) != 0) {
+    if (ftruncate(fd, (off_t)bytes) != 0) {
         close(fd);
         return OMPI_ERROR;
     }
-    void *m = mmap(NULL, sizeof(struct mini_chan), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    void *m = mmap(NULL, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
     close(fd);
     if (m == MAP_FAILED) return OMPI_ERROR;
     chans[slot].comm = c;
     chans[slot].ch = (struct mini_chan *)m;
     chans[slot].calls = 0;
+    chans[slot].bars = 0;
+    chans[slot].map_bytes = bytes;
     snprintf(chans[slot].name, sizeof(chans[slot].name), "%s", shm);
     return OMPI_SUCCESS;
 }
@@ -839,10 +953,21 @@ static void chan_release(ompi_communicator_t *c)
 {
     for (int i = 0; i < 64; ++i)
         if (chans[i].comm == c) {
-            munmap(chans[i].ch, sizeof(struct mini_chan));
+            munmap(chans[i].ch, chans[i].map_bytes);
             if (c->c_my_rank == 0) shm_unlink(chans[i].name);
             chans[i].comm = NULL;
         }
+}
+
+/* every rank of the communicator reaches barrier number k before any leaves it */
+static void chan_barrier(ompi_communicator_t *c, int ci)
+{
+    struct mini_chan *ch = chans[ci].ch;
+    const int n = c->c_local_group->grp_proc_count;
+    const uint64_t k = ++chans[ci].bars;
+    atomic_store_explicit(&ch->bar[c->c_my_rank], k, memory_order_release);
+    for (int q = 0; q < n; ++q)
+        while (atomic_load_explicit(&ch->bar[q], memory_order_acquire) < k) sched_yield();
 }
 
 /* linear bcast of <= 4 KiB of host memory: the root waits until every rank acknowledged the
@@ -869,26 +994,65 @@ static int chan_bcast(ompi_communicator_t *c, struct mini_chan *ch, uint64_t *ca
     return OMPI_SUCCESS;
 }
 
+/* ------------------------------------------------------------------ device-buffer guard
+ * A host component (coll/basic, coll/tuned, libnbc) reads and writes its buffers with the CPU:
+ * handed hipMalloc memory it faults.  The harness's lower-priority modules check every buffer
+ * pointer they are given instead, so a test sees the fault as a failed call: the pointer is
+ * reported, counted, and the call returns MINI_ERR_DEVICE_BUFFER.  The query is the engine's own
+ * (resolved at run time: libmi355x_rt is loaded before any component). */
+#define MINI_ERR_DEVICE_BUFFER 78
+static int device_hits;
+static int on_device(const void *p)
+{
+    static int (*is_dev)(const void *, int *);
+    static int looked;
+    if (!looked) {
+        is_dev = (int (*)(const void *, int *))dlsym(RTLD_DEFAULT, "mi355x_ptr_is_device");
+        looked = 1;
+    }
+    int d = 0;
+    if (!p || p == MPI_IN_PLACE || !is_dev || is_dev(p, &d) != 0) return 0;
+    return d;
+}
+static int guard(const char *fn, int n, ...)
+{
+    va_list ap;
+    va_start(ap, n);
+    int bad = 0;
+    for (int i = 0; i < n; ++i) {
+        const void *p = va_arg(ap, const void *);
+        if (on_device(p)) {
+            fprintf(stderr, "[mini] %s: device buffer %p handed to a host component\n", fn, p);
+            bad = 1;
+        }
+    }
+    va_end(ap);
+    if (bad) device_hits++;
+    return bad;
+}
+int mini_device_hits(void) { return device_hits; }
+
 /* a stub "lower-priority" module for tests: records which function ran and returns `marker`
  * (bcast on a communicator with a host channel really broadcasts host buffers) */
 static int stub_calls[16];
 static int stub_marker = 77;
 static int st_allreduce(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o,
                         struct ompi_communicator_t *c, mca_coll_base_module_t *m)
-{ (void)s; (void)r; (void)n; (void)d; (void)o; (void)c; (void)m; stub_calls[0]++; return stub_marker; }
+{ if (guard("st_allreduce", 2, s, r)) return MINI_ERR_DEVICE_BUFFER; (void)s; (void)r; (void)n; (void)d; (void)o; (void)c; (void)m; stub_calls[0]++; return stub_marker; }
 static int st_rsb(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o,
                   struct ompi_communicator_t *c, mca_coll_base_module_t *m)
-{ (void)s; (void)r; (void)n; (void)d; (void)o; (void)c; (void)m; stub_calls[1]++; return stub_marker; }
+{ if (guard("st_rsb", 2, s, r)) return MINI_ERR_DEVICE_BUFFER; (void)s; (void)r; (void)n; (void)d; (void)o; (void)c; (void)m; stub_calls[1]++; return stub_marker; }
 static int st_rs(void *s, void *r, int *n, struct ompi_datatype_t *d, struct ompi_op_t *o,
                  struct ompi_communicator_t *c, mca_coll_base_module_t *m)
-{ (void)s; (void)r; (void)n; (void)d; (void)o; (void)c; (void)m; stub_calls[2]++; return stub_marker; }
+{ if (guard("st_rs", 2, s, r)) return MINI_ERR_DEVICE_BUFFER; (void)s; (void)r; (void)n; (void)d; (void)o; (void)c; (void)m; stub_calls[2]++; return stub_marker; }
 static int st_allgather(void *s, int sc, struct ompi_datatype_t *sd, void *r, int rc, struct ompi_datatype_t *rd,
                         struct ompi_communicator_t *c, mca_coll_base_module_t *m)
-{ (void)s; (void)sc; (void)sd; (void)r; (void)rc; (void)rd; (void)c; (void)m; stub_calls[3]++; return stub_marker; }
+{ if (guard("st_allgather", 2, s, r)) return MINI_ERR_DEVICE_BUFFER; (void)s; (void)sc; (void)sd; (void)r; (void)rc; (void)rd; (void)c; (void)m; stub_calls[3]++; return stub_marker; }
 static int st_bcast(void *b, int n, struct ompi_datatype_t *d, int root, struct ompi_communicator_t *c,
                     mca_coll_base_module_t *m)
 {
     (void)m;
+    if (guard("st_bcast", 1, b)) return MINI_ERR_DEVICE_BUFFER;
     stub_calls[4]++;
     uint64_t *calls = NULL;
     struct mini_chan *ch = chan_of(c, &calls);
@@ -897,33 +1061,33 @@ static int st_bcast(void *b, int n, struct ompi_datatype_t *d, int root, struct 
 }
 static int st_reduce(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o, int root,
                      struct ompi_communicator_t *c, mca_coll_base_module_t *m)
-{ (void)s; (void)r; (void)n; (void)d; (void)o; (void)root; (void)c; (void)m; stub_calls[5]++; return stub_marker; }
+{ if (guard("st_reduce", 2, s, r)) return MINI_ERR_DEVICE_BUFFER; (void)s; (void)r; (void)n; (void)d; (void)o; (void)root; (void)c; (void)m; stub_calls[5]++; return stub_marker; }
 
 static int st_iallreduce(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o,
                          struct ompi_communicator_t *c, ompi_request_t **req, mca_coll_base_module_t *m)
-{ (void)s; (void)r; (void)n; (void)d; (void)o; (void)c; (void)m; *req = &ompi_request_null.request; stub_calls[6]++; return stub_marker; }
+{ if (guard("st_iallreduce", 2, s, r)) return MINI_ERR_DEVICE_BUFFER; (void)s; (void)r; (void)n; (void)d; (void)o; (void)c; (void)m; *req = &ompi_request_null.request; stub_calls[6]++; return stub_marker; }
 
 static int st_gather(void *s, int sc, struct ompi_datatype_t *sd, void *r, int rc, struct ompi_datatype_t *rd,
                      int root, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
-{ (void)s; (void)sc; (void)sd; (void)r; (void)rc; (void)rd; (void)root; (void)c; (void)m; stub_calls[7]++; return stub_marker; }
+{ if (guard("st_gather", 2, s, r)) return MINI_ERR_DEVICE_BUFFER; (void)s; (void)sc; (void)sd; (void)r; (void)rc; (void)rd; (void)root; (void)c; (void)m; stub_calls[7]++; return stub_marker; }
 static int st_alltoall(void *s, int sc, struct ompi_datatype_t *sd, void *r, int rc, struct ompi_datatype_t *rd,
                        struct ompi_communicator_t *c, mca_coll_base_module_t *m)
-{ (void)s; (void)sc; (void)sd; (void)r; (void)rc; (void)rd; (void)c; (void)m; stub_calls[8]++; return stub_marker; }
+{ if (guard("st_alltoall", 2, s, r)) return MINI_ERR_DEVICE_BUFFER; (void)s; (void)sc; (void)sd; (void)r; (void)rc; (void)rd; (void)c; (void)m; stub_calls[8]++; return stub_marker; }
 static int st_scan(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o,
                    struct ompi_communicator_t *c, mca_coll_base_module_t *m)
-{ (void)s; (void)r; (void)n; (void)d; (void)o; (void)c; (void)m; stub_calls[9]++; return stub_marker; }
+{ if (guard("st_scan", 2, s, r)) return MINI_ERR_DEVICE_BUFFER; (void)s; (void)r; (void)n; (void)d; (void)o; (void)c; (void)m; stub_calls[9]++; return stub_marker; }
 static int st_gatherv(void *s, int sc, struct ompi_datatype_t *sd, void *r, int *rc, int *dp,
                       struct ompi_datatype_t *rd, int root, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
-{ (void)s; (void)sc; (void)sd; (void)r; (void)rc; (void)dp; (void)rd; (void)root; (void)c; (void)m; stub_calls[10]++; return stub_marker; }
+{ if (guard("st_gatherv", 2, s, r)) return MINI_ERR_DEVICE_BUFFER; (void)s; (void)sc; (void)sd; (void)r; (void)rc; (void)dp; (void)rd; (void)root; (void)c; (void)m; stub_calls[10]++; return stub_marker; }
 static int st_scatterv(void *s, int *sc, int *dp, struct ompi_datatype_t *sd, void *r, int rc,
                        struct ompi_datatype_t *rd, int root, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
-{ (void)s; (void)sc; (void)dp; (void)sd; (void)r; (void)rc; (void)rd; (void)root; (void)c; (void)m; stub_calls[11]++; return stub_marker; }
+{ if (guard("st_scatterv", 2, s, r)) return MINI_ERR_DEVICE_BUFFER; (void)s; (void)sc; (void)dp; (void)sd; (void)r; (void)rc; (void)rd; (void)root; (void)c; (void)m; stub_calls[11]++; return stub_marker; }
 static int st_allgatherv(void *s, int sc, struct ompi_datatype_t *sd, void *r, int *rc, int *dp,
                          struct ompi_datatype_t *rd, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
-{ (void)s; (void)sc; (void)sd; (void)r; (void)rc; (void)dp; (void)rd; (void)c; (void)m; stub_calls[12]++; return stub_marker; }
+{ if (guard("st_allgatherv", 2, s, r)) return MINI_ERR_DEVICE_BUFFER; (void)s; (void)sc; (void)sd; (void)r; (void)rc; (void)dp; (void)rd; (void)c; (void)m; stub_calls[12]++; return stub_marker; }
 static int st_alltoallv(void *s, int *sc, int *sdp, struct ompi_datatype_t *sd, void *r, int *rc, int *rdp,
                         struct ompi_datatype_t *rd, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
-{ (void)s; (void)sc; (void)sdp; (void)sd; (void)r; (void)rc; (void)rdp; (void)rd; (void)c; (void)m; stub_calls[13]++; return stub_marker; }
+{ if (guard("st_alltoallv", 2, s, r)) return MINI_ERR_DEVICE_BUFFER; (void)s; (void)sc; (void)sdp; (void)sd; (void)r; (void)rc; (void)rdp; (void)rd; (void)c; (void)m; stub_calls[13]++; return stub_marker; }
 
 mca_coll_base_module_t *mini_stub_module(void)
 {
@@ -948,6 +1112,413 @@ mca_coll_base_module_t *mini_stub_module(void)
 }
 int mini_stub_calls(int which) { return (which >= 0 && which < 16) ? stub_calls[which] : -1; }
 int mini_stub_marker(void) { return stub_marker; }
+
+/* ------------------------------------------------------------------ host module
+ * The lower-priority module the engine's declined calls land on, doing what coll/basic over ob1 +
+ * sm does with host buffers: the data really moves (through the communicator's host channel, in
+ * slot-sized pieces) and is reduced on the CPU by ompi_op_reduce (op.h:540-636) -- an intrinsic
+ * op through its selected slot functions (op/hip's, which hand host buffers to the base loops), a
+ * user op through its C function.  Orders are coll/basic's: reduce and allreduce linear,
+ * rbuf = r[n-1], then r[i] op rbuf for i = n-2..0 (coll_basic_reduce.c:215-250); scan and exscan
+ * the rank-order chain p[k] = p[k-1] op r[k] (coll_basic_scan.c:84-110, coll_basic_exscan.c:
+ * 63-104).  Types: any with true_lb == 0 (instances extent apart, true_ub bytes each).  Nonblocking
+ * forms are queued and run in order from an opal_progress callback, so their requests complete
+ * only under MPI_Wait / MPI_Test, as libnbc's do.  Every buffer passes the device guard. */
+static int host_calls[16];
+
+static void host_op_reduce(ompi_op_t *op, void *in, void *inout, int count, ompi_datatype_t *dt)
+{
+    if (count <= 0) return;
+    if (op->o_flags & OMPI_OP_FLAGS_INTRINSIC) {
+        const int t = ompi_op_ddt_map[dt->id];
+        op->o_func.intrinsic.fns[t](in, inout, &count, &dt, op->o_func.intrinsic.modules[t]);
+    } else {
+        ((void (*)(void *, void *, int *, ompi_datatype_t **))op->o_func.c_fn)(in, inout, &count, &dt);
+    }
+}
+
+static size_t span_of(const ompi_datatype_t *dt, size_t k)
+{
+    return k ? (size_t)(dt->super.true_ub + (ptrdiff_t)(k - 1) * (dt->super.ub - dt->super.lb)) : 0;
+}
+
+/* Reduce the ranks' `total`-instance contributions (src; NULL: contributes nothing -- never
+ * happens in MPI, every rank contributes) over instances [lo, lo + cnt) into dst (cnt instances;
+ * NULL: this rank only contributes).  chain < 0: linear order over all ranks; chain >= 0: the
+ * scan chain over ranks 0..chain. */
+static int host_reduce(ompi_communicator_t *c, const char *src, size_t total, size_t lo, size_t cnt, int chain,
+                       char *dst, ompi_datatype_t *dt, ompi_op_t *op)
+{
+    const int ci = chan_index(c);
+    if (ci < 0) return stub_marker;  /* no channel: the bare stub's answer */
+    if (dt->super.true_lb != 0) return OMPI_ERR_NOT_SUPPORTED;
+    struct mini_chan *ch = chans[ci].ch;
+    const int n = c->c_local_group->grp_proc_count, me = c->c_my_rank;
+    const size_t ext = (size_t)(dt->super.ub - dt->super.lb);
+    const size_t per = ext ? MINI_SLOT_BYTES / ext : 0;
+    if (per == 0) return OMPI_ERR_NOT_SUPPORTED;
+    char *acc = malloc(MINI_SLOT_BYTES), *tmp = malloc(MINI_SLOT_BYTES);
+    if (!acc || !tmp) {
+        free(acc);
+        free(tmp);
+        return OMPI_ERR_OUT_OF_RESOURCE;
+    }
+    for (size_t c0 = 0; c0 < total || (total == 0 && c0 == 0); c0 += per) {
+        if (total == 0) break;
+        const size_t k = total - c0 < per ? total - c0 : per;
+        memcpy(chan_slot(ch, me), src + c0 * ext, span_of(dt, k));
+        chan_barrier(c, ci);
+        const size_t a = c0 > lo ? c0 : lo, b = (c0 + k < lo + cnt) ? c0 + k : lo + cnt;
+        if (dst && a < b) {
+            const size_t off = (a - c0) * ext, m = b - a, bytes = span_of(dt, m);
+            if (chain < 0) {
+                memcpy(acc, chan_slot(ch, n - 1) + off, bytes);
+                for (int i = n - 2; i >= 0; --i) host_op_reduce(op, chan_slot(ch, i) + off, acc, (int)m, dt);
+            } else {
+                memcpy(acc, chan_slot(ch, 0) + off, bytes);
+                for (int q = 1; q <= chain; ++q) {
+                    memcpy(tmp, chan_slot(ch, q) + off, bytes);
+                    host_op_reduce(op, acc, tmp, (int)m, dt);
+                    char *sw = acc;
+                    acc = tmp;
+                    tmp = sw;
+                }
+            }
+            memcpy(dst + (a - lo) * ext, acc, bytes);
+        }
+        chan_barrier(c, ci);
+    }
+    free(acc);
+    free(tmp);
+    return OMPI_SUCCESS;
+}
+
+/* root's `total` instances to every rank, slot-sized pieces through the root's slot */
+static int host_bcast(ompi_communicator_t *c, char *buf, size_t total, ompi_datatype_t *dt, int root)
+{
+    const int ci = chan_index(c);
+    if (ci < 0) return stub_marker;
+    if (dt->super.true_lb != 0 || !(dt->super.flags & OPAL_DATATYPE_FLAG_CONTIGUOUS)) return OMPI_ERR_NOT_SUPPORTED;
+    struct mini_chan *ch = chans[ci].ch;
+    const size_t ext = (size_t)(dt->super.ub - dt->super.lb), per = ext ? MINI_SLOT_BYTES / ext : 0;
+    if (per == 0) return OMPI_ERR_NOT_SUPPORTED;
+    for (size_t c0 = 0; c0 < total; c0 += per) {
+        const size_t k = total - c0 < per ? total - c0 : per;
+        if (c->c_my_rank == root) memcpy(chan_slot(ch, root), buf + c0 * ext, span_of(dt, k));
+        chan_barrier(c, ci);
+        if (c->c_my_rank != root) memcpy(buf + c0 * ext, chan_slot(ch, root), span_of(dt, k));
+        chan_barrier(c, ci);
+    }
+    return OMPI_SUCCESS;
+}
+
+static int h_allreduce(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                       struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)m;
+    host_calls[0]++;
+    if (guard("allreduce", 2, s, r)) return MINI_ERR_DEVICE_BUFFER;
+    if (n < 0) return OMPI_ERR_BAD_PARAM;
+    const char *src = s == MPI_IN_PLACE ? (const char *)r : (const char *)s;
+    char *copy = NULL;
+    if (s == MPI_IN_PLACE) {  /* rbuf is both the contribution and the result */
+        copy = malloc(span_of(d, (size_t)n) + 1);
+        if (!copy) return OMPI_ERR_OUT_OF_RESOURCE;
+        memcpy(copy, r, span_of(d, (size_t)n));
+        src = copy;
+    }
+    const int rc = host_reduce(c, src, (size_t)n, 0, (size_t)n, -1, (char *)r, d, o);
+    free(copy);
+    return rc;
+}
+
+static int h_reduce(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o, int root,
+                    struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)m;
+    host_calls[5]++;
+    const int me = c->c_my_rank;
+    if (guard("reduce", 2, s, me == root ? r : NULL)) return MINI_ERR_DEVICE_BUFFER;
+    if (n < 0) return OMPI_ERR_BAD_PARAM;
+    const char *src = s == MPI_IN_PLACE ? (const char *)r : (const char *)s;
+    char *copy = NULL;
+    if (s == MPI_IN_PLACE) {
+        copy = malloc(span_of(d, (size_t)n) + 1);
+        if (!copy) return OMPI_ERR_OUT_OF_RESOURCE;
+        memcpy(copy, r, span_of(d, (size_t)n));
+        src = copy;
+    }
+    const int rc = host_reduce(c, src, (size_t)n, 0, (size_t)n, -1, me == root ? (char *)r : NULL, d, o);
+    free(copy);
+    return rc;
+}
+
+/* reduce_scatter(_block): my block of the linear reduction (coll/basic reduces to 0 and scatters) */
+static int h_rs_common(void *s, void *r, const int *counts, int rcount, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                       struct ompi_communicator_t *c)
+{
+    const int n = c->c_local_group->grp_proc_count, me = c->c_my_rank;
+    size_t total = 0, lo = 0;
+    for (int q = 0; q < n; ++q) {
+        const int k = counts ? counts[q] : rcount;
+        if (k < 0) return OMPI_ERR_BAD_PARAM;
+        if (q < me) lo += (size_t)k;
+        total += (size_t)k;
+    }
+    const size_t mine = (size_t)(counts ? counts[me] : rcount);
+    const char *src = s == MPI_IN_PLACE ? (const char *)r : (const char *)s;
+    char *copy = NULL;
+    if (s == MPI_IN_PLACE) {
+        copy = malloc(span_of(d, total) + 1);
+        if (!copy) return OMPI_ERR_OUT_OF_RESOURCE;
+        memcpy(copy, r, span_of(d, total));
+        src = copy;
+    }
+    const int rc = host_reduce(c, src, total, lo, mine, -1, (char *)r, d, o);
+    free(copy);
+    return rc;
+}
+
+static int h_rsb(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                 struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)m;
+    host_calls[1]++;
+    if (guard("reduce_scatter_block", 2, s, r)) return MINI_ERR_DEVICE_BUFFER;
+    return h_rs_common(s, r, NULL, n, d, o, c);
+}
+
+static int h_rs(void *s, void *r, int *counts, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)m;
+    host_calls[2]++;
+    if (guard("reduce_scatter", 2, s, r)) return MINI_ERR_DEVICE_BUFFER;
+    return h_rs_common(s, r, counts, 0, d, o, c);
+}
+
+static int h_scan_common(int exclusive, void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                         struct ompi_communicator_t *c)
+{
+    if (n < 0) return OMPI_ERR_BAD_PARAM;
+    const int me = c->c_my_rank;
+    const char *src = s == MPI_IN_PLACE ? (const char *)r : (const char *)s;
+    char *copy = NULL;
+    if (s == MPI_IN_PLACE) {
+        copy = malloc(span_of(d, (size_t)n) + 1);
+        if (!copy) return OMPI_ERR_OUT_OF_RESOURCE;
+        memcpy(copy, r, span_of(d, (size_t)n));
+        src = copy;
+    }
+    const int last = exclusive ? me - 1 : me;  /* exscan: rank 0's rbuf is left alone */
+    const int rc = host_reduce(c, src, (size_t)n, 0, (size_t)n, last < 0 ? 0 : last, last < 0 ? NULL : (char *)r, d, o);
+    free(copy);
+    return rc;
+}
+
+static int h_scan(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                  struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)m;
+    host_calls[9]++;
+    if (guard("scan", 2, s, r)) return MINI_ERR_DEVICE_BUFFER;
+    return h_scan_common(0, s, r, n, d, o, c);
+}
+
+static int h_exscan(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                    struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)m;
+    host_calls[10]++;
+    if (guard("exscan", 2, s, r)) return MINI_ERR_DEVICE_BUFFER;
+    return h_scan_common(1, s, r, n, d, o, c);
+}
+
+static int h_bcast(void *b, int n, struct ompi_datatype_t *d, int root, struct ompi_communicator_t *c,
+                   mca_coll_base_module_t *m)
+{
+    (void)m;
+    host_calls[4]++;
+    if (guard("bcast", 1, b)) return MINI_ERR_DEVICE_BUFFER;
+    if (n < 0) return OMPI_ERR_BAD_PARAM;
+    return host_bcast(c, (char *)b, (size_t)n, d, root);
+}
+
+/* allgather as n bcasts of the ranks' blocks (coll/basic: gather to 0 + bcast) */
+static int h_allgather(void *s, int sc, struct ompi_datatype_t *sd, void *r, int rc, struct ompi_datatype_t *rd,
+                       struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)m;
+    host_calls[3]++;
+    if (guard("allgather", 2, s, r)) return MINI_ERR_DEVICE_BUFFER;
+    if (rc < 0) return OMPI_ERR_BAD_PARAM;
+    const int n = c->c_local_group->grp_proc_count, me = c->c_my_rank;
+    const size_t ext = (size_t)(rd->super.ub - rd->super.lb);
+    if (s != MPI_IN_PLACE) {
+        if ((size_t)sc * sd->super.size != (size_t)rc * rd->super.size || !(sd->super.flags & OPAL_DATATYPE_FLAG_NO_GAPS) ||
+            !(rd->super.flags & OPAL_DATATYPE_FLAG_NO_GAPS))
+            return OMPI_ERR_NOT_SUPPORTED;
+        memcpy((char *)r + (size_t)me * rc * ext, s, (size_t)rc * rd->super.size);
+    }
+    for (int q = 0; q < n; ++q) {
+        const int e = host_bcast(c, (char *)r + (size_t)q * rc * ext, (size_t)rc, rd, q);
+        if (e) return e;
+    }
+    return OMPI_SUCCESS;
+}
+
+/* ---- nonblocking: queued, run in posting order from the progress callback */
+typedef struct mini_hreq {
+    ompi_request_t super;
+    int kind;  /* 0 allreduce, 1 reduce, 2 rsb, 3 allgather, 4 bcast */
+    void *s, *r;
+    int n, n2, root;
+    struct ompi_datatype_t *d, *d2;
+    struct ompi_op_t *o;
+    struct ompi_communicator_t *c;
+    struct mini_hreq *next;
+} mini_hreq_t;
+static mini_hreq_t *hq_head, *hq_tail;
+static int hq_running, hq_registered;
+
+static int hreq_free(ompi_request_t **rp)
+{
+    mini_hreq_t *q = (mini_hreq_t *)*rp;
+    if (!q->super.req_complete) return MPI_ERR_REQUEST;
+    mi355x_obj_release(&q->super.super.super.super);
+    *rp = &ompi_request_null.request;
+    return OMPI_SUCCESS;
+}
+static opal_class_t mini_hreq_t_class = {"mini_hreq_t", &ompi_request_t_class, NULL, NULL, 0, 0, NULL, NULL,
+                                         sizeof(mini_hreq_t)};
+
+static int hq_progress(void)
+{
+    if (hq_running || !hq_head) return 0;
+    hq_running = 1;
+    int done = 0;
+    while (hq_head) {
+        mini_hreq_t *q = hq_head;
+        hq_head = q->next;
+        if (!hq_head) hq_tail = NULL;
+        int rc;
+        switch (q->kind) {
+        case 0: rc = h_allreduce(q->s, q->r, q->n, q->d, q->o, q->c, NULL); break;
+        case 1: rc = h_reduce(q->s, q->r, q->n, q->d, q->o, q->root, q->c, NULL); break;
+        case 2: rc = h_rsb(q->s, q->r, q->n, q->d, q->o, q->c, NULL); break;
+        case 3: rc = h_allgather(q->s, q->n, q->d, q->r, q->n2, q->d2, q->c, NULL); break;
+        default: rc = h_bcast(q->r, q->n, q->d, q->root, q->c, NULL); break;
+        }
+        q->super.req_status.MPI_ERROR = rc;
+        q->super.req_complete = true;
+        q->super.req_state = OMPI_REQUEST_INACTIVE;
+        done++;
+    }
+    hq_running = 0;
+    return done;
+}
+
+static int hq_post(mini_hreq_t proto, ompi_request_t **req)
+{
+    mini_hreq_t *q = (mini_hreq_t *)mi355x_obj_new(&mini_hreq_t_class);
+    if (!q) return OMPI_ERR_OUT_OF_RESOURCE;
+    const ompi_request_t base = q->super;
+    *q = proto;
+    q->super = base;
+    q->super.req_type = OMPI_REQUEST_COLL;
+    q->super.req_free = hreq_free;
+    q->super.req_complete = false;
+    q->super.req_state = OMPI_REQUEST_ACTIVE;
+    q->super.req_status.MPI_ERROR = 0;
+    q->next = NULL;
+    if (hq_tail) hq_tail->next = q;
+    else hq_head = q;
+    hq_tail = q;
+    if (!hq_registered) {
+        opal_progress_register(hq_progress);
+        hq_registered = 1;
+    }
+    *req = &q->super;
+    return OMPI_SUCCESS;
+}
+
+static int h_iallreduce(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                        struct ompi_communicator_t *c, ompi_request_t **req, mca_coll_base_module_t *m)
+{
+    (void)m;
+    host_calls[6]++;
+    if (guard("iallreduce", 2, s, r)) return MINI_ERR_DEVICE_BUFFER;
+    return hq_post((mini_hreq_t){.kind = 0, .s = s, .r = r, .n = n, .d = d, .o = o, .c = c}, req);
+}
+static int h_ireduce(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o, int root,
+                     struct ompi_communicator_t *c, ompi_request_t **req, mca_coll_base_module_t *m)
+{
+    (void)m;
+    host_calls[11]++;
+    if (guard("ireduce", 2, s, c->c_my_rank == root ? r : NULL)) return MINI_ERR_DEVICE_BUFFER;
+    return hq_post((mini_hreq_t){.kind = 1, .s = s, .r = r, .n = n, .root = root, .d = d, .o = o, .c = c}, req);
+}
+static int h_irsb(void *s, void *r, int n, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                  struct ompi_communicator_t *c, ompi_request_t **req, mca_coll_base_module_t *m)
+{
+    (void)m;
+    host_calls[12]++;
+    if (guard("ireduce_scatter_block", 2, s, r)) return MINI_ERR_DEVICE_BUFFER;
+    return hq_post((mini_hreq_t){.kind = 2, .s = s, .r = r, .n = n, .d = d, .o = o, .c = c}, req);
+}
+static int h_iallgather(void *s, int sc, struct ompi_datatype_t *sd, void *r, int rc, struct ompi_datatype_t *rd,
+                        struct ompi_communicator_t *c, ompi_request_t **req, mca_coll_base_module_t *m)
+{
+    (void)m;
+    host_calls[13]++;
+    if (guard("iallgather", 2, s, r)) return MINI_ERR_DEVICE_BUFFER;
+    return hq_post((mini_hreq_t){.kind = 3, .s = s, .r = r, .n = sc, .n2 = rc, .d = sd, .d2 = rd, .c = c}, req);
+}
+static int h_ibcast(void *b, int n, struct ompi_datatype_t *d, int root, struct ompi_communicator_t *c,
+                    ompi_request_t **req, mca_coll_base_module_t *m)
+{
+    (void)m;
+    host_calls[14]++;
+    if (guard("ibcast", 1, b)) return MINI_ERR_DEVICE_BUFFER;
+    return hq_post((mini_hreq_t){.kind = 4, .r = b, .n = n, .root = root, .d = d, .c = c}, req);
+}
+
+/* the host module: real host collectives for the reduction slots and bcast / allgather (the stub's
+ * counting functions for the rest) */
+mca_coll_base_module_t *mini_host_module(void)
+{
+    mca_coll_base_module_t *m = mini_stub_module();
+    m->coll_allreduce = h_allreduce;
+    m->coll_reduce = h_reduce;
+    m->coll_reduce_scatter_block = h_rsb;
+    m->coll_reduce_scatter = h_rs;
+    m->coll_scan = h_scan;
+    m->coll_exscan = h_exscan;
+    m->coll_bcast = h_bcast;
+    m->coll_allgather = h_allgather;
+    m->coll_iallreduce = h_iallreduce;
+    m->coll_ireduce = h_ireduce;
+    m->coll_ireduce_scatter_block = h_irsb;
+    m->coll_iallgather = h_iallgather;
+    m->coll_ibcast = h_ibcast;
+    return m;
+}
+int mini_host_calls(int which) { return (which >= 0 && which < 16) ? host_calls[which] : -1; }
+
+/* MPI_Op_create (ompi_op_create_user, op.c:351-400): not intrinsic, commutative or not, the C
+ * function in o_func.c_fn; its f2c index lies past the predefined ops */
+ompi_op_t *mini_op_create_user(void *fn, int commute)
+{
+    mini_init();
+    ompi_op_t *op = (ompi_op_t *)mi355x_obj_new(&ompi_op_t_class);
+    memset((char *)op + sizeof(opal_object_t), 0, sizeof(*op) - sizeof(opal_object_t));
+    snprintf(op->o_name, sizeof(op->o_name), "user op");
+    op->op_type = MI355X_OP_MAX_;
+    op->o_f_to_c_index = 100;
+    op->o_flags = commute ? OMPI_OP_FLAGS_COMMUTE : 0;
+    op->o_func.c_fn = fn;
+    return op;
+}
 
 /* layout facts for tests/test_boundary.py */
 size_t mini_offsetof(int which)

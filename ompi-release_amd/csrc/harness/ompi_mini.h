@@ -12,6 +12,8 @@ extern "C" {
 void mini_init(void);
 ompi_datatype_t *mini_datatype(int id);
 int mini_datatype_id_for_slot(int slot);
+void mini_datatype_fields(const ompi_datatype_t *d, int64_t out[7]);
+const void *mini_datatype_desc(const ompi_datatype_t *d);
 ompi_datatype_t *mini_datatype_create_raw(const void *desc, uint32_t used, size_t size, ptrdiff_t lb, ptrdiff_t ub,
                                           ptrdiff_t true_lb, ptrdiff_t true_ub, uint16_t flags);
 void mini_datatype_destroy(ompi_datatype_t *d);
@@ -40,6 +42,10 @@ void *mini_comm_fn(ompi_communicator_t *c, int which);
 mca_coll_base_module_t *mini_stub_module(void);
 int mini_stub_calls(int which);
 int mini_stub_marker(void);
+mca_coll_base_module_t *mini_host_module(void);  /* real host collectives over the channel */
+int mini_host_calls(int which);
+int mini_device_hits(void);  /* device buffers the host modules were handed */
+ompi_op_t *mini_op_create_user(void *fn, int commute);
 size_t mini_offsetof(int which);
 /* the PML slot: a counting stub as the selected PML, and the bindings' MCA_PML_CALL paths */
 int mini_var_count(void);

@@ -134,13 +134,35 @@ static int is_dev(const void *p)
     return d;
 }
 
-/* the element type slot when the datatype is a predefined, gap-free reducible type; else -1 */
+/* The op slot of a datatype the engine can reduce, else -1.  The test is the reference's own: a
+ * type predefined as an MPI type (ompi_datatype_is_predefined, ompi_datatype.h:149-152 -- libmpi
+ * clears the OPAL flag on the MPI-2 pair types, ompi_datatype_module.c:415-416, 431-432, so that
+ * flag would reject every MAXLOC/MINLOC type) whose id maps to an op slot (ompi_op_ddt_map, the
+ * lookup ompi_op_reduce makes, op.h:570-574).  The engine moves count x extent bytes: the slot's
+ * element is the C layout of the type (pair padding included), so the extent must equal it and
+ * the type must start at its lower bound -- NO_GAPS is not required (MPI_DOUBLE_INT is 12 bytes of
+ * data in a 16-byte extent, MPI_SHORT_INT 6 in 8). */
 static int reducible_type(const struct ompi_datatype_t *dt)
 {
-    if (!(dt->super.flags & OPAL_DATATYPE_FLAG_PREDEFINED)) return -1;
-    if (!(dt->super.flags & OPAL_DATATYPE_FLAG_NO_GAPS)) return -1;
+    if (!(dt->super.flags & OMPI_DATATYPE_FLAG_PREDEFINED)) return -1;
     if (dt->id < 0 || dt->id >= OMPI_DATATYPE_MPI_MAX_PREDEFINED) return -1;
-    return ompi_op_ddt_map[dt->id];
+    const int t = ompi_op_ddt_map[dt->id];
+    if (t < 0) return -1;
+    const size_t esz = mi355x_type_size(t);
+    if (esz == 0 || dt->super.lb != 0 || dt->super.true_lb != 0 || (size_t)(dt->super.ub - dt->super.lb) != esz) return -1;
+    return t;
+}
+
+/* the op slot the engine would reduce dt as, or -1 (exported for the boundary tests) */
+int mca_coll_mi355x_reducible_type(const struct ompi_datatype_t *dt) { return reducible_type(dt); }
+
+/* bytes spanned by `count` instances of dt: true_extent + (count - 1) x extent, the staging size
+ * coll/cuda uses (coll_cuda_allreduce.c:44-46) */
+static size_t dt_span(const struct ompi_datatype_t *dt, size_t count)
+{
+    if (count == 0) return 0;
+    const ptrdiff_t ext = dt->super.ub - dt->super.lb, text = dt->super.true_ub - dt->super.true_lb;
+    return (size_t)(text + (ptrdiff_t)(count - 1) * ext);
 }
 
 /* counts are size_t here: a block count times the communicator size (allgather's unpack of n
@@ -320,6 +342,93 @@ static int copy_back(void *host, const void *dev, size_t bytes, int rc)
         if (r_ == 0) return PREV_CALL;                                                 \
     } while (0)
 
+/* ------------------------------------------------------------------ coll/cuda's host staging
+ * A reduction the engine declines -- a user-defined MPI_Op, or a type with no engine slot (the x87
+ * long double slots the engine has no fold for) -- goes to the lower-priority component, which
+ * reads and writes the buffers on the CPU (coll/tuned: opal_datatype_copy_content_same_ddt and
+ * ompi_op_reduce on the user's pointers, coll_tuned_allreduce.c:166, 182-185).  Every device
+ * buffer of such a call is staged through host memory around it, exactly what coll/cuda does for
+ * each call it intercepts (coll_cuda_allreduce.c:43-75, coll_cuda_reduce.c:43-78,
+ * coll_cuda_reduce_scatter_block.c:45-83, coll_cuda_scan.c:41-76, coll_cuda_exscan.c:41-76;
+ * saved functions coll_cuda_module.c:120-157): the span true_extent + (count - 1) x extent is
+ * copied from the type's true lower bound and the host component gets the copy minus true_lb.
+ * (coll/cuda copies from the buffer pointer itself and passes copy - true_lb, which is the same
+ * thing for every type with true_lb == 0, the predefined ones.)  Nonblocking forms stage at
+ * initiation and copy back when the host request completes. */
+unsigned long mca_coll_mi355x_staged_calls;  /* calls that went through this staging (tests read it) */
+
+typedef struct {
+    char *h;       /* host copy (malloc); NULL: the buffer is not staged */
+    char *d;       /* first byte of the device span */
+    size_t back;   /* bytes copied back when the call succeeded (0: an input only) */
+} hstage_t;
+
+/* stage *arg when it is device memory (span bytes from its true lower bound); *arg becomes the
+ * pointer the host component gets.  fill: copy the device contents in. */
+static int hstage(hstage_t *s, void **arg, const struct ompi_datatype_t *dt, size_t span, int fill, size_t back)
+{
+    memset(s, 0, sizeof(*s));
+    void *buf = *arg;
+    if (!buf || buf == MPI_IN_PLACE || !is_dev(buf)) return OMPI_SUCCESS;
+    s->h = (char *)malloc(span ? span : 1);
+    if (!s->h) return OMPI_ERR_OUT_OF_RESOURCE;
+    s->d = (char *)buf + dt->super.true_lb;
+    s->back = back;
+    if (fill && span && mi355x_memcpy(s->h, s->d, span) != MI355X_SUCCESS) {
+        fprintf(stderr, "[coll/mi355x] staging: %s\n", mi355x_last_error());
+        free(s->h);
+        s->h = NULL;
+        return OMPI_ERROR;
+    }
+    *arg = s->h - dt->super.true_lb;
+    return OMPI_SUCCESS;
+}
+
+/* copy the result back (when rc is success) and release the copy; returns the call's status */
+static int hunstage(hstage_t *s, int rc)
+{
+    if (!s->h) return rc;
+    if (rc == OMPI_SUCCESS && s->back && mi355x_memcpy(s->d, s->h, s->back) != MI355X_SUCCESS) {
+        fprintf(stderr, "[coll/mi355x] staging: %s\n", mi355x_last_error());
+        rc = OMPI_ERROR;
+    }
+    free(s->h);
+    s->h = NULL;
+    return rc;
+}
+
+/* stage the send and receive sides of a reduction; on failure nothing stays staged */
+static int hstage2(hstage_t st[2], void **sa, size_t sspan, void **ra, size_t rspan, int rfill, size_t rback,
+                   const struct ompi_datatype_t *dt)
+{
+    int rc = hstage(&st[0], sa, dt, sspan, 1, 0);
+    if (rc == OMPI_SUCCESS && (rc = hstage(&st[1], ra, dt, rspan, rfill, rback)) != OMPI_SUCCESS) hunstage(&st[0], rc);
+    if (rc == OMPI_SUCCESS && (st[0].h || st[1].h)) __atomic_add_fetch(&mca_coll_mi355x_staged_calls, 1, __ATOMIC_RELAXED);
+    return rc;
+}
+
+static int hunstage2(hstage_t st[2], int rc)
+{
+    hunstage(&st[0], rc);
+    return hunstage(&st[1], rc);
+}
+
+/* the engine reduces (op, type slot t) on the device */
+static int engine_op(const struct ompi_op_t *op, int t)
+{
+    return (op->o_flags & OMPI_OP_FLAGS_INTRINSIC) && t >= 0 && mi355x_comm_op_supported(op->o_f_to_c_index, t);
+}
+
+static int staged_allreduce(mca_coll_mi355x_module_t *m, void *sbuf, void *rbuf, int count,
+                            struct ompi_datatype_t *dtype, struct ompi_op_t *op, struct ompi_communicator_t *comm)
+{
+    const size_t span = dt_span(dtype, (size_t)count);
+    hstage_t st[2];
+    const int rc = hstage2(st, &sbuf, span, &rbuf, span, sbuf == MPI_IN_PLACE, span, dtype);
+    if (rc != OMPI_SUCCESS) return rc;
+    return hunstage2(st, m->prev_allreduce(sbuf, rbuf, count, dtype, op, comm, m->prev_allreduce_module));
+}
+
 /* ------------------------------------------------------------------ collectives */
 int mca_coll_mi355x_allreduce(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
                               struct ompi_op_t *op, struct ompi_communicator_t *comm,
@@ -328,8 +437,8 @@ int mca_coll_mi355x_allreduce(void *sbuf, void *rbuf, int count, struct ompi_dat
     mca_coll_mi355x_module_t *m = MOD(module);
     const int inplace = (sbuf == MPI_IN_PLACE);
     const int t = reducible_type(dtype);
-    if (!(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 || !mi355x_op_supported(op->o_f_to_c_index, t) || count < 0)
-        return m->prev_allreduce(sbuf, rbuf, count, dtype, op, comm, m->prev_allreduce_module);
+    if (count < 0) return m->prev_allreduce(sbuf, rbuf, count, dtype, op, comm, m->prev_allreduce_module);
+    if (!engine_op(op, t)) return staged_allreduce(m, sbuf, rbuf, count, dtype, op, comm);
     const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
     ROUTE_OR(m->prev_allreduce(sbuf, rbuf, count, dtype, op, comm, m->prev_allreduce_module));
     if (dev) return map_rc(mi355x_allreduce(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)count, t, op->o_f_to_c_index, NULL));
@@ -350,9 +459,17 @@ int mca_coll_mi355x_reduce(void *sbuf, void *rbuf, int count, struct ompi_dataty
     const int me = mi355x_comm_rank_of(comm);
     const int inplace = (sbuf == MPI_IN_PLACE);
     const int t = reducible_type(dtype);
-    if ((inplace && me != root) || !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 ||
-        !mi355x_op_supported(op->o_f_to_c_index, t) || count < 0)
+    if ((inplace && me != root) || count < 0)
         return m->prev_reduce(sbuf, rbuf, count, dtype, op, root, comm, m->prev_reduce_module);
+    if (!engine_op(op, t)) {  /* coll_cuda_reduce.c:43-78; only the root's rbuf is significant */
+        const size_t span = dt_span(dtype, (size_t)count);
+        hstage_t st[2];
+        void *ra = me == root ? rbuf : NULL;
+        const int rc = hstage2(st, &sbuf, span, &ra, span, inplace, span, dtype);
+        if (rc != OMPI_SUCCESS) return rc;
+        return hunstage2(st, m->prev_reduce(sbuf, me == root ? ra : rbuf, count, dtype, op, root, comm,
+                                            m->prev_reduce_module));
+    }
     const int dev = (me != root || is_dev(rbuf)) && (inplace || is_dev(sbuf));
     ROUTE_OR(m->prev_reduce(sbuf, rbuf, count, dtype, op, root, comm, m->prev_reduce_module));
     if (dev)
@@ -373,8 +490,17 @@ int mca_coll_mi355x_reduce_scatter_block(void *sbuf, void *rbuf, int rcount, str
     mca_coll_mi355x_module_t *m = MOD(module);
     const int inplace = (sbuf == MPI_IN_PLACE);
     const int t = reducible_type(dtype);
-    if (!(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 || !mi355x_op_supported(op->o_f_to_c_index, t) || rcount < 0)
+    if (rcount < 0)
         return m->prev_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, m->prev_reduce_scatter_block_module);
+    if (!engine_op(op, t)) {  /* coll_cuda_reduce_scatter_block.c:45-83 (in place: rbuf holds the n blocks) */
+        const size_t in = dt_span(dtype, (size_t)rcount * (size_t)mi355x_comm_size_of(comm));
+        const size_t out = dt_span(dtype, (size_t)rcount);
+        hstage_t st[2];
+        const int rc = hstage2(st, &sbuf, in, &rbuf, inplace ? in : out, inplace, out, dtype);
+        if (rc != OMPI_SUCCESS) return rc;
+        return hunstage2(st, m->prev_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm,
+                                                          m->prev_reduce_scatter_block_module));
+    }
     const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
     ROUTE_OR(m->prev_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, m->prev_reduce_scatter_block_module));
     if (dev)
@@ -396,14 +522,19 @@ int mca_coll_mi355x_reduce_scatter(void *sbuf, void *rbuf, int *rcounts, struct 
     mca_coll_mi355x_module_t *m = MOD(module);
     const int inplace = (sbuf == MPI_IN_PLACE);
     const int t = reducible_type(dtype);
-    if (!(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 || !mi355x_op_supported(op->o_f_to_c_index, t))
-        return m->prev_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, m->prev_reduce_scatter_module);
-    const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
-    ROUTE_OR(m->prev_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, m->prev_reduce_scatter_module));
-    if (dev) return map_rc(mi355x_reduce_scatter(m->engine, inplace ? NULL : sbuf, rbuf, rcounts, t, op->o_f_to_c_index, NULL));
     const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm);
     size_t total = 0;
     for (int q = 0; q < n; ++q) total += (size_t)(rcounts[q] > 0 ? rcounts[q] : 0);
+    if (!engine_op(op, t)) {  /* staged like reduce_scatter_block (in place: rbuf holds every block) */
+        const size_t in = dt_span(dtype, total), out = dt_span(dtype, (size_t)(rcounts[me] > 0 ? rcounts[me] : 0));
+        hstage_t st[2];
+        const int rc = hstage2(st, &sbuf, in, &rbuf, inplace ? in : out, inplace, out, dtype);
+        if (rc != OMPI_SUCCESS) return rc;
+        return hunstage2(st, m->prev_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, m->prev_reduce_scatter_module));
+    }
+    const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
+    ROUTE_OR(m->prev_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, m->prev_reduce_scatter_module));
+    if (dev) return map_rc(mi355x_reduce_scatter(m->engine, inplace ? NULL : sbuf, rbuf, rcounts, t, op->o_f_to_c_index, NULL));
     const size_t esz = mi355x_type_size(t), in = total * esz, out = (size_t)(rcounts[me] > 0 ? rcounts[me] : 0) * esz;
     int rc = MI355X_SUCCESS;
     void *rd = inplace ? dev_in(m, 1, rbuf, in, &rc) : dev_out(m, 1, rbuf, out, &rc);
@@ -727,12 +858,34 @@ static int scan_common(mca_coll_mi355x_module_t *m, int exclusive, void *sbuf, v
 {
     const int inplace = (sbuf == MPI_IN_PLACE);
     const int t = reducible_type(dtype);
-    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 ||
-        count < 0 || !mi355x_op_supported(op->o_f_to_c_index, t))
-        return exclusive ? m->prev_exscan(sbuf, rbuf, count, dtype, op, comm, m->prev_exscan_module)
-                         : m->prev_scan(sbuf, rbuf, count, dtype, op, comm, m->prev_scan_module);
-    return map_rc((exclusive ? mi355x_exscan : mi355x_scan)(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)count, t,
-                                                            op->o_f_to_c_index, NULL));
+#define SCAN_PREV(S, R)                                                                              \
+    (exclusive ? m->prev_exscan(S, R, count, dtype, op, comm, m->prev_exscan_module)                 \
+               : m->prev_scan(S, R, count, dtype, op, comm, m->prev_scan_module))
+    if (count < 0) return SCAN_PREV(sbuf, rbuf);
+    if (!engine_op(op, t)) {
+        /* coll_cuda_scan.c:41-76 / coll_cuda_exscan.c:41-76; rbuf is copied in for MPI_IN_PLACE and
+         * for exscan (rank 0's rbuf is left as it was) */
+        const size_t span = dt_span(dtype, (size_t)count);
+        hstage_t st[2];
+        const int rc = hstage2(st, &sbuf, span, &rbuf, span, inplace || exclusive, span, dtype);
+        if (rc != OMPI_SUCCESS) return rc;
+        return hunstage2(st, SCAN_PREV(sbuf, rbuf));
+    }
+    /* every rank votes its buffer kind, as for allreduce: a rank with host buffers joins the engine
+     * on device copies when a peer has device buffers */
+    const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
+    ROUTE_OR(SCAN_PREV(sbuf, rbuf));
+#undef SCAN_PREV
+    if (dev)
+        return map_rc((exclusive ? mi355x_exscan : mi355x_scan)(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)count,
+                                                                t, op->o_f_to_c_index, NULL));
+    const size_t bytes = (size_t)count * mi355x_type_size(t);
+    int rc = MI355X_SUCCESS;
+    void *rd = (inplace || exclusive) ? dev_in(m, 1, rbuf, bytes, &rc) : dev_out(m, 1, rbuf, bytes, &rc);
+    const void *sd = inplace ? NULL : dev_in(m, 0, sbuf, bytes, &rc);
+    if (rc == MI355X_SUCCESS)
+        rc = (exclusive ? mi355x_exscan : mi355x_scan)(m->engine, sd, rd, (size_t)count, t, op->o_f_to_c_index, NULL);
+    return map_rc(copy_back(rbuf, rd, bytes, rc));
 }
 
 int mca_coll_mi355x_scan(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
@@ -775,6 +928,10 @@ typedef struct mi355x_nbreq_t {
     struct ompi_datatype_t *pdt;
     int ppeer, ptag, pmode;
     int free_called;               /* MPI_Request_free while active: released at completion */
+    /* a declined nonblocking reduction: the lower-priority component's request on host copies of
+     * the device buffers (coll/cuda's staging, copied back when it completes) */
+    ompi_request_t *inner;
+    hstage_t hs[2];
 } mi355x_nbreq_t;
 
 static pthread_mutex_t nb_lock = PTHREAD_MUTEX_INITIALIZER;
@@ -787,6 +944,7 @@ static int nb_registered;
 static int nbreq_free(ompi_request_t **rp)
 {
     mi355x_nbreq_t *r = (mi355x_nbreq_t *)*rp;
+    if (true != r->super.req_complete && r->inner) return MPI_ERR_REQUEST;
     if (true != r->super.req_complete && r->eng) {
         if (!r->p2p) return MPI_ERR_REQUEST;
         pthread_mutex_lock(&nb_lock);
@@ -836,6 +994,8 @@ static void nbreq_construct(opal_object_t *o)
     r->pdt = NULL;
     r->ppeer = r->ptag = r->pmode = 0;
     r->free_called = 0;
+    r->inner = NULL;
+    memset(r->hs, 0, sizeof(r->hs));
 }
 
 /* completion-time unpack of a derived-datatype nonblocking collective (local work only) */
@@ -867,6 +1027,22 @@ static int nb_progress(void)
     int completed = 0;
     for (mi355x_nbreq_t **p = &nb_active; *p;) {
         mi355x_nbreq_t *r = *p;
+        if (r->inner) {  /* a staged host request: done when the lower-priority request is */
+            if (true != r->inner->req_complete) {
+                p = &r->next;
+                continue;
+            }
+            *p = r->next;
+            ompi_request_t *in = r->inner;
+            int rc = in->req_status.MPI_ERROR;
+            r->inner = NULL;
+            if (in != &ompi_request_null.request && in->req_free) in->req_free(&in);
+            rc = hunstage2(r->hs, rc);
+            r->super.req_status.MPI_ERROR = rc;
+            mi355x_ompi_request_complete(&r->super, true);
+            completed++;
+            continue;
+        }
         int done = 0;
         const int rc0 = mi355x_request_test(r->eng, &done);
         if (!done) {
@@ -985,6 +1161,48 @@ static int nb_start(mi355x_request_t *eng, struct ompi_communicator_t *comm, omp
         return m->prev_##FN(__VA_ARGS__, m->prev_##FN##_module);                      \
     } while (0)
 
+/* hand the lower-priority component's request to MPI: as it is when nothing was staged, else
+ * wrapped so that the staged results are copied back when it completes (nb_progress) */
+static int nb_staged_start(struct ompi_communicator_t *comm, ompi_request_t **request, hstage_t st[2],
+                           ompi_request_t *inner, int rc)
+{
+    if (!st[0].h && !st[1].h) {
+        if (rc == OMPI_SUCCESS) *request = inner;
+        return rc;
+    }
+    if (rc != OMPI_SUCCESS) return hunstage2(st, rc);
+    mi355x_nbreq_t *r = (mi355x_nbreq_t *)mi355x_obj_new(&mi355x_nbreq_t_class);
+    if (!r) {  /* cannot wrap: finish the call here (the staged copies must outlive it) */
+        while (true != inner->req_complete) opal_progress();
+        const int err = inner->req_status.MPI_ERROR;
+        if (inner != &ompi_request_null.request && inner->req_free) inner->req_free(&inner);
+        return hunstage2(st, err) == OMPI_SUCCESS ? OMPI_ERR_OUT_OF_RESOURCE : OMPI_ERROR;
+    }
+    r->inner = inner;
+    r->hs[0] = st[0];
+    r->hs[1] = st[1];
+    r->super.req_complete = false;
+    r->super.req_persistent = false;
+    r->super.req_state = OMPI_REQUEST_ACTIVE;
+    r->super.req_status.MPI_ERROR = 0;
+    r->super.req_mpi_object.comm = comm;
+    nb_activate(r);
+    *request = &r->super;
+    return OMPI_SUCCESS;
+}
+
+/* the declined / host-buffer form of a nonblocking reduction: device buffers staged to the host */
+#define NB_STAGED(FN, SSPAN, RSPAN, RFILL, RBACK, DT, ...)                                       \
+    do {                                                                                          \
+        if (!m->prev_##FN) return OMPI_ERR_NOT_SUPPORTED;                                         \
+        hstage_t st_[2];                                                                          \
+        int rc_ = hstage2(st_, &sbuf, (SSPAN), &rbuf, (RSPAN), (RFILL), (RBACK), (DT));           \
+        if (rc_ != OMPI_SUCCESS) return rc_;                                                      \
+        ompi_request_t *in_ = NULL;                                                               \
+        rc_ = m->prev_##FN(__VA_ARGS__, &in_, m->prev_##FN##_module);                             \
+        return nb_staged_start(comm, request, st_, in_, rc_);                                     \
+    } while (0)
+
 int mca_coll_mi355x_iallreduce(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
                                struct ompi_communicator_t *comm, ompi_request_t **request,
                                mca_coll_base_module_t *module)
@@ -992,9 +1210,11 @@ int mca_coll_mi355x_iallreduce(void *sbuf, void *rbuf, int count, struct ompi_da
     mca_coll_mi355x_module_t *m = MOD(module);
     const int inplace = (sbuf == MPI_IN_PLACE);
     const int t = reducible_type(dtype);
-    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 ||
-        !mi355x_op_supported(op->o_f_to_c_index, t))
-        NB_FALLBACK(iallreduce, sbuf, rbuf, count, dtype, op, comm, request);
+    if (count < 0) NB_FALLBACK(iallreduce, sbuf, rbuf, count, dtype, op, comm, request);
+    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || !engine_op(op, t)) {
+        const size_t span = dt_span(dtype, (size_t)count);
+        NB_STAGED(iallreduce, span, span, inplace, span, dtype, sbuf, rbuf, count, dtype, op, comm);
+    }
     mi355x_request_t *eng = NULL;
     int rc = mi355x_iallreduce(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)count, t, op->o_f_to_c_index, NULL, &eng);
     return rc ? map_rc(rc) : nb_start(eng, comm, request);
@@ -1008,9 +1228,12 @@ int mca_coll_mi355x_ireduce(void *sbuf, void *rbuf, int count, struct ompi_datat
     const int me = mi355x_comm_rank_of(comm);
     const int inplace = (sbuf == MPI_IN_PLACE);
     const int t = reducible_type(dtype);
-    if ((me == root && !is_dev(rbuf)) || (!inplace && !is_dev(sbuf)) || (inplace && me != root) ||
-        !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 || !mi355x_op_supported(op->o_f_to_c_index, t))
-        NB_FALLBACK(ireduce, sbuf, rbuf, count, dtype, op, root, comm, request);
+    if (count < 0 || (inplace && me != root)) NB_FALLBACK(ireduce, sbuf, rbuf, count, dtype, op, root, comm, request);
+    if ((me == root && !is_dev(rbuf)) || (!inplace && !is_dev(sbuf)) || !engine_op(op, t)) {
+        const size_t span = dt_span(dtype, (size_t)count);
+        if (me != root) rbuf = NULL;  /* not significant off the root: never staged */
+        NB_STAGED(ireduce, span, span, inplace, span, dtype, sbuf, rbuf, count, dtype, op, root, comm);
+    }
     mi355x_request_t *eng = NULL;
     int rc = mi355x_ireduce(m->engine, inplace ? NULL : sbuf, me == root ? rbuf : NULL, (size_t)count, t,
                             op->o_f_to_c_index, root, NULL, &eng);
@@ -1024,9 +1247,13 @@ int mca_coll_mi355x_ireduce_scatter_block(void *sbuf, void *rbuf, int rcount, st
     mca_coll_mi355x_module_t *m = MOD(module);
     const int inplace = (sbuf == MPI_IN_PLACE);
     const int t = reducible_type(dtype);
-    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC) || t < 0 ||
-        !mi355x_op_supported(op->o_f_to_c_index, t))
-        NB_FALLBACK(ireduce_scatter_block, sbuf, rbuf, rcount, dtype, op, comm, request);
+    if (rcount < 0) NB_FALLBACK(ireduce_scatter_block, sbuf, rbuf, rcount, dtype, op, comm, request);
+    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || !engine_op(op, t)) {
+        const size_t in = dt_span(dtype, (size_t)rcount * (size_t)mi355x_comm_size_of(comm));
+        const size_t out = dt_span(dtype, (size_t)rcount);
+        NB_STAGED(ireduce_scatter_block, in, inplace ? in : out, inplace, out, dtype, sbuf, rbuf, rcount, dtype, op,
+                  comm);
+    }
     mi355x_request_t *eng = NULL;
     int rc = mi355x_ireduce_scatter_block(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)rcount, t,
                                           op->o_f_to_c_index, NULL, &eng);
@@ -1069,8 +1296,21 @@ int mca_coll_mi355x_iallgather(void *sbuf, int scount, struct ompi_datatype_t *s
     mca_coll_mi355x_module_t *m = MOD(module);
     const int inplace = (sbuf == MPI_IN_PLACE);
     size_t rb = 0, sb = 0;
-    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || rcount < 0 || (!inplace && scount < 0))
+    if (rcount < 0 || (!inplace && scount < 0))
         NB_FALLBACK(iallgather, sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, request);
+    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf))) {  /* a host side: device sides staged */
+        if (!m->prev_iallgather) return OMPI_ERR_NOT_SUPPORTED;
+        const size_t n = (size_t)mi355x_comm_size_of(comm);
+        hstage_t st[2];
+        int rc = hstage(&st[0], &sbuf, sdtype, inplace ? 0 : dt_span(sdtype, (size_t)scount), 1, 0);
+        if (rc != OMPI_SUCCESS) return rc;
+        const size_t rspan = dt_span(rdtype, (size_t)rcount * n);
+        if ((rc = hstage(&st[1], &rbuf, rdtype, rspan, inplace, rspan)) != OMPI_SUCCESS) return hunstage(&st[0], rc);
+        if (st[0].h || st[1].h) __atomic_add_fetch(&mca_coll_mi355x_staged_calls, 1, __ATOMIC_RELAXED);
+        ompi_request_t *inner = NULL;
+        rc = m->prev_iallgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, &inner, m->prev_iallgather_module);
+        return nb_staged_start(comm, request, st, inner, rc);
+    }
     mi355x_request_t *eng = NULL;
     if (contiguous_bytes(rdtype, rcount, &rb) && (inplace || (contiguous_bytes(sdtype, scount, &sb) && sb == rb))) {
         int rc = mi355x_iallgather(m->engine, inplace ? NULL : sbuf, rbuf, rb, NULL, &eng);

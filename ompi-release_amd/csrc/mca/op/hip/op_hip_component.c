@@ -65,8 +65,10 @@ static void die(const char *what)
     abort();
 }
 
-/* x87 long double slots have no GPU form: op/hip takes them only to stage device buffers */
-static int host_only_type(int t)
+/* x87 long double slots: MAX/MIN (and MAXLOC/MINLOC on MPI_LONG_DOUBLE_INT) compare and select,
+ * which the GPU does exactly on the 80-bit encoding; SUM/PROD need 80-bit arithmetic, so op/hip
+ * takes those slots only to stage device buffers to the base loops */
+static int x87_type(int t)
 {
     return t == MI355X_T_LONG_DOUBLE || t == MI355X_T_C_LONG_DOUBLE_COMPLEX || t == MI355X_T_LONG_DOUBLE_INT;
 }
@@ -114,7 +116,7 @@ void mca_op_hip_2buff(void *in, void *inout, int *count, struct ompi_datatype_t 
         m->prev2[t](in, inout, count, dtype, m->prev2_mod[t]);
         return;
     }
-    if (host_only_type(t)) {
+    if (!mi355x_op_supported(m->op, t)) {  /* an x87 arithmetic slot */
         staged_host2(m, t, in, inout, count, dtype, din, dio);
         return;
     }
@@ -152,7 +154,7 @@ void mca_op_hip_3buff(void *in1, void *in2, void *out, int *count, struct ompi_d
         return;
     }
     const size_t bytes = (size_t)*count * mi355x_type_size(t);
-    if (host_only_type(t)) {
+    if (!mi355x_op_supported(m->op, t)) {  /* an x87 arithmetic slot */
         void *h1 = malloc(bytes), *h2 = malloc(bytes), *ho = malloc(bytes);
         if (!h1 || !h2 || !ho || mi355x_memcpy(h1, in1, bytes) || mi355x_memcpy(h2, in2, bytes)) die("stage");
         m->prev3[t](h1, h2, ho, count, dtype, m->prev3_mod[t]);
@@ -246,9 +248,7 @@ static struct ompi_op_base_module_1_0_0_t *component_op_query(struct ompi_op_t *
     m->op = code;
     m->super.opm_enable = module_enable;
     for (int t = 0; t < OMPI_OP_BASE_TYPE_MAX; ++t) {
-        if (mi355x_op_supported(code, t) || (host_only_type(t) && (code == MI355X_OP_MAX || code == MI355X_OP_MIN ||
-                                                                  code == MI355X_OP_SUM || code == MI355X_OP_PROD ||
-                                                                  code == MI355X_OP_MAXLOC || code == MI355X_OP_MINLOC))) {
+        if (mi355x_op_supported(code, t) || (x87_type(t) && (code == MI355X_OP_SUM || code == MI355X_OP_PROD))) {
             m->super.opm_fns[t] = mca_op_hip_2buff;
             m->super.opm_3buff_fns[t] = mca_op_hip_3buff;
         }

@@ -456,4 +456,9 @@ int launch_tree_slot(int op, int type, const TreeArgs &a, hipStream_t s)
     return sl->tree(a, s);
 }
 
+bool coll_slot_supported(int op, int type) { return cslot(op, type) != nullptr; }
+
 } // namespace mi355x
+
+// every kernel family of the engine instantiates the same slot list (slot_list.hpp)
+extern "C" int mi355x_comm_op_supported(int op, int type) { return mi355x::coll_slot_supported(op, type) ? 1 : 0; }

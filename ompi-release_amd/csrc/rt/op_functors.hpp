@@ -41,6 +41,53 @@ static_assert(sizeof(p_2int) == 8, "2int");
 static_assert(sizeof(p_short_int) == 8, "short_int");
 static_assert(sizeof(cf32) == 8 && sizeof(cf64) == 16, "complex");
 
+// x86-64 `long double`: the x87 80-bit extended format (64-bit significand with an explicit
+// integer bit, 15-bit exponent, sign) in 16 bytes of storage aligned to 16.  The GPU has no
+// arithmetic for it, but MAX/MIN/MAXLOC/MINLOC only compare and select, and an x87 compare is
+// exact integer work on the encoding:
+//   * NaNs, and the encodings the 387 rejects as invalid operands (pseudo-NaN / pseudo-infinity:
+//     exponent 0x7fff with the integer bit clear; unnormals: exponent 1..0x7ffe with the integer
+//     bit clear), compare unordered -- every relation false, as FCOMI/FUCOMI report them;
+//   * zero, denormals and pseudo-denormals (exponent 0) take effective exponent 1, so a
+//     pseudo-denormal equals the normal of the same significand and +0 == -0;
+//   * ordered values compare by sign, then (effective exponent, significand) lexicographically.
+// A selected operand keeps its bits (FLD / FSTP of an m80 operand copy them unchanged).
+struct alignas(16) f80 {
+    uint64_t m;
+    uint16_t se;
+    uint16_t pad[3];
+};
+static_assert(sizeof(f80) == 16, "x86-64 long double storage");
+
+#define MI_DEV __device__ __forceinline__
+// -1 / 0 / +1, or 2 when unordered
+MI_DEV int x87_cmp(const f80 &a, const f80 &b)
+{
+    uint32_t ea = a.se & 0x7fffu, eb = b.se & 0x7fffu;
+    const bool ia = (a.m >> 63) != 0, ib = (b.m >> 63) != 0;
+    const bool oka = ea == 0x7fffu ? (ia && (a.m << 1) == 0) : (ea == 0 || ia);
+    const bool okb = eb == 0x7fffu ? (ib && (b.m << 1) == 0) : (eb == 0 || ib);
+    if (!oka || !okb) return 2;
+    if (ea == 0) ea = 1;
+    if (eb == 0) eb = 1;
+    if (a.m == 0 && b.m == 0) return 0;  // +-0 (an ordered nonzero value has a nonzero significand)
+    const bool na = (a.se >> 15) != 0, nb = (b.se >> 15) != 0;
+    if (na != nb) return na ? -1 : 1;
+    const int mag = ea != eb ? (ea < eb ? -1 : 1) : (a.m != b.m ? (a.m < b.m ? -1 : 1) : 0);
+    return na ? -mag : mag;
+}
+MI_DEV bool operator>(const f80 &a, const f80 &b) { return x87_cmp(a, b) == 1; }
+MI_DEV bool operator<(const f80 &a, const f80 &b) { return x87_cmp(a, b) == -1; }
+MI_DEV bool operator==(const f80 &a, const f80 &b) { return x87_cmp(a, b) == 0; }
+#undef MI_DEV
+
+// MPI_LONG_DOUBLE_INT: {long double v; int k;} -- 32 bytes (LOC_STRUCT, op_base_functions.c:554)
+struct alignas(16) p_ldouble_int {
+    f80 v;
+    int k;
+};
+static_assert(sizeof(p_ldouble_int) == 32, "long_double_int");
+
 // unsigned twin used for wrap-around integer arithmetic (signed overflow is UB in C++; the
 // reference relies on gcc's two's-complement code generation, which this reproduces)
 template <typename T> struct uns { using type = T; };

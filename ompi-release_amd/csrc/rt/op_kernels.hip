@@ -211,12 +211,30 @@ static int launch_shape(const StreamArgs &args, hipStream_t s)
     return MI355X_SUCCESS;
 }
 
+// elements wider than one 16-B vector (MPI_LONG_DOUBLE_INT, 32 B): one element per lane, two
+// dwordx4 accesses each (the pair is consumed whole by the lane that loads it)
+template <class F, bool THREE>
+__global__ __launch_bounds__(256) void k_wide(const typename F::T *a, const typename F::T *b, typename F::T *o, size_t n)
+{
+    const size_t nthr = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nthr) o[i] = apply<F, THREE>(a[i], b[i]);
+}
+
 template <class F, bool THREE>
 static int launch(const void *a, const void *b, void *out, size_t n, hipStream_t s)
 {
     using T = typename F::T;
-    constexpr size_t EPV = 16 / sizeof(T);
     if (n == 0) return MI355X_SUCCESS;
+    if constexpr (sizeof(T) > 16) {
+        size_t blocks = (n + 255) / 256;
+        const size_t cap = (size_t)stream_tune().blocks_per_cu * (size_t)device_cu_count();
+        if (blocks > cap) blocks = cap;
+        hipLaunchKernelGGL((k_wide<F, THREE>), dim3((unsigned)blocks), dim3(256), 0, s, static_cast<const T *>(a),
+                           static_cast<const T *>(b), static_cast<T *>(out), n);
+        MI_HIP(hipGetLastError());
+        return MI355X_SUCCESS;
+    } else {
+    constexpr size_t EPV = 16 / sizeof(T);
     StreamArgs args;
     args.a = a;
     args.b = b;
@@ -255,6 +273,7 @@ static int launch(const void *a, const void *b, void *out, size_t n, hipStream_t
         return ntm ? launch_shape<F, THREE, kDefaultUnroll, 3>(args, s)
                    : launch_shape<F, THREE, kDefaultUnroll, 0>(args, s);
     }
+    }
 }
 
 // ------------------------------------------------------------------ dispatch table
@@ -288,8 +307,7 @@ struct Table {
     Slot s[MI355X_OP_MAX_][MI355X_T_MAX];
     Table()
     {
-        // groups as in op_base_functions.c:1373-1457 (Fortran types disabled; long double
-        // slots have no GPU form)
+        // groups as in op_base_functions.c:1373-1457 (Fortran types disabled)
         put_ints<OpMax>(s, MI355X_OP_MAX);
         put<OpMax<float>>(s, MI355X_OP_MAX, MI355X_T_FLOAT);
         put<OpMax<double>>(s, MI355X_OP_MAX, MI355X_T_DOUBLE);
@@ -328,6 +346,12 @@ struct Table {
         put<OpLoc<p_long_int, false>>(s, MI355X_OP_MINLOC, MI355X_T_LONG_INT);
         put<OpLoc<p_2int, false>>(s, MI355X_OP_MINLOC, MI355X_T_2INT);
         put<OpLoc<p_short_int, false>>(s, MI355X_OP_MINLOC, MI355X_T_SHORT_INT);
+        // x87 long double: the compare-and-select slots (SUM/PROD need 80-bit arithmetic and
+        // stay on the host base loops, op/hip stages them)
+        put<OpMax<f80>>(s, MI355X_OP_MAX, MI355X_T_LONG_DOUBLE);
+        put<OpMin<f80>>(s, MI355X_OP_MIN, MI355X_T_LONG_DOUBLE);
+        put<OpLoc<p_ldouble_int, true>>(s, MI355X_OP_MAXLOC, MI355X_T_LONG_DOUBLE_INT);
+        put<OpLoc<p_ldouble_int, false>>(s, MI355X_OP_MINLOC, MI355X_T_LONG_DOUBLE_INT);
     }
 };
 

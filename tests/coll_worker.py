@@ -758,6 +758,225 @@ def tuned_vars_main():
     print(f"rank {rank} tuned_vars OK", flush=True)
 
 
+def _linear(oracle, code, slot, xs):
+    """coll/basic's linear reduction order (coll_basic_reduce.c:215-250): acc = x[n-1], then
+    acc = x[i] op acc for i = n-2..0, through the oracle's 2-buff loop"""
+    acc = xs[-1].copy()
+    for x in reversed(xs[:-1]):
+        assert oracle.oracle_op_2buff(code, slot, x.ctypes.data, acc.ctypes.data, len(acc)) == 0
+    return acc
+
+
+def staging_main():
+    """coll/cuda's host staging (coll_cuda_allreduce.c:43-75 & siblings) for the reductions the engine
+    declines, over a lower-priority module that really reduces on the CPU (the harness's host module:
+    coll/basic's orders through the host channel) and fails any call that hands it device memory:
+      * a non-commutative user MPI_Op (a op b = 3a + b on MPI_INT) on device buffers, rank 0 on host
+        buffers: allreduce (also in place), reduce, reduce_scatter_block, reduce_scatter, scan, exscan,
+        iallreduce, ireduce, ireduce_scatter_block;
+      * MPI_SUM / MPI_PROD over MPI_LONG_DOUBLE and MAXLOC / MINLOC over MPI_LONG_DOUBLE_INT (no
+        engine fold: 80-bit arithmetic / 32-byte pairs) on device buffers;
+      * MAXLOC / MINLOC over the other five pair types (built as libmpi builds them: OPAL-predefined
+        flag cleared, DOUBLE_INT 12 bytes in 16) and MAX / MIN over MPI_LONG_DOUBLE on device
+        buffers are served by the engine, bit-exact with the oracle, with nothing staged;
+      * host buffers on every rank reach the host module and come back reduced.
+    The host module never saw a device pointer."""
+    rank, size = int(sys.argv[1]), int(sys.argv[2])
+    import torch
+    torch.cuda.set_device(rank % torch.cuda.device_count())
+    m = mini()
+    L, pkg = m.lib, m.pkg
+    oracle = load_oracle()
+    m.install_oracle_base(oracle)
+    vp = ctypes.c_void_p
+    L.mini_host_module.restype = vp
+    L.mini_op_create_user.restype = vp
+    L.mini_op_create_user.argtypes = [vp, ctypes.c_int]
+    comm = L.mini_comm_create(rank, size, 42)
+    assert L.mini_comm_set_channel(comm, sys.argv[3].encode()) == 0
+    L.mini_comm_install(comm, L.mini_host_module())
+    assert L.mini_coll_select(comm, m.component_ptr(m.coll, "mca_coll_mi355x_component")) == 90
+    staged = ctypes.c_ulong.in_dll(m.coll, "mca_coll_mi355x_staged_calls")
+    ptrs = lambda arrs: (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    host = rank == 0
+
+    def put(a, on_host=False):
+        if on_host:
+            h = np.ascontiguousarray(a).copy()
+            return h, h.ctypes.data, (lambda: h.copy())
+        d = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).cuda()
+        return d, d.data_ptr(), (lambda: d.cpu().numpy().view(a.dtype).copy())
+
+    say = lambda what: print(f"rank {rank} staging: {what}", flush=True)
+    say("selected")
+    # ---- 1. a non-commutative user op: inout = 3 * in + inout (int32, wrapping)
+    USER = ctypes.CFUNCTYPE(None, vp, vp, ctypes.POINTER(ctypes.c_int), vp)
+
+    @USER
+    def user_fn(invec, inoutvec, lenp, dtp):
+        n = lenp[0]
+        a = np.ctypeslib.as_array(ctypes.cast(invec, ctypes.POINTER(ctypes.c_int32)), (n,))
+        b = np.ctypeslib.as_array(ctypes.cast(inoutvec, ctypes.POINTER(ctypes.c_int32)), (n,))
+        b[:] = a * np.int32(3) + b
+
+    uop = L.mini_op_create_user(ctypes.cast(user_fn, vp).value, 0)
+    idt = m.dtype_for_slot(pkg.T["INT32"])
+    f = lambda a, b: (a * np.int32(3) + b).astype(np.int32)   # a op b, a = in, b = inout
+    count = 70_003   # several host-channel slots
+    xs = [(np.arange(count, dtype=np.int32) * (r + 2) + 11 * r).astype(np.int32) for r in range(size)]
+    lin = xs[-1].copy()
+    for x in reversed(xs[:-1]):
+        lin = f(x, lin)
+    before = staged.value
+    sk, sp, _ = put(xs[rank], host)   # (keep the buffer alive)
+    rb, rp, rread = put(np.zeros(count, np.int32), host)
+    torch.cuda.synchronize()
+    assert L.mini_allreduce(comm, sp, rp, count, idt, uop) == 0
+    assert np.array_equal(rread(), lin), "user-op allreduce"
+    ib, ip, iread = put(xs[rank], host)
+    torch.cuda.synchronize()
+    assert L.mini_allreduce(comm, 1, ip, count, idt, uop) == 0      # MPI_IN_PLACE
+    assert np.array_equal(iread(), lin), "user-op allreduce in place"
+    root = size - 1
+    rb2, rp2, rread2 = put(np.zeros(count, np.int32), host)
+    torch.cuda.synchronize()
+    assert L.mini_reduce(comm, sp, rp2 if rank == root else None, count, idt, uop, root) == 0
+    if rank == root:
+        assert np.array_equal(rread2(), lin), "user-op reduce"
+    rc = 3001
+    ys = [(np.arange(rc * size, dtype=np.int32) - 77 * r).astype(np.int32) for r in range(size)]
+    ylin = ys[-1].copy()
+    for y in reversed(ys[:-1]):
+        ylin = f(y, ylin)
+    yk, ysp, _ = put(ys[rank], host)
+    ob, op_, oread = put(np.zeros(rc, np.int32), host)
+    torch.cuda.synchronize()
+    assert L.mini_reduce_scatter_block(comm, ysp, op_, rc, idt, uop) == 0
+    assert np.array_equal(oread(), ylin[rank * rc:(rank + 1) * rc]), "user-op reduce_scatter_block"
+    counts = [rc - 5 * q for q in range(size)]
+    tot = sum(counts)
+    lo = sum(counts[:rank])
+    vk, vsp, _ = put(ys[rank][:tot], host)
+    wb, wp, wread = put(np.zeros(counts[rank], np.int32), host)
+    torch.cuda.synchronize()
+    assert L.mini_reduce_scatter(comm, vsp, wp, (ctypes.c_int * size)(*counts), idt, uop) == 0
+    assert np.array_equal(wread(), ylin[:tot][lo:lo + counts[rank]]), "user-op reduce_scatter"
+    chain = [xs[0].copy()]
+    for x in xs[1:]:
+        chain.append(f(chain[-1], x))
+    for exclusive in (0, 1):
+        sentinel = np.full(count, -9, np.int32)
+        cb, cp, cread = put(sentinel, host)
+        torch.cuda.synchronize()
+        fn = L.mini_exscan if exclusive else L.mini_scan
+        assert fn(comm, sp, cp, count, idt, uop) == 0
+        want = (chain[rank - 1] if rank else sentinel) if exclusive else chain[rank]
+        assert np.array_equal(cread(), want), ("user-op scan", exclusive)
+    say("blocking user-op calls done")
+    # nonblocking forms: staged at initiation, copied back when the host request completes
+    reqs = [ctypes.c_void_p() for _ in range(3)]
+    nb1, np1, nread1 = put(np.zeros(count, np.int32), host)
+    nb2, np2, nread2 = put(np.zeros(count, np.int32), host)
+    nb3, np3, nread3 = put(np.zeros(rc, np.int32), host)
+    torch.cuda.synchronize()
+    assert L.mini_iallreduce(comm, sp, np1, count, idt, uop, ctypes.byref(reqs[0])) == 0
+    assert L.mini_ireduce(comm, sp, np2 if rank == 0 else None, count, idt, uop, 0, ctypes.byref(reqs[1])) == 0
+    assert L.mini_ireduce_scatter_block(comm, ysp, np3, rc, idt, uop, ctypes.byref(reqs[2])) == 0
+    for q in reqs:
+        assert L.mini_wait(ctypes.byref(q)) == 0
+    assert np.array_equal(nread1(), lin), "user-op iallreduce"
+    if rank == 0:
+        assert np.array_equal(nread2(), lin), "user-op ireduce"
+    assert np.array_equal(nread3(), ylin[rank * rc:(rank + 1) * rc]), "user-op ireduce_scatter_block"
+    # ten calls, each staged once on a rank with device buffers (rank 0's host buffers need none)
+    assert staged.value - before == (0 if host else 10), staged.value - before
+    L.mini_op_destroy(uop)
+
+    say("user op done")
+    # ---- 2. x87 slots with no engine fold: SUM / PROD over LONG_DOUBLE, MAXLOC / MINLOC over
+    #         LONG_DOUBLE_INT -- device buffers staged to the host module (coll/basic's linear order)
+    for opname, tname in (("SUM", "LONG_DOUBLE"), ("PROD", "LONG_DOUBLE"), ("MAXLOC", "LONG_DOUBLE_INT"),
+                          ("MINLOC", "LONG_DOUBLE_INT")):
+        code, slot = pkg.OP[opname], pkg.T[tname]
+        assert not pkg.rt().mi355x_comm_op_supported(code, slot)
+        op = m.select_op(code)
+        dt = m.dtype_for_slot(slot)
+        n = 20_001
+        xs2 = [opdata.make(tname, n, 40 + r) for r in range(size)]
+        want = _linear(oracle, code, slot, xs2)
+        before = staged.value
+        d, dp, read = put(xs2[rank])
+        o, opp, oread2 = put(np.zeros_like(xs2[0]))
+        torch.cuda.synchronize()
+        assert L.mini_allreduce(comm, dp, opp, n, dt, op) == 0
+        opdata.assert_same(tname, opname, oread2(), want, "staged x87 allreduce")
+        assert staged.value == before + 1, "the x87 call was not staged"
+        L.mini_op_destroy(op)
+
+    say("staged x87 done")
+    # ---- 3. engine-served: MAXLOC / MINLOC over the five other pair types, MAX / MIN over LONG_DOUBLE
+    for opname in ("MAXLOC", "MINLOC"):
+        for tname in ("FLOAT_INT", "DOUBLE_INT", "LONG_INT", "2INT", "SHORT_INT"):
+            code, slot = pkg.OP[opname], pkg.T[tname]
+            dt = m.dtype_for_slot(slot)
+            fn = m.coll.mca_coll_mi355x_reducible_type
+            fn.argtypes = [ctypes.c_void_p]
+            assert fn(dt) == slot, tname
+            op = m.select_op(code)
+            for n in (1, 4001, 100_003):
+                xs3 = [opdata.make(tname, n, 60 + r) for r in range(size)]
+                outs = [np.zeros_like(xs3[0]) for _ in range(size)]
+                oracle.oracle_allreduce(0, size, n, slot, code, 0, ptrs(xs3), ptrs(outs))
+                before = staged.value
+                d, dp, read = put(xs3[rank])
+                o, opp, oread3 = put(np.zeros_like(xs3[0]))
+                torch.cuda.synchronize()
+                assert L.mini_allreduce(comm, dp, opp, n, dt, op) == 0
+                opdata.assert_same(tname, opname, oread3(), outs[rank], f"engine pair allreduce n={n}")
+                assert staged.value == before, f"{opname}/{tname} was staged, not served by the engine"
+                # MPI_Reduce to the last rank
+                want = np.zeros_like(xs3[0])
+                oracle.oracle_reduce(0, size, size - 1, n, slot, code, 0, ptrs(xs3), want.ctypes.data)
+                r2, rp3, rread3 = put(np.zeros_like(xs3[0]))
+                torch.cuda.synchronize()
+                assert L.mini_reduce(comm, dp, rp3 if rank == size - 1 else None, n, dt, op, size - 1) == 0
+                if rank == size - 1:
+                    opdata.assert_same(tname, opname, rread3(), want, f"engine pair reduce n={n}")
+            L.mini_op_destroy(op)
+    for opname in ("MAX", "MIN"):
+        code, slot = pkg.OP[opname], pkg.T["LONG_DOUBLE"]
+        assert pkg.rt().mi355x_comm_op_supported(code, slot)
+        op = m.select_op(code)
+        dt = m.dtype_for_slot(slot)
+        n = 30_007
+        xs4 = [opdata.make("LONG_DOUBLE", n, 80 + r) for r in range(size)]
+        outs = [np.zeros_like(xs4[0]) for _ in range(size)]
+        oracle.oracle_allreduce(0, size, n, slot, code, 0, ptrs(xs4), ptrs(outs))
+        before = staged.value
+        d, dp, read = put(xs4[rank])
+        o, opp, oread4 = put(np.zeros_like(xs4[0]))
+        torch.cuda.synchronize()
+        assert L.mini_allreduce(comm, dp, opp, n, dt, op) == 0
+        opdata.assert_same("LONG_DOUBLE", opname, oread4(), outs[rank], "engine x87 allreduce")
+        assert staged.value == before
+        L.mini_op_destroy(op)
+
+    say("engine pairs done")
+    # ---- 4. host buffers on every rank: the host module reduces them (coll/basic's linear order)
+    op = m.select_op(pkg.OP["SUM"])
+    fdt = m.dtype_for_slot(pkg.T["FLOAT"])
+    xs5 = [opdata.make("FLOAT", 50_000, 90 + r) for r in range(size)]
+    want = _linear(oracle, pkg.OP["SUM"], pkg.T["FLOAT"], xs5)
+    h = xs5[rank].copy()
+    out = np.zeros_like(h)
+    assert L.mini_allreduce(comm, h.ctypes.data, out.ctypes.data, 50_000, fdt, op) == 0
+    opdata.assert_same("FLOAT", "SUM", out, want, "host-buffer allreduce through the host module")
+    L.mini_op_destroy(op)
+    assert L.mini_device_hits() == 0, "a device pointer reached the host module"
+    L.mini_comm_destroy(comm)
+    print(f"rank {rank} staging OK", flush=True)
+
+
 def main():
     if len(sys.argv) > 4 and sys.argv[4] == "split":
         return split_main()
@@ -765,6 +984,8 @@ def main():
         return pml_main()
     if len(sys.argv) > 4 and sys.argv[4] == "tuned_vars":
         return tuned_vars_main()
+    if len(sys.argv) > 4 and sys.argv[4] == "staging":
+        return staging_main()
     rank, size = int(sys.argv[1]), int(sys.argv[2])
     import torch
     ndev = torch.cuda.device_count()

@@ -289,3 +289,77 @@ def test_mca_variables_registered(monkeypatch):
     finally:
         prio.value, oprio.value = saved
         ctypes.c_ulonglong.in_dll(m.coll, "mca_coll_mi355x_rcache_size_limit").value = 0
+
+
+# ---- the MPI-2 pair types as libmpi builds them (DECLARE_MPI2_COMPOSED_{STRUCT,BLOCK}_DDT,
+#      ompi_datatype_module.c:391-437, instantiated :471-509) and the engine's datatype gate
+OMPI_PREDEFINED, OMPI_DATA_INT, OMPI_DATA_C = 0x0200, 0x1000, 0x4000   # ompi_datatype.h:51-59
+OPAL_PREDEFINED = 0x0002                                               # opal_datatype.h:66
+PAIRS = {  # name: (ompi id, struct members as (opal basic, displacement) | block of 2, extra flags)
+    "2INT": (0x1A, "block", "INT4", OMPI_DATA_C | OMPI_DATA_INT),
+    "FLOAT_INT": (0x20, [("FLOAT4", 0), ("INT4", 4)], None, OMPI_DATA_C),
+    "DOUBLE_INT": (0x21, [("FLOAT8", 0), ("INT4", 8)], None, OMPI_DATA_C),
+    "LONG_DOUBLE_INT": (0x22, [("FLOAT16", 0), ("INT4", 16)], None, OMPI_DATA_C),
+    "LONG_INT": (0x23, [("INT8", 0), ("INT4", 8)], None, OMPI_DATA_C | OMPI_DATA_INT),
+    "SHORT_INT": (0x24, [("INT2", 0), ("INT4", 4)], None, OMPI_DATA_C | OMPI_DATA_INT),
+}
+
+
+def _restated_pair(name):
+    """the pair type through the restated opal_datatype_add (oracle/opal_types.py), then the
+    OPAL -> OMPI predefined flag swap of ompi_datatype_module.c:415-416 / :431-432"""
+    import opal_types as ot
+    _, members, block, extra = PAIRS[name]
+    if members == "block":
+        t = ot.contiguous(2, ot.OpalType.basic(block))
+    else:
+        t = ot.struct_([1, 1], [d for _, d in members], [ot.OpalType.basic(b) for b, _ in members])
+    t.commit()
+    flags = (t.flags | extra) & ~OPAL_PREDEFINED | OMPI_PREDEFINED
+    return t, flags
+
+
+@pytest.mark.parametrize("name", list(PAIRS))
+def test_pair_types_as_libmpi_builds_them(name):
+    """the harness's pair types carry what a real Open MPI 1.8.5 passes: OPAL predefined flag
+    cleared, MPI predefined set, the struct's size / bounds / contiguity (DOUBLE_INT and LONG_INT
+    12 bytes in a 16-byte extent, SHORT_INT 6 with a hole in 8, LONG_DOUBLE_INT 20 in 32) and its
+    committed description records"""
+    import sys
+    sys.path.insert(0, str(REPO / "oracle"))
+    m = mini()
+    L = m.lib
+    L.mini_datatype_fields.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
+    L.mini_datatype_desc.restype = ctypes.c_void_p
+    L.mini_datatype_desc.argtypes = [ctypes.c_void_p]
+    t, flags = _restated_pair(name)
+    dt = L.mini_datatype(PAIRS[name][0])
+    f = (ctypes.c_int64 * 7)()
+    L.mini_datatype_fields(dt, f)
+    assert list(f[:6]) == [flags, t.size, t.lb, t.ub, t.true_lb, t.true_ub], (name, list(f), flags, t.size, t.ub)
+    assert not (f[0] & OPAL_PREDEFINED) and f[0] & OMPI_PREDEFINED
+    desc = t.desc_bytes()
+    assert f[6] * 32 + 32 == len(desc)           # `used` excludes commit's END_LOOP (optimize.c:257)
+    assert ctypes.string_at(L.mini_datatype_desc(dt), len(desc)) == desc
+    # the engine's gate: the pair's op slot, by MPI-predefined flag + ompi_op_ddt_map + extent
+    L2 = m.coll
+    L2.mca_coll_mi355x_reducible_type.argtypes = [ctypes.c_void_p]
+    assert L2.mca_coll_mi355x_reducible_type(dt) == m.pkg.T[name]
+    assert m.pkg.type_size(m.pkg.T[name]) == t.ub - t.lb
+
+
+def test_reducible_type_gate(pkg):
+    """every predefined reducible type maps to its slot; a derived type, a resized predefined-id
+    type and a type offset from its lower bound do not"""
+    m = mini()
+    fn = m.coll.mca_coll_mi355x_reducible_type
+    fn.argtypes = [ctypes.c_void_p]
+    for slot in range(39):
+        dt = m.dtype_for_slot(slot)
+        if dt is not None:
+            assert fn(dt) == slot, pkg.TYPES[slot]
+    import ddtcases
+    desc, used, tsize, lb, ub = ddtcases.opal_vector(4, 4, 8)
+    d = m.derived(desc, used, tsize, lb, ub)
+    assert fn(d) == -1
+    m.lib.mini_datatype_destroy(d)

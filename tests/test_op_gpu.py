@@ -41,17 +41,82 @@ def _host(t, off_bytes, like: np.ndarray) -> np.ndarray:
 
 
 def test_slot_coverage(gpu, pkg, oracle):
-    """every reference slot with a GPU-representable type has a kernel (108 of 116)"""
+    """every reference slot has a kernel (112 of 116) except the x87 long double SUM/PROD slots,
+    which need 80-bit arithmetic (op/hip stages them to the base loops); the x87 compare-only slots
+    (MAX/MIN on LONG_DOUBLE, MAXLOC/MINLOC on LONG_DOUBLE_INT) are GPU kernels"""
     have, missing = 0, []
     for op in range(15):
         for ty in range(len(pkg.TYPES)):
             if oracle.oracle_has_op(op, ty):
                 if pkg.op_supported(op, ty):
                     have += 1
-                elif "LONG_DOUBLE" not in pkg.TYPES[ty]:
+                elif not ("LONG_DOUBLE" in pkg.TYPES[ty] and pkg.OPS[op] in ("SUM", "PROD")):
                     missing.append((pkg.OPS[op], pkg.TYPES[ty]))
     assert not missing, missing
-    assert have == 108
+    assert have == 112
+
+
+def _x87(m, se):
+    """an 80-bit x87 value in 16 bytes of storage (padding bytes set to 0xA5: never compared)"""
+    b = bytearray(16)
+    b[0:8] = int(m).to_bytes(8, "little")
+    b[8:10] = int(se).to_bytes(2, "little")
+    b[10:16] = b"\xa5" * 6
+    return bytes(b)
+
+
+def x87_adversarial():
+    """every class of the 80-bit encoding, both signs: zeros, denormals, pseudo-denormals (equal to
+    the normal of the same significand), normals, the largest finite, infinities, quiet and
+    signalling NaNs, and the invalid operands of the 387 -- pseudo-NaN / pseudo-infinity and
+    unnormals (integer bit clear), which compare unordered"""
+    I = 1 << 63
+    vals = [(0, 0), (1, 0), (0x7FFFFFFFFFFFFFFF, 0), (I, 0), (I | 5, 0), (I, 1), (I | 5, 1), (I, 0x3FFF),
+            (I | 1, 0x3FFF), (I | (1 << 62), 0x3FFF), (0xFFFFFFFFFFFFFFFF, 0x7FFE), (I, 0x7FFF),
+            (I | (1 << 62), 0x7FFF), (I | 1, 0x7FFF), (1 << 62, 0x7FFF), (0, 0x7FFF), (5, 0x3FFF), (0, 0x4000)]
+    out = []
+    for mant, exp in vals:
+        for sign in (0, 0x8000):
+            out.append(_x87(mant, exp | sign))
+    return out
+
+
+@pytest.mark.parametrize("tname", ["LONG_DOUBLE", "LONG_DOUBLE_INT"])
+def test_x87_compare_slots(gpu, pkg, oracle, tname):
+    """MAX/MIN (LONG_DOUBLE) and MAXLOC/MINLOC (LONG_DOUBLE_INT) on the GPU against the oracle's C
+    loops, which run on this host's x87 unit (op_base_functions.c:110, :170, :576, :598): every
+    ordered pair of the adversarial encodings, 2-buff and 3-buff, bit-exact in the 10 value bytes"""
+    torch = gpu
+    enc = x87_adversarial()
+    pairs = [(x, y) for x in enc for y in enc]
+    dt = opdata.dtype_of(tname)
+    a = np.zeros(len(pairs), dtype=dt)
+    b = np.zeros(len(pairs), dtype=dt)
+    av = a.view(np.uint8).reshape(len(pairs), dt.itemsize)
+    bv = b.view(np.uint8).reshape(len(pairs), dt.itemsize)
+    for i, (x, y) in enumerate(pairs):
+        av[i, :16] = np.frombuffer(x, np.uint8)
+        bv[i, :16] = np.frombuffer(y, np.uint8)
+    if tname == "LONG_DOUBLE_INT":
+        a["k"] = np.arange(len(pairs)) % 7
+        b["k"] = np.arange(len(pairs)) % 5
+    ops = ("MAX", "MIN") if tname == "LONG_DOUBLE" else ("MAXLOC", "MINLOC")
+    s = torch.cuda.current_stream().cuda_stream
+    for opname in ops:
+        op, ty = pkg.OP[opname], pkg.T[tname]
+        assert pkg.op_supported(op, ty)
+        ta, pa = _dev(torch, a)
+        tb, pb = _dev(torch, b)
+        to, po = _dev(torch, np.zeros_like(a))
+        pkg.op_reduce_3buff(op, ty, pa, pb, po, len(pairs), s)
+        pkg.op_reduce(op, ty, pa, pb, len(pairs), s)
+        torch.cuda.synchronize()
+        want3 = np.zeros_like(a)
+        assert oracle.oracle_op_3buff(op, ty, a.ctypes.data, b.ctypes.data, want3.ctypes.data, len(pairs)) == 0
+        want2 = b.copy()
+        assert oracle.oracle_op_2buff(op, ty, a.ctypes.data, want2.ctypes.data, len(pairs)) == 0
+        opdata.assert_same(tname, opname, _host(to, 0, a), want3, "x87 3buff")
+        opdata.assert_same(tname, opname, _host(tb, 0, a), want2, "x87 2buff")
 
 
 @pytest.mark.parametrize("offs", [(0, 0, 0), (1, 1, 1), (1, 0, 2)], ids=["aligned", "comisaligned", "misaligned"])
