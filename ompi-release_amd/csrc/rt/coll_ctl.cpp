@@ -1,0 +1,400 @@
+// coll_ctl.cpp -- the engine's control segment and rendezvous: rank liveness, the host barrier,
+// buffer registration (the IPC export cache), the per-call exchange of every rank's buffers and
+// the call's finish, the per-communicator scratch (split out of coll_comm.cpp, no change).
+
+#include <fcntl.h>
+#include <immintrin.h>
+#include <poll.h>
+#include <sched.h>
+#include <signal.h>
+#include <sys/mman.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <sys/un.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <cerrno>
+#include <chrono>
+#include <condition_variable>
+#include <cstddef>
+#include <deque>
+#include <functional>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "coll_internal.hpp"
+#include "coll_sched.hpp"
+#include "rt_internal.hpp"
+
+#include "comm_internal.hpp"
+
+#include "coll_comm_int.hpp"
+
+namespace mi355x {
+
+CollTune &coll_tune()
+{
+    static CollTune t;
+    return t;
+}
+
+} // namespace mi355x
+
+namespace mi355x {
+
+
+// ----------------------------------------------------------------- liveness
+// a process exists and has not exited (a zombie -- exited, not yet reaped by its parent -- is gone)
+bool pid_alive(pid_t pid)
+{
+    if (pid <= 0) return false;
+    if (kill(pid, 0) != 0 && errno == ESRCH) return false;
+    char path[64], buf[512];
+    snprintf(path, sizeof(path), "/proc/%d/stat", (int)pid);
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return true;  // (no /proc: trust kill)
+    const ssize_t n = read(fd, buf, sizeof(buf) - 1);
+    close(fd);
+    if (n <= 0) return true;
+    buf[n] = 0;
+    const char *p = strrchr(buf, ')');
+    return !(p && p[1] == ' ' && (p[2] == 'Z' || p[2] == 'X'));
+}
+
+// A peer process that died without setting the abort flag (SIGKILL, the OOM killer) would leave
+// the others spinning in an unbounded wait (the buffer-kind vote) or until timeout_s.  Waits check
+// every rank's published pid now and then; a rank whose process is gone aborts the communicator.
+// (Loopback ranks share this process.)
+bool peer_gone(mi355x_comm *c)
+{
+    if (c->loopback || c->size == 1) return false;
+    for (int q = 0; q < c->size; ++q) {
+        const pid_t pid = (pid_t)c->ctrl->slot[q].pid;
+        if (q == c->rank || pid <= 0) continue;
+        if (!pid_alive(pid)) {
+            c->ctrl->abort_flag.store(1);
+            set_error(MI355X_ERR_PEER, "rank %d (pid %d) is gone: the communicator is aborted", q, (int)pid);
+            return true;
+        }
+    }
+    return false;
+}
+
+// ----------------------------------------------------------------- barrier
+int barrier(mi355x_comm *c)
+{
+    if (c->size == 1) return MI355X_SUCCESS;
+    Ctrl *k = c->ctrl;
+    const uint64_t gen = k->bar_gen.load(std::memory_order_acquire);
+    if (k->bar_count.fetch_add(1, std::memory_order_acq_rel) == (uint64_t)c->size - 1) {
+        k->bar_count.store(0, std::memory_order_relaxed);
+        k->bar_gen.fetch_add(1, std::memory_order_release);
+        return MI355X_SUCCESS;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    unsigned spins = 0;
+    while (k->bar_gen.load(std::memory_order_acquire) == gen) {
+        if (k->abort_flag.load(std::memory_order_relaxed))
+            return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
+        if (++spins > 2048) {
+            sched_yield();
+            // a peer may be blocked sending us dmabuf fds (full socket queue): drain it while we wait
+            if (c->fd_sock >= 0 && (spins & 255) == 0 && c->reg_mtx.try_lock()) {
+                (void)fd_drain(c, false);
+                c->reg_mtx.unlock();
+            }
+            if ((spins & 0xffff) == 0) {
+                if (peer_gone(c)) return MI355X_ERR_PEER;
+                const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                if (el > c->timeout_s) {
+                    k->abort_flag.store(1);
+                    // which rank is behind: every rank's published call number
+                    char who[256] = "";
+                    size_t w = 0;
+                    for (int r = 0; r < c->size && w + 24 < sizeof(who); ++r)
+                        w += (size_t)snprintf(who + w, sizeof(who) - w, " r%d:%llu", r,
+                                              (unsigned long long)k->slot[r].seq.load());
+                    return set_error(MI355X_ERR_TIMEOUT, "barrier timed out after %.0f s (rank %d, %llu of %d arrived; calls%s)",
+                                     el, c->rank, (unsigned long long)k->bar_count.load(), c->size, who);
+                }
+            }
+        }
+    }
+    return MI355X_SUCCESS;
+}
+
+// ----------------------------------------------------------------- registration
+uint64_t buffer_id(const void *p)
+{
+    unsigned long long id = 0;
+    if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)p) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return (uint64_t)id;
+}
+
+int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
+{
+    std::lock_guard<std::recursive_mutex> reg_guard(c->reg_mtx);
+    std::memset(d, 0, sizeof(*d));
+    if (!p) return MI355X_SUCCESS;
+    d->present = 1;
+    if (c->loopback) {
+        d->raw = (uint64_t)(uintptr_t)p;
+        if (!force) {
+            void *base = nullptr;
+            size_t sz = 0;
+            MI_HIP(hipMemGetAddressRange(&base, &sz, (void *)p));
+            d->staged = sz >= c->ipc_max;
+        }
+        return MI355X_SUCCESS;
+    }
+    const uintptr_t up = (uintptr_t)p;
+    const uint64_t id = buffer_id(p);
+    for (size_t i = 0; i < c->local_regs.size(); ++i) {
+        const LocalReg &r = c->local_regs[i];
+        if (up >= r.base && up < r.base + r.size) {
+            if (r.id == id && id != 0 && (r.has_h || !force)) {
+                if (!force && r.size >= c->ipc_max) {
+                    d->staged = 1;
+                    d->base = r.base;
+                    d->off = up - r.base;
+                    d->id = r.id;
+                    d->size = r.size;
+                    return MI355X_SUCCESS;
+                }
+                d->h = r.h;
+                d->off = up - r.base;
+                d->base = r.base;
+                d->id = r.id;
+                d->size = r.size;
+                return MI355X_SUCCESS;
+            }
+            drop_reg(c->local_regs[i]);
+            c->local_regs.erase(c->local_regs.begin() + (long)i);  // freed and reallocated: stale
+            break;
+        }
+    }
+    void *base = nullptr;
+    size_t sz = 0;
+    MI_HIP(hipMemGetAddressRange(&base, &sz, (void *)p));
+    TRACE(c, "register %p: base %p size %zu id %llu", p, base, sz, (unsigned long long)id);
+    LocalReg reg;
+    std::memset(&reg, 0, sizeof(reg));
+    reg.fd = -1;
+    reg.base = (uintptr_t)base;
+    reg.size = sz;
+    reg.id = id;
+    if (!force && sz >= c->ipc_max) {
+        // never exported (hipIpcOpenMemHandle hangs on such allocations): staged data flow
+        reg.has_h = false;
+        if (id != 0) c->local_regs.push_back(reg);
+        d->staged = 1;
+        d->base = reg.base;
+        d->off = up - reg.base;
+        d->id = id;
+        d->size = sz;
+        return MI355X_SUCCESS;
+    }
+    MI_HIP(hipIpcGetMemHandle(&reg.h, base));
+    reg.has_h = true;
+    // without an allocation id the entry cannot be validated later: do not cache it
+    if (id != 0) c->local_regs.push_back(reg);
+    d->h = reg.h;
+    d->off = up - reg.base;
+    d->base = reg.base;
+    d->id = id;
+    d->size = sz;
+    return MI355X_SUCCESS;
+}
+
+
+} // namespace mi355x
+
+namespace mi355x {
+
+// Publish nbuf local buffers, meet every rank, and resolve every rank's buffers:
+// peers[b][r] = rank r's buffer b mapped into this process.  When any rank published a buffer
+// that cannot be exported, nothing is mapped and *staged is set on every rank alike (callers
+// that pass staged == NULL get an error instead).  force: export regardless of allocation size
+// (the staging buffers themselves).
+void svc_park(mi355x_comm *c);
+
+int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t sig[4],
+             std::vector<std::vector<void *>> &peers, bool *staged, bool force, bool persistent)
+{
+    if (!c->svc_keep) svc_park(c);  // a host-synchronised call: the resident service steps aside (svc_park)
+    c->seq++;
+    if (staged) *staged = false;
+    RankSlot &s = c->ctrl->slot[c->rank];
+    for (int b = 0; b < nbuf; ++b) {
+        int rc = local_handle(c, mine[b], &s.buf[b], force);
+        if (rc) return rc;
+    }
+    s.nbuf = nbuf;
+    for (int i = 0; i < 4; ++i) s.sig[i] = sig[i];
+    s.seq.store(c->seq, std::memory_order_release);
+    TRACE(c, "published %d buffers", nbuf);
+    int rc = barrier(c);
+    TRACE(c, "exchange barrier passed (rc %d)", rc);
+    if (rc) return rc;
+    bool any_staged = false;
+    for (int r = 0; r < c->size; ++r) {
+        RankSlot &o = c->ctrl->slot[r];
+        if (o.seq.load(std::memory_order_acquire) != c->seq)
+            return set_error(MI355X_ERR_PEER, "rank %d is in call %llu, rank %d in call %llu", r,
+                             (unsigned long long)o.seq.load(), c->rank, (unsigned long long)c->seq);
+        if (o.sig[0] != sig[0] || o.sig[1] != sig[1] || o.sig[2] != sig[2] || o.sig[3] != sig[3])
+            return set_error(MI355X_ERR_ARG, "collective arguments differ between rank %d and rank %d", r, c->rank);
+        for (int b = 0; b < nbuf; ++b) any_staged = any_staged || o.buf[b].staged;
+    }
+    peers.assign(nbuf, std::vector<void *>(c->size, nullptr));
+    if (any_staged && !c->loopback) {
+        if (c->dmabuf_state == 0) {
+            rc = barrier(c);  // every rank has read the staged flags before the probe reuses the slots
+            if (rc) return rc;
+            rc = probe_dmabuf(c);
+            if (rc) return rc;
+        }
+        if (c->dmabuf_state == 1) {
+            // second round: the large allocations go out as dmabuf fds, then everything is mapped
+            BufDesc *ds[kMaxBufs];
+            int nd = 0;
+            for (int b = 0; b < nbuf; ++b)
+                if (s.buf[b].staged) ds[nd++] = &s.buf[b];
+            if (nd) {
+                rc = export_dmabufs(c, ds, nd, ~0ull);
+                if (rc) return rc;
+            }
+            rc = barrier(c);
+            if (rc) return rc;
+            any_staged = false;
+        }
+    }
+    if (any_staged) {
+        if (!staged) return set_error(MI355X_ERR_UNSUPPORTED, "buffer allocation too large to export");
+        *staged = true;
+        TRACE(c, "staged data flow");
+        // the staged flow publishes again at once (the staging buffers): nobody may overwrite
+        // its slot before every rank has read this exchange's slots
+        return barrier(c);
+    }
+    for (int r = 0; r < c->size; ++r) {
+        RankSlot &o = c->ctrl->slot[r];
+        for (int b = 0; b < nbuf; ++b) {
+            if (r == c->rank) {
+                peers[b][r] = const_cast<void *>(mine[b]);
+            } else {
+                PeerMap *pm = nullptr;
+                rc = map_peer(c, r, o.buf[b], &peers[b][r], &pm);
+                if (rc) return rc;
+                if (persistent && pm) pm->persistent = true;
+            }
+        }
+    }
+    return MI355X_SUCCESS;
+}
+
+// finish: every rank's work queued on its stream so far has completed (so no rank still reads a
+// peer's buffer, and my results are in place).  With the control segment registered, the GPU's
+// command processor writes this finish point's number into my RankSlot::done right behind my
+// kernels (hipStreamWriteValue64) and I poll every rank's word: the kernel's completion reaches
+// every host without a hipStreamSynchronize wake-up and without a second barrier round.
+// Otherwise: stream sync + barrier.
+int finish(mi355x_comm *c, hipStream_t s)
+{
+    if (!c->ctrl_dev || c->size == 1) {
+        TRACE(c, "finish: stream sync");
+        MI_HIP(hipStreamSynchronize(s));
+        TRACE(c, "finish: barrier");
+        return barrier(c);
+    }
+    const uint64_t v = ++c->done_seq;
+    char *word = c->ctrl_dev + ((char *)&c->ctrl->slot[c->rank].done - (char *)c->ctrl);
+    MI_HIP(hipStreamWriteValue64(s, word, v, 0));
+    TRACE(c, "finish %llu: polling the ranks' completion words", (unsigned long long)v);
+    Ctrl *k = c->ctrl;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int q = 0; q < c->size; ++q) {
+        unsigned spins = 0;
+        while (k->slot[q].done.load(std::memory_order_acquire) < v) {
+            if (k->abort_flag.load(std::memory_order_relaxed))
+                return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
+            if (++spins > 4096) {
+                sched_yield();
+                if ((spins & 0xffff) == 0 && hipStreamQuery(s) != hipErrorNotReady && q == c->rank &&
+                    k->slot[q].done.load(std::memory_order_acquire) < v)
+                    return set_error(MI355X_ERR_HIP, "stream finished without writing its completion word");
+                if ((spins & 0xffff) == 0 && peer_gone(c)) return MI355X_ERR_PEER;
+                if ((spins & 0xffff) == 0 &&
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
+                    k->abort_flag.store(1);
+                    return set_error(MI355X_ERR_TIMEOUT, "rank %d: finish %llu timed out waiting for rank %d (at %llu)",
+                                     c->rank, (unsigned long long)v, q, (unsigned long long)k->slot[q].done.load());
+                }
+            }
+        }
+    }
+    return MI355X_SUCCESS;
+}
+
+// register the control segment with HIP so the command processor can write completion words into
+// it (multi-process communicators; MI355X_DONE_WORDS=0 keeps stream sync + barrier).  Every rank
+// decides the same way or the finish points would not pair: the outcome is agreed on with a
+// barrier round through the segment.
+int setup_done_words(mi355x_comm *c)
+{
+    const char *env = getenv("MI355X_DONE_WORDS");
+    bool ok = env && atoi(env) != 0 && c->size > 1 && !c->loopback;
+    if (ok) {
+        ok = hipHostRegister(c->ctrl, ctrl_bytes(c->size), hipHostRegisterMapped) == hipSuccess;
+        if (ok) {
+            c->ctrl_registered = true;
+            void *dptr = nullptr;
+            ok = hipHostGetDevicePointer(&dptr, c->ctrl, 0) == hipSuccess && dptr;
+            c->ctrl_dev = ok ? (char *)dptr : nullptr;
+        }
+        (void)hipGetLastError();
+    }
+    c->ctrl->slot[c->rank].done.store(ok ? 1 : 2, std::memory_order_release);
+    int rc = barrier(c);
+    if (rc) return rc;
+    bool all = true;
+    for (int q = 0; q < c->size; ++q) all = all && c->ctrl->slot[q].done.load(std::memory_order_acquire) == 1;
+    rc = barrier(c);   // every rank has read the setup words before they are reset
+    if (rc) return rc;
+    c->ctrl->slot[c->rank].done.store(0, std::memory_order_release);
+    if (!all) c->ctrl_dev = nullptr;
+    c->done_seq = 0;
+    return barrier(c);
+}
+
+// The scratch may be exported to peers (MPI_Reduce's owner blocks): never a small allocation
+// (small hipMallocs can fail hipIpcOpenMemHandle on the importer with "invalid device
+// pointer"), and grown geometrically so it is rarely freed while peers hold a mapping.
+int ensure_scratch(mi355x_comm *c, size_t bytes)
+{
+    if (c->scratch_bytes >= bytes) return MI355X_SUCCESS;
+    size_t want = std::max<size_t>((size_t)8 << 20, c->scratch_bytes * 2);
+    while (want < bytes) want *= 2;
+    if (c->scratch) MI_HIP(hipFree(c->scratch));
+    c->scratch = nullptr;
+    c->scratch_bytes = 0;
+    MI_HIP(hipMalloc(&c->scratch, want));
+    c->scratch_bytes = want;
+    return MI355X_SUCCESS;
+}
+
+
+} // namespace mi355x

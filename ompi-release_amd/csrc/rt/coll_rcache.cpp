@@ -1,0 +1,154 @@
+// coll_rcache.cpp -- the bounded peer-mapping cache (mpool/rgpusm's registration cache):
+// mapping peers' allocations and LRU eviction (split out of coll_comm.cpp).
+
+#include <fcntl.h>
+#include <immintrin.h>
+#include <poll.h>
+#include <sched.h>
+#include <signal.h>
+#include <sys/mman.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <sys/un.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <cerrno>
+#include <chrono>
+#include <condition_variable>
+#include <cstddef>
+#include <deque>
+#include <functional>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "coll_internal.hpp"
+#include "coll_sched.hpp"
+#include "rt_internal.hpp"
+
+#include "comm_internal.hpp"
+
+#include "coll_comm_int.hpp"
+
+namespace mi355x {
+
+
+// Bounded peer-mapping cache (mpool/rgpusm's rcache_size_limit with LRU eviction,
+// mpool_rgpusm_component.c:92-100, mpool_rgpusm_module.c:104-120,396-419): when the hipIpc mappings
+// of peers' allocations exceed rcache_max_maps (count) or rcache_limit (bytes), the least recently
+// used ones that the current call does not use, that no point-to-point read has pinned and that
+// are not the communicator's own regions are closed.  A mapping keeps the exporter's allocation
+// alive on ROCm, so a long job that churns allocations would otherwise hold every freed block of
+// every peer.  Both limits default to 0 = unlimited, as in the reference.  dmabuf imports (>= 2 GiB
+// allocations) are not evicted: their fd reaches a peer once.
+bool evictable(const mi355x_comm *c, const PeerMap &m, const PeerMap *keep)
+{
+    return &m != keep && !m.persistent && m.pins == 0 && !m.ext && m.last_use != c->seq;
+}
+
+void rcache_trim(mi355x_comm *c, const PeerMap *keep)
+{
+    if (!c->rcache_max_maps && !c->rcache_limit) return;
+    for (;;) {
+        size_t nmaps = 0, bytes = 0;
+        auto lru = c->peer_maps.end();
+        for (auto it = c->peer_maps.begin(); it != c->peer_maps.end(); ++it) {
+            if (it->second.persistent || it->second.ext) continue;
+            nmaps++;
+            bytes += it->second.bytes;
+            if (evictable(c, it->second, keep) && (lru == c->peer_maps.end() || it->second.last_use < lru->second.last_use))
+                lru = it;
+        }
+        const bool over = (c->rcache_max_maps && nmaps > c->rcache_max_maps) || (c->rcache_limit && bytes > c->rcache_limit);
+        if (!over || lru == c->peer_maps.end()) return;
+        TRACE(c, "rcache: evict peer %d base %llx (%zu maps, %zu bytes)", lru->first.peer,
+              (unsigned long long)lru->first.base, nmaps, bytes);
+        close_map(lru->second);
+        c->peer_maps.erase(lru);
+        c->rcache_evictions++;
+    }
+}
+
+size_t peer_map_count(const mi355x_comm *c)
+{
+    size_t n = 0;
+    for (const auto &kv : c->peer_maps) n += !kv.second.persistent && !kv.second.ext;
+    return n;
+}
+
+int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **entry)
+{
+    std::lock_guard<std::recursive_mutex> reg_guard(c->reg_mtx);
+    *out = nullptr;
+    if (entry) *entry = nullptr;
+    if (!d.present) return MI355X_SUCCESS;
+    if (c->loopback) {
+        *out = (void *)(uintptr_t)d.raw;
+        return MI355X_SUCCESS;
+    }
+    HandleKey key;
+    key.peer = peer;
+    key.base = d.base;
+    auto it = c->peer_maps.find(key);
+    if (it != c->peer_maps.end() && (it->second.id != d.id || (d.id == 0 && it->second.pins == 0))) {
+        if (it->second.ext) drop_stash(c, peer, it->second.id);  // the peer replaced that allocation
+        close_map(it->second);
+        c->peer_maps.erase(it);
+        it = c->peer_maps.end();
+    }
+    if (it == c->peer_maps.end() && d.dmabuf) {
+        void *mapped = nullptr;
+        hipExternalMemory_t ext = nullptr;
+        int rc = import_dmabuf(c, peer, d.id, d.size, &mapped, &ext);
+        if (rc) return rc;
+        it = c->peer_maps.emplace(key, PeerMap{d.id, mapped, c->seq, ext}).first;
+    }
+    void *base;
+    if (it != c->peer_maps.end()) {
+        base = it->second.mapped;
+        it->second.last_use = c->seq;
+    } else {
+        TRACE(c, "open peer %d base %llx id %llu", peer, (unsigned long long)d.base, (unsigned long long)d.id);
+        hipError_t e = hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess);
+        TRACE(c, "opened peer %d -> %p (%s)", peer, base, hipGetErrorString(e));
+        if (e != hipSuccess) {
+            // A mapping of an allocation the peer has since freed can still hold the block the new
+            // allocation was carved from (small allocations share blocks): the open then fails
+            // with "invalid device pointer".  Drop this peer's mappings that the current call does
+            // not use and try once more.
+            (void)hipGetLastError();
+            int dropped = 0;
+            for (auto m = c->peer_maps.begin(); m != c->peer_maps.end();) {
+                if (m->first.peer == peer && m->second.last_use != c->seq && m->second.pins == 0 &&
+                    !m->second.persistent) {
+                    close_map(m->second);
+                    m = c->peer_maps.erase(m);
+                    dropped++;
+                } else {
+                    ++m;
+                }
+            }
+            TRACE(c, "open failed; dropped %d stale mappings of peer %d, retrying", dropped, peer);
+            e = dropped ? hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess) : e;
+            if (e != hipSuccess)
+                return set_error(MI355X_ERR_PEER, "hipIpcOpenMemHandle(rank %d): %s", peer, hipGetErrorString(e));
+        }
+        it = c->peer_maps.emplace(key, PeerMap{d.id, base, c->seq, nullptr}).first;
+        it->second.bytes = d.size;
+        rcache_trim(c, &it->second);
+    }
+    if (entry) *entry = &it->second;
+    *out = (char *)base + d.off;
+    return MI355X_SUCCESS;
+}
+
+} // namespace mi355x
