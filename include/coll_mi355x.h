@@ -14,9 +14,11 @@
  *                                      incl. ompi_coll_tuned_reduce_intra_dec_fixed (:343-446)
  * with results identical to the tuned/basic schedules (same per-element operand order).
  *
- * Host buffers, user-defined ops, non-contiguous or non-reducible datatypes go to the function
- * that was installed in the slot before this module (snapshotted at enable time, retained, as
- * coll/cuda does at coll_cuda_module.c:120-157).
+ * Host buffers, user-defined ops and types the engine has no fold for go to the function that
+ * was installed in the slot before this module (snapshotted at enable time, retained, as coll/cuda
+ * does at coll_cuda_module.c:120-157) -- with every device buffer of such a call staged through
+ * host memory around it, as coll/cuda stages every call it intercepts
+ * (coll_cuda_allreduce.c:43-75, coll_cuda_reduce_scatter_block.c:45-83).
  *
  * Host facts the component reads from the Open MPI 1.8 launcher environment:
  *   OMPI_COMM_WORLD_SIZE / OMPI_COMM_WORLD_LOCAL_SIZE  (orte/mca/ess/base/ess_base_put.c:76,87)
@@ -140,6 +142,20 @@ extern int mca_coll_mi355x_pml_hook;            /* 1 = point-to-point on engine 
 extern int mca_coll_mi355x_mixed_buffers;       /* 1 = ranks may mix host and device buffers in a call */
 extern int mca_coll_mi355x_rcache_max_maps;     /* peer mappings kept open per communicator (0 = unlimited) */
 extern unsigned long long mca_coll_mi355x_rcache_size_limit; /* the same in bytes (mpool_rgpusm_rcache_size_limit) */
+/* the engine's crossovers and flow parameters (MI355X_KNOB_* on every communicator's engine) */
+extern int mca_coll_mi355x_pipe_min_ranks;               /* 4: pipelined allreduce from this many ranks (0 never) */
+extern int mca_coll_mi355x_pipe_chunk_kib;               /* 0: auto */
+extern int mca_coll_mi355x_pipe_wg_per_cu;               /* 2 */
+extern int mca_coll_mi355x_pipe_wt;                      /* 1: write-through fold results */
+extern unsigned long long mca_coll_mi355x_one_phase_max; /* 1 MiB */
+extern unsigned long long mca_coll_mi355x_svc_max;       /* 32 KiB */
+extern unsigned long long mca_coll_mi355x_svc_pull_max;  /* 128 KiB */
+extern unsigned long long mca_coll_mi355x_svc_copy_max;  /* 1 MiB */
+extern int mca_coll_mi355x_svc_idle_us;                  /* 1000 */
+extern int mca_coll_mi355x_svc_shrink_us;                /* 100 */
+extern int mca_coll_mi355x_selftest;                     /* 1 */
+/* the engine of a communicator coll/mi355x serves (NULL otherwise): for tools and tests */
+struct mi355x_comm *mca_coll_mi355x_engine_of(struct ompi_communicator_t *comm);
 
 /* Reductions the engine declines (user-defined ops; types with no engine slot) go to the
  * lower-priority component with every device buffer staged through host memory, as coll/cuda does

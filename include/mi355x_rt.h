@@ -232,7 +232,19 @@ enum mi355x_knob {
     MI355X_KNOB_SVC_SHRINK_US = 36,     /* (per communicator; env MI355X_SVC_SHRINK_US, default 100; 0: never)
                                            microseconds without a call after which every workgroup of the
                                            service but the first leaves (applies from its next launch) */
-    MI355X_KNOB_SVC_REGROWS = 37        /* (read-only) calls that relaunched a shrunk service's full grid */
+    MI355X_KNOB_SVC_REGROWS = 37,       /* (read-only) calls that relaunched a shrunk service's full grid */
+    MI355X_KNOB_DEV_SETUP = 38,         /* (read-only) 1 once the communicator's device-side setup has run: it
+                                           is deferred from mi355x_comm_create to the first device-buffer
+                                           reduction / allgather / bcast (smcuda's lazy rule,
+                                           btl/smcuda/README:36-40); a communicator that only ever sees host
+                                           buffers allocates no device memory */
+    MI355X_KNOB_SETUP_US = 39,          /* (read-only) wall time of that setup, microseconds (in the call that
+                                           triggered it) */
+    MI355X_KNOB_SELFTEST = 40,          /* (per communicator, same value on every rank; env MI355X_SELFTEST, default
+                                           1) 1: the device setup self-tests the cross-device flows and turns a
+                                           flow that failed on any rank off on every rank; 0: trusts them.  Only
+                                           a value set before the device setup takes effect. */
+    MI355X_KNOB_PIPE_CALLS = 41         /* (read-only) allreduces served by the pipelined flow */
 };
 /* cross-device flows (MI355X_KNOB_FLOWS) */
 enum mi355x_flow {

@@ -111,6 +111,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "mi355x_event_record": (i, [vp, vp]),
         "mi355x_event_elapsed_ms": (i, [vp, vp, c.POINTER(c.c_float)]),
         "mi355x_op_supported": (i, [i, i]),
+        "mi355x_comm_op_supported": (i, [i, i]),
         "mi355x_type_size": (sz, [i]),
         "mi355x_op_reduce": (i, [i, i, vp, vp, sz, vp]),
         "mi355x_op_reduce_3buff": (i, [i, i, vp, vp, vp, sz, vp]),
@@ -222,6 +223,11 @@ def op_supported(op: int, ty: int) -> bool:
     return bool(rt().mi355x_op_supported(op, ty))
 
 
+def comm_op_supported(op: int, ty: int) -> bool:
+    """the collective engine folds (op, ty) on the device (op/hip's slots less the 32-byte pairs)"""
+    return bool(rt().mi355x_comm_op_supported(op, ty))
+
+
 def type_size(ty: int) -> int:
     return int(rt().mi355x_type_size(ty))
 
@@ -258,7 +264,8 @@ KNOB = {"ALLREDUCE_ALG": 1, "REDUCE_ALG": 2, "REDUCE_SCATTER_ALG": 3, "BLOCKS_PE
         "SVC_PULL_COPY_MAX_BYTES": 24, "RCACHE_MAX_MAPS": 25, "RCACHE_SIZE_LIMIT": 26, "PEER_MAPS": 27,
         "RCACHE_EVICTIONS": 28, "FLOWS": 29, "FLOWS_FAILED": 30, "CREATE_US": 31, "SELFTEST_US": 32,
         "SVC_OWNER": 33, "SVC_CLAIMS": 34, "SVC_IDLE_US": 35,
-        "SVC_SHRINK_US": 36, "SVC_REGROWS": 37}
+        "SVC_SHRINK_US": 36, "SVC_REGROWS": 37, "DEV_SETUP": 38, "SETUP_US": 39, "SELFTEST": 40,
+        "PIPE_CALLS": 41}
 FLOW = {"SVC_LL": 1, "SVC_PULL": 2, "SVC_COPY": 4, "SVC_RS": 8, "PIPE": 16}
 # coll/tuned COLLTYPE ids (coll_tuned.h:41-58)
 COLL = {"ALLGATHER": 0, "ALLREDUCE": 2, "BCAST": 7, "REDUCE": 11, "REDUCESCATTER": 12}

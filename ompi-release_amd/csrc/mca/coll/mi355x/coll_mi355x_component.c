@@ -292,6 +292,19 @@ static int map_rc(int rc)
 int mca_coll_mi355x_mixed_buffers = 1;
 int mca_coll_mi355x_rcache_max_maps = 0;
 unsigned long long mca_coll_mi355x_rcache_size_limit = 0;
+/* the engine's crossovers and flow parameters (registered in component_register, applied to every
+ * communicator's engine in module_enable; defaults = the engine's own) */
+int mca_coll_mi355x_pipe_min_ranks = 4;
+int mca_coll_mi355x_pipe_chunk_kib = 0;
+int mca_coll_mi355x_pipe_wg_per_cu = 2;
+int mca_coll_mi355x_pipe_wt = 1;
+unsigned long long mca_coll_mi355x_one_phase_max = 1ull << 20;
+unsigned long long mca_coll_mi355x_svc_max = 32ull << 10;
+unsigned long long mca_coll_mi355x_svc_pull_max = 128ull << 10;
+unsigned long long mca_coll_mi355x_svc_copy_max = 1ull << 20;
+int mca_coll_mi355x_svc_idle_us = 1000;
+int mca_coll_mi355x_svc_shrink_us = 100;
+int mca_coll_mi355x_selftest = 1;
 
 /* 1: run the engine (*dev: this rank's buffers are all device memory); 0: the host path on every
  * rank; < 0: an error (the vote failed or timed out) */
@@ -1802,6 +1815,46 @@ static void apply_tuned_params(mca_coll_mi355x_module_t *m)
         if (m->prev_##FN##_module) mi355x_obj_retain(&m->prev_##FN##_module->super); \
     } while (0)
 
+/* The engine's crossovers as MCA variables, applied to each communicator's engine the way
+ * coll/tuned applies its forced-algorithm variables per communicator (coll_tuned_module.c:178-226).
+ * They are set before the engine's device-side setup runs (it waits for the first device-buffer
+ * collective), so the ones that size that setup -- the service limits -- take effect in it.  Every
+ * rank of a communicator must see the same values (as for coll/tuned's variables). */
+static int set_knob(mca_coll_mi355x_module_t *m, int knob, long v, const char *name)
+{
+    if (mi355x_comm_set(m->engine, knob, v) == MI355X_SUCCESS) return OMPI_SUCCESS;
+    fprintf(stderr, "[coll/mi355x] coll_mi355x_%s = %ld rejected: %s\n", name, v, mi355x_last_error());
+    return OMPI_ERR_BAD_PARAM;
+}
+
+static int apply_engine_params(mca_coll_mi355x_module_t *m, struct ompi_communicator_t *comm)
+{
+    const int n = mi355x_comm_size_of(comm);
+    int rc = OMPI_SUCCESS;
+#define KNOB(K, V, NAME) if (rc == OMPI_SUCCESS) rc = set_knob(m, MI355X_KNOB_##K, (long)(V), NAME)
+    KNOB(SELFTEST, mca_coll_mi355x_selftest != 0, "selftest");
+    KNOB(PIPE, mca_coll_mi355x_pipe_min_ranks > 0 && n >= mca_coll_mi355x_pipe_min_ranks, "pipe_min_ranks");
+    KNOB(PIPE_CHUNK_KIB, mca_coll_mi355x_pipe_chunk_kib, "pipe_chunk_kib");
+    KNOB(PIPE_WG_PER_CU, mca_coll_mi355x_pipe_wg_per_cu, "pipe_wg_per_cu");
+    KNOB(PIPE_WT, mca_coll_mi355x_pipe_wt != 0, "pipe_wt");
+    KNOB(ONE_PHASE_MAX_BYTES, mca_coll_mi355x_one_phase_max, "one_phase_max");
+    KNOB(SVC_MAX_BYTES, mca_coll_mi355x_svc_max, "svc_max");
+    KNOB(SVC_PULL_MAX_BYTES, mca_coll_mi355x_svc_pull_max, "svc_pull_max");
+    KNOB(SVC_PULL_COPY_MAX_BYTES, mca_coll_mi355x_svc_copy_max, "svc_copy_max");
+    KNOB(SVC_IDLE_US, mca_coll_mi355x_svc_idle_us, "svc_idle_us");
+    KNOB(SVC_SHRINK_US, mca_coll_mi355x_svc_shrink_us, "svc_shrink_us");
+#undef KNOB
+    return rc;
+}
+
+/* the engine of a communicator this component serves, or NULL (tools and tests) */
+struct mi355x_comm *mca_coll_mi355x_engine_of(struct ompi_communicator_t *comm)
+{
+    if (!comm || comm->c_coll.coll_allreduce != mca_coll_mi355x_allreduce || !comm->c_coll.coll_allreduce_module)
+        return NULL;
+    return MOD(comm->c_coll.coll_allreduce_module)->engine;
+}
+
 /* coll_module_enable (coll.h:176-178): runs after every lower-priority module is installed */
 static int module_enable(mca_coll_base_module_t *module, struct ompi_communicator_t *comm)
 {
@@ -1859,7 +1912,7 @@ static int module_enable(mca_coll_base_module_t *module, struct ompi_communicato
     if (mca_coll_mi355x_rcache_size_limit > 0)
         mi355x_comm_set(m->engine, MI355X_KNOB_RCACHE_SIZE_LIMIT, (long)mca_coll_mi355x_rcache_size_limit);
     apply_tuned_params(m);
-    return OMPI_SUCCESS;
+    return apply_engine_params(m, comm);
 }
 
 /* an int parameter: through the MCA variable system when libopen-pal provides it (in-tree build,
@@ -1908,6 +1961,34 @@ static int component_register(void)
                  "recently used beyond it are closed (0 = unlimited)", OPAL_INFO_LVL_9, &mca_coll_mi355x_rcache_max_maps);
     register_ull("rcache_size_limit", "The same bound in bytes of mapped peer allocations, as mpool_rgpusm_rcache_size_limit "
                  "(0 = unlimited)", OPAL_INFO_LVL_9, &mca_coll_mi355x_rcache_size_limit);
+    /* the engine's crossovers, in the manner of coll/tuned's knobs (coll_tuned_component.c:115-170,
+     * coll_tuned_allreduce.c:949-1005); the defaults were chosen where the ranks shared one GPU */
+    register_int("pipe_min_ranks", "Communicators of at least this many ranks run large allreduces through the "
+                 "pipelined copy||reduce flow (one persistent launch, per-chunk flags); 0 = never", OPAL_INFO_LVL_5,
+                 &mca_coll_mi355x_pipe_min_ranks);
+    register_int("pipe_chunk_kib", "Chunk size of the pipelined allreduce in KiB (0 = about 512 chunks per ring block)",
+                 OPAL_INFO_LVL_6, &mca_coll_mi355x_pipe_chunk_kib);
+    register_int("pipe_wg_per_cu", "Workgroups per CU of the pipelined allreduce (1..8)", OPAL_INFO_LVL_6,
+                 &mca_coll_mi355x_pipe_wg_per_cu);
+    register_int("pipe_wt", "Pipelined allreduce: 1 = fold results stored write-through with system-scope ready flags, "
+                 "0 = stored and released by the producer's fence", OPAL_INFO_LVL_9, &mca_coll_mi355x_pipe_wt);
+    register_ull("one_phase_max", "Per-rank message bytes up to which an allreduce runs the one-launch ring-ordered flow "
+                 "instead of the two-phase one", OPAL_INFO_LVL_6, &mca_coll_mi355x_one_phase_max);
+    register_ull("svc_max", "Per-rank message bytes up to which small allreduce / reduce / allgather / bcast / "
+                 "reduce_scatter_block calls go to the resident LL service in its LL form (svc_max, svc_pull_max and "
+                 "svc_copy_max all 0: no service)", OPAL_INFO_LVL_5,
+                 &mca_coll_mi355x_svc_max);
+    register_ull("svc_pull_max", "Per-rank bytes up to which the service serves allreduce in its pull form (above "
+                 "svc_max)", OPAL_INFO_LVL_6, &mca_coll_mi355x_svc_pull_max);
+    register_ull("svc_copy_max", "Per-rank bytes up to which the service copies allgather / bcast (above svc_max)",
+                 OPAL_INFO_LVL_6, &mca_coll_mi355x_svc_copy_max);
+    register_int("svc_idle_us", "Idle time after which the resident service's kernel leaves the GPU, microseconds "
+                 "(100 .. 60000000)", OPAL_INFO_LVL_6, &mca_coll_mi355x_svc_idle_us);
+    register_int("svc_shrink_us", "Idle time after which the resident service shrinks to one workgroup, microseconds "
+                 "(0 = never)", OPAL_INFO_LVL_6, &mca_coll_mi355x_svc_shrink_us);
+    register_int("selftest", "Run the cross-device flows' self-tests at a communicator's first device-buffer collective "
+                 "(a flow that fails on any rank is turned off on every rank); 0 = trust every flow", OPAL_INFO_LVL_9,
+                 &mca_coll_mi355x_selftest);
     return OMPI_SUCCESS;
 }
 static int component_open(void) { return OMPI_SUCCESS; }

@@ -81,6 +81,7 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     c->size = size;
     c->device = device;
     c->timeout_s = env_double("MI355X_TIMEOUT_S", 600.0);
+    c->selftest = env_double("MI355X_SELFTEST", 1.0) != 0.0;
     c->shm_name = std::string("/mi355x_") + key;
     for (char &ch : c->shm_name)
         if (ch != '/' && !isalnum((unsigned char)ch) && ch != '_' && ch != '-') ch = '_';
@@ -105,7 +106,7 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
         }
     } else {
         const auto t0 = std::chrono::steady_clock::now();
-        for (;;) {
+        for (int tries = 0;; ++tries) {
             fd = shm_open(c->shm_name.c_str(), O_RDWR, 0600);
             if (fd >= 0) {
                 struct stat st;
@@ -117,7 +118,9 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
                 delete c;
                 return set_error(MI355X_ERR_TIMEOUT, "rank %d: control segment %s never appeared", rank, key);
             }
-            usleep(1000);
+            // ranks that enter together (an MPI_Comm_dup after a barrier) find rank 0's segment within
+            // tens of microseconds: poll finely first, then back off
+            usleep(tries < 200 ? 10 : 1000);
         }
     }
     void *m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
@@ -128,7 +131,8 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     }
     c->ctrl = (Ctrl *)m;
     if (rank == 0) {
-        std::memset(m, 0, bytes);
+        // (a fresh O_EXCL object: ftruncate zero-filled it, and touching every page here would
+        // only fault the peers' envelope rings in early)
         c->ctrl->size = (uint32_t)size;
         uint64_t secret = 0;
         FILE *ur = fopen("/dev/urandom", "rb");
@@ -140,13 +144,14 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
         __atomic_store_n(&c->ctrl->magic, kMagic, __ATOMIC_RELEASE);
     } else {
         const auto t0 = std::chrono::steady_clock::now();
-        while (__atomic_load_n(&c->ctrl->magic, __ATOMIC_ACQUIRE) != kMagic) {
+        for (int tries = 0; __atomic_load_n(&c->ctrl->magic, __ATOMIC_ACQUIRE) != kMagic; ++tries) {
             if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
                 munmap(m, bytes);
                 delete c;
                 return set_error(MI355X_ERR_TIMEOUT, "rank %d: control segment never initialised", rank);
             }
-            usleep(200);
+            if (tries < 2000) sched_yield();
+            else usleep(200);
         }
     }
     c->ctrl->slot[rank].pid = (int32_t)getpid();
@@ -179,12 +184,9 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     c->rcache_max_maps = (size_t)std::max(0.0, env_double("MI355X_RCACHE_MAX_MAPS", 0.0));
     c->rcache_limit = (size_t)std::max(0.0, env_double("MI355X_RCACHE_SIZE_LIMIT", 0.0));
     c->gated = size > 1;
-    if (rc == MI355X_SUCCESS && size > 1) rc = setup_done_words(c);
-    if (rc == MI355X_SUCCESS && size > 1) rc = ll_selftest(c);
-    if (rc == MI355X_SUCCESS && size > 1) {
-        svc_setup(c);
-        rc = pipe_selftest(c);
-    }
+    // nothing device-side happens here: the LL region, the service's queue, the flows' self-tests
+    // and their allocations wait for the first device-buffer collective (dev_setup), so a
+    // host-only communicator costs one barrier and no device memory
     if (rc) {
         mi355x_comm_destroy(c);
         return rc;
@@ -235,6 +237,7 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
     for (hipEvent_t e : c->tev)
         if (e) (void)hipEventDestroy(e);
     if (c->nb_stream) (void)hipStreamDestroy(c->nb_stream);
+    if (c->setup_s) (void)hipStreamDestroy(c->setup_s);
     for (auto &kv : c->peer_maps) close_map(kv.second);
     for (LocalReg &r : c->local_regs) drop_reg(r);
     for (auto &kv : c->fd_stash) close(kv.second);
@@ -396,6 +399,10 @@ int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
     case MI355X_KNOB_FLOWS_FAILED: *value = (long)c->flows_failed; break;
     case MI355X_KNOB_CREATE_US: *value = (long)c->create_us; break;
     case MI355X_KNOB_SELFTEST_US: *value = (long)c->selftest_us; break;
+    case MI355X_KNOB_DEV_SETUP: *value = c->dev_ready ? 1 : 0; break;
+    case MI355X_KNOB_SELFTEST: *value = c->selftest ? 1 : 0; break;
+    case MI355X_KNOB_PIPE_CALLS: *value = (long)c->pipe_calls; break;
+    case MI355X_KNOB_SETUP_US: *value = (long)c->setup_us; break;
     case MI355X_KNOB_SVC_OWNER: *value = c->svc_ok ? 1 : 0; break;
     case MI355X_KNOB_SVC_CLAIMS: *value = (long)c->svc_epoch; break;
     case MI355X_KNOB_SVC_IDLE_US: *value = (long)(c->svc_idle_s * 1e6 + 0.5); break;
@@ -425,7 +432,23 @@ int mi355x_comm_phase_ms(const mi355x_comm_t *c, float *phase1_ms, float *phase2
 int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
+    if (!c->dev_ready && !c->loopback && c->size > 1) {
+        // limits that size or depend on the device setup: kept for dev_setup (which sizes the LL
+        // region by them) and applied through this function once the self-tests have run
+        size_t *field = knob == MI355X_KNOB_LL_MAX_BYTES ? &c->ll_max
+                        : knob == MI355X_KNOB_SVC_MAX_BYTES ? &c->svc_max
+                        : knob == MI355X_KNOB_SVC_PULL_MAX_BYTES ? &c->svc_pull_max
+                        : knob == MI355X_KNOB_SVC_PULL_COPY_MAX_BYTES ? &c->svc_copy_max : nullptr;
+        if (field) {
+            const long hi = (knob == MI355X_KNOB_LL_MAX_BYTES || knob == MI355X_KNOB_SVC_MAX_BYTES) ? (64l << 20) : (1l << 30);
+            if (value < 0 || value > hi) return set_error(MI355X_ERR_ARG, "knob %d out of range", knob);
+            *field = (size_t)value;
+            c->preset.emplace_back(knob, value);
+            return MI355X_SUCCESS;
+        }
+    }
     switch (knob) {
+    case MI355X_KNOB_SELFTEST: c->selftest = value != 0; break;  // (read by the device setup)
     case MI355X_KNOB_ALLREDUCE_ALG: c->knob_allreduce = (int)value; break;
     case MI355X_KNOB_REDUCE_ALG: c->knob_reduce = (int)value; break;
     case MI355X_KNOB_REDUCE_SCATTER_ALG: c->knob_rs = (int)value; break;

@@ -95,7 +95,7 @@ void gate_exit(mi355x_comm *c);
 bool svc_revoke(mi355x_comm *x);
 int ll_resync(mi355x_comm *c);
 unsigned selftest_injected();
-bool selftest_on();
+bool selftest_on(const mi355x_comm *c);
 uint32_t st_val(uint64_t seed, int q, size_t i);
 int agree_flows(mi355x_comm *c, unsigned mine, unsigned *all);
 int svc_selftest(mi355x_comm *c);
@@ -103,6 +103,8 @@ int pipe_selftest(mi355x_comm *c);
 int svc_claim(mi355x_comm *c);
 int svc_maybe_claim(mi355x_comm *c, bool sized);
 void svc_setup(mi355x_comm *c);
+int dev_setup(mi355x_comm *c);
+hipStream_t setup_stream(mi355x_comm *c);
 int ensure_pipe(mi355x_comm *c);
 int pipe_allreduce(mi355x_comm *c, int op, int type, const Program &pr,
                           const std::vector<std::vector<void *>> &P, size_t count, hipStream_t s);

@@ -383,6 +383,15 @@ int setup_done_words(mi355x_comm *c)
 // The scratch may be exported to peers (MPI_Reduce's owner blocks): never a small allocation
 // (small hipMallocs can fail hipIpcOpenMemHandle on the importer with "invalid device
 // pointer"), and grown geometrically so it is rarely freed while peers hold a mapping.
+// The engine's own stream for setup-time fills and copies: a non-blocking stream, so setup never
+// waits for -- or makes wait -- the application's streams (no hipDeviceSynchronize anywhere on the
+// setup paths); nullptr when it cannot be created (the caller's error path reports the HIP error).
+hipStream_t setup_stream(mi355x_comm *c)
+{
+    if (!c->setup_s && hipStreamCreateWithFlags(&c->setup_s, hipStreamNonBlocking) != hipSuccess) c->setup_s = nullptr;
+    return c->setup_s;
+}
+
 int ensure_scratch(mi355x_comm *c, size_t bytes)
 {
     if (c->scratch_bytes >= bytes) return MI355X_SUCCESS;

@@ -48,6 +48,7 @@ int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count,
     int rc = check_common(c, op, type);
     if (rc) return rc;
     if (count == 0) return MI355X_SUCCESS;
+    if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     hipStream_t s = resolve_stream(stream);
     const size_t esz = mi355x_type_size(type);
     const void *in = sbuf ? sbuf : rbuf;
@@ -215,7 +216,10 @@ int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count,
     }
     // multi-process: the fold of my block and the pulls of the others in one pipelined launch
     // (coll_pipe.hip); loopback ranks share one process's queues, so they keep two phases
-    if (pipe) return pipe_allreduce(c, op, type, pr, P, count, s);
+    if (pipe) {
+        c->pipe_calls++;
+        return pipe_allreduce(c, op, type, pr, P, count, s);
+    }
     // phase 1: reduce own block locally; phase 2: pull every other block from its owner
     const bool tp = c->time_phases && c->tev[0];
     if (tp) MI_HIP(hipEventRecord(c->tev[0], s));
@@ -265,6 +269,7 @@ int reduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, in
     if (root < 0 || root >= c->size) return set_error(MI355X_ERR_ARG, "bad root");
     if (!sbuf && c->rank != root) return set_error(MI355X_ERR_ARG, "MPI_IN_PLACE is only valid at the root");
     if (count == 0) return MI355X_SUCCESS;
+    if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     hipStream_t s = resolve_stream(stream);
     const size_t esz = mi355x_type_size(type);
     const void *in = sbuf ? sbuf : rbuf;
@@ -360,6 +365,7 @@ int reduce_scatter_block_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, si
     if (rc) return rc;
     const size_t count = rcount * (size_t)c->size;
     if (count == 0) return MI355X_SUCCESS;
+    if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     hipStream_t s = resolve_stream(stream);
     const size_t esz = mi355x_type_size(type);
     const void *in = sbuf ? sbuf : rbuf;
@@ -425,6 +431,7 @@ int reduce_scatter_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, const in
     }
     const size_t count = disp[c->size];
     if (count == 0) return MI355X_SUCCESS;
+    if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     hipStream_t s = resolve_stream(stream);
     const size_t esz = mi355x_type_size(type);
     const void *in = sbuf ? sbuf : rbuf;
@@ -506,6 +513,7 @@ int allgather_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t bytes,
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     if (bytes == 0) return MI355X_SUCCESS;
+    if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     hipStream_t s = resolve_stream(stream);
     const void *src = sbuf ? sbuf : (const char *)rbuf + (size_t)c->rank * bytes;
     int rc0 = svc_maybe_claim(c, bytes <= std::max(c->svc_max, c->svc_copy_max));
@@ -572,6 +580,7 @@ int bcast_impl(mi355x_comm_t *c, void *buf, size_t bytes, int root, void *stream
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     if (root < 0 || root >= c->size) return set_error(MI355X_ERR_ARG, "bad root");
     if (bytes == 0 || c->size == 1) return MI355X_SUCCESS;
+    if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     hipStream_t s = resolve_stream(stream);
     int rc0 = svc_maybe_claim(c, bytes <= std::max(c->svc_max, c->svc_copy_max));
     if (rc0) return rc0;

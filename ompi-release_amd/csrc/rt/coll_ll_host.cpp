@@ -82,10 +82,12 @@ int ensure_ll(mi355x_comm *c)
     if (c->ll_base) (void)hipFree(c->ll_base);
     c->ll_base = nullptr;
     MI_HIP(hipExtMallocWithFlags((void **)&c->ll_base, total, hipDeviceMallocUncached));
-    MI_HIP(hipMemset(c->ll_base, 0, total));
+    hipStream_t ss = setup_stream(c);
+    if (!ss) return set_error(MI355X_ERR_HIP, "rank %d: cannot create the setup stream", c->rank);
+    MI_HIP(hipMemsetAsync(c->ll_base, 0, total, ss));
     if (!c->ll_ctr) MI_HIP(hipMalloc((void **)&c->ll_ctr, sizeof(uint64_t)));
-    MI_HIP(hipMemset(c->ll_ctr, 0, sizeof(uint64_t)));
-    MI_HIP(hipDeviceSynchronize());
+    MI_HIP(hipMemsetAsync(c->ll_ctr, 0, sizeof(uint64_t), ss));
+    MI_HIP(hipStreamSynchronize(ss));
     if (!c->ll_err) MI_HIP(hipHostMalloc((void **)&c->ll_err, sizeof(uint32_t), hipHostMallocCoherent));
     c->ll_slot = want;
     c->ll_bytes = total;
@@ -142,8 +144,8 @@ int ll_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s)
     if (rc) return rc;
     MI_HIP(hipStreamSynchronize(s));
     if (__atomic_load_n(c->ll_err, __ATOMIC_ACQUIRE)) {
-        (void)hipMemset(c->ll_ctr, 0, sizeof(uint64_t));  // its count is off now: restart it
-        (void)hipDeviceSynchronize();
+        (void)hipMemsetAsync(c->ll_ctr, 0, sizeof(uint64_t), s);  // its count is off now: restart it
+        (void)hipStreamSynchronize(s);
         c->ll_ctr_base = 0;
         return set_error(MI355X_ERR_TIMEOUT, "rank %d: LL call %llu timed out waiting for a peer", c->rank,
                          (unsigned long long)seq);
@@ -171,9 +173,10 @@ int ll_selftest(mi355x_comm *c)
     if (rc) return rc;
     const size_t per = std::min<size_t>(8192, c->ll_slot), n = (size_t)c->size;
     char *buf = nullptr;
-    bool ok = hipMalloc((void **)&buf, per * (n + 1)) == hipSuccess;
-    if (ok) ok = hipMemset(buf, c->rank + 1, per) == hipSuccess && hipMemset(buf + per, 0, per * n) == hipSuccess &&
-                 hipDeviceSynchronize() == hipSuccess;
+    hipStream_t ss = setup_stream(c);
+    bool ok = ss && hipMalloc((void **)&buf, per * (n + 1)) == hipSuccess;
+    if (ok) ok = hipMemsetAsync(buf, c->rank + 1, per, ss) == hipSuccess &&
+                 hipMemsetAsync(buf + per, 0, per * n, ss) == hipSuccess && hipStreamSynchronize(ss) == hipSuccess;
     if (ok) {
         LLArgs a;
         std::memset(&a, 0, sizeof(a));
@@ -184,12 +187,13 @@ int ll_selftest(mi355x_comm *c)
         a.push_mask = ~0ull;
         const double saved = c->timeout_s;
         c->timeout_s = env_double("MI355X_LL_PROBE_S", 5.0);
-        ok = ll_run(c, a, 0, 0, nullptr) == MI355X_SUCCESS;
+        ok = ll_run(c, a, 0, 0, ss) == MI355X_SUCCESS;
         c->timeout_s = saved;
     }
     if (ok) {
         std::vector<unsigned char> h(per * n);
-        ok = hipMemcpy(h.data(), buf + per, per * n, hipMemcpyDeviceToHost) == hipSuccess;
+        ok = hipMemcpyAsync(h.data(), buf + per, per * n, hipMemcpyDeviceToHost, ss) == hipSuccess &&
+             hipStreamSynchronize(ss) == hipSuccess;
         for (size_t q = 0; q < n && ok; ++q)
             for (size_t i = 0; i < per && ok; i += 509) ok = h[q * per + i] == (unsigned char)(q + 1);
     }

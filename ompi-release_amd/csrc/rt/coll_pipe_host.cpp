@@ -51,11 +51,13 @@ int ensure_pipe(mi355x_comm *c)
     const size_t n = (size_t)c->size;
     const size_t bytes = (n * kPipeKmax * sizeof(uint64_t) + 4095) / 4096 * 4096;
     MI_HIP(hipExtMallocWithFlags((void **)&c->pipe_base, bytes, hipDeviceMallocUncached));
-    MI_HIP(hipMemset(c->pipe_base, 0, bytes));
+    hipStream_t ss = setup_stream(c);
+    if (!ss) return set_error(MI355X_ERR_HIP, "rank %d: cannot create the setup stream", c->rank);
+    MI_HIP(hipMemsetAsync(c->pipe_base, 0, bytes, ss));
     MI_HIP(hipMalloc((void **)&c->pipe_queue, sizeof(uint64_t)));
-    MI_HIP(hipMemset(c->pipe_queue, 0, sizeof(uint64_t)));
+    MI_HIP(hipMemsetAsync(c->pipe_queue, 0, sizeof(uint64_t), ss));
     if (!c->ll_err) MI_HIP(hipHostMalloc((void **)&c->ll_err, sizeof(uint32_t), hipHostMallocCoherent));
-    MI_HIP(hipDeviceSynchronize());
+    MI_HIP(hipStreamSynchronize(ss));
     c->pipe_kmax = kPipeKmax;
     c->pipe_qbase = 0;
     c->pipe_seq = 0;
@@ -176,8 +178,8 @@ int pipe_allreduce(mi355x_comm *c, int op, int type, const Program &pr,
     MI_HIP(hipStreamSynchronize(s));
     if (__atomic_load_n(c->ll_err, __ATOMIC_ACQUIRE)) {
         // the counter no longer has its expected value: start it over for the next call
-        (void)hipMemset(c->pipe_queue, 0, sizeof(uint64_t));
-        (void)hipDeviceSynchronize();
+        (void)hipMemsetAsync(c->pipe_queue, 0, sizeof(uint64_t), s);
+        (void)hipStreamSynchronize(s);
         c->pipe_qbase = 0;
         c->ctrl->abort_flag.store(1);
         return set_error(MI355X_ERR_TIMEOUT, "rank %d: pipelined allreduce %llu timed out waiting for a peer", c->rank,

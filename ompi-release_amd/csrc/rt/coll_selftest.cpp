@@ -65,7 +65,7 @@ unsigned selftest_injected()
     return m;
 }
 
-bool selftest_on() { return env_double("MI355X_SELFTEST", 1.0) != 0.0; }
+bool selftest_on(const mi355x_comm *c) { return c->selftest; }
 
 uint32_t st_val(uint64_t seed, int q, size_t i)
 {
@@ -83,10 +83,12 @@ struct SelfTest {
     char *in = nullptr, *out = nullptr;
     size_t cap = 0;
     bool ok = true;
+    hipStream_t s = nullptr;  // the engine's setup stream: the application's streams are never waited for
     SelfTest(mi355x_comm *c_, uint64_t salt, size_t bytes) : c(c_), cap(bytes)
     {
         seed = c->ctrl->secret ^ (salt * 0x632be59bd9b4e019ull);
-        ok = hipMalloc((void **)&in, cap) == hipSuccess && hipMalloc((void **)&out, cap) == hipSuccess;
+        s = setup_stream(c);
+        ok = s && hipMalloc((void **)&in, cap) == hipSuccess && hipMalloc((void **)&out, cap) == hipSuccess;
     }
     ~SelfTest()
     {
@@ -99,14 +101,14 @@ struct SelfTest {
     {
         std::vector<uint32_t> h(count);
         for (size_t i = 0; i < count; ++i) h[i] = st_val(seed + (uint64_t)t, c->rank, i);
-        // (the null stream only: the application's other streams are not waited for)
-        return ok && count * 4 <= cap && hipMemcpy(in, h.data(), count * 4, hipMemcpyHostToDevice) == hipSuccess &&
-               hipMemsetAsync(out, 0xa5, cap, nullptr) == hipSuccess && hipStreamSynchronize(nullptr) == hipSuccess;
+        return ok && count * 4 <= cap && hipMemcpyAsync(in, h.data(), count * 4, hipMemcpyHostToDevice, s) == hipSuccess &&
+               hipMemsetAsync(out, 0xa5, cap, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
     }
     bool fetch(std::vector<uint32_t> &h, size_t count)
     {
         h.assign(count, 0);
-        return hipMemcpy(h.data(), out, count * 4, hipMemcpyDeviceToHost) == hipSuccess;
+        return hipMemcpyAsync(h.data(), out, count * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
+               hipStreamSynchronize(s) == hipSuccess;
     }
     // element i of the SUM over every rank's input of test t
     uint32_t sum(int t, size_t i) const
@@ -140,7 +142,7 @@ int svc_selftest(mi355x_comm *c)
 {
     c->svc_flows_tested = true;
     const unsigned tested = MI355X_FLOW_SVC_LL | MI355X_FLOW_SVC_PULL | MI355X_FLOW_SVC_COPY | MI355X_FLOW_SVC_RS;
-    if (!selftest_on()) return MI355X_SUCCESS;
+    if (!selftest_on(c)) return MI355X_SUCCESS;
     const auto t0 = std::chrono::steady_clock::now();
     const int n = c->size;
     // the flows' mechanisms at fixed sizes, whatever the limits are set to now; nothing forced
@@ -173,10 +175,10 @@ int svc_selftest(mi355x_comm *c)
         {
             bool ok = st.prepare(1, 2048);
             const uint64_t b = c->svc_calls;
-            ok = ok && allgather_impl(c, st.in, st.out, 8192, nullptr) == MI355X_SUCCESS && st.fetch(h, 2048 * (size_t)n);
+            ok = ok && allgather_impl(c, st.in, st.out, 8192, st.s) == MI355X_SUCCESS && st.fetch(h, 2048 * (size_t)n);
             for (int q = 0; q < n && ok; ++q)
                 for (size_t i = 0; i < 2048 && ok; ++i) ok = h[(size_t)q * 2048 + i] == st_val(st.seed + 1, q, i);
-            ok = ok && st.prepare(2, 2048) && allreduce_impl(c, st.in, st.out, 2048, i32, sum, nullptr) == MI355X_SUCCESS &&
+            ok = ok && st.prepare(2, 2048) && allreduce_impl(c, st.in, st.out, 2048, i32, sum, st.s) == MI355X_SUCCESS &&
                  st.fetch(h, 2048);
             for (size_t i = 0; i < 2048 && ok; ++i) ok = h[i] == st.sum(2, i);
             if (ok && served(b, 2)) pass |= MI355X_FLOW_SVC_LL;
@@ -186,24 +188,24 @@ int svc_selftest(mi355x_comm *c)
             const size_t cnt = 12288;  // 48 KiB
             bool ok = st.prepare(3, cnt);
             const uint64_t b = c->svc_calls;
-            ok = ok && allreduce_impl(c, st.in, st.out, cnt, i32, sum, nullptr) == MI355X_SUCCESS && st.fetch(h, cnt);
+            ok = ok && allreduce_impl(c, st.in, st.out, cnt, i32, sum, st.s) == MI355X_SUCCESS && st.fetch(h, cnt);
             for (size_t i = 0; i < cnt && ok; ++i) ok = h[i] == st.sum(3, i);
             if (ok && served(b, 1)) pass |= MI355X_FLOW_SVC_PULL;
             // pull copies: allgather of every peer's block, bcast of the last rank's buffer
             ok = st.prepare(4, cnt);
             const uint64_t b2 = c->svc_calls;
-            ok = ok && allgather_impl(c, st.in, st.out, cnt * 4, nullptr) == MI355X_SUCCESS && st.fetch(h, cnt * (size_t)n);
+            ok = ok && allgather_impl(c, st.in, st.out, cnt * 4, st.s) == MI355X_SUCCESS && st.fetch(h, cnt * (size_t)n);
             for (int q = 0; q < n && ok; ++q)
                 for (size_t i = 0; i < cnt && ok; ++i) ok = h[(size_t)q * cnt + i] == st_val(st.seed + 4, q, i);
-            ok = ok && st.prepare(5, cnt) && hipMemcpy(st.out, st.in, cnt * 4, hipMemcpyDeviceToDevice) == hipSuccess &&
-                 bcast_impl(c, st.out, cnt * 4, n - 1, nullptr) == MI355X_SUCCESS && st.fetch(h, cnt);
+            ok = ok && st.prepare(5, cnt) && hipMemcpyAsync(st.out, st.in, cnt * 4, hipMemcpyDeviceToDevice, st.s) == hipSuccess &&
+                 bcast_impl(c, st.out, cnt * 4, n - 1, st.s) == MI355X_SUCCESS && st.fetch(h, cnt);
             for (size_t i = 0; i < cnt && ok; ++i) ok = h[i] == st_val(st.seed + 5, n - 1, i);
             if (ok && served(b2, 2)) pass |= MI355X_FLOW_SVC_COPY;
             // reduce-scatter form: my 16 KiB block evaluated from the peers' mapped inputs
             const size_t rc_ = 4096;
             ok = st.prepare(6, rc_ * (size_t)n);
             const uint64_t b3 = c->svc_calls;
-            ok = ok && reduce_scatter_block_impl(c, st.in, st.out, rc_, i32, sum, nullptr) == MI355X_SUCCESS &&
+            ok = ok && reduce_scatter_block_impl(c, st.in, st.out, rc_, i32, sum, st.s) == MI355X_SUCCESS &&
                  st.fetch(h, rc_);
             for (size_t i = 0; i < rc_ && ok; ++i) ok = h[i] == st.sum(6, (size_t)c->rank * rc_ + i);
             if (ok && served(b3, 1)) pass |= MI355X_FLOW_SVC_RS;
@@ -245,7 +247,7 @@ int svc_selftest(mi355x_comm *c)
 // allreduce of 128 KiB blocks in 16 KiB chunks (8 per block), forced onto the pipelined flow.
 int pipe_selftest(mi355x_comm *c)
 {
-    if (!selftest_on()) return MI355X_SUCCESS;
+    if (!selftest_on(c)) return MI355X_SUCCESS;
     const auto t0 = std::chrono::steady_clock::now();
     const int n = c->size;
     const size_t count = (size_t)n * 32768;
@@ -270,7 +272,7 @@ int pipe_selftest(mi355x_comm *c)
         std::vector<uint32_t> h;
         const uint64_t refused = c->pipe_refused;
         bool ok = st.prepare(7, count) &&
-                  allreduce_impl(c, st.in, st.out, count, MI355X_T_INT32, MI355X_OP_SUM, nullptr) == MI355X_SUCCESS &&
+                  allreduce_impl(c, st.in, st.out, count, MI355X_T_INT32, MI355X_OP_SUM, st.s) == MI355X_SUCCESS &&
                   st.fetch(h, count);
         for (size_t i = 0; i < count && ok; ++i) ok = h[i] == st.sum(7, i);
         admitted = c->pipe_refused == refused;
@@ -372,6 +374,36 @@ int svc_maybe_claim(mi355x_comm *c, bool sized)
 }
 
 // at creation: the service's settings (the claim itself waits for a service-sized call)
+// The communicator's device-side setup: the completion words, the LL region and its self-test, the
+// service's resources and the pipelined flow's self-test, with their allocations.  Deferred from
+// mi355x_comm_create to the first device-buffer collective, as smcuda checks CUDA IPC support
+// "lazily, when the first GPU access occurs, rather than during MPI_Init() time"
+// (btl/smcuda/README:36-40): a communicator that only ever moves host buffers (a dup for a host
+// library, a split used for bookkeeping) costs one barrier and no device memory.  Collective:
+// every rank reaches it in the same call, because every collective entry calls it before its
+// first step and collectives are called in the same order on every rank.  Knobs set before it
+// (preset) are applied once the self-tests have decided what this communicator may use.
+int dev_setup(mi355x_comm *c)
+{
+    if (c->dev_ready) return MI355X_SUCCESS;
+    c->dev_ready = true;  // (the self-tests below run collectives themselves)
+    if (c->size < 2 || c->loopback) return MI355X_SUCCESS;
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = setup_done_words(c);
+    if (rc == MI355X_SUCCESS) rc = ll_selftest(c);
+    if (rc == MI355X_SUCCESS) {
+        svc_setup(c);
+        rc = pipe_selftest(c);
+    }
+    std::vector<std::pair<int, long>> pre;
+    pre.swap(c->preset);
+    for (const auto &kv : pre)
+        if (rc == MI355X_SUCCESS) rc = mi355x_comm_set(c, kv.first, kv.second);
+    c->setup_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    TRACE(c, "device setup: %.0f us, rc %d", c->setup_us, rc);
+    return rc;
+}
+
 void svc_setup(mi355x_comm *c)
 {
     c->svc_max = (size_t)std::max(0.0, env_double("MI355X_SVC_MAX_BYTES", (double)c->svc_max));

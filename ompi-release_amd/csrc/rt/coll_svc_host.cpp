@@ -488,14 +488,15 @@ bool svc_revoke(mi355x_comm *x)
 // service self-test failed somewhere, ranks may disagree on the call number or hold stale granules.
 int ll_resync(mi355x_comm *c)
 {
-    (void)svc_stop(c);
-    (void)hipDeviceSynchronize();
+    (void)svc_stop(c);  // (every LL launch of this communicator was synchronised by its caller)
     int rc = barrier(c);
     if (rc) return rc;
     if (c->svc_stuck) return set_error(MI355X_ERR_HIP, "rank %d: the resident service did not leave", c->rank);
-    MI_HIP(hipMemset(c->ll_base, 0, c->ll_bytes));
-    MI_HIP(hipMemset(c->ll_ctr, 0, sizeof(uint64_t)));
-    MI_HIP(hipDeviceSynchronize());
+    hipStream_t ss = setup_stream(c);
+    if (!ss) return set_error(MI355X_ERR_HIP, "rank %d: cannot create the setup stream", c->rank);
+    MI_HIP(hipMemsetAsync(c->ll_base, 0, c->ll_bytes, ss));
+    MI_HIP(hipMemsetAsync(c->ll_ctr, 0, sizeof(uint64_t), ss));
+    MI_HIP(hipStreamSynchronize(ss));
     c->ll_seq = 0;
     c->ll_ctr_base = 0;
     if (c->ll_err) *c->ll_err = 0;

@@ -350,6 +350,13 @@ struct mi355x_comm {
     uint64_t gate_calls = 0;                      // gated calls completed (RankSlot::calls)
     size_t ll_bytes = 0;                          // LL region size (ll_resync)
     double create_us = 0, selftest_us = 0;
+    // device-side setup (done words, LL region + self-test, the service's resources, the pipelined
+    // flow's self-test), deferred from creation to the first device-buffer collective (dev_setup)
+    bool dev_ready = false;
+    bool selftest = true;                         // MI355X_KNOB_SELFTEST (env MI355X_SELFTEST)
+    double setup_us = 0;
+    hipStream_t setup_s = nullptr;                // the engine's own stream for setup-time copies
+    std::vector<std::pair<int, long>> preset;     // knobs set before dev_setup, applied after it
     bool svc_stuck = false;                       // a service kernel never left (its memory is leaked, never reused)
     uint64_t *svc_trace = nullptr;                // MI355X_SVC_TRACE=1: stage stamps (device memory), printed at destroy
     // pipelined allreduce (coll_pipe.hip): per-chunk ready flags in an uncached region that
@@ -373,6 +380,7 @@ struct mi355x_comm {
     int pipe_token = -1;                          // token table slot of my GPU (-1: not looked up)
     int pipe_entry = -1;                          // my registration in that token's holder list while held
     uint64_t pipe_refused = 0;                    // calls that fell back because a token was taken
+    uint64_t pipe_calls = 0;                      // allreduces served by the pipelined flow
     // finish() by device-written completion words (see RankSlot::done): the control segment
     // registered with HIP (hipHostRegister) and its device address; 0 = stream sync + barrier
     // MI355X_LAT_PROFILE=1: host time of the small-message allreduce's steps (entry -> input sync

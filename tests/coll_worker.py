@@ -977,6 +977,77 @@ def staging_main():
     print(f"rank {rank} staging OK", flush=True)
 
 
+def mca_vars_main():
+    """the engine's crossovers as coll_mi355x_* MCA variables (registered through the harness's
+    variable system, which reads OMPI_MCA_<name> like libopen-pal's environment source): with
+    pipe_min_ranks = 2 and the service limits svc_max / svc_pull_max / svc_copy_max = 0 a 2-rank communicator runs a large allreduce through the
+    pipelined flow (PIPE_CALLS) and keeps small calls off the resident service; re-registered with
+    the defaults, the next communicator does neither -- both exact vs the oracle"""
+    import os
+    rank, size = int(sys.argv[1]), int(sys.argv[2])
+    import torch
+    torch.cuda.set_device(rank % torch.cuda.device_count())
+    m = mini()
+    L, pkg = m.lib, m.pkg
+    oracle = load_oracle()
+    m.install_oracle_base(oracle)
+    comp = m.component_ptr(m.coll, "mca_coll_mi355x_component")
+    m.coll.mca_coll_mi355x_engine_of.restype = ctypes.c_void_p
+    m.coll.mca_coll_mi355x_engine_of.argtypes = [ctypes.c_void_p]
+    rt = pkg.rt()
+    ptrs = lambda arrs: (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+
+    def knob(eng, name):
+        v = ctypes.c_long(0)
+        assert rt.mi355x_comm_get(ctypes.c_void_p(eng), pkg.KNOB[name], ctypes.byref(v)) == 0
+        return v.value
+
+    fdt = m.dtype_for_slot(pkg.T["FLOAT"])
+    op = m.select_op(pkg.OP["SUM"])
+    count = 1 << 20
+    xs = [opdata.make("FLOAT", count, 300 + r) for r in range(size)]
+    outs = [np.zeros_like(xs[0]) for _ in range(size)]
+    oracle.oracle_allreduce(0, size, count, pkg.T["FLOAT"], pkg.OP["SUM"], 0, ptrs(xs), ptrs(outs))
+    names = ("pipe_min_ranks", "svc_max", "svc_pull_max", "svc_copy_max")
+    off = {"pipe_min_ranks": "2", "svc_max": "0", "svc_pull_max": "0", "svc_copy_max": "0"}
+    for step, (env, pipe, svc) in enumerate(((off, 1, 0), ({}, 0, 32 << 10))):
+        for k in names:
+            os.environ.pop("OMPI_MCA_coll_mi355x_" + k, None)
+        for k, v in env.items():
+            os.environ["OMPI_MCA_coll_mi355x_" + k] = v
+        assert L.mini_component_register(comp) == 0
+        comm = L.mini_comm_create(rank, size, 50 + step)
+        assert L.mini_comm_set_channel(comm, f"{sys.argv[3]}_{step}".encode()) == 0
+        L.mini_comm_install(comm, L.mini_stub_module())
+        assert L.mini_coll_select(comm, comp) == 90
+        eng = m.coll.mca_coll_mi355x_engine_of(comm)
+        assert eng
+        assert knob(eng, "PIPE") == pipe, ("PIPE", knob(eng, "PIPE"))
+        assert knob(eng, "DEV_SETUP") == 0
+        dx = torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda()
+        dr = torch.zeros_like(dx)
+        torch.cuda.synchronize()
+        assert L.mini_allreduce(comm, dx.data_ptr(), dr.data_ptr(), count, fdt, op) == 0
+        opdata.assert_same("FLOAT", "SUM", dr.cpu().numpy().view(np.float32), outs[rank], f"mca vars step {step}")
+        assert knob(eng, "PIPE_CALLS") == pipe, ("PIPE_CALLS", knob(eng, "PIPE_CALLS"))
+        if svc == 0:
+            assert knob(eng, "SVC_MAX_BYTES") == 0
+            calls0 = knob(eng, "SVC_CALLS")
+            x = torch.ones(256, device="cuda")
+            y = torch.empty_like(x)
+            torch.cuda.synchronize()
+            for _ in range(40):
+                assert L.mini_allreduce(comm, x.data_ptr(), y.data_ptr(), 256, fdt, op) == 0
+            assert bool(torch.all(y == size).item())
+            assert knob(eng, "SVC_CALLS") == calls0, "svc_max = 0, yet the service served"
+        L.mini_comm_destroy(comm)
+    for k in names:
+        os.environ.pop("OMPI_MCA_coll_mi355x_" + k, None)
+    assert L.mini_component_register(comp) == 0
+    L.mini_op_destroy(op)
+    print(f"rank {rank} mca_vars OK", flush=True)
+
+
 def main():
     if len(sys.argv) > 4 and sys.argv[4] == "split":
         return split_main()
@@ -986,6 +1057,8 @@ def main():
         return tuned_vars_main()
     if len(sys.argv) > 4 and sys.argv[4] == "staging":
         return staging_main()
+    if len(sys.argv) > 4 and sys.argv[4] == "mca_vars":
+        return mca_vars_main()
     rank, size = int(sys.argv[1]), int(sys.argv[2])
     import torch
     ndev = torch.cuda.device_count()

@@ -294,7 +294,7 @@ def svc_all_slots(pkg, comm, rank, size, oracle, torch):
     k = ncalls = 0
     for code in range(1, 13):
         for ty in range(len(pkg.TYPES)):
-            if not (oracle.oracle_has_op(code, ty) and pkg.op_supported(code, ty)):
+            if not (oracle.oracle_has_op(code, ty) and pkg.comm_op_supported(code, ty)):
                 continue
             tname, opname = pkg.TYPES[ty], pkg.OPS[code]
             esz = pkg.type_size(ty)
@@ -475,7 +475,7 @@ def pipe_all_slots(pkg, comm, rank, size, oracle, torch):
     k = 0
     for code in range(1, 13):
         for ty in range(len(pkg.TYPES)):
-            if not (oracle.oracle_has_op(code, ty) and pkg.op_supported(code, ty)):
+            if not (oracle.oracle_has_op(code, ty) and pkg.comm_op_supported(code, ty)):
                 continue
             tname, opname = pkg.TYPES[ty], pkg.OPS[code]
             esz = pkg.type_size(ty)
@@ -975,6 +975,62 @@ def svc_stress(key, rank, size, dev):
     print(f"rank {rank} svc_stress OK", flush=True)
 
 
+def lazy_setup(key, rank, size, dev):
+    """smcuda's lazy rule (btl/smcuda/README:36-40): creating a communicator does no device work.
+    Five communicators are created after a barrier of an existing one (an MPI_Comm_dup of an
+    already-synchronised group): each is host-only until its first device-buffer collective
+    (DEV_SETUP 0; no device memory taken on the GPU, which every rank shares here), creation is
+    timed; then one allreduce on device buffers runs the device setup and is exact."""
+    import json
+    import time
+    import torch
+    torch.cuda.set_device(dev)
+    torch.zeros(1, device="cuda")  # this process's HIP context and allocator first
+    torch.cuda.synchronize()
+    pkg = load_pkg()
+    base = pkg.Comm.create(key + "b", rank, size, dev)
+    base.barrier()
+    free0 = torch.cuda.mem_get_info()[0]
+    base.barrier()
+    comms, wall = [], []
+    for rep in range(5):
+        base.barrier()
+        t0 = time.perf_counter()
+        c = pkg.Comm.create(f"{key}d{rep}", rank, size, dev)
+        wall.append((time.perf_counter() - t0) * 1e6)
+        comms.append(c)
+        assert c.get("DEV_SETUP") == 0, "device setup ran at creation"
+        c.barrier()  # host-only use
+        assert c.vote(0) == 0
+    base.barrier()
+    free1 = torch.cuda.mem_get_info()[0]
+    base.barrier()
+    assert free1 == free0, f"host-only communicators took {free0 - free1} bytes of device memory"
+    assert all(c.get("DEV_SETUP") == 0 for c in comms)
+    create_us = [c.get("CREATE_US") for c in comms]
+    # the first device-buffer collective runs the setup, collectively
+    c = comms[-1]
+    x = torch.full((4096,), float(rank + 1), device="cuda")
+    y = torch.empty_like(x)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    c.allreduce(x.data_ptr(), y.data_ptr(), 4096, pkg.T["FLOAT"], pkg.OP["SUM"])
+    first_ms = (time.perf_counter() - t0) * 1e3
+    assert bool(torch.all(y == size * (size + 1) / 2).item())
+    assert c.get("DEV_SETUP") == 1 and all(k.get("DEV_SETUP") == 0 for k in comms[:-1])
+    setup_us = c.get("SETUP_US")
+    for k in comms:
+        k.barrier()
+        k.destroy()
+    base.barrier()
+    base.destroy()
+    wall.sort()
+    print(json.dumps({"rank": rank, "n": size, "create_wall_us": [round(w, 1) for w in wall],
+                      "create_us_knob": create_us, "device_bytes_taken": free0 - free1,
+                      "first_device_call_ms": round(first_ms, 2), "device_setup_us": setup_us}), flush=True)
+    print(f"rank {rank} lazy OK", flush=True)
+
+
 def done_words(key, rank, size, dev):
     """MI355X_DONE_WORDS=1 (finish points by command-processor-written completion words, off by
     default: slower back to back on this platform, profiles/r03_small_latency.jsonl): every flow that
@@ -1180,6 +1236,8 @@ def _main():
         return token_check(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "done_words":
         return done_words(key, rank, size, dev)
+    if len(sys.argv) > 5 and sys.argv[5] == "lazy":
+        return lazy_setup(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "host_bw":
         return host_bw(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "svc":

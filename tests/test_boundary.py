@@ -282,6 +282,12 @@ def test_mca_variables_registered(monkeypatch):
         # the peer-mapping cache bounds (mpool_rgpusm_rcache_size_limit: bytes, unsigned long long)
         assert names["coll_mi355x_rcache_max_maps"] == 0
         assert ctypes.c_ulonglong.in_dll(m.coll, "mca_coll_mi355x_rcache_size_limit").value == 3 << 30
+        # the engine's crossovers (coll_tuned_component.c:115-170 style), with the engine's defaults
+        engine_vars = {"pipe_min_ranks": 4, "pipe_chunk_kib": 0, "pipe_wg_per_cu": 2, "pipe_wt": 1,
+                       "one_phase_max": 1 << 20, "svc_max": 32 << 10, "svc_pull_max": 128 << 10,
+                       "svc_copy_max": 1 << 20, "svc_idle_us": 1000, "svc_shrink_us": 100, "selftest": 1}
+        for name, dflt in engine_vars.items():
+            assert names.get("coll_mi355x_" + name) == dflt, (name, names.get("coll_mi355x_" + name))
         _coll_env(monkeypatch)
         comm = L.mini_comm_create(0, 4, 17)
         mod, p = _comm_query(m, comm)

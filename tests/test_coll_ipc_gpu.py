@@ -190,3 +190,18 @@ def test_vote_notices_dead_peer(gpu):
     out, _ = procs[0].communicate(timeout=120)
     procs[1].communicate(timeout=60)
     assert procs[0].returncode == 0 and "rank 0 vote_dead OK" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("size", [2, 8])
+def test_lazy_device_setup(gpu, size):
+    """smcuda's lazy rule (btl/smcuda/README:36-40): a communicator created after a barrier (an
+    MPI_Comm_dup of a synchronised group) does no device work -- DEV_SETUP stays 0 and the GPU's free
+    memory is unchanged while every rank holds five host-only communicators -- and the first
+    device-buffer allreduce runs the device setup collectively and is exact (ipc_worker.py::lazy_setup);
+    the per-rank creation times are printed"""
+    import json
+    outs = _run_mode(gpu, "lazy", size, timeout=200)
+    for out in outs:
+        row = json.loads(next(ln for ln in out.splitlines() if ln.startswith("{")))
+        print(json.dumps(row))
+        assert row["device_bytes_taken"] == 0

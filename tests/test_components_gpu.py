@@ -239,3 +239,11 @@ def test_declined_reductions_staged_through_host(gpu, size):
     other five pair types (flags as libmpi sets them) and MAX/MIN over MPI_LONG_DOUBLE served by the
     engine, exact vs the oracle"""
     _run_workers(size, "staging")
+
+
+def test_engine_crossovers_are_mca_variables(gpu):
+    """coll_mi355x_pipe_min_ranks / svc_max (and the other crossovers) registered as MCA variables
+    (coll_tuned_component.c:115-170 style) decide the engine's flows: pipe_min_ranks = 2 puts a
+    2-rank communicator's large allreduce on the pipelined flow, svc_max = 0 keeps small calls off the
+    resident service; the defaults do neither at 2 ranks; results exact (coll_worker.py::mca_vars_main)"""
+    _run_workers(2, "mca_vars")
