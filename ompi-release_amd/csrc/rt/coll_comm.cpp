@@ -154,6 +154,8 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
             else usleep(200);
         }
     }
+    c->ctrl->slot[rank].pid_start = proc_start_time(getpid());
+    c->ctrl->slot[rank].pid_ns = pid_namespace();
     c->ctrl->slot[rank].pid = (int32_t)getpid();
     c->ctrl->slot[rank].dev = device;
     uint64_t uid = 1469598103934665603ull;

@@ -32,6 +32,7 @@ extern std::map<int, SvcRes> g_svc_res;
 
 bool pid_alive(pid_t pid);
 bool peer_gone(mi355x_comm *c);
+uint64_t pid_namespace();
 int barrier(mi355x_comm *c);
 uint64_t buffer_id(const void *p);
 int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force);
@@ -54,7 +55,7 @@ int probe_dmabuf(mi355x_comm *c);
 bool evictable(const mi355x_comm *c, const PeerMap &m, const PeerMap *keep);
 void rcache_trim(mi355x_comm *c, const PeerMap *keep);
 size_t peer_map_count(const mi355x_comm *c);
-int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **entry);
+int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **entry, bool coll);
 int run_program(int op, int type, const Program &pr, const std::vector<void *> &in,
                        const std::vector<void *> &dst, size_t off, size_t len, hipStream_t s);
 int stage_peers(mi355x_comm *c, std::vector<void *> &sp);

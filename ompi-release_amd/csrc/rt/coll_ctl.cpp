@@ -75,13 +75,30 @@ bool pid_alive(pid_t pid)
 // the others spinning in an unbounded wait (the buffer-kind vote) or until timeout_s.  Waits check
 // every rank's published pid now and then; a rank whose process is gone aborts the communicator.
 // (Loopback ranks share this process.)
+// The pid is checked only where it means the same process: in this process's PID namespace (a
+// pid published from another namespace is trusted alive), and with the start time it had when
+// it was published (a pid the kernel gave to a new process is a dead peer).
+uint64_t pid_namespace()
+{
+    struct stat st;
+    return stat("/proc/self/ns/pid", &st) == 0 ? (uint64_t)st.st_ino : 0;
+}
+
 bool peer_gone(mi355x_comm *c)
 {
     if (c->loopback || c->size == 1) return false;
+    static const uint64_t my_ns = pid_namespace();
     for (int q = 0; q < c->size; ++q) {
-        const pid_t pid = (pid_t)c->ctrl->slot[q].pid;
+        const RankSlot &sl = c->ctrl->slot[q];
+        const pid_t pid = (pid_t)sl.pid;
         if (q == c->rank || pid <= 0) continue;
-        if (!pid_alive(pid)) {
+        if (sl.pid_ns && my_ns && sl.pid_ns != my_ns) continue;  // unverifiable here: alive
+        bool gone = !pid_alive(pid);
+        if (!gone && sl.pid_start) {
+            const uint64_t now = proc_start_time(pid);
+            gone = now != 0 && now != sl.pid_start;  // (0: unreadable -- alive)
+        }
+        if (gone) {
             c->ctrl->abort_flag.store(1);
             set_error(MI355X_ERR_PEER, "rank %d (pid %d) is gone: the communicator is aborted", q, (int)pid);
             return true;

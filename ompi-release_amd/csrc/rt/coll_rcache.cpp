@@ -45,14 +45,16 @@ namespace mi355x {
 // Bounded peer-mapping cache (mpool/rgpusm's rcache_size_limit with LRU eviction,
 // mpool_rgpusm_component.c:92-100, mpool_rgpusm_module.c:104-120,396-419): when the hipIpc mappings
 // of peers' allocations exceed rcache_max_maps (count) or rcache_limit (bytes), the least recently
-// used ones that the current call does not use, that no point-to-point read has pinned and that
-// are not the communicator's own regions are closed.  A mapping keeps the exporter's allocation
+// used ones that the current collective does not use, that no point-to-point read has pinned and
+// that are not the communicator's own regions are closed.  Recency is a clock every use ticks --
+// collective or point-to-point -- so the bounds hold in phases of point-to-point traffic alone
+// (a mapping a point-to-point read made is evictable once the read has finished and unpinned it).  A mapping keeps the exporter's allocation
 // alive on ROCm, so a long job that churns allocations would otherwise hold every freed block of
 // every peer.  Both limits default to 0 = unlimited, as in the reference.  dmabuf imports (>= 2 GiB
 // allocations) are not evicted: their fd reaches a peer once.
 bool evictable(const mi355x_comm *c, const PeerMap &m, const PeerMap *keep)
 {
-    return &m != keep && !m.persistent && m.pins == 0 && !m.ext && m.last_use != c->seq;
+    return &m != keep && !m.persistent && m.pins == 0 && !m.ext && m.coll_use != c->seq;
 }
 
 void rcache_trim(mi355x_comm *c, const PeerMap *keep)
@@ -85,7 +87,7 @@ size_t peer_map_count(const mi355x_comm *c)
     return n;
 }
 
-int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **entry)
+int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **entry, bool coll)
 {
     std::lock_guard<std::recursive_mutex> reg_guard(c->reg_mtx);
     *out = nullptr;
@@ -110,12 +112,13 @@ int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **e
         hipExternalMemory_t ext = nullptr;
         int rc = import_dmabuf(c, peer, d.id, d.size, &mapped, &ext);
         if (rc) return rc;
-        it = c->peer_maps.emplace(key, PeerMap{d.id, mapped, c->seq, ext}).first;
+        it = c->peer_maps.emplace(key, PeerMap{d.id, mapped, ++c->use_clock, ext}).first;
     }
     void *base;
     if (it != c->peer_maps.end()) {
         base = it->second.mapped;
-        it->second.last_use = c->seq;
+        it->second.last_use = ++c->use_clock;
+        if (coll) it->second.coll_use = c->seq;
     } else {
         TRACE(c, "open peer %d base %llx id %llu", peer, (unsigned long long)d.base, (unsigned long long)d.id);
         hipError_t e = hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess);
@@ -128,7 +131,7 @@ int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **e
             (void)hipGetLastError();
             int dropped = 0;
             for (auto m = c->peer_maps.begin(); m != c->peer_maps.end();) {
-                if (m->first.peer == peer && m->second.last_use != c->seq && m->second.pins == 0 &&
+                if (m->first.peer == peer && m->second.coll_use != c->seq && m->second.pins == 0 &&
                     !m->second.persistent) {
                     close_map(m->second);
                     m = c->peer_maps.erase(m);
@@ -142,8 +145,9 @@ int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **e
             if (e != hipSuccess)
                 return set_error(MI355X_ERR_PEER, "hipIpcOpenMemHandle(rank %d): %s", peer, hipGetErrorString(e));
         }
-        it = c->peer_maps.emplace(key, PeerMap{d.id, base, c->seq, nullptr}).first;
+        it = c->peer_maps.emplace(key, PeerMap{d.id, base, ++c->use_clock, nullptr}).first;
         it->second.bytes = d.size;
+        if (coll) it->second.coll_use = c->seq;
         rcache_trim(c, &it->second);
     }
     if (entry) *entry = &it->second;

@@ -76,6 +76,13 @@ uint32_t st_val(uint64_t seed, int q, size_t i)
     return (uint32_t)(x & 0xffffff);  // (sums of <= 64 ranks stay below 2^31)
 }
 
+// restores the communicator's last_algorithm when a self-test that ran collectives of its own returns
+struct LastAlgKeeper {
+    mi355x_comm *c;
+    int alg;
+    ~LastAlgKeeper() { c->last_alg = alg; }
+};
+
 // device buffers of the self-test: my input (n x count int32 for the reduce_scatter block), output
 struct SelfTest {
     mi355x_comm *c;
@@ -140,6 +147,7 @@ namespace mi355x {
 // The service's flows, at its first claim (the service is claimed on every rank; collective).
 int svc_selftest(mi355x_comm *c)
 {
+    LastAlgKeeper keep_alg{c, c->last_alg};  // (the test's own calls must not show in last_algorithm)
     c->svc_flows_tested = true;
     const unsigned tested = MI355X_FLOW_SVC_LL | MI355X_FLOW_SVC_PULL | MI355X_FLOW_SVC_COPY | MI355X_FLOW_SVC_RS;
     if (!selftest_on(c)) return MI355X_SUCCESS;
@@ -247,6 +255,7 @@ int svc_selftest(mi355x_comm *c)
 // allreduce of 128 KiB blocks in 16 KiB chunks (8 per block), forced onto the pipelined flow.
 int pipe_selftest(mi355x_comm *c)
 {
+    LastAlgKeeper keep_alg{c, c->last_alg};  // (the test's own calls must not show in last_algorithm)
     if (!selftest_on(c)) return MI355X_SUCCESS;
     const auto t0 = std::chrono::steady_clock::now();
     const int n = c->size;

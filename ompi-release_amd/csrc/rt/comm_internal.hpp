@@ -69,6 +69,8 @@ struct alignas(64) RankSlot {
     int32_t svc_claim, svc_ok;    // resident LL service at creation: this process's service is mine
                                   // (1) or taken (2); its self-test passed (1) or failed (2)
     uint64_t dev_uid;             // hash of the device's PCI bus id: ranks sharing one GPU
+    uint64_t pid_start;           // the process's start time (/proc/<pid>/stat field 22): a recycled pid differs
+    uint64_t pid_ns;              // inode of its PID namespace: a pid from another namespace is not checked
     // mi355x_comm_vote: call v's entry at [v % kVoteRing] = (v << 1) | (this rank's buffers are
     // device memory); a ring because a rank with device buffers publishes and moves on
     std::atomic<uint64_t> vote[kVoteRing];
@@ -162,8 +164,9 @@ struct HandleKey {
 struct PeerMap {
     uint64_t id;
     void *mapped;
-    uint64_t last_use;             // call (seq) that last used the mapping
+    uint64_t last_use;             // LRU stamp (use_clock) of the last collective or point-to-point use
     hipExternalMemory_t ext;       // dmabuf import (NULL: hipIpcOpenMemHandle mapping)
+    uint64_t coll_use = ~0ull;     // collective (seq) that last used it (~0: point-to-point only)
     int pins = 0;                  // in-flight point-to-point reads: never closed meanwhile
     bool persistent = false;       // a region the engine keeps mapped for the communicator's
                                    // life (LL and pipeline flag regions): never dropped
@@ -243,6 +246,7 @@ struct mi355x_request {
     const void *dual_src = nullptr;       // send (kEnvDual): the caller's device bytes
     uint64_t hoff = 0;                    // send (kEnvDual): the host copy's arena offset and generation
     uint32_t hgen = 0;
+    mi355x::BufDesc hdesc{};              // send (kEnvDual): the host copy's slot as a host-arena send names it
     void *stage = nullptr;                // receive: device staging slot (host destination)
     std::vector<char> htmp;               // receive: host copy awaiting the host convertor
     unsigned char inl[mi355x::kP2PInline]; // send: an inline payload until its envelope is posted
@@ -350,6 +354,7 @@ struct mi355x_comm {
     uint64_t gate_calls = 0;                      // gated calls completed (RankSlot::calls)
     size_t ll_bytes = 0;                          // LL region size (ll_resync)
     double create_us = 0, selftest_us = 0;
+    uint64_t use_clock = 0;                       // LRU clock of the peer-mapping cache (every use ticks it)
     // device-side setup (done words, LL region + self-test, the service's resources, the pipelined
     // flow's self-test), deferred from creation to the first device-buffer collective (dev_setup)
     bool dev_ready = false;
@@ -423,7 +428,7 @@ int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force);
 // export the large allocation of `d` as a dmabuf fd and pass it to every rank in `peers` that
 // has not received it yet
 int export_dmabuf(mi355x_comm *c, BufDesc *d, uint64_t peers);
-int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **entry = nullptr);
+int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **entry = nullptr, bool coll = true);
 size_t peer_map_count(const mi355x_comm *c);  // evictable-kind peer mappings currently open
 // publish nbuf buffers, meet every rank, map every rank's buffers: peers[b][r] (coll_comm.cpp)
 // persistent: the mappings stay for the communicator's life (never dropped to make room)

@@ -135,6 +135,9 @@ struct P2P {
     std::deque<mi355x_request *> queued;   // sends waiting for a free envelope, posting order
     std::vector<mi355x_request *> sending; // announced, waiting for the receiver's FIN
     std::vector<mi355x_request *> reading; // matched receives whose pull is in flight
+    // matched receives of a dual message whose device buffer could not be mapped here: they wait
+    // for the sender's host copy (claim 1) instead of claiming the pull
+    std::vector<std::pair<mi355x_request *, P2PMsg>> dual_wait;
     DevArena arena;                        // exportable: packed / buffered device payloads
     DevArena rstage;                       // receive side: device staging of host receives
     HostArena harena;                      // host payloads (shared memory)
@@ -472,11 +475,22 @@ static void start_read(mi355x_comm *c, P2P *p, mi355x_request *r, const P2PMsg &
     hipStream_t s = nullptr;
     int rc = MI355X_SUCCESS;
     // a small device payload offered two ways: pull it from the device buffer unless the sender's
-    // host copy was taken first (claim 1)
+    // host copy was taken first (claim 1).  The device pull is claimed only once the sender's buffer
+    // is mapped here: if the mapping fails (an allocation a peer freed and reused can make hipIpc
+    // refuse it) the receive waits for the host copy, which the sender takes when nobody claims.
     bool dual_host = false;
     if (env->flags & kEnvDual) {
+        dual_host = env->claim.load(std::memory_order_acquire) == claim_word(msg.m, 1);
+        if (!dual_host && msg.src != c->rank && !c->loopback) {
+            void *mapped = nullptr;
+            if (map_peer(c, msg.src, env->buf, &mapped, nullptr, false) != MI355X_SUCCESS) {
+                (void)hipGetLastError();
+                p->dual_wait.emplace_back(r, msg);
+                return;
+            }
+        }
         uint64_t z = claim_word(msg.m, 0);
-        dual_host = !env->claim.compare_exchange_strong(z, claim_word(msg.m, 2), std::memory_order_acq_rel);
+        if (!dual_host) dual_host = !env->claim.compare_exchange_strong(z, claim_word(msg.m, 2), std::memory_order_acq_rel);
     }
     BufDesc hdesc = env->buf;
     if (dual_host) {
@@ -567,7 +581,7 @@ static void start_read(mi355x_comm *c, P2P *p, mi355x_request *r, const P2PMsg &
     } else {
         void *mapped = nullptr;
         PeerMap *pm = nullptr;
-        rc = map_peer(c, msg.src, env->buf, &mapped, &pm);
+        rc = map_peer(c, msg.src, env->buf, &mapped, &pm, false);
         if (rc) return fail(rc);
         if (pm) {
             pm->pins++;
@@ -721,7 +735,17 @@ int p2p_progress(mi355x_comm *c)
             ++it;
         }
     }
-    // 2. new envelopes, 3. match posted receives in posting order against the arrivals
+    // 2. new envelopes, 3. match posted receives in posting order against the arrivals (first the
+    //    matched dual receives whose host copy has come)
+    for (size_t i = 0; i < p->dual_wait.size();) {
+        const auto w = p->dual_wait[i];
+        if (w.second.env->claim.load(std::memory_order_acquire) != claim_word(w.second.m, 1)) {
+            ++i;
+            continue;
+        }
+        p->dual_wait.erase(p->dual_wait.begin() + (ptrdiff_t)i);
+        start_read(c, p, w.first, w.second);
+    }
     drain_mailboxes(c, p);
     for (auto it = p->posted.begin(); it != p->posted.end();) {
         mi355x_request *r = *it;
@@ -827,6 +851,22 @@ static mi355x_request *new_request(mi355x_comm *c, int kind)
     return r;
 }
 
+// (kEnvDual, not announced yet) turn r into a plain host-arena send: the copy into its slot now
+static int dual_to_host(mi355x_comm *c, P2P *p, mi355x_request *r)
+{
+    int rc = dual_copy_launch(c, p, r);
+    if (rc == MI355X_SUCCESS && hipEventSynchronize(r->ev) != hipSuccess)
+        rc = set_error(MI355X_ERR_HIP, "device-to-host copy of a small send failed");
+    if (r->ev) {
+        p->evpool.push_back(r->ev);
+        r->ev = nullptr;
+    }
+    if (rc) return rc;
+    r->env_flags = kEnvHost;
+    std::memcpy(&r->desc, &r->hdesc, sizeof(r->desc));
+    return MI355X_SUCCESS;
+}
+
 // announce r (queue it behind an earlier send to the same destination); the caller's request is
 // r, or -- eager -- a completed twin while the engine keeps r until the FIN
 static mi355x_request *post_send(mi355x_comm *c, P2P *p, mi355x_request *r, bool eager, bool dual = false)
@@ -845,8 +885,18 @@ static mi355x_request *post_send(mi355x_comm *c, P2P *p, mi355x_request *r, bool
     }
     bool earlier = false;   // an earlier send to the same destination still queued: keep order
     for (mi355x_request *q : p->queued) earlier = earlier || q->peer == r->peer;
-    if (!earlier && try_announce(c, r)) p->sending.push_back(r);
-    else p->queued.push_back(r);
+    if (!earlier && try_announce(c, r)) {
+        p->sending.push_back(r);
+        return user;
+    }
+    if (dual && dual_to_host(c, p, r) == MI355X_SUCCESS) {
+        // no envelope free for it now: it cannot be offered two ways, so it takes the host form at
+        // once and its caller completes (eager), as every small send must even when the peer's
+        // ring is full
+        complete(user, MI355X_SUCCESS);
+        r->twin = nullptr;
+    }
+    p->queued.push_back(r);
     return user;
 }
 
@@ -960,7 +1010,9 @@ static int isend(mi355x_comm *c, const void *buf, size_t count, const mi355x_ddt
     // within MI355X_P2P_DUAL_DELAY_US (10 us) of the announcement (p2p_progress), so a waiting
     // receiver's pull never competes with it.  MI355X_P2P_DUAL=0 keeps the host-arena-only form.
     static const bool dual_on = !(getenv("MI355X_P2P_DUAL") && atoi(getenv("MI355X_P2P_DUAL")) == 0);
-    if (dual_on && dev && small && contig && bytes && dest != c->rank && !c->loopback && p->harena.cur.dbase != nullptr) {
+    // (MPI_Bsend is local: it keeps the eager host form, never waiting on a receiver's claim)
+    if (dual_on && dev && small && contig && bytes && mode != MI355X_SEND_BUFFERED && dest != c->rank && !c->loopback &&
+        p->harena.cur.dbase != nullptr) {
         BufDesc hd;
         void *slot = nullptr;
         if ((rc = local_handle(c, ubuf, &desc, false))) return bail(rc);
@@ -974,6 +1026,7 @@ static int isend(mi355x_comm *c, const void *buf, size_t count, const mi355x_ddt
             r->env_flags = kEnvDual;
             r->hoff = hd.off;
             r->hgen = (uint32_t)hd.id;
+            std::memcpy(&r->hdesc, &hd, sizeof(hd));
             std::memcpy(&r->desc, &desc, sizeof(desc));
             *out = post_send(c, p, r, false, true);
             return MI355X_SUCCESS;

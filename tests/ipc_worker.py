@@ -565,6 +565,26 @@ def p2p_checks(pkg, comm, rank, size, oracle, torch):
     for r in sreqs:
         r.wait()
     assert np.array_equal(dst.cpu().numpy(), pattern(prv, 64 * k, 99)), "queued messages"
+    # more small DEVICE sends in flight than the 32 envelopes of a pair, none received yet: every
+    # send (standard small = eager, and MPI_Bsend) must complete locally -- a send that finds the
+    # ring full takes the host copy at once instead of waiting for a receiver's claim -- and the
+    # receiver gets them all, in order, only after every send has completed
+    k2 = 48
+    src2 = [torch.from_numpy(pattern(rank, 1024, 600 + i)).cuda() for i in range(k2)]
+    torch.cuda.synchronize()
+    sreqs = [comm.isend(src2[i].data_ptr(), 1024, nxt, 700 + i, mode="BUFFERED" if i % 5 == 4 else None)
+             for i in range(k2)]
+    for r in sreqs:
+        r.wait()      # before any receive is posted anywhere (the barrier below)
+    for i in range(k2):
+        src2[i].fill_(0)   # the caller may reuse an eager send's buffer
+    comm.barrier()
+    dst2 = torch.zeros(k2 * 1024, dtype=torch.uint8, device="cuda")
+    for i in range(k2):
+        st = comm.recv(dst2[i * 1024:(i + 1) * 1024].data_ptr(), 1024, prv, pkg.ANY_TAG)
+        assert st[1] == 700 + i, ("order of eager device sends", i, st)
+    for i in range(k2):
+        assert np.array_equal(dst2[i * 1024:(i + 1) * 1024].cpu().numpy(), pattern(prv, 1024, 600 + i)), ("eager", i)
     # MPI_Type_vector(stride 2, block 64) floats: packed by the sender, received contiguous
     nvec = 1000
     od = oracle.oracle_ddt_vector(nvec, 64, 128, 4)

@@ -22,6 +22,8 @@
 #   queue_probe    what a resident kernel costs HIP launch-to-completion   -> queue_probe.jsonl
 #   unpack_ceiling tools/build/unpack_ceiling (convertor unpack ceiling)   -> unpack_ceiling.jsonl
 #   host_p2p       host -> host point-to-point rates between two processes -> host_p2p.log
+#   op_overhead    what op/hip adds to host-buffer reductions (tools/build/op_host_overhead) -> op_overhead.jsonl
+#                  and an 8 B host-buffer allreduce with / without the components (small_ar_c host_mini)
 #   p2p_lat        point-to-point ping-pong latency, host and device buffers, 8 B - 64 KiB -> p2p_lat.jsonl
 #   interference   the resident service beside compute streams (tools/svc_interference.py) -> svc_interference.jsonl
 #   ab_host        host-synchronised small-call latency, this tree vs a build staged in ab_old/ (A/B)
@@ -87,6 +89,9 @@ for step in "$@"; do
     tests)
         run pytest_sel 1000 $PYT -rP ${TESTS:-tests} ${K:+-k "$K"}
         grep -E "PASSED|FAILED|SKIPPED|ERROR|passed|failed" $O/pytest_sel.log | tail -40 ;;
+    op_overhead)
+        run op_overhead 120 ./tools/build/op_host_overhead
+        grep '^{' $O/op_overhead.log | tee $O/op_overhead.jsonl ;;
     smoke)
         run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
         tail -2 $O/smoke.log ;;
