@@ -6,6 +6,8 @@
 
 #include <map>
 #include <mutex>
+#include <sys/socket.h>
+#include <sys/un.h>
 
 #include "comm_internal.hpp"
 
@@ -105,6 +107,9 @@ int svc_claim(mi355x_comm *c);
 int svc_maybe_claim(mi355x_comm *c, bool sized);
 void svc_setup(mi355x_comm *c);
 int dev_setup(mi355x_comm *c);
+bool coll_slot_supported(int op, int type);  // coll_kernels.hip: the fold families carry (op, type)
+int gather_fold(mi355x_comm *c, const void *in, size_t count, int type, int op, size_t e0, size_t ne, int chain,
+                void *dst, hipStream_t s);
 hipStream_t setup_stream(mi355x_comm *c);
 int ensure_pipe(mi355x_comm *c);
 int pipe_allreduce(mi355x_comm *c, int op, int type, const Program &pr,

@@ -118,8 +118,8 @@ bool allreduce_tree_program(mi355x_comm *c, int alg, size_t count, size_t esz, P
 int check_common(mi355x_comm *c, int op, int type)
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
-    if (!mi355x_comm_op_supported(op, type))
-        return set_error(MI355X_ERR_UNSUPPORTED, "no engine fold for op %d type %d", op, type);
+    if (!mi355x_op_supported(op, type))
+        return set_error(MI355X_ERR_UNSUPPORTED, "no GPU kernel for op %d type %d", op, type);
     return MI355X_SUCCESS;
 }
 

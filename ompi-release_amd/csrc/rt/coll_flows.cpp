@@ -50,6 +50,10 @@ int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count,
     if (count == 0) return MI355X_SUCCESS;
     if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     hipStream_t s = resolve_stream(stream);
+    if (!coll_slot_supported(op, type)) {  // (no fold kernel carries the slot: gather-then-fold, coll_gfold.cpp)
+        c->last_alg = 1;
+        return gather_fold(c, sbuf ? sbuf : rbuf, count, type, op, 0, count, -1, rbuf, s);
+    }
     const size_t esz = mi355x_type_size(type);
     const void *in = sbuf ? sbuf : rbuf;
     if (c->size == 1) {
@@ -271,6 +275,10 @@ int reduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, in
     if (count == 0) return MI355X_SUCCESS;
     if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     hipStream_t s = resolve_stream(stream);
+    if (!coll_slot_supported(op, type)) {  // (no fold kernel carries the slot: gather-then-fold, coll_gfold.cpp)
+        c->last_alg = 1;
+        return gather_fold(c, sbuf ? sbuf : rbuf, count, type, op, 0, count, -1, c->rank == root ? rbuf : nullptr, s);
+    }
     const size_t esz = mi355x_type_size(type);
     const void *in = sbuf ? sbuf : rbuf;
     const bool am_root = (c->rank == root);
@@ -367,6 +375,10 @@ int reduce_scatter_block_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, si
     if (count == 0) return MI355X_SUCCESS;
     if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     hipStream_t s = resolve_stream(stream);
+    if (!coll_slot_supported(op, type)) {  // (no fold kernel carries the slot: gather-then-fold, coll_gfold.cpp)
+        c->last_alg = 1;
+        return gather_fold(c, sbuf ? sbuf : rbuf, count, type, op, (size_t)c->rank * rcount, rcount, -1, rbuf, s);
+    }
     const size_t esz = mi355x_type_size(type);
     const void *in = sbuf ? sbuf : rbuf;
     Program pr;
@@ -433,6 +445,10 @@ int reduce_scatter_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, const in
     if (count == 0) return MI355X_SUCCESS;
     if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     hipStream_t s = resolve_stream(stream);
+    if (!coll_slot_supported(op, type)) {  // (no fold kernel carries the slot: gather-then-fold, coll_gfold.cpp)
+        c->last_alg = 1;
+        return gather_fold(c, sbuf ? sbuf : rbuf, count, type, op, disp[c->rank], (size_t)rcounts[c->rank], -1, rbuf, s);
+    }
     const size_t esz = mi355x_type_size(type);
     const void *in = sbuf ? sbuf : rbuf;
     const int alg = pick_reduce_scatter(c, count, esz);

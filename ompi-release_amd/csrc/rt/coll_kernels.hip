@@ -460,5 +460,5 @@ bool coll_slot_supported(int op, int type) { return cslot(op, type) != nullptr; 
 
 } // namespace mi355x
 
-// every kernel family of the engine instantiates the same slot list (slot_list.hpp)
-extern "C" int mi355x_comm_op_supported(int op, int type) { return mi355x::coll_slot_supported(op, type) ? 1 : 0; }
+// every op/hip slot: the fold families' (slot_list.hpp) directly, the others gather-then-fold (coll_gfold.cpp)
+extern "C" int mi355x_comm_op_supported(int op, int type) { return mi355x_op_supported(op, type); }

@@ -354,6 +354,8 @@ struct mi355x_comm {
     uint64_t gate_calls = 0;                      // gated calls completed (RankSlot::calls)
     size_t ll_bytes = 0;                          // LL region size (ll_resync)
     double create_us = 0, selftest_us = 0;
+    void *gf_buf = nullptr;                       // gather-then-fold slots (coll_gfold.cpp): every rank's input
+    size_t gf_bytes = 0;
     uint64_t use_clock = 0;                       // LRU clock of the peer-mapping cache (every use ticks it)
     // device-side setup (done words, LL region + self-test, the service's resources, the pipelined
     // flow's self-test), deferred from creation to the first device-buffer collective (dev_setup)

@@ -774,8 +774,9 @@ def staging_main():
       * a non-commutative user MPI_Op (a op b = 3a + b on MPI_INT) on device buffers, rank 0 on host
         buffers: allreduce (also in place), reduce, reduce_scatter_block, reduce_scatter, scan, exscan,
         iallreduce, ireduce, ireduce_scatter_block;
-      * MPI_SUM / MPI_PROD over MPI_LONG_DOUBLE and MAXLOC / MINLOC over MPI_LONG_DOUBLE_INT (no
-        engine fold: 80-bit arithmetic / 32-byte pairs) on device buffers;
+      * MPI_SUM / MPI_PROD over MPI_LONG_DOUBLE (no 80-bit arithmetic on the GPU) on device buffers;
+      * MAXLOC / MINLOC over MPI_LONG_DOUBLE_INT served by the engine's gather-then-fold form
+        (allreduce, reduce, reduce_scatter_block, scan; coll/basic's orders), nothing staged;
       * MAXLOC / MINLOC over the other five pair types (built as libmpi builds them: OPAL-predefined
         flag cleared, DOUBLE_INT 12 bytes in 16) and MAX / MIN over MPI_LONG_DOUBLE on device
         buffers are served by the engine, bit-exact with the oracle, with nothing staged;
@@ -893,10 +894,9 @@ def staging_main():
     L.mini_op_destroy(uop)
 
     say("user op done")
-    # ---- 2. x87 slots with no engine fold: SUM / PROD over LONG_DOUBLE, MAXLOC / MINLOC over
-    #         LONG_DOUBLE_INT -- device buffers staged to the host module (coll/basic's linear order)
-    for opname, tname in (("SUM", "LONG_DOUBLE"), ("PROD", "LONG_DOUBLE"), ("MAXLOC", "LONG_DOUBLE_INT"),
-                          ("MINLOC", "LONG_DOUBLE_INT")):
+    # ---- 2. x87 arithmetic slots (no 80-bit arithmetic on the GPU): SUM / PROD over LONG_DOUBLE --
+    #         device buffers staged to the host module (coll/basic's linear order)
+    for opname, tname in (("SUM", "LONG_DOUBLE"), ("PROD", "LONG_DOUBLE")):
         code, slot = pkg.OP[opname], pkg.T[tname]
         assert not pkg.rt().mi355x_comm_op_supported(code, slot)
         op = m.select_op(code)
@@ -912,7 +912,43 @@ def staging_main():
         opdata.assert_same(tname, opname, oread2(), want, "staged x87 allreduce")
         assert staged.value == before + 1, "the x87 call was not staged"
         L.mini_op_destroy(op)
-
+    # MAXLOC / MINLOC over MPI_LONG_DOUBLE_INT (32-byte pairs): served by the engine's gather-then-
+    # fold form (coll/basic's orders on the GPU) -- allreduce, reduce, reduce_scatter_block, scan
+    for opname in ("MAXLOC", "MINLOC"):
+        tname = "LONG_DOUBLE_INT"
+        code, slot = pkg.OP[opname], pkg.T[tname]
+        assert pkg.rt().mi355x_comm_op_supported(code, slot)
+        op = m.select_op(code)
+        dt = m.dtype_for_slot(slot)
+        n, rc_ = 20_001, 3001
+        xs2 = [opdata.make(tname, n, 40 + r) for r in range(size)]
+        want = _linear(oracle, code, slot, xs2)
+        before = staged.value
+        d, dp, read = put(xs2[rank])
+        o, opp, oread2 = put(np.zeros_like(xs2[0]))
+        torch.cuda.synchronize()
+        assert L.mini_allreduce(comm, dp, opp, n, dt, op) == 0
+        opdata.assert_same(tname, opname, oread2(), want, "engine LDI allreduce")
+        o3, opp3, oread3 = put(np.zeros_like(xs2[0]))
+        torch.cuda.synchronize()
+        assert L.mini_reduce(comm, dp, opp3 if rank == 0 else None, n, dt, op, 0) == 0
+        if rank == 0:
+            opdata.assert_same(tname, opname, oread3(), want, "engine LDI reduce")
+        ys2 = [opdata.make(tname, rc_ * size, 70 + r) for r in range(size)]
+        ywant = _linear(oracle, code, slot, ys2)
+        yd, ydp, _ = put(ys2[rank])
+        yo, yop, yread = put(np.zeros(rc_, dtype=ys2[0].dtype))
+        torch.cuda.synchronize()
+        assert L.mini_reduce_scatter_block(comm, ydp, yop, rc_, dt, op) == 0
+        opdata.assert_same(tname, opname, yread(), ywant[rank * rc_:(rank + 1) * rc_], "engine LDI rsb")
+        swant = [np.zeros_like(xs2[0]) for _ in range(size)]
+        oracle.oracle_scan(0, size, n, slot, code, ptrs(xs2), ptrs(swant))
+        so, sop, sread = put(np.zeros_like(xs2[0]))
+        torch.cuda.synchronize()
+        assert L.mini_scan(comm, dp, sop, n, dt, op) == 0
+        opdata.assert_same(tname, opname, sread(), swant[rank], "engine LDI scan")
+        assert staged.value == before, "MPI_LONG_DOUBLE_INT was staged, not served by the engine"
+        L.mini_op_destroy(op)
     say("staged x87 done")
     # ---- 3. engine-served: MAXLOC / MINLOC over the five other pair types, MAX / MIN over LONG_DOUBLE
     for opname in ("MAXLOC", "MINLOC"):

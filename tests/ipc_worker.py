@@ -294,7 +294,7 @@ def svc_all_slots(pkg, comm, rank, size, oracle, torch):
     k = ncalls = 0
     for code in range(1, 13):
         for ty in range(len(pkg.TYPES)):
-            if not (oracle.oracle_has_op(code, ty) and pkg.comm_op_supported(code, ty)):
+            if not (oracle.oracle_has_op(code, ty) and pkg.comm_op_supported(code, ty) and pkg.type_size(ty) <= 16):
                 continue
             tname, opname = pkg.TYPES[ty], pkg.OPS[code]
             esz = pkg.type_size(ty)
@@ -475,7 +475,7 @@ def pipe_all_slots(pkg, comm, rank, size, oracle, torch):
     k = 0
     for code in range(1, 13):
         for ty in range(len(pkg.TYPES)):
-            if not (oracle.oracle_has_op(code, ty) and pkg.comm_op_supported(code, ty)):
+            if not (oracle.oracle_has_op(code, ty) and pkg.comm_op_supported(code, ty) and pkg.type_size(ty) <= 16):
                 continue
             tname, opname = pkg.TYPES[ty], pkg.OPS[code]
             esz = pkg.type_size(ty)
