@@ -326,7 +326,7 @@ int mi355x_comm_vote(mi355x_comm_t *c, int device, int *any_device)
                 return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
             if (++spins > 2048) {
                 if ((spins & 63) == 0) {
-                    if (c->p2p) (void)p2p_progress(c);
+                    p2p_progress_all();
                     if (g_progress_hook) g_progress_hook();
                 }
                 if ((spins & 0xffff) == 0 && peer_gone(c)) return MI355X_ERR_PEER;

@@ -125,6 +125,7 @@ int barrier(mi355x_comm *c)
             return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
         if (++spins > 2048) {
             sched_yield();
+            if ((spins & 63) == 0) p2p_progress_all();  // queued eager sends a peer may be waiting for
             // a peer may be blocked sending us dmabuf fds (full socket queue): drain it while we wait
             if (c->fd_sock >= 0 && (spins & 255) == 0 && c->reg_mtx.try_lock()) {
                 (void)fd_drain(c, false);

@@ -462,5 +462,6 @@ struct CallGate {
     CallGate &operator=(const CallGate &) = delete;
 };
 int p2p_progress(mi355x_comm *c);
+void p2p_progress_all();  // every communicator's point-to-point (the engine's host-side waits)
 int p2p_wait(mi355x_request *r);
 } // namespace mi355x

@@ -148,6 +148,13 @@ struct P2P {
 
 static void seg_drop(HostSeg &g, bool owner);
 
+// Every communicator with point-to-point state, so that any of the engine's host-side waits can
+// progress all of them -- as ob1's waits run opal_progress over every pending request: an eager
+// send that found its peer's ring full completed for its caller but is announced only by a later
+// progress pass, and its receiver may be what the waiting rank is waiting for.
+static std::mutex g_p2p_mtx;
+static std::vector<mi355x_comm *> g_p2p_comms;
+
 static P2P *p2p_of(mi355x_comm *c)
 {
     if (!c->p2p) {
@@ -155,8 +162,17 @@ static P2P *p2p_of(mi355x_comm *c)
         p->send_seq.assign((size_t)c->size, 0);
         p->recv_seq.assign((size_t)c->size, 0);
         c->p2p = p;
+        std::lock_guard<std::mutex> g(g_p2p_mtx);
+        g_p2p_comms.push_back(c);
     }
     return c->p2p;
+}
+
+void p2p_progress_all()
+{
+    std::unique_lock<std::mutex> g(g_p2p_mtx, std::try_to_lock);  // (another thread progresses them now)
+    if (!g.owns_lock()) return;
+    for (mi355x_comm *c : g_p2p_comms) (void)p2p_progress(c);
 }
 
 static int p2p_stream(mi355x_comm *c, P2P *p, hipStream_t *s)
@@ -173,6 +189,10 @@ void p2p_destroy(mi355x_comm *c)
 {
     P2P *p = c->p2p;
     if (!p) return;
+    {
+        std::lock_guard<std::mutex> g(g_p2p_mtx);  // (waits out a progress pass over it)
+        g_p2p_comms.erase(std::remove(g_p2p_comms.begin(), g_p2p_comms.end(), c), g_p2p_comms.end());
+    }
     if (p->stream) {
         (void)hipStreamSynchronize(p->stream);
         (void)hipStreamDestroy(p->stream);
@@ -1174,6 +1194,7 @@ int p2p_wait(mi355x_request *r)
         p2p_progress(c);
         if (r->done.load(std::memory_order_acquire)) break;
         if (++spins > 64) {
+            if ((spins & 63) == 0) p2p_progress_all();  // (the other communicators' queued sends)
             sched_yield();
             if ((spins & 0x3ff) == 0 &&
                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s)

@@ -8,7 +8,7 @@
  *              restated here: inout[i] = inout[i] + in[i])
  *   table      ompi_op_reduce through an op selected WITHOUT op/hip (the reference's dispatch)
  *   op_hip     ompi_op_reduce through an op selected WITH op/hip (mca_op_hip_2buff in the slot)
- *   ptr_query  mi355x_ptr_is_device on a host pointer, alone
+ *   ptr_query  mi355x_ptr_is_device on the same host pointer, alone
  * at count 1, 16, 1 Ki and 64 Ki floats; one JSON line per (variant, count), nanoseconds per call
  * (median of 7 timed batches).  Needs the HIP runtime (the pointer query), so it runs on the GPU box.
  * build: make -C tools (links libompi_mini + libmi355x_rt; dlopens mca_op_hip.so) */
@@ -81,9 +81,11 @@ int main(int argc, char **argv)
     }
     ompi_datatype_t *dt = mini_datatype(mini_datatype_id_for_slot(MI355X_T_FLOAT));
     const int counts[] = {1, 16, 1024, 65536};
-    float *a = calloc(65536, sizeof(float)), *b = calloc(65536, sizeof(float));
     for (int ci = 0; ci < 4; ++ci) {
         const int n = counts[ci];
+        /* the buffers a host reduction of this size gets from malloc: the brk heap below glibc's mmap
+         * threshold (128 KiB), an anonymous mapping above it */
+        float *a = calloc((size_t)n, sizeof(float)), *b = calloc((size_t)n, sizeof(float));
         const long reps = n <= 16 ? 200000 : n <= 1024 ? 50000 : 2000;
         double med[4];
         for (int v = 0; v < 4; ++v) {
@@ -110,6 +112,8 @@ int main(int argc, char **argv)
                    v == V_OPHIP ? "" : "");
         printf("{\"count\": %d, \"op_hip_over_table_ns\": %.1f, \"op_hip_over_table_frac\": %.4f}\n", n,
                med[V_OPHIP] - med[V_TABLE], (med[V_OPHIP] - med[V_TABLE]) / med[V_TABLE]);
+        free(a);
+        free(b);
     }
     fflush(stdout);
     mini_op_destroy(plain);
