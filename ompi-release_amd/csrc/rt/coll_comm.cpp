@@ -370,6 +370,14 @@ int mi355x_debug_pipe_token(mi355x_comm_t *c, int acquire)
     if (c->pipe_entry >= 0) pipe_token_release(c);
     return 0;
 }
+// the service limits a communicator reports: its own once the device setup decided it may have
+// the service; before that setup (deferred to the first device-buffer collective) the configured
+// ones, which it will have unless that setup finds the service unusable
+static bool svc_limit_visible(const mi355x_comm_t *c)
+{
+    return c->svc_ok || c->svc_want || (!c->dev_ready && !c->loopback && c->size > 1);
+}
+
 int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
 {
     if (!c || !value) return set_error(MI355X_ERR_ARG, "NULL argument");
@@ -392,12 +400,12 @@ int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
     case MI355X_KNOB_PIPE_CHUNK_KIB: *value = coll_tune().pipe_chunk_kib; break;
     case MI355X_KNOB_PIPE_WT: *value = coll_tune().pipe_wt; break;
     case MI355X_KNOB_ONE_PHASE_MAX_BYTES: *value = (long)c->one_phase_max; break;
-    case MI355X_KNOB_SVC_MAX_BYTES: *value = (c->svc_ok || c->svc_want) ? (long)c->svc_max : 0; break;
+    case MI355X_KNOB_SVC_MAX_BYTES: *value = svc_limit_visible(c) ? (long)c->svc_max : 0; break;
     case MI355X_KNOB_SVC_CALLS: *value = (long)c->svc_calls; break;
     case MI355X_KNOB_SVC_LAUNCHES: *value = (long)c->svc_launches; break;
     case MI355X_KNOB_SVC_RESIDENT: *value = c->svcq && svc_resident(c->svcq) ? 1 : 0; break;
-    case MI355X_KNOB_SVC_PULL_MAX_BYTES: *value = (c->svc_ok || c->svc_want) ? (long)c->svc_pull_max : 0; break;
-    case MI355X_KNOB_SVC_PULL_COPY_MAX_BYTES: *value = (c->svc_ok || c->svc_want) ? (long)c->svc_copy_max : 0; break;
+    case MI355X_KNOB_SVC_PULL_MAX_BYTES: *value = svc_limit_visible(c) ? (long)c->svc_pull_max : 0; break;
+    case MI355X_KNOB_SVC_PULL_COPY_MAX_BYTES: *value = svc_limit_visible(c) ? (long)c->svc_copy_max : 0; break;
     case MI355X_KNOB_FLOWS: *value = (long)c->flows; break;
     case MI355X_KNOB_FLOWS_FAILED: *value = (long)c->flows_failed; break;
     case MI355X_KNOB_CREATE_US: *value = (long)c->create_us; break;

@@ -1084,6 +1084,60 @@ def mca_vars_main():
     print(f"rank {rank} mca_vars OK", flush=True)
 
 
+def host8_main():
+    """(measurement, not a test) an 8-byte host-buffer MPI_Allreduce through the harness: the host
+    module alone (what the reference runs: coll/tuned over ob1/sm, here coll/basic's order over the
+    channel), with coll/mi355x selected on top (the call votes its buffer kind, then reaches the host
+    module, whose ompi_op_reduce dispatches through op/hip's slot), and with coll_mi355x_mixed_buffers
+    = 0 (no vote).  One JSON line per variant from rank 0: microseconds per call (median of 5 batches
+    of 2000, Python's ctypes call included in every variant alike)."""
+    import json
+    import os
+    import time
+    rank, size = int(sys.argv[1]), int(sys.argv[2])
+    import torch
+    torch.cuda.set_device(rank % torch.cuda.device_count())
+    m = mini()
+    L, pkg = m.lib, m.pkg
+    oracle = load_oracle()
+    m.install_oracle_base(oracle)
+    L.mini_host_module.restype = ctypes.c_void_p
+    comp = m.component_ptr(m.coll, "mca_coll_mi355x_component")
+    fdt = m.dtype_for_slot(pkg.T["DOUBLE"])
+    rows = []
+    for step, (variant, with_hip, mixed) in enumerate((("host_module", False, 1), ("coll_mi355x", True, 1),
+                                                        ("coll_mi355x_no_vote", True, 0))):
+        os.environ["OMPI_MCA_coll_mi355x_mixed_buffers"] = str(mixed)
+        assert L.mini_component_register(comp) == 0
+        op = m.select_op(pkg.OP["SUM"], with_hip=with_hip)
+        comm = L.mini_comm_create(rank, size, 60 + step)
+        assert L.mini_comm_set_channel(comm, f"{sys.argv[3]}_{step}".encode()) == 0
+        L.mini_comm_install(comm, L.mini_host_module())
+        if with_hip:
+            assert L.mini_coll_select(comm, comp) == 90
+        x = np.full(1, float(rank + 1))
+        y = np.zeros(1)
+        px, py = x.ctypes.data, y.ctypes.data
+        for _ in range(200):
+            assert L.mini_allreduce(comm, px, py, 1, fdt, op) == 0
+        batches = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            for _ in range(2000):
+                L.mini_allreduce(comm, px, py, 1, fdt, op)
+            batches.append((time.perf_counter() - t0) / 2000 * 1e6)
+        assert y[0] == size * (size + 1) / 2
+        rows.append({"variant": variant, "n": size, "bytes": 8, "us_per_call": round(sorted(batches)[2], 3)})
+        L.mini_comm_destroy(comm)
+        L.mini_op_destroy(op)
+    os.environ.pop("OMPI_MCA_coll_mi355x_mixed_buffers", None)
+    assert L.mini_component_register(comp) == 0
+    if rank == 0:
+        for r in rows:
+            print(json.dumps(r), flush=True)
+    print(f"rank {rank} host8 OK", flush=True)
+
+
 def main():
     if len(sys.argv) > 4 and sys.argv[4] == "split":
         return split_main()
@@ -1095,6 +1149,8 @@ def main():
         return staging_main()
     if len(sys.argv) > 4 and sys.argv[4] == "mca_vars":
         return mca_vars_main()
+    if len(sys.argv) > 4 and sys.argv[4] == "host8":
+        return host8_main()
     rank, size = int(sys.argv[1]), int(sys.argv[2])
     import torch
     ndev = torch.cuda.device_count()

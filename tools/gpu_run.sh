@@ -91,7 +91,11 @@ for step in "$@"; do
         grep -E "PASSED|FAILED|SKIPPED|ERROR|passed|failed" $O/pytest_sel.log | tail -40 ;;
     op_overhead)
         run op_overhead 120 ./tools/build/op_host_overhead
-        grep '^{' $O/op_overhead.log | tee $O/op_overhead.jsonl ;;
+        grep '^{' $O/op_overhead.log | tee $O/op_overhead.jsonl
+        for n in 2 4; do
+            run host8_n$n 200 bash tools/run_worker.sh host8 $n 150
+            grep -h '^{' $O/w0.log | tee -a $O/op_overhead.jsonl
+        done ;;
     smoke)
         run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
         tail -2 $O/smoke.log ;;
