@@ -103,6 +103,8 @@ int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **e
     auto it = c->peer_maps.find(key);
     if (it != c->peer_maps.end() && (it->second.id != d.id || (d.id == 0 && it->second.pins == 0))) {
         if (it->second.ext) drop_stash(c, peer, it->second.id);  // the peer replaced that allocation
+        TRACE(c, "replace peer %d base %llx: id %llu -> %llu (was at %p)", peer, (unsigned long long)d.base,
+              (unsigned long long)it->second.id, (unsigned long long)d.id, it->second.mapped);
         close_map(it->second);
         c->peer_maps.erase(it);
         it = c->peer_maps.end();
@@ -144,6 +146,15 @@ int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **e
             e = dropped ? hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess) : e;
             if (e != hipSuccess)
                 return set_error(MI355X_ERR_PEER, "hipIpcOpenMemHandle(rank %d): %s", peer, hipGetErrorString(e));
+        }
+        if (debug_on()) {
+            for (const auto &kv : c->peer_maps) {  // a new mapping must not overlap a live one
+                const uintptr_t a0 = (uintptr_t)kv.second.mapped, b0 = (uintptr_t)base;
+                if (!kv.second.ext && a0 < b0 + d.size && b0 < a0 + kv.second.bytes)
+                    TRACE(c, "ALIAS: peer %d base %llx id %llu mapped at %p overlaps peer %d base %llx id %llu at %p",
+                          peer, (unsigned long long)d.base, (unsigned long long)d.id, base, kv.first.peer,
+                          (unsigned long long)kv.first.base, (unsigned long long)kv.second.id, kv.second.mapped);
+            }
         }
         it = c->peer_maps.emplace(key, PeerMap{d.id, base, ++c->use_clock, nullptr}).first;
         it->second.bytes = d.size;

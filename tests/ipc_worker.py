@@ -1152,12 +1152,21 @@ def rcache(key, rank, size, dev):
         keep = []
         for k in range(64):
             # distinct allocations: each larger than the last, all alive until the round ends
-            x = torch.full((n + k * (1 << 19),), float(rank + 1 + k + 100 * rnd), device="cuda")
+            # rank r contributes m * 256**r (m = 1 + k + 64 rnd < 256): a wrong sum names, digit by
+            # digit, whose buffer of which call every rank's contribution came from
+            m = 1 + k + 64 * rnd
+            x = torch.full((n + k * (1 << 19),), float(m * 256 ** rank), device="cuda")
             y = torch.full_like(x, float("nan"))
             torch.cuda.synchronize()
             comm.allreduce(x.data_ptr(), y.data_ptr(), n, pkg.T["FLOAT"], pkg.OP["SUM"])
-            want = sum(r + 1 + k + 100 * rnd for r in range(size))
-            assert bool(torch.all(y[:n] == want).item()), ("rcache allreduce", rnd, k)
+            want = sum(m * 256 ** r for r in range(size))
+            bad = (y[:n] != want).nonzero()
+            if bad.numel():
+                got = int(y[int(bad[0])].item())
+                print("rcache: wrong sum", rnd, k, "per-rank m:", [(got >> (8 * r)) & 255 for r in range(size)],
+                      "want", m, "bad", bad.numel(), "alg", comm.last_algorithm(), "maps", comm.get("PEER_MAPS"),
+                      hex(x.data_ptr()), hex(y.data_ptr()), flush=True)
+            assert bad.numel() == 0, ("rcache allreduce", rnd, k)
             peak = max(peak, comm.get("PEER_MAPS"))
             keep += [x, y]
         comm.barrier()  # no peer still reads them
