@@ -38,6 +38,8 @@ uint64_t pid_namespace();
 int barrier(mi355x_comm *c);
 uint64_t buffer_id(const void *p);
 int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force);
+void retire_map(mi355x_comm *c, const PeerMap &m);
+void flush_retired(mi355x_comm *c);
 int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t sig[4],
              std::vector<std::vector<void *>> &peers, bool *staged, bool force, bool persistent);
 int finish(mi355x_comm *c, hipStream_t s);
@@ -49,6 +51,7 @@ int fd_drain(mi355x_comm *c, bool wait);
 int send_fds(mi355x_comm *c, int peer, const int *fds, const uint64_t *ids, int nfd);
 int send_fd(mi355x_comm *c, int peer, int fd, uint64_t id);
 int take_fd(mi355x_comm *c, int peer, uint64_t id, int *out);
+int serve_fd(mi355x_comm *c, int peer, uint64_t id);
 void drop_stash(mi355x_comm *c, int peer, uint64_t id);
 int export_dmabufs(mi355x_comm *c, BufDesc *const *ds, int nd, uint64_t peers);
 int export_dmabuf(mi355x_comm *c, BufDesc *d, uint64_t peers);

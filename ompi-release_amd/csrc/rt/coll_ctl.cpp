@@ -162,6 +162,15 @@ uint64_t buffer_id(const void *p)
     return (uint64_t)id;
 }
 
+// an allocation of `bytes` goes to the peers as a dmabuf fd rather than a hipIpc handle: always from
+// ipc_max up (hipIpcOpenMemHandle never returns for those), and at any size while the peer-mapping
+// cache is bounded -- evicting hipIpc mappings while allocations churn hands peers wrong memory on
+// this platform (coll_rcache.cpp, retire_map) -- unless the dmabuf route failed its probe
+static bool via_dmabuf(const mi355x_comm *c, size_t bytes)
+{
+    return bytes >= c->ipc_max || ((c->rcache_max_maps || c->rcache_limit) && c->dmabuf_state != -1);
+}
+
 int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
 {
     std::lock_guard<std::recursive_mutex> reg_guard(c->reg_mtx);
@@ -184,7 +193,7 @@ int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
         const LocalReg &r = c->local_regs[i];
         if (up >= r.base && up < r.base + r.size) {
             if (r.id == id && id != 0 && (r.has_h || !force)) {
-                if (!force && r.size >= c->ipc_max) {
+                if (!force && !r.has_h) {  // (registered for the dmabuf route)
                     d->staged = 1;
                     d->base = r.base;
                     d->off = up - r.base;
@@ -214,8 +223,20 @@ int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
     reg.base = (uintptr_t)base;
     reg.size = sz;
     reg.id = id;
-    if (!force && sz >= c->ipc_max) {
-        // never exported (hipIpcOpenMemHandle hangs on such allocations): staged data flow
+    bool dm = !force && via_dmabuf(c, sz);
+    if (dm && sz < c->ipc_max) {
+        // (bounded cache) only an allocation with a buffer object of its own exports as a dmabuf --
+        // the runtime sub-allocates small ones: those keep the hipIpc route
+        if (hipMemGetHandleForAddressRange(&reg.fd, (hipDeviceptr_t)base, sz, hipMemRangeHandleTypeDmaBufFd, 0) !=
+            hipSuccess) {
+            (void)hipGetLastError();
+            reg.fd = -1;
+            dm = false;
+        }
+    }
+    if (dm) {
+        // the dmabuf route (hipIpcOpenMemHandle never returns for allocations >= ipc_max): fds
+        // passed by export_dmabufs, or the staged data flow when that route is off
         reg.has_h = false;
         if (id != 0) c->local_regs.push_back(reg);
         d->staged = 1;
@@ -225,8 +246,27 @@ int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
         d->size = sz;
         return MI355X_SUCCESS;
     }
-    MI_HIP(hipIpcGetMemHandle(&reg.h, base));
+    if (hipIpcGetMemHandle(&reg.h, base) != hipSuccess) {
+        // seen on ROCm 7.2 under heavy allocation churn ("invalid argument" for a live allocation):
+        // this call moves the buffer through the staging buffers instead (every rank sees staged
+        // = 2 and takes the staged data flow), nothing is cached
+        (void)hipGetLastError();
+        if (force) return set_error(MI355X_ERR_HIP, "hipIpcGetMemHandle(%p) failed", base);
+        TRACE(c, "hipIpcGetMemHandle(%p) failed: staged data flow for this call", base);
+        d->staged = 2;
+        d->base = reg.base;
+        d->off = up - reg.base;
+        d->id = id;
+        d->size = sz;
+        return MI355X_SUCCESS;
+    }
     reg.has_h = true;
+    if (debug_on()) {
+        uint32_t w[16];
+        std::memcpy(w, &reg.h, sizeof(w));
+        TRACE(c, "export %p handle %08x %08x %08x %08x %08x %08x %08x %08x %08x %08x %08x %08x", base, w[0], w[1], w[2],
+              w[3], w[4], w[5], w[6], w[7], w[8], w[9], w[10], w[11]);
+    }
     // without an allocation id the entry cannot be validated later: do not cache it
     if (id != 0) c->local_regs.push_back(reg);
     d->h = reg.h;
@@ -261,13 +301,14 @@ int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t s
         if (rc) return rc;
     }
     s.nbuf = nbuf;
+    s.retiring = c->retired_maps.empty() ? 0 : 1;
     for (int i = 0; i < 4; ++i) s.sig[i] = sig[i];
     s.seq.store(c->seq, std::memory_order_release);
     TRACE(c, "published %d buffers", nbuf);
     int rc = barrier(c);
     TRACE(c, "exchange barrier passed (rc %d)", rc);
     if (rc) return rc;
-    bool any_staged = false;
+    bool any_staged = false, no_export = false;
     for (int r = 0; r < c->size; ++r) {
         RankSlot &o = c->ctrl->slot[r];
         if (o.seq.load(std::memory_order_acquire) != c->seq)
@@ -275,10 +316,23 @@ int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t s
                              (unsigned long long)o.seq.load(), c->rank, (unsigned long long)c->seq);
         if (o.sig[0] != sig[0] || o.sig[1] != sig[1] || o.sig[2] != sig[2] || o.sig[3] != sig[3])
             return set_error(MI355X_ERR_ARG, "collective arguments differ between rank %d and rank %d", r, c->rank);
-        for (int b = 0; b < nbuf; ++b) any_staged = any_staged || o.buf[b].staged;
+        for (int b = 0; b < nbuf; ++b) {
+            any_staged = any_staged || o.buf[b].staged;
+            no_export = no_export || o.buf[b].staged == 2;
+        }
+    }
+    // the close window (coll_rcache.cpp, retire_map): when any rank holds retired mappings, every
+    // rank closes its own here -- after every rank's exports of this call, before anybody opens --
+    // and meets once more, so no close overlaps a peer's IPC export or import
+    bool window = false;
+    for (int r = 0; r < c->size; ++r) window = window || c->ctrl->slot[r].retiring != 0;
+    if (window) {
+        flush_retired(c);
+        rc = barrier(c);
+        if (rc) return rc;
     }
     peers.assign(nbuf, std::vector<void *>(c->size, nullptr));
-    if (any_staged && !c->loopback) {
+    if (any_staged && !c->loopback && !no_export) {
         if (c->dmabuf_state == 0) {
             rc = barrier(c);  // every rank has read the staged flags before the probe reuses the slots
             if (rc) return rc;
@@ -308,17 +362,26 @@ int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t s
         // its slot before every rank has read this exchange's slots
         return barrier(c);
     }
-    for (int r = 0; r < c->size; ++r) {
-        RankSlot &o = c->ctrl->slot[r];
-        for (int b = 0; b < nbuf; ++b) {
-            if (r == c->rank) {
-                peers[b][r] = const_cast<void *>(mine[b]);
-            } else {
-                PeerMap *pm = nullptr;
-                rc = map_peer(c, r, o.buf[b], &peers[b][r], &pm);
-                if (rc) return rc;
-                if (persistent && pm) pm->persistent = true;
+    static const bool turns = getenv("MI355X_IMPORT_TURNS") && atoi(getenv("MI355X_IMPORT_TURNS")) > 0;
+    for (int t = 0; t < (turns ? c->size : 1); ++t) {
+        if (!turns || t == c->rank) {
+            for (int r = 0; r < c->size; ++r) {
+                RankSlot &o = c->ctrl->slot[r];
+                for (int b = 0; b < nbuf; ++b) {
+                    if (r == c->rank) {
+                        peers[b][r] = const_cast<void *>(mine[b]);
+                    } else {
+                        PeerMap *pm = nullptr;
+                        rc = map_peer(c, r, o.buf[b], &peers[b][r], &pm);
+                        if (rc) return rc;
+                        if (persistent && pm) pm->persistent = true;
+                    }
+                }
             }
+        }
+        if (turns) {
+            rc = barrier(c);
+            if (rc) return rc;
         }
     }
     return MI355X_SUCCESS;
@@ -351,6 +414,10 @@ int finish(mi355x_comm *c, hipStream_t s)
                 return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
             if (++spins > 4096) {
                 sched_yield();
+                if (c->fd_sock >= 0 && (spins & 255) == 0 && c->reg_mtx.try_lock()) {
+                    (void)fd_drain(c, false);  // a peer may be asking for a dmabuf fd (serve_fd)
+                    c->reg_mtx.unlock();
+                }
                 if ((spins & 0xffff) == 0 && hipStreamQuery(s) != hipErrorNotReady && q == c->rank &&
                     k->slot[q].done.load(std::memory_order_acquire) < v)
                     return set_error(MI355X_ERR_HIP, "stream finished without writing its completion word");

@@ -50,11 +50,20 @@ namespace mi355x {
 // creation under an abstract name derived from the control segment's (node-unique) name; the
 // receiver checks the sender's pid (SO_PASSCRED) against the rank's published pid.
 constexpr int kFdMax = 8;  // fds per message (a call exports at most kMaxBufs buffers)
+// kind 0: nfd fds for allocations id[0..nfd); kind 1: a request for allocation id[0]'s fd (an
+// importer that closed its import, or never got the fd, asks its exporter again); kind 2: that
+// allocation is not registered with the exporter any more
+enum : int32_t { kFdGive = 0, kFdAsk = 1, kFdGone = 2 };
+constexpr int kStashGone = -2;  // fd_stash value for a kFdGone answer
 struct FdMsg {
     int32_t from;
     int32_t nfd;
+    int32_t kind;
+    int32_t pad;
     uint64_t id[kFdMax];
 };
+
+static int send_msg(mi355x_comm *c, int peer, const FdMsg &m, const int *fds, int nfd);
 
 void fd_sock_addr(const mi355x_comm *c, int rank, sockaddr_un *a, socklen_t *len)
 {
@@ -129,8 +138,19 @@ int fd_drain(mi355x_comm *c, bool wait)
                 pid = cr.pid;
             }
         }
-        const bool ok = got == (ssize_t)sizeof(m) && nfd > 0 && m.nfd == nfd && m.from >= 0 && m.from < c->size &&
-                        pid == (pid_t)c->ctrl->slot[m.from].pid;
+        const bool from_rank = got == (ssize_t)sizeof(m) && m.from >= 0 && m.from < c->size &&
+                               pid == (pid_t)c->ctrl->slot[m.from].pid;
+        if (from_rank && nfd == 0 && m.nfd == 0 && m.kind == kFdAsk) {
+            int rc = serve_fd(c, m.from, m.id[0]);
+            if (rc) return rc;
+            continue;
+        }
+        if (from_rank && nfd == 0 && m.nfd == 0 && m.kind == kFdGone) {
+            c->fd_stash[std::make_pair((int)m.from, m.id[0])] = kStashGone;
+            if (wait) return MI355X_SUCCESS;
+            continue;
+        }
+        const bool ok = from_rank && nfd > 0 && m.nfd == nfd && m.kind == kFdGive;
         for (int i = 0; i < nfd; ++i) {
             if (!ok) {  // not from a rank of this communicator: drop it
                 close(fds[i]);
@@ -138,22 +158,18 @@ int fd_drain(mi355x_comm *c, bool wait)
             }
             const auto key = std::make_pair((int)m.from, m.id[i]);
             auto it = c->fd_stash.find(key);
-            if (it != c->fd_stash.end()) close(it->second);
+            if (it != c->fd_stash.end() && it->second >= 0) close(it->second);
             c->fd_stash[key] = fds[i];
         }
         if (wait && ok) return MI355X_SUCCESS;
     }
 }
 
-// one message carrying nfd fds and their allocation ids to `peer`.  Caller holds reg_mtx.
-int send_fds(mi355x_comm *c, int peer, const int *fds, const uint64_t *ids, int nfd)
+// one message to `peer`: nfd fds (SCM_RIGHTS) and their allocation ids, or a request / answer
+// without fds.  Caller holds reg_mtx.
+static int send_msg(mi355x_comm *c, int peer, const FdMsg &m, const int *fds, int nfd)
 {
-    FdMsg m;
-    std::memset(&m, 0, sizeof(m));
-    m.from = c->rank;
-    m.nfd = nfd;
-    for (int i = 0; i < nfd; ++i) m.id[i] = ids[i];
-    iovec iov{&m, sizeof(m)};
+    iovec iov{const_cast<FdMsg *>(&m), sizeof(m)};
     alignas(cmsghdr) char ctl[CMSG_SPACE(sizeof(int) * kFdMax)];
     std::memset(ctl, 0, sizeof(ctl));
     sockaddr_un a;
@@ -165,26 +181,66 @@ int send_fds(mi355x_comm *c, int peer, const int *fds, const uint64_t *ids, int 
     h.msg_namelen = len;
     h.msg_iov = &iov;
     h.msg_iovlen = 1;
-    h.msg_control = ctl;
-    h.msg_controllen = CMSG_SPACE(sizeof(int) * (size_t)nfd);
-    cmsghdr *cm = CMSG_FIRSTHDR(&h);
-    cm->cmsg_level = SOL_SOCKET;
-    cm->cmsg_type = SCM_RIGHTS;
-    cm->cmsg_len = CMSG_LEN(sizeof(int) * (size_t)nfd);
-    std::memcpy(CMSG_DATA(cm), fds, sizeof(int) * (size_t)nfd);
+    if (nfd > 0) {
+        h.msg_control = ctl;
+        h.msg_controllen = CMSG_SPACE(sizeof(int) * (size_t)nfd);
+        cmsghdr *cm = CMSG_FIRSTHDR(&h);
+        cm->cmsg_level = SOL_SOCKET;
+        cm->cmsg_type = SCM_RIGHTS;
+        cm->cmsg_len = CMSG_LEN(sizeof(int) * (size_t)nfd);
+        std::memcpy(CMSG_DATA(cm), fds, sizeof(int) * (size_t)nfd);
+    }
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
         if (sendmsg(c->fd_sock, &h, MSG_DONTWAIT | MSG_NOSIGNAL) == (ssize_t)sizeof(m)) return MI355X_SUCCESS;
         if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR)
             return set_error(MI355X_ERR_PEER, "sending dmabuf fds to rank %d: %s", peer, strerror(errno));
         // the peer's queue is full (net.unix.max_dgram_qlen): it drains it whenever it waits
-        // (barrier, its own sends, its imports) -- keep ours drained meanwhile too
+        // (barrier, finish, its own sends, its imports) -- keep ours drained meanwhile too
         int rc = fd_drain(c, false);
         if (rc) return rc;
         if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s)
             return set_error(MI355X_ERR_TIMEOUT, "rank %d: fd queue of rank %d stays full", c->rank, peer);
         usleep(50);
     }
+}
+
+int send_fds(mi355x_comm *c, int peer, const int *fds, const uint64_t *ids, int nfd)
+{
+    FdMsg m;
+    std::memset(&m, 0, sizeof(m));
+    m.from = c->rank;
+    m.nfd = nfd;
+    m.kind = kFdGive;
+    for (int i = 0; i < nfd; ++i) m.id[i] = ids[i];
+    return send_msg(c, peer, m, fds, nfd);
+}
+
+// a peer asks for the fd of my allocation `id` again: export it afresh, send it, close my copy (an
+// exporter keeps no fd of its own, so a freed allocation is held only by the imports of it)
+int serve_fd(mi355x_comm *c, int peer, uint64_t id)
+{
+    FdMsg m;
+    std::memset(&m, 0, sizeof(m));
+    m.from = c->rank;
+    m.id[0] = id;
+    for (const LocalReg &r : c->local_regs) {
+        if (r.id != id) continue;
+        int fd = -1;
+        if (hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)r.base, r.size, hipMemRangeHandleTypeDmaBufFd, 0) !=
+            hipSuccess) {
+            (void)hipGetLastError();
+            break;
+        }
+        TRACE(c, "dmabuf: rank %d asked again for allocation %llu", peer, (unsigned long long)id);
+        m.kind = kFdGive;
+        m.nfd = 1;
+        const int rc = send_msg(c, peer, m, &fd, 1);
+        close(fd);
+        return rc;
+    }
+    m.kind = kFdGone;
+    return send_msg(c, peer, m, nullptr, 0);
 }
 
 int send_fd(mi355x_comm *c, int peer, int fd, uint64_t id) { return send_fds(c, peer, &fd, &id, 1); }
@@ -195,9 +251,22 @@ int take_fd(mi355x_comm *c, int peer, uint64_t id, int *out)
     const auto key = std::make_pair(peer, id);
     int rc = fd_drain(c, false);
     if (rc) return rc;
+    if (c->fd_stash.find(key) == c->fd_stash.end()) {  // (closed an import of it, or never got it: ask)
+        FdMsg m;
+        std::memset(&m, 0, sizeof(m));
+        m.from = c->rank;
+        m.kind = kFdAsk;
+        m.id[0] = id;
+        rc = send_msg(c, peer, m, nullptr, 0);
+        if (rc) return rc;
+    }
     while (c->fd_stash.find(key) == c->fd_stash.end()) {
         rc = fd_drain(c, true);
         if (rc) return rc;
+    }
+    if (c->fd_stash[key] == kStashGone) {
+        c->fd_stash.erase(key);
+        return set_error(MI355X_ERR_PEER, "rank %d no longer has allocation %llu registered", peer, (unsigned long long)id);
     }
     *out = fcntl(c->fd_stash[key], F_DUPFD_CLOEXEC, 0);
     if (*out < 0) return set_error(MI355X_ERR_PEER, "dup of a dmabuf fd: %s", strerror(errno));
@@ -209,12 +278,14 @@ void drop_stash(mi355x_comm *c, int peer, uint64_t id)
 {
     auto it = c->fd_stash.find(std::make_pair(peer, id));
     if (it == c->fd_stash.end()) return;
-    close(it->second);
+    if (it->second >= 0) close(it->second);
     c->fd_stash.erase(it);
 }
 
-// export the large allocations of ds[0..nd) as dmabuf fds and pass every one to every rank in
-// `peers` that has not received it yet: one message per peer
+// pass the dmabuf fds of the allocations of ds[0..nd) to every rank in `peers` that has not had
+// them yet: one message per peer.  The export is made for the sends and closed after them (the
+// fds in flight and the peers' imports hold the allocation; a peer that later needs one again asks,
+// serve_fd), so an exporter never keeps a freed allocation alive itself.
 int export_dmabufs(mi355x_comm *c, BufDesc *const *ds, int nd, uint64_t peers)
 {
     std::lock_guard<std::recursive_mutex> reg_guard(c->reg_mtx);
@@ -225,35 +296,36 @@ int export_dmabufs(mi355x_comm *c, BufDesc *const *ds, int nd, uint64_t peers)
             if (r.base == ds[i]->base && r.id == ds[i]->id) regs[i] = &r;
         if (!regs[i])
             return set_error(MI355X_ERR_PEER, "large allocation not registered (id %llu)", (unsigned long long)ds[i]->id);
-        LocalReg &r = *regs[i];
-        if (r.fd < 0) {
-            MI_HIP(hipMemGetHandleForAddressRange(&r.fd, (hipDeviceptr_t)r.base, r.size,
-                                                  hipMemRangeHandleTypeDmaBufFd, 0));
-            r.sent = 0;
-        }
         ds[i]->dmabuf = 1;
-        ds[i]->fd = r.fd;
-        ds[i]->size = r.size;
+        ds[i]->fd = -1;
+        ds[i]->size = regs[i]->size;
     }
-    for (int q = 0; q < c->size; ++q) {
+    int rc = MI355X_SUCCESS;
+    for (int q = 0; q < c->size && !rc; ++q) {
         if (q == c->rank || !((peers >> q) & 1u)) continue;
         int fds[kFdMax];
         uint64_t ids[kFdMax];
         int k = 0;
         for (int i = 0; i < nd; ++i) {
-            if ((regs[i]->sent >> q) & 1u) continue;
+            LocalReg &r = *regs[i];
+            if ((r.sent >> q) & 1u) continue;
             bool dup = false;  // two buffers of one allocation: one fd
-            for (int j = 0; j < k; ++j) dup = dup || ids[j] == regs[i]->id;
+            for (int j = 0; j < k; ++j) dup = dup || ids[j] == r.id;
             if (dup) continue;
-            fds[k] = regs[i]->fd;
-            ids[k++] = regs[i]->id;
+            if (r.fd < 0) {
+                MI_HIP(hipMemGetHandleForAddressRange(&r.fd, (hipDeviceptr_t)r.base, r.size,
+                                                      hipMemRangeHandleTypeDmaBufFd, 0));
+            }
+            fds[k] = r.fd;
+            ids[k++] = r.id;
         }
         if (!k) continue;
-        int rc = send_fds(c, q, fds, ids, k);
-        if (rc) return rc;
-        for (int i = 0; i < nd; ++i) regs[i]->sent |= 1ull << q;
+        rc = send_fds(c, q, fds, ids, k);
+        if (!rc)
+            for (int i = 0; i < nd; ++i) regs[i]->sent |= 1ull << q;
     }
-    return MI355X_SUCCESS;
+    for (int i = 0; i < nd; ++i) drop_reg(*regs[i]);  // (closes this call's exports; the registration stays)
+    return rc;
 }
 
 int export_dmabuf(mi355x_comm *c, BufDesc *d, uint64_t peers)
@@ -287,6 +359,7 @@ int import_dmabuf(mi355x_comm *c, int peer, uint64_t id, size_t size, void **map
         return set_error(MI355X_ERR_PEER, "hipExternalMemoryGetMappedBuffer(rank %d): %s", peer, hipGetErrorString(e));
     }
     TRACE(c, "dmabuf import from rank %d: %zu bytes at %p", peer, size, *mapped);
+    drop_stash(c, peer, id);  // (the import holds the allocation now)
     return MI355X_SUCCESS;
 }
 

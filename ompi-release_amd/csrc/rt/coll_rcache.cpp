@@ -50,11 +50,34 @@ namespace mi355x {
 // collective or point-to-point -- so the bounds hold in phases of point-to-point traffic alone
 // (a mapping a point-to-point read made is evictable once the read has finished and unpinned it).  A mapping keeps the exporter's allocation
 // alive on ROCm, so a long job that churns allocations would otherwise hold every freed block of
-// every peer.  Both limits default to 0 = unlimited, as in the reference.  dmabuf imports (>= 2 GiB
-// allocations) are not evicted: their fd reaches a peer once.
+// every peer.  Both limits default to 0 = unlimited, as in the reference.  With a bound set, every
+// allocation travels as a dmabuf fd (local_handle, via_dmabuf): see retire_map for why hipIpc
+// mappings are not closed under churn; an evicted dmabuf import is asked for again (serve_fd).
+// hipIpcCloseMemHandle in one process while a peer process exports (hipIpcGetMemHandle) or
+// imports can hand that peer the wrong allocation -- a third rank's buffer through one rank's
+// handle -- or fail the export / import with "invalid argument" (ROCm 7.2, dmabuf IPC mode;
+// tools/ipc_repro.hip reproduces it with plain hipMalloc / hipIpc* calls and no engine:
+// profiles/r05_ipc_close_race.jsonl).  So an evicted mapping is only retired in the mapping phase
+// and closed in the next exchange's close window (exchange(): after every rank's exports, before
+// anybody opens, then one more barrier).  A replaced mapping (same exporter base, new allocation
+// id) is still closed at once: an import with the same handle words left open would be handed
+// back by hipIpcOpenMemHandle instead of the new allocation.
+void retire_map(mi355x_comm *c, const PeerMap &m)
+{
+    c->retired_maps.push_back(m);
+    if (c->retired_maps.size() > 256) flush_retired(c);  // (point-to-point-only phases: bounded)
+}
+
+void flush_retired(mi355x_comm *c)
+{
+    std::lock_guard<std::recursive_mutex> reg_guard(c->reg_mtx);
+    for (PeerMap &m : c->retired_maps) close_map(m);
+    c->retired_maps.clear();
+}
+
 bool evictable(const mi355x_comm *c, const PeerMap &m, const PeerMap *keep)
 {
-    return &m != keep && !m.persistent && m.pins == 0 && !m.ext && m.coll_use != c->seq;
+    return &m != keep && !m.persistent && m.pins == 0 && m.coll_use != c->seq;
 }
 
 void rcache_trim(mi355x_comm *c, const PeerMap *keep)
@@ -64,7 +87,7 @@ void rcache_trim(mi355x_comm *c, const PeerMap *keep)
         size_t nmaps = 0, bytes = 0;
         auto lru = c->peer_maps.end();
         for (auto it = c->peer_maps.begin(); it != c->peer_maps.end(); ++it) {
-            if (it->second.persistent || it->second.ext) continue;
+            if (it->second.persistent) continue;
             nmaps++;
             bytes += it->second.bytes;
             if (evictable(c, it->second, keep) && (lru == c->peer_maps.end() || it->second.last_use < lru->second.last_use))
@@ -74,7 +97,7 @@ void rcache_trim(mi355x_comm *c, const PeerMap *keep)
         if (!over || lru == c->peer_maps.end()) return;
         TRACE(c, "rcache: evict peer %d base %llx (%zu maps, %zu bytes)", lru->first.peer,
               (unsigned long long)lru->first.base, nmaps, bytes);
-        close_map(lru->second);
+        retire_map(c, lru->second);
         c->peer_maps.erase(lru);
         c->rcache_evictions++;
     }
@@ -83,7 +106,7 @@ void rcache_trim(mi355x_comm *c, const PeerMap *keep)
 size_t peer_map_count(const mi355x_comm *c)
 {
     size_t n = 0;
-    for (const auto &kv : c->peer_maps) n += !kv.second.persistent && !kv.second.ext;
+    for (const auto &kv : c->peer_maps) n += !kv.second.persistent;
     return n;
 }
 
@@ -105,7 +128,7 @@ int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **e
         if (it->second.ext) drop_stash(c, peer, it->second.id);  // the peer replaced that allocation
         TRACE(c, "replace peer %d base %llx: id %llu -> %llu (was at %p)", peer, (unsigned long long)d.base,
               (unsigned long long)it->second.id, (unsigned long long)d.id, it->second.mapped);
-        close_map(it->second);
+        close_map(it->second);  // (now: an import with the same handle words still open would be handed back)
         c->peer_maps.erase(it);
         it = c->peer_maps.end();
     }
@@ -115,6 +138,9 @@ int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **e
         int rc = import_dmabuf(c, peer, d.id, d.size, &mapped, &ext);
         if (rc) return rc;
         it = c->peer_maps.emplace(key, PeerMap{d.id, mapped, ++c->use_clock, ext}).first;
+        it->second.bytes = d.size;
+        if (coll) it->second.coll_use = c->seq;
+        rcache_trim(c, &it->second);
     }
     void *base;
     if (it != c->peer_maps.end()) {
@@ -122,7 +148,13 @@ int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **e
         it->second.last_use = ++c->use_clock;
         if (coll) it->second.coll_use = c->seq;
     } else {
-        TRACE(c, "open peer %d base %llx id %llu", peer, (unsigned long long)d.base, (unsigned long long)d.id);
+        if (debug_on()) {
+            uint32_t w[16];
+            std::memcpy(w, &d.h, sizeof(w));
+            TRACE(c, "open peer %d base %llx id %llu handle %08x %08x %08x %08x %08x %08x %08x %08x %08x %08x %08x %08x",
+                  peer, (unsigned long long)d.base, (unsigned long long)d.id, w[0], w[1], w[2], w[3], w[4], w[5], w[6],
+                  w[7], w[8], w[9], w[10], w[11]);
+        }
         hipError_t e = hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess);
         TRACE(c, "opened peer %d -> %p (%s)", peer, base, hipGetErrorString(e));
         if (e != hipSuccess) {
@@ -131,7 +163,8 @@ int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **e
             // with "invalid device pointer".  Drop this peer's mappings that the current call does
             // not use and try once more.
             (void)hipGetLastError();
-            int dropped = 0;
+            int dropped = (int)c->retired_maps.size();
+            flush_retired(c);
             for (auto m = c->peer_maps.begin(); m != c->peer_maps.end();) {
                 if (m->first.peer == peer && m->second.coll_use != c->seq && m->second.pins == 0 &&
                     !m->second.persistent) {

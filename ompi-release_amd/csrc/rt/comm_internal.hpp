@@ -51,7 +51,8 @@ struct BufDesc {
     uint64_t present;  // 0: NULL buffer
     uint64_t base;     // exporter's allocation base (its VA; the peer-map key)
     uint64_t id;       // exporter's allocation id (HIP_POINTER_ATTRIBUTE_BUFFER_ID)
-    uint64_t staged;   // 1: allocation too large for hipIpc* (>= ipc_max): dmabuf or staged flow
+    uint64_t staged;   // 1: the dmabuf route (>= ipc_max, or a bounded cache) or the staged flow;
+                       // 2: not exportable at all this call: the staged flow
     uint64_t size;     // dmabuf: the exported allocation's size
     int32_t dmabuf;    // 1: exported as a dmabuf fd (fd is a descriptor of the exporter process)
     int32_t fd;
@@ -59,7 +60,8 @@ struct BufDesc {
 
 struct alignas(64) RankSlot {
     std::atomic<uint64_t> seq;
-    int32_t pid, dev, nbuf, pad;
+    int32_t pid, dev, nbuf;
+    int32_t retiring;             // this rank holds retired peer mappings to close in the call's close window
     uint64_t sig[4];
     BufDesc buf[kMaxBufs];
     int32_t probe_fd, probe_ok;   // dmabuf capability probe
@@ -261,6 +263,9 @@ struct mi355x_comm {
     uint64_t seq = 0;
     uint64_t vote_seq = 0;                        // mi355x_comm_vote calls made
     std::map<mi355x::HandleKey, mi355x::PeerMap> peer_maps;
+    // mappings evicted during a call's mapping phase: closed in the next exchange's close window,
+    // never while a peer exports or imports (coll_rcache.cpp: retire_map)
+    std::vector<mi355x::PeerMap> retired_maps;
     // peer-mapping cache bounds (MI355X_RCACHE_MAX_MAPS / MI355X_RCACHE_SIZE_LIMIT, knobs of the same
     // names; 0 = unlimited, the default, as mpool_rgpusm_rcache_size_limit): LRU eviction
     size_t rcache_max_maps = 0, rcache_limit = 0;

@@ -1110,6 +1110,8 @@ static int isend(mi355x_comm *c, const void *buf, size_t count, const mi355x_ddt
         }
         if ((rc = local_handle(c, src, &desc, false))) return bail(rc);
         desc.raw = (uint64_t)(uintptr_t)src;
+        if (desc.staged == 2 && !c->loopback && dest != c->rank)
+            return bail(set_error(MI355X_ERR_HIP, "send buffer could not be exported (hipIpcGetMemHandle failed)"));
         if (desc.staged && !c->loopback && dest != c->rank) {
             const char *env = getenv("MI355X_DMABUF");
             if ((env && atoi(env) == 0) || c->dmabuf_state == -1)
