@@ -76,11 +76,17 @@ uint32_t st_val(uint64_t seed, int q, size_t i)
     return (uint32_t)(x & 0xffffff);  // (sums of <= 64 ranks stay below 2^31)
 }
 
-// restores the communicator's last_algorithm when a self-test that ran collectives of its own returns
+// restores the communicator's last_algorithm and pipelined-call count when a self-test that ran
+// collectives of its own returns (its calls are not the caller's)
 struct LastAlgKeeper {
     mi355x_comm *c;
     int alg;
-    ~LastAlgKeeper() { c->last_alg = alg; }
+    uint64_t pipe_calls = c->pipe_calls;
+    ~LastAlgKeeper()
+    {
+        c->last_alg = alg;
+        c->pipe_calls = pipe_calls;
+    }
 };
 
 // device buffers of the self-test: my input (n x count int32 for the reduce_scatter block), output

@@ -1046,7 +1046,10 @@ def mca_vars_main():
     oracle.oracle_allreduce(0, size, count, pkg.T["FLOAT"], pkg.OP["SUM"], 0, ptrs(xs), ptrs(outs))
     names = ("pipe_min_ranks", "svc_max", "svc_pull_max", "svc_copy_max")
     off = {"pipe_min_ranks": "2", "svc_max": "0", "svc_pull_max": "0", "svc_copy_max": "0"}
-    for step, (env, pipe, svc) in enumerate(((off, 1, 0), ({}, 0, 32 << 10))):
+    # (a registration takes the storage's current value as its default, as mca_base_var does, so the
+    # second step names the shipped defaults instead of relying on a re-registration to reset them)
+    dflt = {"pipe_min_ranks": "4", "svc_max": str(32 << 10), "svc_pull_max": str(128 << 10), "svc_copy_max": str(1 << 20)}
+    for step, (env, pipe, svc) in enumerate(((off, 1, 0), (dflt, 0, 32 << 10))):
         for k in names:
             os.environ.pop("OMPI_MCA_coll_mi355x_" + k, None)
         for k, v in env.items():

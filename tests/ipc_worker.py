@@ -1151,7 +1151,7 @@ def rcache(key, rank, size, dev):
         comm.set("IPC_MAX_BYTES", int(os.environ["RCACHE_IPC_MAX"]))
     n = (1 << 20) // 4
     peak = 0
-    for rnd in range(2):
+    for rnd in range(int(os.environ.get("RCACHE_ROUNDS", "2"))):
         keep = []
         for k in range(64):
             # distinct allocations: each larger than the last, all alive until the round ends
