@@ -71,12 +71,14 @@ typedef struct mca_coll_mi355x_module_t {
     int ddt_next;
     void *scratch[2];          /* send-side and receive-side staging (device memory) */
     size_t scratch_bytes[2];
+    int mixed;                 /* coll_mi355x_mixed_buffers when the module was enabled */
 } mca_coll_mi355x_module_t;
 
 static void module_construct(opal_object_t *o)
 {
     mca_coll_mi355x_module_t *m = (mca_coll_mi355x_module_t *)o;
     memset((char *)m + sizeof(mca_coll_base_module_t), 0, sizeof(*m) - sizeof(mca_coll_base_module_t));
+    m->mixed = mca_coll_mi355x_mixed_buffers;
 }
 
 static void release_prev(mca_coll_base_module_t *p)
@@ -310,7 +312,7 @@ int mca_coll_mi355x_selftest = 1;
  * rank; < 0: an error (the vote failed or timed out) */
 static int route(mca_coll_mi355x_module_t *m, int dev)
 {
-    if (!mca_coll_mi355x_mixed_buffers) return dev;
+    if (!m->mixed) return dev;
     int any = dev;
     const int rc = mi355x_comm_vote(m->engine, dev, &any);
     if (rc != MI355X_SUCCESS) {
@@ -1036,6 +1038,7 @@ static opal_class_t mi355x_nbreq_t_class = {"mca_coll_mi355x_request_t", &ompi_r
 /* opal_progress callback: complete the requests whose engine call has finished */
 static int nb_progress(void)
 {
+    if (!__atomic_load_n(&nb_active, __ATOMIC_ACQUIRE)) return 0;  /* (every opal_progress call lands here) */
     if (pthread_mutex_trylock(&nb_lock)) return 0;
     int completed = 0;
     for (mi355x_nbreq_t **p = &nb_active; *p;) {

@@ -1092,8 +1092,8 @@ def host8_main():
     module alone (what the reference runs: coll/tuned over ob1/sm, here coll/basic's order over the
     channel), with coll/mi355x selected on top (the call votes its buffer kind, then reaches the host
     module, whose ompi_op_reduce dispatches through op/hip's slot), and with coll_mi355x_mixed_buffers
-    = 0 (no vote).  One JSON line per variant from rank 0: microseconds per call (median of 5 batches
-    of 2000, Python's ctypes call included in every variant alike)."""
+    = 0 (no vote).  One JSON line per variant from rank 0: microseconds per call (median of 15
+    interleaved batches of 1000, Python's ctypes call included in every variant alike)."""
     import json
     import os
     import time
@@ -1107,9 +1107,11 @@ def host8_main():
     L.mini_host_module.restype = ctypes.c_void_p
     comp = m.component_ptr(m.coll, "mca_coll_mi355x_component")
     fdt = m.dtype_for_slot(pkg.T["DOUBLE"])
-    rows = []
-    for step, (variant, with_hip, mixed) in enumerate((("host_module", False, 1), ("coll_mi355x", True, 1),
-                                                        ("coll_mi355x_no_vote", True, 0))):
+    # the three set-ups side by side (one communicator each), their batches interleaved so that
+    # drift over the run touches every variant alike: 15 rounds x 3 variants x 1000 calls
+    variants = (("host_module", False, 1), ("coll_mi355x", True, 1), ("coll_mi355x_no_vote", True, 0))
+    setups = []
+    for step, (variant, with_hip, mixed) in enumerate(variants):
         os.environ["OMPI_MCA_coll_mi355x_mixed_buffers"] = str(mixed)
         assert L.mini_component_register(comp) == 0
         op = m.select_op(pkg.OP["SUM"], with_hip=with_hip)
@@ -1118,19 +1120,24 @@ def host8_main():
         L.mini_comm_install(comm, L.mini_host_module())
         if with_hip:
             assert L.mini_coll_select(comm, comp) == 90
-        x = np.full(1, float(rank + 1))
-        y = np.zeros(1)
-        px, py = x.ctypes.data, y.ctypes.data
+        setups.append((variant, comm, op))
+    x = np.full(1, float(rank + 1))
+    y = np.zeros(1)
+    px, py = x.ctypes.data, y.ctypes.data
+    times = {v: [] for v, _, _ in setups}
+    for variant, comm, op in setups:
         for _ in range(200):
             assert L.mini_allreduce(comm, px, py, 1, fdt, op) == 0
-        batches = []
-        for _ in range(5):
+    for _ in range(15):
+        for variant, comm, op in setups:
             t0 = time.perf_counter()
-            for _ in range(2000):
+            for _ in range(1000):
                 L.mini_allreduce(comm, px, py, 1, fdt, op)
-            batches.append((time.perf_counter() - t0) / 2000 * 1e6)
-        assert y[0] == size * (size + 1) / 2
-        rows.append({"variant": variant, "n": size, "bytes": 8, "us_per_call": round(sorted(batches)[2], 3)})
+            times[variant].append((time.perf_counter() - t0) / 1000 * 1e6)
+            assert y[0] == size * (size + 1) / 2
+    rows = [{"variant": v, "n": size, "bytes": 8, "us_per_call": round(sorted(t)[len(t) // 2], 3),
+             "us_min_batch": round(min(t), 3)} for v, t in times.items()]
+    for variant, comm, op in setups:
         L.mini_comm_destroy(comm)
         L.mini_op_destroy(op)
     os.environ.pop("OMPI_MCA_coll_mi355x_mixed_buffers", None)
