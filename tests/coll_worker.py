@@ -1109,7 +1109,8 @@ def host8_main():
     fdt = m.dtype_for_slot(pkg.T["DOUBLE"])
     # the three set-ups side by side (one communicator each), their batches interleaved so that
     # drift over the run touches every variant alike: 15 rounds x 3 variants x 1000 calls
-    variants = (("host_module", False, 1), ("coll_mi355x", True, 1), ("coll_mi355x_no_vote", True, 0))
+    variants = (("host_module", False, 1), ("host_module_op_hip", True, 1), ("coll_mi355x", True, 1),
+                ("coll_mi355x_no_vote", True, 0))
     setups = []
     for step, (variant, with_hip, mixed) in enumerate(variants):
         os.environ["OMPI_MCA_coll_mi355x_mixed_buffers"] = str(mixed)
@@ -1118,7 +1119,7 @@ def host8_main():
         comm = L.mini_comm_create(rank, size, 60 + step)
         assert L.mini_comm_set_channel(comm, f"{sys.argv[3]}_{step}".encode()) == 0
         L.mini_comm_install(comm, L.mini_host_module())
-        if with_hip:
+        if variant.startswith("coll_mi355x"):
             assert L.mini_coll_select(comm, comp) == 90
         setups.append((variant, comm, op))
     x = np.full(1, float(rank + 1))

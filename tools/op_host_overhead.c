@@ -16,6 +16,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <time.h>
 
 #include "../ompi-release_amd/csrc/harness/ompi_mini.h"
@@ -114,6 +115,30 @@ int main(int argc, char **argv)
                med[V_OPHIP] - med[V_TABLE], (med[V_OPHIP] - med[V_TABLE]) / med[V_TABLE]);
         free(a);
         free(b);
+    }
+    /* the classification of host memory outside the brk heap and the stack: a private anonymous
+     * mapping (glibc's allocations above the mmap threshold) and a shared one (shared-memory
+     * segments), each with the op_hip reduction at count 16 on it */
+    for (int kind = 0; kind < 2; ++kind) {
+        const size_t bytes = (size_t)1 << 20;
+        float *m = (float *)mmap(NULL, bytes, PROT_READ | PROT_WRITE, (kind ? MAP_SHARED : MAP_PRIVATE) | MAP_ANONYMOUS, -1, 0);
+        if (m == MAP_FAILED) continue;
+        memset(m, 0, bytes);
+        double tq[7], tr[7];
+        for (int k = 0; k < 7; ++k) {
+            int d = 0;
+            double t0 = now_ns();
+            for (long r = 0; r < 100000; ++r) mi355x_ptr_is_device(m + 1024, &d);
+            tq[k] = (now_ns() - t0) / 1e5;
+            t0 = now_ns();
+            for (long r = 0; r < 100000; ++r) mini_op_reduce(hip, m, m + 4096, 16, dt);
+            tr[k] = (now_ns() - t0) / 1e5;
+        }
+        qsort(tq, 7, sizeof(double), cmp_d);
+        qsort(tr, 7, sizeof(double), cmp_d);
+        printf("{\"variant\": \"ptr_query_%s\", \"ns_per_call\": %.1f}\n", kind ? "mmap_shared" : "mmap_private", tq[3]);
+        printf("{\"variant\": \"op_hip_%s\", \"count\": 16, \"ns_per_call\": %.1f}\n", kind ? "mmap_shared" : "mmap_private", tr[3]);
+        munmap(m, bytes);
     }
     fflush(stdout);
     mini_op_destroy(plain);
