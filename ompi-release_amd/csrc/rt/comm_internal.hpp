@@ -435,6 +435,7 @@ int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force);
 // export the large allocation of `d` as a dmabuf fd and pass it to every rank in `peers` that
 // has not received it yet
 int export_dmabuf(mi355x_comm *c, BufDesc *d, uint64_t peers);
+int fd_drain(mi355x_comm *c, bool wait);  // receive queued dmabuf fds, serve fd requests (caller holds reg_mtx)
 int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **entry = nullptr, bool coll = true);
 size_t peer_map_count(const mi355x_comm *c);  // evictable-kind peer mappings currently open
 // publish nbuf buffers, meet every rank, map every rank's buffers: peers[b][r] (coll_comm.cpp)

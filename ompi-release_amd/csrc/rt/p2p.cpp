@@ -128,6 +128,7 @@ struct HostArena {
 struct P2P {
     std::recursive_mutex mtx;
     hipStream_t stream = nullptr;
+    unsigned fd_polls = 0;                  // p2p_progress calls (a dmabuf fd request check every 32)
     std::vector<uint64_t> send_seq;        // next message number, per destination
     std::vector<uint64_t> recv_seq;        // next message number to drain, per source
     std::deque<P2PMsg> unexpected;         // arrival order (per source: send order)
@@ -743,6 +744,12 @@ int p2p_progress(mi355x_comm *c)
     DeviceGuard dg(c->device);
     P2P *p = p2p_of(c);
     std::lock_guard<std::recursive_mutex> g(p->mtx);
+    // a receiver that closed its import of one of my send buffers asks me for its dmabuf fd again
+    // (serve_fd): serve it while I wait in point-to-point too (now and then: one syscall)
+    if (c->dmabuf_state != -1 && c->fd_sock >= 0 && (++p->fd_polls & 31) == 0 && c->reg_mtx.try_lock()) {
+        (void)fd_drain(c, false);
+        c->reg_mtx.unlock();
+    }
     // 1. announce queued sends, in order; a destination whose ring is full holds its later sends
     uint64_t blocked = 0;  // destinations whose ring is full (bit per rank; kMaxRanks = 64)
     for (auto it = p->queued.begin(); it != p->queued.end();) {

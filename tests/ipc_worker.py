@@ -1136,6 +1136,43 @@ def host_bw(key, rank, size, dev):
     print(f"rank {rank} host_bw OK", flush=True)
 
 
+def rcache_p2p(key, rank, size, dev):
+    """the bounded peer-mapping cache in a point-to-point-only phase (ADVICE r4): 2 ranks, bound 4;
+    rank 0 sends 24 distinct device buffers to rank 1 (the receiver pulls each from the sender's
+    allocation), then sends the first 8 again -- mappings evicted meanwhile are opened again (a
+    dmabuf fd asked for again from the sender, which serves the request while it waits in its send);
+    the receiver's open mappings stay within the bound, every payload exact"""
+    import torch
+    torch.cuda.set_device(dev)
+    pkg = load_pkg()
+    comm = pkg.Comm.create(key, rank, size, dev)
+    comm.set("RCACHE_MAX_MAPS", 4)
+    keep = []
+    peak = 0
+    for k in list(range(24)) + list(range(8)):
+        n = (1 << 18) + k * (1 << 17)
+        if rank == 0:
+            if k >= len(keep):
+                keep.append(torch.full((n,), float(k + 1), device="cuda"))
+                torch.cuda.synchronize()
+            comm.send(keep[k].data_ptr(), n * 4, 1, k)
+        else:
+            y = torch.zeros(n, device="cuda")
+            torch.cuda.synchronize()
+            comm.recv(y.data_ptr(), n * 4, 0, k)
+            torch.cuda.synchronize()
+            assert bool(torch.all(y == float(k + 1)).item()), ("rcache_p2p payload", k)
+            peak = max(peak, comm.get("PEER_MAPS"))
+    ev = comm.get("RCACHE_EVICTIONS")
+    if rank == 1:
+        assert peak <= 4, f"{peak} peer mappings open under a bound of 4"
+        assert ev > 0, "no evictions"
+        print(f"rank {rank} rcache_p2p: peak {peak} mappings, {ev} evictions", flush=True)
+    comm.barrier()
+    comm.destroy()
+    print(f"rank {rank} rcache_p2p OK", flush=True)
+
+
 def rcache(key, rank, size, dev):
     """the bounded peer-mapping cache (RCACHE_MAX_MAPS, mpool/rgpusm's LRU): 64 distinct allocations
     per rank, each one a 1 MiB allreduce's input and output, then freed and 64 more -- the open
@@ -1269,6 +1306,8 @@ def _main():
         return vote_dead(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "rcache":
         return rcache(key, rank, size, dev)
+    if len(sys.argv) > 5 and sys.argv[5] == "rcache_p2p":
+        return rcache_p2p(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "token_hold":
         return token_hold(key, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "token_check":

@@ -179,6 +179,14 @@ def test_bounded_peer_mapping_cache(gpu):
     print(next(line for line in outs[0].splitlines() if "rcache:" in line))
 
 
+def test_bounded_peer_mapping_cache_p2p_only(gpu):
+    """the bound holds in a point-to-point-only phase (the LRU clock ticks on every use),
+    evicted mappings are opened again when their buffer comes back, payloads exact
+    (ipc_worker.py::rcache_p2p)"""
+    outs = _run_mode(gpu, "rcache_p2p", 2)
+    print(next(line for line in outs[1].splitlines() if "rcache_p2p:" in line))
+
+
 @pytest.mark.xfail(strict=False, reason="ROCm 7.2 IPC under allocation churn (DESIGN.md §9): the first call after every "
                    "rank freed its 64 exported allocations at once (torch.cuda.empty_cache) has read a third rank's "
                    "buffer in about one run of five even with the close window and the dmabuf route")
