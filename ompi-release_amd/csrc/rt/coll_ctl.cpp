@@ -362,26 +362,17 @@ int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t s
         // its slot before every rank has read this exchange's slots
         return barrier(c);
     }
-    static const bool turns = getenv("MI355X_IMPORT_TURNS") && atoi(getenv("MI355X_IMPORT_TURNS")) > 0;
-    for (int t = 0; t < (turns ? c->size : 1); ++t) {
-        if (!turns || t == c->rank) {
-            for (int r = 0; r < c->size; ++r) {
-                RankSlot &o = c->ctrl->slot[r];
-                for (int b = 0; b < nbuf; ++b) {
-                    if (r == c->rank) {
-                        peers[b][r] = const_cast<void *>(mine[b]);
-                    } else {
-                        PeerMap *pm = nullptr;
-                        rc = map_peer(c, r, o.buf[b], &peers[b][r], &pm);
-                        if (rc) return rc;
-                        if (persistent && pm) pm->persistent = true;
-                    }
-                }
+    for (int r = 0; r < c->size; ++r) {
+        RankSlot &o = c->ctrl->slot[r];
+        for (int b = 0; b < nbuf; ++b) {
+            if (r == c->rank) {
+                peers[b][r] = const_cast<void *>(mine[b]);
+            } else {
+                PeerMap *pm = nullptr;
+                rc = map_peer(c, r, o.buf[b], &peers[b][r], &pm);
+                if (rc) return rc;
+                if (persistent && pm) pm->persistent = true;
             }
-        }
-        if (turns) {
-            rc = barrier(c);
-            if (rc) return rc;
         }
     }
     return MI355X_SUCCESS;

@@ -1184,8 +1184,6 @@ def rcache(key, rank, size, dev):
     bound = int(os.environ.get("RCACHE_BOUND", "16"))  # (experiments: 0 = unbounded)
     comm.set("RCACHE_MAX_MAPS", bound)
     assert comm.get("RCACHE_MAX_MAPS") == bound
-    if os.environ.get("RCACHE_IPC_MAX"):  # (experiment: every allocation through the dmabuf route)
-        comm.set("IPC_MAX_BYTES", int(os.environ["RCACHE_IPC_MAX"]))
     n = (1 << 20) // 4
     peak = 0
     for rnd in range(int(os.environ.get("RCACHE_ROUNDS", "2"))):
@@ -1201,18 +1199,11 @@ def rcache(key, rank, size, dev):
             comm.allreduce(x.data_ptr(), y.data_ptr(), n, pkg.T["FLOAT"], pkg.OP["SUM"])
             want = sum(m * 256 ** r for r in range(size))
             bad = (y[:n] != want).nonzero()
-            if bad.numel() or (os.environ.get("MI355X_DEBUG") and rnd == 1 and k == 0):
-                got = int(y[int(bad[0]) if bad.numel() else 0].item())
+            if bad.numel():
+                got = int(y[int(bad[0])].item())
                 print("rcache: wrong sum", rnd, k, "per-rank m:", [(got >> (8 * r)) & 255 for r in range(size)],
                       "want", m, "bad", bad.numel(), "alg", comm.last_algorithm(), "maps", comm.get("PEER_MAPS"),
                       hex(x.data_ptr()), hex(y.data_ptr()), flush=True)
-                fds = {}
-                for f in os.listdir("/proc/self/fd"):
-                    try:
-                        fds[int(f)] = os.readlink(f"/proc/self/fd/{f}")
-                    except OSError:
-                        pass
-                print("rcache: pid", os.getpid(), "fds", sorted(fds.items()), flush=True)
             assert bad.numel() == 0, ("rcache allreduce", rnd, k)
             peak = max(peak, comm.get("PEER_MAPS"))
             keep += [x, y]
