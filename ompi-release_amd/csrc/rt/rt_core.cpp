@@ -5,6 +5,7 @@
 // dlopen'ed, because this library only exists on a ROCm node.
 #include "rt_internal.hpp"
 
+#include <hsa/hsa_ext_amd.h>
 #include <pthread.h>
 #include <unistd.h>
 
@@ -149,8 +150,7 @@ int mi355x_memset_async(void *dst, int value, size_t bytes, void *stream)
 // threshold, MPI_Reduce_local's and coll/tuned's small temporaries among them -- and the calling
 // thread's stack.  Both are ordinary anonymous mappings the process owns; the HIP runtime places
 // device allocations in mappings of its own, never inside them, so the answer is exact.  Every
-// other pointer (mmap'd host buffers, device memory) takes hipPointerGetAttributes (~0.1 us on
-// MI355X, profiles/r05_op_host_overhead.jsonl).
+// other pointer (mmap'd host buffers, device memory) asks the runtime (rocr_unknown below).
 namespace mi355x {
 static uintptr_t heap_start()
 {
@@ -195,11 +195,27 @@ static bool known_host(const void *p)
 }
 } // namespace mi355x
 
+// Memory ROCr has no record of is ordinary host memory: every device allocation of the process --
+// hipMalloc, pools, uncached / fine-grained, IPC and dmabuf imports, VMM mappings (PyTorch's
+// expandable segments) -- is a ROCr allocation it can name.  hsa_amd_pointer_info answers that in
+// ~42 ns where hipPointerGetAttributes takes ~100 (profiles/r05_ptrinfo.jsonl: VMM-mapped device
+// memory reports type 6, managed 5, hipMalloc / hipHostMalloc 1, unregistered host 0); pointers ROCr
+// does know still go to HIP for its exact memory type.  Before the runtime is initialised the call
+// fails and HIP (which initialises it) answers.
+static bool rocr_unknown(const void *p)
+{
+    hsa_amd_pointer_info_t info;
+    std::memset(&info, 0, sizeof(info));
+    info.size = sizeof(info);
+    return hsa_amd_pointer_info(p, &info, nullptr, nullptr, nullptr) == HSA_STATUS_SUCCESS &&
+           info.type == HSA_EXT_POINTER_TYPE_UNKNOWN;
+}
+
 int mi355x_ptr_is_device(const void *p, int *is_device)
 {
     if (!is_device) return set_error(MI355X_ERR_ARG, "is_device is NULL");
     *is_device = 0;
-    if (!p || known_host(p)) return MI355X_SUCCESS;
+    if (!p || known_host(p) || rocr_unknown(p)) return MI355X_SUCCESS;
     hipPointerAttribute_t attr;
     std::memset(&attr, 0, sizeof(attr));
     hipError_t e = hipPointerGetAttributes(&attr, p);
