@@ -244,7 +244,10 @@ enum mi355x_knob {
                                            1) 1: the device setup self-tests the cross-device flows and turns a
                                            flow that failed on any rank off on every rank; 0: trusts them.  Only
                                            a value set before the device setup takes effect. */
-    MI355X_KNOB_PIPE_CALLS = 41         /* (read-only) allreduces served by the pipelined flow */
+    MI355X_KNOB_PIPE_CALLS = 41,        /* (read-only) allreduces served by the pipelined flow */
+    MI355X_KNOB_EXPORT_MISMATCHES = 42  /* (read-only) new dmabuf exports of the bounded peer-mapping cache that
+                                           named another buffer object (checked, that call staged instead;
+                                           env MI355X_EXPORT_CHECK=0 turns the check off) */
 };
 /* cross-device flows (MI355X_KNOB_FLOWS) */
 enum mi355x_flow {

@@ -265,7 +265,7 @@ KNOB = {"ALLREDUCE_ALG": 1, "REDUCE_ALG": 2, "REDUCE_SCATTER_ALG": 3, "BLOCKS_PE
         "RCACHE_EVICTIONS": 28, "FLOWS": 29, "FLOWS_FAILED": 30, "CREATE_US": 31, "SELFTEST_US": 32,
         "SVC_OWNER": 33, "SVC_CLAIMS": 34, "SVC_IDLE_US": 35,
         "SVC_SHRINK_US": 36, "SVC_REGROWS": 37, "DEV_SETUP": 38, "SETUP_US": 39, "SELFTEST": 40,
-        "PIPE_CALLS": 41}
+        "PIPE_CALLS": 41, "EXPORT_MISMATCHES": 42}
 FLOW = {"SVC_LL": 1, "SVC_PULL": 2, "SVC_COPY": 4, "SVC_RS": 8, "PIPE": 16}
 # coll/tuned COLLTYPE ids (coll_tuned.h:41-58)
 COLL = {"ALLGATHER": 0, "ALLREDUCE": 2, "BCAST": 7, "REDUCE": 11, "REDUCESCATTER": 12}

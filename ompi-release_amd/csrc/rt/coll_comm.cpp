@@ -82,6 +82,7 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     c->device = device;
     c->timeout_s = env_double("MI355X_TIMEOUT_S", 600.0);
     c->selftest = env_double("MI355X_SELFTEST", 1.0) != 0.0;
+    c->export_check = env_double("MI355X_EXPORT_CHECK", 1.0) != 0.0;
     c->shm_name = std::string("/mi355x_") + key;
     for (char &ch : c->shm_name)
         if (ch != '/' && !isalnum((unsigned char)ch) && ch != '_' && ch != '-') ch = '_';
@@ -414,6 +415,7 @@ int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
     case MI355X_KNOB_DEV_SETUP: *value = c->dev_ready ? 1 : 0; break;
     case MI355X_KNOB_SELFTEST: *value = c->selftest ? 1 : 0; break;
     case MI355X_KNOB_PIPE_CALLS: *value = (long)c->pipe_calls; break;
+    case MI355X_KNOB_EXPORT_MISMATCHES: *value = (long)c->export_mismatches; break;
     case MI355X_KNOB_SETUP_US: *value = (long)c->setup_us; break;
     case MI355X_KNOB_SVC_OWNER: *value = c->svc_ok ? 1 : 0; break;
     case MI355X_KNOB_SVC_CLAIMS: *value = (long)c->svc_epoch; break;

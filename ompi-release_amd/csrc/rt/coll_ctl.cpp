@@ -171,6 +171,50 @@ static bool via_dmabuf(const mi355x_comm *c, size_t bytes)
     return bytes >= c->ipc_max || ((c->rcache_max_maps || c->rcache_limit) && c->dmabuf_state != -1);
 }
 
+// does the dmabuf fd `fd` name the allocation [base, base + bytes)?  Imports it here and compares
+// 16 bytes at three offsets with the allocation itself (the allocation's own contents: a wrong
+// buffer object reads differently unless both hold the same bytes there).  1 yes, 0 no, -1 the
+// import itself failed (unknown).
+static int export_names(void *base, size_t bytes, int fd)
+{
+    const int mine = fcntl(fd, F_DUPFD_CLOEXEC, 0);
+    if (mine < 0) return -1;
+    hipExternalMemoryHandleDesc hd;
+    std::memset(&hd, 0, sizeof(hd));
+    hd.type = hipExternalMemoryHandleTypeOpaqueFd;
+    hd.handle.fd = mine;
+    hd.size = bytes;
+    hipExternalMemory_t ext = nullptr;
+    if (hipImportExternalMemory(&ext, &hd) != hipSuccess) {
+        (void)hipGetLastError();
+        close(mine);
+        return -1;
+    }
+    hipExternalMemoryBufferDesc bd;
+    std::memset(&bd, 0, sizeof(bd));
+    bd.size = bytes;
+    void *m = nullptr;
+    int same = -1;
+    if (hipExternalMemoryGetMappedBuffer(&m, ext, &bd) == hipSuccess) {
+        same = 1;
+        const size_t offs[3] = {0, (bytes / 2) & ~(size_t)15, bytes >= 16 ? bytes - 16 : 0};
+        for (size_t o : offs) {
+            unsigned char a[16], b[16];
+            const size_t n = bytes < 16 ? bytes : 16;
+            if (hipMemcpy(a, (char *)base + o, n, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(b, (char *)m + o, n, hipMemcpyDeviceToHost) != hipSuccess) {
+                same = -1;
+                break;
+            }
+            if (std::memcmp(a, b, n) != 0) same = 0;
+        }
+        (void)hipFree(m);
+    }
+    (void)hipGetLastError();
+    (void)hipDestroyExternalMemory(ext);
+    return same;
+}
+
 int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
 {
     std::lock_guard<std::recursive_mutex> reg_guard(c->reg_mtx);
@@ -230,6 +274,15 @@ int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
         if (hipMemGetHandleForAddressRange(&reg.fd, (hipDeviceptr_t)base, sz, hipMemRangeHandleTypeDmaBufFd, 0) !=
             hipSuccess) {
             (void)hipGetLastError();
+            reg.fd = -1;
+            dm = false;
+        } else if (c->export_check && export_names(base, sz, reg.fd) == 0) {
+            // the fd names another range: the runtime exports the whole buffer object an allocation
+            // was carved from (small allocations share one), from its start -- such an allocation
+            // keeps the hipIpc route (whose handle carries the offset)
+            c->export_mismatches++;
+            TRACE(c, "dmabuf export of %p names another range: hipIpc route", base);
+            close(reg.fd);
             reg.fd = -1;
             dm = false;
         }

@@ -1211,6 +1211,7 @@ def rcache(key, rank, size, dev):
         del keep, x, y
         torch.cuda.empty_cache()
     ev = comm.get("RCACHE_EVICTIONS")
+    print(f"rank {rank} rcache export mismatches: {comm.get('EXPORT_MISMATCHES')}", flush=True)
     assert peak <= 16, f"{peak} peer mappings open under a bound of 16"
     assert ev > 0, "no evictions"
     print(f"rank {rank} rcache: peak {peak} mappings, {ev} evictions", flush=True)
