@@ -38,6 +38,26 @@ uint64_t pid_namespace();
 int barrier(mi355x_comm *c);
 uint64_t buffer_id(const void *p);
 int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force);
+// the stream a collective runs on, for the setup work it triggers (device setup, dmabuf probe, LL
+// resync): ordered with the call's own work and never a stream of its own -- a second stream per
+// process is a second hardware queue, and eight processes sharing one GPU then time-slice their
+// queues: the 8-rank 1 GiB allreduce rehearsal took 22.9 ms per call instead of 3.7 while every
+// rank held an idle setup stream (profiles/r05_setup_stream_bisect.txt)
+struct CallStream {
+    mi355x_comm *c;
+    hipStream_t prev;
+    CallStream(mi355x_comm *c_, hipStream_t s) : c(c_), prev(c_->call_s)
+    {
+        c->call_s = s;  // (NULL is the null stream: call_depth says whether call_s is set)
+        c->call_depth++;
+    }
+    ~CallStream()
+    {
+        c->call_depth--;
+        c->call_s = prev;
+    }
+};
+
 void retire_map(mi355x_comm *c, const PeerMap &m);
 void flush_retired(mi355x_comm *c);
 int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t sig[4],

@@ -515,9 +515,16 @@ int setup_done_words(mi355x_comm *c)
 // The engine's own stream for setup-time fills and copies: a non-blocking stream, so setup never
 // waits for -- or makes wait -- the application's streams (no hipDeviceSynchronize anywhere on the
 // setup paths); nullptr when it cannot be created (the caller's error path reports the HIP error).
+// the stream setup work runs on: inside a collective its own stream (CallStream), else a stream of
+// the communicator's own, made on first use (the null stream if that fails: still correct, it
+// only orders with more of the device's work)
 hipStream_t setup_stream(mi355x_comm *c)
 {
-    if (!c->setup_s && hipStreamCreateWithFlags(&c->setup_s, hipStreamNonBlocking) != hipSuccess) c->setup_s = nullptr;
+    if (c->call_depth > 0) return c->call_s;
+    if (!c->setup_s && hipStreamCreateWithFlags(&c->setup_s, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        c->setup_s = nullptr;
+    }
     return c->setup_s;
 }
 

@@ -376,7 +376,7 @@ int probe_dmabuf(mi355x_comm *c)
     RankSlot &me = c->ctrl->slot[c->rank];
     if (ok && hipMalloc(&buf, sz) != hipSuccess) ok = false;
     hipStream_t ss = setup_stream(c);
-    if (ok && (!ss || hipMemsetAsync(buf, c->rank + 1, sz, ss) != hipSuccess)) ok = false;
+    if (ok && hipMemsetAsync(buf, c->rank + 1, sz, ss) != hipSuccess) ok = false;
     if (ok && hipStreamSynchronize(ss) != hipSuccess) ok = false;
     if (ok && hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)buf, sz, hipMemRangeHandleTypeDmaBufFd, 0) != hipSuccess)
         ok = false;

@@ -48,8 +48,9 @@ int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count,
     int rc = check_common(c, op, type);
     if (rc) return rc;
     if (count == 0) return MI355X_SUCCESS;
-    if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     hipStream_t s = resolve_stream(stream);
+    CallStream call_stream(c, s);  // (the setup work of this call, if any, runs on its stream)
+    if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     if (!coll_slot_supported(op, type)) {  // (no fold kernel carries the slot: gather-then-fold, coll_gfold.cpp)
         c->last_alg = 1;
         return gather_fold(c, sbuf ? sbuf : rbuf, count, type, op, 0, count, -1, rbuf, s);
@@ -273,8 +274,9 @@ int reduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, in
     if (root < 0 || root >= c->size) return set_error(MI355X_ERR_ARG, "bad root");
     if (!sbuf && c->rank != root) return set_error(MI355X_ERR_ARG, "MPI_IN_PLACE is only valid at the root");
     if (count == 0) return MI355X_SUCCESS;
-    if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     hipStream_t s = resolve_stream(stream);
+    CallStream call_stream(c, s);  // (the setup work of this call, if any, runs on its stream)
+    if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     if (!coll_slot_supported(op, type)) {  // (no fold kernel carries the slot: gather-then-fold, coll_gfold.cpp)
         c->last_alg = 1;
         return gather_fold(c, sbuf ? sbuf : rbuf, count, type, op, 0, count, -1, c->rank == root ? rbuf : nullptr, s);
@@ -373,8 +375,9 @@ int reduce_scatter_block_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, si
     if (rc) return rc;
     const size_t count = rcount * (size_t)c->size;
     if (count == 0) return MI355X_SUCCESS;
-    if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     hipStream_t s = resolve_stream(stream);
+    CallStream call_stream(c, s);  // (the setup work of this call, if any, runs on its stream)
+    if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     if (!coll_slot_supported(op, type)) {  // (no fold kernel carries the slot: gather-then-fold, coll_gfold.cpp)
         c->last_alg = 1;
         return gather_fold(c, sbuf ? sbuf : rbuf, count, type, op, (size_t)c->rank * rcount, rcount, -1, rbuf, s);
@@ -443,8 +446,9 @@ int reduce_scatter_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, const in
     }
     const size_t count = disp[c->size];
     if (count == 0) return MI355X_SUCCESS;
-    if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     hipStream_t s = resolve_stream(stream);
+    CallStream call_stream(c, s);  // (the setup work of this call, if any, runs on its stream)
+    if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     if (!coll_slot_supported(op, type)) {  // (no fold kernel carries the slot: gather-then-fold, coll_gfold.cpp)
         c->last_alg = 1;
         return gather_fold(c, sbuf ? sbuf : rbuf, count, type, op, disp[c->rank], (size_t)rcounts[c->rank], -1, rbuf, s);
@@ -529,8 +533,9 @@ int allgather_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t bytes,
 {
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     if (bytes == 0) return MI355X_SUCCESS;
-    if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     hipStream_t s = resolve_stream(stream);
+    CallStream call_stream(c, s);  // (the setup work of this call, if any, runs on its stream)
+    if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     const void *src = sbuf ? sbuf : (const char *)rbuf + (size_t)c->rank * bytes;
     int rc0 = svc_maybe_claim(c, bytes <= std::max(c->svc_max, c->svc_copy_max));
     if (rc0) return rc0;
@@ -596,8 +601,9 @@ int bcast_impl(mi355x_comm_t *c, void *buf, size_t bytes, int root, void *stream
     if (!c) return set_error(MI355X_ERR_ARG, "comm is NULL");
     if (root < 0 || root >= c->size) return set_error(MI355X_ERR_ARG, "bad root");
     if (bytes == 0 || c->size == 1) return MI355X_SUCCESS;
-    if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     hipStream_t s = resolve_stream(stream);
+    CallStream call_stream(c, s);  // (the setup work of this call, if any, runs on its stream)
+    if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     int rc0 = svc_maybe_claim(c, bytes <= std::max(c->svc_max, c->svc_copy_max));
     if (rc0) return rc0;
     if (ll_usable(c, bytes)) {

@@ -83,7 +83,6 @@ int ensure_ll(mi355x_comm *c)
     c->ll_base = nullptr;
     MI_HIP(hipExtMallocWithFlags((void **)&c->ll_base, total, hipDeviceMallocUncached));
     hipStream_t ss = setup_stream(c);
-    if (!ss) return set_error(MI355X_ERR_HIP, "rank %d: cannot create the setup stream", c->rank);
     MI_HIP(hipMemsetAsync(c->ll_base, 0, total, ss));
     if (!c->ll_ctr) MI_HIP(hipMalloc((void **)&c->ll_ctr, sizeof(uint64_t)));
     MI_HIP(hipMemsetAsync(c->ll_ctr, 0, sizeof(uint64_t), ss));
@@ -174,7 +173,7 @@ int ll_selftest(mi355x_comm *c)
     const size_t per = std::min<size_t>(8192, c->ll_slot), n = (size_t)c->size;
     char *buf = nullptr;
     hipStream_t ss = setup_stream(c);
-    bool ok = ss && hipMalloc((void **)&buf, per * (n + 1)) == hipSuccess;
+    bool ok = hipMalloc((void **)&buf, per * (n + 1)) == hipSuccess;
     if (ok) ok = hipMemsetAsync(buf, c->rank + 1, per, ss) == hipSuccess &&
                  hipMemsetAsync(buf + per, 0, per * n, ss) == hipSuccess && hipStreamSynchronize(ss) == hipSuccess;
     if (ok) {

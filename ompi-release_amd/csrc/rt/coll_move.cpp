@@ -57,6 +57,7 @@ static int gatherv_impl(mi355x_comm *c, const void *sbuf, size_t sbytes, void *r
     if (am_root && (!rcounts || !displs)) return set_error(MI355X_ERR_ARG, "gatherv: counts at the root are NULL");
     if (!am_root && !sbuf && sbytes) return set_error(MI355X_ERR_ARG, "MPI_IN_PLACE is only valid at the root");
     hipStream_t s = resolve_stream(stream);
+    CallStream call_stream(c, s);
     MI_HIP(hipStreamSynchronize(s));
     c->ctrl->slot[c->rank].varg[0] = (int64_t)(sbuf ? sbytes : 0);
     const void *mine[1] = {sbytes ? sbuf : nullptr};
@@ -92,6 +93,7 @@ static int scatterv_impl(mi355x_comm *c, const void *sbuf, const size_t *scounts
     if (am_root && (!scounts || !displs)) return set_error(MI355X_ERR_ARG, "scatterv: counts at the root are NULL");
     if (!am_root && !rbuf && rbytes) return set_error(MI355X_ERR_ARG, "MPI_IN_PLACE is only valid at the root");
     hipStream_t s = resolve_stream(stream);
+    CallStream call_stream(c, s);
     MI_HIP(hipStreamSynchronize(s));
     bool any = false;
     if (am_root)
@@ -130,6 +132,7 @@ static int allgatherv_impl(mi355x_comm *c, const void *sbuf, size_t sbytes, void
     if (rc) return rc;
     if (!rcounts || !displs) return set_error(MI355X_ERR_ARG, "allgatherv: counts are NULL");
     hipStream_t s = resolve_stream(stream);
+    CallStream call_stream(c, s);
     MI_HIP(hipStreamSynchronize(s));
     const int me = c->rank;
     const void *src = sbuf ? sbuf : (const char *)rbuf + displs[me];
@@ -163,6 +166,7 @@ static int alltoallv_impl(mi355x_comm *c, const void *sbuf, const size_t *scount
     if (!rcounts || !rdispls || (sbuf && (!scounts || !sdispls)))
         return set_error(MI355X_ERR_ARG, "alltoallv: counts are NULL");
     hipStream_t s = resolve_stream(stream);
+    CallStream call_stream(c, s);
     const int n = c->size, me = c->rank;
     const void *src = sbuf;
     if (!sbuf) {
@@ -216,6 +220,7 @@ static int scan_impl(mi355x_comm *c, const void *sbuf, void *rbuf, size_t count,
     if (c->size > kMaxRanks) return set_error(MI355X_ERR_UNSUPPORTED, "communicator larger than %d ranks", kMaxRanks);
     if (count == 0) return MI355X_SUCCESS;
     hipStream_t s = resolve_stream(stream);
+    CallStream call_stream(c, s);
     const size_t esz = mi355x_type_size(type);
     const int me = c->rank;
     const void *in = sbuf ? sbuf : rbuf;

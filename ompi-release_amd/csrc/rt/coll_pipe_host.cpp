@@ -52,7 +52,6 @@ int ensure_pipe(mi355x_comm *c)
     const size_t bytes = (n * kPipeKmax * sizeof(uint64_t) + 4095) / 4096 * 4096;
     MI_HIP(hipExtMallocWithFlags((void **)&c->pipe_base, bytes, hipDeviceMallocUncached));
     hipStream_t ss = setup_stream(c);
-    if (!ss) return set_error(MI355X_ERR_HIP, "rank %d: cannot create the setup stream", c->rank);
     MI_HIP(hipMemsetAsync(c->pipe_base, 0, bytes, ss));
     MI_HIP(hipMalloc((void **)&c->pipe_queue, sizeof(uint64_t)));
     MI_HIP(hipMemsetAsync(c->pipe_queue, 0, sizeof(uint64_t), ss));

@@ -96,12 +96,12 @@ struct SelfTest {
     char *in = nullptr, *out = nullptr;
     size_t cap = 0;
     bool ok = true;
-    hipStream_t s = nullptr;  // the engine's setup stream: the application's streams are never waited for
+    hipStream_t s = nullptr;  // setup_stream: the stream of the collective that runs the self-test
     SelfTest(mi355x_comm *c_, uint64_t salt, size_t bytes) : c(c_), cap(bytes)
     {
         seed = c->ctrl->secret ^ (salt * 0x632be59bd9b4e019ull);
         s = setup_stream(c);
-        ok = s && hipMalloc((void **)&in, cap) == hipSuccess && hipMalloc((void **)&out, cap) == hipSuccess;
+        ok = hipMalloc((void **)&in, cap) == hipSuccess && hipMalloc((void **)&out, cap) == hipSuccess;
     }
     ~SelfTest()
     {

@@ -493,7 +493,6 @@ int ll_resync(mi355x_comm *c)
     if (rc) return rc;
     if (c->svc_stuck) return set_error(MI355X_ERR_HIP, "rank %d: the resident service did not leave", c->rank);
     hipStream_t ss = setup_stream(c);
-    if (!ss) return set_error(MI355X_ERR_HIP, "rank %d: cannot create the setup stream", c->rank);
     MI_HIP(hipMemsetAsync(c->ll_base, 0, c->ll_bytes, ss));
     MI_HIP(hipMemsetAsync(c->ll_ctr, 0, sizeof(uint64_t), ss));
     MI_HIP(hipStreamSynchronize(ss));

@@ -266,6 +266,8 @@ struct mi355x_comm {
     // mappings evicted during a call's mapping phase: closed in the next exchange's close window,
     // never while a peer exports or imports (coll_rcache.cpp: retire_map)
     std::vector<mi355x::PeerMap> retired_maps;
+    hipStream_t call_s = nullptr;     // the stream of the collective in progress (CallStream): setup work uses it
+    int call_depth = 0;               // collectives in progress on this thread of control (call_s valid when > 0)
     bool export_check = true;         // verify each new dmabuf export of the bounded cache (MI355X_EXPORT_CHECK=0: off)
     uint64_t export_mismatches = 0;   // exports that named another buffer object
     // peer-mapping cache bounds (MI355X_RCACHE_MAX_MAPS / MI355X_RCACHE_SIZE_LIMIT, knobs of the same
