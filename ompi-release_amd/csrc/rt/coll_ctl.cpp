@@ -175,7 +175,7 @@ static bool via_dmabuf(const mi355x_comm *c, size_t bytes)
 // 16 bytes at three offsets with the allocation itself (the allocation's own contents: a wrong
 // buffer object reads differently unless both hold the same bytes there).  1 yes, 0 no, -1 the
 // import itself failed (unknown).
-static int export_names(void *base, size_t bytes, int fd)
+static int export_names(void *base, size_t bytes, int fd, hipStream_t s)
 {
     const int mine = fcntl(fd, F_DUPFD_CLOEXEC, 0);
     if (mine < 0) return -1;
@@ -201,8 +201,9 @@ static int export_names(void *base, size_t bytes, int fd)
         for (size_t o : offs) {
             unsigned char a[16], b[16];
             const size_t n = bytes < 16 ? bytes : 16;
-            if (hipMemcpy(a, (char *)base + o, n, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(b, (char *)m + o, n, hipMemcpyDeviceToHost) != hipSuccess) {
+            if (hipMemcpyAsync(a, (char *)base + o, n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipMemcpyAsync(b, (char *)m + o, n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess) {
                 same = -1;
                 break;
             }
@@ -276,7 +277,7 @@ int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
             (void)hipGetLastError();
             reg.fd = -1;
             dm = false;
-        } else if (c->export_check && export_names(base, sz, reg.fd) == 0) {
+        } else if (c->export_check && export_names(base, sz, reg.fd, setup_stream(c)) == 0) {
             // the fd names another range: the runtime exports the whole buffer object an allocation
             // was carved from (small allocations share one), from its start -- such an allocation
             // keeps the hipIpc route (whose handle carries the offset)

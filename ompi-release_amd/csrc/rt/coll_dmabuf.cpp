@@ -225,7 +225,7 @@ int serve_fd(mi355x_comm *c, int peer, uint64_t id)
     m.from = c->rank;
     m.id[0] = id;
     for (const LocalReg &r : c->local_regs) {
-        if (r.id != id) continue;
+        if (r.id != id || r.has_h) continue;  // (an allocation on the hipIpc route never went out as a dmabuf)
         int fd = -1;
         if (hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)r.base, r.size, hipMemRangeHandleTypeDmaBufFd, 0) !=
             hipSuccess) {
