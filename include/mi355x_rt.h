@@ -150,8 +150,8 @@ enum mi355x_knob {
     MI355X_KNOB_LL_MAX_BYTES = 9,       /* per-rank message bytes up to which allreduce / allgather /
                                            bcast / reduce take the one-shot low-latency path (0 = never;
                                            default 0, or env MI355X_LL_MAX_BYTES; multi-process
-                                           communicators of <= 8 ranks whose creation-time self-test
-                                           passed -- otherwise the knob stays 0) */
+                                           communicators of <= 8 ranks whose LL self-test (device
+                                           setup) passed -- otherwise the knob stays 0) */
     MI355X_KNOB_TIME_PHASES = 11,       /* 1: time the two kernels of the direct allreduce with HIP
                                            events on the call's stream (mi355x_comm_phase_ms) */
     MI355X_KNOB_COPY_BLOCK_KIB = 12,    /* bytes per block of the pull-copy kernel, KiB (4..256, default 4) */
@@ -221,8 +221,8 @@ enum mi355x_knob {
                                            every rank (the host-synchronised flows take its calls) */
     MI355X_KNOB_FLOWS_FAILED = 30,      /* (read-only) the flows whose self-test failed on some rank */
     MI355X_KNOB_CREATE_US = 31,         /* (read-only) wall time of mi355x_comm_create, microseconds */
-    MI355X_KNOB_SELFTEST_US = 32,       /* (read-only) of which the flow self-tests at creation; plus the
-                                           service flows' self-test at the service's first claim */
+    MI355X_KNOB_SELFTEST_US = 32,       /* (read-only) the flow self-tests of the device setup (first device
+                                           collective); plus the service flows' self-test at its first claim */
     MI355X_KNOB_SVC_OWNER = 33,         /* (read-only) 1 while this communicator owns its process's
                                            resident service */
     MI355X_KNOB_SVC_CLAIMS = 34,        /* (read-only) times this communicator has taken the service */
@@ -258,7 +258,7 @@ enum mi355x_flow {
     MI355X_FLOW_PIPE = 16      /* pipelined allreduce (per-chunk flags written into the peers) */
 };
 int mi355x_comm_set(mi355x_comm_t *comm, int knob, long value);
-/* current value of a knob (LL_MAX_BYTES reads 0 when the creation-time LL self-test failed) */
+/* current value of a knob (LL_MAX_BYTES reads 0 when the device setup's LL self-test failed) */
 int mi355x_comm_get(const mi355x_comm_t *comm, int knob, long *value);
 /* device time of the last timed direct allreduce: phase 1 (k_fold, the owner's block from every
  * rank) and phase 2 (k_multicopy, the other blocks from their owners); with the pipelined flow
