@@ -155,6 +155,12 @@ def bench_op(args, pkg, torch):
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
     traffic, traffic_from = pmc_traffic("op_3buff_sum_float")
     u, bpc, nt = pkg.get_tune()
+    config = {"workload": "op/hip 3-buff MPI_SUM MPI_FLOAT, 1 GiB per operand (BASELINE configs[1])",
+              "count": n, "bytes_per_operand": n * 4, "launch": {"unroll": u, "blocks_per_cu": bpc,
+                                                                  "nontemporal": nt}}
+    if not args.no_sweep:
+        # the rest of configs[1] (every slot, both forms), timed after the headline's region
+        config["sweep"] = sweep_op(pkg, torch, a, b, o)
     return {
         "metric": "MPI_Allreduce busbw GB/s (1 GiB fp32, np=8) + op/hip reduce HBM GB/s",
         "value": round(value, 2),
@@ -168,15 +174,68 @@ def bench_op(args, pkg, torch):
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (torch.randn on device)",
-        "config": {"workload": "op/hip 3-buff MPI_SUM MPI_FLOAT, 1 GiB per operand (BASELINE configs[1])",
-                   "count": n, "bytes_per_operand": n * 4, "launch": {"unroll": u, "blocks_per_cu": bpc,
-                                                                      "nontemporal": nt}},
+        "config": config,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_from": traffic_from,
                      "kernel_avg_ms": round(avg_ms, 5),
                      "kernel_avg_from": "HIP events around the K launches / K" + (" (one HIP graph replay)" if graph is not None else ""),
                      "alg_bytes_per_launch": alg_bytes},
     }
+
+
+# 2 reads + 1 write cannot beat 3 / (2/6.9 + 1/6.2) TB/s on this machine: the measured read-only
+# and write-only stream rates (tools/op_ceiling.hip, profiles/r02_op_ceiling.jsonl)
+OP_CEILING_GBS = 6640.0
+
+
+def sweep_op(pkg, torch, a, b, o, reps: int = 5):
+    """BASELINE configs[1] as a whole: every op/hip GPU slot (op x predefined type), 2-buff and
+    3-buff, on 1 GiB per operand (the headline's buffers re-typed), after the headline's timed
+    region.  Per slot and form: one untimed launch, then `reps` launches between one HIP event pair
+    on the launch stream (span / reps).  Algorithmic bytes = 3 x 2^30 per launch for both forms
+    (2-buff: read in, read + write inout; op_base_functions.c:39-103 / 606-683)."""
+    s = torch.cuda.current_stream()
+    sh = s.cuda_stream
+    pa, pb, po = a.data_ptr(), b.data_ptr(), o.data_ptr()
+    nbytes = a.numel() * a.element_size()
+    rows = []
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for op in range(1, len(pkg.OPS)):
+        for ty in range(len(pkg.TYPES)):
+            if not pkg.op_supported(op, ty):
+                continue
+            n = nbytes // pkg.type_size(ty)
+            res = {}
+            for form in ("2buff", "3buff"):
+                if form == "3buff":
+                    f = lambda: pkg.op_reduce_3buff(op, ty, pa, pb, po, n, sh)
+                else:
+                    f = lambda: pkg.op_reduce(op, ty, pa, po, n, sh)
+                f()
+                e0.record(s)
+                for _ in range(reps):
+                    f()
+                e1.record(s)
+                e1.synchronize()
+                ms = e0.elapsed_time(e1) / reps
+                res[form] = round(3 * n * pkg.type_size(ty) / (ms * 1e-3) / 1e9, 1)
+            rows.append((pkg.OPS[op], pkg.TYPES[ty], pkg.type_size(ty), res["2buff"], res["3buff"]))
+
+    def summary(idx):
+        vals = sorted(r[idx] for r in rows)
+        worst = min(rows, key=lambda r: r[idx])
+        med = vals[len(vals) // 2] if len(vals) % 2 else 0.5 * (vals[len(vals) // 2 - 1] + vals[len(vals) // 2])
+        return {"min_GBps": vals[0], "median_GBps": round(med, 1), "max_GBps": vals[-1],
+                "worst": {"slot": f"{worst[0]}/{worst[1]}", "GBps": worst[idx],
+                          "frac_peak": round(worst[idx] / HBM_PEAK_GBS, 4),
+                          "frac_ceiling": round(worst[idx] / OP_CEILING_GBS, 4)},
+                "slots_below_0.90_ceiling": [f"{r[0]}/{r[1]}" for r in rows if r[idx] < 0.9 * OP_CEILING_GBS]}
+
+    return {"slots": len(rows), "bytes_per_operand": nbytes, "reps": reps,
+            "ceiling_2r1w_GBps": OP_CEILING_GBS, "ceiling_from": "profiles/r02_op_ceiling.jsonl",
+            "two_buff": summary(3), "three_buff": summary(4),
+            "table": {f"{r[0]}/{r[1]}": [r[3], r[4]] for r in rows},
+            "table_columns": ["GBps_2buff", "GBps_3buff"]}
 
 
 def _free_port() -> int:
@@ -215,6 +274,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", action="store_true", help="N = 1: replay the K timed launches as one HIP graph")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-sweep", action="store_true", help="N = 1: skip the configs[1] slot sweep")
     ap.add_argument("--no-legs", action="store_true", help="N > 1: skip the other configs' legs")
     ap.add_argument("--no-autotune", action="store_true",
                     help="N > 1: time the engine's default allreduce flow only (for profiling one configuration)")

@@ -267,6 +267,32 @@ static int stage(struct mca_coll_mi355x_module_t *m, int pack, void *buf, size_t
                 : mi355x_unpack(d, count, buf, 0, p, bytes, NULL, NULL);
 }
 
+/* stage() for a buffer that may be host memory: dense host layouts are copied, derived ones go
+ * through the host convertor (mi355x_pack_host / mi355x_unpack_host) and a host bounce buffer --
+ * the GPU convertor never touches host memory */
+static int xstage(struct mca_coll_mi355x_module_t *m, int pack, void *buf, size_t count, const struct ompi_datatype_t *dt,
+                  void *p, size_t bytes, int host)
+{
+    if (!host) return stage(m, pack, buf, count, dt, p, bytes);
+    size_t cb;
+    if (bytes == 0) return MI355X_SUCCESS;
+    if (contiguous_bytes_n(dt, count, &cb)) return pack ? mi355x_memcpy(p, buf, bytes) : mi355x_memcpy(buf, p, bytes);
+    mi355x_ddt_t *d = ddt_of(m, dt);
+    if (!d) return MI355X_ERR_UNSUPPORTED;
+    void *tmp = malloc(bytes);
+    if (!tmp) return MI355X_ERR_NOMEM;
+    int rc;
+    if (pack) {
+        rc = mi355x_pack_host(d, count, buf, 0, tmp, bytes);
+        if (rc == MI355X_SUCCESS) rc = mi355x_memcpy(p, tmp, bytes);
+    } else {
+        rc = mi355x_memcpy(tmp, p, bytes);
+        if (rc == MI355X_SUCCESS) rc = mi355x_unpack_host(d, count, buf, 0, tmp, bytes);
+    }
+    free(tmp);
+    return rc;
+}
+
 static int map_rc(int rc)
 {
     switch (rc) {
@@ -664,6 +690,9 @@ typedef struct {
     int n;
     char *base;
     mi355x_ddt_t *d;          /* NULL: dense, view == base */
+    int host;                 /* host memory (a rank joining a call whose peers hold device buffers):
+                                 the view is a device staging copy, moved by xstage */
+    const struct ompi_datatype_t *dt;
     char *view;
     size_t bytes[SIDE_MAX], off[SIDE_MAX], cnt[SIDE_MAX];
     ptrdiff_t udisp[SIDE_MAX];
@@ -691,13 +720,15 @@ static int side_init(mca_coll_mi355x_module_t *m, side_t *s, int slot, void *buf
         s->udisp[q] = dq * ext;
         next = dq + c;
     }
-    if (dense(dt)) {
+    s->dt = dt;
+    s->host = !is_dev(buf);
+    if (dense(dt) && !s->host) {
         s->view = s->base;
         for (int q = 0; q < n; ++q) s->off[q] = (size_t)s->udisp[q];
         return OMPI_SUCCESS;
     }
-    s->d = ddt_of(m, dt);
-    if (!s->d) {
+    s->d = dense(dt) ? NULL : ddt_of(m, dt);
+    if (!s->d && !dense(dt)) {
         fprintf(stderr, "[coll/mi355x] the GPU convertor cannot describe datatype %s\n", dt->name);
         return OMPI_ERR_NOT_SUPPORTED;
     }
@@ -711,22 +742,23 @@ static int side_init(mca_coll_mi355x_module_t *m, side_t *s, int slot, void *buf
 }
 
 /* piece q (or every piece, q < 0): user layout -> view (pack) or view -> user layout (unpack) */
-static int side_move(side_t *s, int q, int pack)
+static int side_move(mca_coll_mi355x_module_t *m, side_t *s, int q, int pack)
 {
-    if (!s->d) return MI355X_SUCCESS;
+    if (!s->d && !s->host) return MI355X_SUCCESS;
     for (int p = (q < 0 ? 0 : q); p < (q < 0 ? s->n : q + 1); ++p) {
         if (!s->bytes[p]) continue;
-        int rc = pack ? mi355x_pack(s->d, s->cnt[p], s->base + s->udisp[p], 0, s->view + s->off[p], s->bytes[p], NULL, NULL)
-                      : mi355x_unpack(s->d, s->cnt[p], s->base + s->udisp[p], 0, s->view + s->off[p], s->bytes[p], NULL, NULL);
+        int rc = s->host ? xstage(m, pack, s->base + s->udisp[p], s->cnt[p], s->dt, s->view + s->off[p], s->bytes[p], 1)
+                 : pack ? mi355x_pack(s->d, s->cnt[p], s->base + s->udisp[p], 0, s->view + s->off[p], s->bytes[p], NULL, NULL)
+                        : mi355x_unpack(s->d, s->cnt[p], s->base + s->udisp[p], 0, s->view + s->off[p], s->bytes[p], NULL, NULL);
         if (rc) return rc;
     }
     return MI355X_SUCCESS;
 }
 
-static int finish_unpack(side_t *s, int rc)
+static int finish_unpack(mca_coll_mi355x_module_t *m, side_t *s, int rc)
 {
-    if (rc == MI355X_SUCCESS && s && s->d) {
-        rc = side_move(s, -1, 0);
+    if (rc == MI355X_SUCCESS && s && (s->d || s->host)) {
+        rc = side_move(m, s, -1, 0);
         if (rc == MI355X_SUCCESS) rc = mi355x_stream_sync(NULL);
     }
     return map_rc(rc);
@@ -738,17 +770,19 @@ int mca_coll_mi355x_gather(void *sbuf, int scount, struct ompi_datatype_t *sdtyp
 {
     mca_coll_mi355x_module_t *m = MOD(module);
     const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm), inplace = (sbuf == MPI_IN_PLACE);
-    if ((me == root && !is_dev(rbuf)) || (!inplace && !is_dev(sbuf)) || (inplace && me != root))
+    if (inplace && me != root)
         return m->prev_gather(sbuf, scount, sdtype, rbuf, rcount, rdtype, root, comm, m->prev_gather_module);
+    const int dev = (me != root || is_dev(rbuf)) && (inplace || is_dev(sbuf));
+    ROUTE_OR(m->prev_gather(sbuf, scount, sdtype, rbuf, rcount, rdtype, root, comm, m->prev_gather_module));
     side_t snd, rcv;
     int rc = OMPI_SUCCESS;
     if (!inplace && (rc = side_init(m, &snd, 0, sbuf, sdtype, 1, NULL, scount, NULL))) return rc;
     if (me == root && (rc = side_init(m, &rcv, 1, rbuf, rdtype, n, NULL, rcount, NULL))) return rc;
     const size_t bytes = inplace ? rcv.bytes[me] : snd.bytes[0];
-    int erc = inplace ? side_move(&rcv, me, 1) : side_move(&snd, 0, 1);
+    int erc = inplace ? side_move(m, &rcv, me, 1) : side_move(m, &snd, 0, 1);
     if (erc == MI355X_SUCCESS)
         erc = mi355x_gather(m->engine, inplace ? NULL : snd.view, me == root ? rcv.view : NULL, bytes, root, NULL);
-    return finish_unpack(me == root ? &rcv : NULL, erc);
+    return finish_unpack(m, me == root ? &rcv : NULL, erc);
 }
 
 int mca_coll_mi355x_gatherv(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int *rcounts,
@@ -757,18 +791,20 @@ int mca_coll_mi355x_gatherv(void *sbuf, int scount, struct ompi_datatype_t *sdty
 {
     mca_coll_mi355x_module_t *m = MOD(module);
     const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm), inplace = (sbuf == MPI_IN_PLACE);
-    if (n > SIDE_MAX || (me == root && !is_dev(rbuf)) || (!inplace && !is_dev(sbuf)) || (inplace && me != root))
+    if (n > SIDE_MAX || (inplace && me != root))
         return m->prev_gatherv(sbuf, scount, sdtype, rbuf, rcounts, disps, rdtype, root, comm, m->prev_gatherv_module);
+    const int dev = (me != root || is_dev(rbuf)) && (inplace || is_dev(sbuf));
+    ROUTE_OR(m->prev_gatherv(sbuf, scount, sdtype, rbuf, rcounts, disps, rdtype, root, comm, m->prev_gatherv_module));
     side_t snd, rcv;
     int rc = OMPI_SUCCESS;
     if (!inplace && (rc = side_init(m, &snd, 0, sbuf, sdtype, 1, NULL, scount, NULL))) return rc;
     if (me == root && (rc = side_init(m, &rcv, 1, rbuf, rdtype, n, rcounts, 0, disps))) return rc;
-    int erc = inplace ? side_move(&rcv, me, 1) : side_move(&snd, 0, 1);
+    int erc = inplace ? side_move(m, &rcv, me, 1) : side_move(m, &snd, 0, 1);
     if (erc == MI355X_SUCCESS)
         erc = mi355x_gatherv(m->engine, inplace ? NULL : snd.view, inplace ? 0 : snd.bytes[0],
                              me == root ? rcv.view : NULL, me == root ? rcv.bytes : NULL,
                              me == root ? rcv.off : NULL, root, NULL);
-    return finish_unpack(me == root ? &rcv : NULL, erc);
+    return finish_unpack(m, me == root ? &rcv : NULL, erc);
 }
 
 int mca_coll_mi355x_scatter(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
@@ -777,17 +813,19 @@ int mca_coll_mi355x_scatter(void *sbuf, int scount, struct ompi_datatype_t *sdty
 {
     mca_coll_mi355x_module_t *m = MOD(module);
     const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm), inplace = (rbuf == MPI_IN_PLACE);
-    if ((me == root && !is_dev(sbuf)) || (!inplace && !is_dev(rbuf)) || (inplace && me != root))
+    if (inplace && me != root)
         return m->prev_scatter(sbuf, scount, sdtype, rbuf, rcount, rdtype, root, comm, m->prev_scatter_module);
+    const int dev = (me != root || is_dev(sbuf)) && (inplace || is_dev(rbuf));
+    ROUTE_OR(m->prev_scatter(sbuf, scount, sdtype, rbuf, rcount, rdtype, root, comm, m->prev_scatter_module));
     side_t snd, rcv;
     int rc = OMPI_SUCCESS;
     if (me == root && (rc = side_init(m, &snd, 0, sbuf, sdtype, n, NULL, scount, NULL))) return rc;
     if (!inplace && (rc = side_init(m, &rcv, 1, rbuf, rdtype, 1, NULL, rcount, NULL))) return rc;
     const size_t bytes = me == root ? snd.bytes[0] : rcv.bytes[0];
-    int erc = me == root ? side_move(&snd, -1, 1) : MI355X_SUCCESS;
+    int erc = me == root ? side_move(m, &snd, -1, 1) : MI355X_SUCCESS;
     if (erc == MI355X_SUCCESS)
         erc = mi355x_scatter(m->engine, me == root ? snd.view : NULL, inplace ? NULL : rcv.view, bytes, root, NULL);
-    return finish_unpack(inplace ? NULL : &rcv, erc);
+    return finish_unpack(m, inplace ? NULL : &rcv, erc);
 }
 
 int mca_coll_mi355x_scatterv(void *sbuf, int *scounts, int *disps, struct ompi_datatype_t *sdtype, void *rbuf,
@@ -796,19 +834,21 @@ int mca_coll_mi355x_scatterv(void *sbuf, int *scounts, int *disps, struct ompi_d
 {
     mca_coll_mi355x_module_t *m = MOD(module);
     const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm), inplace = (rbuf == MPI_IN_PLACE);
-    if (n > SIDE_MAX || (me == root && !is_dev(sbuf)) || (!inplace && !is_dev(rbuf)) || (inplace && me != root))
+    if (n > SIDE_MAX || (inplace && me != root))
         return m->prev_scatterv(sbuf, scounts, disps, sdtype, rbuf, rcount, rdtype, root, comm,
                                 m->prev_scatterv_module);
+    const int dev = (me != root || is_dev(sbuf)) && (inplace || is_dev(rbuf));
+    ROUTE_OR(m->prev_scatterv(sbuf, scounts, disps, sdtype, rbuf, rcount, rdtype, root, comm, m->prev_scatterv_module));
     side_t snd, rcv;
     int rc = OMPI_SUCCESS;
     if (me == root && (rc = side_init(m, &snd, 0, sbuf, sdtype, n, scounts, 0, disps))) return rc;
     if (!inplace && (rc = side_init(m, &rcv, 1, rbuf, rdtype, 1, NULL, rcount, NULL))) return rc;
-    int erc = me == root ? side_move(&snd, -1, 1) : MI355X_SUCCESS;
+    int erc = me == root ? side_move(m, &snd, -1, 1) : MI355X_SUCCESS;
     if (erc == MI355X_SUCCESS)
         erc = mi355x_scatterv(m->engine, me == root ? snd.view : NULL, me == root ? snd.bytes : NULL,
                               me == root ? snd.off : NULL, inplace ? NULL : rcv.view, inplace ? 0 : rcv.bytes[0], root,
                               NULL);
-    return finish_unpack(inplace ? NULL : &rcv, erc);
+    return finish_unpack(m, inplace ? NULL : &rcv, erc);
 }
 
 int mca_coll_mi355x_allgatherv(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int *rcounts,
@@ -817,17 +857,19 @@ int mca_coll_mi355x_allgatherv(void *sbuf, int scount, struct ompi_datatype_t *s
 {
     mca_coll_mi355x_module_t *m = MOD(module);
     const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm), inplace = (sbuf == MPI_IN_PLACE);
-    if (n > SIDE_MAX || !is_dev(rbuf) || (!inplace && !is_dev(sbuf)))
+    if (n > SIDE_MAX)
         return m->prev_allgatherv(sbuf, scount, sdtype, rbuf, rcounts, disps, rdtype, comm, m->prev_allgatherv_module);
+    const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
+    ROUTE_OR(m->prev_allgatherv(sbuf, scount, sdtype, rbuf, rcounts, disps, rdtype, comm, m->prev_allgatherv_module));
     side_t snd, rcv;
     int rc = OMPI_SUCCESS;
     if (!inplace && (rc = side_init(m, &snd, 0, sbuf, sdtype, 1, NULL, scount, NULL))) return rc;
     if ((rc = side_init(m, &rcv, 1, rbuf, rdtype, n, rcounts, 0, disps))) return rc;
-    int erc = inplace ? side_move(&rcv, me, 1) : side_move(&snd, 0, 1);
+    int erc = inplace ? side_move(m, &rcv, me, 1) : side_move(m, &snd, 0, 1);
     if (erc == MI355X_SUCCESS)
         erc = mi355x_allgatherv(m->engine, inplace ? NULL : snd.view, inplace ? 0 : snd.bytes[0], rcv.view, rcv.bytes,
                                 rcv.off, NULL);
-    return finish_unpack(&rcv, erc);
+    return finish_unpack(m, &rcv, erc);
 }
 
 int mca_coll_mi355x_alltoall(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
@@ -836,16 +878,17 @@ int mca_coll_mi355x_alltoall(void *sbuf, int scount, struct ompi_datatype_t *sdt
 {
     mca_coll_mi355x_module_t *m = MOD(module);
     const int n = mi355x_comm_size_of(comm), inplace = (sbuf == MPI_IN_PLACE);
-    if (n > SIDE_MAX || !is_dev(rbuf) || (!inplace && !is_dev(sbuf)))
-        return m->prev_alltoall(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_alltoall_module);
+    if (n > SIDE_MAX) return m->prev_alltoall(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_alltoall_module);
+    const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
+    ROUTE_OR(m->prev_alltoall(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_alltoall_module));
     side_t snd, rcv;
     int rc = OMPI_SUCCESS;
     if (!inplace && (rc = side_init(m, &snd, 0, sbuf, sdtype, n, NULL, scount, NULL))) return rc;
     if ((rc = side_init(m, &rcv, 1, rbuf, rdtype, n, NULL, rcount, NULL))) return rc;
     if (!inplace && snd.bytes[0] != rcv.bytes[0]) return OMPI_ERR_BAD_PARAM;
-    int erc = inplace ? side_move(&rcv, -1, 1) : side_move(&snd, -1, 1);
+    int erc = inplace ? side_move(m, &rcv, -1, 1) : side_move(m, &snd, -1, 1);
     if (erc == MI355X_SUCCESS) erc = mi355x_alltoall(m->engine, inplace ? NULL : snd.view, rcv.view, rcv.bytes[0], NULL);
-    return finish_unpack(&rcv, erc);
+    return finish_unpack(m, &rcv, erc);
 }
 
 int mca_coll_mi355x_alltoallv(void *sbuf, int *scounts, int *sdisps, struct ompi_datatype_t *sdtype, void *rbuf,
@@ -854,18 +897,21 @@ int mca_coll_mi355x_alltoallv(void *sbuf, int *scounts, int *sdisps, struct ompi
 {
     mca_coll_mi355x_module_t *m = MOD(module);
     const int n = mi355x_comm_size_of(comm), inplace = (sbuf == MPI_IN_PLACE);
-    if (n > SIDE_MAX || !is_dev(rbuf) || (!inplace && !is_dev(sbuf)))
+    if (n > SIDE_MAX)
         return m->prev_alltoallv(sbuf, scounts, sdisps, sdtype, rbuf, rcounts, rdisps, rdtype, comm,
                                  m->prev_alltoallv_module);
+    const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
+    ROUTE_OR(m->prev_alltoallv(sbuf, scounts, sdisps, sdtype, rbuf, rcounts, rdisps, rdtype, comm,
+                               m->prev_alltoallv_module));
     side_t snd, rcv;
     int rc = OMPI_SUCCESS;
     if (!inplace && (rc = side_init(m, &snd, 0, sbuf, sdtype, n, scounts, 0, sdisps))) return rc;
     if ((rc = side_init(m, &rcv, 1, rbuf, rdtype, n, rcounts, 0, rdisps))) return rc;
-    int erc = inplace ? side_move(&rcv, -1, 1) : side_move(&snd, -1, 1);
+    int erc = inplace ? side_move(m, &rcv, -1, 1) : side_move(m, &snd, -1, 1);
     if (erc == MI355X_SUCCESS)
         erc = mi355x_alltoallv(m->engine, inplace ? NULL : snd.view, inplace ? NULL : snd.bytes,
                                inplace ? NULL : snd.off, rcv.view, rcv.bytes, rcv.off, NULL);
-    return finish_unpack(&rcv, erc);
+    return finish_unpack(m, &rcv, erc);
 }
 
 static int scan_common(mca_coll_mi355x_module_t *m, int exclusive, void *sbuf, void *rbuf, int count,
@@ -935,6 +981,7 @@ typedef struct mi355x_nbreq_t {
     size_t ucount;
     mi355x_ddt_t *ud;
     mi355x_ddt_t *pd;              /* layout of the initiation-time pack (kept until completion) */
+    int uhost;                     /* ubuf is host memory: copied (ud NULL) or host-unpacked (ud) */
     /* persistent point-to-point (pml_isend_init / pml_irecv_init): 1 send, 2 receive, 0 none; the
      * arguments each MPI_Start posts */
     int pers;
@@ -1003,6 +1050,7 @@ static void nbreq_construct(opal_object_t *o)
     r->ucount = 0;
     r->ud = NULL;
     r->pd = NULL;
+    r->uhost = 0;
     r->pers = 0;
     r->pbuf = NULL;
     r->pcount = 0;
@@ -1017,7 +1065,12 @@ static void nbreq_construct(opal_object_t *o)
 static int nb_finish_stage(mi355x_nbreq_t *r, int rc)
 {
     if (!r->stage) return rc;
-    if (rc == MI355X_SUCCESS && r->ubuf) {
+    if (rc == MI355X_SUCCESS && r->ubuf && r->uhost && r->ud) {  /* host layout: host convertor */
+        void *tmp = malloc(r->stage_bytes ? r->stage_bytes : 1);
+        rc = tmp ? mi355x_memcpy(tmp, r->stage, r->stage_bytes) : MI355X_ERR_NOMEM;
+        if (rc == MI355X_SUCCESS) rc = mi355x_unpack_host(r->ud, r->ucount, r->ubuf, 0, tmp, r->stage_bytes);
+        free(tmp);
+    } else if (rc == MI355X_SUCCESS && r->ubuf) {
         rc = r->ud ? mi355x_unpack(r->ud, r->ucount, r->ubuf, 0, r->stage, r->stage_bytes, NULL, NULL)
                    : mi355x_memcpy_async(r->ubuf, r->stage, r->stage_bytes, NULL);
         if (rc == MI355X_SUCCESS) rc = mi355x_stream_sync(NULL);
@@ -1106,6 +1159,7 @@ struct nb_stage {
     size_t ucount;
     mi355x_ddt_t *ud; /* owned by the request; NULL with ubuf set: a plain copy */
     mi355x_ddt_t *pd; /* layout of the initiation-time pack, owned by the request */
+    int uhost;        /* ubuf is host memory (the host convertor unpacks a derived layout) */
 };
 
 static void nb_stage_release(struct nb_stage *st)
@@ -1148,6 +1202,7 @@ static int nb_start_full(mi355x_request_t *eng, struct ompi_communicator_t *comm
         r->ucount = st->ucount;
         r->ud = st->ud;
         r->pd = st->pd;
+        r->uhost = st->uhost;
     }
     if (p2p) r->super.req_type = OMPI_REQUEST_PML;
     r->super.req_complete = false;
@@ -1207,6 +1262,42 @@ static int nb_staged_start(struct ompi_communicator_t *comm, ompi_request_t **re
     return OMPI_SUCCESS;
 }
 
+/* A nonblocking initiation may not wait for its peers (a vote would: MPI lets a rank start the
+ * call, then block in point-to-point its peer needs before that peer starts it), so with mixed
+ * buffers allowed the path depends only on what every rank shares -- the op and the type: every
+ * rank enters the engine, and a rank whose buffers are host memory joins on device copies made at
+ * initiation (its input) and copied back at completion (its output).  With
+ * coll_mi355x_mixed_buffers = 0 every rank must use one kind, and host buffers go to the
+ * lower-priority component as before. */
+static int nb_host_join(mca_coll_mi355x_module_t *m, void *sbuf, void *rbuf, int inplace, size_t in_bytes,
+                        size_t out_bytes, int rsig, void **sd, void **rd, struct nb_stage *st)
+{
+    const int rh = rsig && !is_dev(rbuf), sh = !inplace && !is_dev(sbuf);
+    memset(st, 0, sizeof(*st));
+    *sd = inplace ? NULL : sbuf;
+    *rd = rsig ? rbuf : NULL;
+    const size_t rspan = inplace ? in_bytes : out_bytes;
+    const size_t a = (rh ? rspan : 0) + (sh ? in_bytes : 0);
+    if (mi355x_malloc(&st->stage, a ? a : 1) != MI355X_SUCCESS) return MI355X_ERR_NOMEM;
+    int rc = MI355X_SUCCESS;
+    if (rh) {
+        *rd = st->stage;
+        st->bytes = out_bytes;
+        st->ubuf = rbuf;
+        st->uhost = 1;
+        if (inplace && in_bytes) rc = mi355x_memcpy(st->stage, rbuf, in_bytes);
+    }
+    if (sh && rc == MI355X_SUCCESS) {
+        *sd = (char *)st->stage + (rh ? rspan : 0);
+        if (in_bytes) rc = mi355x_memcpy(*sd, sbuf, in_bytes);
+    }
+    if (rc != MI355X_SUCCESS) {
+        mi355x_free(st->stage);
+        st->stage = NULL;
+    }
+    return rc;
+}
+
 /* the declined / host-buffer form of a nonblocking reduction: device buffers staged to the host */
 #define NB_STAGED(FN, SSPAN, RSPAN, RFILL, RBACK, DT, ...)                                       \
     do {                                                                                          \
@@ -1227,11 +1318,24 @@ int mca_coll_mi355x_iallreduce(void *sbuf, void *rbuf, int count, struct ompi_da
     const int inplace = (sbuf == MPI_IN_PLACE);
     const int t = reducible_type(dtype);
     if (count < 0) NB_FALLBACK(iallreduce, sbuf, rbuf, count, dtype, op, comm, request);
-    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || !engine_op(op, t)) {
+    const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
+    if (!engine_op(op, t) || (!dev && !m->mixed)) {
         const size_t span = dt_span(dtype, (size_t)count);
         NB_STAGED(iallreduce, span, span, inplace, span, dtype, sbuf, rbuf, count, dtype, op, comm);
     }
     mi355x_request_t *eng = NULL;
+    if (!dev) {  /* host buffers: join the engine on device copies (nb_host_join) */
+        const size_t bytes = (size_t)count * mi355x_type_size(t);
+        struct nb_stage st;
+        void *sd, *rd;
+        int rc = nb_host_join(m, sbuf, rbuf, inplace, bytes, bytes, 1, &sd, &rd, &st);
+        if (rc == MI355X_SUCCESS) rc = mi355x_iallreduce(m->engine, sd, rd, (size_t)count, t, op->o_f_to_c_index, NULL, &eng);
+        if (rc != MI355X_SUCCESS) {
+            nb_stage_release(&st);
+            return map_rc(rc);
+        }
+        return nb_start_full(eng, comm, request, 0, &st);
+    }
     int rc = mi355x_iallreduce(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)count, t, op->o_f_to_c_index, NULL, &eng);
     return rc ? map_rc(rc) : nb_start(eng, comm, request);
 }
@@ -1245,12 +1349,26 @@ int mca_coll_mi355x_ireduce(void *sbuf, void *rbuf, int count, struct ompi_datat
     const int inplace = (sbuf == MPI_IN_PLACE);
     const int t = reducible_type(dtype);
     if (count < 0 || (inplace && me != root)) NB_FALLBACK(ireduce, sbuf, rbuf, count, dtype, op, root, comm, request);
-    if ((me == root && !is_dev(rbuf)) || (!inplace && !is_dev(sbuf)) || !engine_op(op, t)) {
+    const int dev = (me != root || is_dev(rbuf)) && (inplace || is_dev(sbuf));
+    if (!engine_op(op, t) || (!dev && !m->mixed)) {
         const size_t span = dt_span(dtype, (size_t)count);
         if (me != root) rbuf = NULL;  /* not significant off the root: never staged */
         NB_STAGED(ireduce, span, span, inplace, span, dtype, sbuf, rbuf, count, dtype, op, root, comm);
     }
     mi355x_request_t *eng = NULL;
+    if (!dev) {  /* host buffers: join the engine on device copies (nb_host_join) */
+        const size_t bytes = (size_t)count * mi355x_type_size(t);
+        struct nb_stage st;
+        void *sd, *rd;
+        int rc = nb_host_join(m, sbuf, rbuf, inplace, bytes, bytes, me == root, &sd, &rd, &st);
+        if (rc == MI355X_SUCCESS)
+            rc = mi355x_ireduce(m->engine, sd, rd, (size_t)count, t, op->o_f_to_c_index, root, NULL, &eng);
+        if (rc != MI355X_SUCCESS) {
+            nb_stage_release(&st);
+            return map_rc(rc);
+        }
+        return nb_start_full(eng, comm, request, 0, &st);
+    }
     int rc = mi355x_ireduce(m->engine, inplace ? NULL : sbuf, me == root ? rbuf : NULL, (size_t)count, t,
                             op->o_f_to_c_index, root, NULL, &eng);
     return rc ? map_rc(rc) : nb_start(eng, comm, request);
@@ -1264,13 +1382,27 @@ int mca_coll_mi355x_ireduce_scatter_block(void *sbuf, void *rbuf, int rcount, st
     const int inplace = (sbuf == MPI_IN_PLACE);
     const int t = reducible_type(dtype);
     if (rcount < 0) NB_FALLBACK(ireduce_scatter_block, sbuf, rbuf, rcount, dtype, op, comm, request);
-    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf)) || !engine_op(op, t)) {
+    const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
+    if (!engine_op(op, t) || (!dev && !m->mixed)) {
         const size_t in = dt_span(dtype, (size_t)rcount * (size_t)mi355x_comm_size_of(comm));
         const size_t out = dt_span(dtype, (size_t)rcount);
         NB_STAGED(ireduce_scatter_block, in, inplace ? in : out, inplace, out, dtype, sbuf, rbuf, rcount, dtype, op,
                   comm);
     }
     mi355x_request_t *eng = NULL;
+    if (!dev) {  /* host buffers: join the engine on device copies (nb_host_join) */
+        const size_t out = (size_t)rcount * mi355x_type_size(t), in = out * (size_t)mi355x_comm_size_of(comm);
+        struct nb_stage st;
+        void *sd, *rd;
+        int rc = nb_host_join(m, sbuf, rbuf, inplace, in, out, 1, &sd, &rd, &st);
+        if (rc == MI355X_SUCCESS)
+            rc = mi355x_ireduce_scatter_block(m->engine, sd, rd, (size_t)rcount, t, op->o_f_to_c_index, NULL, &eng);
+        if (rc != MI355X_SUCCESS) {
+            nb_stage_release(&st);
+            return map_rc(rc);
+        }
+        return nb_start_full(eng, comm, request, 0, &st);
+    }
     int rc = mi355x_ireduce_scatter_block(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)rcount, t,
                                           op->o_f_to_c_index, NULL, &eng);
     return rc ? map_rc(rc) : nb_start(eng, comm, request);
@@ -1314,7 +1446,8 @@ int mca_coll_mi355x_iallgather(void *sbuf, int scount, struct ompi_datatype_t *s
     size_t rb = 0, sb = 0;
     if (rcount < 0 || (!inplace && scount < 0))
         NB_FALLBACK(iallgather, sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, request);
-    if (!is_dev(rbuf) || (!inplace && !is_dev(sbuf))) {  /* a host side: device sides staged */
+    const int rh = !is_dev(rbuf), sh = !inplace && !is_dev(sbuf);
+    if ((rh || sh) && !m->mixed) {  /* a host side, one kind per call: device sides staged to the host */
         if (!m->prev_iallgather) return OMPI_ERR_NOT_SUPPORTED;
         const size_t n = (size_t)mi355x_comm_size_of(comm);
         hstage_t st[2];
@@ -1328,20 +1461,36 @@ int mca_coll_mi355x_iallgather(void *sbuf, int scount, struct ompi_datatype_t *s
         return nb_staged_start(comm, request, st, inner, rc);
     }
     mi355x_request_t *eng = NULL;
-    if (contiguous_bytes(rdtype, rcount, &rb) && (inplace || (contiguous_bytes(sdtype, scount, &sb) && sb == rb))) {
+    if (!rh && !sh && contiguous_bytes(rdtype, rcount, &rb) &&
+        (inplace || (contiguous_bytes(sdtype, scount, &sb) && sb == rb))) {
         int rc = mi355x_iallgather(m->engine, inplace ? NULL : sbuf, rbuf, rb, NULL, &eng);
         return rc ? map_rc(rc) : nb_start(eng, comm, request);
     }
+    /* derived layouts or host sides (a host rank joins the engine, nb_host_join): my block packed
+     * into the per-request staging buffer now, the n blocks moved out of it at completion */
     const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm);
     const size_t blk = (size_t)rcount * rdtype->super.size;
     if (!inplace && (size_t)scount * sdtype->super.size != blk) return OMPI_ERR_BAD_PARAM;
-    struct nb_stage st = {NULL, blk * (size_t)n, NULL, 0, NULL, NULL};
+    struct nb_stage st = {NULL, blk * (size_t)n, NULL, 0, NULL, NULL, 0};
     if (mi355x_malloc(&st.stage, st.bytes ? st.bytes : 1) != MI355X_SUCCESS) return OMPI_ERR_OUT_OF_RESOURCE;
     const ptrdiff_t rext = rdtype->super.ub - rdtype->super.lb;
-    int rc = inplace ? nb_stage_side(1, (char *)rbuf + (ptrdiff_t)me * rcount * rext, rcount, rdtype,
+    int rc;
+    if (inplace && rh)
+        rc = xstage(m, 1, (char *)rbuf + (ptrdiff_t)me * rcount * rext, rcount, rdtype, (char *)st.stage + blk * me, blk, 1);
+    else if (sh)
+        rc = xstage(m, 1, sbuf, scount, sdtype, (char *)st.stage + blk * me, blk, 1);
+    else
+        rc = inplace ? nb_stage_side(1, (char *)rbuf + (ptrdiff_t)me * rcount * rext, rcount, rdtype,
                                      (char *)st.stage + blk * me, blk, &st)
                      : nb_stage_side(1, sbuf, scount, sdtype, (char *)st.stage + blk * me, blk, &st);
-    if (rc == MI355X_SUCCESS) rc = nb_stage_side(0, rbuf, (size_t)rcount * (size_t)n, rdtype, st.stage, st.bytes, &st);
+    if (rc == MI355X_SUCCESS && rh) {
+        st.ubuf = rbuf;
+        st.ucount = (size_t)rcount * (size_t)n;
+        st.uhost = 1;
+        if (!contiguous_bytes_n(rdtype, st.ucount, &rb) && !(st.ud = ddt_private(rdtype))) rc = MI355X_ERR_UNSUPPORTED;
+    } else if (rc == MI355X_SUCCESS) {
+        rc = nb_stage_side(0, rbuf, (size_t)rcount * (size_t)n, rdtype, st.stage, st.bytes, &st);
+    }
     if (rc == MI355X_SUCCESS) rc = mi355x_iallgather(m->engine, NULL, st.stage, blk, NULL, &eng);
     if (rc != MI355X_SUCCESS) {
         if (rc == MI355X_ERR_UNSUPPORTED)
@@ -1358,16 +1507,27 @@ int mca_coll_mi355x_ibcast(void *buff, int count, struct ompi_datatype_t *dataty
 {
     mca_coll_mi355x_module_t *m = MOD(module);
     size_t bytes = 0;
-    if (!is_dev(buff) || count < 0) NB_FALLBACK(ibcast, buff, count, datatype, root, comm, request);
+    const int host = !is_dev(buff);
+    if (count < 0 || (host && !m->mixed)) NB_FALLBACK(ibcast, buff, count, datatype, root, comm, request);
     mi355x_request_t *eng = NULL;
-    if (contiguous_bytes(datatype, count, &bytes)) {
+    if (!host && contiguous_bytes(datatype, count, &bytes)) {
         int rc = mi355x_ibcast(m->engine, buff, bytes, root, NULL, &eng);
         return rc ? map_rc(rc) : nb_start(eng, comm, request);
     }
     const int me = mi355x_comm_rank_of(comm);
-    struct nb_stage st = {NULL, (size_t)count * datatype->super.size, NULL, 0, NULL, NULL};
+    struct nb_stage st = {NULL, (size_t)count * datatype->super.size, NULL, 0, NULL, NULL, 0};
     if (mi355x_malloc(&st.stage, st.bytes ? st.bytes : 1) != MI355X_SUCCESS) return OMPI_ERR_OUT_OF_RESOURCE;
-    int rc = nb_stage_side(me == root, buff, count, datatype, st.stage, st.bytes, &st);
+    int rc = MI355X_SUCCESS;
+    if (!host) {
+        rc = nb_stage_side(me == root, buff, count, datatype, st.stage, st.bytes, &st);
+    } else if (me == root) {  /* a host rank joining the engine (nb_host_join): packed / copied now */
+        rc = xstage(m, 1, buff, (size_t)count, datatype, st.stage, st.bytes, 1);
+    } else {                  /* ... or moved out of the staging buffer at completion */
+        st.ubuf = buff;
+        st.ucount = (size_t)count;
+        st.uhost = 1;
+        if (!contiguous_bytes(datatype, count, &bytes) && !(st.ud = ddt_private(datatype))) rc = MI355X_ERR_UNSUPPORTED;
+    }
     if (rc == MI355X_SUCCESS) rc = mi355x_ibcast(m->engine, st.stage, st.bytes, root, NULL, &eng);
     if (rc != MI355X_SUCCESS) {
         if (rc == MI355X_ERR_UNSUPPORTED)

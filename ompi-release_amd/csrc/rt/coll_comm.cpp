@@ -250,7 +250,10 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
     if (c->pipe_queue) (void)hipFree(c->pipe_queue);
     if (c->pipe_dbg) (void)hipHostFree(c->pipe_dbg);
     if (c->scratch) (void)hipFree(c->scratch);
-    if (c->gf_buf) (void)hipFree(c->gf_buf);
+    if (c->gf_buf) {  // (stream-ordered allocation, coll_gfold.cpp)
+        (void)hipFreeAsync(c->gf_buf, nullptr);
+        (void)hipStreamSynchronize(nullptr);
+    }
     if (c->stage) (void)hipFree(c->stage);
     if (!c->svc_stuck) {  // (a service kernel that never left may still read and write these)
         if (c->ll_base) (void)hipFree(c->ll_base);

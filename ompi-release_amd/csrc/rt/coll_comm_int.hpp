@@ -43,6 +43,7 @@ int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force);
 // process is a second hardware queue, and eight processes sharing one GPU then time-slice their
 // queues: the 8-rank 1 GiB allreduce rehearsal took 22.9 ms per call instead of 3.7 while every
 // rank held an idle setup stream (profiles/r05_setup_stream_bisect.txt)
+void gfold_idle(mi355x_comm *c, hipStream_t s);  // coll_gfold.cpp
 struct CallStream {
     mi355x_comm *c;
     hipStream_t prev;
@@ -50,6 +51,7 @@ struct CallStream {
     {
         c->call_s = s;  // (NULL is the null stream: call_depth says whether call_s is set)
         c->call_depth++;
+        if (c->gf_buf) gfold_idle(c, s);  // (an idle gather-then-fold buffer is dropped on this stream)
     }
     ~CallStream()
     {
@@ -131,8 +133,22 @@ int svc_maybe_claim(mi355x_comm *c, bool sized);
 void svc_setup(mi355x_comm *c);
 int dev_setup(mi355x_comm *c);
 bool coll_slot_supported(int op, int type);  // coll_kernels.hip: the fold families carry (op, type)
-int gather_fold(mi355x_comm *c, const void *in, size_t count, int type, int op, size_t e0, size_t ne, int chain,
-                void *dst, hipStream_t s);
+// gather-then-fold (coll_gfold.cpp): elements [e0, e0 + ne) evaluated with `pr`, results to dst
+struct GfSeg {
+    size_t e0 = 0, ne = 0;
+    Program pr;
+    char *dst = nullptr;  // where element e0's result goes (nullptr: evaluate nothing)
+};
+int gather_fold(mi355x_comm *c, const void *in, size_t count, int type, int op, const std::vector<GfSeg> &segs,
+                hipStream_t s);
+void gfold_idle(mi355x_comm *c, hipStream_t s);
+int gfold_allreduce(mi355x_comm *c, const void *in, void *rbuf, size_t count, int type, int op, hipStream_t s);
+int gfold_reduce(mi355x_comm *c, const void *in, void *rbuf, size_t count, int type, int op, int root, hipStream_t s);
+int gfold_reduce_scatter_block(mi355x_comm *c, const void *in, void *rbuf, size_t rcount, int type, int op,
+                               hipStream_t s);
+int gfold_reduce_scatter(mi355x_comm *c, const void *in, void *rbuf, const size_t *disp, int type, int op,
+                         hipStream_t s);
+int gfold_scan(mi355x_comm *c, const void *in, void *rbuf, size_t count, int type, int op, int last, hipStream_t s);
 hipStream_t setup_stream(mi355x_comm *c);
 int ensure_pipe(mi355x_comm *c);
 int pipe_allreduce(mi355x_comm *c, int op, int type, const Program &pr,

@@ -171,49 +171,21 @@ static bool via_dmabuf(const mi355x_comm *c, size_t bytes)
     return bytes >= c->ipc_max || ((c->rcache_max_maps || c->rcache_limit) && c->dmabuf_state != -1);
 }
 
-// does the dmabuf fd `fd` name the allocation [base, base + bytes)?  Imports it here and compares
-// 16 bytes at three offsets with the allocation itself (the allocation's own contents: a wrong
-// buffer object reads differently unless both hold the same bytes there).  1 yes, 0 no, -1 the
-// import itself failed (unknown).
-static int export_names(void *base, size_t bytes, int fd, hipStream_t s)
+// does the dmabuf fd `fd` name the allocation [base, base + bytes) itself?  The runtime exports the
+// whole buffer object an allocation lives in, from the object's start; the allocation is at offset
+// 0 of an object of exactly its size iff the two sizes agree (an allocation carved at offset o > 0
+// out of an object leaves the object at least o + bytes long).  So the check is on identity -- the
+// object's size, read from the fd (dma-buf's llseek), against the allocation's
+// hipMemGetAddressRange size -- as the reference checks identity (IPC handle bytes memcmp'd,
+// common_cuda.c:1581; CU_POINTER_ATTRIBUTE_BUFFER_ID, :1937-1958), never contents.  1 yes, 0 no
+// (another range: such an allocation keeps the hipIpc route, whose handle carries the offset),
+// -1 the fd's size is unknown (treated as no).
+static int export_names(size_t bytes, int fd)
 {
-    const int mine = fcntl(fd, F_DUPFD_CLOEXEC, 0);
-    if (mine < 0) return -1;
-    hipExternalMemoryHandleDesc hd;
-    std::memset(&hd, 0, sizeof(hd));
-    hd.type = hipExternalMemoryHandleTypeOpaqueFd;
-    hd.handle.fd = mine;
-    hd.size = bytes;
-    hipExternalMemory_t ext = nullptr;
-    if (hipImportExternalMemory(&ext, &hd) != hipSuccess) {
-        (void)hipGetLastError();
-        close(mine);
-        return -1;
-    }
-    hipExternalMemoryBufferDesc bd;
-    std::memset(&bd, 0, sizeof(bd));
-    bd.size = bytes;
-    void *m = nullptr;
-    int same = -1;
-    if (hipExternalMemoryGetMappedBuffer(&m, ext, &bd) == hipSuccess) {
-        same = 1;
-        const size_t offs[3] = {0, (bytes / 2) & ~(size_t)15, bytes >= 16 ? bytes - 16 : 0};
-        for (size_t o : offs) {
-            unsigned char a[16], b[16];
-            const size_t n = bytes < 16 ? bytes : 16;
-            if (hipMemcpyAsync(a, (char *)base + o, n, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                hipMemcpyAsync(b, (char *)m + o, n, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                hipStreamSynchronize(s) != hipSuccess) {
-                same = -1;
-                break;
-            }
-            if (std::memcmp(a, b, n) != 0) same = 0;
-        }
-        (void)hipFree(m);
-    }
-    (void)hipGetLastError();
-    (void)hipDestroyExternalMemory(ext);
-    return same;
+    const off_t end = lseek(fd, 0, SEEK_END);
+    if (end < 0) return -1;
+    (void)lseek(fd, 0, SEEK_SET);
+    return (size_t)end == bytes ? 1 : 0;
 }
 
 int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
@@ -277,7 +249,7 @@ int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
             (void)hipGetLastError();
             reg.fd = -1;
             dm = false;
-        } else if (c->export_check && export_names(base, sz, reg.fd, setup_stream(c)) == 0) {
+        } else if (c->export_check && export_names(sz, reg.fd) != 1) {
             // the fd names another range: the runtime exports the whole buffer object an allocation
             // was carved from (small allocations share one), from its start -- such an allocation
             // keeps the hipIpc route (whose handle carries the offset)

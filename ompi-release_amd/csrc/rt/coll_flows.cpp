@@ -52,8 +52,7 @@ int allreduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count,
     CallStream call_stream(c, s);  // (the setup work of this call, if any, runs on its stream)
     if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     if (!coll_slot_supported(op, type)) {  // (no fold kernel carries the slot: gather-then-fold, coll_gfold.cpp)
-        c->last_alg = 1;
-        return gather_fold(c, sbuf ? sbuf : rbuf, count, type, op, 0, count, -1, rbuf, s);
+        return gfold_allreduce(c, sbuf ? sbuf : rbuf, rbuf, count, type, op, s);
     }
     const size_t esz = mi355x_type_size(type);
     const void *in = sbuf ? sbuf : rbuf;
@@ -278,8 +277,7 @@ int reduce_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, size_t count, in
     CallStream call_stream(c, s);  // (the setup work of this call, if any, runs on its stream)
     if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     if (!coll_slot_supported(op, type)) {  // (no fold kernel carries the slot: gather-then-fold, coll_gfold.cpp)
-        c->last_alg = 1;
-        return gather_fold(c, sbuf ? sbuf : rbuf, count, type, op, 0, count, -1, c->rank == root ? rbuf : nullptr, s);
+        return gfold_reduce(c, sbuf ? sbuf : rbuf, rbuf, count, type, op, root, s);
     }
     const size_t esz = mi355x_type_size(type);
     const void *in = sbuf ? sbuf : rbuf;
@@ -379,8 +377,7 @@ int reduce_scatter_block_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, si
     CallStream call_stream(c, s);  // (the setup work of this call, if any, runs on its stream)
     if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     if (!coll_slot_supported(op, type)) {  // (no fold kernel carries the slot: gather-then-fold, coll_gfold.cpp)
-        c->last_alg = 1;
-        return gather_fold(c, sbuf ? sbuf : rbuf, count, type, op, (size_t)c->rank * rcount, rcount, -1, rbuf, s);
+        return gfold_reduce_scatter_block(c, sbuf ? sbuf : rbuf, rbuf, rcount, type, op, s);
     }
     const size_t esz = mi355x_type_size(type);
     const void *in = sbuf ? sbuf : rbuf;
@@ -450,8 +447,7 @@ int reduce_scatter_impl(mi355x_comm_t *c, const void *sbuf, void *rbuf, const in
     CallStream call_stream(c, s);  // (the setup work of this call, if any, runs on its stream)
     if (const int rs_ = dev_setup(c)) return rs_;  // (first device-buffer collective: collective setup)
     if (!coll_slot_supported(op, type)) {  // (no fold kernel carries the slot: gather-then-fold, coll_gfold.cpp)
-        c->last_alg = 1;
-        return gather_fold(c, sbuf ? sbuf : rbuf, count, type, op, disp[c->rank], (size_t)rcounts[c->rank], -1, rbuf, s);
+        return gfold_reduce_scatter(c, sbuf ? sbuf : rbuf, rbuf, disp.data(), type, op, s);
     }
     const size_t esz = mi355x_type_size(type);
     const void *in = sbuf ? sbuf : rbuf;

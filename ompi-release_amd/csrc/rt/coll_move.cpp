@@ -226,8 +226,7 @@ static int scan_impl(mi355x_comm *c, const void *sbuf, void *rbuf, size_t count,
     const void *in = sbuf ? sbuf : rbuf;
     const int last = exclusive ? me - 1 : me;   // fold over ranks 0..last
     if (!coll_slot_supported(op, type)) {  // (no fold kernel carries the slot: gather-then-fold, coll_gfold.cpp)
-        c->last_alg = 1;
-        return gather_fold(c, in, count, type, op, 0, count, last < 0 ? 0 : last, last < 0 ? nullptr : rbuf, s);
+        return gfold_scan(c, in, rbuf, count, type, op, last, s);
     }
     // in place, rbuf is also an input the later ranks read: the result goes to scratch first
     const bool via_scratch = !sbuf && last >= 0 && !(last == 0 && me == 0);

@@ -365,6 +365,7 @@ struct mi355x_comm {
     double create_us = 0, selftest_us = 0;
     void *gf_buf = nullptr;                       // gather-then-fold slots (coll_gfold.cpp): every rank's input
     size_t gf_bytes = 0;
+    double gf_used = 0;                           // last gather-then-fold call (steady clock, s)
     uint64_t use_clock = 0;                       // LRU clock of the peer-mapping cache (every use ticks it)
     // device-side setup (done words, LL region + self-test, the service's resources, the pipelined
     // flow's self-test), deferred from creation to the first device-buffer collective (dev_setup)

@@ -146,20 +146,38 @@ template <typename E> struct OpProd {
     static MI_DEV T op3(T o, T a) { return ProdImpl<E, __is_integral(E)>::f(o, a); }
 };
 
+// Logical ops on 1- and 2-byte elements also have a whole-word form (`swar`): the streaming
+// kernels apply `word` to each 32-bit word of a 16-B vector instead of testing every element.
+// nz(x) leaves the top bit of each element set iff the element is nonzero (the low bits are
+// cleared first, so the add never carries across elements); the result is 1 / 0 per element,
+// what the element form returns.
+template <typename E> struct Swar {
+    static constexpr bool on = sizeof(E) <= 2;
+    static constexpr uint32_t lo = sizeof(E) == 1 ? 0x7f7f7f7fu : 0x7fff7fffu;
+    static constexpr int top = 8 * sizeof(E) - 1;
+    static MI_DEV uint32_t nz(uint32_t x) { return (((x & lo) + lo) | x) & ~lo; }
+    static MI_DEV uint32_t ones(uint32_t m) { return m >> top; }
+};
 template <typename E> struct OpLand {
     using T = E;
+    static constexpr bool swar = Swar<E>::on;
     static MI_DEV T op2(T o, T a) { return (T)((o != 0) && (a != 0)); }
     static MI_DEV T op3(T o, T a) { return (T)((o != 0) && (a != 0)); }
+    static MI_DEV uint32_t word(uint32_t o, uint32_t a) { return Swar<E>::ones(Swar<E>::nz(o) & Swar<E>::nz(a)); }
 };
 template <typename E> struct OpLor {
     using T = E;
+    static constexpr bool swar = Swar<E>::on;
     static MI_DEV T op2(T o, T a) { return (T)((o != 0) || (a != 0)); }
     static MI_DEV T op3(T o, T a) { return (T)((o != 0) || (a != 0)); }
+    static MI_DEV uint32_t word(uint32_t o, uint32_t a) { return Swar<E>::ones(Swar<E>::nz(o) | Swar<E>::nz(a)); }
 };
 template <typename E> struct OpLxor {
     using T = E;
+    static constexpr bool swar = Swar<E>::on;
     static MI_DEV T op2(T o, T a) { return (T)((o != 0 ? 1 : 0) ^ (a != 0 ? 1 : 0)); }
     static MI_DEV T op3(T o, T a) { return (T)((o != 0 ? 1 : 0) ^ (a != 0 ? 1 : 0)); }
+    static MI_DEV uint32_t word(uint32_t o, uint32_t a) { return Swar<E>::ones(Swar<E>::nz(o) ^ Swar<E>::nz(a)); }
 };
 template <typename E> struct OpBand {
     using T = E;

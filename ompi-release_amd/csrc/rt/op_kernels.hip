@@ -47,6 +47,30 @@ __device__ __forceinline__ typename F::T apply(const typename F::T &xa, const ty
         return F::op2(xb, xa);
 }
 
+// the functor has a whole-word form for its element size (op_functors.hpp, Swar)
+template <class F, class = void> struct HasWord : std::false_type {};
+template <class F> struct HasWord<F, std::enable_if_t<F::swar>> : std::true_type {};
+
+// one 16-B vector of results from the raw operand vectors (word form when the functor has one)
+template <class F, bool THREE>
+__device__ __forceinline__ u32x4 apply_vec(const u32x4 &ra, const u32x4 &rb)
+{
+    u32x4 out;
+    if constexpr (HasWord<F>::value) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) out[k] = F::word(ra[k], rb[k]);
+    } else {
+        using T = typename F::T;
+        Vec16<T> xa, xb, r;
+        __builtin_memcpy(&xa, &ra, 16);
+        __builtin_memcpy(&xb, &rb, 16);
+#pragma unroll
+        for (int j = 0; j < (int)(16 / sizeof(T)); ++j) r.e[j] = apply<F, THREE>(xa.e[j], xb.e[j]);
+        __builtin_memcpy(&out, &r, 16);
+    }
+    return out;
+}
+
 template <bool NT, typename V> __device__ __forceinline__ V vload(const V *p)
 {
     u32x4 raw;
@@ -103,10 +127,14 @@ __global__ __launch_bounds__(256) void k_stream(StreamArgs args)
         for (int u = 0; u < U; ++u) {
             const size_t i = base + (size_t)u * nthr;
             if (i < nvec) {
-                V r;
-#pragma unroll
-                for (int j = 0; j < EPV; ++j) r.e[j] = apply<F, THREE>(xa[u].e[j], xb[u].e[j]);
-                vstore<(NTM & 2) != 0>(ov + i, r);
+                u32x4 ra, rb;
+                __builtin_memcpy(&ra, &xa[u], 16);
+                __builtin_memcpy(&rb, &xb[u], 16);
+                const u32x4 r = apply_vec<F, THREE>(ra, rb);
+                if constexpr ((NTM & 2) != 0)
+                    __builtin_nontemporal_store(r, reinterpret_cast<u32x4 *>(ov + i));
+                else
+                    *reinterpret_cast<u32x4 *>(ov + i) = r;
             }
         }
     }
@@ -158,13 +186,11 @@ __global__ __launch_bounds__(1024) void k_chunk(StreamArgs args)
     for (int u = 0; u < U; ++u) {
         const size_t i = base + (size_t)u * tpb;
         if (i < nvec) {
-            V xa[1], xb[1];
-            __builtin_memcpy(&xa[0], &ra[u], 16);
-            __builtin_memcpy(&xb[0], &rb[u], 16);
-            V r;
-#pragma unroll
-            for (int j = 0; j < EPV; ++j) r.e[j] = apply<F, THREE>(xa[0].e[j], xb[0].e[j]);
-            vstore<(NTM & 2) != 0>(ov + i, r);
+            const u32x4 r = apply_vec<F, THREE>(ra[u], rb[u]);
+            if constexpr ((NTM & 2) != 0)
+                __builtin_nontemporal_store(r, reinterpret_cast<u32x4 *>(ov + i));
+            else
+                *reinterpret_cast<u32x4 *>(ov + i) = r;
         }
     }
     if (blockIdx.x == 0) {
@@ -211,13 +237,59 @@ static int launch_shape(const StreamArgs &args, hipStream_t s)
     return MI355X_SUCCESS;
 }
 
-// elements wider than one 16-B vector (MPI_LONG_DOUBLE_INT, 32 B): one element per lane, two
-// dwordx4 accesses each (the pair is consumed whole by the lane that loads it)
+// elements wider than one 16-B vector (MPI_LONG_DOUBLE_INT, 32 B), operands not 16-B aligned:
+// one element per lane (the pair is consumed whole by the lane that loads it)
 template <class F, bool THREE>
 __global__ __launch_bounds__(256) void k_wide(const typename F::T *a, const typename F::T *b, typename F::T *o, size_t n)
 {
     const size_t nthr = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nthr) o[i] = apply<F, THREE>(a[i], b[i]);
+}
+
+// 32-B elements on 16-B aligned operands: one 16-B half per lane, so every wave instruction
+// moves 1 KiB contiguous (the one-element-per-lane form strides 32 B per lane: two half-used
+// instructions per operand, 0.80 of the 2R+1W ceiling, profiles/r06_bench_sweep.json).  The two
+// lanes of an element swap halves with one DPP quad permute per dword (no LDS), both evaluate the
+// element, each stores its own half.  One-shot grid, non-temporal beyond the Infinity Cache, as
+// k_chunk.
+template <class F, bool THREE, int NTM>
+__global__ __launch_bounds__(1024) void k_wide_halves(const u32x4 *a, const u32x4 *b, u32x4 *o, size_t nhalf)
+{
+    using T = typename F::T;
+    static_assert(sizeof(T) == 32, "two halves per element");
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = i < nhalf;  // nhalf is even and pairs start at even i: both lanes or neither
+    u32x4 ra = {0, 0, 0, 0}, rb = {0, 0, 0, 0};
+    if (live) {
+        if constexpr ((NTM & 1) != 0) {
+            ra = __builtin_nontemporal_load(a + i);
+            rb = __builtin_nontemporal_load(b + i);
+        } else {
+            ra = a[i];
+            rb = b[i];
+        }
+    }
+    u32x4 pa, pb;  // the partner lane's halves: quad_perm [1,0,3,2] swaps lanes 2k and 2k+1
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        pa[k] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)ra[k], 0xB1, 0xF, 0xF, false);
+        pb[k] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)rb[k], 0xB1, 0xF, 0xF, false);
+    }
+    if (!live) return;
+    const bool hi = (i & 1) != 0;
+    u32x4 ea[2] = {hi ? pa : ra, hi ? ra : pa};
+    u32x4 eb[2] = {hi ? pb : rb, hi ? rb : pb};
+    T xa, xb;
+    __builtin_memcpy(&xa, ea, 32);
+    __builtin_memcpy(&xb, eb, 32);
+    const T r = apply<F, THREE>(xa, xb);
+    u32x4 er[2];
+    __builtin_memcpy(er, &r, 32);
+    const u32x4 mine = hi ? er[1] : er[0];
+    if constexpr ((NTM & 2) != 0)
+        __builtin_nontemporal_store(mine, o + i);
+    else
+        o[i] = mine;
 }
 
 template <class F, bool THREE>
@@ -226,6 +298,19 @@ static int launch(const void *a, const void *b, void *out, size_t n, hipStream_t
     using T = typename F::T;
     if (n == 0) return MI355X_SUCCESS;
     if constexpr (sizeof(T) > 16) {
+        if ((((uintptr_t)a | (uintptr_t)b | (uintptr_t)out) & 15) == 0 && n < ((size_t)1 << 40)) {
+            const size_t nhalf = 2 * n;
+            const size_t blocks = (nhalf + 1023) / 1024;
+            const bool nt = 3 * n * sizeof(T) > ((size_t)256 << 20);
+            const u32x4 *ha = static_cast<const u32x4 *>(a), *hb = static_cast<const u32x4 *>(b);
+            u32x4 *ho = static_cast<u32x4 *>(out);
+            if (nt)
+                hipLaunchKernelGGL((k_wide_halves<F, THREE, 3>), dim3((unsigned)blocks), dim3(1024), 0, s, ha, hb, ho, nhalf);
+            else
+                hipLaunchKernelGGL((k_wide_halves<F, THREE, 0>), dim3((unsigned)blocks), dim3(1024), 0, s, ha, hb, ho, nhalf);
+            MI_HIP(hipGetLastError());
+            return MI355X_SUCCESS;
+        }
         size_t blocks = (n + 255) / 256;
         const size_t cap = (size_t)stream_tune().blocks_per_cu * (size_t)device_cu_count();
         if (blocks > cap) blocks = cap;

@@ -1220,6 +1220,67 @@ def rcache(key, rank, size, dev):
     print(f"rank {rank} rcache OK", flush=True)
 
 
+def carved(key, rank, size, dev):
+    """the bounded cache's dmabuf export check is on identity, not contents: the runtime carves small
+    hipMallocs out of one buffer object and exports the whole object from its start, so a carved
+    allocation's fd names another range.  Every rank takes a carved 64 KiB allocation (found here by
+    its fd's size) whose bytes at the old content check's three sample offsets are zero -- as are the
+    object's first bytes (every allocation of the object zero-filled) -- makes it its allreduce input,
+    and the engine must send it the hipIpc way (EXPORT_MISMATCHES + 1) with an exact result"""
+    import torch
+    torch.cuda.set_device(dev)
+    hip = ctypes.CDLL("libamdhip64.so")
+    vp, sz_t = ctypes.c_void_p, ctypes.c_size_t
+    hip.hipMalloc.argtypes = [ctypes.POINTER(vp), sz_t]
+    hip.hipMemset.argtypes = [vp, ctypes.c_int, sz_t]
+    hip.hipMemcpy.argtypes = [vp, vp, sz_t, ctypes.c_int]
+    hip.hipFree.argtypes = [vp]
+    hip.hipMemGetHandleForAddressRange.argtypes = [ctypes.POINTER(ctypes.c_int), vp, sz_t, ctypes.c_int,
+                                                   ctypes.c_ulonglong]
+    pkg = load_pkg()
+    comm = pkg.Comm.create(key, rank, size, dev)
+    comm.set("RCACHE_MAX_MAPS", 16)   # a bounded cache: allocations go as dmabuf fds
+    nb = 64 << 10
+    allocs, found = [], None
+    for _ in range(32):
+        p = vp()
+        assert hip.hipMalloc(ctypes.byref(p), nb) == 0
+        assert hip.hipMemset(p, 0, nb) == 0
+        allocs.append(p.value)
+    for p in allocs:
+        fd = ctypes.c_int(-1)
+        if hip.hipMemGetHandleForAddressRange(ctypes.byref(fd), vp(p), nb, 1, 0) != 0:
+            continue
+        end = os.lseek(fd.value, 0, os.SEEK_END)
+        os.close(fd.value)
+        if end > nb:
+            found = p
+            break
+    assert found is not None, "no carved allocation among 32 small hipMallocs"
+    count = nb // 4
+    x = np.arange(count, dtype=np.float32) * (rank + 1) + 7 * rank + 1
+    for o in (0, (nb // 2) & ~15, nb - 16):   # the old check's sample offsets: zero, like the object's start
+        x[o // 4:o // 4 + 4] = 0
+    assert hip.hipMemcpy(vp(found), vp(x.ctypes.data), nb, 1) == 0   # hipMemcpyHostToDevice
+    y = torch.full((count,), float("nan"), device="cuda")
+    torch.cuda.synchronize()
+    before = comm.get("EXPORT_MISMATCHES")
+    comm.allreduce(found, y.data_ptr(), count, pkg.T["FLOAT"], pkg.OP["SUM"])
+    want = sum(np.arange(count, dtype=np.float32) * (r + 1) + 7 * r + 1 for r in range(size))
+    for o in (0, (nb // 2) & ~15, nb - 16):
+        want[o // 4:o // 4 + 4] = 0
+    got = y.cpu().numpy()
+    assert np.array_equal(got, want), ("carved allreduce", np.nonzero(got != want)[0][:8])
+    mism = comm.get("EXPORT_MISMATCHES") - before
+    assert mism >= 1, "the carved allocation was exported as a dmabuf fd"
+    comm.barrier()
+    for p in allocs:
+        hip.hipFree(vp(p))
+    comm.destroy()
+    print(f"rank {rank} carved: mismatches +{mism}", flush=True)
+    print(f"rank {rank} carved OK", flush=True)
+
+
 def vote_dead(key, rank, size, dev):
     """a peer process that dies without a word (os._exit right after creation): the surviving
     host-buffer rank waiting in the buffer-kind vote (an unbounded wait) returns an error within
@@ -1300,6 +1361,8 @@ def _main():
         return rcache(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "rcache_p2p":
         return rcache_p2p(key, rank, size, dev)
+    if len(sys.argv) > 5 and sys.argv[5] == "carved":
+        return carved(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "token_hold":
         return token_hold(key, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "token_check":

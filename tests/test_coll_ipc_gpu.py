@@ -197,6 +197,15 @@ def test_bounded_peer_mapping_cache_across_frees(gpu):
     print(next(line for line in outs[0].splitlines() if "rcache:" in line))
 
 
+def test_bounded_cache_export_check_is_identity(gpu):
+    """a zero-filled small allocation carved at a non-zero offset of a runtime buffer object, whose
+    bytes at the old content check's sample offsets equal the object's start: the identity check
+    (the fd's size vs the allocation's) sends it the hipIpc way and the allreduce on it is exact
+    (ipc_worker.py::carved; common_cuda.c:1581, :1937-1958 check identity too)"""
+    outs = _run_mode(gpu, "carved", 2)
+    print(next(line for line in outs[0].splitlines() if "carved:" in line))
+
+
 def test_vote_notices_dead_peer(gpu):
     """the buffer-kind vote waits without a timeout; a peer that dies without setting the abort flag
     is noticed by its pid (ipc_worker.py::vote_dead)"""

@@ -155,6 +155,37 @@ def test_all_slots(gpu, pkg, oracle, offs):
     assert not bad, "\n".join(bad[:20])
 
 
+@pytest.mark.parametrize("offs", [(0, 0, 0), (32, 48, 16), (8, 8, 8), (0, 8, 0)],
+                         ids=["halves", "halves_offset", "wide_8", "wide_mixed"])
+@pytest.mark.parametrize("n", [1, 2, 3, 1023, 1024, 1025, 50_021])
+def test_long_double_int_kernels(gpu, pkg, oracle, offs, n):
+    """the two 32-byte kernels: 16-B aligned operands take k_wide_halves (one half per lane, the
+    partner's half by a DPP swap), any 8-B misalignment the element-per-lane k_wide; both bit-exact
+    vs the oracle (op_base_functions.c:576-598, :661-683), on counts around the 1024-lane block"""
+    torch = gpu
+    tname = "LONG_DOUBLE_INT"
+    for opname in ("MAXLOC", "MINLOC"):
+        op, ty = pkg.OP[opname], pkg.T[tname]
+        a = opdata.make(tname, n, 5)
+        b = opdata.make(tname, n, 6)
+        o1, o2, o3 = offs
+        ta, pa = _dev(torch, a, o1)
+        tb, pb = _dev(torch, b, o2)
+        to, po = _dev(torch, np.zeros_like(a), o3)
+        s = torch.cuda.current_stream().cuda_stream
+        pkg.op_reduce_3buff(op, ty, pa, pb, po, n, s)
+        pkg.op_reduce(op, ty, pa, pb, n, s)
+        torch.cuda.synchronize()
+        want3 = np.zeros_like(a)
+        assert oracle.oracle_op_3buff(op, ty, a.ctypes.data, b.ctypes.data, want3.ctypes.data, n) == 0
+        want2 = b.copy()
+        assert oracle.oracle_op_2buff(op, ty, a.ctypes.data, want2.ctypes.data, n) == 0
+        opdata.assert_same(tname, opname, _host(to, o3, a), want3, f"3buff {offs} n={n}")
+        opdata.assert_same(tname, opname, _host(tb, o2, a), want2, f"2buff {offs} n={n}")
+        # nothing written past the last element
+        assert not to[o3 + a.nbytes:].cpu().numpy().any()
+
+
 def test_small_counts(gpu, pkg, oracle):
     """count = 0, 1, 2, 15, 16, 17 (all of the body empty or one vector)"""
     torch = gpu
