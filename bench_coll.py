@@ -92,8 +92,9 @@ def extra_legs(args, pkg, torch, comm, world, rank, dev, legs, key):
         del x, y
     legs["allreduce_sweep_f32"] = sweep
     # what coll/mi355x's buffer-kind vote (mi355x_comm_vote) adds to every component collective
-    # of the mixed-buffer set: a device-buffer rank only publishes; a host-buffer rank waits for
-    # every rank's vote (the sweep above calls the engine directly, without the vote)
+    # of the mixed-buffer set: in a window after device calls a device-buffer rank only publishes,
+    # after host-only calls a host-buffer rank does; every 32nd call every rank waits (the sweep
+    # above calls the engine directly, without the vote)
     legs["buffer_kind_vote_us"] = {
         "device_rank": round(_timed(dist, torch, lambda: comm.vote(True), 200, 5) * 1e6, 3),
         "host_ranks": round(_timed(dist, torch, lambda: comm.vote(False), 200, 5) * 1e6, 3)}

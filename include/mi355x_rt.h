@@ -109,11 +109,16 @@ int mi355x_comm_barrier(mi355x_comm_t *comm);
 /* Buffer-kind agreement for one collective call.  coll/cuda tolerates ranks that mix host and
  * device buffers in one collective (each rank stages its own, coll_cuda_allreduce.c:30-77); the
  * engine needs every rank in the same protocol.  Every rank calls this once per collective, in the
- * collective's call order: a rank whose buffers are device memory (device = 1) publishes and
- * returns at once with *any_device = 1 (it will run the engine); a rank with host buffers waits
- * until every rank has published this call and learns whether any of them holds device buffers
- * (then it runs the engine too, on staged copies; else every rank takes the host path). */
-int mi355x_comm_vote(mi355x_comm_t *comm, int device, int *any_device);
+ * collective's call order, and learns whether the call runs in the engine (*engine = 1: a host rank
+ * joins on device copies) or in the lower-priority host component (*engine = 0: a device rank
+ * stages its buffers to the host, as coll/cuda does).  Only one side of a call waits for the
+ * others' votes, and which one is agreed window by window: every 32nd call every rank waits (a
+ * checkpoint: all ranks see every vote, and learn whether any rank used device buffers in the
+ * window just ended); in a window after device use the host ranks wait and the device ranks only
+ * publish (a mixed call runs in the engine), in a window without it the device ranks wait and the
+ * host ranks only publish (a mixed call runs on the host) -- so a host-only program pays one store
+ * per call and a device program nothing more. */
+int mi355x_comm_vote(mi355x_comm_t *comm, int device, int *engine);
 /* algorithm id of the last collective, coll/tuned numbering (allreduce: 1 linear, 2 nonoverlapping,
  * 3 recursive doubling, 4 ring, 5 segmented ring; reduce: 1 linear, 2 chain, 3 pipeline, 4 binary,
  * 5 binomial; reduce_scatter: 1 non-overlapping, 2 recursive halving, 3 ring) */
@@ -245,9 +250,12 @@ enum mi355x_knob {
                                            flow that failed on any rank off on every rank; 0: trusts them.  Only
                                            a value set before the device setup takes effect. */
     MI355X_KNOB_PIPE_CALLS = 41,        /* (read-only) allreduces served by the pipelined flow */
-    MI355X_KNOB_EXPORT_MISMATCHES = 42  /* (read-only) new dmabuf exports of the bounded peer-mapping cache that
+    MI355X_KNOB_EXPORT_MISMATCHES = 42, /* (read-only) new dmabuf exports of the bounded peer-mapping cache that
                                            named another buffer object (checked, that call staged instead;
                                            env MI355X_EXPORT_CHECK=0 turns the check off) */
+    MI355X_KNOB_SELFTEST_REUSED = 43    /* (read-only) flow verdicts this communicator took over from an earlier
+                                           communicator of the same processes on the same GPUs (a dup / split):
+                                           1 the device setup's (LL, pipelined), 2 also the service's */
 };
 /* cross-device flows (MI355X_KNOB_FLOWS) */
 enum mi355x_flow {

@@ -265,7 +265,7 @@ KNOB = {"ALLREDUCE_ALG": 1, "REDUCE_ALG": 2, "REDUCE_SCATTER_ALG": 3, "BLOCKS_PE
         "RCACHE_EVICTIONS": 28, "FLOWS": 29, "FLOWS_FAILED": 30, "CREATE_US": 31, "SELFTEST_US": 32,
         "SVC_OWNER": 33, "SVC_CLAIMS": 34, "SVC_IDLE_US": 35,
         "SVC_SHRINK_US": 36, "SVC_REGROWS": 37, "DEV_SETUP": 38, "SETUP_US": 39, "SELFTEST": 40,
-        "PIPE_CALLS": 41, "EXPORT_MISMATCHES": 42}
+        "PIPE_CALLS": 41, "EXPORT_MISMATCHES": 42, "SELFTEST_REUSED": 43}
 FLOW = {"SVC_LL": 1, "SVC_PULL": 2, "SVC_COPY": 4, "SVC_RS": 8, "PIPE": 16}
 # coll/tuned COLLTYPE ids (coll_tuned.h:41-58)
 COLL = {"ALLGATHER": 0, "ALLREDUCE": 2, "BCAST": 7, "REDUCE": 11, "REDUCESCATTER": 12}
@@ -309,7 +309,7 @@ class Comm:
         check(rt().mi355x_comm_barrier(self.h), "mi355x_comm_barrier")
 
     def vote(self, device: bool) -> bool:
-        """mi355x_comm_vote: this rank's buffer kind for one collective; True if any rank has device buffers"""
+        """mi355x_comm_vote: this rank's buffer kind for one collective; True if the call runs in the engine"""
         anyd = ctypes.c_int(0)
         check(rt().mi355x_comm_vote(self.h, 1 if device else 0, ctypes.byref(anyd)), "mi355x_comm_vote")
         return bool(anyd.value)

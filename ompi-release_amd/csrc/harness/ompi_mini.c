@@ -1157,10 +1157,16 @@ static int host_reduce(ompi_communicator_t *c, const char *src, size_t total, si
     const size_t ext = (size_t)(dt->super.ub - dt->super.lb);
     const size_t per = ext ? MINI_SLOT_BYTES / ext : 0;
     if (per == 0) return OMPI_ERR_NOT_SUPPORTED;
-    char *acc = malloc(MINI_SLOT_BYTES), *tmp = malloc(MINI_SLOT_BYTES);
-    if (!acc || !tmp) {
+    /* the operands of every ompi_op_reduce are private heap buffers of the message's size, as in
+     * coll/basic: the result buffer, and a receive buffer each peer's piece lands in first
+     * (coll_basic_reduce.c:204-250: free_buffer = malloc(true_extent + (count - 1) x extent), the
+     * PML receives into it, then ompi_op_reduce(op, inbuf, rbuf, ...)) -- never the shared segment */
+    const size_t piece = span_of(dt, total < per ? total : per) + 1;
+    char *acc = malloc(piece), *tmp = malloc(piece), *inb = malloc(piece);
+    if (!acc || !tmp || !inb) {
         free(acc);
         free(tmp);
+        free(inb);
         return OMPI_ERR_OUT_OF_RESOURCE;
     }
     for (size_t c0 = 0; c0 < total || (total == 0 && c0 == 0); c0 += per) {
@@ -1173,7 +1179,10 @@ static int host_reduce(ompi_communicator_t *c, const char *src, size_t total, si
             const size_t off = (a - c0) * ext, m = b - a, bytes = span_of(dt, m);
             if (chain < 0) {
                 memcpy(acc, chan_slot(ch, n - 1) + off, bytes);
-                for (int i = n - 2; i >= 0; --i) host_op_reduce(op, chan_slot(ch, i) + off, acc, (int)m, dt);
+                for (int i = n - 2; i >= 0; --i) {
+                    memcpy(inb, chan_slot(ch, i) + off, bytes);
+                    host_op_reduce(op, inb, acc, (int)m, dt);
+                }
             } else {
                 memcpy(acc, chan_slot(ch, 0) + off, bytes);
                 for (int q = 1; q <= chain; ++q) {
@@ -1190,6 +1199,7 @@ static int host_reduce(ompi_communicator_t *c, const char *src, size_t total, si
     }
     free(acc);
     free(tmp);
+    free(inb);
     return OMPI_SUCCESS;
 }
 
@@ -1367,6 +1377,69 @@ static int h_allgather(void *s, int sc, struct ompi_datatype_t *sd, void *r, int
     return OMPI_SUCCESS;
 }
 
+/* dense layouts only (the host module's gather / alltoall move bytes) */
+static int h_dense(const struct ompi_datatype_t *d)
+{
+    return (d->super.flags & OPAL_DATATYPE_FLAG_NO_GAPS) && d->super.true_lb == 0 &&
+           (size_t)(d->super.ub - d->super.lb) == d->super.size;
+}
+
+/* MPI_Gather: rank q's block broadcast by q through its slot, kept by the root (coll/basic's linear
+ * gather moves the same bytes, coll_basic_gather.c:40-110) */
+static int h_gather(void *s, int sc, struct ompi_datatype_t *sd, void *r, int rc, struct ompi_datatype_t *rd, int root,
+                    struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)m;
+    const int n = c->c_local_group->grp_proc_count, me = c->c_my_rank;
+    if (chan_index(c) < 0) return stub_marker;
+    if (guard("gather", 2, s == MPI_IN_PLACE ? NULL : s, me == root ? r : NULL)) return MINI_ERR_DEVICE_BUFFER;
+    if ((s != MPI_IN_PLACE && !h_dense(sd)) || (me == root && !h_dense(rd))) return OMPI_ERR_NOT_SUPPORTED;
+    const size_t blk = me == root ? (size_t)rc * rd->super.size : (size_t)sc * sd->super.size;
+    ompi_datatype_t *bytes = (ompi_datatype_t *)&ompi_mpi_byte;
+    char *tmp = malloc(blk + 1);
+    if (!tmp) return OMPI_ERR_OUT_OF_RESOURCE;
+    if (me == root && s != MPI_IN_PLACE) memcpy((char *)r + (size_t)root * blk, s, blk);
+    int e = OMPI_SUCCESS;
+    for (int q = 0; q < n && e == OMPI_SUCCESS; ++q) {
+        if (q == root) continue;
+        char *b = me == q ? (char *)s : me == root ? (char *)r + (size_t)q * blk : tmp;
+        e = host_bcast(c, b, blk, bytes, q);
+    }
+    free(tmp);
+    return e;
+}
+
+/* MPI_Alltoall: each rank's n blocks broadcast by it; every rank keeps its own block */
+static int h_alltoall(void *s, int sc, struct ompi_datatype_t *sd, void *r, int rc, struct ompi_datatype_t *rd,
+                      struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)m;
+    (void)sc;
+    (void)sd;
+    const int n = c->c_local_group->grp_proc_count, me = c->c_my_rank;
+    if (chan_index(c) < 0) return stub_marker;
+    if (guard("alltoall", 2, s == MPI_IN_PLACE ? NULL : s, r)) return MINI_ERR_DEVICE_BUFFER;
+    if ((s != MPI_IN_PLACE && !h_dense(sd)) || !h_dense(rd)) return OMPI_ERR_NOT_SUPPORTED;
+    const size_t blk = (size_t)rc * rd->super.size, all = blk * (size_t)n;
+    ompi_datatype_t *bytes = (ompi_datatype_t *)&ompi_mpi_byte;
+    char *mine = malloc(all + 1), *tmp = malloc(all + 1);
+    if (!mine || !tmp) {
+        free(mine);
+        free(tmp);
+        return OMPI_ERR_OUT_OF_RESOURCE;
+    }
+    memcpy(mine, s == MPI_IN_PLACE ? r : s, all);
+    int e = OMPI_SUCCESS;
+    for (int q = 0; q < n && e == OMPI_SUCCESS; ++q) {
+        if (me == q) memcpy(tmp, mine, all);
+        e = host_bcast(c, tmp, all, bytes, q);
+        if (e == OMPI_SUCCESS) memcpy((char *)r + (size_t)q * blk, tmp + (size_t)me * blk, blk);
+    }
+    free(mine);
+    free(tmp);
+    return e;
+}
+
 /* ---- nonblocking: queued, run in posting order from the progress callback */
 typedef struct mini_hreq {
     ompi_request_t super;
@@ -1496,6 +1569,8 @@ mca_coll_base_module_t *mini_host_module(void)
     m->coll_exscan = h_exscan;
     m->coll_bcast = h_bcast;
     m->coll_allgather = h_allgather;
+    m->coll_gather = h_gather;
+    m->coll_alltoall = h_alltoall;
     m->coll_iallreduce = h_iallreduce;
     m->coll_ireduce = h_ireduce;
     m->coll_ireduce_scatter_block = h_irsb;

@@ -334,18 +334,21 @@ int mca_coll_mi355x_svc_idle_us = 1000;
 int mca_coll_mi355x_svc_shrink_us = 100;
 int mca_coll_mi355x_selftest = 1;
 
-/* 1: run the engine (*dev: this rank's buffers are all device memory); 0: the host path on every
- * rank; < 0: an error (the vote failed or timed out) */
+/* 1: the call runs in the engine (a rank with host buffers joins on device copies); 0: it runs in
+ * the previous component on every rank (a rank with device buffers stages them to the host, as
+ * coll/cuda does); < 0: an error (the vote failed).  dev: this rank's buffers are all device
+ * memory.  Which side of a call waits for the other's votes is agreed per window of calls
+ * (mi355x_comm_vote), so a host-only program pays a store per call, a device program nothing. */
 static int route(mca_coll_mi355x_module_t *m, int dev)
 {
     if (!m->mixed) return dev;
-    int any = dev;
-    const int rc = mi355x_comm_vote(m->engine, dev, &any);
+    int engine = dev;
+    const int rc = mi355x_comm_vote(m->engine, dev, &engine);
     if (rc != MI355X_SUCCESS) {
         fprintf(stderr, "[coll/mi355x] %s\n", mi355x_last_error());
         return -1;
     }
-    return any;
+    return engine;
 }
 
 /* device copy of a host input (scratch slot `slot`), or the buffer itself when it is on the device */
@@ -376,11 +379,14 @@ static int copy_back(void *host, const void *dev, size_t bytes, int rc)
     return mi355x_memcpy(host, dev, bytes);
 }
 
-#define ROUTE_OR(PREV_CALL)                                                            \
+/* PREV_CALL: the previous component on this rank's own (host) buffers; STAGED_CALL: the same with
+ * this rank's device buffers staged through host memory (a device rank in a call that runs on the
+ * host) */
+#define ROUTE_OR(PREV_CALL, STAGED_CALL)                                               \
     do {                                                                               \
         const int r_ = route(m, dev);                                                  \
         if (r_ < 0) return OMPI_ERROR;                                                 \
-        if (r_ == 0) return PREV_CALL;                                                 \
+        if (r_ == 0) return dev ? (STAGED_CALL) : (PREV_CALL);                         \
     } while (0)
 
 /* ------------------------------------------------------------------ coll/cuda's host staging
@@ -470,6 +476,82 @@ static int staged_allreduce(mca_coll_mi355x_module_t *m, void *sbuf, void *rbuf,
     return hunstage2(st, m->prev_allreduce(sbuf, rbuf, count, dtype, op, comm, m->prev_allreduce_module));
 }
 
+/* coll_cuda_reduce.c:43-78; only the root's rbuf is significant */
+static int staged_reduce(mca_coll_mi355x_module_t *m, void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                         struct ompi_op_t *op, int root, struct ompi_communicator_t *comm)
+{
+    const int me = mi355x_comm_rank_of(comm), inplace = (sbuf == MPI_IN_PLACE);
+    const size_t span = dt_span(dtype, (size_t)count);
+    hstage_t st[2];
+    void *ra = me == root ? rbuf : NULL;
+    const int rc = hstage2(st, &sbuf, span, &ra, span, inplace, span, dtype);
+    if (rc != OMPI_SUCCESS) return rc;
+    return hunstage2(st, m->prev_reduce(sbuf, me == root ? ra : rbuf, count, dtype, op, root, comm, m->prev_reduce_module));
+}
+
+/* coll_cuda_reduce_scatter_block.c:45-83 (in place: rbuf holds the n blocks) */
+static int staged_reduce_scatter_block(mca_coll_mi355x_module_t *m, void *sbuf, void *rbuf, int rcount,
+                                       struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                       struct ompi_communicator_t *comm)
+{
+    const int inplace = (sbuf == MPI_IN_PLACE);
+    const size_t in = dt_span(dtype, (size_t)rcount * (size_t)mi355x_comm_size_of(comm));
+    const size_t out = dt_span(dtype, (size_t)rcount);
+    hstage_t st[2];
+    const int rc = hstage2(st, &sbuf, in, &rbuf, inplace ? in : out, inplace, out, dtype);
+    if (rc != OMPI_SUCCESS) return rc;
+    return hunstage2(st, m->prev_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm,
+                                                      m->prev_reduce_scatter_block_module));
+}
+
+/* staged like reduce_scatter_block (in place: rbuf holds every block) */
+static int staged_reduce_scatter(mca_coll_mi355x_module_t *m, void *sbuf, void *rbuf, int *rcounts,
+                                 struct ompi_datatype_t *dtype, struct ompi_op_t *op, struct ompi_communicator_t *comm)
+{
+    const int inplace = (sbuf == MPI_IN_PLACE);
+    const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm);
+    size_t total = 0;
+    for (int q = 0; q < n; ++q) total += (size_t)(rcounts[q] > 0 ? rcounts[q] : 0);
+    const size_t in = dt_span(dtype, total), out = dt_span(dtype, (size_t)(rcounts[me] > 0 ? rcounts[me] : 0));
+    hstage_t st[2];
+    const int rc = hstage2(st, &sbuf, in, &rbuf, inplace ? in : out, inplace, out, dtype);
+    if (rc != OMPI_SUCCESS) return rc;
+    return hunstage2(st, m->prev_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, m->prev_reduce_scatter_module));
+}
+
+/* the send and receive sides of a data-movement call staged to the host (coll/cuda's rule applied
+ * to the movement collectives): the send span copied in; the receive span copied in too (its gaps
+ * keep their bytes) and back after the call.  A side is (buffer, type, span); NULL / MPI_IN_PLACE /
+ * host buffers are left alone. */
+static int stage_move(hstage_t st[2], void **sa, const struct ompi_datatype_t *sdt, size_t sspan, void **ra,
+                      const struct ompi_datatype_t *rdt, size_t rspan)
+{
+    memset(st, 0, 2 * sizeof(hstage_t));
+    int rc = sa ? hstage(&st[0], sa, sdt, sspan, 1, 0) : OMPI_SUCCESS;
+    if (rc == OMPI_SUCCESS && ra && (rc = hstage(&st[1], ra, rdt, rspan, 1, rspan)) != OMPI_SUCCESS) hunstage(&st[0], rc);
+    if (rc == OMPI_SUCCESS && (st[0].h || st[1].h)) __atomic_add_fetch(&mca_coll_mi355x_staged_calls, 1, __ATOMIC_RELAXED);
+    return rc;
+}
+
+/* bytes spanned by piece q = counts[q] instances at disps[q] extents (NULL disps: consecutive),
+ * over every piece; SIZE_MAX when a displacement is negative (not staged: an error) */
+static size_t vspan(const struct ompi_datatype_t *dt, int n, const int *counts, const int *disps)
+{
+    const ptrdiff_t ext = dt->super.ub - dt->super.lb;
+    size_t best = 0, next = 0;
+    for (int q = 0; q < n; ++q) {
+        const size_t c = counts[q] > 0 ? (size_t)counts[q] : 0;
+        const long d = disps ? (long)disps[q] : (long)next;
+        if (d < 0) return (size_t)-1;
+        next = (size_t)d + c;
+        if (c) {
+            const size_t e = (size_t)d * (size_t)ext + dt_span(dt, c);
+            if (e > best) best = e;
+        }
+    }
+    return best;
+}
+
 /* ------------------------------------------------------------------ collectives */
 int mca_coll_mi355x_allreduce(void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
                               struct ompi_op_t *op, struct ompi_communicator_t *comm,
@@ -481,7 +563,8 @@ int mca_coll_mi355x_allreduce(void *sbuf, void *rbuf, int count, struct ompi_dat
     if (count < 0) return m->prev_allreduce(sbuf, rbuf, count, dtype, op, comm, m->prev_allreduce_module);
     if (!engine_op(op, t)) return staged_allreduce(m, sbuf, rbuf, count, dtype, op, comm);
     const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
-    ROUTE_OR(m->prev_allreduce(sbuf, rbuf, count, dtype, op, comm, m->prev_allreduce_module));
+    ROUTE_OR(m->prev_allreduce(sbuf, rbuf, count, dtype, op, comm, m->prev_allreduce_module),
+             staged_allreduce(m, sbuf, rbuf, count, dtype, op, comm));
     if (dev) return map_rc(mi355x_allreduce(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)count, t, op->o_f_to_c_index, NULL));
     const size_t bytes = (size_t)count * mi355x_type_size(t);
     int rc = MI355X_SUCCESS;
@@ -502,17 +585,10 @@ int mca_coll_mi355x_reduce(void *sbuf, void *rbuf, int count, struct ompi_dataty
     const int t = reducible_type(dtype);
     if ((inplace && me != root) || count < 0)
         return m->prev_reduce(sbuf, rbuf, count, dtype, op, root, comm, m->prev_reduce_module);
-    if (!engine_op(op, t)) {  /* coll_cuda_reduce.c:43-78; only the root's rbuf is significant */
-        const size_t span = dt_span(dtype, (size_t)count);
-        hstage_t st[2];
-        void *ra = me == root ? rbuf : NULL;
-        const int rc = hstage2(st, &sbuf, span, &ra, span, inplace, span, dtype);
-        if (rc != OMPI_SUCCESS) return rc;
-        return hunstage2(st, m->prev_reduce(sbuf, me == root ? ra : rbuf, count, dtype, op, root, comm,
-                                            m->prev_reduce_module));
-    }
+    if (!engine_op(op, t)) return staged_reduce(m, sbuf, rbuf, count, dtype, op, root, comm);
     const int dev = (me != root || is_dev(rbuf)) && (inplace || is_dev(sbuf));
-    ROUTE_OR(m->prev_reduce(sbuf, rbuf, count, dtype, op, root, comm, m->prev_reduce_module));
+    ROUTE_OR(m->prev_reduce(sbuf, rbuf, count, dtype, op, root, comm, m->prev_reduce_module),
+             staged_reduce(m, sbuf, rbuf, count, dtype, op, root, comm));
     if (dev)
         return map_rc(mi355x_reduce(m->engine, inplace ? NULL : sbuf, me == root ? rbuf : NULL, (size_t)count, t,
                                     op->o_f_to_c_index, root, NULL));
@@ -533,17 +609,10 @@ int mca_coll_mi355x_reduce_scatter_block(void *sbuf, void *rbuf, int rcount, str
     const int t = reducible_type(dtype);
     if (rcount < 0)
         return m->prev_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, m->prev_reduce_scatter_block_module);
-    if (!engine_op(op, t)) {  /* coll_cuda_reduce_scatter_block.c:45-83 (in place: rbuf holds the n blocks) */
-        const size_t in = dt_span(dtype, (size_t)rcount * (size_t)mi355x_comm_size_of(comm));
-        const size_t out = dt_span(dtype, (size_t)rcount);
-        hstage_t st[2];
-        const int rc = hstage2(st, &sbuf, in, &rbuf, inplace ? in : out, inplace, out, dtype);
-        if (rc != OMPI_SUCCESS) return rc;
-        return hunstage2(st, m->prev_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm,
-                                                          m->prev_reduce_scatter_block_module));
-    }
+    if (!engine_op(op, t)) return staged_reduce_scatter_block(m, sbuf, rbuf, rcount, dtype, op, comm);
     const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
-    ROUTE_OR(m->prev_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, m->prev_reduce_scatter_block_module));
+    ROUTE_OR(m->prev_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, m->prev_reduce_scatter_block_module),
+             staged_reduce_scatter_block(m, sbuf, rbuf, rcount, dtype, op, comm));
     if (dev)
         return map_rc(mi355x_reduce_scatter_block(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)rcount, t,
                                                   op->o_f_to_c_index, NULL));
@@ -566,15 +635,10 @@ int mca_coll_mi355x_reduce_scatter(void *sbuf, void *rbuf, int *rcounts, struct 
     const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm);
     size_t total = 0;
     for (int q = 0; q < n; ++q) total += (size_t)(rcounts[q] > 0 ? rcounts[q] : 0);
-    if (!engine_op(op, t)) {  /* staged like reduce_scatter_block (in place: rbuf holds every block) */
-        const size_t in = dt_span(dtype, total), out = dt_span(dtype, (size_t)(rcounts[me] > 0 ? rcounts[me] : 0));
-        hstage_t st[2];
-        const int rc = hstage2(st, &sbuf, in, &rbuf, inplace ? in : out, inplace, out, dtype);
-        if (rc != OMPI_SUCCESS) return rc;
-        return hunstage2(st, m->prev_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, m->prev_reduce_scatter_module));
-    }
+    if (!engine_op(op, t)) return staged_reduce_scatter(m, sbuf, rbuf, rcounts, dtype, op, comm);
     const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
-    ROUTE_OR(m->prev_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, m->prev_reduce_scatter_module));
+    ROUTE_OR(m->prev_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, m->prev_reduce_scatter_module),
+             staged_reduce_scatter(m, sbuf, rbuf, rcounts, dtype, op, comm));
     if (dev) return map_rc(mi355x_reduce_scatter(m->engine, inplace ? NULL : sbuf, rbuf, rcounts, t, op->o_f_to_c_index, NULL));
     const size_t esz = mi355x_type_size(t), in = total * esz, out = (size_t)(rcounts[me] > 0 ? rcounts[me] : 0) * esz;
     int rc = MI355X_SUCCESS;
@@ -582,6 +646,29 @@ int mca_coll_mi355x_reduce_scatter(void *sbuf, void *rbuf, int *rcounts, struct 
     const void *sd = inplace ? NULL : dev_in(m, 0, sbuf, in, &rc);
     if (rc == MI355X_SUCCESS) rc = mi355x_reduce_scatter(m->engine, sd, rd, rcounts, t, op->o_f_to_c_index, NULL);
     return map_rc(copy_back(rbuf, rd, out, rc));
+}
+
+static int staged_allgather(mca_coll_mi355x_module_t *m, void *sbuf, int scount, struct ompi_datatype_t *sdtype,
+                            void *rbuf, int rcount, struct ompi_datatype_t *rdtype, struct ompi_communicator_t *comm)
+{
+    hstage_t st[2];
+    void *s = sbuf, *r = rbuf;
+    int rc = stage_move(st, &s, sdtype, dt_span(sdtype, (size_t)scount), &r, rdtype,
+                        dt_span(rdtype, (size_t)rcount * (size_t)mi355x_comm_size_of(comm)));
+    if (rc != OMPI_SUCCESS) return rc;
+    return hunstage2(st, m->prev_allgather(s, scount, sdtype, r, rcount, rdtype, comm, m->prev_allgather_module));
+}
+
+static int staged_bcast(mca_coll_mi355x_module_t *m, void *buff, int count, struct ompi_datatype_t *datatype, int root,
+                        struct ompi_communicator_t *comm)
+{
+    hstage_t st[2];
+    void *b = buff;
+    const size_t span = dt_span(datatype, (size_t)count);
+    const int me = mi355x_comm_rank_of(comm);
+    int rc = me == root ? stage_move(st, &b, datatype, span, NULL, NULL, 0) : stage_move(st, NULL, NULL, 0, &b, datatype, span);
+    if (rc != OMPI_SUCCESS) return rc;
+    return hunstage2(st, m->prev_bcast(b, count, datatype, root, comm, m->prev_bcast_module));
 }
 
 int mca_coll_mi355x_allgather(void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
@@ -593,8 +680,9 @@ int mca_coll_mi355x_allgather(void *sbuf, int scount, struct ompi_datatype_t *sd
     if (rcount < 0 || (!inplace && scount < 0))
         return m->prev_allgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_allgather_module);
     const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
-    ROUTE_OR(m->prev_allgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_allgather_module));
     const int n = mi355x_comm_size_of(comm), me = mi355x_comm_rank_of(comm);
+    ROUTE_OR(m->prev_allgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_allgather_module),
+             staged_allgather(m, sbuf, scount, sdtype, rbuf, rcount, rdtype, comm));
     size_t rb = 0, sb = 0;
     if (!dev) {  /* host buffers in a call where peers hold device ones: dense layouts, staged */
         if (!contiguous_bytes(rdtype, rcount, &rb) || (!inplace && (!contiguous_bytes(sdtype, scount, &sb) || sb != rb))) {
@@ -639,7 +727,8 @@ int mca_coll_mi355x_bcast(void *buff, int count, struct ompi_datatype_t *datatyp
     size_t bytes = 0;
     if (count < 0) return m->prev_bcast(buff, count, datatype, root, comm, m->prev_bcast_module);
     const int dev = is_dev(buff);
-    ROUTE_OR(m->prev_bcast(buff, count, datatype, root, comm, m->prev_bcast_module));
+    ROUTE_OR(m->prev_bcast(buff, count, datatype, root, comm, m->prev_bcast_module),
+             staged_bcast(m, buff, count, datatype, root, comm));
     const int me = mi355x_comm_rank_of(comm);
     if (!dev) {  /* host buffer in a call where peers hold device ones: dense layouts, staged */
         if (!contiguous_bytes(datatype, count, &bytes)) {
@@ -773,7 +862,14 @@ int mca_coll_mi355x_gather(void *sbuf, int scount, struct ompi_datatype_t *sdtyp
     if (inplace && me != root)
         return m->prev_gather(sbuf, scount, sdtype, rbuf, rcount, rdtype, root, comm, m->prev_gather_module);
     const int dev = (me != root || is_dev(rbuf)) && (inplace || is_dev(sbuf));
-    ROUTE_OR(m->prev_gather(sbuf, scount, sdtype, rbuf, rcount, rdtype, root, comm, m->prev_gather_module));
+    ROUTE_OR(m->prev_gather(sbuf, scount, sdtype, rbuf, rcount, rdtype, root, comm, m->prev_gather_module), ({
+                 hstage_t st_[2];
+                 void *s_ = sbuf, *r_ = rbuf;
+                 int rc_ = stage_move(st_, inplace ? NULL : &s_, sdtype, dt_span(sdtype, (size_t)scount),
+                                      me == root ? &r_ : NULL, rdtype, dt_span(rdtype, (size_t)rcount * (size_t)n));
+                 rc_ == OMPI_SUCCESS ? hunstage2(st_, m->prev_gather(s_, scount, sdtype, r_, rcount, rdtype, root, comm,
+                                                                     m->prev_gather_module)) : rc_;
+             }));
     side_t snd, rcv;
     int rc = OMPI_SUCCESS;
     if (!inplace && (rc = side_init(m, &snd, 0, sbuf, sdtype, 1, NULL, scount, NULL))) return rc;
@@ -794,7 +890,16 @@ int mca_coll_mi355x_gatherv(void *sbuf, int scount, struct ompi_datatype_t *sdty
     if (n > SIDE_MAX || (inplace && me != root))
         return m->prev_gatherv(sbuf, scount, sdtype, rbuf, rcounts, disps, rdtype, root, comm, m->prev_gatherv_module);
     const int dev = (me != root || is_dev(rbuf)) && (inplace || is_dev(sbuf));
-    ROUTE_OR(m->prev_gatherv(sbuf, scount, sdtype, rbuf, rcounts, disps, rdtype, root, comm, m->prev_gatherv_module));
+    ROUTE_OR(m->prev_gatherv(sbuf, scount, sdtype, rbuf, rcounts, disps, rdtype, root, comm, m->prev_gatherv_module), ({
+                 hstage_t st_[2];
+                 void *s_ = sbuf, *r_ = rbuf;
+                 const size_t rs_ = me == root ? vspan(rdtype, n, rcounts, disps) : 0;
+                 int rc_ = rs_ == (size_t)-1 ? OMPI_ERR_NOT_SUPPORTED
+                                             : stage_move(st_, inplace ? NULL : &s_, sdtype, dt_span(sdtype, (size_t)scount),
+                                                          me == root ? &r_ : NULL, rdtype, rs_);
+                 rc_ == OMPI_SUCCESS ? hunstage2(st_, m->prev_gatherv(s_, scount, sdtype, r_, rcounts, disps, rdtype, root,
+                                                                      comm, m->prev_gatherv_module)) : rc_;
+             }));
     side_t snd, rcv;
     int rc = OMPI_SUCCESS;
     if (!inplace && (rc = side_init(m, &snd, 0, sbuf, sdtype, 1, NULL, scount, NULL))) return rc;
@@ -816,7 +921,14 @@ int mca_coll_mi355x_scatter(void *sbuf, int scount, struct ompi_datatype_t *sdty
     if (inplace && me != root)
         return m->prev_scatter(sbuf, scount, sdtype, rbuf, rcount, rdtype, root, comm, m->prev_scatter_module);
     const int dev = (me != root || is_dev(sbuf)) && (inplace || is_dev(rbuf));
-    ROUTE_OR(m->prev_scatter(sbuf, scount, sdtype, rbuf, rcount, rdtype, root, comm, m->prev_scatter_module));
+    ROUTE_OR(m->prev_scatter(sbuf, scount, sdtype, rbuf, rcount, rdtype, root, comm, m->prev_scatter_module), ({
+                 hstage_t st_[2];
+                 void *s_ = sbuf, *r_ = rbuf;
+                 int rc_ = stage_move(st_, me == root ? &s_ : NULL, sdtype, dt_span(sdtype, (size_t)scount * (size_t)n),
+                                      inplace ? NULL : &r_, rdtype, dt_span(rdtype, (size_t)rcount));
+                 rc_ == OMPI_SUCCESS ? hunstage2(st_, m->prev_scatter(s_, scount, sdtype, r_, rcount, rdtype, root, comm,
+                                                                      m->prev_scatter_module)) : rc_;
+             }));
     side_t snd, rcv;
     int rc = OMPI_SUCCESS;
     if (me == root && (rc = side_init(m, &snd, 0, sbuf, sdtype, n, NULL, scount, NULL))) return rc;
@@ -838,7 +950,16 @@ int mca_coll_mi355x_scatterv(void *sbuf, int *scounts, int *disps, struct ompi_d
         return m->prev_scatterv(sbuf, scounts, disps, sdtype, rbuf, rcount, rdtype, root, comm,
                                 m->prev_scatterv_module);
     const int dev = (me != root || is_dev(sbuf)) && (inplace || is_dev(rbuf));
-    ROUTE_OR(m->prev_scatterv(sbuf, scounts, disps, sdtype, rbuf, rcount, rdtype, root, comm, m->prev_scatterv_module));
+    ROUTE_OR(m->prev_scatterv(sbuf, scounts, disps, sdtype, rbuf, rcount, rdtype, root, comm, m->prev_scatterv_module), ({
+                 hstage_t st_[2];
+                 void *s_ = sbuf, *r_ = rbuf;
+                 const size_t ss_ = me == root ? vspan(sdtype, n, scounts, disps) : 0;
+                 int rc_ = ss_ == (size_t)-1 ? OMPI_ERR_NOT_SUPPORTED
+                                             : stage_move(st_, me == root ? &s_ : NULL, sdtype, ss_, inplace ? NULL : &r_,
+                                                          rdtype, dt_span(rdtype, (size_t)rcount));
+                 rc_ == OMPI_SUCCESS ? hunstage2(st_, m->prev_scatterv(s_, scounts, disps, sdtype, r_, rcount, rdtype, root,
+                                                                       comm, m->prev_scatterv_module)) : rc_;
+             }));
     side_t snd, rcv;
     int rc = OMPI_SUCCESS;
     if (me == root && (rc = side_init(m, &snd, 0, sbuf, sdtype, n, scounts, 0, disps))) return rc;
@@ -860,7 +981,16 @@ int mca_coll_mi355x_allgatherv(void *sbuf, int scount, struct ompi_datatype_t *s
     if (n > SIDE_MAX)
         return m->prev_allgatherv(sbuf, scount, sdtype, rbuf, rcounts, disps, rdtype, comm, m->prev_allgatherv_module);
     const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
-    ROUTE_OR(m->prev_allgatherv(sbuf, scount, sdtype, rbuf, rcounts, disps, rdtype, comm, m->prev_allgatherv_module));
+    ROUTE_OR(m->prev_allgatherv(sbuf, scount, sdtype, rbuf, rcounts, disps, rdtype, comm, m->prev_allgatherv_module), ({
+                 hstage_t st_[2];
+                 void *s_ = sbuf, *r_ = rbuf;
+                 const size_t rs_ = vspan(rdtype, n, rcounts, disps);
+                 int rc_ = rs_ == (size_t)-1 ? OMPI_ERR_NOT_SUPPORTED
+                                             : stage_move(st_, inplace ? NULL : &s_, sdtype, dt_span(sdtype, (size_t)scount),
+                                                          &r_, rdtype, rs_);
+                 rc_ == OMPI_SUCCESS ? hunstage2(st_, m->prev_allgatherv(s_, scount, sdtype, r_, rcounts, disps, rdtype, comm,
+                                                                         m->prev_allgatherv_module)) : rc_;
+             }));
     side_t snd, rcv;
     int rc = OMPI_SUCCESS;
     if (!inplace && (rc = side_init(m, &snd, 0, sbuf, sdtype, 1, NULL, scount, NULL))) return rc;
@@ -880,7 +1010,14 @@ int mca_coll_mi355x_alltoall(void *sbuf, int scount, struct ompi_datatype_t *sdt
     const int n = mi355x_comm_size_of(comm), inplace = (sbuf == MPI_IN_PLACE);
     if (n > SIDE_MAX) return m->prev_alltoall(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_alltoall_module);
     const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
-    ROUTE_OR(m->prev_alltoall(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_alltoall_module));
+    ROUTE_OR(m->prev_alltoall(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_alltoall_module), ({
+                 hstage_t st_[2];
+                 void *s_ = sbuf, *r_ = rbuf;
+                 int rc_ = stage_move(st_, inplace ? NULL : &s_, sdtype, dt_span(sdtype, (size_t)scount * (size_t)n), &r_,
+                                      rdtype, dt_span(rdtype, (size_t)rcount * (size_t)n));
+                 rc_ == OMPI_SUCCESS ? hunstage2(st_, m->prev_alltoall(s_, scount, sdtype, r_, rcount, rdtype, comm,
+                                                                       m->prev_alltoall_module)) : rc_;
+             }));
     side_t snd, rcv;
     int rc = OMPI_SUCCESS;
     if (!inplace && (rc = side_init(m, &snd, 0, sbuf, sdtype, n, NULL, scount, NULL))) return rc;
@@ -902,7 +1039,16 @@ int mca_coll_mi355x_alltoallv(void *sbuf, int *scounts, int *sdisps, struct ompi
                                  m->prev_alltoallv_module);
     const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
     ROUTE_OR(m->prev_alltoallv(sbuf, scounts, sdisps, sdtype, rbuf, rcounts, rdisps, rdtype, comm,
-                               m->prev_alltoallv_module));
+                               m->prev_alltoallv_module), ({
+                 hstage_t st_[2];
+                 void *s_ = sbuf, *r_ = rbuf;
+                 const size_t ss_ = inplace ? 0 : vspan(sdtype, n, scounts, sdisps), rs_ = vspan(rdtype, n, rcounts, rdisps);
+                 int rc_ = (ss_ == (size_t)-1 || rs_ == (size_t)-1)
+                               ? OMPI_ERR_NOT_SUPPORTED
+                               : stage_move(st_, inplace ? NULL : &s_, sdtype, ss_, &r_, rdtype, rs_);
+                 rc_ == OMPI_SUCCESS ? hunstage2(st_, m->prev_alltoallv(s_, scounts, sdisps, sdtype, r_, rcounts, rdisps,
+                                                                        rdtype, comm, m->prev_alltoallv_module)) : rc_;
+             }));
     side_t snd, rcv;
     int rc = OMPI_SUCCESS;
     if (!inplace && (rc = side_init(m, &snd, 0, sbuf, sdtype, n, scounts, 0, sdisps))) return rc;
@@ -923,19 +1069,22 @@ static int scan_common(mca_coll_mi355x_module_t *m, int exclusive, void *sbuf, v
     (exclusive ? m->prev_exscan(S, R, count, dtype, op, comm, m->prev_exscan_module)                 \
                : m->prev_scan(S, R, count, dtype, op, comm, m->prev_scan_module))
     if (count < 0) return SCAN_PREV(sbuf, rbuf);
-    if (!engine_op(op, t)) {
-        /* coll_cuda_scan.c:41-76 / coll_cuda_exscan.c:41-76; rbuf is copied in for MPI_IN_PLACE and
-         * for exscan (rank 0's rbuf is left as it was) */
-        const size_t span = dt_span(dtype, (size_t)count);
-        hstage_t st[2];
-        const int rc = hstage2(st, &sbuf, span, &rbuf, span, inplace || exclusive, span, dtype);
-        if (rc != OMPI_SUCCESS) return rc;
-        return hunstage2(st, SCAN_PREV(sbuf, rbuf));
-    }
+    /* coll_cuda_scan.c:41-76 / coll_cuda_exscan.c:41-76; rbuf is copied in for MPI_IN_PLACE and
+     * for exscan (rank 0's rbuf is left as it was) */
+#define SCAN_STAGED()                                                                                 \
+    ({                                                                                                \
+        const size_t span_ = dt_span(dtype, (size_t)count);                                          \
+        hstage_t st_[2];                                                                              \
+        void *s_ = sbuf, *r_ = rbuf;                                                                  \
+        const int rc_ = hstage2(st_, &s_, span_, &r_, span_, inplace || exclusive, span_, dtype);     \
+        rc_ != OMPI_SUCCESS ? rc_ : hunstage2(st_, SCAN_PREV(s_, r_));                                \
+    })
+    if (!engine_op(op, t)) return SCAN_STAGED();
     /* every rank votes its buffer kind, as for allreduce: a rank with host buffers joins the engine
      * on device copies when a peer has device buffers */
     const int dev = is_dev(rbuf) && (inplace || is_dev(sbuf));
-    ROUTE_OR(SCAN_PREV(sbuf, rbuf));
+    ROUTE_OR(SCAN_PREV(sbuf, rbuf), SCAN_STAGED());
+#undef SCAN_STAGED
 #undef SCAN_PREV
     if (dev)
         return map_rc((exclusive ? mi355x_exscan : mi355x_scan)(m->engine, inplace ? NULL : sbuf, rbuf, (size_t)count,

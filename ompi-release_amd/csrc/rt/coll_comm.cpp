@@ -300,33 +300,51 @@ int mi355x_set_progress_hook(void (*progress)(void))
     return MI355X_SUCCESS;
 }
 
-// A host-buffer rank waits here for its peers' votes.  It must not stall other work meanwhile: the
-// wait drives the caller's progress engine (opal_progress through the hook) and this
-// communicator's point-to-point, so a peer that first needs an outstanding send of ours to
-// complete still gets there (ob1's blocking waits progress the same way, req_wait.c).  The wait is
-// unbounded, like a host collective's receive: a rank that is late by minutes (checkpoint I/O) is
-// not an error, and nothing poisons the communicator.
-int mi355x_comm_vote(mi355x_comm_t *c, int device, int *any_device)
+// The buffer-kind vote (mi355x_rt.h).  One side of a call waits for every vote: both at a window's
+// checkpoint (every kVoteWindow-th call), the host ranks in a window that follows device use (they
+// join the engine on device copies when a peer holds device buffers), the device ranks otherwise
+// (they stage to the host component when a peer holds host buffers).  The mode of the next window
+// is a function of the checkpoint's votes, which every rank reads, so every rank agrees on it.  A
+// non-waiting rank may run ahead: a host rank by many host calls (a bcast root), a device rank by
+// at most the engine's own slack, since every engine call needs every rank; so a waiter that finds
+// a peer's ring entry already reused by a later call knows that peer did not wait in the engine --
+// it voted host.  A waiter must not stall other work: the wait drives the caller's progress engine
+// (opal_progress through the hook) and this communicator's point-to-point, so a peer that first
+// needs an outstanding send of ours to complete still gets there (ob1's blocking waits progress the
+// same way, req_wait.c).  The wait is unbounded, like a host collective's receive: a rank that is
+// late by minutes (checkpoint I/O) is not an error, and nothing poisons the communicator.
+int mi355x_comm_vote(mi355x_comm_t *c, int device, int *engine)
 {
-    if (!c || !any_device) return set_error(MI355X_ERR_ARG, "NULL argument");
-    *any_device = device ? 1 : 0;
+    if (!c || !engine) return set_error(MI355X_ERR_ARG, "NULL argument");
+    *engine = device ? 1 : 0;
     if (c->size == 1) return MI355X_SUCCESS;
     const uint64_t s = ++c->vote_seq;
+    const bool ckpt = (s % kVoteWindow) == 0;
+    if (device) c->vote_window_dev = true;
     Ctrl *k = c->ctrl;
-    k->slot[c->rank].vote[s % kVoteRing].store((s << 1) | (device ? 1u : 0u), std::memory_order_release);
-    if (device) return MI355X_SUCCESS;
+    const uint64_t word = (s << 2) | ((ckpt && c->vote_window_dev) ? 2u : 0u) | (device ? 1u : 0u);
+    k->slot[c->rank].vote[s % kVoteRing].store(word, std::memory_order_release);
+    const bool wait = ckpt || (c->vote_host_waits ? !device : device);
+    if (!wait) return MI355X_SUCCESS;  // (*engine = device: a host rank is never in the engine here, nor a device rank out of it)
+    bool any_dev = device, all_dev = device, win_dev = c->vote_window_dev;
     for (int r = 0; r < c->size; ++r) {
         if (r == c->rank) continue;
         unsigned spins = 0;
         for (;;) {
             const uint64_t v = k->slot[r].vote[s % kVoteRing].load(std::memory_order_acquire);
-            if ((v >> 1) == s) {
-                if (v & 1u) *any_device = 1;
+            if ((v >> 2) == s) {
+                any_dev = any_dev || (v & 1u);
+                all_dev = all_dev && (v & 1u);
+                win_dev = win_dev || (v & 2u);
                 break;
             }
-            if ((v >> 1) > s)
-                return set_error(MI355X_ERR_PEER, "rank %d is %d or more collectives ahead of rank %d", r,
-                                 kVoteRing, c->rank);
+            if ((v >> 2) > s) {
+                if (ckpt || c->vote_host_waits)  // (every rank waits at a checkpoint; a device rank in this mode is in the engine)
+                    return set_error(MI355X_ERR_PEER, "rank %d is %d or more collectives ahead of rank %d", r,
+                                     kVoteRing, c->rank);
+                all_dev = false;  // a host rank that ran ahead
+                break;
+            }
             if (k->abort_flag.load(std::memory_order_relaxed))
                 return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
             if (++spins > 2048) {
@@ -338,6 +356,13 @@ int mi355x_comm_vote(mi355x_comm_t *c, int device, int *any_device)
                 sched_yield();
             }
         }
+    }
+    if (ckpt) {
+        *engine = any_dev ? 1 : 0;  // a mixed checkpoint call runs in the engine
+        c->vote_host_waits = win_dev;
+        c->vote_window_dev = false;
+    } else {
+        *engine = c->vote_host_waits ? (any_dev ? 1 : 0) : (all_dev ? 1 : 0);
     }
     return MI355X_SUCCESS;
 }
@@ -415,6 +440,7 @@ int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
     case MI355X_KNOB_FLOWS_FAILED: *value = (long)c->flows_failed; break;
     case MI355X_KNOB_CREATE_US: *value = (long)c->create_us; break;
     case MI355X_KNOB_SELFTEST_US: *value = (long)c->selftest_us; break;
+    case MI355X_KNOB_SELFTEST_REUSED: *value = (long)c->selftest_reused; break;
     case MI355X_KNOB_DEV_SETUP: *value = c->dev_ready ? 1 : 0; break;
     case MI355X_KNOB_SELFTEST: *value = c->selftest ? 1 : 0; break;
     case MI355X_KNOB_PIPE_CALLS: *value = (long)c->pipe_calls; break;

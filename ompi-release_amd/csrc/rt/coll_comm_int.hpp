@@ -94,6 +94,7 @@ int staged_bcast(mi355x_comm *c, void *buf, size_t bytes, int root, hipStream_t 
 bool svc_usable(const mi355x_comm *c, size_t bytes);
 bool ll_usable(const mi355x_comm *c, size_t bytes);
 int ensure_ll(mi355x_comm *c);
+void verdict_store(mi355x_comm *c);  // coll_selftest.cpp: flow verdicts for the member set
 int ll_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s);
 int ll_selftest(mi355x_comm *c);
 uint64_t mono_ns();

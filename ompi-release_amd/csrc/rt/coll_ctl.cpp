@@ -3,6 +3,7 @@
 // the call's finish, the per-communicator scratch (split out of coll_comm.cpp, no change).
 
 #include <fcntl.h>
+#include <hsa/hsa_ext_amd.h>
 #include <immintrin.h>
 #include <poll.h>
 #include <sched.h>
@@ -171,21 +172,28 @@ static bool via_dmabuf(const mi355x_comm *c, size_t bytes)
     return bytes >= c->ipc_max || ((c->rcache_max_maps || c->rcache_limit) && c->dmabuf_state != -1);
 }
 
-// does the dmabuf fd `fd` name the allocation [base, base + bytes) itself?  The runtime exports the
-// whole buffer object an allocation lives in, from the object's start; the allocation is at offset
-// 0 of an object of exactly its size iff the two sizes agree (an allocation carved at offset o > 0
-// out of an object leaves the object at least o + bytes long).  So the check is on identity -- the
-// object's size, read from the fd (dma-buf's llseek), against the allocation's
-// hipMemGetAddressRange size -- as the reference checks identity (IPC handle bytes memcmp'd,
-// common_cuda.c:1581; CU_POINTER_ATTRIBUTE_BUFFER_ID, :1937-1958), never contents.  1 yes, 0 no
-// (another range: such an allocation keeps the hipIpc route, whose handle carries the offset),
-// -1 the fd's size is unknown (treated as no).
-static int export_names(size_t bytes, int fd)
+// does the dmabuf fd `fd` name the allocation at `base` itself, from its first byte?  The runtime
+// exports the whole buffer object an allocation lives in, from the object's start: the ROCr
+// allocation the HIP allocation was carved from (the runtime sub-allocates small hipMallocs out of
+// 2 MiB objects; an allocation of its own has an object of its size rounded up to 2 MiB --
+// tools/probe/bo_sizes.py, profiles/r06_bo_sizes.jsonl).  So the check is on identity, as the
+// reference's is (IPC handle bytes memcmp'd, common_cuda.c:1581; CU_POINTER_ATTRIBUTE_BUFFER_ID,
+// :1937-1958), never on contents: ROCr's allocation containing `base` must start at `base`
+// (hsa_amd_pointer_info's agentBaseAddress), and the fd must be that allocation (its size, read with
+// dma-buf's llseek, equals ROCr's sizeInBytes).  1 yes; 0 no (such an allocation keeps the hipIpc
+// route, whose handle carries the offset); -1 unknown (treated as no).
+static int export_names(void *base, int fd)
 {
     const off_t end = lseek(fd, 0, SEEK_END);
     if (end < 0) return -1;
     (void)lseek(fd, 0, SEEK_SET);
-    return (size_t)end == bytes ? 1 : 0;
+    hsa_amd_pointer_info_t info;
+    std::memset(&info, 0, sizeof(info));
+    info.size = sizeof(info);
+    if (hsa_amd_pointer_info(base, &info, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+        info.type == HSA_EXT_POINTER_TYPE_UNKNOWN)
+        return -1;
+    return (info.agentBaseAddress == base && (size_t)end == info.sizeInBytes) ? 1 : 0;
 }
 
 int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
@@ -249,7 +257,7 @@ int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force)
             (void)hipGetLastError();
             reg.fd = -1;
             dm = false;
-        } else if (c->export_check && export_names(sz, reg.fd) != 1) {
+        } else if (c->export_check && export_names(base, reg.fd) != 1) {
             // the fd names another range: the runtime exports the whole buffer object an allocation
             // was carved from (small allocations share one), from its start -- such an allocation
             // keeps the hipIpc route (whose handle carries the offset)

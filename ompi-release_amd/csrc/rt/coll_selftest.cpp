@@ -254,6 +254,7 @@ int svc_selftest(mi355x_comm *c)
     }
     c->selftest_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     TRACE(c, "service flow self-test: passed here 0x%x, agreed 0x%x", pass, all & tested);
+    verdict_store(c);
     return MI355X_SUCCESS;
 }
 
@@ -388,6 +389,99 @@ int svc_maybe_claim(mi355x_comm *c, bool sized)
     return svc_claim(c);
 }
 
+// ---- flow verdicts reused across communicators.  The self-tests above check mechanisms between
+// processes and GPUs -- IPC-mapped LL regions, flag hand-offs over xGMI, the resident service's
+// forms -- not anything of one communicator, so a communicator whose members are the same processes
+// on the same GPUs as an earlier one (an MPI_Comm_dup, a split that keeps the group) takes the
+// earlier verdicts over instead of running the tests again (31.7 ms at 2 ranks, 71 ms at 8,
+// profiles/r05_lazy_setup.txt).  Key: the sorted set of (device uid, pid, process start time) of
+// the members; every rank publishes a hash of the verdicts it holds for the key, and they are
+// reused only if every rank holds the same ones -- so a flow that failed anywhere stays off for
+// the dup as well.
+struct FlowVerdict {
+    bool ll_ok = false;
+    unsigned flows = 0, failed = 0;  // MI355X_FLOW_* agreed on / turned off
+    bool pipe_tested = false, svc_tested = false;
+};
+static std::mutex g_verdict_mtx;
+static std::map<std::string, FlowVerdict> g_verdicts;
+
+static std::string member_key(const mi355x_comm *c)
+{
+    std::vector<std::array<uint64_t, 3>> m;
+    for (int q = 0; q < c->size; ++q) {
+        const RankSlot &r = c->ctrl->slot[q];
+        m.push_back({r.dev_uid, (uint64_t)(uint32_t)r.pid, r.pid_start});
+    }
+    std::sort(m.begin(), m.end());
+    std::string k;
+    char b[64];
+    for (const auto &e : m) {
+        snprintf(b, sizeof(b), "%llx:%llx:%llx;", (unsigned long long)e[0], (unsigned long long)e[1],
+                 (unsigned long long)e[2]);
+        k += b;
+    }
+    return k;
+}
+
+static uint64_t verdict_hash(const std::string &key, const FlowVerdict &v)
+{
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
+    for (char ch : key) mix((unsigned char)ch);
+    mix(v.ll_ok);
+    mix(v.flows);
+    mix(v.failed);
+    mix(v.pipe_tested);
+    mix(v.svc_tested);
+    return h | 1;  // (0 means "none")
+}
+
+// record this communicator's verdicts (after its tests; every rank of it records the same)
+void verdict_store(mi355x_comm *c)
+{
+    if (c->size < 2 || c->loopback || !selftest_on(c)) return;
+    FlowVerdict v;
+    v.ll_ok = c->ll_ok;
+    v.flows = c->flows;
+    v.failed = c->flows_failed;
+    v.pipe_tested = !c->pipe_untested;
+    v.svc_tested = c->svc_flows_tested;
+    std::lock_guard<std::mutex> g(g_verdict_mtx);
+    g_verdicts[member_key(c)] = v;
+}
+
+// collective: take over verdicts every rank holds for this member set; true if taken
+static int verdict_reuse(mi355x_comm *c, FlowVerdict *out, bool *reused)
+{
+    *reused = false;
+    if (!selftest_on(c) || env_double("MI355X_SELFTEST_REUSE", 1.0) == 0.0) return MI355X_SUCCESS;
+    const std::string key = member_key(c);
+    FlowVerdict v;
+    bool have = false;
+    {
+        std::lock_guard<std::mutex> g(g_verdict_mtx);
+        auto it = g_verdicts.find(key);
+        if (it != g_verdicts.end()) {
+            v = it->second;
+            have = true;
+        }
+    }
+    const uint64_t h = have ? verdict_hash(key, v) : 0;
+    c->ctrl->slot[c->rank].verdict.store(h, std::memory_order_release);
+    int rc = barrier(c);
+    if (rc) return rc;
+    bool all = h != 0;
+    for (int q = 0; q < c->size && all; ++q) all = c->ctrl->slot[q].verdict.load(std::memory_order_acquire) == h;
+    rc = barrier(c);  // every rank has read the hashes before they are rewritten
+    if (rc) return rc;
+    if (all) {
+        *out = v;
+        *reused = true;
+    }
+    return MI355X_SUCCESS;
+}
+
 // at creation: the service's settings (the claim itself waits for a service-sized call)
 // The communicator's device-side setup: the completion words, the LL region and its self-test, the
 // service's resources and the pipelined flow's self-test, with their allocations.  Deferred from
@@ -405,10 +499,32 @@ int dev_setup(mi355x_comm *c)
     if (c->size < 2 || c->loopback) return MI355X_SUCCESS;
     const auto t0 = std::chrono::steady_clock::now();
     int rc = setup_done_words(c);
-    if (rc == MI355X_SUCCESS) rc = ll_selftest(c);
-    if (rc == MI355X_SUCCESS) {
-        svc_setup(c);
-        rc = pipe_selftest(c);
+    FlowVerdict v;
+    bool reused = false;
+    if (rc == MI355X_SUCCESS) rc = verdict_reuse(c, &v, &reused);
+    if (rc == MI355X_SUCCESS && reused) {
+        // an earlier communicator of these processes tested the flows: its verdicts, no tests
+        c->ll_ok = v.ll_ok;
+        if (c->ll_ok) rc = ensure_ll(c);
+        else c->ll_max = 0;
+        const unsigned tested = MI355X_FLOW_PIPE | (v.svc_tested ? (unsigned)(MI355X_FLOW_SVC_LL | MI355X_FLOW_SVC_PULL |
+                                                                              MI355X_FLOW_SVC_COPY | MI355X_FLOW_SVC_RS)
+                                                                   : 0u);
+        c->flows = (c->flows & ~tested) | (v.flows & tested);
+        c->flows_failed |= v.failed & tested;
+        c->pipe_untested = !v.pipe_tested;
+        if (!(c->flows & MI355X_FLOW_PIPE)) c->pipe_on = false;
+        c->svc_flows_tested = v.svc_tested;
+        c->selftest_reused = v.svc_tested ? 2 : 1;
+        if (rc == MI355X_SUCCESS) svc_setup(c);
+        TRACE(c, "device setup: flow verdicts of an earlier communicator of these processes reused (flows 0x%x)", c->flows);
+    } else {
+        if (rc == MI355X_SUCCESS) rc = ll_selftest(c);
+        if (rc == MI355X_SUCCESS) {
+            svc_setup(c);
+            rc = pipe_selftest(c);
+        }
+        if (rc == MI355X_SUCCESS) verdict_store(c);
     }
     std::vector<std::pair<int, long>> pre;
     pre.swap(c->preset);

@@ -42,7 +42,8 @@ inline bool debug_on()
 
 constexpr uint64_t kMagic = 0x4d49333535584331ull;  // "MI355XC1"
 constexpr int kMaxBufs = 3;
-constexpr int kVoteRing = 64;  // buffer-kind votes a rank keeps (mi355x_comm_vote)
+constexpr int kVoteRing = 64;    // buffer-kind votes a rank keeps (mi355x_comm_vote)
+constexpr int kVoteWindow = 32;  // calls per vote window: every rank waits at each window's last call
 
 struct BufDesc {
     hipIpcMemHandle_t h;
@@ -73,8 +74,9 @@ struct alignas(64) RankSlot {
     uint64_t dev_uid;             // hash of the device's PCI bus id: ranks sharing one GPU
     uint64_t pid_start;           // the process's start time (/proc/<pid>/stat field 22): a recycled pid differs
     uint64_t pid_ns;              // inode of its PID namespace: a pid from another namespace is not checked
-    // mi355x_comm_vote: call v's entry at [v % kVoteRing] = (v << 1) | (this rank's buffers are
-    // device memory); a ring because a rank with device buffers publishes and moves on
+    // mi355x_comm_vote: call v's entry at [v % kVoteRing] = (v << 2) | (window flag << 1) | (this
+    // rank's buffers are device memory); a ring because one side of a call publishes and moves on.
+    // The window flag (checkpoint calls only): this rank voted device somewhere in the window
     std::atomic<uint64_t> vote[kVoteRing];
     // pipelined allreduce admission for the call whose exchange carries sequence s:
     // (s << 1) | (this rank holds its GPU's pipelined-grid token)
@@ -88,6 +90,8 @@ struct alignas(64) RankSlot {
     // so only while every rank is between the same two calls); calls = gated calls completed
     alignas(64) std::atomic<uint32_t> gate;
     uint32_t flow_ok;                 // flow self-test: the MI355X_FLOW_* this rank saw exact
+    std::atomic<uint64_t> verdict;    // device setup: hash of the flow verdicts this process holds for
+                                      // the communicator's member set (0: none), agreed before reuse
     std::atomic<uint64_t> calls;
     std::atomic<uint64_t> svc_last_ns;  // CLOCK_MONOTONIC time of this rank's last service call
 };
@@ -262,6 +266,8 @@ struct mi355x_comm {
     std::string shm_name;
     uint64_t seq = 0;
     uint64_t vote_seq = 0;                        // mi355x_comm_vote calls made
+    bool vote_host_waits = true;                  // this window's mode: host ranks wait (else device ranks)
+    bool vote_window_dev = false;                 // this rank voted device in the current window
     std::map<mi355x::HandleKey, mi355x::PeerMap> peer_maps;
     // mappings evicted during a call's mapping phase: closed in the next exchange's close window,
     // never while a peer exports or imports (coll_rcache.cpp: retire_map)
@@ -349,6 +355,7 @@ struct mi355x_comm {
     bool svc_want = false;                        // may claim (multi-process, <= 8 ranks, LL self-test ok)
     bool svc_attached = false;                    // counted among the users of the process's service resources
     bool svc_flows_tested = false;                // the service flows' self-test has run (first claim)
+    int selftest_reused = 0;                      // MI355X_KNOB_SELFTEST_REUSED
     uint64_t svc_epoch = 0;                       // successful claims (same on every rank)
     uint64_t svc_tries = 0;                       // service-sized calls made without the service
     uint64_t svc_retry = 16;                      // a claim is attempted every svc_retry such calls

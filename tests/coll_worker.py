@@ -1224,9 +1224,99 @@ def staging_main():
     assert L.mini_allreduce(comm, h.ctypes.data, out.ctypes.data, 50_000, fdt, op) == 0
     opdata.assert_same("FLOAT", "SUM", out, want, "host-buffer allreduce through the host module")
     L.mini_op_destroy(op)
+    vote_windows(m, oracle, rank, size, torch, staged, put)
     assert L.mini_device_hits() == 0, "a device pointer reached the host module"
     L.mini_comm_destroy(comm)
     print(f"rank {rank} staging OK", flush=True)
+
+
+def vote_windows(m, oracle, rank, size, torch, staged, put):
+    """the buffer-kind vote's windows (mi355x_comm_vote, 32 calls each): after a window of host-only
+    calls the device ranks wait and the host ranks only publish, so a mixed call runs in the host
+    component with the device ranks staging their buffers (coll/cuda's way, coll_cuda_allreduce.c:
+    43-75) -- allreduce, reduce, bcast, allgather, gather, alltoall -- while an all-device call still
+    runs in the engine; after a window with device calls the host ranks wait again and a mixed call
+    runs in the engine.  Every result exact; no device pointer reaches the host module."""
+    L, pkg = m.lib, m.pkg
+    comm = L.mini_comm_create(rank, size, 77)
+    assert L.mini_comm_set_channel(comm, (sys.argv[3] + "_votes").encode()) == 0
+    L.mini_comm_install(comm, L.mini_host_module())
+    assert L.mini_coll_select(comm, m.component_ptr(m.coll, "mca_coll_mi355x_component")) == 90
+    idt = m.dtype_for_slot(pkg.T["INT32"])
+    op = m.select_op(pkg.OP["SUM"])
+    calls = [0]
+    n = 4099
+    xs = [(np.arange(n, dtype=np.int32) * (r + 3) - 5 * r).astype(np.int32) for r in range(size)]
+    total = sum(xs)
+
+    def allreduce(host_rank0, all_host=False):
+        on_host = all_host or (host_rank0 and rank == 0)
+        x, px, _ = put(xs[rank], on_host)
+        y, py, rd = put(np.zeros(n, np.int32), on_host)
+        torch.cuda.synchronize()
+        assert L.mini_allreduce(comm, px, py, n, idt, op) == 0
+        calls[0] += 1
+        assert np.array_equal(rd(), total), ("vote window allreduce", calls[0])
+
+    def fill_to_checkpoint():
+        while calls[0] % 32:
+            allreduce(False, all_host=True)
+
+    say = lambda what: print(f"rank {rank} vote windows: {what}", flush=True)
+    # window 1: host calls only -> window 2: device ranks wait
+    fill_to_checkpoint() if calls[0] else [allreduce(False, all_host=True) for _ in range(32)]
+    say("host window done")
+    dev_rank = rank != 0
+    before = staged.value
+    allreduce(True)                                           # mixed: on the host, device ranks staged
+    assert staged.value - before == (1 if dev_rank else 0), ("mixed call not staged to the host", staged.value - before)
+    mixed = lambda a: put(a, rank == 0)
+    say("mixed allreduce staged")
+    # reduce to a device root
+    root = size - 1
+    x, px, _ = mixed(xs[rank])
+    r_, pr, rr = mixed(np.zeros(n, np.int32))
+    torch.cuda.synchronize()
+    assert L.mini_reduce(comm, px, pr if rank == root else None, n, idt, op, root) == 0
+    calls[0] += 1
+    if rank == root:
+        assert np.array_equal(rr(), total), "vote window mixed reduce"
+    # bcast from the host rank
+    b, pb, rb = mixed(np.full(n, 11 if rank == 0 else -1, np.int32))
+    torch.cuda.synchronize()
+    assert L.mini_bcast(comm, pb, n, idt, 0) == 0
+    calls[0] += 1
+    assert (rb() == 11).all(), "vote window mixed bcast"
+    # allgather, gather, alltoall
+    g, pg, rg = mixed(np.full(n * size, -1, np.int32))
+    torch.cuda.synchronize()
+    assert L.mini_allgather(comm, px, n, idt, pg, n, idt) == 0
+    calls[0] += 1
+    assert np.array_equal(rg(), np.concatenate(xs)), "vote window mixed allgather"
+    g2, pg2, rg2 = mixed(np.full(n * size, -1, np.int32))
+    torch.cuda.synchronize()
+    assert L.mini_gather(comm, px, n, idt, pg2 if rank == root else None, n, idt, root) == 0
+    calls[0] += 1
+    if rank == root:
+        assert np.array_equal(rg2(), np.concatenate(xs)), "vote window mixed gather"
+    k = 100
+    piece = lambda r, q: np.arange(k, dtype=np.int32) + 1000 * q + 100000 * r
+    sa, psa, _ = mixed(np.concatenate([piece(rank, q) for q in range(size)]))
+    ra, pra, rra = mixed(np.full(k * size, -1, np.int32))
+    torch.cuda.synchronize()
+    assert L.mini_alltoall(comm, psa, k, idt, pra, k, idt) == 0
+    calls[0] += 1
+    assert np.array_equal(rra(), np.concatenate([piece(q, rank) for q in range(size)])), "vote window mixed alltoall"
+    say("mixed movement on the host")
+    staged_mid = staged.value
+    allreduce(False)                                          # all device: still the engine
+    assert staged.value == staged_mid, "an all-device call was staged"
+    fill_to_checkpoint()                                      # window 2 had device calls ->
+    before = staged.value                                     # window 3: host ranks wait
+    allreduce(True)                                           # mixed: in the engine, nothing staged
+    assert staged.value == before, "a mixed call after device use was staged to the host"
+    L.mini_op_destroy(op)
+    L.mini_comm_destroy(comm)
 
 
 def mca_vars_main():

@@ -904,6 +904,34 @@ def selftest(key, rank, size, dev):
         assert served == 0 and comm.get("SVC_LAUNCHES") == 0, "a service that could not open on one rank serves no rank"
     print(f"rank {rank} flows {flows:#x} failed {failed:#x} create_us {create_us} selftest_us {st_us} "
           f"claim_selftest_us {comm.get('SELFTEST_US') - st_us} served {served}", flush=True)
+    # a dup of the same processes takes the verdicts over (no tests): a flow that failed anywhere is
+    # off for the dup too, on every rank, and its calls stay exact
+    import time
+    dup = pkg.Comm.create(key + "dup", rank, size, dev)
+    comm.barrier()
+    t0 = time.perf_counter()
+    dup.allreduce(x.data_ptr(), y.data_ptr(), 1000, f32, SUM)
+    dup_ms = (time.perf_counter() - t0) * 1e3
+    assert bool(torch.all(y == size * (size + 1) / 2).item())
+    assert dup.get("SELFTEST_REUSED") == (1 if open_fail else 2), dup.get("SELFTEST_REUSED")
+    assert dup.get("SELFTEST_US") == 0
+    assert dup.get("FLOWS") == comm.get("FLOWS") and dup.get("FLOWS_FAILED") == comm.get("FLOWS_FAILED"), \
+        (dup.get("FLOWS"), dup.get("FLOWS_FAILED"))
+    if expect == pkg.FLOW["PIPE"]:
+        dup.set("PIPE", 1)
+        assert dup.get("PIPE") == 0, "a flow that failed its self-test cannot be forced on in a dup"
+    for count in (3, 12288, size * 300_000):
+        xs = [opdata.make("FLOAT", count, 160 + r) for r in range(size)]
+        outs = [np.zeros_like(xs[0]) for _ in range(size)]
+        oracle.oracle_allreduce(0, size, count, f32, SUM, 0, ptrs(xs), ptrs(outs))
+        dx = torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda()
+        dr = torch.full_like(dx, 0x5a)
+        torch.cuda.synchronize()
+        dup.allreduce(dx.data_ptr(), dr.data_ptr(), count, f32, SUM)
+        opdata.assert_same("FLOAT", "SUM", dr.cpu().numpy().view(np.float32), outs[rank], f"dup allreduce {count}")
+    print(f"rank {rank} dup: first device call {dup_ms:.2f} ms, setup_us {dup.get('SETUP_US')}", flush=True)
+    dup.barrier()
+    dup.destroy()
     comm.barrier()
     comm.destroy()
     print(f"rank {rank} selftest OK", flush=True)
@@ -1038,7 +1066,17 @@ def lazy_setup(key, rank, size, dev):
     first_ms = (time.perf_counter() - t0) * 1e3
     assert bool(torch.all(y == size * (size + 1) / 2).item())
     assert c.get("DEV_SETUP") == 1 and all(k.get("DEV_SETUP") == 0 for k in comms[:-1])
+    assert c.get("SELFTEST_REUSED") == 0 or c.get("SELFTEST_US") == 0
     setup_us = c.get("SETUP_US")
+    # the next communicator of the same processes (a dup): the flow verdicts are taken over
+    c2 = comms[-2]
+    base.barrier()
+    t0 = time.perf_counter()
+    c2.allreduce(x.data_ptr(), y.data_ptr(), 4096, pkg.T["FLOAT"], pkg.OP["SUM"])
+    dup_ms = (time.perf_counter() - t0) * 1e3
+    assert bool(torch.all(y == size * (size + 1) / 2).item())
+    assert c2.get("SELFTEST_REUSED") >= 1 and c2.get("SELFTEST_US") == 0, (c2.get("SELFTEST_REUSED"), c2.get("SELFTEST_US"))
+    dup_setup_us = c2.get("SETUP_US")
     for k in comms:
         k.barrier()
         k.destroy()
@@ -1047,7 +1085,8 @@ def lazy_setup(key, rank, size, dev):
     wall.sort()
     print(json.dumps({"rank": rank, "n": size, "create_wall_us": [round(w, 1) for w in wall],
                       "create_us_knob": create_us, "device_bytes_taken": free0 - free1,
-                      "first_device_call_ms": round(first_ms, 2), "device_setup_us": setup_us}), flush=True)
+                      "first_device_call_ms": round(first_ms, 2), "device_setup_us": setup_us,
+                      "dup_first_device_call_ms": round(dup_ms, 2), "dup_device_setup_us": dup_setup_us}), flush=True)
     print(f"rank {rank} lazy OK", flush=True)
 
 
