@@ -415,20 +415,20 @@ int mi355x_comm_get(const mi355x_comm_t *c, int knob, long *value)
     case MI355X_KNOB_ALLREDUCE_ALG: *value = c->knob_allreduce; break;
     case MI355X_KNOB_REDUCE_ALG: *value = c->knob_reduce; break;
     case MI355X_KNOB_REDUCE_SCATTER_ALG: *value = c->knob_rs; break;
-    case MI355X_KNOB_BLOCKS_PER_CU: *value = coll_tune().blocks_per_cu; break;
+    case MI355X_KNOB_BLOCKS_PER_CU: *value = c->tune.blocks_per_cu; break;
     case MI355X_KNOB_TIMEOUT_S: *value = (long)c->timeout_s; break;
-    case MI355X_KNOB_PUSH: *value = coll_tune().push; break;
+    case MI355X_KNOB_PUSH: *value = c->tune.push; break;
     case MI355X_KNOB_IPC_MAX_BYTES: *value = (long)c->ipc_max; break;
     case MI355X_KNOB_STAGE_BYTES: *value = (long)c->stage_bytes; break;
     case MI355X_KNOB_PIPE_REFUSED: *value = (long)c->pipe_refused; break;
     case MI355X_KNOB_LL_MAX_BYTES: *value = (long)c->ll_max; break;
     case MI355X_KNOB_REDUCE_CHAIN_FANOUT: *value = c->chain_fanout; break;
     case MI355X_KNOB_TIME_PHASES: *value = c->time_phases ? 1 : 0; break;
-    case MI355X_KNOB_COPY_BLOCK_KIB: *value = coll_tune().copy_block_kib; break;
+    case MI355X_KNOB_COPY_BLOCK_KIB: *value = c->tune.copy_block_kib; break;
     case MI355X_KNOB_PIPE: *value = c->pipe_on ? 1 : 0; break;
-    case MI355X_KNOB_PIPE_WG_PER_CU: *value = coll_tune().pipe_wg_per_cu; break;
-    case MI355X_KNOB_PIPE_CHUNK_KIB: *value = coll_tune().pipe_chunk_kib; break;
-    case MI355X_KNOB_PIPE_WT: *value = coll_tune().pipe_wt; break;
+    case MI355X_KNOB_PIPE_WG_PER_CU: *value = c->tune.pipe_wg_per_cu; break;
+    case MI355X_KNOB_PIPE_CHUNK_KIB: *value = c->tune.pipe_chunk_kib; break;
+    case MI355X_KNOB_PIPE_WT: *value = c->tune.pipe_wt; break;
     case MI355X_KNOB_ONE_PHASE_MAX_BYTES: *value = (long)c->one_phase_max; break;
     case MI355X_KNOB_SVC_MAX_BYTES: *value = svc_limit_visible(c) ? (long)c->svc_max : 0; break;
     case MI355X_KNOB_SVC_CALLS: *value = (long)c->svc_calls; break;
@@ -498,10 +498,10 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
     case MI355X_KNOB_BLOCKS_PER_CU:
         // up to 1024: with that many the streaming kernels' grids are one-shot (every thread one pass)
         if (value < 1 || value > 1024) return set_error(MI355X_ERR_ARG, "blocks_per_cu out of range");
-        coll_tune().blocks_per_cu = (int)value;
+        c->tune.blocks_per_cu = (int)value;
         break;
     case MI355X_KNOB_TIMEOUT_S: c->timeout_s = (double)value; break;
-    case MI355X_KNOB_PUSH: coll_tune().push = value ? 1 : 0; break;
+    case MI355X_KNOB_PUSH: c->tune.push = value ? 1 : 0; break;
     case MI355X_KNOB_IPC_MAX_BYTES:
         if (value < 0) return set_error(MI355X_ERR_ARG, "ipc_max_bytes < 0");
         c->ipc_max = (size_t)value;
@@ -512,18 +512,18 @@ int mi355x_comm_set(mi355x_comm_t *c, int knob, long value)
         break;
     case MI355X_KNOB_COPY_BLOCK_KIB:
         if (value < 4 || value > 256) return set_error(MI355X_ERR_ARG, "copy_block_kib out of range");
-        coll_tune().copy_block_kib = (int)value;
+        c->tune.copy_block_kib = (int)value;
         break;
     case MI355X_KNOB_PIPE: c->pipe_on = value != 0 && (c->flows & MI355X_FLOW_PIPE); break;  // (a failed self-test keeps it off)
     case MI355X_KNOB_PIPE_WG_PER_CU:
         if (value < 1 || value > 8) return set_error(MI355X_ERR_ARG, "pipe_wg_per_cu out of range");
-        coll_tune().pipe_wg_per_cu = (int)value;
+        c->tune.pipe_wg_per_cu = (int)value;
         break;
     case MI355X_KNOB_PIPE_CHUNK_KIB:
         if (value < 0 || value > (1l << 20)) return set_error(MI355X_ERR_ARG, "pipe_chunk_kib out of range");
-        coll_tune().pipe_chunk_kib = (int)value;
+        c->tune.pipe_chunk_kib = (int)value;
         break;
-    case MI355X_KNOB_PIPE_WT: coll_tune().pipe_wt = value != 0; break;
+    case MI355X_KNOB_PIPE_WT: c->tune.pipe_wt = value != 0; break;
     case MI355X_KNOB_ONE_PHASE_MAX_BYTES:
         if (value < 0 || value > (1l << 30)) return set_error(MI355X_ERR_ARG, "one_phase_max_bytes out of range");
         c->one_phase_max = (size_t)value;

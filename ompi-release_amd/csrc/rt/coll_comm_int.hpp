@@ -47,7 +47,8 @@ void gfold_idle(mi355x_comm *c, hipStream_t s);  // coll_gfold.cpp
 struct CallStream {
     mi355x_comm *c;
     hipStream_t prev;
-    CallStream(mi355x_comm *c_, hipStream_t s) : c(c_), prev(c_->call_s)
+    CollTune *prev_tune;
+    CallStream(mi355x_comm *c_, hipStream_t s) : c(c_), prev(c_->call_s), prev_tune(coll_tune_use(&c_->tune))
     {
         c->call_s = s;  // (NULL is the null stream: call_depth says whether call_s is set)
         c->call_depth++;
@@ -57,6 +58,7 @@ struct CallStream {
     {
         c->call_depth--;
         c->call_s = prev;
+        coll_tune_use(prev_tune);
     }
 };
 

@@ -43,10 +43,21 @@
 
 namespace mi355x {
 
-CollTune &coll_tune()
+// The launch-shape knobs are per communicator (coll/tuned's forced values are per communicator too,
+// coll_tuned_module.c:178-226): each engine call runs with its communicator's CollTune, installed
+// for the calling thread by CallStream; outside a call (point-to-point pulls) the process defaults.
+CollTune &coll_tune_default()
 {
     static CollTune t;
     return t;
+}
+static thread_local CollTune *t_tune = nullptr;
+CollTune &coll_tune() { return t_tune ? *t_tune : coll_tune_default(); }
+CollTune *coll_tune_use(CollTune *t)
+{
+    CollTune *prev = t_tune;
+    t_tune = t;
+    return prev;
 }
 
 } // namespace mi355x
@@ -126,7 +137,7 @@ int barrier(mi355x_comm *c)
             return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
         if (++spins > 2048) {
             sched_yield();
-            if ((spins & 63) == 0) p2p_progress_all();  // queued eager sends a peer may be waiting for
+            if ((spins & 63) == 0) p2p_progress_all(true);  // queued eager sends a peer may be waiting for
             // a peer may be blocked sending us dmabuf fds (full socket queue): drain it while we wait
             if (c->fd_sock >= 0 && (spins & 255) == 0 && c->reg_mtx.try_lock()) {
                 (void)fd_drain(c, false);
@@ -396,6 +407,12 @@ int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t s
         // its slot before every rank has read this exchange's slots
         return barrier(c);
     }
+    // Every rank publishes (call, mapping state) when its opens are done.  A rank whose open failed
+    // (kOpenRetry: stale mappings of that peer retired, map_peer) closes them only once every peer
+    // is past its own opens -- done, or failing too -- so no close overlaps a peer's import, and
+    // retries only once every failing rank has closed.  The common path costs one store.
+    enum { kMapped = 1, kMapFailed = 2, kMapClosed = 3 };
+    std::vector<std::pair<int, int>> failed;
     for (int r = 0; r < c->size; ++r) {
         RankSlot &o = c->ctrl->slot[r];
         for (int b = 0; b < nbuf; ++b) {
@@ -404,11 +421,47 @@ int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t s
             } else {
                 PeerMap *pm = nullptr;
                 rc = map_peer(c, r, o.buf[b], &peers[b][r], &pm);
+                if (rc == kOpenRetry) {
+                    failed.emplace_back(r, b);
+                    continue;
+                }
                 if (rc) return rc;
                 if (persistent && pm) pm->persistent = true;
             }
         }
     }
+    std::atomic<uint64_t> &st = c->ctrl->slot[c->rank].map_state;
+    if (failed.empty()) {
+        st.store((c->seq << 2) | kMapped, std::memory_order_release);
+        return MI355X_SUCCESS;
+    }
+    auto wait_all = [&](bool allow_failed) -> int {
+        for (int r = 0; r < c->size; ++r) {
+            const auto t0 = std::chrono::steady_clock::now();
+            for (;;) {
+                const uint64_t v = c->ctrl->slot[r].map_state.load(std::memory_order_acquire);
+                if ((v >> 2) > c->seq || ((v >> 2) == c->seq && ((v & 3) != kMapFailed || allow_failed))) break;
+                if (c->ctrl->abort_flag.load(std::memory_order_relaxed)) return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
+                if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s)
+                    return set_error(MI355X_ERR_TIMEOUT, "rank %d: the mapping window timed out waiting for rank %d", c->rank, r);
+                sched_yield();
+            }
+        }
+        return MI355X_SUCCESS;
+    };
+    st.store((c->seq << 2) | kMapFailed, std::memory_order_release);
+    if ((rc = wait_all(true))) return rc;   // every rank is past its opens
+    flush_retired(c);
+    st.store((c->seq << 2) | kMapClosed, std::memory_order_release);
+    if ((rc = wait_all(false))) return rc;  // every failing rank has closed
+    for (const auto &f : failed) {
+        PeerMap *pm = nullptr;
+        rc = map_peer(c, f.first, c->ctrl->slot[f.first].buf[f.second], &peers[f.second][f.first], &pm);
+        if (rc == kOpenRetry) rc = set_error(MI355X_ERR_PEER, "hipIpcOpenMemHandle(rank %d) failed twice", f.first);
+        if (rc) return rc;
+        if (persistent && pm) pm->persistent = true;
+    }
+    st.store((c->seq << 2) | kMapped, std::memory_order_release);
     return MI355X_SUCCESS;
 }
 

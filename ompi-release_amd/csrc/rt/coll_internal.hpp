@@ -212,7 +212,9 @@ struct CollTune {
     // (faster at every n measured: rehearsal n = 8 3.50-3.78 vs 4.69 ms, n = 4 2.03 vs 2.29)
     int pipe_wt = 1;
 };
-CollTune &coll_tune();
+CollTune &coll_tune();          // the calling engine call's communicator's (else the process defaults)
+CollTune &coll_tune_default();  // the process defaults new communicators start from
+CollTune *coll_tune_use(CollTune *t);  // install t for this thread; returns the previous one
 
 int launch_fold_slot(int op, int type, const FoldArgs &a, hipStream_t s);
 int launch_ring_all_slot(int op, int type, const RingAllArgs &a, hipStream_t s);

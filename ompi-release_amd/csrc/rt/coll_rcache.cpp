@@ -62,10 +62,18 @@ namespace mi355x {
 // anybody opens, then one more barrier).  A replaced mapping (same exporter base, new allocation
 // id) is still closed at once: an import with the same handle words left open would be handed
 // back by hipIpcOpenMemHandle instead of the new allocation.
+// A dmabuf import (the route every allocation with a buffer object of its own takes under a bound)
+// is released at once: the race is hipIpcCloseMemHandle's.  A hipIpc mapping waits for a close
+// window however many accumulate: in a point-to-point-only phase they are closed at the next
+// collective's exchange, never eagerly while peers export or import.
 void retire_map(mi355x_comm *c, const PeerMap &m)
 {
+    if (m.ext) {
+        PeerMap x = m;
+        close_map(x);
+        return;
+    }
     c->retired_maps.push_back(m);
-    if (c->retired_maps.size() > 256) flush_retired(c);  // (point-to-point-only phases: bounded)
 }
 
 void flush_retired(mi355x_comm *c)
@@ -160,23 +168,29 @@ int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **e
         if (e != hipSuccess) {
             // A mapping of an allocation the peer has since freed can still hold the block the new
             // allocation was carved from (small allocations share blocks): the open then fails
-            // with "invalid device pointer".  Drop this peer's mappings that the current call does
-            // not use and try once more.
+            // with "invalid device pointer".  This peer's mappings that the current call does not
+            // use must go before one more try -- but closing hipIpc mappings while peers export or
+            // import hands them wrong memory (retire_map), so inside a collective they are only
+            // retired here and the exchange closes them in a window of its own (kOpenRetry);
+            // point-to-point reads have no such window and close them at once.
             (void)hipGetLastError();
             int dropped = (int)c->retired_maps.size();
-            flush_retired(c);
             for (auto m = c->peer_maps.begin(); m != c->peer_maps.end();) {
                 if (m->first.peer == peer && m->second.coll_use != c->seq && m->second.pins == 0 &&
                     !m->second.persistent) {
-                    close_map(m->second);
+                    retire_map(c, m->second);
                     m = c->peer_maps.erase(m);
                     dropped++;
                 } else {
                     ++m;
                 }
             }
-            TRACE(c, "open failed; dropped %d stale mappings of peer %d, retrying", dropped, peer);
-            e = dropped ? hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess) : e;
+            TRACE(c, "open failed; retired %d stale mappings of peer %d", dropped, peer);
+            if (dropped && coll) return kOpenRetry;
+            if (dropped) {  // (point-to-point: no window to wait for -- closed now, as before)
+                flush_retired(c);
+                e = hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess);
+            }
             if (e != hipSuccess)
                 return set_error(MI355X_ERR_PEER, "hipIpcOpenMemHandle(rank %d): %s", peer, hipGetErrorString(e));
         }

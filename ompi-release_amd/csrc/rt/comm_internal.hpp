@@ -63,6 +63,7 @@ struct alignas(64) RankSlot {
     std::atomic<uint64_t> seq;
     int32_t pid, dev, nbuf;
     int32_t retiring;             // this rank holds retired peer mappings to close in the call's close window
+    std::atomic<uint64_t> map_state;  // exchange: (call << 2) | 1 opens done, 2 an open failed, 3 closed (coll_ctl.cpp)
     uint64_t sig[4];
     BufDesc buf[kMaxBufs];
     int32_t probe_fd, probe_ok;   // dmabuf capability probe
@@ -373,6 +374,7 @@ struct mi355x_comm {
     void *gf_buf = nullptr;                       // gather-then-fold slots (coll_gfold.cpp): every rank's input
     size_t gf_bytes = 0;
     double gf_used = 0;                           // last gather-then-fold call (steady clock, s)
+    mi355x::CollTune tune = mi355x::coll_tune_default();  // launch-shape knobs of this communicator's calls
     uint64_t use_clock = 0;                       // LRU clock of the peer-mapping cache (every use ticks it)
     // device-side setup (done words, LL region + self-test, the service's resources, the pipelined
     // flow's self-test), deferred from creation to the first device-buffer collective (dev_setup)
@@ -448,6 +450,8 @@ int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force);
 // has not received it yet
 int export_dmabuf(mi355x_comm *c, BufDesc *d, uint64_t peers);
 int fd_drain(mi355x_comm *c, bool wait);  // receive queued dmabuf fds, serve fd requests (caller holds reg_mtx)
+// map_peer's "retry after a close window" (an open failed and stale mappings were retired)
+constexpr int kOpenRetry = 1;
 int map_peer(mi355x_comm *c, int peer, const BufDesc &d, void **out, PeerMap **entry = nullptr, bool coll = true);
 size_t peer_map_count(const mi355x_comm *c);  // evictable-kind peer mappings currently open
 // publish nbuf buffers, meet every rank, map every rank's buffers: peers[b][r] (coll_comm.cpp)
@@ -480,6 +484,6 @@ struct CallGate {
     CallGate &operator=(const CallGate &) = delete;
 };
 int p2p_progress(mi355x_comm *c);
-void p2p_progress_all();  // every communicator's point-to-point (the engine's host-side waits)
+void p2p_progress_all(bool from_collective = false);  // every communicator's point-to-point (the engine's host-side waits)
 int p2p_wait(mi355x_request *r);
 } // namespace mi355x

@@ -139,6 +139,9 @@ struct P2P {
     // matched receives of a dual message whose device buffer could not be mapped here: they wait
     // for the sender's host copy (claim 1) instead of claiming the pull
     std::vector<std::pair<mi355x_request *, P2PMsg>> dual_wait;
+    // matched receives whose read needs a peer mapping, matched in a progress pass made from inside
+    // a collective's barrier (a close window may be open on some rank): started at the next pass
+    std::vector<std::pair<mi355x_request *, P2PMsg>> deferred;
     DevArena arena;                        // exportable: packed / buffered device payloads
     DevArena rstage;                       // receive side: device staging of host receives
     HostArena harena;                      // host payloads (shared memory)
@@ -169,11 +172,27 @@ static P2P *p2p_of(mi355x_comm *c)
     return c->p2p;
 }
 
-void p2p_progress_all()
+// fault injection for tests (MI355X_P2P_INJECT, read once): 1 the dual offer's host copy fails
+// (sender), 2 the first mapping of a dual sender's device buffer fails (receiver), 4 every such
+// mapping fails (receiver)
+static unsigned p2p_inject()
+{
+    static const unsigned v = (unsigned)atoi(getenv("MI355X_P2P_INJECT") ? getenv("MI355X_P2P_INJECT") : "0");
+    return v;
+}
+
+// set while a progress pass runs from inside a collective's barrier: reads that would open a peer
+// mapping wait (hipIpc opens must not overlap a peer's close window, coll_rcache.cpp)
+static thread_local bool t_defer_maps = false;
+
+void p2p_progress_all(bool from_collective)
 {
     std::unique_lock<std::mutex> g(g_p2p_mtx, std::try_to_lock);  // (another thread progresses them now)
     if (!g.owns_lock()) return;
+    const bool saved = t_defer_maps;
+    t_defer_maps = from_collective;
     for (mi355x_comm *c : g_p2p_comms) (void)p2p_progress(c);
+    t_defer_maps = saved;
 }
 
 static int p2p_stream(mi355x_comm *c, P2P *p, hipStream_t *s)
@@ -480,6 +499,11 @@ static void start_read(mi355x_comm *c, P2P *p, mi355x_request *r, const P2PMsg &
     r->st_bytes = env->bytes;
     r->st_error = env->bytes > r->bytes ? MI355X_ERR_TRUNCATE : MI355X_SUCCESS;
     const size_t n = std::min<size_t>(env->bytes, r->bytes);
+    if (t_defer_maps && n && msg.src != c->rank && !c->loopback && !(env->flags & (kEnvHost | kEnvInline)) &&
+        !((env->flags & kEnvDual) && env->claim.load(std::memory_order_acquire) == claim_word(msg.m, 1))) {
+        p->deferred.emplace_back(r, msg);  // (its read opens a peer mapping: not from inside a barrier)
+        return;
+    }
     auto fin = [&]() { env->done.store(msg.m + 1, std::memory_order_release); };
     auto fail = [&](int rc) {
         fin();  // the sender must not hang
@@ -504,14 +528,19 @@ static void start_read(mi355x_comm *c, P2P *p, mi355x_request *r, const P2PMsg &
         dual_host = env->claim.load(std::memory_order_acquire) == claim_word(msg.m, 1);
         if (!dual_host && msg.src != c->rank && !c->loopback) {
             void *mapped = nullptr;
-            if (map_peer(c, msg.src, env->buf, &mapped, nullptr, false) != MI355X_SUCCESS) {
+            static std::atomic<int> injected_once{0};
+            const bool inject = (p2p_inject() & 4) || ((p2p_inject() & 2) && injected_once.exchange(1) == 0);
+            if (inject || map_peer(c, msg.src, env->buf, &mapped, nullptr, false) != MI355X_SUCCESS) {
                 (void)hipGetLastError();
                 p->dual_wait.emplace_back(r, msg);
                 return;
             }
         }
         uint64_t z = claim_word(msg.m, 0);
-        if (!dual_host) dual_host = !env->claim.compare_exchange_strong(z, claim_word(msg.m, 2), std::memory_order_acq_rel);
+        // (a failed CAS leaves the word in z: 1 the host copy was taken; 3 it failed -- pull the
+        // device buffer, which is mapped, and the sender waits for this FIN)
+        if (!dual_host && !env->claim.compare_exchange_strong(z, claim_word(msg.m, 2), std::memory_order_acq_rel))
+            dual_host = z == claim_word(msg.m, 1);
     }
     BufDesc hdesc = env->buf;
     if (dual_host) {
@@ -764,9 +793,34 @@ int p2p_progress(mi355x_comm *c)
     }
     // 2. new envelopes, 3. match posted receives in posting order against the arrivals (first the
     //    matched dual receives whose host copy has come)
+    if (!t_defer_maps && !p->deferred.empty()) {
+        std::vector<std::pair<mi355x_request *, P2PMsg>> d;
+        d.swap(p->deferred);
+        for (const auto &w : d) start_read(c, p, w.first, w.second);
+    }
     for (size_t i = 0; i < p->dual_wait.size();) {
         const auto w = p->dual_wait[i];
-        if (w.second.env->claim.load(std::memory_order_acquire) != claim_word(w.second.m, 1)) {
+        const uint64_t cl = w.second.env->claim.load(std::memory_order_acquire);
+        if (cl == claim_word(w.second.m, 3)) {
+            // the sender's host copy failed: the device buffer is the only source left -- one more
+            // try to map it (outside a barrier), else the receive fails (the FIN lets the send end)
+            if (t_defer_maps) {
+                ++i;
+                continue;
+            }
+            p->dual_wait.erase(p->dual_wait.begin() + (ptrdiff_t)i);
+            void *mapped = nullptr;
+            if ((p2p_inject() & 4) || map_peer(c, w.second.src, w.second.env->buf, &mapped, nullptr, false) != MI355X_SUCCESS) {
+                (void)hipGetLastError();
+                w.second.env->done.store(w.second.m + 1, std::memory_order_release);
+                complete(w.first, set_error(MI355X_ERR_PEER, "rank %d: neither the device buffer of rank %d's small "
+                                                             "send nor its host copy is readable", c->rank, w.second.src));
+                continue;
+            }
+            start_read(c, p, w.first, w.second);
+            continue;
+        }
+        if (cl != claim_word(w.second.m, 1)) {
             ++i;
             continue;
         }
@@ -827,7 +881,15 @@ int p2p_progress(mi355x_comm *c)
         const bool fin = r->env->done.load(std::memory_order_acquire) >= r->msg + 1;
         if ((r->env_flags & kEnvDual) && !fin && !r->copy_launched &&
             r->env->claim.load(std::memory_order_acquire) == claim_word(r->msg, 0) && dual_copy_due(r)) {
-            if (dual_copy_launch(c, p, r) != MI355X_SUCCESS) r->copy_done = true;  // (then only the pull remains)
+            if ((p2p_inject() & 1) || dual_copy_launch(c, p, r) != MI355X_SUCCESS) {
+                // no host copy: tell a receiver that could not map the device buffer (claim 3) --
+                // it tries the mapping once more or fails its receive, and its FIN ends this send
+                // (without this both sides waited for each other)
+                (void)hipGetLastError();
+                r->copy_done = true;
+                uint64_t z = claim_word(r->msg, 0);
+                (void)r->env->claim.compare_exchange_strong(z, claim_word(r->msg, 3), std::memory_order_acq_rel);
+            }
         }
         if ((r->env_flags & kEnvDual) && r->copy_launched && !r->copy_done) {
             const hipError_t e = hipEventQuery(r->ev);
@@ -838,6 +900,9 @@ int p2p_progress(mi355x_comm *c)
                     r->twin) {
                     complete(r->twin, MI355X_SUCCESS);
                     r->twin = nullptr;
+                } else if (e != hipSuccess) {  // the copy failed: as a failed launch (claim 3)
+                    (void)hipGetLastError();
+                    (void)r->env->claim.compare_exchange_strong(z, claim_word(r->msg, 3), std::memory_order_acq_rel);
                 }
             }
         }

@@ -1259,6 +1259,39 @@ def rcache(key, rank, size, dev):
     print(f"rank {rank} rcache OK", flush=True)
 
 
+def p2p_fault(key, rank, size, dev):
+    """a small device send offered two ways (device buffer + host copy) whose host copy FAILS on the
+    sender (MI355X_P2P_INJECT=1) while the receiver cannot map the device buffer at first
+    (P2P_EXPECT=ok: the first mapping fails, INJECT=2) or ever (P2P_EXPECT=fail, INJECT=4): the sender
+    publishes claim 3, the receiver maps again and pulls (exact) or fails its receive with an error,
+    and the sender's send completes either way -- neither side waits for the other forever"""
+    import torch
+    torch.cuda.set_device(dev)
+    pkg = load_pkg()
+    comm = pkg.Comm.create(key, rank, size, dev)
+    expect = os.environ.get("P2P_EXPECT", "ok")
+    n = 1000  # > the inline limit, <= the 4 KiB eager limit: a dual offer
+    data = (np.arange(n) * 7 % 251).astype(np.uint8)
+    if rank == 0:
+        s = torch.from_numpy(data).cuda()
+        torch.cuda.synchronize()
+        comm.send(s.data_ptr(), n, 1, 5)
+    else:
+        d = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        req = comm.irecv(d.data_ptr(), n, 0, 5)
+        try:
+            req.wait()
+            assert expect == "ok", "the receive succeeded although the buffer was never readable"
+            assert np.array_equal(d.cpu().numpy(), data), "p2p fault: wrong bytes"
+        except pkg.MI355XError as e:
+            assert expect == "fail", f"the receive failed: {e}"
+            assert "readable" in str(e), e
+    comm.barrier()
+    comm.destroy()
+    print(f"rank {rank} p2p_fault: {expect}", flush=True)
+    print(f"rank {rank} p2p_fault OK", flush=True)
+
+
 def carved(key, rank, size, dev):
     """the bounded cache's dmabuf export check is on identity, not contents: the runtime carves small
     hipMallocs out of one buffer object and exports the whole object from its start, so a carved
@@ -1402,6 +1435,8 @@ def _main():
         return rcache_p2p(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "carved":
         return carved(key, rank, size, dev)
+    if len(sys.argv) > 5 and sys.argv[5] == "p2p_fault":
+        return p2p_fault(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "token_hold":
         return token_hold(key, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "token_check":
