@@ -1265,13 +1265,25 @@ def p2p_fault(key, rank, size, dev):
     (P2P_EXPECT=ok: the first mapping fails, INJECT=2) or ever (P2P_EXPECT=fail, INJECT=4): the sender
     publishes claim 3, the receiver maps again and pulls (exact) or fails its receive with an error,
     and the sender's send completes either way -- neither side waits for the other forever"""
+    expect = os.environ.get("P2P_EXPECT", "ok")
+    # (read by the engine at its first point-to-point pass)
+    os.environ["MI355X_P2P_INJECT"] = "1" if rank == 0 else ("2" if expect == "ok" else "4")
+    os.environ["MI355X_P2P_DUAL_DELAY_US"] = "0"
     import torch
     torch.cuda.set_device(dev)
     pkg = load_pkg()
     comm = pkg.Comm.create(key, rank, size, dev)
-    expect = os.environ.get("P2P_EXPECT", "ok")
     n = 1000  # > the inline limit, <= the 4 KiB eager limit: a dual offer
     data = (np.arange(n) * 7 % 251).astype(np.uint8)
+    # a first host message sets up (and registers) the sender's host arena: only then are small
+    # device sends offered two ways
+    warm = np.arange(2000, dtype=np.uint8)
+    if rank == 0:
+        comm.send(warm.ctypes.data, warm.nbytes, 1, 4)
+    else:
+        got = np.zeros_like(warm)
+        comm.recv(got.ctypes.data, got.nbytes, 0, 4)
+        assert np.array_equal(got, warm)
     if rank == 0:
         s = torch.from_numpy(data).cuda()
         torch.cuda.synchronize()

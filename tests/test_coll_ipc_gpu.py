@@ -202,9 +202,7 @@ def test_p2p_dual_offer_copy_failure(gpu, expect):
     """a small device send whose host copy fails on the sender while the receiver cannot map the
     device buffer (at first, or ever): claim 3 tells the receiver, which pulls after mapping again or
     fails its receive, and the send completes (ADVICE r5; ipc_worker.py::p2p_fault)"""
-    rank_env = {0: {"MI355X_P2P_INJECT": "1", "MI355X_P2P_DUAL_DELAY_US": "0"},
-                1: {"MI355X_P2P_INJECT": "2" if expect == "ok" else "4"}}
-    _run_mode(gpu, "p2p_fault", 2, extra_env={"P2P_EXPECT": expect}, rank_env=rank_env, timeout=120)
+    _run_mode(gpu, "p2p_fault", 2, extra_env={"P2P_EXPECT": expect}, timeout=120)
 
 
 def test_bounded_cache_export_check_is_identity(gpu):
