@@ -65,9 +65,10 @@ static void die(const char *what)
     abort();
 }
 
-/* x87 long double slots: MAX/MIN (and MAXLOC/MINLOC on MPI_LONG_DOUBLE_INT) compare and select,
- * which the GPU does exactly on the 80-bit encoding; SUM/PROD need 80-bit arithmetic, so op/hip
- * takes those slots only to stage device buffers to the base loops */
+/* x87 long double slots: MAX/MIN (and MAXLOC/MINLOC on MPI_LONG_DOUBLE_INT) compare and select on
+ * the 80-bit encoding, SUM/PROD (real and complex) run the x87 add / multiply restated in integer
+ * arithmetic (f80_arith.hpp) -- every slot has a GPU kernel; the staging below stays for a runtime
+ * without one */
 static int x87_type(int t)
 {
     return t == MI355X_T_LONG_DOUBLE || t == MI355X_T_C_LONG_DOUBLE_COMPLEX || t == MI355X_T_LONG_DOUBLE_INT;

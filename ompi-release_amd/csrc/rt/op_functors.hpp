@@ -21,6 +21,7 @@
 #include <type_traits>
 
 #include "../../../include/mi355x_types.h"
+#include "f80_arith.hpp"
 
 namespace mi355x {
 
@@ -79,6 +80,22 @@ MI_DEV int x87_cmp(const f80 &a, const f80 &b)
 MI_DEV bool operator>(const f80 &a, const f80 &b) { return x87_cmp(a, b) == 1; }
 MI_DEV bool operator<(const f80 &a, const f80 &b) { return x87_cmp(a, b) == -1; }
 MI_DEV bool operator==(const f80 &a, const f80 &b) { return x87_cmp(a, b) == 0; }
+MI_DEV bool operator!=(const f80 &a, const f80 &b) { return x87_cmp(a, b) != 0; }
+// SUM / PROD: the x87 unit's add / multiply restated in integer arithmetic (f80_arith.hpp; checked
+// bit for bit against the host's x87 by tools/f80_check.cpp); a selected or computed value's pad
+// bytes are zero (never compared: the reference stores 10 bytes)
+MI_DEV x87::Bits f80_bits(const f80 &x) { return x87::Bits{x.m, x.se}; }
+MI_DEV f80 f80_of(x87::Bits b)
+{
+    f80 r;
+    r.m = b.m;
+    r.se = b.se;
+    r.pad[0] = r.pad[1] = r.pad[2] = 0;
+    return r;
+}
+MI_DEV f80 operator+(const f80 &a, const f80 &b) { return f80_of(x87::add(f80_bits(a), f80_bits(b), false)); }
+MI_DEV f80 operator-(const f80 &a, const f80 &b) { return f80_of(x87::add(f80_bits(a), f80_bits(b), true)); }
+MI_DEV f80 operator*(const f80 &a, const f80 &b) { return f80_of(x87::mul(f80_bits(a), f80_bits(b))); }
 #undef MI_DEV
 
 // MPI_LONG_DOUBLE_INT: {long double v; int k;} -- 32 bytes (LOC_STRUCT, op_base_functions.c:554)
@@ -196,13 +213,31 @@ template <typename E> struct OpBxor {
 };
 
 // ------------------------------------------------------------------ complex
+// x86-64 `long double _Complex`: two 16-byte x87 values (C_LONG_DOUBLE_COMPLEX, 32 bytes)
+struct alignas(16) cf80 {
+    f80 re, im;
+};
+static_assert(sizeof(cf80) == 32, "long double complex");
+
 template <typename R> struct CplxOf;
 template <> struct CplxOf<float> { using type = cf32; };
 template <> struct CplxOf<double> { using type = cf64; };
+template <> struct CplxOf<f80> { using type = cf80; };
 
 template <typename R> MI_DEV bool is_nan(R x) { return x != x; }
 template <typename R> MI_DEV bool is_inf(R x) { return __builtin_isinf(x); }
 template <typename R> MI_DEV R copysgn(R m, R s) { return __builtin_copysign(m, s); }
+template <typename R> MI_DEV R cst(double v) { return (R)v; }
+// x87: isnan is an unordered self-compare (NaNs and the invalid encodings), isinf exact infinity,
+// copysign the sign bit
+template <> MI_DEV bool is_nan<f80>(f80 x) { return x87_cmp(x, x) == 2; }
+template <> MI_DEV bool is_inf<f80>(f80 x) { return x87::kind(f80_bits(x)) == 2; }
+template <> MI_DEV f80 copysgn<f80>(f80 m, f80 s)
+{
+    m.se = (uint16_t)((m.se & 0x7fffu) | (s.se & 0x8000u));
+    return m;
+}
+template <> MI_DEV f80 cst<f80>(double v) { return f80_of(x87::from_double(v)); }
 
 // (a + ib) * (c + id) as GCC evaluates `_Complex` multiplication without -ffast-math:
 // x = ac - bd, y = ad + bc; if both are NaN, libgcc's __mul?c3 recovery rules (C99 G.5.1).
@@ -213,29 +248,29 @@ template <typename R> MI_DEV typename CplxOf<R>::type cmul(R a, R b, R c, R d)
     if (is_nan(x) && is_nan(y)) {
         bool recalc = false;
         if (is_inf(a) || is_inf(b)) {
-            a = copysgn(is_inf(a) ? (R)1 : (R)0, a);
-            b = copysgn(is_inf(b) ? (R)1 : (R)0, b);
-            if (is_nan(c)) c = copysgn((R)0, c);
-            if (is_nan(d)) d = copysgn((R)0, d);
+            a = copysgn(is_inf(a) ? cst<R>(1) : cst<R>(0), a);
+            b = copysgn(is_inf(b) ? cst<R>(1) : cst<R>(0), b);
+            if (is_nan(c)) c = copysgn(cst<R>(0), c);
+            if (is_nan(d)) d = copysgn(cst<R>(0), d);
             recalc = true;
         }
         if (is_inf(c) || is_inf(d)) {
-            c = copysgn(is_inf(c) ? (R)1 : (R)0, c);
-            d = copysgn(is_inf(d) ? (R)1 : (R)0, d);
-            if (is_nan(a)) a = copysgn((R)0, a);
-            if (is_nan(b)) b = copysgn((R)0, b);
+            c = copysgn(is_inf(c) ? cst<R>(1) : cst<R>(0), c);
+            d = copysgn(is_inf(d) ? cst<R>(1) : cst<R>(0), d);
+            if (is_nan(a)) a = copysgn(cst<R>(0), a);
+            if (is_nan(b)) b = copysgn(cst<R>(0), b);
             recalc = true;
         }
         if (!recalc && (is_inf(ac) || is_inf(bd) || is_inf(ad) || is_inf(bc))) {
-            if (is_nan(a)) a = copysgn((R)0, a);
-            if (is_nan(b)) b = copysgn((R)0, b);
-            if (is_nan(c)) c = copysgn((R)0, c);
-            if (is_nan(d)) d = copysgn((R)0, d);
+            if (is_nan(a)) a = copysgn(cst<R>(0), a);
+            if (is_nan(b)) b = copysgn(cst<R>(0), b);
+            if (is_nan(c)) c = copysgn(cst<R>(0), c);
+            if (is_nan(d)) d = copysgn(cst<R>(0), d);
             recalc = true;
         }
         if (recalc) {
-            x = (R)__builtin_inf() * (a * c - b * d);
-            y = (R)__builtin_inf() * (a * d + b * c);
+            x = cst<R>(__builtin_inf()) * (a * c - b * d);
+            y = cst<R>(__builtin_inf()) * (a * d + b * c);
         }
     }
     typename CplxOf<R>::type r;
@@ -247,6 +282,7 @@ template <typename R> MI_DEV typename CplxOf<R>::type cmul(R a, R b, R c, R d)
 template <typename C> struct RealOf;
 template <> struct RealOf<cf32> { using type = float; };
 template <> struct RealOf<cf64> { using type = double; };
+template <> struct RealOf<cf80> { using type = f80; };
 
 template <typename C> struct OpCsum {
     using T = C;

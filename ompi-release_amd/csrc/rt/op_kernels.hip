@@ -431,10 +431,14 @@ struct Table {
         put<OpLoc<p_long_int, false>>(s, MI355X_OP_MINLOC, MI355X_T_LONG_INT);
         put<OpLoc<p_2int, false>>(s, MI355X_OP_MINLOC, MI355X_T_2INT);
         put<OpLoc<p_short_int, false>>(s, MI355X_OP_MINLOC, MI355X_T_SHORT_INT);
-        // x87 long double: the compare-and-select slots (SUM/PROD need 80-bit arithmetic and
-        // stay on the host base loops, op/hip stages them)
+        // x87 long double: compare-and-select (MAX/MIN) and the x87 add / multiply restated in
+        // integer arithmetic (SUM/PROD, f80_arith.hpp), real and complex
         put<OpMax<f80>>(s, MI355X_OP_MAX, MI355X_T_LONG_DOUBLE);
         put<OpMin<f80>>(s, MI355X_OP_MIN, MI355X_T_LONG_DOUBLE);
+        put<OpSum<f80>>(s, MI355X_OP_SUM, MI355X_T_LONG_DOUBLE);
+        put<OpProd<f80>>(s, MI355X_OP_PROD, MI355X_T_LONG_DOUBLE);
+        put<OpCsum<cf80>>(s, MI355X_OP_SUM, MI355X_T_C_LONG_DOUBLE_COMPLEX);
+        put<OpCprod<cf80>>(s, MI355X_OP_PROD, MI355X_T_C_LONG_DOUBLE_COMPLEX);
         put<OpLoc<p_ldouble_int, true>>(s, MI355X_OP_MAXLOC, MI355X_T_LONG_DOUBLE_INT);
         put<OpLoc<p_ldouble_int, false>>(s, MI355X_OP_MINLOC, MI355X_T_LONG_DOUBLE_INT);
     }

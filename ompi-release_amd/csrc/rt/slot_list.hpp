@@ -1,8 +1,7 @@
 // slot_list.hpp -- the (MPI_Op, element type) slots that have a GPU kernel, as one list shared by
-// the kernel families (the 3-buff table of op_base_functions.c:1460-1543 minus the x87
-// `long double` SUM/PROD slots, which need 80-bit arithmetic and are staged to the host base loops,
-// and MPI_LONG_DOUBLE_INT, whose 32-byte pairs op/hip's kernels reduce but the engine's
-// 16-byte-vector families do not carry).
+// the kernel families (the 3-buff table of op_base_functions.c:1460-1543 minus the two 32-byte
+// types -- MPI_LONG_DOUBLE_INT and C_LONG_DOUBLE_COMPLEX -- which op/hip's kernels reduce but the
+// engine's 16-byte-vector families do not carry: the engine serves those by gather-then-fold).
 //
 //   for_each_slot([&](auto tag, int op, int type) { using F = typename decltype(tag)::type; ... });
 #pragma once
@@ -67,9 +66,12 @@ template <class Put> __host__ __device__ inline void for_each_slot(Put &&put)
     put(SlotTag<OpLoc<p_long_int, false>>{}, MI355X_OP_MINLOC, MI355X_T_LONG_INT);
     put(SlotTag<OpLoc<p_2int, false>>{}, MI355X_OP_MINLOC, MI355X_T_2INT);
     put(SlotTag<OpLoc<p_short_int, false>>{}, MI355X_OP_MINLOC, MI355X_T_SHORT_INT);
-    // x87 long double MAX/MIN: compare-and-select on the 80-bit encoding (op_functors.hpp)
+    // x87 long double MAX/MIN: compare-and-select on the 80-bit encoding; SUM/PROD: the x87 add
+    // and multiply in integer arithmetic (op_functors.hpp, f80_arith.hpp)
     put(SlotTag<OpMax<f80>>{}, MI355X_OP_MAX, MI355X_T_LONG_DOUBLE);
     put(SlotTag<OpMin<f80>>{}, MI355X_OP_MIN, MI355X_T_LONG_DOUBLE);
+    put(SlotTag<OpSum<f80>>{}, MI355X_OP_SUM, MI355X_T_LONG_DOUBLE);
+    put(SlotTag<OpProd<f80>>{}, MI355X_OP_PROD, MI355X_T_LONG_DOUBLE);
 }
 
 } // namespace mi355x

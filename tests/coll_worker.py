@@ -932,7 +932,8 @@ def staging_main():
       * a non-commutative user MPI_Op (a op b = 3a + b on MPI_INT) on device buffers, rank 0 on host
         buffers: allreduce (also in place), reduce, reduce_scatter_block, reduce_scatter, scan, exscan,
         iallreduce, ireduce, ireduce_scatter_block;
-      * MPI_SUM / MPI_PROD over MPI_LONG_DOUBLE (no 80-bit arithmetic on the GPU) on device buffers;
+      * MPI_SUM / MPI_PROD over MPI_LONG_DOUBLE and C_LONG_DOUBLE_COMPLEX served by the engine (the x87
+        add / multiply on the GPU), bit-exact with the oracle's schedule on the host's x87;
       * MAXLOC / MINLOC over MPI_LONG_DOUBLE_INT served by the engine's gather-then-fold form
         (allreduce, reduce, reduce_scatter_block, reduce_scatter, scan) in coll/tuned's order for the
         decision and for forced algorithms, on NaN-bearing pairs, nothing staged;
@@ -1053,23 +1054,26 @@ def staging_main():
     L.mini_op_destroy(uop)
 
     say("user op done")
-    # ---- 2. x87 arithmetic slots (no 80-bit arithmetic on the GPU): SUM / PROD over LONG_DOUBLE --
-    #         device buffers staged to the host module (coll/basic's linear order)
-    for opname, tname in (("SUM", "LONG_DOUBLE"), ("PROD", "LONG_DOUBLE")):
+    # ---- 2. x87 arithmetic slots: SUM / PROD over LONG_DOUBLE (16 B, the engine's fold families)
+    #         and C_LONG_DOUBLE_COMPLEX (32 B, gather-then-fold) -- the x87 add / multiply on the GPU
+    #         (f80_arith.hpp), engine-served in the reference schedule's order, nothing staged
+    for opname, tname in (("SUM", "LONG_DOUBLE"), ("PROD", "LONG_DOUBLE"), ("SUM", "C_LONG_DOUBLE_COMPLEX"),
+                          ("PROD", "C_LONG_DOUBLE_COMPLEX")):
         code, slot = pkg.OP[opname], pkg.T[tname]
-        assert not pkg.rt().mi355x_comm_op_supported(code, slot)
+        assert pkg.rt().mi355x_comm_op_supported(code, slot)
         op = m.select_op(code)
         dt = m.dtype_for_slot(slot)
-        n = 20_001
-        xs2 = [opdata.make(tname, n, 40 + r) for r in range(size)]
-        want = _linear(oracle, code, slot, xs2)
-        before = staged.value
-        d, dp, read = put(xs2[rank])
-        o, opp, oread2 = put(np.zeros_like(xs2[0]))
-        torch.cuda.synchronize()
-        assert L.mini_allreduce(comm, dp, opp, n, dt, op) == 0
-        opdata.assert_same(tname, opname, oread2(), want, "staged x87 allreduce")
-        assert staged.value == before + 1, "the x87 call was not staged"
+        for n in (3, 20_001):
+            xs2 = [opdata.make(tname, n, 40 + r) for r in range(size)]
+            outs = [np.zeros_like(xs2[0]) for _ in range(size)]
+            oracle.oracle_allreduce(0, size, n, slot, code, 0, ptrs(xs2), ptrs(outs))
+            before = staged.value
+            d, dp, read = put(xs2[rank])
+            o, opp, oread2 = put(np.zeros_like(xs2[0]))
+            torch.cuda.synchronize()
+            assert L.mini_allreduce(comm, dp, opp, n, dt, op) == 0
+            opdata.assert_same(tname, opname, oread2(), outs[rank], f"engine x87 {opname} allreduce n={n}")
+            assert staged.value == before, "an x87 SUM / PROD call was staged"
         L.mini_op_destroy(op)
     # MAXLOC / MINLOC over MPI_LONG_DOUBLE_INT (32-byte pairs): served by the engine's gather-then-
     # fold form in the per-element order of the algorithm coll/tuned runs -- the fixed decision, then

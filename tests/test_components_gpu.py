@@ -234,7 +234,7 @@ def test_declined_reductions_staged_through_host(gpu, size):
     """coll/cuda's host staging (coll_cuda_allreduce.c:43-75, coll_cuda_reduce.c,
     coll_cuda_reduce_scatter_block.c:45-83, coll_cuda_scan.c, coll_cuda_exscan.c) for every reduction
     the engine declines, over a lower-priority module that reduces on the CPU and fails on device
-    memory: a user MPI_Op and MPI_SUM/PROD over MPI_LONG_DOUBLE on device buffers, blocking and
+    memory: a user MPI_Op on device buffers, blocking and
     nonblocking, exact; MAXLOC/MINLOC over all six pair types (flags as libmpi sets them; the 32-byte
     MPI_LONG_DOUBLE_INT through the gather-then-fold form) and MAX/MIN over MPI_LONG_DOUBLE served by
     the engine, exact vs the oracle"""

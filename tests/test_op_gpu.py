@@ -41,19 +41,19 @@ def _host(t, off_bytes, like: np.ndarray) -> np.ndarray:
 
 
 def test_slot_coverage(gpu, pkg, oracle):
-    """every reference slot has a kernel (112 of 116) except the x87 long double SUM/PROD slots,
-    which need 80-bit arithmetic (op/hip stages them to the base loops); the x87 compare-only slots
-    (MAX/MIN on LONG_DOUBLE, MAXLOC/MINLOC on LONG_DOUBLE_INT) are GPU kernels"""
+    """every reference slot has a GPU kernel (116 of 116): the x87 long double slots too -- MAX/MIN
+    and MAXLOC/MINLOC compare and select on the 80-bit encoding, SUM/PROD (real and complex) run the
+    x87 add / multiply restated in integer arithmetic (f80_arith.hpp)"""
     have, missing = 0, []
     for op in range(15):
         for ty in range(len(pkg.TYPES)):
             if oracle.oracle_has_op(op, ty):
                 if pkg.op_supported(op, ty):
                     have += 1
-                elif not ("LONG_DOUBLE" in pkg.TYPES[ty] and pkg.OPS[op] in ("SUM", "PROD")):
+                else:
                     missing.append((pkg.OPS[op], pkg.TYPES[ty]))
     assert not missing, missing
-    assert have == 112
+    assert have == 116
 
 
 def _x87(m, se):
@@ -117,6 +117,73 @@ def test_x87_compare_slots(gpu, pkg, oracle, tname):
         assert oracle.oracle_op_2buff(op, ty, a.ctypes.data, want2.ctypes.data, len(pairs)) == 0
         opdata.assert_same(tname, opname, _host(to, 0, a), want3, "x87 3buff")
         opdata.assert_same(tname, opname, _host(tb, 0, a), want2, "x87 2buff")
+
+
+def _x87_random(n, seed):
+    """n random 80-bit values over the whole exponent range (normals, denormals, values near
+    overflow and underflow), both signs, in 16 bytes of storage"""
+    rng = np.random.default_rng(seed)
+    out = np.zeros((n, 16), dtype=np.uint8)
+    m = rng.integers(0, 2**63, n, dtype=np.uint64) | (np.uint64(1) << np.uint64(63))
+    mode = rng.integers(0, 4, n)
+    e = np.where(mode == 0, rng.integers(0, 0x7fff, n), np.where(mode == 1, rng.integers(0, 140, n),
+                 np.where(mode == 2, 0x7ffe - rng.integers(0, 140, n), 0x3fff + rng.integers(-65, 65, n))))
+    m = np.where(e == 0, m & np.uint64(2**63 - 1), m)
+    se = (e | (rng.integers(0, 2, n) << 15)).astype(np.uint16)
+    out[:, :8] = m.view(np.uint8).reshape(n, 8)
+    out[:, 8:10] = se.view(np.uint8).reshape(n, 2)
+    return out
+
+
+@pytest.mark.parametrize("tname", ["LONG_DOUBLE", "C_LONG_DOUBLE_COMPLEX"])
+def test_x87_arith_slots(gpu, pkg, oracle, tname):
+    """SUM / PROD on x87 long double (real and complex) on the GPU against the oracle's C loops,
+    which run on this host's x87 unit (op_base_functions.c:110-170; complex PROD through GCC's
+    inline multiply + libgcc __mulxc3): every ordered pair of the adversarial encodings (NaNs of
+    equal significands and both signs, invalid encodings, infinities, denormals) and 200k random
+    pairs over the whole exponent range, 2-buff and 3-buff, bit-exact in the 10 value bytes"""
+    torch = gpu
+    enc = [np.frombuffer(x, np.uint8) for x in x87_adversarial()]
+    pairs = np.array([(x, y) for x in enc for y in enc], dtype=np.uint8)   # (P, 2, 16)
+    ra, rb = _x87_random(200_000, 1), _x87_random(200_000, 2)
+    A = np.concatenate([pairs[:, 0], ra])
+    B = np.concatenate([pairs[:, 1], rb])
+    dt = opdata.dtype_of(tname)
+    if tname == "C_LONG_DOUBLE_COMPLEX":  # re from one list, im from the other, both roles
+        n = len(A) // 2
+        a = np.zeros(n, dtype=dt)
+        b = np.zeros(n, dtype=dt)
+        av, bv = a.view(np.uint8).reshape(n, 32), b.view(np.uint8).reshape(n, 32)
+        av[:, :16], av[:, 16:] = A[:n], B[n:2 * n]
+        bv[:, :16], bv[:, 16:] = B[:n], A[n:2 * n]
+    else:
+        n = len(A)
+        a = np.zeros(n, dtype=dt)
+        b = np.zeros(n, dtype=dt)
+        a.view(np.uint8).reshape(n, 16)[:] = A
+        b.view(np.uint8).reshape(n, 16)[:] = B
+    s = torch.cuda.current_stream().cuda_stream
+    for opname in ("SUM", "PROD"):
+        op, ty = pkg.OP[opname], pkg.T[tname]
+        assert pkg.op_supported(op, ty)
+        ta, pa = _dev(torch, a)
+        tb, pb = _dev(torch, b)
+        to, po = _dev(torch, np.zeros_like(a))
+        pkg.op_reduce_3buff(op, ty, pa, pb, po, n, s)
+        pkg.op_reduce(op, ty, pa, pb, n, s)
+        torch.cuda.synchronize()
+        want3 = np.zeros_like(a)
+        assert oracle.oracle_op_3buff(op, ty, a.ctypes.data, b.ctypes.data, want3.ctypes.data, n) == 0
+        want2 = b.copy()
+        assert oracle.oracle_op_2buff(op, ty, a.ctypes.data, want2.ctypes.data, n) == 0
+        nb = 10
+        for got, want, form in ((_host(to, 0, a), want3, "3buff"), (_host(tb, 0, a), want2, "2buff")):
+            g = got.view(np.uint8).reshape(n, -1)
+            w = want.view(np.uint8).reshape(n, -1)
+            cols = list(range(nb)) + ([16 + i for i in range(nb)] if tname == "C_LONG_DOUBLE_COMPLEX" else [])
+            bad = np.nonzero((g[:, cols] != w[:, cols]).any(1))[0]
+            assert len(bad) == 0, (f"{opname} {form}: {len(bad)} of {n} differ; first", bad[:4].tolist(),
+                                   g[bad[:2]].tolist(), w[bad[:2]].tolist())
 
 
 @pytest.mark.parametrize("offs", [(0, 0, 0), (1, 1, 1), (1, 0, 2)], ids=["aligned", "comisaligned", "misaligned"])
