@@ -78,11 +78,13 @@ def comms(gpu, pkg):
 def test_allreduce(gpu, pkg, oracle, comms, n, alg, inplace, push):
     torch = gpu
     cs = comms(n)
-    cs[0].set("PUSH", push)
+    for c in cs:  # (a per-communicator knob: the same value on every rank)
+        c.set("PUSH", push)
     try:
         _allreduce_cases(torch, pkg, oracle, cs, n, alg, inplace)
     finally:
-        cs[0].set("PUSH", 0)
+        for c in cs:
+            c.set("PUSH", 0)
 
 
 def _allreduce_cases(torch, pkg, oracle, cs, n, alg, inplace):
@@ -264,7 +266,8 @@ def test_reduce_scatter(gpu, pkg, oracle, comms, n, rsalg):
 def test_allgather(gpu, pkg, comms, n, nbytes, inplace, push):
     torch = gpu
     cs = comms(n)
-    cs[0].set("PUSH", push)
+    for c in cs:  # (a per-communicator knob: the same value on every rank)
+        c.set("PUSH", push)
     src = [torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda") for _ in range(n)]
     dst = [torch.zeros(n * nbytes, dtype=torch.uint8, device="cuda") for _ in range(n)]
     if inplace:
@@ -273,7 +276,8 @@ def test_allgather(gpu, pkg, comms, n, nbytes, inplace, push):
     torch.cuda.synchronize()
     run_ranks(n, lambda r: cs[r].allgather(None if inplace else src[r].data_ptr(), dst[r].data_ptr(), nbytes))
     torch.cuda.synchronize()
-    cs[0].set("PUSH", 0)
+    for c in cs:
+        c.set("PUSH", 0)
     want = torch.cat(src)
     for r in range(n):
         assert torch.equal(dst[r], want), r
