@@ -188,6 +188,23 @@ def bench_op(args, pkg, torch):
 OP_CEILING_GBS = 6640.0
 
 
+def fill_x87(torch, bufs):
+    """Valid x87 extended values in every 16-B unit: significand with its integer bit set, exponent
+    0x3fff +- 16, random sign (the padding bytes 10..15 zero).  Used for the long double slots, whose
+    integer-arithmetic kernels take a different path for the invalid encodings random bits produce."""
+    g = torch.Generator(device=bufs[0].device)
+    g.manual_seed(87)
+    for t in bufs:
+        w = t.view(torch.int64).view(-1, 2)
+        w[:, 0] = torch.randint(-2**63, 2**63 - 1, (w.shape[0],), device=t.device, dtype=torch.int64,
+                                generator=g) | (-2**63)
+        e = torch.randint(0x3fff - 16, 0x3fff + 17, (w.shape[0],), device=t.device, dtype=torch.int64,
+                          generator=g)
+        sgn = torch.randint(0, 2, (w.shape[0],), device=t.device, dtype=torch.int64, generator=g)
+        w[:, 1] = e | (sgn << 15)
+    torch.cuda.synchronize()
+
+
 def sweep_op(pkg, torch, a, b, o, reps: int = 5):
     """BASELINE configs[1] as a whole: every op/hip GPU slot (op x predefined type), 2-buff and
     3-buff, on 1 GiB per operand (the headline's buffers re-typed), after the headline's timed
@@ -200,10 +217,16 @@ def sweep_op(pkg, torch, a, b, o, reps: int = 5):
     nbytes = a.numel() * a.element_size()
     rows = []
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for op in range(1, len(pkg.OPS)):
-        for ty in range(len(pkg.TYPES)):
+    x87 = [i for i, t in enumerate(pkg.TYPES) if "LONG_DOUBLE" in t]
+    order = [t for t in range(len(pkg.TYPES)) if t not in x87] + x87
+    refilled = False
+    for ty in order:
+        for op in range(1, len(pkg.OPS)):
             if not pkg.op_supported(op, ty):
                 continue
+            if ty in x87 and not refilled:
+                fill_x87(torch, (a, b, o))
+                refilled = True
             n = nbytes // pkg.type_size(ty)
             res = {}
             for form in ("2buff", "3buff"):
@@ -232,6 +255,9 @@ def sweep_op(pkg, torch, a, b, o, reps: int = 5):
                 "slots_below_0.90_ceiling": [f"{r[0]}/{r[1]}" for r in rows if r[idx] < 0.9 * OP_CEILING_GBS]}
 
     return {"slots": len(rows), "bytes_per_operand": nbytes, "reps": reps,
+            "x87_data": "the long double slots run last, on operands refilled with valid x87 encodings "
+                        "(explicit integer bit, exponent within 2^+-16, random sign and significand): "
+                        "the headline's fp32 bits read as x87 values are half invalid encodings",
             "ceiling_2r1w_GBps": OP_CEILING_GBS, "ceiling_from": "profiles/r02_op_ceiling.jsonl",
             "two_buff": summary(3), "three_buff": summary(4),
             "table": {f"{r[0]}/{r[1]}": [r[3], r[4]] for r in rows},

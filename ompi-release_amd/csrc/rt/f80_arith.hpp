@@ -118,9 +118,56 @@ MI_HD int32_t eff_exp(Bits x)
     return e ? e : 1;
 }
 
+// both operands normal (exponent 1..0x7ffe, integer bit set): the fast paths' precondition
+MI_HD bool both_normal(Bits a, Bits b)
+{
+    return ((a.m & b.m) >> 63) != 0 && (uint32_t)(a.se & 0x7fff) - 1u < 0x7ffeu &&
+           (uint32_t)(b.se & 0x7fff) - 1u < 0x7ffeu;
+}
+
+// round a significand whose leading one is at bit 127 (hi:lo) with exponent field E to nearest even,
+// when the result is certainly normal and finite (1 <= E < 0x7ffe; a carry out of the significand
+// then still leaves E <= 0x7ffe) -- round_pack's normal case, without its normalise / denormal /
+// overflow steps
+MI_HD Bits round_normal(uint32_t sign, int32_t E, uint64_t hi, uint64_t lo)
+{
+    if ((lo >> 63) && ((lo << 1) != 0 || (hi & 1))) {
+        hi += 1;
+        if (hi == 0) {
+            hi = kInt;
+            E += 1;
+        }
+    }
+    return Bits{hi, (uint16_t)((sign << 15) | (uint32_t)E)};
+}
+
 // a + b (b's sign flipped first when sub: the NaN and invalid rules look at the operands as given)
 MI_HD Bits add(Bits a, Bits b, bool sub)
 {
+    if (both_normal(a, b)) {  // the common case: no specials, normal result unless it says otherwise
+        const uint32_t sa = a.se >> 15, sb = (uint32_t)((b.se >> 15) ^ (sub ? 1 : 0));
+        const int32_t ea = a.se & 0x7fff, eb = b.se & 0x7fff;
+        const bool bl = eb > ea || (eb == ea && b.m > a.m);  // |b| > |a|: b leads
+        const int32_t E0 = bl ? eb : ea;
+        const u128 A = (u128)(bl ? b.m : a.m) << 64;
+        const u128 B = shr_sticky((u128)(bl ? a.m : b.m) << 64, bl ? eb - ea : ea - eb);
+        u128 S;
+        int32_t E = E0;
+        if (sa == sb) {
+            S = A + B;
+            if (S < A) {
+                S = shr_sticky(S, 1) | ((u128)1 << 127);
+                E += 1;
+            }
+        } else {
+            S = A - B;
+            if (S == 0) return Bits{0, 0};
+            const int lz = clz128(S);  // exact when lz > 1 (the operands were within one binade)
+            S <<= lz;
+            E -= lz;
+        }
+        if (E >= 1 && E < 0x7ffe) return round_normal(bl ? sb : sa, E, (uint64_t)(S >> 64), (uint64_t)S);
+    }
     const int ka = kind(a), kb = kind(b);
     if (ka == 4 || kb == 4) return indefinite();
     if (ka == 3 || kb == 3) return nan_result(a, b, ka, kb);
@@ -161,6 +208,17 @@ MI_HD Bits add(Bits a, Bits b, bool sub)
 
 MI_HD Bits mul(Bits a, Bits b)
 {
+    if (both_normal(a, b)) {  // product of two normal significands: leading one at bit 127 or 126
+        const u128 P = (u128)a.m * (u128)b.m;
+        uint64_t hi = (uint64_t)(P >> 64), lo = (uint64_t)P;
+        int32_t E = (int32_t)(a.se & 0x7fff) + (int32_t)(b.se & 0x7fff) - 16383 + 1;
+        if (!(hi >> 63)) {
+            hi = (hi << 1) | (lo >> 63);
+            lo <<= 1;
+            E -= 1;
+        }
+        if (E >= 1 && E < 0x7ffe) return round_normal((uint32_t)((a.se ^ b.se) >> 15), E, hi, lo);
+    }
     const int ka = kind(a), kb = kind(b);
     if (ka == 4 || kb == 4) return indefinite();
     if (ka == 3 || kb == 3) return nan_result(a, b, ka, kb);

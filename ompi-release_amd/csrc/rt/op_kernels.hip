@@ -252,6 +252,68 @@ __global__ __launch_bounds__(256) void k_wide(const typename F::T *a, const type
 // lanes of an element swap halves with one DPP quad permute per dword (no LDS), both evaluate the
 // element, each stores its own half.  One-shot grid, non-temporal beyond the Infinity Cache, as
 // k_chunk.
+// The complex x87 slots evaluate one component per lane instead of the whole element twice: the
+// lane holding the real halves computes the real part, its partner the imaginary part.  CSUM needs
+// nothing from the partner; CPROD reads the partner's halves for the cross products and, when both
+// parts come out NaN (the pair agrees on that through one more DPP swap), both lanes redo the whole
+// product under the recovery rules of cmul.  The integer x87 arithmetic makes these two slots
+// VALU-bound, so halving the work per lane is what moves them toward the memory ceiling.
+template <class F> struct PerComponent : std::false_type {};
+template <> struct PerComponent<OpCsum<cf80>> : std::true_type {};
+template <> struct PerComponent<OpCprod<cf80>> : std::true_type {};
+
+__device__ __forceinline__ f80 f80_of_vec(u32x4 v)
+{
+    f80 x;
+    __builtin_memcpy(&x, &v, 16);
+    return x;
+}
+
+__device__ __forceinline__ u32x4 vec_of_f80(f80 x)
+{
+    u32x4 v;
+    __builtin_memcpy(&v, &x, 16);
+    return v;
+}
+
+__device__ __forceinline__ u32x4 dpp_swap(u32x4 v)  // lanes 2k <-> 2k+1 (quad_perm [1,0,3,2])
+{
+    u32x4 p;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) p[k] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v[k], 0xB1, 0xF, 0xF, false);
+    return p;
+}
+
+template <class F, bool THREE>
+__device__ __forceinline__ u32x4 component(u32x4 ra, u32x4 rb, bool hi)
+{
+    // operand roles as apply(): 2-buff op2(inout = b, in = a), 3-buff op3(in1 = a, in2 = b)
+    const u32x4 vo = THREE ? ra : rb, va = THREE ? rb : ra;
+    const f80 om = f80_of_vec(vo), am = f80_of_vec(va);
+    if constexpr (std::is_same<F, OpCsum<cf80>>::value) {
+        return vec_of_f80(om + am);  // (o.re + a.re) or (o.im + a.im)
+    } else {
+        const u32x4 po = dpp_swap(vo), pa = dpp_swap(va);
+        const f80 op = f80_of_vec(po), ap = f80_of_vec(pa);
+        // cmul(a, b, c, d) with a = o.re, b = o.im, c = a.re, d = a.im: x = ac - bd, y = ad + bc
+        // one instruction stream for both lanes of the pair (the wave alternates lo / hi lanes, so
+        // a branch on hi would run both paths): operands selected, subtract flag per lane
+        const f80 m1 = (hi ? op : om) * am, m2 = (hi ? om : op) * ap;
+        const f80 r = f80_of(x87::add(f80_bits(m1), f80_bits(m2), !hi));
+        // cmul changes the result only when both parts are NaN and an operand or one of the four
+        // products is infinite (it recomputes then); the pair shares "NaN" and "a product of mine
+        // is infinite" in one swapped word
+        const int mine = (is_nan(r) ? 1 : 0) | (is_inf(m1) || is_inf(m2) ? 2 : 0);
+        const int partner = __builtin_amdgcn_update_dpp(0, mine, 0xB1, 0xF, 0xF, false);
+        const bool inf_operand = is_inf(om) || is_inf(op) || is_inf(am) || is_inf(ap);
+        if ((mine & partner & 1) && (inf_operand || ((mine | partner) & 2))) {
+            const cf80 w = hi ? cmul<f80>(op, om, ap, am) : cmul<f80>(om, op, am, ap);
+            return vec_of_f80(hi ? w.im : w.re);
+        }
+        return vec_of_f80(r);
+    }
+}
+
 template <class F, bool THREE, int NTM>
 __global__ __launch_bounds__(1024) void k_wide_halves(const u32x4 *a, const u32x4 *b, u32x4 *o, size_t nhalf)
 {
@@ -269,14 +331,18 @@ __global__ __launch_bounds__(1024) void k_wide_halves(const u32x4 *a, const u32x
             rb = b[i];
         }
     }
-    u32x4 pa, pb;  // the partner lane's halves: quad_perm [1,0,3,2] swaps lanes 2k and 2k+1
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        pa[k] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)ra[k], 0xB1, 0xF, 0xF, false);
-        pb[k] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)rb[k], 0xB1, 0xF, 0xF, false);
-    }
-    if (!live) return;
     const bool hi = (i & 1) != 0;
+    if constexpr (PerComponent<F>::value) {
+        const u32x4 mine = component<F, THREE>(ra, rb, hi);  // (every lane: the DPP swaps inside)
+        if (!live) return;
+        if constexpr ((NTM & 2) != 0)
+            __builtin_nontemporal_store(mine, o + i);
+        else
+            o[i] = mine;
+        return;
+    }
+    const u32x4 pa = dpp_swap(ra), pb = dpp_swap(rb);  // the partner lane's halves
+    if (!live) return;
     u32x4 ea[2] = {hi ? pa : ra, hi ? ra : pa};
     u32x4 eb[2] = {hi ? pb : rb, hi ? rb : pb};
     T xa, xb;
