@@ -240,7 +240,6 @@ int mi355x_comm_destroy(mi355x_comm_t *c)
     for (hipEvent_t e : c->tev)
         if (e) (void)hipEventDestroy(e);
     if (c->nb_stream) (void)hipStreamDestroy(c->nb_stream);
-    if (c->setup_s) (void)hipStreamDestroy(c->setup_s);
     flush_retired(c);
     for (auto &kv : c->peer_maps) close_map(kv.second);
     for (LocalReg &r : c->local_regs) drop_reg(r);

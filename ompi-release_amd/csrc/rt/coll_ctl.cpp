@@ -546,21 +546,13 @@ int setup_done_words(mi355x_comm *c)
 // The scratch may be exported to peers (MPI_Reduce's owner blocks): never a small allocation
 // (small hipMallocs can fail hipIpcOpenMemHandle on the importer with "invalid device
 // pointer"), and grown geometrically so it is rarely freed while peers hold a mapping.
-// The engine's own stream for setup-time fills and copies: a non-blocking stream, so setup never
-// waits for -- or makes wait -- the application's streams (no hipDeviceSynchronize anywhere on the
-// setup paths); nullptr when it cannot be created (the caller's error path reports the HIP error).
-// the stream setup work runs on: inside a collective its own stream (CallStream), else a stream of
-// the communicator's own, made on first use (the null stream if that fails: still correct, it
-// only orders with more of the device's work)
-hipStream_t setup_stream(mi355x_comm *c)
-{
-    if (c->call_depth > 0) return c->call_s;
-    if (!c->setup_s && hipStreamCreateWithFlags(&c->setup_s, hipStreamNonBlocking) != hipSuccess) {
-        (void)hipGetLastError();
-        c->setup_s = nullptr;
-    }
-    return c->setup_s;
-}
+// The stream setup-time fills and copies run on: inside a collective, the call's own stream
+// (CallStream), so setup orders with the caller's work and never waits for -- or makes wait -- the
+// application's other streams (no hipDeviceSynchronize anywhere on the setup paths).  Every setup
+// path runs inside a collective; outside one (a communicator set up eagerly at creation) the null
+// stream.  No per-communicator stream: an idle extra queue per communicator measurably slows
+// co-located ranks (profiles/r05_setup_stream_bisect.txt).
+hipStream_t setup_stream(mi355x_comm *c) { return c->call_depth > 0 ? c->call_s : nullptr; }
 
 int ensure_scratch(mi355x_comm *c, size_t bytes)
 {

@@ -381,7 +381,6 @@ struct mi355x_comm {
     bool dev_ready = false;
     bool selftest = true;                         // MI355X_KNOB_SELFTEST (env MI355X_SELFTEST)
     double setup_us = 0;
-    hipStream_t setup_s = nullptr;                // the engine's own stream for setup-time copies
     std::vector<std::pair<int, long>> preset;     // knobs set before dev_setup, applied after it
     bool svc_stuck = false;                       // a service kernel never left (its memory is leaked, never reused)
     uint64_t *svc_trace = nullptr;                // MI355X_SVC_TRACE=1: stage stamps (device memory), printed at destroy
