@@ -1,8 +1,9 @@
 // coll_gfold.cpp -- the engine's form for the op/hip slots its fold families do not carry.
 //
-// MPI_LONG_DOUBLE_INT's pairs are 32 bytes, twice the 16-byte vector the engine's fold, pipelined
-// and LL kernel families are built around; op/hip reduces them on the GPU (k_wide_halves, exact x87
-// compare on the 80-bit encoding).  The engine serves such a slot as gather-then-fold: every rank's
+// MPI_LONG_DOUBLE_INT's pairs and MPI_C_LONG_DOUBLE_COMPLEX's values are 32 bytes, twice the
+// 16-byte vector the engine's fold, pipelined and LL kernel families are built around; op/hip
+// reduces them on the GPU (k_wide_halves: exact x87 compare on the 80-bit encoding, x87 add /
+// multiply in integer arithmetic).  The engine serves such a slot as gather-then-fold: every rank's
 // input is gathered window by window into a per-communicator device buffer (mi355x_allgather's
 // flows, over xGMI), then each rank evaluates the elements it owns with op/hip's 2-buff kernel, in
 // the per-element order of the algorithm coll/tuned would run for the call -- the same programs
