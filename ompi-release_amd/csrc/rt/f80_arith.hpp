@@ -148,25 +148,46 @@ MI_HD Bits add(Bits a, Bits b, bool sub)
         const uint32_t sa = a.se >> 15, sb = (uint32_t)((b.se >> 15) ^ (sub ? 1 : 0));
         const int32_t ea = a.se & 0x7fff, eb = b.se & 0x7fff;
         const bool bl = eb > ea || (eb == ea && b.m > a.m);  // |b| > |a|: b leads
-        const int32_t E0 = bl ? eb : ea;
-        const u128 A = (u128)(bl ? b.m : a.m) << 64;
-        const u128 B = shr_sticky((u128)(bl ? a.m : b.m) << 64, bl ? eb - ea : ea - eb);
-        u128 S;
-        int32_t E = E0;
+        const uint64_t ma = bl ? b.m : a.m, mb = bl ? a.m : b.m;
+        const uint32_t d = (uint32_t)(bl ? eb - ea : ea - eb);
+        // the trailing significand aligned: (mb << 64) >> d as bh:blo, shifted-out bits sticky in
+        // bit 0 (64-bit halves: the operands' low halves are zero, so half the u128 work is known)
+        uint64_t bh, blo;
+        if (d < 64) {
+            bh = mb >> d;
+            blo = d ? mb << (64 - d) : 0;
+        } else if (d < 128) {
+            bh = 0;
+            blo = (mb >> (d - 64)) | (d > 64 && (mb << (128 - d)) != 0 ? 1 : 0);
+        } else {
+            bh = 0;
+            blo = 1;  // (mb != 0: a normal significand)
+        }
+        uint64_t hi, lo;
+        int32_t E = bl ? eb : ea;
         if (sa == sb) {
-            S = A + B;
-            if (S < A) {
-                S = shr_sticky(S, 1) | ((u128)1 << 127);
+            hi = ma + bh;
+            lo = blo;
+            if (hi < ma) {  // carry out of bit 127: one place right, the bit shifted out sticky
+                lo = (lo >> 1) | (hi << 63) | (lo & 1);
+                hi = (hi >> 1) | kInt;
                 E += 1;
             }
         } else {
-            S = A - B;
-            if (S == 0) return Bits{0, 0};
-            const int lz = clz128(S);  // exact when lz > 1 (the operands were within one binade)
-            S <<= lz;
+            lo = 0 - blo;
+            hi = ma - bh - (blo != 0 ? 1 : 0);
+            if ((hi | lo) == 0) return Bits{0, 0};
+            const int lz = hi ? __builtin_clzll(hi) : 64 + __builtin_clzll(lo);  // exact when lz > 1
+            if (lz >= 64) {
+                hi = lo << (lz - 64);
+                lo = 0;
+            } else if (lz > 0) {
+                hi = (hi << lz) | (lo >> (64 - lz));
+                lo <<= lz;
+            }
             E -= lz;
         }
-        if (E >= 1 && E < 0x7ffe) return round_normal(bl ? sb : sa, E, (uint64_t)(S >> 64), (uint64_t)S);
+        if (E >= 1 && E < 0x7ffe) return round_normal(bl ? sb : sa, E, hi, lo);
     }
     const int ka = kind(a), kb = kind(b);
     if (ka == 4 || kb == 4) return indefinite();

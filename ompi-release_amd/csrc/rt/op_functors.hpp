@@ -228,9 +228,9 @@ template <typename R> MI_DEV bool is_nan(R x) { return x != x; }
 template <typename R> MI_DEV bool is_inf(R x) { return __builtin_isinf(x); }
 template <typename R> MI_DEV R copysgn(R m, R s) { return __builtin_copysign(m, s); }
 template <typename R> MI_DEV R cst(double v) { return (R)v; }
-// x87: isnan is an unordered self-compare (NaNs and the invalid encodings), isinf exact infinity,
+// x87: isnan is an unordered self-compare (NaNs and the invalid encodings: kind 3 and 4), isinf exact infinity,
 // copysign the sign bit
-template <> MI_DEV bool is_nan<f80>(f80 x) { return x87_cmp(x, x) == 2; }
+template <> MI_DEV bool is_nan<f80>(f80 x) { return x87::kind(f80_bits(x)) >= 3; }  // == x87_cmp(x, x) == 2
 template <> MI_DEV bool is_inf<f80>(f80 x) { return x87::kind(f80_bits(x)) == 2; }
 template <> MI_DEV f80 copysgn<f80>(f80 m, f80 s)
 {

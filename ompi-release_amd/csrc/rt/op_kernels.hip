@@ -303,10 +303,11 @@ __device__ __forceinline__ u32x4 component(u32x4 ra, u32x4 rb, bool hi)
         // cmul changes the result only when both parts are NaN and an operand or one of the four
         // products is infinite (it recomputes then); the pair shares "NaN" and "a product of mine
         // is infinite" in one swapped word
-        const int mine = (is_nan(r) ? 1 : 0) | (is_inf(m1) || is_inf(m2) ? 2 : 0);
+        int mine = 0;
+        if (is_nan(r)) mine = 1 | (is_inf(m1) || is_inf(m2) ? 2 : 0);  // (never taken on finite data)
         const int partner = __builtin_amdgcn_update_dpp(0, mine, 0xB1, 0xF, 0xF, false);
-        const bool inf_operand = is_inf(om) || is_inf(op) || is_inf(am) || is_inf(ap);
-        if ((mine & partner & 1) && (inf_operand || ((mine | partner) & 2))) {
+        if ((mine & partner & 1) &&
+            (((mine | partner) & 2) || is_inf(om) || is_inf(op) || is_inf(am) || is_inf(ap))) {
             const cf80 w = hi ? cmul<f80>(op, om, ap, am) : cmul<f80>(om, op, am, ap);
             return vec_of_f80(hi ? w.im : w.re);
         }
