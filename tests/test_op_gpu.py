@@ -141,7 +141,8 @@ def test_x87_arith_slots(gpu, pkg, oracle, tname):
     which run on this host's x87 unit (op_base_functions.c:110-170; complex PROD through GCC's
     inline multiply + libgcc __mulxc3): every ordered pair of the adversarial encodings (NaNs of
     equal significands and both signs, invalid encodings, infinities, denormals) and 200k random
-    pairs over the whole exponent range, 2-buff and 3-buff, bit-exact in the 10 value bytes"""
+    pairs over the whole exponent range (complex: also every combination of 11 specials in the four
+    parts), 2-buff and 3-buff, bit-exact in the 10 value bytes"""
     torch = gpu
     enc = [np.frombuffer(x, np.uint8) for x in x87_adversarial()]
     pairs = np.array([(x, y) for x in enc for y in enc], dtype=np.uint8)   # (P, 2, 16)
@@ -150,12 +151,23 @@ def test_x87_arith_slots(gpu, pkg, oracle, tname):
     B = np.concatenate([pairs[:, 1], rb])
     dt = opdata.dtype_of(tname)
     if tname == "C_LONG_DOUBLE_COMPLEX":  # re from one list, im from the other, both roles
-        n = len(A) // 2
+        # plus every (a.re, a.im, b.re, b.im) over a set of specials, so each branch of the Annex G
+        # recovery (an infinite operand part, an infinite product, NaN parts) meets every other
+        I = 1 << 63
+        spec = [np.frombuffer(_x87(m, e), np.uint8) for m, e in
+                [(0, 0), (0, 0x8000), (I, 0x3FFF), (I, 0xBFFF), (I, 0x7FFF), (I, 0xFFFF), (I | (1 << 62), 0x7FFF),
+                 (I | 1, 0xFFFF), (0xFFFFFFFFFFFFFFFF, 0x7FFE), (5, 0), (5, 0x3FFF)]]
+        k = len(spec)
+        idx = np.indices((k, k, k, k)).reshape(4, -1)
+        S = np.array(spec, dtype=np.uint8)
+        n0 = len(A) // 2
+        n = n0 + idx.shape[1]
         a = np.zeros(n, dtype=dt)
         b = np.zeros(n, dtype=dt)
         av, bv = a.view(np.uint8).reshape(n, 32), b.view(np.uint8).reshape(n, 32)
-        av[:, :16], av[:, 16:] = A[:n], B[n:2 * n]
-        bv[:, :16], bv[:, 16:] = B[:n], A[n:2 * n]
+        av[:n0, :16], av[:n0, 16:] = A[:n0], B[n0:2 * n0]
+        bv[:n0, :16], bv[:n0, 16:] = B[:n0], A[n0:2 * n0]
+        av[n0:, :16], av[n0:, 16:], bv[n0:, :16], bv[n0:, 16:] = S[idx[0]], S[idx[1]], S[idx[2]], S[idx[3]]
     else:
         n = len(A)
         a = np.zeros(n, dtype=dt)
