@@ -120,6 +120,56 @@ bool peer_gone(mi355x_comm *c)
 }
 
 // ----------------------------------------------------------------- barrier
+// Point-to-point progress from inside a collective's barrier.  MPI's progress rule: a receive
+// posted before the collective completes while its sender waits in a blocking send (ob1 progresses
+// posted receives inside any blocking call), so the pass may read a payload and open a peer mapping
+// for it -- which must not overlap a peer's closes (coll_rcache.cpp, retire_map).  The pass announces
+// itself (opening) and then looks for a member that is closing; a closer announces itself (closing)
+// and then waits for every opening pass to end (close_window).  Sequentially consistent stores and
+// loads on both sides (Dekker): one of the two always sees the other, so a pass either opens with no
+// close of this communicator in flight or defers its opens to a later pass.
+void barrier_progress(mi355x_comm *c)
+{
+    RankSlot &me = c->ctrl->slot[c->rank];
+    me.opening.store(1, std::memory_order_seq_cst);
+    bool closing = false;
+    for (int r = 0; r < c->size && !closing; ++r)
+        closing = r != c->rank && c->ctrl->slot[r].closing.load(std::memory_order_seq_cst) != 0;
+    p2p_progress_all(closing);
+    me.opening.store(0, std::memory_order_release);
+}
+
+// close this rank's retired mappings while no member's barrier pass may be opening one
+static int close_window(mi355x_comm *c)
+{
+    RankSlot &me = c->ctrl->slot[c->rank];
+    me.closing.store(1, std::memory_order_seq_cst);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int r = 0; r < c->size; ++r) {
+        unsigned spins = 0;
+        while (r != c->rank && c->ctrl->slot[r].opening.load(std::memory_order_seq_cst) != 0) {
+            // the pass may wait for a dmabuf fd of mine (take_fd): keep serving them meanwhile
+            if ((++spins & 63) == 0) {
+                p2p_progress_all(true);
+                if (c->fd_sock >= 0 && c->reg_mtx.try_lock()) {
+                    (void)fd_drain(c, false);
+                    c->reg_mtx.unlock();
+                }
+            }
+            if ((spins & 0xffff) == 0 &&
+                (c->ctrl->abort_flag.load(std::memory_order_relaxed) || peer_gone(c) ||
+                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s)) {
+                me.closing.store(0, std::memory_order_release);
+                return set_error(MI355X_ERR_PEER, "rank %d: rank %d's progress pass never ended", c->rank, r);
+            }
+            sched_yield();
+        }
+    }
+    flush_retired(c);
+    me.closing.store(0, std::memory_order_release);
+    return MI355X_SUCCESS;
+}
+
 int barrier(mi355x_comm *c)
 {
     if (c->size == 1) return MI355X_SUCCESS;
@@ -137,7 +187,7 @@ int barrier(mi355x_comm *c)
             return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
         if (++spins > 2048) {
             sched_yield();
-            if ((spins & 63) == 0) p2p_progress_all(true);  // queued eager sends a peer may be waiting for
+            if ((spins & 63) == 0) barrier_progress(c);  // a peer may wait in a send for a receive of mine
             // a peer may be blocked sending us dmabuf fds (full socket queue): drain it while we wait
             if (c->fd_sock >= 0 && (spins & 255) == 0 && c->reg_mtx.try_lock()) {
                 (void)fd_drain(c, false);
@@ -372,7 +422,7 @@ int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t s
     bool window = false;
     for (int r = 0; r < c->size; ++r) window = window || c->ctrl->slot[r].retiring != 0;
     if (window) {
-        flush_retired(c);
+        if ((rc = close_window(c))) return rc;
         rc = barrier(c);
         if (rc) return rc;
     }
@@ -444,6 +494,11 @@ int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t s
                 if (c->ctrl->abort_flag.load(std::memory_order_relaxed)) return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
                 if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s)
                     return set_error(MI355X_ERR_TIMEOUT, "rank %d: the mapping window timed out waiting for rank %d", c->rank, r);
+                // a peer's open may wait for a dmabuf fd of mine (take_fd): serve them meanwhile
+                if (c->fd_sock >= 0 && c->reg_mtx.try_lock()) {
+                    (void)fd_drain(c, false);
+                    c->reg_mtx.unlock();
+                }
                 sched_yield();
             }
         }
@@ -451,7 +506,7 @@ int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t s
     };
     st.store((c->seq << 2) | kMapFailed, std::memory_order_release);
     if ((rc = wait_all(true))) return rc;   // every rank is past its opens
-    flush_retired(c);
+    if ((rc = close_window(c))) return rc;
     st.store((c->seq << 2) | kMapClosed, std::memory_order_release);
     if ((rc = wait_all(false))) return rc;  // every failing rank has closed
     for (const auto &f : failed) {
@@ -496,6 +551,7 @@ int finish(mi355x_comm *c, hipStream_t s)
                     (void)fd_drain(c, false);  // a peer may be asking for a dmabuf fd (serve_fd)
                     c->reg_mtx.unlock();
                 }
+                if ((spins & 255) == 0) barrier_progress(c);
                 if ((spins & 0xffff) == 0 && hipStreamQuery(s) != hipErrorNotReady && q == c->rank &&
                     k->slot[q].done.load(std::memory_order_acquire) < v)
                     return set_error(MI355X_ERR_HIP, "stream finished without writing its completion word");

@@ -64,6 +64,8 @@ struct alignas(64) RankSlot {
     int32_t pid, dev, nbuf;
     int32_t retiring;             // this rank holds retired peer mappings to close in the call's close window
     std::atomic<uint64_t> map_state;  // exchange: (call << 2) | 1 opens done, 2 an open failed, 3 closed (coll_ctl.cpp)
+    std::atomic<uint32_t> opening;    // a barrier's progress pass that may open peer mappings runs (barrier_progress)
+    std::atomic<uint32_t> closing;    // this rank closes retired peer mappings (close_window)
     uint64_t sig[4];
     BufDesc buf[kMaxBufs];
     int32_t probe_fd, probe_ok;   // dmabuf capability probe
@@ -483,6 +485,6 @@ struct CallGate {
     CallGate &operator=(const CallGate &) = delete;
 };
 int p2p_progress(mi355x_comm *c);
-void p2p_progress_all(bool from_collective = false);  // every communicator's point-to-point (the engine's host-side waits)
+void p2p_progress_all(bool defer_maps = false);  // every communicator's point-to-point (the engine's host-side waits)
 int p2p_wait(mi355x_request *r);
 } // namespace mi355x

@@ -181,16 +181,17 @@ static unsigned p2p_inject()
     return v;
 }
 
-// set while a progress pass runs from inside a collective's barrier: reads that would open a peer
-// mapping wait (hipIpc opens must not overlap a peer's close window, coll_rcache.cpp)
+// set while a progress pass must not open peer mappings -- from inside a collective's barrier while
+// a member closes its retired ones (coll_ctl.cpp, barrier_progress / close_window: hipIpc opens must
+// not overlap a peer's closes, coll_rcache.cpp): reads that would open one wait for a later pass
 static thread_local bool t_defer_maps = false;
 
-void p2p_progress_all(bool from_collective)
+void p2p_progress_all(bool defer_maps)
 {
     std::unique_lock<std::mutex> g(g_p2p_mtx, std::try_to_lock);  // (another thread progresses them now)
     if (!g.owns_lock()) return;
     const bool saved = t_defer_maps;
-    t_defer_maps = from_collective;
+    t_defer_maps = defer_maps;
     for (mi355x_comm *c : g_p2p_comms) (void)p2p_progress(c);
     t_defer_maps = saved;
 }

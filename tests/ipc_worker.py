@@ -1304,6 +1304,43 @@ def p2p_fault(key, rank, size, dev):
     print(f"rank {rank} p2p_fault OK", flush=True)
 
 
+def p2p_in_coll(key, rank, size, dev):
+    """MPI's progress rule across a collective: rank 0 posts a receive of a device payload (pulled
+    from the sender's allocation: a peer mapping to open) and enters an allreduce; rank 1 completes
+    a blocking send of it first (its FIN comes only once rank 0 has read the payload), then enters
+    the allreduce.  Rank 0's progress inside the collective's barrier must serve the receive (ob1
+    progresses a posted receive inside any blocking call).  Twice: the receive on the collective's
+    own communicator, then on a second one"""
+    import torch
+    torch.cuda.set_device(dev)
+    pkg = load_pkg()
+    comm = pkg.Comm.create(key, rank, size, dev)
+    other = pkg.Comm.create(key + "_p", rank, size, dev)
+    n = 4 << 20  # 16 MiB of fp32: neither inline nor a dual offer
+    x = torch.full((256,), float(rank + 1), device="cuda")
+    y = torch.zeros_like(x)
+    for it, pc in enumerate((comm, other)):
+        if rank == 0:
+            d = torch.zeros(n, device="cuda")
+            torch.cuda.synchronize()
+            req = pc.irecv(d.data_ptr(), n * 4, 1, 7 + it)
+            comm.allreduce(x.data_ptr(), y.data_ptr(), 256, pkg.T["FLOAT"], pkg.OP["SUM"])
+            req.wait()
+            torch.cuda.synchronize()
+            assert bool(torch.all(d == float(11 + it)).item()), ("p2p_in_coll payload", it)
+        else:
+            s = torch.full((n,), float(11 + it), device="cuda")
+            torch.cuda.synchronize()
+            pc.send(s.data_ptr(), n * 4, 0, 7 + it)
+            comm.allreduce(x.data_ptr(), y.data_ptr(), 256, pkg.T["FLOAT"], pkg.OP["SUM"])
+        torch.cuda.synchronize()
+        assert bool(torch.all(y == float(size * (size + 1) // 2)).item()), ("p2p_in_coll allreduce", it)
+    comm.barrier()
+    other.destroy()
+    comm.destroy()
+    print(f"rank {rank} p2p_in_coll OK", flush=True)
+
+
 def carved(key, rank, size, dev):
     """the bounded cache's dmabuf export check is on identity, not contents: the runtime carves small
     hipMallocs out of one buffer object and exports the whole object from its start, so a carved
@@ -1449,6 +1486,8 @@ def _main():
         return carved(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "p2p_fault":
         return p2p_fault(key, rank, size, dev)
+    if len(sys.argv) > 5 and sys.argv[5] == "p2p_in_coll":
+        return p2p_in_coll(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "token_hold":
         return token_hold(key, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "token_check":

@@ -46,7 +46,8 @@ def test_ipc_ranks(gpu, size):
 def _run_mode(gpu, mode, size=2, timeout=280, extra_env=None, key=None, rank_env=None):
     key = key or "t" + uuid.uuid4().hex[:12]
     ndev = gpu.cuda.device_count()
-    env = dict(os.environ, MI355X_TIMEOUT_S="60", **(extra_env or {}))
+    env = dict(os.environ, MI355X_TIMEOUT_S="60")
+    env.update(extra_env or {})
     procs = [subprocess.Popen([sys.executable, str(HERE / "ipc_worker.py"), key, str(r), str(size), str(r % ndev), mode],
                               env=dict(env, **((rank_env or {}).get(r, {}))), stdout=subprocess.PIPE,
                               stderr=subprocess.STDOUT, text=True) for r in range(size)]
@@ -203,6 +204,14 @@ def test_p2p_dual_offer_copy_failure(gpu, expect):
     device buffer (at first, or ever): claim 3 tells the receiver, which pulls after mapping again or
     fails its receive, and the send completes (ADVICE r5; ipc_worker.py::p2p_fault)"""
     _run_mode(gpu, "p2p_fault", 2, extra_env={"P2P_EXPECT": expect}, timeout=120)
+
+
+def test_p2p_receive_progresses_inside_a_collective(gpu):
+    """a receive posted before a collective is served by the progress the collective's barrier
+    makes while its peer is still in the matching blocking send (MPI's progress rule; ob1 progresses
+    posted receives inside any blocking call, opal_progress): on the collective's communicator and
+    on another one (ipc_worker.py::p2p_in_coll)"""
+    _run_mode(gpu, "p2p_in_coll", 2, extra_env={"MI355X_TIMEOUT_S": "30"}, timeout=120)
 
 
 def test_bounded_cache_export_check_is_identity(gpu):
