@@ -485,6 +485,7 @@ struct CallGate {
     CallGate &operator=(const CallGate &) = delete;
 };
 int p2p_progress(mi355x_comm *c);
+bool p2p_pending();  // any point-to-point work a progress pass could advance
 void p2p_progress_all(bool defer_maps = false);  // every communicator's point-to-point (the engine's host-side waits)
 int p2p_wait(mi355x_request *r);
 } // namespace mi355x

@@ -139,8 +139,9 @@ struct P2P {
     // matched receives of a dual message whose device buffer could not be mapped here: they wait
     // for the sender's host copy (claim 1) instead of claiming the pull
     std::vector<std::pair<mi355x_request *, P2PMsg>> dual_wait;
-    // matched receives whose read needs a peer mapping, matched in a progress pass made from inside
-    // a collective's barrier (a close window may be open on some rank): started at the next pass
+    // matched receives whose read needs a peer mapping, matched in a progress pass that must not
+    // open one (a member of the collective it runs from is closing, barrier_progress): started at
+    // the next pass that may
     std::vector<std::pair<mi355x_request *, P2PMsg>> deferred;
     DevArena arena;                        // exportable: packed / buffered device payloads
     DevArena rstage;                       // receive side: device staging of host receives
@@ -185,6 +186,24 @@ static unsigned p2p_inject()
 // a member closes its retired ones (coll_ctl.cpp, barrier_progress / close_window: hipIpc opens must
 // not overlap a peer's closes, coll_rcache.cpp): reads that would open one wait for a later pass
 static thread_local bool t_defer_maps = false;
+
+// any point-to-point work a progress pass could advance (a receive posted or matched, a send queued
+// or in flight): a collective's device wait then polls and progresses instead of blocking (ll_run).
+// Conservative when another thread holds the locks.
+bool p2p_pending()
+{
+    std::unique_lock<std::mutex> g(g_p2p_mtx, std::try_to_lock);
+    if (!g.owns_lock()) return true;
+    for (mi355x_comm *c : g_p2p_comms) {
+        P2P *p = c->p2p;
+        std::unique_lock<std::recursive_mutex> pg(p->mtx, std::try_to_lock);
+        if (!pg.owns_lock()) return true;
+        if (!p->posted.empty() || !p->queued.empty() || !p->sending.empty() || !p->reading.empty() ||
+            !p->dual_wait.empty() || !p->deferred.empty())
+            return true;
+    }
+    return false;
+}
 
 void p2p_progress_all(bool defer_maps)
 {

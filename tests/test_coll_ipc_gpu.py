@@ -206,12 +206,19 @@ def test_p2p_dual_offer_copy_failure(gpu, expect):
     _run_mode(gpu, "p2p_fault", 2, extra_env={"P2P_EXPECT": expect}, timeout=120)
 
 
-def test_p2p_receive_progresses_inside_a_collective(gpu):
-    """a receive posted before a collective is served by the progress the collective's barrier
-    makes while its peer is still in the matching blocking send (MPI's progress rule; ob1 progresses
+@pytest.mark.parametrize("flow", ["service", "ll", "host"])
+def test_p2p_receive_progresses_inside_a_collective(gpu, flow):
+    """a receive posted before a collective is served by the progress the collective's host waits
+    make while its peer is still in the matching blocking send (MPI's progress rule; ob1 progresses
     posted receives inside any blocking call, opal_progress): on the collective's communicator and
-    on another one (ipc_worker.py::p2p_in_coll)"""
-    _run_mode(gpu, "p2p_in_coll", 2, extra_env={"MI355X_TIMEOUT_S": "30"}, timeout=120)
+    on another one, with the small allreduce served by the resident service (default), by per-call
+    LL launches, or by the host-synchronised flow (ipc_worker.py::p2p_in_coll)"""
+    env = {"MI355X_TIMEOUT_S": "30"}
+    if flow != "service":
+        env["MI355X_SVC"] = "0"
+    if flow == "ll":
+        env["MI355X_LL_MAX_BYTES"] = "65536"
+    _run_mode(gpu, "p2p_in_coll", 2, extra_env=env, timeout=120)
 
 
 def test_bounded_cache_export_check_is_identity(gpu):
