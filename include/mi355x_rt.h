@@ -434,8 +434,9 @@ int mi355x_imrecv(mi355x_comm_t *comm, void *buf, size_t count, const mi355x_ddt
  * cancelled (ob1 cancels no send either, pml_ob1_sendreq.c:126-131). */
 int mi355x_request_cancel(mi355x_request_t *req);
 int mi355x_request_cancelled(const mi355x_request_t *req, int *cancelled);
-/* the engine's waits on host-buffer collectives (the buffer-kind vote) call this between polls:
- * coll/mi355x passes opal_progress, so requests other ranks depend on keep moving */
+/* the engine's host-side waits (the buffer-kind vote, and inside collectives the barriers, finish
+ * points and completion waits) call this between polls: coll/mi355x passes opal_progress, so
+ * requests other ranks depend on keep moving (MPI's progress rule, as ob1's blocking waits) */
 int mi355x_set_progress_hook(void (*progress)(void));
 
 /* ---------------------------------------------------------------- GPU convertor */

@@ -299,6 +299,19 @@ int mi355x_set_progress_hook(void (*progress)(void))
     return MI355X_SUCCESS;
 }
 
+} // extern "C"
+
+void mi355x::run_progress_hook()
+{
+    static thread_local bool inside = false;  // (its callbacks may wait in the engine again)
+    if (!g_progress_hook || inside) return;
+    inside = true;
+    g_progress_hook();
+    inside = false;
+}
+
+extern "C" {
+
 // The buffer-kind vote (mi355x_rt.h).  One side of a call waits for every vote: both at a window's
 // checkpoint (every kVoteWindow-th call), the host ranks in a window that follows device use (they
 // join the engine on device copies when a peer holds device buffers), the device ranks otherwise
@@ -349,7 +362,7 @@ int mi355x_comm_vote(mi355x_comm_t *c, int device, int *engine)
             if (++spins > 2048) {
                 if ((spins & 63) == 0) {
                     p2p_progress_all();
-                    if (g_progress_hook) g_progress_hook();
+                    run_progress_hook();
                 }
                 if ((spins & 0xffff) == 0 && peer_gone(c)) return MI355X_ERR_PEER;
                 sched_yield();

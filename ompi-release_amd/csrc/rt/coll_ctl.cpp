@@ -120,7 +120,7 @@ bool peer_gone(mi355x_comm *c)
 }
 
 // ----------------------------------------------------------------- barrier
-// Point-to-point progress from inside a collective's barrier.  MPI's progress rule: a receive
+// Point-to-point progress from inside a collective's host waits.  MPI's progress rule: a receive
 // posted before the collective completes while its sender waits in a blocking send (ob1 progresses
 // posted receives inside any blocking call), so the pass may read a payload and open a peer mapping
 // for it -- which must not overlap a peer's closes (coll_rcache.cpp, retire_map).  The pass announces
@@ -136,31 +136,39 @@ void barrier_progress(mi355x_comm *c)
     for (int r = 0; r < c->size && !closing; ++r)
         closing = r != c->rank && c->ctrl->slot[r].closing.load(std::memory_order_seq_cst) != 0;
     p2p_progress_all(closing);
+    // a peer may be blocked sending us dmabuf fds (full socket queue) or asking for one (serve_fd:
+    // an export -- so not while a member closes either)
+    if (!closing && c->fd_sock >= 0 && c->reg_mtx.try_lock()) {
+        (void)fd_drain(c, false);
+        c->reg_mtx.unlock();
+    }
+    // and the caller's progress engine (opal_progress: ob1's requests on other communicators, the
+    // component's nonblocking requests), under the same rule for the reads it starts
+    const bool prev = p2p_defer_maps(closing);
+    run_progress_hook();
+    (void)p2p_defer_maps(prev);
     me.opening.store(0, std::memory_order_release);
 }
 
-// close this rank's retired mappings while no member's barrier pass may be opening one
+// close this rank's retired mappings while no member's progress pass may be opening one.  A pass
+// that stays open (its read waits for a dmabuf fd from a rank that is itself waiting here) is not
+// waited out: after kCloseWaitMs the closes are left for the next window (the mappings stay retired,
+// so the next exchange opens one again), and nothing is exported meanwhile -- serving an fd request
+// here would be an export overlapping the other closers' closes, the race the window exists for.
 static int close_window(mi355x_comm *c)
 {
+    constexpr double kCloseWaitMs = 20.0;
     RankSlot &me = c->ctrl->slot[c->rank];
     me.closing.store(1, std::memory_order_seq_cst);
     const auto t0 = std::chrono::steady_clock::now();
     for (int r = 0; r < c->size; ++r) {
         unsigned spins = 0;
         while (r != c->rank && c->ctrl->slot[r].opening.load(std::memory_order_seq_cst) != 0) {
-            // the pass may wait for a dmabuf fd of mine (take_fd): keep serving them meanwhile
-            if ((++spins & 63) == 0) {
-                p2p_progress_all(true);
-                if (c->fd_sock >= 0 && c->reg_mtx.try_lock()) {
-                    (void)fd_drain(c, false);
-                    c->reg_mtx.unlock();
-                }
-            }
-            if ((spins & 0xffff) == 0 &&
-                (c->ctrl->abort_flag.load(std::memory_order_relaxed) || peer_gone(c) ||
-                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s)) {
+            if ((++spins & 255) == 0 &&
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > kCloseWaitMs) {
                 me.closing.store(0, std::memory_order_release);
-                return set_error(MI355X_ERR_PEER, "rank %d: rank %d's progress pass never ended", c->rank, r);
+                TRACE(c, "close window: rank %d's progress pass is still open; closes left for the next window", r);
+                return MI355X_SUCCESS;
             }
             sched_yield();
         }
@@ -187,12 +195,7 @@ int barrier(mi355x_comm *c)
             return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
         if (++spins > 2048) {
             sched_yield();
-            if ((spins & 63) == 0) barrier_progress(c);  // a peer may wait in a send for a receive of mine
-            // a peer may be blocked sending us dmabuf fds (full socket queue): drain it while we wait
-            if (c->fd_sock >= 0 && (spins & 255) == 0 && c->reg_mtx.try_lock()) {
-                (void)fd_drain(c, false);
-                c->reg_mtx.unlock();
-            }
+            if ((spins & 63) == 0) barrier_progress(c);  // a peer may wait in a send for a receive of mine, or for fds
             if ((spins & 0xffff) == 0) {
                 if (peer_gone(c)) return MI355X_ERR_PEER;
                 const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -494,11 +497,6 @@ int exchange(mi355x_comm *c, int nbuf, const void *const *mine, const uint64_t s
                 if (c->ctrl->abort_flag.load(std::memory_order_relaxed)) return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
                 if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s)
                     return set_error(MI355X_ERR_TIMEOUT, "rank %d: the mapping window timed out waiting for rank %d", c->rank, r);
-                // a peer's open may wait for a dmabuf fd of mine (take_fd): serve them meanwhile
-                if (c->fd_sock >= 0 && c->reg_mtx.try_lock()) {
-                    (void)fd_drain(c, false);
-                    c->reg_mtx.unlock();
-                }
                 sched_yield();
             }
         }
@@ -547,11 +545,7 @@ int finish(mi355x_comm *c, hipStream_t s)
                 return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
             if (++spins > 4096) {
                 sched_yield();
-                if (c->fd_sock >= 0 && (spins & 255) == 0 && c->reg_mtx.try_lock()) {
-                    (void)fd_drain(c, false);  // a peer may be asking for a dmabuf fd (serve_fd)
-                    c->reg_mtx.unlock();
-                }
-                if ((spins & 255) == 0) barrier_progress(c);
+                if ((spins & 255) == 0) barrier_progress(c);  // (a peer may be asking for a dmabuf fd, serve_fd)
                 if ((spins & 0xffff) == 0 && hipStreamQuery(s) != hipErrorNotReady && q == c->rank &&
                     k->slot[q].done.load(std::memory_order_acquire) < v)
                     return set_error(MI355X_ERR_HIP, "stream finished without writing its completion word");

@@ -187,6 +187,13 @@ static unsigned p2p_inject()
 // not overlap a peer's closes, coll_rcache.cpp): reads that would open one wait for a later pass
 static thread_local bool t_defer_maps = false;
 
+bool p2p_defer_maps(bool on)
+{
+    const bool prev = t_defer_maps;
+    t_defer_maps = on;
+    return prev;
+}
+
 // any point-to-point work a progress pass could advance (a receive posted or matched, a send queued
 // or in flight): a collective's device wait then polls and progresses instead of blocking (ll_run).
 // Conservative when another thread holds the locks.
@@ -795,7 +802,10 @@ int p2p_progress(mi355x_comm *c)
     std::lock_guard<std::recursive_mutex> g(p->mtx);
     // a receiver that closed its import of one of my send buffers asks me for its dmabuf fd again
     // (serve_fd): serve it while I wait in point-to-point too (now and then: one syscall)
-    if (c->dmabuf_state != -1 && c->fd_sock >= 0 && (++p->fd_polls & 31) == 0 && c->reg_mtx.try_lock()) {
+    // (not in a pass that must not open mappings: serving one is an export, which must not overlap a
+    // member's closes either)
+    if (!t_defer_maps && c->dmabuf_state != -1 && c->fd_sock >= 0 && (++p->fd_polls & 31) == 0 &&
+        c->reg_mtx.try_lock()) {
         (void)fd_drain(c, false);
         c->reg_mtx.unlock();
     }
