@@ -301,14 +301,20 @@ int mi355x_set_progress_hook(void (*progress)(void))
 
 } // extern "C"
 
+// set while the hook runs (its callbacks may wait in the engine again) and for good on the engine's
+// own threads (a nonblocking collective's worker): the caller's progress engine runs only on the
+// caller's threads, as MPI's thread level allows
+static thread_local bool t_hook_blocked = false;
+
 void mi355x::run_progress_hook()
 {
-    static thread_local bool inside = false;  // (its callbacks may wait in the engine again)
-    if (!g_progress_hook || inside) return;
-    inside = true;
+    if (!g_progress_hook || t_hook_blocked) return;
+    t_hook_blocked = true;
     g_progress_hook();
-    inside = false;
+    t_hook_blocked = false;
 }
+
+void mi355x::progress_hook_off_this_thread() { t_hook_blocked = true; }
 
 extern "C" {
 

@@ -141,6 +141,7 @@ void drain(mi355x_comm *c)
 void worker_main(mi355x_comm *c)
 {
     (void)hipSetDevice(c->device);
+    progress_hook_off_this_thread();
     for (;;) {
         mi355x_request *r;
         {
