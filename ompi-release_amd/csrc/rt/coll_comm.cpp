@@ -80,7 +80,7 @@ int mi355x_comm_create(const char *key, int rank, int size, int device, mi355x_c
     c->rank = rank;
     c->size = size;
     c->device = device;
-    c->timeout_s = env_double("MI355X_TIMEOUT_S", 600.0);
+    c->timeout_s = env_double("MI355X_TIMEOUT_S", kDefaultTimeoutS);
     c->selftest = env_double("MI355X_SELFTEST", 1.0) != 0.0;
     c->export_check = env_double("MI355X_EXPORT_CHECK", 1.0) != 0.0;
     c->shm_name = std::string("/mi355x_") + key;
@@ -215,7 +215,7 @@ int mi355x_comm_create_loopback(int size, int device, mi355x_comm_t **comms)
         c->ctrl = shared->ctrl;
         c->loopback = true;
         c->loop = shared;
-        c->timeout_s = env_double("MI355X_TIMEOUT_S", 600.0);
+        c->timeout_s = env_double("MI355X_TIMEOUT_S", kDefaultTimeoutS);
         shared->refs++;
         comms[r] = c;
     }

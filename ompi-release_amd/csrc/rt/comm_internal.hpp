@@ -42,6 +42,11 @@ inline bool debug_on()
 
 constexpr uint64_t kMagic = 0x4d49333535584331ull;  // "MI355XC1"
 constexpr int kMaxBufs = 3;
+// every wait's bound unless MI355X_TIMEOUT_S / the TIMEOUT_S knob says otherwise: one day.  MPI's
+// waits are unbounded -- a rank late by minutes or hours (checkpoint I/O) is not an error -- and a
+// dead peer is found by its pid and start time (peer_gone), not by a timeout; the bound only turns a
+// hang into an error eventually (tests set seconds)
+constexpr double kDefaultTimeoutS = 86400.0;
 constexpr int kVoteRing = 64;    // buffer-kind votes a rank keeps (mi355x_comm_vote)
 constexpr int kVoteWindow = 32;  // calls per vote window: every rank waits at each window's last call
 
@@ -434,7 +439,7 @@ struct mi355x_comm {
     int chain_fanout = mi355x::kDefaultChainFanout;
     const mi355x_rules_t *rules = nullptr;        // coll/tuned dynamic rules (not owned)
     int last_alg = -1;
-    double timeout_s = 600.0;
+    double timeout_s = mi355x::kDefaultTimeoutS;
     bool time_phases = false;                     // MI355X_KNOB_TIME_PHASES
     hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
     float phase_ms[2] = {-1.f, -1.f};
