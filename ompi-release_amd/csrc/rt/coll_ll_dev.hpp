@@ -139,10 +139,16 @@ static __device__ bool ll_wait_acks(const LLArgs &a)
     __syncthreads();
     if (a.src && t < a.n && t != a.me && ((a.push_mask >> t) & 1u) && a.seq > 2) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        unsigned spins = 0;
         while (ll_load(a.my_ack + t) + 2 < a.seq) {
             __builtin_amdgcn_s_sleep(1);
             if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
                 __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                timed_out = 1;
+                break;
+            }
+            // the call failed elsewhere, or the host gave up on a peer that is gone (ll_err_set)
+            if ((++spins & 255u) == 0 && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
                 timed_out = 1;
                 break;
             }
@@ -226,9 +232,12 @@ static __device__ bool ll_recv(const LLArgs &a, const LLBlock &k, uint64_t qmask
             for (int h = 0; h < 2; ++h)
                 if (((pending >> (q * 2 + h)) & 1u) && load_pair(q, h)) pending &= ~(1u << (q * 2 + h));
         }
-        if ((++spins & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
-            __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            return false;
+        if ((++spins & 255u) == 0) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+                __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return false;
+            }
+            if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return false;  // (as above)
         }
     }
     return true;

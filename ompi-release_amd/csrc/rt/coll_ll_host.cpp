@@ -141,17 +141,24 @@ int ll_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s)
     a.timeout_ticks = (uint64_t)(c->timeout_s * 1e8);  // s_memrealtime: 100 MHz
     rc = (a.mode == LL_AR || a.mode == LL_RED) ? launch_ll_slot(op, type, a, s) : launch_ll_copy(a, s);
     if (rc) return rc;
-    if (p2p_pending()) {
-        // the kernel waits for every peer, and a peer that has not called yet may be waiting in
-        // point-to-point for this rank (MPI's progress rule): poll and progress instead of blocking
-        for (unsigned spins = 1; hipStreamQuery(s) == hipErrorNotReady; ++spins)
-            if ((spins & 63u) == 0) barrier_progress(c);
+    // the kernel waits for every peer: poll instead of blocking -- a peer that has not called yet may
+    // be waiting in point-to-point for this rank (MPI's progress rule), and a peer that is gone
+    // sends the kernel away through the error word
+    bool gone = false;
+    for (unsigned spins = 1; hipStreamQuery(s) == hipErrorNotReady; ++spins) {
+        if ((spins & 63u) == 0) barrier_progress(c);
+        if (!gone && (spins & 0x3fffu) == 0 && peer_gone(c)) {
+            gone = true;  // (peer_gone set the error and aborted the communicator)
+            __atomic_store_n(c->ll_err, 1u, __ATOMIC_RELEASE);
+        }
+        if (spins > 4096) sched_yield();
     }
     MI_HIP(hipStreamSynchronize(s));
     if (__atomic_load_n(c->ll_err, __ATOMIC_ACQUIRE)) {
         (void)hipMemsetAsync(c->ll_ctr, 0, sizeof(uint64_t), s);  // its count is off now: restart it
         (void)hipStreamSynchronize(s);
         c->ll_ctr_base = 0;
+        if (gone) return MI355X_ERR_PEER;
         return set_error(MI355X_ERR_TIMEOUT, "rank %d: LL call %llu timed out waiting for a peer", c->rank,
                          (unsigned long long)seq);
     }

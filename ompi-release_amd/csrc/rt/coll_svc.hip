@@ -27,7 +27,8 @@
 // allgather and bcast to 1 MiB; LL_PULL_RS, reduce_scatter(_block) up to 128 KiB per block) replace
 // step 3's granules by reads of the peers' mapped inputs, and step 4 waits until every peer has
 // read this rank's.
-// Every wait is bounded (timeout_ticks; the error word is set and the workgroup leaves).
+// Every wait is bounded (timeout_ticks; the error word is set and the workgroup leaves) and leaves
+// early once the error word is set -- by another workgroup, or by the host when a peer is gone.
 #include "coll_ll_dev.hpp"
 #include "slot_list.hpp"
 
@@ -262,6 +263,7 @@ static __device__ bool svc_pull_handshake(const SvcArgs &g, uint64_t want)
         if (q != g.me) ll_store(reinterpret_cast<uint64_t *>(g.peer_ll[q]) + kSvcPullDoneWord + g.me, want);
     const uint64_t *mine = reinterpret_cast<const uint64_t *>(g.my_ll) + kSvcPullDoneWord;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned spins = 0;
     for (int q = 0; q < g.n; ++q) {
         if (q == g.me) continue;
         while (ll_load(mine + q) < want) {
@@ -270,6 +272,8 @@ static __device__ bool svc_pull_handshake(const SvcArgs &g, uint64_t want)
                 __hip_atomic_store(g.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 return false;
             }
+            // the host gave up on a peer that is gone (svc_call)
+            if ((++spins & 255u) == 0 && __hip_atomic_load(g.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return false;
         }
     }
     return true;

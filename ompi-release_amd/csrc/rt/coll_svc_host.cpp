@@ -173,6 +173,12 @@ int svc_call(mi355x_comm *c, const SvcCall &call, uint64_t part)
                            (unsigned long long)seq);
             break;
         }
+        if ((spins & 0x3ffffu) == 0 && peer_gone(c)) {
+            // the kernel may wait for that peer until its own bound: the error word sends it away
+            __atomic_store_n(const_cast<uint32_t *>(err), 1u, __ATOMIC_RELEASE);
+            rc = MI355X_ERR_PEER;
+            break;
+        }
     }
     if (rc) {
         svc_stop(c);

@@ -1426,6 +1426,39 @@ def vote_dead(key, rank, size, dev):
     print(f"rank {rank} vote_dead OK", flush=True)
 
 
+def dead_peer(key, rank, size, dev):
+    """a peer process that dies without a word after one device allreduce: the surviving rank's next
+    small device allreduce -- through the resident service, a per-call LL launch or the host flow
+    (DEAD_FLOW, set up by the caller's environment) -- returns an error naming the gone peer within
+    seconds, although every wait's bound is far away (MI355X_TIMEOUT_S=100): the host finds the peer
+    gone by its pid and sends the waiting kernel away through the error word"""
+    import time
+    import torch
+    torch.cuda.set_device(dev)
+    pkg = load_pkg()
+    comm = pkg.Comm.create(key, rank, size, dev)
+    x = torch.full((256,), float(rank + 1), device="cuda")
+    y = torch.zeros_like(x)
+    comm.allreduce(x.data_ptr(), y.data_ptr(), 256, pkg.T["FLOAT"], pkg.OP["SUM"])
+    torch.cuda.synchronize()
+    assert bool(torch.all(y == 3.0).item())
+    comm.barrier()
+    if rank == 1:
+        os._exit(0)
+    time.sleep(0.5)
+    t0 = time.time()
+    try:
+        comm.allreduce(x.data_ptr(), y.data_ptr(), 256, pkg.T["FLOAT"], pkg.OP["SUM"])
+        torch.cuda.synchronize()
+        raise AssertionError("the allreduce returned although its peer is gone")
+    except pkg.MI355XError as e:
+        assert "gone" in str(e) or "aborted" in str(e), e
+    dt = time.time() - t0
+    assert dt < 30, dt
+    print(f"rank {rank} dead peer ({os.environ.get('DEAD_FLOW')}): noticed after {dt:.2f} s", flush=True)
+    print(f"rank {rank} dead_peer OK", flush=True)
+
+
 def token_hold(key, dev):
     """a one-rank communicator takes its GPU's pipelined-grid admission token (as a rank inside a
     pipelined allreduce holds it) and sleeps until the test SIGKILLs it"""
@@ -1478,6 +1511,8 @@ def _main():
         return selftest(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "vote_dead":
         return vote_dead(key, rank, size, dev)
+    if len(sys.argv) > 5 and sys.argv[5] == "dead_peer":
+        return dead_peer(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "rcache":
         return rcache(key, rank, size, dev)
     if len(sys.argv) > 5 and sys.argv[5] == "rcache_p2p":

@@ -230,6 +230,25 @@ def test_bounded_cache_export_check_is_identity(gpu):
     print(next(line for line in outs[0].splitlines() if "carved:" in line))
 
 
+@pytest.mark.parametrize("flow", ["service", "ll", "host"])
+def test_device_collective_notices_dead_peer(gpu, flow):
+    """every wait's bound is a day by default (MPI's waits are unbounded); a peer that dies without a
+    word is still noticed by its pid within seconds, the resident service's and an LL launch's
+    device-side waits included (ipc_worker.py::dead_peer)"""
+    key = "t" + uuid.uuid4().hex[:12]
+    env = dict(os.environ, MI355X_TIMEOUT_S="100", DEAD_FLOW=flow)  # (far beyond the 30 s the test allows)
+    if flow != "service":
+        env["MI355X_SVC"] = "0"
+    if flow == "ll":
+        env["MI355X_LL_MAX_BYTES"] = "65536"
+    procs = [subprocess.Popen([sys.executable, str(HERE / "ipc_worker.py"), key, str(r), "2", "0", "dead_peer"],
+                              env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    out, _ = procs[0].communicate(timeout=120)
+    procs[1].communicate(timeout=60)
+    assert procs[0].returncode == 0 and "rank 0 dead_peer OK" in out, out[-3000:]
+    print(next(line for line in out.splitlines() if "dead peer" in line))
+
+
 def test_vote_notices_dead_peer(gpu):
     """the buffer-kind vote waits without a timeout; a peer that dies without setting the abort flag
     is noticed by its pid (ipc_worker.py::vote_dead)"""
