@@ -1298,7 +1298,10 @@ int p2p_wait(mi355x_request *r)
         p2p_progress(c);
         if (r->done.load(std::memory_order_acquire)) break;
         if (++spins > 64) {
-            if ((spins & 63) == 0) p2p_progress_all();  // (the other communicators' queued sends)
+            if ((spins & 63) == 0) {
+                p2p_progress_all();  // (the other communicators' queued sends)
+                run_progress_hook();  // (and the caller's: ob1's requests a peer may need first)
+            }
             sched_yield();
             if ((spins & 0x3ff) == 0 &&
                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s)
