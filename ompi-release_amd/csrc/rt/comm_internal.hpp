@@ -490,7 +490,6 @@ struct CallGate {
     CallGate &operator=(const CallGate &) = delete;
 };
 int p2p_progress(mi355x_comm *c);
-bool p2p_pending();  // any point-to-point work a progress pass could advance
 bool p2p_defer_maps(bool on);  // this thread's passes defer reads that open a peer mapping; returns the old value
 void run_progress_hook();      // the caller's progress engine (mi355x_set_progress_hook: opal_progress), not re-entered
 void progress_hook_off_this_thread();  // an engine thread: never runs the caller's progress engine

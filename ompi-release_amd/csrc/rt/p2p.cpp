@@ -194,24 +194,6 @@ bool p2p_defer_maps(bool on)
     return prev;
 }
 
-// any point-to-point work a progress pass could advance (a receive posted or matched, a send queued
-// or in flight): a collective's device wait then polls and progresses instead of blocking (ll_run).
-// Conservative when another thread holds the locks.
-bool p2p_pending()
-{
-    std::unique_lock<std::mutex> g(g_p2p_mtx, std::try_to_lock);
-    if (!g.owns_lock()) return true;
-    for (mi355x_comm *c : g_p2p_comms) {
-        P2P *p = c->p2p;
-        std::unique_lock<std::recursive_mutex> pg(p->mtx, std::try_to_lock);
-        if (!pg.owns_lock()) return true;
-        if (!p->posted.empty() || !p->queued.empty() || !p->sending.empty() || !p->reading.empty() ||
-            !p->dual_wait.empty() || !p->deferred.empty())
-            return true;
-    }
-    return false;
-}
-
 void p2p_progress_all(bool defer_maps)
 {
     std::unique_lock<std::mutex> g(g_p2p_mtx, std::try_to_lock);  // (another thread progresses them now)
