@@ -174,8 +174,24 @@ int pipe_allreduce(mi355x_comm *c, int op, int type, const Program &pr,
             }
         }
     }
+    // every peer is in this call (the exchange met them), but one may die inside it: poll, and a
+    // peer that is gone sends the kernel's flag waits away through the error word
+    bool gone = false;
+    for (unsigned spins = 1; hipStreamQuery(s) == hipErrorNotReady; ++spins) {
+        if (spins > 256) sched_yield();
+        if (!gone && (spins & 0x3fffu) == 0 && peer_gone(c)) {
+            gone = true;
+            __atomic_store_n(c->ll_err, 1u, __ATOMIC_RELEASE);
+        }
+    }
     MI_HIP(hipStreamSynchronize(s));
     if (__atomic_load_n(c->ll_err, __ATOMIC_ACQUIRE)) {
+        if (gone) {
+            (void)hipMemsetAsync(c->pipe_queue, 0, sizeof(uint64_t), s);
+            (void)hipStreamSynchronize(s);
+            c->pipe_qbase = 0;
+            return MI355X_ERR_PEER;
+        }
         // the counter no longer has its expected value: start it over for the next call
         (void)hipMemsetAsync(c->pipe_queue, 0, sizeof(uint64_t), s);
         (void)hipStreamSynchronize(s);
