@@ -268,6 +268,9 @@ def run(args, pkg, torch):
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    # a measurement run bounds its waits (communicator creation included) at minutes, not the
+    # engine's default of a day: a rank that failed before creating a communicator ends the run
+    os.environ.setdefault("MI355X_TIMEOUT_S", "300")
     if world < 2:
         raise SystemExit("bench_coll needs WORLD_SIZE >= 2")
     local = local % max(1, torch.cuda.device_count())  # one-GPU rehearsal: ranks share device 0
