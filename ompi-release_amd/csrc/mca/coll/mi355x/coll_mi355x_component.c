@@ -333,6 +333,7 @@ unsigned long long mca_coll_mi355x_svc_copy_max = 1ull << 20;
 int mca_coll_mi355x_svc_idle_us = 1000;
 int mca_coll_mi355x_svc_shrink_us = 100;
 int mca_coll_mi355x_selftest = 1;
+int mca_coll_mi355x_timeout_s = 0;  /* 0: the engine's own (MI355X_TIMEOUT_S, else one day) */
 
 /* 1: the call runs in the engine (a rank with host buffers joins on device copies); 0: it runs in
  * the previous component on every rank (a rank with device buffers stages them to the host, as
@@ -2155,6 +2156,7 @@ static int apply_engine_params(mca_coll_mi355x_module_t *m, struct ompi_communic
     KNOB(SVC_PULL_COPY_MAX_BYTES, mca_coll_mi355x_svc_copy_max, "svc_copy_max");
     KNOB(SVC_IDLE_US, mca_coll_mi355x_svc_idle_us, "svc_idle_us");
     KNOB(SVC_SHRINK_US, mca_coll_mi355x_svc_shrink_us, "svc_shrink_us");
+    if (mca_coll_mi355x_timeout_s > 0) KNOB(TIMEOUT_S, mca_coll_mi355x_timeout_s, "timeout_s");
 #undef KNOB
     return rc;
 }
@@ -2301,6 +2303,9 @@ static int component_register(void)
     register_int("selftest", "Run the cross-device flows' self-tests at a communicator's first device-buffer collective "
                  "(a flow that fails on any rank is turned off on every rank); 0 = trust every flow", OPAL_INFO_LVL_9,
                  &mca_coll_mi355x_selftest);
+    register_int("timeout_s", "Bound of every wait of the engine, seconds (0 = the engine's own: MI355X_TIMEOUT_S, "
+                 "else one day -- MPI's waits are unbounded; a rank whose process is gone is noticed without it)",
+                 OPAL_INFO_LVL_9, &mca_coll_mi355x_timeout_s);
     return OMPI_SUCCESS;
 }
 static int component_open(void) { return OMPI_SUCCESS; }

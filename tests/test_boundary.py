@@ -285,7 +285,8 @@ def test_mca_variables_registered(monkeypatch):
         # the engine's crossovers (coll_tuned_component.c:115-170 style), with the engine's defaults
         engine_vars = {"pipe_min_ranks": 4, "pipe_chunk_kib": 0, "pipe_wg_per_cu": 2, "pipe_wt": 1,
                        "one_phase_max": 1 << 20, "svc_max": 32 << 10, "svc_pull_max": 128 << 10,
-                       "svc_copy_max": 1 << 20, "svc_idle_us": 1000, "svc_shrink_us": 100, "selftest": 1}
+                       "svc_copy_max": 1 << 20, "svc_idle_us": 1000, "svc_shrink_us": 100, "selftest": 1,
+                       "timeout_s": 0}
         for name, dflt in engine_vars.items():
             assert names.get("coll_mi355x_" + name) == dflt, (name, names.get("coll_mi355x_" + name))
         _coll_env(monkeypatch)
