@@ -38,7 +38,7 @@ uint64_t pid_namespace();
 int barrier(mi355x_comm *c);
 // point-to-point progress from a host wait inside a collective (MPI's progress rule), gated against
 // the members' close windows (coll_ctl.cpp)
-void barrier_progress(mi355x_comm *c);
+void barrier_progress(mi355x_comm *c, bool drain_fds = true);
 uint64_t buffer_id(const void *p);
 int local_handle(mi355x_comm *c, const void *p, BufDesc *d, bool force);
 // the stream a collective runs on, for the setup work it triggers (device setup, dmabuf probe, LL

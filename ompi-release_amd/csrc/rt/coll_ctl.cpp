@@ -128,7 +128,7 @@ bool peer_gone(mi355x_comm *c)
 // and then waits for every opening pass to end (close_window).  Sequentially consistent stores and
 // loads on both sides (Dekker): one of the two always sees the other, so a pass either opens with no
 // close of this communicator in flight or defers its opens to a later pass.
-void barrier_progress(mi355x_comm *c)
+void barrier_progress(mi355x_comm *c, bool drain_fds)
 {
     RankSlot &me = c->ctrl->slot[c->rank];
     me.opening.store(1, std::memory_order_seq_cst);
@@ -138,7 +138,7 @@ void barrier_progress(mi355x_comm *c)
     p2p_progress_all(closing);
     // a peer may be blocked sending us dmabuf fds (full socket queue) or asking for one (serve_fd:
     // an export -- so not while a member closes either)
-    if (!closing && c->fd_sock >= 0 && c->reg_mtx.try_lock()) {
+    if (drain_fds && !closing && c->fd_sock >= 0 && c->reg_mtx.try_lock()) {
         (void)fd_drain(c, false);
         c->reg_mtx.unlock();
     }
@@ -195,7 +195,9 @@ int barrier(mi355x_comm *c)
             return set_error(MI355X_ERR_PEER, "a peer aborted the communicator");
         if (++spins > 2048) {
             sched_yield();
-            if ((spins & 63) == 0) barrier_progress(c);  // a peer may wait in a send for a receive of mine, or for fds
+            // a peer may wait in a send for a receive of mine, or for fds (those every 256th spin:
+            // each one served is an export)
+            if ((spins & 63) == 0) barrier_progress(c, (spins & 255) == 0);
             if ((spins & 0xffff) == 0) {
                 if (peer_gone(c)) return MI355X_ERR_PEER;
                 const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

@@ -146,7 +146,7 @@ int ll_run(mi355x_comm *c, LLArgs &a, int op, int type, hipStream_t s)
     // sends the kernel away through the error word
     bool gone = false;
     for (unsigned spins = 1; hipStreamQuery(s) == hipErrorNotReady; ++spins) {
-        if ((spins & 63u) == 0) barrier_progress(c);
+        if ((spins & 63u) == 0) barrier_progress(c, false);
         if (!gone && (spins & 0x3fffu) == 0 && peer_gone(c)) {
             gone = true;  // (peer_gone set the error and aborted the communicator)
             __atomic_store_n(c->ll_err, 1u, __ATOMIC_RELEASE);

@@ -156,7 +156,7 @@ int svc_call(mi355x_comm *c, const SvcCall &call, uint64_t part)
         _mm_pause();
         if (spins & 255u) continue;
         // a peer that has not called yet may be waiting in a send for a receive of mine
-        if ((spins & 1023u) == 0) barrier_progress(c);
+        if ((spins & 1023u) == 0) barrier_progress(c, false);
         if (__atomic_load_n(err, __ATOMIC_ACQUIRE)) {
             rc = set_error(MI355X_ERR_TIMEOUT, "rank %d: service call %llu timed out waiting for a peer", c->rank,
                            (unsigned long long)seq);
